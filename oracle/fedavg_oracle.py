@@ -1,0 +1,180 @@
+"""CPU oracle for the FedAvg weighted-aggregation hot path -- TEST INFRASTRUCTURE ONLY.
+
+Only ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline`` leg may import this
+module.  It is the checker, never the thing measured or shipped: ``nvflare_amd`` (the product) never
+imports it.
+
+Three restatements of ``WeightedAggregationHelper.add`` / ``get_result``
+(``nvflare/app_common/aggregators/weighted_aggregation_helper.py:153-240``), all bit-exact with the
+reference on the golden vectors in ``tests/golden/`` (pinned by ``tests/test_oracle_golden.py``):
+
+* ``fedavg_c``            -- plain C restatement (``oracle/fedavg_oracle.c``), element by element in
+                             arrival order; optionally multi-threaded over elements (OpenMP).
+* ``numpy_mode_reference`` -- the numpy branch as numpy ops (``:188-193``, ``:210-214``, ``:236``).
+* ``torch_mode_reference`` -- the torch branch as torch CPU ops (``:181-187``, ``:203-209``, ``:233``).
+
+Plus ``synth_values``: the host twin of the device synthetic-input generator used by ``bench.py`` for
+full-size spot checks.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+from typing import Optional, Sequence
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "build", "liboracle_fedavg.so")
+_lib = None
+
+MODE_NUMPY = 0
+MODE_TORCH = 1
+FIN_NONE = 0
+FIN_NUMPY_SCALE = 1
+FIN_TORCH_DIV = 2
+
+
+def build(force: bool = False) -> str:
+    """Compile the C restatement with ``oracle/Makefile`` (gcc, -ffp-contract=off)."""
+    if force or not os.path.exists(_LIB_PATH):
+        subprocess.run(["make", "-s", "-C", _HERE], check=True)
+    return _LIB_PATH
+
+
+def load():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            build()
+        lib = ctypes.CDLL(_LIB_PATH)
+        for name, ct in (("oracle_fedavg_f32", ctypes.c_float), ("oracle_fedavg_f64", ctypes.c_double)):
+            fn = getattr(lib, name)
+            fn.restype = None
+            fn.argtypes = [
+                ctypes.POINTER(ctypes.c_void_p),
+                ctypes.c_int,
+                ctypes.POINTER(ctypes.c_double),
+                ctypes.c_int,
+                ctypes.c_int,
+                ctypes.c_int,
+                ctypes.c_double,
+                ctypes.c_void_p,
+                ctypes.c_void_p,
+                ctypes.c_size_t,
+                ctypes.c_int,
+            ]
+        lib.oracle_synth_value.restype = ctypes.c_float
+        lib.oracle_synth_value.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64]
+        lib.oracle_synth_fill_f32.restype = None
+        lib.oracle_synth_fill_f32.argtypes = [
+            ctypes.c_uint64,
+            ctypes.c_uint64,
+            ctypes.c_void_p,
+            ctypes.c_size_t,
+            ctypes.c_void_p,
+        ]
+        _lib = lib
+    return _lib
+
+
+def fedavg_c(
+    rows: Sequence[np.ndarray],
+    weights: Sequence[float],
+    mode: int,
+    weighted: bool = True,
+    fin: Optional[int] = None,
+    count: Optional[float] = None,
+    acc_in: Optional[np.ndarray] = None,
+    nthreads: int = 1,
+) -> np.ndarray:
+    """C restatement: weighted arrival-order accumulate, then the mode's finalisation.
+
+    ``rows`` are the client arrays in arrival order (same dtype, float32 or float64, same size).
+    ``count`` defaults to the fp64 arrival-order sum of ``weights`` (``weighted_aggregation_helper.py:201,216``).
+    ``fin`` defaults to the mode's ``get_result`` step.
+    """
+    lib = load()
+    dtype = np.dtype(rows[0].dtype) if rows else np.dtype(acc_in.dtype)
+    if dtype == np.float32:
+        fn = lib.oracle_fedavg_f32
+    elif dtype == np.float64:
+        fn = lib.oracle_fedavg_f64
+    else:
+        raise TypeError(f"oracle supports float32/float64 rows, got {dtype}")
+    rows = [np.ascontiguousarray(r, dtype=dtype).reshape(-1) for r in rows]
+    n = rows[0].size if rows else acc_in.size
+    for r in rows:
+        if r.size != n:
+            raise ValueError("all rows must have the same size")
+    if count is None:
+        count = 0.0
+        for i, w in enumerate(weights):
+            count = w if i == 0 else count + w
+    if fin is None:
+        fin = FIN_TORCH_DIV if mode == MODE_TORCH else FIN_NUMPY_SCALE
+    K = len(rows)
+    ptrs = (ctypes.c_void_p * max(K, 1))(*[r.ctypes.data for r in rows])
+    w = (ctypes.c_double * max(K, 1))(*[float(x) for x in weights])
+    out = np.empty(n, dtype=dtype)
+    acc_ptr = None
+    if acc_in is not None:
+        acc_in = np.ascontiguousarray(acc_in, dtype=dtype).reshape(-1)
+        acc_ptr = acc_in.ctypes.data
+    elif K == 0:
+        raise ValueError("need at least one row or an acc_in")
+    fn(ptrs, K, w, int(mode), int(bool(weighted)), int(fin), float(count), acc_ptr, out.ctypes.data, n, int(nthreads))
+    return out
+
+
+def numpy_mode_reference(rows, weights, weighted: bool = True, count: Optional[float] = None):
+    """numpy branch restated with numpy ops (``weighted_aggregation_helper.py:188-193,210-214,236``)."""
+    total = None
+    c = None
+    for v, w in zip(rows, weights):
+        if total is None:
+            total = v * w if weighted else v.copy()
+            c = w
+        else:
+            total = total + v * w if weighted else total + v
+            c = c + w
+    if count is not None:
+        c = count
+    return total * (1.0 / c)
+
+
+def torch_mode_reference(rows, weights, weighted: bool = True, count: Optional[float] = None):
+    """torch branch restated with torch CPU ops (``weighted_aggregation_helper.py:181-187,203-209,233``).
+
+    ``rows`` are CPU torch tensors.  Uses all of torch's intra-op threads (the CPU baseline mode)."""
+    total = None
+    c = None
+    for v, w in zip(rows, weights):
+        if total is None:
+            total = v.mul(w) if weighted else v.clone()
+            c = w
+        else:
+            if weighted:
+                total.add_(v, alpha=w)
+            else:
+                total.add_(v)
+            c = c + w
+    if count is not None:
+        c = count
+    return total.div_(c)
+
+
+def synth_values(seed: int, row: int, cols: np.ndarray) -> np.ndarray:
+    """Host twin of the device generator ``fedavg_fill_synthetic_f32`` (bit-identical values)."""
+    lib = load()
+    cols = np.ascontiguousarray(cols, dtype=np.uint64)
+    out = np.empty(cols.size, dtype=np.float32)
+    lib.oracle_synth_fill_f32(int(seed), int(row), cols.ctypes.data, cols.size, out.ctypes.data)
+    return out
+
+
+def synth_weights(K: int):
+    """Synthetic per-client weights of SURVEY.md section 8d: aggregation_weight 1.0 x NUM_STEPS (1 + 37k mod 100)."""
+    return [1.0 * float(1 + (37 * k) % 100) for k in range(K)]

@@ -1,0 +1,278 @@
+"""Generate the golden vectors in tests/golden/ by running the NVFlare reference itself.
+
+Runs ONLY in the build container, where the reference tree is mounted read-only at /root/reference.
+Nothing here runs on the GPU box; the outputs (``helper_cases.npz`` + ``helper_cases.json``) are plain
+data: inputs, weights and the reference's outputs.
+
+``import nvflare`` fails in the container with an ordinary ModuleNotFoundError (``cryptography``,
+pulled in by ``nvflare/__init__.py:21-23``); this is not a permission denial.  The script registers
+``nvflare``, ``nvflare.app_opt`` and ``nvflare.app_opt.pt`` as bare namespace packages whose
+``__path__`` points into the reference tree, then imports the aggregation modules normally
+(SURVEY.md section 8c).  No reference source is copied.
+
+Reference code exercised:
+  nvflare/app_common/aggregators/weighted_aggregation_helper.py:153-240  (helper cases)
+  nvflare/app_common/aggregators/intime_accumulate_model_aggregator.py   (intime cases)
+  nvflare/app_common/aggregators/dxo_aggregator.py:71-191
+
+Usage:  python tests/golden/make_golden.py [--ref /root/reference]
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import random
+import sys
+import types
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def install_shim(ref_root: str) -> None:
+    for name, sub in (("nvflare", "nvflare"), ("nvflare.app_opt", "nvflare/app_opt"), ("nvflare.app_opt.pt", "nvflare/app_opt/pt")):
+        if name not in sys.modules:
+            m = types.ModuleType(name)
+            m.__path__ = [os.path.join(ref_root, sub)]
+            sys.modules[name] = m
+    if ref_root not in sys.path:
+        sys.path.insert(0, ref_root)
+
+
+class Store:
+    def __init__(self):
+        self.arrays = {}
+        self.n = 0
+
+    def put(self, arr, tag="a") -> str:
+        if isinstance(arr, torch.Tensor):
+            arr = arr.detach().cpu().numpy()
+        arr = np.asarray(arr)
+        name = f"{tag}{self.n:05d}"
+        self.n += 1
+        self.arrays[name] = arr
+        return name
+
+
+def to_container(arr: np.ndarray, container: str):
+    if container == "torch":
+        return torch.from_numpy(np.array(arr, copy=True))
+    return np.array(arr, copy=True)
+
+
+def special_values(rng, n, dtype=np.float32):
+    base = rng.standard_normal(n).astype(dtype)
+    specials = np.array(
+        [0.0, -0.0, np.inf, -np.inf, np.nan, 1e-40, -3e-42, 1.4e-45, 3.0e38, -3.0e38, 1e-38, 65504.0, 1.0, -1.0],
+        dtype=dtype,
+    )
+    idx = rng.choice(n, size=min(n, 3 * specials.size), replace=False)
+    base[idx] = np.resize(specials, idx.size)
+    return base
+
+
+def run_helper_case(store, cases, name, container, contributions, exclude_vars=None, weigh_by_local_iter=True):
+    """contributions: list of (contributor_name, weight, {key: np.ndarray})"""
+    from nvflare.app_common.aggregators.weighted_aggregation_helper import WeightedAggregationHelper
+
+    helper = WeightedAggregationHelper(exclude_vars=exclude_vars, weigh_by_local_iter=weigh_by_local_iter)
+    rec = []
+    for cname, w, data in contributions:
+        dmap = {k: store.put(v, "in") for k, v in data.items()}
+        rec.append({"name": cname, "weight": w, "data": dmap})
+        helper.add({k: to_container(v, container) for k, v in data.items()}, w, cname, 0)
+    result = helper.get_result()
+    stats = helper.last_aggregation_stats
+    exp = {}
+    exp_dtype = {}
+    for k, v in result.items():
+        if isinstance(v, torch.Tensor):
+            exp_dtype[k] = str(v.dtype).replace("torch.", "")
+        else:
+            exp_dtype[k] = str(np.asarray(v).dtype)
+        exp[k] = store.put(v, "out")
+    cases.append(
+        {
+            "kind": "helper",
+            "name": name,
+            "container": container,
+            "exclude_vars": exclude_vars,
+            "weigh_by_local_iter": weigh_by_local_iter,
+            "contributions": rec,
+            "expected": exp,
+            "expected_dtype": exp_dtype,
+            "stats": stats,
+        }
+    )
+
+
+def run_intime_case(store, cases, name, container, clients, expected_data_kind, aggregation_weights=None, exclude_vars=None):
+    """clients: list of (contributor_name, {dxo_key or '': (n_iter, {key: array})})"""
+    from nvflare.apis.dxo import DXO, DataKind, MetaKey, from_shareable
+    from nvflare.apis.fl_constant import ReservedKey
+    from nvflare.apis.fl_context import FLContext
+    from nvflare.apis.shareable import Shareable
+    from nvflare.app_common.aggregators.intime_accumulate_model_aggregator import InTimeAccumulateWeightedAggregator
+    from nvflare.app_common.app_constant import AppConstants
+
+    agg = InTimeAccumulateWeightedAggregator(
+        exclude_vars=exclude_vars, aggregation_weights=aggregation_weights, expected_data_kind=expected_data_kind
+    )
+    agg._initialize(agg.aggregation_weights, agg.exclude_vars, agg.expected_data_kind)
+    fl_ctx = FLContext()
+    fl_ctx.set_prop(AppConstants.CURRENT_ROUND, 0)
+    rec = []
+    for cname, dxos in clients:
+        entry = {"name": cname, "dxos": {}}
+        if "" in dxos:
+            n_iter, data = dxos[""]
+            kind = expected_data_kind
+            dxo = DXO(kind, data={k: to_container(v, container) for k, v in data.items()}, meta={MetaKey.NUM_STEPS_CURRENT_ROUND: n_iter})
+            entry["dxos"][""] = {"n_iter": n_iter, "kind": kind, "data": {k: store.put(v, "in") for k, v in data.items()}}
+        else:
+            sub = {}
+            for dk, (n_iter, data) in dxos.items():
+                kind = expected_data_kind[dk]
+                sub[dk] = DXO(kind, data={k: to_container(v, container) for k, v in data.items()}, meta={MetaKey.NUM_STEPS_CURRENT_ROUND: n_iter})
+                entry["dxos"][dk] = {"n_iter": n_iter, "kind": kind, "data": {k: store.put(v, "in") for k, v in data.items()}}
+            dxo = DXO(DataKind.COLLECTION, data=sub)
+        s = Shareable()
+        s.set_peer_props({ReservedKey.IDENTITY_NAME: cname})
+        s.add_cookie(AppConstants.CONTRIBUTION_ROUND, 0)
+        entry["accepted"] = bool(agg.accept(dxo.update_shareable(s), fl_ctx))
+        rec.append(entry)
+    result = from_shareable(agg.aggregate(fl_ctx))
+    stats = fl_ctx.get_prop(AppConstants.AGGREGATION_STATS)
+    expected = {}
+    if result.data_kind == DataKind.COLLECTION:
+        for dk, sub in result.data.items():
+            expected[dk] = {"kind": sub.data_kind, "data": {k: store.put(v, "out") for k, v in sub.data.items()}}
+    else:
+        expected[""] = {"kind": result.data_kind, "data": {k: store.put(v, "out") for k, v in result.data.items()}}
+    cases.append(
+        {
+            "kind": "intime",
+            "name": name,
+            "container": container,
+            "expected_data_kind": expected_data_kind,
+            "aggregation_weights": aggregation_weights,
+            "exclude_vars": exclude_vars,
+            "clients": rec,
+            "expected": expected,
+            "stats": stats,
+        }
+    )
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--ref", default="/root/reference")
+    args = ap.parse_args()
+    install_shim(args.ref)
+    torch.set_num_threads(8)
+
+    rng = np.random.default_rng(20261015)
+    random.seed(20261015)
+    store = Store()
+    cases = []
+
+    def rweights(K):
+        # the reference tests' style: random.random() aggregation weight x integer NUM_STEPS
+        return [random.random() * float(random.randint(1, 50)) for _ in range(K)]
+
+    for container in ("numpy", "torch"):
+        # 1. plain fp32, ragged sizes, random weights
+        for K, P in ((1, 1003), (2, 1003), (8, 4099), (64, 2053)):
+            rows = [rng.standard_normal(P).astype(np.float32) for _ in range(K)]
+            ws = rweights(K)
+            run_helper_case(store, cases, f"{container}_f32_k{K}_p{P}", container,
+                            [(f"site-{i+1}", ws[i], {"w": rows[i]}) for i in range(K)])
+        # 2. synthetic weights of the bench (integers)
+        K, P = 16, 777
+        rows = [rng.standard_normal(P).astype(np.float32) for _ in range(K)]
+        ws = [1.0 * float(1 + (37 * k) % 100) for k in range(K)]
+        run_helper_case(store, cases, f"{container}_f32_intweights_k{K}", container,
+                        [(f"site-{i+1}", ws[i], {"w": rows[i]}) for i in range(K)])
+        # 3. special values: denormals, signed zeros, inf, nan, overflow; tiny and huge weights
+        K, P = 6, 509
+        rows = [special_values(rng, P) for _ in range(K)]
+        ws = [1e-30, 3.5, 1e30, 0.1, 7.0, 2.0 ** -126]
+        run_helper_case(store, cases, f"{container}_f32_special", container,
+                        [(f"site-{i+1}", ws[i], {"w": rows[i]}) for i in range(K)])
+        # 4. denormal-only path (results stay subnormal)
+        K, P = 4, 256
+        rows = [(rng.standard_normal(P) * 1e-39).astype(np.float32) for _ in range(K)]
+        ws = [0.75, 1.25, 3.0, 0.5]
+        run_helper_case(store, cases, f"{container}_f32_denormal", container,
+                        [(f"site-{i+1}", ws[i], {"w": rows[i]}) for i in range(K)])
+        # 5. unweighted (weigh_by_local_iter=False)
+        K, P = 5, 300
+        rows = [rng.standard_normal(P).astype(np.float32) for _ in range(K)]
+        ws = rweights(K)
+        run_helper_case(store, cases, f"{container}_f32_unweighted", container,
+                        [(f"site-{i+1}", ws[i], {"w": rows[i]}) for i in range(K)], weigh_by_local_iter=False)
+        # 6. fp64 inputs
+        K, P = 5, 37
+        rows = [rng.random(P) for _ in range(K)]
+        ws = rweights(K)
+        run_helper_case(store, cases, f"{container}_f64_k{K}", container,
+                        [(f"site-{i+1}", ws[i], {"w": rows[i]}) for i in range(K)])
+        # 7. int64 inputs (torch: promoted to fp32; numpy: promoted to fp64)
+        K, P = 3, 7
+        rows = [rng.integers(-1000, 1000, P).astype(np.int64) for _ in range(K)]
+        ws = [2.0, 3.0, 0.5]
+        run_helper_case(store, cases, f"{container}_i64_k{K}", container,
+                        [(f"site-{i+1}", ws[i], {"count": rows[i]}) for i in range(K)])
+        # 8. partial keys, shapes, 0-d and empty arrays
+        shapes = {"conv.weight": (4, 3, 3, 3), "conv.bias": (4,), "fc.weight": (10, 33), "scalar": (), "empty": (0,), "fc.bias": (10,)}
+        def mk(keys):
+            return {k: rng.standard_normal(shapes[k]).astype(np.float32) for k in keys}
+        contribs = [
+            ("site-1", 1.5, mk(["conv.weight", "conv.bias", "fc.weight", "scalar", "empty"])),
+            ("site-2", 2.0, mk(["conv.weight", "fc.weight", "fc.bias", "scalar"])),
+            ("site-3", 0.25, mk(["conv.bias", "fc.weight", "fc.bias", "empty"])),
+            ("site-4", 4.0, mk(["conv.weight", "conv.bias", "fc.weight", "fc.bias", "scalar", "empty"])),
+        ]
+        run_helper_case(store, cases, f"{container}_partial_keys", container, contribs)
+        # 9. exclude_vars
+        run_helper_case(store, cases, f"{container}_exclude_vars", container, contribs, exclude_vars="bias|scalar")
+        # 10. permuted arrival order of the same contributions (different bits)
+        K, P = 8, 1021
+        rows = [rng.standard_normal(P).astype(np.float32) for _ in range(K)]
+        ws = rweights(K)
+        base = [(f"site-{i+1}", ws[i], {"w": rows[i]}) for i in range(K)]
+        perm = list(rng.permutation(K))
+        run_helper_case(store, cases, f"{container}_order_a", container, base)
+        run_helper_case(store, cases, f"{container}_order_b", container, [base[i] for i in perm])
+        # 11. many keys with ragged sizes (flattened-arena packing)
+        sizes = [1, 3, 63, 64, 65, 127, 1000, 4097, 5]
+        K = 7
+        ws = rweights(K)
+        contribs = [(f"site-{i+1}", ws[i], {f"k{j}": rng.standard_normal(s).astype(np.float32) for j, s in enumerate(sizes)}) for i in range(K)]
+        run_helper_case(store, cases, f"{container}_many_keys", container, contribs)
+
+    # InTime-level flows (numpy containers, as the SAG numpy jobs deliver them)
+    for container in ("numpy", "torch"):
+        K = 6
+        names = [f"client_{i}" for i in range(K)]
+        aw = {n: random.random() for n in names}
+        clients = [(n, {"": (random.randint(1, 50), {"var1": rng.standard_normal((6, 6)).astype(np.float32)})}) for n in names]
+        run_intime_case(store, cases, f"{container}_intime_single", container, clients, "WEIGHT_DIFF", aggregation_weights=aw)
+        dk = {"dxo_0": "WEIGHT_DIFF", "dxo_1": "WEIGHTS"}
+        aw2 = {d: {n: random.random() for n in names} for d in dk}
+        clients = [(n, {d: (random.randint(1, 50), {"var1": rng.standard_normal(4).astype(np.float32), "bias": rng.standard_normal(3).astype(np.float32)}) for d in dk}) for n in names]
+        run_intime_case(store, cases, f"{container}_intime_collection", container, clients, dk, aggregation_weights=aw2, exclude_vars={"dxo_0": "bias", "dxo_1": ""})
+
+    np.savez_compressed(os.path.join(HERE, "helper_cases.npz"), **store.arrays)
+    with open(os.path.join(HERE, "helper_cases.json"), "w") as f:
+        json.dump({"generator": "tests/golden/make_golden.py", "reference": "NVFlare (/root/reference, ~2.9.0-dev)",
+                   "numpy": np.__version__, "torch": torch.__version__, "cases": cases}, f, indent=1, default=str)
+    print(f"wrote {len(cases)} cases, {len(store.arrays)} arrays")
+
+
+if __name__ == "__main__":
+    main()
