@@ -1,0 +1,258 @@
+#!/usr/bin/env python3
+"""Benchmark of the MI355X FedAvg weighted aggregation (BASELINE.json metric).
+
+One step = one aggregation: the arrival-ordered weighted accumulate-and-finalise kernel over K
+device-resident client rows of P fp32 params -> P fp32 results (weighted_aggregation_helper.py:153-240,
+torch-mode arithmetic by default).  Inputs are resident in HBM before the timed region starts.
+
+  python bench.py [--gpus N --steps K --warmup W]          # default: 64 clients x 1e9 params, 1 GPU
+  torchrun --nproc-per-node N bench.py --gpus N ...        # weak scaling: each GPU aggregates its own
+                                                           # 1e9-param bucket, no data-path collective
+
+Prints ONE JSON line (rank 0).  value = GiB/s aggregated = 4*K*P*N*steps / t / 2^30 with t the max over
+ranks of the barrier+synchronize bracketed wall time.  roofline.achieved uses the algorithmic bytes
+(4*K*P + 4*P per launch) over the average kernel duration measured with HIP events on the stream the
+kernel runs on.  cpu_baseline times the oracle restatement (torch CPU ops, all threads) on a bounded
+sample of the same workload, and the same leg spot-checks sampled device outputs bit-exactly against
+the oracle (test infrastructure; never the measured path).
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+METRIC = "GiB/s aggregated (device-resident FedAvg, K clients × P fp32 params); % HBM peak"
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--clients", type=int, default=64)
+    ap.add_argument("--params", type=float, default=1e9, help="fp32 params per GPU bucket")
+    ap.add_argument("--mode", choices=["torch", "numpy"], default="torch")
+    ap.add_argument("--blocks-per-cu", type=int, default=0)
+    ap.add_argument("--unroll", type=int, default=0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-sample-params", type=int, default=8 * 1024 * 1024)
+    ap.add_argument("--spot-check", type=int, default=4096, help="sampled outputs checked against the oracle")
+    ap.add_argument("--traffic-bytes", type=float, default=None,
+                    help="HBM bytes per launch from a separate rocprofv3 --pmc pass (reported in roofline.traffic)")
+    ap.add_argument("--seed", type=int, default=1000)
+    return ap.parse_args()
+
+
+def dist_setup(args):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+
+    if world > 1:
+        import torch.distributed as dist
+
+        torch.cuda.set_device(local)
+        dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
+    if world != args.gpus and rank == 0:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
+    return world, rank, local
+
+
+def barrier_sync(world, ctx):
+    import torch
+
+    ctx.sync()
+    torch.cuda.synchronize()
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.barrier()
+
+
+def max_over_ranks(world, value: float) -> float:
+    if world == 1:
+        return value
+    import torch
+    import torch.distributed as dist
+
+    t = torch.tensor([value], dtype=torch.float64, device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def cpu_baseline_and_spot_check(args, ctx, rows, out_buf, weights, count, P, col0, op):
+    """Oracle leg (test infrastructure): time the reference restatement on the host, then check sampled
+    device outputs bit-for-bit against the oracle computed from the host twin of the generator."""
+    import torch
+
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from oracle import fedavg_oracle as orc
+
+    K = len(rows)
+    res = {}
+    # -- spot check at full size -----------------------------------------------------------------
+    if args.spot_check > 0:
+        rng = np.random.default_rng(7)
+        idx = np.unique(np.concatenate([rng.integers(0, P, args.spot_check, dtype=np.int64), [0, P - 1]]))
+        host_rows = [orc.synth_values(args.seed, k, (idx + col0).astype(np.uint64)) for k in range(K)]
+        mode = orc.MODE_TORCH if op == 1 else orc.MODE_NUMPY
+        exp = orc.fedavg_c(host_rows, weights, mode)
+        got = ctx.gather_f32(out_buf.ptr, idx.astype(np.uint64))
+        mism = int(np.count_nonzero(exp.view(np.uint32) != got.view(np.uint32)))
+        res["spot_check"] = {"sampled": int(idx.size), "mismatches": mism, "oracle": "oracle/fedavg_oracle.c"}
+    # -- CPU baseline: the reference's torch CPU op sequence on a bounded sample ------------------
+    if not args.no_cpu_baseline:
+        Ps = int(min(args.cpu_sample_params, P))
+        gen = [np.random.default_rng(1000 + k).standard_normal(Ps, dtype=np.float32) for k in range(K)]
+        trows = [torch.from_numpy(g) for g in gen]
+        threads = torch.get_num_threads()
+        reps, t_tot = 0, 0.0
+        while t_tot < 10.0 and reps < 200:
+            t0 = time.perf_counter()
+            if op == 1:
+                orc.torch_mode_reference(trows, weights)
+            else:
+                orc.numpy_mode_reference(gen, weights)
+            t_tot += time.perf_counter() - t0
+            reps += 1
+        gibs = 4.0 * K * Ps * reps / t_tot / 2**30
+        # single-thread numpy restatement (the numpy-job path) for context
+        t0 = time.perf_counter()
+        orc.numpy_mode_reference(gen, weights)
+        t_np = time.perf_counter() - t0
+        res["cpu_baseline"] = {
+            "value": round(gibs, 3),
+            "unit": "GiB/s",
+            "cores": threads if op == 1 else 1,
+            "kind": "port",
+            "sample": f"{K} clients x {Ps} fp32 params (numpy default_rng(1000+k) N(0,1)), "
+                      f"{'torch CPU mul/add_(alpha)/div_' if op == 1 else 'numpy v*w / t+v*w / t*(1/c)'} "
+                      f"restatement of weighted_aggregation_helper.py:181-236, {reps} reps in {t_tot:.1f}s",
+            "numpy_single_thread_GiBs": round(4.0 * K * Ps / t_np / 2**30, 3),
+            "host_cpu_count": os.cpu_count(),
+        }
+    return res
+
+
+def main():
+    args = parse()
+    world, rank, local = dist_setup(args)
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from nvflare_amd import _native as N
+    from nvflare_amd.device import DeviceContext
+
+    ctx = DeviceContext.get(local)
+    if args.blocks_per_cu or args.unroll:
+        ctx.set_launch(args.blocks_per_cu, args.unroll)
+    K = int(args.clients)
+    P = int(args.params)
+    op = N.FEDAVG_OP_TORCH if args.mode == "torch" else N.FEDAVG_OP_NUMPY
+    fin = N.FEDAVG_FIN_DIV if args.mode == "torch" else N.FEDAVG_FIN_SCALE
+    col0 = rank * P  # weak scaling: rank r owns param bucket [r*P, (r+1)*P)
+
+    free, total = ctx.mem_info()
+    need = (K + 1) * P * 4
+    if need > free:
+        raise SystemExit(f"rank {rank}: workload needs {need / 2**30:.1f} GiB, device has {free / 2**30:.1f} GiB free")
+
+    # stacked client rows [K][P] (one allocation per client slot) + the result bucket
+    rows = [ctx.alloc(P * 4) for _ in range(K)]
+    out = ctx.alloc(P * 4)
+    for k, b in enumerate(rows):
+        ctx.fill_synthetic_f32(b.ptr, P, args.seed, k, col0)
+    ctx.sync()
+    # per-client weights: aggregation_weight 1.0 x NUM_STEPS_CURRENT_ROUND = 1 + (37k mod 100)
+    weights = [1.0 * float(1 + (37 * k) % 100) for k in range(K)]
+    count = None
+    for w in weights:
+        count = w if count is None else count + w
+    ptrs = [b.ptr for b in rows]
+
+    def step():
+        ctx.accumulate(ptrs, weights, P, out.ptr, N.FEDAVG_F32, N.FEDAVG_F32, op, fin, count)
+
+    for _ in range(args.warmup):
+        step()
+    barrier_sync(world, ctx)
+
+    ctx.timing_begin()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    barrier_sync(world, ctx)
+    t1 = time.perf_counter()
+    ev_ms = ctx.timing_end()
+
+    wall = max_over_ranks(world, t1 - t0)
+    kernel_ms = ev_ms / args.steps
+    kernel_ms_max = max_over_ranks(world, kernel_ms)
+
+    extra = {}
+    if rank == 0 and world == 1:
+        extra = cpu_baseline_and_spot_check(args, ctx, rows, out, weights, count, P, col0, op)
+
+    if rank == 0:
+        bytes_step = 4.0 * K * P * world  # aggregated client bytes per step, all ranks
+        value = bytes_step * args.steps / wall / 2**30
+        alg_bytes_launch = 4.0 * K * P + 4.0 * P
+        achieved = alg_bytes_launch / (kernel_ms / 1e3) / 1e9
+        line = {
+            "metric": METRIC,
+            "value": round(value, 2),
+            "unit": "GiB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(wall / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic: device counter-hash generator (Irwin-Hall(4) ~N(0,1)), host twin in oracle/",
+            "config": {
+                "workload": f"{K} clients x {P} fp32 params per GPU, weighted FedAvg, {args.mode}-mode arithmetic",
+                "clients": K,
+                "params_per_gpu": P,
+                "mode": args.mode,
+                "parallelism": f"param-bucket shards x{world}, no data-path collective",
+            },
+            "pct_hbm_peak": round(100.0 * achieved / HBM_PEAK_GBS, 2),
+            "roofline": {
+                "bound": "hbm",
+                "achieved": round(achieved, 1),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": args.traffic_bytes,
+                "kernel_ms_avg": round(kernel_ms, 4),
+                "kernel_ms_avg_max_rank": round(kernel_ms_max, 4),
+                "alg_bytes_per_launch": alg_bytes_launch,
+            },
+        }
+        if "cpu_baseline" in extra:
+            line["cpu_baseline"] = extra["cpu_baseline"]
+        else:
+            line["cpu_baseline"] = None
+        if "spot_check" in extra:
+            line["spot_check"] = extra["spot_check"]
+        print(json.dumps(line), flush=True)
+        if "spot_check" in extra and extra["spot_check"]["mismatches"]:
+            print("SPOT CHECK FAILED", file=sys.stderr)
+            sys.exit(3)
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,134 @@
+/*
+ * nvflare_amd_fedavg.h -- C-ABI of the MI355X (gfx950) FedAvg weighted-aggregation library
+ * (libnvflare_amd_fedavg.so).
+ *
+ * This is the drop-in boundary: NVFlare's Aggregator surface is Python
+ * (nvflare/app_common/abstract/aggregator.py:22-58); the Python adapter in nvflare_amd/ binds the
+ * entry points below with ctypes (INTEGRATION.md shows the binding).  The reference has no native
+ * code on this path: every entry point replaces a Python/numpy/torch operation, cited per function.
+ *
+ * Conventions follow the reference's own C-ABI (integration/xgboost/encryption_plugins/shared/
+ * plugins/plugin_main.cc:24-111): an opaque handle, int return code (0 = success), a thread-local
+ * error string (fedavg_last_error), and no C++ exception ever crosses the ABI.  Plain pointers and
+ * sizes only; no torch types.  One handle is used by one host thread at a time (the adapter holds a
+ * lock, mirroring weighted_aggregation_helper.py:162,228).
+ *
+ * Device pointers passed to fedavg_accumulate may come from fedavg_malloc or from any other HIP
+ * allocation on the handle's device (e.g. a torch tensor's data_ptr(): zero-copy hand-off).
+ */
+#ifndef NVFLARE_AMD_FEDAVG_H
+#define NVFLARE_AMD_FEDAVG_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FEDAVG_ABI_VERSION 1
+
+/* element types of client rows (in_dtype) and of the running sum / result (acc_dtype) */
+enum fedavg_dtype {
+    FEDAVG_F32 = 0,
+    FEDAVG_F64 = 1,
+    FEDAVG_I32 = 2,
+    FEDAVG_I64 = 3,
+};
+
+/* per-step arithmetic, reference weighted_aggregation_helper.py:
+ *   FEDAVG_OP_NUMPY      first T = v*w, then T = T + v*w  (two roundings per step)   :188-193, :210-214
+ *   FEDAVG_OP_TORCH      first T = v*w, then T = fma(v, w, T) (torch add_ alpha)     :181-187, :203-209
+ *   FEDAVG_OP_UNWEIGHTED first T = v,   then T = T + v (weigh_by_local_iter=False)   :186-199, :208-215 */
+enum fedavg_op {
+    FEDAVG_OP_NUMPY = 0,
+    FEDAVG_OP_TORCH = 1,
+    FEDAVG_OP_UNWEIGHTED = 2,
+};
+
+/* finalisation after the last row, reference get_result (:226-240):
+ *   FEDAVG_FIN_NONE   keep the running sum (a later call continues it through acc_in)
+ *   FEDAVG_FIN_SCALE  numpy: T * acc_t(1.0 / count)                                   :236
+ *   FEDAVG_FIN_DIV    torch: T / acc_t(count), correctly rounded                         :233 */
+enum fedavg_fin {
+    FEDAVG_FIN_NONE = 0,
+    FEDAVG_FIN_SCALE = 1,
+    FEDAVG_FIN_DIV = 2,
+};
+
+typedef struct fedavg_ctx fedavg_ctx;
+
+/* Last error message of the calling thread ("" if none). */
+const char* fedavg_last_error(void);
+int fedavg_abi_version(void);
+int fedavg_device_count(int* n);
+
+/* Handle bound to one HIP device: owns a compute stream, a copy stream, timing events and a pinned
+ * staging ring for pageable host buffers. */
+int fedavg_create(int device, fedavg_ctx** out);
+int fedavg_destroy(fedavg_ctx* ctx);
+int fedavg_device_info(fedavg_ctx* ctx, int* num_cus, size_t* free_bytes, size_t* total_bytes);
+
+/* Run compute work on an external HIP stream (e.g. torch.cuda.current_stream().cuda_stream);
+ * NULL restores the handle's own stream. */
+int fedavg_set_stream(fedavg_ctx* ctx, void* stream);
+int fedavg_get_stream(fedavg_ctx* ctx, void** stream);
+
+/* Device memory owned by the caller through this handle. */
+int fedavg_malloc(fedavg_ctx* ctx, size_t nbytes, void** dptr);
+int fedavg_free(fedavg_ctx* ctx, void* dptr);
+
+/* Stage client bytes into device memory (replaces the host-side arrays that
+ * weighted_aggregation_helper.py:170-216 reads).  Pageable sources are copied through the pinned
+ * ring with the DMA overlapped; on return the caller may reuse `src` (the aggregator must not alias
+ * caller arrays, weighted_aggregation_helper.py:181-199).  Later compute on the handle is ordered
+ * after the copy. */
+int fedavg_h2d(fedavg_ctx* ctx, void* dst, const void* src, size_t nbytes);
+/* dst_pitch/src_pitch/width in bytes, `height` rows: strided H2D (tiled slabs). */
+int fedavg_h2d_2d(fedavg_ctx* ctx, void* dst, size_t dst_pitch, const void* src, size_t src_pitch,
+                  size_t width, size_t height);
+/* Device -> host; returns when the bytes are in `dst` (waits for prior compute on the handle). */
+int fedavg_d2h(fedavg_ctx* ctx, void* dst, const void* src, size_t nbytes);
+int fedavg_d2d(fedavg_ctx* ctx, void* dst, const void* src, size_t nbytes);
+int fedavg_memset(fedavg_ctx* ctx, void* dst, int value, size_t nbytes);
+int fedavg_sync(fedavg_ctx* ctx);
+
+/* THE HOT PATH.  For every element i < n, in arrival order k = 0..k_rows-1:
+ *   acc = acc_in ? acc_in[i] : first(rows[0][i])      (first row consumed when acc_in == NULL)
+ *   acc = step(acc, rows[k][i], acc_t(weights[k]))
+ *   out[i] = fin(acc)
+ * rows: host array of k_rows DEVICE pointers, each to n elements of in_dtype.
+ * weights: host array of k_rows fp64 weights; rounded to acc_dtype as the reference does.
+ * count: fp64 arrival-order sum of weights (weighted_aggregation_helper.py:201,216), used by fin.
+ * acc_in may equal out (in-place continuation).  Any k_rows >= 0 (k_rows == 0 needs acc_in).
+ * Supported (in_dtype, acc_dtype): (F32,F32) vectorised fast path; (F64,F64); (F32,F64);
+ * (I32|I64, F32); (I32|I64, F64). */
+int fedavg_accumulate(fedavg_ctx* ctx, const void* const* rows, const double* weights, int k_rows,
+                      const void* acc_in, void* out, size_t n, int in_dtype, int acc_dtype, int op,
+                      int fin, double count);
+
+/* Timing of the kernels launched by the last fedavg_accumulate call, measured with HIP events on
+ * the stream they ran on (enable first; costs two event records per call). */
+int fedavg_set_timing(fedavg_ctx* ctx, int enable);
+int fedavg_last_kernel_ms(fedavg_ctx* ctx, float* ms);
+
+/* Event bracket over a region of compute-stream work (e.g. K back-to-back fedavg_accumulate calls):
+ * begin records a start event, end records a stop event, waits for it and returns the elapsed ms. */
+int fedavg_timing_begin(fedavg_ctx* ctx);
+int fedavg_timing_end(fedavg_ctx* ctx, float* ms);
+
+/* Launch tuning (0 = default): blocks per CU of the streaming kernel, rows unrolled per group. */
+int fedavg_set_launch(fedavg_ctx* ctx, int blocks_per_cu, int unroll);
+
+/* Synthetic inputs for benchmarks/tests: dst[j] = synth(seed, row, col0 + j), fp32, bit-identical
+ * to the host twin oracle_synth_value() in oracle/fedavg_oracle.c. */
+int fedavg_fill_synthetic_f32(fedavg_ctx* ctx, float* dst, size_t n, uint64_t seed, uint64_t row,
+                              uint64_t col0);
+/* Gather m fp32 elements src[idx[j]] (idx: host array) into host_out (spot checks at full size). */
+int fedavg_gather_f32(fedavg_ctx* ctx, const float* src, const uint64_t* idx, size_t m, float* host_out);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* NVFLARE_AMD_FEDAVG_H */

@@ -1,0 +1,56 @@
+"""Build libnvflare_amd_fedavg.so in-tree with hipcc for gfx950 (no torch, no cmake).
+
+The library lands in nvflare_amd/lib/ so that it travels with the repository snapshot to the GPU box
+(git-ignored, not gpurun-ignored)."""
+
+from __future__ import annotations
+
+import os
+import subprocess
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(PKG)
+CSRC = os.path.join(PKG, "csrc")
+LIB_DIR = os.path.join(PKG, "lib")
+LIB_NAME = "libnvflare_amd_fedavg.so"
+LIB_PATH = os.path.join(LIB_DIR, LIB_NAME)
+SOURCES = ["fedavg_kernels.hip", "fedavg_capi.cpp"]
+HEADERS = ["fedavg_internal.h"]
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = "gfx950"
+
+# -ffp-contract=off: the numpy-mode multiply and add must round separately (bit parity with the
+# reference); the torch mode uses explicit fma builtins.  No fast-math: IEEE division, denormals kept.
+FLAGS = ["-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off", "-fno-fast-math", f"--offload-arch={ARCH}",
+         "-Wall", "-Wno-unused-command-line-argument"]
+
+
+def _inputs():
+    files = [os.path.join(CSRC, s) for s in SOURCES + HEADERS]
+    files.append(os.path.join(ROOT, "include", "nvflare_amd_fedavg.h"))
+    return files
+
+
+def needs_build() -> bool:
+    if not os.path.exists(LIB_PATH):
+        return True
+    t = os.path.getmtime(LIB_PATH)
+    return any(os.path.getmtime(f) > t for f in _inputs())
+
+
+def build_library(force: bool = False, verbose: bool = False) -> str:
+    if not force and not needs_build():
+        return LIB_PATH
+    os.makedirs(LIB_DIR, exist_ok=True)
+    tmp = LIB_PATH + ".tmp"
+    cmd = [HIPCC, *FLAGS, f"-I{os.path.join(ROOT, 'include')}", f"-I{CSRC}",
+           *[os.path.join(CSRC, s) for s in SOURCES], "-o", tmp, "-lpthread"]
+    if verbose:
+        print(" ".join(cmd))
+    subprocess.run(cmd, check=True)
+    os.replace(tmp, LIB_PATH)
+    return LIB_PATH
+
+
+if __name__ == "__main__":
+    print(build_library(force=True, verbose=True))

@@ -1,0 +1,139 @@
+"""ctypes binding of libnvflare_amd_fedavg.so (include/nvflare_amd_fedavg.h).
+
+There is no CPU fallback: if the HIP library is missing or cannot be loaded, every entry point raises.
+``import torch`` happens first when torch is importable, so that the process has ONE HIP runtime:
+torch ships its own ``libamdhip64.so.7`` and the dynamic loader then binds this library's
+``libamdhip64.so.7`` dependency to the already-loaded copy (same SONAME).
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+from ._build import LIB_PATH
+
+try:  # share torch's HIP runtime when torch is present (see module docstring)
+    import torch  # noqa: F401
+except Exception:  # pragma: no cover - torch is part of the image
+    torch = None
+
+FEDAVG_F32 = 0
+FEDAVG_F64 = 1
+FEDAVG_I32 = 2
+FEDAVG_I64 = 3
+
+FEDAVG_OP_NUMPY = 0
+FEDAVG_OP_TORCH = 1
+FEDAVG_OP_UNWEIGHTED = 2
+
+FEDAVG_FIN_NONE = 0
+FEDAVG_FIN_SCALE = 1
+FEDAVG_FIN_DIV = 2
+
+ABI_VERSION = 1
+
+c_void_p = ctypes.c_void_p
+c_int = ctypes.c_int
+c_size_t = ctypes.c_size_t
+c_u64 = ctypes.c_uint64
+c_double = ctypes.c_double
+c_float = ctypes.c_float
+
+# name -> argtypes (every function returns int rc, except the two noted)
+_SIGNATURES = {
+    "fedavg_device_count": [ctypes.POINTER(c_int)],
+    "fedavg_create": [c_int, ctypes.POINTER(c_void_p)],
+    "fedavg_destroy": [c_void_p],
+    "fedavg_device_info": [c_void_p, ctypes.POINTER(c_int), ctypes.POINTER(c_size_t), ctypes.POINTER(c_size_t)],
+    "fedavg_set_stream": [c_void_p, c_void_p],
+    "fedavg_get_stream": [c_void_p, ctypes.POINTER(c_void_p)],
+    "fedavg_malloc": [c_void_p, c_size_t, ctypes.POINTER(c_void_p)],
+    "fedavg_free": [c_void_p, c_void_p],
+    "fedavg_h2d": [c_void_p, c_void_p, c_void_p, c_size_t],
+    "fedavg_h2d_2d": [c_void_p, c_void_p, c_size_t, c_void_p, c_size_t, c_size_t, c_size_t],
+    "fedavg_d2h": [c_void_p, c_void_p, c_void_p, c_size_t],
+    "fedavg_d2d": [c_void_p, c_void_p, c_void_p, c_size_t],
+    "fedavg_memset": [c_void_p, c_void_p, c_int, c_size_t],
+    "fedavg_sync": [c_void_p],
+    "fedavg_accumulate": [
+        c_void_p,  # ctx
+        ctypes.POINTER(c_void_p),  # rows
+        ctypes.POINTER(c_double),  # weights
+        c_int,  # k_rows
+        c_void_p,  # acc_in
+        c_void_p,  # out
+        c_size_t,  # n
+        c_int,  # in_dtype
+        c_int,  # acc_dtype
+        c_int,  # op
+        c_int,  # fin
+        c_double,  # count
+    ],
+    "fedavg_set_timing": [c_void_p, c_int],
+    "fedavg_last_kernel_ms": [c_void_p, ctypes.POINTER(c_float)],
+    "fedavg_timing_begin": [c_void_p],
+    "fedavg_timing_end": [c_void_p, ctypes.POINTER(c_float)],
+    "fedavg_set_launch": [c_void_p, c_int, c_int],
+    "fedavg_fill_synthetic_f32": [c_void_p, c_void_p, c_size_t, c_u64, c_u64, c_u64],
+    "fedavg_gather_f32": [c_void_p, c_void_p, c_void_p, c_size_t, c_void_p],
+}
+EXPORTED = ["fedavg_last_error", "fedavg_abi_version", *_SIGNATURES.keys()]
+
+
+class FedAvgError(RuntimeError):
+    """An error reported by the HIP library (its fedavg_last_error string)."""
+
+
+_lib = None
+_lib_lock = threading.Lock()
+
+
+def lib_path() -> str:
+    return os.environ.get("NVFLARE_AMD_FEDAVG_LIB", LIB_PATH)
+
+
+def load():
+    """Load the HIP library (raises if it is missing: there is no CPU fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lib_lock:
+        if _lib is not None:
+            return _lib
+        path = lib_path()
+        if not os.path.exists(path):
+            raise FedAvgError(
+                f"HIP library {path} is missing; build it with `python -m nvflare_amd._build` "
+                "(hipcc --offload-arch=gfx950). nvflare_amd has no CPU fallback."
+            )
+        lib = ctypes.CDLL(path)
+        lib.fedavg_last_error.restype = ctypes.c_char_p
+        lib.fedavg_last_error.argtypes = []
+        lib.fedavg_abi_version.restype = c_int
+        lib.fedavg_abi_version.argtypes = []
+        for name, argtypes in _SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.restype = c_int
+            fn.argtypes = argtypes
+        if lib.fedavg_abi_version() != ABI_VERSION:
+            raise FedAvgError(f"ABI mismatch: library {lib.fedavg_abi_version()} != python {ABI_VERSION}")
+        _lib = lib
+        return lib
+
+
+def check(rc: int, what: str = "") -> None:
+    if rc != 0:
+        msg = load().fedavg_last_error().decode(errors="replace")
+        raise FedAvgError(f"{what}: {msg}" if what else msg)
+
+
+def call(name: str, *args) -> None:
+    check(getattr(load(), name)(*args), name)
+
+
+def device_count() -> int:
+    n = c_int(0)
+    call("fedavg_device_count", ctypes.byref(n))
+    return n.value

@@ -1,0 +1,58 @@
+"""NVFlare API types for the drop-in: the real ``nvflare`` classes when importable, so the GPU
+aggregator plugs into a live NVFlare server unchanged; otherwise the minimal stand-ins in
+``_standins.py``.  ``NVFLARE_AMD_FORCE_STANDINS=1`` forces the stand-ins."""
+
+from __future__ import annotations
+
+import os
+
+HAVE_NVFLARE = False
+if os.environ.get("NVFLARE_AMD_FORCE_STANDINS", "0") != "1":
+    try:
+        from nvflare.apis.dxo import DXO, DataKind, MetaKey, from_shareable  # noqa: F401
+        from nvflare.apis.event_type import EventType  # noqa: F401
+        from nvflare.apis.fl_component import FLComponent  # noqa: F401
+        from nvflare.apis.fl_constant import ReservedKey, ReturnCode  # noqa: F401
+        from nvflare.apis.fl_context import FLContext  # noqa: F401
+        from nvflare.apis.shareable import Shareable  # noqa: F401
+        from nvflare.app_common.abstract.aggregator import Aggregator  # noqa: F401
+        from nvflare.app_common.app_constant import AppConstants  # noqa: F401
+        from nvflare.fuel.utils.log_utils import get_module_logger  # noqa: F401
+
+        HAVE_NVFLARE = True
+    except Exception:
+        HAVE_NVFLARE = False
+
+if not HAVE_NVFLARE:
+    from ._standins import (  # noqa: F401
+        DXO,
+        Aggregator,
+        AppConstants,
+        DataKind,
+        EventType,
+        FLComponent,
+        FLContext,
+        MetaKey,
+        ReservedKey,
+        ReturnCode,
+        Shareable,
+        from_shareable,
+        get_module_logger,
+    )
+
+__all__ = [
+    "HAVE_NVFLARE",
+    "DXO",
+    "Aggregator",
+    "AppConstants",
+    "DataKind",
+    "EventType",
+    "FLComponent",
+    "FLContext",
+    "MetaKey",
+    "ReservedKey",
+    "ReturnCode",
+    "Shareable",
+    "from_shareable",
+    "get_module_logger",
+]

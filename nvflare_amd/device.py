@@ -1,0 +1,200 @@
+"""Device handle and device buffers over the C-ABI (one handle per HIP device, shared per process)."""
+
+from __future__ import annotations
+
+import ctypes
+import threading
+import weakref
+from typing import Dict, Optional, Sequence
+
+import numpy as np
+
+from . import _native as N
+
+_NP_TO_DT = {
+    np.dtype(np.float32): N.FEDAVG_F32,
+    np.dtype(np.float64): N.FEDAVG_F64,
+    np.dtype(np.int32): N.FEDAVG_I32,
+    np.dtype(np.int64): N.FEDAVG_I64,
+}
+
+
+def fedavg_dtype(dt) -> int:
+    dt = np.dtype(dt)
+    if dt not in _NP_TO_DT:
+        raise TypeError(f"nvflare_amd: dtype {dt} has no device kernel")
+    return _NP_TO_DT[dt]
+
+
+class DeviceBuffer:
+    """Device memory owned through a DeviceContext; freed on close() or garbage collection."""
+
+    __slots__ = ("ctx", "ptr", "nbytes", "_fin", "__weakref__")
+
+    def __init__(self, ctx: "DeviceContext", nbytes: int):
+        self.ctx = ctx
+        self.nbytes = int(nbytes)
+        p = ctypes.c_void_p(0)
+        N.call("fedavg_malloc", ctx.handle, ctypes.c_size_t(self.nbytes), ctypes.byref(p))
+        self.ptr = p.value or 0
+        self._fin = weakref.finalize(self, DeviceContext._free_ptr, ctx, self.ptr)
+
+    def close(self) -> None:
+        if self._fin.alive:
+            self._fin()
+        self.ptr = 0
+
+    def __repr__(self) -> str:
+        return f"DeviceBuffer(ptr=0x{self.ptr:x}, nbytes={self.nbytes}, device={self.ctx.device})"
+
+
+class DeviceContext:
+    """Python view of a fedavg_ctx (C-ABI handle) bound to one device."""
+
+    _instances: Dict[int, "DeviceContext"] = {}
+    _instances_lock = threading.Lock()
+
+    def __init__(self, device: int = 0):
+        self.device = int(device)
+        h = ctypes.c_void_p(0)
+        N.call("fedavg_create", ctypes.c_int(self.device), ctypes.byref(h))
+        self.handle = h.value
+        self.lock = threading.RLock()
+        ncu = ctypes.c_int(0)
+        free = ctypes.c_size_t(0)
+        total = ctypes.c_size_t(0)
+        N.call("fedavg_device_info", self.handle, ctypes.byref(ncu), ctypes.byref(free), ctypes.byref(total))
+        self.num_cus = ncu.value
+        self.total_bytes = total.value
+
+    # -- shared per-process handles ------------------------------------------------------------
+    @classmethod
+    def get(cls, device: int = 0) -> "DeviceContext":
+        with cls._instances_lock:
+            ctx = cls._instances.get(device)
+            if ctx is None:
+                ctx = cls(device)
+                cls._instances[device] = ctx
+            return ctx
+
+    @staticmethod
+    def _free_ptr(ctx: "DeviceContext", ptr: int) -> None:
+        if ptr and ctx.handle:
+            try:
+                N.call("fedavg_free", ctx.handle, ctypes.c_void_p(ptr))
+            except Exception:
+                pass
+
+    def close(self) -> None:
+        if self.handle:
+            N.call("fedavg_destroy", self.handle)
+            self.handle = None
+
+    # -- memory / copies -------------------------------------------------------------------------
+    def mem_info(self):
+        free = ctypes.c_size_t(0)
+        total = ctypes.c_size_t(0)
+        N.call("fedavg_device_info", self.handle, None, ctypes.byref(free), ctypes.byref(total))
+        return free.value, total.value
+
+    def alloc(self, nbytes: int) -> DeviceBuffer:
+        return DeviceBuffer(self, nbytes)
+
+    def h2d(self, dst_ptr: int, host: np.ndarray) -> None:
+        host = np.ascontiguousarray(host)
+        if host.nbytes:
+            N.call("fedavg_h2d", self.handle, ctypes.c_void_p(dst_ptr), ctypes.c_void_p(host.ctypes.data),
+                   ctypes.c_size_t(host.nbytes))
+
+    def h2d_ptr(self, dst_ptr: int, src_ptr: int, nbytes: int) -> None:
+        if nbytes:
+            N.call("fedavg_h2d", self.handle, ctypes.c_void_p(dst_ptr), ctypes.c_void_p(src_ptr), ctypes.c_size_t(nbytes))
+
+    def d2h(self, host: np.ndarray, src_ptr: int) -> None:
+        if not host.flags.c_contiguous:
+            raise ValueError("d2h destination must be C-contiguous")
+        if host.nbytes:
+            N.call("fedavg_d2h", self.handle, ctypes.c_void_p(host.ctypes.data), ctypes.c_void_p(src_ptr),
+                   ctypes.c_size_t(host.nbytes))
+
+    def d2h_ptr(self, dst_ptr: int, src_ptr: int, nbytes: int) -> None:
+        if nbytes:
+            N.call("fedavg_d2h", self.handle, ctypes.c_void_p(dst_ptr), ctypes.c_void_p(src_ptr), ctypes.c_size_t(nbytes))
+
+    def d2d(self, dst_ptr: int, src_ptr: int, nbytes: int) -> None:
+        if nbytes:
+            N.call("fedavg_d2d", self.handle, ctypes.c_void_p(dst_ptr), ctypes.c_void_p(src_ptr), ctypes.c_size_t(nbytes))
+
+    def sync(self) -> None:
+        N.call("fedavg_sync", self.handle)
+
+    def set_stream(self, stream_ptr: Optional[int]) -> None:
+        N.call("fedavg_set_stream", self.handle, ctypes.c_void_p(stream_ptr or 0))
+
+    def stream(self) -> int:
+        s = ctypes.c_void_p(0)
+        N.call("fedavg_get_stream", self.handle, ctypes.byref(s))
+        return s.value or 0
+
+    # -- compute ---------------------------------------------------------------------------------
+    def accumulate(
+        self,
+        rows: Sequence[int],
+        weights: Sequence[float],
+        n: int,
+        out_ptr: int,
+        in_dtype: int,
+        acc_dtype: int,
+        op: int,
+        fin: int,
+        count: float = 1.0,
+        acc_in_ptr: Optional[int] = None,
+    ) -> None:
+        k = len(rows)
+        rows_arr = (ctypes.c_void_p * max(k, 1))(*rows)
+        w_arr = (ctypes.c_double * max(k, 1))(*[float(w) for w in weights])
+        N.call(
+            "fedavg_accumulate",
+            self.handle,
+            rows_arr,
+            w_arr,
+            ctypes.c_int(k),
+            ctypes.c_void_p(acc_in_ptr or 0),
+            ctypes.c_void_p(out_ptr),
+            ctypes.c_size_t(n),
+            ctypes.c_int(in_dtype),
+            ctypes.c_int(acc_dtype),
+            ctypes.c_int(op),
+            ctypes.c_int(fin),
+            ctypes.c_double(float(count)),
+        )
+
+    def set_timing(self, enable: bool) -> None:
+        N.call("fedavg_set_timing", self.handle, ctypes.c_int(1 if enable else 0))
+
+    def last_kernel_ms(self) -> float:
+        ms = ctypes.c_float(0.0)
+        N.call("fedavg_last_kernel_ms", self.handle, ctypes.byref(ms))
+        return float(ms.value)
+
+    def timing_begin(self) -> None:
+        N.call("fedavg_timing_begin", self.handle)
+
+    def timing_end(self) -> float:
+        ms = ctypes.c_float(0.0)
+        N.call("fedavg_timing_end", self.handle, ctypes.byref(ms))
+        return float(ms.value)
+
+    def set_launch(self, blocks_per_cu: int = 0, unroll: int = 0) -> None:
+        N.call("fedavg_set_launch", self.handle, ctypes.c_int(blocks_per_cu), ctypes.c_int(unroll))
+
+    def fill_synthetic_f32(self, dst_ptr: int, n: int, seed: int, row: int, col0: int = 0) -> None:
+        N.call("fedavg_fill_synthetic_f32", self.handle, ctypes.c_void_p(dst_ptr), ctypes.c_size_t(n),
+               ctypes.c_uint64(seed), ctypes.c_uint64(row), ctypes.c_uint64(col0))
+
+    def gather_f32(self, src_ptr: int, idx: np.ndarray) -> np.ndarray:
+        idx = np.ascontiguousarray(idx, dtype=np.uint64)
+        out = np.empty(idx.size, dtype=np.float32)
+        N.call("fedavg_gather_f32", self.handle, ctypes.c_void_p(src_ptr), ctypes.c_void_p(idx.ctypes.data),
+               ctypes.c_size_t(idx.size), ctypes.c_void_p(out.ctypes.data))
+        return out
