@@ -71,12 +71,29 @@ _SIGNATURES = {
         c_int,  # fin
         c_double,  # count
     ],
+    "fedavg_accumulate_tiled": [
+        c_void_p,  # ctx
+        c_void_p,  # slab
+        c_int,  # k_max
+        c_size_t,  # tile_elems
+        ctypes.POINTER(c_int),  # slots
+        ctypes.POINTER(c_double),  # weights
+        c_int,  # k_rows
+        c_void_p,  # acc_in
+        c_void_p,  # out
+        c_size_t,  # n
+        c_int,  # op
+        c_int,  # fin
+        c_double,  # count
+    ],
     "fedavg_set_timing": [c_void_p, c_int],
     "fedavg_last_kernel_ms": [c_void_p, ctypes.POINTER(c_float)],
     "fedavg_timing_begin": [c_void_p],
     "fedavg_timing_end": [c_void_p, ctypes.POINTER(c_float)],
     "fedavg_set_launch": [c_void_p, c_int, c_int],
+    "fedavg_set_variant": [c_void_p, c_int],
     "fedavg_fill_synthetic_f32": [c_void_p, c_void_p, c_size_t, c_u64, c_u64, c_u64],
+    "fedavg_fill_synthetic_tiled_f32": [c_void_p, c_void_p, c_int, c_size_t, c_size_t, c_u64, c_u64],
     "fedavg_gather_f32": [c_void_p, c_void_p, c_void_p, c_size_t, c_void_p],
 }
 EXPORTED = ["fedavg_last_error", "fedavg_abi_version", *_SIGNATURES.keys()]

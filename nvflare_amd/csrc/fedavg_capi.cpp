@@ -109,6 +109,7 @@ struct fedavg_ctx {
     int ring_next = 0;
     int blocks_per_cu = 0;  // 0 = default
     int unroll = 0;         // 0 = default
+    int variant = 0;        // streaming-kernel variant (bit 0: 2 columns per lane, bit 1: temporal loads)
 
     hipStream_t compute() const { return ext_stream ? ext_stream : own_stream; }
     void activate() const { HIP_CHECK(hipSetDevice(device)); }
@@ -130,6 +131,12 @@ int stream_grid(const fedavg_ctx* ctx, int64_t work_items) {
     const int64_t cap = (int64_t)ctx->num_cus * bpc;
     const int64_t need = (work_items + fedavg::kBlock - 1) / fedavg::kBlock;
     return (int)std::max<int64_t>(1, std::min<int64_t>(cap, need));
+}
+
+// streaming kernel grid: tiles of (VEC * kBlock) float4
+int stream_grid_tiles(const fedavg_ctx* ctx, int64_t n4) {
+    const int vec = (ctx->variant & 1) ? 2 : 1;
+    return stream_grid(ctx, (n4 + vec - 1) / vec);
 }
 
 // H2D of `height` rows; pageable sources go through the pinned ring (memcpy on the host threads,
@@ -393,6 +400,14 @@ int fedavg_timing_end(fedavg_ctx* ctx, float* ms) {
     });
 }
 
+int fedavg_set_variant(fedavg_ctx* ctx, int variant) {
+    return guarded([&] {
+        if (!ctx) throw Error("ctx is NULL");
+        if (variant < 0 || variant > 3) throw Error("variant must be 0..3");
+        ctx->variant = variant;
+    });
+}
+
 int fedavg_set_launch(fedavg_ctx* ctx, int blocks_per_cu, int unroll) {
     return guarded([&] {
         if (!ctx) throw Error("ctx is NULL");
@@ -459,7 +474,7 @@ int fedavg_accumulate(fedavg_ctx* ctx, const void* const* rows, const double* we
                 if (n4 > 0) {
                     HIP_CHECK(fedavg::launch_rows_f32x4(tab, kc, static_cast<const float*>(cur_in),
                                                         static_cast<float*>(out), n4, op, fin_c, (float)fin_d,
-                                                        stream_grid(ctx, n4), ctx->unroll, s));
+                                                        stream_grid_tiles(ctx, n4), ctx->unroll, ctx->variant, s));
                 }
                 if (tail > 0) {
                     fedavg::RowTableGeneric gt;
@@ -495,6 +510,59 @@ int fedavg_accumulate(fedavg_ctx* ctx, const void* const* rows, const double* we
             HIP_CHECK(hipEventRecord(ctx->ev_stop, s));
             ctx->timed_valid = true;
         }
+    });
+}
+
+int fedavg_accumulate_tiled(fedavg_ctx* ctx, const void* slab, int k_max, size_t tile_elems, const int* slots,
+                            const double* weights, int k_rows, const void* acc_in, void* out, size_t n, int op, int fin,
+                            double count) {
+    return guarded([&] {
+        if (!ctx) throw Error("ctx is NULL");
+        if (k_rows < 0 || (k_rows == 0 && !acc_in)) throw Error("k_rows == 0 requires acc_in");
+        if (k_rows > fedavg::kMaxRowsPerLaunch) throw Error("tiled path takes at most 128 rows per call");
+        if (tile_elems % (4 * fedavg::kBlock) != 0 || tile_elems / (4 * fedavg::kBlock) == 0 ||
+            tile_elems / (4 * fedavg::kBlock) > 4 || tile_elems / (4 * fedavg::kBlock) == 3)
+            throw Error("tile_elems must be 1024, 2048 or 4096");
+        if (n % 4 != 0) throw Error("tiled path needs n % 4 == 0");
+        if (op < FEDAVG_OP_NUMPY || op > FEDAVG_OP_UNWEIGHTED || fin < FEDAVG_FIN_NONE || fin > FEDAVG_FIN_DIV)
+            throw Error("bad op/fin");
+        if (n == 0) return;
+        if (!slab || !out) throw Error("NULL pointer");
+        fedavg::SlotTableF32 tab;
+        memset(&tab, 0, sizeof(tab));
+        for (int j = 0; j < k_rows; ++j) {
+            if (slots[j] < 0 || slots[j] >= k_max) throw Error("slot out of range");
+            tab.slot[j] = slots[j];
+            tab.w[j] = (float)weights[j];
+        }
+        ctx->activate();
+        hipStream_t s = ctx->compute();
+        if (ctx->timing) HIP_CHECK(hipEventRecord(ctx->ev_start, s));
+        const double fin_d = (fin == FEDAVG_FIN_SCALE) ? (1.0 / count) : count;
+        const int64_t n4 = (int64_t)(n / 4);
+        const int64_t tile4 = (int64_t)(tile_elems / 4);
+        const int64_t n_tiles = (n4 + tile4 - 1) / tile4;
+        const int bpc = ctx->blocks_per_cu > 0 ? ctx->blocks_per_cu : 2;
+        const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)ctx->num_cus * bpc, n_tiles));
+        HIP_CHECK(fedavg::launch_tiled_f32x4(tab, k_rows, static_cast<const float*>(slab), k_max, tile4,
+                                             static_cast<const float*>(acc_in), static_cast<float*>(out), n4, op, fin,
+                                             (float)fin_d, grid, ctx->variant, s));
+        if (ctx->timing) {
+            HIP_CHECK(hipEventRecord(ctx->ev_stop, s));
+            ctx->timed_valid = true;
+        }
+    });
+}
+
+int fedavg_fill_synthetic_tiled_f32(fedavg_ctx* ctx, float* slab, int k_max, size_t tile_elems, size_t n, uint64_t seed,
+                                    uint64_t col0) {
+    return guarded([&] {
+        if (!ctx || !slab) throw Error("NULL argument");
+        const int64_t n_tiles = (int64_t)((n + tile_elems - 1) / tile_elems);
+        const int64_t total = n_tiles * (int64_t)k_max * (int64_t)tile_elems;
+        ctx->activate();
+        HIP_CHECK(fedavg::launch_fill_synthetic_tiled_f32(slab, k_max, (int64_t)tile_elems, total, seed, col0,
+                                                          stream_grid(ctx, total), ctx->compute()));
     });
 }
 

@@ -97,33 +97,125 @@ __device__ __forceinline__ void store4(f32x4* p, f32x4 v) {
 
 // ---------------------------------------------------------------------------------------------
 // fp32 streaming kernel: out[i] = fin( fold_k step(acc, rows[k][i], w[k]) ), f32x4 per lane
+//   VEC    float4 columns per lane per tile (tile = VEC * kBlock float4; lane j owns j, j+kBlock, ...)
+//   UNROLL rows whose loads are issued before their arrival-ordered arithmetic
+//   NT     nontemporal load hint (every client byte is read exactly once)
 // ---------------------------------------------------------------------------------------------
-template <int OP, int FIN, bool ACC_IN, int UNROLL, bool NT>
+template <int OP, int FIN, bool ACC_IN, int UNROLL, bool NT, int VEC>
 __global__ void __launch_bounds__(kBlock) fedavg_rows_f32x4(const RowTableF32 tab, const int K,
                                                              const f32x4* acc_in, f32x4* out,
                                                              const int64_t n4, const float fin_val) {
-    const int64_t stride = (int64_t)gridDim.x * kBlock;
-    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n4; i += stride) {
-        f32x4 acc;
-        int k = 0;
-        if constexpr (ACC_IN) {
-            acc = load4<false>(acc_in + i);
+    constexpr int64_t kTile = (int64_t)VEC * kBlock;
+    const int64_t stride = (int64_t)gridDim.x * kTile;
+    for (int64_t base = (int64_t)blockIdx.x * kTile + threadIdx.x; base < n4; base += stride) {
+        if (VEC == 1 || base + (VEC - 1) * kBlock < n4) {
+            f32x4 acc[VEC];
+            int k = 0;
+            if constexpr (ACC_IN) {
+#pragma unroll
+                for (int c = 0; c < VEC; ++c) acc[c] = load4<false>(acc_in + base + c * kBlock);
+            } else {
+#pragma unroll
+                for (int c = 0; c < VEC; ++c) acc[c] = first4<OP>(load4<NT>(tab.rows[0] + base + c * kBlock), tab.w[0]);
+                k = 1;
+            }
+            // groups of UNROLL clients: issue all loads, then the arrival-ordered arithmetic
+            for (; k + UNROLL <= K; k += UNROLL) {
+                f32x4 v[UNROLL][VEC];
+#pragma unroll
+                for (int j = 0; j < UNROLL; ++j)
+#pragma unroll
+                    for (int c = 0; c < VEC; ++c) v[j][c] = load4<NT>(tab.rows[k + j] + base + c * kBlock);
+#pragma unroll
+                for (int j = 0; j < UNROLL; ++j)
+#pragma unroll
+                    for (int c = 0; c < VEC; ++c) acc[c] = step4<OP>(acc[c], v[j][c], tab.w[k + j]);
+            }
+            for (; k < K; ++k) {
+#pragma unroll
+                for (int c = 0; c < VEC; ++c)
+                    acc[c] = step4<OP>(acc[c], load4<NT>(tab.rows[k] + base + c * kBlock), tab.w[k]);
+            }
+#pragma unroll
+            for (int c = 0; c < VEC; ++c) store4<false>(out + base + c * kBlock, fin4<FIN>(acc[c], fin_val));
         } else {
-            acc = first4<OP>(load4<NT>(tab.rows[0] + i), tab.w[0]);
-            k = 1;
+            // ragged last tile (VEC > 1): column by column
+            for (int c = 0; c < VEC; ++c) {
+                const int64_t i = base + c * kBlock;
+                if (i >= n4) break;
+                f32x4 a;
+                int k = 0;
+                if constexpr (ACC_IN) {
+                    a = load4<false>(acc_in + i);
+                } else {
+                    a = first4<OP>(load4<NT>(tab.rows[0] + i), tab.w[0]);
+                    k = 1;
+                }
+                for (; k < K; ++k) a = step4<OP>(a, load4<NT>(tab.rows[k] + i), tab.w[k]);
+                store4<false>(out + i, fin4<FIN>(a, fin_val));
+            }
         }
-        // groups of UNROLL clients: issue all loads, then the arrival-ordered arithmetic
-        for (; k + UNROLL <= K; k += UNROLL) {
-            f32x4 v[UNROLL];
-#pragma unroll
-            for (int j = 0; j < UNROLL; ++j) v[j] = load4<NT>(tab.rows[k + j] + i);
-#pragma unroll
-            for (int j = 0; j < UNROLL; ++j) acc = step4<OP>(acc, v[j], tab.w[k + j]);
-        }
-        for (; k < K; ++k) acc = step4<OP>(acc, load4<NT>(tab.rows[k] + i), tab.w[k]);
-        store4<false>(out + i, fin4<FIN>(acc, fin_val));
     }
 }
+
+// ---------------------------------------------------------------------------------------------
+// fp32 tiled-slab kernel: clients interleaved per tile, slab[t][slot][T4] (f32x4 units).  The K rows of
+// one tile are contiguous, so a block streams K*T4*16 contiguous bytes per tile.
+// ---------------------------------------------------------------------------------------------
+template <int OP, int FIN, bool ACC_IN, int UNROLL, bool NT, int CPL>
+__global__ void __launch_bounds__(kBlock) fedavg_tiled_f32x4(const SlotTableF32 tab, const int K,
+                                                              const f32x4* __restrict__ slab, const int64_t k_max,
+                                                              const f32x4* acc_in, f32x4* out, const int64_t n4,
+                                                              const float fin_val) {
+    constexpr int64_t T4 = (int64_t)CPL * kBlock;  // tile width in f32x4 (CPL columns per lane)
+    const int64_t n_tiles = (n4 + T4 - 1) / T4;
+    for (int64_t t = blockIdx.x; t < n_tiles; t += gridDim.x) {
+        const f32x4* tile = slab + t * k_max * T4;
+        const int64_t col0 = t * T4 + threadIdx.x;
+        f32x4 acc[CPL];
+        int k = 0;
+        if constexpr (ACC_IN) {
+#pragma unroll
+            for (int c = 0; c < CPL; ++c) {
+                const int64_t i = col0 + c * kBlock;
+                acc[c] = i < n4 ? load4<false>(acc_in + i) : f32x4{0, 0, 0, 0};
+            }
+        } else {
+            const f32x4* r = tile + (int64_t)tab.slot[0] * T4 + threadIdx.x;
+#pragma unroll
+            for (int c = 0; c < CPL; ++c) acc[c] = first4<OP>(load4<NT>(r + c * kBlock), tab.w[0]);
+            k = 1;
+        }
+        for (; k + UNROLL <= K; k += UNROLL) {
+            f32x4 v[UNROLL][CPL];
+#pragma unroll
+            for (int j = 0; j < UNROLL; ++j) {
+                const f32x4* r = tile + (int64_t)tab.slot[k + j] * T4 + threadIdx.x;
+#pragma unroll
+                for (int c = 0; c < CPL; ++c) v[j][c] = load4<NT>(r + c * kBlock);
+            }
+#pragma unroll
+            for (int j = 0; j < UNROLL; ++j)
+#pragma unroll
+                for (int c = 0; c < CPL; ++c) acc[c] = step4<OP>(acc[c], v[j][c], tab.w[k + j]);
+        }
+        for (; k < K; ++k) {
+            const f32x4* r = tile + (int64_t)tab.slot[k] * T4 + threadIdx.x;
+#pragma unroll
+            for (int c = 0; c < CPL; ++c) acc[c] = step4<OP>(acc[c], load4<NT>(r + c * kBlock), tab.w[k]);
+        }
+#pragma unroll
+        for (int c = 0; c < CPL; ++c) {
+            const int64_t i = col0 + c * kBlock;
+            if (i < n4) store4<false>(out + i, fin4<FIN>(acc[c], fin_val));
+        }
+    }
+}
+
+// synthetic fill of a tiled slab: element (tile t, slot k, j) = synth(seed, k, col0 + t*T + j)
+__global__ void __launch_bounds__(kBlock) fedavg_fill_synthetic_tiled_f32(float* slab, const int64_t k_max,
+                                                                           const int64_t tile_elems, const int64_t total,
+                                                                           const uint64_t seed, const uint64_t col0);
 
 // ---------------------------------------------------------------------------------------------
 // generic scalar kernel: any (Tin, Tacc) pair, any alignment (tails, small keys, fp64, ints)
@@ -177,6 +269,24 @@ __global__ void __launch_bounds__(kBlock) fedavg_fill_synthetic_f32(float* dst, 
     }
 }
 
+__global__ void __launch_bounds__(kBlock) fedavg_fill_synthetic_tiled_f32(float* slab, const int64_t k_max,
+                                                                           const int64_t tile_elems, const int64_t total,
+                                                                           const uint64_t seed, const uint64_t col0) {
+    const int64_t stride = (int64_t)gridDim.x * kBlock;
+    for (int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x; e < total; e += stride) {
+        const int64_t t = e / (k_max * tile_elems);
+        const int64_t rem = e - t * k_max * tile_elems;
+        const uint64_t row = (uint64_t)(rem / tile_elems);
+        const uint64_t col = col0 + (uint64_t)(t * tile_elems + (rem - (int64_t)row * tile_elems));
+        const uint64_t base = (seed * 0x9E3779B97F4A7C15ULL) ^ (row * 0xD1B54A32D192ED03ULL);
+        int32_t s = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) s += (int32_t)(mix32(base + col * 4ULL + (uint64_t)j) >> 8);
+        s -= (int32_t)(1 << 25);
+        slab[e] = (float)s * 1.0323827e-07f;
+    }
+}
+
 __global__ void __launch_bounds__(kBlock) fedavg_gather_f32(const float* src, const uint64_t* idx, float* dst,
                                                              const int64_t m) {
     const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
@@ -186,56 +296,72 @@ __global__ void __launch_bounds__(kBlock) fedavg_gather_f32(const float* src, co
 // ---------------------------------------------------------------------------------------------
 // launchers
 // ---------------------------------------------------------------------------------------------
-template <int OP, int FIN, bool ACC_IN, int UNROLL>
-static hipError_t launch_f32x4_u(const RowTableF32& tab, int K, const float* acc_in, float* out, int64_t n4,
+template <int OP, int FIN, bool ACC_IN, int UNROLL, bool NT, int VEC>
+static hipError_t launch_f32x4_v(const RowTableF32& tab, int K, const float* acc_in, float* out, int64_t n4,
                                  float fin_val, int grid, hipStream_t s) {
-    hipLaunchKernelGGL((fedavg_rows_f32x4<OP, FIN, ACC_IN, UNROLL, true>), dim3(grid), dim3(kBlock), 0, s, tab, K,
+    hipLaunchKernelGGL((fedavg_rows_f32x4<OP, FIN, ACC_IN, UNROLL, NT, VEC>), dim3(grid), dim3(kBlock), 0, s, tab, K,
                        reinterpret_cast<const f32x4*>(acc_in), reinterpret_cast<f32x4*>(out), n4, fin_val);
     return hipGetLastError();
 }
 
+// variant bit 0: VEC=2 columns per lane; bit 1: plain (temporal) loads instead of nontemporal
+template <int OP, int FIN, bool ACC_IN, int UNROLL>
+static hipError_t launch_f32x4_u(const RowTableF32& tab, int K, const float* acc_in, float* out, int64_t n4,
+                                 float fin_val, int grid, int variant, hipStream_t s) {
+    switch (variant & 3) {
+        case 1:
+            return launch_f32x4_v<OP, FIN, ACC_IN, UNROLL, true, 2>(tab, K, acc_in, out, n4, fin_val, grid, s);
+        case 2:
+            return launch_f32x4_v<OP, FIN, ACC_IN, UNROLL, false, 1>(tab, K, acc_in, out, n4, fin_val, grid, s);
+        case 3:
+            return launch_f32x4_v<OP, FIN, ACC_IN, UNROLL, false, 2>(tab, K, acc_in, out, n4, fin_val, grid, s);
+        default:
+            return launch_f32x4_v<OP, FIN, ACC_IN, UNROLL, true, 1>(tab, K, acc_in, out, n4, fin_val, grid, s);
+    }
+}
+
 template <int OP, int FIN, bool ACC_IN>
 static hipError_t launch_f32x4_a(const RowTableF32& tab, int K, const float* acc_in, float* out, int64_t n4,
-                                 float fin_val, int grid, int unroll, hipStream_t s) {
+                                 float fin_val, int grid, int unroll, int variant, hipStream_t s) {
     switch (unroll) {
         case 4:
-            return launch_f32x4_u<OP, FIN, ACC_IN, 4>(tab, K, acc_in, out, n4, fin_val, grid, s);
+            return launch_f32x4_u<OP, FIN, ACC_IN, 4>(tab, K, acc_in, out, n4, fin_val, grid, variant, s);
         case 16:
-            return launch_f32x4_u<OP, FIN, ACC_IN, 16>(tab, K, acc_in, out, n4, fin_val, grid, s);
+            return launch_f32x4_u<OP, FIN, ACC_IN, 16>(tab, K, acc_in, out, n4, fin_val, grid, variant, s);
         default:
-            return launch_f32x4_u<OP, FIN, ACC_IN, 8>(tab, K, acc_in, out, n4, fin_val, grid, s);
+            return launch_f32x4_u<OP, FIN, ACC_IN, 8>(tab, K, acc_in, out, n4, fin_val, grid, variant, s);
     }
 }
 
 template <int OP, int FIN>
 static hipError_t launch_f32x4_f(const RowTableF32& tab, int K, const float* acc_in, float* out, int64_t n4,
-                                 float fin_val, int grid, int unroll, hipStream_t s) {
-    if (acc_in) return launch_f32x4_a<OP, FIN, true>(tab, K, acc_in, out, n4, fin_val, grid, unroll, s);
-    return launch_f32x4_a<OP, FIN, false>(tab, K, acc_in, out, n4, fin_val, grid, unroll, s);
+                                 float fin_val, int grid, int unroll, int variant, hipStream_t s) {
+    if (acc_in) return launch_f32x4_a<OP, FIN, true>(tab, K, acc_in, out, n4, fin_val, grid, unroll, variant, s);
+    return launch_f32x4_a<OP, FIN, false>(tab, K, acc_in, out, n4, fin_val, grid, unroll, variant, s);
 }
 
 template <int OP>
 static hipError_t launch_f32x4_o(const RowTableF32& tab, int K, const float* acc_in, float* out, int64_t n4, int fin,
-                                 float fin_val, int grid, int unroll, hipStream_t s) {
+                                 float fin_val, int grid, int unroll, int variant, hipStream_t s) {
     switch (fin) {
         case FEDAVG_FIN_SCALE:
-            return launch_f32x4_f<OP, FEDAVG_FIN_SCALE>(tab, K, acc_in, out, n4, fin_val, grid, unroll, s);
+            return launch_f32x4_f<OP, FEDAVG_FIN_SCALE>(tab, K, acc_in, out, n4, fin_val, grid, unroll, variant, s);
         case FEDAVG_FIN_DIV:
-            return launch_f32x4_f<OP, FEDAVG_FIN_DIV>(tab, K, acc_in, out, n4, fin_val, grid, unroll, s);
+            return launch_f32x4_f<OP, FEDAVG_FIN_DIV>(tab, K, acc_in, out, n4, fin_val, grid, unroll, variant, s);
         default:
-            return launch_f32x4_f<OP, FEDAVG_FIN_NONE>(tab, K, acc_in, out, n4, fin_val, grid, unroll, s);
+            return launch_f32x4_f<OP, FEDAVG_FIN_NONE>(tab, K, acc_in, out, n4, fin_val, grid, unroll, variant, s);
     }
 }
 
 hipError_t launch_rows_f32x4(const RowTableF32& tab, int K, const float* acc_in, float* out, int64_t n4, int op,
-                             int fin, float fin_val, int grid, int unroll, hipStream_t s) {
+                             int fin, float fin_val, int grid, int unroll, int variant, hipStream_t s) {
     switch (op) {
         case FEDAVG_OP_TORCH:
-            return launch_f32x4_o<FEDAVG_OP_TORCH>(tab, K, acc_in, out, n4, fin, fin_val, grid, unroll, s);
+            return launch_f32x4_o<FEDAVG_OP_TORCH>(tab, K, acc_in, out, n4, fin, fin_val, grid, unroll, variant, s);
         case FEDAVG_OP_UNWEIGHTED:
-            return launch_f32x4_o<FEDAVG_OP_UNWEIGHTED>(tab, K, acc_in, out, n4, fin, fin_val, grid, unroll, s);
+            return launch_f32x4_o<FEDAVG_OP_UNWEIGHTED>(tab, K, acc_in, out, n4, fin, fin_val, grid, unroll, variant, s);
         default:
-            return launch_f32x4_o<FEDAVG_OP_NUMPY>(tab, K, acc_in, out, n4, fin, fin_val, grid, unroll, s);
+            return launch_f32x4_o<FEDAVG_OP_NUMPY>(tab, K, acc_in, out, n4, fin, fin_val, grid, unroll, variant, s);
     }
 }
 
@@ -319,6 +445,75 @@ hipError_t launch_gather_f32(const float* src, const uint64_t* idx, float* dst, 
     const int grid = (int)((m + kBlock - 1) / kBlock);
     if (grid == 0) return hipSuccess;
     hipLaunchKernelGGL(fedavg_gather_f32, dim3(grid), dim3(kBlock), 0, s, src, idx, dst, m);
+    return hipGetLastError();
+}
+
+template <int OP, int FIN, bool ACC_IN, int CPL>
+static hipError_t launch_tiled_c(const SlotTableF32& tab, int K, const float* slab, int64_t k_max, const float* acc_in,
+                                 float* out, int64_t n4, float fin_val, int grid, int variant, hipStream_t s) {
+    const f32x4* sl = reinterpret_cast<const f32x4*>(slab);
+    const f32x4* ai = reinterpret_cast<const f32x4*>(acc_in);
+    f32x4* o = reinterpret_cast<f32x4*>(out);
+    if (variant & 2) {
+        hipLaunchKernelGGL((fedavg_tiled_f32x4<OP, FIN, ACC_IN, 8, false, CPL>), dim3(grid), dim3(kBlock), 0, s, tab, K,
+                           sl, k_max, ai, o, n4, fin_val);
+    } else {
+        hipLaunchKernelGGL((fedavg_tiled_f32x4<OP, FIN, ACC_IN, 8, true, CPL>), dim3(grid), dim3(kBlock), 0, s, tab, K,
+                           sl, k_max, ai, o, n4, fin_val);
+    }
+    return hipGetLastError();
+}
+
+template <int OP, int FIN>
+static hipError_t launch_tiled_f(const SlotTableF32& tab, int K, const float* slab, int64_t k_max, int64_t tile4,
+                                 const float* acc_in, float* out, int64_t n4, float fin_val, int grid, int variant,
+                                 hipStream_t s) {
+    const bool a = acc_in != nullptr;
+    switch (tile4 / kBlock) {
+        case 2:
+            return a ? launch_tiled_c<OP, FIN, true, 2>(tab, K, slab, k_max, acc_in, out, n4, fin_val, grid, variant, s)
+                     : launch_tiled_c<OP, FIN, false, 2>(tab, K, slab, k_max, acc_in, out, n4, fin_val, grid, variant, s);
+        case 4:
+            return a ? launch_tiled_c<OP, FIN, true, 4>(tab, K, slab, k_max, acc_in, out, n4, fin_val, grid, variant, s)
+                     : launch_tiled_c<OP, FIN, false, 4>(tab, K, slab, k_max, acc_in, out, n4, fin_val, grid, variant, s);
+        case 1:
+            return a ? launch_tiled_c<OP, FIN, true, 1>(tab, K, slab, k_max, acc_in, out, n4, fin_val, grid, variant, s)
+                     : launch_tiled_c<OP, FIN, false, 1>(tab, K, slab, k_max, acc_in, out, n4, fin_val, grid, variant, s);
+        default:
+            return hipErrorInvalidValue;
+    }
+}
+
+hipError_t launch_tiled_f32x4(const SlotTableF32& tab, int K, const float* slab, int64_t k_max, int64_t tile4,
+                              const float* acc_in, float* out, int64_t n4, int op, int fin, float fin_val, int grid,
+                              int variant, hipStream_t s) {
+#define FEDAVG_TILED_FIN(OPV)                                                                                   \
+    switch (fin) {                                                                                              \
+        case FEDAVG_FIN_SCALE:                                                                                  \
+            return launch_tiled_f<OPV, FEDAVG_FIN_SCALE>(tab, K, slab, k_max, tile4, acc_in, out, n4, fin_val, grid, \
+                                                         variant, s);                                           \
+        case FEDAVG_FIN_DIV:                                                                                    \
+            return launch_tiled_f<OPV, FEDAVG_FIN_DIV>(tab, K, slab, k_max, tile4, acc_in, out, n4, fin_val, grid,   \
+                                                       variant, s);                                             \
+        default:                                                                                                \
+            return launch_tiled_f<OPV, FEDAVG_FIN_NONE>(tab, K, slab, k_max, tile4, acc_in, out, n4, fin_val, grid,  \
+                                                        variant, s);                                            \
+    }
+    switch (op) {
+        case FEDAVG_OP_TORCH:
+            FEDAVG_TILED_FIN(FEDAVG_OP_TORCH)
+        case FEDAVG_OP_UNWEIGHTED:
+            FEDAVG_TILED_FIN(FEDAVG_OP_UNWEIGHTED)
+        default:
+            FEDAVG_TILED_FIN(FEDAVG_OP_NUMPY)
+    }
+#undef FEDAVG_TILED_FIN
+}
+
+hipError_t launch_fill_synthetic_tiled_f32(float* slab, int64_t k_max, int64_t tile_elems, int64_t total, uint64_t seed,
+                                           uint64_t col0, int grid, hipStream_t s) {
+    hipLaunchKernelGGL(fedavg_fill_synthetic_tiled_f32, dim3(grid), dim3(kBlock), 0, s, slab, k_max, tile_elems, total,
+                       seed, col0);
     return hipGetLastError();
 }
 

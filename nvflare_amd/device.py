@@ -169,6 +169,20 @@ class DeviceContext:
             ctypes.c_double(float(count)),
         )
 
+    def accumulate_tiled(self, slab_ptr: int, k_max: int, tile_elems: int, slots, weights, n: int, out_ptr: int,
+                         op: int, fin: int, count: float = 1.0, acc_in_ptr: Optional[int] = None) -> None:
+        k = len(slots)
+        s_arr = (ctypes.c_int * max(k, 1))(*[int(s) for s in slots])
+        w_arr = (ctypes.c_double * max(k, 1))(*[float(w) for w in weights])
+        N.call("fedavg_accumulate_tiled", self.handle, ctypes.c_void_p(slab_ptr), ctypes.c_int(k_max),
+               ctypes.c_size_t(tile_elems), s_arr, w_arr, ctypes.c_int(k), ctypes.c_void_p(acc_in_ptr or 0),
+               ctypes.c_void_p(out_ptr), ctypes.c_size_t(n), ctypes.c_int(op), ctypes.c_int(fin),
+               ctypes.c_double(float(count)))
+
+    def fill_synthetic_tiled_f32(self, slab_ptr: int, k_max: int, tile_elems: int, n: int, seed: int, col0: int = 0):
+        N.call("fedavg_fill_synthetic_tiled_f32", self.handle, ctypes.c_void_p(slab_ptr), ctypes.c_int(k_max),
+               ctypes.c_size_t(tile_elems), ctypes.c_size_t(n), ctypes.c_uint64(seed), ctypes.c_uint64(col0))
+
     def set_timing(self, enable: bool) -> None:
         N.call("fedavg_set_timing", self.handle, ctypes.c_int(1 if enable else 0))
 
@@ -187,6 +201,9 @@ class DeviceContext:
 
     def set_launch(self, blocks_per_cu: int = 0, unroll: int = 0) -> None:
         N.call("fedavg_set_launch", self.handle, ctypes.c_int(blocks_per_cu), ctypes.c_int(unroll))
+
+    def set_variant(self, variant: int = 0) -> None:
+        N.call("fedavg_set_variant", self.handle, ctypes.c_int(variant))
 
     def fill_synthetic_f32(self, dst_ptr: int, n: int, seed: int, row: int, col0: int = 0) -> None:
         N.call("fedavg_fill_synthetic_f32", self.handle, ctypes.c_void_p(dst_ptr), ctypes.c_size_t(n),

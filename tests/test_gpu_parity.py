@@ -228,18 +228,23 @@ def test_kernel_generic_dtypes(ctx, oracle, in_dt, acc_dt):
         assert same_bits(got, exp)
 
 
+@pytest.mark.parametrize("variant", [0, 1, 2, 3])
 @pytest.mark.parametrize("bpc,unroll", [(1, 4), (2, 8), (4, 16), (8, 8), (16, 4)])
-def test_launch_variants_same_bits(ctx, oracle, bpc, unroll):
+def test_launch_variants_same_bits(ctx, oracle, bpc, unroll, variant):
     rng = np.random.default_rng(21)
-    rows = [rng.standard_normal(300_001).astype(np.float32) for _ in range(33)]
+    n = 300_001 + variant  # ragged tiles for the 2-column variants too
+    rows = [rng.standard_normal(n).astype(np.float32) for _ in range(33)]
     ws = [float(1 + (37 * k) % 100) for k in range(33)]
-    exp = oracle.fedavg_c(rows, ws, oracle.MODE_TORCH, nthreads=4)
-    ctx.set_launch(bpc, unroll)
-    try:
-        got = _run_kernel(ctx, rows, ws, 1, 2, _sum(ws))
-    finally:
-        ctx.set_launch(0, 0)
-    assert same_bits(got, exp)
+    for op, fin, mode in ((1, 2, oracle.MODE_TORCH), (0, 1, oracle.MODE_NUMPY)):
+        exp = oracle.fedavg_c(rows, ws, mode, fin=fin, nthreads=4)
+        ctx.set_launch(bpc, unroll)
+        ctx.set_variant(variant)
+        try:
+            got = _run_kernel(ctx, rows, ws, op, fin, _sum(ws))
+        finally:
+            ctx.set_launch(0, 0)
+            ctx.set_variant(0)
+        assert same_bits(got, exp)
 
 
 def test_large_k64(ctx, oracle):
@@ -280,3 +285,30 @@ def test_timing_events(ctx):
     assert 0.0 < ms < 1000.0
     for b in bufs:
         b.close()
+
+
+@pytest.mark.parametrize("tile", [1024, 2048, 4096])
+@pytest.mark.parametrize("variant", [0, 2])
+def test_tiled_slab_vs_oracle(ctx, oracle, tile, variant):
+    """Tiled slab layout (client segments interleaved per tile) with a permuted arrival order."""
+    K, n = 13, 3 * 4096 + 1024 + 12  # ragged last tile
+    k_max = 16
+    n_tiles = (n + tile - 1) // tile
+    slab = ctx.alloc(n_tiles * k_max * tile * 4)
+    ctx.fill_synthetic_tiled_f32(slab.ptr, k_max, tile, n, 77, 5)
+    order = [int(x) for x in np.random.default_rng(tile).permutation(k_max)[:K]]
+    ws = [0.25 + 1.5 * j for j in range(K)]
+    rows = [oracle.synth_values(77, s, np.arange(5, 5 + n, dtype=np.uint64)) for s in order]
+    out = ctx.alloc(n * 4)
+    ctx.set_variant(variant)
+    try:
+        for op, fin, mode in ((1, 2, oracle.MODE_TORCH), (0, 1, oracle.MODE_NUMPY), (2, 1, oracle.MODE_NUMPY)):
+            ctx.accumulate_tiled(slab.ptr, k_max, tile, order, ws, n, out.ptr, op, fin, _sum(ws))
+            got = np.empty(n, np.float32)
+            ctx.d2h(got, out.ptr)
+            exp = oracle.fedavg_c(rows, ws, mode, weighted=(op != 2), fin=fin)
+            assert same_bits(got, exp), (op, fin)
+    finally:
+        ctx.set_variant(0)
+        slab.close()
+        out.close()
