@@ -110,7 +110,7 @@ int fedavg_accumulate(fedavg_ctx* ctx, const void* const* rows, const double* we
 /* Tiled-slab variant of the hot path (fp32): client rows interleaved per tile,
  *   slab[t][slot][tile_elems] with t = i / tile_elems,
  * so one tile's K client segments are contiguous in HBM.  slots[k] is the slot of the k-th arrival.
- * tile_elems in {1024, 2048, 4096}; n % 4 == 0; k_rows <= 128. */
+ * tile_elems in {1024, 2048, 4096, 8192}; n % 4 == 0; k_rows <= 128. */
 int fedavg_accumulate_tiled(fedavg_ctx* ctx, const void* slab, int k_max, size_t tile_elems, const int* slots,
                             const double* weights, int k_rows, const void* acc_in, void* out, size_t n, int op,
                             int fin, double count);
@@ -127,7 +127,8 @@ int fedavg_timing_end(fedavg_ctx* ctx, float* ms);
 
 /* Launch tuning (0 = default): blocks per CU of the streaming kernel, rows unrolled per group. */
 int fedavg_set_launch(fedavg_ctx* ctx, int blocks_per_cu, int unroll);
-/* Streaming-kernel variant: bit 0 = two float4 columns per lane, bit 1 = temporal (cached) loads. */
+/* Streaming-kernel variant: bit 0 = two float4 columns per lane (rows kernel), bit 1 = temporal (cached)
+ * loads, bit 2 = software-pipelined tiled kernel (tiled path, K % unroll == 0). */
 int fedavg_set_variant(fedavg_ctx* ctx, int variant);
 
 /* Synthetic inputs for benchmarks/tests: dst[j] = synth(seed, row, col0 + j), fp32, bit-identical

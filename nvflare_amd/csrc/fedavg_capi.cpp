@@ -403,7 +403,7 @@ int fedavg_timing_end(fedavg_ctx* ctx, float* ms) {
 int fedavg_set_variant(fedavg_ctx* ctx, int variant) {
     return guarded([&] {
         if (!ctx) throw Error("ctx is NULL");
-        if (variant < 0 || variant > 3) throw Error("variant must be 0..3");
+        if (variant < 0 || variant > 7) throw Error("variant must be 0..7");
         ctx->variant = variant;
     });
 }
@@ -520,9 +520,8 @@ int fedavg_accumulate_tiled(fedavg_ctx* ctx, const void* slab, int k_max, size_t
         if (!ctx) throw Error("ctx is NULL");
         if (k_rows < 0 || (k_rows == 0 && !acc_in)) throw Error("k_rows == 0 requires acc_in");
         if (k_rows > fedavg::kMaxRowsPerLaunch) throw Error("tiled path takes at most 128 rows per call");
-        if (tile_elems % (4 * fedavg::kBlock) != 0 || tile_elems / (4 * fedavg::kBlock) == 0 ||
-            tile_elems / (4 * fedavg::kBlock) > 4 || tile_elems / (4 * fedavg::kBlock) == 3)
-            throw Error("tile_elems must be 1024, 2048 or 4096");
+        if (tile_elems != 1024 && tile_elems != 2048 && tile_elems != 4096 && tile_elems != 8192)
+            throw Error("tile_elems must be 1024, 2048, 4096 or 8192");
         if (n % 4 != 0) throw Error("tiled path needs n % 4 == 0");
         if (op < FEDAVG_OP_NUMPY || op > FEDAVG_OP_UNWEIGHTED || fin < FEDAVG_FIN_NONE || fin > FEDAVG_FIN_DIV)
             throw Error("bad op/fin");
@@ -546,7 +545,7 @@ int fedavg_accumulate_tiled(fedavg_ctx* ctx, const void* slab, int k_max, size_t
         const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)ctx->num_cus * bpc, n_tiles));
         HIP_CHECK(fedavg::launch_tiled_f32x4(tab, k_rows, static_cast<const float*>(slab), k_max, tile4,
                                              static_cast<const float*>(acc_in), static_cast<float*>(out), n4, op, fin,
-                                             (float)fin_d, grid, ctx->variant, s));
+                                             (float)fin_d, grid, ctx->unroll, ctx->variant, s));
         if (ctx->timing) {
             HIP_CHECK(hipEventRecord(ctx->ev_stop, s));
             ctx->timed_valid = true;

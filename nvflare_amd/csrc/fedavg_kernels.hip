@@ -212,6 +212,85 @@ __global__ void __launch_bounds__(kBlock) fedavg_tiled_f32x4(const SlotTableF32 
     }
 }
 
+// Software-pipelined form of the tiled kernel (K % UNROLL == 0): the loads of the next group of UNROLL
+// clients -- possibly in the block's next tile -- are issued before the current group's arithmetic, so a
+// wave keeps 2 * UNROLL * CPL 16-byte loads in flight instead of draining at every group boundary.
+template <int OP, int FIN, bool ACC_IN, int UNROLL, bool NT, int CPL>
+__global__ void __launch_bounds__(kBlock) fedavg_tiled_pipe_f32x4(const SlotTableF32 tab, const int K,
+                                                                   const f32x4* __restrict__ slab, const int64_t k_max,
+                                                                   const f32x4* acc_in, f32x4* out, const int64_t n4,
+                                                                   const float fin_val) {
+    constexpr int64_t T4 = (int64_t)CPL * kBlock;
+    const int64_t n_tiles = (n4 + T4 - 1) / T4;
+    const int G = K / UNROLL;  // groups per tile
+    int64_t t = blockIdx.x;
+    if (t >= n_tiles) return;
+    f32x4 bufA[UNROLL][CPL], bufB[UNROLL][CPL];
+    auto issue = [&](f32x4 (&b)[UNROLL][CPL], int64_t tt, int g) {
+        const f32x4* tile = slab + tt * k_max * T4 + threadIdx.x;
+#pragma unroll
+        for (int j = 0; j < UNROLL; ++j) {
+            const f32x4* r = tile + (int64_t)tab.slot[g * UNROLL + j] * T4;
+#pragma unroll
+            for (int c = 0; c < CPL; ++c) b[j][c] = load4<NT>(r + c * kBlock);
+        }
+    };
+    // consume one group from `cur` after issuing the next group into `nxt`; returns false when done
+    f32x4 acc[CPL];
+    int g = 0;
+    auto stage = [&](f32x4 (&cur)[UNROLL][CPL], f32x4 (&nxt)[UNROLL][CPL]) -> bool {
+        int64_t tn = t;
+        int gn = g + 1;
+        if (gn == G) {
+            gn = 0;
+            tn = t + gridDim.x;
+        }
+        const bool more = tn < n_tiles;
+        // always issue (the last prefetch re-reads the current tile): a conditional issue would make
+        // the compiler's vmcnt bookkeeping fall back to vmcnt(0) at the join and drain the pipeline
+        issue(nxt, more ? tn : t, gn);
+        if (g == 0) {
+            if constexpr (ACC_IN) {
+#pragma unroll
+                for (int c = 0; c < CPL; ++c) {
+                    const int64_t i = t * T4 + threadIdx.x + c * kBlock;
+                    acc[c] = i < n4 ? load4<false>(acc_in + i) : f32x4{0, 0, 0, 0};
+                }
+#pragma unroll
+                for (int j = 0; j < UNROLL; ++j)
+#pragma unroll
+                    for (int c = 0; c < CPL; ++c) acc[c] = step4<OP>(acc[c], cur[j][c], tab.w[j]);
+            } else {
+#pragma unroll
+                for (int c = 0; c < CPL; ++c) acc[c] = first4<OP>(cur[0][c], tab.w[0]);
+#pragma unroll
+                for (int j = 1; j < UNROLL; ++j)
+#pragma unroll
+                    for (int c = 0; c < CPL; ++c) acc[c] = step4<OP>(acc[c], cur[j][c], tab.w[j]);
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < UNROLL; ++j)
+#pragma unroll
+                for (int c = 0; c < CPL; ++c) acc[c] = step4<OP>(acc[c], cur[j][c], tab.w[g * UNROLL + j]);
+        }
+        if (g == G - 1) {
+#pragma unroll
+            for (int c = 0; c < CPL; ++c) {
+                const int64_t i = t * T4 + threadIdx.x + c * kBlock;
+                if (i < n4) store4<false>(out + i, fin4<FIN>(acc[c], fin_val));
+            }
+        }
+        t = tn;
+        g = gn;
+        return more;
+    };
+    issue(bufA, t, 0);
+    // ping-pong between the two register buffers: no register copies, so no wait on in-flight loads
+    while (stage(bufA, bufB) && stage(bufB, bufA)) {
+    }
+}
+
 // synthetic fill of a tiled slab: element (tile t, slot k, j) = synth(seed, k, col0 + t*T + j)
 __global__ void __launch_bounds__(kBlock) fedavg_fill_synthetic_tiled_f32(float* slab, const int64_t k_max,
                                                                            const int64_t tile_elems, const int64_t total,
@@ -448,56 +527,77 @@ hipError_t launch_gather_f32(const float* src, const uint64_t* idx, float* dst, 
     return hipGetLastError();
 }
 
-template <int OP, int FIN, bool ACC_IN, int CPL>
-static hipError_t launch_tiled_c(const SlotTableF32& tab, int K, const float* slab, int64_t k_max, const float* acc_in,
+template <int OP, int FIN, bool ACC_IN, int CPL, int UNROLL>
+static hipError_t launch_tiled_u(const SlotTableF32& tab, int K, const float* slab, int64_t k_max, const float* acc_in,
                                  float* out, int64_t n4, float fin_val, int grid, int variant, hipStream_t s) {
     const f32x4* sl = reinterpret_cast<const f32x4*>(slab);
     const f32x4* ai = reinterpret_cast<const f32x4*>(acc_in);
     f32x4* o = reinterpret_cast<f32x4*>(out);
-    if (variant & 2) {
-        hipLaunchKernelGGL((fedavg_tiled_f32x4<OP, FIN, ACC_IN, 8, false, CPL>), dim3(grid), dim3(kBlock), 0, s, tab, K,
-                           sl, k_max, ai, o, n4, fin_val);
+    if ((variant & 4) && K >= UNROLL && K % UNROLL == 0) {
+        if (variant & 2) {
+            hipLaunchKernelGGL((fedavg_tiled_pipe_f32x4<OP, FIN, ACC_IN, UNROLL, false, CPL>), dim3(grid), dim3(kBlock),
+                               0, s, tab, K, sl, k_max, ai, o, n4, fin_val);
+        } else {
+            hipLaunchKernelGGL((fedavg_tiled_pipe_f32x4<OP, FIN, ACC_IN, UNROLL, true, CPL>), dim3(grid), dim3(kBlock),
+                               0, s, tab, K, sl, k_max, ai, o, n4, fin_val);
+        }
+    } else if (variant & 2) {
+        hipLaunchKernelGGL((fedavg_tiled_f32x4<OP, FIN, ACC_IN, UNROLL, false, CPL>), dim3(grid), dim3(kBlock), 0, s,
+                           tab, K, sl, k_max, ai, o, n4, fin_val);
     } else {
-        hipLaunchKernelGGL((fedavg_tiled_f32x4<OP, FIN, ACC_IN, 8, true, CPL>), dim3(grid), dim3(kBlock), 0, s, tab, K,
-                           sl, k_max, ai, o, n4, fin_val);
+        hipLaunchKernelGGL((fedavg_tiled_f32x4<OP, FIN, ACC_IN, UNROLL, true, CPL>), dim3(grid), dim3(kBlock), 0, s,
+                           tab, K, sl, k_max, ai, o, n4, fin_val);
     }
     return hipGetLastError();
 }
 
+template <int OP, int FIN, bool ACC_IN, int CPL>
+static hipError_t launch_tiled_c(const SlotTableF32& tab, int K, const float* slab, int64_t k_max, const float* acc_in,
+                                 float* out, int64_t n4, float fin_val, int grid, int unroll, int variant,
+                                 hipStream_t s) {
+    if (unroll == 4)
+        return launch_tiled_u<OP, FIN, ACC_IN, CPL, 4>(tab, K, slab, k_max, acc_in, out, n4, fin_val, grid, variant, s);
+    return launch_tiled_u<OP, FIN, ACC_IN, CPL, 8>(tab, K, slab, k_max, acc_in, out, n4, fin_val, grid, variant, s);
+}
+
 template <int OP, int FIN>
 static hipError_t launch_tiled_f(const SlotTableF32& tab, int K, const float* slab, int64_t k_max, int64_t tile4,
-                                 const float* acc_in, float* out, int64_t n4, float fin_val, int grid, int variant,
-                                 hipStream_t s) {
-    const bool a = acc_in != nullptr;
+                                 const float* acc_in, float* out, int64_t n4, float fin_val, int grid, int unroll,
+                                 int variant, hipStream_t s) {
+#define FEDAVG_TILED_CPL(C)                                                                                        \
+    return acc_in ? launch_tiled_c<OP, FIN, true, C>(tab, K, slab, k_max, acc_in, out, n4, fin_val, grid, unroll,  \
+                                                     variant, s)                                                   \
+                  : launch_tiled_c<OP, FIN, false, C>(tab, K, slab, k_max, acc_in, out, n4, fin_val, grid, unroll, \
+                                                      variant, s);
     switch (tile4 / kBlock) {
-        case 2:
-            return a ? launch_tiled_c<OP, FIN, true, 2>(tab, K, slab, k_max, acc_in, out, n4, fin_val, grid, variant, s)
-                     : launch_tiled_c<OP, FIN, false, 2>(tab, K, slab, k_max, acc_in, out, n4, fin_val, grid, variant, s);
-        case 4:
-            return a ? launch_tiled_c<OP, FIN, true, 4>(tab, K, slab, k_max, acc_in, out, n4, fin_val, grid, variant, s)
-                     : launch_tiled_c<OP, FIN, false, 4>(tab, K, slab, k_max, acc_in, out, n4, fin_val, grid, variant, s);
         case 1:
-            return a ? launch_tiled_c<OP, FIN, true, 1>(tab, K, slab, k_max, acc_in, out, n4, fin_val, grid, variant, s)
-                     : launch_tiled_c<OP, FIN, false, 1>(tab, K, slab, k_max, acc_in, out, n4, fin_val, grid, variant, s);
+            FEDAVG_TILED_CPL(1)
+        case 2:
+            FEDAVG_TILED_CPL(2)
+        case 4:
+            FEDAVG_TILED_CPL(4)
+        case 8:
+            FEDAVG_TILED_CPL(8)
         default:
             return hipErrorInvalidValue;
     }
+#undef FEDAVG_TILED_CPL
 }
 
 hipError_t launch_tiled_f32x4(const SlotTableF32& tab, int K, const float* slab, int64_t k_max, int64_t tile4,
                               const float* acc_in, float* out, int64_t n4, int op, int fin, float fin_val, int grid,
-                              int variant, hipStream_t s) {
+                              int unroll, int variant, hipStream_t s) {
 #define FEDAVG_TILED_FIN(OPV)                                                                                   \
     switch (fin) {                                                                                              \
         case FEDAVG_FIN_SCALE:                                                                                  \
             return launch_tiled_f<OPV, FEDAVG_FIN_SCALE>(tab, K, slab, k_max, tile4, acc_in, out, n4, fin_val, grid, \
-                                                         variant, s);                                           \
+                                                         unroll, variant, s);                                           \
         case FEDAVG_FIN_DIV:                                                                                    \
             return launch_tiled_f<OPV, FEDAVG_FIN_DIV>(tab, K, slab, k_max, tile4, acc_in, out, n4, fin_val, grid,   \
-                                                       variant, s);                                             \
+                                                       unroll, variant, s);                                             \
         default:                                                                                                \
             return launch_tiled_f<OPV, FEDAVG_FIN_NONE>(tab, K, slab, k_max, tile4, acc_in, out, n4, fin_val, grid,  \
-                                                        variant, s);                                            \
+                                                        unroll, variant, s);                                            \
     }
     switch (op) {
         case FEDAVG_OP_TORCH:

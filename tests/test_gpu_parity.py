@@ -287,12 +287,14 @@ def test_timing_events(ctx):
         b.close()
 
 
-@pytest.mark.parametrize("tile", [1024, 2048, 4096])
-@pytest.mark.parametrize("variant", [0, 2])
-def test_tiled_slab_vs_oracle(ctx, oracle, tile, variant):
-    """Tiled slab layout (client segments interleaved per tile) with a permuted arrival order."""
-    K, n = 13, 3 * 4096 + 1024 + 12  # ragged last tile
-    k_max = 16
+@pytest.mark.parametrize("tile", [1024, 2048, 4096, 8192])
+@pytest.mark.parametrize("variant", [0, 2, 4, 6])
+@pytest.mark.parametrize("K,unroll", [(13, 8), (16, 4), (16, 8), (24, 8)])
+def test_tiled_slab_vs_oracle(ctx, oracle, tile, variant, K, unroll):
+    """Tiled slab layout (client segments interleaved per tile) with a permuted arrival order; variants 4/6
+    take the software-pipelined kernel when K % unroll == 0 (and include grid-stride tile reuse)."""
+    n = 7 * 4096 + 1024 + 12  # ragged last tile
+    k_max = 24
     n_tiles = (n + tile - 1) // tile
     slab = ctx.alloc(n_tiles * k_max * tile * 4)
     ctx.fill_synthetic_tiled_f32(slab.ptr, k_max, tile, n, 77, 5)
@@ -301,6 +303,7 @@ def test_tiled_slab_vs_oracle(ctx, oracle, tile, variant):
     rows = [oracle.synth_values(77, s, np.arange(5, 5 + n, dtype=np.uint64)) for s in order]
     out = ctx.alloc(n * 4)
     ctx.set_variant(variant)
+    ctx.set_launch(1 if variant & 4 else 0, unroll)  # few blocks: several tiles per block
     try:
         for op, fin, mode in ((1, 2, oracle.MODE_TORCH), (0, 1, oracle.MODE_NUMPY), (2, 1, oracle.MODE_NUMPY)):
             ctx.accumulate_tiled(slab.ptr, k_max, tile, order, ws, n, out.ptr, op, fin, _sum(ws))
@@ -310,5 +313,6 @@ def test_tiled_slab_vs_oracle(ctx, oracle, tile, variant):
             assert same_bits(got, exp), (op, fin)
     finally:
         ctx.set_variant(0)
+        ctx.set_launch(0, 0)
         slab.close()
         out.close()

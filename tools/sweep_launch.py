@@ -85,18 +85,19 @@ def sweep_tiled(args, ctx, K, P):
     ws = [float(1 + (37 * k) % 100) for k in range(K)]
     cnt = sum(ws)
     op, fin = (1, 2) if args.mode == "torch" else (0, 1)
-    configs = list(itertools.product(tiles, [int(x) for x in args.bpc.split(",")], [int(x) for x in args.variant.split(",")]))
+    configs = list(itertools.product(tiles, [int(x) for x in args.bpc.split(",")], [int(x) for x in args.variant.split(",")],
+                                     [int(x) for x in args.unroll.split(",")]))
     times = {c: [] for c in configs}
     alg = 4.0 * K * P + 4.0 * P
     filled = None
     for r in range(args.rounds):
         for c in configs:
-            tile, bpc, var = c
+            tile, bpc, var, unr = c
             if filled != tile:
                 ctx.fill_synthetic_tiled_f32(slab.ptr, K, tile, P, 1000, 0)
                 ctx.sync()
                 filled = tile
-            ctx.set_launch(bpc, 0)
+            ctx.set_launch(bpc, unr)
             ctx.set_variant(var)
             ctx.accumulate_tiled(slab.ptr, K, tile, list(range(K)), ws, P, out.ptr, op, fin, cnt)
             ctx.timing_begin()
@@ -107,7 +108,7 @@ def sweep_tiled(args, ctx, K, P):
     res = []
     for c, t in times.items():
         med = float(np.median(t))
-        res.append({"layout": "tiled", "tile": c[0], "bpc": c[1], "variant": c[2], "ms_median": round(med, 4),
+        res.append({"layout": "tiled", "tile": c[0], "bpc": c[1], "variant": c[2], "unroll": c[3], "ms_median": round(med, 4),
                     "ms_min": round(min(t), 4), "GBps_median": round(alg / med / 1e6, 1),
                     "frac_peak": round(alg / med / 1e6 / 8000, 4)})
     res.sort(key=lambda x: x["ms_median"])
