@@ -107,13 +107,15 @@ int fedavg_accumulate(fedavg_ctx* ctx, const void* const* rows, const double* we
                       const void* acc_in, void* out, size_t n, int in_dtype, int acc_dtype, int op,
                       int fin, double count);
 
-/* Tiled-slab variant of the hot path (fp32): client rows interleaved per tile,
- *   slab[t][slot][tile_elems] with t = i / tile_elems,
- * so one tile's K client segments are contiguous in HBM.  slots[k] is the slot of the k-th arrival.
- * tile_elems in {1024, 2048, 4096, 8192}; n % 4 == 0; k_rows <= 128. */
-int fedavg_accumulate_tiled(fedavg_ctx* ctx, const void* slab, int k_max, size_t tile_elems, const int* slots,
-                            const double* weights, int k_rows, const void* acc_in, void* out, size_t n, int op,
-                            int fin, double count);
+/* Tiled-slab variant of the hot path (fp32): client rows interleaved per tile.  Element i of the
+ * client in slot s lives at  slab[(i / tile_elems) * tile_stride + s * seg_stride + i % tile_elems],
+ * so one tile's client segments are contiguous in HBM (padding in the strides staggers the DRAM
+ * channels that concurrently streamed tiles start on).  slots[k] is the slot of the k-th arrival.
+ * tile_elems in {1024, 2048, 4096, 8192}; strides in elements, multiples of 4, seg_stride >= tile_elems,
+ * tile_stride >= k_max * seg_stride; n % 4 == 0; k_rows <= 128; out/acc_in are flat [n]. */
+int fedavg_accumulate_tiled(fedavg_ctx* ctx, const void* slab, size_t tile_elems, size_t seg_stride,
+                            size_t tile_stride, int k_max, const int* slots, const double* weights, int k_rows,
+                            const void* acc_in, void* out, size_t n, int op, int fin, double count);
 
 /* Timing of the kernels launched by the last fedavg_accumulate call, measured with HIP events on
  * the stream they ran on (enable first; costs two event records per call). */
@@ -136,8 +138,8 @@ int fedavg_set_variant(fedavg_ctx* ctx, int variant);
 int fedavg_fill_synthetic_f32(fedavg_ctx* ctx, float* dst, size_t n, uint64_t seed, uint64_t row,
                               uint64_t col0);
 /* Same values laid out as a tiled slab (see fedavg_accumulate_tiled): slot k holds synth row k. */
-int fedavg_fill_synthetic_tiled_f32(fedavg_ctx* ctx, float* slab, int k_max, size_t tile_elems, size_t n,
-                                    uint64_t seed, uint64_t col0);
+int fedavg_fill_synthetic_tiled_f32(fedavg_ctx* ctx, float* slab, int k_max, size_t tile_elems, size_t seg_stride,
+                                    size_t tile_stride, size_t n, uint64_t seed, uint64_t col0);
 /* Gather m fp32 elements src[idx[j]] (idx: host array) into host_out (spot checks at full size). */
 int fedavg_gather_f32(fedavg_ctx* ctx, const float* src, const uint64_t* idx, size_t m, float* host_out);
 

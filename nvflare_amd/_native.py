@@ -74,8 +74,10 @@ _SIGNATURES = {
     "fedavg_accumulate_tiled": [
         c_void_p,  # ctx
         c_void_p,  # slab
-        c_int,  # k_max
         c_size_t,  # tile_elems
+        c_size_t,  # seg_stride
+        c_size_t,  # tile_stride
+        c_int,  # k_max
         ctypes.POINTER(c_int),  # slots
         ctypes.POINTER(c_double),  # weights
         c_int,  # k_rows
@@ -93,7 +95,7 @@ _SIGNATURES = {
     "fedavg_set_launch": [c_void_p, c_int, c_int],
     "fedavg_set_variant": [c_void_p, c_int],
     "fedavg_fill_synthetic_f32": [c_void_p, c_void_p, c_size_t, c_u64, c_u64, c_u64],
-    "fedavg_fill_synthetic_tiled_f32": [c_void_p, c_void_p, c_int, c_size_t, c_size_t, c_u64, c_u64],
+    "fedavg_fill_synthetic_tiled_f32": [c_void_p, c_void_p, c_int, c_size_t, c_size_t, c_size_t, c_size_t, c_u64, c_u64],
     "fedavg_gather_f32": [c_void_p, c_void_p, c_void_p, c_size_t, c_void_p],
 }
 EXPORTED = ["fedavg_last_error", "fedavg_abi_version", *_SIGNATURES.keys()]

@@ -513,20 +513,26 @@ int fedavg_accumulate(fedavg_ctx* ctx, const void* const* rows, const double* we
     });
 }
 
-int fedavg_accumulate_tiled(fedavg_ctx* ctx, const void* slab, int k_max, size_t tile_elems, const int* slots,
-                            const double* weights, int k_rows, const void* acc_in, void* out, size_t n, int op, int fin,
-                            double count) {
+int fedavg_accumulate_tiled(fedavg_ctx* ctx, const void* slab, size_t tile_elems, size_t seg_stride, size_t tile_stride,
+                            int k_max, const int* slots, const double* weights, int k_rows, const void* acc_in, void* out,
+                            size_t n, int op, int fin, double count) {
     return guarded([&] {
         if (!ctx) throw Error("ctx is NULL");
         if (k_rows < 0 || (k_rows == 0 && !acc_in)) throw Error("k_rows == 0 requires acc_in");
         if (k_rows > fedavg::kMaxRowsPerLaunch) throw Error("tiled path takes at most 128 rows per call");
         if (tile_elems != 1024 && tile_elems != 2048 && tile_elems != 4096 && tile_elems != 8192)
             throw Error("tile_elems must be 1024, 2048, 4096 or 8192");
+        if (seg_stride < tile_elems || seg_stride % 4 || tile_stride % 4 || k_max <= 0 ||
+            tile_stride < (size_t)k_max * seg_stride)
+            throw Error("need seg_stride >= tile_elems, tile_stride >= k_max * seg_stride, both multiples of 4");
         if (n % 4 != 0) throw Error("tiled path needs n % 4 == 0");
         if (op < FEDAVG_OP_NUMPY || op > FEDAVG_OP_UNWEIGHTED || fin < FEDAVG_FIN_NONE || fin > FEDAVG_FIN_DIV)
             throw Error("bad op/fin");
         if (n == 0) return;
         if (!slab || !out) throw Error("NULL pointer");
+        if (reinterpret_cast<uintptr_t>(slab) % 16 || reinterpret_cast<uintptr_t>(out) % 16 ||
+            reinterpret_cast<uintptr_t>(acc_in) % 16)
+            throw Error("tiled path needs 16-byte aligned slab/out/acc_in");
         fedavg::SlotTableF32 tab;
         memset(&tab, 0, sizeof(tab));
         for (int j = 0; j < k_rows; ++j) {
@@ -543,9 +549,10 @@ int fedavg_accumulate_tiled(fedavg_ctx* ctx, const void* slab, int k_max, size_t
         const int64_t n_tiles = (n4 + tile4 - 1) / tile4;
         const int bpc = ctx->blocks_per_cu > 0 ? ctx->blocks_per_cu : 2;
         const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)ctx->num_cus * bpc, n_tiles));
-        HIP_CHECK(fedavg::launch_tiled_f32x4(tab, k_rows, static_cast<const float*>(slab), k_max, tile4,
-                                             static_cast<const float*>(acc_in), static_cast<float*>(out), n4, op, fin,
-                                             (float)fin_d, grid, ctx->unroll, ctx->variant, s));
+        HIP_CHECK(fedavg::launch_tiled_f32x4(tab, k_rows, static_cast<const float*>(slab), (int64_t)seg_stride / 4,
+                                             (int64_t)tile_stride / 4, tile4, static_cast<const float*>(acc_in),
+                                             static_cast<float*>(out), n4, op, fin, (float)fin_d, grid, ctx->unroll,
+                                             ctx->variant, s));
         if (ctx->timing) {
             HIP_CHECK(hipEventRecord(ctx->ev_stop, s));
             ctx->timed_valid = true;
@@ -553,14 +560,16 @@ int fedavg_accumulate_tiled(fedavg_ctx* ctx, const void* slab, int k_max, size_t
     });
 }
 
-int fedavg_fill_synthetic_tiled_f32(fedavg_ctx* ctx, float* slab, int k_max, size_t tile_elems, size_t n, uint64_t seed,
-                                    uint64_t col0) {
+int fedavg_fill_synthetic_tiled_f32(fedavg_ctx* ctx, float* slab, int k_max, size_t tile_elems, size_t seg_stride,
+                                    size_t tile_stride, size_t n, uint64_t seed, uint64_t col0) {
     return guarded([&] {
         if (!ctx || !slab) throw Error("NULL argument");
+        if (seg_stride < tile_elems || tile_stride < (size_t)k_max * seg_stride) throw Error("bad strides");
         const int64_t n_tiles = (int64_t)((n + tile_elems - 1) / tile_elems);
         const int64_t total = n_tiles * (int64_t)k_max * (int64_t)tile_elems;
         ctx->activate();
-        HIP_CHECK(fedavg::launch_fill_synthetic_tiled_f32(slab, k_max, (int64_t)tile_elems, total, seed, col0,
+        HIP_CHECK(fedavg::launch_fill_synthetic_tiled_f32(slab, k_max, (int64_t)tile_elems, (int64_t)seg_stride,
+                                                          (int64_t)tile_stride, (int64_t)n, seed, col0,
                                                           stream_grid(ctx, total), ctx->compute()));
     });
 }

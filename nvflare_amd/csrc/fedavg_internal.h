@@ -32,11 +32,12 @@ struct RowTableGeneric {
 
 hipError_t launch_rows_f32x4(const RowTableF32& tab, int K, const float* acc_in, float* out, int64_t n4, int op,
                              int fin, float fin_val, int grid, int unroll, int variant, hipStream_t s);
-hipError_t launch_tiled_f32x4(const SlotTableF32& tab, int K, const float* slab, int64_t k_max, int64_t tile4,
+hipError_t launch_tiled_f32x4(const SlotTableF32& tab, int K, const float* slab, int64_t seg4, int64_t tstride4,
+                              int64_t tile4,
                               const float* acc_in, float* out, int64_t n4, int op, int fin, float fin_val, int grid,
                               int unroll, int variant, hipStream_t s);
-hipError_t launch_fill_synthetic_tiled_f32(float* slab, int64_t k_max, int64_t tile_elems, int64_t total, uint64_t seed,
-                                           uint64_t col0, int grid, hipStream_t s);
+hipError_t launch_fill_synthetic_tiled_f32(float* slab, int64_t k_max, int64_t tile_elems, int64_t seg, int64_t tstride,
+                                           int64_t n, uint64_t seed, uint64_t col0, int grid, hipStream_t s);
 hipError_t launch_rows_generic(const RowTableGeneric& tab, int K, const void* acc_in, void* out, int64_t n,
                                int in_dtype, int acc_dtype, int op, int fin, double fin_val, int grid,
                                hipStream_t s);

@@ -164,13 +164,13 @@ __global__ void __launch_bounds__(kBlock) fedavg_rows_f32x4(const RowTableF32 ta
 // ---------------------------------------------------------------------------------------------
 template <int OP, int FIN, bool ACC_IN, int UNROLL, bool NT, int CPL>
 __global__ void __launch_bounds__(kBlock) fedavg_tiled_f32x4(const SlotTableF32 tab, const int K,
-                                                              const f32x4* __restrict__ slab, const int64_t k_max,
-                                                              const f32x4* acc_in, f32x4* out, const int64_t n4,
-                                                              const float fin_val) {
+                                                              const f32x4* __restrict__ slab, const int64_t seg4,
+                                                              const int64_t tstride4, const f32x4* acc_in, f32x4* out,
+                                                              const int64_t n4, const float fin_val) {
     constexpr int64_t T4 = (int64_t)CPL * kBlock;  // tile width in f32x4 (CPL columns per lane)
     const int64_t n_tiles = (n4 + T4 - 1) / T4;
     for (int64_t t = blockIdx.x; t < n_tiles; t += gridDim.x) {
-        const f32x4* tile = slab + t * k_max * T4;
+        const f32x4* tile = slab + t * tstride4;
         const int64_t col0 = t * T4 + threadIdx.x;
         f32x4 acc[CPL];
         int k = 0;
@@ -181,7 +181,7 @@ __global__ void __launch_bounds__(kBlock) fedavg_tiled_f32x4(const SlotTableF32 
                 acc[c] = i < n4 ? load4<false>(acc_in + i) : f32x4{0, 0, 0, 0};
             }
         } else {
-            const f32x4* r = tile + (int64_t)tab.slot[0] * T4 + threadIdx.x;
+            const f32x4* r = tile + (int64_t)tab.slot[0] * seg4 + threadIdx.x;
 #pragma unroll
             for (int c = 0; c < CPL; ++c) acc[c] = first4<OP>(load4<NT>(r + c * kBlock), tab.w[0]);
             k = 1;
@@ -190,7 +190,7 @@ __global__ void __launch_bounds__(kBlock) fedavg_tiled_f32x4(const SlotTableF32 
             f32x4 v[UNROLL][CPL];
 #pragma unroll
             for (int j = 0; j < UNROLL; ++j) {
-                const f32x4* r = tile + (int64_t)tab.slot[k + j] * T4 + threadIdx.x;
+                const f32x4* r = tile + (int64_t)tab.slot[k + j] * seg4 + threadIdx.x;
 #pragma unroll
                 for (int c = 0; c < CPL; ++c) v[j][c] = load4<NT>(r + c * kBlock);
             }
@@ -200,7 +200,7 @@ __global__ void __launch_bounds__(kBlock) fedavg_tiled_f32x4(const SlotTableF32 
                 for (int c = 0; c < CPL; ++c) acc[c] = step4<OP>(acc[c], v[j][c], tab.w[k + j]);
         }
         for (; k < K; ++k) {
-            const f32x4* r = tile + (int64_t)tab.slot[k] * T4 + threadIdx.x;
+            const f32x4* r = tile + (int64_t)tab.slot[k] * seg4 + threadIdx.x;
 #pragma unroll
             for (int c = 0; c < CPL; ++c) acc[c] = step4<OP>(acc[c], load4<NT>(r + c * kBlock), tab.w[k]);
         }
@@ -217,9 +217,9 @@ __global__ void __launch_bounds__(kBlock) fedavg_tiled_f32x4(const SlotTableF32 
 // wave keeps 2 * UNROLL * CPL 16-byte loads in flight instead of draining at every group boundary.
 template <int OP, int FIN, bool ACC_IN, int UNROLL, bool NT, int CPL>
 __global__ void __launch_bounds__(kBlock) fedavg_tiled_pipe_f32x4(const SlotTableF32 tab, const int K,
-                                                                   const f32x4* __restrict__ slab, const int64_t k_max,
-                                                                   const f32x4* acc_in, f32x4* out, const int64_t n4,
-                                                                   const float fin_val) {
+                                                                   const f32x4* __restrict__ slab, const int64_t seg4,
+                                                                   const int64_t tstride4, const f32x4* acc_in,
+                                                                   f32x4* out, const int64_t n4, const float fin_val) {
     constexpr int64_t T4 = (int64_t)CPL * kBlock;
     const int64_t n_tiles = (n4 + T4 - 1) / T4;
     const int G = K / UNROLL;  // groups per tile
@@ -227,10 +227,10 @@ __global__ void __launch_bounds__(kBlock) fedavg_tiled_pipe_f32x4(const SlotTabl
     if (t >= n_tiles) return;
     f32x4 bufA[UNROLL][CPL], bufB[UNROLL][CPL];
     auto issue = [&](f32x4 (&b)[UNROLL][CPL], int64_t tt, int g) {
-        const f32x4* tile = slab + tt * k_max * T4 + threadIdx.x;
+        const f32x4* tile = slab + tt * tstride4 + threadIdx.x;
 #pragma unroll
         for (int j = 0; j < UNROLL; ++j) {
-            const f32x4* r = tile + (int64_t)tab.slot[g * UNROLL + j] * T4;
+            const f32x4* r = tile + (int64_t)tab.slot[g * UNROLL + j] * seg4;
 #pragma unroll
             for (int c = 0; c < CPL; ++c) b[j][c] = load4<NT>(r + c * kBlock);
         }
@@ -293,7 +293,8 @@ __global__ void __launch_bounds__(kBlock) fedavg_tiled_pipe_f32x4(const SlotTabl
 
 // synthetic fill of a tiled slab: element (tile t, slot k, j) = synth(seed, k, col0 + t*T + j)
 __global__ void __launch_bounds__(kBlock) fedavg_fill_synthetic_tiled_f32(float* slab, const int64_t k_max,
-                                                                           const int64_t tile_elems, const int64_t total,
+                                                                           const int64_t tile_elems, const int64_t seg,
+                                                                           const int64_t tstride, const int64_t n,
                                                                            const uint64_t seed, const uint64_t col0);
 
 // ---------------------------------------------------------------------------------------------
@@ -349,20 +350,25 @@ __global__ void __launch_bounds__(kBlock) fedavg_fill_synthetic_f32(float* dst, 
 }
 
 __global__ void __launch_bounds__(kBlock) fedavg_fill_synthetic_tiled_f32(float* slab, const int64_t k_max,
-                                                                           const int64_t tile_elems, const int64_t total,
+                                                                           const int64_t tile_elems, const int64_t seg,
+                                                                           const int64_t tstride, const int64_t n,
                                                                            const uint64_t seed, const uint64_t col0) {
+    // logical element (row, i) of every slot row k < k_max, i < n_tiles * tile_elems
+    const int64_t n_tiles = (n + tile_elems - 1) / tile_elems;
+    const int64_t total = n_tiles * k_max * tile_elems;
     const int64_t stride = (int64_t)gridDim.x * kBlock;
     for (int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x; e < total; e += stride) {
         const int64_t t = e / (k_max * tile_elems);
         const int64_t rem = e - t * k_max * tile_elems;
-        const uint64_t row = (uint64_t)(rem / tile_elems);
-        const uint64_t col = col0 + (uint64_t)(t * tile_elems + (rem - (int64_t)row * tile_elems));
-        const uint64_t base = (seed * 0x9E3779B97F4A7C15ULL) ^ (row * 0xD1B54A32D192ED03ULL);
+        const int64_t row = rem / tile_elems;
+        const int64_t j = rem - row * tile_elems;
+        const uint64_t col = col0 + (uint64_t)(t * tile_elems + j);
+        const uint64_t base = (seed * 0x9E3779B97F4A7C15ULL) ^ ((uint64_t)row * 0xD1B54A32D192ED03ULL);
         int32_t s = 0;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) s += (int32_t)(mix32(base + col * 4ULL + (uint64_t)j) >> 8);
+        for (int q = 0; q < 4; ++q) s += (int32_t)(mix32(base + col * 4ULL + (uint64_t)q) >> 8);
         s -= (int32_t)(1 << 25);
-        slab[e] = (float)s * 1.0323827e-07f;
+        slab[t * tstride + row * seg + j] = (float)s * 1.0323827e-07f;
     }
 }
 
@@ -528,46 +534,50 @@ hipError_t launch_gather_f32(const float* src, const uint64_t* idx, float* dst, 
 }
 
 template <int OP, int FIN, bool ACC_IN, int CPL, int UNROLL>
-static hipError_t launch_tiled_u(const SlotTableF32& tab, int K, const float* slab, int64_t k_max, const float* acc_in,
-                                 float* out, int64_t n4, float fin_val, int grid, int variant, hipStream_t s) {
+static hipError_t launch_tiled_u(const SlotTableF32& tab, int K, const float* slab, int64_t seg4, int64_t tstride4,
+                                 const float* acc_in, float* out, int64_t n4, float fin_val, int grid, int variant,
+                                 hipStream_t s) {
     const f32x4* sl = reinterpret_cast<const f32x4*>(slab);
     const f32x4* ai = reinterpret_cast<const f32x4*>(acc_in);
     f32x4* o = reinterpret_cast<f32x4*>(out);
     if ((variant & 4) && K >= UNROLL && K % UNROLL == 0) {
         if (variant & 2) {
             hipLaunchKernelGGL((fedavg_tiled_pipe_f32x4<OP, FIN, ACC_IN, UNROLL, false, CPL>), dim3(grid), dim3(kBlock),
-                               0, s, tab, K, sl, k_max, ai, o, n4, fin_val);
+                               0, s, tab, K, sl, seg4, tstride4, ai, o, n4, fin_val);
         } else {
             hipLaunchKernelGGL((fedavg_tiled_pipe_f32x4<OP, FIN, ACC_IN, UNROLL, true, CPL>), dim3(grid), dim3(kBlock),
-                               0, s, tab, K, sl, k_max, ai, o, n4, fin_val);
+                               0, s, tab, K, sl, seg4, tstride4, ai, o, n4, fin_val);
         }
     } else if (variant & 2) {
         hipLaunchKernelGGL((fedavg_tiled_f32x4<OP, FIN, ACC_IN, UNROLL, false, CPL>), dim3(grid), dim3(kBlock), 0, s,
-                           tab, K, sl, k_max, ai, o, n4, fin_val);
+                           tab, K, sl, seg4, tstride4, ai, o, n4, fin_val);
     } else {
         hipLaunchKernelGGL((fedavg_tiled_f32x4<OP, FIN, ACC_IN, UNROLL, true, CPL>), dim3(grid), dim3(kBlock), 0, s,
-                           tab, K, sl, k_max, ai, o, n4, fin_val);
+                           tab, K, sl, seg4, tstride4, ai, o, n4, fin_val);
     }
     return hipGetLastError();
 }
 
 template <int OP, int FIN, bool ACC_IN, int CPL>
-static hipError_t launch_tiled_c(const SlotTableF32& tab, int K, const float* slab, int64_t k_max, const float* acc_in,
-                                 float* out, int64_t n4, float fin_val, int grid, int unroll, int variant,
-                                 hipStream_t s) {
+static hipError_t launch_tiled_c(const SlotTableF32& tab, int K, const float* slab, int64_t seg4, int64_t tstride4,
+                                 const float* acc_in, float* out, int64_t n4, float fin_val, int grid, int unroll,
+                                 int variant, hipStream_t s) {
     if (unroll == 4)
-        return launch_tiled_u<OP, FIN, ACC_IN, CPL, 4>(tab, K, slab, k_max, acc_in, out, n4, fin_val, grid, variant, s);
-    return launch_tiled_u<OP, FIN, ACC_IN, CPL, 8>(tab, K, slab, k_max, acc_in, out, n4, fin_val, grid, variant, s);
+        return launch_tiled_u<OP, FIN, ACC_IN, CPL, 4>(tab, K, slab, seg4, tstride4, acc_in, out, n4, fin_val, grid,
+                                                       variant, s);
+    return launch_tiled_u<OP, FIN, ACC_IN, CPL, 8>(tab, K, slab, seg4, tstride4, acc_in, out, n4, fin_val, grid,
+                                                   variant, s);
 }
 
 template <int OP, int FIN>
-static hipError_t launch_tiled_f(const SlotTableF32& tab, int K, const float* slab, int64_t k_max, int64_t tile4,
+static hipError_t launch_tiled_f(const SlotTableF32& tab, int K, const float* slab, int64_t seg4, int64_t tstride4,
+                                 int64_t tile4,
                                  const float* acc_in, float* out, int64_t n4, float fin_val, int grid, int unroll,
                                  int variant, hipStream_t s) {
 #define FEDAVG_TILED_CPL(C)                                                                                        \
-    return acc_in ? launch_tiled_c<OP, FIN, true, C>(tab, K, slab, k_max, acc_in, out, n4, fin_val, grid, unroll,  \
+    return acc_in ? launch_tiled_c<OP, FIN, true, C>(tab, K, slab, seg4, tstride4, acc_in, out, n4, fin_val, grid, unroll,  \
                                                      variant, s)                                                   \
-                  : launch_tiled_c<OP, FIN, false, C>(tab, K, slab, k_max, acc_in, out, n4, fin_val, grid, unroll, \
+                  : launch_tiled_c<OP, FIN, false, C>(tab, K, slab, seg4, tstride4, acc_in, out, n4, fin_val, grid, unroll, \
                                                       variant, s);
     switch (tile4 / kBlock) {
         case 1:
@@ -584,19 +594,20 @@ static hipError_t launch_tiled_f(const SlotTableF32& tab, int K, const float* sl
 #undef FEDAVG_TILED_CPL
 }
 
-hipError_t launch_tiled_f32x4(const SlotTableF32& tab, int K, const float* slab, int64_t k_max, int64_t tile4,
+hipError_t launch_tiled_f32x4(const SlotTableF32& tab, int K, const float* slab, int64_t seg4, int64_t tstride4,
+                              int64_t tile4,
                               const float* acc_in, float* out, int64_t n4, int op, int fin, float fin_val, int grid,
                               int unroll, int variant, hipStream_t s) {
 #define FEDAVG_TILED_FIN(OPV)                                                                                   \
     switch (fin) {                                                                                              \
         case FEDAVG_FIN_SCALE:                                                                                  \
-            return launch_tiled_f<OPV, FEDAVG_FIN_SCALE>(tab, K, slab, k_max, tile4, acc_in, out, n4, fin_val, grid, \
+            return launch_tiled_f<OPV, FEDAVG_FIN_SCALE>(tab, K, slab, seg4, tstride4, tile4, acc_in, out, n4, fin_val, grid, \
                                                          unroll, variant, s);                                           \
         case FEDAVG_FIN_DIV:                                                                                    \
-            return launch_tiled_f<OPV, FEDAVG_FIN_DIV>(tab, K, slab, k_max, tile4, acc_in, out, n4, fin_val, grid,   \
+            return launch_tiled_f<OPV, FEDAVG_FIN_DIV>(tab, K, slab, seg4, tstride4, tile4, acc_in, out, n4, fin_val, grid,   \
                                                        unroll, variant, s);                                             \
         default:                                                                                                \
-            return launch_tiled_f<OPV, FEDAVG_FIN_NONE>(tab, K, slab, k_max, tile4, acc_in, out, n4, fin_val, grid,  \
+            return launch_tiled_f<OPV, FEDAVG_FIN_NONE>(tab, K, slab, seg4, tstride4, tile4, acc_in, out, n4, fin_val, grid,  \
                                                         unroll, variant, s);                                            \
     }
     switch (op) {
@@ -610,10 +621,10 @@ hipError_t launch_tiled_f32x4(const SlotTableF32& tab, int K, const float* slab,
 #undef FEDAVG_TILED_FIN
 }
 
-hipError_t launch_fill_synthetic_tiled_f32(float* slab, int64_t k_max, int64_t tile_elems, int64_t total, uint64_t seed,
-                                           uint64_t col0, int grid, hipStream_t s) {
-    hipLaunchKernelGGL(fedavg_fill_synthetic_tiled_f32, dim3(grid), dim3(kBlock), 0, s, slab, k_max, tile_elems, total,
-                       seed, col0);
+hipError_t launch_fill_synthetic_tiled_f32(float* slab, int64_t k_max, int64_t tile_elems, int64_t seg, int64_t tstride,
+                                           int64_t n, uint64_t seed, uint64_t col0, int grid, hipStream_t s) {
+    hipLaunchKernelGGL(fedavg_fill_synthetic_tiled_f32, dim3(grid), dim3(kBlock), 0, s, slab, k_max, tile_elems, seg,
+                       tstride, n, seed, col0);
     return hipGetLastError();
 }
 

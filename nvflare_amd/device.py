@@ -26,6 +26,30 @@ def fedavg_dtype(dt) -> int:
     return _NP_TO_DT[dt]
 
 
+class TiledLayout:
+    """Geometry of a tiled client slab (see fedavg_accumulate_tiled in include/nvflare_amd_fedavg.h).
+
+    Element i of the client in slot s is at  (i // tile) * tile_stride + s * seg_stride + i % tile.
+    seg_pad / tile_pad (elements) stagger the DRAM channels concurrently streamed tiles start on."""
+
+    __slots__ = ("tile", "k_max", "seg_stride", "tile_stride")
+
+    def __init__(self, tile: int, k_max: int, seg_pad: int = 0, tile_pad: int = 0):
+        self.tile = int(tile)
+        self.k_max = int(k_max)
+        self.seg_stride = self.tile + int(seg_pad)
+        self.tile_stride = self.k_max * self.seg_stride + int(tile_pad)
+
+    def n_tiles(self, n: int) -> int:
+        return (int(n) + self.tile - 1) // self.tile
+
+    def slab_elems(self, n: int) -> int:
+        return self.n_tiles(n) * self.tile_stride
+
+    def __repr__(self):
+        return f"TiledLayout(tile={self.tile}, k_max={self.k_max}, seg_stride={self.seg_stride}, tile_stride={self.tile_stride})"
+
+
 class DeviceBuffer:
     """Device memory owned through a DeviceContext; freed on close() or garbage collection."""
 
@@ -169,19 +193,21 @@ class DeviceContext:
             ctypes.c_double(float(count)),
         )
 
-    def accumulate_tiled(self, slab_ptr: int, k_max: int, tile_elems: int, slots, weights, n: int, out_ptr: int,
-                         op: int, fin: int, count: float = 1.0, acc_in_ptr: Optional[int] = None) -> None:
+    def accumulate_tiled(self, slab_ptr: int, layout, slots, weights, n: int, out_ptr: int, op: int, fin: int,
+                         count: float = 1.0, acc_in_ptr: Optional[int] = None) -> None:
+        """layout: TiledLayout (tile_elems, seg_stride, tile_stride, k_max)."""
         k = len(slots)
         s_arr = (ctypes.c_int * max(k, 1))(*[int(s) for s in slots])
         w_arr = (ctypes.c_double * max(k, 1))(*[float(w) for w in weights])
-        N.call("fedavg_accumulate_tiled", self.handle, ctypes.c_void_p(slab_ptr), ctypes.c_int(k_max),
-               ctypes.c_size_t(tile_elems), s_arr, w_arr, ctypes.c_int(k), ctypes.c_void_p(acc_in_ptr or 0),
-               ctypes.c_void_p(out_ptr), ctypes.c_size_t(n), ctypes.c_int(op), ctypes.c_int(fin),
-               ctypes.c_double(float(count)))
+        N.call("fedavg_accumulate_tiled", self.handle, ctypes.c_void_p(slab_ptr), ctypes.c_size_t(layout.tile),
+               ctypes.c_size_t(layout.seg_stride), ctypes.c_size_t(layout.tile_stride), ctypes.c_int(layout.k_max),
+               s_arr, w_arr, ctypes.c_int(k), ctypes.c_void_p(acc_in_ptr or 0), ctypes.c_void_p(out_ptr),
+               ctypes.c_size_t(n), ctypes.c_int(op), ctypes.c_int(fin), ctypes.c_double(float(count)))
 
-    def fill_synthetic_tiled_f32(self, slab_ptr: int, k_max: int, tile_elems: int, n: int, seed: int, col0: int = 0):
-        N.call("fedavg_fill_synthetic_tiled_f32", self.handle, ctypes.c_void_p(slab_ptr), ctypes.c_int(k_max),
-               ctypes.c_size_t(tile_elems), ctypes.c_size_t(n), ctypes.c_uint64(seed), ctypes.c_uint64(col0))
+    def fill_synthetic_tiled_f32(self, slab_ptr: int, layout, n: int, seed: int, col0: int = 0):
+        N.call("fedavg_fill_synthetic_tiled_f32", self.handle, ctypes.c_void_p(slab_ptr), ctypes.c_int(layout.k_max),
+               ctypes.c_size_t(layout.tile), ctypes.c_size_t(layout.seg_stride), ctypes.c_size_t(layout.tile_stride),
+               ctypes.c_size_t(n), ctypes.c_uint64(seed), ctypes.c_uint64(col0))
 
     def set_timing(self, enable: bool) -> None:
         N.call("fedavg_set_timing", self.handle, ctypes.c_int(1 if enable else 0))

@@ -290,14 +290,17 @@ def test_timing_events(ctx):
 @pytest.mark.parametrize("tile", [1024, 2048, 4096, 8192])
 @pytest.mark.parametrize("variant", [0, 2, 4, 6])
 @pytest.mark.parametrize("K,unroll", [(13, 8), (16, 4), (16, 8), (24, 8)])
-def test_tiled_slab_vs_oracle(ctx, oracle, tile, variant, K, unroll):
+@pytest.mark.parametrize("seg_pad,tile_pad", [(0, 0), (64, 1040)])
+def test_tiled_slab_vs_oracle(ctx, oracle, tile, variant, K, unroll, seg_pad, tile_pad):
     """Tiled slab layout (client segments interleaved per tile) with a permuted arrival order; variants 4/6
     take the software-pipelined kernel when K % unroll == 0 (and include grid-stride tile reuse)."""
+    from nvflare_amd.device import TiledLayout
+
     n = 7 * 4096 + 1024 + 12  # ragged last tile
-    k_max = 24
-    n_tiles = (n + tile - 1) // tile
-    slab = ctx.alloc(n_tiles * k_max * tile * 4)
-    ctx.fill_synthetic_tiled_f32(slab.ptr, k_max, tile, n, 77, 5)
+    lay = TiledLayout(tile, 24, seg_pad, tile_pad)
+    k_max = lay.k_max
+    slab = ctx.alloc(lay.slab_elems(n) * 4)
+    ctx.fill_synthetic_tiled_f32(slab.ptr, lay, n, 77, 5)
     order = [int(x) for x in np.random.default_rng(tile).permutation(k_max)[:K]]
     ws = [0.25 + 1.5 * j for j in range(K)]
     rows = [oracle.synth_values(77, s, np.arange(5, 5 + n, dtype=np.uint64)) for s in order]
@@ -306,7 +309,7 @@ def test_tiled_slab_vs_oracle(ctx, oracle, tile, variant, K, unroll):
     ctx.set_launch(1 if variant & 4 else 0, unroll)  # few blocks: several tiles per block
     try:
         for op, fin, mode in ((1, 2, oracle.MODE_TORCH), (0, 1, oracle.MODE_NUMPY), (2, 1, oracle.MODE_NUMPY)):
-            ctx.accumulate_tiled(slab.ptr, k_max, tile, order, ws, n, out.ptr, op, fin, _sum(ws))
+            ctx.accumulate_tiled(slab.ptr, lay, order, ws, n, out.ptr, op, fin, _sum(ws))
             got = np.empty(n, np.float32)
             ctx.d2h(got, out.ptr)
             exp = oracle.fedavg_c(rows, ws, mode, weighted=(op != 2), fin=fin)
