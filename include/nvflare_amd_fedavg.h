@@ -130,7 +130,8 @@ int fedavg_timing_end(fedavg_ctx* ctx, float* ms);
 /* Launch tuning (0 = default): blocks per CU of the streaming kernel, rows unrolled per group. */
 int fedavg_set_launch(fedavg_ctx* ctx, int blocks_per_cu, int unroll);
 /* Streaming-kernel variant: bit 0 = two float4 columns per lane (rows kernel), bit 1 = temporal (cached)
- * loads, bit 2 = software-pipelined tiled kernel (tiled path, K % unroll == 0). */
+ * loads, bit 2 = software-pipelined tiled kernel (tiled path, K % unroll == 0), bit 3 = nontemporal
+ * result stores. */
 int fedavg_set_variant(fedavg_ctx* ctx, int variant);
 
 /* Synthetic inputs for benchmarks/tests: dst[j] = synth(seed, row, col0 + j), fp32, bit-identical

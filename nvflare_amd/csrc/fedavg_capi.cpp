@@ -403,7 +403,7 @@ int fedavg_timing_end(fedavg_ctx* ctx, float* ms) {
 int fedavg_set_variant(fedavg_ctx* ctx, int variant) {
     return guarded([&] {
         if (!ctx) throw Error("ctx is NULL");
-        if (variant < 0 || variant > 7) throw Error("variant must be 0..7");
+        if (variant < 0 || variant > 15) throw Error("variant must be 0..15");
         ctx->variant = variant;
     });
 }

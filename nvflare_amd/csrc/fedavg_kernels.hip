@@ -101,7 +101,7 @@ __device__ __forceinline__ void store4(f32x4* p, f32x4 v) {
 //   UNROLL rows whose loads are issued before their arrival-ordered arithmetic
 //   NT     nontemporal load hint (every client byte is read exactly once)
 // ---------------------------------------------------------------------------------------------
-template <int OP, int FIN, bool ACC_IN, int UNROLL, bool NT, int VEC>
+template <int OP, int FIN, bool ACC_IN, int UNROLL, bool NT, int VEC, bool NTS = false>
 __global__ void __launch_bounds__(kBlock) fedavg_rows_f32x4(const RowTableF32 tab, const int K,
                                                              const f32x4* acc_in, f32x4* out,
                                                              const int64_t n4, const float fin_val) {
@@ -137,7 +137,7 @@ __global__ void __launch_bounds__(kBlock) fedavg_rows_f32x4(const RowTableF32 ta
                     acc[c] = step4<OP>(acc[c], load4<NT>(tab.rows[k] + base + c * kBlock), tab.w[k]);
             }
 #pragma unroll
-            for (int c = 0; c < VEC; ++c) store4<false>(out + base + c * kBlock, fin4<FIN>(acc[c], fin_val));
+            for (int c = 0; c < VEC; ++c) store4<NTS>(out + base + c * kBlock, fin4<FIN>(acc[c], fin_val));
         } else {
             // ragged last tile (VEC > 1): column by column
             for (int c = 0; c < VEC; ++c) {
@@ -162,7 +162,7 @@ __global__ void __launch_bounds__(kBlock) fedavg_rows_f32x4(const RowTableF32 ta
 // fp32 tiled-slab kernel: clients interleaved per tile, slab[t][slot][T4] (f32x4 units).  The K rows of
 // one tile are contiguous, so a block streams K*T4*16 contiguous bytes per tile.
 // ---------------------------------------------------------------------------------------------
-template <int OP, int FIN, bool ACC_IN, int UNROLL, bool NT, int CPL>
+template <int OP, int FIN, bool ACC_IN, int UNROLL, bool NT, int CPL, bool NTS = false>
 __global__ void __launch_bounds__(kBlock) fedavg_tiled_f32x4(const SlotTableF32 tab, const int K,
                                                               const f32x4* __restrict__ slab, const int64_t seg4,
                                                               const int64_t tstride4, const f32x4* acc_in, f32x4* out,
@@ -207,7 +207,7 @@ __global__ void __launch_bounds__(kBlock) fedavg_tiled_f32x4(const SlotTableF32 
 #pragma unroll
         for (int c = 0; c < CPL; ++c) {
             const int64_t i = col0 + c * kBlock;
-            if (i < n4) store4<false>(out + i, fin4<FIN>(acc[c], fin_val));
+            if (i < n4) store4<NTS>(out + i, fin4<FIN>(acc[c], fin_val));
         }
     }
 }
@@ -383,9 +383,14 @@ __global__ void __launch_bounds__(kBlock) fedavg_gather_f32(const float* src, co
 // ---------------------------------------------------------------------------------------------
 template <int OP, int FIN, bool ACC_IN, int UNROLL, bool NT, int VEC>
 static hipError_t launch_f32x4_v(const RowTableF32& tab, int K, const float* acc_in, float* out, int64_t n4,
-                                 float fin_val, int grid, hipStream_t s) {
-    hipLaunchKernelGGL((fedavg_rows_f32x4<OP, FIN, ACC_IN, UNROLL, NT, VEC>), dim3(grid), dim3(kBlock), 0, s, tab, K,
-                       reinterpret_cast<const f32x4*>(acc_in), reinterpret_cast<f32x4*>(out), n4, fin_val);
+                                 float fin_val, int grid, int variant, hipStream_t s) {
+    if (variant & 8) {
+        hipLaunchKernelGGL((fedavg_rows_f32x4<OP, FIN, ACC_IN, UNROLL, NT, VEC, true>), dim3(grid), dim3(kBlock), 0, s,
+                           tab, K, reinterpret_cast<const f32x4*>(acc_in), reinterpret_cast<f32x4*>(out), n4, fin_val);
+    } else {
+        hipLaunchKernelGGL((fedavg_rows_f32x4<OP, FIN, ACC_IN, UNROLL, NT, VEC>), dim3(grid), dim3(kBlock), 0, s, tab,
+                           K, reinterpret_cast<const f32x4*>(acc_in), reinterpret_cast<f32x4*>(out), n4, fin_val);
+    }
     return hipGetLastError();
 }
 
@@ -395,13 +400,13 @@ static hipError_t launch_f32x4_u(const RowTableF32& tab, int K, const float* acc
                                  float fin_val, int grid, int variant, hipStream_t s) {
     switch (variant & 3) {
         case 1:
-            return launch_f32x4_v<OP, FIN, ACC_IN, UNROLL, true, 2>(tab, K, acc_in, out, n4, fin_val, grid, s);
+            return launch_f32x4_v<OP, FIN, ACC_IN, UNROLL, true, 2>(tab, K, acc_in, out, n4, fin_val, grid, variant, s);
         case 2:
-            return launch_f32x4_v<OP, FIN, ACC_IN, UNROLL, false, 1>(tab, K, acc_in, out, n4, fin_val, grid, s);
+            return launch_f32x4_v<OP, FIN, ACC_IN, UNROLL, false, 1>(tab, K, acc_in, out, n4, fin_val, grid, variant, s);
         case 3:
-            return launch_f32x4_v<OP, FIN, ACC_IN, UNROLL, false, 2>(tab, K, acc_in, out, n4, fin_val, grid, s);
+            return launch_f32x4_v<OP, FIN, ACC_IN, UNROLL, false, 2>(tab, K, acc_in, out, n4, fin_val, grid, variant, s);
         default:
-            return launch_f32x4_v<OP, FIN, ACC_IN, UNROLL, true, 1>(tab, K, acc_in, out, n4, fin_val, grid, s);
+            return launch_f32x4_v<OP, FIN, ACC_IN, UNROLL, true, 1>(tab, K, acc_in, out, n4, fin_val, grid, variant, s);
     }
 }
 
@@ -548,6 +553,9 @@ static hipError_t launch_tiled_u(const SlotTableF32& tab, int K, const float* sl
             hipLaunchKernelGGL((fedavg_tiled_pipe_f32x4<OP, FIN, ACC_IN, UNROLL, true, CPL>), dim3(grid), dim3(kBlock),
                                0, s, tab, K, sl, seg4, tstride4, ai, o, n4, fin_val);
         }
+    } else if (variant & 8) {
+        hipLaunchKernelGGL((fedavg_tiled_f32x4<OP, FIN, ACC_IN, UNROLL, true, CPL, true>), dim3(grid), dim3(kBlock), 0,
+                           s, tab, K, sl, seg4, tstride4, ai, o, n4, fin_val);
     } else if (variant & 2) {
         hipLaunchKernelGGL((fedavg_tiled_f32x4<OP, FIN, ACC_IN, UNROLL, false, CPL>), dim3(grid), dim3(kBlock), 0, s,
                            tab, K, sl, seg4, tstride4, ai, o, n4, fin_val);
