@@ -39,10 +39,12 @@ def parse():
     ap.add_argument("--clients", type=int, default=64)
     ap.add_argument("--params", type=float, default=1e9, help="fp32 params per GPU bucket")
     ap.add_argument("--mode", choices=["torch", "numpy"], default="torch")
-    ap.add_argument("--blocks-per-cu", type=int, default=0)
-    ap.add_argument("--unroll", type=int, default=0)
+    ap.add_argument("--blocks-per-cu", type=int, default=0, help="0 = library default (2)")
+    ap.add_argument("--unroll", type=int, default=0, help="0 = library default (4)")
+    ap.add_argument("--variant", type=int, default=0, help="cache policy bits (0 = nontemporal loads+stores)")
+    ap.add_argument("--tile", type=int, default=4096, help="slab tile width (elements)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-sample-params", type=int, default=8 * 1024 * 1024)
+    ap.add_argument("--cpu-sample-params", type=int, default=16 * 1024 * 1024)
     ap.add_argument("--spot-check", type=int, default=4096, help="sampled outputs checked against the oracle")
     ap.add_argument("--traffic-bytes", type=float, default=None,
                     help="HBM bytes per launch from a separate rocprofv3 --pmc pass (reported in roofline.traffic)")
@@ -88,7 +90,7 @@ def max_over_ranks(world, value: float) -> float:
     return float(t.item())
 
 
-def cpu_baseline_and_spot_check(args, ctx, rows, out_buf, weights, count, P, col0, op):
+def cpu_baseline_and_spot_check(args, ctx, K, out_buf, weights, count, P, col0, op):
     """Oracle leg (test infrastructure): time the reference restatement on the host, then check sampled
     device outputs bit-for-bit against the oracle computed from the host twin of the generator."""
     import torch
@@ -96,7 +98,6 @@ def cpu_baseline_and_spot_check(args, ctx, rows, out_buf, weights, count, P, col
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     from oracle import fedavg_oracle as orc
 
-    K = len(rows)
     res = {}
     # -- spot check at full size -----------------------------------------------------------------
     if args.spot_check > 0:
@@ -115,7 +116,7 @@ def cpu_baseline_and_spot_check(args, ctx, rows, out_buf, weights, count, P, col
         trows = [torch.from_numpy(g) for g in gen]
         threads = torch.get_num_threads()
         reps, t_tot = 0, 0.0
-        while t_tot < 10.0 and reps < 200:
+        while t_tot < 10.0 and reps < 2000:
             t0 = time.perf_counter()
             if op == 1:
                 orc.torch_mode_reference(trows, weights)
@@ -147,11 +148,11 @@ def main():
     world, rank, local = dist_setup(args)
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     from nvflare_amd import _native as N
-    from nvflare_amd.device import DeviceContext
+    from nvflare_amd.device import DeviceContext, TiledLayout
 
     ctx = DeviceContext.get(local)
-    if args.blocks_per_cu or args.unroll:
-        ctx.set_launch(args.blocks_per_cu, args.unroll)
+    ctx.set_launch(args.blocks_per_cu, args.unroll)
+    ctx.set_variant(args.variant)
     K = int(args.clients)
     P = int(args.params)
     op = N.FEDAVG_OP_TORCH if args.mode == "torch" else N.FEDAVG_OP_NUMPY
@@ -159,25 +160,26 @@ def main():
     col0 = rank * P  # weak scaling: rank r owns param bucket [r*P, (r+1)*P)
 
     free, total = ctx.mem_info()
-    need = (K + 1) * P * 4
+    lay = TiledLayout(args.tile, K)  # the engine's slab layout: K client slots interleaved per tile
+    need = lay.slab_elems(P) * 4 + P * 4
     if need > free:
         raise SystemExit(f"rank {rank}: workload needs {need / 2**30:.1f} GiB, device has {free / 2**30:.1f} GiB free")
 
-    # stacked client rows [K][P] (one allocation per client slot) + the result bucket
-    rows = [ctx.alloc(P * 4) for _ in range(K)]
-    out = ctx.alloc(P * 4)
-    for k, b in enumerate(rows):
-        ctx.fill_synthetic_f32(b.ptr, P, args.seed, k, col0)
+    end = (P + 3) // 4 * 4
+    slab = ctx.alloc(lay.slab_elems(P) * 4)
+    out = ctx.alloc(end * 4)
+    bases = [slab.ptr + lay.slot_offset_elems(k) * 4 for k in range(K)]
+    for k, base in enumerate(bases):
+        ctx.fill_synthetic_f32(base, P, args.seed, k, col0, lay.tile, lay.tile_stride)
     ctx.sync()
     # per-client weights: aggregation_weight 1.0 x NUM_STEPS_CURRENT_ROUND = 1 + (37k mod 100)
     weights = [1.0 * float(1 + (37 * k) % 100) for k in range(K)]
     count = None
     for w in weights:
         count = w if count is None else count + w
-    ptrs = [b.ptr for b in rows]
 
     def step():
-        ctx.accumulate(ptrs, weights, P, out.ptr, N.FEDAVG_F32, N.FEDAVG_F32, op, fin, count)
+        ctx.accumulate_tiled(bases, weights, lay.tile, lay.tile_stride, 0, end, out.ptr, op, fin, count)
 
     for _ in range(args.warmup):
         step()
@@ -197,7 +199,7 @@ def main():
 
     extra = {}
     if rank == 0 and world == 1:
-        extra = cpu_baseline_and_spot_check(args, ctx, rows, out, weights, count, P, col0, op)
+        extra = cpu_baseline_and_spot_check(args, ctx, K, out, weights, count, P, col0, op)
 
     if rank == 0:
         bytes_step = 4.0 * K * P * world  # aggregated client bytes per step, all ranks
@@ -223,6 +225,7 @@ def main():
                 "params_per_gpu": P,
                 "mode": args.mode,
                 "parallelism": f"param-bucket shards x{world}, no data-path collective",
+                "layout": f"tiled slab, {lay.tile}-element tiles x {K} slots",
             },
             "pct_hbm_peak": round(100.0 * achieved / HBM_PEAK_GBS, 2),
             "roofline": {

@@ -84,16 +84,20 @@ int fedavg_free(fedavg_ctx* ctx, void* dptr);
  * caller arrays, weighted_aggregation_helper.py:181-199).  Later compute on the handle is ordered
  * after the copy. */
 int fedavg_h2d(fedavg_ctx* ctx, void* dst, const void* src, size_t nbytes);
-/* dst_pitch/src_pitch/width in bytes, `height` rows: strided H2D (tiled slabs). */
-int fedavg_h2d_2d(fedavg_ctx* ctx, void* dst, size_t dst_pitch, const void* src, size_t src_pitch,
-                  size_t width, size_t height);
+/* The same into TILED client storage: logical byte b (b >= logical_offset) of one client's flat row is
+ * written to base + (b / tile_bytes) * tile_stride_bytes + b % tile_bytes (see fedavg_accumulate_tiled). */
+int fedavg_h2d_tiled(fedavg_ctx* ctx, void* base, size_t tile_bytes, size_t tile_stride_bytes,
+                     size_t logical_offset, const void* src, size_t nbytes);
+/* Device-resident source (e.g. a torch tensor on the GPU) into tiled client storage, on the compute stream. */
+int fedavg_d2d_tiled(fedavg_ctx* ctx, void* base, size_t tile_bytes, size_t tile_stride_bytes,
+                     size_t logical_offset, const void* src, size_t nbytes);
 /* Device -> host; returns when the bytes are in `dst` (waits for prior compute on the handle). */
 int fedavg_d2h(fedavg_ctx* ctx, void* dst, const void* src, size_t nbytes);
 int fedavg_d2d(fedavg_ctx* ctx, void* dst, const void* src, size_t nbytes);
 int fedavg_memset(fedavg_ctx* ctx, void* dst, int value, size_t nbytes);
 int fedavg_sync(fedavg_ctx* ctx);
 
-/* THE HOT PATH.  For every element i < n, in arrival order k = 0..k_rows-1:
+/* THE HOT PATH, contiguous client rows.  For every element i < n, in arrival order k = 0..k_rows-1:
  *   acc = acc_in ? acc_in[i] : first(rows[0][i])      (first row consumed when acc_in == NULL)
  *   acc = step(acc, rows[k][i], acc_t(weights[k]))
  *   out[i] = fin(acc)
@@ -101,21 +105,23 @@ int fedavg_sync(fedavg_ctx* ctx);
  * weights: host array of k_rows fp64 weights; rounded to acc_dtype as the reference does.
  * count: fp64 arrival-order sum of weights (weighted_aggregation_helper.py:201,216), used by fin.
  * acc_in may equal out (in-place continuation).  Any k_rows >= 0 (k_rows == 0 needs acc_in).
- * Supported (in_dtype, acc_dtype): (F32,F32) vectorised fast path; (F64,F64); (F32,F64);
- * (I32|I64, F32); (I32|I64, F64). */
+ * Supported (in_dtype, acc_dtype): (F32,F32) streaming fast path (16-byte aligned pointers; whole tiles
+ * of fedavg_set_tile elements, the ragged tail and unaligned rows take a scalar kernel); (F64,F64);
+ * (F32,F64); (I32|I64, F32); (I32|I64, F64). */
 int fedavg_accumulate(fedavg_ctx* ctx, const void* const* rows, const double* weights, int k_rows,
                       const void* acc_in, void* out, size_t n, int in_dtype, int acc_dtype, int op,
                       int fin, double count);
 
-/* Tiled-slab variant of the hot path (fp32): client rows interleaved per tile.  Element i of the
- * client in slot s lives at  slab[(i / tile_elems) * tile_stride + s * seg_stride + i % tile_elems],
- * so one tile's client segments are contiguous in HBM (padding in the strides staggers the DRAM
- * channels that concurrently streamed tiles start on).  slots[k] is the slot of the k-th arrival.
- * tile_elems in {1024, 2048, 4096, 8192}; strides in elements, multiples of 4, seg_stride >= tile_elems,
- * tile_stride >= k_max * seg_stride; n % 4 == 0; k_rows <= 128; out/acc_in are flat [n]. */
-int fedavg_accumulate_tiled(fedavg_ctx* ctx, const void* slab, size_t tile_elems, size_t seg_stride,
-                            size_t tile_stride, int k_max, const int* slots, const double* weights, int k_rows,
-                            const void* acc_in, void* out, size_t n, int op, int fin, double count);
+/* THE HOT PATH, tiled client storage (fp32; the engine's slab layout).  Element i of client k lives at
+ *   bases[k] + (i / tile_elems) * tile_stride + i % tile_elems          (in elements)
+ * so a slab of S clients with tile_stride = S * tile_elems keeps one tile's S client segments contiguous
+ * in HBM.  Computes out[i] for begin <= i < end with the same per-element sequence as fedavg_accumulate;
+ * out and acc_in are flat arrays indexed by i.  Every client's storage must cover the whole tiles that
+ * [begin, end) touches.  tile_elems in {1024, 2048, 4096, 8192}; tile_stride, begin, end multiples of 4;
+ * pointers 16-byte aligned; any k_rows (more than 128 are chained through out). */
+int fedavg_accumulate_tiled(fedavg_ctx* ctx, const void* const* bases, const double* weights, int k_rows,
+                            size_t tile_elems, size_t tile_stride, size_t begin, size_t end,
+                            const void* acc_in, void* out, int op, int fin, double count);
 
 /* Timing of the kernels launched by the last fedavg_accumulate call, measured with HIP events on
  * the stream they ran on (enable first; costs two event records per call). */
@@ -127,20 +133,20 @@ int fedavg_last_kernel_ms(fedavg_ctx* ctx, float* ms);
 int fedavg_timing_begin(fedavg_ctx* ctx);
 int fedavg_timing_end(fedavg_ctx* ctx, float* ms);
 
-/* Launch tuning (0 = default): blocks per CU of the streaming kernel, rows unrolled per group. */
+/* Launch tuning (0 = default): blocks per CU of the streaming kernel (default 2), clients whose loads
+ * are issued together (4 or 8, default 4). */
 int fedavg_set_launch(fedavg_ctx* ctx, int blocks_per_cu, int unroll);
-/* Streaming-kernel variant: bit 0 = two float4 columns per lane (rows kernel), bit 1 = temporal (cached)
- * loads, bit 2 = software-pipelined tiled kernel (tiled path, K % unroll == 0), bit 3 = nontemporal
- * result stores. */
+/* Streaming-kernel cache policy: bit 0 = temporal (cached) client loads, bit 1 = temporal result stores
+ * (default 0: both nontemporal -- every byte is touched once). */
 int fedavg_set_variant(fedavg_ctx* ctx, int variant);
+/* Tile width used by fedavg_accumulate for contiguous rows (default 4096 elements). */
+int fedavg_set_tile(fedavg_ctx* ctx, int tile_elems);
 
-/* Synthetic inputs for benchmarks/tests: dst[j] = synth(seed, row, col0 + j), fp32, bit-identical
- * to the host twin oracle_synth_value() in oracle/fedavg_oracle.c. */
-int fedavg_fill_synthetic_f32(fedavg_ctx* ctx, float* dst, size_t n, uint64_t seed, uint64_t row,
-                              uint64_t col0);
-/* Same values laid out as a tiled slab (see fedavg_accumulate_tiled): slot k holds synth row k. */
-int fedavg_fill_synthetic_tiled_f32(fedavg_ctx* ctx, float* slab, int k_max, size_t tile_elems, size_t seg_stride,
-                                    size_t tile_stride, size_t n, uint64_t seed, uint64_t col0);
+/* Synthetic inputs for benchmarks/tests: logical element j of a client row (tiled like
+ * fedavg_accumulate_tiled; tile_elems == 0 means contiguous) = synth(seed, row, col0 + j), fp32,
+ * bit-identical to the host twin oracle_synth_value() in oracle/fedavg_oracle.c. */
+int fedavg_fill_synthetic_f32(fedavg_ctx* ctx, float* dst, size_t n, size_t tile_elems, size_t tile_stride,
+                              uint64_t seed, uint64_t row, uint64_t col0);
 /* Gather m fp32 elements src[idx[j]] (idx: host array) into host_out (spot checks at full size). */
 int fedavg_gather_f32(fedavg_ctx* ctx, const float* src, const uint64_t* idx, size_t m, float* host_out);
 

@@ -52,7 +52,8 @@ _SIGNATURES = {
     "fedavg_malloc": [c_void_p, c_size_t, ctypes.POINTER(c_void_p)],
     "fedavg_free": [c_void_p, c_void_p],
     "fedavg_h2d": [c_void_p, c_void_p, c_void_p, c_size_t],
-    "fedavg_h2d_2d": [c_void_p, c_void_p, c_size_t, c_void_p, c_size_t, c_size_t, c_size_t],
+    "fedavg_h2d_tiled": [c_void_p, c_void_p, c_size_t, c_size_t, c_size_t, c_void_p, c_size_t],
+    "fedavg_d2d_tiled": [c_void_p, c_void_p, c_size_t, c_size_t, c_size_t, c_void_p, c_size_t],
     "fedavg_d2h": [c_void_p, c_void_p, c_void_p, c_size_t],
     "fedavg_d2d": [c_void_p, c_void_p, c_void_p, c_size_t],
     "fedavg_memset": [c_void_p, c_void_p, c_int, c_size_t],
@@ -73,17 +74,15 @@ _SIGNATURES = {
     ],
     "fedavg_accumulate_tiled": [
         c_void_p,  # ctx
-        c_void_p,  # slab
-        c_size_t,  # tile_elems
-        c_size_t,  # seg_stride
-        c_size_t,  # tile_stride
-        c_int,  # k_max
-        ctypes.POINTER(c_int),  # slots
+        ctypes.POINTER(c_void_p),  # bases
         ctypes.POINTER(c_double),  # weights
         c_int,  # k_rows
+        c_size_t,  # tile_elems
+        c_size_t,  # tile_stride
+        c_size_t,  # begin
+        c_size_t,  # end
         c_void_p,  # acc_in
         c_void_p,  # out
-        c_size_t,  # n
         c_int,  # op
         c_int,  # fin
         c_double,  # count
@@ -94,8 +93,8 @@ _SIGNATURES = {
     "fedavg_timing_end": [c_void_p, ctypes.POINTER(c_float)],
     "fedavg_set_launch": [c_void_p, c_int, c_int],
     "fedavg_set_variant": [c_void_p, c_int],
-    "fedavg_fill_synthetic_f32": [c_void_p, c_void_p, c_size_t, c_u64, c_u64, c_u64],
-    "fedavg_fill_synthetic_tiled_f32": [c_void_p, c_void_p, c_int, c_size_t, c_size_t, c_size_t, c_size_t, c_u64, c_u64],
+    "fedavg_set_tile": [c_void_p, c_int],
+    "fedavg_fill_synthetic_f32": [c_void_p, c_void_p, c_size_t, c_size_t, c_size_t, c_u64, c_u64, c_u64],
     "fedavg_gather_f32": [c_void_p, c_void_p, c_void_p, c_size_t, c_void_p],
 }
 EXPORTED = ["fedavg_last_error", "fedavg_abi_version", *_SIGNATURES.keys()]

@@ -8,7 +8,6 @@
 #include <string.h>
 
 #include <algorithm>
-#include <cstdio>
 #include <exception>
 #include <new>
 #include <string>
@@ -27,13 +26,13 @@ struct Error : std::exception {
     const char* what() const noexcept override { return msg.c_str(); }
 };
 
-#define HIP_CHECK(expr)                                                                                 \
-    do {                                                                                                \
-        hipError_t _e = (expr);                                                                         \
-        if (_e != hipSuccess) {                                                                         \
+#define HIP_CHECK(expr)                                                                                     \
+    do {                                                                                                    \
+        hipError_t _e = (expr);                                                                             \
+        if (_e != hipSuccess) {                                                                             \
             throw Error(std::string(#expr) + " failed: " + hipGetErrorName(_e) + " (" + hipGetErrorString(_e) + \
-                        ")");                                                                           \
-        }                                                                                               \
+                        ")");                                                                               \
+        }                                                                                                   \
     } while (0)
 
 template <typename F>
@@ -55,21 +54,12 @@ int guarded(F&& f) {
 }
 
 constexpr int kRingSlots = 4;
-constexpr size_t kRingBytes = 64ull << 20;  // 64 MiB per pinned slot
+constexpr size_t kRingBytes = 64ull << 20;  // 64 MiB per pinned staging slot
 constexpr size_t kParallelCopyMin = 8ull << 20;
 constexpr int kCopyThreads = 8;
 
-size_t dtype_size(int dt) {
-    switch (dt) {
-        case FEDAVG_F32:
-        case FEDAVG_I32:
-            return 4;
-        case FEDAVG_F64:
-        case FEDAVG_I64:
-            return 8;
-        default:
-            throw Error("unknown dtype " + std::to_string(dt));
-    }
+void check_dtype(int dt) {
+    if (dt < FEDAVG_F32 || dt > FEDAVG_I64) throw Error("unknown dtype " + std::to_string(dt));
 }
 
 void parallel_memcpy(void* dst, const void* src, size_t n) {
@@ -77,11 +67,10 @@ void parallel_memcpy(void* dst, const void* src, size_t n) {
         memcpy(dst, src, n);
         return;
     }
-    const int nt = kCopyThreads;
-    const size_t chunk = ((n + nt - 1) / nt + 4095) & ~size_t(4095);
+    const size_t chunk = ((n + kCopyThreads - 1) / kCopyThreads + 4095) & ~size_t(4095);
     std::vector<std::thread> th;
-    th.reserve(nt);
-    for (int t = 0; t < nt; ++t) {
+    th.reserve(kCopyThreads);
+    for (int t = 0; t < kCopyThreads; ++t) {
         const size_t off = (size_t)t * chunk;
         if (off >= n) break;
         const size_t len = std::min(chunk, n - off);
@@ -107,9 +96,10 @@ struct fedavg_ctx {
     hipEvent_t ring_ev[kRingSlots] = {};
     bool ring_used[kRingSlots] = {};
     int ring_next = 0;
-    int blocks_per_cu = 0;  // 0 = default
-    int unroll = 0;         // 0 = default
-    int variant = 0;        // streaming-kernel variant (bit 0: 2 columns per lane, bit 1: temporal loads)
+    int blocks_per_cu = fedavg::kDefaultBlocksPerCu;
+    int unroll = fedavg::kDefaultUnroll;
+    int variant = 0;
+    int tile = fedavg::kDefaultTile;  // tile width of the contiguous-rows entry point
 
     hipStream_t compute() const { return ext_stream ? ext_stream : own_stream; }
     void activate() const { HIP_CHECK(hipSetDevice(device)); }
@@ -127,59 +117,155 @@ bool is_pinned_host(const void* p) {
 }
 
 int stream_grid(const fedavg_ctx* ctx, int64_t work_items) {
-    const int bpc = ctx->blocks_per_cu > 0 ? ctx->blocks_per_cu : 8;
-    const int64_t cap = (int64_t)ctx->num_cus * bpc;
+    const int64_t cap = (int64_t)ctx->num_cus * 8;
     const int64_t need = (work_items + fedavg::kBlock - 1) / fedavg::kBlock;
     return (int)std::max<int64_t>(1, std::min<int64_t>(cap, need));
 }
 
-// streaming kernel grid: tiles of (VEC * kBlock) float4
-int stream_grid_tiles(const fedavg_ctx* ctx, int64_t n4) {
-    const int vec = (ctx->variant & 1) ? 2 : 1;
-    return stream_grid(ctx, (n4 + vec - 1) / vec);
-}
+bool valid_tile(size_t t) { return t == 1024 || t == 2048 || t == 4096 || t == 8192; }
 
-// H2D of `height` rows; pageable sources go through the pinned ring (memcpy on the host threads,
-// DMA on the copy stream, overlapped slot by slot).  The compute stream waits on the copies.
-void h2d_impl(fedavg_ctx* ctx, char* dst, size_t dpitch, const char* src, size_t spitch, size_t width,
-              size_t height) {
-    if (width == 0 || height == 0) return;
-    ctx->activate();
-    const bool contiguous = (dpitch == width && spitch == width);
-    if (is_pinned_host(src)) {
-        if (contiguous) {
-            HIP_CHECK(hipMemcpyAsync(dst, src, width * height, hipMemcpyHostToDevice, ctx->copy_stream));
-        } else {
-            HIP_CHECK(hipMemcpy2DAsync(dst, dpitch, src, spitch, width, height, hipMemcpyHostToDevice,
-                                       ctx->copy_stream));
-        }
-        // the caller may reuse a pinned source right after return: wait for this copy
-        HIP_CHECK(hipStreamSynchronize(ctx->copy_stream));
+// Copy `len` bytes from `src` into the tiled storage of one client: logical byte b of the client's flat
+// row lands at dst + (b / tile_b) * tstride_b + b % tile_b.  Issued as (partial head, one 2-D copy of
+// whole tiles, partial tail) on `s`.
+void copy_into_tiles(char* dst, size_t tile_b, size_t tstride_b, size_t logical_off, const char* src, size_t len,
+                     hipMemcpyKind kind, hipStream_t s) {
+    if (tstride_b == tile_b) {
+        HIP_CHECK(hipMemcpyAsync(dst + logical_off, src, len, kind, s));
         return;
     }
-    if (contiguous) {
-        width = width * height;
-        height = 1;
-        dpitch = spitch = width;
+    size_t b = logical_off;
+    const size_t end = logical_off + len;
+    auto place = [&](size_t lb) { return dst + (lb / tile_b) * tstride_b + lb % tile_b; };
+    if (b % tile_b) {
+        const size_t head = std::min(end, (b / tile_b + 1) * tile_b) - b;
+        HIP_CHECK(hipMemcpyAsync(place(b), src, head, kind, s));
+        src += head;
+        b += head;
     }
-    for (size_t r = 0; r < height; ++r) {
-        size_t off = 0;
-        while (off < width) {
-            const int slot = ctx->ring_next;
-            ctx->ring_next = (ctx->ring_next + 1) % kRingSlots;
-            if (ctx->ring_used[slot]) HIP_CHECK(hipEventSynchronize(ctx->ring_ev[slot]));
-            const size_t len = std::min(kRingBytes, width - off);
-            parallel_memcpy(ctx->ring[slot], src + r * spitch + off, len);
-            HIP_CHECK(hipMemcpyAsync(dst + r * dpitch + off, ctx->ring[slot], len, hipMemcpyHostToDevice,
-                                     ctx->copy_stream));
-            HIP_CHECK(hipEventRecord(ctx->ring_ev[slot], ctx->copy_stream));
-            ctx->ring_used[slot] = true;
-            off += len;
-        }
+    const size_t full = (end - b) / tile_b;
+    if (full) {
+        HIP_CHECK(hipMemcpy2DAsync(place(b), tstride_b, src, tile_b, tile_b, full, kind, s));
+        src += full * tile_b;
+        b += full * tile_b;
+    }
+    if (b < end) HIP_CHECK(hipMemcpyAsync(place(b), src, end - b, kind, s));
+}
+
+// H2D into (tiled) client storage.  Pageable sources go through the pinned ring: the host threads copy a
+// 64 MiB slot while the DMA engine drains the previous ones.  The compute stream waits on the copies; the
+// caller may reuse `src` as soon as this returns.
+void h2d_impl(fedavg_ctx* ctx, char* dst, size_t tile_b, size_t tstride_b, size_t logical_off, const char* src,
+              size_t len) {
+    if (len == 0) return;
+    ctx->activate();
+    if (is_pinned_host(src)) {
+        copy_into_tiles(dst, tile_b, tstride_b, logical_off, src, len, hipMemcpyHostToDevice, ctx->copy_stream);
+        HIP_CHECK(hipStreamSynchronize(ctx->copy_stream));  // a pinned source may be reused on return
+        return;
+    }
+    size_t done = 0;
+    while (done < len) {
+        const int slot = ctx->ring_next;
+        ctx->ring_next = (ctx->ring_next + 1) % kRingSlots;
+        if (ctx->ring_used[slot]) HIP_CHECK(hipEventSynchronize(ctx->ring_ev[slot]));
+        const size_t n = std::min(kRingBytes, len - done);
+        parallel_memcpy(ctx->ring[slot], src + done, n);
+        copy_into_tiles(dst, tile_b, tstride_b, logical_off + done, static_cast<const char*>(ctx->ring[slot]), n,
+                        hipMemcpyHostToDevice, ctx->copy_stream);
+        HIP_CHECK(hipEventRecord(ctx->ring_ev[slot], ctx->copy_stream));
+        ctx->ring_used[slot] = true;
+        done += n;
     }
     HIP_CHECK(hipEventRecord(ctx->ev_copy_done, ctx->copy_stream));
     HIP_CHECK(hipStreamWaitEvent(ctx->compute(), ctx->ev_copy_done, 0));
 }
+
+void check_op_fin(int op, int fin) {
+    if (op < FEDAVG_OP_NUMPY || op > FEDAVG_OP_UNWEIGHTED) throw Error("bad op " + std::to_string(op));
+    if (fin < FEDAVG_FIN_NONE || fin > FEDAVG_FIN_DIV) throw Error("bad fin " + std::to_string(fin));
+}
+
+// finalisation scalar, computed on the host exactly as the reference computes it:
+//   numpy  T * (1.0 / count): python fp64 reciprocal, then cast to the array dtype
+//   torch  T.div_(count):     the scalar operand cast to the tensor dtype
+double fin_scalar(int fin, double count) { return fin == FEDAVG_FIN_SCALE ? 1.0 / count : count; }
+
+// Tile-kernel launches over [b, e) (elements, multiples of 4) for any number of clients: chunks of at
+// most kMaxRowsPerLaunch clients, later chunks continuing in place through `out`.
+void run_tiles(fedavg_ctx* ctx, const void* const* bases, const double* weights, int k_rows, int64_t tile,
+               int64_t tstride, int64_t b, int64_t e, const float* acc_in, float* out, int op, int fin, double count,
+               hipStream_t s) {
+    fedavg::TileLaunch L;
+    L.op = op;
+    L.unroll = ctx->unroll;
+    L.variant = ctx->variant;
+    L.tile4 = tile / 4;
+    L.tstride4 = tstride / 4;
+    L.b4 = b / 4;
+    L.e4 = e / 4;
+    const int64_t n_tiles = (L.e4 - 1) / L.tile4 - L.b4 / L.tile4 + 1;
+    L.grid = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)ctx->num_cus * ctx->blocks_per_cu, n_tiles));
+    const float fv = (float)fin_scalar(fin, count);
+    int k0 = 0;
+    const float* cur_in = acc_in;
+    do {
+        const int kc = std::min(k_rows - k0, fedavg::kMaxRowsPerLaunch);
+        memset(&L.tab, 0, sizeof(L.tab));
+        for (int j = 0; j < kc; ++j) {
+            L.tab.rows[j] = static_cast<const fedavg::f32x4*>(bases[k0 + j]);
+            L.tab.w[j] = (float)weights[k0 + j];  // fp64 host weight -> fp32, round to nearest
+        }
+        L.k = kc;
+        L.fin = (k0 + kc >= k_rows) ? fin : FEDAVG_FIN_NONE;
+        L.fin_val = fv;
+        L.acc_in = cur_in;
+        L.out = out;
+        HIP_CHECK(fedavg::launch_tiles_f32x4(L, s));
+        cur_in = out;
+        k0 += kc;
+    } while (k0 < k_rows);
+}
+
+void run_generic(fedavg_ctx* ctx, const void* const* rows, const double* weights, int k_rows, size_t elem_off,
+                 const void* acc_in, void* out, int64_t n, int in_dtype, int acc_dtype, int op, int fin, double count,
+                 hipStream_t s) {
+    const size_t in_sz = (in_dtype == FEDAVG_F64 || in_dtype == FEDAVG_I64) ? 8 : 4;
+    const size_t acc_sz = acc_dtype == FEDAVG_F64 ? 8 : 4;
+    const double fd = fin_scalar(fin, count);
+    int k0 = 0;
+    const char* cur_in = acc_in ? static_cast<const char*>(acc_in) + elem_off * acc_sz : nullptr;
+    char* o = static_cast<char*>(out) + elem_off * acc_sz;
+    do {
+        const int kc = std::min(k_rows - k0, fedavg::kMaxRowsPerLaunch);
+        fedavg::RowTableGeneric gt;
+        memset(&gt, 0, sizeof(gt));
+        for (int j = 0; j < kc; ++j) {
+            gt.rows[j] = static_cast<const char*>(rows[k0 + j]) + elem_off * in_sz;
+            // weight rounded to the accumulator type on the host (the kernel's cast is then exact)
+            gt.w[j] = acc_dtype == FEDAVG_F32 ? (double)(float)weights[k0 + j] : weights[k0 + j];
+        }
+        const bool last = k0 + kc >= k_rows;
+        const double fv = acc_dtype == FEDAVG_F32 ? (double)(float)fd : fd;
+        HIP_CHECK(fedavg::launch_rows_generic(gt, kc, cur_in, o, n, in_dtype, acc_dtype, op,
+                                              last ? fin : FEDAVG_FIN_NONE, fv, stream_grid(ctx, n), s));
+        cur_in = o;
+        k0 += kc;
+    } while (k0 < k_rows);
+}
+
+struct TimingScope {
+    fedavg_ctx* ctx;
+    hipStream_t s;
+    TimingScope(fedavg_ctx* c, hipStream_t st) : ctx(c), s(st) {
+        if (ctx->timing) HIP_CHECK(hipEventRecord(ctx->ev_start, s));
+    }
+    void done() {
+        if (ctx->timing) {
+            HIP_CHECK(hipEventRecord(ctx->ev_stop, s));
+            ctx->timed_valid = true;
+        }
+    }
+};
 
 }  // namespace
 
@@ -217,9 +303,9 @@ int fedavg_create(int device, fedavg_ctx** out) {
             HIP_CHECK(hipStreamCreateWithFlags(&ctx->copy_stream, hipStreamNonBlocking));
             HIP_CHECK(hipEventCreate(&ctx->ev_start));
             HIP_CHECK(hipEventCreate(&ctx->ev_stop));
-            HIP_CHECK(hipEventCreateWithFlags(&ctx->ev_copy_done, hipEventDisableTiming));
             HIP_CHECK(hipEventCreate(&ctx->ev_region_start));
             HIP_CHECK(hipEventCreate(&ctx->ev_region_stop));
+            HIP_CHECK(hipEventCreateWithFlags(&ctx->ev_copy_done, hipEventDisableTiming));
             for (int i = 0; i < kRingSlots; ++i) {
                 HIP_CHECK(hipHostMalloc(&ctx->ring[i], kRingBytes, hipHostMallocDefault));
                 HIP_CHECK(hipEventCreateWithFlags(&ctx->ring_ev[i], hipEventDisableTiming));
@@ -242,11 +328,8 @@ int fedavg_destroy(fedavg_ctx* ctx) {
             if (ctx->ring[i]) (void)hipHostFree(ctx->ring[i]);
             if (ctx->ring_ev[i]) (void)hipEventDestroy(ctx->ring_ev[i]);
         }
-        if (ctx->ev_start) (void)hipEventDestroy(ctx->ev_start);
-        if (ctx->ev_stop) (void)hipEventDestroy(ctx->ev_stop);
-        if (ctx->ev_copy_done) (void)hipEventDestroy(ctx->ev_copy_done);
-        if (ctx->ev_region_start) (void)hipEventDestroy(ctx->ev_region_start);
-        if (ctx->ev_region_stop) (void)hipEventDestroy(ctx->ev_region_stop);
+        for (hipEvent_t ev : {ctx->ev_start, ctx->ev_stop, ctx->ev_copy_done, ctx->ev_region_start, ctx->ev_region_stop})
+            if (ev) (void)hipEventDestroy(ev);
         if (ctx->own_stream) (void)hipStreamDestroy(ctx->own_stream);
         if (ctx->copy_stream) (void)hipStreamDestroy(ctx->copy_stream);
     });
@@ -306,18 +389,32 @@ int fedavg_h2d(fedavg_ctx* ctx, void* dst, const void* src, size_t nbytes) {
         if (!ctx) throw Error("ctx is NULL");
         if (nbytes == 0) return;
         if (!dst || !src) throw Error("NULL pointer");
-        h2d_impl(ctx, static_cast<char*>(dst), nbytes, static_cast<const char*>(src), nbytes, nbytes, 1);
+        h2d_impl(ctx, static_cast<char*>(dst), nbytes, nbytes, 0, static_cast<const char*>(src), nbytes);
     });
 }
 
-int fedavg_h2d_2d(fedavg_ctx* ctx, void* dst, size_t dst_pitch, const void* src, size_t src_pitch, size_t width,
-                  size_t height) {
+int fedavg_h2d_tiled(fedavg_ctx* ctx, void* base, size_t tile_bytes, size_t tile_stride_bytes, size_t logical_offset,
+                     const void* src, size_t nbytes) {
     return guarded([&] {
         if (!ctx) throw Error("ctx is NULL");
-        if (width == 0 || height == 0) return;
-        if (!dst || !src) throw Error("NULL pointer");
-        if (dst_pitch < width || src_pitch < width) throw Error("pitch smaller than width");
-        h2d_impl(ctx, static_cast<char*>(dst), dst_pitch, static_cast<const char*>(src), src_pitch, width, height);
+        if (nbytes == 0) return;
+        if (!base || !src) throw Error("NULL pointer");
+        if (tile_bytes == 0 || tile_stride_bytes < tile_bytes) throw Error("bad tile geometry");
+        h2d_impl(ctx, static_cast<char*>(base), tile_bytes, tile_stride_bytes, logical_offset,
+                 static_cast<const char*>(src), nbytes);
+    });
+}
+
+int fedavg_d2d_tiled(fedavg_ctx* ctx, void* base, size_t tile_bytes, size_t tile_stride_bytes, size_t logical_offset,
+                     const void* src, size_t nbytes) {
+    return guarded([&] {
+        if (!ctx) throw Error("ctx is NULL");
+        if (nbytes == 0) return;
+        if (!base || !src) throw Error("NULL pointer");
+        if (tile_bytes == 0 || tile_stride_bytes < tile_bytes) throw Error("bad tile geometry");
+        ctx->activate();
+        copy_into_tiles(static_cast<char*>(base), tile_bytes, tile_stride_bytes, logical_offset,
+                        static_cast<const char*>(src), nbytes, hipMemcpyDeviceToDevice, ctx->compute());
     });
 }
 
@@ -361,6 +458,78 @@ int fedavg_sync(fedavg_ctx* ctx) {
     });
 }
 
+int fedavg_accumulate(fedavg_ctx* ctx, const void* const* rows, const double* weights, int k_rows,
+                      const void* acc_in, void* out, size_t n, int in_dtype, int acc_dtype, int op, int fin,
+                      double count) {
+    return guarded([&] {
+        if (!ctx) throw Error("ctx is NULL");
+        if (k_rows < 0) throw Error("k_rows < 0");
+        if (k_rows == 0 && !acc_in) throw Error("k_rows == 0 requires acc_in");
+        check_op_fin(op, fin);
+        check_dtype(in_dtype);
+        check_dtype(acc_dtype);
+        if (acc_dtype != FEDAVG_F32 && acc_dtype != FEDAVG_F64) throw Error("acc_dtype must be F32 or F64");
+        if (acc_dtype == FEDAVG_F32 && in_dtype == FEDAVG_F64) throw Error("unsupported (F64 -> F32) pair");
+        if (n == 0) {
+            ctx->timed_valid = false;
+            return;
+        }
+        if (!out) throw Error("out is NULL");
+        if (k_rows > 0 && (!rows || !weights)) throw Error("rows/weights NULL");
+        for (int k = 0; k < k_rows; ++k)
+            if (!rows[k]) throw Error("row " + std::to_string(k) + " is NULL");
+        ctx->activate();
+        hipStream_t s = ctx->compute();
+        TimingScope ts(ctx, s);
+        bool vec = in_dtype == FEDAVG_F32 && acc_dtype == FEDAVG_F32 && reinterpret_cast<uintptr_t>(out) % 16 == 0 &&
+                   reinterpret_cast<uintptr_t>(acc_in) % 16 == 0;
+        for (int k = 0; vec && k < k_rows; ++k) vec = reinterpret_cast<uintptr_t>(rows[k]) % 16 == 0;
+        // contiguous rows are tiled storage with tile_stride == tile: whole tiles take the streaming kernel,
+        // the ragged remainder (< one tile) the scalar kernel
+        const int64_t tile = ctx->tile;
+        const int64_t n_full = vec ? ((int64_t)n / tile) * tile : 0;
+        if (n_full > 0) {
+            run_tiles(ctx, rows, weights, k_rows, tile, tile, 0, n_full, static_cast<const float*>(acc_in),
+                      static_cast<float*>(out), op, fin, count, s);
+        }
+        if ((int64_t)n > n_full) {
+            run_generic(ctx, rows, weights, k_rows, (size_t)n_full, acc_in, out, (int64_t)n - n_full, in_dtype,
+                        acc_dtype, op, fin, count, s);
+        }
+        ts.done();
+    });
+}
+
+int fedavg_accumulate_tiled(fedavg_ctx* ctx, const void* const* bases, const double* weights, int k_rows,
+                            size_t tile_elems, size_t tile_stride, size_t begin, size_t end, const void* acc_in,
+                            void* out, int op, int fin, double count) {
+    return guarded([&] {
+        if (!ctx) throw Error("ctx is NULL");
+        if (k_rows < 0 || (k_rows == 0 && !acc_in)) throw Error("k_rows == 0 requires acc_in");
+        check_op_fin(op, fin);
+        if (!valid_tile(tile_elems)) throw Error("tile_elems must be 1024, 2048, 4096 or 8192");
+        if (tile_stride < tile_elems || tile_stride % 4) throw Error("tile_stride must be >= tile_elems, multiple of 4");
+        if (begin % 4 || end % 4 || end < begin) throw Error("begin/end must be multiples of 4 with begin <= end");
+        if (end == begin) {
+            ctx->timed_valid = false;
+            return;
+        }
+        if (!out) throw Error("out is NULL");
+        if (reinterpret_cast<uintptr_t>(out) % 16 || reinterpret_cast<uintptr_t>(acc_in) % 16)
+            throw Error("out/acc_in must be 16-byte aligned");
+        if (k_rows > 0 && (!bases || !weights)) throw Error("bases/weights NULL");
+        for (int k = 0; k < k_rows; ++k)
+            if (!bases[k] || reinterpret_cast<uintptr_t>(bases[k]) % 16)
+                throw Error("base " + std::to_string(k) + " NULL or not 16-byte aligned");
+        ctx->activate();
+        hipStream_t s = ctx->compute();
+        TimingScope ts(ctx, s);
+        run_tiles(ctx, bases, weights, k_rows, (int64_t)tile_elems, (int64_t)tile_stride, (int64_t)begin, (int64_t)end,
+                  static_cast<const float*>(acc_in), static_cast<float*>(out), op, fin, count, s);
+        ts.done();
+    });
+}
+
 int fedavg_set_timing(fedavg_ctx* ctx, int enable) {
     return guarded([&] {
         if (!ctx) throw Error("ctx is NULL");
@@ -372,7 +541,7 @@ int fedavg_set_timing(fedavg_ctx* ctx, int enable) {
 int fedavg_last_kernel_ms(fedavg_ctx* ctx, float* ms) {
     return guarded([&] {
         if (!ctx || !ms) throw Error("NULL argument");
-        if (!ctx->timed_valid) throw Error("no timed fedavg_accumulate call (enable with fedavg_set_timing)");
+        if (!ctx->timed_valid) throw Error("no timed accumulate call (enable with fedavg_set_timing)");
         ctx->activate();
         HIP_CHECK(hipEventSynchronize(ctx->ev_stop));
         HIP_CHECK(hipEventElapsedTime(ms, ctx->ev_start, ctx->ev_stop));
@@ -400,188 +569,44 @@ int fedavg_timing_end(fedavg_ctx* ctx, float* ms) {
     });
 }
 
+int fedavg_set_launch(fedavg_ctx* ctx, int blocks_per_cu, int unroll) {
+    return guarded([&] {
+        if (!ctx) throw Error("ctx is NULL");
+        if (blocks_per_cu < 0 || blocks_per_cu > 32) throw Error("blocks_per_cu out of range");
+        if (unroll != 0 && unroll != 4 && unroll != 8) throw Error("unroll must be 0, 4 or 8");
+        ctx->blocks_per_cu = blocks_per_cu ? blocks_per_cu : fedavg::kDefaultBlocksPerCu;
+        ctx->unroll = unroll ? unroll : fedavg::kDefaultUnroll;
+    });
+}
+
 int fedavg_set_variant(fedavg_ctx* ctx, int variant) {
     return guarded([&] {
         if (!ctx) throw Error("ctx is NULL");
-        if (variant < 0 || variant > 15) throw Error("variant must be 0..15");
+        if (variant < 0 || variant > 3) throw Error("variant must be 0..3");
         ctx->variant = variant;
     });
 }
 
-int fedavg_set_launch(fedavg_ctx* ctx, int blocks_per_cu, int unroll) {
+int fedavg_set_tile(fedavg_ctx* ctx, int tile_elems) {
     return guarded([&] {
         if (!ctx) throw Error("ctx is NULL");
-        if (blocks_per_cu < 0 || blocks_per_cu > 64) throw Error("blocks_per_cu out of range");
-        if (unroll != 0 && unroll != 4 && unroll != 8 && unroll != 16) throw Error("unroll must be 0, 4, 8 or 16");
-        ctx->blocks_per_cu = blocks_per_cu;
-        ctx->unroll = unroll;
+        if (tile_elems == 0) tile_elems = fedavg::kDefaultTile;
+        if (!valid_tile((size_t)tile_elems)) throw Error("tile_elems must be 1024, 2048, 4096 or 8192");
+        ctx->tile = tile_elems;
     });
 }
 
-int fedavg_accumulate(fedavg_ctx* ctx, const void* const* rows, const double* weights, int k_rows,
-                      const void* acc_in, void* out, size_t n, int in_dtype, int acc_dtype, int op, int fin,
-                      double count) {
-    return guarded([&] {
-        if (!ctx) throw Error("ctx is NULL");
-        if (k_rows < 0) throw Error("k_rows < 0");
-        if (k_rows == 0 && !acc_in) throw Error("k_rows == 0 requires acc_in");
-        if (op < FEDAVG_OP_NUMPY || op > FEDAVG_OP_UNWEIGHTED) throw Error("bad op");
-        if (fin < FEDAVG_FIN_NONE || fin > FEDAVG_FIN_DIV) throw Error("bad fin");
-        const size_t in_sz = dtype_size(in_dtype);
-        const size_t acc_sz = dtype_size(acc_dtype);
-        (void)in_sz;
-        if (acc_dtype != FEDAVG_F32 && acc_dtype != FEDAVG_F64) throw Error("acc_dtype must be F32 or F64");
-        const bool pair_ok = (acc_dtype == FEDAVG_F32 && in_dtype != FEDAVG_F64) || acc_dtype == FEDAVG_F64;
-        if (!pair_ok) throw Error("unsupported (in_dtype, acc_dtype) pair");
-        if (n == 0) {
-            ctx->timed_valid = false;
-            return;
-        }
-        if (!out) throw Error("out is NULL");
-        if (k_rows > 0 && (!rows || !weights)) throw Error("rows/weights NULL");
-        for (int k = 0; k < k_rows; ++k)
-            if (!rows[k]) throw Error("row " + std::to_string(k) + " is NULL");
-        ctx->activate();
-        hipStream_t s = ctx->compute();
-        if (ctx->timing) HIP_CHECK(hipEventRecord(ctx->ev_start, s));
-
-        // finalisation scalar, computed on the host exactly as the reference computes it:
-        //   numpy  T * (1.0 / count): python fp64 reciprocal, then cast to the array dtype
-        //   torch  T.div_(count):     the scalar operand cast to the tensor dtype
-        const double fin_d = (fin == FEDAVG_FIN_SCALE) ? (1.0 / count) : count;
-
-        const bool vec_ok = in_dtype == FEDAVG_F32 && acc_dtype == FEDAVG_F32;
-        bool aligned = vec_ok && (reinterpret_cast<uintptr_t>(out) % 16 == 0) &&
-                       (!acc_in || reinterpret_cast<uintptr_t>(acc_in) % 16 == 0);
-        for (int k = 0; aligned && k < k_rows; ++k) aligned = reinterpret_cast<uintptr_t>(rows[k]) % 16 == 0;
-
-        // chunks of at most kMaxRowsPerLaunch rows; each later chunk continues in place through `out`
-        int k0 = 0;
-        const void* cur_in = acc_in;
-        do {
-            const int kc = std::min(k_rows - k0, fedavg::kMaxRowsPerLaunch);
-            const bool last = (k0 + kc >= k_rows);
-            const int fin_c = last ? fin : FEDAVG_FIN_NONE;
-            if (aligned) {
-                fedavg::RowTableF32 tab;
-                memset(&tab, 0, sizeof(tab));
-                for (int j = 0; j < kc; ++j) {
-                    tab.rows[j] = static_cast<const fedavg::f32x4*>(rows[k0 + j]);
-                    tab.w[j] = (float)weights[k0 + j];  // fp64 host weight -> fp32, round to nearest
-                }
-                const int64_t n4 = (int64_t)(n / 4);
-                const int64_t tail = (int64_t)(n % 4);
-                if (n4 > 0) {
-                    HIP_CHECK(fedavg::launch_rows_f32x4(tab, kc, static_cast<const float*>(cur_in),
-                                                        static_cast<float*>(out), n4, op, fin_c, (float)fin_d,
-                                                        stream_grid_tiles(ctx, n4), ctx->unroll, ctx->variant, s));
-                }
-                if (tail > 0) {
-                    fedavg::RowTableGeneric gt;
-                    memset(&gt, 0, sizeof(gt));
-                    for (int j = 0; j < kc; ++j) {
-                        gt.rows[j] = static_cast<const float*>(rows[k0 + j]) + n4 * 4;
-                        gt.w[j] = (double)(float)weights[k0 + j];
-                    }
-                    const void* tin = cur_in ? static_cast<const void*>(static_cast<const float*>(cur_in) + n4 * 4)
-                                             : nullptr;
-                    HIP_CHECK(fedavg::launch_rows_generic(gt, kc, tin, static_cast<float*>(out) + n4 * 4, tail,
-                                                          FEDAVG_F32, FEDAVG_F32, op, fin_c, (double)(float)fin_d, 1,
-                                                          s));
-                }
-            } else {
-                fedavg::RowTableGeneric gt;
-                memset(&gt, 0, sizeof(gt));
-                for (int j = 0; j < kc; ++j) {
-                    gt.rows[j] = rows[k0 + j];
-                    // weight rounded to the accumulator type on the host (the kernel's cast is then exact)
-                    gt.w[j] = acc_dtype == FEDAVG_F32 ? (double)(float)weights[k0 + j] : weights[k0 + j];
-                }
-                const double fv = acc_dtype == FEDAVG_F32 ? (double)(float)fin_d : fin_d;
-                HIP_CHECK(fedavg::launch_rows_generic(gt, kc, cur_in, out, (int64_t)n, in_dtype, acc_dtype, op, fin_c,
-                                                      fv, stream_grid(ctx, (int64_t)n), s));
-            }
-            (void)acc_sz;
-            cur_in = out;
-            k0 += kc;
-        } while (k0 < k_rows);
-
-        if (ctx->timing) {
-            HIP_CHECK(hipEventRecord(ctx->ev_stop, s));
-            ctx->timed_valid = true;
-        }
-    });
-}
-
-int fedavg_accumulate_tiled(fedavg_ctx* ctx, const void* slab, size_t tile_elems, size_t seg_stride, size_t tile_stride,
-                            int k_max, const int* slots, const double* weights, int k_rows, const void* acc_in, void* out,
-                            size_t n, int op, int fin, double count) {
-    return guarded([&] {
-        if (!ctx) throw Error("ctx is NULL");
-        if (k_rows < 0 || (k_rows == 0 && !acc_in)) throw Error("k_rows == 0 requires acc_in");
-        if (k_rows > fedavg::kMaxRowsPerLaunch) throw Error("tiled path takes at most 128 rows per call");
-        if (tile_elems != 1024 && tile_elems != 2048 && tile_elems != 4096 && tile_elems != 8192)
-            throw Error("tile_elems must be 1024, 2048, 4096 or 8192");
-        if (seg_stride < tile_elems || seg_stride % 4 || tile_stride % 4 || k_max <= 0 ||
-            tile_stride < (size_t)k_max * seg_stride)
-            throw Error("need seg_stride >= tile_elems, tile_stride >= k_max * seg_stride, both multiples of 4");
-        if (n % 4 != 0) throw Error("tiled path needs n % 4 == 0");
-        if (op < FEDAVG_OP_NUMPY || op > FEDAVG_OP_UNWEIGHTED || fin < FEDAVG_FIN_NONE || fin > FEDAVG_FIN_DIV)
-            throw Error("bad op/fin");
-        if (n == 0) return;
-        if (!slab || !out) throw Error("NULL pointer");
-        if (reinterpret_cast<uintptr_t>(slab) % 16 || reinterpret_cast<uintptr_t>(out) % 16 ||
-            reinterpret_cast<uintptr_t>(acc_in) % 16)
-            throw Error("tiled path needs 16-byte aligned slab/out/acc_in");
-        fedavg::SlotTableF32 tab;
-        memset(&tab, 0, sizeof(tab));
-        for (int j = 0; j < k_rows; ++j) {
-            if (slots[j] < 0 || slots[j] >= k_max) throw Error("slot out of range");
-            tab.slot[j] = slots[j];
-            tab.w[j] = (float)weights[j];
-        }
-        ctx->activate();
-        hipStream_t s = ctx->compute();
-        if (ctx->timing) HIP_CHECK(hipEventRecord(ctx->ev_start, s));
-        const double fin_d = (fin == FEDAVG_FIN_SCALE) ? (1.0 / count) : count;
-        const int64_t n4 = (int64_t)(n / 4);
-        const int64_t tile4 = (int64_t)(tile_elems / 4);
-        const int64_t n_tiles = (n4 + tile4 - 1) / tile4;
-        const int bpc = ctx->blocks_per_cu > 0 ? ctx->blocks_per_cu : 2;
-        const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)ctx->num_cus * bpc, n_tiles));
-        HIP_CHECK(fedavg::launch_tiled_f32x4(tab, k_rows, static_cast<const float*>(slab), (int64_t)seg_stride / 4,
-                                             (int64_t)tile_stride / 4, tile4, static_cast<const float*>(acc_in),
-                                             static_cast<float*>(out), n4, op, fin, (float)fin_d, grid, ctx->unroll,
-                                             ctx->variant, s));
-        if (ctx->timing) {
-            HIP_CHECK(hipEventRecord(ctx->ev_stop, s));
-            ctx->timed_valid = true;
-        }
-    });
-}
-
-int fedavg_fill_synthetic_tiled_f32(fedavg_ctx* ctx, float* slab, int k_max, size_t tile_elems, size_t seg_stride,
-                                    size_t tile_stride, size_t n, uint64_t seed, uint64_t col0) {
-    return guarded([&] {
-        if (!ctx || !slab) throw Error("NULL argument");
-        if (seg_stride < tile_elems || tile_stride < (size_t)k_max * seg_stride) throw Error("bad strides");
-        const int64_t n_tiles = (int64_t)((n + tile_elems - 1) / tile_elems);
-        const int64_t total = n_tiles * (int64_t)k_max * (int64_t)tile_elems;
-        ctx->activate();
-        HIP_CHECK(fedavg::launch_fill_synthetic_tiled_f32(slab, k_max, (int64_t)tile_elems, (int64_t)seg_stride,
-                                                          (int64_t)tile_stride, (int64_t)n, seed, col0,
-                                                          stream_grid(ctx, total), ctx->compute()));
-    });
-}
-
-int fedavg_fill_synthetic_f32(fedavg_ctx* ctx, float* dst, size_t n, uint64_t seed, uint64_t row, uint64_t col0) {
+int fedavg_fill_synthetic_f32(fedavg_ctx* ctx, float* dst, size_t n, size_t tile_elems, size_t tile_stride,
+                              uint64_t seed, uint64_t row, uint64_t col0) {
     return guarded([&] {
         if (!ctx) throw Error("ctx is NULL");
         if (n == 0) return;
         if (!dst) throw Error("dst is NULL");
+        if (tile_elems == 0) tile_elems = tile_stride = n;
+        if (tile_stride < tile_elems) throw Error("tile_stride < tile_elems");
         ctx->activate();
-        HIP_CHECK(fedavg::launch_fill_synthetic_f32(dst, (int64_t)n, seed, row, col0, stream_grid(ctx, (int64_t)n),
-                                                    ctx->compute()));
+        HIP_CHECK(fedavg::launch_fill_synthetic_f32(dst, (int64_t)n, (int64_t)tile_elems, (int64_t)tile_stride, seed,
+                                                    row, col0, stream_grid(ctx, (int64_t)n), ctx->compute()));
     });
 }
 

@@ -10,18 +10,22 @@ namespace fedavg {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int kBlock = 256;          // 4 waves of 64 lanes
-constexpr int kMaxRowsPerLaunch = 128;  // rows per launch carried in the kernel-argument segment
+constexpr int kBlock = 256;             // 4 waves of 64 lanes
+constexpr int kMaxRowsPerLaunch = 128;  // clients per launch carried in the kernel-argument segment
 
-// Row table passed BY VALUE in the kernarg segment: wave-uniform pointers/weights live in SGPRs.
+// launch defaults, from the MI355X sweeps recorded in profiles/r01
+constexpr int kDefaultTile = 4096;      // elements per client segment per tile (16 KiB)
+constexpr int kDefaultBlocksPerCu = 2;  // 8 waves per CU
+constexpr int kDefaultUnroll = 4;       // clients whose loads are in flight together per lane
+
+// variant bits (fedavg_set_variant)
+constexpr int kVariantTemporalLoads = 1;
+constexpr int kVariantTemporalStores = 2;
+
+// Per-launch client table passed BY VALUE in the kernarg segment: wave-uniform base pointers and
+// weights are loaded with s_load into SGPRs.
 struct RowTableF32 {
     const f32x4* rows[kMaxRowsPerLaunch];
-    float w[kMaxRowsPerLaunch];
-};
-
-// Tiled slab: per launch, the slot (client row inside each tile) and weight of every client in arrival order.
-struct SlotTableF32 {
-    int slot[kMaxRowsPerLaunch];
     float w[kMaxRowsPerLaunch];
 };
 
@@ -30,19 +34,26 @@ struct RowTableGeneric {
     double w[kMaxRowsPerLaunch];
 };
 
-hipError_t launch_rows_f32x4(const RowTableF32& tab, int K, const float* acc_in, float* out, int64_t n4, int op,
-                             int fin, float fin_val, int grid, int unroll, int variant, hipStream_t s);
-hipError_t launch_tiled_f32x4(const SlotTableF32& tab, int K, const float* slab, int64_t seg4, int64_t tstride4,
-                              int64_t tile4,
-                              const float* acc_in, float* out, int64_t n4, int op, int fin, float fin_val, int grid,
-                              int unroll, int variant, hipStream_t s);
-hipError_t launch_fill_synthetic_tiled_f32(float* slab, int64_t k_max, int64_t tile_elems, int64_t seg, int64_t tstride,
-                                           int64_t n, uint64_t seed, uint64_t col0, int grid, hipStream_t s);
+struct TileLaunch {
+    RowTableF32 tab;
+    int k;
+    int op, fin;
+    int unroll, variant;
+    int grid;
+    int64_t tile4;     // tile width, f32x4 units
+    int64_t tstride4;  // tile stride of every client's storage, f32x4 units
+    int64_t b4, e4;    // global f32x4 range
+    const float* acc_in;
+    float* out;
+    float fin_val;
+};
+
+hipError_t launch_tiles_f32x4(const TileLaunch& L, hipStream_t s);
 hipError_t launch_rows_generic(const RowTableGeneric& tab, int K, const void* acc_in, void* out, int64_t n,
                                int in_dtype, int acc_dtype, int op, int fin, double fin_val, int grid,
                                hipStream_t s);
-hipError_t launch_fill_synthetic_f32(float* dst, int64_t n, uint64_t seed, uint64_t row, uint64_t col0, int grid,
-                                     hipStream_t s);
+hipError_t launch_fill_synthetic_f32(float* dst, int64_t n, int64_t tile, int64_t tstride, uint64_t seed, uint64_t row,
+                                     uint64_t col0, int grid, hipStream_t s);
 hipError_t launch_gather_f32(const float* src, const uint64_t* idx, float* dst, int64_t m, hipStream_t s);
 
 }  // namespace fedavg

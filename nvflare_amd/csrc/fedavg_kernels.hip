@@ -6,19 +6,20 @@
 //   weigh_by_local_iter=False :186-199, :208-215 (T = v; T = T + v)
 //
 // Design:
-//   * One pass over the stacked client rows: every element reads K client values once and writes its
-//     result once -- 4*K + 4 bytes per fp32 parameter, no temporaries, HBM-bound (no MFMA: this is
-//     elementwise, not a contraction).
-//   * The per-element operation sequence is exactly the reference's, in arrival order, so the result
-//     is bitwise equal to the reference (not merely within 1 ulp).  This file MUST be compiled with
-//     -ffp-contract=off: the numpy mode's multiply and add round separately; the torch mode calls
-//     __builtin_fmaf explicitly.  fp32 denormals are preserved (gfx950 default IEEE mode).
-//   * Row pointers and fp32 weights travel in the kernel-argument segment: they are wave-uniform, so
-//     the compiler keeps them in SGPRs (s_load from kernarg) and every client row is read with a
-//     saddr-form global_load_dwordx4 (uniform 64-bit base + per-lane 32-bit offset).
-//   * Each lane owns 4 consecutive floats (16 B); a wave reads 1 KiB contiguous per client row; loads
-//     of UNROLL consecutive clients are issued before the dependent arithmetic (memory-level
-//     parallelism), with nontemporal hints because every byte is read exactly once.
+//   * One pass: every parameter reads its K client values once and writes its result once -- 4K + 4 bytes
+//     per fp32 parameter, no temporaries.  HBM-bound; no MFMA (elementwise, not a contraction).
+//   * The per-element operation sequence is the reference's, in arrival order, so results are bitwise
+//     equal to the reference.  Compile with -ffp-contract=off (numpy mode rounds the multiply and the add
+//     separately); the torch mode calls __builtin_fmaf.  fp32 denormals are preserved (IEEE mode).
+//   * Client data is TILED: element i of client k is at  base[k] + (i / TILE) * tile_stride + i % TILE.
+//     With tile_stride == TILE this is a contiguous row; the engine's slabs interleave the K clients per
+//     tile (tile_stride = slots * TILE) so one tile's K client segments are contiguous in HBM and a block
+//     streams them as one sequential run.  Measured on MI355X (profiles/r01): 83 % of HBM spec = 96 % of
+//     the chip's own streaming-read ceiling, against 75 % for K independent row streams.
+//   * Base pointers and fp32 weights travel in the kernel-argument segment: wave-uniform, kept in SGPRs.
+//   * Each lane owns CPL float4 columns of a tile (a wave reads 1 KiB contiguous per client and column
+//     group); UNROLL clients' loads are issued before their arrival-ordered arithmetic.  Loads and the
+//     result stores are nontemporal: every byte is touched exactly once.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -96,103 +97,45 @@ __device__ __forceinline__ void store4(f32x4* p, f32x4 v) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// fp32 streaming kernel: out[i] = fin( fold_k step(acc, rows[k][i], w[k]) ), f32x4 per lane
-//   VEC    float4 columns per lane per tile (tile = VEC * kBlock float4; lane j owns j, j+kBlock, ...)
-//   UNROLL rows whose loads are issued before their arrival-ordered arithmetic
-//   NT     nontemporal load hint (every client byte is read exactly once)
+// THE HOT KERNEL.  Global f32x4 index range [b4, e4); tiles t = b4/T4 .. (e4-1)/T4 are dealt to blocks
+// round-robin.  For every column of a tile:
+//     acc = ACC_IN ? acc_in[i] : first(client 0);  acc = step(acc, client k) for k = 1..K-1 in order;
+//     out[i] = fin(acc)                  (only for i in [b4, e4): partial edge tiles are masked at store)
+// Client loads are unconditional: the caller guarantees every client's tiled storage covers whole
+// tiles (slabs are allocated in whole tiles; the pointer-list entry point sends ragged tails elsewhere).
 // ---------------------------------------------------------------------------------------------
-template <int OP, int FIN, bool ACC_IN, int UNROLL, bool NT, int VEC, bool NTS = false>
-__global__ void __launch_bounds__(kBlock) fedavg_rows_f32x4(const RowTableF32 tab, const int K,
-                                                             const f32x4* acc_in, f32x4* out,
-                                                             const int64_t n4, const float fin_val) {
-    constexpr int64_t kTile = (int64_t)VEC * kBlock;
-    const int64_t stride = (int64_t)gridDim.x * kTile;
-    for (int64_t base = (int64_t)blockIdx.x * kTile + threadIdx.x; base < n4; base += stride) {
-        if (VEC == 1 || base + (VEC - 1) * kBlock < n4) {
-            f32x4 acc[VEC];
-            int k = 0;
-            if constexpr (ACC_IN) {
-#pragma unroll
-                for (int c = 0; c < VEC; ++c) acc[c] = load4<false>(acc_in + base + c * kBlock);
-            } else {
-#pragma unroll
-                for (int c = 0; c < VEC; ++c) acc[c] = first4<OP>(load4<NT>(tab.rows[0] + base + c * kBlock), tab.w[0]);
-                k = 1;
-            }
-            // groups of UNROLL clients: issue all loads, then the arrival-ordered arithmetic
-            for (; k + UNROLL <= K; k += UNROLL) {
-                f32x4 v[UNROLL][VEC];
-#pragma unroll
-                for (int j = 0; j < UNROLL; ++j)
-#pragma unroll
-                    for (int c = 0; c < VEC; ++c) v[j][c] = load4<NT>(tab.rows[k + j] + base + c * kBlock);
-#pragma unroll
-                for (int j = 0; j < UNROLL; ++j)
-#pragma unroll
-                    for (int c = 0; c < VEC; ++c) acc[c] = step4<OP>(acc[c], v[j][c], tab.w[k + j]);
-            }
-            for (; k < K; ++k) {
-#pragma unroll
-                for (int c = 0; c < VEC; ++c)
-                    acc[c] = step4<OP>(acc[c], load4<NT>(tab.rows[k] + base + c * kBlock), tab.w[k]);
-            }
-#pragma unroll
-            for (int c = 0; c < VEC; ++c) store4<NTS>(out + base + c * kBlock, fin4<FIN>(acc[c], fin_val));
-        } else {
-            // ragged last tile (VEC > 1): column by column
-            for (int c = 0; c < VEC; ++c) {
-                const int64_t i = base + c * kBlock;
-                if (i >= n4) break;
-                f32x4 a;
-                int k = 0;
-                if constexpr (ACC_IN) {
-                    a = load4<false>(acc_in + i);
-                } else {
-                    a = first4<OP>(load4<NT>(tab.rows[0] + i), tab.w[0]);
-                    k = 1;
-                }
-                for (; k < K; ++k) a = step4<OP>(a, load4<NT>(tab.rows[k] + i), tab.w[k]);
-                store4<false>(out + i, fin4<FIN>(a, fin_val));
-            }
-        }
-    }
-}
-
-// ---------------------------------------------------------------------------------------------
-// fp32 tiled-slab kernel: clients interleaved per tile, slab[t][slot][T4] (f32x4 units).  The K rows of
-// one tile are contiguous, so a block streams K*T4*16 contiguous bytes per tile.
-// ---------------------------------------------------------------------------------------------
-template <int OP, int FIN, bool ACC_IN, int UNROLL, bool NT, int CPL, bool NTS = false>
-__global__ void __launch_bounds__(kBlock) fedavg_tiled_f32x4(const SlotTableF32 tab, const int K,
-                                                              const f32x4* __restrict__ slab, const int64_t seg4,
-                                                              const int64_t tstride4, const f32x4* acc_in, f32x4* out,
-                                                              const int64_t n4, const float fin_val) {
-    constexpr int64_t T4 = (int64_t)CPL * kBlock;  // tile width in f32x4 (CPL columns per lane)
-    const int64_t n_tiles = (n4 + T4 - 1) / T4;
-    for (int64_t t = blockIdx.x; t < n_tiles; t += gridDim.x) {
-        const f32x4* tile = slab + t * tstride4;
-        const int64_t col0 = t * T4 + threadIdx.x;
+template <int OP, int FIN, bool ACC_IN, int UNROLL, int CPL, bool NTL, bool NTS>
+__global__ void __launch_bounds__(kBlock) fedavg_tiles_f32x4(const RowTableF32 tab, const int K,
+                                                              const int64_t tstride4, const f32x4* acc_in,
+                                                              f32x4* out, const int64_t b4, const int64_t e4,
+                                                              const float fin_val) {
+    constexpr int64_t T4 = (int64_t)CPL * kBlock;
+    const int64_t t_last = (e4 - 1) / T4;
+    for (int64_t t = b4 / T4 + blockIdx.x; t <= t_last; t += gridDim.x) {
+        const int64_t off = t * tstride4 + threadIdx.x;  // offset inside each client's tiled storage
+        const int64_t col = t * T4 + threadIdx.x;        // global f32x4 index of column group 0
         f32x4 acc[CPL];
         int k = 0;
         if constexpr (ACC_IN) {
 #pragma unroll
             for (int c = 0; c < CPL; ++c) {
-                const int64_t i = col0 + c * kBlock;
-                acc[c] = i < n4 ? load4<false>(acc_in + i) : f32x4{0, 0, 0, 0};
+                const int64_t i = col + c * kBlock;
+                acc[c] = (i >= b4 && i < e4) ? load4<false>(acc_in + i) : f32x4{0, 0, 0, 0};
             }
         } else {
-            const f32x4* r = tile + (int64_t)tab.slot[0] * seg4 + threadIdx.x;
+            const f32x4* r = tab.rows[0] + off;
 #pragma unroll
-            for (int c = 0; c < CPL; ++c) acc[c] = first4<OP>(load4<NT>(r + c * kBlock), tab.w[0]);
+            for (int c = 0; c < CPL; ++c) acc[c] = first4<OP>(load4<NTL>(r + c * kBlock), tab.w[0]);
             k = 1;
         }
+        // groups of UNROLL clients: issue all their loads, then the arrival-ordered arithmetic
         for (; k + UNROLL <= K; k += UNROLL) {
             f32x4 v[UNROLL][CPL];
 #pragma unroll
             for (int j = 0; j < UNROLL; ++j) {
-                const f32x4* r = tile + (int64_t)tab.slot[k + j] * seg4 + threadIdx.x;
+                const f32x4* r = tab.rows[k + j] + off;
 #pragma unroll
-                for (int c = 0; c < CPL; ++c) v[j][c] = load4<NT>(r + c * kBlock);
+                for (int c = 0; c < CPL; ++c) v[j][c] = load4<NTL>(r + c * kBlock);
             }
 #pragma unroll
             for (int j = 0; j < UNROLL; ++j)
@@ -200,105 +143,20 @@ __global__ void __launch_bounds__(kBlock) fedavg_tiled_f32x4(const SlotTableF32 
                 for (int c = 0; c < CPL; ++c) acc[c] = step4<OP>(acc[c], v[j][c], tab.w[k + j]);
         }
         for (; k < K; ++k) {
-            const f32x4* r = tile + (int64_t)tab.slot[k] * seg4 + threadIdx.x;
+            const f32x4* r = tab.rows[k] + off;
 #pragma unroll
-            for (int c = 0; c < CPL; ++c) acc[c] = step4<OP>(acc[c], load4<NT>(r + c * kBlock), tab.w[k]);
+            for (int c = 0; c < CPL; ++c) acc[c] = step4<OP>(acc[c], load4<NTL>(r + c * kBlock), tab.w[k]);
         }
 #pragma unroll
         for (int c = 0; c < CPL; ++c) {
-            const int64_t i = col0 + c * kBlock;
-            if (i < n4) store4<NTS>(out + i, fin4<FIN>(acc[c], fin_val));
+            const int64_t i = col + c * kBlock;
+            if (i >= b4 && i < e4) store4<NTS>(out + i, fin4<FIN>(acc[c], fin_val));
         }
     }
 }
-
-// Software-pipelined form of the tiled kernel (K % UNROLL == 0): the loads of the next group of UNROLL
-// clients -- possibly in the block's next tile -- are issued before the current group's arithmetic, so a
-// wave keeps 2 * UNROLL * CPL 16-byte loads in flight instead of draining at every group boundary.
-template <int OP, int FIN, bool ACC_IN, int UNROLL, bool NT, int CPL>
-__global__ void __launch_bounds__(kBlock) fedavg_tiled_pipe_f32x4(const SlotTableF32 tab, const int K,
-                                                                   const f32x4* __restrict__ slab, const int64_t seg4,
-                                                                   const int64_t tstride4, const f32x4* acc_in,
-                                                                   f32x4* out, const int64_t n4, const float fin_val) {
-    constexpr int64_t T4 = (int64_t)CPL * kBlock;
-    const int64_t n_tiles = (n4 + T4 - 1) / T4;
-    const int G = K / UNROLL;  // groups per tile
-    int64_t t = blockIdx.x;
-    if (t >= n_tiles) return;
-    f32x4 bufA[UNROLL][CPL], bufB[UNROLL][CPL];
-    auto issue = [&](f32x4 (&b)[UNROLL][CPL], int64_t tt, int g) {
-        const f32x4* tile = slab + tt * tstride4 + threadIdx.x;
-#pragma unroll
-        for (int j = 0; j < UNROLL; ++j) {
-            const f32x4* r = tile + (int64_t)tab.slot[g * UNROLL + j] * seg4;
-#pragma unroll
-            for (int c = 0; c < CPL; ++c) b[j][c] = load4<NT>(r + c * kBlock);
-        }
-    };
-    // consume one group from `cur` after issuing the next group into `nxt`; returns false when done
-    f32x4 acc[CPL];
-    int g = 0;
-    auto stage = [&](f32x4 (&cur)[UNROLL][CPL], f32x4 (&nxt)[UNROLL][CPL]) -> bool {
-        int64_t tn = t;
-        int gn = g + 1;
-        if (gn == G) {
-            gn = 0;
-            tn = t + gridDim.x;
-        }
-        const bool more = tn < n_tiles;
-        // always issue (the last prefetch re-reads the current tile): a conditional issue would make
-        // the compiler's vmcnt bookkeeping fall back to vmcnt(0) at the join and drain the pipeline
-        issue(nxt, more ? tn : t, gn);
-        if (g == 0) {
-            if constexpr (ACC_IN) {
-#pragma unroll
-                for (int c = 0; c < CPL; ++c) {
-                    const int64_t i = t * T4 + threadIdx.x + c * kBlock;
-                    acc[c] = i < n4 ? load4<false>(acc_in + i) : f32x4{0, 0, 0, 0};
-                }
-#pragma unroll
-                for (int j = 0; j < UNROLL; ++j)
-#pragma unroll
-                    for (int c = 0; c < CPL; ++c) acc[c] = step4<OP>(acc[c], cur[j][c], tab.w[j]);
-            } else {
-#pragma unroll
-                for (int c = 0; c < CPL; ++c) acc[c] = first4<OP>(cur[0][c], tab.w[0]);
-#pragma unroll
-                for (int j = 1; j < UNROLL; ++j)
-#pragma unroll
-                    for (int c = 0; c < CPL; ++c) acc[c] = step4<OP>(acc[c], cur[j][c], tab.w[j]);
-            }
-        } else {
-#pragma unroll
-            for (int j = 0; j < UNROLL; ++j)
-#pragma unroll
-                for (int c = 0; c < CPL; ++c) acc[c] = step4<OP>(acc[c], cur[j][c], tab.w[g * UNROLL + j]);
-        }
-        if (g == G - 1) {
-#pragma unroll
-            for (int c = 0; c < CPL; ++c) {
-                const int64_t i = t * T4 + threadIdx.x + c * kBlock;
-                if (i < n4) store4<false>(out + i, fin4<FIN>(acc[c], fin_val));
-            }
-        }
-        t = tn;
-        g = gn;
-        return more;
-    };
-    issue(bufA, t, 0);
-    // ping-pong between the two register buffers: no register copies, so no wait on in-flight loads
-    while (stage(bufA, bufB) && stage(bufB, bufA)) {
-    }
-}
-
-// synthetic fill of a tiled slab: element (tile t, slot k, j) = synth(seed, k, col0 + t*T + j)
-__global__ void __launch_bounds__(kBlock) fedavg_fill_synthetic_tiled_f32(float* slab, const int64_t k_max,
-                                                                           const int64_t tile_elems, const int64_t seg,
-                                                                           const int64_t tstride, const int64_t n,
-                                                                           const uint64_t seed, const uint64_t col0);
 
 // ---------------------------------------------------------------------------------------------
-// generic scalar kernel: any (Tin, Tacc) pair, any alignment (tails, small keys, fp64, ints)
+// generic scalar kernel: any (Tin, Tacc) pair, contiguous rows, any alignment (ragged tails, fp64, ints)
 // ---------------------------------------------------------------------------------------------
 template <typename Tin, typename Tacc, int OP, int FIN, bool ACC_IN>
 __global__ void __launch_bounds__(kBlock) fedavg_rows_generic(const RowTableGeneric tab, const int K,
@@ -324,7 +182,8 @@ __global__ void __launch_bounds__(kBlock) fedavg_rows_generic(const RowTableGene
 }
 
 // ---------------------------------------------------------------------------------------------
-// synthetic inputs (bit-identical host twin: oracle/fedavg_oracle.c oracle_synth_value)
+// synthetic inputs (bit-identical host twin: oracle/fedavg_oracle.c oracle_synth_value), written to a
+// tiled row: logical element i goes to dst[(i / tile) * tile_stride + i % tile]
 // ---------------------------------------------------------------------------------------------
 __device__ __forceinline__ uint32_t mix32(uint64_t x) {
     x ^= x >> 33;
@@ -335,7 +194,8 @@ __device__ __forceinline__ uint32_t mix32(uint64_t x) {
     return (uint32_t)x;
 }
 
-__global__ void __launch_bounds__(kBlock) fedavg_fill_synthetic_f32(float* dst, const int64_t n, const uint64_t seed,
+__global__ void __launch_bounds__(kBlock) fedavg_fill_synthetic_f32(float* dst, const int64_t n, const int64_t tile,
+                                                                     const int64_t tstride, const uint64_t seed,
                                                                      const uint64_t row, const uint64_t col0) {
     const uint64_t base = (seed * 0x9E3779B97F4A7C15ULL) ^ (row * 0xD1B54A32D192ED03ULL);
     const int64_t stride = (int64_t)gridDim.x * kBlock;
@@ -345,30 +205,8 @@ __global__ void __launch_bounds__(kBlock) fedavg_fill_synthetic_f32(float* dst, 
 #pragma unroll
         for (int j = 0; j < 4; ++j) s += (int32_t)(mix32(base + col * 4ULL + (uint64_t)j) >> 8);
         s -= (int32_t)(1 << 25);
-        dst[i] = (float)s * 1.0323827e-07f;
-    }
-}
-
-__global__ void __launch_bounds__(kBlock) fedavg_fill_synthetic_tiled_f32(float* slab, const int64_t k_max,
-                                                                           const int64_t tile_elems, const int64_t seg,
-                                                                           const int64_t tstride, const int64_t n,
-                                                                           const uint64_t seed, const uint64_t col0) {
-    // logical element (row, i) of every slot row k < k_max, i < n_tiles * tile_elems
-    const int64_t n_tiles = (n + tile_elems - 1) / tile_elems;
-    const int64_t total = n_tiles * k_max * tile_elems;
-    const int64_t stride = (int64_t)gridDim.x * kBlock;
-    for (int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x; e < total; e += stride) {
-        const int64_t t = e / (k_max * tile_elems);
-        const int64_t rem = e - t * k_max * tile_elems;
-        const int64_t row = rem / tile_elems;
-        const int64_t j = rem - row * tile_elems;
-        const uint64_t col = col0 + (uint64_t)(t * tile_elems + j);
-        const uint64_t base = (seed * 0x9E3779B97F4A7C15ULL) ^ ((uint64_t)row * 0xD1B54A32D192ED03ULL);
-        int32_t s = 0;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) s += (int32_t)(mix32(base + col * 4ULL + (uint64_t)q) >> 8);
-        s -= (int32_t)(1 << 25);
-        slab[t * tstride + row * seg + j] = (float)s * 1.0323827e-07f;
+        const int64_t t = i / tile;
+        dst[t * tstride + (i - t * tile)] = (float)s * 1.0323827e-07f;
     }
 }
 
@@ -381,77 +219,74 @@ __global__ void __launch_bounds__(kBlock) fedavg_gather_f32(const float* src, co
 // ---------------------------------------------------------------------------------------------
 // launchers
 // ---------------------------------------------------------------------------------------------
-template <int OP, int FIN, bool ACC_IN, int UNROLL, bool NT, int VEC>
-static hipError_t launch_f32x4_v(const RowTableF32& tab, int K, const float* acc_in, float* out, int64_t n4,
-                                 float fin_val, int grid, int variant, hipStream_t s) {
-    if (variant & 8) {
-        hipLaunchKernelGGL((fedavg_rows_f32x4<OP, FIN, ACC_IN, UNROLL, NT, VEC, true>), dim3(grid), dim3(kBlock), 0, s,
-                           tab, K, reinterpret_cast<const f32x4*>(acc_in), reinterpret_cast<f32x4*>(out), n4, fin_val);
+template <int OP, int FIN, bool ACC_IN, int UNROLL, int CPL>
+static hipError_t launch_tiles_v(const TileLaunch& L, hipStream_t s) {
+    const f32x4* ai = reinterpret_cast<const f32x4*>(L.acc_in);
+    f32x4* o = reinterpret_cast<f32x4*>(L.out);
+    const bool ntl = !(L.variant & kVariantTemporalLoads);
+    const bool nts = !(L.variant & kVariantTemporalStores);
+#define FEDAVG_LAUNCH_TILES(NTL, NTS)                                                                                \
+    hipLaunchKernelGGL((fedavg_tiles_f32x4<OP, FIN, ACC_IN, UNROLL, CPL, NTL, NTS>), dim3(L.grid), dim3(kBlock), 0, \
+                       s, L.tab, L.k, L.tstride4, ai, o, L.b4, L.e4, L.fin_val)
+    if (ntl && nts) {
+        FEDAVG_LAUNCH_TILES(true, true);
+    } else if (ntl) {
+        FEDAVG_LAUNCH_TILES(true, false);
+    } else if (nts) {
+        FEDAVG_LAUNCH_TILES(false, true);
     } else {
-        hipLaunchKernelGGL((fedavg_rows_f32x4<OP, FIN, ACC_IN, UNROLL, NT, VEC>), dim3(grid), dim3(kBlock), 0, s, tab,
-                           K, reinterpret_cast<const f32x4*>(acc_in), reinterpret_cast<f32x4*>(out), n4, fin_val);
+        FEDAVG_LAUNCH_TILES(false, false);
     }
+#undef FEDAVG_LAUNCH_TILES
     return hipGetLastError();
 }
 
-// variant bit 0: VEC=2 columns per lane; bit 1: plain (temporal) loads instead of nontemporal
-template <int OP, int FIN, bool ACC_IN, int UNROLL>
-static hipError_t launch_f32x4_u(const RowTableF32& tab, int K, const float* acc_in, float* out, int64_t n4,
-                                 float fin_val, int grid, int variant, hipStream_t s) {
-    switch (variant & 3) {
-        case 1:
-            return launch_f32x4_v<OP, FIN, ACC_IN, UNROLL, true, 2>(tab, K, acc_in, out, n4, fin_val, grid, variant, s);
-        case 2:
-            return launch_f32x4_v<OP, FIN, ACC_IN, UNROLL, false, 1>(tab, K, acc_in, out, n4, fin_val, grid, variant, s);
-        case 3:
-            return launch_f32x4_v<OP, FIN, ACC_IN, UNROLL, false, 2>(tab, K, acc_in, out, n4, fin_val, grid, variant, s);
-        default:
-            return launch_f32x4_v<OP, FIN, ACC_IN, UNROLL, true, 1>(tab, K, acc_in, out, n4, fin_val, grid, variant, s);
-    }
-}
-
 template <int OP, int FIN, bool ACC_IN>
-static hipError_t launch_f32x4_a(const RowTableF32& tab, int K, const float* acc_in, float* out, int64_t n4,
-                                 float fin_val, int grid, int unroll, int variant, hipStream_t s) {
-    switch (unroll) {
+static hipError_t launch_tiles_a(const TileLaunch& L, hipStream_t s) {
+    const int64_t cpl = L.tile4 / kBlock;
+    const bool u8 = L.unroll == 8;
+#define FEDAVG_TILES_CPL(C) \
+    return u8 ? launch_tiles_v<OP, FIN, ACC_IN, 8, C>(L, s) : launch_tiles_v<OP, FIN, ACC_IN, 4, C>(L, s);
+    switch (cpl) {
+        case 1:
+            FEDAVG_TILES_CPL(1)
+        case 2:
+            FEDAVG_TILES_CPL(2)
         case 4:
-            return launch_f32x4_u<OP, FIN, ACC_IN, 4>(tab, K, acc_in, out, n4, fin_val, grid, variant, s);
-        case 16:
-            return launch_f32x4_u<OP, FIN, ACC_IN, 16>(tab, K, acc_in, out, n4, fin_val, grid, variant, s);
+            FEDAVG_TILES_CPL(4)
+        case 8:
+            FEDAVG_TILES_CPL(8)
         default:
-            return launch_f32x4_u<OP, FIN, ACC_IN, 8>(tab, K, acc_in, out, n4, fin_val, grid, variant, s);
+            return hipErrorInvalidValue;
     }
+#undef FEDAVG_TILES_CPL
 }
 
 template <int OP, int FIN>
-static hipError_t launch_f32x4_f(const RowTableF32& tab, int K, const float* acc_in, float* out, int64_t n4,
-                                 float fin_val, int grid, int unroll, int variant, hipStream_t s) {
-    if (acc_in) return launch_f32x4_a<OP, FIN, true>(tab, K, acc_in, out, n4, fin_val, grid, unroll, variant, s);
-    return launch_f32x4_a<OP, FIN, false>(tab, K, acc_in, out, n4, fin_val, grid, unroll, variant, s);
+static hipError_t launch_tiles_f(const TileLaunch& L, hipStream_t s) {
+    return L.acc_in ? launch_tiles_a<OP, FIN, true>(L, s) : launch_tiles_a<OP, FIN, false>(L, s);
 }
 
 template <int OP>
-static hipError_t launch_f32x4_o(const RowTableF32& tab, int K, const float* acc_in, float* out, int64_t n4, int fin,
-                                 float fin_val, int grid, int unroll, int variant, hipStream_t s) {
-    switch (fin) {
+static hipError_t launch_tiles_o(const TileLaunch& L, hipStream_t s) {
+    switch (L.fin) {
         case FEDAVG_FIN_SCALE:
-            return launch_f32x4_f<OP, FEDAVG_FIN_SCALE>(tab, K, acc_in, out, n4, fin_val, grid, unroll, variant, s);
+            return launch_tiles_f<OP, FEDAVG_FIN_SCALE>(L, s);
         case FEDAVG_FIN_DIV:
-            return launch_f32x4_f<OP, FEDAVG_FIN_DIV>(tab, K, acc_in, out, n4, fin_val, grid, unroll, variant, s);
+            return launch_tiles_f<OP, FEDAVG_FIN_DIV>(L, s);
         default:
-            return launch_f32x4_f<OP, FEDAVG_FIN_NONE>(tab, K, acc_in, out, n4, fin_val, grid, unroll, variant, s);
+            return launch_tiles_f<OP, FEDAVG_FIN_NONE>(L, s);
     }
 }
 
-hipError_t launch_rows_f32x4(const RowTableF32& tab, int K, const float* acc_in, float* out, int64_t n4, int op,
-                             int fin, float fin_val, int grid, int unroll, int variant, hipStream_t s) {
-    switch (op) {
+hipError_t launch_tiles_f32x4(const TileLaunch& L, hipStream_t s) {
+    switch (L.op) {
         case FEDAVG_OP_TORCH:
-            return launch_f32x4_o<FEDAVG_OP_TORCH>(tab, K, acc_in, out, n4, fin, fin_val, grid, unroll, variant, s);
+            return launch_tiles_o<FEDAVG_OP_TORCH>(L, s);
         case FEDAVG_OP_UNWEIGHTED:
-            return launch_f32x4_o<FEDAVG_OP_UNWEIGHTED>(tab, K, acc_in, out, n4, fin, fin_val, grid, unroll, variant, s);
+            return launch_tiles_o<FEDAVG_OP_UNWEIGHTED>(L, s);
         default:
-            return launch_f32x4_o<FEDAVG_OP_NUMPY>(tab, K, acc_in, out, n4, fin, fin_val, grid, unroll, variant, s);
+            return launch_tiles_o<FEDAVG_OP_NUMPY>(L, s);
     }
 }
 
@@ -525,9 +360,10 @@ hipError_t launch_rows_generic(const RowTableGeneric& tab, int K, const void* ac
     return hipErrorInvalidValue;
 }
 
-hipError_t launch_fill_synthetic_f32(float* dst, int64_t n, uint64_t seed, uint64_t row, uint64_t col0, int grid,
-                                     hipStream_t s) {
-    hipLaunchKernelGGL(fedavg_fill_synthetic_f32, dim3(grid), dim3(kBlock), 0, s, dst, n, seed, row, col0);
+hipError_t launch_fill_synthetic_f32(float* dst, int64_t n, int64_t tile, int64_t tstride, uint64_t seed, uint64_t row,
+                                     uint64_t col0, int grid, hipStream_t s) {
+    hipLaunchKernelGGL(fedavg_fill_synthetic_f32, dim3(grid), dim3(kBlock), 0, s, dst, n, tile, tstride, seed, row,
+                       col0);
     return hipGetLastError();
 }
 
@@ -535,104 +371,6 @@ hipError_t launch_gather_f32(const float* src, const uint64_t* idx, float* dst, 
     const int grid = (int)((m + kBlock - 1) / kBlock);
     if (grid == 0) return hipSuccess;
     hipLaunchKernelGGL(fedavg_gather_f32, dim3(grid), dim3(kBlock), 0, s, src, idx, dst, m);
-    return hipGetLastError();
-}
-
-template <int OP, int FIN, bool ACC_IN, int CPL, int UNROLL>
-static hipError_t launch_tiled_u(const SlotTableF32& tab, int K, const float* slab, int64_t seg4, int64_t tstride4,
-                                 const float* acc_in, float* out, int64_t n4, float fin_val, int grid, int variant,
-                                 hipStream_t s) {
-    const f32x4* sl = reinterpret_cast<const f32x4*>(slab);
-    const f32x4* ai = reinterpret_cast<const f32x4*>(acc_in);
-    f32x4* o = reinterpret_cast<f32x4*>(out);
-    if ((variant & 4) && K >= UNROLL && K % UNROLL == 0) {
-        if (variant & 2) {
-            hipLaunchKernelGGL((fedavg_tiled_pipe_f32x4<OP, FIN, ACC_IN, UNROLL, false, CPL>), dim3(grid), dim3(kBlock),
-                               0, s, tab, K, sl, seg4, tstride4, ai, o, n4, fin_val);
-        } else {
-            hipLaunchKernelGGL((fedavg_tiled_pipe_f32x4<OP, FIN, ACC_IN, UNROLL, true, CPL>), dim3(grid), dim3(kBlock),
-                               0, s, tab, K, sl, seg4, tstride4, ai, o, n4, fin_val);
-        }
-    } else if (variant & 8) {
-        hipLaunchKernelGGL((fedavg_tiled_f32x4<OP, FIN, ACC_IN, UNROLL, true, CPL, true>), dim3(grid), dim3(kBlock), 0,
-                           s, tab, K, sl, seg4, tstride4, ai, o, n4, fin_val);
-    } else if (variant & 2) {
-        hipLaunchKernelGGL((fedavg_tiled_f32x4<OP, FIN, ACC_IN, UNROLL, false, CPL>), dim3(grid), dim3(kBlock), 0, s,
-                           tab, K, sl, seg4, tstride4, ai, o, n4, fin_val);
-    } else {
-        hipLaunchKernelGGL((fedavg_tiled_f32x4<OP, FIN, ACC_IN, UNROLL, true, CPL>), dim3(grid), dim3(kBlock), 0, s,
-                           tab, K, sl, seg4, tstride4, ai, o, n4, fin_val);
-    }
-    return hipGetLastError();
-}
-
-template <int OP, int FIN, bool ACC_IN, int CPL>
-static hipError_t launch_tiled_c(const SlotTableF32& tab, int K, const float* slab, int64_t seg4, int64_t tstride4,
-                                 const float* acc_in, float* out, int64_t n4, float fin_val, int grid, int unroll,
-                                 int variant, hipStream_t s) {
-    if (unroll == 4)
-        return launch_tiled_u<OP, FIN, ACC_IN, CPL, 4>(tab, K, slab, seg4, tstride4, acc_in, out, n4, fin_val, grid,
-                                                       variant, s);
-    return launch_tiled_u<OP, FIN, ACC_IN, CPL, 8>(tab, K, slab, seg4, tstride4, acc_in, out, n4, fin_val, grid,
-                                                   variant, s);
-}
-
-template <int OP, int FIN>
-static hipError_t launch_tiled_f(const SlotTableF32& tab, int K, const float* slab, int64_t seg4, int64_t tstride4,
-                                 int64_t tile4,
-                                 const float* acc_in, float* out, int64_t n4, float fin_val, int grid, int unroll,
-                                 int variant, hipStream_t s) {
-#define FEDAVG_TILED_CPL(C)                                                                                        \
-    return acc_in ? launch_tiled_c<OP, FIN, true, C>(tab, K, slab, seg4, tstride4, acc_in, out, n4, fin_val, grid, unroll,  \
-                                                     variant, s)                                                   \
-                  : launch_tiled_c<OP, FIN, false, C>(tab, K, slab, seg4, tstride4, acc_in, out, n4, fin_val, grid, unroll, \
-                                                      variant, s);
-    switch (tile4 / kBlock) {
-        case 1:
-            FEDAVG_TILED_CPL(1)
-        case 2:
-            FEDAVG_TILED_CPL(2)
-        case 4:
-            FEDAVG_TILED_CPL(4)
-        case 8:
-            FEDAVG_TILED_CPL(8)
-        default:
-            return hipErrorInvalidValue;
-    }
-#undef FEDAVG_TILED_CPL
-}
-
-hipError_t launch_tiled_f32x4(const SlotTableF32& tab, int K, const float* slab, int64_t seg4, int64_t tstride4,
-                              int64_t tile4,
-                              const float* acc_in, float* out, int64_t n4, int op, int fin, float fin_val, int grid,
-                              int unroll, int variant, hipStream_t s) {
-#define FEDAVG_TILED_FIN(OPV)                                                                                   \
-    switch (fin) {                                                                                              \
-        case FEDAVG_FIN_SCALE:                                                                                  \
-            return launch_tiled_f<OPV, FEDAVG_FIN_SCALE>(tab, K, slab, seg4, tstride4, tile4, acc_in, out, n4, fin_val, grid, \
-                                                         unroll, variant, s);                                           \
-        case FEDAVG_FIN_DIV:                                                                                    \
-            return launch_tiled_f<OPV, FEDAVG_FIN_DIV>(tab, K, slab, seg4, tstride4, tile4, acc_in, out, n4, fin_val, grid,   \
-                                                       unroll, variant, s);                                             \
-        default:                                                                                                \
-            return launch_tiled_f<OPV, FEDAVG_FIN_NONE>(tab, K, slab, seg4, tstride4, tile4, acc_in, out, n4, fin_val, grid,  \
-                                                        unroll, variant, s);                                            \
-    }
-    switch (op) {
-        case FEDAVG_OP_TORCH:
-            FEDAVG_TILED_FIN(FEDAVG_OP_TORCH)
-        case FEDAVG_OP_UNWEIGHTED:
-            FEDAVG_TILED_FIN(FEDAVG_OP_UNWEIGHTED)
-        default:
-            FEDAVG_TILED_FIN(FEDAVG_OP_NUMPY)
-    }
-#undef FEDAVG_TILED_FIN
-}
-
-hipError_t launch_fill_synthetic_tiled_f32(float* slab, int64_t k_max, int64_t tile_elems, int64_t seg, int64_t tstride,
-                                           int64_t n, uint64_t seed, uint64_t col0, int grid, hipStream_t s) {
-    hipLaunchKernelGGL(fedavg_fill_synthetic_tiled_f32, dim3(grid), dim3(kBlock), 0, s, slab, k_max, tile_elems, seg,
-                       tstride, n, seed, col0);
     return hipGetLastError();
 }
 

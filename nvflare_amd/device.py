@@ -27,18 +27,18 @@ def fedavg_dtype(dt) -> int:
 
 
 class TiledLayout:
-    """Geometry of a tiled client slab (see fedavg_accumulate_tiled in include/nvflare_amd_fedavg.h).
+    """Geometry of a tiled client slab (fedavg_accumulate_tiled in include/nvflare_amd_fedavg.h).
 
-    Element i of the client in slot s is at  (i // tile) * tile_stride + s * seg_stride + i % tile.
-    seg_pad / tile_pad (elements) stagger the DRAM channels concurrently streamed tiles start on."""
+    A slab holds `slots` clients; element i of the client in slot s is at
+        s * tile + (i // tile) * tile_stride + i % tile,   tile_stride = slots * tile
+    so each tile's client segments are contiguous in HBM."""
 
-    __slots__ = ("tile", "k_max", "seg_stride", "tile_stride")
+    __slots__ = ("tile", "slots", "tile_stride")
 
-    def __init__(self, tile: int, k_max: int, seg_pad: int = 0, tile_pad: int = 0):
+    def __init__(self, tile: int, slots: int):
         self.tile = int(tile)
-        self.k_max = int(k_max)
-        self.seg_stride = self.tile + int(seg_pad)
-        self.tile_stride = self.k_max * self.seg_stride + int(tile_pad)
+        self.slots = int(slots)
+        self.tile_stride = self.slots * self.tile
 
     def n_tiles(self, n: int) -> int:
         return (int(n) + self.tile - 1) // self.tile
@@ -46,8 +46,11 @@ class TiledLayout:
     def slab_elems(self, n: int) -> int:
         return self.n_tiles(n) * self.tile_stride
 
+    def slot_offset_elems(self, slot: int) -> int:
+        return int(slot) * self.tile
+
     def __repr__(self):
-        return f"TiledLayout(tile={self.tile}, k_max={self.k_max}, seg_stride={self.seg_stride}, tile_stride={self.tile_stride})"
+        return f"TiledLayout(tile={self.tile}, slots={self.slots}, tile_stride={self.tile_stride})"
 
 
 class DeviceBuffer:
@@ -193,21 +196,30 @@ class DeviceContext:
             ctypes.c_double(float(count)),
         )
 
-    def accumulate_tiled(self, slab_ptr: int, layout, slots, weights, n: int, out_ptr: int, op: int, fin: int,
-                         count: float = 1.0, acc_in_ptr: Optional[int] = None) -> None:
-        """layout: TiledLayout (tile_elems, seg_stride, tile_stride, k_max)."""
-        k = len(slots)
-        s_arr = (ctypes.c_int * max(k, 1))(*[int(s) for s in slots])
+    def accumulate_tiled(self, bases: Sequence[int], weights: Sequence[float], tile: int, tile_stride: int,
+                         begin: int, end: int, out_ptr: int, op: int, fin: int, count: float = 1.0,
+                         acc_in_ptr: Optional[int] = None) -> None:
+        k = len(bases)
+        b_arr = (ctypes.c_void_p * max(k, 1))(*bases)
         w_arr = (ctypes.c_double * max(k, 1))(*[float(w) for w in weights])
-        N.call("fedavg_accumulate_tiled", self.handle, ctypes.c_void_p(slab_ptr), ctypes.c_size_t(layout.tile),
-               ctypes.c_size_t(layout.seg_stride), ctypes.c_size_t(layout.tile_stride), ctypes.c_int(layout.k_max),
-               s_arr, w_arr, ctypes.c_int(k), ctypes.c_void_p(acc_in_ptr or 0), ctypes.c_void_p(out_ptr),
-               ctypes.c_size_t(n), ctypes.c_int(op), ctypes.c_int(fin), ctypes.c_double(float(count)))
+        N.call("fedavg_accumulate_tiled", self.handle, b_arr, w_arr, ctypes.c_int(k), ctypes.c_size_t(tile),
+               ctypes.c_size_t(tile_stride), ctypes.c_size_t(begin), ctypes.c_size_t(end),
+               ctypes.c_void_p(acc_in_ptr or 0), ctypes.c_void_p(out_ptr), ctypes.c_int(op), ctypes.c_int(fin),
+               ctypes.c_double(float(count)))
 
-    def fill_synthetic_tiled_f32(self, slab_ptr: int, layout, n: int, seed: int, col0: int = 0):
-        N.call("fedavg_fill_synthetic_tiled_f32", self.handle, ctypes.c_void_p(slab_ptr), ctypes.c_int(layout.k_max),
-               ctypes.c_size_t(layout.tile), ctypes.c_size_t(layout.seg_stride), ctypes.c_size_t(layout.tile_stride),
-               ctypes.c_size_t(n), ctypes.c_uint64(seed), ctypes.c_uint64(col0))
+    def h2d_tiled(self, base_ptr: int, tile_bytes: int, tile_stride_bytes: int, logical_offset: int, src_ptr: int,
+                  nbytes: int) -> None:
+        if nbytes:
+            N.call("fedavg_h2d_tiled", self.handle, ctypes.c_void_p(base_ptr), ctypes.c_size_t(tile_bytes),
+                   ctypes.c_size_t(tile_stride_bytes), ctypes.c_size_t(logical_offset), ctypes.c_void_p(src_ptr),
+                   ctypes.c_size_t(nbytes))
+
+    def d2d_tiled(self, base_ptr: int, tile_bytes: int, tile_stride_bytes: int, logical_offset: int, src_ptr: int,
+                  nbytes: int) -> None:
+        if nbytes:
+            N.call("fedavg_d2d_tiled", self.handle, ctypes.c_void_p(base_ptr), ctypes.c_size_t(tile_bytes),
+                   ctypes.c_size_t(tile_stride_bytes), ctypes.c_size_t(logical_offset), ctypes.c_void_p(src_ptr),
+                   ctypes.c_size_t(nbytes))
 
     def set_timing(self, enable: bool) -> None:
         N.call("fedavg_set_timing", self.handle, ctypes.c_int(1 if enable else 0))
@@ -231,9 +243,14 @@ class DeviceContext:
     def set_variant(self, variant: int = 0) -> None:
         N.call("fedavg_set_variant", self.handle, ctypes.c_int(variant))
 
-    def fill_synthetic_f32(self, dst_ptr: int, n: int, seed: int, row: int, col0: int = 0) -> None:
+    def fill_synthetic_f32(self, dst_ptr: int, n: int, seed: int, row: int, col0: int = 0, tile: int = 0,
+                           tile_stride: int = 0) -> None:
         N.call("fedavg_fill_synthetic_f32", self.handle, ctypes.c_void_p(dst_ptr), ctypes.c_size_t(n),
-               ctypes.c_uint64(seed), ctypes.c_uint64(row), ctypes.c_uint64(col0))
+               ctypes.c_size_t(tile), ctypes.c_size_t(tile_stride), ctypes.c_uint64(seed), ctypes.c_uint64(row),
+               ctypes.c_uint64(col0))
+
+    def set_tile(self, tile: int = 0) -> None:
+        N.call("fedavg_set_tile", self.handle, ctypes.c_int(tile))
 
     def gather_f32(self, src_ptr: int, idx: np.ndarray) -> np.ndarray:
         idx = np.ascontiguousarray(idx, dtype=np.uint64)

@@ -3,18 +3,22 @@
 Reference semantics: nvflare/app_common/aggregators/weighted_aggregation_helper.py:153-240.
 Design:
 
-* Every ``add`` STAGES the contributor's arrays into HBM (H2D for host arrays, D2D for device
-  tensors): nothing is computed on the host and the caller's arrays are never aliased
-  (``:181-199``).  fp32 keys of one contribution share one *slot*: a device buffer laid out by a
-  process-wide per-helper key layout (each key at a 256-byte aligned element offset), so the K slots of
-  a round form the stacked ``[K][P]`` client matrix the kernel streams.  Other dtypes (fp64, int32,
-  int64) get a buffer per key per contribution and go through the generic kernel.
-* ``get_result`` launches the arrival-ordered K-way accumulate-and-finalise kernel over every run of
-  keys that share the same contributor list (one launch for the usual all-keys-from-all-clients case),
-  then copies the results back in one D2H.
-* If the resident slots would exceed the budget (``max_resident_bytes``, default 85 % of HBM), the
-  pending slots are FOLDED into a device accumulator (same kernel, ``FIN_NONE``) and recycled; the
-  per-element operation sequence is unchanged, so the bits are too.
+* ``add`` STAGES a contribution's arrays into HBM (H2D for host arrays, D2D for device tensors);
+  nothing is computed on the host and the caller's arrays are never aliased (``:181-199``).
+* fp32 keys live in one flat per-helper layout (each key at a 256-byte aligned element offset).  A
+  contribution's fp32 keys occupy one SLOT of a tiled SLAB: a slab holds S clients, and element i of the
+  client in slot s sits at ``s*T + (i // T) * S*T + i % T`` (T = 4096), so every tile's S client
+  segments are contiguous in HBM and the kernel streams them sequentially.
+* ``result`` launches the arrival-ordered K-way accumulate-and-finalise kernel over every run of keys
+  that share the same contributor list (one launch for the usual all-keys-from-all-clients case) and
+  copies the results back in one D2H.  Other dtypes (fp64, int32, int64) get a buffer per key per
+  contribution and the generic kernel.
+* If the staged slots would exceed the HBM budget (``max_resident_bytes``, default HBM - 8 GiB), the
+  pending contributions are FOLDED into a device accumulator (same kernel, ``FIN_NONE``) and their slots
+  recycled; the per-element operation sequence is unchanged, so the bits are too.
+* Slabs persist across rounds.  In the first round they grow geometrically (16, 32, 64, ... slots); at
+  ``reset`` a round that needed several slabs is consolidated into one slab of the observed client count,
+  so later rounds aggregate in a single launch.
 
 Numerics are the reference's, per container type (finding 2):
 numpy -> ``FEDAVG_OP_NUMPY`` + ``FEDAVG_FIN_SCALE``; torch -> ``FEDAVG_OP_TORCH`` + ``FEDAVG_FIN_DIV``;
@@ -30,16 +34,18 @@ from typing import Any, Dict, List, Optional, Tuple
 import numpy as np
 
 from . import _native as N
-from .device import DeviceBuffer, DeviceContext, fedavg_dtype
+from .device import DeviceBuffer, DeviceContext, TiledLayout, fedavg_dtype
 
 try:
     import torch
 except Exception:  # pragma: no cover
     torch = None
 
-ALIGN_ELEMS = 64  # 256 B for fp32: every key starts on a 256-byte boundary inside a slot
+ALIGN_ELEMS = 64  # 256 B: every fp32 key starts on a 256-byte boundary of the flat layout
+TILE = 4096  # elements per client segment per tile (the kernel's default geometry)
 
 _TORCH_TO_NP = {}
+_NP_TO_TORCH = {}
 if torch is not None:
     _TORCH_TO_NP = {
         torch.float32: np.dtype(np.float32),
@@ -55,64 +61,9 @@ def is_torch_tensor(v) -> bool:
 
 
 def is_device_array(v) -> bool:
-    """Arrays/tensors that take the HIP path; everything else (python numbers, opaque objects such as
-    HE ciphertexts) follows the reference's object protocol on the host."""
+    """Arrays/tensors take the HIP path; everything else (python numbers, opaque objects such as HE
+    ciphertexts) follows the reference's object protocol on the host."""
     return isinstance(v, np.ndarray) or is_torch_tensor(v)
-
-
-class _Staged:
-    """One contribution's device copy of one key (or its place inside a slot)."""
-
-    __slots__ = ("ptr", "weight", "owner")
-
-    def __init__(self, ptr: int, weight: float, owner):
-        self.ptr = ptr
-        self.weight = weight
-        self.owner = owner  # _Slot or DeviceBuffer keeping the memory alive
-
-
-class _Slot:
-    """One contribution's fp32 arena (all its fp32 keys at their layout offsets)."""
-
-    __slots__ = ("buf", "refs")
-
-    def __init__(self, buf: DeviceBuffer):
-        self.buf = buf
-        self.refs = 0
-
-
-class _KeyState:
-    __slots__ = (
-        "name",
-        "shape",
-        "container",
-        "torch_device",
-        "in_np",
-        "acc_np",
-        "op",
-        "fin",
-        "n",
-        "arena",
-        "offset",
-        "pending",
-        "acc_valid",
-        "acc_buf",
-        "count",
-    )
-
-    def __init__(self):
-        self.pending: List[_Staged] = []
-        self.acc_valid = False
-        self.acc_buf: Optional[DeviceBuffer] = None
-        self.count = None
-
-    @property
-    def in_dt(self):
-        return fedavg_dtype(self.in_np)
-
-    @property
-    def acc_dt(self):
-        return fedavg_dtype(self.acc_np)
 
 
 def _resolve_types(v, weight, weighted: bool) -> Tuple[str, np.dtype, np.dtype, int, int]:
@@ -157,29 +108,90 @@ def _resolve_types(v, weight, weighted: bool) -> Tuple[str, np.dtype, np.dtype, 
 
 
 def _default_budget(ctx: DeviceContext) -> int:
+    """HBM the engine may hold: everything but an 8 GiB reserve (torch, the runtime, other helpers)."""
     env = os.environ.get("NVFLARE_AMD_MAX_RESIDENT_BYTES")
     if env:
         return int(float(env))
-    return int(ctx.total_bytes * 0.85)
+    return max(int(ctx.total_bytes) - (8 << 30), int(ctx.total_bytes) // 2)
+
+
+class _Slab:
+    """S client slots in one tiled allocation covering `capacity` elements of the flat layout."""
+
+    __slots__ = ("buf", "layout", "capacity", "free")
+
+    def __init__(self, buf: DeviceBuffer, layout: TiledLayout, capacity: int):
+        self.buf = buf
+        self.layout = layout
+        self.capacity = capacity
+        self.free = list(range(layout.slots - 1, -1, -1))  # pop() hands out slot 0 first
+
+
+class _Slot:
+    __slots__ = ("slab", "index", "refs")
+
+    def __init__(self, slab: _Slab, index: int):
+        self.slab = slab
+        self.index = index
+        self.refs = 0
+
+    @property
+    def base(self) -> int:
+        return self.slab.buf.ptr + self.slab.layout.slot_offset_elems(self.index) * 4
+
+
+class _Staged:
+    """One contribution's device copy of one key: a slot of a slab (fp32) or its own buffer."""
+
+    __slots__ = ("weight", "slot", "buf")
+
+    def __init__(self, weight, slot: Optional[_Slot] = None, buf: Optional[DeviceBuffer] = None):
+        self.weight = weight
+        self.slot = slot
+        self.buf = buf
+
+
+class _KeyState:
+    __slots__ = ("name", "shape", "container", "torch_device", "in_np", "acc_np", "op", "fin", "n", "arena",
+                 "offset", "pending", "acc_valid", "acc_buf", "count")
+
+    def __init__(self):
+        self.pending: List[_Staged] = []
+        self.acc_valid = False
+        self.acc_buf: Optional[DeviceBuffer] = None
+        self.count = None
+
+    @property
+    def in_dt(self):
+        return fedavg_dtype(self.in_np)
+
+    @property
+    def acc_dt(self):
+        return fedavg_dtype(self.acc_np)
 
 
 class DeviceFedAvg:
     """Arrival-ordered weighted accumulation of client arrays on one HIP device."""
 
-    def __init__(self, device: Optional[int] = None, max_resident_bytes: Optional[int] = None):
+    def __init__(self, device: Optional[int] = None, max_resident_bytes: Optional[int] = None,
+                 slab_slots: Optional[int] = None):
         if device is None:
             device = int(os.environ.get("NVFLARE_AMD_DEVICE", "0"))
         self.device = int(device)
         self._ctx: Optional[DeviceContext] = None  # opened on first use (config checks need no GPU)
         self._max_resident_bytes = max_resident_bytes
+        env_slots = os.environ.get("NVFLARE_AMD_SLAB_SLOTS")
+        self.slab_slots = int(slab_slots or (int(env_slots) if env_slots else 0))  # 0 = adaptive
         self.lock = threading.RLock()
-        self.layout_elems = 0  # fp32 arena layout size (elements)
+        self.layout_elems = 0  # flat fp32 layout size (elements)
         self.keys: Dict[str, _KeyState] = {}
         self.arena_acc: Optional[DeviceBuffer] = None
-        self._free_slots: List[DeviceBuffer] = []
+        self.slabs: List[_Slab] = []
         self._live_slots: List[_Slot] = []
         self._side_bufs: List[DeviceBuffer] = []
-        self.stats = {"h2d_bytes": 0, "folds": 0, "launches": 0}
+        self._round_clients = 0
+        self.peak_clients = 0
+        self.stats = {"h2d_bytes": 0, "folds": 0, "launches": 0, "slabs_allocated": 0}
 
     @property
     def ctx(self) -> DeviceContext:
@@ -193,40 +205,73 @@ class DeviceFedAvg:
             self._max_resident_bytes = _default_budget(self.ctx)
         return self._max_resident_bytes
 
-    # ------------------------------------------------------------------ memory accounting
+    # ------------------------------------------------------------------ memory
     def _resident_bytes(self) -> int:
-        live = sum(s.buf.nbytes for s in self._live_slots)
+        slabs = sum(s.buf.nbytes for s in self.slabs)
         side = sum(b.nbytes for b in self._side_bufs)
         acc = self.arena_acc.nbytes if self.arena_acc is not None else 0
-        return live + side + acc + sum(b.nbytes for b in self._free_slots)
+        return slabs + side + acc
 
-    def _acquire_slot(self, nbytes: int) -> _Slot:
-        best = None
-        for i, b in enumerate(self._free_slots):
-            if b.nbytes >= nbytes and (best is None or b.nbytes < self._free_slots[best].nbytes):
-                best = i
-        if best is not None:
-            return _Slot(self._free_slots.pop(best))
-        if self._resident_bytes() + nbytes > self.max_resident_bytes:
-            self._fold()
-            while self._free_slots and self._resident_bytes() + nbytes > self.max_resident_bytes:
-                self._free_slots.pop().close()
-            for i, b in enumerate(self._free_slots):
-                if b.nbytes >= nbytes:
-                    return _Slot(self._free_slots.pop(i))
-        try:
-            return _Slot(self.ctx.alloc(nbytes))
-        except N.FedAvgError:
-            self._fold()
-            for b in self._free_slots:
-                b.close()
-            self._free_slots.clear()
-            return _Slot(self.ctx.alloc(nbytes))
+    def _next_slab_slots(self) -> int:
+        if self.slab_slots:
+            return self.slab_slots
+        if not self.slabs:
+            return 16 if self.peak_clients == 0 else max(8, (self.peak_clients + 7) // 8 * 8)
+        return min(128, 2 * self.slabs[-1].layout.slots)
+
+    def _new_slab(self, capacity: int, min_slots: int = 0) -> Optional[_Slab]:
+        """Allocate a slab for clients of flat extent <= capacity, sized to the remaining budget (but at
+        least `min_slots` slots)."""
+        n_tiles = (capacity + TILE - 1) // TILE
+        per_slot = n_tiles * TILE * 4
+        room = self.max_resident_bytes - self._resident_bytes() - 4 * (self.layout_elems + ALIGN_ELEMS)
+        slots = max(min_slots, min(self._next_slab_slots(), room // per_slot if per_slot else 0))
+        while slots >= max(1, min_slots):
+            layout = TiledLayout(TILE, int(slots))
+            try:
+                buf = self.ctx.alloc(layout.slab_elems(capacity) * 4)
+            except N.FedAvgError:
+                if slots == 1:
+                    return None
+                slots = max(1, slots // 2)
+                continue
+            slab = _Slab(buf, layout, n_tiles * TILE)
+            self.slabs.append(slab)
+            self.stats["slabs_allocated"] += 1
+            return slab
+        return None
+
+    def _find_free(self, extent: int) -> Optional[_Slot]:
+        for slab in self.slabs:
+            if slab.capacity >= extent and slab.free:
+                slot = _Slot(slab, slab.free.pop())
+                self._live_slots.append(slot)
+                return slot
+        return None
+
+    def _acquire_slot(self, extent: int) -> _Slot:
+        slot = self._find_free(extent)
+        if slot is None and self._new_slab(max(extent, self.layout_elems)) is not None:
+            slot = self._find_free(extent)
+        if slot is None and self._live_slots:
+            self._fold()  # over budget: fold what is staged (frees every slot, keeps the slabs)
+            slot = self._find_free(extent)
+        if slot is None:
+            # the remaining slabs cannot hold this client: drop them and make room for at least one slot
+            for s in self.slabs:
+                s.buf.close()
+            self.slabs.clear()
+            if self._new_slab(max(extent, self.layout_elems), min_slots=1) is not None:
+                slot = self._find_free(extent)
+        if slot is None:
+            raise N.FedAvgError(f"nvflare_amd: cannot stage a client of {extent} fp32 elements on device "
+                                f"{self.device} (HBM budget {self.max_resident_bytes} bytes)")
+        return slot
 
     def _release_slot(self, slot: _Slot) -> None:
         if slot in self._live_slots:
             self._live_slots.remove(slot)
-            self._free_slots.append(slot.buf)
+            slot.slab.free.append(slot.index)
 
     # ------------------------------------------------------------------ layout
     def _register_key(self, name: str, v, weight, weighted: bool) -> _KeyState:
@@ -262,10 +307,10 @@ class DeviceFedAvg:
         return st
 
     def _ensure_arena_acc(self) -> None:
-        need = self.layout_elems * 4
+        need = max(self.layout_elems, ALIGN_ELEMS) * 4
         if self.arena_acc is not None and self.arena_acc.nbytes >= need:
             return
-        new = self.ctx.alloc(max(need, 4))
+        new = self.ctx.alloc(need)
         if self.arena_acc is not None:
             self.ctx.d2d(new.ptr, self.arena_acc.ptr, self.arena_acc.nbytes)
             self.ctx.sync()
@@ -273,104 +318,116 @@ class DeviceFedAvg:
         self.arena_acc = new
 
     # ------------------------------------------------------------------ staging
-    def _stage(self, dst_ptr: int, v) -> None:
+    @staticmethod
+    def _source(v):
+        """(pointer, nbytes, on_device) of a contiguous view of v."""
         if is_torch_tensor(v):
             t = v.detach()
             if not t.is_contiguous():
                 t = t.contiguous()
-            nbytes = t.numel() * t.element_size()
-            if t.device.type == "cpu":
-                self.ctx.h2d_ptr(dst_ptr, t.data_ptr(), nbytes)
-            else:
-                if t.device.index != self.ctx.device:
-                    raise ValueError(f"nvflare_amd: tensor on {t.device}, engine on device {self.ctx.device}")
-                # order the copy after the producer's work on torch's current stream
-                torch.cuda.current_stream(t.device).synchronize()
-                self.ctx.d2d(dst_ptr, t.data_ptr(), nbytes)
-        else:
-            a = np.ascontiguousarray(v)
-            self.ctx.h2d_ptr(dst_ptr, a.ctypes.data, a.nbytes)
-        self.stats["h2d_bytes"] += int(v.nbytes) if isinstance(v, np.ndarray) else int(v.numel() * v.element_size())
+            if t.device.type != "cpu":
+                torch.cuda.current_stream(t.device).synchronize()  # producer's work done before we read
+            return t, t.data_ptr(), t.numel() * t.element_size(), t.device.type != "cpu"
+        a = np.ascontiguousarray(v)
+        return a, a.ctypes.data, a.nbytes, False
+
+    def _check_device(self, v) -> None:
+        if is_torch_tensor(v) and v.device.type != "cpu" and v.device.index != self.ctx.device:
+            raise ValueError(f"nvflare_amd: tensor on {v.device}, engine on device {self.ctx.device}")
 
     def add(self, items: List[Tuple[str, Any]], weight, weighted: bool) -> None:
         """Stage one contribution's device-path arrays (already filtered by exclude_vars)."""
         with self.lock, self.ctx.lock:
             states = [(self._register_key(k, v, weight, weighted), v) for k, v in items]
+            for _, v in states:
+                self._check_device(v)
+            self._round_clients += 1
             arena_items = [(st, v) for st, v in states if st.arena and st.n > 0]
             if arena_items:
-                end = max(st.offset + st.n for st, _ in arena_items)
-                slot = self._acquire_slot(end * 4)
-                self._live_slots.append(slot)
+                extent = max(st.offset + st.n for st, _ in arena_items)
+                slot = self._acquire_slot(extent)
+                lay = slot.slab.layout
                 for st, v in arena_items:
-                    ptr = slot.buf.ptr + st.offset * 4
-                    self._stage(ptr, v)
-                    st.pending.append(_Staged(ptr, weight, slot))
+                    keep, ptr, nbytes, on_dev = self._source(v)
+                    copy = self.ctx.d2d_tiled if on_dev else self.ctx.h2d_tiled
+                    copy(slot.base, lay.tile * 4, lay.tile_stride * 4, st.offset * 4, ptr, nbytes)
+                    del keep
+                    st.pending.append(_Staged(weight, slot=slot))
                     slot.refs += 1
+                    self.stats["h2d_bytes"] += nbytes
             for st, v in states:
                 if st.arena or st.n == 0:
                     if st.n == 0:
-                        st.pending.append(_Staged(0, weight, None))
+                        st.pending.append(_Staged(weight))
                     continue
                 buf = self.ctx.alloc(st.n * st.in_np.itemsize)
                 self._side_bufs.append(buf)
-                self._stage(buf.ptr, v)
-                st.pending.append(_Staged(buf.ptr, weight, buf))
+                keep, ptr, nbytes, on_dev = self._source(v)
+                if on_dev:
+                    self.ctx.d2d(buf.ptr, ptr, nbytes)
+                else:
+                    self.ctx.h2d_ptr(buf.ptr, ptr, nbytes)
+                del keep
+                st.pending.append(_Staged(weight, buf=buf))
+                self.stats["h2d_bytes"] += nbytes
             for st, _ in states:
                 st.count = weight if st.count is None else st.count + weight
 
     # ------------------------------------------------------------------ compute
     def _runs(self):
-        """Group arena keys (offset order) into maximal runs with identical launch parameters."""
+        """Arena keys in offset order, grouped into maximal runs with identical launch parameters."""
         arena = sorted((st for st in self.keys.values() if st.arena and st.n > 0), key=lambda s: s.offset)
         runs = []
         for st in arena:
-            sig = (
-                tuple(p.owner.buf.ptr for p in st.pending),
-                tuple(p.weight for p in st.pending),
-                st.acc_valid,
-                st.op,
-                st.fin,
-                st.count,
-            )
+            sig = (tuple(id(p.slot) for p in st.pending), tuple(p.weight for p in st.pending), st.acc_valid, st.op,
+                   st.fin, st.count)
             if runs and runs[-1][0] == sig:
                 runs[-1][1].append(st)
             else:
                 runs.append((sig, [st]))
-        return runs
+        return [g for _, g in runs]
+
+    def _launch_run(self, group: List[_KeyState], final: bool) -> None:
+        first, last = group[0], group[-1]
+        begin = first.offset
+        end = (last.offset + last.n + 3) // 4 * 4  # inside the key's 256-byte aligned extent
+        pend = first.pending
+        if not pend and not (final and first.acc_valid):
+            return
+        out = self.arena_acc.ptr
+        acc_in = out if first.acc_valid else None
+        fin = first.fin if final else N.FEDAVG_FIN_NONE
+        if not pend:  # finalise an already folded sum
+            self.ctx.accumulate_tiled([], [], TILE, TILE, begin, end, out, first.op, fin, float(first.count), acc_in)
+            self.stats["launches"] += 1
+            return
+        # consecutive contributions staged in slabs of the same geometry go in one launch; a change of
+        # geometry chains the next launch through the accumulator (arrival order is preserved)
+        segs: List[List[_Staged]] = []
+        for p in pend:
+            if segs and segs[-1][-1].slot.slab.layout.tile_stride == p.slot.slab.layout.tile_stride:
+                segs[-1].append(p)
+            else:
+                segs.append([p])
+        for i, seg in enumerate(segs):
+            lay = seg[0].slot.slab.layout
+            self.ctx.accumulate_tiled([p.slot.base for p in seg], [p.weight for p in seg], lay.tile, lay.tile_stride,
+                                      begin, end, out, first.op, fin if i == len(segs) - 1 else N.FEDAVG_FIN_NONE,
+                                      float(first.count), acc_in)
+            acc_in = out
+            self.stats["launches"] += 1
 
     def _launch_arena(self, final: bool) -> None:
         if not any(st.arena and st.n > 0 for st in self.keys.values()):
             return
         self._ensure_arena_acc()
-        for _, group in self._runs():
-            first, last = group[0], group[-1]
-            n = last.offset + last.n - first.offset
-            rows = [p.owner.buf.ptr + first.offset * 4 for p in first.pending]
-            weights = [p.weight for p in first.pending]
-            if not rows and not (final and first.acc_valid):
-                continue
-            if not rows and not first.acc_valid:
-                continue
-            out = self.arena_acc.ptr + first.offset * 4
-            self.ctx.accumulate(
-                rows,
-                weights,
-                n,
-                out,
-                N.FEDAVG_F32,
-                N.FEDAVG_F32,
-                first.op,
-                first.fin if final else N.FEDAVG_FIN_NONE,
-                float(first.count),
-                acc_in_ptr=out if first.acc_valid else None,
-            )
-            self.stats["launches"] += 1
+        for group in self._runs():
+            self._launch_run(group, final)
             for st in group:
                 for p in st.pending:
-                    if isinstance(p.owner, _Slot):
-                        p.owner.refs -= 1
-                        if p.owner.refs == 0:
-                            self._release_slot(p.owner)
+                    p.slot.refs -= 1
+                    if p.slot.refs == 0:
+                        self._release_slot(p.slot)
                 st.pending = []
                 st.acc_valid = True
 
@@ -382,9 +439,8 @@ class DeviceFedAvg:
                 continue
             if st.acc_buf is None:
                 st.acc_buf = self.ctx.alloc(st.n * st.acc_np.itemsize)
-            rows = [p.ptr for p in st.pending]
             self.ctx.accumulate(
-                rows,
+                [p.buf.ptr for p in st.pending],
                 [p.weight for p in st.pending],
                 st.n,
                 st.acc_buf.ptr,
@@ -412,19 +468,15 @@ class DeviceFedAvg:
     def result(self) -> Dict[str, Any]:
         """Finalise every key on the device and return host (or device-tensor) results."""
         with self.lock, self.ctx.lock:
-            # device tensors from torch: make sure their producers finished before we read
             self._launch_arena(final=True)
             self._launch_side(final=True)
-            out: Dict[str, Any] = {}
             host_arena = None
             if self.layout_elems and any(st.arena and st.n > 0 and st.torch_device is None for st in self.keys.values()):
                 host_arena = np.empty(self.layout_elems, dtype=np.float32)
                 self.ctx.d2h(host_arena, self.arena_acc.ptr)
             else:
                 self.ctx.sync()
-            for name, st in self.keys.items():
-                out[name] = self._materialize(st, host_arena)
-            return out
+            return {name: self._materialize(st, host_arena) for name, st in self.keys.items()}
 
     def _materialize(self, st: _KeyState, host_arena):
         if st.n == 0:
@@ -432,19 +484,15 @@ class DeviceFedAvg:
                 return torch.empty(st.shape, dtype=_NP_TO_TORCH[st.acc_np],
                                    device=st.torch_device if st.torch_device is not None else "cpu")
             arr = np.empty(st.shape, dtype=st.acc_np)
+        elif st.torch_device is not None:
+            t = torch.empty(st.shape, dtype=_NP_TO_TORCH[st.acc_np], device=st.torch_device)
+            src = self.arena_acc.ptr + st.offset * 4 if st.arena else st.acc_buf.ptr
+            self.ctx.d2d(t.data_ptr(), src, st.n * st.acc_np.itemsize)
+            self.ctx.sync()
+            return t
         elif st.arena:
-            if st.torch_device is not None:
-                t = torch.empty(st.shape, dtype=_NP_TO_TORCH[st.acc_np], device=st.torch_device)
-                self.ctx.d2d(t.data_ptr(), self.arena_acc.ptr + st.offset * 4, st.n * 4)
-                self.ctx.sync()
-                return t
-            arr = host_arena[st.offset : st.offset + st.n].reshape(st.shape)
+            arr = host_arena[st.offset: st.offset + st.n].reshape(st.shape)
         else:
-            if st.torch_device is not None:
-                t = torch.empty(st.shape, dtype=_NP_TO_TORCH[st.acc_np], device=st.torch_device)
-                self.ctx.d2d(t.data_ptr(), st.acc_buf.ptr, st.n * st.acc_np.itemsize)
-                self.ctx.sync()
-                return t
             arr = np.empty(st.shape, dtype=st.acc_np)
             self.ctx.d2h(arr.reshape(-1) if arr.ndim else arr.reshape(1), st.acc_buf.ptr)
         if st.container == "torch":
@@ -455,7 +503,9 @@ class DeviceFedAvg:
 
     # ------------------------------------------------------------------ lifetime
     def reset(self) -> None:
-        """Drop the round's state; slot buffers are kept for reuse by the next round."""
+        """Drop the round's state; slabs are kept (and consolidated) for the next round."""
+        self.peak_clients = max(self.peak_clients, self._round_clients)
+        self._round_clients = 0
         if self._ctx is None:
             self.keys.clear()
             self.layout_elems = 0
@@ -469,6 +519,11 @@ class DeviceFedAvg:
             for st in self.keys.values():
                 if st.acc_buf is not None:
                     st.acc_buf.close()
+            if len(self.slabs) > 1 and not self.slab_slots:
+                # a round needed several slabs: next round gets one slab of the observed client count
+                for s in self.slabs:
+                    s.buf.close()
+                self.slabs.clear()
             self.keys.clear()
             self.layout_elems = 0
 
@@ -476,9 +531,9 @@ class DeviceFedAvg:
         """Free every device buffer held by this engine."""
         with self.lock:
             self.reset()
-            for b in self._free_slots:
-                b.close()
-            self._free_slots.clear()
+            for s in self.slabs:
+                s.buf.close()
+            self.slabs.clear()
             if self.arena_acc is not None:
                 self.arena_acc.close()
                 self.arena_acc = None

@@ -229,21 +229,23 @@ def test_kernel_generic_dtypes(ctx, oracle, in_dt, acc_dt):
 
 
 @pytest.mark.parametrize("variant", [0, 1, 2, 3])
-@pytest.mark.parametrize("bpc,unroll", [(1, 4), (2, 8), (4, 16), (8, 8), (16, 4)])
-def test_launch_variants_same_bits(ctx, oracle, bpc, unroll, variant):
+@pytest.mark.parametrize("bpc,unroll,tile", [(1, 4, 1024), (2, 8, 2048), (4, 4, 4096), (8, 8, 8192), (2, 4, 4096)])
+def test_launch_variants_same_bits(ctx, oracle, bpc, unroll, tile, variant):
     rng = np.random.default_rng(21)
-    n = 300_001 + variant  # ragged tiles for the 2-column variants too
+    n = 300_001 + variant  # whole tiles on the streaming kernel + a ragged tail on the scalar kernel
     rows = [rng.standard_normal(n).astype(np.float32) for _ in range(33)]
     ws = [float(1 + (37 * k) % 100) for k in range(33)]
     for op, fin, mode in ((1, 2, oracle.MODE_TORCH), (0, 1, oracle.MODE_NUMPY)):
         exp = oracle.fedavg_c(rows, ws, mode, fin=fin, nthreads=4)
         ctx.set_launch(bpc, unroll)
         ctx.set_variant(variant)
+        ctx.set_tile(tile)
         try:
             got = _run_kernel(ctx, rows, ws, op, fin, _sum(ws))
         finally:
             ctx.set_launch(0, 0)
             ctx.set_variant(0)
+            ctx.set_tile(0)
         assert same_bits(got, exp)
 
 
@@ -261,7 +263,7 @@ def test_large_k64(ctx, oracle):
 def test_synthetic_generator_matches_host(ctx, oracle):
     n = 1_000_003
     b = ctx.alloc(n * 4)
-    ctx.fill_synthetic_f32(b.ptr, n, seed=9, row=5, col0=123)
+    ctx.fill_synthetic_f32(b.ptr, n, 9, 5, 123)
     dev = np.empty(n, dtype=np.float32)
     ctx.d2h(dev, b.ptr)
     host = oracle.synth_values(9, 5, np.arange(123, 123 + n, dtype=np.uint64))
@@ -275,7 +277,7 @@ def test_timing_events(ctx):
     n = 1 << 20
     bufs = [ctx.alloc(n * 4) for _ in range(4)]
     for i, b in enumerate(bufs):
-        ctx.fill_synthetic_f32(b.ptr, n, 1, i)
+        ctx.fill_synthetic_f32(b.ptr, n, 1, i, 0)
     ctx.set_timing(True)
     try:
         ctx.accumulate([b.ptr for b in bufs[:3]], [1.0, 2.0, 3.0], n, bufs[3].ptr, 0, 0, 1, 2, 6.0)
@@ -288,34 +290,108 @@ def test_timing_events(ctx):
 
 
 @pytest.mark.parametrize("tile", [1024, 2048, 4096, 8192])
-@pytest.mark.parametrize("variant", [0, 2, 4, 6])
-@pytest.mark.parametrize("K,unroll", [(13, 8), (16, 4), (16, 8), (24, 8)])
-@pytest.mark.parametrize("seg_pad,tile_pad", [(0, 0), (64, 1040)])
-def test_tiled_slab_vs_oracle(ctx, oracle, tile, variant, K, unroll, seg_pad, tile_pad):
-    """Tiled slab layout (client segments interleaved per tile) with a permuted arrival order; variants 4/6
-    take the software-pipelined kernel when K % unroll == 0 (and include grid-stride tile reuse)."""
+@pytest.mark.parametrize("K,slots", [(13, 16), (16, 16), (24, 24), (130, 130)])
+@pytest.mark.parametrize("begin,end", [(0, None), (64, None), (4096 + 128, 3 * 4096 - 64), (8, 12)])
+def test_tiled_slab_vs_oracle(ctx, oracle, tile, K, slots, begin, end):
+    """Tiled slab (clients interleaved per tile), permuted arrival order, sub-ranges that start and end
+    mid-tile (only [begin, end) of the flat output is written), >128 clients chained through the output."""
     from nvflare_amd.device import TiledLayout
 
     n = 7 * 4096 + 1024 + 12  # ragged last tile
-    lay = TiledLayout(tile, 24, seg_pad, tile_pad)
-    k_max = lay.k_max
+    end = n if end is None else end
+    lay = TiledLayout(tile, slots)
     slab = ctx.alloc(lay.slab_elems(n) * 4)
-    ctx.fill_synthetic_tiled_f32(slab.ptr, lay, n, 77, 5)
-    order = [int(x) for x in np.random.default_rng(tile).permutation(k_max)[:K]]
+    for s_ in range(slots):
+        ctx.fill_synthetic_f32(slab.ptr + lay.slot_offset_elems(s_) * 4, n, 77, s_, 5, tile, lay.tile_stride)
+    order = [int(x) for x in np.random.default_rng(tile + K).permutation(slots)[:K]]
     ws = [0.25 + 1.5 * j for j in range(K)]
-    rows = [oracle.synth_values(77, s, np.arange(5, 5 + n, dtype=np.uint64)) for s in order]
-    out = ctx.alloc(n * 4)
-    ctx.set_variant(variant)
-    ctx.set_launch(1 if variant & 4 else 0, unroll)  # few blocks: several tiles per block
+    rows = [oracle.synth_values(77, s_, np.arange(5, 5 + n, dtype=np.uint64)) for s_ in order]
+    bases = [slab.ptr + lay.slot_offset_elems(s_) * 4 for s_ in order]
+    out = ctx.alloc(n * 4 + 64)
+    sentinel = np.full(n, 12345.0, np.float32)
     try:
         for op, fin, mode in ((1, 2, oracle.MODE_TORCH), (0, 1, oracle.MODE_NUMPY), (2, 1, oracle.MODE_NUMPY)):
-            ctx.accumulate_tiled(slab.ptr, lay, order, ws, n, out.ptr, op, fin, _sum(ws))
+            ctx.h2d_ptr(out.ptr, sentinel.ctypes.data, sentinel.nbytes)
+            e4 = (end + 3) // 4 * 4
+            ctx.accumulate_tiled(bases, ws, tile, lay.tile_stride, begin, e4, out.ptr, op, fin, _sum(ws))
             got = np.empty(n, np.float32)
             ctx.d2h(got, out.ptr)
-            exp = oracle.fedavg_c(rows, ws, mode, weighted=(op != 2), fin=fin)
-            assert same_bits(got, exp), (op, fin)
+            exp = oracle.fedavg_c(rows, ws, mode, weighted=(op != 2), fin=fin, nthreads=4)
+            assert same_bits(got[begin:e4], exp[begin:e4]), (op, fin)
+            assert np.all(got[:begin] == 12345.0) and np.all(got[e4:] == 12345.0)
     finally:
-        ctx.set_variant(0)
-        ctx.set_launch(0, 0)
         slab.close()
         out.close()
+
+
+@pytest.mark.parametrize("tile", [1024, 4096])
+def test_h2d_tiled_staging(ctx, oracle, tile):
+    """Host arrays staged into tiled slots at arbitrary (4-aligned) logical offsets, pageable and pinned."""
+    from nvflare_amd.device import TiledLayout
+
+    K, slots, n = 5, 8, 3 * tile + 100
+    lay = TiledLayout(tile, slots)
+    slab = ctx.alloc(lay.slab_elems(n) * 4)
+    rng = np.random.default_rng(tile)
+    rows = [rng.standard_normal(n).astype(np.float32) for _ in range(K)]
+    cuts = [0, 4, tile - 4, tile + 36, 2 * tile, n]
+    for k, r in enumerate(rows):
+        base = slab.ptr + lay.slot_offset_elems(k) * 4
+        for a, b in zip(cuts[:-1], cuts[1:]):  # staged piecewise, like several keys of one client
+            piece = np.ascontiguousarray(r[a:b])
+            if k % 2:
+                piece = torch.from_numpy(piece).pin_memory().numpy()
+            ctx.h2d_tiled(base, tile * 4, lay.tile_stride * 4, a * 4, piece.ctypes.data, piece.nbytes)
+    ws = [1.0, 2.5, 0.125, 7.0, 3.0]
+    out = ctx.alloc(n * 4 + 64)
+    e4 = (n + 3) // 4 * 4
+    ctx.accumulate_tiled([slab.ptr + lay.slot_offset_elems(k) * 4 for k in range(K)], ws, tile, lay.tile_stride, 0, e4,
+                         out.ptr, 1, 2, _sum(ws))
+    got = np.empty(n, np.float32)
+    ctx.d2h(got, out.ptr)
+    assert same_bits(got, oracle.fedavg_c(rows, ws, oracle.MODE_TORCH))
+    slab.close()
+    out.close()
+
+
+def test_d2d_tiled_staging_from_torch(ctx, oracle):
+    from nvflare_amd.device import TiledLayout
+
+    tile, K, n = 2048, 3, 2 * 2048 + 8
+    lay = TiledLayout(tile, K)
+    slab = ctx.alloc(lay.slab_elems(n) * 4)
+    rows = [torch.randn(n, generator=torch.Generator().manual_seed(k)) for k in range(K)]
+    for k, r in enumerate(rows):
+        t = r.to("cuda:0")
+        torch.cuda.synchronize()
+        ctx.d2d_tiled(slab.ptr + lay.slot_offset_elems(k) * 4, tile * 4, lay.tile_stride * 4, 0, t.data_ptr(), t.numel() * 4)
+    ws = [0.5, 1.5, 2.0]
+    out = ctx.alloc(n * 4)
+    ctx.accumulate_tiled([slab.ptr + lay.slot_offset_elems(k) * 4 for k in range(K)], ws, tile, lay.tile_stride, 0, n,
+                         out.ptr, 0, 1, _sum(ws))
+    got = np.empty(n, np.float32)
+    ctx.d2h(got, out.ptr)
+    assert same_bits(got, oracle.fedavg_c([r.numpy() for r in rows], ws, oracle.MODE_NUMPY))
+    slab.close()
+    out.close()
+
+
+@pytest.mark.parametrize("slots", [1, 2, 3])
+def test_engine_multi_slab_chaining(oracle, slots):
+    """Few slots per slab: a round spans several slabs (launches chained through the accumulator) and the
+    next round is consolidated into one slab -- bits unchanged either way."""
+    from nvflare_amd.engine import DeviceFedAvg
+
+    rng = np.random.default_rng(slots)
+    K = 7
+    eng = DeviceFedAvg(slab_slots=slots)
+    for rnd in range(2):
+        rows = [rng.standard_normal(10_000 + 3).astype(np.float32) for _ in range(K)]
+        ws = [float(1 + k) for k in range(K)]
+        for k in range(K):
+            eng.add([("w", rows[k])], ws[k], True)
+        got = eng.result()["w"]
+        eng.reset()
+        assert same_bits(got, oracle.fedavg_c(rows, ws, oracle.MODE_NUMPY))
+    assert eng.stats["slabs_allocated"] >= 1
+    eng.release()

@@ -41,30 +41,23 @@ def main():
     for k, b in enumerate(rows):
         ctx.fill_synthetic_f32(b.ptr, P, 1000, k, 0)
     lay = TiledLayout(4096, K)
-    lay2 = TiledLayout(2048, K)
     slab = ctx.alloc(lay.slab_elems(P) * 4)
+    for k in range(K):
+        ctx.fill_synthetic_f32(slab.ptr + lay.slot_offset_elems(k) * 4, P, 1000, k, 0, lay.tile, lay.tile_stride)
     out = ctx.alloc(P * 4)
     ws = [float(1 + (37 * k) % 100) for k in range(K)]
     cnt = sum(ws)
     alg = 4.0 * K * P + 4.0 * P
-    ptrs = [b.ptr for b in rows]
+    row_ptrs = [b.ptr for b in rows]
+    slab_bases = [slab.ptr + lay.slot_offset_elems(k) * 4 for k in range(K)]
 
-    def rows_run(bpc, unroll, variant):
+    def run(bases, tstride, bpc, unroll, variant):
         ctx.set_launch(bpc, unroll)
         ctx.set_variant(variant)
-        ctx.accumulate(ptrs, ws, P, out.ptr, 0, 0, 1, 2, cnt)
+        ctx.accumulate_tiled(bases, ws, 4096, tstride, 0, P, out.ptr, 1, 2, cnt)
         ctx.timing_begin()
         for _ in range(3):
-            ctx.accumulate(ptrs, ws, P, out.ptr, 0, 0, 1, 2, cnt)
-        return ctx.timing_end() / 3
-
-    def tiled_run(layout, bpc, unroll, variant):
-        ctx.set_launch(bpc, unroll)
-        ctx.set_variant(variant)
-        ctx.accumulate_tiled(slab.ptr, layout, list(range(K)), ws, P, out.ptr, 1, 2, cnt)
-        ctx.timing_begin()
-        for _ in range(3):
-            ctx.accumulate_tiled(slab.ptr, layout, list(range(K)), ws, P, out.ptr, 1, 2, cnt)
+            ctx.accumulate_tiled(bases, ws, 4096, tstride, 0, P, out.ptr, 1, 2, cnt)
         return ctx.timing_end() / 3
 
     def probe_run(mode, bpc):
@@ -76,25 +69,17 @@ def main():
     cases = {
         "probe_read_nt_bpc1": (lambda: probe_run(0, 1), lay.slab_elems(P) * 4.0),
         "probe_read_bpc1": (lambda: probe_run(1, 1), lay.slab_elems(P) * 4.0),
-        "rows_b2_u4_temporal": (lambda: rows_run(2, 4, 2), alg),
-        "rows_b2_u4_temporal_ntstore": (lambda: rows_run(2, 4, 10), alg),
-        "rows_b1_u4_temporal_vec2": (lambda: rows_run(1, 4, 3), alg),
-        "rows_b8_u8_nt(default)": (lambda: rows_run(8, 8, 0), alg),
-        "tiled4096_b2_u4_nt": (lambda: tiled_run(lay, 2, 4, 0), alg),
-        "tiled4096_b2_u4_nt_ntstore": (lambda: tiled_run(lay, 2, 4, 8), alg),
-        "tiled4096_b2_u4_temporal": (lambda: tiled_run(lay, 2, 4, 2), alg),
-        "tiled2048_b1_u4_nt": (lambda: tiled_run(lay2, 1, 4, 0), alg),
-        "tiled2048_b2_u8_temporal": (lambda: tiled_run(lay2, 2, 8, 2), alg),
+        "rows_b2_u4_nt": (lambda: run(row_ptrs, 4096, 2, 4, 0), alg),
+        "rows_b2_u4_temporal": (lambda: run(row_ptrs, 4096, 2, 4, 3), alg),
+        "slab_b2_u4_nt": (lambda: run(slab_bases, lay.tile_stride, 2, 4, 0), alg),
+        "slab_b2_u4_nt_loads_temporal_stores": (lambda: run(slab_bases, lay.tile_stride, 2, 4, 2), alg),
+        "slab_b2_u8_nt": (lambda: run(slab_bases, lay.tile_stride, 2, 8, 0), alg),
+        "slab_b1_u8_nt": (lambda: run(slab_bases, lay.tile_stride, 1, 8, 0), alg),
+        "slab_b3_u4_nt": (lambda: run(slab_bases, lay.tile_stride, 3, 4, 0), alg),
     }
     t = {k: [] for k in cases}
-    filled = None
     for r in range(args.rounds):
         for name, (fn, _) in cases.items():
-            want = lay2 if "tiled2048" in name else lay
-            if filled is not want:
-                ctx.fill_synthetic_tiled_f32(slab.ptr, want, P, 1000, 0)
-                ctx.sync()
-                filled = want
             t[name].append(fn())
         print(f"round {r}", file=sys.stderr, flush=True)
     ctx.set_launch(0, 0)
