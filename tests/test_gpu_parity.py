@@ -72,7 +72,8 @@ def test_helper_golden_bitexact_with_folding(case):
     out = h.get_result()
     for k, name in case["expected"].items():
         assert same_bits(_as_numpy(out[k]).reshape(ARRAYS[name].shape), ARRAYS[name]), k
-    assert h.engine.stats["folds"] >= 1
+    if len(case["contributions"]) > 1:
+        assert h.engine.stats["folds"] >= 1
 
 
 @pytest.mark.parametrize("case", [c for c in HCASES if c["container"] == "torch"][:4],
