@@ -47,7 +47,8 @@ def parse():
     ap.add_argument("--cpu-sample-params", type=int, default=16 * 1024 * 1024)
     ap.add_argument("--spot-check", type=int, default=4096, help="sampled outputs checked against the oracle")
     ap.add_argument("--traffic-bytes", type=float, default=None,
-                    help="HBM bytes per launch from a separate rocprofv3 --pmc pass (reported in roofline.traffic)")
+                    help="HBM bytes per launch from a separate rocprofv3 --pmc pass (default: profiles/pmc_traffic.json "
+                         "when its config matches this run)")
     ap.add_argument("--seed", type=int, default=1000)
     return ap.parse_args()
 
@@ -143,6 +144,23 @@ def cpu_baseline_and_spot_check(args, ctx, K, out_buf, weights, count, P, col0, 
     return res
 
 
+def pmc_traffic(args, K, P):
+    """HBM bytes per launch measured by rocprofv3 PMC passes of this same command (profiles/pmc_traffic.json),
+    only when that measurement's configuration is this run's."""
+    if args.traffic_bytes is not None:
+        return args.traffic_bytes, "--traffic-bytes"
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            rec = json.load(f)
+    except (OSError, ValueError):
+        return None, None
+    cfg = rec.get("config", {})
+    if (cfg.get("clients"), cfg.get("params"), cfg.get("tile"), cfg.get("mode")) == (K, P, args.tile, args.mode):
+        return float(rec["bytes_per_launch"]), "profiles/pmc_traffic.json"
+    return None, None
+
+
 def main():
     args = parse()
     world, rank, local = dist_setup(args)
@@ -205,6 +223,7 @@ def main():
         bytes_step = 4.0 * K * P * world  # aggregated client bytes per step, all ranks
         value = bytes_step * args.steps / wall / 2**30
         alg_bytes_launch = 4.0 * K * P + 4.0 * P
+        traffic, traffic_src = pmc_traffic(args, K, P)
         achieved = alg_bytes_launch / (kernel_ms / 1e3) / 1e9
         line = {
             "metric": METRIC,
@@ -234,7 +253,8 @@ def main():
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": args.traffic_bytes,
+                "traffic": traffic,
+                "traffic_source": traffic_src,
                 "kernel_ms_avg": round(kernel_ms, 4),
                 "kernel_ms_avg_max_rank": round(kernel_ms_max, 4),
                 "alg_bytes_per_launch": alg_bytes_launch,
