@@ -81,14 +81,22 @@ def barrier_sync(world, ctx):
 
 
 def max_over_ranks(world, value: float) -> float:
+    """MAX over ranks (RCCL on GPUs; gloo in the CPU tests).  Timing only -- no data-path collective."""
     if world == 1:
         return value
     import torch
     import torch.distributed as dist
 
-    t = torch.tensor([value], dtype=torch.float64, device="cuda")
+    dev = "cuda" if dist.get_backend() == "nccl" else "cpu"
+    t = torch.tensor([value], dtype=torch.float64, device=dev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
+
+
+def rank_bucket(rank: int, P: int):
+    """Weak scaling: rank r aggregates global params [r*P, (r+1)*P) of every client (sharding.bucket_ranges
+    with equal per-GPU buckets); returns the generator column offset of the bucket."""
+    return rank * P
 
 
 def cpu_baseline_and_spot_check(args, ctx, K, out_buf, weights, count, P, col0, op):
@@ -175,7 +183,7 @@ def main():
     P = int(args.params)
     op = N.FEDAVG_OP_TORCH if args.mode == "torch" else N.FEDAVG_OP_NUMPY
     fin = N.FEDAVG_FIN_DIV if args.mode == "torch" else N.FEDAVG_FIN_SCALE
-    col0 = rank * P  # weak scaling: rank r owns param bucket [r*P, (r+1)*P)
+    col0 = rank_bucket(rank, P)  # weak scaling: rank r owns param bucket [r*P, (r+1)*P)
 
     free, total = ctx.mem_info()
     lay = TiledLayout(args.tile, K)  # the engine's slab layout: K client slots interleaved per tile

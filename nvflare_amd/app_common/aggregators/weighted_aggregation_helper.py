@@ -23,6 +23,7 @@ import threading
 from typing import Any, Callable, Dict, Optional, Set
 
 from ...engine import DeviceFedAvg, is_device_array, is_torch_tensor
+from ...sharding import ShardedFedAvg
 
 
 def _is_aggregatable_metric_value(v: Any) -> bool:
@@ -94,6 +95,9 @@ def compute_key_match_stats(contributions: Dict[str, Any]) -> dict:
     return _stats(len(contributions), contributions.keys(), counts, len(counts), 0)
 
 
+_ON_DEVICE = "device"  # marker in self.total: the key's running sum lives in the engine
+
+
 class _HostValue:
     """Running sum of one non-array key, with the reference's object arithmetic."""
 
@@ -110,6 +114,7 @@ class WeightedAggregationHelper(object):
         weigh_by_local_iter: bool = True,
         device: Optional[int] = None,
         max_resident_bytes: Optional[int] = None,
+        devices: Optional[list] = None,
     ):
         """Weighted aggregation on the MI355X (drop-in for weighted_aggregation_helper.py:117-131).
 
@@ -119,12 +124,18 @@ class WeightedAggregationHelper(object):
                 divided by the sum of weights).
             device: HIP device index (default: $NVFLARE_AMD_DEVICE or 0).
             max_resident_bytes: HBM budget for staged contributions before they are folded.
+            devices: several HIP devices: every key is split into per-device parameter buckets
+                (sharding.ShardedFedAvg; host arrays only), bit-identical to one device.
         """
         super().__init__()
         self.lock = threading.Lock()
         self.exclude_vars = re.compile(exclude_vars) if exclude_vars else None
         self.weigh_by_local_iter = weigh_by_local_iter
-        self._engine = DeviceFedAvg(device=device, max_resident_bytes=max_resident_bytes)
+        if devices and len(devices) > 1:
+            self._engine = ShardedFedAvg(devices, max_resident_bytes=max_resident_bytes)
+        else:
+            dev = devices[0] if devices else device
+            self._engine = DeviceFedAvg(device=dev, max_resident_bytes=max_resident_bytes)
         self.last_aggregation_stats = None
         self.reset_stats()
 
@@ -164,7 +175,7 @@ class WeightedAggregationHelper(object):
             if device_items:
                 self._engine.add(device_items, weight, self.weigh_by_local_iter)
                 for k, _ in device_items:
-                    self.total[k] = self._engine.keys[k]
+                    self.total[k] = _ON_DEVICE
             for k, v in host_items:
                 self._add_host(k, v, weight)
             for k, _ in device_items:

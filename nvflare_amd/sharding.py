@@ -1,0 +1,130 @@
+"""Parameter-bucket sharding of the FedAvg aggregation across GPUs.
+
+Every parameter is an independent unit of the hot path, so the flattened model splits into contiguous
+buckets, one per GPU; each GPU aggregates its bucket of every client with the same arrival order and
+weights.  No collective touches the data, and the result is bit-identical to one GPU -- which a
+client-sharded RCCL reduce would not be (it re-associates the sums).
+
+* ``bucket_ranges``   -- the partition (aligned so every bucket boundary is a whole tile).
+* ``ShardedFedAvg``   -- one process, N devices: each contribution's arrays are sliced (views, no copy)
+                         and staged to every device's engine from a thread per device, so the N PCIe
+                         links run in parallel; results are reassembled per key.
+* ``bench.py`` under torchrun uses the same partition with one process per GPU.
+"""
+
+from __future__ import annotations
+
+import threading
+from concurrent.futures import ThreadPoolExecutor
+from typing import Any, Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from .engine import DeviceFedAvg, is_torch_tensor
+
+BUCKET_ALIGN = 4096  # elements: a bucket boundary never splits a kernel tile
+
+
+def bucket_ranges(total: int, parts: int, align: int = BUCKET_ALIGN) -> List[Tuple[int, int]]:
+    """Split [0, total) into `parts` contiguous ranges whose inner boundaries are multiples of `align`
+    and whose sizes differ by at most one `align` unit."""
+    if parts < 1:
+        raise ValueError("parts must be >= 1")
+    units = (total + align - 1) // align
+    base, extra = divmod(units, parts)
+    out, start = [], 0
+    for r in range(parts):
+        # the extra units go to the LAST buckets, so the partial last unit evens out instead of adding up
+        n_units = base + (1 if r >= parts - extra else 0)
+        end = min(total, start + n_units * align)
+        out.append((start, end))
+        start = end
+    return out
+
+
+def _flat_view(v):
+    if is_torch_tensor(v):
+        t = v.detach()
+        return t.contiguous().reshape(-1)
+    return np.ascontiguousarray(v).reshape(-1)
+
+
+class ShardedFedAvg:
+    """DeviceFedAvg over several devices, by parameter bucket: every key of n elements is split into
+    `len(devices)` contiguous, tile-aligned pieces (keys shorter than one tile stay whole on one
+    device).  Partial keys and keys first seen late work exactly as on one device, bucket by bucket."""
+
+    def __init__(self, devices: Sequence[int], max_resident_bytes: Optional[int] = None):
+        self.devices = list(devices)
+        if not self.devices:
+            raise ValueError("at least one device")
+        self.engines = [DeviceFedAvg(device=d, max_resident_bytes=max_resident_bytes) for d in self.devices]
+        self.lock = threading.RLock()
+        self._pool = ThreadPoolExecutor(max_workers=len(self.devices), thread_name_prefix="nvflare-amd-shard")
+        self._shapes: Dict[str, tuple] = {}
+
+    def _pieces(self, bucket: int, items):
+        """(subkey, 1-D slice view) of every key overlapping `bucket`."""
+        out = []
+        for k, v in items:
+            n = int(np.prod(v.shape, dtype=np.int64)) if v.shape else 1
+            lo, hi = bucket_ranges(n, len(self.engines))[bucket]
+            if lo < hi or (n == 0 and bucket == 0):
+                out.append((f"{k}\x00{lo}", _flat_view(v)[lo:hi]))
+        return out
+
+    def add(self, items: List[Tuple[str, Any]], weight, weighted: bool) -> None:
+        with self.lock:
+            for k, v in items:
+                self._shapes.setdefault(k, tuple(v.shape))
+            futs = [self._pool.submit(eng.add, self._pieces(b, items), weight, weighted)
+                    for b, eng in enumerate(self.engines)]
+            for f in futs:
+                f.result()
+
+    def result(self) -> Dict[str, Any]:
+        with self.lock:
+            parts = list(self._pool.map(lambda e: e.result() if e.keys else {}, self.engines))
+            pieces: Dict[str, List[Tuple[int, Any]]] = {}
+            for res in parts:
+                for sub, arr in res.items():
+                    k, off = sub.split("\x00")
+                    pieces.setdefault(k, []).append((int(off), arr))
+            out = {}
+            for k, plist in pieces.items():
+                plist.sort(key=lambda x: x[0])
+                shape = self._shapes[k]
+                arrs = [a for _, a in plist]
+                if is_torch_tensor(arrs[0]):
+                    import torch
+
+                    flat = torch.cat([a.reshape(-1) for a in arrs]) if len(arrs) > 1 else arrs[0].reshape(-1)
+                    out[k] = flat.reshape(shape)
+                else:
+                    flat = np.concatenate([np.asarray(a).reshape(-1) for a in arrs]) if len(arrs) > 1 else np.asarray(arrs[0]).reshape(-1)
+                    res = flat.reshape(shape)
+                    out[k] = res[()] if res.ndim == 0 else res
+            return out
+
+    @property
+    def keys(self):
+        return {s.split("\x00")[0] for e in self.engines for s in e.keys}
+
+    @property
+    def stats(self):
+        agg = {}
+        for e in self.engines:
+            for k, v in e.stats.items():
+                agg[k] = agg.get(k, 0) + v
+        return agg
+
+    def reset(self) -> None:
+        with self.lock:
+            for e in self.engines:
+                e.reset()
+            self._shapes.clear()
+
+    def release(self) -> None:
+        for e in self.engines:
+            e.release()
+        self._pool.shutdown(wait=True)

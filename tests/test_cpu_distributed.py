@@ -1,0 +1,111 @@
+"""Multi-process (gloo, world_size 2) checks of the parameter-bucket sharding on CPU.
+
+The HIP kernel cannot run here, so each rank computes its bucket with the CPU oracle (test
+infrastructure) from the host twin of the bench's synthetic generator; rank 0 reassembles and compares
+bit-for-bit with a single-process aggregation of the whole model.  This is the partition the bench's
+torchrun path and sharding.ShardedFedAvg use: per-element order is unchanged, so no collective is needed
+and the bits cannot change."""
+
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from nvflare_amd.sharding import BUCKET_ALIGN, bucket_ranges
+
+
+@pytest.mark.parametrize("total", [0, 1, 4095, 4096, 4097, 10 * 4096 + 3, 1_000_000])
+@pytest.mark.parametrize("parts", [1, 2, 3, 8])
+def test_bucket_ranges_partition(total, parts):
+    r = bucket_ranges(total, parts)
+    assert len(r) == parts
+    assert r[0][0] == 0 and r[-1][1] == total
+    for (a0, a1), (b0, b1) in zip(r[:-1], r[1:]):
+        assert a1 == b0 and a0 <= a1
+        assert a1 % BUCKET_ALIGN == 0 or a1 == total
+    sizes = [b - a for a, b in r]
+    assert max(sizes) - min(sizes) <= BUCKET_ALIGN
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, P, K, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import bench
+        from oracle import fedavg_oracle as orc
+
+        col0 = bench.rank_bucket(rank, P)
+        rows = [orc.synth_values(1000, k, np.arange(col0, col0 + P, dtype=np.uint64)) for k in range(K)]
+        ws = orc.synth_weights(K)
+        part = orc.fedavg_c(rows, ws, orc.MODE_TORCH)
+        gathered = [None] * world if rank == 0 else None
+        dist.gather_object(part, gathered, dst=0)
+        t = bench.max_over_ranks(world, float(rank + 1))
+        if rank == 0:
+            q.put((np.concatenate(gathered), t))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_weak_scaling_buckets_gloo(oracle):
+    world, P, K = 2, 12_345, 9
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, P, K, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res, tmax = q.get(timeout=120)
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    rows = [oracle.synth_values(1000, k, np.arange(world * P, dtype=np.uint64)) for k in range(K)]
+    full = oracle.fedavg_c(rows, oracle.synth_weights(K), oracle.MODE_TORCH)
+    assert np.array_equal(res.view(np.uint32), full.view(np.uint32))
+    assert tmax == 2.0  # max over ranks
+
+
+def test_sharded_pieces_reassemble(oracle):
+    """ShardedFedAvg's slicing and reassembly (host side), checked with the oracle per bucket."""
+    from nvflare_amd.sharding import ShardedFedAvg
+
+    rng = np.random.default_rng(0)
+    shapes = {"a": (3, 5000), "b": (7,), "c": (), "d": (0,), "e": (2, 4096)}
+    K = 4
+    data = [{k: rng.standard_normal(s).astype(np.float32) for k, s in shapes.items()} for _ in range(K)]
+    ws = [1.0, 2.0, 0.5, 3.0]
+    sh = ShardedFedAvg.__new__(ShardedFedAvg)  # host-side methods only (no device engines)
+    sh.engines = [None, None, None]
+    pieces = [dict(sh._pieces(b, list(data[0].items()))) for b in range(3)]
+    covered = {}
+    for b, pc in enumerate(pieces):
+        for sub, arr in pc.items():
+            k, off = sub.split("\x00")
+            covered.setdefault(k, []).append((int(off), arr.size))
+    for k, s in shapes.items():
+        n = int(np.prod(s)) if s else 1
+        spans = sorted(covered[k])
+        assert spans[0][0] == 0 and sum(x for _, x in spans) == n
+    # bucket-wise oracle == whole-key oracle
+    for k, s in shapes.items():
+        n = int(np.prod(s)) if s else 1
+        if n == 0:
+            continue
+        whole = oracle.fedavg_c([d[k].reshape(-1) for d in data], ws, oracle.MODE_NUMPY)
+        parts = []
+        for lo, hi in bucket_ranges(n, 3):
+            if hi > lo:
+                parts.append(oracle.fedavg_c([d[k].reshape(-1)[lo:hi] for d in data], ws, oracle.MODE_NUMPY))
+        assert np.array_equal(np.concatenate(parts).view(np.uint32), whole.view(np.uint32))

@@ -76,6 +76,27 @@ def test_helper_golden_bitexact_with_folding(case):
         assert h.engine.stats["folds"] >= 1
 
 
+@pytest.mark.parametrize("case", [c for c in HCASES if "partial" in c["name"] or "many_keys" in c["name"]
+                                  or "k64" in c["name"] or "special" in c["name"]],
+                         ids=[c["name"] for c in HCASES if "partial" in c["name"] or "many_keys" in c["name"]
+                              or "k64" in c["name"] or "special" in c["name"]])
+def test_helper_golden_bitexact_sharded(case):
+    """Parameter-bucket sharding over 3 engines (here all on device 0): same bits as one device."""
+    from nvflare_amd.app_common.aggregators.weighted_aggregation_helper import WeightedAggregationHelper
+
+    h = WeightedAggregationHelper(exclude_vars=case["exclude_vars"], weigh_by_local_iter=case["weigh_by_local_iter"],
+                                  devices=[0, 0, 0])
+    for c in case["contributions"]:
+        h.add({k: _container(ARRAYS[n], case["container"]) for k, n in c["data"].items()}, c["weight"], c["name"], 0)
+    out = h.get_result()
+    assert set(out) == set(case["expected"])
+    for k, name in case["expected"].items():
+        got = _as_numpy(out[k])
+        assert str(got.dtype) == case["expected_dtype"][k]
+        assert same_bits(got.reshape(ARRAYS[name].shape), ARRAYS[name]), k
+    h.engine.release()
+
+
 @pytest.mark.parametrize("case", [c for c in HCASES if c["container"] == "torch"][:4],
                          ids=[c["name"] for c in HCASES if c["container"] == "torch"][:4])
 def test_helper_device_tensors(case):
