@@ -88,10 +88,16 @@ int fedavg_h2d(fedavg_ctx* ctx, void* dst, const void* src, size_t nbytes);
  * written to base + (b / tile_bytes) * tile_stride_bytes + b % tile_bytes (see fedavg_accumulate_tiled). */
 int fedavg_h2d_tiled(fedavg_ctx* ctx, void* base, size_t tile_bytes, size_t tile_stride_bytes,
                      size_t logical_offset, const void* src, size_t nbytes);
+/* Several host pieces of one client at once (its keys: sorted, non-overlapping logical byte offsets),
+ * packed into the pinned ring by logical position so each 64 MiB leaves in one tiled DMA. */
+int fedavg_h2d_tiled_multi(fedavg_ctx* ctx, void* base, size_t tile_bytes, size_t tile_stride_bytes,
+                           int n_pieces, const size_t* logical_offsets, const void* const* srcs,
+                           const size_t* nbytes);
 /* Device-resident source (e.g. a torch tensor on the GPU) into tiled client storage, on the compute stream. */
 int fedavg_d2d_tiled(fedavg_ctx* ctx, void* base, size_t tile_bytes, size_t tile_stride_bytes,
                      size_t logical_offset, const void* src, size_t nbytes);
-/* Device -> host; returns when the bytes are in `dst` (waits for prior compute on the handle). */
+/* Device -> host; returns when the bytes are in `dst` (waits for prior compute on the handle).  Large
+ * pageable destinations are drained through the pinned ring by the host copy threads. */
 int fedavg_d2h(fedavg_ctx* ctx, void* dst, const void* src, size_t nbytes);
 int fedavg_d2d(fedavg_ctx* ctx, void* dst, const void* src, size_t nbytes);
 int fedavg_memset(fedavg_ctx* ctx, void* dst, int value, size_t nbytes);

@@ -180,6 +180,56 @@ void h2d_impl(fedavg_ctx* ctx, char* dst, size_t tile_b, size_t tstride_b, size_
     HIP_CHECK(hipStreamWaitEvent(ctx->compute(), ctx->ev_copy_done, 0));
 }
 
+// Several host pieces of one client (its keys, in increasing logical order, non-overlapping) packed into
+// the pinned ring by LOGICAL position, so each 64 MiB slot leaves in one tiled DMA however many keys it
+// holds.  Gaps between pieces (key alignment padding) are copied as don't-care bytes.
+void h2d_multi_impl(fedavg_ctx* ctx, char* dst, size_t tile_b, size_t tstride_b, int n, const size_t* offs,
+                    const void* const* srcs, const size_t* lens) {
+    ctx->activate();
+    int i = 0;
+    while (i < n && lens[i] == 0) ++i;
+    while (i < n) {
+        const size_t win0 = offs[i];
+        const int slot = ctx->ring_next;
+        ctx->ring_next = (ctx->ring_next + 1) % kRingSlots;
+        if (ctx->ring_used[slot]) HIP_CHECK(hipEventSynchronize(ctx->ring_ev[slot]));
+        char* ring = static_cast<char*>(ctx->ring[slot]);
+        size_t win_end = win0;
+        // fill the slot with whole or partial pieces while they fit
+        while (i < n) {
+            if (lens[i] == 0) {
+                ++i;
+                continue;
+            }
+            if (offs[i] < win_end) throw Error("h2d pieces must be sorted and non-overlapping");
+            const size_t rel = offs[i] - win0;
+            if (rel >= kRingBytes) break;
+            const size_t take = std::min(lens[i], kRingBytes - rel);
+            parallel_memcpy(ring + rel, srcs[i], take);
+            win_end = offs[i] + take;
+            if (take < lens[i]) break;  // the rest of this piece goes to the next slot
+            ++i;
+        }
+        if (win_end > win0) {
+            copy_into_tiles(dst, tile_b, tstride_b, win0, ring, win_end - win0, hipMemcpyHostToDevice,
+                            ctx->copy_stream);
+            HIP_CHECK(hipEventRecord(ctx->ring_ev[slot], ctx->copy_stream));
+            ctx->ring_used[slot] = true;
+        }
+        if (i < n && offs[i] < win_end) {
+            // split piece: continue from win_end in a fresh slot
+            const size_t done = win_end - offs[i];
+            const size_t rest_off = win_end;
+            const void* rest_src = static_cast<const char*>(srcs[i]) + done;
+            const size_t rest_len = lens[i] - done;
+            h2d_multi_impl(ctx, dst, tile_b, tstride_b, 1, &rest_off, &rest_src, &rest_len);
+            ++i;
+        }
+    }
+    HIP_CHECK(hipEventRecord(ctx->ev_copy_done, ctx->copy_stream));
+    HIP_CHECK(hipStreamWaitEvent(ctx->compute(), ctx->ev_copy_done, 0));
+}
+
 void check_op_fin(int op, int fin) {
     if (op < FEDAVG_OP_NUMPY || op > FEDAVG_OP_UNWEIGHTED) throw Error("bad op " + std::to_string(op));
     if (fin < FEDAVG_FIN_NONE || fin > FEDAVG_FIN_DIV) throw Error("bad fin " + std::to_string(fin));
@@ -405,6 +455,20 @@ int fedavg_h2d_tiled(fedavg_ctx* ctx, void* base, size_t tile_bytes, size_t tile
     });
 }
 
+int fedavg_h2d_tiled_multi(fedavg_ctx* ctx, void* base, size_t tile_bytes, size_t tile_stride_bytes, int n_pieces,
+                           const size_t* logical_offsets, const void* const* srcs, const size_t* nbytes) {
+    return guarded([&] {
+        if (!ctx) throw Error("ctx is NULL");
+        if (n_pieces <= 0) return;
+        if (!base || !logical_offsets || !srcs || !nbytes) throw Error("NULL pointer");
+        if (tile_bytes == 0 || tile_stride_bytes < tile_bytes) throw Error("bad tile geometry");
+        for (int i = 0; i < n_pieces; ++i)
+            if (nbytes[i] && !srcs[i]) throw Error("NULL source piece");
+        h2d_multi_impl(ctx, static_cast<char*>(base), tile_bytes, tile_stride_bytes, n_pieces, logical_offsets, srcs,
+                       nbytes);
+    });
+}
+
 int fedavg_d2d_tiled(fedavg_ctx* ctx, void* base, size_t tile_bytes, size_t tile_stride_bytes, size_t logical_offset,
                      const void* src, size_t nbytes) {
     return guarded([&] {
@@ -424,8 +488,31 @@ int fedavg_d2h(fedavg_ctx* ctx, void* dst, const void* src, size_t nbytes) {
         if (nbytes == 0) return;
         if (!dst || !src) throw Error("NULL pointer");
         ctx->activate();
-        HIP_CHECK(hipMemcpyAsync(dst, src, nbytes, hipMemcpyDeviceToHost, ctx->compute()));
-        HIP_CHECK(hipStreamSynchronize(ctx->compute()));
+        hipStream_t s = ctx->compute();
+        if (nbytes < kParallelCopyMin || is_pinned_host(dst)) {
+            HIP_CHECK(hipMemcpyAsync(dst, src, nbytes, hipMemcpyDeviceToHost, s));
+            HIP_CHECK(hipStreamSynchronize(s));
+            return;
+        }
+        // pageable destination: DMA into the pinned ring, drained by the host threads one slot behind
+        for (int i = 0; i < kRingSlots; ++i)
+            if (ctx->ring_used[i]) HIP_CHECK(hipEventSynchronize(ctx->ring_ev[i]));
+        const size_t nchunks = (nbytes + kRingBytes - 1) / kRingBytes;
+        auto issue = [&](size_t c) {
+            const int slot = (int)(c % kRingSlots);
+            const size_t off = c * kRingBytes, len = std::min(kRingBytes, nbytes - off);
+            HIP_CHECK(hipMemcpyAsync(ctx->ring[slot], static_cast<const char*>(src) + off, len, hipMemcpyDeviceToHost, s));
+            HIP_CHECK(hipEventRecord(ctx->ring_ev[slot], s));
+            ctx->ring_used[slot] = true;
+        };
+        for (size_t c = 0; c < nchunks && c < (size_t)kRingSlots; ++c) issue(c);
+        for (size_t c = 0; c < nchunks; ++c) {
+            const int slot = (int)(c % kRingSlots);
+            const size_t off = c * kRingBytes, len = std::min(kRingBytes, nbytes - off);
+            HIP_CHECK(hipEventSynchronize(ctx->ring_ev[slot]));
+            parallel_memcpy(static_cast<char*>(dst) + off, ctx->ring[slot], len);
+            if (c + kRingSlots < nchunks) issue(c + kRingSlots);
+        }
     });
 }
 

@@ -214,6 +214,17 @@ class DeviceContext:
                    ctypes.c_size_t(tile_stride_bytes), ctypes.c_size_t(logical_offset), ctypes.c_void_p(src_ptr),
                    ctypes.c_size_t(nbytes))
 
+    def h2d_tiled_multi(self, base_ptr: int, tile_bytes: int, tile_stride_bytes: int, pieces) -> None:
+        """pieces: [(logical_byte_offset, src_ptr, nbytes)] sorted by offset, non-overlapping."""
+        n = len(pieces)
+        if not n:
+            return
+        offs = (ctypes.c_size_t * n)(*[p[0] for p in pieces])
+        srcs = (ctypes.c_void_p * n)(*[p[1] for p in pieces])
+        lens = (ctypes.c_size_t * n)(*[p[2] for p in pieces])
+        N.call("fedavg_h2d_tiled_multi", self.handle, ctypes.c_void_p(base_ptr), ctypes.c_size_t(tile_bytes),
+               ctypes.c_size_t(tile_stride_bytes), ctypes.c_int(n), offs, srcs, lens)
+
     def d2d_tiled(self, base_ptr: int, tile_bytes: int, tile_stride_bytes: int, logical_offset: int, src_ptr: int,
                   nbytes: int) -> None:
         if nbytes:

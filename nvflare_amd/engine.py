@@ -347,14 +347,20 @@ class DeviceFedAvg:
                 extent = max(st.offset + st.n for st, _ in arena_items)
                 slot = self._acquire_slot(extent)
                 lay = slot.slab.layout
-                for st, v in arena_items:
-                    keep, ptr, nbytes, on_dev = self._source(v)
-                    copy = self.ctx.d2d_tiled if on_dev else self.ctx.h2d_tiled
-                    copy(slot.base, lay.tile * 4, lay.tile_stride * 4, st.offset * 4, ptr, nbytes)
-                    del keep
+                host_pieces, keep = [], []
+                for st, v in sorted(arena_items, key=lambda x: x[0].offset):
+                    src, ptr, nbytes, on_dev = self._source(v)
+                    if on_dev:
+                        self.ctx.d2d_tiled(slot.base, lay.tile * 4, lay.tile_stride * 4, st.offset * 4, ptr, nbytes)
+                    else:
+                        host_pieces.append((st.offset * 4, ptr, nbytes))
+                        keep.append(src)
                     st.pending.append(_Staged(weight, slot=slot))
                     slot.refs += 1
                     self.stats["h2d_bytes"] += nbytes
+                # every host key of this client in one pass through the pinned ring (one DMA per 64 MiB)
+                self.ctx.h2d_tiled_multi(slot.base, lay.tile * 4, lay.tile_stride * 4, host_pieces)
+                del keep
             for st, v in states:
                 if st.arena or st.n == 0:
                     if st.n == 0:

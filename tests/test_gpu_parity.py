@@ -417,3 +417,37 @@ def test_engine_multi_slab_chaining(oracle, slots):
         assert same_bits(got, oracle.fedavg_c(rows, ws, oracle.MODE_NUMPY))
     assert eng.stats["slabs_allocated"] >= 1
     eng.release()
+
+
+def test_h2d_tiled_multi_packs_keys(ctx, oracle):
+    """Many keys of one client staged in one call: pieces spanning ring-slot boundaries (> 64 MiB),
+    zero-length pieces, gaps, pageable and pinned sources."""
+    from nvflare_amd.device import TiledLayout
+
+    tile, K = 4096, 3
+    sizes = [5, 0, 4096, 17 * 1024 * 1024 + 3, 64, 1, 3 * 4096 + 7]  # one piece larger than a ring slot
+    offs, off = [], 0
+    for n in sizes:
+        offs.append(off)
+        off += (n + 63) // 64 * 64
+    n_total = off
+    lay = TiledLayout(tile, K)
+    slab = ctx.alloc(lay.slab_elems(n_total) * 4)
+    rng = np.random.default_rng(3)
+    clients = [[rng.standard_normal(n).astype(np.float32) for n in sizes] for _ in range(K)]
+    for k, arrs in enumerate(clients):
+        srcs = [a if k != 1 else torch.from_numpy(a).pin_memory().numpy() for a in arrs]
+        ctx.h2d_tiled_multi(slab.ptr + lay.slot_offset_elems(k) * 4, tile * 4, lay.tile_stride * 4,
+                            [(o * 4, a.ctypes.data, a.nbytes) for o, a in zip(offs, srcs)])
+    ws = [0.5, 2.0, 1.25]
+    out = ctx.alloc(n_total * 4)
+    ctx.accumulate_tiled([slab.ptr + lay.slot_offset_elems(k) * 4 for k in range(K)], ws, tile, lay.tile_stride, 0,
+                         n_total, out.ptr, 0, 1, _sum(ws))
+    got = np.empty(n_total, np.float32)
+    ctx.d2h(got, out.ptr)  # > 8 MiB: drained through the pinned ring
+    for j, (o, n) in enumerate(zip(offs, sizes)):
+        if n:
+            exp = oracle.fedavg_c([clients[k][j] for k in range(K)], ws, oracle.MODE_NUMPY)
+            assert same_bits(got[o:o + n], exp), j
+    slab.close()
+    out.close()
