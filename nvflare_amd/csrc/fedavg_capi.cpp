@@ -79,6 +79,46 @@ void parallel_memcpy(void* dst, const void* src, size_t n) {
     for (auto& x : th) x.join();
 }
 
+// Copy a list of (dst, src, len) segments with the host copy threads, split by bytes (not by segment), so
+// a ring slot filled from hundreds of small keys copies as fast as one large one.
+struct Seg {
+    char* dst;
+    const char* src;
+    size_t len;
+};
+
+void parallel_gather(const std::vector<Seg>& segs) {
+    size_t total = 0;
+    for (const Seg& s : segs) total += s.len;
+    if (total < kParallelCopyMin) {
+        for (const Seg& s : segs) memcpy(s.dst, s.src, s.len);
+        return;
+    }
+    const size_t share = (total + kCopyThreads - 1) / kCopyThreads;
+    std::vector<std::thread> th;
+    th.reserve(kCopyThreads);
+    size_t seg = 0, seg_off = 0;
+    for (int t = 0; t < kCopyThreads && seg < segs.size(); ++t) {
+        // this thread's work: `share` bytes starting at (seg, seg_off)
+        std::vector<Seg> mine;
+        size_t need = share;
+        while (need && seg < segs.size()) {
+            const size_t take = std::min(need, segs[seg].len - seg_off);
+            mine.push_back({segs[seg].dst + seg_off, segs[seg].src + seg_off, take});
+            need -= take;
+            seg_off += take;
+            if (seg_off == segs[seg].len) {
+                ++seg;
+                seg_off = 0;
+            }
+        }
+        th.emplace_back([mine] {
+            for (const Seg& s : mine) memcpy(s.dst, s.src, s.len);
+        });
+    }
+    for (auto& x : th) x.join();
+}
+
 }  // namespace
 
 struct fedavg_ctx {
@@ -195,6 +235,7 @@ void h2d_multi_impl(fedavg_ctx* ctx, char* dst, size_t tile_b, size_t tstride_b,
         if (ctx->ring_used[slot]) HIP_CHECK(hipEventSynchronize(ctx->ring_ev[slot]));
         char* ring = static_cast<char*>(ctx->ring[slot]);
         size_t win_end = win0;
+        std::vector<Seg> segs;
         // fill the slot with whole or partial pieces while they fit
         while (i < n) {
             if (lens[i] == 0) {
@@ -205,11 +246,12 @@ void h2d_multi_impl(fedavg_ctx* ctx, char* dst, size_t tile_b, size_t tstride_b,
             const size_t rel = offs[i] - win0;
             if (rel >= kRingBytes) break;
             const size_t take = std::min(lens[i], kRingBytes - rel);
-            parallel_memcpy(ring + rel, srcs[i], take);
+            segs.push_back({ring + rel, static_cast<const char*>(srcs[i]), take});
             win_end = offs[i] + take;
             if (take < lens[i]) break;  // the rest of this piece goes to the next slot
             ++i;
         }
+        parallel_gather(segs);
         if (win_end > win0) {
             copy_into_tiles(dst, tile_b, tstride_b, win0, ring, win_end - win0, hipMemcpyHostToDevice,
                             ctx->copy_stream);
