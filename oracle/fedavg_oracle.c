@@ -108,3 +108,75 @@ float oracle_synth_value(uint64_t seed, uint64_t row, uint64_t col) {
 void oracle_synth_fill_f32(uint64_t seed, uint64_t row, const uint64_t* cols, size_t n, float* out) {
     for (size_t i = 0; i < n; ++i) out[i] = oracle_synth_value(seed, row, cols[i]);
 }
+
+/* ------------------------------------------------------------------------------------------------
+ * Server-optimizer epilogues, applied to the aggregated update
+ * d = fin(acc) of each element (computed exactly as above):
+ *   ADD_BASE  w = base + d            full_model_shareable_generator.py:58-67 (WEIGHT_DIFF apply)
+ *   SGD       torch/optim/sgd.py _single_tensor_sgd on grad g = -1.0 * d   (app_opt/pt/fedopt.py:175)
+ *   ADAM      torch/optim/adam.py _single_tensor_adam (:347-551) on g = -1.0 * d
+ * Rounding sequence pinned against torch 2.10 CPU (tests/test_fedopt_oracle.py):
+ *   add(alpha)  fma(b, alpha, a);   lerp  |w| < .5 ? fma(w, e - s, s) : fma(w - 1, e - s, e)
+ *   addcmul     fma(val * t1, t2, self);   addcdiv  self + (val * t1) / t2
+ *   sqrt        IEEE (correctly rounded).  torch CPU's MKL sqrt is not: ~0.6 % of its results are 1 ulp
+ *               off, so Adam params are compared within 1 ulp, m and v bit-exactly.
+ * Scalars follow torch: python-float hyperparameters and bias corrections computed in fp64, cast to
+ * fp32 where they meet a tensor.
+ * ------------------------------------------------------------------------------------------------ */
+enum { ORACLE_EPI_NONE = 0, ORACLE_EPI_ADD_BASE = 1, ORACLE_EPI_SGD = 2, ORACLE_EPI_ADAM = 3 };
+
+typedef struct {
+    int kind;
+    int first_step;  /* SGD: momentum buffer starts as a clone of the gradient */
+    int nesterov;
+    int maximize;
+    int decoupled_weight_decay; /* AdamW */
+    double lr, momentum, dampening, weight_decay; /* SGD (+ lr, weight_decay for Adam) */
+    double beta1, beta2, eps, step;               /* Adam: step after increment (1, 2, ...) */
+} oracle_epilogue;
+
+static inline float lerp_torch(float s, float e, float w) {
+    const float d = e - s;
+    return fabsf(w) < 0.5f ? fmaf(w, d, s) : fmaf(w - 1.0f, d, e);
+}
+
+void oracle_epilogue_apply(const float* delta, size_t n, const oracle_epilogue* epi, float* p, float* m, float* v,
+                           const float* base, float* out) {
+    for (size_t i = 0; i < n; ++i) {
+        const float d = delta[i];
+        if (epi->kind == ORACLE_EPI_NONE) {
+            out[i] = d;
+        } else if (epi->kind == ORACLE_EPI_ADD_BASE) {
+            out[i] = base[i] + d;
+        } else if (epi->kind == ORACLE_EPI_SGD) {
+            float g = epi->maximize ? d : -d;
+            if (epi->weight_decay != 0.0) g = fmaf(p[i], (float)epi->weight_decay, g);
+            if (epi->momentum != 0.0) {
+                float b;
+                if (epi->first_step) b = g;
+                else b = fmaf(g, (float)(1.0 - epi->dampening), m[i] * (float)epi->momentum);
+                m[i] = b;
+                g = epi->nesterov ? fmaf(b, (float)epi->momentum, g) : b;
+            }
+            p[i] = fmaf(g, (float)(-epi->lr), p[i]);
+        } else { /* ADAM */
+            float g = epi->maximize ? d : -d;
+            float pv = p[i];
+            if (epi->weight_decay != 0.0) {
+                if (epi->decoupled_weight_decay) pv = pv * (float)(1.0 - epi->lr * epi->weight_decay);
+                else g = fmaf(pv, (float)epi->weight_decay, g);
+            }
+            const float mm = lerp_torch(m[i], g, (float)(1.0 - epi->beta1));
+            const float vv = fmaf((float)(1.0 - epi->beta2) * g, g, v[i] * (float)epi->beta2);
+            const double bc1 = 1.0 - pow(epi->beta1, epi->step);
+            const double bc2 = 1.0 - pow(epi->beta2, epi->step);
+            const float step_size_neg = (float)(-(epi->lr / bc1));
+            const float bc2s = (float)sqrt(bc2);
+            const float denom = sqrtf(vv) / bc2s + (float)epi->eps;
+            pv = pv + (step_size_neg * mm) / denom;
+            m[i] = mm;
+            v[i] = vv;
+            p[i] = pv;
+        }
+    }
+}

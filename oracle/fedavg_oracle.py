@@ -178,3 +178,48 @@ def synth_values(seed: int, row: int, cols: np.ndarray) -> np.ndarray:
 def synth_weights(K: int):
     """Synthetic per-client weights of SURVEY.md section 8d: aggregation_weight 1.0 x NUM_STEPS (1 + 37k mod 100)."""
     return [1.0 * float(1 + (37 * k) % 100) for k in range(K)]
+
+
+# ---------------------------------------------------------------------------------------------------
+# server-optimizer epilogues (rows a9/a10): see oracle_epilogue_apply in fedavg_oracle.c
+# ---------------------------------------------------------------------------------------------------
+EPI_NONE, EPI_ADD_BASE, EPI_SGD, EPI_ADAM = 0, 1, 2, 3
+
+
+class _Epi(ctypes.Structure):
+    _fields_ = [
+        ("kind", ctypes.c_int),
+        ("first_step", ctypes.c_int),
+        ("nesterov", ctypes.c_int),
+        ("maximize", ctypes.c_int),
+        ("decoupled_weight_decay", ctypes.c_int),
+        ("lr", ctypes.c_double),
+        ("momentum", ctypes.c_double),
+        ("dampening", ctypes.c_double),
+        ("weight_decay", ctypes.c_double),
+        ("beta1", ctypes.c_double),
+        ("beta2", ctypes.c_double),
+        ("eps", ctypes.c_double),
+        ("step", ctypes.c_double),
+    ]
+
+
+def epilogue_apply(delta, kind, p=None, m=None, v=None, base=None, **hp):
+    """Apply an epilogue to the aggregated update `delta` (fp32).  p/m/v are updated IN PLACE (copies
+    are the caller's business); returns `out` for NONE/ADD_BASE and p otherwise."""
+    lib = load()
+    fn = lib.oracle_epilogue_apply
+    fn.restype = None
+    fn.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(_Epi)] + [ctypes.c_void_p] * 5
+    delta = np.ascontiguousarray(delta, dtype=np.float32).reshape(-1)
+    e = _Epi()
+    e.kind = kind
+    for k, val in hp.items():
+        setattr(e, k, val)
+    out = np.empty_like(delta)
+
+    def ptr(a):
+        return None if a is None else a.ctypes.data
+
+    fn(delta.ctypes.data, delta.size, ctypes.byref(e), ptr(p), ptr(m), ptr(v), ptr(base), out.ctypes.data)
+    return out if kind in (EPI_NONE, EPI_ADD_BASE) else p

@@ -1,0 +1,103 @@
+"""Pin the server-optimizer epilogue restatement (oracle/fedavg_oracle.c, oracle_epilogue_apply) against
+torch's own CPU optimizers, which NVFlare's FedOpt calls (app_opt/pt/fedopt.py:157-182 with
+torch/optim/sgd.py and torch/optim/adam.py _single_tensor_*).  No NVFlare test pins these numerics
+("parity unpinned" upstream); torch 2.10 CPU is the pin here.
+
+Tolerances:  SGD (all options) and Adam's exp_avg / exp_avg_sq: bit-exact.  Adam params: torch CPU's
+sqrt goes through MKL and is not correctly rounded (~0.6 % of results 1 ulp off); the restatement and the
+GPU use IEEE sqrt, so a param may differ by one rounding of `p + update` per step:
+    |p - p_torch| <= steps * spacing(max(|p_0|, |p_torch|, lr))      (elementwise)
+(lr bounds the magnitude of an Adam update; measured: max |diff| = 2^-22 after 5 steps, 0.01-0.1 % of
+elements differ at all)."""
+
+import numpy as np
+import pytest
+import torch
+
+from golden_util import same_bits
+
+
+def _ulp_diff(a, b):
+    ia = a.view(np.int32).astype(np.int64)
+    ib = b.view(np.int32).astype(np.int64)
+    ia = np.where(ia < 0, -(ia & 0x7FFFFFFF), ia)
+    ib = np.where(ib < 0, -(ib & 0x7FFFFFFF), ib)
+    return np.abs(ia - ib)
+
+
+def _torch_steps(opt_cls, kw, p0, deltas):
+    p = torch.nn.Parameter(torch.from_numpy(p0.copy()))
+    opt = opt_cls([p], foreach=False, **kw)
+    for d in deltas:
+        opt.zero_grad()
+        p.grad = torch.tensor(-1.0 * d)  # fedopt.py:175
+        opt.step()
+    return p.detach().numpy().copy(), opt.state[p]
+
+
+@pytest.mark.parametrize("kw", [
+    dict(lr=1.0),
+    dict(lr=0.7, momentum=0.9),
+    dict(lr=0.05, momentum=0.6, dampening=0.1),
+    dict(lr=0.05, momentum=0.9, nesterov=True),
+    dict(lr=0.1, momentum=0.9, weight_decay=1e-2),
+    dict(lr=0.3, maximize=True, momentum=0.5),
+])
+def test_sgd_bit_exact_vs_torch(oracle, kw):
+    rng = np.random.default_rng(0)
+    n = 100_003
+    p0 = rng.standard_normal(n).astype(np.float32)
+    deltas = [(rng.standard_normal(n) * 0.1).astype(np.float32) for _ in range(4)]
+    tp, st = _torch_steps(torch.optim.SGD, kw, p0, deltas)
+    p, buf = p0.copy(), np.zeros(n, np.float32)
+    for s, d in enumerate(deltas):
+        oracle.epilogue_apply(d, oracle.EPI_SGD, p=p, m=buf, first_step=int(s == 0), lr=kw["lr"],
+                              momentum=kw.get("momentum", 0.0), dampening=kw.get("dampening", 0.0),
+                              weight_decay=kw.get("weight_decay", 0.0), nesterov=int(kw.get("nesterov", False)),
+                              maximize=int(kw.get("maximize", False)))
+    assert same_bits(p, tp)
+    if kw.get("momentum"):
+        assert same_bits(buf, st["momentum_buffer"].numpy())
+
+
+@pytest.mark.parametrize("cls,kw", [
+    (torch.optim.Adam, dict(lr=1e-3)),
+    (torch.optim.Adam, dict(lr=1e-2, betas=(0.8, 0.99), eps=1e-6)),
+    (torch.optim.Adam, dict(lr=1e-3, weight_decay=1e-2)),
+    (torch.optim.AdamW, dict(lr=1e-3, weight_decay=1e-2)),
+    (torch.optim.Adam, dict(lr=1e-3, betas=(0.3, 0.999))),  # lerp weight >= 0.5 branch
+])
+def test_adam_vs_torch(oracle, cls, kw):
+    rng = np.random.default_rng(1)
+    n = 200_003
+    p0 = rng.standard_normal(n).astype(np.float32)
+    deltas = [(rng.standard_normal(n) * 0.01).astype(np.float32) for _ in range(5)]
+    tp, st = _torch_steps(cls, kw, p0, deltas)
+    b1, b2 = kw.get("betas", (0.9, 0.999))
+    p, m, v = p0.copy(), np.zeros(n, np.float32), np.zeros(n, np.float32)
+    for s, d in enumerate(deltas):
+        oracle.epilogue_apply(d, oracle.EPI_ADAM, p=p, m=m, v=v, lr=kw["lr"], beta1=b1, beta2=b2,
+                              eps=kw.get("eps", 1e-8), weight_decay=kw.get("weight_decay", 0.0 if cls is torch.optim.Adam else 1e-2),
+                              decoupled_weight_decay=int(cls is torch.optim.AdamW), step=float(s + 1))
+    if kw.get("weight_decay") and cls is torch.optim.Adam:
+        # coupled weight decay feeds p (a rounding off through torch's sqrt) back into g = -d + wd*p,
+        # so m and v inherit it at the scale of wd*|p|: compare within that
+        for ours, ref in ((m, st["exp_avg"].numpy()), (v, st["exp_avg_sq"].numpy())):
+            scale = np.maximum(np.abs(ref), np.float32(kw["weight_decay"]) * np.abs(p0))
+            assert np.all(np.abs(ours.astype(np.float64) - ref) <= len(deltas) * np.spacing(scale))
+    else:
+        assert same_bits(m, st["exp_avg"].numpy()), "exp_avg"
+        assert same_bits(v, st["exp_avg_sq"].numpy()), "exp_avg_sq"
+    steps = len(deltas)
+    tol = steps * np.spacing(np.maximum(np.maximum(np.abs(p0), np.abs(tp)), np.float32(kw["lr"]))).astype(np.float64)
+    diff = np.abs(p.astype(np.float64) - tp.astype(np.float64))
+    assert np.all(diff <= tol), float((diff / tol).max())
+    assert float((diff > 0).mean()) < 0.01
+
+
+def test_add_base_matches_numpy_generator(oracle):
+    """full_model_shareable_generator.py:58-67: weights[k] = weights[k] + diff[k] (numpy fp32 add)."""
+    rng = np.random.default_rng(2)
+    base = rng.standard_normal(10_001).astype(np.float32)
+    d = rng.standard_normal(10_001).astype(np.float32)
+    assert same_bits(oracle.epilogue_apply(d, oracle.EPI_ADD_BASE, base=base), base + d)
