@@ -56,6 +56,29 @@ enum fedavg_fin {
     FEDAVG_FIN_DIV = 2,
 };
 
+/* server-optimizer epilogue fused behind the finalisation (fedavg_accumulate_tiled_epi) */
+enum fedavg_epi {
+    FEDAVG_EPI_NONE = 0,
+    FEDAVG_EPI_ADD_BASE = 1, /* w = base + d        full_model_shareable_generator.py:58-67 */
+    FEDAVG_EPI_SGD = 2,      /* torch SGD on g = -d   app_opt/pt/fedopt.py:157-182 */
+    FEDAVG_EPI_ADAM = 3,     /* torch Adam/AdamW on g = -d  (torch/optim/adam.py:347-551) */
+};
+
+typedef struct fedavg_epilogue {
+    int kind;                   /* enum fedavg_epi */
+    int first_step;             /* SGD: the momentum buffer starts as a clone of the gradient */
+    int nesterov;               /* SGD */
+    int maximize;               /* SGD/Adam: optimise the positive update */
+    int decoupled_weight_decay; /* Adam: AdamW */
+    double lr, momentum, dampening, weight_decay;
+    double beta1, beta2, eps;
+    double step;                /* Adam: step count after this update (1, 2, ...) */
+    float* param;               /* SGD/Adam: flat fp32 params, updated in place */
+    float* state1;              /* SGD momentum buffer / Adam exp_avg (in place) */
+    float* state2;              /* Adam exp_avg_sq (in place) */
+    const float* base;          /* ADD_BASE: flat fp32 base weights (out may alias it) */
+} fedavg_epilogue;
+
 typedef struct fedavg_ctx fedavg_ctx;
 
 /* Last error message of the calling thread ("" if none). */
@@ -128,6 +151,14 @@ int fedavg_accumulate(fedavg_ctx* ctx, const void* const* rows, const double* we
 int fedavg_accumulate_tiled(fedavg_ctx* ctx, const void* const* bases, const double* weights, int k_rows,
                             size_t tile_elems, size_t tile_stride, size_t begin, size_t end,
                             const void* acc_in, void* out, int op, int fin, double count);
+
+/* fedavg_accumulate_tiled with a server-optimizer epilogue applied per element to d = fin(acc) in the
+ * same launch (rows a9/a10): ADD_BASE writes base + d to out; SGD/ADAM update epi->param/state in place
+ * and also store d to out when out != NULL.  More than 128 clients need out (scratch for the chain). */
+int fedavg_accumulate_tiled_epi(fedavg_ctx* ctx, const void* const* bases, const double* weights, int k_rows,
+                                size_t tile_elems, size_t tile_stride, size_t begin, size_t end,
+                                const void* acc_in, void* out, int op, int fin, double count,
+                                const fedavg_epilogue* epi);
 
 /* Timing of the kernels launched by the last fedavg_accumulate call, measured with HIP events on
  * the stream they ran on (enable first; costs two event records per call). */

@@ -89,6 +89,22 @@ _SIGNATURES = {
         c_int,  # fin
         c_double,  # count
     ],
+    "fedavg_accumulate_tiled_epi": [
+        c_void_p,  # ctx
+        ctypes.POINTER(c_void_p),  # bases
+        ctypes.POINTER(c_double),  # weights
+        c_int,  # k_rows
+        c_size_t,  # tile_elems
+        c_size_t,  # tile_stride
+        c_size_t,  # begin
+        c_size_t,  # end
+        c_void_p,  # acc_in
+        c_void_p,  # out
+        c_int,  # op
+        c_int,  # fin
+        c_double,  # count
+        c_void_p,  # const fedavg_epilogue*
+    ],
     "fedavg_set_timing": [c_void_p, c_int],
     "fedavg_last_kernel_ms": [c_void_p, ctypes.POINTER(c_float)],
     "fedavg_timing_begin": [c_void_p],
@@ -100,6 +116,36 @@ _SIGNATURES = {
     "fedavg_gather_f32": [c_void_p, c_void_p, c_void_p, c_size_t, c_void_p],
 }
 EXPORTED = ["fedavg_last_error", "fedavg_abi_version", *_SIGNATURES.keys()]
+
+
+FEDAVG_EPI_NONE = 0
+FEDAVG_EPI_ADD_BASE = 1
+FEDAVG_EPI_SGD = 2
+FEDAVG_EPI_ADAM = 3
+
+
+class Epilogue(ctypes.Structure):
+    """struct fedavg_epilogue (include/nvflare_amd_fedavg.h)."""
+
+    _fields_ = [
+        ("kind", c_int),
+        ("first_step", c_int),
+        ("nesterov", c_int),
+        ("maximize", c_int),
+        ("decoupled_weight_decay", c_int),
+        ("lr", c_double),
+        ("momentum", c_double),
+        ("dampening", c_double),
+        ("weight_decay", c_double),
+        ("beta1", c_double),
+        ("beta2", c_double),
+        ("eps", c_double),
+        ("step", c_double),
+        ("param", c_void_p),
+        ("state1", c_void_p),
+        ("state2", c_void_p),
+        ("base", c_void_p),
+    ]
 
 
 class FedAvgError(RuntimeError):

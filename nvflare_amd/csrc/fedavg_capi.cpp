@@ -8,6 +8,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <cmath>
 #include <exception>
 #include <new>
 #include <string>
@@ -316,6 +317,39 @@ void run_tiles(fedavg_ctx* ctx, const void* const* bases, const double* weights,
         cur_in = out;
         k0 += kc;
     } while (k0 < k_rows);
+}
+
+// Epilogue scalars as torch computes them: python-float (fp64) hyperparameters and bias corrections,
+// cast to fp32 where they meet a tensor (oracle/fedavg_oracle.c oracle_epilogue_apply mirrors this).
+fedavg::EpiParams make_epi(const fedavg_epilogue& e) {
+    fedavg::EpiParams E;
+    memset(&E, 0, sizeof(E));
+    E.kind = e.kind;
+    E.first_step = e.first_step;
+    E.nesterov = e.nesterov;
+    E.maximize = e.maximize;
+    E.decoupled_weight_decay = e.decoupled_weight_decay;
+    E.has_weight_decay = e.weight_decay != 0.0;
+    E.has_momentum = e.momentum != 0.0;
+    E.weight_decay = (float)e.weight_decay;
+    E.momentum = (float)e.momentum;
+    E.one_minus_dampening = (float)(1.0 - e.dampening);
+    E.neg_lr = (float)(-e.lr);
+    E.decoupled_scale = (float)(1.0 - e.lr * e.weight_decay);
+    E.one_minus_beta1 = (float)(1.0 - e.beta1);
+    E.one_minus_beta1_m1 = E.one_minus_beta1 - 1.0f;  // lerp_vec: weight - vec_t(1), in fp32
+    E.one_minus_beta2 = (float)(1.0 - e.beta2);
+    E.beta2 = (float)e.beta2;
+    const double bc1 = 1.0 - std::pow(e.beta1, e.step);
+    const double bc2 = 1.0 - std::pow(e.beta2, e.step);
+    E.step_size_neg = (float)(-(e.lr / bc1));
+    E.bias_correction2_sqrt = (float)std::pow(bc2, 0.5);
+    E.eps = (float)e.eps;
+    E.param = e.param;
+    E.state1 = e.state1;
+    E.state2 = e.state2;
+    E.base = e.base;
+    return E;
 }
 
 void run_generic(fedavg_ctx* ctx, const void* const* rows, const double* weights, int k_rows, size_t elem_off,
@@ -655,6 +689,74 @@ int fedavg_accumulate_tiled(fedavg_ctx* ctx, const void* const* bases, const dou
         TimingScope ts(ctx, s);
         run_tiles(ctx, bases, weights, k_rows, (int64_t)tile_elems, (int64_t)tile_stride, (int64_t)begin, (int64_t)end,
                   static_cast<const float*>(acc_in), static_cast<float*>(out), op, fin, count, s);
+        ts.done();
+    });
+}
+
+int fedavg_accumulate_tiled_epi(fedavg_ctx* ctx, const void* const* bases, const double* weights, int k_rows,
+                                size_t tile_elems, size_t tile_stride, size_t begin, size_t end, const void* acc_in,
+                                void* out, int op, int fin, double count, const fedavg_epilogue* epi) {
+    return guarded([&] {
+        if (!ctx || !epi) throw Error("NULL argument");
+        if (epi->kind == FEDAVG_EPI_NONE) {
+            if (fedavg_accumulate_tiled(ctx, bases, weights, k_rows, tile_elems, tile_stride, begin, end, acc_in, out,
+                                        op, fin, count))
+                throw Error(g_last_error);
+            return;
+        }
+        if (epi->kind < FEDAVG_EPI_ADD_BASE || epi->kind > FEDAVG_EPI_ADAM) throw Error("bad epilogue kind");
+        if (k_rows < 0 || (k_rows == 0 && !acc_in)) throw Error("k_rows == 0 requires acc_in");
+        check_op_fin(op, fin);
+        if (tile_elems != (size_t)fedavg::kDefaultTile)
+            throw Error("the epilogue kernel runs the default tile (" + std::to_string(fedavg::kDefaultTile) + ")");
+        if (tile_stride < tile_elems || tile_stride % 4) throw Error("tile_stride must be >= tile_elems, multiple of 4");
+        if (begin % 4 || end % 4 || end < begin) throw Error("begin/end must be multiples of 4 with begin <= end");
+        if (end == begin) return;
+        auto misaligned = [](const void* p) { return reinterpret_cast<uintptr_t>(p) % 16 != 0; };
+        if (epi->kind == FEDAVG_EPI_ADD_BASE && (!epi->base || !out)) throw Error("ADD_BASE needs base and out");
+        if (epi->kind == FEDAVG_EPI_SGD && (!epi->param || (epi->momentum != 0.0 && !epi->state1)))
+            throw Error("SGD needs param (and state1 with momentum)");
+        if (epi->kind == FEDAVG_EPI_ADAM && (!epi->param || !epi->state1 || !epi->state2))
+            throw Error("ADAM needs param, state1 (exp_avg), state2 (exp_avg_sq)");
+        if (epi->kind == FEDAVG_EPI_ADAM && epi->step < 1.0) throw Error("ADAM step must be >= 1");
+        if (k_rows > fedavg::kMaxRowsPerLaunch && !out) throw Error("more than 128 clients need out as scratch");
+        for (const void* p : {(const void*)epi->param, (const void*)epi->state1, (const void*)epi->state2,
+                              (const void*)epi->base, (const void*)out, acc_in})
+            if (misaligned(p)) throw Error("epilogue/out/acc_in pointers must be 16-byte aligned");
+        for (int k = 0; k < k_rows; ++k)
+            if (!bases[k] || misaligned(bases[k])) throw Error("base " + std::to_string(k) + " NULL or misaligned");
+        ctx->activate();
+        hipStream_t s = ctx->compute();
+        TimingScope ts(ctx, s);
+        // leading chunks (beyond 128 clients) accumulate into out; the last chunk runs the epilogue
+        int head = k_rows > fedavg::kMaxRowsPerLaunch ? (k_rows - 1) / fedavg::kMaxRowsPerLaunch * fedavg::kMaxRowsPerLaunch : 0;
+        const float* cur_in = static_cast<const float*>(acc_in);
+        if (head > 0) {
+            run_tiles(ctx, bases, weights, head, (int64_t)tile_elems, (int64_t)tile_stride, (int64_t)begin,
+                      (int64_t)end, cur_in, static_cast<float*>(out), op, FEDAVG_FIN_NONE, count, s);
+            cur_in = static_cast<const float*>(out);
+        }
+        fedavg::TileLaunch L;
+        memset(&L.tab, 0, sizeof(L.tab));
+        for (int j = head; j < k_rows; ++j) {
+            L.tab.rows[j - head] = static_cast<const fedavg::f32x4*>(bases[j]);
+            L.tab.w[j - head] = (float)weights[j];
+        }
+        L.k = k_rows - head;
+        L.op = op;
+        L.fin = fin;
+        L.unroll = fedavg::kDefaultUnroll;
+        L.variant = 0;
+        L.tile4 = (int64_t)tile_elems / 4;
+        L.tstride4 = (int64_t)tile_stride / 4;
+        L.b4 = (int64_t)begin / 4;
+        L.e4 = (int64_t)end / 4;
+        const int64_t n_tiles = (L.e4 - 1) / L.tile4 - L.b4 / L.tile4 + 1;
+        L.grid = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)ctx->num_cus * ctx->blocks_per_cu, n_tiles));
+        L.fin_val = (float)fin_scalar(fin, count);
+        L.acc_in = cur_in;
+        L.out = static_cast<float*>(out);
+        HIP_CHECK(fedavg::launch_tiles_epi_f32x4(L, make_epi(*epi), s));
         ts.done();
     });
 }

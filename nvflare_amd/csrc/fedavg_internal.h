@@ -48,7 +48,22 @@ struct TileLaunch {
     float fin_val;
 };
 
+// Epilogue scalars, precomputed on the host exactly as torch computes them (python fp64, cast to fp32
+// where they meet a tensor) -- see fedavg_capi.cpp make_epi().
+struct EpiParams {
+    int kind;
+    int first_step, nesterov, maximize, decoupled_weight_decay, has_weight_decay, has_momentum;
+    float weight_decay, momentum, one_minus_dampening, neg_lr;                  // SGD
+    float decoupled_scale, one_minus_beta1, one_minus_beta1_m1, one_minus_beta2; // Adam
+    float beta2, step_size_neg, bias_correction2_sqrt, eps;
+    float* param;
+    float* state1;  // SGD momentum buffer / Adam exp_avg
+    float* state2;  // Adam exp_avg_sq
+    const float* base;
+};
+
 hipError_t launch_tiles_f32x4(const TileLaunch& L, hipStream_t s);
+hipError_t launch_tiles_epi_f32x4(const TileLaunch& L, const EpiParams& E, hipStream_t s);
 hipError_t launch_rows_generic(const RowTableGeneric& tab, int K, const void* acc_in, void* out, int64_t n,
                                int in_dtype, int acc_dtype, int op, int fin, double fin_val, int grid,
                                hipStream_t s);

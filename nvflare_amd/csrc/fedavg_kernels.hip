@@ -156,6 +156,127 @@ __global__ void __launch_bounds__(kBlock) fedavg_tiles_f32x4(const RowTableF32 t
 }
 
 // ---------------------------------------------------------------------------------------------
+// The hot kernel with a server-optimizer EPILOGUE fused behind the finalisation (SURVEY.md section 8
+// rows a9/a10): d = fin(acc) is not stored but consumed per element by
+//   EPI_ADD_BASE  w = base + d                          full_model_shareable_generator.py:58-67
+//   EPI_SGD       torch _single_tensor_sgd on g = -d     app_opt/pt/fedopt.py:157-182
+//   EPI_ADAM      torch _single_tensor_adam on g = -d    torch/optim/adam.py:347-551
+// Per parameter: 4K bytes of client reads + 12 B (p, m, v) read + 12 B written for Adam, so the
+// optimizer costs one pass instead of the reference's separate aggregate / H2D / step / D2H round trip.
+// Rounding sequence pinned against torch CPU by tests/test_fedopt_oracle.py (fma for add(alpha), lerp
+// and addcmul; IEEE sqrt).  Geometry fixed at the tuned default (T = 4096, unroll 4, nontemporal).
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ float lerp_torch(float s, float e, float w, float w_m1) {
+    const float d = e - s;
+    return fabsf(w) < 0.5f ? __builtin_fmaf(w, d, s) : __builtin_fmaf(w_m1, d, e);
+}
+
+template <int EPI>
+__device__ __forceinline__ void epilogue4(const EpiParams& E, const int64_t i, const f32x4 d, f32x4* out) {
+    f32x4* p4 = reinterpret_cast<f32x4*>(E.param) + i;
+    if constexpr (EPI == FEDAVG_EPI_ADD_BASE) {
+        const f32x4 b = load4<true>(reinterpret_cast<const f32x4*>(E.base) + i);
+        store4<true>(out + i, b + d);
+    } else if constexpr (EPI == FEDAVG_EPI_SGD) {
+        f32x4 p = load4<true>(p4);
+        f32x4 buf;
+        if (E.has_momentum && !E.first_step) buf = load4<true>(reinterpret_cast<const f32x4*>(E.state1) + i);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            float g = E.maximize ? d[c] : -d[c];
+            if (E.has_weight_decay) g = __builtin_fmaf(p[c], E.weight_decay, g);
+            if (E.has_momentum) {
+                const float b = E.first_step ? g : __builtin_fmaf(g, E.one_minus_dampening, buf[c] * E.momentum);
+                buf[c] = b;
+                g = E.nesterov ? __builtin_fmaf(b, E.momentum, g) : b;
+            }
+            p[c] = __builtin_fmaf(g, E.neg_lr, p[c]);
+        }
+        store4<true>(p4, p);
+        if (E.has_momentum) store4<true>(reinterpret_cast<f32x4*>(E.state1) + i, buf);
+    } else {  // EPI_ADAM
+        f32x4 p = load4<true>(p4);
+        f32x4 m = load4<true>(reinterpret_cast<const f32x4*>(E.state1) + i);
+        f32x4 v = load4<true>(reinterpret_cast<const f32x4*>(E.state2) + i);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            float g = E.maximize ? d[c] : -d[c];
+            float pv = p[c];
+            if (E.has_weight_decay) {
+                if (E.decoupled_weight_decay) pv = pv * E.decoupled_scale;
+                else g = __builtin_fmaf(pv, E.weight_decay, g);
+            }
+            const float mm = lerp_torch(m[c], g, E.one_minus_beta1, E.one_minus_beta1_m1);
+            const float vv = __builtin_fmaf(E.one_minus_beta2 * g, g, v[c] * E.beta2);
+            const float denom = __builtin_sqrtf(vv) / E.bias_correction2_sqrt + E.eps;
+            pv = pv + (E.step_size_neg * mm) / denom;
+            m[c] = mm;
+            v[c] = vv;
+            p[c] = pv;
+        }
+        store4<true>(p4, p);
+        store4<true>(reinterpret_cast<f32x4*>(E.state1) + i, m);
+        store4<true>(reinterpret_cast<f32x4*>(E.state2) + i, v);
+    }
+}
+
+template <int OP, int FIN, bool ACC_IN, int EPI>
+__global__ void __launch_bounds__(kBlock) fedavg_tiles_epi_f32x4(const RowTableF32 tab, const int K,
+                                                                  const int64_t tstride4, const f32x4* acc_in,
+                                                                  f32x4* out, const int64_t b4, const int64_t e4,
+                                                                  const float fin_val, const EpiParams E) {
+    constexpr int UNROLL = kDefaultUnroll;
+    constexpr int CPL = kDefaultTile / (4 * kBlock);
+    constexpr int64_t T4 = (int64_t)CPL * kBlock;
+    const int64_t t_last = (e4 - 1) / T4;
+    for (int64_t t = b4 / T4 + blockIdx.x; t <= t_last; t += gridDim.x) {
+        const int64_t off = t * tstride4 + threadIdx.x;
+        const int64_t col = t * T4 + threadIdx.x;
+        f32x4 acc[CPL];
+        int k = 0;
+        if constexpr (ACC_IN) {
+#pragma unroll
+            for (int c = 0; c < CPL; ++c) {
+                const int64_t i = col + c * kBlock;
+                acc[c] = (i >= b4 && i < e4) ? load4<false>(acc_in + i) : f32x4{0, 0, 0, 0};
+            }
+        } else {
+            const f32x4* r = tab.rows[0] + off;
+#pragma unroll
+            for (int c = 0; c < CPL; ++c) acc[c] = first4<OP>(load4<true>(r + c * kBlock), tab.w[0]);
+            k = 1;
+        }
+        for (; k + UNROLL <= K; k += UNROLL) {
+            f32x4 v[UNROLL][CPL];
+#pragma unroll
+            for (int j = 0; j < UNROLL; ++j) {
+                const f32x4* r = tab.rows[k + j] + off;
+#pragma unroll
+                for (int c = 0; c < CPL; ++c) v[j][c] = load4<true>(r + c * kBlock);
+            }
+#pragma unroll
+            for (int j = 0; j < UNROLL; ++j)
+#pragma unroll
+                for (int c = 0; c < CPL; ++c) acc[c] = step4<OP>(acc[c], v[j][c], tab.w[k + j]);
+        }
+        for (; k < K; ++k) {
+            const f32x4* r = tab.rows[k] + off;
+#pragma unroll
+            for (int c = 0; c < CPL; ++c) acc[c] = step4<OP>(acc[c], load4<true>(r + c * kBlock), tab.w[k]);
+        }
+#pragma unroll
+        for (int c = 0; c < CPL; ++c) {
+            const int64_t i = col + c * kBlock;
+            if (i >= b4 && i < e4) {
+                const f32x4 d = fin4<FIN>(acc[c], fin_val);
+                if (out != nullptr && EPI != FEDAVG_EPI_ADD_BASE) store4<true>(out + i, d);
+                epilogue4<EPI>(E, i, d, out);
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
 // generic scalar kernel: any (Tin, Tacc) pair, contiguous rows, any alignment (ragged tails, fp64, ints)
 // ---------------------------------------------------------------------------------------------
 template <typename Tin, typename Tacc, int OP, int FIN, bool ACC_IN>
@@ -287,6 +408,57 @@ hipError_t launch_tiles_f32x4(const TileLaunch& L, hipStream_t s) {
             return launch_tiles_o<FEDAVG_OP_UNWEIGHTED>(L, s);
         default:
             return launch_tiles_o<FEDAVG_OP_NUMPY>(L, s);
+    }
+}
+
+template <int OP, int FIN, bool ACC_IN>
+static hipError_t launch_epi_a(const TileLaunch& L, const EpiParams& E, hipStream_t s) {
+    const f32x4* ai = reinterpret_cast<const f32x4*>(L.acc_in);
+    f32x4* o = reinterpret_cast<f32x4*>(L.out);
+    switch (E.kind) {
+        case FEDAVG_EPI_ADD_BASE:
+            hipLaunchKernelGGL((fedavg_tiles_epi_f32x4<OP, FIN, ACC_IN, FEDAVG_EPI_ADD_BASE>), dim3(L.grid),
+                               dim3(kBlock), 0, s, L.tab, L.k, L.tstride4, ai, o, L.b4, L.e4, L.fin_val, E);
+            break;
+        case FEDAVG_EPI_SGD:
+            hipLaunchKernelGGL((fedavg_tiles_epi_f32x4<OP, FIN, ACC_IN, FEDAVG_EPI_SGD>), dim3(L.grid), dim3(kBlock),
+                               0, s, L.tab, L.k, L.tstride4, ai, o, L.b4, L.e4, L.fin_val, E);
+            break;
+        case FEDAVG_EPI_ADAM:
+            hipLaunchKernelGGL((fedavg_tiles_epi_f32x4<OP, FIN, ACC_IN, FEDAVG_EPI_ADAM>), dim3(L.grid), dim3(kBlock),
+                               0, s, L.tab, L.k, L.tstride4, ai, o, L.b4, L.e4, L.fin_val, E);
+            break;
+        default:
+            return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+template <int OP, int FIN>
+static hipError_t launch_epi_f(const TileLaunch& L, const EpiParams& E, hipStream_t s) {
+    return L.acc_in ? launch_epi_a<OP, FIN, true>(L, E, s) : launch_epi_a<OP, FIN, false>(L, E, s);
+}
+
+template <int OP>
+static hipError_t launch_epi_o(const TileLaunch& L, const EpiParams& E, hipStream_t s) {
+    switch (L.fin) {
+        case FEDAVG_FIN_SCALE:
+            return launch_epi_f<OP, FEDAVG_FIN_SCALE>(L, E, s);
+        case FEDAVG_FIN_DIV:
+            return launch_epi_f<OP, FEDAVG_FIN_DIV>(L, E, s);
+        default:
+            return launch_epi_f<OP, FEDAVG_FIN_NONE>(L, E, s);
+    }
+}
+
+hipError_t launch_tiles_epi_f32x4(const TileLaunch& L, const EpiParams& E, hipStream_t s) {
+    switch (L.op) {
+        case FEDAVG_OP_TORCH:
+            return launch_epi_o<FEDAVG_OP_TORCH>(L, E, s);
+        case FEDAVG_OP_UNWEIGHTED:
+            return launch_epi_o<FEDAVG_OP_UNWEIGHTED>(L, E, s);
+        default:
+            return launch_epi_o<FEDAVG_OP_NUMPY>(L, E, s);
     }
 }
 

@@ -171,7 +171,7 @@ void oracle_epilogue_apply(const float* delta, size_t n, const oracle_epilogue* 
             const double bc1 = 1.0 - pow(epi->beta1, epi->step);
             const double bc2 = 1.0 - pow(epi->beta2, epi->step);
             const float step_size_neg = (float)(-(epi->lr / bc1));
-            const float bc2s = (float)sqrt(bc2);
+            const float bc2s = (float)pow(bc2, 0.5); /* python: bias_correction2**0.5 */
             const float denom = sqrtf(vv) / bc2s + (float)epi->eps;
             pv = pv + (step_size_neg * mm) / denom;
             m[i] = mm;

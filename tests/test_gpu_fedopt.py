@@ -1,0 +1,191 @@
+"""GPU parity of the fused server-optimizer epilogues (rows a9/a10) against the CPU oracle, bit-exact
+(both use IEEE arithmetic; the oracle itself is pinned to torch CPU by tests/test_fedopt_oracle.py)."""
+
+import numpy as np
+import pytest
+
+from golden_util import same_bits
+
+pytestmark = pytest.mark.gpu
+
+TILE = 4096
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    from nvflare_amd.device import DeviceContext
+
+    return DeviceContext.get(0)
+
+
+def _sum(ws):
+    c = None
+    for w in ws:
+        c = w if c is None else c + w
+    return c
+
+
+class _Dev:
+    """Slab of K client rows + flat p/m/v/base buffers on the device."""
+
+    def __init__(self, ctx, rows, n):
+        from nvflare_amd.device import TiledLayout
+
+        self.ctx = ctx
+        self.K = len(rows)
+        self.n = n
+        self.lay = TiledLayout(TILE, max(self.K, 1))
+        self.slab = ctx.alloc(self.lay.slab_elems(n) * 4)
+        self.bases = [self.slab.ptr + self.lay.slot_offset_elems(k) * 4 for k in range(self.K)]
+        for b, r in zip(self.bases, rows):
+            ctx.h2d_tiled(b, TILE * 4, self.lay.tile_stride * 4, 0, r.ctypes.data, r.nbytes)
+        self.n4 = (n + 3) // 4 * 4
+        self.bufs = {}
+
+    def buf(self, name, host=None):
+        if name not in self.bufs:
+            self.bufs[name] = self.ctx.alloc(self.n4 * 4 + 16)
+        if host is not None:
+            self.ctx.h2d_ptr(self.bufs[name].ptr, host.ctypes.data, host.nbytes)
+        return self.bufs[name].ptr
+
+    def get(self, name):
+        out = np.empty(self.n, np.float32)
+        self.ctx.d2h(out, self.bufs[name].ptr)
+        return out
+
+    def close(self):
+        self.slab.close()
+        for b in self.bufs.values():
+            b.close()
+
+
+def _epi(kind, **kw):
+    from nvflare_amd import _native as N
+
+    e = N.Epilogue()
+    e.kind = kind
+    for k, v in kw.items():
+        setattr(e, k, v)
+    return e
+
+
+@pytest.mark.parametrize("K", [5, 130])
+@pytest.mark.parametrize("op,fin,mode", [(1, 2, 1), (0, 1, 0)])
+def test_add_base_epilogue(ctx, oracle, K, op, fin, mode):
+    rng = np.random.default_rng(K)
+    n = 3 * TILE + 100
+    rows = [rng.standard_normal(n).astype(np.float32) for _ in range(K)]
+    ws = [float(1 + (37 * k) % 100) for k in range(K)]
+    base = rng.standard_normal(n).astype(np.float32)
+    dev = _Dev(ctx, rows, n)
+    try:
+        out = dev.buf("out", base)  # in place: out aliases base
+        e = _epi(2 - 1, base=out)  # FEDAVG_EPI_ADD_BASE
+        ctx.accumulate_tiled_epi(dev.bases, ws, TILE, dev.lay.tile_stride, 0, dev.n4, out, op, fin, _sum(ws), e)
+        d = oracle.fedavg_c(rows, ws, mode, fin=fin)
+        assert same_bits(dev.get("out"), oracle.epilogue_apply(d, oracle.EPI_ADD_BASE, base=base))
+    finally:
+        dev.close()
+
+
+SGD_CASES = [
+    dict(lr=1.0),
+    dict(lr=0.7, momentum=0.9),
+    dict(lr=0.05, momentum=0.6, dampening=0.1),
+    dict(lr=0.05, momentum=0.9, nesterov=1),
+    dict(lr=0.1, momentum=0.9, weight_decay=1e-2),
+    dict(lr=0.3, maximize=1, momentum=0.5),
+]
+
+
+@pytest.mark.parametrize("hp", SGD_CASES)
+def test_sgd_epilogue_multi_round(ctx, oracle, hp):
+    rng = np.random.default_rng(7)
+    n, K = 2 * TILE + 44, 6
+    p = rng.standard_normal(n).astype(np.float32)
+    buf = np.zeros(n, np.float32)
+    ws = [0.5 + k for k in range(K)]
+    dev = None
+    try:
+        for rnd in range(3):
+            rows = [(rng.standard_normal(n) * 0.1).astype(np.float32) for _ in range(K)]
+            if dev is not None:
+                for b, r in zip(dev.bases, rows):
+                    ctx.h2d_tiled(b, TILE * 4, dev.lay.tile_stride * 4, 0, r.ctypes.data, r.nbytes)
+            else:
+                dev = _Dev(ctx, rows, n)
+                dev.buf("p", p)
+                dev.buf("m", buf)
+            e = _epi(2, param=dev.buf("p"), state1=dev.buf("m"), first_step=int(rnd == 0), **hp)
+            ctx.accumulate_tiled_epi(dev.bases, ws, TILE, dev.lay.tile_stride, 0, dev.n4, None, 1, 2, _sum(ws), e)
+            d = oracle.fedavg_c(rows, ws, oracle.MODE_TORCH)
+            oracle.epilogue_apply(d, oracle.EPI_SGD, p=p, m=buf, first_step=int(rnd == 0), **hp)
+            assert same_bits(dev.get("p"), p), rnd
+            if hp.get("momentum"):
+                assert same_bits(dev.get("m"), buf), rnd
+    finally:
+        dev.close()
+
+
+ADAM_CASES = [
+    dict(lr=1e-3, beta1=0.9, beta2=0.999, eps=1e-8),
+    dict(lr=1e-2, beta1=0.8, beta2=0.99, eps=1e-6),
+    dict(lr=1e-3, beta1=0.9, beta2=0.999, eps=1e-8, weight_decay=1e-2),
+    dict(lr=1e-3, beta1=0.9, beta2=0.999, eps=1e-8, weight_decay=1e-2, decoupled_weight_decay=1),
+    dict(lr=1e-3, beta1=0.3, beta2=0.999, eps=1e-8),
+    dict(lr=1e-3, beta1=0.9, beta2=0.999, eps=1e-8, maximize=1),
+]
+
+
+@pytest.mark.parametrize("hp", ADAM_CASES)
+@pytest.mark.parametrize("K", [4, 129])
+def test_adam_epilogue_multi_round(ctx, oracle, hp, K):
+    rng = np.random.default_rng(11)
+    n = 2 * TILE + 8
+    p = rng.standard_normal(n).astype(np.float32)
+    m = np.zeros(n, np.float32)
+    v = np.zeros(n, np.float32)
+    ws = [float(1 + k % 7) for k in range(K)]
+    dev = None
+    try:
+        for step in (1, 2, 3):
+            rows = [(rng.standard_normal(n) * 0.01).astype(np.float32) for _ in range(K)]
+            if dev is None:
+                dev = _Dev(ctx, rows, n)
+                dev.buf("p", p)
+                dev.buf("m", m)
+                dev.buf("v", v)
+            else:
+                for b, r in zip(dev.bases, rows):
+                    ctx.h2d_tiled(b, TILE * 4, dev.lay.tile_stride * 4, 0, r.ctypes.data, r.nbytes)
+            e = _epi(3, param=dev.buf("p"), state1=dev.buf("m"), state2=dev.buf("v"), step=float(step), **hp)
+            out = dev.buf("d") if K > 128 else None
+            ctx.accumulate_tiled_epi(dev.bases, ws, TILE, dev.lay.tile_stride, 0, dev.n4, out, 1, 2, _sum(ws), e)
+            d = oracle.fedavg_c(rows, ws, oracle.MODE_TORCH)
+            oracle.epilogue_apply(d, oracle.EPI_ADAM, p=p, m=m, v=v, step=float(step), **hp)
+            assert same_bits(dev.get("m"), m), step
+            assert same_bits(dev.get("v"), v), step
+            assert same_bits(dev.get("p"), p), step
+    finally:
+        dev.close()
+
+
+def test_epilogue_on_precomputed_update(ctx, oracle):
+    """k_rows = 0: the epilogue applied to an update already in HBM (the generator path: H2D of the
+    aggregated diff, then the optimizer step on device)."""
+    rng = np.random.default_rng(5)
+    n = TILE + 4
+    delta = rng.standard_normal(n).astype(np.float32)
+    p = rng.standard_normal(n).astype(np.float32)
+    m = np.zeros(n, np.float32)
+    v = np.zeros(n, np.float32)
+    dev = _Dev(ctx, [], n)
+    try:
+        dp, dm, dv, dd = dev.buf("p", p), dev.buf("m", m), dev.buf("v", v), dev.buf("delta", delta)
+        e = _epi(3, param=dp, state1=dm, state2=dv, step=1.0, lr=1e-3, beta1=0.9, beta2=0.999, eps=1e-8)
+        ctx.accumulate_tiled_epi([], [], TILE, TILE, 0, dev.n4, None, 1, 0, 1.0, e, acc_in_ptr=dd)
+        oracle.epilogue_apply(delta, oracle.EPI_ADAM, p=p, m=m, v=v, step=1.0, lr=1e-3, beta1=0.9, beta2=0.999, eps=1e-8)
+        assert same_bits(dev.get("p"), p) and same_bits(dev.get("m"), m) and same_bits(dev.get("v"), v)
+    finally:
+        dev.close()
