@@ -43,6 +43,8 @@ def parse():
     ap.add_argument("--unroll", type=int, default=0, help="0 = library default (4)")
     ap.add_argument("--variant", type=int, default=0, help="cache policy bits (0 = nontemporal loads+stores)")
     ap.add_argument("--tile", type=int, default=4096, help="slab tile width (elements)")
+    ap.add_argument("--epilogue", choices=["none", "add_base", "sgd", "adam"], default="none",
+                    help="fused server update (config 5 = adam: FedOpt Adam on the aggregated deltas)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-params", type=int, default=16 * 1024 * 1024)
     ap.add_argument("--spot-check", type=int, default=4096, help="sampled outputs checked against the oracle")
@@ -193,7 +195,9 @@ def main():
 
     end = (P + 3) // 4 * 4
     slab = ctx.alloc(lay.slab_elems(P) * 4)
-    out = ctx.alloc(end * 4)
+    epi_bufs = {"none": 1, "add_base": 1, "sgd": 2, "adam": 3}[args.epilogue]  # out | p+buf | p+m+v
+    state = [ctx.alloc(end * 4) for _ in range(epi_bufs)]
+    out = state[0]
     bases = [slab.ptr + lay.slot_offset_elems(k) * 4 for k in range(K)]
     for k, base in enumerate(bases):
         ctx.fill_synthetic_f32(base, P, args.seed, k, col0, lay.tile, lay.tile_stride)
@@ -204,8 +208,35 @@ def main():
     for w in weights:
         count = w if count is None else count + w
 
+    epi = None
+    if args.epilogue != "none":
+        for j, b in enumerate(state):  # initial params (or base weights), zero optimizer state
+            if j == 0:
+                ctx.fill_synthetic_f32(b.ptr, end, args.seed + 7, 0, col0)
+            else:
+                N.call("fedavg_memset", ctx.handle, N.c_void_p(b.ptr), N.c_int(0), N.c_size_t(end * 4))
+        epi = N.Epilogue()
+        epi.kind = {"add_base": N.FEDAVG_EPI_ADD_BASE, "sgd": N.FEDAVG_EPI_SGD, "adam": N.FEDAVG_EPI_ADAM}[args.epilogue]
+        if args.epilogue == "add_base":
+            epi.base = out.ptr
+        elif args.epilogue == "sgd":
+            epi.param, epi.state1 = state[0].ptr, state[1].ptr
+            epi.lr, epi.momentum = 1.0, 0.9
+        else:
+            epi.param, epi.state1, epi.state2 = state[0].ptr, state[1].ptr, state[2].ptr
+            epi.lr, epi.beta1, epi.beta2, epi.eps = 1e-3, 0.9, 0.999, 1e-8
+        ctx.sync()
+    n_step = [0]
+
     def step():
-        ctx.accumulate_tiled(bases, weights, lay.tile, lay.tile_stride, 0, end, out.ptr, op, fin, count)
+        if epi is None:
+            ctx.accumulate_tiled(bases, weights, lay.tile, lay.tile_stride, 0, end, out.ptr, op, fin, count)
+            return
+        n_step[0] += 1
+        epi.step = float(n_step[0])
+        epi.first_step = int(n_step[0] == 1)
+        ctx.accumulate_tiled_epi(bases, weights, lay.tile, lay.tile_stride, 0, end,
+                                 out.ptr if args.epilogue == "add_base" else None, op, fin, count, epi)
 
     for _ in range(args.warmup):
         step()
@@ -225,12 +256,15 @@ def main():
 
     extra = {}
     if rank == 0 and world == 1:
+        if args.epilogue != "none":
+            args.spot_check = 0  # the spot check covers the plain aggregation output only
         extra = cpu_baseline_and_spot_check(args, ctx, K, out, weights, count, P, col0, op)
 
     if rank == 0:
         bytes_step = 4.0 * K * P * world  # aggregated client bytes per step, all ranks
         value = bytes_step * args.steps / wall / 2**30
-        alg_bytes_launch = 4.0 * K * P + 4.0 * P
+        epi_bytes = {"none": 4.0, "add_base": 8.0, "sgd": 16.0, "adam": 24.0}[args.epilogue]
+        alg_bytes_launch = 4.0 * K * P + epi_bytes * P
         traffic, traffic_src = pmc_traffic(args, K, P)
         achieved = alg_bytes_launch / (kernel_ms / 1e3) / 1e9
         line = {
@@ -247,7 +281,9 @@ def main():
             "dtype": "f32",
             "data": "synthetic: device counter-hash generator (Irwin-Hall(4) ~N(0,1)), host twin in oracle/",
             "config": {
-                "workload": f"{K} clients x {P} fp32 params per GPU, weighted FedAvg, {args.mode}-mode arithmetic",
+                "workload": f"{K} clients x {P} fp32 params per GPU, weighted FedAvg, {args.mode}-mode arithmetic"
+                            + ("" if args.epilogue == "none" else f", fused {args.epilogue} server update"),
+                "epilogue": args.epilogue,
                 "clients": K,
                 "params_per_gpu": P,
                 "mode": args.mode,
