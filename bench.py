@@ -214,7 +214,7 @@ def main():
             if j == 0:
                 ctx.fill_synthetic_f32(b.ptr, end, args.seed + 7, 0, col0)
             else:
-                N.call("fedavg_memset", ctx.handle, N.c_void_p(b.ptr), N.c_int(0), N.c_size_t(end * 4))
+                ctx.memset(b.ptr, 0, end * 4)
         epi = N.Epilogue()
         epi.kind = {"add_base": N.FEDAVG_EPI_ADD_BASE, "sgd": N.FEDAVG_EPI_SGD, "adam": N.FEDAVG_EPI_ADAM}[args.epilogue]
         if args.epilogue == "add_base":

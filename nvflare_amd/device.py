@@ -152,6 +152,10 @@ class DeviceContext:
         if nbytes:
             N.call("fedavg_d2d", self.handle, ctypes.c_void_p(dst_ptr), ctypes.c_void_p(src_ptr), ctypes.c_size_t(nbytes))
 
+    def memset(self, dst_ptr: int, value: int, nbytes: int) -> None:
+        if nbytes:
+            N.call("fedavg_memset", self.handle, ctypes.c_void_p(dst_ptr), ctypes.c_int(value), ctypes.c_size_t(nbytes))
+
     def sync(self) -> None:
         N.call("fedavg_sync", self.handle)
 
