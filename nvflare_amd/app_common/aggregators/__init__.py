@@ -1,4 +1,5 @@
 from .dxo_aggregator import DXOAggregator
+from .fedavg_model_aggregator import DeviceFedAvgModelAggregator
 from .intime_accumulate_model_aggregator import InTimeAccumulateWeightedAggregator
 from .weighted_aggregation_helper import AggregationStatsKey, WeightedAggregationHelper
 
@@ -8,6 +9,7 @@ __all__ = [
     "AccumulateWeightedAggregator",
     "AggregationStatsKey",
     "DXOAggregator",
+    "DeviceFedAvgModelAggregator",
     "InTimeAccumulateWeightedAggregator",
     "WeightedAggregationHelper",
 ]

@@ -18,6 +18,10 @@ if os.environ.get("NVFLARE_AMD_FORCE_STANDINS", "0") != "1":
         from nvflare.app_common.abstract.aggregator import Aggregator  # noqa: F401
         from nvflare.app_common.app_constant import AppConstants  # noqa: F401
         from nvflare.fuel.utils.log_utils import get_module_logger  # noqa: F401
+        from nvflare.apis.fl_constant import FLMetaKey  # noqa: F401
+        from nvflare.app_common.abstract.fl_model import FLModel, ParamsType  # noqa: F401
+        from nvflare.app_common.aggregators.model_aggregator import ModelAggregator  # noqa: F401
+        from nvflare.app_common.utils.fl_model_utils import FLModelUtils  # noqa: F401
 
         HAVE_NVFLARE = True
     except Exception:
@@ -32,6 +36,11 @@ if not HAVE_NVFLARE:
         EventType,
         FLComponent,
         FLContext,
+        FLMetaKey,
+        FLModel,
+        FLModelUtils,
+        ModelAggregator,
+        ParamsType,
         MetaKey,
         ReservedKey,
         ReturnCode,
@@ -49,6 +58,11 @@ __all__ = [
     "EventType",
     "FLComponent",
     "FLContext",
+    "FLMetaKey",
+    "FLModel",
+    "FLModelUtils",
+    "ModelAggregator",
+    "ParamsType",
     "MetaKey",
     "ReservedKey",
     "ReturnCode",

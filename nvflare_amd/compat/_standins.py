@@ -8,6 +8,10 @@ repository's tests).  They reproduce the behaviour the aggregation path relies o
 * ``FLContext.get_prop/set_prop``                                 nvflare/apis/fl_context.py:134-175
 * ``FLComponent`` logging helpers and ``handle_event``            nvflare/apis/fl_component.py:28-231
 * ``Aggregator`` ABC                                               nvflare/app_common/abstract/aggregator.py:22-58
+* ``FLModel`` / ``ParamsType``                                     nvflare/app_common/abstract/fl_model.py:22-110
+* ``ModelAggregator`` ABC and the ``FLModelUtils`` conversions it uses
+                                                  nvflare/app_common/aggregators/model_aggregator.py:26-83,
+                                                  nvflare/app_common/utils/fl_model_utils.py:46-149
 * constants: ``ReservedKey`` (fl_constant.py:69-80), ``ReturnCode`` (:26-36),
   ``AppConstants`` (app_common/app_constant.py:33-79), ``EventType.START_RUN`` (apis/event_type.py:22)
 """
@@ -61,8 +65,16 @@ class ReservedHeaderKey:
     CONTENT_TYPE = "__content_type__"
 
 
+class FLMetaKey:
+    NUM_STEPS_CURRENT_ROUND = "NUM_STEPS_CURRENT_ROUND"
+    INITIAL_METRICS = "initial_metrics"
+
+
 class AppConstants:
     CURRENT_ROUND = "current_round"
+    START_ROUND = "start_round"
+    CLIENT_UNKNOWN = "unknown"
+    METRICS_AGGREGATION_INFO = "metrics_aggregation_info"
     NUM_ROUNDS = "num_rounds"
     CONTRIBUTION_ROUND = "contribution_round"
     GLOBAL_MODEL = "global_model"
@@ -267,3 +279,128 @@ class Aggregator(FLComponent, ABC):
     @abstractmethod
     def aggregate(self, fl_ctx: FLContext) -> Shareable:
         pass
+
+
+class ParamsType(str, Enum):
+    FULL = "FULL"
+    DIFF = "DIFF"
+
+
+class FLModel:
+    """The FLModel fields the FedAvg path reads and writes (fl_model.py:38-110; no validation helpers)."""
+
+    def __init__(self, params_type=None, params=None, optimizer_params=None, metrics=None, start_round=0,
+                 current_round=None, total_rounds=None, meta=None):
+        if params_type is None:
+            if params is not None:
+                params_type = ParamsType.FULL
+        else:
+            params_type = ParamsType(params_type)
+        if params_type in (ParamsType.FULL, ParamsType.DIFF) and params is None:
+            raise ValueError(f"params must be provided when params_type is {params_type}")
+        if metrics is not None and not isinstance(metrics, dict):
+            raise TypeError(f"metrics must be dict, but got {type(metrics)}")
+        for name, val in (("start_round", start_round), ("current_round", current_round), ("total_rounds", total_rounds)):
+            if val is not None and (not isinstance(val, int) or val < 0):
+                raise ValueError(f"{name} must be a non-negative int, but got {val!r}")
+        if meta is not None and not isinstance(meta, dict):
+            raise TypeError(f"meta must be dict, but got {type(meta)}")
+        self.params_type = params_type
+        self.params = params
+        self.optimizer_params = optimizer_params
+        self.metrics = metrics
+        self.start_round = start_round
+        self.current_round = current_round
+        self.total_rounds = total_rounds
+        self.meta = {} if meta is None else meta
+
+
+_PARAMS_TYPE_TO_KIND = {ParamsType.FULL.value: DataKind.WEIGHTS, ParamsType.DIFF.value: DataKind.WEIGHT_DIFF}
+_KIND_TO_PARAMS_TYPE = {DataKind.WEIGHTS: ParamsType.FULL, DataKind.WEIGHT_DIFF: ParamsType.DIFF}
+
+
+class FLModelUtils:
+    @staticmethod
+    def to_shareable(fl_model: FLModel) -> Shareable:
+        if fl_model.params is None and fl_model.metrics is None:
+            raise ValueError("FLModel without params and metrics is NOT supported.")
+        if fl_model.params is not None:
+            if fl_model.params_type is None:
+                fl_model.params_type = ParamsType.FULL
+            kind = _PARAMS_TYPE_TO_KIND.get(ParamsType(fl_model.params_type).value)
+            meta = {} if fl_model.metrics is None else {FLMetaKey.INITIAL_METRICS: fl_model.metrics}
+            dxo = DXO(kind, data=fl_model.params, meta=meta)
+        else:
+            dxo = DXO(DataKind.METRICS, data=fl_model.metrics, meta={})
+        dxo.meta.update(fl_model.meta or {})
+        s = dxo.to_shareable()
+        for key, val in ((AppConstants.START_ROUND, fl_model.start_round), (AppConstants.CURRENT_ROUND, fl_model.current_round),
+                         (AppConstants.NUM_ROUNDS, fl_model.total_rounds)):
+            if val is not None:
+                s.set_header(key, val)
+        return s
+
+    @staticmethod
+    def from_shareable(shareable: Shareable, fl_ctx: Optional[FLContext] = None) -> FLModel:
+        dxo = from_shareable(shareable)
+        meta = dict(dxo.meta)
+        metrics = params = params_type = None
+        if dxo.data_kind == DataKind.METRICS:
+            metrics = dxo.data
+        else:
+            params = dxo.data
+            params_type = _KIND_TO_PARAMS_TYPE.get(dxo.data_kind, ParamsType.FULL)
+            metrics = meta.get(FLMetaKey.INITIAL_METRICS)
+        return FLModel(params_type=params_type, params=params, metrics=metrics,
+                       start_round=shareable.get_header(AppConstants.START_ROUND, None),
+                       current_round=shareable.get_header(AppConstants.CURRENT_ROUND, None),
+                       total_rounds=shareable.get_header(AppConstants.NUM_ROUNDS, None), meta=meta)
+
+
+class ModelAggregator(Aggregator):
+    """FLModel-level aggregator ABC (model_aggregator.py:26-83)."""
+
+    def __init__(self):
+        super().__init__()
+        self.fl_ctx = None
+
+    def handle_event(self, event_type: str, fl_ctx: FLContext):
+        if event_type == EventType.START_RUN:
+            self.fl_ctx = fl_ctx
+
+    @abstractmethod
+    def accept_model(self, model: FLModel):
+        raise NotImplementedError
+
+    @abstractmethod
+    def aggregate_model(self) -> FLModel:
+        raise NotImplementedError
+
+    @abstractmethod
+    def reset_stats(self):
+        raise NotImplementedError
+
+    def accept(self, shareable: Shareable, fl_ctx: FLContext) -> bool:
+        self.fl_ctx = fl_ctx
+        self.accept_model(FLModelUtils.from_shareable(shareable, fl_ctx))
+        return True
+
+    def aggregate(self, fl_ctx: FLContext) -> Shareable:
+        self.fl_ctx = fl_ctx
+        return FLModelUtils.to_shareable(self.aggregate_model())
+
+    def reset(self, fl_ctx: FLContext):
+        self.fl_ctx = fl_ctx
+        self.reset_stats()
+
+    def info(self, message: str):
+        self.log_info(self.fl_ctx, message)
+
+    def warning(self, message: str):
+        self.log_warning(self.fl_ctx, message)
+
+    def error(self, message: str):
+        self.log_error(self.fl_ctx, message)
+
+    def exception(self, message: str):
+        self.log_exception(self.fl_ctx, message)

@@ -28,6 +28,7 @@ numpy -> ``FEDAVG_OP_NUMPY`` + ``FEDAVG_FIN_SCALE``; torch -> ``FEDAVG_OP_TORCH`
 from __future__ import annotations
 
 import os
+import math
 import threading
 from typing import Any, Dict, List, Optional, Tuple
 
@@ -149,6 +150,9 @@ class _Staged:
         self.weight = weight
         self.slot = slot
         self.buf = buf
+
+
+_FLT_MAX = float(np.finfo(np.float32).max)
 
 
 class _KeyState:
@@ -274,6 +278,20 @@ class DeviceFedAvg:
             slot.slab.free.append(slot.index)
 
     # ------------------------------------------------------------------ layout
+    def _check_torch_alpha(self, items, weight, weighted: bool) -> None:
+        """torch's ``T.add_(v, alpha=w)`` (weighted_aggregation_helper.py:205-207) refuses a finite alpha
+        outside the fp32 range for an fp32 total.  Raise the same RuntimeError, before anything of this
+        contribution is staged (the reference fails part-way through the keys instead)."""
+        if not weighted:
+            return
+        w = float(weight)
+        if not (math.isfinite(w) and abs(w) > _FLT_MAX):
+            return
+        for k, _ in items:
+            st = self.keys.get(k)
+            if st is not None and st.container == "torch" and st.acc_np == np.dtype(np.float32):
+                raise RuntimeError("value cannot be converted to type float without overflow")
+
     def _register_key(self, name: str, v, weight, weighted: bool) -> _KeyState:
         container, in_np, acc_np, op, fin = _resolve_types(v, weight, weighted)
         st = self.keys.get(name)
@@ -338,6 +356,7 @@ class DeviceFedAvg:
     def add(self, items: List[Tuple[str, Any]], weight, weighted: bool) -> None:
         """Stage one contribution's device-path arrays (already filtered by exclude_vars)."""
         with self.lock, self.ctx.lock:
+            self._check_torch_alpha(items, weight, weighted)
             states = [(self._register_key(k, v, weight, weighted), v) for k, v in items]
             for _, v in states:
                 self._check_device(v)

@@ -12,10 +12,13 @@ pulled in by ``nvflare/__init__.py:21-23``); this is not a permission denial.  T
 
 Reference code exercised:
   nvflare/app_common/aggregators/weighted_aggregation_helper.py:153-240  (helper cases)
+  nvflare/app_common/workflows/base_fedavg.py:93-230  (``--set fedavg``: aggregate_fn cases)
+  nvflare/app_common/workflows/fedavg.py:268-366      (``--set fedavg``: built-in in-time FedAvg cases)
   nvflare/app_common/aggregators/intime_accumulate_model_aggregator.py   (intime cases)
   nvflare/app_common/aggregators/dxo_aggregator.py:71-191
 
-Usage:  python tests/golden/make_golden.py [--ref /root/reference]
+Usage:  python tests/golden/make_golden.py [--ref /root/reference] [--set helper|fedavg]
+        (helper -> helper_cases.{npz,json}; fedavg -> fedavg_cases.{npz,json})
 """
 
 from __future__ import annotations
@@ -168,12 +171,112 @@ def run_intime_case(store, cases, name, container, clients, expected_data_kind, 
     )
 
 
+def _jsonable_steps(v):
+    """NUM_STEPS values are recorded with a type tag so the JSON round trip keeps them exact."""
+    if v is None:
+        return {"t": "none"}
+    if isinstance(v, bool):
+        return {"t": "bool", "v": v}
+    if isinstance(v, int):
+        return {"t": "int", "v": v}
+    if isinstance(v, float):
+        return {"t": "float", "v": repr(v)}
+    return {"t": "str", "v": str(v)}
+
+
+def _fl_models(store, container, clients):
+    """clients: [(name, num_steps, {key: arr}, metrics)] -> (FLModels, json record)"""
+    from nvflare.apis.fl_constant import FLMetaKey
+    from nvflare.app_common.abstract.fl_model import FLModel
+
+    models, rec = [], []
+    for name, steps, data, metrics in clients:
+        meta = {"client_name": name}
+        if steps is not None:
+            meta[FLMetaKey.NUM_STEPS_CURRENT_ROUND] = steps
+        models.append(FLModel(params={k: to_container(v, container) for k, v in data.items()}, metrics=metrics,
+                              current_round=3, meta=meta))
+        rec.append({"name": name, "num_steps": _jsonable_steps(steps), "data": {k: store.put(v, "in") for k, v in data.items()},
+                    "metrics": metrics})
+    return models, rec
+
+
+def _result_record(store, model):
+    return {
+        "params": {k: store.put(v, "out") for k, v in model.params.items()},
+        "params_dtype": {k: (str(v.dtype).replace("torch.", "") if isinstance(v, torch.Tensor) else str(np.asarray(v).dtype))
+                         for k, v in model.params.items()},
+        "params_type": str(model.params_type.value if model.params_type is not None else None),
+        "metrics": model.metrics,
+        "meta": {k: v for k, v in model.meta.items()},
+        "current_round": model.current_round,
+    }
+
+
+def run_fedavg_fn_case(store, cases, name, container, clients):
+    from nvflare.app_common.workflows.base_fedavg import BaseFedAvg
+
+    models, rec = _fl_models(store, container, clients)
+    out = BaseFedAvg.aggregate_fn(models)
+    cases.append({"kind": "aggregate_fn", "name": name, "container": container, "clients": rec, "expected": _result_record(store, out)})
+
+
+def run_fedavg_intime_case(store, cases, name, container, clients, aggregation_weights):
+    """FedAvg's built-in in-time path: _aggregate_one_result per client, then _get_aggregated_result."""
+    from nvflare.app_common.aggregators.weighted_aggregation_helper import WeightedAggregationHelper
+    from nvflare.app_common.workflows.fedavg import FedAvg
+
+    wf = FedAvg(num_clients=len(clients), num_rounds=1, aggregation_weights=aggregation_weights)
+    wf.info = wf.warning = lambda *a, **k: None
+    wf.fl_ctx = None
+    wf.current_round = 3
+    wf._aggr_helper = WeightedAggregationHelper()
+    wf._aggr_metrics_helper = WeightedAggregationHelper()
+    wf._expected_count = len(clients)
+    models, rec = _fl_models(store, container, clients)
+    accepted = [bool(wf._aggregate_one_result(m)) for m in models]
+    out = wf._get_aggregated_result()
+    cases.append({"kind": "fedavg_intime", "name": name, "container": container, "aggregation_weights": aggregation_weights,
+                  "clients": rec, "accepted": accepted, "expected": _result_record(store, out)})
+
+
+def main_fedavg():
+    rng = np.random.default_rng(20261016)
+    store = Store()
+    cases = []
+    odd_steps = [3, None, True, -2, float("nan"), "7", 2.5, "abc", 0, float("inf"), 1e300, False]
+    for container in ("numpy", "torch"):
+        # torch's add_(alpha=1e300) raises for an fp32 total (tests/test_gpu_fedavg_path.py checks that we
+        # raise too); the torch cases use the largest finite-in-fp32 weight instead
+        steps = odd_steps if container == "numpy" else [3e38 if s == 1e300 else s for s in odd_steps]
+        K = len(steps)
+        clients = [(f"site-{i+1}", steps[i], {"w": rng.standard_normal(1031).astype(np.float32),
+                                                  "b": rng.standard_normal(7).astype(np.float32)},
+                    {"acc": float(rng.random()), "flag": bool(i % 2), "info": {"x": 1}, "tag": "s"}) for i in range(K)]
+        run_fedavg_fn_case(store, cases, f"{container}_fn_weight_rule", container, clients)
+        # a client without metrics disables metric aggregation; one unnamed client
+        clients2 = [(f"site-{i+1}" if i else "", int(rng.integers(1, 60)), {"layer.weight": rng.standard_normal((17, 5)).astype(np.float32)},
+                     None if i == 2 else {"loss": float(rng.random())}) for i in range(5)]
+        run_fedavg_fn_case(store, cases, f"{container}_fn_no_metrics", container, clients2)
+        aw = {f"site-{i+1}": float(rng.random()) * 3 for i in range(0, K, 2)}
+        run_fedavg_intime_case(store, cases, f"{container}_intime_weights", container, clients, aw)
+        run_fedavg_intime_case(store, cases, f"{container}_intime_plain", container, clients2, None)
+    np.savez_compressed(os.path.join(HERE, "fedavg_cases.npz"), **store.arrays)
+    with open(os.path.join(HERE, "fedavg_cases.json"), "w") as f:
+        json.dump({"generator": "tests/golden/make_golden.py --set fedavg", "reference": "NVFlare (/root/reference, ~2.9.0-dev)",
+                   "numpy": np.__version__, "torch": torch.__version__, "cases": cases}, f, indent=1, default=str)
+    print(f"wrote {len(cases)} fedavg cases, {len(store.arrays)} arrays")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ref", default="/root/reference")
+    ap.add_argument("--set", choices=["helper", "fedavg"], default="helper")
     args = ap.parse_args()
     install_shim(args.ref)
     torch.set_num_threads(8)
+    if args.set == "fedavg":
+        return main_fedavg()
 
     rng = np.random.default_rng(20261015)
     random.seed(20261015)

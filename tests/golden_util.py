@@ -61,3 +61,54 @@ def same_bits(a: np.ndarray, b: np.ndarray) -> bool:
     ua = a[~an].view(np.uint8)
     ub = b[~bn].view(np.uint8)
     return np.array_equal(ua, ub)
+
+
+def load_fedavg_golden():
+    """FedAvg-workflow cases (make_golden.py --set fedavg): BaseFedAvg.aggregate_fn and FedAvg's in-time path."""
+    if "f" not in _cache:
+        with open(os.path.join(GOLDEN_DIR, "fedavg_cases.json")) as f:
+            meta = json.load(f)
+        arrays = dict(np.load(os.path.join(GOLDEN_DIR, "fedavg_cases.npz"), allow_pickle=False))
+        _cache["f"] = (meta, arrays)
+    return _cache["f"]
+
+
+def decode_steps(rec):
+    t = rec["t"]
+    if t == "none":
+        return None
+    if t == "float":
+        return float(rec["v"])
+    return rec["v"]
+
+
+def fl_models_from_case(case, arrays, FLModel, container):
+    import torch
+
+    models = []
+    for c in case["clients"]:
+        meta = {"client_name": c["name"]}
+        steps = c["num_steps"]
+        if steps["t"] != "none":
+            meta["NUM_STEPS_CURRENT_ROUND"] = decode_steps(steps)
+        params = {}
+        for k, name in c["data"].items():
+            a = np.array(arrays[name], copy=True)
+            params[k] = torch.from_numpy(a) if container == "torch" else a
+        models.append(FLModel(params=params, metrics=c["metrics"], current_round=3, meta=meta))
+    return models
+
+
+def same_metrics(a, b) -> bool:
+    """Exact equality of metric dicts (python floats; NaN == NaN)."""
+    import math
+
+    if a is None or b is None:
+        return a is None and b is None
+    if set(a) != set(b):
+        return False
+    for k in a:
+        x, y = float(a[k]), float(b[k])
+        if not (x == y or (math.isnan(x) and math.isnan(y))):
+            return False
+    return True
