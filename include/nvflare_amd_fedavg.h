@@ -154,7 +154,8 @@ int fedavg_accumulate_tiled(fedavg_ctx* ctx, const void* const* bases, const dou
 
 /* fedavg_accumulate_tiled with a server-optimizer epilogue applied per element to d = fin(acc) in the
  * same launch (rows a9/a10): ADD_BASE writes base + d to out; SGD/ADAM update epi->param/state in place
- * and also store d to out when out != NULL.  More than 128 clients need out (scratch for the chain). */
+ * and also store d to out when out != NULL.  More than 128 clients are chained through a partial sum
+ * kept in out, or in a stream-ordered scratch when out is NULL or aliases an epilogue operand. */
 int fedavg_accumulate_tiled_epi(fedavg_ctx* ctx, const void* const* bases, const double* weights, int k_rows,
                                 size_t tile_elems, size_t tile_stride, size_t begin, size_t end,
                                 const void* acc_in, void* out, int op, int fin, double count,

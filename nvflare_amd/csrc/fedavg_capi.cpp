@@ -719,7 +719,6 @@ int fedavg_accumulate_tiled_epi(fedavg_ctx* ctx, const void* const* bases, const
         if (epi->kind == FEDAVG_EPI_ADAM && (!epi->param || !epi->state1 || !epi->state2))
             throw Error("ADAM needs param, state1 (exp_avg), state2 (exp_avg_sq)");
         if (epi->kind == FEDAVG_EPI_ADAM && epi->step < 1.0) throw Error("ADAM step must be >= 1");
-        if (k_rows > fedavg::kMaxRowsPerLaunch && !out) throw Error("more than 128 clients need out as scratch");
         for (const void* p : {(const void*)epi->param, (const void*)epi->state1, (const void*)epi->state2,
                               (const void*)epi->base, (const void*)out, acc_in})
             if (misaligned(p)) throw Error("epilogue/out/acc_in pointers must be 16-byte aligned");
@@ -728,13 +727,24 @@ int fedavg_accumulate_tiled_epi(fedavg_ctx* ctx, const void* const* bases, const
         ctx->activate();
         hipStream_t s = ctx->compute();
         TimingScope ts(ctx, s);
-        // leading chunks (beyond 128 clients) accumulate into out; the last chunk runs the epilogue
+        // Leading chunks (beyond 128 clients) accumulate a partial sum; the last chunk runs the epilogue.
+        // The partial sum goes to out unless out is absent or aliases an epilogue operand (in-place
+        // WEIGHT_DIFF apply: out == base) -- then to a stream-ordered scratch covering [begin, end).
         int head = k_rows > fedavg::kMaxRowsPerLaunch ? (k_rows - 1) / fedavg::kMaxRowsPerLaunch * fedavg::kMaxRowsPerLaunch : 0;
         const float* cur_in = static_cast<const float*>(acc_in);
+        void* scratch = nullptr;
         if (head > 0) {
+            float* partial = static_cast<float*>(out);
+            const void* operands[] = {epi->base, epi->param, epi->state1, epi->state2};
+            bool alias = !out;
+            for (const void* q : operands) alias = alias || (q && q == out);
+            if (alias) {
+                HIP_CHECK(hipMallocAsync(&scratch, (end - begin) * sizeof(float), s));
+                partial = static_cast<float*>(scratch) - begin;  // indexed by global element, touched on [begin, end)
+            }
             run_tiles(ctx, bases, weights, head, (int64_t)tile_elems, (int64_t)tile_stride, (int64_t)begin,
-                      (int64_t)end, cur_in, static_cast<float*>(out), op, FEDAVG_FIN_NONE, count, s);
-            cur_in = static_cast<const float*>(out);
+                      (int64_t)end, cur_in, partial, op, FEDAVG_FIN_NONE, count, s);
+            cur_in = partial;
         }
         fedavg::TileLaunch L;
         memset(&L.tab, 0, sizeof(L.tab));
@@ -756,7 +766,9 @@ int fedavg_accumulate_tiled_epi(fedavg_ctx* ctx, const void* const* bases, const
         L.fin_val = (float)fin_scalar(fin, count);
         L.acc_in = cur_in;
         L.out = static_cast<float*>(out);
-        HIP_CHECK(fedavg::launch_tiles_epi_f32x4(L, make_epi(*epi), s));
+        const hipError_t rc = fedavg::launch_tiles_epi_f32x4(L, make_epi(*epi), s);
+        if (scratch) HIP_CHECK(hipFreeAsync(scratch, s));
+        HIP_CHECK(rc);
         ts.done();
     });
 }
