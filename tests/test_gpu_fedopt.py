@@ -128,6 +128,26 @@ def test_sgd_epilogue_multi_round(ctx, oracle, hp):
         dev.close()
 
 
+def test_sgd_epilogue_many_clients_no_out(ctx, oracle):
+    """K > 128 with out=NULL: the chain's partial sum lives in a stream-ordered scratch."""
+    rng = np.random.default_rng(11)
+    n, K = TILE + 36, 131
+    rows = [rng.standard_normal(n).astype(np.float32) for _ in range(K)]
+    ws = [float(1 + (37 * k) % 100) for k in range(K)]
+    p = rng.standard_normal(n).astype(np.float32)
+    m = rng.standard_normal(n).astype(np.float32)
+    dev = _Dev(ctx, rows, n)
+    try:
+        e = _epi(2, param=dev.buf("p", p), state1=dev.buf("m", m), lr=0.5, momentum=0.9)
+        ctx.accumulate_tiled_epi(dev.bases, ws, TILE, dev.lay.tile_stride, 0, dev.n4, None, 1, 2, _sum(ws), e)
+        d = oracle.fedavg_c(rows, ws, oracle.MODE_TORCH)
+        oracle.epilogue_apply(d, oracle.EPI_SGD, p=p, m=m, lr=0.5, momentum=0.9)
+        assert same_bits(dev.get("p"), p)
+        assert same_bits(dev.get("m"), m)
+    finally:
+        dev.close()
+
+
 ADAM_CASES = [
     dict(lr=1e-3, beta1=0.9, beta2=0.999, eps=1e-8),
     dict(lr=1e-2, beta1=0.8, beta2=0.99, eps=1e-6),
