@@ -165,9 +165,12 @@ def pmc_traffic(args, K, P):
             rec = json.load(f)
     except (OSError, ValueError):
         return None, None
-    cfg = rec.get("config", {})
-    if (cfg.get("clients"), cfg.get("params"), cfg.get("tile"), cfg.get("mode")) == (K, P, args.tile, args.mode):
-        return float(rec["bytes_per_launch"]), "profiles/pmc_traffic.json"
+    want = {"clients": K, "params": P, "tile": args.tile, "mode": args.mode, "epilogue": args.epilogue}
+    for r in rec.get("records", []):
+        cfg = dict(r.get("config", {}))
+        cfg.setdefault("epilogue", "none")
+        if all(cfg.get(k) == v for k, v in want.items()):
+            return float(r["bytes_per_launch"]), "profiles/pmc_traffic.json"
     return None, None
 
 

@@ -171,16 +171,37 @@ __device__ __forceinline__ float lerp_torch(float s, float e, float w, float w_m
     return fabsf(w) < 0.5f ? __builtin_fmaf(w, d, s) : __builtin_fmaf(w_m1, d, e);
 }
 
+// Epilogue operands of one f32x4 column group, loaded at the START of the tile so their HBM latency
+// hides behind the client stream instead of stalling the wave after the last client.
+struct EpiIn {
+    f32x4 a, b, c;  // ADD_BASE: base | SGD: p, momentum buffer | ADAM: p, exp_avg, exp_avg_sq
+};
+
 template <int EPI>
-__device__ __forceinline__ void epilogue4(const EpiParams& E, const int64_t i, const f32x4 d, f32x4* out) {
+__device__ __forceinline__ EpiIn epi_load(const EpiParams& E, const int64_t i) {
+    EpiIn in;
+    if constexpr (EPI == FEDAVG_EPI_ADD_BASE) {
+        in.a = load4<true>(reinterpret_cast<const f32x4*>(E.base) + i);
+    } else if constexpr (EPI == FEDAVG_EPI_SGD) {
+        in.a = load4<true>(reinterpret_cast<const f32x4*>(E.param) + i);
+        if (E.has_momentum && !E.first_step) in.b = load4<true>(reinterpret_cast<const f32x4*>(E.state1) + i);
+    } else {
+        in.a = load4<true>(reinterpret_cast<const f32x4*>(E.param) + i);
+        in.b = load4<true>(reinterpret_cast<const f32x4*>(E.state1) + i);
+        in.c = load4<true>(reinterpret_cast<const f32x4*>(E.state2) + i);
+    }
+    return in;
+}
+
+template <int EPI>
+__device__ __forceinline__ void epilogue4(const EpiParams& E, const int64_t i, const f32x4 d, const EpiIn& in,
+                                          f32x4* out) {
     f32x4* p4 = reinterpret_cast<f32x4*>(E.param) + i;
     if constexpr (EPI == FEDAVG_EPI_ADD_BASE) {
-        const f32x4 b = load4<true>(reinterpret_cast<const f32x4*>(E.base) + i);
-        store4<true>(out + i, b + d);
+        store4<true>(out + i, in.a + d);
     } else if constexpr (EPI == FEDAVG_EPI_SGD) {
-        f32x4 p = load4<true>(p4);
-        f32x4 buf;
-        if (E.has_momentum && !E.first_step) buf = load4<true>(reinterpret_cast<const f32x4*>(E.state1) + i);
+        f32x4 p = in.a;
+        f32x4 buf = in.b;
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
             float g = E.maximize ? d[c] : -d[c];
@@ -195,9 +216,9 @@ __device__ __forceinline__ void epilogue4(const EpiParams& E, const int64_t i, c
         store4<true>(p4, p);
         if (E.has_momentum) store4<true>(reinterpret_cast<f32x4*>(E.state1) + i, buf);
     } else {  // EPI_ADAM
-        f32x4 p = load4<true>(p4);
-        f32x4 m = load4<true>(reinterpret_cast<const f32x4*>(E.state1) + i);
-        f32x4 v = load4<true>(reinterpret_cast<const f32x4*>(E.state2) + i);
+        f32x4 p = in.a;
+        f32x4 m = in.b;
+        f32x4 v = in.c;
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
             float g = E.maximize ? d[c] : -d[c];
@@ -232,6 +253,12 @@ __global__ void __launch_bounds__(kBlock) fedavg_tiles_epi_f32x4(const RowTableF
     for (int64_t t = b4 / T4 + blockIdx.x; t <= t_last; t += gridDim.x) {
         const int64_t off = t * tstride4 + threadIdx.x;
         const int64_t col = t * T4 + threadIdx.x;
+        EpiIn pre[CPL];
+#pragma unroll
+        for (int c = 0; c < CPL; ++c) {
+            const int64_t i = col + c * kBlock;
+            if (i >= b4 && i < e4) pre[c] = epi_load<EPI>(E, i);
+        }
         f32x4 acc[CPL];
         int k = 0;
         if constexpr (ACC_IN) {
@@ -270,7 +297,7 @@ __global__ void __launch_bounds__(kBlock) fedavg_tiles_epi_f32x4(const RowTableF
             if (i >= b4 && i < e4) {
                 const f32x4 d = fin4<FIN>(acc[c], fin_val);
                 if (out != nullptr && EPI != FEDAVG_EPI_ADD_BASE) store4<true>(out + i, d);
-                epilogue4<EPI>(E, i, d, out);
+                epilogue4<EPI>(E, i, d, pre[c], out);
             }
         }
     }
