@@ -756,7 +756,7 @@ int fedavg_accumulate_tiled_epi(fedavg_ctx* ctx, const void* const* bases, const
         L.op = op;
         L.fin = fin;
         L.unroll = fedavg::kDefaultUnroll;
-        L.variant = 0;
+        L.variant = ctx->variant & fedavg::kVariantEpiLateLoads;
         L.tile4 = (int64_t)tile_elems / 4;
         L.tstride4 = (int64_t)tile_stride / 4;
         L.b4 = (int64_t)begin / 4;
@@ -825,7 +825,7 @@ int fedavg_set_launch(fedavg_ctx* ctx, int blocks_per_cu, int unroll) {
 int fedavg_set_variant(fedavg_ctx* ctx, int variant) {
     return guarded([&] {
         if (!ctx) throw Error("ctx is NULL");
-        if (variant < 0 || variant > 3) throw Error("variant must be 0..3");
+        if (variant < 0 || variant > 7) throw Error("variant must be 0..7");
         ctx->variant = variant;
     });
 }

@@ -241,7 +241,7 @@ __device__ __forceinline__ void epilogue4(const EpiParams& E, const int64_t i, c
     }
 }
 
-template <int OP, int FIN, bool ACC_IN, int EPI>
+template <int OP, int FIN, bool ACC_IN, int EPI, bool PRE>
 __global__ void __launch_bounds__(kBlock) fedavg_tiles_epi_f32x4(const RowTableF32 tab, const int K,
                                                                   const int64_t tstride4, const f32x4* acc_in,
                                                                   f32x4* out, const int64_t b4, const int64_t e4,
@@ -254,10 +254,12 @@ __global__ void __launch_bounds__(kBlock) fedavg_tiles_epi_f32x4(const RowTableF
         const int64_t off = t * tstride4 + threadIdx.x;
         const int64_t col = t * T4 + threadIdx.x;
         EpiIn pre[CPL];
+        if constexpr (PRE) {
 #pragma unroll
-        for (int c = 0; c < CPL; ++c) {
-            const int64_t i = col + c * kBlock;
-            if (i >= b4 && i < e4) pre[c] = epi_load<EPI>(E, i);
+            for (int c = 0; c < CPL; ++c) {
+                const int64_t i = col + c * kBlock;
+                if (i >= b4 && i < e4) pre[c] = epi_load<EPI>(E, i);
+            }
         }
         f32x4 acc[CPL];
         int k = 0;
@@ -297,6 +299,7 @@ __global__ void __launch_bounds__(kBlock) fedavg_tiles_epi_f32x4(const RowTableF
             if (i >= b4 && i < e4) {
                 const f32x4 d = fin4<FIN>(acc[c], fin_val);
                 if (out != nullptr && EPI != FEDAVG_EPI_ADD_BASE) store4<true>(out + i, d);
+                if constexpr (!PRE) pre[c] = epi_load<EPI>(E, i);
                 epilogue4<EPI>(E, i, d, pre[c], out);
             }
         }
@@ -438,27 +441,33 @@ hipError_t launch_tiles_f32x4(const TileLaunch& L, hipStream_t s) {
     }
 }
 
-template <int OP, int FIN, bool ACC_IN>
-static hipError_t launch_epi_a(const TileLaunch& L, const EpiParams& E, hipStream_t s) {
+template <int OP, int FIN, bool ACC_IN, bool PRE>
+static hipError_t launch_epi_p(const TileLaunch& L, const EpiParams& E, hipStream_t s) {
     const f32x4* ai = reinterpret_cast<const f32x4*>(L.acc_in);
     f32x4* o = reinterpret_cast<f32x4*>(L.out);
     switch (E.kind) {
         case FEDAVG_EPI_ADD_BASE:
-            hipLaunchKernelGGL((fedavg_tiles_epi_f32x4<OP, FIN, ACC_IN, FEDAVG_EPI_ADD_BASE>), dim3(L.grid),
+            hipLaunchKernelGGL((fedavg_tiles_epi_f32x4<OP, FIN, ACC_IN, FEDAVG_EPI_ADD_BASE, PRE>), dim3(L.grid),
                                dim3(kBlock), 0, s, L.tab, L.k, L.tstride4, ai, o, L.b4, L.e4, L.fin_val, E);
             break;
         case FEDAVG_EPI_SGD:
-            hipLaunchKernelGGL((fedavg_tiles_epi_f32x4<OP, FIN, ACC_IN, FEDAVG_EPI_SGD>), dim3(L.grid), dim3(kBlock),
+            hipLaunchKernelGGL((fedavg_tiles_epi_f32x4<OP, FIN, ACC_IN, FEDAVG_EPI_SGD, PRE>), dim3(L.grid), dim3(kBlock),
                                0, s, L.tab, L.k, L.tstride4, ai, o, L.b4, L.e4, L.fin_val, E);
             break;
         case FEDAVG_EPI_ADAM:
-            hipLaunchKernelGGL((fedavg_tiles_epi_f32x4<OP, FIN, ACC_IN, FEDAVG_EPI_ADAM>), dim3(L.grid), dim3(kBlock),
+            hipLaunchKernelGGL((fedavg_tiles_epi_f32x4<OP, FIN, ACC_IN, FEDAVG_EPI_ADAM, PRE>), dim3(L.grid), dim3(kBlock),
                                0, s, L.tab, L.k, L.tstride4, ai, o, L.b4, L.e4, L.fin_val, E);
             break;
         default:
             return hipErrorInvalidValue;
     }
     return hipGetLastError();
+}
+
+template <int OP, int FIN, bool ACC_IN>
+static hipError_t launch_epi_a(const TileLaunch& L, const EpiParams& E, hipStream_t s) {
+    return (L.variant & kVariantEpiLateLoads) ? launch_epi_p<OP, FIN, ACC_IN, false>(L, E, s)
+                                              : launch_epi_p<OP, FIN, ACC_IN, true>(L, E, s);
 }
 
 template <int OP, int FIN>
