@@ -1,0 +1,384 @@
+"""Drop-in ``PTFedOptModelShareableGenerator`` with the server optimizer step on the MI355X (row a10 / f1).
+
+Reference: ``nvflare/app_opt/pt/fedopt.py:29-270``.  Same constructor, START_RUN set-up (model from the
+engine or a module, optimizer / lr scheduler built from ``{'path'|'class_path', 'args'}``), the same
+``system_panic`` conditions, WEIGHT_DIFF-only input, ``-1.0 * diff`` as the gradient of every named
+parameter present in the diff, FedAvg (``base + diff``) for the other keys, and the same output
+representation (torch tensors if the global model holds tensors, numpy otherwise).
+
+What differs is where the step runs.  The reference sets ``param.grad`` and calls
+``optimizer.step()``; here the model's parameters are re-pointed into ONE flat fp32 buffer in HBM and
+``torch.optim.SGD`` / ``Adam`` / ``AdamW`` steps are executed by the HIP fused-epilogue kernel
+(``fedavg_accumulate_tiled_epi`` with the aggregated difference as ``acc_in``), with torch's
+single-tensor rounding sequence (``tests/test_fedopt_oracle.py``).  The torch optimizer object is kept
+for its ``param_groups`` (read every step, so lr schedulers work unchanged) and its ``state`` is filled
+with views of the device buffers (``momentum_buffer`` / ``exp_avg`` / ``exp_avg_sq`` / ``step``), so
+``optimizer.state_dict()`` checkpoints as before.  Other optimizers, and amsgrad, raise: there is no
+CPU fallback.
+
+``device`` names the HIP device ("cuda:N" or N); "cpu" (and None) select $NVFLARE_AMD_DEVICE / 0 --
+the product has no CPU path.
+"""
+
+from __future__ import annotations
+
+import importlib
+import os
+import time
+import warnings
+from typing import Dict, List, Optional, Tuple
+
+import numpy as np
+import torch
+
+from ... import _native as N
+from ...app_common.shareablegenerators.full_model_shareable_generator import (
+    FullModelShareableGenerator,
+    apply_weight_diff,
+)
+from ...compat import (
+    AppConstants,
+    DataKind,
+    EventType,
+    FLContext,
+    Learnable,
+    MetaKey,
+    ModelLearnableKey,
+    Shareable,
+    from_shareable,
+    make_model_learnable,
+)
+from ...device import DeviceContext
+
+_ALIGN = 64  # elements per parameter slot boundary (256 B), as in the aggregation engine
+
+
+def hip_device_index(device) -> int:
+    """HIP device index for a reference-style ``device`` argument."""
+    if isinstance(device, int):
+        return device
+    if device is not None:
+        d = torch.device(device)
+        if d.type == "cuda":
+            return 0 if d.index is None else d.index
+    return int(os.environ.get("NVFLARE_AMD_DEVICE", "0"))
+
+
+def build_component_from_args(args: dict):
+    """``{'path'|'class_path', 'args'}`` -> instance (what ``engine.build_component`` does for these)."""
+    path = args.get("path") or args.get("class_path") or args.get("name")
+    if not path:
+        raise ValueError(f"component args need 'path' or 'class_path': {args}")
+    mod, _, cls = path.rpartition(".")
+    return getattr(importlib.import_module(mod), cls)(**args.get("args", {}))
+
+
+class _Slot:
+    __slots__ = ("name", "param", "offset", "n", "step", "has_momentum_buffer")
+
+    def __init__(self, name, param, offset, n):
+        self.name, self.param, self.offset, self.n = name, param, offset, n
+        self.step = 0.0
+        self.has_momentum_buffer = False
+
+
+class DeviceServerOptimizer:
+    """Flat HBM image of a model's parameters plus optimizer state, stepped by the HIP epilogue kernel.
+
+    Layout: parameter ``j`` occupies ``[offset_j, offset_j + n_j)`` of the flat buffers ``p`` (the live
+    parameter storage: ``param.data`` is a view of it), ``m`` (momentum buffer / exp_avg), ``v``
+    (exp_avg_sq) and ``g`` (staged aggregated difference), offsets 256-byte aligned."""
+
+    def __init__(self, model: torch.nn.Module, optimizer: torch.optim.Optimizer, device: int):
+        self.hip_device = device
+        self.torch_device = torch.device("cuda", device)
+        self.ctx = DeviceContext.get(device)
+        self.model = model
+        self.optimizer = optimizer
+        self.kind = self._kind(optimizer)
+        self._bind()
+
+    @staticmethod
+    def _kind(optimizer) -> int:
+        if isinstance(optimizer, torch.optim.SGD):
+            return N.FEDAVG_EPI_SGD
+        if isinstance(optimizer, torch.optim.Adam):  # AdamW subclasses Adam (decoupled_weight_decay=True)
+            for g in optimizer.param_groups:
+                if g.get("amsgrad"):
+                    raise NotImplementedError("nvflare_amd: Adam(amsgrad=True) has no device kernel")
+            return N.FEDAVG_EPI_ADAM
+        raise NotImplementedError(
+            f"nvflare_amd: server optimizer {type(optimizer).__module__}.{type(optimizer).__name__} has no device "
+            "kernel (supported: torch.optim.SGD, Adam, AdamW)")
+
+    def _group_of(self) -> Dict[int, dict]:
+        return {id(p): g for g in self.optimizer.param_groups for p in g["params"]}
+
+    def _bind(self) -> None:
+        named = list(self.model.named_parameters())
+        groups = self._group_of()
+        slots, off = [], 0
+        for name, p in named:
+            if p.dtype != torch.float32:
+                raise TypeError(f"nvflare_amd: parameter {name!r} is {p.dtype}; the device optimizer runs float32")
+            slots.append(_Slot(name, p, off, p.numel()))
+            off += (p.numel() + _ALIGN - 1) // _ALIGN * _ALIGN
+        total = max(off, _ALIGN)
+        dev = self.torch_device
+        self.p = torch.zeros(total, dtype=torch.float32, device=dev)
+        self.m = torch.zeros(total, dtype=torch.float32, device=dev)
+        self.v = torch.zeros(total, dtype=torch.float32, device=dev)
+        self.g = torch.zeros(total, dtype=torch.float32, device=dev)
+        with torch.no_grad():
+            for s in slots:
+                view = self.p[s.offset:s.offset + s.n].view(s.param.shape)
+                view.copy_(s.param.detach().to(dev))
+                s.param.data = view
+                st = self.optimizer.state.get(s.param) or {}
+                # resume from optimizer state present before binding (e.g. a loaded state_dict)
+                if "momentum_buffer" in st and st["momentum_buffer"] is not None:
+                    self.m[s.offset:s.offset + s.n].copy_(st["momentum_buffer"].reshape(-1).to(dev))
+                    s.has_momentum_buffer = True
+                if "exp_avg" in st:
+                    self.m[s.offset:s.offset + s.n].copy_(st["exp_avg"].reshape(-1).to(dev))
+                    self.v[s.offset:s.offset + s.n].copy_(st["exp_avg_sq"].reshape(-1).to(dev))
+                    s.step = float(st["step"])
+                if id(s.param) not in groups:
+                    raise ValueError(f"nvflare_amd: parameter {s.name!r} is not managed by the optimizer")
+        self.model.to(dev)  # buffers follow; parameters already live in self.p
+        self.slots = slots
+        self.by_name = {s.name: s for s in slots}
+        torch.cuda.synchronize(dev)
+
+    def is_bound(self) -> bool:
+        named = dict(self.model.named_parameters())
+        if set(named) != set(self.by_name):
+            return False
+        base = self.p.data_ptr()
+        return all(named[s.name] is s.param and s.param.data_ptr() == base + 4 * s.offset for s in self.slots)
+
+    def _expose_state(self, s: _Slot) -> None:
+        st = self.optimizer.state[s.param]
+        if self.kind == N.FEDAVG_EPI_SGD:
+            if s.has_momentum_buffer:  # torch stores the buffer only when momentum != 0
+                st["momentum_buffer"] = self.m[s.offset:s.offset + s.n].view(s.param.shape)
+        else:
+            st["step"] = torch.tensor(s.step, dtype=torch.float32)
+            st["exp_avg"] = self.m[s.offset:s.offset + s.n].view(s.param.shape)
+            st["exp_avg_sq"] = self.v[s.offset:s.offset + s.n].view(s.param.shape)
+
+    def _epilogue(self, group: dict, s: _Slot) -> "N.Epilogue":
+        e = N.Epilogue()
+        e.kind = self.kind
+        e.maximize = int(bool(group.get("maximize", False)))
+        e.lr = float(group["lr"])
+        e.weight_decay = float(group.get("weight_decay", 0.0))
+        e.param = self.p.data_ptr()
+        e.state1 = self.m.data_ptr()
+        if self.kind == N.FEDAVG_EPI_SGD:
+            e.momentum = float(group.get("momentum", 0.0))
+            e.dampening = float(group.get("dampening", 0.0))
+            e.nesterov = int(bool(group.get("nesterov", False)))
+            e.first_step = int(not s.has_momentum_buffer)
+        else:
+            b1, b2 = group["betas"]
+            e.beta1, e.beta2, e.eps = float(b1), float(b2), float(group["eps"])
+            e.decoupled_weight_decay = int(bool(group.get("decoupled_weight_decay", False)))
+            e.state2 = self.v.data_ptr()
+            e.step = s.step + 1.0
+        return e
+
+    def step(self, model_diff: Dict) -> List[str]:
+        """One server step on g = -diff for every parameter named in ``model_diff``; returns their names."""
+        groups = self._group_of()
+        present = []
+        with torch.no_grad():
+            for s in self.slots:
+                if s.name not in model_diff:
+                    continue
+                d = model_diff[s.name]
+                t = d.detach() if isinstance(d, torch.Tensor) else torch.as_tensor(np.asarray(d))
+                if t.dtype != torch.float32:  # param.grad = ... would refuse a different dtype
+                    raise RuntimeError(f"assigned grad has data of a different type ({t.dtype}) for {s.name!r}")
+                if tuple(t.shape) != tuple(s.param.shape):
+                    raise RuntimeError(f"assigned grad has data of a different size for {s.name!r}")
+                self.g[s.offset:s.offset + s.n].copy_(t.reshape(-1), non_blocking=False)
+                present.append(s)
+        if not present:
+            return []
+        torch.cuda.synchronize(self.torch_device)
+        # one launch per run of consecutive stepped parameters sharing group and per-parameter state
+        runs: List[Tuple[tuple, List[_Slot]]] = []
+        for s in present:
+            g = groups[id(s.param)]
+            key = (id(g), s.step, s.has_momentum_buffer)
+            prev = runs[-1][1][-1] if runs else None
+            contiguous = prev is not None and self.slots.index(s) == self.slots.index(prev) + 1
+            if runs and runs[-1][0] == key and contiguous:
+                runs[-1][1].append(s)
+            else:
+                runs.append((key, [s]))
+        # torch's copies above are complete (synchronised); the kernels run on the context's own stream
+        with self.ctx.lock:
+            for key, run in runs:
+                e = self._epilogue(groups[id(run[0].param)], run[0])
+                begin = run[0].offset
+                end = (run[-1].offset + run[-1].n + 3) // 4 * 4
+                self.ctx.accumulate_tiled_epi([], [], 4096, 4096, begin, end, None, N.FEDAVG_OP_TORCH,
+                                              N.FEDAVG_FIN_NONE, 1.0, e, acc_in_ptr=self.g.data_ptr())
+            self.ctx.sync()
+        for s in present:
+            s.step += 1.0
+            if self.kind == N.FEDAVG_EPI_SGD and groups[id(s.param)].get("momentum", 0.0) != 0.0:
+                s.has_momentum_buffer = True
+            self._expose_state(s)
+        return [s.name for s in present]
+
+
+class PTFedOptModelShareableGenerator(FullModelShareableGenerator):
+    def __init__(self, optimizer_args: dict = None, lr_scheduler_args: dict = None, source_model="model", device=None):
+        """Same arguments as the reference (fedopt.py:30-81); ``device`` picks the HIP device."""
+        super().__init__(device=hip_device_index(device) if device not in (None, "cpu") else None)
+        if not optimizer_args:
+            self.logger.warning("No optimizer_args provided. Using FedOpt with SGD and lr 1.0")
+            optimizer_args = {"path": "torch.optim.SGD", "args": {"lr": 1.0}}
+        if not isinstance(optimizer_args, dict):
+            raise TypeError(
+                "optimizer_args must be a dict of format, e.g. {'path': 'torch.optim.SGD', 'args': {'lr': 1.0}}."
+            )
+        if lr_scheduler_args is not None and not isinstance(lr_scheduler_args, dict):
+            raise TypeError(
+                "lr_scheduler_args must be a dict of format, e.g. "
+                "{'path': 'torch.optim.lr_scheduler.CosineAnnealingLR', 'args': {'T_max': 100}}."
+            )
+        self.source_model = source_model
+        self.optimizer_args = optimizer_args
+        self.lr_scheduler_args = lr_scheduler_args
+        self.model = None
+        self.optimizer = None
+        self.lr_scheduler = None
+        self.device = device
+        self.optimizer_name = None
+        self.lr_scheduler_name = None
+        self._dev_opt: Optional[DeviceServerOptimizer] = None
+
+    @staticmethod
+    def _get_component_name(component_args):
+        if component_args is None:
+            return None
+        return component_args.get("path") or component_args.get("class_path") or component_args.get("name", None)
+
+    def handle_event(self, event_type: str, fl_ctx: FLContext):
+        if event_type != EventType.START_RUN:
+            return
+        engine = fl_ctx.get_engine()
+        self.device = torch.device("cuda", hip_device_index(self.device))
+        if isinstance(self.source_model, str):
+            self.model = engine.get_component(self.source_model) if engine is not None else None
+        else:
+            self.model = self.source_model
+        if self.model is None:
+            self.system_panic("Model is not available", fl_ctx)
+            return
+        if not isinstance(self.model, torch.nn.Module):
+            self.system_panic(f"Expected model to be a torch.nn.Module but got {type(self.model)}", fl_ctx)
+            return
+        self.model.to(self.device)
+        build = getattr(engine, "build_component", None) or build_component_from_args
+        try:
+            self.optimizer_args.setdefault("args", {})
+            self.optimizer_args["args"]["params"] = self.model.parameters()
+            self.optimizer = build(self.optimizer_args)
+            self.optimizer_name = self._get_component_name(self.optimizer_args)
+        except Exception as e:
+            self.system_panic(f"Exception while parsing `optimizer_args`({self.optimizer_args}): {e}", fl_ctx)
+            return
+        if self.lr_scheduler_args is not None:
+            try:
+                self.lr_scheduler_name = self._get_component_name(self.lr_scheduler_args)
+                self.lr_scheduler_args.setdefault("args", {})
+                self.lr_scheduler_args["args"]["optimizer"] = self.optimizer
+                self.lr_scheduler = build(self.lr_scheduler_args)
+            except Exception as e:
+                self.system_panic(f"Exception while parsing `lr_scheduler_args`({self.lr_scheduler_args}): {e}", fl_ctx)
+                return
+
+    def device_optimizer(self) -> DeviceServerOptimizer:
+        """The HBM image of (model, optimizer); (re)bound when either changed since the last step."""
+        d = self._dev_opt
+        if d is None or d.model is not self.model or d.optimizer is not self.optimizer or not d.is_bound():
+            self._dev_opt = DeviceServerOptimizer(self.model, self.optimizer, hip_device_index(self.device))
+        return self._dev_opt
+
+    def server_update(self, model_diff):
+        """fedopt.py:157-182: the optimizer step on g = -diff, then the lr scheduler; returns
+        (state_dict, names of the stepped parameters)."""
+        self.model.train()
+        dev = self.device_optimizer()
+        updated_params = dev.step(model_diff)
+        if self.lr_scheduler is not None:
+            with warnings.catch_warnings():  # the step ran on the device, not through optimizer.step()
+                warnings.simplefilter("ignore", UserWarning)
+                self.lr_scheduler.step()
+        return self.model.state_dict(), updated_params
+
+    def shareable_to_learnable(self, shareable: Shareable, fl_ctx: FLContext) -> Learnable:
+        dxo = from_shareable(shareable)
+        if dxo.data_kind != DataKind.WEIGHT_DIFF:
+            self.system_panic("FedOpt is only implemented for data_kind == DataKind.WEIGHT_DIFF", fl_ctx)
+            return Learnable()
+        processed_algorithm = dxo.get_meta_prop(MetaKey.PROCESSED_ALGORITHM)
+        if processed_algorithm is not None:
+            self.system_panic(f"FedOpt is not implemented for shareable processed by {processed_algorithm}", fl_ctx)
+            return Learnable()
+        model_diff = dxo.data
+        base_model = fl_ctx.get_prop(AppConstants.GLOBAL_MODEL)
+        if not base_model:
+            self.system_panic(reason="No global base model!", fl_ctx=fl_ctx)
+            return base_model
+        base_model_weights = base_model[ModelLearnableKey.WEIGHTS]
+        if base_model_weights:
+            preserve_torch = any(isinstance(v, torch.Tensor) for v in base_model_weights.values())
+        else:
+            preserve_torch = any(isinstance(v, torch.Tensor) for v in model_diff.values())
+
+        start = time.time()
+        weights, updated_params = self.server_update(model_diff)
+        secs = time.time() - start
+
+        start = time.time()
+        weights = self._to_host(weights, preserve_torch)
+        secs_detach = time.time() - start
+
+        # FedAvg for the keys the optimizer does not own (e.g. batch-norm statistics), fedopt.py:247-263
+        rest = [k for k in model_diff if k not in updated_params]
+        base = {}
+        for key in rest:
+            base_value = base_model_weights[key] if key in base_model_weights else weights[key]
+            value = model_diff[key]
+            if preserve_torch:
+                base_value = base_value.detach().cpu() if isinstance(base_value, torch.Tensor) else torch.as_tensor(base_value)
+                value = value.detach().cpu() if isinstance(value, torch.Tensor) else torch.as_tensor(value)
+            base[key] = (base_value, value)
+        merged = apply_weight_diff(self._adder, {k: b for k, (b, _) in base.items()}, {k: d for k, (_, d) in base.items()})
+        weights.update(merged)
+
+        self.log_info(
+            fl_ctx,
+            f"FedOpt ({self.optimizer_name}, {self.device}) server model update "
+            f"round {fl_ctx.get_prop(AppConstants.CURRENT_ROUND)}, "
+            f"{self.lr_scheduler_name if self.lr_scheduler_name else ''} "
+            f"lr: {self.optimizer.param_groups[-1]['lr']}, "
+            f"fedopt layers: {len(updated_params)}, fedavg layers: {len(rest)}, "
+            f"update: {secs} secs., detach: {secs_detach} secs.",
+        )
+        return make_model_learnable(weights, dxo.get_meta_props())
+
+    @staticmethod
+    def _to_host(state: Dict, preserve_torch: bool) -> Dict:
+        """state_dict -> host copies (``.detach().cpu().clone()`` / ``.numpy()``, fedopt.py:238-244)."""
+        out = {}
+        for k, v in state.items():
+            h = v.detach().cpu()
+            out[k] = h.clone() if preserve_torch else h.numpy()
+        return out

@@ -22,6 +22,14 @@ if os.environ.get("NVFLARE_AMD_FORCE_STANDINS", "0") != "1":
         from nvflare.app_common.abstract.fl_model import FLModel, ParamsType  # noqa: F401
         from nvflare.app_common.aggregators.model_aggregator import ModelAggregator  # noqa: F401
         from nvflare.app_common.utils.fl_model_utils import FLModelUtils  # noqa: F401
+        from nvflare.app_common.abstract.learnable import Learnable  # noqa: F401
+        from nvflare.app_common.abstract.model import (  # noqa: F401
+            ModelLearnable,
+            ModelLearnableKey,
+            make_model_learnable,
+            model_learnable_to_dxo,
+        )
+        from nvflare.app_common.abstract.shareable_generator import ShareableGenerator  # noqa: F401
 
         HAVE_NVFLARE = True
     except Exception:
@@ -39,14 +47,20 @@ if not HAVE_NVFLARE:
         FLMetaKey,
         FLModel,
         FLModelUtils,
+        Learnable,
         ModelAggregator,
+        ModelLearnable,
+        ModelLearnableKey,
         ParamsType,
         MetaKey,
         ReservedKey,
         ReturnCode,
         Shareable,
+        ShareableGenerator,
         from_shareable,
         get_module_logger,
+        make_model_learnable,
+        model_learnable_to_dxo,
     )
 
 __all__ = [
@@ -61,12 +75,18 @@ __all__ = [
     "FLMetaKey",
     "FLModel",
     "FLModelUtils",
+    "Learnable",
     "ModelAggregator",
+    "ModelLearnable",
+    "ModelLearnableKey",
     "ParamsType",
     "MetaKey",
     "ReservedKey",
     "ReturnCode",
     "Shareable",
+    "ShareableGenerator",
     "from_shareable",
     "get_module_logger",
+    "make_model_learnable",
+    "model_learnable_to_dxo",
 ]

@@ -12,6 +12,8 @@ repository's tests).  They reproduce the behaviour the aggregation path relies o
 * ``ModelAggregator`` ABC and the ``FLModelUtils`` conversions it uses
                                                   nvflare/app_common/aggregators/model_aggregator.py:26-83,
                                                   nvflare/app_common/utils/fl_model_utils.py:46-149
+* ``ShareableGenerator``, ``Learnable``, ``ModelLearnable`` helpers  app_common/abstract/shareable_generator.py,
+                                                  learnable.py, model.py:25-71
 * constants: ``ReservedKey`` (fl_constant.py:69-80), ``ReturnCode`` (:26-36),
   ``AppConstants`` (app_common/app_constant.py:33-79), ``EventType.START_RUN`` (apis/event_type.py:22)
 """
@@ -44,6 +46,7 @@ class MetaKey:
 
 
 class ReservedKey:
+    ENGINE = "__engine__"
     IDENTITY_NAME = "__identity_name__"
     RC = "__rc__"
     COOKIE_JAR = "__cookie_jar__"
@@ -71,13 +74,13 @@ class FLMetaKey:
 
 
 class AppConstants:
+    GLOBAL_MODEL = "global_model"
     CURRENT_ROUND = "current_round"
     START_ROUND = "start_round"
     CLIENT_UNKNOWN = "unknown"
     METRICS_AGGREGATION_INFO = "metrics_aggregation_info"
     NUM_ROUNDS = "num_rounds"
     CONTRIBUTION_ROUND = "contribution_round"
-    GLOBAL_MODEL = "global_model"
     AGGREGATION_STATS = "_aggregation_stats"
 
 
@@ -225,6 +228,9 @@ class FLContext:
 
     def get_identity_name(self, default=""):
         return self.get_prop(ReservedKey.IDENTITY_NAME, default)
+
+    def get_engine(self):
+        return self.get_prop(ReservedKey.ENGINE)
 
 
 def get_module_logger(module: str = None, name: str = None):
@@ -404,3 +410,44 @@ class ModelAggregator(Aggregator):
 
     def exception(self, message: str):
         self.log_exception(self.fl_ctx, message)
+
+
+class Learnable(dict):
+    def is_empty(self):
+        return False
+
+
+class ModelLearnableKey:
+    WEIGHTS = "weights"
+    META = "meta"
+
+
+class ModelLearnable(Learnable):
+    def is_empty(self):
+        return not self.get(ModelLearnableKey.WEIGHTS)
+
+
+def make_model_learnable(weights, meta_props) -> ModelLearnable:
+    ml = ModelLearnable()
+    ml[ModelLearnableKey.WEIGHTS] = weights
+    ml[ModelLearnableKey.META] = meta_props
+    return ml
+
+
+def model_learnable_to_dxo(ml: ModelLearnable) -> DXO:
+    if not isinstance(ml, ModelLearnable):
+        raise ValueError(f"invalid model learnable: expect Model type but got {type(ml)}")
+    for key in (ModelLearnableKey.WEIGHTS, ModelLearnableKey.META):
+        if key not in ml:
+            raise ValueError(f"invalid model learnable: missing {key}")
+    return DXO(data_kind=DataKind.WEIGHTS, data=ml[ModelLearnableKey.WEIGHTS], meta=ml[ModelLearnableKey.META])
+
+
+class ShareableGenerator(FLComponent, ABC):
+    @abstractmethod
+    def learnable_to_shareable(self, model: Learnable, fl_ctx: FLContext) -> Shareable:
+        pass
+
+    @abstractmethod
+    def shareable_to_learnable(self, shareable: Shareable, fl_ctx: FLContext) -> Learnable:
+        pass

@@ -14,11 +14,14 @@ Reference code exercised:
   nvflare/app_common/aggregators/weighted_aggregation_helper.py:153-240  (helper cases)
   nvflare/app_common/workflows/base_fedavg.py:93-230  (``--set fedavg``: aggregate_fn cases)
   nvflare/app_common/workflows/fedavg.py:268-366      (``--set fedavg``: built-in in-time FedAvg cases)
+  nvflare/app_opt/pt/fedopt.py:157-270                 (``--set fedopt``: PTFedOptModelShareableGenerator, CPU)
+  nvflare/app_common/shareablegenerators/full_model_shareable_generator.py:37-83  (``--set fedopt``)
   nvflare/app_common/aggregators/intime_accumulate_model_aggregator.py   (intime cases)
   nvflare/app_common/aggregators/dxo_aggregator.py:71-191
 
-Usage:  python tests/golden/make_golden.py [--ref /root/reference] [--set helper|fedavg]
-        (helper -> helper_cases.{npz,json}; fedavg -> fedavg_cases.{npz,json})
+Usage:  python tests/golden/make_golden.py [--ref /root/reference] [--set helper|fedavg|fedopt]
+        (helper -> helper_cases.{npz,json}; fedavg -> fedavg_cases.{npz,json};
+         fedopt -> fedopt_cases.{npz,json})
 """
 
 from __future__ import annotations
@@ -268,15 +271,119 @@ def main_fedavg():
     print(f"wrote {len(cases)} fedavg cases, {len(store.arrays)} arrays")
 
 
+FEDOPT_CONFIGS = [
+    # (name, optimizer_args, lr_scheduler_args)
+    ("sgd_default", {"path": "torch.optim.SGD", "args": {"lr": 1.0}}, None),
+    ("sgd_momentum_wd", {"path": "torch.optim.SGD", "args": {"lr": 0.5, "momentum": 0.9, "dampening": 0.1, "weight_decay": 1e-3}}, None),
+    ("sgd_nesterov", {"path": "torch.optim.SGD", "args": {"lr": 0.3, "momentum": 0.9, "nesterov": True}}, None),
+    ("sgd_steplr", {"path": "torch.optim.SGD", "args": {"lr": 1.0, "momentum": 0.6}},
+     {"path": "torch.optim.lr_scheduler.StepLR", "args": {"step_size": 1, "gamma": 0.5}}),
+    ("adam_default", {"path": "torch.optim.Adam", "args": {"lr": 1e-3}}, None),
+    ("adam_wd", {"path": "torch.optim.Adam", "args": {"lr": 1e-2, "betas": [0.8, 0.99], "eps": 1e-6, "weight_decay": 1e-2}}, None),
+    ("adamw", {"path": "torch.optim.AdamW", "args": {"lr": 1e-2, "weight_decay": 0.1}}, None),
+    ("adam_cosine", {"path": "torch.optim.Adam", "args": {"lr": 1e-2, "maximize": False}},
+     {"path": "torch.optim.lr_scheduler.CosineAnnealingLR", "args": {"T_max": 5}}),
+]
+
+
+def fedopt_model():
+    """Small model with fp32 params, BatchNorm buffers (incl. int64 num_batches_tracked) and a plain
+    buffer; the test side rebuilds the same architecture (tests/test_gpu_fedopt_generator.py)."""
+    class Net(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.lin1 = torch.nn.Linear(7, 64)
+            self.bn = torch.nn.BatchNorm1d(64)
+            self.lin2 = torch.nn.Linear(64, 90, bias=False)
+            self.register_buffer("offset", torch.zeros(5))
+
+    return Net()
+
+
+def _import_path(path):
+    import importlib
+
+    mod, _, cls = path.rpartition(".")
+    return getattr(importlib.import_module(mod), cls)
+
+
+def main_fedopt():
+    from nvflare.apis.dxo import DXO, DataKind
+    from nvflare.apis.fl_context import FLContext
+    from nvflare.app_common.abstract.model import ModelLearnableKey, make_model_learnable
+    from nvflare.app_common.app_constant import AppConstants
+    from nvflare.app_opt.pt.fedopt import PTFedOptModelShareableGenerator
+
+    rng = np.random.default_rng(20261017)
+    torch.manual_seed(0)
+    store = Store()
+    cases = []
+    init_model = fedopt_model()
+    init_state = {k: v.detach().clone() for k, v in init_model.state_dict().items()}
+    init_names = {k: store.put(v, "init") for k, v in init_state.items()}
+    n_rounds = 3
+    for container in ("numpy", "torch"):
+        configs = FEDOPT_CONFIGS if container == "numpy" else [FEDOPT_CONFIGS[1], FEDOPT_CONFIGS[4]]
+        for name, opt_args, sched_args in configs:
+            model = fedopt_model()
+            model.load_state_dict(init_state)
+            gen = PTFedOptModelShareableGenerator(optimizer_args=json.loads(json.dumps(opt_args)), device="cpu")
+            gen.model = model
+            gen.device = torch.device("cpu")
+            args = dict(opt_args["args"])
+            if "betas" in args:
+                args["betas"] = tuple(args["betas"])
+            gen.optimizer = _import_path(opt_args["path"])(model.parameters(), **args)
+            gen.optimizer_name = opt_args["path"]
+            if sched_args:
+                gen.lr_scheduler = _import_path(sched_args["path"])(gen.optimizer, **sched_args["args"])
+                gen.lr_scheduler_name = sched_args["path"]
+            weights = {k: (v.numpy().copy() if container == "numpy" else v.clone()) for k, v in init_state.items()}
+            rounds = []
+            for rnd in range(n_rounds):
+                diff = {}
+                for k, v in init_state.items():
+                    if rnd == 1 and k == "lin2.weight":
+                        continue  # a parameter missing from one round's aggregate: not stepped that round
+                    if v.dtype == torch.int64:
+                        a = np.array(rnd + 1, dtype=np.int64).reshape(v.shape)
+                    else:
+                        a = (rng.standard_normal(tuple(v.shape)) * 0.05).astype(np.float32)
+                    diff[k] = a
+                fl_ctx = FLContext()
+                fl_ctx.set_prop(AppConstants.GLOBAL_MODEL, make_model_learnable(weights, {}), private=True, sticky=True)
+                fl_ctx.set_prop(AppConstants.CURRENT_ROUND, rnd, private=True, sticky=False)
+                cdiff = {k: to_container(v, container) for k, v in diff.items()}
+                learnable = gen.shareable_to_learnable(DXO(DataKind.WEIGHT_DIFF, data=cdiff, meta={"m": rnd}).to_shareable(), fl_ctx)
+                weights = learnable[ModelLearnableKey.WEIGHTS]
+                rounds.append({
+                    "diff": {k: store.put(v, "diff") for k, v in diff.items()},
+                    "weights": {k: store.put(v, "w") for k, v in weights.items()},
+                    "weights_type": {k: type(v).__name__ for k, v in weights.items()},
+                    "lr_after": gen.optimizer.param_groups[-1]["lr"],
+                    "meta": learnable[ModelLearnableKey.META],
+                })
+            cases.append({"kind": "fedopt", "name": f"{container}_{name}", "container": container, "optimizer_args": opt_args,
+                          "lr_scheduler_args": sched_args, "init": init_names, "rounds": rounds})
+    np.savez_compressed(os.path.join(HERE, "fedopt_cases.npz"), **store.arrays)
+    with open(os.path.join(HERE, "fedopt_cases.json"), "w") as f:
+        json.dump({"generator": "tests/golden/make_golden.py --set fedopt", "reference": "NVFlare (/root/reference, ~2.9.0-dev)",
+                   "numpy": np.__version__, "torch": torch.__version__, "torch_threads": torch.get_num_threads(),
+                   "cases": cases}, f, indent=1, default=str)
+    print(f"wrote {len(cases)} fedopt cases, {len(store.arrays)} arrays")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ref", default="/root/reference")
-    ap.add_argument("--set", choices=["helper", "fedavg"], default="helper")
+    ap.add_argument("--set", choices=["helper", "fedavg", "fedopt"], default="helper")
     args = ap.parse_args()
     install_shim(args.ref)
     torch.set_num_threads(8)
     if args.set == "fedavg":
         return main_fedavg()
+    if args.set == "fedopt":
+        return main_fedopt()
 
     rng = np.random.default_rng(20261015)
     random.seed(20261015)

@@ -112,3 +112,34 @@ def same_metrics(a, b) -> bool:
         if not (x == y or (math.isnan(x) and math.isnan(y))):
             return False
     return True
+
+
+def load_fedopt_golden():
+    """PTFedOptModelShareableGenerator cases (make_golden.py --set fedopt), reference run on CPU."""
+    if "o" not in _cache:
+        with open(os.path.join(GOLDEN_DIR, "fedopt_cases.json")) as f:
+            meta = json.load(f)
+        arrays = dict(np.load(os.path.join(GOLDEN_DIR, "fedopt_cases.npz"), allow_pickle=False))
+        _cache["o"] = (meta, arrays)
+    return _cache["o"]
+
+
+def fedopt_model():
+    """Same architecture as make_golden.py's fedopt_model (state is loaded from the fixture)."""
+    import torch
+
+    class Net(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.lin1 = torch.nn.Linear(7, 64)
+            self.bn = torch.nn.BatchNorm1d(64)
+            self.lin2 = torch.nn.Linear(64, 90, bias=False)
+            self.register_buffer("offset", torch.zeros(5))
+
+    return Net()
+
+
+def adam_param_tolerance(p0, p_ref, lr, steps):
+    """|p - p_torch| bound for Adam params (torch CPU's MKL sqrt is not correctly rounded; see
+    tests/test_fedopt_oracle.py): steps * spacing(max(|p0|, |p_torch|, lr))."""
+    return steps * np.spacing(np.maximum(np.maximum(np.abs(p0), np.abs(p_ref)), np.float32(lr))).astype(np.float64)

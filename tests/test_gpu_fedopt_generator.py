@@ -1,0 +1,134 @@
+"""Drop-in FedOpt shareable generator on the GPU vs the reference generator's own outputs.
+
+tests/golden/fedopt_cases.* hold three rounds of ``PTFedOptModelShareableGenerator.shareable_to_learnable``
+(nvflare/app_opt/pt/fedopt.py:184-270, run on CPU by make_golden.py --set fedopt) for SGD (plain,
+momentum + dampening + weight decay, nesterov, StepLR), Adam (default, betas/eps/weight decay,
+CosineAnnealingLR) and AdamW, numpy and torch containers, a BatchNorm model (fp32 running stats and an
+int64 ``num_batches_tracked`` go through the FedAvg ``base + diff`` branch) and a parameter missing from
+round 2 (not stepped that round).
+
+Bar: every SGD output and every non-parameter key bit-exact; Adam parameters within
+``steps * spacing(max(|p0|, |p_torch|, lr))`` (torch CPU's MKL sqrt is not correctly rounded, see
+tests/test_fedopt_oracle.py); lr schedule and meta identical."""
+
+import numpy as np
+import pytest
+import torch
+
+from golden_util import adam_param_tolerance, fedopt_model, load_fedopt_golden, same_bits
+from nvflare_amd.app_opt.pt import PTFedOptModelShareableGenerator
+from nvflare_amd.compat import DXO, AppConstants, DataKind, EventType, FLContext, ModelLearnableKey, make_model_learnable
+
+pytestmark = pytest.mark.gpu
+
+META, ARRAYS = load_fedopt_golden()
+CASES = META["cases"]
+
+
+def _container(a, container):
+    a = np.array(a, copy=True)
+    return torch.from_numpy(a) if container == "torch" else a
+
+
+def _np(v):
+    return v.numpy() if isinstance(v, torch.Tensor) else np.asarray(v)
+
+
+@pytest.mark.parametrize("case", CASES, ids=lambda c: c["name"])
+def test_fedopt_generator_matches_reference(case):
+    container = case["container"]
+    model = fedopt_model()
+    model.load_state_dict({k: torch.from_numpy(np.array(ARRAYS[v], copy=True)) for k, v in case["init"].items()})
+    import copy
+
+    gen = PTFedOptModelShareableGenerator(optimizer_args=copy.deepcopy(case["optimizer_args"]),
+                                          lr_scheduler_args=copy.deepcopy(case["lr_scheduler_args"]),
+                                          source_model=model, device="cuda:0")
+    gen.handle_event(EventType.START_RUN, FLContext())
+    assert gen.optimizer is not None
+    is_adam = "Adam" in case["optimizer_args"]["path"]
+    lr = case["optimizer_args"]["args"]["lr"]
+    param_names = {n for n, _ in model.named_parameters()}
+    weights = {k: _container(ARRAYS[v], container) for k, v in case["init"].items()}
+    steps = {n: 0 for n in param_names}
+    for rnd, exp in enumerate(case["rounds"]):
+        fl_ctx = FLContext()
+        fl_ctx.set_prop(AppConstants.GLOBAL_MODEL, make_model_learnable(weights, {}), private=True, sticky=True)
+        fl_ctx.set_prop(AppConstants.CURRENT_ROUND, rnd, private=True, sticky=False)
+        diff = {k: _container(ARRAYS[v], container) for k, v in exp["diff"].items()}
+        learnable = gen.shareable_to_learnable(DXO(DataKind.WEIGHT_DIFF, data=diff, meta={"m": rnd}).to_shareable(), fl_ctx)
+        out = learnable[ModelLearnableKey.WEIGHTS]
+        assert learnable[ModelLearnableKey.META] == exp["meta"]
+        assert set(out) == set(exp["weights"])
+        for n in param_names:
+            if n in diff:
+                steps[n] += 1
+        for k, name in exp["weights"].items():
+            assert type(out[k]).__name__ == exp["weights_type"][k], k
+            got, ref = _np(out[k]), ARRAYS[name]
+            assert got.dtype == ref.dtype and got.shape == ref.shape, k
+            if is_adam and k in param_names:
+                p0 = ARRAYS[case["init"][k]]
+                tol = adam_param_tolerance(p0, ref, lr, max(steps[k], 1))
+                diff_abs = np.abs(got.astype(np.float64) - ref.astype(np.float64))
+                assert np.all(diff_abs <= tol), (case["name"], rnd, k, float((diff_abs / tol).max()))
+            else:
+                assert same_bits(got, ref), (case["name"], rnd, k)
+        assert gen.optimizer.param_groups[-1]["lr"] == exp["lr_after"]
+        weights = out
+
+
+def test_fedopt_generator_optimizer_state_views():
+    """optimizer.state holds views of the device buffers after a step (checkpointable as with torch)."""
+    model = fedopt_model()
+    gen = PTFedOptModelShareableGenerator(optimizer_args={"path": "torch.optim.Adam", "args": {"lr": 1e-3}},
+                                          source_model=model, device=0)
+    gen.handle_event(EventType.START_RUN, FLContext())
+    w = {k: v.detach().cpu().numpy().copy() for k, v in model.state_dict().items()}
+    fl_ctx = FLContext()
+    fl_ctx.set_prop(AppConstants.GLOBAL_MODEL, make_model_learnable(w, {}))
+    diff = {k: np.full(v.shape, 0.01, np.float32) for k, v in w.items() if v.dtype == np.float32}
+    gen.shareable_to_learnable(DXO(DataKind.WEIGHT_DIFF, data=diff).to_shareable(), fl_ctx)
+    sd = gen.optimizer.state_dict()
+    p = model.lin1.weight
+    st = gen.optimizer.state[p]
+    assert float(st["step"]) == 1.0
+    assert st["exp_avg"].device.type == "cuda" and st["exp_avg"].shape == p.shape
+    # exp_avg after one step = (1 - beta1) * g with g = -0.01
+    assert torch.allclose(st["exp_avg"].cpu(), torch.full(p.shape, -0.001))
+    assert len(sd["state"]) == len(list(model.parameters()))
+
+
+def test_fedopt_generator_rejects_unsupported_optimizer():
+    model = fedopt_model()
+    gen = PTFedOptModelShareableGenerator(optimizer_args={"path": "torch.optim.RMSprop", "args": {"lr": 1e-3}},
+                                          source_model=model, device=0)
+    gen.handle_event(EventType.START_RUN, FLContext())
+    w = {k: v.detach().cpu().numpy().copy() for k, v in model.state_dict().items()}
+    fl_ctx = FLContext()
+    fl_ctx.set_prop(AppConstants.GLOBAL_MODEL, make_model_learnable(w, {}))
+    diff = {"lin1.weight": np.zeros((64, 7), np.float32)}
+    with pytest.raises(NotImplementedError, match="RMSprop"):
+        gen.shareable_to_learnable(DXO(DataKind.WEIGHT_DIFF, data=diff).to_shareable(), fl_ctx)
+
+
+def test_full_model_generator_weight_diff_apply():
+    """full_model_shareable_generator.py:58-67 on the device: bit-exact numpy / torch adds, host ints."""
+    from nvflare_amd.app_common.shareablegenerators import FullModelShareableGenerator
+
+    rng = np.random.default_rng(3)
+    gen = FullModelShareableGenerator(device=0)
+    for container in ("numpy", "torch"):
+        base = {"a": rng.standard_normal((33, 129)).astype(np.float32), "b": rng.standard_normal(5000).astype(np.float32),
+                "n": np.array(7, np.int64), "s": np.array(1.5, np.float32)}
+        diff = {"a": rng.standard_normal((33, 129)).astype(np.float32), "b": rng.standard_normal(5000).astype(np.float32),
+                "n": np.array(2, np.int64), "s": np.array(0.25, np.float32)}
+        expect = {k: base[k] + diff[k] for k in base}
+        cb = {k: _container(v, container) for k, v in base.items()}
+        cd = {k: _container(v, container) for k, v in diff.items()}
+        fl_ctx = FLContext()
+        fl_ctx.set_prop(AppConstants.GLOBAL_MODEL, make_model_learnable(cb, {}))
+        out = gen.shareable_to_learnable(DXO(DataKind.WEIGHT_DIFF, data=cd, meta={"x": 1}).to_shareable(), fl_ctx)
+        for k in base:
+            assert same_bits(_np(out[ModelLearnableKey.WEIGHTS][k]), np.asarray(expect[k])), (container, k)
+        assert out[ModelLearnableKey.META] == {"x": 1}
