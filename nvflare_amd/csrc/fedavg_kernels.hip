@@ -466,8 +466,8 @@ static hipError_t launch_epi_p(const TileLaunch& L, const EpiParams& E, hipStrea
 
 template <int OP, int FIN, bool ACC_IN>
 static hipError_t launch_epi_a(const TileLaunch& L, const EpiParams& E, hipStream_t s) {
-    return (L.variant & kVariantEpiLateLoads) ? launch_epi_p<OP, FIN, ACC_IN, false>(L, E, s)
-                                              : launch_epi_p<OP, FIN, ACC_IN, true>(L, E, s);
+    return (L.variant & kVariantEpiPrefetch) ? launch_epi_p<OP, FIN, ACC_IN, true>(L, E, s)
+                                             : launch_epi_p<OP, FIN, ACC_IN, false>(L, E, s);
 }
 
 template <int OP, int FIN>

@@ -57,7 +57,7 @@ class Store:
     def put(self, arr, tag="a") -> str:
         if isinstance(arr, torch.Tensor):
             arr = arr.detach().cpu().numpy()
-        arr = np.asarray(arr)
+        arr = np.array(arr, copy=True)  # snapshot: a reference result may alias live state (fedopt on CPU)
         name = f"{tag}{self.n:05d}"
         self.n += 1
         self.arrays[name] = arr

@@ -46,11 +46,12 @@ def main():
 
     rows = []
     ms = timed(lambda: ctx.accumulate_tiled(bases, ws, lay.tile, lay.tile_stride, 0, end, out.ptr, 1, 2, cnt))
-    rows.append(("none", 0, ms, 4.0 * K * P + 4.0 * P))
+    rows.append(("none", 0, 2, ms, 4.0 * K * P + 4.0 * P))
     for epi_name, kind, extra in (("add_base", N.FEDAVG_EPI_ADD_BASE, 8.0), ("sgd", N.FEDAVG_EPI_SGD, 16.0),
                                   ("adam", N.FEDAVG_EPI_ADAM, 24.0)):
-        for variant in (0, 4):
+        for variant, bpc in ((0, 2), (4, 2), (0, 3), (0, 4), (4, 3)):
             ctx.set_variant(variant)
+            ctx.set_launch(bpc, 0)
             e = N.Epilogue()
             e.kind = kind
             e.lr, e.momentum, e.beta1, e.beta2, e.eps, e.step = 1e-3, 0.9, 0.9, 0.999, 1e-8, 1.0
@@ -61,10 +62,11 @@ def main():
                 e.param, e.state1, e.state2 = bufs[0].ptr, bufs[1].ptr, bufs[2].ptr
                 o = None
             ms = timed(lambda: ctx.accumulate_tiled_epi(bases, ws, lay.tile, lay.tile_stride, 0, end, o, 1, 2, cnt, e))
-            rows.append((epi_name, variant, ms, 4.0 * K * P + extra * P))
+            rows.append((epi_name, variant, bpc, ms, 4.0 * K * P + extra * P))
     ctx.set_variant(0)
-    for name, variant, ms, b in rows:
-        print(json.dumps({"epilogue": name, "variant": variant, "ms": round(ms, 3), "GBps": round(b / ms / 1e6, 1),
+    ctx.set_launch(0, 0)
+    for name, variant, bpc, ms, b in rows:
+        print(json.dumps({"epilogue": name, "variant": variant, "blocks_per_cu": bpc, "ms": round(ms, 3), "GBps": round(b / ms / 1e6, 1),
                           "frac_8TBps": round(b / ms / 1e6 / 8000, 4)}), flush=True)
 
 
