@@ -79,6 +79,26 @@ typedef struct fedavg_epilogue {
     const float* base;          /* ADD_BASE: flat fp32 base weights (out may alias it) */
 } fedavg_epilogue;
 
+/* Quantized payload formats (nvflare/app_opt/pt/quantization/dequantizer.py:47-185, row f4). */
+enum fedavg_qtype {
+    FEDAVG_Q_F16 = 1,        /* "float16": fp16 values                                   */
+    FEDAVG_Q_BF16 = 2,       /* bf16 values                                              */
+    FEDAVG_Q_BLOCKWISE8 = 3, /* "blockwise8": uint8 codes, fp32 code[256], fp32 absmax   */
+    FEDAVG_Q_FP4 = 4,        /* "float4": packed nibbles (high first), fp32 absmax       */
+    FEDAVG_Q_NF4 = 5,        /* "normfloat4": packed nibbles (high first), fp32 absmax   */
+    FEDAVG_Q_ADA_U8 = 6,     /* "adaquant": uint8 levels, fp64 norm / level / offset     */
+    FEDAVG_Q_ADA_U16 = 7,    /* "adaquant": uint16 levels                                */
+};
+
+typedef struct fedavg_quant {
+    int qtype;          /* enum fedavg_qtype */
+    int has_norm;       /* adaquant: 0 = all-constant tensor (value -offset) */
+    size_t blocksize;   /* blockwise8 / fp4 / nf4: elements per absmax entry (multiple of 4) */
+    const float* absmax; /* device pointer */
+    const float* code;   /* device pointer, blockwise8 only (256 entries) */
+    double norm, level, offset; /* adaquant */
+} fedavg_quant;
+
 typedef struct fedavg_ctx fedavg_ctx;
 
 /* Last error message of the calling thread ("" if none). */
@@ -160,6 +180,14 @@ int fedavg_accumulate_tiled_epi(fedavg_ctx* ctx, const void* const* bases, const
                                 size_t tile_elems, size_t tile_stride, size_t begin, size_t end,
                                 const void* acc_in, void* out, int op, int fin, double count,
                                 const fedavg_epilogue* epi);
+
+/* Dequantize n elements of a device-resident payload q into fp32, written at logical element offset
+ * logical_offset of a tiled buffer (tile_elems, tile_stride; 0, 0 = flat).  The aggregation slab layout,
+ * so a quantized contribution is dequantized straight into its client slot.  Replaces the per-format
+ * branches of ModelDequantizer.dequantization (dequantizer.py:98-160) + the fp32 cast (:168-173).
+ * logical_offset and tile_elems multiples of 4; the 16-byte-aligned out must cover the written range. */
+int fedavg_dequantize(fedavg_ctx* ctx, const fedavg_quant* qs, const void* q, size_t n, float* out_base,
+                      size_t tile_elems, size_t tile_stride, size_t logical_offset);
 
 /* Timing of the kernels launched by the last fedavg_accumulate call, measured with HIP events on
  * the stream they ran on (enable first; costs two event records per call). */

@@ -114,6 +114,7 @@ _SIGNATURES = {
     "fedavg_set_tile": [c_void_p, c_int],
     "fedavg_fill_synthetic_f32": [c_void_p, c_void_p, c_size_t, c_size_t, c_size_t, c_u64, c_u64, c_u64],
     "fedavg_gather_f32": [c_void_p, c_void_p, c_void_p, c_size_t, c_void_p],
+    "fedavg_dequantize": [c_void_p, c_void_p, c_void_p, c_size_t, c_void_p, c_size_t, c_size_t, c_size_t],
 }
 EXPORTED = ["fedavg_last_error", "fedavg_abi_version", *_SIGNATURES.keys()]
 
@@ -145,6 +146,30 @@ class Epilogue(ctypes.Structure):
         ("state1", c_void_p),
         ("state2", c_void_p),
         ("base", c_void_p),
+    ]
+
+
+FEDAVG_Q_F16 = 1
+FEDAVG_Q_BF16 = 2
+FEDAVG_Q_BLOCKWISE8 = 3
+FEDAVG_Q_FP4 = 4
+FEDAVG_Q_NF4 = 5
+FEDAVG_Q_ADA_U8 = 6
+FEDAVG_Q_ADA_U16 = 7
+
+
+class Quant(ctypes.Structure):
+    """struct fedavg_quant (include/nvflare_amd_fedavg.h)."""
+
+    _fields_ = [
+        ("qtype", c_int),
+        ("has_norm", c_int),
+        ("blocksize", c_size_t),
+        ("absmax", c_void_p),
+        ("code", c_void_p),
+        ("norm", c_double),
+        ("level", c_double),
+        ("offset", c_double),
     ]
 
 

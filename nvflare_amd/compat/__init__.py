@@ -30,6 +30,7 @@ if os.environ.get("NVFLARE_AMD_FORCE_STANDINS", "0") != "1":
             model_learnable_to_dxo,
         )
         from nvflare.app_common.abstract.shareable_generator import ShareableGenerator  # noqa: F401
+        from nvflare.apis.dxo_filter import DXOFilter  # noqa: F401
 
         HAVE_NVFLARE = True
     except Exception:
@@ -39,6 +40,7 @@ if not HAVE_NVFLARE:
     from ._standins import (  # noqa: F401
         DXO,
         Aggregator,
+        DXOFilter,
         AppConstants,
         DataKind,
         EventType,
@@ -66,6 +68,7 @@ if not HAVE_NVFLARE:
 __all__ = [
     "HAVE_NVFLARE",
     "DXO",
+    "DXOFilter",
     "Aggregator",
     "AppConstants",
     "DataKind",

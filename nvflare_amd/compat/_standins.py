@@ -12,6 +12,7 @@ repository's tests).  They reproduce the behaviour the aggregation path relies o
 * ``ModelAggregator`` ABC and the ``FLModelUtils`` conversions it uses
                                                   nvflare/app_common/aggregators/model_aggregator.py:26-83,
                                                   nvflare/app_common/utils/fl_model_utils.py:46-149
+* ``DXOFilter`` (process / process_dxo / filter history)          nvflare/apis/dxo_filter.py:26-140
 * ``ShareableGenerator``, ``Learnable``, ``ModelLearnable`` helpers  app_common/abstract/shareable_generator.py,
                                                   learnable.py, model.py:25-71
 * constants: ``ReservedKey`` (fl_constant.py:69-80), ``ReturnCode`` (:26-36),
@@ -175,6 +176,26 @@ class DXO:
 
     def get_meta_props(self):
         return self.meta
+
+    def remove_meta_props(self, keys):
+        if self.meta and keys:
+            for k in keys:
+                self.meta.pop(k, None)
+
+    def add_filter_history(self, filter_name):
+        if not filter_name:
+            return
+        hist = self.get_meta_prop(MetaKey.FILTER_HISTORY)
+        if not hist:
+            hist = []
+            self.set_meta_prop(MetaKey.FILTER_HISTORY, hist)
+        if isinstance(filter_name, str):
+            hist.append(filter_name)
+        else:
+            hist.extend(filter_name)
+
+    def get_filter_history(self):
+        return self.get_meta_prop(MetaKey.FILTER_HISTORY)
 
     def to_dict(self) -> dict:
         return {"kind": self.data_kind, "data": self.data, "meta": self.meta}
@@ -451,3 +472,58 @@ class ShareableGenerator(FLComponent, ABC):
     @abstractmethod
     def shareable_to_learnable(self, shareable: Shareable, fl_ctx: FLContext) -> Learnable:
         pass
+
+
+class DXOFilter(FLComponent, ABC):
+    """DXO-level filter (dxo_filter.py:26-140, without the job-audit event)."""
+
+    def __init__(self, supported_data_kinds=None, data_kinds_to_filter=None):
+        super().__init__()
+        if supported_data_kinds and not isinstance(supported_data_kinds, list):
+            raise ValueError(f"supported_data_kinds must be a list of str but got {type(supported_data_kinds)}")
+        if data_kinds_to_filter and not isinstance(data_kinds_to_filter, list):
+            raise ValueError(f"data_kinds_to_filter must be a list of str but got {type(data_kinds_to_filter)}")
+        if supported_data_kinds and data_kinds_to_filter:
+            if not all(dk in supported_data_kinds for dk in data_kinds_to_filter):
+                raise ValueError(f"invalid data kinds: {data_kinds_to_filter}. Only support {supported_data_kinds}")
+        self.data_kinds = data_kinds_to_filter or supported_data_kinds
+
+    def process(self, shareable: Shareable, fl_ctx: FLContext):
+        if shareable.get_return_code() != ReturnCode.OK:
+            return shareable
+        try:
+            dxo = from_shareable(shareable)
+        except Exception:
+            return shareable
+        if dxo.data is None:
+            return shareable
+        start = [dxo]
+        self._filter_dxos(start, shareable, fl_ctx)
+        return start[0].update_shareable(shareable)
+
+    @abstractmethod
+    def process_dxo(self, dxo: DXO, shareable: Shareable, fl_ctx: FLContext):
+        pass
+
+    def _apply_filter(self, dxo: DXO, shareable, fl_ctx) -> DXO:
+        if not dxo.data:
+            return dxo
+        result = self.process_dxo(dxo, shareable, fl_ctx)
+        if not result:
+            return dxo
+        if not isinstance(result, DXO):
+            raise RuntimeError(f"Result from {self.__class__.__name__} is {type(result)} - must be DXO")
+        if result is not dxo:
+            result.add_filter_history(dxo.get_filter_history())
+        result.add_filter_history(self.__class__.__name__)
+        return result
+
+    def _filter_dxos(self, coll, shareable, fl_ctx):
+        items = list(enumerate(coll)) if isinstance(coll, list) else list(coll.items())
+        for k, v in items:
+            if not isinstance(v, DXO):
+                continue
+            if v.data_kind == DataKind.COLLECTION:
+                self._filter_dxos(v.data, shareable, fl_ctx)
+            elif not self.data_kinds or v.data_kind in self.data_kinds:
+                coll[k] = self._apply_filter(v, shareable, fl_ctx)

@@ -839,6 +839,43 @@ int fedavg_set_tile(fedavg_ctx* ctx, int tile_elems) {
     });
 }
 
+int fedavg_dequantize(fedavg_ctx* ctx, const fedavg_quant* qs, const void* q, size_t n, float* out_base,
+                      size_t tile_elems, size_t tile_stride, size_t logical_offset) {
+    return guarded([&] {
+        if (!ctx || !qs) throw Error("NULL argument");
+        if (n == 0) return;
+        if (!q || !out_base) throw Error("q / out_base is NULL");
+        if (qs->qtype < FEDAVG_Q_F16 || qs->qtype > FEDAVG_Q_ADA_U16) throw Error("bad qtype");
+        const bool blocked = qs->qtype == FEDAVG_Q_BLOCKWISE8 || qs->qtype == FEDAVG_Q_FP4 || qs->qtype == FEDAVG_Q_NF4;
+        if (blocked && (!qs->absmax || qs->blocksize == 0 || qs->blocksize % 4))
+            throw Error("blocked formats need absmax and a blocksize that is a positive multiple of 4");
+        if (qs->qtype == FEDAVG_Q_BLOCKWISE8 && !qs->code) throw Error("blockwise8 needs code");
+        if (qs->qtype >= FEDAVG_Q_ADA_U8 && qs->has_norm && !(qs->level > 0.0)) throw Error("adaquant needs level > 0");
+        if (tile_elems == 0) tile_elems = tile_stride = (logical_offset + n + 3) / 4 * 4;
+        if (tile_stride < tile_elems || tile_elems % 4 || tile_stride % 4 || logical_offset % 4)
+            throw Error("tile_elems, tile_stride and logical_offset must be multiples of 4, stride >= tile");
+        if (reinterpret_cast<uintptr_t>(out_base) % 16) throw Error("out_base must be 16-byte aligned");
+        ctx->activate();
+        fedavg::DequantLaunch L;
+        L.qtype = qs->qtype;
+        L.q = q;
+        L.n = (int64_t)n;
+        L.absmax = qs->absmax;
+        L.code = qs->code;
+        L.blocksize = blocked ? (int64_t)qs->blocksize : 1;
+        L.norm = qs->norm;
+        L.level = qs->level;
+        L.offset = qs->offset;
+        L.has_norm = qs->has_norm;
+        L.out = out_base;
+        L.tile = (int64_t)tile_elems;
+        L.tstride = (int64_t)tile_stride;
+        L.elem0 = (int64_t)logical_offset;
+        L.grid = stream_grid(ctx, ((int64_t)n + 3) / 4);
+        HIP_CHECK(fedavg::launch_dequant_f32(L, ctx->compute()));
+    });
+}
+
 int fedavg_fill_synthetic_f32(fedavg_ctx* ctx, float* dst, size_t n, size_t tile_elems, size_t tile_stride,
                               uint64_t seed, uint64_t row, uint64_t col0) {
     return guarded([&] {

@@ -63,7 +63,22 @@ struct EpiParams {
     const float* base;
 };
 
+struct DequantLaunch {
+    int qtype;
+    const void* q;
+    int64_t n;
+    const float* absmax;
+    const float* code;
+    int64_t blocksize;
+    double norm, level, offset;
+    int has_norm;
+    float* out;
+    int64_t tile, tstride, elem0;
+    int grid;
+};
+
 hipError_t launch_tiles_f32x4(const TileLaunch& L, hipStream_t s);
+hipError_t launch_dequant_f32(const DequantLaunch& L, hipStream_t s);
 hipError_t launch_tiles_epi_f32x4(const TileLaunch& L, const EpiParams& E, hipStream_t s);
 hipError_t launch_rows_generic(const RowTableGeneric& tab, int K, const void* acc_in, void* out, int64_t n,
                                int in_dtype, int acc_dtype, int op, int fin, double fin_val, int grid,

@@ -269,6 +269,14 @@ class DeviceContext:
     def set_variant(self, variant: int = 0) -> None:
         N.call("fedavg_set_variant", self.handle, ctypes.c_int(variant))
 
+    def dequantize(self, quant: "N.Quant", q_ptr: int, n: int, out_ptr: int, tile: int = 0, tile_stride: int = 0,
+                   logical_offset: int = 0) -> None:
+        """Dequantize n elements of the device payload at q_ptr into fp32 (fedavg_dequantize)."""
+        if n:
+            N.call("fedavg_dequantize", self.handle, ctypes.cast(ctypes.pointer(quant), ctypes.c_void_p),
+                   ctypes.c_void_p(q_ptr), ctypes.c_size_t(n), ctypes.c_void_p(out_ptr), ctypes.c_size_t(tile),
+                   ctypes.c_size_t(tile_stride), ctypes.c_size_t(logical_offset))
+
     def fill_synthetic_f32(self, dst_ptr: int, n: int, seed: int, row: int, col0: int = 0, tile: int = 0,
                            tile_stride: int = 0) -> None:
         N.call("fedavg_fill_synthetic_f32", self.handle, ctypes.c_void_p(dst_ptr), ctypes.c_size_t(n),

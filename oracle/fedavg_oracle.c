@@ -27,6 +27,7 @@
 #include <math.h>
 #include <stddef.h>
 #include <stdint.h>
+#include <string.h>
 
 #ifdef _OPENMP
 #include <omp.h>
@@ -178,5 +179,90 @@ void oracle_epilogue_apply(const float* delta, size_t n, const oracle_epilogue* 
             v[i] = vv;
             p[i] = pv;
         }
+    }
+}
+
+/* ------------------------------------------------------------------------------------------------
+ * Dequantisation, nvflare/app_opt/pt/quantization/dequantizer.py:47-185.
+ *   float16     fp16 -> fp32 (exact widening)                                     :98-100, :168-173
+ *   blockwise8  code[q[i]] * absmax[i / blocksize]          bitsandbytes dequantize_blockwise (kernel
+ *               kDequantizeBlockwise, General8bit: one fp32 multiply)
+ *   float4      (fp4(nib) * absmax[i / blocksize]) * sign   bitsandbytes dDequantizeFP4Tree
+ *   normfloat4  nf4(nib) * absmax[i / blocksize]            bitsandbytes dDequantizeNF4
+ *               byte k: element 2k = high nibble, 2k+1 = low nibble
+ *   adaquant    (float)(((double)q * norm) / level - offset)   ada_quant.py:76-87 (+ .float(), :168-173)
+ * bitsandbytes is third-party (setup.cfg:74, unpinned) and absent here: its published arithmetic is
+ * restated; "parity unpinned" for blockwise8 / float4 / normfloat4.
+ * ------------------------------------------------------------------------------------------------ */
+enum { ORACLE_Q_F16 = 1, ORACLE_Q_BF16 = 2, ORACLE_Q_BLOCKWISE8 = 3, ORACLE_Q_FP4 = 4, ORACLE_Q_NF4 = 5,
+       ORACLE_Q_ADA_U8 = 6, ORACLE_Q_ADA_U16 = 7 };
+
+static const float oracle_nf4[16] = {-1.0f, -0.6961928009986877f, -0.5250730514526367f, -0.39491748809814453f,
+                                     -0.28444138169288635f, -0.18477343022823334f, -0.09105003625154495f, 0.0f,
+                                     0.07958029955625534f, 0.16093020141124725f, 0.24611230194568634f,
+                                     0.33791524171829224f, 0.44070982933044434f, 0.5626170039176941f,
+                                     0.7229568362236023f, 1.0f};
+static const float oracle_fp4[8] = {0.0f, 5.208333333e-03f, 0.66666667f, 1.0f, 0.33333333f, 0.5f, 0.16666667f, 0.25f};
+
+static float oracle_half_to_float(uint16_t h) {
+    const uint32_t sign = (uint32_t)(h >> 15) << 31;
+    uint32_t e = (h >> 10) & 0x1f, m = h & 0x3ff;
+    uint32_t bits;
+    if (e == 0) {
+        if (m == 0) {
+            bits = sign;
+        } else { /* subnormal half: normalise */
+            int sh = 0;
+            while (!(m & 0x400)) { m <<= 1; ++sh; }
+            m &= 0x3ff;
+            bits = sign | ((uint32_t)(127 - 15 + 1 - sh) << 23) | (m << 13);
+        }
+    } else if (e == 31) {
+        bits = sign | 0x7f800000u | (m << 13);
+    } else {
+        bits = sign | ((e + 127 - 15) << 23) | (m << 13);
+    }
+    float f;
+    memcpy(&f, &bits, 4);
+    return f;
+}
+
+void oracle_dequantize(int qtype, const void* q, size_t n, const float* absmax, const float* code, size_t blocksize,
+                       double norm, double level, double offset, int has_norm, float* out) {
+    const uint8_t* q8 = (const uint8_t*)q;
+    const uint16_t* q16 = (const uint16_t*)q;
+    for (size_t i = 0; i < n; ++i) {
+        float v;
+        switch (qtype) {
+            case ORACLE_Q_F16: v = oracle_half_to_float(q16[i]); break;
+            case ORACLE_Q_BF16: {
+                const uint32_t b = (uint32_t)q16[i] << 16;
+                memcpy(&v, &b, 4);
+                break;
+            }
+            case ORACLE_Q_BLOCKWISE8: v = code[q8[i]] * absmax[i / blocksize]; break;
+            case ORACLE_Q_FP4:
+            case ORACLE_Q_NF4: {
+                const unsigned byte = q8[i >> 1];
+                const unsigned nib = (i & 1) ? (byte & 15u) : (byte >> 4);
+                const float am = absmax[i / blocksize];
+                if (qtype == ORACLE_Q_NF4) {
+                    v = oracle_nf4[nib] * am;
+                } else {
+                    const float sign = (nib & 8u) ? -1.0f : 1.0f;
+                    v = (oracle_fp4[nib & 7u] * am) * sign;
+                }
+                break;
+            }
+            default: { /* adaquant */
+                if (!has_norm) {
+                    v = (float)(0.0 - offset);
+                } else {
+                    const double x = qtype == ORACLE_Q_ADA_U8 ? (double)q8[i] : (double)q16[i];
+                    v = (float)((x * norm) / level - offset);
+                }
+            }
+        }
+        out[i] = v;
     }
 }

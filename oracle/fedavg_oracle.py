@@ -223,3 +223,25 @@ def epilogue_apply(delta, kind, p=None, m=None, v=None, base=None, **hp):
 
     fn(delta.ctypes.data, delta.size, ctypes.byref(e), ptr(p), ptr(m), ptr(v), ptr(base), out.ctypes.data)
     return out if kind in (EPI_NONE, EPI_ADD_BASE) else p
+
+
+# ---------------------------------------------------------------------------------------------------
+# dequantisation (row f4): see oracle_dequantize in fedavg_oracle.c
+# ---------------------------------------------------------------------------------------------------
+Q_F16, Q_BF16, Q_BLOCKWISE8, Q_FP4, Q_NF4, Q_ADA_U8, Q_ADA_U16 = 1, 2, 3, 4, 5, 6, 7
+
+
+def dequantize(qtype, q, n, absmax=None, code=None, blocksize=0, norm=0.0, level=1.0, offset=0.0, has_norm=True):
+    """Dequantize n elements of payload q (numpy) into a new float32 array."""
+    lib = load()
+    fn = lib.oracle_dequantize
+    fn.restype = None
+    fn.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
+                   ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_int, ctypes.c_void_p]
+    q = np.ascontiguousarray(q)
+    out = np.empty(n, np.float32)
+    am = None if absmax is None else np.ascontiguousarray(absmax, dtype=np.float32)
+    cd = None if code is None else np.ascontiguousarray(code, dtype=np.float32)
+    fn(int(qtype), q.ctypes.data, int(n), None if am is None else am.ctypes.data, None if cd is None else cd.ctypes.data,
+       int(blocksize), float(norm), float(level), float(offset), int(bool(has_norm)), out.ctypes.data)
+    return out
