@@ -23,6 +23,7 @@ import threading
 from typing import Any, Callable, Dict, Optional, Set
 
 from ...engine import DeviceFedAvg, is_device_array, is_torch_tensor
+from ...quantized import QuantizedPayload
 from ...sharding import ShardedFedAvg
 
 
@@ -166,8 +167,13 @@ class WeightedAggregationHelper(object):
                     continue
                 self.key_contribution_counts[k] = self.key_contribution_counts.get(k, 0) + 1
                 materialize = getattr(v, "materialize", None)
-                if callable(materialize):  # lazy disk-offloaded refs (weighted_aggregation_helper.py:170-175)
+                device_quantized = isinstance(v, QuantizedPayload) and not isinstance(self._engine, ShardedFedAvg)
+                if callable(materialize) and not device_quantized:
+                    # lazy disk-offloaded refs (weighted_aggregation_helper.py:170-175); quantized payloads
+                    # stay compressed until the engine dequantizes them into their slot
                     v = materialize()
+                if isinstance(v, QuantizedPayload) and isinstance(self.total.get(k), _HostValue):
+                    v = v.materialize()
                 if is_device_array(v) and not isinstance(self.total.get(k), _HostValue):
                     device_items.append((k, v))
                 else:

@@ -36,6 +36,7 @@ import numpy as np
 
 from . import _native as N
 from .device import DeviceBuffer, DeviceContext, TiledLayout, fedavg_dtype
+from .quantized import QuantizedPayload, stager
 
 try:
     import torch
@@ -64,12 +65,20 @@ def is_torch_tensor(v) -> bool:
 def is_device_array(v) -> bool:
     """Arrays/tensors take the HIP path; everything else (python numbers, opaque objects such as HE
     ciphertexts) follows the reference's object protocol on the host."""
-    return isinstance(v, np.ndarray) or is_torch_tensor(v)
+    return isinstance(v, (np.ndarray, QuantizedPayload)) or is_torch_tensor(v)
+
+
+def _type_proxy(v):
+    """An empty array / tensor with the container and dtype a QuantizedPayload dequantizes to."""
+    if isinstance(v, QuantizedPayload):
+        return torch.empty(0, dtype=v.dtype) if v.container == "torch" else np.empty(0, v.out_dtype)
+    return v
 
 
 def _resolve_types(v, weight, weighted: bool) -> Tuple[str, np.dtype, np.dtype, int, int]:
     """(container, input dtype, accumulator/result dtype, op, fin) as the reference's numpy / torch
     arithmetic would produce them (weighted_aggregation_helper.py:181-216, :233-236)."""
+    v = _type_proxy(v)
     if is_torch_tensor(v):
         tdt = v.dtype
         if tdt not in _TORCH_TO_NP:
@@ -355,6 +364,10 @@ class DeviceFedAvg:
 
     def add(self, items: List[Tuple[str, Any]], weight, weighted: bool) -> None:
         """Stage one contribution's device-path arrays (already filtered by exclude_vars)."""
+        # quantized payloads dequantize on the device straight into their fp32 slot; other dtypes take
+        # the generic path from their (device-dequantized) host values
+        items = [(k, v.materialize() if isinstance(v, QuantizedPayload) and v.out_dtype != np.float32 else v)
+                 for k, v in items]
         with self.lock, self.ctx.lock:
             self._check_torch_alpha(items, weight, weighted)
             states = [(self._register_key(k, v, weight, weighted), v) for k, v in items]
@@ -367,7 +380,14 @@ class DeviceFedAvg:
                 slot = self._acquire_slot(extent)
                 lay = slot.slab.layout
                 host_pieces, keep = [], []
+                quantized = []
                 for st, v in sorted(arena_items, key=lambda x: x[0].offset):
+                    if isinstance(v, QuantizedPayload):
+                        quantized.append((st, v))
+                        st.pending.append(_Staged(weight, slot=slot))
+                        slot.refs += 1
+                        self.stats["h2d_bytes"] += v.nbytes
+                        continue
                     src, ptr, nbytes, on_dev = self._source(v)
                     if on_dev:
                         self.ctx.d2d_tiled(slot.base, lay.tile * 4, lay.tile_stride * 4, st.offset * 4, ptr, nbytes)
@@ -380,6 +400,8 @@ class DeviceFedAvg:
                 # every host key of this client in one pass through the pinned ring (one DMA per 64 MiB)
                 self.ctx.h2d_tiled_multi(slot.base, lay.tile * 4, lay.tile_stride * 4, host_pieces)
                 del keep
+                for st, v in quantized:  # compressed bytes over PCIe, fp32 written into the slot by the GPU
+                    stager().dequantize_into(self.ctx, v, slot.base, lay.tile, lay.tile_stride, st.offset)
             for st, v in states:
                 if st.arena or st.n == 0:
                     if st.n == 0:

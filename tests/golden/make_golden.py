@@ -16,12 +16,13 @@ Reference code exercised:
   nvflare/app_common/workflows/fedavg.py:268-366      (``--set fedavg``: built-in in-time FedAvg cases)
   nvflare/app_opt/pt/fedopt.py:157-270                 (``--set fedopt``: PTFedOptModelShareableGenerator, CPU)
   nvflare/app_common/shareablegenerators/full_model_shareable_generator.py:37-83  (``--set fedopt``)
+  nvflare/app_opt/pt/quantization/ada_quant.py:39-87  (``--set quant``: AdaQuantizer quantize / dequantized)
   nvflare/app_common/aggregators/intime_accumulate_model_aggregator.py   (intime cases)
   nvflare/app_common/aggregators/dxo_aggregator.py:71-191
 
-Usage:  python tests/golden/make_golden.py [--ref /root/reference] [--set helper|fedavg|fedopt]
+Usage:  python tests/golden/make_golden.py [--ref /root/reference] [--set helper|fedavg|fedopt|quant]
         (helper -> helper_cases.{npz,json}; fedavg -> fedavg_cases.{npz,json};
-         fedopt -> fedopt_cases.{npz,json})
+         fedopt -> fedopt_cases.{npz,json}; quant -> quant_cases.{npz,json})
 """
 
 from __future__ import annotations
@@ -373,10 +374,50 @@ def main_fedopt():
     print(f"wrote {len(cases)} fedopt cases, {len(store.arrays)} arrays")
 
 
+def main_quant():
+    """AdaQuantizer round trips from the reference (ada_quant.py imports only bz2 / numpy / torch; the
+    bitsandbytes formats cannot be produced here -- bitsandbytes is not installed)."""
+    from nvflare.app_opt.pt.quantization.ada_quant import AdaQuantizer
+
+    rng = np.random.default_rng(20261018)
+    store = Store()
+    cases = []
+    inputs = {
+        "normal_4099": rng.standard_normal(4099).astype(np.float32),
+        "normal_2d": rng.standard_normal((33, 130)).astype(np.float32),
+        "wide_range_u16": (rng.standard_normal(5000) * 300.0).astype(np.float32),
+        "constant": np.full((7, 3), 0.625, np.float32),
+        "compressible": np.repeat(rng.standard_normal(16).astype(np.float32), 512),
+        "tiny": rng.standard_normal(5).astype(np.float32),
+    }
+    for name, arr in inputs.items():
+        for compression in (True, False):
+            q, st = AdaQuantizer(compression=compression).quantize(torch.from_numpy(arr.copy()))
+            qt = q if isinstance(q, torch.Tensor) else torch.as_tensor(q)  # dequantizer.py:150-153
+            deq = AdaQuantizer().dequantized(qt, st) if st else qt
+            out = deq.float().numpy() if isinstance(deq, torch.Tensor) else np.asarray(deq, np.float32)
+            rec_state = {}
+            for k, v in st.items():
+                if isinstance(v, np.ndarray):
+                    rec_state[k] = {"array": store.put(v, "qs")}
+                else:
+                    rec_state[k] = v
+            qv = q.numpy() if isinstance(q, torch.Tensor) else np.asarray(q)
+            cases.append({"kind": "adaquant", "name": f"{name}_{'bz2' if compression else 'raw'}",
+                          "input": store.put(arr, "in"), "quantized": store.put(qv, "q"),
+                          "quantized_dtype": str(qv.dtype), "quant_state": rec_state,
+                          "expected": store.put(out, "out")})
+    np.savez_compressed(os.path.join(HERE, "quant_cases.npz"), **store.arrays)
+    with open(os.path.join(HERE, "quant_cases.json"), "w") as f:
+        json.dump({"generator": "tests/golden/make_golden.py --set quant", "reference": "NVFlare (/root/reference, ~2.9.0-dev)",
+                   "numpy": np.__version__, "torch": torch.__version__, "cases": cases}, f, indent=1, default=str)
+    print(f"wrote {len(cases)} quant cases, {len(store.arrays)} arrays")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ref", default="/root/reference")
-    ap.add_argument("--set", choices=["helper", "fedavg", "fedopt"], default="helper")
+    ap.add_argument("--set", choices=["helper", "fedavg", "fedopt", "quant"], default="helper")
     args = ap.parse_args()
     install_shim(args.ref)
     torch.set_num_threads(8)
@@ -384,6 +425,8 @@ def main():
         return main_fedavg()
     if args.set == "fedopt":
         return main_fedopt()
+    if args.set == "quant":
+        return main_quant()
 
     rng = np.random.default_rng(20261015)
     random.seed(20261015)

@@ -143,3 +143,18 @@ def adam_param_tolerance(p0, p_ref, lr, steps):
     """|p - p_torch| bound for Adam params (torch CPU's MKL sqrt is not correctly rounded; see
     tests/test_fedopt_oracle.py): steps * spacing(max(|p0|, |p_torch|, lr))."""
     return steps * np.spacing(np.maximum(np.maximum(np.abs(p0), np.abs(p_ref)), np.float32(lr))).astype(np.float64)
+
+
+def load_quant_golden():
+    """AdaQuantizer round trips of the reference (make_golden.py --set quant)."""
+    if "q" not in _cache:
+        with open(os.path.join(GOLDEN_DIR, "quant_cases.json")) as f:
+            meta = json.load(f)
+        arrays = dict(np.load(os.path.join(GOLDEN_DIR, "quant_cases.npz"), allow_pickle=False))
+        _cache["q"] = (meta, arrays)
+    return _cache["q"]
+
+
+def adaquant_state(case, arrays):
+    """The case's quant_state with its arrays restored."""
+    return {k: (arrays[v["array"]] if isinstance(v, dict) else v) for k, v in case["quant_state"].items()}
