@@ -203,8 +203,8 @@ int fedavg_timing_end(fedavg_ctx* ctx, float* ms);
  * are issued together (4 or 8, default 4). */
 int fedavg_set_launch(fedavg_ctx* ctx, int blocks_per_cu, int unroll);
 /* Streaming-kernel cache policy: bit 0 = temporal (cached) client loads, bit 1 = temporal result stores
- * (default 0: both nontemporal -- every byte is touched once); bit 2 = epilogue kernel prefetches its
- * operands (base / p / m / v) at tile start instead of loading them after the client loop. */
+ * (default 0: both nontemporal -- every byte is touched once); bit 2 = epilogue kernel software-pipelined
+ * across tiles (the next tile's first client loads overlap the epilogue). */
 int fedavg_set_variant(fedavg_ctx* ctx, int variant);
 /* Tile width used by fedavg_accumulate for contiguous rows (default 4096 elements). */
 int fedavg_set_tile(fedavg_ctx* ctx, int tile_elems);

@@ -21,7 +21,7 @@ constexpr int kDefaultUnroll = 4;       // clients whose loads are in flight tog
 // variant bits (fedavg_set_variant)
 constexpr int kVariantTemporalLoads = 1;
 constexpr int kVariantTemporalStores = 2;
-constexpr int kVariantEpiPrefetch = 4;  // epilogue kernel: prefetch base/p/m/v at tile start (default: after the client loop)
+constexpr int kVariantEpiPrefetch = 4;  // epilogue kernel: software-pipelined across tiles (see fedavg_tiles_epi_f32x4)
 
 // Per-launch client table passed BY VALUE in the kernarg segment: wave-uniform base pointers and
 // weights are loaded with s_load into SGPRs.

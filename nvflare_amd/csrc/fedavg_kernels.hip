@@ -241,7 +241,10 @@ __device__ __forceinline__ void epilogue4(const EpiParams& E, const int64_t i, c
     }
 }
 
-template <int OP, int FIN, bool ACC_IN, int EPI, bool PRE>
+// PIPE: software-pipelined across tiles -- after the client loop of tile t the lane issues the epilogue
+// operand loads of t, then the first UNROLL client loads of its next tile, and only then waits for the
+// operands and runs the epilogue (ALU, three store streams) while the next tile's loads are in flight.
+template <int OP, int FIN, bool ACC_IN, int EPI, bool PIPE>
 __global__ void __launch_bounds__(kBlock) fedavg_tiles_epi_f32x4(const RowTableF32 tab, const int K,
                                                                   const int64_t tstride4, const f32x4* acc_in,
                                                                   f32x4* out, const int64_t b4, const int64_t e4,
@@ -250,17 +253,22 @@ __global__ void __launch_bounds__(kBlock) fedavg_tiles_epi_f32x4(const RowTableF
     constexpr int CPL = kDefaultTile / (4 * kBlock);
     constexpr int64_t T4 = (int64_t)CPL * kBlock;
     const int64_t t_last = (e4 - 1) / T4;
-    for (int64_t t = b4 / T4 + blockIdx.x; t <= t_last; t += gridDim.x) {
+    const int g0 = PIPE ? (K < UNROLL ? K : UNROLL) : 0;  // clients carried over from the previous tile
+    f32x4 nxt[UNROLL][CPL];
+    int64_t t = b4 / T4 + blockIdx.x;
+    if constexpr (PIPE) {
+        if (t <= t_last) {
+            const int64_t off = t * tstride4 + threadIdx.x;
+#pragma unroll
+            for (int j = 0; j < UNROLL; ++j)
+                if (j < g0)
+#pragma unroll
+                    for (int c = 0; c < CPL; ++c) nxt[j][c] = load4<true>(tab.rows[j] + off + c * kBlock);
+        }
+    }
+    for (; t <= t_last; t += gridDim.x) {
         const int64_t off = t * tstride4 + threadIdx.x;
         const int64_t col = t * T4 + threadIdx.x;
-        EpiIn pre[CPL];
-        if constexpr (PRE) {
-#pragma unroll
-            for (int c = 0; c < CPL; ++c) {
-                const int64_t i = col + c * kBlock;
-                if (i >= b4 && i < e4) pre[c] = epi_load<EPI>(E, i);
-            }
-        }
         f32x4 acc[CPL];
         int k = 0;
         if constexpr (ACC_IN) {
@@ -269,11 +277,24 @@ __global__ void __launch_bounds__(kBlock) fedavg_tiles_epi_f32x4(const RowTableF
                 const int64_t i = col + c * kBlock;
                 acc[c] = (i >= b4 && i < e4) ? load4<false>(acc_in + i) : f32x4{0, 0, 0, 0};
             }
-        } else {
+        } else if constexpr (!PIPE) {
             const f32x4* r = tab.rows[0] + off;
 #pragma unroll
             for (int c = 0; c < CPL; ++c) acc[c] = first4<OP>(load4<true>(r + c * kBlock), tab.w[0]);
             k = 1;
+        }
+        if constexpr (PIPE) {  // consume the carried group (clients 0 .. g0-1)
+#pragma unroll
+            for (int j = 0; j < UNROLL; ++j) {
+                if (j < g0) {
+#pragma unroll
+                    for (int c = 0; c < CPL; ++c) {
+                        if (!ACC_IN && j == 0) acc[c] = first4<OP>(nxt[0][c], tab.w[0]);
+                        else acc[c] = step4<OP>(acc[c], nxt[j][c], tab.w[j]);
+                    }
+                }
+            }
+            k = g0;
         }
         for (; k + UNROLL <= K; k += UNROLL) {
             f32x4 v[UNROLL][CPL];
@@ -293,13 +314,29 @@ __global__ void __launch_bounds__(kBlock) fedavg_tiles_epi_f32x4(const RowTableF
 #pragma unroll
             for (int c = 0; c < CPL; ++c) acc[c] = step4<OP>(acc[c], load4<true>(r + c * kBlock), tab.w[k]);
         }
+        EpiIn pre[CPL];
+#pragma unroll
+        for (int c = 0; c < CPL; ++c) {
+            const int64_t i = col + c * kBlock;
+            if (i >= b4 && i < e4) pre[c] = epi_load<EPI>(E, i);
+        }
+        if constexpr (PIPE) {
+            const int64_t tn = t + gridDim.x;
+            if (tn <= t_last) {
+                const int64_t offn = tn * tstride4 + threadIdx.x;
+#pragma unroll
+                for (int j = 0; j < UNROLL; ++j)
+                    if (j < g0)
+#pragma unroll
+                        for (int c = 0; c < CPL; ++c) nxt[j][c] = load4<true>(tab.rows[j] + offn + c * kBlock);
+            }
+        }
 #pragma unroll
         for (int c = 0; c < CPL; ++c) {
             const int64_t i = col + c * kBlock;
             if (i >= b4 && i < e4) {
                 const f32x4 d = fin4<FIN>(acc[c], fin_val);
                 if (out != nullptr && EPI != FEDAVG_EPI_ADD_BASE) store4<true>(out + i, d);
-                if constexpr (!PRE) pre[c] = epi_load<EPI>(E, i);
                 epilogue4<EPI>(E, i, d, pre[c], out);
             }
         }

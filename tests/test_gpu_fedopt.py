@@ -209,3 +209,45 @@ def test_epilogue_on_precomputed_update(ctx, oracle):
         assert same_bits(dev.get("p"), p) and same_bits(dev.get("m"), m) and same_bits(dev.get("v"), v)
     finally:
         dev.close()
+
+
+@pytest.mark.parametrize("variant", [0, 4])
+@pytest.mark.parametrize("K,kind", [(6, 3), (2, 3), (1, 2), (5, 1), (0, 3)])
+def test_epilogue_variants_multi_tile_per_block(ctx, oracle, variant, K, kind):
+    """More tiles than blocks (every block walks several tiles), so the software-pipelined variant carries
+    client loads across tiles; ragged client groups (K % 4 != 0), K = 1 and K = 0 (acc_in only)."""
+    rng = np.random.default_rng(100 + K)
+    n = 1100 * TILE + 12
+    rows = [rng.standard_normal(n).astype(np.float32) for _ in range(K)]
+    ws = [float(1 + (37 * k) % 100) for k in range(K)]
+    acc0 = rng.standard_normal(n).astype(np.float32) if K == 0 else None
+    p = rng.standard_normal(n).astype(np.float32)
+    m = (rng.standard_normal(n) * 0.1).astype(np.float32)
+    v = (rng.random(n) * 0.01).astype(np.float32)
+    base = rng.standard_normal(n).astype(np.float32)
+    hp = dict(lr=1e-3, beta1=0.9, beta2=0.999, eps=1e-8, step=3.0) if kind == 3 else dict(lr=0.5, momentum=0.9)
+    dev = _Dev(ctx, rows, n)
+    ctx.set_variant(variant)
+    try:
+        if kind == 1:
+            out = dev.buf("out")
+            e = _epi(1, base=dev.buf("base", base))
+        else:
+            out = None
+            e = _epi(kind, param=dev.buf("p", p), state1=dev.buf("m", m), state2=dev.buf("v", v), **hp)
+        acc_ptr = dev.buf("acc", acc0) if K == 0 else None
+        fin = 2 if K else 0
+        count = _sum(ws) if K else 1.0
+        ctx.accumulate_tiled_epi(dev.bases, ws, TILE, dev.lay.tile_stride, 0, dev.n4, out, 1, fin, count, e,
+                                 acc_in_ptr=acc_ptr)
+        d = oracle.fedavg_c(rows, ws, oracle.MODE_TORCH, nthreads=8) if K else acc0
+        if kind == 1:
+            assert same_bits(dev.get("out"), oracle.epilogue_apply(d, oracle.EPI_ADD_BASE, base=base))
+        else:
+            oracle.epilogue_apply(d, kind, p=p, m=m, v=v, **hp)
+            assert same_bits(dev.get("p"), p) and same_bits(dev.get("m"), m)
+            if kind == 3:
+                assert same_bits(dev.get("v"), v)
+    finally:
+        ctx.set_variant(0)
+        dev.close()
