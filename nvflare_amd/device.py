@@ -3,6 +3,7 @@
 from __future__ import annotations
 
 import ctypes
+import os
 import threading
 import weakref
 from typing import Dict, Optional, Sequence
@@ -96,7 +97,11 @@ class DeviceContext:
 
     # -- shared per-process handles ------------------------------------------------------------
     @classmethod
-    def get(cls, device: int = 0) -> "DeviceContext":
+    def get(cls, device: Optional[int] = None) -> "DeviceContext":
+        """The process-wide context of a HIP device (None: $NVFLARE_AMD_DEVICE, default 0)."""
+        if device is None:
+            device = int(os.environ.get("NVFLARE_AMD_DEVICE", "0"))
+        device = int(device)
         with cls._instances_lock:
             ctx = cls._instances.get(device)
             if ctx is None:

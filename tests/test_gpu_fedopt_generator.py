@@ -8,7 +8,7 @@ int64 ``num_batches_tracked`` go through the FedAvg ``base + diff`` branch) and 
 round 2 (not stepped that round).
 
 Bar: every SGD output and every non-parameter key bit-exact; Adam parameters within
-``steps * spacing(max(|p0|, |p_torch|, lr))`` (torch CPU's MKL sqrt is not correctly rounded, see
+``2 * steps * spacing(max(|p0|, |p_torch|, lr))`` (torch CPU's MKL sqrt is not correctly rounded, see
 tests/test_fedopt_oracle.py); lr schedule and meta identical."""
 
 import numpy as np
