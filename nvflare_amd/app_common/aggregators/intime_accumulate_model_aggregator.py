@@ -57,16 +57,20 @@ class InTimeAccumulateWeightedAggregator(Aggregator):
         expected_data_kind: Union[DataKind, Dict[str, DataKind]] = DataKind.WEIGHT_DIFF,
         weigh_by_local_iter: bool = True,
         device: Optional[int] = None,
+        defer_result: bool = False,
     ):
         """Accumulated weighted (FedAvg) aggregation on the MI355X.
 
         Args: as the reference (intime_accumulate_model_aggregator.py:48-90), plus ``device``, the HIP
-        device index of the aggregation engine (default $NVFLARE_AMD_DEVICE or 0).
+        device index of the aggregation engine (default $NVFLARE_AMD_DEVICE or 0), and ``defer_result``:
+        the aggregated fp32 values stay in HBM as ``DeferredAggregate`` objects until read, so the device
+        FedOpt generator steps the model in the same launch as the aggregation (nvflare_amd/deferred.py).
         """
         super().__init__()
         self._single_dxo_key = ""
         self._weigh_by_local_iter = weigh_by_local_iter
         self._device = device
+        self._defer_result = defer_result
         self.aggregation_weights = aggregation_weights
         self.exclude_vars = exclude_vars
         self.expected_data_kind = expected_data_kind
@@ -136,6 +140,7 @@ class InTimeAccumulateWeightedAggregator(Aggregator):
                 name_postfix=k,
                 weigh_by_local_iter=self._weigh_by_local_iter,
                 device=self._device,
+                defer_result=self._defer_result,
             )
             for k in self.expected_data_kind
         }

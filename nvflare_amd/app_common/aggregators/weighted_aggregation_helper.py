@@ -116,6 +116,7 @@ class WeightedAggregationHelper(object):
         device: Optional[int] = None,
         max_resident_bytes: Optional[int] = None,
         devices: Optional[list] = None,
+        defer_result: bool = False,
     ):
         """Weighted aggregation on the MI355X (drop-in for weighted_aggregation_helper.py:117-131).
 
@@ -127,11 +128,15 @@ class WeightedAggregationHelper(object):
             max_resident_bytes: HBM budget for staged contributions before they are folded.
             devices: several HIP devices: every key is split into per-device parameter buckets
                 (sharding.ShardedFedAvg; host arrays only), bit-identical to one device.
+            defer_result: ``get_result`` returns the fp32 keys as ``DeferredAggregate`` values that stay
+                in HBM until read (``materialize()`` / ``np.asarray``) or consumed by the device FedOpt
+                generator in the same launch as its optimizer step (nvflare_amd/deferred.py).
         """
         super().__init__()
         self.lock = threading.Lock()
         self.exclude_vars = re.compile(exclude_vars) if exclude_vars else None
         self.weigh_by_local_iter = weigh_by_local_iter
+        self.defer_result = bool(defer_result)
         if devices and len(devices) > 1:
             self._engine = ShardedFedAvg(devices, max_resident_bytes=max_resident_bytes)
         else:
@@ -217,7 +222,12 @@ class WeightedAggregationHelper(object):
     def get_result(self):
         """Divide the weighted sums by the sums of weights (weighted_aggregation_helper.py:226-240)."""
         with self.lock:
-            device_results = self._engine.result() if self._engine.keys else {}
+            if not self._engine.keys:
+                device_results = {}
+            elif self.defer_result and isinstance(self._engine, DeviceFedAvg):
+                device_results = self._engine.result_deferred()
+            else:
+                device_results = self._engine.result()
             aggregated = {}
             for k, v in self.total.items():
                 if isinstance(v, _HostValue):

@@ -24,6 +24,7 @@ from ...compat import (
     from_shareable,
     model_learnable_to_dxo,
 )
+from ...deferred import DeferredAggregate, materialize_deferred
 from ...engine import is_torch_tensor
 from ._device_apply import DeviceAdder
 
@@ -37,14 +38,40 @@ def _fp32_host_view(v):
     return None
 
 
+def _apply_deferred(weights: Dict, diff: Dict, keys) -> list:
+    """Keys whose difference is a pending DeferredAggregate (aggregator ``defer_result=True``) and whose
+    base is an fp32 host array of the same container: aggregated and added in one launch
+    (DeferredRound.fused_apply), so the difference never crosses PCIe.  Returns the keys left to do."""
+    import torch
+
+    by_round = {}
+    for k in keys:
+        d = diff[k]
+        if not isinstance(d, DeferredAggregate) or not d.round.fusable(d.name):
+            continue
+        vb = _fp32_host_view(weights[k])
+        if vb is None or vb[1] != (d.container == "torch"):
+            continue
+        by_round.setdefault(id(d.round), (d.round, {}))[1][d.name] = (k, vb[0], vb[1])
+    done = set()
+    for rnd, items in by_round.values():
+        res = rnd.fused_apply({name: base for name, (_, base, _) in items.items()})
+        for name, r in res.items():
+            k, _, is_torch = items[name]
+            weights[k] = torch.from_numpy(r) if is_torch else r
+            done.add(k)
+    return [k for k in keys if k not in done]
+
+
 def apply_weight_diff(adder: DeviceAdder, weights: Dict, diff: Dict, keys=None) -> Dict:
     """weights[k] = weights[k] + diff[k] for k in keys (default: every key of diff); GPU for fp32 pairs."""
     import torch
 
     keys = list(diff) if keys is None else list(keys)
+    keys = _apply_deferred(weights, diff, keys)
     dev_pairs, dev_keys, dev_torch = [], [], []
     for k in keys:
-        b, d = weights[k], diff[k]
+        b, d = weights[k], materialize_deferred(diff[k])
         vb, vd = _fp32_host_view(b), _fp32_host_view(d)
         if vb is not None and vd is not None and vb[1] == vd[1] and vb[0].shape == vd[0].shape:
             dev_pairs.append((vb[0], vd[0]))

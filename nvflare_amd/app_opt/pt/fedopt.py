@@ -48,7 +48,8 @@ from ...compat import (
     from_shareable,
     make_model_learnable,
 )
-from ...device import DeviceContext
+from ...deferred import DeferredAggregate, FusedEntry, materialize_deferred
+from ...device import DeviceContext, HostArenaPool
 
 _ALIGN = 64  # elements per parameter slot boundary (256 B), as in the aggregation engine
 
@@ -87,7 +88,8 @@ class DeviceServerOptimizer:
 
     Layout: parameter ``j`` occupies ``[offset_j, offset_j + n_j)`` of the flat buffers ``p`` (the live
     parameter storage: ``param.data`` is a view of it), ``m`` (momentum buffer / exp_avg), ``v``
-    (exp_avg_sq) and ``g`` (staged aggregated difference), offsets 256-byte aligned."""
+    (exp_avg_sq) and ``g`` (staged aggregated difference, allocated on first use: a round whose
+    differences are deferred aggregates never needs it), offsets 256-byte aligned."""
 
     def __init__(self, model: torch.nn.Module, optimizer: torch.optim.Optimizer, device: int):
         self.hip_device = device
@@ -128,7 +130,8 @@ class DeviceServerOptimizer:
         self.p = torch.zeros(total, dtype=torch.float32, device=dev)
         self.m = torch.zeros(total, dtype=torch.float32, device=dev)
         self.v = torch.zeros(total, dtype=torch.float32, device=dev)
-        self.g = torch.zeros(total, dtype=torch.float32, device=dev)
+        self.g = None
+        self.host_pool = HostArenaPool()  # host copies of p returned by the generator, reused when released
         with torch.no_grad():
             for s in slots:
                 view = self.p[s.offset:s.offset + s.n].view(s.param.shape)
@@ -189,23 +192,30 @@ class DeviceServerOptimizer:
         return e
 
     def step(self, model_diff: Dict) -> List[str]:
-        """One server step on g = -diff for every parameter named in ``model_diff``; returns their names."""
+        """One server step on g = -diff for every parameter named in ``model_diff``; returns their names.
+
+        Differences that are ``DeferredAggregate`` values of a round still staged on this device are
+        aggregated and stepped in the same launch (``_fused_step``); the others are copied in and stepped
+        with ``K = 0`` (the aggregated difference as ``acc_in``)."""
         groups = self._group_of()
         present = []
+        fused = self._fused_step(model_diff, groups)
         with torch.no_grad():
             for s in self.slots:
-                if s.name not in model_diff:
+                if s.name not in model_diff or s.name in fused:
                     continue
-                d = model_diff[s.name]
+                d = materialize_deferred(model_diff[s.name])
                 t = d.detach() if isinstance(d, torch.Tensor) else torch.as_tensor(np.asarray(d))
                 if t.dtype != torch.float32:  # param.grad = ... would refuse a different dtype
                     raise RuntimeError(f"assigned grad has data of a different type ({t.dtype}) for {s.name!r}")
                 if tuple(t.shape) != tuple(s.param.shape):
                     raise RuntimeError(f"assigned grad has data of a different size for {s.name!r}")
+                if self.g is None:
+                    self.g = torch.zeros_like(self.p)
                 self.g[s.offset:s.offset + s.n].copy_(t.reshape(-1), non_blocking=False)
                 present.append(s)
         if not present:
-            return []
+            return [s.name for s in self.slots if s.name in fused]
         torch.cuda.synchronize(self.torch_device)
         # one launch per run of consecutive stepped parameters sharing group and per-parameter state
         runs: List[Tuple[tuple, List[_Slot]]] = []
@@ -227,12 +237,39 @@ class DeviceServerOptimizer:
                 self.ctx.accumulate_tiled_epi([], [], 4096, 4096, begin, end, None, N.FEDAVG_OP_TORCH,
                                               N.FEDAVG_FIN_NONE, 1.0, e, acc_in_ptr=self.g.data_ptr())
             self.ctx.sync()
-        for s in present:
+        self._advance(present, groups)
+        return [s.name for s in self.slots if s.name in fused or s in present]
+
+    def _advance(self, stepped: List[_Slot], groups: Dict[int, dict]) -> None:
+        for s in stepped:
             s.step += 1.0
             if self.kind == N.FEDAVG_EPI_SGD and groups[id(s.param)].get("momentum", 0.0) != 0.0:
                 s.has_momentum_buffer = True
             self._expose_state(s)
-        return [s.name for s in present]
+
+    def _fused_step(self, model_diff: Dict, groups: Dict[int, dict]) -> set:
+        """Aggregation + optimizer step in one launch for the parameters whose difference is a deferred
+        aggregate on this device (same shape; fp32 by construction).  Returns the names stepped."""
+        cand = {}
+        for s in self.slots:
+            d = model_diff.get(s.name)
+            if isinstance(d, DeferredAggregate) and d.fusable(self.hip_device) and tuple(d.shape) == tuple(s.param.shape):
+                cand.setdefault(id(d.round), (d.round, {}))[1][d.name] = s
+        done = set()
+        if not cand:
+            return done
+        torch.cuda.synchronize(self.torch_device)  # p, m, v written by torch (binding, checkpoint loads)
+        for rnd, by_key in cand.values():
+            entries = {}
+            for key, s in by_key.items():
+                g = groups[id(s.param)]
+                entries[key] = FusedEntry(s.offset, self._epilogue(g, s), (id(g), s.step, s.has_momentum_buffer))
+            names = set(rnd.fused_step(entries))
+            stepped = [s for key, s in by_key.items() if key in names]
+            self.ctx.sync()
+            self._advance(stepped, groups)
+            done.update(s.name for s in stepped)
+        return done
 
 
 class PTFedOptModelShareableGenerator(FullModelShareableGenerator):
@@ -340,14 +377,15 @@ class PTFedOptModelShareableGenerator(FullModelShareableGenerator):
         if base_model_weights:
             preserve_torch = any(isinstance(v, torch.Tensor) for v in base_model_weights.values())
         else:
-            preserve_torch = any(isinstance(v, torch.Tensor) for v in model_diff.values())
+            preserve_torch = any(isinstance(v, torch.Tensor) or (isinstance(v, DeferredAggregate) and v.container == "torch")
+                                 for v in model_diff.values())
 
         start = time.time()
         weights, updated_params = self.server_update(model_diff)
         secs = time.time() - start
 
         start = time.time()
-        weights = self._to_host(weights, preserve_torch)
+        weights = self._to_host(weights, preserve_torch, self._dev_opt)
         secs_detach = time.time() - start
 
         # FedAvg for the keys the optimizer does not own (e.g. batch-norm statistics), fedopt.py:247-263
@@ -356,6 +394,12 @@ class PTFedOptModelShareableGenerator(FullModelShareableGenerator):
         for key in rest:
             base_value = base_model_weights[key] if key in base_model_weights else weights[key]
             value = model_diff[key]
+            if isinstance(value, DeferredAggregate) and (value.container == "torch") == preserve_torch \
+                    and isinstance(base_value, torch.Tensor) == preserve_torch \
+                    and not (isinstance(base_value, torch.Tensor) and base_value.device.type != "cpu"):
+                base[key] = (base_value, value)  # aggregated and added in one launch (apply_weight_diff)
+                continue
+            value = materialize_deferred(value)
             if preserve_torch:
                 base_value = base_value.detach().cpu() if isinstance(base_value, torch.Tensor) else torch.as_tensor(base_value)
                 value = value.detach().cpu() if isinstance(value, torch.Tensor) else torch.as_tensor(value)
@@ -375,10 +419,25 @@ class PTFedOptModelShareableGenerator(FullModelShareableGenerator):
         return make_model_learnable(weights, dxo.get_meta_props())
 
     @staticmethod
-    def _to_host(state: Dict, preserve_torch: bool) -> Dict:
-        """state_dict -> host copies (``.detach().cpu().clone()`` / ``.numpy()``, fedopt.py:238-244)."""
+    def _to_host(state: Dict, preserve_torch: bool, dev: Optional[DeviceServerOptimizer] = None) -> Dict:
+        """state_dict -> host copies (``.detach().cpu().clone()`` / ``.numpy()``, fedopt.py:238-244).
+
+        The parameters live in one flat HBM buffer: it comes back in ONE D2H through the handle's pinned
+        ring (a pageable ``.cpu()`` per tensor is several times slower); each parameter is a view of that
+        fresh host copy, as the aggregation engine's numpy results are views of its host arena."""
         out = {}
+        host_p = None
+        if dev is not None and dev.slots:
+            torch.cuda.synchronize(dev.torch_device)
+            host_p = dev.host_pool.take(dev.p.numel())
+            dev.ctx.d2h(host_p, dev.p.data_ptr())
+        base = dev.p.data_ptr() if host_p is not None else 0
         for k, v in state.items():
+            s = dev.by_name.get(k) if host_p is not None else None
+            if s is not None and v.dtype == torch.float32 and v.is_contiguous() and v.data_ptr() == base + 4 * s.offset:
+                h = host_p[s.offset:s.offset + s.n].reshape(tuple(v.shape))
+                out[k] = torch.from_numpy(h) if preserve_torch else h
+                continue
             h = v.detach().cpu()
             out[k] = h.clone() if preserve_torch else h.numpy()
         return out

@@ -35,7 +35,7 @@ from typing import Any, Dict, List, Optional, Tuple
 import numpy as np
 
 from . import _native as N
-from .device import DeviceBuffer, DeviceContext, TiledLayout, fedavg_dtype
+from .device import DeviceBuffer, DeviceContext, HostArenaPool, TiledLayout, fedavg_dtype
 from .quantized import QuantizedPayload, stager
 
 try:
@@ -166,11 +166,12 @@ _FLT_MAX = float(np.finfo(np.float32).max)
 
 class _KeyState:
     __slots__ = ("name", "shape", "container", "torch_device", "in_np", "acc_np", "op", "fin", "n", "arena",
-                 "offset", "pending", "acc_valid", "acc_buf", "count")
+                 "offset", "pending", "acc_valid", "acc_buf", "count", "done")
 
     def __init__(self):
         self.pending: List[_Staged] = []
         self.acc_valid = False
+        self.done = False  # finalised in the arena by a fused server-optimizer launch (deferred rounds)
         self.acc_buf: Optional[DeviceBuffer] = None
         self.count = None
 
@@ -204,6 +205,8 @@ class DeviceFedAvg:
         self._side_bufs: List[DeviceBuffer] = []
         self._round_clients = 0
         self.peak_clients = 0
+        self._deferred = None  # DeferredRound still holding slots (result_deferred)
+        self._host_pool = HostArenaPool()
         self.stats = {"h2d_bytes": 0, "folds": 0, "launches": 0, "slabs_allocated": 0}
 
     @property
@@ -369,6 +372,7 @@ class DeviceFedAvg:
         items = [(k, v.materialize() if isinstance(v, QuantizedPayload) and v.out_dtype != np.float32 else v)
                  for k, v in items]
         with self.lock, self.ctx.lock:
+            self._settle()
             self._check_torch_alpha(items, weight, weighted)
             states = [(self._register_key(k, v, weight, weighted), v) for k, v in items]
             for _, v in states:
@@ -421,9 +425,11 @@ class DeviceFedAvg:
                 st.count = weight if st.count is None else st.count + weight
 
     # ------------------------------------------------------------------ compute
-    def _runs(self):
+    def _runs(self, keys: Optional[Dict[str, _KeyState]] = None):
         """Arena keys in offset order, grouped into maximal runs with identical launch parameters."""
-        arena = sorted((st for st in self.keys.values() if st.arena and st.n > 0), key=lambda s: s.offset)
+        keys = self.keys if keys is None else keys
+        arena = sorted((st for st in keys.values() if st.arena and st.n > 0 and not st.done),
+                       key=lambda s: s.offset)
         runs = []
         for st in arena:
             sig = (tuple(id(p.slot) for p in st.pending), tuple(p.weight for p in st.pending), st.acc_valid, st.op,
@@ -434,19 +440,31 @@ class DeviceFedAvg:
                 runs.append((sig, [st]))
         return [g for _, g in runs]
 
-    def _launch_run(self, group: List[_KeyState], final: bool) -> None:
+    def _launch_run(self, group: List[_KeyState], final: bool, out: Optional[int] = None,
+                    epi: Optional["N.Epilogue"] = None) -> None:
+        """Launch the kernels for one run of keys into the flat accumulator ``out`` (default: the arena).
+        With ``epi`` the last launch carries the server-optimizer epilogue (deferred rounds)."""
         first, last = group[0], group[-1]
         begin = first.offset
         end = (last.offset + last.n + 3) // 4 * 4  # inside the key's 256-byte aligned extent
         pend = first.pending
         if not pend and not (final and first.acc_valid):
             return
-        out = self.arena_acc.ptr
+        out = self.arena_acc.ptr if out is None else out
         acc_in = out if first.acc_valid else None
         fin = first.fin if final else N.FEDAVG_FIN_NONE
-        if not pend:  # finalise an already folded sum
-            self.ctx.accumulate_tiled([], [], TILE, TILE, begin, end, out, first.op, fin, float(first.count), acc_in)
+
+        def launch(bases, weights, tile, stride, fin_, last_launch):
+            if epi is not None and last_launch:
+                self.ctx.accumulate_tiled_epi(bases, weights, tile, stride, begin, end, out, first.op, fin_,
+                                              float(first.count), epi, acc_in)
+            else:
+                self.ctx.accumulate_tiled(bases, weights, tile, stride, begin, end, out, first.op, fin_,
+                                          float(first.count), acc_in)
             self.stats["launches"] += 1
+
+        if not pend:  # finalise an already folded sum
+            launch([], [], TILE, TILE, fin, True)
             return
         # consecutive contributions staged in slabs of the same geometry go in one launch; a change of
         # geometry chains the next launch through the accumulator (arrival order is preserved)
@@ -458,25 +476,34 @@ class DeviceFedAvg:
                 segs.append([p])
         for i, seg in enumerate(segs):
             lay = seg[0].slot.slab.layout
-            self.ctx.accumulate_tiled([p.slot.base for p in seg], [p.weight for p in seg], lay.tile, lay.tile_stride,
-                                      begin, end, out, first.op, fin if i == len(segs) - 1 else N.FEDAVG_FIN_NONE,
-                                      float(first.count), acc_in)
+            last_launch = i == len(segs) - 1
+            launch([p.slot.base for p in seg], [p.weight for p in seg], lay.tile, lay.tile_stride,
+                   fin if last_launch else N.FEDAVG_FIN_NONE, last_launch)
             acc_in = out
-            self.stats["launches"] += 1
 
-    def _launch_arena(self, final: bool) -> None:
-        if not any(st.arena and st.n > 0 for st in self.keys.values()):
+    def _launch_arena(self, final: bool, keys: Optional[Dict[str, _KeyState]] = None,
+                      out: Optional[int] = None) -> None:
+        keys = self.keys if keys is None else keys
+        if not any(st.arena and st.n > 0 and not st.done for st in keys.values()):
             return
-        self._ensure_arena_acc()
-        for group in self._runs():
-            self._launch_run(group, final)
-            for st in group:
-                for p in st.pending:
-                    p.slot.refs -= 1
-                    if p.slot.refs == 0:
-                        self._release_slot(p.slot)
-                st.pending = []
-                st.acc_valid = True
+        if out is None:
+            self._ensure_arena_acc()
+        for group in self._runs(keys):
+            self._launch_run(group, final, out)
+            self._consume(group)
+            if final:
+                for st in group:
+                    st.done = True
+
+    def _consume(self, group: List[_KeyState]) -> None:
+        """The group's staged slots are folded into its accumulator: drop them (recycle at refs == 0)."""
+        for st in group:
+            for p in st.pending:
+                p.slot.refs -= 1
+                if p.slot.refs == 0:
+                    self._release_slot(p.slot)
+            st.pending = []
+            st.acc_valid = True
 
     def _launch_side(self, final: bool) -> None:
         for st in self.keys.values():
@@ -515,15 +542,55 @@ class DeviceFedAvg:
     def result(self) -> Dict[str, Any]:
         """Finalise every key on the device and return host (or device-tensor) results."""
         with self.lock, self.ctx.lock:
+            self._settle()
             self._launch_arena(final=True)
             self._launch_side(final=True)
             host_arena = None
             if self.layout_elems and any(st.arena and st.n > 0 and st.torch_device is None for st in self.keys.values()):
-                host_arena = np.empty(self.layout_elems, dtype=np.float32)
+                host_arena = self._host_pool.take(self.layout_elems)
                 self.ctx.d2h(host_arena, self.arena_acc.ptr)
             else:
                 self.ctx.sync()
             return {name: self._materialize(st, host_arena) for name, st in self.keys.items()}
+
+    def result_deferred(self) -> Dict[str, Any]:
+        """``result()`` with the fp32 arena keys left on the device: they come back as ``DeferredAggregate``
+        values (nvflare_amd/deferred.py) whose aggregation runs when one is materialised -- or inside a
+        server-optimizer launch (``DeferredRound.fused_step``), so the aggregated difference never crosses
+        PCIe.  Other keys are finalised now, as in ``result()``.  The round keeps its slots until it is
+        settled: by the fused step, by a materialisation, or by the next ``add`` / ``result``."""
+        from .deferred import DeferredAggregate, DeferredRound
+
+        with self.lock, self.ctx.lock:
+            self._settle()
+            self._launch_side(final=True)
+            self.ctx.sync()
+            deferred = {n: st for n, st in self.keys.items() if st.arena and st.n > 0}
+            eager = {n: self._materialize(st, None) for n, st in self.keys.items() if n not in deferred}
+            if not deferred:
+                return eager
+            self._ensure_arena_acc()
+            acc, self.arena_acc = self.arena_acc, None  # the round owns this accumulator from now on
+            rnd = DeferredRound(self, deferred, acc)
+            self._deferred = rnd
+            return {n: eager[n] if n in eager else DeferredAggregate(rnd, n) for n in self.keys}
+
+    def _settle(self) -> None:
+        """Finish an outstanding deferred round on the device (its values stay readable) and recycle its
+        slots.  Called before anything else touches the slabs."""
+        rnd, self._deferred = self._deferred, None
+        if rnd is not None:
+            rnd.settle()
+            self._consolidate()
+
+    def _consolidate(self) -> None:
+        if self._live_slots or self._deferred is not None:
+            return
+        if len(self.slabs) > 1 and not self.slab_slots:
+            # a round needed several slabs: next round gets one slab of the observed client count
+            for s in self.slabs:
+                s.buf.close()
+            self.slabs.clear()
 
     def _materialize(self, st: _KeyState, host_arena):
         if st.n == 0:
@@ -558,25 +625,25 @@ class DeviceFedAvg:
             self.layout_elems = 0
             return
         with self.lock, self.ctx.lock:
-            for slot in list(self._live_slots):
-                self._release_slot(slot)
+            if self._deferred is None:  # a deferred round keeps its slots until it is settled
+                for slot in list(self._live_slots):
+                    self._release_slot(slot)
             for b in self._side_bufs:
                 b.close()
             self._side_bufs.clear()
             for st in self.keys.values():
                 if st.acc_buf is not None:
                     st.acc_buf.close()
-            if len(self.slabs) > 1 and not self.slab_slots:
-                # a round needed several slabs: next round gets one slab of the observed client count
-                for s in self.slabs:
-                    s.buf.close()
-                self.slabs.clear()
+            self._consolidate()
             self.keys.clear()
             self.layout_elems = 0
 
     def release(self) -> None:
         """Free every device buffer held by this engine."""
         with self.lock:
+            if self._ctx is not None:
+                with self.ctx.lock:
+                    self._settle()
             self.reset()
             for s in self.slabs:
                 s.buf.close()
