@@ -34,6 +34,15 @@ enum fedavg_dtype {
     FEDAVG_F64 = 1,
     FEDAVG_I32 = 2,
     FEDAVG_I64 = 3,
+    FEDAVG_F16 = 4,  /* IEEE binary16 (numpy float16 / torch.float16) */
+    FEDAVG_BF16 = 5, /* bfloat16 (torch.bfloat16) */
+    FEDAVG_U8 = 6,
+    FEDAVG_I8 = 7,
+    FEDAVG_I16 = 8,
+    FEDAVG_BOOL = 9, /* one byte, 0 or 1 */
+    FEDAVG_U16 = 10,
+    FEDAVG_U32 = 11,
+    FEDAVG_U64 = 12,
 };
 
 /* per-step arithmetic, reference weighted_aggregation_helper.py:
@@ -156,7 +165,14 @@ int fedavg_sync(fedavg_ctx* ctx);
  * acc_in may equal out (in-place continuation).  Any k_rows >= 0 (k_rows == 0 needs acc_in).
  * Supported (in_dtype, acc_dtype): (F32,F32) streaming fast path (16-byte aligned pointers; whole tiles
  * of fedavg_set_tile elements, the ragged tail and unaligned rows take a scalar kernel); (F64,F64);
- * (F32,F64); (I32|I64, F32); (I32|I64, F64). */
+ * (F32|F16,F64); (F16,F32); (I32|I64, F32|F64); (U8|I8|I16|BOOL, F32|F64); (U16|U32|U64, F64).
+ * 16-bit accumulators, (F16,F16) and (BF16,BF16), run the reference's reduced-precision sequence in fp32
+ * registers with a rounding to the 16-bit format after every reference operation:
+ *   NUMPY (float16 arrays, NEP 50: w -> half(w) from fp64):  first h(v*w)   step h(T + h(v*w))   SCALE h(T*half(1/count))
+ *   TORCH (CPU vectorised path: mul/div in fp32 with the scalar as float, add_ alpha rounded to the format):
+ *                                   first r(v*float(w))   step r(fma(v, r(w), T))   DIV r(T/float(count))
+ *   UNWEIGHTED                      first v               step r(T + v)
+ * (weighted_aggregation_helper.py:181-236 with float16 / bfloat16 values). */
 int fedavg_accumulate(fedavg_ctx* ctx, const void* const* rows, const double* weights, int k_rows,
                       const void* acc_in, void* out, size_t n, int in_dtype, int acc_dtype, int op,
                       int fin, double count);

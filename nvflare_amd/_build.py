@@ -14,7 +14,7 @@ CSRC = os.path.join(PKG, "csrc")
 LIB_DIR = os.path.join(PKG, "lib")
 LIB_NAME = "libnvflare_amd_fedavg.so"
 LIB_PATH = os.path.join(LIB_DIR, LIB_NAME)
-SOURCES = ["fedavg_kernels.hip", "fedavg_dequant.hip", "fedavg_capi.cpp"]
+SOURCES = ["fedavg_kernels.hip", "fedavg_narrow.hip", "fedavg_dequant.hip", "fedavg_capi.cpp"]
 HEADERS = ["fedavg_internal.h"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"

@@ -23,6 +23,15 @@ FEDAVG_F32 = 0
 FEDAVG_F64 = 1
 FEDAVG_I32 = 2
 FEDAVG_I64 = 3
+FEDAVG_F16 = 4
+FEDAVG_BF16 = 5
+FEDAVG_U8 = 6
+FEDAVG_I8 = 7
+FEDAVG_I16 = 8
+FEDAVG_BOOL = 9
+FEDAVG_U16 = 10
+FEDAVG_U32 = 11
+FEDAVG_U64 = 12
 
 FEDAVG_OP_NUMPY = 0
 FEDAVG_OP_TORCH = 1

@@ -60,7 +60,61 @@ constexpr size_t kParallelCopyMin = 8ull << 20;
 constexpr int kCopyThreads = 8;
 
 void check_dtype(int dt) {
-    if (dt < FEDAVG_F32 || dt > FEDAVG_I64) throw Error("unknown dtype " + std::to_string(dt));
+    if (dt < FEDAVG_F32 || dt > FEDAVG_U64) throw Error("unknown dtype " + std::to_string(dt));
+}
+
+size_t dtype_size(int dt) {
+    switch (dt) {
+        case FEDAVG_F64:
+        case FEDAVG_I64:
+        case FEDAVG_U64:
+            return 8;
+        case FEDAVG_F32:
+        case FEDAVG_I32:
+        case FEDAVG_U32:
+            return 4;
+        case FEDAVG_F16:
+        case FEDAVG_BF16:
+        case FEDAVG_I16:
+        case FEDAVG_U16:
+            return 2;
+        default:
+            return 1;
+    }
+}
+
+// The value of the float16 nearest to d (round to nearest even, subnormals, overflow to inf), rounded
+// directly from fp64 -- numpy's npy_double_to_half, which NEP 50 applies to a python float meeting a
+// float16 array.
+float half_value(double d) {
+    if (std::isnan(d)) return NAN;
+    const double a = std::fabs(d);
+    if (a >= 65520.0) return std::copysign(INFINITY, (float)d);  // halfway to 2^16 rounds to even = inf
+    double q = 0x1p-24;                                            // subnormal quantum
+    if (a >= 0x1p-14) {
+        int e;
+        std::frexp(a, &e);  // a in [2^(e-1), 2^e)
+        q = std::ldexp(1.0, e - 11);
+    }
+    return (float)std::copysign(std::nearbyint(a / q) * q, d);
+}
+
+// The value of the bfloat16 nearest to f (c10::BFloat16 round_to_nearest_even).
+float bf16_value(float f) {
+    if (std::isnan(f)) return NAN;
+    uint32_t u;
+    memcpy(&u, &f, 4);
+    u = (u + 0x7fffu + ((u >> 16) & 1u)) & 0xffff0000u;
+    float r;
+    memcpy(&r, &u, 4);
+    return r;
+}
+
+// fp32 value a python float takes when torch casts it to the tensor's 16-bit dtype (Scalar::to<T>():
+// fp64 -> fp32 -> 16-bit)
+float torch16_value(int fmt, double w) {
+    const float f = (float)w;
+    return fmt == FEDAVG_BF16 ? bf16_value(f) : half_value((double)f);
 }
 
 void parallel_memcpy(void* dst, const void* src, size_t n) {
@@ -355,8 +409,8 @@ fedavg::EpiParams make_epi(const fedavg_epilogue& e) {
 void run_generic(fedavg_ctx* ctx, const void* const* rows, const double* weights, int k_rows, size_t elem_off,
                  const void* acc_in, void* out, int64_t n, int in_dtype, int acc_dtype, int op, int fin, double count,
                  hipStream_t s) {
-    const size_t in_sz = (in_dtype == FEDAVG_F64 || in_dtype == FEDAVG_I64) ? 8 : 4;
-    const size_t acc_sz = acc_dtype == FEDAVG_F64 ? 8 : 4;
+    const size_t in_sz = dtype_size(in_dtype);
+    const size_t acc_sz = dtype_size(acc_dtype);
     const double fd = fin_scalar(fin, count);
     int k0 = 0;
     const char* cur_in = acc_in ? static_cast<const char*>(acc_in) + elem_off * acc_sz : nullptr;
@@ -375,6 +429,39 @@ void run_generic(fedavg_ctx* ctx, const void* const* rows, const double* weights
         HIP_CHECK(fedavg::launch_rows_generic(gt, kc, cur_in, o, n, in_dtype, acc_dtype, op,
                                               last ? fin : FEDAVG_FIN_NONE, fv, stream_grid(ctx, n), s));
         cur_in = o;
+        k0 += kc;
+    } while (k0 < k_rows);
+}
+
+// 16-bit accumulators: chunks of at most kMaxRowsPerLaunch clients chained through `out`; the weights
+// are rounded here exactly as the reference library rounds them (see fedavg_narrow.hip).
+void run_narrow(fedavg_ctx* ctx, const void* const* rows, const double* weights, int k_rows, const void* acc_in,
+                void* out, int64_t n, int fmt, int op, int fin, double count, hipStream_t s) {
+    float fv = 0.0f;
+    if (fin == FEDAVG_FIN_SCALE)  // numpy: total * (1.0 / count), the python float cast to the array dtype
+        fv = fmt == FEDAVG_F16 ? half_value(1.0 / count) : bf16_value((float)(1.0 / count));
+    else if (fin == FEDAVG_FIN_DIV)  // torch: div_ by a CPU scalar in fp32
+        fv = (float)count;
+    int k0 = 0;
+    const void* cur_in = acc_in;
+    do {
+        const int kc = std::min(k_rows - k0, fedavg::kMaxRowsPerLaunch);
+        fedavg::RowTableNarrow t;
+        memset(&t, 0, sizeof(t));
+        for (int j = 0; j < kc; ++j) {
+            const double w = weights[k0 + j];
+            t.rows[j] = rows[k0 + j];
+            if (op == FEDAVG_OP_NUMPY) {
+                t.w_first[j] = t.w_step[j] = fmt == FEDAVG_F16 ? half_value(w) : bf16_value((float)w);
+            } else {  // torch: mul keeps the scalar in fp32, add_ casts alpha to the tensor dtype
+                t.w_first[j] = (float)w;
+                t.w_step[j] = torch16_value(fmt, w);
+            }
+        }
+        const bool last = k0 + kc >= k_rows;
+        HIP_CHECK(fedavg::launch_rows_narrow(t, kc, cur_in, out, n, fmt, op, last ? fin : FEDAVG_FIN_NONE, fv,
+                                             stream_grid(ctx, n), s));
+        cur_in = out;
         k0 += kc;
     } while (k0 < k_rows);
 }
@@ -631,8 +718,16 @@ int fedavg_accumulate(fedavg_ctx* ctx, const void* const* rows, const double* we
         check_op_fin(op, fin);
         check_dtype(in_dtype);
         check_dtype(acc_dtype);
-        if (acc_dtype != FEDAVG_F32 && acc_dtype != FEDAVG_F64) throw Error("acc_dtype must be F32 or F64");
-        if (acc_dtype == FEDAVG_F32 && in_dtype == FEDAVG_F64) throw Error("unsupported (F64 -> F32) pair");
+        const bool narrow = acc_dtype == FEDAVG_F16 || acc_dtype == FEDAVG_BF16;
+        if (narrow) {
+            if (in_dtype != acc_dtype) throw Error("a 16-bit accumulator needs inputs of the same dtype");
+        } else if (acc_dtype != FEDAVG_F32 && acc_dtype != FEDAVG_F64) {
+            throw Error("acc_dtype must be F32, F64, F16 or BF16");
+        } else if (in_dtype == FEDAVG_BF16 ||
+                   (acc_dtype == FEDAVG_F32 && (in_dtype == FEDAVG_F64 || in_dtype == FEDAVG_U16 ||
+                                                in_dtype == FEDAVG_U32 || in_dtype == FEDAVG_U64))) {
+            throw Error("unsupported (in_dtype, acc_dtype) pair");
+        }
         if (n == 0) {
             ctx->timed_valid = false;
             return;
@@ -644,6 +739,11 @@ int fedavg_accumulate(fedavg_ctx* ctx, const void* const* rows, const double* we
         ctx->activate();
         hipStream_t s = ctx->compute();
         TimingScope ts(ctx, s);
+        if (narrow) {
+            run_narrow(ctx, rows, weights, k_rows, acc_in, out, (int64_t)n, acc_dtype, op, fin, count, s);
+            ts.done();
+            return;
+        }
         bool vec = in_dtype == FEDAVG_F32 && acc_dtype == FEDAVG_F32 && reinterpret_cast<uintptr_t>(out) % 16 == 0 &&
                    reinterpret_cast<uintptr_t>(acc_in) % 16 == 0;
         for (int k = 0; vec && k < k_rows; ++k) vec = reinterpret_cast<uintptr_t>(rows[k]) % 16 == 0;

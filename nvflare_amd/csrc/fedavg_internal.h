@@ -35,6 +35,14 @@ struct RowTableGeneric {
     double w[kMaxRowsPerLaunch];
 };
 
+// 16-bit accumulators (fedavg_narrow.hip): per-client weight of the first operation and of the later
+// steps, both already rounded on the host the way the reference library rounds them (fp32 values).
+struct RowTableNarrow {
+    const void* rows[kMaxRowsPerLaunch];
+    float w_first[kMaxRowsPerLaunch];
+    float w_step[kMaxRowsPerLaunch];
+};
+
 struct TileLaunch {
     RowTableF32 tab;
     int k;
@@ -83,6 +91,8 @@ hipError_t launch_tiles_epi_f32x4(const TileLaunch& L, const EpiParams& E, hipSt
 hipError_t launch_rows_generic(const RowTableGeneric& tab, int K, const void* acc_in, void* out, int64_t n,
                                int in_dtype, int acc_dtype, int op, int fin, double fin_val, int grid,
                                hipStream_t s);
+hipError_t launch_rows_narrow(const RowTableNarrow& tab, int K, const void* acc_in, void* out, int64_t n, int fmt,
+                              int op, int fin, float fin_val, int grid, hipStream_t s);
 hipError_t launch_fill_synthetic_f32(float* dst, int64_t n, int64_t tile, int64_t tstride, uint64_t seed, uint64_t row,
                                      uint64_t col0, int grid, hipStream_t s);
 hipError_t launch_gather_f32(const float* src, const uint64_t* idx, float* dst, int64_t m, hipStream_t s);

@@ -577,14 +577,25 @@ static hipError_t launch_generic_t(const RowTableGeneric& tab, int K, const void
 hipError_t launch_rows_generic(const RowTableGeneric& tab, int K, const void* acc_in, void* out, int64_t n,
                                int in_dtype, int acc_dtype, int op, int fin, double fin_val, int grid,
                                hipStream_t s) {
+    // integer / bool inputs are promoted to the accumulator type before the first operation, as numpy
+    // (-> float64) and torch (-> float32, the default dtype) promote them
     if (acc_dtype == FEDAVG_F32) {
         switch (in_dtype) {
             case FEDAVG_F32:
                 return launch_generic_t<float, float>(tab, K, acc_in, out, n, op, fin, fin_val, grid, s);
+            case FEDAVG_F16:
+                return launch_generic_t<_Float16, float>(tab, K, acc_in, out, n, op, fin, fin_val, grid, s);
             case FEDAVG_I32:
                 return launch_generic_t<int32_t, float>(tab, K, acc_in, out, n, op, fin, fin_val, grid, s);
             case FEDAVG_I64:
                 return launch_generic_t<int64_t, float>(tab, K, acc_in, out, n, op, fin, fin_val, grid, s);
+            case FEDAVG_U8:
+            case FEDAVG_BOOL:
+                return launch_generic_t<uint8_t, float>(tab, K, acc_in, out, n, op, fin, fin_val, grid, s);
+            case FEDAVG_I8:
+                return launch_generic_t<int8_t, float>(tab, K, acc_in, out, n, op, fin, fin_val, grid, s);
+            case FEDAVG_I16:
+                return launch_generic_t<int16_t, float>(tab, K, acc_in, out, n, op, fin, fin_val, grid, s);
             default:
                 return hipErrorInvalidValue;
         }
@@ -594,10 +605,25 @@ hipError_t launch_rows_generic(const RowTableGeneric& tab, int K, const void* ac
                 return launch_generic_t<double, double>(tab, K, acc_in, out, n, op, fin, fin_val, grid, s);
             case FEDAVG_F32:
                 return launch_generic_t<float, double>(tab, K, acc_in, out, n, op, fin, fin_val, grid, s);
+            case FEDAVG_F16:
+                return launch_generic_t<_Float16, double>(tab, K, acc_in, out, n, op, fin, fin_val, grid, s);
             case FEDAVG_I32:
                 return launch_generic_t<int32_t, double>(tab, K, acc_in, out, n, op, fin, fin_val, grid, s);
             case FEDAVG_I64:
                 return launch_generic_t<int64_t, double>(tab, K, acc_in, out, n, op, fin, fin_val, grid, s);
+            case FEDAVG_U8:
+            case FEDAVG_BOOL:
+                return launch_generic_t<uint8_t, double>(tab, K, acc_in, out, n, op, fin, fin_val, grid, s);
+            case FEDAVG_I8:
+                return launch_generic_t<int8_t, double>(tab, K, acc_in, out, n, op, fin, fin_val, grid, s);
+            case FEDAVG_I16:
+                return launch_generic_t<int16_t, double>(tab, K, acc_in, out, n, op, fin, fin_val, grid, s);
+            case FEDAVG_U16:
+                return launch_generic_t<uint16_t, double>(tab, K, acc_in, out, n, op, fin, fin_val, grid, s);
+            case FEDAVG_U32:
+                return launch_generic_t<uint32_t, double>(tab, K, acc_in, out, n, op, fin, fin_val, grid, s);
+            case FEDAVG_U64:
+                return launch_generic_t<uint64_t, double>(tab, K, acc_in, out, n, op, fin, fin_val, grid, s);
             default:
                 return hipErrorInvalidValue;
         }

@@ -1,0 +1,210 @@
+// fedavg_narrow.hip -- weighted FedAvg over float16 / bfloat16 client values with a 16-bit running sum.
+//
+// Reference: weighted_aggregation_helper.py:181-236 when the client arrays are float16 (numpy) or
+// float16 / bfloat16 tensors (torch): the total keeps the input's 16-bit dtype and every library
+// operation rounds to it.  The library sequence, restated per element:
+//
+//   numpy float16 (NEP 50: the python weight becomes half(w), computed on the host from fp64):
+//       first  T = h(v * w)                   numpy half loops compute in fp32 and round once
+//       step   T = h(T + h(v * w))            (:210-214, two library operations)
+//       SCALE  T = h(T * half(1.0 / count))   (:236)
+//   torch CPU float16 / bfloat16 (vectorised kernels, fp32 "opmath"):
+//       first  T = r(v * float(w))            mul with a CPU scalar keeps the scalar as float
+//       step   T = r(fma(v, r(w), T))         add_(v, alpha=w): alpha cast to the tensor dtype, vec::fmadd
+//       DIV    T = r(T / float(count))        div_ with a CPU scalar, fp32 division
+//   weigh_by_local_iter=False: first T = v, step T = r(T + v).
+//
+// The running value lives in an fp32 register but always holds a representable 16-bit value, so partial
+// sums chain through 16-bit acc_in / out buffers without changing a bit.  Bytes per element: 2K + 2;
+// HBM-bound like the fp32 kernel.  Each lane handles 8 consecutive elements with 16-byte loads when every
+// pointer is 16-byte aligned; the remainder and unaligned rows take the per-element loop.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "fedavg_internal.h"
+
+namespace fedavg {
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+template <int FMT>
+__device__ __forceinline__ float load16(uint16_t b) {
+    if constexpr (FMT == FEDAVG_BF16) {
+        return __uint_as_float((uint32_t)b << 16);
+    } else {
+        _Float16 h;
+        __builtin_memcpy(&h, &b, 2);
+        return (float)h;
+    }
+}
+
+template <int FMT>
+__device__ __forceinline__ uint16_t bits16(float x) {
+    if constexpr (FMT == FEDAVG_BF16) {
+        // c10::BFloat16 round_to_nearest_even: NaN -> 0x7FC0, else add the rounding bias and truncate
+        const uint32_t u = __float_as_uint(x);
+        if ((u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)0x7fc0u;
+        return (uint16_t)((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
+    } else {
+        // The fp32 value must exist before it is narrowed: without this barrier LLVM folds
+        // fptrunc(fma(a, b, c)) into v_fma_mixlo_f16, which rounds the exact result to fp16 ONCE -- torch
+        // rounds to fp32 first and then to fp16 (a different result when the fp32 rounding makes a tie).
+        asm volatile("" : "+v"(x));
+        const _Float16 h = (_Float16)x;  // v_cvt_f16_f32: round to nearest even, fp16 denormals kept
+        uint16_t b;
+        __builtin_memcpy(&b, &h, 2);
+        return b;
+    }
+}
+
+template <int FMT>
+__device__ __forceinline__ float rnd(float x) {
+    return load16<FMT>(bits16<FMT>(x));
+}
+
+template <int FMT, int OP>
+__device__ __forceinline__ float first16(float v, float w) {
+    if constexpr (OP == FEDAVG_OP_UNWEIGHTED) {
+        return v;
+    } else {
+        return rnd<FMT>(v * w);
+    }
+}
+
+template <int FMT, int OP>
+__device__ __forceinline__ float step16(float t, float v, float w) {
+    if constexpr (OP == FEDAVG_OP_TORCH) {
+        return rnd<FMT>(__builtin_fmaf(v, w, t));
+    } else if constexpr (OP == FEDAVG_OP_NUMPY) {
+        return rnd<FMT>(t + rnd<FMT>(v * w));
+    } else {
+        return rnd<FMT>(t + v);
+    }
+}
+
+template <int FMT, int FIN>
+__device__ __forceinline__ float fin16(float t, float s) {
+    if constexpr (FIN == FEDAVG_FIN_SCALE) {
+        return rnd<FMT>(t * s);
+    } else if constexpr (FIN == FEDAVG_FIN_DIV) {
+        return rnd<FMT>(t / s);
+    } else {
+        return t;
+    }
+}
+
+template <int FMT, int OP, int FIN, bool ACC_IN>
+__device__ __forceinline__ float elem16(const RowTableNarrow& tab, int K, const uint16_t* acc_in, int64_t i, float fv) {
+    float t;
+    int k = 0;
+    if constexpr (ACC_IN) {
+        t = load16<FMT>(acc_in[i]);
+    } else {
+        t = first16<FMT, OP>(load16<FMT>(static_cast<const uint16_t*>(tab.rows[0])[i]), tab.w_first[0]);
+        k = 1;
+    }
+    for (; k < K; ++k) t = step16<FMT, OP>(t, load16<FMT>(static_cast<const uint16_t*>(tab.rows[k])[i]), tab.w_step[k]);
+    return fin16<FMT, FIN>(t, fv);
+}
+
+__device__ __forceinline__ uint16_t half_of(const u32x4& v, int j) {
+    return (uint16_t)((v[j >> 1] >> ((j & 1) * 16)) & 0xffffu);
+}
+
+template <int FMT, int OP, int FIN, bool ACC_IN, bool VEC>
+__global__ void __launch_bounds__(kBlock) fedavg_rows_narrow(const RowTableNarrow tab, const int K,
+                                                              const uint16_t* acc_in, uint16_t* out, const int64_t n,
+                                                              const float fv) {
+    const int64_t stride = (int64_t)gridDim.x * kBlock;
+    const int64_t tid = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    int64_t done = 0;
+    if constexpr (VEC) {
+        const int64_t n8 = n / 8;
+        for (int64_t g = tid; g < n8; g += stride) {
+            float t[8];
+            int k = 0;
+            if constexpr (ACC_IN) {
+                const u32x4 a = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(acc_in) + g);
+#pragma unroll
+                for (int j = 0; j < 8; ++j) t[j] = load16<FMT>(half_of(a, j));
+            } else {
+                const u32x4 a = __builtin_nontemporal_load(static_cast<const u32x4*>(tab.rows[0]) + g);
+#pragma unroll
+                for (int j = 0; j < 8; ++j) t[j] = first16<FMT, OP>(load16<FMT>(half_of(a, j)), tab.w_first[0]);
+                k = 1;
+            }
+            for (; k < K; ++k) {
+                const u32x4 v = __builtin_nontemporal_load(static_cast<const u32x4*>(tab.rows[k]) + g);
+                const float w = tab.w_step[k];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) t[j] = step16<FMT, OP>(t[j], load16<FMT>(half_of(v, j)), w);
+            }
+            u32x4 o;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                o[j] = (uint32_t)bits16<FMT>(fin16<FMT, FIN>(t[2 * j], fv)) |
+                       ((uint32_t)bits16<FMT>(fin16<FMT, FIN>(t[2 * j + 1], fv)) << 16);
+            }
+            __builtin_nontemporal_store(o, reinterpret_cast<u32x4*>(out) + g);
+        }
+        done = n8 * 8;
+    }
+    for (int64_t i = done + tid; i < n; i += stride) out[i] = bits16<FMT>(elem16<FMT, OP, FIN, ACC_IN>(tab, K, acc_in, i, fv));
+}
+
+template <int FMT, int OP, int FIN, bool ACC_IN>
+static hipError_t launch_n_v(const RowTableNarrow& tab, int K, const void* acc_in, void* out, int64_t n, float fv,
+                             int grid, bool vec, hipStream_t s) {
+    if (vec) {
+        hipLaunchKernelGGL((fedavg_rows_narrow<FMT, OP, FIN, ACC_IN, true>), dim3(grid), dim3(kBlock), 0, s, tab, K,
+                           static_cast<const uint16_t*>(acc_in), static_cast<uint16_t*>(out), n, fv);
+    } else {
+        hipLaunchKernelGGL((fedavg_rows_narrow<FMT, OP, FIN, ACC_IN, false>), dim3(grid), dim3(kBlock), 0, s, tab, K,
+                           static_cast<const uint16_t*>(acc_in), static_cast<uint16_t*>(out), n, fv);
+    }
+    return hipGetLastError();
+}
+
+template <int FMT, int OP, int FIN>
+static hipError_t launch_n_a(const RowTableNarrow& tab, int K, const void* acc_in, void* out, int64_t n, float fv,
+                             int grid, bool vec, hipStream_t s) {
+    return acc_in ? launch_n_v<FMT, OP, FIN, true>(tab, K, acc_in, out, n, fv, grid, vec, s)
+                  : launch_n_v<FMT, OP, FIN, false>(tab, K, acc_in, out, n, fv, grid, vec, s);
+}
+
+template <int FMT, int OP>
+static hipError_t launch_n_f(const RowTableNarrow& tab, int K, const void* acc_in, void* out, int64_t n, int fin,
+                             float fv, int grid, bool vec, hipStream_t s) {
+    switch (fin) {
+        case FEDAVG_FIN_SCALE:
+            return launch_n_a<FMT, OP, FEDAVG_FIN_SCALE>(tab, K, acc_in, out, n, fv, grid, vec, s);
+        case FEDAVG_FIN_DIV:
+            return launch_n_a<FMT, OP, FEDAVG_FIN_DIV>(tab, K, acc_in, out, n, fv, grid, vec, s);
+        default:
+            return launch_n_a<FMT, OP, FEDAVG_FIN_NONE>(tab, K, acc_in, out, n, fv, grid, vec, s);
+    }
+}
+
+template <int FMT>
+static hipError_t launch_n_o(const RowTableNarrow& tab, int K, const void* acc_in, void* out, int64_t n, int op, int fin,
+                             float fv, int grid, bool vec, hipStream_t s) {
+    switch (op) {
+        case FEDAVG_OP_TORCH:
+            return launch_n_f<FMT, FEDAVG_OP_TORCH>(tab, K, acc_in, out, n, fin, fv, grid, vec, s);
+        case FEDAVG_OP_UNWEIGHTED:
+            return launch_n_f<FMT, FEDAVG_OP_UNWEIGHTED>(tab, K, acc_in, out, n, fin, fv, grid, vec, s);
+        default:
+            return launch_n_f<FMT, FEDAVG_OP_NUMPY>(tab, K, acc_in, out, n, fin, fv, grid, vec, s);
+    }
+}
+
+hipError_t launch_rows_narrow(const RowTableNarrow& tab, int K, const void* acc_in, void* out, int64_t n, int fmt,
+                              int op, int fin, float fin_val, int grid, hipStream_t s) {
+    bool vec = reinterpret_cast<uintptr_t>(out) % 16 == 0 && reinterpret_cast<uintptr_t>(acc_in) % 16 == 0;
+    for (int k = 0; vec && k < K; ++k) vec = reinterpret_cast<uintptr_t>(tab.rows[k]) % 16 == 0;
+    if (fmt == FEDAVG_BF16) return launch_n_o<FEDAVG_BF16>(tab, K, acc_in, out, n, op, fin, fin_val, grid, vec, s);
+    if (fmt == FEDAVG_F16) return launch_n_o<FEDAVG_F16>(tab, K, acc_in, out, n, op, fin, fin_val, grid, vec, s);
+    return hipErrorInvalidValue;
+}
+
+}  // namespace fedavg

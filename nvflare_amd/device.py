@@ -12,11 +12,23 @@ import numpy as np
 
 from . import _native as N
 
+# numpy has no bfloat16: the engine carries torch.bfloat16 keys as 2-byte raw values of this dtype
+BF16_NP = np.dtype("V2")
+
 _NP_TO_DT = {
     np.dtype(np.float32): N.FEDAVG_F32,
     np.dtype(np.float64): N.FEDAVG_F64,
     np.dtype(np.int32): N.FEDAVG_I32,
     np.dtype(np.int64): N.FEDAVG_I64,
+    np.dtype(np.float16): N.FEDAVG_F16,
+    BF16_NP: N.FEDAVG_BF16,
+    np.dtype(np.uint8): N.FEDAVG_U8,
+    np.dtype(np.int8): N.FEDAVG_I8,
+    np.dtype(np.int16): N.FEDAVG_I16,
+    np.dtype(np.bool_): N.FEDAVG_BOOL,
+    np.dtype(np.uint16): N.FEDAVG_U16,
+    np.dtype(np.uint32): N.FEDAVG_U32,
+    np.dtype(np.uint64): N.FEDAVG_U64,
 }
 
 

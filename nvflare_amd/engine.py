@@ -35,7 +35,7 @@ from typing import Any, Dict, List, Optional, Tuple
 import numpy as np
 
 from . import _native as N
-from .device import DeviceBuffer, DeviceContext, HostArenaPool, TiledLayout, fedavg_dtype
+from .device import BF16_NP, DeviceBuffer, DeviceContext, HostArenaPool, TiledLayout, fedavg_dtype
 from .quantized import QuantizedPayload, stager
 
 try:
@@ -54,8 +54,23 @@ if torch is not None:
         torch.float64: np.dtype(np.float64),
         torch.int32: np.dtype(np.int32),
         torch.int64: np.dtype(np.int64),
+        torch.float16: np.dtype(np.float16),
+        torch.bfloat16: BF16_NP,
+        torch.uint8: np.dtype(np.uint8),
+        torch.int8: np.dtype(np.int8),
+        torch.int16: np.dtype(np.int16),
+        torch.bool: np.dtype(np.bool_),
     }
     _NP_TO_TORCH = {v: k for k, v in _TORCH_TO_NP.items()}
+
+_F16 = np.dtype(np.float16)
+_F32 = np.dtype(np.float32)
+_F64 = np.dtype(np.float64)
+# numpy dtypes with a device kernel; integer and bool arrays accumulate in float64 (numpy promotion)
+_NUMPY_INPUTS = {_F16, _F32, _F64} | {np.dtype(t) for t in (np.int8, np.int16, np.int32, np.int64, np.uint8, np.uint16,
+                                                             np.uint32, np.uint64, np.bool_)}
+# (input, accumulator) pairs the C-ABI accepts (include/nvflare_amd_fedavg.h, fedavg_accumulate)
+_ACC_F32_INPUTS = {_F32, _F16} | {np.dtype(t) for t in (np.int8, np.int16, np.int32, np.int64, np.uint8, np.bool_)}
 
 
 def is_torch_tensor(v) -> bool:
@@ -77,14 +92,18 @@ def _type_proxy(v):
 
 def _resolve_types(v, weight, weighted: bool) -> Tuple[str, np.dtype, np.dtype, int, int]:
     """(container, input dtype, accumulator/result dtype, op, fin) as the reference's numpy / torch
-    arithmetic would produce them (weighted_aggregation_helper.py:181-216, :233-236)."""
+    arithmetic would produce them (weighted_aggregation_helper.py:181-216, :233-236).
+
+    float16 / bfloat16 values keep a 16-bit total (both libraries keep the array dtype); integer and bool
+    values are promoted: torch to the default dtype (float32), numpy to float64 (NEP 50: a python float
+    meeting an integer array gives float64).  bfloat16 is carried as ``device.BF16_NP``."""
     v = _type_proxy(v)
     if is_torch_tensor(v):
         tdt = v.dtype
         if tdt not in _TORCH_TO_NP:
             raise TypeError(f"nvflare_amd: torch dtype {tdt} is not supported by the device kernels")
         in_np = _TORCH_TO_NP[tdt]
-        if in_np.kind == "i":
+        if in_np.kind in "iub":
             if not weighted:
                 # reference: v.clone() stays integer and div_(count) raises on an integer tensor
                 raise TypeError("nvflare_amd: integer tensors need weigh_by_local_iter=True (reference raises in div_)")
@@ -94,26 +113,27 @@ def _resolve_types(v, weight, weighted: bool) -> Tuple[str, np.dtype, np.dtype, 
         op = N.FEDAVG_OP_TORCH if weighted else N.FEDAVG_OP_UNWEIGHTED
         return "torch", in_np, acc_np, op, N.FEDAVG_FIN_DIV
     in_np = np.dtype(v.dtype)
-    if in_np not in (np.dtype(np.float32), np.dtype(np.float64), np.dtype(np.int32), np.dtype(np.int64)):
+    if in_np not in _NUMPY_INPUTS:
         raise TypeError(f"nvflare_amd: numpy dtype {in_np} is not supported by the device kernels")
     if weighted:
         if isinstance(weight, np.generic):
             acc_np = np.result_type(in_np, np.dtype(type(weight)))
-        elif isinstance(weight, (bool, int)) and in_np.kind == "i":
+        elif isinstance(weight, (bool, int)) and in_np.kind in "iub":
             raise TypeError("nvflare_amd: integer arrays with an integer weight accumulate in integers; unsupported")
         else:
             acc_np = np.result_type(in_np, 1.0)  # NEP 50: python float is weak
         op = N.FEDAVG_OP_NUMPY
     else:
-        if in_np.kind == "i":
+        if in_np.kind in "iub":
             raise TypeError("nvflare_amd: integer arrays need weigh_by_local_iter=True")
         if isinstance(weight, np.generic):
             raise TypeError("nvflare_amd: numpy-scalar weights with weigh_by_local_iter=False change the result dtype; unsupported")
         acc_np = in_np
         op = N.FEDAVG_OP_UNWEIGHTED
     acc_np = np.dtype(acc_np)
-    if acc_np not in (np.dtype(np.float32), np.dtype(np.float64)):
-        raise TypeError(f"nvflare_amd: accumulator dtype {acc_np} unsupported")
+    ok = (acc_np == _F64 or (acc_np == _F32 and in_np in _ACC_F32_INPUTS) or (acc_np == _F16 and in_np == _F16))
+    if not ok:
+        raise TypeError(f"nvflare_amd: ({in_np} -> {acc_np}) accumulation unsupported")
     return "numpy", in_np, acc_np, op, N.FEDAVG_FIN_SCALE
 
 
@@ -610,6 +630,8 @@ class DeviceFedAvg:
             arr = np.empty(st.shape, dtype=st.acc_np)
             self.ctx.d2h(arr.reshape(-1) if arr.ndim else arr.reshape(1), st.acc_buf.ptr)
         if st.container == "torch":
+            if st.acc_np == BF16_NP:
+                return torch.from_numpy(arr.view(np.uint16)).view(torch.bfloat16)
             return torch.from_numpy(arr)
         if arr.ndim == 0:
             return arr[()]  # numpy arithmetic on 0-d arrays returns a numpy scalar

@@ -12,6 +12,11 @@ reference on the golden vectors in ``tests/golden/`` (pinned by ``tests/test_ora
                              arrival order; optionally multi-threaded over elements (OpenMP).
 * ``numpy_mode_reference`` -- the numpy branch as numpy ops (``:188-193``, ``:210-214``, ``:236``).
 * ``torch_mode_reference`` -- the torch branch as torch CPU ops (``:181-187``, ``:203-209``, ``:233``).
+* ``torch16_vector_reference`` -- the torch branch for float16 / bfloat16 tensors, restated in numpy
+                             with explicit roundings: torch CPU's vectorised kernels compute in fp32
+                             (mul / div with the scalar as float, add_ as one fp32 fma with alpha cast to
+                             the tensor dtype) and round to 16 bits after each op.  Pinned bitwise on the
+                             elements torch computes on its vector path (tests/golden/dtype_cases.*).
 
 Plus ``synth_values``: the host twin of the device synthetic-input generator used by ``bench.py`` for
 full-size spot checks.
@@ -164,6 +169,62 @@ def torch_mode_reference(rows, weights, weighted: bool = True, count: Optional[f
     if count is not None:
         c = count
     return total.div_(c)
+
+
+def bf16_round(x) -> np.ndarray:
+    """fp32 -> value of the nearest bfloat16, as fp32 (c10::BFloat16 round_to_nearest_even; NaN -> 0x7FC0)."""
+    x = np.asarray(x, dtype=np.float32)
+    u = x.view(np.uint32).astype(np.uint64)
+    r = ((u + 0x7FFF + ((u >> 16) & 1)) & 0xFFFF0000).astype(np.uint32)
+    r = np.where(np.isnan(x), np.uint32(0x7FC00000), r)
+    return r.view(np.float32)
+
+
+def round16(x, fmt: str) -> np.ndarray:
+    """fp32 -> value of the nearest ``fmt`` ("float16" | "bfloat16") number, as fp32 (round to nearest even)."""
+    x = np.asarray(x, dtype=np.float32)
+    if fmt == "bfloat16":
+        return bf16_round(x)
+    with np.errstate(over="ignore"):
+        return x.astype(np.float16).astype(np.float32)
+
+
+def bf16_bits_to_f32(bits) -> np.ndarray:
+    return (np.asarray(bits, dtype=np.uint16).astype(np.uint32) << 16).view(np.float32)
+
+
+def f32_to_bf16_bits(x) -> np.ndarray:
+    return (bf16_round(x).view(np.uint32) >> 16).astype(np.uint16)
+
+
+def torch16_vector_reference(rows, weights, fmt: str, weighted: bool = True, count: Optional[float] = None):
+    """torch branch for ``fmt`` tensors (weighted_aggregation_helper.py:181-187, :203-209, :233), as torch
+    CPU's vectorised kernels compute it.  ``rows``: fp32 arrays holding ``fmt`` values; returns fp32 values
+    of the ``fmt`` result.
+
+    first  T = r(v * float32(w))            mul_kernel, reduced float with a CPU scalar: opmath fp32
+    step   T = r(fma32(v, r(float32(w)), T)) ufunc add: alpha.to<scalar_t>(), Vectorized fmadd in fp32
+    unweighted step T = r(T + v)
+    final  T = r(T / float32(count))         div_true_kernel, reduced float with a CPU scalar
+    (fma32 is evaluated exactly in fp64 -- the product of two 16-bit values is exact there -- then rounded
+    once to fp32.)"""
+    with np.errstate(over="ignore", invalid="ignore"):
+        total, c = None, None
+        for v, w in zip(rows, weights):
+            v = np.asarray(v, dtype=np.float32)
+            if total is None:
+                total = round16(v * np.float32(w), fmt) if weighted else v.copy()
+                c = w
+            else:
+                if weighted:
+                    a = np.float64(round16(np.float32(w), fmt))
+                    total = round16((v.astype(np.float64) * a + total.astype(np.float64)).astype(np.float32), fmt)
+                else:
+                    total = round16(total + v, fmt)
+                c = c + w
+        if count is not None:
+            c = count
+        return round16(total / np.float32(c), fmt)
 
 
 def synth_values(seed: int, row: int, cols: np.ndarray) -> np.ndarray:

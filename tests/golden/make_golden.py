@@ -20,9 +20,10 @@ Reference code exercised:
   nvflare/app_common/aggregators/intime_accumulate_model_aggregator.py   (intime cases)
   nvflare/app_common/aggregators/dxo_aggregator.py:71-191
 
-Usage:  python tests/golden/make_golden.py [--ref /root/reference] [--set helper|fedavg|fedopt|quant]
+Usage:  python tests/golden/make_golden.py [--ref /root/reference] [--set helper|fedavg|fedopt|quant|dtypes]
         (helper -> helper_cases.{npz,json}; fedavg -> fedavg_cases.{npz,json};
-         fedopt -> fedopt_cases.{npz,json}; quant -> quant_cases.{npz,json})
+         fedopt -> fedopt_cases.{npz,json}; quant -> quant_cases.{npz,json};
+         dtypes -> dtype_cases.{npz,json}: float16 / bfloat16 / integer / bool client arrays)
 """
 
 from __future__ import annotations
@@ -414,10 +415,109 @@ def main_quant():
     print(f"wrote {len(cases)} quant cases, {len(store.arrays)} arrays")
 
 
+def _put_any(arrays, tag, v):
+    """Store one array of any dtype: (name, dtype string).  bfloat16 is kept as its uint16 bit pattern."""
+    name = f"{tag}{len(arrays):05d}"
+    if isinstance(v, torch.Tensor):
+        dt = str(v.dtype).replace("torch.", "")
+        a = v.detach().cpu()
+        a = a.view(torch.int16).numpy().view(np.uint16) if v.dtype == torch.bfloat16 else a.numpy()
+    else:
+        a = np.asarray(v)
+        dt = str(a.dtype)
+    arrays[name] = np.array(a, copy=True)
+    return name, dt
+
+
+def _as_container(a: np.ndarray, dt: str, container: str):
+    if container == "numpy":
+        return np.array(a, copy=True)
+    if dt == "bfloat16":
+        return torch.from_numpy(np.array(a, copy=True)).to(torch.float32).to(torch.bfloat16)
+    return torch.from_numpy(np.array(a, copy=True))
+
+
+def main_dtypes():
+    """Reduced-precision and integer client arrays through the reference helper (weighted_aggregation_helper.py:
+    153-240): numpy float16 / uint8 / int8 / int16 / bool / uint16 / uint32 / uint64, torch float16 / bfloat16 /
+    uint8 / int8 / int16 / bool.  torch runs single-threaded: its 16-bit add_ computes the vectorised path
+    (one fp32 fma, one rounding) except on the last n % 32 elements of each thread's chunk, which take the
+    scalar path -- recorded as ``vector_end`` so the tests know which elements the vector semantics cover."""
+    from nvflare.app_common.aggregators.weighted_aggregation_helper import WeightedAggregationHelper
+
+    torch.set_num_threads(1)
+    rng = np.random.default_rng(20261016)
+    arrays, cases = {}, {}
+
+    def values(n, dt, special=False):
+        if dt in ("float16", "bfloat16"):
+            a = (rng.standard_normal(n) * 3).astype(np.float32)
+            if special:
+                sp = np.array([0.0, -0.0, np.inf, -np.inf, np.nan, 6e-8, -3e-5, 65504.0, -65504.0, 1e-40, 3e38, 1.0],
+                              np.float32)
+                idx = rng.choice(n, size=min(n, 2 * sp.size), replace=False)
+                a[idx] = np.resize(sp, idx.size)
+            if dt == "float16":
+                with np.errstate(over="ignore"):
+                    return a.astype(np.float16)
+            return torch.from_numpy(a).to(torch.bfloat16).view(torch.int16).numpy().view(np.uint16)
+        if dt == "bool":
+            return rng.integers(0, 2, n).astype(np.bool_)
+        info = np.iinfo(np.dtype(dt))
+        return rng.integers(max(info.min, -10 ** 6), min(info.max, 10 ** 6), n, endpoint=True).astype(dt)
+
+    def case(name, container, dt, n, K, weights, weighted=True, special=False):
+        rows = [values(n, dt, special) for _ in range(K)]
+        h = WeightedAggregationHelper(weigh_by_local_iter=weighted)
+        for k, r in enumerate(rows):
+            src = r if dt != "bfloat16" else r  # bit patterns; converted below
+            if dt == "bfloat16":
+                v = torch.from_numpy(src.view(np.int16).copy()).view(torch.bfloat16)
+            else:
+                v = torch.from_numpy(src.copy()) if container == "torch" else src.copy()
+            h.add({"w": v}, weights[k], f"site-{k}", 0)
+        out = h.get_result()["w"]
+        rec = {"container": container, "dtype": dt, "n": n, "weighted": weighted,
+               "weights": [repr(w) if isinstance(w, np.generic) else w for w in weights],
+               "weight_types": [type(w).__name__ for w in weights],
+               "rows": [_put_any(arrays, "in", r)[0] for r in rows]}
+        rec["expected"], rec["expected_dtype"] = _put_any(arrays, "out", out)
+        rec["vector_end"] = n - n % 32 if container == "torch" and dt in ("float16", "bfloat16") else n
+        cases[name] = rec
+
+    def rw(K):
+        return [random.random() * float(random.randint(1, 50)) for _ in range(K)]
+
+    random.seed(20261016)
+    for n in (64 * 40, 1003):
+        for K in (1, 5, 9):
+            case(f"numpy_float16_k{K}_n{n}", "numpy", "float16", n, K, rw(K))
+            for dt in ("float16", "bfloat16"):
+                case(f"torch_{dt}_k{K}_n{n}", "torch", dt, n, K, rw(K))
+    for dt in ("float16", "bfloat16"):
+        case(f"torch_{dt}_special", "torch", dt, 64 * 8, 6, [1e-3, 3.5, 1e3, 0.1, 7.0, 2.0 ** -20], special=True)
+        case(f"torch_{dt}_unweighted", "torch", dt, 64 * 9 + 5, 5, rw(5), weighted=False)
+        case(f"torch_{dt}_intweights", "torch", dt, 64 * 16, 16, [1.0 * float(1 + (37 * k) % 100) for k in range(16)])
+    case("numpy_float16_special", "numpy", "float16", 509, 6, [1e-3, 3.5, 1e3, 0.1, 7.0, 2.0 ** -20], special=True)
+    case("numpy_float16_unweighted", "numpy", "float16", 300, 5, rw(5), weighted=False)
+    case("numpy_float16_intweights", "numpy", "float16", 777, 16, [1.0 * float(1 + (37 * k) % 100) for k in range(16)])
+    case("numpy_float16_f32weights", "numpy", "float16", 333, 4, [np.float32(x) for x in rw(4)])
+    case("numpy_float16_f64weights", "numpy", "float16", 333, 4, [np.float64(x) for x in rw(4)])
+    for dt in ("uint8", "int8", "int16", "bool", "uint16", "uint32", "uint64"):
+        case(f"numpy_{dt}", "numpy", dt, 257, 5, rw(5))
+    for dt in ("uint8", "int8", "int16", "bool"):
+        case(f"torch_{dt}", "torch", dt, 257, 5, rw(5))
+    np.savez_compressed(os.path.join(HERE, "dtype_cases.npz"), **arrays)
+    with open(os.path.join(HERE, "dtype_cases.json"), "w") as f:
+        json.dump({"generator": "tests/golden/make_golden.py --set dtypes", "reference": "NVFlare (/root/reference, ~2.9.0-dev)",
+                   "numpy": np.__version__, "torch": torch.__version__, "torch_threads": 1, "cases": cases}, f, indent=1)
+    print(f"wrote {len(cases)} dtype cases, {len(arrays)} arrays")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ref", default="/root/reference")
-    ap.add_argument("--set", choices=["helper", "fedavg", "fedopt", "quant"], default="helper")
+    ap.add_argument("--set", choices=["helper", "fedavg", "fedopt", "quant", "dtypes"], default="helper")
     args = ap.parse_args()
     install_shim(args.ref)
     torch.set_num_threads(8)
@@ -427,6 +527,8 @@ def main():
         return main_fedopt()
     if args.set == "quant":
         return main_quant()
+    if args.set == "dtypes":
+        return main_dtypes()
 
     rng = np.random.default_rng(20261015)
     random.seed(20261015)

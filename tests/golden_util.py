@@ -160,3 +160,65 @@ def load_quant_golden():
 def adaquant_state(case, arrays):
     """The case's quant_state with its arrays restored."""
     return {k: (arrays[v["array"]] if isinstance(v, dict) else v) for k, v in case["quant_state"].items()}
+
+
+# --- reduced-precision / integer client arrays (make_golden.py --set dtypes) -------------------------------
+def load_dtype_golden():
+    if "d" not in _cache:
+        with open(os.path.join(GOLDEN_DIR, "dtype_cases.json")) as f:
+            meta = json.load(f)
+        arrays = dict(np.load(os.path.join(GOLDEN_DIR, "dtype_cases.npz"), allow_pickle=False))
+        _cache["d"] = (meta, arrays)
+    return _cache["d"]
+
+
+def dtype_case_weights(case):
+    """Weights as the reference received them (python floats, or numpy scalars of the recorded type)."""
+    out = []
+    for w, t in zip(case["weights"], case["weight_types"]):
+        if t in ("float32", "float64", "float16"):
+            out.append(getattr(np, t)(float(w[w.index("(") + 1:-1])))
+        else:
+            out.append(w)
+    return out
+
+
+def dtype_case_inputs(case, arrays):
+    """Client values as the reference received them (numpy arrays or CPU tensors; bfloat16 from bits)."""
+    import torch
+
+    rows = []
+    for name in case["rows"]:
+        a = np.array(arrays[name], copy=True)
+        if case["dtype"] == "bfloat16":
+            rows.append(torch.from_numpy(a.view(np.int16)).view(torch.bfloat16))
+        elif case["container"] == "torch":
+            rows.append(torch.from_numpy(a))
+        else:
+            rows.append(a)
+    return rows
+
+
+def as_f32_values(v, dtype: str) -> np.ndarray:
+    """fp32 values of a 16-bit result (numpy array, tensor or stored bits)."""
+    import torch
+
+    if isinstance(v, torch.Tensor):
+        v = v.view(torch.int16).numpy().view(np.uint16) if v.dtype == torch.bfloat16 else v.numpy()
+    v = np.asarray(v)
+    if dtype == "bfloat16":
+        return (v.astype(np.uint32) << 16).view(np.float32)
+    return v.astype(np.float32)
+
+
+def torch16_tail_tolerance(rows_f32, weights, expected_f32, dtype: str) -> np.ndarray:
+    """Bound for torch's scalar-tail elements (the last n % 32 of a thread's chunk), where torch rounds the
+    add_ product and the sum separately instead of one fp32 fma: at most one 16-bit rounding per step of
+    the running sum, whose magnitude is bounded by sum_k |w_k v_k|, scaled by the final division."""
+    mag = np.zeros_like(expected_f32, dtype=np.float64)
+    for r, w in zip(rows_f32, weights):
+        mag += np.abs(r.astype(np.float64) * float(w))
+    count = float(sum(float(w) for w in weights))
+    ulp_bits = 10 if dtype == "float16" else 7
+    ulp = lambda x: np.exp2(np.floor(np.log2(np.maximum(np.abs(x), 1e-30))) - ulp_bits)
+    return (len(rows_f32) + 1) * ulp(mag) / abs(count) + ulp(expected_f32)

@@ -126,18 +126,26 @@ def test_string_data_kind_from_job_config():
 
 
 # --- dtype promotion table used by the engine: checked against numpy / torch themselves --------------------
-@pytest.mark.parametrize("dt", [np.float32, np.float64, np.int32, np.int64])
-@pytest.mark.parametrize("weight", [0.75, np.float64(0.75), np.float32(0.75)])
+@pytest.mark.parametrize("dt", [np.float32, np.float64, np.int32, np.int64, np.float16, np.uint8, np.int8, np.int16,
+                                np.bool_, np.uint16, np.uint32, np.uint64])
+@pytest.mark.parametrize("weight", [0.75, np.float64(0.75), np.float32(0.75), np.float16(0.75)])
 def test_numpy_promotion_table(dt, weight):
     from nvflare_amd.engine import _resolve_types
 
     v = np.ones(3, dtype=dt)
-    _, in_np, acc_np, op, fin = _resolve_types(v, weight, True)
     ref = (v * weight + v * weight) * (1.0 / (weight + weight))
+    unsupported = (ref.dtype == np.float32 and np.dtype(dt) in (np.dtype(np.uint16), np.dtype(np.uint32), np.dtype(np.uint64))) or \
+        (ref.dtype == np.float16 and np.dtype(dt) != np.float16)
+    if unsupported:  # no (input, accumulator) kernel: refused, never computed on the host
+        with pytest.raises(TypeError):
+            _resolve_types(v, weight, True)
+        return
+    _, in_np, acc_np, op, fin = _resolve_types(v, weight, True)
     assert acc_np == ref.dtype
 
 
-@pytest.mark.parametrize("dt", [torch.float32, torch.float64, torch.int32, torch.int64])
+@pytest.mark.parametrize("dt", [torch.float32, torch.float64, torch.int32, torch.int64, torch.float16, torch.bfloat16,
+                                torch.uint8, torch.int8, torch.int16, torch.bool])
 def test_torch_promotion_table(dt):
     from nvflare_amd.engine import _NP_TO_TORCH, _resolve_types
 
@@ -152,9 +160,9 @@ def test_unsupported_dtypes_raise():
     from nvflare_amd.engine import _resolve_types
 
     with pytest.raises(TypeError):
-        _resolve_types(np.ones(3, np.float16), 1.0, True)
+        _resolve_types(np.ones(3, np.complex64), 1.0, True)
     with pytest.raises(TypeError):
-        _resolve_types(torch.ones(3, dtype=torch.bfloat16), 1.0, True)
+        _resolve_types(torch.ones(3, dtype=torch.complex64), 1.0, True)
     with pytest.raises(TypeError):
         _resolve_types(torch.ones(3, dtype=torch.int64), 1.0, False)
 

@@ -1,0 +1,162 @@
+"""GPU parity for float16 / bfloat16 / integer / bool client arrays.
+
+1. The drop-in helper on the reference's own outputs (tests/golden/dtype_cases.*): bit-exact for numpy
+   float16 and every integer / bool case (numpy and torch); torch float16 / bfloat16 bit-exact on the
+   elements torch computes on its vectorised path, within ``torch16_tail_tolerance`` on torch's scalar tail
+   (see tests/test_cpu_dtypes.py -- the oracle shows the same split).
+2. The 16-bit kernel through the C-ABI against the oracle, bit-exact on EVERY element: both formats, all
+   ops, K up to 131 (chained launches), ragged n, unaligned rows (per-element path), acc_in continuation.
+3. Device-resident bfloat16 tensors in, device tensor out."""
+
+import numpy as np
+import pytest
+import torch
+
+from golden_util import (
+    as_f32_values,
+    dtype_case_inputs,
+    dtype_case_weights,
+    load_dtype_golden,
+    same_bits,
+    torch16_tail_tolerance,
+)
+from oracle import fedavg_oracle as orc
+
+pytestmark = pytest.mark.gpu
+
+META, ARRAYS = load_dtype_golden()
+CASES = sorted(META["cases"].items())
+
+
+@pytest.mark.parametrize("name,case", CASES, ids=[n for n, _ in CASES])
+def test_helper_dtype_golden(name, case):
+    from nvflare_amd.app_common.aggregators.weighted_aggregation_helper import WeightedAggregationHelper
+
+    rows = dtype_case_inputs(case, ARRAYS)
+    ws = dtype_case_weights(case)
+    h = WeightedAggregationHelper(weigh_by_local_iter=case["weighted"])
+    for k, (r, w) in enumerate(zip(rows, ws)):
+        h.add({"w": r}, w, f"site-{k}", 0)
+    got = h.get_result()["w"]
+    dt = case["dtype"]
+    exp_bits = ARRAYS[case["expected"]]
+    if case["container"] == "torch":
+        assert isinstance(got, torch.Tensor)
+        assert str(got.dtype).replace("torch.", "") == case["expected_dtype"]
+    else:
+        assert str(np.asarray(got).dtype) == case["expected_dtype"]
+    if case["container"] != "torch" or dt not in ("float16", "bfloat16"):
+        g = got.numpy() if isinstance(got, torch.Tensor) else np.asarray(got)
+        assert same_bits(g, exp_bits), name
+        return
+    g, exp = as_f32_values(got, dt), as_f32_values(exp_bits, dt)
+    ve = case["vector_end"]
+    assert same_bits(g[:ve], exp[:ve]), name
+    rows_f32 = [as_f32_values(r, dt)[ve:] for r in rows]
+    tol = torch16_tail_tolerance(rows_f32, ws, exp[ve:], dt)
+    d = np.abs(g[ve:].astype(np.float64) - exp[ve:].astype(np.float64))
+    assert np.all((d <= tol) | (np.isnan(g[ve:]) & np.isnan(exp[ve:])) | (g[ve:] == exp[ve:])), name
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    from nvflare_amd.device import DeviceContext
+
+    return DeviceContext.get(0)
+
+
+def _bits(x_f32, fmt):
+    if fmt == "bfloat16":
+        return orc.f32_to_bf16_bits(x_f32)
+    return x_f32.astype(np.float16).view(np.uint16)
+
+
+def _vals(bits, fmt):
+    if fmt == "bfloat16":
+        return orc.bf16_bits_to_f32(bits)
+    return bits.view(np.float16).astype(np.float32)
+
+
+def _kernel16(ctx, rows_bits, weights, fmt, op, fin, count, acc_in_bits=None, offset=0):
+    """fedavg_accumulate with (fmt, fmt) dtypes on device buffers; rows at `offset` elements past 16 B."""
+    from nvflare_amd import _native as N
+
+    code = N.FEDAVG_BF16 if fmt == "bfloat16" else N.FEDAVG_F16
+    n = rows_bits[0].size if rows_bits else acc_in_bits.size
+    bufs, ptrs = [], []
+    for r in rows_bits:
+        b = ctx.alloc((n + offset) * 2 + 16)
+        bufs.append(b)
+        p = b.ptr + offset * 2
+        ctx.h2d_ptr(p, r.ctypes.data, r.nbytes)
+        ptrs.append(p)
+    ob = ctx.alloc((n + offset) * 2 + 16)
+    optr = ob.ptr + offset * 2
+    acc_ptr = None
+    if acc_in_bits is not None:
+        ctx.h2d_ptr(optr, acc_in_bits.ctypes.data, acc_in_bits.nbytes)
+        acc_ptr = optr
+    ctx.accumulate(ptrs, weights, n, optr, code, code, op, fin, count, acc_in_ptr=acc_ptr)
+    out = np.empty(n, dtype=np.uint16)
+    ctx.d2h(out, optr)
+    for b in bufs + [ob]:
+        b.close()
+    return out
+
+
+def _count(ws):
+    c = None
+    for w in ws:
+        c = w if c is None else c + w
+    return c
+
+
+CONFIGS = [("bfloat16", "torch"), ("float16", "torch"), ("float16", "numpy"), ("bfloat16", "unweighted"),
+           ("float16", "unweighted_numpy")]
+
+
+@pytest.mark.parametrize("fmt,mode", CONFIGS)
+@pytest.mark.parametrize("K,n,offset", [(1, 1, 0), (3, 7, 0), (5, 4099, 0), (5, 4099, 1), (131, 1000, 0), (8, 65536 + 24, 3)])
+def test_kernel16_vs_oracle(ctx, fmt, mode, K, n, offset):
+    from nvflare_amd import _native as N
+
+    rng = np.random.default_rng(K * 1000 + n + offset)
+    rows = [_bits((rng.standard_normal(n) * 4).astype(np.float32), fmt) for _ in range(K)]
+    ws = [float(rng.random() * 20 + 1e-3) for _ in range(K)]
+    vals = [_vals(r, fmt) for r in rows]
+    if mode == "torch":
+        op, fin = N.FEDAVG_OP_TORCH, N.FEDAVG_FIN_DIV
+        exp = orc.torch16_vector_reference(vals, ws, fmt)
+    elif mode == "unweighted":
+        op, fin = N.FEDAVG_OP_UNWEIGHTED, N.FEDAVG_FIN_DIV
+        exp = orc.torch16_vector_reference(vals, ws, fmt, weighted=False)
+    elif mode == "numpy":
+        op, fin = N.FEDAVG_OP_NUMPY, N.FEDAVG_FIN_SCALE
+        exp = orc.numpy_mode_reference([r.view(np.float16) for r in rows], ws).astype(np.float32)
+    else:
+        op, fin = N.FEDAVG_OP_UNWEIGHTED, N.FEDAVG_FIN_SCALE
+        exp = orc.numpy_mode_reference([r.view(np.float16) for r in rows], ws, weighted=False).astype(np.float32)
+    got = _vals(_kernel16(ctx, rows, ws, fmt, op, fin, _count(ws), offset=offset), fmt)
+    assert same_bits(got, exp)
+    if K >= 3:  # split the clients over two calls: partial sum in 16 bits, continued through acc_in
+        part = _kernel16(ctx, rows[:2], ws[:2], fmt, op, N.FEDAVG_FIN_NONE, 1.0, offset=offset)
+        full = _kernel16(ctx, rows[2:], ws[2:], fmt, op, fin, _count(ws), acc_in_bits=part, offset=offset)
+        assert same_bits(_vals(full, fmt), exp)
+
+
+def test_device_bf16_tensors_through_helper():
+    from nvflare_amd.app_common.aggregators.weighted_aggregation_helper import WeightedAggregationHelper
+
+    rng = np.random.default_rng(7)
+    rows = [torch.from_numpy(rng.standard_normal(10_000).astype(np.float32)).to(torch.bfloat16) for _ in range(6)]
+    ws = [float(1 + k) for k in range(6)]
+    h = WeightedAggregationHelper()
+    for k, r in enumerate(rows):
+        h.add({"w": r.to("cuda:0"), "h": r.to(torch.float16).to("cuda:0")}, ws[k], f"s{k}", 0)
+    out = h.get_result()
+    assert out["w"].device.type == "cuda" and out["w"].dtype == torch.bfloat16
+    assert out["h"].device.type == "cuda" and out["h"].dtype == torch.float16
+    exp = orc.torch16_vector_reference([as_f32_values(r, "bfloat16") for r in rows], ws, "bfloat16")
+    assert same_bits(as_f32_values(out["w"].cpu(), "bfloat16"), exp)
+    exp_h = orc.torch16_vector_reference([r.to(torch.float16).numpy().astype(np.float32) for r in rows], ws, "float16")
+    assert same_bits(out["h"].cpu().numpy().astype(np.float32), exp_h)
