@@ -459,8 +459,12 @@ void run_narrow(fedavg_ctx* ctx, const void* const* rows, const double* weights,
             }
         }
         const bool last = k0 + kc >= k_rows;
-        HIP_CHECK(fedavg::launch_rows_narrow(t, kc, cur_in, out, n, fmt, op, last ? fin : FEDAVG_FIN_NONE, fv,
-                                             stream_grid(ctx, n), s));
+        // one lane per 8 elements; 2 x blocks_per_cu resident blocks per CU stride over the K row streams
+        // (4 by default: +2 % over 2, flat above -- profiles/r01/narrow_sweep.jsonl)
+        const int64_t need = (n / 8 + fedavg::kBlock) / fedavg::kBlock;
+        const int grid =
+            (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)ctx->num_cus * 2 * ctx->blocks_per_cu, need));
+        HIP_CHECK(fedavg::launch_rows_narrow(t, kc, cur_in, out, n, fmt, op, last ? fin : FEDAVG_FIN_NONE, fv, grid, s));
         cur_in = out;
         k0 += kc;
     } while (k0 < k_rows);

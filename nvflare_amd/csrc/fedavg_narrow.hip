@@ -133,6 +133,18 @@ __global__ void __launch_bounds__(kBlock) fedavg_rows_narrow(const RowTableNarro
                 for (int j = 0; j < 8; ++j) t[j] = first16<FMT, OP>(load16<FMT>(half_of(a, j)), tab.w_first[0]);
                 k = 1;
             }
+            // four clients' loads in flight before their arrival-ordered arithmetic (as the fp32 kernel)
+            for (; k + 4 <= K; k += 4) {
+                u32x4 v[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) v[u] = __builtin_nontemporal_load(static_cast<const u32x4*>(tab.rows[k + u]) + g);
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const float w = tab.w_step[k + u];
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) t[j] = step16<FMT, OP>(t[j], load16<FMT>(half_of(v[u], j)), w);
+                }
+            }
             for (; k < K; ++k) {
                 const u32x4 v = __builtin_nontemporal_load(static_cast<const u32x4*>(tab.rows[k]) + g);
                 const float w = tab.w_step[k];

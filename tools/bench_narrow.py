@@ -1,0 +1,64 @@
+#!/usr/bin/env python3
+"""Throughput of the 16-bit (float16 / bfloat16) aggregation kernel: K device-resident client rows of P
+values -> P values, torch-mode arithmetic (fedavg_narrow.hip).  Algorithmic bytes per launch 2*K*P + 2*P.
+
+  python tools/bench_narrow.py [--clients 64 --params 1e9 --fmt bfloat16 --steps 10]
+"""
+
+import argparse
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--clients", type=int, default=64)
+    ap.add_argument("--params", type=float, default=1e9)
+    ap.add_argument("--fmt", choices=["bfloat16", "float16"], default="bfloat16")
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--mode", choices=["torch", "numpy"], default="torch")
+    ap.add_argument("--blocks-per-cu", default="2", help="comma list: interleaved same-process sweep")
+    args = ap.parse_args()
+    import torch
+
+    from nvflare_amd import _native as N
+    from nvflare_amd.device import DeviceContext
+
+    K, P = args.clients, int(args.params)
+    ctx = DeviceContext.get(0)
+    tdt = torch.bfloat16 if args.fmt == "bfloat16" else torch.float16
+    g = torch.Generator(device="cuda:0")
+    g.manual_seed(0)
+    rows = [torch.randn(P, dtype=tdt, device="cuda:0", generator=g) for _ in range(K)]
+    out = torch.empty(P, dtype=tdt, device="cuda:0")
+    torch.cuda.synchronize()
+    code = N.FEDAVG_BF16 if args.fmt == "bfloat16" else N.FEDAVG_F16
+    op = N.FEDAVG_OP_TORCH if args.mode == "torch" else N.FEDAVG_OP_NUMPY
+    fin = N.FEDAVG_FIN_DIV if args.mode == "torch" else N.FEDAVG_FIN_SCALE
+    ws = [float(1 + (37 * k) % 100) for k in range(K)]
+    ptrs = [r.data_ptr() for r in rows]
+    alg = 2.0 * K * P + 2.0 * P
+    bpcs = [int(b) for b in args.blocks_per_cu.split(",")]
+    res = {b: [] for b in bpcs}
+    for rep in range(3):
+        for b in bpcs:
+            ctx.set_launch(b, 0)
+            ctx.accumulate(ptrs, ws, P, out.data_ptr(), code, code, op, fin, sum(ws))
+            ctx.sync()
+            ctx.timing_begin()
+            for _ in range(args.steps):
+                ctx.accumulate(ptrs, ws, P, out.data_ptr(), code, code, op, fin, sum(ws))
+            res[b].append(ctx.timing_end() / args.steps)
+    for b in bpcs:
+        ms = sorted(res[b])[len(res[b]) // 2]
+        print(json.dumps({"tool": "bench_narrow", "fmt": args.fmt, "mode": args.mode, "clients": K, "params": P,
+                          "blocks_per_cu": b, "kernel_ms": round(ms, 3), "alg_GBs": round(alg / ms / 1e6, 1),
+                          "frac_of_8TBs": round(alg / ms / 1e6 / 8000.0, 4),
+                          "GiBs_aggregated": round(2.0 * K * P / (ms / 1e3) / 2 ** 30, 1)}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
