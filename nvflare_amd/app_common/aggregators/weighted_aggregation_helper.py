@@ -23,6 +23,7 @@ import threading
 from typing import Any, Callable, Dict, Optional, Set
 
 from ...engine import DeviceFedAvg, is_device_array, is_torch_tensor
+from ...ingest import as_mapped
 from ...quantized import QuantizedPayload
 from ...sharding import ShardedFedAvg
 
@@ -173,7 +174,13 @@ class WeightedAggregationHelper(object):
                 self.key_contribution_counts[k] = self.key_contribution_counts.get(k, 0) + 1
                 materialize = getattr(v, "materialize", None)
                 device_quantized = isinstance(v, QuantizedPayload) and not isinstance(self._engine, ShardedFedAvg)
-                if callable(materialize) and not device_quantized:
+                mapped = None
+                if callable(materialize) and not device_quantized and not isinstance(self._engine, ShardedFedAvg) \
+                        and not isinstance(self.total.get(k), _HostValue):
+                    mapped = as_mapped(v)  # disk-offloaded safetensors ref: staged from the mmap, no tensor built
+                if mapped is not None:
+                    v = mapped
+                elif callable(materialize) and not device_quantized:
                     # lazy disk-offloaded refs (weighted_aggregation_helper.py:170-175); quantized payloads
                     # stay compressed until the engine dequantizes them into their slot
                     v = materialize()

@@ -36,6 +36,7 @@ import numpy as np
 
 from . import _native as N
 from .device import BF16_NP, DeviceBuffer, DeviceContext, HostArenaPool, TiledLayout, fedavg_dtype
+from .ingest import MappedTensor
 from .quantized import QuantizedPayload, stager
 
 try:
@@ -80,13 +81,15 @@ def is_torch_tensor(v) -> bool:
 def is_device_array(v) -> bool:
     """Arrays/tensors take the HIP path; everything else (python numbers, opaque objects such as HE
     ciphertexts) follows the reference's object protocol on the host."""
-    return isinstance(v, (np.ndarray, QuantizedPayload)) or is_torch_tensor(v)
+    return isinstance(v, (np.ndarray, QuantizedPayload, MappedTensor)) or is_torch_tensor(v)
 
 
 def _type_proxy(v):
     """An empty array / tensor with the container and dtype a QuantizedPayload dequantizes to."""
     if isinstance(v, QuantizedPayload):
         return torch.empty(0, dtype=v.dtype) if v.container == "torch" else np.empty(0, v.out_dtype)
+    if isinstance(v, MappedTensor):  # a disk-offloaded tensor: materialises as a CPU torch tensor
+        return torch.empty(0, dtype=v.dtype)
     return v
 
 
@@ -370,7 +373,10 @@ class DeviceFedAvg:
     # ------------------------------------------------------------------ staging
     @staticmethod
     def _source(v):
-        """(pointer, nbytes, on_device) of a contiguous view of v."""
+        """(keep-alive, pointer, nbytes, on_device) of a contiguous view of v."""
+        if isinstance(v, MappedTensor):  # bytes straight from the page cache of the safetensors file
+            keep, ptr, nbytes = v.host_view()
+            return keep, ptr, nbytes, False
         if is_torch_tensor(v):
             t = v.detach()
             if not t.is_contiguous():
