@@ -188,6 +188,14 @@ int fedavg_accumulate_tiled(fedavg_ctx* ctx, const void* const* bases, const dou
                             size_t tile_elems, size_t tile_stride, size_t begin, size_t end,
                             const void* acc_in, void* out, int op, int fin, double count);
 
+/* fedavg_accumulate_tiled for float16 / bfloat16 client storage and totals (fmt = FEDAVG_F16 | FEDAVG_BF16), with
+ * the reduced-precision operation sequence documented at fedavg_accumulate.  tile_elems must be 4096 (8 KiB
+ * segments); tile_stride, begin, end multiples of 8 elements; pointers 16-byte aligned; out / acc_in flat
+ * 16-bit arrays indexed by i; any k_rows (more than 128 are chained through out). */
+int fedavg_accumulate_tiled16(fedavg_ctx* ctx, int fmt, const void* const* bases, const double* weights, int k_rows,
+                              size_t tile_elems, size_t tile_stride, size_t begin, size_t end, const void* acc_in,
+                              void* out, int op, int fin, double count);
+
 /* fedavg_accumulate_tiled with a server-optimizer epilogue applied per element to d = fin(acc) in the
  * same launch (rows a9/a10): ADD_BASE writes base + d to out; SGD/ADAM update epi->param/state in place
  * and also store d to out when out != NULL.  More than 128 clients are chained through a partial sum

@@ -98,6 +98,22 @@ _SIGNATURES = {
         c_int,  # fin
         c_double,  # count
     ],
+    "fedavg_accumulate_tiled16": [
+        c_void_p,  # ctx
+        c_int,  # fmt
+        ctypes.POINTER(c_void_p),  # bases
+        ctypes.POINTER(c_double),  # weights
+        c_int,  # k_rows
+        c_size_t,  # tile_elems
+        c_size_t,  # tile_stride
+        c_size_t,  # begin
+        c_size_t,  # end
+        c_void_p,  # acc_in
+        c_void_p,  # out
+        c_int,  # op
+        c_int,  # fin
+        c_double,  # count
+    ],
     "fedavg_accumulate_tiled_epi": [
         c_void_p,  # ctx
         ctypes.POINTER(c_void_p),  # bases

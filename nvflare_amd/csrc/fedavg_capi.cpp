@@ -433,31 +433,41 @@ void run_generic(fedavg_ctx* ctx, const void* const* rows, const double* weights
     } while (k0 < k_rows);
 }
 
-// 16-bit accumulators: chunks of at most kMaxRowsPerLaunch clients chained through `out`; the weights
-// are rounded here exactly as the reference library rounds them (see fedavg_narrow.hip).
+// 16-bit accumulators: the weights and the finalisation scalar are rounded here exactly as the reference
+// library rounds them (see fedavg_narrow.hip).
+float narrow_fin_value(int fmt, int fin, double count) {
+    if (fin == FEDAVG_FIN_SCALE)  // numpy: total * (1.0 / count), the python float cast to the array dtype
+        return fmt == FEDAVG_F16 ? half_value(1.0 / count) : bf16_value((float)(1.0 / count));
+    if (fin == FEDAVG_FIN_DIV)  // torch: div_ by a CPU scalar in fp32
+        return (float)count;
+    return 0.0f;
+}
+
+void fill_narrow_table(fedavg::RowTableNarrow& t, const void* const* rows, const double* weights, int k0, int kc,
+                       int fmt, int op) {
+    memset(&t, 0, sizeof(t));
+    for (int j = 0; j < kc; ++j) {
+        const double w = weights[k0 + j];
+        t.rows[j] = rows[k0 + j];
+        if (op == FEDAVG_OP_NUMPY) {
+            t.w_first[j] = t.w_step[j] = fmt == FEDAVG_F16 ? half_value(w) : bf16_value((float)w);
+        } else {  // torch: mul keeps the scalar in fp32, add_ casts alpha to the tensor dtype
+            t.w_first[j] = (float)w;
+            t.w_step[j] = torch16_value(fmt, w);
+        }
+    }
+}
+
+// Contiguous 16-bit rows: chunks of at most kMaxRowsPerLaunch clients chained through `out`.
 void run_narrow(fedavg_ctx* ctx, const void* const* rows, const double* weights, int k_rows, const void* acc_in,
                 void* out, int64_t n, int fmt, int op, int fin, double count, hipStream_t s) {
-    float fv = 0.0f;
-    if (fin == FEDAVG_FIN_SCALE)  // numpy: total * (1.0 / count), the python float cast to the array dtype
-        fv = fmt == FEDAVG_F16 ? half_value(1.0 / count) : bf16_value((float)(1.0 / count));
-    else if (fin == FEDAVG_FIN_DIV)  // torch: div_ by a CPU scalar in fp32
-        fv = (float)count;
+    const float fv = narrow_fin_value(fmt, fin, count);
     int k0 = 0;
     const void* cur_in = acc_in;
     do {
         const int kc = std::min(k_rows - k0, fedavg::kMaxRowsPerLaunch);
         fedavg::RowTableNarrow t;
-        memset(&t, 0, sizeof(t));
-        for (int j = 0; j < kc; ++j) {
-            const double w = weights[k0 + j];
-            t.rows[j] = rows[k0 + j];
-            if (op == FEDAVG_OP_NUMPY) {
-                t.w_first[j] = t.w_step[j] = fmt == FEDAVG_F16 ? half_value(w) : bf16_value((float)w);
-            } else {  // torch: mul keeps the scalar in fp32, add_ casts alpha to the tensor dtype
-                t.w_first[j] = (float)w;
-                t.w_step[j] = torch16_value(fmt, w);
-            }
-        }
+        fill_narrow_table(t, rows, weights, k0, kc, fmt, op);
         const bool last = k0 + kc >= k_rows;
         // one lane per 8 elements; 2 x blocks_per_cu resident blocks per CU stride over the K row streams
         // (4 by default: +2 % over 2, flat above -- profiles/r01/narrow_sweep.jsonl)
@@ -465,6 +475,28 @@ void run_narrow(fedavg_ctx* ctx, const void* const* rows, const double* weights,
         const int grid =
             (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)ctx->num_cus * 2 * ctx->blocks_per_cu, need));
         HIP_CHECK(fedavg::launch_rows_narrow(t, kc, cur_in, out, n, fmt, op, last ? fin : FEDAVG_FIN_NONE, fv, grid, s));
+        cur_in = out;
+        k0 += kc;
+    } while (k0 < k_rows);
+}
+
+// Tiled 16-bit client storage over [begin, end) (multiples of 8): chunks of 128 clients chained through out.
+void run_tiles_narrow(fedavg_ctx* ctx, const void* const* bases, const double* weights, int k_rows, int64_t tstride,
+                      int64_t begin, int64_t end, const void* acc_in, void* out, int fmt, int op, int fin, double count,
+                      hipStream_t s) {
+    const float fv = narrow_fin_value(fmt, fin, count);
+    const int64_t T = fedavg::kTile16Elems;
+    const int64_t n_tiles = (end - 1) / T - begin / T + 1;
+    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)ctx->num_cus * ctx->blocks_per_cu, n_tiles));
+    int k0 = 0;
+    const void* cur_in = acc_in;
+    do {
+        const int kc = std::min(k_rows - k0, fedavg::kMaxRowsPerLaunch);
+        fedavg::RowTableNarrow t;
+        fill_narrow_table(t, bases, weights, k0, kc, fmt, op);
+        const bool last = k0 + kc >= k_rows;
+        HIP_CHECK(fedavg::launch_tiles_narrow(t, kc, tstride, cur_in, out, begin, end, fmt, op,
+                                              last ? fin : FEDAVG_FIN_NONE, fv, grid, s));
         cur_in = out;
         k0 += kc;
     } while (k0 < k_rows);
@@ -793,6 +825,37 @@ int fedavg_accumulate_tiled(fedavg_ctx* ctx, const void* const* bases, const dou
         TimingScope ts(ctx, s);
         run_tiles(ctx, bases, weights, k_rows, (int64_t)tile_elems, (int64_t)tile_stride, (int64_t)begin, (int64_t)end,
                   static_cast<const float*>(acc_in), static_cast<float*>(out), op, fin, count, s);
+        ts.done();
+    });
+}
+
+int fedavg_accumulate_tiled16(fedavg_ctx* ctx, int fmt, const void* const* bases, const double* weights, int k_rows,
+                              size_t tile_elems, size_t tile_stride, size_t begin, size_t end, const void* acc_in,
+                              void* out, int op, int fin, double count) {
+    return guarded([&] {
+        if (!ctx) throw Error("ctx is NULL");
+        if (fmt != FEDAVG_F16 && fmt != FEDAVG_BF16) throw Error("fmt must be FEDAVG_F16 or FEDAVG_BF16");
+        if (k_rows < 0 || (k_rows == 0 && !acc_in)) throw Error("k_rows == 0 requires acc_in");
+        check_op_fin(op, fin);
+        if (tile_elems != (size_t)fedavg::kTile16Elems) throw Error("tile_elems must be 4096");
+        if (tile_stride < tile_elems || tile_stride % 8) throw Error("tile_stride must be >= tile_elems, multiple of 8");
+        if (begin % 8 || end % 8 || end < begin) throw Error("begin/end must be multiples of 8 with begin <= end");
+        if (end == begin) {
+            ctx->timed_valid = false;
+            return;
+        }
+        if (!out) throw Error("out is NULL");
+        if (reinterpret_cast<uintptr_t>(out) % 16 || reinterpret_cast<uintptr_t>(acc_in) % 16)
+            throw Error("out/acc_in must be 16-byte aligned");
+        if (k_rows > 0 && (!bases || !weights)) throw Error("bases/weights NULL");
+        for (int k = 0; k < k_rows; ++k)
+            if (!bases[k] || reinterpret_cast<uintptr_t>(bases[k]) % 16)
+                throw Error("base " + std::to_string(k) + " is NULL or not 16-byte aligned");
+        ctx->activate();
+        hipStream_t s = ctx->compute();
+        TimingScope ts(ctx, s);
+        run_tiles_narrow(ctx, bases, weights, k_rows, (int64_t)tile_stride, (int64_t)begin, (int64_t)end, acc_in, out,
+                         fmt, op, fin, count, s);
         ts.done();
     });
 }

@@ -164,6 +164,138 @@ __global__ void __launch_bounds__(kBlock) fedavg_rows_narrow(const RowTableNarro
     for (int64_t i = done + tid; i < n; i += stride) out[i] = bits16<FMT>(elem16<FMT, OP, FIN, ACC_IN>(tab, K, acc_in, i, fv));
 }
 
+// ---------------------------------------------------------------------------------------------
+// TILED storage (the engine's slab layout for 16-bit keys): element i of client k lives at
+//   bases[k] + (i / 4096) * tile_stride + i % 4096      (16-bit elements)
+// A block owns a tile (4096 elements = 8 KiB per client); each lane owns two 8-element groups, so a wave
+// reads 1 KiB contiguous per client and group, and one tile's K client segments form one sequential run
+// (S * 8 KiB) when the slots are interleaved.  Units below are 8-element groups (u32x4).
+// ---------------------------------------------------------------------------------------------
+constexpr int kTile16 = 4096;
+constexpr int kCpl16 = kTile16 / (8 * kBlock);  // 2
+
+template <int FMT, int OP, int FIN, bool ACC_IN>
+__global__ void __launch_bounds__(kBlock) fedavg_tiles_narrow(const RowTableNarrow tab, const int K,
+                                                               const int64_t tstride8, const u32x4* acc_in,
+                                                               u32x4* out, const int64_t b8, const int64_t e8,
+                                                               const float fv) {
+    constexpr int64_t T8 = (int64_t)kCpl16 * kBlock;
+    constexpr int UNROLL = 4;
+    const int64_t t_last = (e8 - 1) / T8;
+    for (int64_t t = b8 / T8 + blockIdx.x; t <= t_last; t += gridDim.x) {
+        const int64_t off = t * tstride8 + threadIdx.x;
+        const int64_t col = t * T8 + threadIdx.x;
+        float acc[kCpl16][8];
+        int k = 0;
+        if constexpr (ACC_IN) {
+#pragma unroll
+            for (int c = 0; c < kCpl16; ++c) {
+                const int64_t i = col + c * kBlock;
+                const u32x4 a = (i >= b8 && i < e8) ? acc_in[i] : u32x4{0, 0, 0, 0};
+#pragma unroll
+                for (int j = 0; j < 8; ++j) acc[c][j] = load16<FMT>(half_of(a, j));
+            }
+        } else {
+            const u32x4* r = static_cast<const u32x4*>(tab.rows[0]) + off;
+#pragma unroll
+            for (int c = 0; c < kCpl16; ++c) {
+                const u32x4 a = __builtin_nontemporal_load(r + c * kBlock);
+#pragma unroll
+                for (int j = 0; j < 8; ++j) acc[c][j] = first16<FMT, OP>(load16<FMT>(half_of(a, j)), tab.w_first[0]);
+            }
+            k = 1;
+        }
+        for (; k + UNROLL <= K; k += UNROLL) {
+            u32x4 v[UNROLL][kCpl16];
+#pragma unroll
+            for (int u = 0; u < UNROLL; ++u) {
+                const u32x4* r = static_cast<const u32x4*>(tab.rows[k + u]) + off;
+#pragma unroll
+                for (int c = 0; c < kCpl16; ++c) v[u][c] = __builtin_nontemporal_load(r + c * kBlock);
+            }
+#pragma unroll
+            for (int u = 0; u < UNROLL; ++u) {
+                const float w = tab.w_step[k + u];
+#pragma unroll
+                for (int c = 0; c < kCpl16; ++c)
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) acc[c][j] = step16<FMT, OP>(acc[c][j], load16<FMT>(half_of(v[u][c], j)), w);
+            }
+        }
+        for (; k < K; ++k) {
+            const u32x4* r = static_cast<const u32x4*>(tab.rows[k]) + off;
+            const float w = tab.w_step[k];
+#pragma unroll
+            for (int c = 0; c < kCpl16; ++c) {
+                const u32x4 v = __builtin_nontemporal_load(r + c * kBlock);
+#pragma unroll
+                for (int j = 0; j < 8; ++j) acc[c][j] = step16<FMT, OP>(acc[c][j], load16<FMT>(half_of(v, j)), w);
+            }
+        }
+#pragma unroll
+        for (int c = 0; c < kCpl16; ++c) {
+            const int64_t i = col + c * kBlock;
+            if (i >= b8 && i < e8) {
+                u32x4 o;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    o[j] = (uint32_t)bits16<FMT>(fin16<FMT, FIN>(acc[c][2 * j], fv)) |
+                           ((uint32_t)bits16<FMT>(fin16<FMT, FIN>(acc[c][2 * j + 1], fv)) << 16);
+                }
+                __builtin_nontemporal_store(o, out + i);
+            }
+        }
+    }
+}
+
+template <int FMT, int OP, int FIN>
+static hipError_t launch_t16_a(const RowTableNarrow& tab, int K, int64_t tstride8, const void* acc_in, void* out,
+                               int64_t b8, int64_t e8, float fv, int grid, hipStream_t s) {
+    if (acc_in) {
+        hipLaunchKernelGGL((fedavg_tiles_narrow<FMT, OP, FIN, true>), dim3(grid), dim3(kBlock), 0, s, tab, K, tstride8,
+                           static_cast<const u32x4*>(acc_in), static_cast<u32x4*>(out), b8, e8, fv);
+    } else {
+        hipLaunchKernelGGL((fedavg_tiles_narrow<FMT, OP, FIN, false>), dim3(grid), dim3(kBlock), 0, s, tab, K, tstride8,
+                           static_cast<const u32x4*>(acc_in), static_cast<u32x4*>(out), b8, e8, fv);
+    }
+    return hipGetLastError();
+}
+
+template <int FMT, int OP>
+static hipError_t launch_t16_f(const RowTableNarrow& tab, int K, int64_t tstride8, const void* acc_in, void* out,
+                               int64_t b8, int64_t e8, int fin, float fv, int grid, hipStream_t s) {
+    switch (fin) {
+        case FEDAVG_FIN_SCALE:
+            return launch_t16_a<FMT, OP, FEDAVG_FIN_SCALE>(tab, K, tstride8, acc_in, out, b8, e8, fv, grid, s);
+        case FEDAVG_FIN_DIV:
+            return launch_t16_a<FMT, OP, FEDAVG_FIN_DIV>(tab, K, tstride8, acc_in, out, b8, e8, fv, grid, s);
+        default:
+            return launch_t16_a<FMT, OP, FEDAVG_FIN_NONE>(tab, K, tstride8, acc_in, out, b8, e8, fv, grid, s);
+    }
+}
+
+template <int FMT>
+static hipError_t launch_t16_o(const RowTableNarrow& tab, int K, int64_t tstride8, const void* acc_in, void* out,
+                               int64_t b8, int64_t e8, int op, int fin, float fv, int grid, hipStream_t s) {
+    switch (op) {
+        case FEDAVG_OP_TORCH:
+            return launch_t16_f<FMT, FEDAVG_OP_TORCH>(tab, K, tstride8, acc_in, out, b8, e8, fin, fv, grid, s);
+        case FEDAVG_OP_UNWEIGHTED:
+            return launch_t16_f<FMT, FEDAVG_OP_UNWEIGHTED>(tab, K, tstride8, acc_in, out, b8, e8, fin, fv, grid, s);
+        default:
+            return launch_t16_f<FMT, FEDAVG_OP_NUMPY>(tab, K, tstride8, acc_in, out, b8, e8, fin, fv, grid, s);
+    }
+}
+
+hipError_t launch_tiles_narrow(const RowTableNarrow& tab, int K, int64_t tstride_elems, const void* acc_in, void* out,
+                               int64_t begin, int64_t end, int fmt, int op, int fin, float fin_val, int grid,
+                               hipStream_t s) {
+    const int64_t ts8 = tstride_elems / 8, b8 = begin / 8, e8 = end / 8;
+    if (fmt == FEDAVG_BF16) return launch_t16_o<FEDAVG_BF16>(tab, K, ts8, acc_in, out, b8, e8, op, fin, fin_val, grid, s);
+    if (fmt == FEDAVG_F16) return launch_t16_o<FEDAVG_F16>(tab, K, ts8, acc_in, out, b8, e8, op, fin, fin_val, grid, s);
+    return hipErrorInvalidValue;
+}
+
 template <int FMT, int OP, int FIN, bool ACC_IN>
 static hipError_t launch_n_v(const RowTableNarrow& tab, int K, const void* acc_in, void* out, int64_t n, float fv,
                              int grid, bool vec, hipStream_t s) {

@@ -148,15 +148,48 @@ def _default_budget(ctx: DeviceContext) -> int:
     return max(int(ctx.total_bytes) - (8 << 30), int(ctx.total_bytes) // 2)
 
 
+_ARENA_FORMATS = {  # element formats that get tiled slabs: (C-ABI code, bytes per element)
+    np.dtype(np.float32): (N.FEDAVG_F32, 4),
+    np.dtype(np.float16): (N.FEDAVG_F16, 2),
+    BF16_NP: (N.FEDAVG_BF16, 2),
+}
+
+
+class _Arena:
+    """One element format's flat key layout, tiled client slabs and accumulator.
+
+    fp32 keys (the hot path) and 16-bit keys (float16 / bfloat16 totals) each get one: a contribution's keys
+    of that format occupy one slot of a slab of the arena, and a run of keys is aggregated by one launch of
+    the format's tiled kernel (``fedavg_accumulate_tiled`` / ``fedavg_accumulate_tiled16``)."""
+
+    __slots__ = ("fmt", "esize", "np_dtype", "layout_elems", "slabs", "live", "acc", "host_pool")
+
+    def __init__(self, np_dtype: np.dtype):
+        self.np_dtype = np_dtype
+        self.fmt, self.esize = _ARENA_FORMATS[np_dtype]
+        self.layout_elems = 0  # flat layout size (elements)
+        self.slabs: List["_Slab"] = []
+        self.live: List["_Slot"] = []
+        self.acc: Optional[DeviceBuffer] = None
+        self.host_pool = HostArenaPool()
+
+    def launch_end(self, st: "_KeyState") -> int:
+        """End of a key's launch range: rounded up to the kernel's vector width, inside the key's 256-byte
+        aligned extent."""
+        q = 4 if self.esize == 4 else 8
+        return (st.offset + st.n + q - 1) // q * q
+
+
 class _Slab:
-    """S client slots in one tiled allocation covering `capacity` elements of the flat layout."""
+    """S client slots in one tiled allocation covering `capacity` elements of an arena's flat layout."""
 
-    __slots__ = ("buf", "layout", "capacity", "free")
+    __slots__ = ("buf", "layout", "capacity", "free", "arena")
 
-    def __init__(self, buf: DeviceBuffer, layout: TiledLayout, capacity: int):
+    def __init__(self, buf: DeviceBuffer, layout: TiledLayout, capacity: int, arena: _Arena):
         self.buf = buf
         self.layout = layout
         self.capacity = capacity
+        self.arena = arena
         self.free = list(range(layout.slots - 1, -1, -1))  # pop() hands out slot 0 first
 
 
@@ -170,11 +203,11 @@ class _Slot:
 
     @property
     def base(self) -> int:
-        return self.slab.buf.ptr + self.slab.layout.slot_offset_elems(self.index) * 4
+        return self.slab.buf.ptr + self.slab.layout.slot_offset_elems(self.index) * self.slab.arena.esize
 
 
 class _Staged:
-    """One contribution's device copy of one key: a slot of a slab (fp32) or its own buffer."""
+    """One contribution's device copy of one key: a slot of a slab (arena keys) or its own buffer."""
 
     __slots__ = ("weight", "slot", "buf")
 
@@ -194,9 +227,10 @@ class _KeyState:
     def __init__(self):
         self.pending: List[_Staged] = []
         self.acc_valid = False
-        self.done = False  # finalised in the arena by a fused server-optimizer launch (deferred rounds)
+        self.done = False  # finalised in its arena accumulator (eagerly, or by a deferred round's fused step)
         self.acc_buf: Optional[DeviceBuffer] = None
         self.count = None
+        self.arena: Optional[_Arena] = None
 
     @property
     def in_dt(self):
@@ -220,16 +254,12 @@ class DeviceFedAvg:
         env_slots = os.environ.get("NVFLARE_AMD_SLAB_SLOTS")
         self.slab_slots = int(slab_slots or (int(env_slots) if env_slots else 0))  # 0 = adaptive
         self.lock = threading.RLock()
-        self.layout_elems = 0  # flat fp32 layout size (elements)
         self.keys: Dict[str, _KeyState] = {}
-        self.arena_acc: Optional[DeviceBuffer] = None
-        self.slabs: List[_Slab] = []
-        self._live_slots: List[_Slot] = []
+        self.arenas: Dict[int, _Arena] = {}  # by element format
         self._side_bufs: List[DeviceBuffer] = []
         self._round_clients = 0
         self.peak_clients = 0
-        self._deferred = None  # DeferredRound still holding slots (result_deferred)
-        self._host_pool = HostArenaPool()
+        self._deferred = None  # DeferredRound still holding fp32 slots (result_deferred)
         self.stats = {"h2d_bytes": 0, "folds": 0, "launches": 0, "slabs_allocated": 0}
 
     @property
@@ -244,72 +274,99 @@ class DeviceFedAvg:
             self._max_resident_bytes = _default_budget(self.ctx)
         return self._max_resident_bytes
 
+    def _arena(self, np_dtype: np.dtype) -> _Arena:
+        a = self.arenas.get(_ARENA_FORMATS[np_dtype][0])
+        if a is None:
+            a = self.arenas[_ARENA_FORMATS[np_dtype][0]] = _Arena(np_dtype)
+        return a
+
+    @property
+    def f32(self) -> _Arena:
+        """The fp32 arena (the hot path; deferred rounds live here)."""
+        return self._arena(np.dtype(np.float32))
+
+    @property
+    def layout_elems(self) -> int:
+        """Elements of the fp32 flat layout (all fp32 keys of the round)."""
+        a = self.arenas.get(N.FEDAVG_F32)
+        return a.layout_elems if a is not None else 0
+
+    @property
+    def slabs(self) -> List[_Slab]:
+        return [s for a in self.arenas.values() for s in a.slabs]
+
+    @property
+    def _live_slots(self) -> List[_Slot]:
+        return [s for a in self.arenas.values() for s in a.live]
+
     # ------------------------------------------------------------------ memory
     def _resident_bytes(self) -> int:
-        slabs = sum(s.buf.nbytes for s in self.slabs)
-        side = sum(b.nbytes for b in self._side_bufs)
-        acc = self.arena_acc.nbytes if self.arena_acc is not None else 0
-        return slabs + side + acc
+        total = sum(b.nbytes for b in self._side_bufs)
+        for a in self.arenas.values():
+            total += sum(s.buf.nbytes for s in a.slabs)
+            total += a.acc.nbytes if a.acc is not None else 0
+        return total
 
-    def _next_slab_slots(self) -> int:
+    def _next_slab_slots(self, arena: _Arena) -> int:
         if self.slab_slots:
             return self.slab_slots
-        if not self.slabs:
+        if not arena.slabs:
             return 16 if self.peak_clients == 0 else max(8, (self.peak_clients + 7) // 8 * 8)
-        return min(128, 2 * self.slabs[-1].layout.slots)
+        return min(128, 2 * arena.slabs[-1].layout.slots)
 
-    def _new_slab(self, capacity: int, min_slots: int = 0) -> Optional[_Slab]:
+    def _new_slab(self, arena: _Arena, capacity: int, min_slots: int = 0) -> Optional[_Slab]:
         """Allocate a slab for clients of flat extent <= capacity, sized to the remaining budget (but at
         least `min_slots` slots)."""
         n_tiles = (capacity + TILE - 1) // TILE
-        per_slot = n_tiles * TILE * 4
-        room = self.max_resident_bytes - self._resident_bytes() - 4 * (self.layout_elems + ALIGN_ELEMS)
-        slots = max(min_slots, min(self._next_slab_slots(), room // per_slot if per_slot else 0))
+        per_slot = n_tiles * TILE * arena.esize
+        room = self.max_resident_bytes - self._resident_bytes() - arena.esize * (arena.layout_elems + ALIGN_ELEMS)
+        slots = max(min_slots, min(self._next_slab_slots(arena), room // per_slot if per_slot else 0))
         while slots >= max(1, min_slots):
             layout = TiledLayout(TILE, int(slots))
             try:
-                buf = self.ctx.alloc(layout.slab_elems(capacity) * 4)
+                buf = self.ctx.alloc(layout.slab_elems(capacity) * arena.esize)
             except N.FedAvgError:
                 if slots == 1:
                     return None
                 slots = max(1, slots // 2)
                 continue
-            slab = _Slab(buf, layout, n_tiles * TILE)
-            self.slabs.append(slab)
+            slab = _Slab(buf, layout, n_tiles * TILE, arena)
+            arena.slabs.append(slab)
             self.stats["slabs_allocated"] += 1
             return slab
         return None
 
-    def _find_free(self, extent: int) -> Optional[_Slot]:
-        for slab in self.slabs:
+    def _find_free(self, arena: _Arena, extent: int) -> Optional[_Slot]:
+        for slab in arena.slabs:
             if slab.capacity >= extent and slab.free:
                 slot = _Slot(slab, slab.free.pop())
-                self._live_slots.append(slot)
+                arena.live.append(slot)
                 return slot
         return None
 
-    def _acquire_slot(self, extent: int) -> _Slot:
-        slot = self._find_free(extent)
-        if slot is None and self._new_slab(max(extent, self.layout_elems)) is not None:
-            slot = self._find_free(extent)
+    def _acquire_slot(self, arena: _Arena, extent: int) -> _Slot:
+        slot = self._find_free(arena, extent)
+        if slot is None and self._new_slab(arena, max(extent, arena.layout_elems)) is not None:
+            slot = self._find_free(arena, extent)
         if slot is None and self._live_slots:
             self._fold()  # over budget: fold what is staged (frees every slot, keeps the slabs)
-            slot = self._find_free(extent)
+            slot = self._find_free(arena, extent)
         if slot is None:
             # the remaining slabs cannot hold this client: drop them and make room for at least one slot
-            for s in self.slabs:
+            for s in arena.slabs:
                 s.buf.close()
-            self.slabs.clear()
-            if self._new_slab(max(extent, self.layout_elems), min_slots=1) is not None:
-                slot = self._find_free(extent)
+            arena.slabs.clear()
+            if self._new_slab(arena, max(extent, arena.layout_elems), min_slots=1) is not None:
+                slot = self._find_free(arena, extent)
         if slot is None:
-            raise N.FedAvgError(f"nvflare_amd: cannot stage a client of {extent} fp32 elements on device "
-                                f"{self.device} (HBM budget {self.max_resident_bytes} bytes)")
+            raise N.FedAvgError(f"nvflare_amd: cannot stage a client of {extent} {arena.np_dtype} elements on "
+                                f"device {self.device} (HBM budget {self.max_resident_bytes} bytes)")
         return slot
 
     def _release_slot(self, slot: _Slot) -> None:
-        if slot in self._live_slots:
-            self._live_slots.remove(slot)
+        live = slot.slab.arena.live
+        if slot in live:
+            live.remove(slot)
             slot.slab.free.append(slot.index)
 
     # ------------------------------------------------------------------ layout
@@ -350,25 +407,25 @@ class DeviceFedAvg:
         st.op = op
         st.fin = fin
         st.n = int(np.prod(shape, dtype=np.int64)) if shape else 1
-        st.arena = in_np == np.dtype(np.float32) and acc_np == np.dtype(np.float32)
-        if st.arena:
-            st.offset = self.layout_elems
-            self.layout_elems += (st.n + ALIGN_ELEMS - 1) // ALIGN_ELEMS * ALIGN_ELEMS
+        if in_np == acc_np and in_np in _ARENA_FORMATS:
+            st.arena = self._arena(in_np)
+            st.offset = st.arena.layout_elems
+            st.arena.layout_elems += (st.n + ALIGN_ELEMS - 1) // ALIGN_ELEMS * ALIGN_ELEMS
         else:
             st.offset = -1
         self.keys[name] = st
         return st
 
-    def _ensure_arena_acc(self) -> None:
-        need = max(self.layout_elems, ALIGN_ELEMS) * 4
-        if self.arena_acc is not None and self.arena_acc.nbytes >= need:
+    def _ensure_acc(self, arena: _Arena) -> None:
+        need = max(arena.layout_elems, ALIGN_ELEMS) * arena.esize
+        if arena.acc is not None and arena.acc.nbytes >= need:
             return
         new = self.ctx.alloc(need)
-        if self.arena_acc is not None:
-            self.ctx.d2d(new.ptr, self.arena_acc.ptr, self.arena_acc.nbytes)
+        if arena.acc is not None:
+            self.ctx.d2d(new.ptr, arena.acc.ptr, arena.acc.nbytes)
             self.ctx.sync()
-            self.arena_acc.close()
-        self.arena_acc = new
+            arena.acc.close()
+        arena.acc = new
 
     # ------------------------------------------------------------------ staging
     @staticmethod
@@ -391,6 +448,36 @@ class DeviceFedAvg:
         if is_torch_tensor(v) and v.device.type != "cpu" and v.device.index != self.ctx.device:
             raise ValueError(f"nvflare_amd: tensor on {v.device}, engine on device {self.ctx.device}")
 
+    def _stage_arena(self, arena: _Arena, items, weight) -> None:
+        """One contribution's keys of one arena into one slot (the slot base + logical offsets)."""
+        extent = max(st.offset + st.n for st, _ in items)
+        slot = self._acquire_slot(arena, extent)
+        lay = slot.slab.layout
+        es = arena.esize
+        host_pieces, keep = [], []
+        quantized = []
+        for st, v in sorted(items, key=lambda x: x[0].offset):
+            if isinstance(v, QuantizedPayload):  # fp32 arena only (dequantizes to fp32)
+                quantized.append((st, v))
+                st.pending.append(_Staged(weight, slot=slot))
+                slot.refs += 1
+                self.stats["h2d_bytes"] += v.nbytes
+                continue
+            src, ptr, nbytes, on_dev = self._source(v)
+            if on_dev:
+                self.ctx.d2d_tiled(slot.base, lay.tile * es, lay.tile_stride * es, st.offset * es, ptr, nbytes)
+            else:
+                host_pieces.append((st.offset * es, ptr, nbytes))
+                keep.append(src)
+            st.pending.append(_Staged(weight, slot=slot))
+            slot.refs += 1
+            self.stats["h2d_bytes"] += nbytes
+        # every host key of this client in one pass through the pinned ring (one DMA per 64 MiB)
+        self.ctx.h2d_tiled_multi(slot.base, lay.tile * es, lay.tile_stride * es, host_pieces)
+        del keep
+        for st, v in quantized:  # compressed bytes over PCIe, fp32 written into the slot by the GPU
+            stager().dequantize_into(self.ctx, v, slot.base, lay.tile, lay.tile_stride, st.offset)
+
     def add(self, items: List[Tuple[str, Any]], weight, weighted: bool) -> None:
         """Stage one contribution's device-path arrays (already filtered by exclude_vars)."""
         # quantized payloads dequantize on the device straight into their fp32 slot; other dtypes take
@@ -404,36 +491,14 @@ class DeviceFedAvg:
             for _, v in states:
                 self._check_device(v)
             self._round_clients += 1
-            arena_items = [(st, v) for st, v in states if st.arena and st.n > 0]
-            if arena_items:
-                extent = max(st.offset + st.n for st, _ in arena_items)
-                slot = self._acquire_slot(extent)
-                lay = slot.slab.layout
-                host_pieces, keep = [], []
-                quantized = []
-                for st, v in sorted(arena_items, key=lambda x: x[0].offset):
-                    if isinstance(v, QuantizedPayload):
-                        quantized.append((st, v))
-                        st.pending.append(_Staged(weight, slot=slot))
-                        slot.refs += 1
-                        self.stats["h2d_bytes"] += v.nbytes
-                        continue
-                    src, ptr, nbytes, on_dev = self._source(v)
-                    if on_dev:
-                        self.ctx.d2d_tiled(slot.base, lay.tile * 4, lay.tile_stride * 4, st.offset * 4, ptr, nbytes)
-                    else:
-                        host_pieces.append((st.offset * 4, ptr, nbytes))
-                        keep.append(src)
-                    st.pending.append(_Staged(weight, slot=slot))
-                    slot.refs += 1
-                    self.stats["h2d_bytes"] += nbytes
-                # every host key of this client in one pass through the pinned ring (one DMA per 64 MiB)
-                self.ctx.h2d_tiled_multi(slot.base, lay.tile * 4, lay.tile_stride * 4, host_pieces)
-                del keep
-                for st, v in quantized:  # compressed bytes over PCIe, fp32 written into the slot by the GPU
-                    stager().dequantize_into(self.ctx, v, slot.base, lay.tile, lay.tile_stride, st.offset)
+            by_arena: Dict[int, Tuple[_Arena, list]] = {}
             for st, v in states:
-                if st.arena or st.n == 0:
+                if st.arena is not None and st.n > 0:
+                    by_arena.setdefault(st.arena.fmt, (st.arena, []))[1].append((st, v))
+            for arena, arena_items in by_arena.values():
+                self._stage_arena(arena, arena_items, weight)
+            for st, v in states:
+                if st.arena is not None or st.n == 0:
                     if st.n == 0:
                         st.pending.append(_Staged(weight))
                     continue
@@ -451,13 +516,15 @@ class DeviceFedAvg:
                 st.count = weight if st.count is None else st.count + weight
 
     # ------------------------------------------------------------------ compute
-    def _runs(self, keys: Optional[Dict[str, _KeyState]] = None):
-        """Arena keys in offset order, grouped into maximal runs with identical launch parameters."""
+    def _runs(self, keys: Optional[Dict[str, _KeyState]] = None, arena: Optional[_Arena] = None):
+        """One arena's keys (default: fp32) in offset order, grouped into maximal runs with identical launch
+        parameters."""
         keys = self.keys if keys is None else keys
-        arena = sorted((st for st in keys.values() if st.arena and st.n > 0 and not st.done),
+        arena = self.f32 if arena is None else arena
+        keyed = sorted((st for st in keys.values() if st.arena is arena and st.n > 0 and not st.done),
                        key=lambda s: s.offset)
         runs = []
-        for st in arena:
+        for st in keyed:
             sig = (tuple(id(p.slot) for p in st.pending), tuple(p.weight for p in st.pending), st.acc_valid, st.op,
                    st.fin, st.count)
             if runs and runs[-1][0] == sig:
@@ -468,25 +535,34 @@ class DeviceFedAvg:
 
     def _launch_run(self, group: List[_KeyState], final: bool, out: Optional[int] = None,
                     epi: Optional["N.Epilogue"] = None) -> None:
-        """Launch the kernels for one run of keys into the flat accumulator ``out`` (default: the arena).
-        With ``epi`` the last launch carries the server-optimizer epilogue (deferred rounds)."""
+        """Launch the kernels for one run of keys into the flat accumulator ``out`` (default: the arena's).
+        With ``epi`` (fp32 only) the last launch carries the server-optimizer epilogue (deferred rounds)."""
         first, last = group[0], group[-1]
+        arena = first.arena
         begin = first.offset
-        end = (last.offset + last.n + 3) // 4 * 4  # inside the key's 256-byte aligned extent
+        end = arena.launch_end(last)
         pend = first.pending
         if not pend and not (final and first.acc_valid):
             return
-        out = self.arena_acc.ptr if out is None else out
+        out = arena.acc.ptr if out is None else out
         acc_in = out if first.acc_valid else None
         fin = first.fin if final else N.FEDAVG_FIN_NONE
+        # a fold can happen while a contribution is being staged (its second arena needs room), before the
+        # contribution's weight is counted: the count only matters to the finalisation
+        count = float(first.count) if first.count is not None else 1.0
+        if epi is not None and arena.fmt != N.FEDAVG_F32:
+            raise TypeError("nvflare_amd: server-optimizer epilogues run on fp32 keys only")
 
         def launch(bases, weights, tile, stride, fin_, last_launch):
-            if epi is not None and last_launch:
-                self.ctx.accumulate_tiled_epi(bases, weights, tile, stride, begin, end, out, first.op, fin_,
-                                              float(first.count), epi, acc_in)
+            if arena.fmt != N.FEDAVG_F32:
+                self.ctx.accumulate_tiled16(arena.fmt, bases, weights, tile, stride, begin, end, out, first.op, fin_,
+                                            count, acc_in)
+            elif epi is not None and last_launch:
+                self.ctx.accumulate_tiled_epi(bases, weights, tile, stride, begin, end, out, first.op, fin_, count,
+                                              epi, acc_in)
             else:
-                self.ctx.accumulate_tiled(bases, weights, tile, stride, begin, end, out, first.op, fin_,
-                                          float(first.count), acc_in)
+                self.ctx.accumulate_tiled(bases, weights, tile, stride, begin, end, out, first.op, fin_, count,
+                                          acc_in)
             self.stats["launches"] += 1
 
         if not pend:  # finalise an already folded sum
@@ -508,22 +584,33 @@ class DeviceFedAvg:
             acc_in = out
 
     def _launch_arena(self, final: bool, keys: Optional[Dict[str, _KeyState]] = None,
-                      out: Optional[int] = None) -> None:
+                      out: Optional[int] = None, arenas: Optional[List[_Arena]] = None) -> None:
+        """Launch every pending run of the given arenas (default: all; with an explicit ``out`` -- a deferred
+        round's accumulator -- the fp32 arena)."""
         keys = self.keys if keys is None else keys
-        if not any(st.arena and st.n > 0 and not st.done for st in keys.values()):
-            return
-        if out is None:
-            self._ensure_arena_acc()
-        for group in self._runs(keys):
-            self._launch_run(group, final, out)
-            self._consume(group)
-            if final:
-                for st in group:
-                    st.done = True
+        if arenas is None:
+            arenas = [self.f32] if out is not None else list(self.arenas.values())
+        for arena in arenas:
+            if not any(st.arena is arena and st.n > 0 and not st.done for st in keys.values()):
+                continue
+            if out is None:
+                self._ensure_acc(arena)
+            for group in self._runs(keys, arena):
+                self._launch_run(group, final, out)
+                self._consume(group)
+                if final:
+                    for st in group:
+                        st.done = True
 
     def _consume(self, group: List[_KeyState]) -> None:
-        """The group's staged slots are folded into its accumulator: drop them (recycle at refs == 0)."""
+        """The group's staged slots are folded into its accumulator: drop them (recycle at refs == 0).
+
+        Only keys that had staged contributions become ``acc_valid``: a fold can run while a contribution is
+        being staged, when a key it introduces is registered but not staged yet -- that key has nothing in
+        the accumulator, and its first contribution must still take the first-operation path."""
         for st in group:
+            if not st.pending:
+                continue
             for p in st.pending:
                 p.slot.refs -= 1
                 if p.slot.refs == 0:
@@ -533,7 +620,7 @@ class DeviceFedAvg:
 
     def _launch_side(self, final: bool) -> None:
         for st in self.keys.values():
-            if st.arena or st.n == 0:
+            if st.arena is not None or st.n == 0:
                 continue
             if not st.pending and not (final and st.acc_valid):
                 continue
@@ -548,7 +635,7 @@ class DeviceFedAvg:
                 st.acc_dt,
                 st.op,
                 st.fin if final else N.FEDAVG_FIN_NONE,
-                float(st.count),
+                float(st.count) if st.count is not None else 1.0,
                 acc_in_ptr=st.acc_buf.ptr if st.acc_valid else None,
             )
             self.stats["launches"] += 1
@@ -565,19 +652,25 @@ class DeviceFedAvg:
         self._side_bufs.clear()
         self.stats["folds"] += 1
 
+    def _host_arenas(self, arenas) -> Dict[int, np.ndarray]:
+        """One D2H per arena holding host-container keys (results are views of these arrays)."""
+        hosts = {}
+        for a in arenas:
+            if a.layout_elems and any(st.arena is a and st.n > 0 and st.torch_device is None for st in self.keys.values()):
+                host = a.host_pool.take(a.layout_elems, a.np_dtype)
+                self.ctx.d2h(host, a.acc.ptr)
+                hosts[a.fmt] = host
+        return hosts
+
     def result(self) -> Dict[str, Any]:
         """Finalise every key on the device and return host (or device-tensor) results."""
         with self.lock, self.ctx.lock:
             self._settle()
             self._launch_arena(final=True)
             self._launch_side(final=True)
-            host_arena = None
-            if self.layout_elems and any(st.arena and st.n > 0 and st.torch_device is None for st in self.keys.values()):
-                host_arena = self._host_pool.take(self.layout_elems)
-                self.ctx.d2h(host_arena, self.arena_acc.ptr)
-            else:
-                self.ctx.sync()
-            return {name: self._materialize(st, host_arena) for name, st in self.keys.items()}
+            hosts = self._host_arenas(self.arenas.values())
+            self.ctx.sync()
+            return {name: self._materialize(st, hosts) for name, st in self.keys.items()}
 
     def result_deferred(self) -> Dict[str, Any]:
         """``result()`` with the fp32 arena keys left on the device: they come back as ``DeferredAggregate``
@@ -589,14 +682,19 @@ class DeviceFedAvg:
 
         with self.lock, self.ctx.lock:
             self._settle()
+            others = [a for a in self.arenas.values() if a.fmt != N.FEDAVG_F32]
+            self._launch_arena(final=True, arenas=others)
             self._launch_side(final=True)
+            hosts = self._host_arenas(others)
             self.ctx.sync()
-            deferred = {n: st for n, st in self.keys.items() if st.arena and st.n > 0}
-            eager = {n: self._materialize(st, None) for n, st in self.keys.items() if n not in deferred}
+            deferred = {n: st for n, st in self.keys.items() if st.arena is not None and st.arena.fmt == N.FEDAVG_F32
+                        and st.n > 0}
+            eager = {n: self._materialize(st, hosts) for n, st in self.keys.items() if n not in deferred}
             if not deferred:
                 return eager
-            self._ensure_arena_acc()
-            acc, self.arena_acc = self.arena_acc, None  # the round owns this accumulator from now on
+            f32 = self.f32
+            self._ensure_acc(f32)
+            acc, f32.acc = f32.acc, None  # the round owns this accumulator from now on
             rnd = DeferredRound(self, deferred, acc)
             self._deferred = rnd
             return {n: eager[n] if n in eager else DeferredAggregate(rnd, n) for n in self.keys}
@@ -610,15 +708,16 @@ class DeviceFedAvg:
             self._consolidate()
 
     def _consolidate(self) -> None:
-        if self._live_slots or self._deferred is not None:
+        if self._deferred is not None or self.slab_slots:
             return
-        if len(self.slabs) > 1 and not self.slab_slots:
-            # a round needed several slabs: next round gets one slab of the observed client count
-            for s in self.slabs:
-                s.buf.close()
-            self.slabs.clear()
+        for a in self.arenas.values():
+            if not a.live and len(a.slabs) > 1:
+                # a round needed several slabs: next round gets one slab of the observed client count
+                for s in a.slabs:
+                    s.buf.close()
+                a.slabs.clear()
 
-    def _materialize(self, st: _KeyState, host_arena):
+    def _materialize(self, st: _KeyState, hosts: Dict[int, np.ndarray]):
         if st.n == 0:
             if st.container == "torch":
                 return torch.empty(st.shape, dtype=_NP_TO_TORCH[st.acc_np],
@@ -626,12 +725,12 @@ class DeviceFedAvg:
             arr = np.empty(st.shape, dtype=st.acc_np)
         elif st.torch_device is not None:
             t = torch.empty(st.shape, dtype=_NP_TO_TORCH[st.acc_np], device=st.torch_device)
-            src = self.arena_acc.ptr + st.offset * 4 if st.arena else st.acc_buf.ptr
+            src = st.arena.acc.ptr + st.offset * st.arena.esize if st.arena is not None else st.acc_buf.ptr
             self.ctx.d2d(t.data_ptr(), src, st.n * st.acc_np.itemsize)
             self.ctx.sync()
             return t
-        elif st.arena:
-            arr = host_arena[st.offset: st.offset + st.n].reshape(st.shape)
+        elif st.arena is not None:
+            arr = hosts[st.arena.fmt][st.offset: st.offset + st.n].reshape(st.shape)
         else:
             arr = np.empty(st.shape, dtype=st.acc_np)
             self.ctx.d2h(arr.reshape(-1) if arr.ndim else arr.reshape(1), st.acc_buf.ptr)
@@ -650,11 +749,14 @@ class DeviceFedAvg:
         self._round_clients = 0
         if self._ctx is None:
             self.keys.clear()
-            self.layout_elems = 0
+            for a in self.arenas.values():
+                a.layout_elems = 0
             return
         with self.lock, self.ctx.lock:
-            if self._deferred is None:  # a deferred round keeps its slots until it is settled
-                for slot in list(self._live_slots):
+            for a in self.arenas.values():
+                if self._deferred is not None and a.fmt == N.FEDAVG_F32:
+                    continue  # a deferred round keeps its fp32 slots until it is settled
+                for slot in list(a.live):
                     self._release_slot(slot)
             for b in self._side_bufs:
                 b.close()
@@ -664,7 +766,8 @@ class DeviceFedAvg:
                     st.acc_buf.close()
             self._consolidate()
             self.keys.clear()
-            self.layout_elems = 0
+            for a in self.arenas.values():
+                a.layout_elems = 0
 
     def release(self) -> None:
         """Free every device buffer held by this engine."""
@@ -673,9 +776,10 @@ class DeviceFedAvg:
                 with self.ctx.lock:
                     self._settle()
             self.reset()
-            for s in self.slabs:
-                s.buf.close()
-            self.slabs.clear()
-            if self.arena_acc is not None:
-                self.arena_acc.close()
-                self.arena_acc = None
+            for a in self.arenas.values():
+                for s in a.slabs:
+                    s.buf.close()
+                a.slabs.clear()
+                if a.acc is not None:
+                    a.acc.close()
+                    a.acc = None

@@ -160,3 +160,84 @@ def test_device_bf16_tensors_through_helper():
     assert same_bits(as_f32_values(out["w"].cpu(), "bfloat16"), exp)
     exp_h = orc.torch16_vector_reference([r.to(torch.float16).numpy().astype(np.float32) for r in rows], ws, "float16")
     assert same_bits(out["h"].cpu().numpy().astype(np.float32), exp_h)
+
+
+# ---------------------------------------------------------------------------------------------------
+# the tiled 16-bit kernel (engine slabs for float16 / bfloat16 keys) against the oracle, every element
+# ---------------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("fmt,mode", CONFIGS)
+@pytest.mark.parametrize("K,slots,begin,end", [(1, 1, 0, 8), (5, 8, 0, 3 * 4096 + 8), (7, 16, 4096 - 8, 2 * 4096 + 64),
+                                               (131, 131, 0, 4096 + 16)])
+def test_tiled16_vs_oracle(ctx, fmt, mode, K, slots, begin, end):
+    from nvflare_amd import _native as N
+    from nvflare_amd.device import TiledLayout
+
+    n = (end + 4095) // 4096 * 4096
+    rng = np.random.default_rng(K + begin + end)
+    rows = [_bits((rng.standard_normal(n) * 4).astype(np.float32), fmt) for _ in range(K)]
+    ws = [float(rng.random() * 20 + 1e-3) for _ in range(K)]
+    vals = [_vals(r[begin:end], fmt) for r in rows]
+    if mode in ("torch", "unweighted"):
+        op = N.FEDAVG_OP_TORCH if mode == "torch" else N.FEDAVG_OP_UNWEIGHTED
+        fin = N.FEDAVG_FIN_DIV
+        exp = orc.torch16_vector_reference(vals, ws, fmt, weighted=mode == "torch")
+    else:
+        op = N.FEDAVG_OP_NUMPY if mode == "numpy" else N.FEDAVG_OP_UNWEIGHTED
+        fin = N.FEDAVG_FIN_SCALE
+        exp = orc.numpy_mode_reference([r[begin:end].view(np.float16) for r in rows], ws,
+                                       weighted=mode == "numpy").astype(np.float32)
+    code = N.FEDAVG_BF16 if fmt == "bfloat16" else N.FEDAVG_F16
+    lay = TiledLayout(4096, slots)
+    slab = ctx.alloc(lay.slab_elems(n) * 2)
+    bases = [slab.ptr + lay.slot_offset_elems(k) * 2 for k in range(K)]
+    for b, r in zip(bases, rows):
+        ctx.h2d_tiled(b, 4096 * 2, lay.tile_stride * 2, 0, r.ctypes.data, r.nbytes)
+    out = ctx.alloc(n * 2)
+    ctx.accumulate_tiled16(code, bases, ws, 4096, lay.tile_stride, begin, end, out.ptr, op, fin, _count(ws))
+    got = np.empty(n, np.uint16)
+    ctx.d2h(got, out.ptr)
+    assert same_bits(_vals(got[begin:end], fmt), exp)
+    if K >= 3:  # first two clients, then the rest continuing through acc_in
+        ctx.accumulate_tiled16(code, bases[:2], ws[:2], 4096, lay.tile_stride, begin, end, out.ptr, op,
+                               N.FEDAVG_FIN_NONE, 1.0)
+        ctx.accumulate_tiled16(code, bases[2:], ws[2:], 4096, lay.tile_stride, begin, end, out.ptr, op, fin,
+                               _count(ws), acc_in_ptr=out.ptr)
+        ctx.d2h(got, out.ptr)
+        assert same_bits(_vals(got[begin:end], fmt), exp)
+    slab.close()
+    out.close()
+
+
+@pytest.mark.parametrize("budget", [None, 1])
+def test_engine_mixed_fp32_bf16_model(budget):
+    """An fp32 + bf16 + fp16 + int64 model through the helper: 16-bit keys in their own tiled arenas, partial
+    keys, several slab geometries (40 clients), folding under a 1-byte budget -- bit-exact vs the oracle."""
+    from nvflare_amd.app_common.aggregators.weighted_aggregation_helper import WeightedAggregationHelper
+
+    rng = np.random.default_rng(9)
+    K = 40
+    shapes = {"a.w": (64, 129), "a.b": (64,), "emb": (5000, 3), "ln": (7,)}
+    clients = []
+    for k in range(K):
+        c = {"a.w": torch.from_numpy(rng.standard_normal(shapes["a.w"]).astype(np.float32)),
+             "a.b": torch.from_numpy(rng.standard_normal(shapes["a.b"]).astype(np.float32)).to(torch.bfloat16),
+             "emb": torch.from_numpy(rng.standard_normal(shapes["emb"]).astype(np.float32)).to(torch.bfloat16),
+             "ln": torch.from_numpy(rng.standard_normal(shapes["ln"]).astype(np.float16)),
+             "steps": torch.tensor(k, dtype=torch.int64)}
+        if k == 3:
+            del c["emb"]  # a partial contribution
+        clients.append(c)
+    ws = [float(1 + (37 * k) % 11) for k in range(K)]
+    h = WeightedAggregationHelper(max_resident_bytes=budget)
+    for k, (c, w) in enumerate(zip(clients, ws)):
+        h.add(c, w, f"s{k}", 0)
+    out = h.get_result()
+    for key in ("a.b", "emb", "ln"):
+        fmt = "bfloat16" if out[key].dtype == torch.bfloat16 else "float16"
+        seq = [(as_f32_values(c[key], fmt).reshape(-1), w) for c, w in zip(clients, ws) if key in c]
+        exp = orc.torch16_vector_reference([r for r, _ in seq], [w for _, w in seq], fmt)
+        assert same_bits(as_f32_values(out[key], fmt).reshape(-1), exp), key
+    exp_w = orc.torch_mode_reference([c["a.w"].clone() for c in clients], ws)
+    assert same_bits(out["a.w"].numpy(), exp_w.numpy())
+    if budget == 1:
+        assert h.engine.stats["folds"] >= 1

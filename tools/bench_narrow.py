@@ -21,6 +21,9 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--mode", choices=["torch", "numpy"], default="torch")
     ap.add_argument("--blocks-per-cu", default="2", help="comma list: interleaved same-process sweep")
+    ap.add_argument("--layout", choices=["rows", "tiled"], default="tiled",
+                    help="rows: K separate client buffers (fedavg_accumulate); tiled: the engine's slab "
+                         "(fedavg_accumulate_tiled16)")
     args = ap.parse_args()
     import torch
 
@@ -32,30 +35,45 @@ def main():
     tdt = torch.bfloat16 if args.fmt == "bfloat16" else torch.float16
     g = torch.Generator(device="cuda:0")
     g.manual_seed(0)
-    rows = [torch.randn(P, dtype=tdt, device="cuda:0", generator=g) for _ in range(K)]
-    out = torch.empty(P, dtype=tdt, device="cuda:0")
+    from nvflare_amd.device import TiledLayout
+
+    lay = TiledLayout(4096, K)
+    if args.layout == "tiled":
+        slab = torch.randn(lay.slab_elems(P), dtype=tdt, device="cuda:0", generator=g)
+        rows = [slab]
+        bases = [slab.data_ptr() + lay.slot_offset_elems(k) * 2 for k in range(K)]
+    else:
+        rows = [torch.randn(P, dtype=tdt, device="cuda:0", generator=g) for _ in range(K)]
+        bases = [r.data_ptr() for r in rows]
+    out = torch.empty((P + 7) // 8 * 8, dtype=tdt, device="cuda:0")
     torch.cuda.synchronize()
     code = N.FEDAVG_BF16 if args.fmt == "bfloat16" else N.FEDAVG_F16
     op = N.FEDAVG_OP_TORCH if args.mode == "torch" else N.FEDAVG_OP_NUMPY
     fin = N.FEDAVG_FIN_DIV if args.mode == "torch" else N.FEDAVG_FIN_SCALE
     ws = [float(1 + (37 * k) % 100) for k in range(K)]
-    ptrs = [r.data_ptr() for r in rows]
+    end = (P + 7) // 8 * 8
+
+    def launch():
+        if args.layout == "tiled":
+            ctx.accumulate_tiled16(code, bases, ws, 4096, lay.tile_stride, 0, end, out.data_ptr(), op, fin, sum(ws))
+        else:
+            ctx.accumulate(bases, ws, P, out.data_ptr(), code, code, op, fin, sum(ws))
     alg = 2.0 * K * P + 2.0 * P
     bpcs = [int(b) for b in args.blocks_per_cu.split(",")]
     res = {b: [] for b in bpcs}
     for rep in range(3):
         for b in bpcs:
             ctx.set_launch(b, 0)
-            ctx.accumulate(ptrs, ws, P, out.data_ptr(), code, code, op, fin, sum(ws))
+            launch()
             ctx.sync()
             ctx.timing_begin()
             for _ in range(args.steps):
-                ctx.accumulate(ptrs, ws, P, out.data_ptr(), code, code, op, fin, sum(ws))
+                launch()
             res[b].append(ctx.timing_end() / args.steps)
     for b in bpcs:
         ms = sorted(res[b])[len(res[b]) // 2]
         print(json.dumps({"tool": "bench_narrow", "fmt": args.fmt, "mode": args.mode, "clients": K, "params": P,
-                          "blocks_per_cu": b, "kernel_ms": round(ms, 3), "alg_GBs": round(alg / ms / 1e6, 1),
+                          "blocks_per_cu": b, "layout": args.layout, "kernel_ms": round(ms, 3), "alg_GBs": round(alg / ms / 1e6, 1),
                           "frac_of_8TBs": round(alg / ms / 1e6 / 8000.0, 4),
                           "GiBs_aggregated": round(2.0 * K * P / (ms / 1e3) / 2 ** 30, 1)}), flush=True)
 
