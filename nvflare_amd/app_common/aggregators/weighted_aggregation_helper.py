@@ -22,7 +22,7 @@ import re
 import threading
 from typing import Any, Callable, Dict, Optional, Set
 
-from ...engine import DeviceFedAvg, is_device_array, is_torch_tensor
+from ...engine import DeviceFedAvg, is_device_array
 from ...ingest import as_mapped
 from ...quantized import QuantizedPayload
 from ...sharding import ShardedFedAvg

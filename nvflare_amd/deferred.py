@@ -20,7 +20,6 @@ reads a value through ``materialize()`` (NVFlare's own lazy-ref protocol, weight
 from __future__ import annotations
 
 import ctypes
-import threading
 from typing import Dict, List, Optional, Tuple
 
 import numpy as np
@@ -66,7 +65,6 @@ class DeferredRound:
         self.acc = acc  # DeviceBuffer over the round's flat layout
         self.settled = False
         self._values: Dict[str, object] = {}
-        self._lock = threading.RLock()
 
     @property
     def device(self) -> int:
