@@ -151,6 +151,13 @@ int fedavg_d2d_tiled(fedavg_ctx* ctx, void* base, size_t tile_bytes, size_t tile
 /* Device -> host; returns when the bytes are in `dst` (waits for prior compute on the handle).  Large
  * pageable destinations are drained through the pinned ring by the host copy threads. */
 int fedavg_d2h(fedavg_ctx* ctx, void* dst, const void* src, size_t nbytes);
+/* Pipelined egress: fedavg_mark records, on the compute stream, that bytes [0, ready_bytes) of the next
+ * fedavg_d2h_marked source are final once the work enqueued so far has run (marks in non-decreasing order);
+ * fedavg_d2h_marked then copies each 64 MiB chunk as soon as its covering mark has fired, so the D2H of the
+ * aggregated model overlaps the launches still producing the rest (get_result, weighted_aggregation_helper.py:
+ * 226-240, on a large model).  Returns when dst holds every byte; consumes the marks. */
+int fedavg_mark(fedavg_ctx* ctx, size_t ready_bytes);
+int fedavg_d2h_marked(fedavg_ctx* ctx, void* dst, const void* src, size_t nbytes);
 int fedavg_d2d(fedavg_ctx* ctx, void* dst, const void* src, size_t nbytes);
 int fedavg_memset(fedavg_ctx* ctx, void* dst, int value, size_t nbytes);
 int fedavg_sync(fedavg_ctx* ctx);

@@ -98,6 +98,8 @@ _SIGNATURES = {
         c_int,  # fin
         c_double,  # count
     ],
+    "fedavg_mark": [c_void_p, c_size_t],
+    "fedavg_d2h_marked": [c_void_p, c_void_p, c_void_p, c_size_t],
     "fedavg_accumulate_tiled16": [
         c_void_p,  # ctx
         c_int,  # fmt

@@ -195,6 +195,9 @@ struct fedavg_ctx {
     int unroll = fedavg::kDefaultUnroll;
     int variant = 0;
     int tile = fedavg::kDefaultTile;  // tile width of the contiguous-rows entry point
+    // readiness marks for fedavg_d2h_marked: (event on the compute stream, bytes of the source final by then)
+    std::vector<std::pair<hipEvent_t, size_t>> marks;
+    std::vector<hipEvent_t> mark_pool;
 
     hipStream_t compute() const { return ext_stream ? ext_stream : own_stream; }
     void activate() const { HIP_CHECK(hipSetDevice(device)); }
@@ -579,6 +582,8 @@ int fedavg_destroy(fedavg_ctx* ctx) {
         }
         for (hipEvent_t ev : {ctx->ev_start, ctx->ev_stop, ctx->ev_copy_done, ctx->ev_region_start, ctx->ev_region_stop})
             if (ev) (void)hipEventDestroy(ev);
+        for (auto& m : ctx->marks) (void)hipEventDestroy(m.first);
+        for (hipEvent_t ev : ctx->mark_pool) (void)hipEventDestroy(ev);
         if (ctx->own_stream) (void)hipStreamDestroy(ctx->own_stream);
         if (ctx->copy_stream) (void)hipStreamDestroy(ctx->copy_stream);
     });
@@ -712,6 +717,87 @@ int fedavg_d2h(fedavg_ctx* ctx, void* dst, const void* src, size_t nbytes) {
             parallel_memcpy(static_cast<char*>(dst) + off, ctx->ring[slot], len);
             if (c + kRingSlots < nchunks) issue(c + kRingSlots);
         }
+    });
+}
+
+int fedavg_mark(fedavg_ctx* ctx, size_t ready_bytes) {
+    return guarded([&] {
+        if (!ctx) throw Error("ctx is NULL");
+        if (!ctx->marks.empty() && ready_bytes < ctx->marks.back().second)
+            throw Error("marks must be recorded in non-decreasing ready_bytes order");
+        ctx->activate();
+        hipEvent_t ev;
+        if (!ctx->mark_pool.empty()) {
+            ev = ctx->mark_pool.back();
+            ctx->mark_pool.pop_back();
+        } else {
+            HIP_CHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        }
+        HIP_CHECK(hipEventRecord(ev, ctx->compute()));
+        ctx->marks.emplace_back(ev, ready_bytes);
+    });
+}
+
+// D2H that starts while the compute stream is still producing `src`: chunk [off, off+len) leaves on the
+// copy stream as soon as the first mark covering off+len has fired (an event recorded right after the
+// launch that finalised those bytes), through the pinned ring drained by the host copy threads.  Bytes
+// past the last mark wait for everything enqueued on the compute stream so far.  Returns when `dst` holds
+// all bytes; the marks are consumed.
+int fedavg_d2h_marked(fedavg_ctx* ctx, void* dst, const void* src, size_t nbytes) {
+    return guarded([&] {
+        if (!ctx) throw Error("ctx is NULL");
+        struct Recycle {  // marks go back to the pool on every exit path
+            fedavg_ctx* c;
+            ~Recycle() {
+                for (auto& m : c->marks) c->mark_pool.push_back(m.first);
+                c->marks.clear();
+            }
+        } recycle{ctx};
+        if (nbytes == 0) return;
+        if (!dst || !src) throw Error("NULL pointer");
+        ctx->activate();
+        HIP_CHECK(hipEventRecord(ctx->ev_copy_done, ctx->compute()));  // "everything so far"
+        size_t mi = 0;
+        auto wait_ready = [&](size_t end) {
+            while (mi < ctx->marks.size() && ctx->marks[mi].second < end) ++mi;
+            hipEvent_t ev = mi < ctx->marks.size() ? ctx->marks[mi].first : ctx->ev_copy_done;
+            HIP_CHECK(hipStreamWaitEvent(ctx->copy_stream, ev, 0));
+        };
+        const bool direct = nbytes < kParallelCopyMin || is_pinned_host(dst);
+        const size_t chunk = direct ? std::max<size_t>(kRingBytes, 1) : kRingBytes;
+        const size_t nchunks = (nbytes + chunk - 1) / chunk;
+        if (direct) {
+            for (size_t c = 0; c < nchunks; ++c) {
+                const size_t off = c * chunk, len = std::min(chunk, nbytes - off);
+                wait_ready(off + len);
+                HIP_CHECK(hipMemcpyAsync(static_cast<char*>(dst) + off, static_cast<const char*>(src) + off, len,
+                                         hipMemcpyDeviceToHost, ctx->copy_stream));
+            }
+            HIP_CHECK(hipStreamSynchronize(ctx->copy_stream));
+            return;
+        }
+        for (int i = 0; i < kRingSlots; ++i)
+            if (ctx->ring_used[i]) HIP_CHECK(hipEventSynchronize(ctx->ring_ev[i]));
+        auto issue = [&](size_t c) {
+            const int slot = (int)(c % kRingSlots);
+            const size_t off = c * chunk, len = std::min(chunk, nbytes - off);
+            wait_ready(off + len);
+            HIP_CHECK(hipMemcpyAsync(ctx->ring[slot], static_cast<const char*>(src) + off, len, hipMemcpyDeviceToHost,
+                                     ctx->copy_stream));
+            HIP_CHECK(hipEventRecord(ctx->ring_ev[slot], ctx->copy_stream));
+            ctx->ring_used[slot] = true;
+        };
+        for (size_t c = 0; c < nchunks && c < (size_t)kRingSlots; ++c) issue(c);
+        for (size_t c = 0; c < nchunks; ++c) {
+            const int slot = (int)(c % kRingSlots);
+            const size_t off = c * chunk, len = std::min(chunk, nbytes - off);
+            HIP_CHECK(hipEventSynchronize(ctx->ring_ev[slot]));
+            parallel_memcpy(static_cast<char*>(dst) + off, ctx->ring[slot], len);
+            if (c + kRingSlots < nchunks) issue(c + kRingSlots);
+        }
+        // later compute (e.g. the next round reusing src) is ordered after these reads
+        HIP_CHECK(hipEventRecord(ctx->ev_copy_done, ctx->copy_stream));
+        HIP_CHECK(hipStreamWaitEvent(ctx->compute(), ctx->ev_copy_done, 0));
     });
 }
 

@@ -193,6 +193,17 @@ class DeviceContext:
             N.call("fedavg_d2h", self.handle, ctypes.c_void_p(host.ctypes.data), ctypes.c_void_p(src_ptr),
                    ctypes.c_size_t(host.nbytes))
 
+    def mark(self, ready_bytes: int) -> None:
+        """Record that bytes [0, ready_bytes) of the next d2h_marked source are final after the work so far."""
+        N.call("fedavg_mark", self.handle, ctypes.c_size_t(int(ready_bytes)))
+
+    def d2h_marked(self, host: np.ndarray, src_ptr: int) -> None:
+        """D2H overlapping the launches still producing src (see mark); returns when host is filled."""
+        if not host.flags.c_contiguous:
+            raise ValueError("d2h_marked needs a C-contiguous host array")
+        N.call("fedavg_d2h_marked", self.handle, ctypes.c_void_p(host.ctypes.data), ctypes.c_void_p(src_ptr),
+               ctypes.c_size_t(host.nbytes))
+
     def d2h_ptr(self, dst_ptr: int, src_ptr: int, nbytes: int) -> None:
         if nbytes:
             N.call("fedavg_d2h", self.handle, ctypes.c_void_p(dst_ptr), ctypes.c_void_p(src_ptr), ctypes.c_size_t(nbytes))

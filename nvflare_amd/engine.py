@@ -46,6 +46,9 @@ except Exception:  # pragma: no cover
 
 ALIGN_ELEMS = 64  # 256 B: every fp32 key starts on a 256-byte boundary of the flat layout
 TILE = 4096  # elements per client segment per tile (the kernel's default geometry)
+# results larger than two of these leave in a pipelined D2H: the finalising launches are split at every
+# EGRESS_CHUNK bytes of results and each finished chunk is copied out while the next ones compute
+EGRESS_CHUNK = 256 << 20
 
 _TORCH_TO_NP = {}
 _NP_TO_TORCH = {}
@@ -534,13 +537,13 @@ class DeviceFedAvg:
         return [g for _, g in runs]
 
     def _launch_run(self, group: List[_KeyState], final: bool, out: Optional[int] = None,
-                    epi: Optional["N.Epilogue"] = None) -> None:
+                    epi: Optional["N.Epilogue"] = None, rng: Optional[Tuple[int, int]] = None) -> None:
         """Launch the kernels for one run of keys into the flat accumulator ``out`` (default: the arena's).
-        With ``epi`` (fp32 only) the last launch carries the server-optimizer epilogue (deferred rounds)."""
+        With ``epi`` (fp32 only) the last launch carries the server-optimizer epilogue (deferred rounds);
+        ``rng`` restricts the launches to a sub-range of the run (pipelined egress)."""
         first, last = group[0], group[-1]
         arena = first.arena
-        begin = first.offset
-        end = arena.launch_end(last)
+        begin, end = rng if rng is not None else (first.offset, arena.launch_end(last))
         pend = first.pending
         if not pend and not (final and first.acc_valid):
             return
@@ -652,23 +655,55 @@ class DeviceFedAvg:
         self._side_bufs.clear()
         self.stats["folds"] += 1
 
-    def _host_arenas(self, arenas) -> Dict[int, np.ndarray]:
+    def _launch_arena_chunked(self, arena: _Arena) -> None:
+        """Final launches of one arena split at every EGRESS_CHUNK bytes of results, with a readiness mark
+        (``fedavg_mark``) after each chunk boundary, for ``fedavg_d2h_marked``."""
+        self._ensure_acc(arena)
+        chunk = max(EGRESS_CHUNK // arena.esize // TILE, 1) * TILE
+        for group in self._runs(self.keys, arena):
+            b, e = group[0].offset, arena.launch_end(group[-1])
+            pos = b
+            while pos < e:
+                hi = min(e, (pos // chunk + 1) * chunk)
+                self._launch_run(group, True, rng=(pos, hi))
+                if hi % chunk == 0:
+                    self.ctx.mark(hi * arena.esize)
+                pos = hi
+            self._consume(group)
+            for st in group:
+                st.done = True
+        self.ctx.mark(arena.layout_elems * arena.esize)
+
+    def _host_arenas(self, arenas, pipelined: Optional[_Arena] = None) -> Dict[int, np.ndarray]:
         """One D2H per arena holding host-container keys (results are views of these arrays)."""
         hosts = {}
-        for a in arenas:
-            if a.layout_elems and any(st.arena is a and st.n > 0 and st.torch_device is None for st in self.keys.values()):
+        for a in sorted(arenas, key=lambda x: x is not pipelined):  # the pipelined D2H first
+            if self._has_host_keys(a):
                 host = a.host_pool.take(a.layout_elems, a.np_dtype)
-                self.ctx.d2h(host, a.acc.ptr)
+                if a is pipelined:
+                    self.ctx.d2h_marked(host, a.acc.ptr)
+                else:
+                    self.ctx.d2h(host, a.acc.ptr)
                 hosts[a.fmt] = host
         return hosts
+
+    def _has_host_keys(self, a: _Arena) -> bool:
+        return bool(a.layout_elems) and any(st.arena is a and st.n > 0 and st.torch_device is None
+                                            for st in self.keys.values())
 
     def result(self) -> Dict[str, Any]:
         """Finalise every key on the device and return host (or device-tensor) results."""
         with self.lock, self.ctx.lock:
             self._settle()
-            self._launch_arena(final=True)
+            # the largest host-bound arena leaves in a pipelined D2H that overlaps its own launches
+            big = [a for a in self.arenas.values()
+                   if a.layout_elems * a.esize >= 2 * EGRESS_CHUNK and self._has_host_keys(a)]
+            pipelined = max(big, key=lambda a: a.layout_elems * a.esize) if big else None
+            if pipelined is not None:
+                self._launch_arena_chunked(pipelined)
+            self._launch_arena(final=True, arenas=[a for a in self.arenas.values() if a is not pipelined])
             self._launch_side(final=True)
-            hosts = self._host_arenas(self.arenas.values())
+            hosts = self._host_arenas(self.arenas.values(), pipelined)
             self.ctx.sync()
             return {name: self._materialize(st, hosts) for name, st in self.keys.items()}
 

@@ -114,6 +114,17 @@ class FakeDeviceContext:
     def d2h(self, host, src):
         host.reshape(-1).view(np.uint8)[:] = self._view(src, host.nbytes)
 
+    def mark(self, ready_bytes):
+        marks = self.__dict__.setdefault("marks", [])
+        assert not marks or ready_bytes >= marks[-1], "marks must be non-decreasing"
+        marks.append(int(ready_bytes))
+
+    def d2h_marked(self, host, src):
+        marks = self.__dict__.pop("marks", [])
+        assert marks and marks[-1] >= host.nbytes, "the last mark must cover the whole copy"
+        self.marked_copies = getattr(self, "marked_copies", 0) + 1
+        self.d2h(host, src)
+
     def d2d(self, dst, src, nbytes):
         self._view(dst, nbytes)[:] = self._view(src, nbytes).copy()
 

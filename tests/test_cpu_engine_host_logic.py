@@ -103,3 +103,26 @@ def test_deferred_round_settles_before_next_round():
         e.reset()
     for v, rows in zip(vals, rounds):
         assert same_bits(np.asarray(v), _one_shot(rows, ws, "numpy"))
+
+
+@pytest.mark.parametrize("slab_slots", [None, 4])
+def test_pipelined_egress_chunks(monkeypatch, slab_slots):
+    """Results above 2 x EGRESS_CHUNK leave through chunked final launches + fedavg_d2h_marked; chunk
+    boundaries fall inside keys, between keys and inside multi-slab chains -- results unchanged."""
+    import nvflare_amd.engine as E
+
+    monkeypatch.setattr(E, "EGRESS_CHUNK", 64 << 10)  # 16 Ki fp32 elements per chunk
+    rng = np.random.default_rng(4)
+    sizes = {"k0": 40_000, "k1": 3, "k2": 70_001, "k3": 16_384}
+    K = 9
+    clients = [{k: rng.standard_normal(n).astype(np.float32) for k, n in sizes.items()} for _ in range(K)]
+    clients[2].pop("k1")  # a partial contribution: k1 forms its own run
+    ws = [float(1 + 3 * k) for k in range(K)]
+    e = fake_engine(slab_slots=slab_slots)
+    for c, w in zip(clients, ws):
+        e.add(list(c.items()), w, True)
+    out = e.result()
+    assert getattr(e.ctx, "marked_copies", 0) == 1
+    for key in sizes:
+        seq = [(c[key], w) for c, w in zip(clients, ws) if key in c]
+        assert same_bits(out[key], _one_shot([v for v, _ in seq], [w for _, w in seq], "numpy")), key
