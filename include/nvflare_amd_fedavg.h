@@ -157,6 +157,8 @@ int fedavg_d2h(fedavg_ctx* ctx, void* dst, const void* src, size_t nbytes);
  * aggregated model overlaps the launches still producing the rest (get_result, weighted_aggregation_helper.py:
  * 226-240, on a large model).  Returns when dst holds every byte; consumes the marks. */
 int fedavg_mark(fedavg_ctx* ctx, size_t ready_bytes);
+/* Drop marks recorded for a copy that will not happen (a producer starts a new marked sequence with it). */
+int fedavg_marks_reset(fedavg_ctx* ctx);
 int fedavg_d2h_marked(fedavg_ctx* ctx, void* dst, const void* src, size_t nbytes);
 int fedavg_d2d(fedavg_ctx* ctx, void* dst, const void* src, size_t nbytes);
 int fedavg_memset(fedavg_ctx* ctx, void* dst, int value, size_t nbytes);

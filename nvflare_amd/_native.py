@@ -99,6 +99,7 @@ _SIGNATURES = {
         c_double,  # count
     ],
     "fedavg_mark": [c_void_p, c_size_t],
+    "fedavg_marks_reset": [c_void_p],
     "fedavg_d2h_marked": [c_void_p, c_void_p, c_void_p, c_size_t],
     "fedavg_accumulate_tiled16": [
         c_void_p,  # ctx

@@ -132,6 +132,7 @@ class DeviceServerOptimizer:
         self.v = torch.zeros(total, dtype=torch.float32, device=dev)
         self.g = None
         self.host_pool = HostArenaPool()  # host copies of p returned by the generator, reused when released
+        self.egress_pending = False  # the last fused step left readiness marks for a pipelined D2H of p
         with torch.no_grad():
             for s in slots:
                 view = self.p[s.offset:s.offset + s.n].view(s.param.shape)
@@ -259,14 +260,29 @@ class DeviceServerOptimizer:
         if not cand:
             return done
         torch.cuda.synchronize(self.torch_device)  # p, m, v written by torch (binding, checkpoint loads)
+        # pipelined egress of the new weights: only when this one round steps every parameter, in a launch order
+        # whose parameter offsets increase (then "bytes [0, X) of p are final" is a true statement per mark)
+        egress = False
+        if len(cand) == 1:
+            rnd, by_key = next(iter(cand.values()))
+            if len(by_key) == len(self.slots):
+                order = sorted(by_key.items(), key=lambda kv: rnd.keys[kv[0]].offset)
+                offs = [s.offset for _, s in order]
+                egress = all(a < b for a, b in zip(offs, offs[1:]))
         for rnd, by_key in cand.values():
             entries = {}
             for key, s in by_key.items():
                 g = groups[id(s.param)]
                 entries[key] = FusedEntry(s.offset, self._epilogue(g, s), (id(g), s.step, s.has_momentum_buffer))
-            names = set(rnd.fused_step(entries))
+            names = set(rnd.fused_step(entries, egress_marks=egress))
             stepped = [s for key, s in by_key.items() if key in names]
-            self.ctx.sync()
+            if egress and len(stepped) == len(self.slots):
+                self.ctx.mark(self.p.numel() * 4)
+                self.egress_pending = True  # _to_host reads p with fedavg_d2h_marked
+            else:
+                if egress:
+                    self.ctx.marks_reset()
+                self.ctx.sync()
             self._advance(stepped, groups)
             done.update(s.name for s in stepped)
         return done
@@ -430,7 +446,12 @@ class PTFedOptModelShareableGenerator(FullModelShareableGenerator):
         if dev is not None and dev.slots:
             torch.cuda.synchronize(dev.torch_device)
             host_p = dev.host_pool.take(dev.p.numel())
-            dev.ctx.d2h(host_p, dev.p.data_ptr())
+            if dev.egress_pending:  # chunks of p leave while the fused launches still run
+                dev.egress_pending = False
+                dev.ctx.d2h_marked(host_p, dev.p.data_ptr())
+                dev.ctx.sync()
+            else:
+                dev.ctx.d2h(host_p, dev.p.data_ptr())
         base = dev.p.data_ptr() if host_p is not None else 0
         for k, v in state.items():
             s = dev.by_name.get(k) if host_p is not None else None

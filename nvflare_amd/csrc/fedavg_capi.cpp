@@ -738,6 +738,14 @@ int fedavg_mark(fedavg_ctx* ctx, size_t ready_bytes) {
     });
 }
 
+int fedavg_marks_reset(fedavg_ctx* ctx) {
+    return guarded([&] {
+        if (!ctx) throw Error("ctx is NULL");
+        for (auto& m : ctx->marks) ctx->mark_pool.push_back(m.first);
+        ctx->marks.clear();
+    });
+}
+
 // D2H that starts while the compute stream is still producing `src`: chunk [off, off+len) leaves on the
 // copy stream as soon as the first mark covering off+len has fired (an event recorded right after the
 // launch that finalised those bytes), through the pinned ring drained by the host copy threads.  Bytes

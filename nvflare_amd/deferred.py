@@ -88,11 +88,21 @@ class DeferredRound:
         st = self.keys.get(name)
         return not self.settled and st is not None and not st.done
 
-    def fused_step(self, entries: Dict[str, FusedEntry]) -> List[str]:
+    def fused_step(self, entries: Dict[str, FusedEntry], egress_marks: bool = False) -> List[str]:
         """Aggregate-and-step every key in ``entries`` that is still pending, one launch per run of keys
         that share the aggregation signature, the entry signature and the layout offset; returns the names
-        stepped.  d = fin(acc) is also stored to the round's accumulator (a later materialize() reads it)."""
+        stepped.  d = fin(acc) is also stored to the round's accumulator (a later materialize() reads it).
+
+        ``egress_marks``: the caller guarantees the entries' optimizer offsets increase with the aggregation
+        offsets and cover the optimizer's whole parameter buffer; launches are then split at every
+        EGRESS_CHUNK bytes and each piece records a readiness mark (``fedavg_mark``) on the parameter
+        bytes it finalised, so the D2H of the new weights (``fedavg_d2h_marked``) overlaps the rest."""
+        from .engine import EGRESS_CHUNK, TILE
+
         eng = self.engine
+        chunk = max(EGRESS_CHUNK // 4 // TILE, 1) * TILE
+        if egress_marks:
+            eng.ctx.marks_reset()
         stepped: List[str] = []
         with self._locked():
             if self.settled:
@@ -104,8 +114,17 @@ class DeferredRound:
                 def flush():
                     if sub:
                         ent = entries[sub[0].name]
-                        epi = _shifted(ent.epi, ent.offset - sub[0].offset)
-                        eng._launch_run(sub, True, self.acc.ptr, epi)
+                        delta = ent.offset - sub[0].offset
+                        epi = _shifted(ent.epi, delta)
+                        if egress_marks:
+                            b, e = sub[0].offset, sub[0].arena.launch_end(sub[-1])
+                            while b < e:
+                                hi = min(e, (b // chunk + 1) * chunk)
+                                eng._launch_run(sub, True, self.acc.ptr, epi, rng=(b, hi))
+                                eng.ctx.mark((hi + delta) * 4)
+                                b = hi
+                        else:
+                            eng._launch_run(sub, True, self.acc.ptr, epi)
                         eng._consume(sub)
                         for st in sub:
                             st.done = True

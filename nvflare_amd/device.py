@@ -197,6 +197,10 @@ class DeviceContext:
         """Record that bytes [0, ready_bytes) of the next d2h_marked source are final after the work so far."""
         N.call("fedavg_mark", self.handle, ctypes.c_size_t(int(ready_bytes)))
 
+    def marks_reset(self) -> None:
+        """Drop recorded marks (start of a new marked sequence, or a copy that will not happen)."""
+        N.call("fedavg_marks_reset", self.handle)
+
     def d2h_marked(self, host: np.ndarray, src_ptr: int) -> None:
         """D2H overlapping the launches still producing src (see mark); returns when host is filled."""
         if not host.flags.c_contiguous:

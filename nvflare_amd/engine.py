@@ -659,6 +659,7 @@ class DeviceFedAvg:
         """Final launches of one arena split at every EGRESS_CHUNK bytes of results, with a readiness mark
         (``fedavg_mark``) after each chunk boundary, for ``fedavg_d2h_marked``."""
         self._ensure_acc(arena)
+        self.ctx.marks_reset()  # a new marked sequence: nothing stale may vouch for these bytes
         chunk = max(EGRESS_CHUNK // arena.esize // TILE, 1) * TILE
         for group in self._runs(self.keys, arena):
             b, e = group[0].offset, arena.launch_end(group[-1])

@@ -119,6 +119,9 @@ class FakeDeviceContext:
         assert not marks or ready_bytes >= marks[-1], "marks must be non-decreasing"
         marks.append(int(ready_bytes))
 
+    def marks_reset(self):
+        self.__dict__.pop("marks", None)
+
     def d2h_marked(self, host, src):
         marks = self.__dict__.pop("marks", [])
         assert marks and marks[-1] >= host.nbytes, "the last mark must cover the whole copy"

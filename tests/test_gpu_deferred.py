@@ -211,3 +211,20 @@ def test_deferred_full_model_weight_diff_apply(container):
                           {k: _np(v.materialize() if isinstance(v, DeferredAggregate) else v).copy() for k, v in diff.items()})
     _assert_same(results[False][0], results[True][0], "weights")
     _assert_same(results[False][1], results[True][1], "diff")
+
+
+@pytest.mark.parametrize("opt", ["adam", "sgd_nesterov"])
+def test_deferred_fedopt_pipelined_weight_egress(monkeypatch, opt):
+    """Fused step split at small EGRESS_CHUNK boundaries with readiness marks; the new weights leave through
+    fedavg_d2h_marked while later pieces compute -- bit-identical to the eager flow."""
+    import nvflare_amd.engine as E
+
+    monkeypatch.setattr(E, "EGRESS_CHUNK", 16 << 10)  # 4096 fp32 params per piece: several per tensor
+    eager, st_e, _ = run_fedopt_sag(False, "torch", opt, 6)
+    fused, st_f, gen = run_fedopt_sag(True, "torch", opt, 6)
+    for (we, de), (wf, df) in zip(eager, fused):
+        _assert_same(we, wf, opt)
+        _assert_same(de, df, opt)
+    for a, b in zip(st_e, st_f):
+        assert same_bits(a, b)
+    assert gen._dev_opt.egress_pending is False
