@@ -3,22 +3,24 @@
 Reference semantics: nvflare/app_common/aggregators/weighted_aggregation_helper.py:153-240.
 Design:
 
-* ``add`` STAGES a contribution's arrays into HBM (H2D for host arrays, D2D for device tensors);
-  nothing is computed on the host and the caller's arrays are never aliased (``:181-199``).
-* fp32 keys live in one flat per-helper layout (each key at a 256-byte aligned element offset).  A
-  contribution's fp32 keys occupy one SLOT of a tiled SLAB: a slab holds S clients, and element i of the
-  client in slot s sits at ``s*T + (i // T) * S*T + i % T`` (T = 4096), so every tile's S client
-  segments are contiguous in HBM and the kernel streams them sequentially.
+* ``add`` STAGES a contribution's arrays into HBM (H2D for host arrays, D2D for device tensors, bytes
+  straight from an mmap for disk-offloaded refs); nothing is computed on the host and the caller's arrays
+  are never aliased (``:181-199``).
+* Keys of one element format (fp32; float16 and bfloat16 totals) live in that format's ARENA: one flat
+  layout (each key at a 256-byte aligned offset), tiled SLABS of client slots, one accumulator.  Element i
+  of the client in slot s sits at ``s*T + (i // T) * S*T + i % T`` (T = 4096) of a slab of S slots, so every
+  tile's S client segments are contiguous in HBM and the kernel streams them sequentially.
 * ``result`` launches the arrival-ordered K-way accumulate-and-finalise kernel over every run of keys
-  that share the same contributor list (one launch for the usual all-keys-from-all-clients case) and
-  copies the results back in one D2H.  Other dtypes (fp64, int32, int64) get a buffer per key per
-  contribution and the generic kernel.
+  that share the same contributor list (one launch per arena for the usual all-keys-from-all-clients case)
+  and copies the results back -- for large models in a pipelined D2H that overlaps the launches.  fp64 and
+  integer / bool keys get a buffer per key per contribution and the generic kernel.
 * If the staged slots would exceed the HBM budget (``max_resident_bytes``, default HBM - 8 GiB), the
-  pending contributions are FOLDED into a device accumulator (same kernel, ``FIN_NONE``) and their slots
+  pending contributions are FOLDED into the accumulators (same kernels, ``FIN_NONE``) and their slots
   recycled; the per-element operation sequence is unchanged, so the bits are too.
 * Slabs persist across rounds.  In the first round they grow geometrically (16, 32, 64, ... slots); at
   ``reset`` a round that needed several slabs is consolidated into one slab of the observed client count,
   so later rounds aggregate in a single launch.
+* ``result_deferred`` leaves the fp32 results in HBM (nvflare_amd/deferred.py) for a fused server step.
 
 Numerics are the reference's, per container type (finding 2):
 numpy -> ``FEDAVG_OP_NUMPY`` + ``FEDAVG_FIN_SCALE``; torch -> ``FEDAVG_OP_TORCH`` + ``FEDAVG_FIN_DIV``;
