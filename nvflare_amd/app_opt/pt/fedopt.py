@@ -276,13 +276,14 @@ class DeviceServerOptimizer:
                 entries[key] = FusedEntry(s.offset, self._epilogue(g, s), (id(g), s.step, s.has_momentum_buffer))
             names = set(rnd.fused_step(entries, egress_marks=egress))
             stepped = [s for key, s in by_key.items() if key in names]
-            if egress and len(stepped) == len(self.slots):
-                self.ctx.mark(self.p.numel() * 4)
-                self.egress_pending = True  # _to_host reads p with fedavg_d2h_marked
-            else:
-                if egress:
-                    self.ctx.marks_reset()
-                self.ctx.sync()
+            with self.ctx.lock:
+                if egress and len(stepped) == len(self.slots):
+                    self.ctx.mark(self.p.numel() * 4)
+                    self.egress_pending = True  # _to_host reads p with fedavg_d2h_marked
+                else:
+                    if egress:
+                        self.ctx.marks_reset()
+                    self.ctx.sync()
             self._advance(stepped, groups)
             done.update(s.name for s in stepped)
         return done
@@ -446,12 +447,13 @@ class PTFedOptModelShareableGenerator(FullModelShareableGenerator):
         if dev is not None and dev.slots:
             torch.cuda.synchronize(dev.torch_device)
             host_p = dev.host_pool.take(dev.p.numel())
-            if dev.egress_pending:  # chunks of p leave while the fused launches still run
-                dev.egress_pending = False
-                dev.ctx.d2h_marked(host_p, dev.p.data_ptr())
-                dev.ctx.sync()
-            else:
-                dev.ctx.d2h(host_p, dev.p.data_ptr())
+            with dev.ctx.lock:  # the handle is shared with the aggregation engine (accepts on other threads)
+                if dev.egress_pending:  # chunks of p leave while the fused launches still run
+                    dev.egress_pending = False
+                    dev.ctx.d2h_marked(host_p, dev.p.data_ptr())
+                    dev.ctx.sync()
+                else:
+                    dev.ctx.d2h(host_p, dev.p.data_ptr())
         base = dev.p.data_ptr() if host_p is not None else 0
         for k, v in state.items():
             s = dev.by_name.get(k) if host_p is not None else None
