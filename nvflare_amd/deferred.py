@@ -101,10 +101,10 @@ class DeferredRound:
 
         eng = self.engine
         chunk = max(EGRESS_CHUNK // 4 // TILE, 1) * TILE
-        if egress_marks:
-            eng.ctx.marks_reset()
         stepped: List[str] = []
         with self._locked():
+            if egress_marks:
+                eng.ctx.marks_reset()
             if self.settled:
                 return stepped
             for group in eng._runs(self.keys):

@@ -38,6 +38,8 @@ import types
 import numpy as np
 import torch
 
+sys.dont_write_bytecode = True  # the reference tree is read-only input: never leave __pycache__ in it
+
 HERE = os.path.dirname(os.path.abspath(__file__))
 
 

@@ -12,6 +12,8 @@ import os
 import sys
 import types
 
+sys.dont_write_bytecode = True  # the reference tree is read-only input: never leave __pycache__ in it
+
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
