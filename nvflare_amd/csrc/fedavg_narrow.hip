@@ -2,7 +2,7 @@
 //
 // Reference: weighted_aggregation_helper.py:181-236 when the client arrays are float16 (numpy) or
 // float16 / bfloat16 tensors (torch): the total keeps the input's 16-bit dtype and every library
-// operation rounds to it.  The library sequence, restated per element (DESIGN.md section 3.5):
+// operation rounds to it.  The library sequence, restated per element (DESIGN.md section 3.4):
 //
 //   numpy float16 (NEP 50: the python weight becomes half(w), computed on the host from fp64):
 //       first  T = h(v * w)                   numpy half loops compute in fp32 and round once
@@ -41,10 +41,14 @@ __device__ __forceinline__ float load16(uint16_t b) {
 template <int FMT>
 __device__ __forceinline__ uint16_t bits16(float x) {
     if constexpr (FMT == FEDAVG_BF16) {
-        // c10::BFloat16 round_to_nearest_even: NaN -> 0x7FC0, else add the rounding bias and truncate
-        const uint32_t u = __float_as_uint(x);
-        if ((u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)0x7fc0u;
-        return (uint16_t)((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
+        // c10::BFloat16 round_to_nearest_even (add the rounding bias, truncate; NaN -> a quiet NaN) is what
+        // gfx950's v_cvt_pk_bf16_f32 does in one instruction: equal bits for every non-NaN fp32 input,
+        // denormals included (exhaustive check over all 2^32 inputs: tools/bf16_cvt_probe.hip).
+        asm volatile("" : "+v"(x));
+        const __bf16 h = (__bf16)x;
+        uint16_t b;
+        __builtin_memcpy(&b, &h, 2);
+        return b;
     } else {
         // The fp32 value must exist before it is narrowed: without this barrier LLVM folds
         // fptrunc(fma(a, b, c)) into v_fma_mixlo_f16, which rounds the exact result to fp16 ONCE -- torch
@@ -173,6 +177,9 @@ __global__ void __launch_bounds__(kBlock) fedavg_rows_narrow(const RowTableNarro
 // ---------------------------------------------------------------------------------------------
 constexpr int kTile16 = 4096;
 constexpr int kCpl16 = kTile16 / (8 * kBlock);  // 2
+#ifndef FEDAVG_NARROW_UNROLL
+#define FEDAVG_NARROW_UNROLL 6  // clients whose loads are in flight together (A/B: profiles/r01/narrow_unroll_ab.jsonl)
+#endif
 
 template <int FMT, int OP, int FIN, bool ACC_IN>
 __global__ void __launch_bounds__(kBlock) fedavg_tiles_narrow(const RowTableNarrow tab, const int K,
@@ -180,7 +187,7 @@ __global__ void __launch_bounds__(kBlock) fedavg_tiles_narrow(const RowTableNarr
                                                                u32x4* out, const int64_t b8, const int64_t e8,
                                                                const float fv) {
     constexpr int64_t T8 = (int64_t)kCpl16 * kBlock;
-    constexpr int UNROLL = 4;
+    constexpr int UNROLL = FEDAVG_NARROW_UNROLL;
     const int64_t t_last = (e8 - 1) / T8;
     for (int64_t t = b8 / T8 + blockIdx.x; t <= t_last; t += gridDim.x) {
         const int64_t off = t * tstride8 + threadIdx.x;
