@@ -1,0 +1,89 @@
+"""Interleaved same-process A/B of launch variant bits (fedavg_set_variant) on the plain aggregation kernel
+and the fused-epilogue kernel: one slab, rounds of (epilogue x variant) so drift and box-to-box HBM variance
+cancel.  Prints one JSON line per measurement and a median summary line per (epilogue, variant).
+
+  python tools/ab_variants.py --clients 64 --params 1e9 --variants 0,4 --epilogues none,adam --rounds 3
+"""
+
+import argparse
+import json
+import os
+import statistics
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+EXTRA = {"none": 4.0, "add_base": 8.0, "sgd": 16.0, "adam": 24.0}  # algorithmic bytes per param beyond 4K
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--clients", type=int, default=64)
+    ap.add_argument("--params", type=float, default=1e9)
+    ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--variants", default="0,4")
+    ap.add_argument("--epilogues", default="none,adam")
+    a = ap.parse_args()
+    from nvflare_amd import _native as N
+    from nvflare_amd.device import DeviceContext, TiledLayout
+
+    ctx = DeviceContext.get(0)
+    K, P = a.clients, int(a.params)
+    lay = TiledLayout(4096, K)
+    end = (P + 3) // 4 * 4
+    slab = ctx.alloc(lay.slab_elems(P) * 4)
+    bases = [slab.ptr + lay.slot_offset_elems(k) * 4 for k in range(K)]
+    for k in range(K):
+        ctx.fill_synthetic_f32(bases[k], P, 1234, k, 0, lay.tile, lay.tile_stride)
+    ws = [float(1 + (37 * k) % 100) for k in range(K)]
+    cnt = sum(ws)
+    bufs = [ctx.alloc(end * 4) for _ in range(3)]
+    for b in bufs:
+        ctx.memset(b.ptr, 0, end * 4)
+    out = ctx.alloc(end * 4)
+    ctx.sync()
+    kinds = {"add_base": N.FEDAVG_EPI_ADD_BASE, "sgd": N.FEDAVG_EPI_SGD, "adam": N.FEDAVG_EPI_ADAM}
+
+    def launcher(epi):
+        if epi == "none":
+            return lambda: ctx.accumulate_tiled(bases, ws, lay.tile, lay.tile_stride, 0, end, out.ptr, 1, 2, cnt)
+        e = N.Epilogue()
+        e.kind = kinds[epi]
+        e.lr, e.momentum, e.beta1, e.beta2, e.eps, e.step = 1e-3, 0.9, 0.9, 0.999, 1e-8, 1.0
+        if epi == "add_base":
+            e.base, o = bufs[0].ptr, out.ptr
+        else:
+            e.param, e.state1, e.state2 = bufs[0].ptr, bufs[1].ptr, bufs[2].ptr
+            o = None
+        return lambda: ctx.accumulate_tiled_epi(bases, ws, lay.tile, lay.tile_stride, 0, end, o, 1, 2, cnt, e)
+
+    variants = [int(v) for v in a.variants.split(",")]
+    epis = a.epilogues.split(",")
+    res = {}
+    for rnd in range(a.rounds):
+        for epi in epis:
+            fn = launcher(epi)
+            for v in variants:
+                ctx.set_variant(v)
+                fn()
+                ctx.timing_begin()
+                for _ in range(a.reps):
+                    fn()
+                ms = ctx.timing_end() / a.reps
+                gbs = (4.0 * K * P + EXTRA[epi] * P) / ms / 1e6
+                res.setdefault((epi, v), []).append(ms)
+                print(json.dumps({"round": rnd, "epilogue": epi, "variant": v, "clients": K, "params": P,
+                                  "ms": round(ms, 4), "GBps": round(gbs, 1), "frac_8TBps": round(gbs / 8000, 4)}),
+                      flush=True)
+    ctx.set_variant(0)
+    for (epi, v), xs in res.items():
+        ms = statistics.median(xs)
+        gbs = (4.0 * K * P + EXTRA[epi] * P) / ms / 1e6
+        print(json.dumps({"summary": True, "epilogue": epi, "variant": v, "clients": K, "params": P,
+                          "median_ms": round(ms, 4), "GBps": round(gbs, 1), "frac_8TBps": round(gbs / 8000, 4)}),
+              flush=True)
+
+
+if __name__ == "__main__":
+    main()
