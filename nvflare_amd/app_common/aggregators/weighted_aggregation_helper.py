@@ -22,6 +22,8 @@ import re
 import threading
 from typing import Any, Callable, Dict, Optional, Set
 
+import numpy as np
+
 from ...engine import DeviceFedAvg, is_device_array
 from ...ingest import as_mapped
 from ...quantized import QuantizedPayload
@@ -167,16 +169,22 @@ class WeightedAggregationHelper(object):
         with self.lock:
             device_items = []
             host_items = []
+            sharded = isinstance(self._engine, ShardedFedAvg)
+            total = self.total
+            kcc = self.key_contribution_counts
             for k, v in data.items():
                 if self.exclude_vars is not None and self.exclude_vars.search(k):
                     self.skipped_keys.add(k)
                     continue
-                self.key_contribution_counts[k] = self.key_contribution_counts.get(k, 0) + 1
+                kcc[k] = kcc.get(k, 0) + 1
+                if type(v) is np.ndarray:  # plain array: no lazy ref, no quantized payload -> device unless host key
+                    (host_items if isinstance(total.get(k), _HostValue) else device_items).append((k, v))
+                    continue
                 materialize = getattr(v, "materialize", None)
-                device_quantized = isinstance(v, QuantizedPayload) and not isinstance(self._engine, ShardedFedAvg)
+                device_quantized = isinstance(v, QuantizedPayload) and not sharded
                 mapped = None
-                if callable(materialize) and not device_quantized and not isinstance(self._engine, ShardedFedAvg) \
-                        and not isinstance(self.total.get(k), _HostValue):
+                if callable(materialize) and not device_quantized and not sharded \
+                        and not isinstance(total.get(k), _HostValue):
                     mapped = as_mapped(v)  # disk-offloaded safetensors ref: staged from the mmap, no tensor built
                 if mapped is not None:
                     v = mapped

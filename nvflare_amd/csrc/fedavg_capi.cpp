@@ -281,13 +281,17 @@ void h2d_impl(fedavg_ctx* ctx, char* dst, size_t tile_b, size_t tstride_b, size_
 // Several host pieces of one client (its keys, in increasing logical order, non-overlapping) packed into
 // the pinned ring by LOGICAL position, so each 64 MiB slot leaves in one tiled DMA however many keys it
 // holds.  Gaps between pieces (key alignment padding) are copied as don't-care bytes.
+// A piece that does not fit the rest of a slot is split: its remainder opens the next slot and the
+// following pieces pack in behind it, so every slot but the last leaves full.
 void h2d_multi_impl(fedavg_ctx* ctx, char* dst, size_t tile_b, size_t tstride_b, int n, const size_t* offs,
                     const void* const* srcs, const size_t* lens) {
     ctx->activate();
     int i = 0;
+    size_t carried = 0;   // bytes of piece i already sent (split across slots)
+    size_t prev_end = 0;  // logical end of the previous piece (pieces sorted, non-overlapping)
     while (i < n && lens[i] == 0) ++i;
     while (i < n) {
-        const size_t win0 = offs[i];
+        const size_t win0 = offs[i] + carried;
         const int slot = ctx->ring_next;
         ctx->ring_next = (ctx->ring_next + 1) % kRingSlots;
         if (ctx->ring_used[slot]) HIP_CHECK(hipEventSynchronize(ctx->ring_ev[slot]));
@@ -300,14 +304,18 @@ void h2d_multi_impl(fedavg_ctx* ctx, char* dst, size_t tile_b, size_t tstride_b,
                 ++i;
                 continue;
             }
-            if (offs[i] < win_end) throw Error("h2d pieces must be sorted and non-overlapping");
-            const size_t rel = offs[i] - win0;
-            if (rel >= kRingBytes) break;
-            const size_t take = std::min(lens[i], kRingBytes - rel);
-            segs.push_back({ring + rel, static_cast<const char*>(srcs[i]), take});
-            win_end = offs[i] + take;
-            if (take < lens[i]) break;  // the rest of this piece goes to the next slot
+            if (carried == 0 && offs[i] < prev_end) throw Error("h2d pieces must be sorted and non-overlapping");
+            const size_t start = offs[i] + carried;
+            const size_t rel = start - win0;
+            if (rel >= kRingBytes) break;  // starts beyond this slot's window: opens the next slot
+            if (carried == 0) prev_end = offs[i] + lens[i];
+            const size_t take = std::min(lens[i] - carried, kRingBytes - rel);
+            segs.push_back({ring + rel, static_cast<const char*>(srcs[i]) + carried, take});
+            win_end = start + take;
+            carried += take;
+            if (carried < lens[i]) break;  // slot full: the rest of this piece opens the next slot
             ++i;
+            carried = 0;
         }
         parallel_gather(segs);
         if (win_end > win0) {
@@ -315,15 +323,6 @@ void h2d_multi_impl(fedavg_ctx* ctx, char* dst, size_t tile_b, size_t tstride_b,
                             ctx->copy_stream);
             HIP_CHECK(hipEventRecord(ctx->ring_ev[slot], ctx->copy_stream));
             ctx->ring_used[slot] = true;
-        }
-        if (i < n && offs[i] < win_end) {
-            // split piece: continue from win_end in a fresh slot
-            const size_t done = win_end - offs[i];
-            const size_t rest_off = win_end;
-            const void* rest_src = static_cast<const char*>(srcs[i]) + done;
-            const size_t rest_len = lens[i] - done;
-            h2d_multi_impl(ctx, dst, tile_b, tstride_b, 1, &rest_off, &rest_src, &rest_len);
-            ++i;
         }
     }
     HIP_CHECK(hipEventRecord(ctx->ev_copy_done, ctx->copy_stream));

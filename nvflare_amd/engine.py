@@ -227,9 +227,10 @@ _FLT_MAX = float(np.finfo(np.float32).max)
 
 class _KeyState:
     __slots__ = ("name", "shape", "container", "torch_device", "in_np", "acc_np", "op", "fin", "n", "arena",
-                 "offset", "pending", "acc_valid", "acc_buf", "count", "done")
+                 "offset", "pending", "acc_valid", "acc_buf", "count", "done", "sig")
 
     def __init__(self):
+        self.sig = None  # (dtype, type(weight), weighted) of plain numpy contributions already type-checked
         self.pending: List[_Staged] = []
         self.acc_valid = False
         self.done = False  # finalised in its arena accumulator (eagerly, or by a deferred round's fused step)
@@ -390,8 +391,12 @@ class DeviceFedAvg:
                 raise RuntimeError("value cannot be converted to type float without overflow")
 
     def _register_key(self, name: str, v, weight, weighted: bool) -> _KeyState:
-        container, in_np, acc_np, op, fin = _resolve_types(v, weight, weighted)
         st = self.keys.get(name)
+        plain = type(v) is np.ndarray
+        if st is not None and plain and st.sig is not None and st.shape == v.shape \
+                and st.sig == (v.dtype, type(weight), weighted):
+            return st  # same inputs to _resolve_types as a contribution already checked: same result
+        container, in_np, acc_np, op, fin = _resolve_types(v, weight, weighted)
         shape = tuple(v.shape)
         if st is not None:
             if st.container != container or st.in_np != in_np or st.acc_np != acc_np:
@@ -401,6 +406,8 @@ class DeviceFedAvg:
                 )
             if st.shape != shape:
                 raise ValueError(f"nvflare_amd: key {name!r} shape {shape} != first contribution's {st.shape}")
+            if plain:
+                st.sig = (v.dtype, type(weight), weighted)
             return st
         st = _KeyState()
         st.name = name
@@ -412,6 +419,8 @@ class DeviceFedAvg:
         st.op = op
         st.fin = fin
         st.n = int(np.prod(shape, dtype=np.int64)) if shape else 1
+        if plain:
+            st.sig = (v.dtype, type(weight), weighted)
         if in_np == acc_np and in_np in _ARENA_FORMATS:
             st.arena = self._arena(in_np)
             st.offset = st.arena.layout_elems
@@ -461,22 +470,27 @@ class DeviceFedAvg:
         es = arena.esize
         host_pieces, keep = [], []
         quantized = []
+        staged = _Staged(weight, slot=slot)  # immutable: shared by every key of this contribution in this slot
+        moved = 0
         for st, v in sorted(items, key=lambda x: x[0].offset):
-            if isinstance(v, QuantizedPayload):  # fp32 arena only (dequantizes to fp32)
+            if type(v) is np.ndarray and v.flags.c_contiguous:  # the common case, without _source's dispatch
+                nbytes = v.nbytes
+                host_pieces.append((st.offset * es, v.ctypes.data, nbytes))
+                keep.append(v)
+            elif isinstance(v, QuantizedPayload):  # fp32 arena only (dequantizes to fp32)
                 quantized.append((st, v))
-                st.pending.append(_Staged(weight, slot=slot))
-                slot.refs += 1
-                self.stats["h2d_bytes"] += v.nbytes
-                continue
-            src, ptr, nbytes, on_dev = self._source(v)
-            if on_dev:
-                self.ctx.d2d_tiled(slot.base, lay.tile * es, lay.tile_stride * es, st.offset * es, ptr, nbytes)
+                nbytes = v.nbytes
             else:
-                host_pieces.append((st.offset * es, ptr, nbytes))
-                keep.append(src)
-            st.pending.append(_Staged(weight, slot=slot))
-            slot.refs += 1
-            self.stats["h2d_bytes"] += nbytes
+                src, ptr, nbytes, on_dev = self._source(v)
+                if on_dev:
+                    self.ctx.d2d_tiled(slot.base, lay.tile * es, lay.tile_stride * es, st.offset * es, ptr, nbytes)
+                else:
+                    host_pieces.append((st.offset * es, ptr, nbytes))
+                    keep.append(src)
+            st.pending.append(staged)
+            moved += nbytes
+        slot.refs += len(items)
+        self.stats["h2d_bytes"] += moved
         # every host key of this client in one pass through the pinned ring (one DMA per 64 MiB)
         self.ctx.h2d_tiled_multi(slot.base, lay.tile * es, lay.tile_stride * es, host_pieces)
         del keep
@@ -494,7 +508,8 @@ class DeviceFedAvg:
             self._check_torch_alpha(items, weight, weighted)
             states = [(self._register_key(k, v, weight, weighted), v) for k, v in items]
             for _, v in states:
-                self._check_device(v)
+                if type(v) is not np.ndarray:
+                    self._check_device(v)
             self._round_clients += 1
             by_arena: Dict[int, Tuple[_Arena, list]] = {}
             for st, v in states:

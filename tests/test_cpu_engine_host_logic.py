@@ -126,3 +126,25 @@ def test_pipelined_egress_chunks(monkeypatch, slab_slots):
     for key in sizes:
         seq = [(c[key], w) for c, w in zip(clients, ws) if key in c]
         assert same_bits(out[key], _one_shot([v for v, _ in seq], [w for _, w in seq], "numpy")), key
+
+
+def test_plain_numpy_fast_path_keeps_type_checks():
+    """Repeat contributions of plain numpy arrays skip type resolution when (dtype, weight type, weighted)
+    and shape match an already-checked contribution; any change still takes the full check."""
+    eng = fake_engine()
+    a = np.arange(10, dtype=np.float32)
+    eng.add([("w", a)], 1.0, True)
+    eng.add([("w", a + 1)], 2.0, True)  # fast path
+    with pytest.raises(TypeError):  # numpy-scalar weight: result dtype float64, not the key's float32
+        eng.add([("w", a)], np.float64(3.0), True)
+    with pytest.raises(TypeError):
+        eng.add([("w", a.astype(np.float64))], 3.0, True)
+    with pytest.raises(ValueError):
+        eng.add([("w", np.arange(11, dtype=np.float32))], 3.0, True)
+    with pytest.raises(TypeError):  # torch tensor for a numpy key
+        eng.add([("w", torch.from_numpy(a))], 3.0, True)
+    eng.add([("w", np.ascontiguousarray(a[::-1]))], 4.0, True)
+    eng.add([("w", a[::-1])], 5.0, True)  # non-contiguous view: staged through a contiguous copy
+    res = eng.result()["w"]
+    vals = [a, a + 1, a[::-1], a[::-1]]
+    assert same_bits(res, _one_shot(vals, [1.0, 2.0, 4.0, 5.0], "numpy"))

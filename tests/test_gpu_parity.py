@@ -419,6 +419,46 @@ def test_engine_multi_slab_chaining(oracle, slots):
     eng.release()
 
 
+def test_h2d_tiled_multi_many_keys_split_across_slots(ctx, oracle):
+    """~240 MB per client in 211 keys: pieces split at every 64 MiB ring-slot boundary, the remainder opening
+    the next slot with later keys packed behind it; bit-exact aggregation of every key."""
+    from nvflare_amd.device import TiledLayout
+
+    tile, K = 4096, 2
+    sizes = [300_017 - 13 * (j % 7) for j in range(211)]
+    offs, off = [], 0
+    for n in sizes:
+        offs.append(off)
+        off += (n + 63) // 64 * 64
+    n_total = off
+    lay = TiledLayout(tile, K)
+    slab = ctx.alloc(lay.slab_elems(n_total) * 4)
+    rng = np.random.default_rng(4)
+    flat = [rng.standard_normal(sum(sizes)).astype(np.float32) for _ in range(K)]
+    clients = []
+    for k in range(K):
+        parts, o = [], 0
+        for n in sizes:
+            parts.append(flat[k][o:o + n])
+            o += n
+        clients.append(parts)
+        ctx.h2d_tiled_multi(slab.ptr + lay.slot_offset_elems(k) * 4, tile * 4, lay.tile_stride * 4,
+                            [(oo * 4, a.ctypes.data, a.nbytes) for oo, a in zip(offs, parts)])
+    ws = [3.0, 1.5]
+    out = ctx.alloc(n_total * 4)
+    ctx.accumulate_tiled([slab.ptr + lay.slot_offset_elems(k) * 4 for k in range(K)], ws, tile, lay.tile_stride, 0,
+                         n_total, out.ptr, 1, 2, _sum(ws))
+    got = np.empty(n_total, np.float32)
+    ctx.d2h(got, out.ptr)
+    exp = oracle.fedavg_c([np.concatenate(c) for c in clients], ws, oracle.MODE_TORCH, nthreads=4)
+    o = 0
+    for oo, n in zip(offs, sizes):
+        assert same_bits(got[oo:oo + n], exp[o:o + n]), oo
+        o += n
+    slab.close()
+    out.close()
+
+
 def test_h2d_tiled_multi_packs_keys(ctx, oracle):
     """Many keys of one client staged in one call: pieces spanning ring-slot boundaries (> 64 MiB),
     zero-length pieces, gaps, pageable and pinned sources."""
