@@ -151,6 +151,10 @@ int fedavg_d2d_tiled(fedavg_ctx* ctx, void* base, size_t tile_bytes, size_t tile
 /* Device -> host; returns when the bytes are in `dst` (waits for prior compute on the handle).  Large
  * pageable destinations are drained through the pinned ring by the host copy threads. */
 int fedavg_d2h(fedavg_ctx* ctx, void* dst, const void* src, size_t nbytes);
+/* Page-lock caller-owned host memory for direct DMA (hipHostRegister, portable across devices): copies to
+ * and from it skip the pinned ring.  The caller unregisters it before the memory is freed. */
+int fedavg_host_register(fedavg_ctx* ctx, void* p, size_t nbytes);
+int fedavg_host_unregister(fedavg_ctx* ctx, void* p);
 /* Pipelined egress: fedavg_mark records, on the compute stream, that bytes [0, ready_bytes) of the next
  * fedavg_d2h_marked source are final once the work enqueued so far has run (marks in non-decreasing order);
  * fedavg_d2h_marked then copies each 64 MiB chunk as soon as its covering mark has fired, so the D2H of the

@@ -66,6 +66,8 @@ _SIGNATURES = {
     "fedavg_h2d_tiled_multi": [c_void_p, c_void_p, c_size_t, c_size_t, c_int, ctypes.POINTER(c_size_t),
                                ctypes.POINTER(c_void_p), ctypes.POINTER(c_size_t)],
     "fedavg_d2h": [c_void_p, c_void_p, c_void_p, c_size_t],
+    "fedavg_host_register": [c_void_p, c_void_p, c_size_t],
+    "fedavg_host_unregister": [c_void_p, c_void_p],
     "fedavg_d2d": [c_void_p, c_void_p, c_void_p, c_size_t],
     "fedavg_memset": [c_void_p, c_void_p, c_int, c_size_t],
     "fedavg_sync": [c_void_p],

@@ -719,6 +719,24 @@ int fedavg_d2h(fedavg_ctx* ctx, void* dst, const void* src, size_t nbytes) {
     });
 }
 
+int fedavg_host_register(fedavg_ctx* ctx, void* p, size_t nbytes) {
+    return guarded([&] {
+        if (!ctx) throw Error("ctx is NULL");
+        if (!p || nbytes == 0) throw Error("nothing to register");
+        ctx->activate();
+        HIP_CHECK(hipHostRegister(p, nbytes, hipHostRegisterPortable));
+    });
+}
+
+int fedavg_host_unregister(fedavg_ctx* ctx, void* p) {
+    return guarded([&] {
+        if (!ctx) throw Error("ctx is NULL");
+        if (!p) throw Error("NULL pointer");
+        ctx->activate();
+        HIP_CHECK(hipHostUnregister(p));
+    });
+}
+
 int fedavg_mark(fedavg_ctx* ctx, size_t ready_bytes) {
     return guarded([&] {
         if (!ctx) throw Error("ctx is NULL");

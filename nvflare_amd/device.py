@@ -75,12 +75,18 @@ class HostArenaPool:
     is alive.  In scatter-and-gather the previous round's result is still referenced while the next one is
     computed, so ``depth`` = 3 lets round r reuse the array of round r - 2."""
 
+    PIN_MIN_BYTES = 16 << 20  # smaller results are cheaper through the pinned ring than to register
+
     def __init__(self, depth: int = 3):
         self._arrs: list = []
         self._depth = depth
         self._lock = threading.Lock()
 
-    def take(self, n: int, dtype=np.float32) -> np.ndarray:
+    def take(self, n: int, dtype=np.float32, pin: Optional["DeviceContext"] = None) -> np.ndarray:
+        """A host array of n elements.  With ``pin``, a new array of at least PIN_MIN_BYTES is page-locked
+        through that context (once; it stays registered while the pool reuses it), so D2H copies into it
+        run at the PCIe rate without the pinned ring's extra host copy; it is unregistered just before
+        its memory is freed (when the pool has dropped it and no view of it is left)."""
         import sys
 
         dtype = np.dtype(dtype)
@@ -92,6 +98,11 @@ class HostArenaPool:
                     self._arrs.append(self._arrs.pop(i))  # most recently used last
                     return a
             a = np.empty(n, dtype=dtype)
+            if pin is not None and a.nbytes >= self.PIN_MIN_BYTES:
+                try:
+                    pin.host_register(a)
+                except N.FedAvgError:  # e.g. a locked-memory limit: the copies go through the pinned ring
+                    pass
             self._arrs.append(a)
             if len(self._arrs) > self._depth:
                 self._arrs.pop(0)
@@ -192,6 +203,21 @@ class DeviceContext:
         if host.nbytes:
             N.call("fedavg_d2h", self.handle, ctypes.c_void_p(host.ctypes.data), ctypes.c_void_p(src_ptr),
                    ctypes.c_size_t(host.nbytes))
+
+    def host_register(self, arr: np.ndarray) -> None:
+        """Page-lock ``arr``'s memory until it is garbage-collected (unregistered first: numpy clears an
+        array's weak references before it frees the data)."""
+        ptr = arr.ctypes.data
+        N.call("fedavg_host_register", self.handle, ctypes.c_void_p(ptr), ctypes.c_size_t(arr.nbytes))
+        fin = weakref.finalize(arr, DeviceContext._unregister_ptr, self, ptr)
+        fin.atexit = False  # at exit the process's memory goes with it
+
+    @staticmethod
+    def _unregister_ptr(ctx: "DeviceContext", ptr: int) -> None:
+        try:
+            N.call("fedavg_host_unregister", ctx.handle, ctypes.c_void_p(ptr))
+        except Exception:  # pragma: no cover - nothing useful to do while an array is being freed
+            pass
 
     def mark(self, ready_bytes: int) -> None:
         """Record that bytes [0, ready_bytes) of the next d2h_marked source are final after the work so far."""

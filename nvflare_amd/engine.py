@@ -697,7 +697,7 @@ class DeviceFedAvg:
         hosts = {}
         for a in sorted(arenas, key=lambda x: x is not pipelined):  # the pipelined D2H first
             if self._has_host_keys(a):
-                host = a.host_pool.take(a.layout_elems, a.np_dtype)
+                host = a.host_pool.take(a.layout_elems, a.np_dtype, pin=self.ctx)
                 if a is pipelined:
                     self.ctx.d2h_marked(host, a.acc.ptr)
                 else:

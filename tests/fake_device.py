@@ -111,6 +111,9 @@ class FakeDeviceContext:
     def d2d_tiled(self, base, tile_b, stride_b, logical_off, src, nbytes):
         self._tiled_write(base, tile_b, stride_b, logical_off, self._view(src, nbytes).copy())
 
+    def host_register(self, arr):
+        self.registered = getattr(self, "registered", 0) + 1  # page-locking has no effect on the CPU
+
     def d2h(self, host, src):
         host.reshape(-1).view(np.uint8)[:] = self._view(src, host.nbytes)
 

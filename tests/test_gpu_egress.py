@@ -40,3 +40,29 @@ def test_pipelined_egress_matches_one_shot(monkeypatch, oracle, container):
         exp = oracle.fedavg_c([a for a, _ in seq], [w for _, w in seq], mode)
         assert same_bits(piped[key], exp), key
         assert same_bits(whole[key], exp), key
+
+
+def test_registered_host_arrays_copy_and_unregister_on_free():
+    """Pool arrays of >= 16 MiB are page-locked for direct D2H; each is unregistered when its memory is freed,
+    so a new array at the same address registers again (hipHostRegister refuses a range registered twice)."""
+    import gc
+
+    from nvflare_amd.device import DeviceContext, HostArenaPool
+
+    ctx = DeviceContext.get(0)
+    n = (HostArenaPool.PIN_MIN_BYTES // 4) + 12345
+    src = np.random.default_rng(5).standard_normal(n).astype(np.float32)
+    buf = ctx.alloc(n * 4)
+    ctx.h2d_ptr(buf.ptr, src.ctypes.data, src.nbytes)
+    for _ in range(4):
+        pool = HostArenaPool(depth=1)
+        a = pool.take(n, np.float32, pin=ctx)
+        ctx.d2h(a, buf.ptr)
+        assert np.array_equal(a.view(np.uint32), src.view(np.uint32))
+        b = pool.take(n, np.float32, pin=ctx)  # `a` is referenced: a new (registered) array, `a` dropped by the pool
+        assert b is not a
+        ctx.d2h(b, buf.ptr)
+        assert np.array_equal(b.view(np.uint32), src.view(np.uint32))
+        del a, b, pool
+        gc.collect()
+    buf.close()
