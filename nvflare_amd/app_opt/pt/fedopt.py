@@ -446,7 +446,7 @@ class PTFedOptModelShareableGenerator(FullModelShareableGenerator):
         host_p = None
         if dev is not None and dev.slots:
             torch.cuda.synchronize(dev.torch_device)
-            host_p = dev.host_pool.take(dev.p.numel())
+            host_p = dev.host_pool.take(dev.p.numel(), pin=dev.ctx)
             with dev.ctx.lock:  # the handle is shared with the aggregation engine (accepts on other threads)
                 if dev.egress_pending:  # chunks of p leave while the fused launches still run
                     dev.egress_pending = False
