@@ -86,6 +86,8 @@ typedef struct fedavg_epilogue {
     float* state1;              /* SGD momentum buffer / Adam exp_avg (in place) */
     float* state2;              /* Adam exp_avg_sq (in place) */
     const float* base;          /* ADD_BASE: flat fp32 base weights (out may alias it) */
+    int amsgrad;                /* Adam: normalise by max_exp_avg_sq = max(max_exp_avg_sq, exp_avg_sq) */
+    float* state3;              /* Adam amsgrad: max_exp_avg_sq (in place) */
 } fedavg_epilogue;
 
 /* Quantized payload formats (nvflare/app_opt/pt/quantization/dequantizer.py:47-185, row f4). */

@@ -176,6 +176,8 @@ class Epilogue(ctypes.Structure):
         ("state1", c_void_p),
         ("state2", c_void_p),
         ("base", c_void_p),
+        ("amsgrad", c_int),
+        ("state3", c_void_p),
     ]
 
 

@@ -12,9 +12,9 @@ What differs is where the step runs.  The reference sets ``param.grad`` and call
 (``fedavg_accumulate_tiled_epi`` with the aggregated difference as ``acc_in``), with torch's
 single-tensor rounding sequence (``tests/test_fedopt_oracle.py``).  The torch optimizer object is kept
 for its ``param_groups`` (read every step, so lr schedulers work unchanged) and its ``state`` is filled
-with views of the device buffers (``momentum_buffer`` / ``exp_avg`` / ``exp_avg_sq`` / ``step``), so
-``optimizer.state_dict()`` checkpoints as before.  Other optimizers, and amsgrad, raise: there is no
-CPU fallback.
+with views of the device buffers (``momentum_buffer`` / ``exp_avg`` / ``exp_avg_sq`` / ``max_exp_avg_sq``
+with amsgrad / ``step``), so ``optimizer.state_dict()`` checkpoints as before.  Other optimizers raise:
+there is no CPU fallback.
 
 ``device`` names the HIP device ("cuda:N" or N); "cpu" (and None) select $NVFLARE_AMD_DEVICE / 0 --
 the product has no CPU path.
@@ -105,9 +105,6 @@ class DeviceServerOptimizer:
         if isinstance(optimizer, torch.optim.SGD):
             return N.FEDAVG_EPI_SGD
         if isinstance(optimizer, torch.optim.Adam):  # AdamW subclasses Adam (decoupled_weight_decay=True)
-            for g in optimizer.param_groups:
-                if g.get("amsgrad"):
-                    raise NotImplementedError("nvflare_amd: Adam(amsgrad=True) has no device kernel")
             return N.FEDAVG_EPI_ADAM
         raise NotImplementedError(
             f"nvflare_amd: server optimizer {type(optimizer).__module__}.{type(optimizer).__name__} has no device "
@@ -130,6 +127,9 @@ class DeviceServerOptimizer:
         self.p = torch.zeros(total, dtype=torch.float32, device=dev)
         self.m = torch.zeros(total, dtype=torch.float32, device=dev)
         self.v = torch.zeros(total, dtype=torch.float32, device=dev)
+        self.vmax = None  # Adam(amsgrad=True): max_exp_avg_sq, allocated with the first amsgrad group
+        if self.kind == N.FEDAVG_EPI_ADAM and any(g.get("amsgrad") for g in self.optimizer.param_groups):
+            self.vmax = torch.zeros(total, dtype=torch.float32, device=dev)
         self.g = None
         self.host_pool = HostArenaPool()  # host copies of p returned by the generator, reused when released
         self.egress_pending = False  # the last fused step left readiness marks for a pipelined D2H of p
@@ -147,6 +147,8 @@ class DeviceServerOptimizer:
                     self.m[s.offset:s.offset + s.n].copy_(st["exp_avg"].reshape(-1).to(dev))
                     self.v[s.offset:s.offset + s.n].copy_(st["exp_avg_sq"].reshape(-1).to(dev))
                     s.step = float(st["step"])
+                if st.get("max_exp_avg_sq") is not None and self.vmax is not None:
+                    self.vmax[s.offset:s.offset + s.n].copy_(st["max_exp_avg_sq"].reshape(-1).to(dev))
                 if id(s.param) not in groups:
                     raise ValueError(f"nvflare_amd: parameter {s.name!r} is not managed by the optimizer")
         self.model.to(dev)  # buffers follow; parameters already live in self.p
@@ -170,6 +172,13 @@ class DeviceServerOptimizer:
             st["step"] = torch.tensor(s.step, dtype=torch.float32)
             st["exp_avg"] = self.m[s.offset:s.offset + s.n].view(s.param.shape)
             st["exp_avg_sq"] = self.v[s.offset:s.offset + s.n].view(s.param.shape)
+            if self._group_of()[id(s.param)].get("amsgrad"):
+                st["max_exp_avg_sq"] = self._max_exp_avg_sq()[s.offset:s.offset + s.n].view(s.param.shape)
+
+    def _max_exp_avg_sq(self) -> torch.Tensor:
+        if self.vmax is None:  # a group switched amsgrad on after binding: torch starts the max at zeros
+            self.vmax = torch.zeros_like(self.v)
+        return self.vmax
 
     def _epilogue(self, group: dict, s: _Slot) -> "N.Epilogue":
         e = N.Epilogue()
@@ -190,6 +199,9 @@ class DeviceServerOptimizer:
             e.decoupled_weight_decay = int(bool(group.get("decoupled_weight_decay", False)))
             e.state2 = self.v.data_ptr()
             e.step = s.step + 1.0
+            if group.get("amsgrad"):
+                e.amsgrad = 1
+                e.state3 = self._max_exp_avg_sq().data_ptr()
         return e
 
     def step(self, model_diff: Dict) -> List[str]:

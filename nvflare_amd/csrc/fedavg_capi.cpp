@@ -405,6 +405,8 @@ fedavg::EpiParams make_epi(const fedavg_epilogue& e) {
     E.state1 = e.state1;
     E.state2 = e.state2;
     E.base = e.base;
+    E.amsgrad = e.kind == FEDAVG_EPI_ADAM && e.amsgrad;
+    E.state3 = e.state3;
     return E;
 }
 
@@ -996,9 +998,11 @@ int fedavg_accumulate_tiled_epi(fedavg_ctx* ctx, const void* const* bases, const
             throw Error("SGD needs param (and state1 with momentum)");
         if (epi->kind == FEDAVG_EPI_ADAM && (!epi->param || !epi->state1 || !epi->state2))
             throw Error("ADAM needs param, state1 (exp_avg), state2 (exp_avg_sq)");
+        if (epi->kind == FEDAVG_EPI_ADAM && epi->amsgrad && !epi->state3)
+            throw Error("ADAM with amsgrad needs state3 (max_exp_avg_sq)");
         if (epi->kind == FEDAVG_EPI_ADAM && epi->step < 1.0) throw Error("ADAM step must be >= 1");
         for (const void* p : {(const void*)epi->param, (const void*)epi->state1, (const void*)epi->state2,
-                              (const void*)epi->base, (const void*)out, acc_in})
+                              (const void*)epi->state3, (const void*)epi->base, (const void*)out, acc_in})
             if (misaligned(p)) throw Error("epilogue/out/acc_in pointers must be 16-byte aligned");
         for (int k = 0; k < k_rows; ++k)
             if (!bases[k] || misaligned(bases[k])) throw Error("base " + std::to_string(k) + " NULL or misaligned");
@@ -1013,7 +1017,7 @@ int fedavg_accumulate_tiled_epi(fedavg_ctx* ctx, const void* const* bases, const
         void* scratch = nullptr;
         if (head > 0) {
             float* partial = static_cast<float*>(out);
-            const void* operands[] = {epi->base, epi->param, epi->state1, epi->state2};
+            const void* operands[] = {epi->base, epi->param, epi->state1, epi->state2, epi->state3};
             bool alias = !out;
             for (const void* q : operands) alias = alias || (q && q == out);
             if (alias) {

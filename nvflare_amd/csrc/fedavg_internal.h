@@ -69,6 +69,8 @@ struct EpiParams {
     float* state1;  // SGD momentum buffer / Adam exp_avg
     float* state2;  // Adam exp_avg_sq
     const float* base;
+    int amsgrad;
+    float* state3;  // Adam amsgrad: max_exp_avg_sq
 };
 
 struct DequantLaunch {

@@ -174,8 +174,15 @@ __device__ __forceinline__ float lerp_torch(float s, float e, float w, float w_m
 // Epilogue operands of one f32x4 column group, loaded at the START of the tile so their HBM latency
 // hides behind the client stream instead of stalling the wave after the last client.
 struct EpiIn {
-    f32x4 a, b, c;  // ADD_BASE: base | SGD: p, momentum buffer | ADAM: p, exp_avg, exp_avg_sq
+    f32x4 a, b, c, d;  // ADD_BASE: base | SGD: p, momentum buffer | ADAM: p, exp_avg, exp_avg_sq (, max_exp_avg_sq)
 };
+
+// torch.maximum: a NaN operand is the result
+__device__ __forceinline__ float max_torch(float a, float b) {
+    if (a != a) return a;
+    if (b != b) return b;
+    return a > b ? a : b;
+}
 
 template <int EPI>
 __device__ __forceinline__ EpiIn epi_load(const EpiParams& E, const int64_t i) {
@@ -189,6 +196,7 @@ __device__ __forceinline__ EpiIn epi_load(const EpiParams& E, const int64_t i) {
         in.a = load4<true>(reinterpret_cast<const f32x4*>(E.param) + i);
         in.b = load4<true>(reinterpret_cast<const f32x4*>(E.state1) + i);
         in.c = load4<true>(reinterpret_cast<const f32x4*>(E.state2) + i);
+        if (E.amsgrad) in.d = load4<true>(reinterpret_cast<const f32x4*>(E.state3) + i);
     }
     return in;
 }
@@ -219,6 +227,7 @@ __device__ __forceinline__ void epilogue4(const EpiParams& E, const int64_t i, c
         f32x4 p = in.a;
         f32x4 m = in.b;
         f32x4 v = in.c;
+        f32x4 vmax = in.d;
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
             float g = E.maximize ? d[c] : -d[c];
@@ -229,7 +238,12 @@ __device__ __forceinline__ void epilogue4(const EpiParams& E, const int64_t i, c
             }
             const float mm = lerp_torch(m[c], g, E.one_minus_beta1, E.one_minus_beta1_m1);
             const float vv = __builtin_fmaf(E.one_minus_beta2 * g, g, v[c] * E.beta2);
-            const float denom = __builtin_sqrtf(vv) / E.bias_correction2_sqrt + E.eps;
+            float vden = vv;
+            if (E.amsgrad) {  // adam.py: torch.maximum(max_exp_avg_sq, exp_avg_sq, out=max_exp_avg_sq)
+                vmax[c] = max_torch(vmax[c], vv);
+                vden = vmax[c];
+            }
+            const float denom = __builtin_sqrtf(vden) / E.bias_correction2_sqrt + E.eps;
             pv = pv + (E.step_size_neg * mm) / denom;
             m[c] = mm;
             v[c] = vv;
@@ -238,6 +252,7 @@ __device__ __forceinline__ void epilogue4(const EpiParams& E, const int64_t i, c
         store4<true>(p4, p);
         store4<true>(reinterpret_cast<f32x4*>(E.state1) + i, m);
         store4<true>(reinterpret_cast<f32x4*>(E.state2) + i, v);
+        if (E.amsgrad) store4<true>(reinterpret_cast<f32x4*>(E.state3) + i, vmax);
     }
 }
 

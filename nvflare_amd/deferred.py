@@ -49,7 +49,7 @@ def _shifted(epi: "N.Epilogue", delta_elems: int) -> "N.Epilogue":
     """A copy of ``epi`` whose flat operand pointers are moved by ``delta_elems`` fp32 elements, so that
     element i of the aggregation layout addresses element i + delta of the optimizer's buffers."""
     e = N.Epilogue.from_buffer_copy(epi)
-    for f in ("param", "state1", "state2", "base"):
+    for f in ("param", "state1", "state2", "state3", "base"):
         p = getattr(e, f)
         if p:
             setattr(e, f, ctypes.c_void_p(p + 4 * delta_elems).value)

@@ -115,7 +115,8 @@ void oracle_synth_fill_f32(uint64_t seed, uint64_t row, const uint64_t* cols, si
  * d = fin(acc) of each element (computed exactly as above):
  *   ADD_BASE  w = base + d            full_model_shareable_generator.py:58-67 (WEIGHT_DIFF apply)
  *   SGD       torch/optim/sgd.py _single_tensor_sgd on grad g = -1.0 * d   (app_opt/pt/fedopt.py:175)
- *   ADAM      torch/optim/adam.py _single_tensor_adam (:347-551) on g = -1.0 * d
+ *   ADAM      torch/optim/adam.py _single_tensor_adam (:347-551) on g = -1.0 * d; amsgrad divides by
+ *             sqrt(vmax), vmax = torch.maximum(vmax, v) kept as a third state
  * Rounding sequence pinned against torch 2.10 CPU (tests/test_fedopt_oracle.py):
  *   add(alpha)  fma(b, alpha, a);   lerp  |w| < .5 ? fma(w, e - s, s) : fma(w - 1, e - s, e)
  *   addcmul     fma(val * t1, t2, self);   addcdiv  self + (val * t1) / t2
@@ -134,7 +135,15 @@ typedef struct {
     int decoupled_weight_decay; /* AdamW */
     double lr, momentum, dampening, weight_decay; /* SGD (+ lr, weight_decay for Adam) */
     double beta1, beta2, eps, step;               /* Adam: step after increment (1, 2, ...) */
+    int amsgrad;                                  /* Adam: normalise by the running max of v (vmax) */
 } oracle_epilogue;
+
+/* torch.maximum: a NaN operand is the result */
+static inline float max_torch(float a, float b) {
+    if (a != a) return a;
+    if (b != b) return b;
+    return a > b ? a : b;
+}
 
 static inline float lerp_torch(float s, float e, float w) {
     const float d = e - s;
@@ -142,7 +151,7 @@ static inline float lerp_torch(float s, float e, float w) {
 }
 
 void oracle_epilogue_apply(const float* delta, size_t n, const oracle_epilogue* epi, float* p, float* m, float* v,
-                           const float* base, float* out) {
+                           float* vmax, const float* base, float* out) {
     for (size_t i = 0; i < n; ++i) {
         const float d = delta[i];
         if (epi->kind == ORACLE_EPI_NONE) {
@@ -173,7 +182,12 @@ void oracle_epilogue_apply(const float* delta, size_t n, const oracle_epilogue* 
             const double bc2 = 1.0 - pow(epi->beta2, epi->step);
             const float step_size_neg = (float)(-(epi->lr / bc1));
             const float bc2s = (float)pow(bc2, 0.5); /* python: bias_correction2**0.5 */
-            const float denom = sqrtf(vv) / bc2s + (float)epi->eps;
+            float vden = vv;
+            if (epi->amsgrad) { /* adam.py: torch.maximum(max_exp_avg_sq, exp_avg_sq, out=max_exp_avg_sq) */
+                vmax[i] = max_torch(vmax[i], vv);
+                vden = vmax[i];
+            }
+            const float denom = sqrtf(vden) / bc2s + (float)epi->eps;
             pv = pv + (step_size_neg * mm) / denom;
             m[i] = mm;
             v[i] = vv;

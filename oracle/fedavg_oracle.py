@@ -262,16 +262,17 @@ class _Epi(ctypes.Structure):
         ("beta2", ctypes.c_double),
         ("eps", ctypes.c_double),
         ("step", ctypes.c_double),
+        ("amsgrad", ctypes.c_int),
     ]
 
 
-def epilogue_apply(delta, kind, p=None, m=None, v=None, base=None, **hp):
-    """Apply an epilogue to the aggregated update `delta` (fp32).  p/m/v are updated IN PLACE (copies
-    are the caller's business); returns `out` for NONE/ADD_BASE and p otherwise."""
+def epilogue_apply(delta, kind, p=None, m=None, v=None, base=None, vmax=None, **hp):
+    """Apply an epilogue to the aggregated update `delta` (fp32).  p/m/v (and vmax with amsgrad=1) are
+    updated IN PLACE (copies are the caller's business); returns `out` for NONE/ADD_BASE and p otherwise."""
     lib = load()
     fn = lib.oracle_epilogue_apply
     fn.restype = None
-    fn.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(_Epi)] + [ctypes.c_void_p] * 5
+    fn.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(_Epi)] + [ctypes.c_void_p] * 6
     delta = np.ascontiguousarray(delta, dtype=np.float32).reshape(-1)
     e = _Epi()
     e.kind = kind
@@ -282,7 +283,9 @@ def epilogue_apply(delta, kind, p=None, m=None, v=None, base=None, **hp):
     def ptr(a):
         return None if a is None else a.ctypes.data
 
-    fn(delta.ctypes.data, delta.size, ctypes.byref(e), ptr(p), ptr(m), ptr(v), ptr(base), out.ctypes.data)
+    if e.amsgrad and vmax is None:
+        raise ValueError("amsgrad needs vmax")
+    fn(delta.ctypes.data, delta.size, ctypes.byref(e), ptr(p), ptr(m), ptr(v), ptr(vmax), ptr(base), out.ctypes.data)
     return out if kind in (EPI_NONE, EPI_ADD_BASE) else p
 
 

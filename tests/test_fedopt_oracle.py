@@ -66,19 +66,29 @@ def test_sgd_bit_exact_vs_torch(oracle, kw):
     (torch.optim.Adam, dict(lr=1e-3, weight_decay=1e-2)),
     (torch.optim.AdamW, dict(lr=1e-3, weight_decay=1e-2)),
     (torch.optim.Adam, dict(lr=1e-3, betas=(0.3, 0.999))),  # lerp weight >= 0.5 branch
+    (torch.optim.Adam, dict(lr=1e-3, amsgrad=True)),
+    (torch.optim.AdamW, dict(lr=1e-3, weight_decay=1e-2, amsgrad=True)),
+    (torch.optim.Adam, dict(lr=1e-3, betas=(0.5, 0.9), amsgrad=True)),  # v falls below its running max often
 ])
 def test_adam_vs_torch(oracle, cls, kw):
     rng = np.random.default_rng(1)
     n = 200_003
     p0 = rng.standard_normal(n).astype(np.float32)
-    deltas = [(rng.standard_normal(n) * 0.01).astype(np.float32) for _ in range(5)]
+    # amsgrad: shrinking later updates let exp_avg_sq fall below its running max (both branches of the max)
+    scales = [1.0, 1.0, 0.05, 1.0, 0.01] if kw.get("amsgrad") else [1.0] * 5
+    deltas = [(rng.standard_normal(n) * 0.01 * sc).astype(np.float32) for sc in scales]
     tp, st = _torch_steps(cls, kw, p0, deltas)
     b1, b2 = kw.get("betas", (0.9, 0.999))
     p, m, v = p0.copy(), np.zeros(n, np.float32), np.zeros(n, np.float32)
+    vmax = np.zeros(n, np.float32)
     for s, d in enumerate(deltas):
-        oracle.epilogue_apply(d, oracle.EPI_ADAM, p=p, m=m, v=v, lr=kw["lr"], beta1=b1, beta2=b2,
+        oracle.epilogue_apply(d, oracle.EPI_ADAM, p=p, m=m, v=v, vmax=vmax, lr=kw["lr"], beta1=b1, beta2=b2,
                               eps=kw.get("eps", 1e-8), weight_decay=kw.get("weight_decay", 0.0 if cls is torch.optim.Adam else 1e-2),
-                              decoupled_weight_decay=int(cls is torch.optim.AdamW), step=float(s + 1))
+                              decoupled_weight_decay=int(cls is torch.optim.AdamW), step=float(s + 1),
+                              amsgrad=int(bool(kw.get("amsgrad"))))
+    if kw.get("amsgrad"):
+        assert same_bits(vmax, st["max_exp_avg_sq"].numpy()), "max_exp_avg_sq"
+        assert np.count_nonzero(vmax != v) > n // 100  # the max branch was exercised
     if kw.get("weight_decay") and cls is torch.optim.Adam:
         # coupled weight decay feeds p (a rounding off through torch's sqrt) back into g = -d + wd*p,
         # so m and v inherit it at the scale of wd*|p|: compare within that

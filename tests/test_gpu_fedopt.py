@@ -251,3 +251,44 @@ def test_epilogue_variants_multi_tile_per_block(ctx, oracle, variant, K, kind):
     finally:
         ctx.set_variant(0)
         dev.close()
+
+
+@pytest.mark.parametrize("K,decoupled", [(7, 0), (3, 1), (0, 0)])
+def test_adam_amsgrad_epilogue(ctx, oracle, K, decoupled):
+    """Adam / AdamW with amsgrad: max_exp_avg_sq (state3) = torch.maximum(max_exp_avg_sq, exp_avg_sq) and the
+    denominator uses it; four steps with shrinking updates so the running max and exp_avg_sq part ways.
+    Bit-exact against the oracle (itself pinned to torch CPU by tests/test_fedopt_oracle.py)."""
+    rng = np.random.default_rng(40 + K)
+    n = 5 * TILE + 12
+    p = rng.standard_normal(n).astype(np.float32)
+    m = np.zeros(n, np.float32)
+    v = np.zeros(n, np.float32)
+    vmax = np.zeros(n, np.float32)
+    hp = dict(lr=1e-3, beta1=0.5, beta2=0.9, eps=1e-8, weight_decay=1e-2 if decoupled else 0.0,
+              decoupled_weight_decay=decoupled)
+    dev = None
+    try:
+        for step, scale in enumerate([1.0, 0.05, 1.0, 0.01]):
+            rows = [(rng.standard_normal(n) * scale).astype(np.float32) for _ in range(K)]
+            ws = [float(1 + (37 * k) % 100) for k in range(K)]
+            delta = (rng.standard_normal(n) * scale).astype(np.float32) if K == 0 else None
+            if dev is not None:
+                kept = {name: dev.get(name) for name in ("p", "m", "v", "vmax")}
+                dev.close()
+            dev = _Dev(ctx, rows, n)
+            if step == 0:
+                kept = {"p": p, "m": m, "v": v, "vmax": vmax}
+            ptrs = {name: dev.buf(name, kept[name]) for name in ("p", "m", "v", "vmax")}
+            e = _epi(3, param=ptrs["p"], state1=ptrs["m"], state2=ptrs["v"], state3=ptrs["vmax"], amsgrad=1,
+                     step=float(step + 1), **hp)
+            acc_ptr = dev.buf("acc", delta) if K == 0 else None
+            ctx.accumulate_tiled_epi(dev.bases, ws, TILE, dev.lay.tile_stride, 0, dev.n4, None, 1,
+                                     2 if K else 0, _sum(ws) if K else 1.0, e, acc_in_ptr=acc_ptr)
+            d = oracle.fedavg_c(rows, ws, oracle.MODE_TORCH, nthreads=8) if K else delta
+            oracle.epilogue_apply(d, oracle.EPI_ADAM, p=p, m=m, v=v, vmax=vmax, amsgrad=1, step=float(step + 1), **hp)
+            assert same_bits(dev.get("p"), p) and same_bits(dev.get("m"), m), step
+            assert same_bits(dev.get("v"), v) and same_bits(dev.get("vmax"), vmax), step
+        assert np.count_nonzero(vmax != v) > n // 100
+    finally:
+        if dev is not None:
+            dev.close()

@@ -132,3 +132,50 @@ def test_full_model_generator_weight_diff_apply():
         for k in base:
             assert same_bits(_np(out[ModelLearnableKey.WEIGHTS][k]), np.asarray(expect[k])), (container, k)
         assert out[ModelLearnableKey.META] == {"x": 1}
+
+
+@pytest.mark.parametrize("cls,args", [("torch.optim.Adam", {"lr": 1e-2, "betas": [0.5, 0.9], "amsgrad": True}),
+                                      ("torch.optim.AdamW", {"lr": 1e-2, "weight_decay": 0.1, "amsgrad": True})])
+def test_fedopt_generator_amsgrad_vs_torch(cls, args):
+    """Adam / AdamW(amsgrad=True) on the device against the reference's arithmetic, torch's CPU optimizer
+    stepping ``param.grad = -diff`` (fedopt.py:157-182), over four rounds with shrinking differences so
+    exp_avg_sq falls below its running max.  m, v and max_exp_avg_sq bit-exact; parameters within
+    ``adam_param_tolerance``; optimizer.state exposes max_exp_avg_sq as a device view."""
+    import copy
+
+    rng = np.random.default_rng(11)
+    model = fedopt_model()
+    ref_model = copy.deepcopy(model)
+    kw = dict(args)
+    if "betas" in kw:
+        kw["betas"] = tuple(kw["betas"])
+    ref_opt = {"torch.optim.Adam": torch.optim.Adam, "torch.optim.AdamW": torch.optim.AdamW}[cls](
+        ref_model.parameters(), foreach=False, **kw)
+    gen = PTFedOptModelShareableGenerator(optimizer_args={"path": cls, "args": copy.deepcopy(args)},
+                                          source_model=model, device="cuda:0")
+    gen.handle_event(EventType.START_RUN, FLContext())
+    w = {k: v.detach().cpu().numpy().copy() for k, v in model.state_dict().items()}
+    p0 = {n: p.detach().cpu().numpy().copy() for n, p in ref_model.named_parameters()}
+    for rnd, scale in enumerate([1.0, 0.02, 1.0, 0.01]):
+        diff = {n: (rng.standard_normal(tuple(p.shape)) * 0.05 * scale).astype(np.float32)
+                for n, p in ref_model.named_parameters()}
+        fl_ctx = FLContext()
+        fl_ctx.set_prop(AppConstants.GLOBAL_MODEL, make_model_learnable(w, {}))
+        out = gen.shareable_to_learnable(DXO(DataKind.WEIGHT_DIFF, data=diff).to_shareable(), fl_ctx)
+        w = out[ModelLearnableKey.WEIGHTS]
+        for n, p in ref_model.named_parameters():
+            p.grad = torch.tensor(-1.0 * diff[n])
+        ref_opt.step()
+        for n, p in ref_model.named_parameters():
+            ref = p.detach().numpy()
+            tol = adam_param_tolerance(p0[n], ref, args["lr"], rnd + 1)
+            assert np.all(np.abs(_np(w[n]).astype(np.float64) - ref.astype(np.float64)) <= tol), (rnd, n)
+    gp = dict(model.named_parameters())
+    moved = 0
+    for n, p in ref_model.named_parameters():
+        st, rst = gen.optimizer.state[gp[n]], ref_opt.state[p]
+        assert st["max_exp_avg_sq"].device.type == "cuda"
+        for key in ("exp_avg", "exp_avg_sq", "max_exp_avg_sq"):
+            assert same_bits(st[key].cpu().numpy(), rst[key].numpy()), (n, key)
+        moved += int((st["max_exp_avg_sq"] != st["exp_avg_sq"]).sum())
+    assert moved > 0
