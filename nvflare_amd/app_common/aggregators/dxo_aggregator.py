@@ -30,18 +30,20 @@ class DXOAggregator(FLComponent):
         weigh_by_local_iter: bool = True,
         device: Optional[int] = None,
         defer_result: bool = False,
+        devices: Optional[list] = None,
     ):
         """Accumulated weighted aggregation of one kind of DXO (dxo_aggregator.py:26-66).
 
-        Args: as the reference, plus ``device`` (HIP device index of the aggregation engine) and
-        ``defer_result`` (fp32 results stay in HBM as ``DeferredAggregate`` values, nvflare_amd/deferred.py).
+        Args: as the reference, plus ``device`` (HIP device index of the aggregation engine),
+        ``defer_result`` (fp32 results stay in HBM as ``DeferredAggregate`` values, nvflare_amd/deferred.py)
+        and ``devices`` (parameter buckets over several HIP devices, nvflare_amd/sharding.py).
         """
         super().__init__()
         self.expected_data_kind = expected_data_kind
         self.aggregation_weights = aggregation_weights or {}
         self.aggregation_helper = WeightedAggregationHelper(
             exclude_vars=exclude_vars, weigh_by_local_iter=weigh_by_local_iter, device=device,
-            defer_result=defer_result,
+            defer_result=defer_result, devices=devices,
         )
         self.warning_count = {}
         self.warning_limit = 10

@@ -58,18 +58,22 @@ class InTimeAccumulateWeightedAggregator(Aggregator):
         weigh_by_local_iter: bool = True,
         device: Optional[int] = None,
         defer_result: bool = False,
+        devices: Optional[list] = None,
     ):
         """Accumulated weighted (FedAvg) aggregation on the MI355X.
 
         Args: as the reference (intime_accumulate_model_aggregator.py:48-90), plus ``device``, the HIP
-        device index of the aggregation engine (default $NVFLARE_AMD_DEVICE or 0), and ``defer_result``:
+        device index of the aggregation engine (default $NVFLARE_AMD_DEVICE or 0), ``defer_result``:
         the aggregated fp32 values stay in HBM as ``DeferredAggregate`` objects until read, so the device
-        FedOpt generator steps the model in the same launch as the aggregation (nvflare_amd/deferred.py).
+        FedOpt generator steps the model in the same launch as the aggregation (nvflare_amd/deferred.py),
+        and ``devices``: several HIP devices, every key split into per-device parameter buckets
+        (nvflare_amd/sharding.py; results are eager, ``defer_result`` applies to one device only).
         """
         super().__init__()
         self._single_dxo_key = ""
         self._weigh_by_local_iter = weigh_by_local_iter
         self._device = device
+        self._devices = devices
         self._defer_result = defer_result
         self.aggregation_weights = aggregation_weights
         self.exclude_vars = exclude_vars
@@ -141,6 +145,7 @@ class InTimeAccumulateWeightedAggregator(Aggregator):
                 weigh_by_local_iter=self._weigh_by_local_iter,
                 device=self._device,
                 defer_result=self._defer_result,
+                devices=self._devices,
             )
             for k in self.expected_data_kind
         }

@@ -231,6 +231,32 @@ def test_aggregate_random(shape, n_clients, oracle):
     assert same_bits(res.reshape(-1), oracle.fedavg_c([r.reshape(-1) for r in rows], ws, oracle.MODE_NUMPY))
 
 
+@pytest.mark.parametrize("defer", [False, True])
+def test_intime_devices_shards_parameter_buckets(oracle, defer):
+    """``devices=[...]`` on the InTime aggregator: every key split into parameter buckets over several engines
+    (here three on device 0), fp32 results bit-exact with the oracle; ``defer_result`` falls back to eager
+    results when sharded."""
+    from nvflare_amd.compat import DXO, AppConstants, DataKind, FLContext, MetaKey, from_shareable
+    from nvflare_amd.sharding import ShardedFedAvg
+
+    rng = np.random.default_rng(17)
+    agg = _intime(devices=[0, 0, 0], defer_result=defer)
+    fl_ctx = FLContext()
+    fl_ctx.set_prop(AppConstants.CURRENT_ROUND, 0)
+    rows, ws = [], []
+    for i in range(5):
+        w = rng.standard_normal(3 * 4096 + 77).astype(np.float32)
+        rows.append(w)
+        ws.append(float(1 + 3 * i))
+        dxo = DXO(DataKind.WEIGHT_DIFF, data={"w": w, "b": w[:10].copy()}, meta={MetaKey.NUM_STEPS_CURRENT_ROUND: 1 + 3 * i})
+        assert _submit(agg, fl_ctx, f"site-{i}", dxo)
+    assert isinstance(agg.dxo_aggregators[""].aggregation_helper.engine, ShardedFedAvg)
+    out = from_shareable(agg.aggregate(fl_ctx)).data
+    assert isinstance(out["w"], np.ndarray)
+    assert same_bits(out["w"], oracle.fedavg_c(rows, ws, oracle.MODE_NUMPY))
+    assert same_bits(out["b"], oracle.fedavg_c([r[:10].copy() for r in rows], ws, oracle.MODE_NUMPY))
+
+
 @pytest.mark.parametrize("num_dxo", [1, 2, 3])
 @pytest.mark.parametrize("n_clients", [10, 50])
 def test_aggregate_random_dxos(num_dxo, n_clients):
