@@ -1,0 +1,89 @@
+"""FedOpt controller server step on the GPU (nvflare_amd/app_opt/pt/fedopt_ctl.py) against the reference's
+arithmetic (fedopt_ctl.py:113-176): torch's CPU optimizer stepping ``param.grad = -1.0 * diff`` for the
+parameters in the aggregate, the lr scheduler after it, ``state_dict()`` to numpy, FedAvg ``base + diff`` for
+the aggregate's other keys (BatchNorm statistics, an int64 counter).  Three rounds, one parameter missing
+from round 2 (not stepped).  SGD bit-exact; Adam parameters within ``adam_param_tolerance``."""
+
+import copy
+
+import numpy as np
+import pytest
+import torch
+
+from golden_util import adam_param_tolerance, fedopt_model, same_bits
+from nvflare_amd.app_opt.pt.fedopt_ctl import DeviceFedOptUpdate
+from nvflare_amd.compat import FLModel
+
+pytestmark = pytest.mark.gpu
+
+
+def _reference_update(model, opt, sched, global_params, diff):
+    opt.zero_grad()
+    updated = []
+    for name, p in model.named_parameters():
+        if name in diff:
+            p.grad = torch.tensor(-1.0 * diff[name])
+            updated.append(name)
+    opt.step()
+    if sched is not None:
+        sched.step()
+    weights = {k: v.detach().cpu().numpy() for k, v in model.state_dict().items()}
+    for k, v in diff.items():
+        if k not in updated:
+            weights[k] = global_params[k] + v
+    return weights
+
+
+@pytest.mark.parametrize("opt_cls,kw,sched", [
+    (torch.optim.SGD, dict(lr=1.0, momentum=0.6), ("CosineAnnealingLR", dict(T_max=3, eta_min=0.9))),
+    (torch.optim.SGD, dict(lr=0.5, momentum=0.9, nesterov=True, weight_decay=1e-3), None),
+    (torch.optim.Adam, dict(lr=1e-2), ("StepLR", dict(step_size=1, gamma=0.5))),
+    (torch.optim.AdamW, dict(lr=1e-2, weight_decay=0.1, amsgrad=True), None),
+])
+def test_fedopt_controller_update_model(opt_cls, kw, sched):
+    rng = np.random.default_rng(5)
+    model = fedopt_model()
+    ref_model = copy.deepcopy(model)
+    ref_opt = opt_cls(ref_model.parameters(), foreach=False, **kw)
+    ref_sched = getattr(torch.optim.lr_scheduler, sched[0])(ref_opt, **sched[1]) if sched else None
+
+    ctl = object.__new__(DeviceFedOptUpdate)  # the attributes the reference controller sets in run()
+    ctl.device = torch.device("cuda:0")
+    ctl.torch_model = model.to(ctl.device)
+    ctl.optimizer = opt_cls(model.parameters(), **kw)
+    ctl.lr_scheduler = getattr(torch.optim.lr_scheduler, sched[0])(ctl.optimizer, **sched[1]) if sched else None
+    ctl.current_round = 0
+    ctl.info = lambda msg: None
+
+    params0 = {k: v.detach().cpu().numpy().copy() for k, v in ref_model.state_dict().items()}
+    g_dev = FLModel(params={k: v.copy() for k, v in params0.items()})
+    g_ref = {k: v.copy() for k, v in params0.items()}
+    is_adam = opt_cls is not torch.optim.SGD
+    names = {n for n, _ in ref_model.named_parameters()}
+    steps = {n: 0 for n in names}
+    for rnd in range(3):
+        diff = {}
+        for k, v in params0.items():
+            if rnd == 1 and k == "lin2.weight":
+                continue
+            if v.dtype == np.int64:
+                diff[k] = np.array(rnd + 1, dtype=np.int64).reshape(v.shape)
+            else:
+                diff[k] = (rng.standard_normal(v.shape) * 0.05).astype(np.float32)
+        for n in names:
+            steps[n] += n in diff
+        ctl.current_round = rnd
+        out = ctl.update_model(g_dev, FLModel(params=diff, meta={"nr_aggregated": 3}, metrics={"loss": 0.5}))
+        exp = _reference_update(ref_model, ref_opt, ref_sched, g_ref, diff)
+        assert out.meta == {"nr_aggregated": 3} and out.metrics == {"loss": 0.5}
+        assert set(out.params) == set(exp)
+        for k, ref in exp.items():
+            got = np.asarray(out.params[k])
+            assert got.dtype == ref.dtype and got.shape == ref.shape, k
+            if is_adam and k in names:
+                tol = adam_param_tolerance(params0[k], ref, kw["lr"], max(steps[k], 1))
+                assert np.all(np.abs(got.astype(np.float64) - ref.astype(np.float64)) <= tol), (rnd, k)
+            else:
+                assert same_bits(got, ref), (rnd, k)
+        assert ctl.optimizer.param_groups[-1]["lr"] == ref_opt.param_groups[-1]["lr"]
+        g_dev, g_ref = out, exp
