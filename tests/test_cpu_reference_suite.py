@@ -65,3 +65,33 @@ def test_reference_fedavg_workflow_tests_same_outcome(tmp_path):
     assert any("workflows.fedavg.WeightedAggregationHelper" in s for s in rep["swapped"]), rep
     assert ours == ref
     assert sum(v == "passed" for v in ours.values()) >= 100
+
+
+FEDOPT_CTL = os.path.join(REF, "nvflare/app_opt/pt/fedopt_ctl.py")
+
+_COMPOSE = r"""
+import os, sys
+sys.dont_write_bytecode = True
+from ref_suite_plugin import _install_shim
+_install_shim(os.environ["NVFLARE_REF_ROOT"])
+import nvflare_amd.compat as compat
+assert compat.HAVE_NVFLARE
+from nvflare.app_opt.pt.fedopt_ctl import FedOpt as Ref
+from nvflare_amd.app_opt.pt.fedopt_ctl import DeviceFedOptUpdate, FedOpt
+assert issubclass(FedOpt, Ref) and issubclass(FedOpt, DeviceFedOptUpdate)
+assert FedOpt.update_model is DeviceFedOptUpdate.update_model
+assert FedOpt.optimizer_update is DeviceFedOptUpdate.optimizer_update
+assert FedOpt.run is Ref.run
+print("composed")
+"""
+
+
+@pytest.mark.skipif(not os.path.exists(FEDOPT_CTL), reason="reference tree not mounted")
+def test_fedopt_controller_composes_with_reference_controller():
+    """With the real nvflare importable, the drop-in FedOpt controller IS the reference controller (its run(),
+    FedAvg rounds, constructor) with the device server step in place of optimizer_update / update_model."""
+    env = dict(os.environ, NVFLARE_REF_ROOT=REF, PYTHONDONTWRITEBYTECODE="1",
+               PYTHONPATH=os.pathsep.join([HERE, os.path.dirname(HERE)]))
+    env.pop("NVFLARE_AMD_FORCE_STANDINS", None)
+    proc = subprocess.run([sys.executable, "-c", _COMPOSE], env=env, capture_output=True, text=True, timeout=300)
+    assert proc.returncode == 0 and "composed" in proc.stdout, (proc.stdout + proc.stderr)[-3000:]
