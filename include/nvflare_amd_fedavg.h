@@ -71,6 +71,7 @@ enum fedavg_epi {
     FEDAVG_EPI_ADD_BASE = 1, /* w = base + d        full_model_shareable_generator.py:58-67 */
     FEDAVG_EPI_SGD = 2,      /* torch SGD on g = -d   app_opt/pt/fedopt.py:157-182 */
     FEDAVG_EPI_ADAM = 3,     /* torch Adam/AdamW on g = -d  (torch/optim/adam.py:347-551) */
+    FEDAVG_EPI_ADAGRAD = 4,  /* torch Adagrad on g = -d  (torch/optim/adagrad.py _single_tensor_adagrad) */
 };
 
 typedef struct fedavg_epilogue {
@@ -88,6 +89,7 @@ typedef struct fedavg_epilogue {
     const float* base;          /* ADD_BASE: flat fp32 base weights (out may alias it) */
     int amsgrad;                /* Adam: normalise by max_exp_avg_sq = max(max_exp_avg_sq, exp_avg_sq) */
     float* state3;              /* Adam amsgrad: max_exp_avg_sq (in place) */
+    double lr_decay;            /* Adagrad: clr = lr / (1 + (step - 1) * lr_decay); state1 = sum, eps */
 } fedavg_epilogue;
 
 /* Quantized payload formats (nvflare/app_opt/pt/quantization/dequantizer.py:47-185, row f4). */

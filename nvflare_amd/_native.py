@@ -153,6 +153,7 @@ FEDAVG_EPI_NONE = 0
 FEDAVG_EPI_ADD_BASE = 1
 FEDAVG_EPI_SGD = 2
 FEDAVG_EPI_ADAM = 3
+FEDAVG_EPI_ADAGRAD = 4
 
 
 class Epilogue(ctypes.Structure):
@@ -178,6 +179,7 @@ class Epilogue(ctypes.Structure):
         ("base", c_void_p),
         ("amsgrad", c_int),
         ("state3", c_void_p),
+        ("lr_decay", c_double),
     ]
 
 

@@ -8,12 +8,12 @@ representation (torch tensors if the global model holds tensors, numpy otherwise
 
 What differs is where the step runs.  The reference sets ``param.grad`` and calls
 ``optimizer.step()``; here the model's parameters are re-pointed into ONE flat fp32 buffer in HBM and
-``torch.optim.SGD`` / ``Adam`` / ``AdamW`` steps are executed by the HIP fused-epilogue kernel
+``torch.optim.SGD`` / ``Adam`` / ``AdamW`` / ``Adagrad`` steps are executed by the HIP fused-epilogue kernel
 (``fedavg_accumulate_tiled_epi`` with the aggregated difference as ``acc_in``), with torch's
 single-tensor rounding sequence (``tests/test_fedopt_oracle.py``).  The torch optimizer object is kept
 for its ``param_groups`` (read every step, so lr schedulers work unchanged) and its ``state`` is filled
 with views of the device buffers (``momentum_buffer`` / ``exp_avg`` / ``exp_avg_sq`` / ``max_exp_avg_sq``
-with amsgrad / ``step``), so ``optimizer.state_dict()`` checkpoints as before.  Other optimizers raise:
+with amsgrad / Adagrad's ``sum`` / ``step``), so ``optimizer.state_dict()`` checkpoints as before.  Other optimizers raise:
 there is no CPU fallback.
 
 ``device`` names the HIP device ("cuda:N" or N); "cpu" (and None) select $NVFLARE_AMD_DEVICE / 0 --
@@ -87,7 +87,7 @@ class DeviceServerOptimizer:
     """Flat HBM image of a model's parameters plus optimizer state, stepped by the HIP epilogue kernel.
 
     Layout: parameter ``j`` occupies ``[offset_j, offset_j + n_j)`` of the flat buffers ``p`` (the live
-    parameter storage: ``param.data`` is a view of it), ``m`` (momentum buffer / exp_avg), ``v``
+    parameter storage: ``param.data`` is a view of it), ``m`` (momentum buffer / exp_avg / Adagrad sum), ``v``
     (exp_avg_sq) and ``g`` (staged aggregated difference, allocated on first use: a round whose
     differences are deferred aggregates never needs it), offsets 256-byte aligned."""
 
@@ -106,9 +106,11 @@ class DeviceServerOptimizer:
             return N.FEDAVG_EPI_SGD
         if isinstance(optimizer, torch.optim.Adam):  # AdamW subclasses Adam (decoupled_weight_decay=True)
             return N.FEDAVG_EPI_ADAM
+        if isinstance(optimizer, torch.optim.Adagrad):
+            return N.FEDAVG_EPI_ADAGRAD
         raise NotImplementedError(
             f"nvflare_amd: server optimizer {type(optimizer).__module__}.{type(optimizer).__name__} has no device "
-            "kernel (supported: torch.optim.SGD, Adam, AdamW)")
+            "kernel (supported: torch.optim.SGD, Adam, AdamW, Adagrad)")
 
     def _group_of(self) -> Dict[int, dict]:
         return {id(p): g for g in self.optimizer.param_groups for p in g["params"]}
@@ -147,6 +149,9 @@ class DeviceServerOptimizer:
                     self.m[s.offset:s.offset + s.n].copy_(st["exp_avg"].reshape(-1).to(dev))
                     self.v[s.offset:s.offset + s.n].copy_(st["exp_avg_sq"].reshape(-1).to(dev))
                     s.step = float(st["step"])
+                if "sum" in st:  # Adagrad: state made at construction (initial_accumulator_value)
+                    self.m[s.offset:s.offset + s.n].copy_(st["sum"].reshape(-1).to(dev))
+                    s.step = float(st["step"])
                 if st.get("max_exp_avg_sq") is not None and self.vmax is not None:
                     self.vmax[s.offset:s.offset + s.n].copy_(st["max_exp_avg_sq"].reshape(-1).to(dev))
                 if id(s.param) not in groups:
@@ -168,6 +173,9 @@ class DeviceServerOptimizer:
         if self.kind == N.FEDAVG_EPI_SGD:
             if s.has_momentum_buffer:  # torch stores the buffer only when momentum != 0
                 st["momentum_buffer"] = self.m[s.offset:s.offset + s.n].view(s.param.shape)
+        elif self.kind == N.FEDAVG_EPI_ADAGRAD:
+            st["step"] = torch.tensor(s.step, dtype=torch.float32)
+            st["sum"] = self.m[s.offset:s.offset + s.n].view(s.param.shape)
         else:
             st["step"] = torch.tensor(s.step, dtype=torch.float32)
             st["exp_avg"] = self.m[s.offset:s.offset + s.n].view(s.param.shape)
@@ -193,6 +201,10 @@ class DeviceServerOptimizer:
             e.dampening = float(group.get("dampening", 0.0))
             e.nesterov = int(bool(group.get("nesterov", False)))
             e.first_step = int(not s.has_momentum_buffer)
+        elif self.kind == N.FEDAVG_EPI_ADAGRAD:
+            e.lr_decay = float(group.get("lr_decay", 0.0))
+            e.eps = float(group["eps"])
+            e.step = s.step + 1.0
         else:
             b1, b2 = group["betas"]
             e.beta1, e.beta2, e.eps = float(b1), float(b2), float(group["eps"])

@@ -399,6 +399,8 @@ fedavg::EpiParams make_epi(const fedavg_epilogue& e) {
     const double bc1 = 1.0 - std::pow(e.beta1, e.step);
     const double bc2 = 1.0 - std::pow(e.beta2, e.step);
     E.step_size_neg = (float)(-(e.lr / bc1));
+    if (e.kind == FEDAVG_EPI_ADAGRAD)  // adagrad.py: clr = lr / (1 + (step - 1) * lr_decay), value = -clr
+        E.step_size_neg = (float)(-(e.lr / (1.0 + (e.step - 1.0) * e.lr_decay)));
     E.bias_correction2_sqrt = (float)std::pow(bc2, 0.5);
     E.eps = (float)e.eps;
     E.param = e.param;
@@ -984,7 +986,7 @@ int fedavg_accumulate_tiled_epi(fedavg_ctx* ctx, const void* const* bases, const
                 throw Error(g_last_error);
             return;
         }
-        if (epi->kind < FEDAVG_EPI_ADD_BASE || epi->kind > FEDAVG_EPI_ADAM) throw Error("bad epilogue kind");
+        if (epi->kind < FEDAVG_EPI_ADD_BASE || epi->kind > FEDAVG_EPI_ADAGRAD) throw Error("bad epilogue kind");
         if (k_rows < 0 || (k_rows == 0 && !acc_in)) throw Error("k_rows == 0 requires acc_in");
         check_op_fin(op, fin);
         if (tile_elems != (size_t)fedavg::kDefaultTile)
@@ -1001,6 +1003,9 @@ int fedavg_accumulate_tiled_epi(fedavg_ctx* ctx, const void* const* bases, const
         if (epi->kind == FEDAVG_EPI_ADAM && epi->amsgrad && !epi->state3)
             throw Error("ADAM with amsgrad needs state3 (max_exp_avg_sq)");
         if (epi->kind == FEDAVG_EPI_ADAM && epi->step < 1.0) throw Error("ADAM step must be >= 1");
+        if (epi->kind == FEDAVG_EPI_ADAGRAD && (!epi->param || !epi->state1))
+            throw Error("ADAGRAD needs param and state1 (sum)");
+        if (epi->kind == FEDAVG_EPI_ADAGRAD && epi->step < 1.0) throw Error("ADAGRAD step must be >= 1");
         for (const void* p : {(const void*)epi->param, (const void*)epi->state1, (const void*)epi->state2,
                               (const void*)epi->state3, (const void*)epi->base, (const void*)out, acc_in})
             if (misaligned(p)) throw Error("epilogue/out/acc_in pointers must be 16-byte aligned");

@@ -192,6 +192,9 @@ __device__ __forceinline__ EpiIn epi_load(const EpiParams& E, const int64_t i) {
     } else if constexpr (EPI == FEDAVG_EPI_SGD) {
         in.a = load4<true>(reinterpret_cast<const f32x4*>(E.param) + i);
         if (E.has_momentum && !E.first_step) in.b = load4<true>(reinterpret_cast<const f32x4*>(E.state1) + i);
+    } else if constexpr (EPI == FEDAVG_EPI_ADAGRAD) {
+        in.a = load4<true>(reinterpret_cast<const f32x4*>(E.param) + i);
+        in.b = load4<true>(reinterpret_cast<const f32x4*>(E.state1) + i);
     } else {
         in.a = load4<true>(reinterpret_cast<const f32x4*>(E.param) + i);
         in.b = load4<true>(reinterpret_cast<const f32x4*>(E.state1) + i);
@@ -223,6 +226,19 @@ __device__ __forceinline__ void epilogue4(const EpiParams& E, const int64_t i, c
         }
         store4<true>(p4, p);
         if (E.has_momentum) store4<true>(reinterpret_cast<f32x4*>(E.state1) + i, buf);
+    } else if constexpr (EPI == FEDAVG_EPI_ADAGRAD) {
+        f32x4 p = in.a;
+        f32x4 sum = in.b;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            float g = E.maximize ? d[c] : -d[c];
+            if (E.has_weight_decay) g = __builtin_fmaf(p[c], E.weight_decay, g);  // grad.add(param, alpha=wd)
+            sum[c] = __builtin_fmaf(g, g, sum[c]);                                 // state_sum.addcmul_(g, g, value=1)
+            const float std_ = __builtin_sqrtf(sum[c]) + E.eps;                    // state_sum.sqrt().add_(eps)
+            p[c] = p[c] + (E.step_size_neg * g) / std_;                            // param.addcdiv_(g, std, value=-clr)
+        }
+        store4<true>(p4, p);
+        store4<true>(reinterpret_cast<f32x4*>(E.state1) + i, sum);
     } else {  // EPI_ADAM
         f32x4 p = in.a;
         f32x4 m = in.b;
@@ -509,6 +525,10 @@ static hipError_t launch_epi_p(const TileLaunch& L, const EpiParams& E, hipStrea
         case FEDAVG_EPI_ADAM:
             hipLaunchKernelGGL((fedavg_tiles_epi_f32x4<OP, FIN, ACC_IN, FEDAVG_EPI_ADAM, PRE>), dim3(L.grid), dim3(kBlock),
                                0, s, L.tab, L.k, L.tstride4, ai, o, L.b4, L.e4, L.fin_val, E);
+            break;
+        case FEDAVG_EPI_ADAGRAD:
+            hipLaunchKernelGGL((fedavg_tiles_epi_f32x4<OP, FIN, ACC_IN, FEDAVG_EPI_ADAGRAD, PRE>), dim3(L.grid),
+                               dim3(kBlock), 0, s, L.tab, L.k, L.tstride4, ai, o, L.b4, L.e4, L.fin_val, E);
             break;
         default:
             return hipErrorInvalidValue;

@@ -115,6 +115,7 @@ void oracle_synth_fill_f32(uint64_t seed, uint64_t row, const uint64_t* cols, si
  * d = fin(acc) of each element (computed exactly as above):
  *   ADD_BASE  w = base + d            full_model_shareable_generator.py:58-67 (WEIGHT_DIFF apply)
  *   SGD       torch/optim/sgd.py _single_tensor_sgd on grad g = -1.0 * d   (app_opt/pt/fedopt.py:175)
+ *   ADAGRAD   torch/optim/adagrad.py _single_tensor_adagrad on g = -1.0 * d (m holds state_sum)
  *   ADAM      torch/optim/adam.py _single_tensor_adam (:347-551) on g = -1.0 * d; amsgrad divides by
  *             sqrt(vmax), vmax = torch.maximum(vmax, v) kept as a third state
  * Rounding sequence pinned against torch 2.10 CPU (tests/test_fedopt_oracle.py):
@@ -125,7 +126,7 @@ void oracle_synth_fill_f32(uint64_t seed, uint64_t row, const uint64_t* cols, si
  * Scalars follow torch: python-float hyperparameters and bias corrections computed in fp64, cast to
  * fp32 where they meet a tensor.
  * ------------------------------------------------------------------------------------------------ */
-enum { ORACLE_EPI_NONE = 0, ORACLE_EPI_ADD_BASE = 1, ORACLE_EPI_SGD = 2, ORACLE_EPI_ADAM = 3 };
+enum { ORACLE_EPI_NONE = 0, ORACLE_EPI_ADD_BASE = 1, ORACLE_EPI_SGD = 2, ORACLE_EPI_ADAM = 3, ORACLE_EPI_ADAGRAD = 4 };
 
 typedef struct {
     int kind;
@@ -136,6 +137,7 @@ typedef struct {
     double lr, momentum, dampening, weight_decay; /* SGD (+ lr, weight_decay for Adam) */
     double beta1, beta2, eps, step;               /* Adam: step after increment (1, 2, ...) */
     int amsgrad;                                  /* Adam: normalise by the running max of v (vmax) */
+    double lr_decay;                              /* Adagrad: clr = lr / (1 + (step - 1) * lr_decay) */
 } oracle_epilogue;
 
 /* torch.maximum: a NaN operand is the result */
@@ -169,6 +171,13 @@ void oracle_epilogue_apply(const float* delta, size_t n, const oracle_epilogue* 
                 g = epi->nesterov ? fmaf(b, (float)epi->momentum, g) : b;
             }
             p[i] = fmaf(g, (float)(-epi->lr), p[i]);
+        } else if (epi->kind == ORACLE_EPI_ADAGRAD) { /* torch/optim/adagrad.py _single_tensor_adagrad, m = sum */
+            float g = epi->maximize ? d : -d;
+            if (epi->weight_decay != 0.0) g = fmaf(p[i], (float)epi->weight_decay, g);
+            const float neg_clr = (float)(-(epi->lr / (1.0 + (epi->step - 1.0) * epi->lr_decay)));
+            m[i] = fmaf(g, g, m[i]);                                  /* state_sum.addcmul_(g, g, value=1) */
+            const float std_ = sqrtf(m[i]) + (float)epi->eps;         /* state_sum.sqrt().add_(eps) */
+            p[i] = p[i] + (neg_clr * g) / std_;                       /* param.addcdiv_(g, std, value=-clr) */
         } else { /* ADAM */
             float g = epi->maximize ? d : -d;
             float pv = p[i];

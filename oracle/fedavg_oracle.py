@@ -244,7 +244,7 @@ def synth_weights(K: int):
 # ---------------------------------------------------------------------------------------------------
 # server-optimizer epilogues (rows a9/a10): see oracle_epilogue_apply in fedavg_oracle.c
 # ---------------------------------------------------------------------------------------------------
-EPI_NONE, EPI_ADD_BASE, EPI_SGD, EPI_ADAM = 0, 1, 2, 3
+EPI_NONE, EPI_ADD_BASE, EPI_SGD, EPI_ADAM, EPI_ADAGRAD = 0, 1, 2, 3, 4
 
 
 class _Epi(ctypes.Structure):
@@ -263,6 +263,7 @@ class _Epi(ctypes.Structure):
         ("eps", ctypes.c_double),
         ("step", ctypes.c_double),
         ("amsgrad", ctypes.c_int),
+        ("lr_decay", ctypes.c_double),
     ]
 
 

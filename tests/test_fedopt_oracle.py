@@ -105,6 +105,36 @@ def test_adam_vs_torch(oracle, cls, kw):
     assert float((diff > 0).mean()) < 0.01
 
 
+@pytest.mark.parametrize("kw", [
+    dict(lr=1e-2),
+    dict(lr=0.1, lr_decay=0.05, weight_decay=1e-3, eps=1e-8),
+    dict(lr=1e-2, initial_accumulator_value=0.1, maximize=True),
+])
+def test_adagrad_vs_torch(oracle, kw):
+    """torch/optim/adagrad.py _single_tensor_adagrad (FedAdagrad): state_sum bit-exact; params within the
+    sqrt bound (torch CPU's vectorised sqrt), as for Adam."""
+    rng = np.random.default_rng(3)
+    n = 200_003
+    p0 = rng.standard_normal(n).astype(np.float32)
+    deltas = [(rng.standard_normal(n) * 0.01).astype(np.float32) for _ in range(5)]
+    tp, st = _torch_steps(torch.optim.Adagrad, kw, p0, deltas)
+    p = p0.copy()
+    s = np.full(n, kw.get("initial_accumulator_value", 0.0), np.float32)
+    for k, d in enumerate(deltas):
+        oracle.epilogue_apply(d, oracle.EPI_ADAGRAD, p=p, m=s, lr=kw["lr"], lr_decay=kw.get("lr_decay", 0.0),
+                              weight_decay=kw.get("weight_decay", 0.0), eps=kw.get("eps", 1e-10),
+                              maximize=int(kw.get("maximize", False)), step=float(k + 1))
+    if kw.get("weight_decay"):  # p feeds back into g: sum inherits p's sqrt-rounding differences at wd scale
+        scale = np.maximum(np.abs(st["sum"].numpy()), np.float32(kw["weight_decay"]) * np.abs(p0))
+        assert np.all(np.abs(s.astype(np.float64) - st["sum"].numpy()) <= len(deltas) * np.spacing(scale))
+    else:
+        assert same_bits(s, st["sum"].numpy()), "sum"
+    tol = len(deltas) * np.spacing(np.maximum(np.maximum(np.abs(p0), np.abs(tp)), np.float32(kw["lr"]))).astype(np.float64)
+    diff = np.abs(p.astype(np.float64) - tp.astype(np.float64))
+    assert np.all(diff <= tol), float((diff / tol).max())
+    assert float((diff > 0).mean()) < 0.01
+
+
 def test_add_base_matches_numpy_generator(oracle):
     """full_model_shareable_generator.py:58-67: weights[k] = weights[k] + diff[k] (numpy fp32 add)."""
     rng = np.random.default_rng(2)

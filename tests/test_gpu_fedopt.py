@@ -292,3 +292,31 @@ def test_adam_amsgrad_epilogue(ctx, oracle, K, decoupled):
     finally:
         if dev is not None:
             dev.close()
+
+
+@pytest.mark.parametrize("K,hp", [(5, dict(lr=0.1, lr_decay=0.05, eps=1e-10)),
+                                  (2, dict(lr=1e-2, weight_decay=1e-3, eps=1e-8, maximize=1)),
+                                  (0, dict(lr=0.5, eps=1e-10))])
+def test_adagrad_epilogue(ctx, oracle, K, hp):
+    """Adagrad (FedAdagrad): state_sum = fma(g, g, sum), p += (-clr * g) / (sqrt(sum) + eps) with
+    clr = lr / (1 + (step - 1) * lr_decay); three steps from a non-zero initial sum, bit-exact vs the oracle
+    (itself pinned to torch CPU by tests/test_fedopt_oracle.py)."""
+    rng = np.random.default_rng(70 + K)
+    n = 3 * TILE + 20
+    p = rng.standard_normal(n).astype(np.float32)
+    s = np.full(n, 0.1, np.float32)
+    for step in range(3):
+        rows = [(rng.standard_normal(n) * 0.05).astype(np.float32) for _ in range(K)]
+        ws = [float(1 + (37 * k) % 100) for k in range(K)]
+        delta = (rng.standard_normal(n) * 0.05).astype(np.float32) if K == 0 else None
+        dev = _Dev(ctx, rows, n)
+        try:
+            e = _epi(4, param=dev.buf("p", p), state1=dev.buf("s", s), step=float(step + 1), **hp)
+            acc_ptr = dev.buf("acc", delta) if K == 0 else None
+            ctx.accumulate_tiled_epi(dev.bases, ws, TILE, dev.lay.tile_stride, 0, dev.n4, None, 1,
+                                     2 if K else 0, _sum(ws) if K else 1.0, e, acc_in_ptr=acc_ptr)
+            d = oracle.fedavg_c(rows, ws, oracle.MODE_TORCH, nthreads=8) if K else delta
+            oracle.epilogue_apply(d, oracle.EPI_ADAGRAD, p=p, m=s, step=float(step + 1), **hp)
+            assert same_bits(dev.get("p"), p) and same_bits(dev.get("s"), s), step
+        finally:
+            dev.close()
