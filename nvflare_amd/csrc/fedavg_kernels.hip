@@ -401,6 +401,44 @@ __global__ void __launch_bounds__(kBlock) fedavg_rows_generic(const RowTableGene
 }
 
 // ---------------------------------------------------------------------------------------------
+// fp64 rows (numpy's default dtype), every pointer 16-byte aligned: each lane owns two consecutive values
+// (one 16-byte load per client), four clients' loads in flight before their arrival-ordered arithmetic,
+// nontemporal loads and stores.  n2 = pairs; an odd last element goes to the scalar kernel.
+// ---------------------------------------------------------------------------------------------
+typedef double f64x2 __attribute__((ext_vector_type(2)));
+
+template <int OP, int FIN, bool ACC_IN>
+__global__ void __launch_bounds__(kBlock) fedavg_rows_f64x2(const RowTableGeneric tab, const int K,
+                                                             const f64x2* acc_in, f64x2* out, const int64_t n2,
+                                                             const double fin_val) {
+    const int64_t stride = (int64_t)gridDim.x * kBlock;
+    for (int64_t g = (int64_t)blockIdx.x * kBlock + threadIdx.x; g < n2; g += stride) {
+        f64x2 acc;
+        int k = 0;
+        if constexpr (ACC_IN) {
+            acc = __builtin_nontemporal_load(acc_in + g);
+        } else {
+            const f64x2 v = __builtin_nontemporal_load(static_cast<const f64x2*>(tab.rows[0]) + g);
+            acc = f64x2{first_op<OP>(v[0], tab.w[0]), first_op<OP>(v[1], tab.w[0])};
+            k = 1;
+        }
+        for (; k + 4 <= K; k += 4) {
+            f64x2 v[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) v[u] = __builtin_nontemporal_load(static_cast<const f64x2*>(tab.rows[k + u]) + g);
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                acc = f64x2{step_op<OP>(acc[0], v[u][0], tab.w[k + u]), step_op<OP>(acc[1], v[u][1], tab.w[k + u])};
+        }
+        for (; k < K; ++k) {
+            const f64x2 v = __builtin_nontemporal_load(static_cast<const f64x2*>(tab.rows[k]) + g);
+            acc = f64x2{step_op<OP>(acc[0], v[0], tab.w[k]), step_op<OP>(acc[1], v[1], tab.w[k])};
+        }
+        __builtin_nontemporal_store(f64x2{fin_op<FIN>(acc[0], fin_val), fin_op<FIN>(acc[1], fin_val)}, out + g);
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
 // synthetic inputs (bit-identical host twin: oracle/fedavg_oracle.c oracle_synth_value), written to a
 // tiled row: logical element i goes to dst[(i / tile) * tile_stride + i % tile]
 // ---------------------------------------------------------------------------------------------
@@ -609,9 +647,66 @@ static hipError_t launch_generic_t(const RowTableGeneric& tab, int K, const void
     }
 }
 
+template <int OP, int FIN>
+static hipError_t launch_f64x2_f(const RowTableGeneric& tab, int K, const void* acc_in, void* out, int64_t n2,
+                                 double fin_val, int grid, hipStream_t s) {
+    if (acc_in) {
+        hipLaunchKernelGGL((fedavg_rows_f64x2<OP, FIN, true>), dim3(grid), dim3(kBlock), 0, s, tab, K,
+                           static_cast<const f64x2*>(acc_in), static_cast<f64x2*>(out), n2, fin_val);
+    } else {
+        hipLaunchKernelGGL((fedavg_rows_f64x2<OP, FIN, false>), dim3(grid), dim3(kBlock), 0, s, tab, K,
+                           static_cast<const f64x2*>(acc_in), static_cast<f64x2*>(out), n2, fin_val);
+    }
+    return hipGetLastError();
+}
+
+template <int OP>
+static hipError_t launch_f64x2_o(const RowTableGeneric& tab, int K, const void* acc_in, void* out, int64_t n2, int fin,
+                                 double fin_val, int grid, hipStream_t s) {
+    switch (fin) {
+        case FEDAVG_FIN_SCALE:
+            return launch_f64x2_f<OP, FEDAVG_FIN_SCALE>(tab, K, acc_in, out, n2, fin_val, grid, s);
+        case FEDAVG_FIN_DIV:
+            return launch_f64x2_f<OP, FEDAVG_FIN_DIV>(tab, K, acc_in, out, n2, fin_val, grid, s);
+        default:
+            return launch_f64x2_f<OP, FEDAVG_FIN_NONE>(tab, K, acc_in, out, n2, fin_val, grid, s);
+    }
+}
+
+// fp64 -> fp64 rows with every pointer 16-byte aligned: the paired kernel over n / 2 pairs, the odd last
+// element (if any) on the scalar kernel.  Returns hipErrorNotSupported when the rows do not qualify.
+static hipError_t launch_rows_f64x2(const RowTableGeneric& tab, int K, const void* acc_in, void* out, int64_t n, int op,
+                                    int fin, double fin_val, int grid, hipStream_t s) {
+    auto aligned = [](const void* p) { return reinterpret_cast<uintptr_t>(p) % 16 == 0; };
+    bool ok = aligned(out) && aligned(acc_in) && n >= 2;
+    for (int k = 0; ok && k < K; ++k) ok = aligned(tab.rows[k]);
+    if (!ok) return hipErrorNotSupported;
+    const int64_t n2 = n / 2;
+    hipError_t e;
+    switch (op) {
+        case FEDAVG_OP_TORCH:
+            e = launch_f64x2_o<FEDAVG_OP_TORCH>(tab, K, acc_in, out, n2, fin, fin_val, grid, s);
+            break;
+        case FEDAVG_OP_UNWEIGHTED:
+            e = launch_f64x2_o<FEDAVG_OP_UNWEIGHTED>(tab, K, acc_in, out, n2, fin, fin_val, grid, s);
+            break;
+        default:
+            e = launch_f64x2_o<FEDAVG_OP_NUMPY>(tab, K, acc_in, out, n2, fin, fin_val, grid, s);
+    }
+    if (e != hipSuccess || n % 2 == 0) return e;
+    RowTableGeneric tail = tab;
+    for (int k = 0; k < K; ++k) tail.rows[k] = static_cast<const double*>(tab.rows[k]) + 2 * n2;
+    const void* tail_in = acc_in ? static_cast<const void*>(static_cast<const double*>(acc_in) + 2 * n2) : nullptr;
+    return launch_generic_t<double, double>(tail, K, tail_in, static_cast<double*>(out) + 2 * n2, 1, op, fin, fin_val, 1, s);
+}
+
 hipError_t launch_rows_generic(const RowTableGeneric& tab, int K, const void* acc_in, void* out, int64_t n,
                                int in_dtype, int acc_dtype, int op, int fin, double fin_val, int grid,
                                hipStream_t s) {
+    if (in_dtype == FEDAVG_F64 && acc_dtype == FEDAVG_F64) {
+        const hipError_t e = launch_rows_f64x2(tab, K, acc_in, out, n, op, fin, fin_val, grid, s);
+        if (e != hipErrorNotSupported) return e;
+    }
     // integer / bool inputs are promoted to the accumulator type before the first operation, as numpy
     // (-> float64) and torch (-> float32, the default dtype) promote them
     if (acc_dtype == FEDAVG_F32) {

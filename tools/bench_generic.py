@@ -1,0 +1,57 @@
+#!/usr/bin/env python3
+"""Throughput of the contiguous-rows entry point (fedavg_accumulate) for fp64 and fp32 values: K separate
+device-resident client rows of P values -> P values, numpy-mode arithmetic.  fp64 (numpy's default dtype)
+and the integer types run the generic kernel; fp32 rows run the streaming kernel.  Algorithmic bytes per
+launch: (K + 1) * P * itemsize.
+
+  python tools/bench_generic.py [--clients 8 --params 125e6 --dtype float64 --steps 10]
+"""
+
+import argparse
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--clients", type=int, default=8)
+    ap.add_argument("--params", type=float, default=125e6)
+    ap.add_argument("--dtype", choices=["float64", "float32"], default="float64")
+    ap.add_argument("--steps", type=int, default=10)
+    args = ap.parse_args()
+    import torch
+
+    from nvflare_amd import _native as N
+    from nvflare_amd.device import DeviceContext
+
+    K, P = args.clients, int(args.params)
+    ctx = DeviceContext.get(0)
+    tdt = torch.float64 if args.dtype == "float64" else torch.float32
+    code = N.FEDAVG_F64 if args.dtype == "float64" else N.FEDAVG_F32
+    g = torch.Generator(device="cuda:0")
+    g.manual_seed(0)
+    rows = [torch.randn(P, dtype=tdt, device="cuda:0", generator=g) for _ in range(K)]
+    out = torch.empty(P, dtype=tdt, device="cuda:0")
+    torch.cuda.synchronize()
+    ws = [float(1 + (37 * k) % 100) for k in range(K)]
+
+    def launch():
+        ctx.accumulate([r.data_ptr() for r in rows], ws, P, out.data_ptr(), code, code, N.FEDAVG_OP_NUMPY,
+                       N.FEDAVG_FIN_SCALE, sum(ws))
+
+    launch()
+    ctx.sync()
+    ctx.timing_begin()
+    for _ in range(args.steps):
+        launch()
+    ms = ctx.timing_end() / args.steps
+    nbytes = (K + 1) * P * rows[0].element_size()
+    print(json.dumps({"tool": "bench_generic", "dtype": args.dtype, "clients": K, "params": P, "kernel_ms": round(ms, 3),
+                      "alg_GBs": round(nbytes / ms / 1e6, 1), "frac_of_8TBs": round(nbytes / ms / 1e6 / 8000, 4)}))
+
+
+if __name__ == "__main__":
+    main()
