@@ -213,6 +213,14 @@ int fedavg_accumulate_tiled16(fedavg_ctx* ctx, int fmt, const void* const* bases
                               size_t tile_elems, size_t tile_stride, size_t begin, size_t end, const void* acc_in,
                               void* out, int op, int fin, double count);
 
+/* fedavg_accumulate_tiled for fp64 client storage and totals (numpy's default dtype; the engine's fp64 arena):
+ * tile_elems = 4096, begin/end multiples of 2, every pointer 16-byte aligned.  fp64 arithmetic in arrival
+ * order with fp64 weights -- numpy: T = T + v*w then T * (1.0/count); torch (float64 tensors): fma, T / count
+ * (weighted_aggregation_helper.py:181-236). */
+int fedavg_accumulate_tiled64(fedavg_ctx* ctx, const void* const* bases, const double* weights, int k_rows,
+                              size_t tile_elems, size_t tile_stride, size_t begin, size_t end, const void* acc_in,
+                              void* out, int op, int fin, double count);
+
 /* fedavg_accumulate_tiled with a server-optimizer epilogue applied per element to d = fin(acc) in the
  * same launch (rows a9/a10): ADD_BASE writes base + d to out; SGD/ADAM update epi->param/state in place
  * and also store d to out when out != NULL.  More than 128 clients are chained through a partial sum

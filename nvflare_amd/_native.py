@@ -119,6 +119,21 @@ _SIGNATURES = {
         c_int,  # fin
         c_double,  # count
     ],
+    "fedavg_accumulate_tiled64": [
+        c_void_p,  # ctx
+        ctypes.POINTER(c_void_p),  # bases
+        ctypes.POINTER(c_double),  # weights
+        c_int,  # k_rows
+        c_size_t,  # tile_elems
+        c_size_t,  # tile_stride
+        c_size_t,  # begin
+        c_size_t,  # end
+        c_void_p,  # acc_in
+        c_void_p,  # out
+        c_int,  # op
+        c_int,  # fin
+        c_double,  # count
+    ],
     "fedavg_accumulate_tiled_epi": [
         c_void_p,  # ctx
         ctypes.POINTER(c_void_p),  # bases

@@ -975,6 +975,54 @@ int fedavg_accumulate_tiled16(fedavg_ctx* ctx, int fmt, const void* const* bases
     });
 }
 
+int fedavg_accumulate_tiled64(fedavg_ctx* ctx, const void* const* bases, const double* weights, int k_rows,
+                              size_t tile_elems, size_t tile_stride, size_t begin, size_t end, const void* acc_in,
+                              void* out, int op, int fin, double count) {
+    return guarded([&] {
+        if (!ctx) throw Error("ctx is NULL");
+        if (k_rows < 0 || (k_rows == 0 && !acc_in)) throw Error("k_rows == 0 requires acc_in");
+        check_op_fin(op, fin);
+        if (tile_elems != (size_t)fedavg::kTile64Elems) throw Error("tile_elems must be 4096");
+        if (tile_stride < tile_elems || tile_stride % 2) throw Error("tile_stride must be >= tile_elems, multiple of 2");
+        if (begin % 2 || end % 2 || end < begin) throw Error("begin/end must be multiples of 2 with begin <= end");
+        if (end == begin) {
+            ctx->timed_valid = false;
+            return;
+        }
+        if (!out) throw Error("out is NULL");
+        if (reinterpret_cast<uintptr_t>(out) % 16 || reinterpret_cast<uintptr_t>(acc_in) % 16)
+            throw Error("out/acc_in must be 16-byte aligned");
+        if (k_rows > 0 && (!bases || !weights)) throw Error("bases/weights NULL");
+        for (int k = 0; k < k_rows; ++k)
+            if (!bases[k] || reinterpret_cast<uintptr_t>(bases[k]) % 16)
+                throw Error("base " + std::to_string(k) + " is NULL or not 16-byte aligned");
+        ctx->activate();
+        hipStream_t s = ctx->compute();
+        TimingScope ts(ctx, s);
+        const int64_t T = fedavg::kTile64Elems;
+        const int64_t n_tiles = ((int64_t)end - 1) / T - (int64_t)begin / T + 1;
+        const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)ctx->num_cus * ctx->blocks_per_cu, n_tiles));
+        const double fv = fin_scalar(fin, count);
+        int k0 = 0;
+        const void* cur_in = acc_in;
+        do {  // more clients than one kernel-argument table holds chain a partial sum through out
+            const int kc = std::min(k_rows - k0, fedavg::kMaxRowsPerLaunch);
+            fedavg::RowTableGeneric t;
+            memset(&t, 0, sizeof(t));
+            for (int j = 0; j < kc; ++j) {
+                t.rows[j] = bases[k0 + j];
+                t.w[j] = weights[k0 + j];
+            }
+            const bool last = k0 + kc >= k_rows;
+            HIP_CHECK(fedavg::launch_tiles_f64(t, kc, (int64_t)tile_stride, cur_in, out, (int64_t)begin, (int64_t)end,
+                                               op, last ? fin : FEDAVG_FIN_NONE, fv, grid, s));
+            cur_in = out;
+            k0 += kc;
+        } while (k0 < k_rows);
+        ts.done();
+    });
+}
+
 int fedavg_accumulate_tiled_epi(fedavg_ctx* ctx, const void* const* bases, const double* weights, int k_rows,
                                 size_t tile_elems, size_t tile_stride, size_t begin, size_t end, const void* acc_in,
                                 void* out, int op, int fin, double count, const fedavg_epilogue* epi) {

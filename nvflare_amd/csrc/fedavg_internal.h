@@ -99,6 +99,9 @@ hipError_t launch_tiles_narrow(const RowTableNarrow& tab, int K, int64_t tstride
                                int64_t begin, int64_t end, int fmt, int op, int fin, float fin_val, int grid,
                                hipStream_t s);
 constexpr int kTile16Elems = 4096;  // the only tile width of the 16-bit tiled kernel
+constexpr int kTile64Elems = 4096;  // the only tile width of the fp64 tiled kernel
+hipError_t launch_tiles_f64(const RowTableGeneric& tab, int K, int64_t tstride_elems, const void* acc_in, void* out,
+                            int64_t begin, int64_t end, int op, int fin, double fin_val, int grid, hipStream_t s);
 hipError_t launch_fill_synthetic_f32(float* dst, int64_t n, int64_t tile, int64_t tstride, uint64_t seed, uint64_t row,
                                      uint64_t col0, int grid, hipStream_t s);
 hipError_t launch_gather_f32(const float* src, const uint64_t* idx, float* dst, int64_t m, hipStream_t s);

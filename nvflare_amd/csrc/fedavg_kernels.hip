@@ -439,6 +439,78 @@ __global__ void __launch_bounds__(kBlock) fedavg_rows_f64x2(const RowTableGeneri
 }
 
 // ---------------------------------------------------------------------------------------------
+// TILED fp64 (the engine's fp64 arena, numpy's default dtype): element i of client k lives at
+//   bases[k] + (i / 4096) * tile_stride + i % 4096          (fp64 elements)
+// A block owns a tile (4096 values = 32 KiB per client); each lane owns 8 f64x2 columns, so a wave reads
+// 1 KiB contiguous per client and column, two clients' loads (16 x 16 B per lane) in flight before their
+// arrival-ordered arithmetic.  Units below are pairs (f64x2).
+// ---------------------------------------------------------------------------------------------
+constexpr int kCpl64 = kTile64Elems / (2 * kBlock);  // 8
+#ifndef FEDAVG_F64_UNROLL
+#define FEDAVG_F64_UNROLL 2  // clients whose loads are in flight together (16 x 16 B per lane)
+#endif
+
+template <int OP, int FIN, bool ACC_IN>
+__global__ void __launch_bounds__(kBlock) fedavg_tiles_f64x2(const RowTableGeneric tab, const int K,
+                                                              const int64_t tstride2, const f64x2* acc_in, f64x2* out,
+                                                              const int64_t b2, const int64_t e2, const double fin_val) {
+    constexpr int64_t T2 = (int64_t)kCpl64 * kBlock;
+    constexpr int UNROLL = FEDAVG_F64_UNROLL;
+    const int64_t t_last = (e2 - 1) / T2;
+    for (int64_t t = b2 / T2 + blockIdx.x; t <= t_last; t += gridDim.x) {
+        const int64_t off = t * tstride2 + threadIdx.x;
+        const int64_t col = t * T2 + threadIdx.x;
+        f64x2 acc[kCpl64];
+        int k = 0;
+        if constexpr (ACC_IN) {
+#pragma unroll
+            for (int c = 0; c < kCpl64; ++c) {
+                const int64_t i = col + c * kBlock;
+                acc[c] = (i >= b2 && i < e2) ? acc_in[i] : f64x2{0, 0};
+            }
+        } else {
+            const f64x2* r = static_cast<const f64x2*>(tab.rows[0]) + off;
+#pragma unroll
+            for (int c = 0; c < kCpl64; ++c) {
+                const f64x2 v = __builtin_nontemporal_load(r + c * kBlock);
+                acc[c] = f64x2{first_op<OP>(v[0], tab.w[0]), first_op<OP>(v[1], tab.w[0])};
+            }
+            k = 1;
+        }
+        for (; k + UNROLL <= K; k += UNROLL) {
+            f64x2 v[UNROLL][kCpl64];
+#pragma unroll
+            for (int u = 0; u < UNROLL; ++u) {
+                const f64x2* r = static_cast<const f64x2*>(tab.rows[k + u]) + off;
+#pragma unroll
+                for (int c = 0; c < kCpl64; ++c) v[u][c] = __builtin_nontemporal_load(r + c * kBlock);
+            }
+#pragma unroll
+            for (int u = 0; u < UNROLL; ++u)
+#pragma unroll
+                for (int c = 0; c < kCpl64; ++c)
+                    acc[c] = f64x2{step_op<OP>(acc[c][0], v[u][c][0], tab.w[k + u]),
+                                   step_op<OP>(acc[c][1], v[u][c][1], tab.w[k + u])};
+        }
+        for (; k < K; ++k) {
+            const f64x2* r = static_cast<const f64x2*>(tab.rows[k]) + off;
+#pragma unroll
+            for (int c = 0; c < kCpl64; ++c) {
+                const f64x2 v = __builtin_nontemporal_load(r + c * kBlock);
+                acc[c] = f64x2{step_op<OP>(acc[c][0], v[0], tab.w[k]), step_op<OP>(acc[c][1], v[1], tab.w[k])};
+            }
+        }
+#pragma unroll
+        for (int c = 0; c < kCpl64; ++c) {
+            const int64_t i = col + c * kBlock;
+            if (i >= b2 && i < e2)
+                __builtin_nontemporal_store(f64x2{fin_op<FIN>(acc[c][0], fin_val), fin_op<FIN>(acc[c][1], fin_val)},
+                                            out + i);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
 // synthetic inputs (bit-identical host twin: oracle/fedavg_oracle.c oracle_synth_value), written to a
 // tiled row: logical element i goes to dst[(i / tile) * tile_stride + i % tile]
 // ---------------------------------------------------------------------------------------------
@@ -698,6 +770,45 @@ static hipError_t launch_rows_f64x2(const RowTableGeneric& tab, int K, const voi
     for (int k = 0; k < K; ++k) tail.rows[k] = static_cast<const double*>(tab.rows[k]) + 2 * n2;
     const void* tail_in = acc_in ? static_cast<const void*>(static_cast<const double*>(acc_in) + 2 * n2) : nullptr;
     return launch_generic_t<double, double>(tail, K, tail_in, static_cast<double*>(out) + 2 * n2, 1, op, fin, fin_val, 1, s);
+}
+
+template <int OP, int FIN>
+static hipError_t launch_t64_f(const RowTableGeneric& tab, int K, int64_t ts2, const void* acc_in, void* out, int64_t b2,
+                               int64_t e2, double fin_val, int grid, hipStream_t s) {
+    if (acc_in) {
+        hipLaunchKernelGGL((fedavg_tiles_f64x2<OP, FIN, true>), dim3(grid), dim3(kBlock), 0, s, tab, K, ts2,
+                           static_cast<const f64x2*>(acc_in), static_cast<f64x2*>(out), b2, e2, fin_val);
+    } else {
+        hipLaunchKernelGGL((fedavg_tiles_f64x2<OP, FIN, false>), dim3(grid), dim3(kBlock), 0, s, tab, K, ts2,
+                           static_cast<const f64x2*>(acc_in), static_cast<f64x2*>(out), b2, e2, fin_val);
+    }
+    return hipGetLastError();
+}
+
+template <int OP>
+static hipError_t launch_t64_o(const RowTableGeneric& tab, int K, int64_t ts2, const void* acc_in, void* out, int64_t b2,
+                               int64_t e2, int fin, double fin_val, int grid, hipStream_t s) {
+    switch (fin) {
+        case FEDAVG_FIN_SCALE:
+            return launch_t64_f<OP, FEDAVG_FIN_SCALE>(tab, K, ts2, acc_in, out, b2, e2, fin_val, grid, s);
+        case FEDAVG_FIN_DIV:
+            return launch_t64_f<OP, FEDAVG_FIN_DIV>(tab, K, ts2, acc_in, out, b2, e2, fin_val, grid, s);
+        default:
+            return launch_t64_f<OP, FEDAVG_FIN_NONE>(tab, K, ts2, acc_in, out, b2, e2, fin_val, grid, s);
+    }
+}
+
+hipError_t launch_tiles_f64(const RowTableGeneric& tab, int K, int64_t tstride_elems, const void* acc_in, void* out,
+                            int64_t begin, int64_t end, int op, int fin, double fin_val, int grid, hipStream_t s) {
+    const int64_t ts2 = tstride_elems / 2, b2 = begin / 2, e2 = end / 2;
+    switch (op) {
+        case FEDAVG_OP_TORCH:
+            return launch_t64_o<FEDAVG_OP_TORCH>(tab, K, ts2, acc_in, out, b2, e2, fin, fin_val, grid, s);
+        case FEDAVG_OP_UNWEIGHTED:
+            return launch_t64_o<FEDAVG_OP_UNWEIGHTED>(tab, K, ts2, acc_in, out, b2, e2, fin, fin_val, grid, s);
+        default:
+            return launch_t64_o<FEDAVG_OP_NUMPY>(tab, K, ts2, acc_in, out, b2, e2, fin, fin_val, grid, s);
+    }
 }
 
 hipError_t launch_rows_generic(const RowTableGeneric& tab, int K, const void* acc_in, void* out, int64_t n,

@@ -312,6 +312,17 @@ class DeviceContext:
                ctypes.c_void_p(acc_in_ptr or 0), ctypes.c_void_p(out_ptr), ctypes.c_int(op), ctypes.c_int(fin),
                ctypes.c_double(float(count)))
 
+    def accumulate_tiled64(self, bases: Sequence[int], weights: Sequence[float], tile: int, tile_stride: int,
+                           begin: int, end: int, out_ptr: int, op: int, fin: int, count: float = 1.0,
+                           acc_in_ptr: Optional[int] = None) -> None:
+        k = len(bases)
+        b_arr = (ctypes.c_void_p * max(k, 1))(*bases)
+        w_arr = (ctypes.c_double * max(k, 1))(*[float(w) for w in weights])
+        N.call("fedavg_accumulate_tiled64", self.handle, b_arr, w_arr, ctypes.c_int(k), ctypes.c_size_t(tile),
+               ctypes.c_size_t(tile_stride), ctypes.c_size_t(begin), ctypes.c_size_t(end),
+               ctypes.c_void_p(acc_in_ptr or 0), ctypes.c_void_p(out_ptr), ctypes.c_int(op), ctypes.c_int(fin),
+               ctypes.c_double(float(count)))
+
     def accumulate_tiled_epi(self, bases: Sequence[int], weights: Sequence[float], tile: int, tile_stride: int,
                              begin: int, end: int, out_ptr: Optional[int], op: int, fin: int, count: float,
                              epilogue: "N.Epilogue", acc_in_ptr: Optional[int] = None) -> None:

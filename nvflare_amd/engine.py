@@ -157,15 +157,17 @@ _ARENA_FORMATS = {  # element formats that get tiled slabs: (C-ABI code, bytes p
     np.dtype(np.float32): (N.FEDAVG_F32, 4),
     np.dtype(np.float16): (N.FEDAVG_F16, 2),
     BF16_NP: (N.FEDAVG_BF16, 2),
+    np.dtype(np.float64): (N.FEDAVG_F64, 8),
 }
 
 
 class _Arena:
     """One element format's flat key layout, tiled client slabs and accumulator.
 
-    fp32 keys (the hot path) and 16-bit keys (float16 / bfloat16 totals) each get one: a contribution's keys
-    of that format occupy one slot of a slab of the arena, and a run of keys is aggregated by one launch of
-    the format's tiled kernel (``fedavg_accumulate_tiled`` / ``fedavg_accumulate_tiled16``)."""
+    fp32 keys (the hot path), 16-bit keys (float16 / bfloat16 totals) and fp64 keys (numpy's default dtype)
+    each get one: a contribution's keys of that format occupy one slot of a slab of the arena, and a run of
+    keys is aggregated by one launch of the format's tiled kernel (``fedavg_accumulate_tiled`` /
+    ``fedavg_accumulate_tiled16`` / ``fedavg_accumulate_tiled64``)."""
 
     __slots__ = ("fmt", "esize", "np_dtype", "layout_elems", "slabs", "live", "acc", "host_pool")
 
@@ -574,7 +576,9 @@ class DeviceFedAvg:
             raise TypeError("nvflare_amd: server-optimizer epilogues run on fp32 keys only")
 
         def launch(bases, weights, tile, stride, fin_, last_launch):
-            if arena.fmt != N.FEDAVG_F32:
+            if arena.fmt == N.FEDAVG_F64:
+                self.ctx.accumulate_tiled64(bases, weights, tile, stride, begin, end, out, first.op, fin_, count, acc_in)
+            elif arena.fmt != N.FEDAVG_F32:
                 self.ctx.accumulate_tiled16(arena.fmt, bases, weights, tile, stride, begin, end, out, first.op, fin_,
                                             count, acc_in)
             elif epi is not None and last_launch:

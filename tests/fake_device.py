@@ -220,6 +220,14 @@ class FakeDeviceContext:
         bits = orc.f32_to_bf16_bits(res) if name == "bfloat16" else res.astype(np.float16).view(np.uint16)
         self._view(out_ptr + begin * 2, (end - begin) * 2)[:] = bits.view(np.uint8)
 
+    def accumulate_tiled64(self, bases, weights, tile, stride, begin, end, out_ptr, op, fin, count=1.0,
+                           acc_in_ptr=None):
+        self.launches.append(("tiled64", len(bases), begin, end))
+        rows = [self._read_tiled(b, tile, stride, begin, end, 8, np.float64) for b in bases]
+        acc = None if acc_in_ptr is None else self._view(acc_in_ptr + begin * 8, (end - begin) * 8).view(np.float64).copy()
+        res = self._agg(rows, weights, op, fin, count, acc)
+        self._view(out_ptr + begin * 8, (end - begin) * 8)[:] = np.asarray(res, dtype=np.float64).view(np.uint8)
+
     def accumulate(self, rows, weights, n, out_ptr, in_dt, acc_dt, op, fin, count, acc_in_ptr=None):
         self.launches.append(("rows", len(rows), 0, n))
         tin, tacc = np.dtype(_NP[in_dt]), np.dtype(_NP[acc_dt])

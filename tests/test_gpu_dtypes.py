@@ -241,3 +241,43 @@ def test_engine_mixed_fp32_bf16_model(budget):
     assert same_bits(out["a.w"].numpy(), exp_w.numpy())
     if budget == 1:
         assert h.engine.stats["folds"] >= 1
+
+
+@pytest.mark.parametrize("mode", ["numpy", "torch", "unweighted"])
+@pytest.mark.parametrize("K,slots,begin,end", [(1, 1, 0, 4096), (3, 4, 64, 3 * 4096 + 130), (130, 131, 8, 2 * 4096)])
+def test_tiled64_vs_oracle(ctx, mode, K, slots, begin, end):
+    """fp64 arena kernel (fedavg_accumulate_tiled64) against the C oracle's fp64 restatement: numpy
+    (v*w then add, T * (1.0/count)), torch (fma, T / count), unweighted; partial ranges, more clients than one
+    launch holds (chained through out), and a continuation through acc_in."""
+    from nvflare_amd import _native as N
+    from nvflare_amd.device import TiledLayout
+
+    n = (end + 4095) // 4096 * 4096
+    rng = np.random.default_rng(K + begin + end)
+    rows = [rng.standard_normal(n) * 4 for _ in range(K)]
+    ws = [float(rng.random() * 20 + 1e-3) for _ in range(K)]
+    weighted = mode != "unweighted"
+    omode = orc.MODE_TORCH if mode == "torch" else orc.MODE_NUMPY
+    op = {"numpy": N.FEDAVG_OP_NUMPY, "torch": N.FEDAVG_OP_TORCH, "unweighted": N.FEDAVG_OP_UNWEIGHTED}[mode]
+    fin = N.FEDAVG_FIN_DIV if mode == "torch" else N.FEDAVG_FIN_SCALE
+    exp = orc.fedavg_c([r[begin:end].copy() for r in rows], ws, omode, weighted=weighted, fin=fin,
+                       count=_count(ws) if weighted else float(K))
+    lay = TiledLayout(4096, slots)
+    slab = ctx.alloc(lay.slab_elems(n) * 8)
+    bases = [slab.ptr + lay.slot_offset_elems(k) * 8 for k in range(K)]
+    for b, r in zip(bases, rows):
+        ctx.h2d_tiled(b, 4096 * 8, lay.tile_stride * 8, 0, r.ctypes.data, r.nbytes)
+    out = ctx.alloc(n * 8)
+    count = _count(ws) if weighted else float(K)
+    ctx.accumulate_tiled64(bases, ws, 4096, lay.tile_stride, begin, end, out.ptr, op, fin, count)
+    got = np.empty(n, np.float64)
+    ctx.d2h(got, out.ptr)
+    assert same_bits(got[begin:end], exp)
+    if K >= 3:
+        ctx.accumulate_tiled64(bases[:2], ws[:2], 4096, lay.tile_stride, begin, end, out.ptr, op, N.FEDAVG_FIN_NONE, 1.0)
+        ctx.accumulate_tiled64(bases[2:], ws[2:], 4096, lay.tile_stride, begin, end, out.ptr, op, fin, count,
+                               acc_in_ptr=out.ptr)
+        ctx.d2h(got, out.ptr)
+        assert same_bits(got[begin:end], exp)
+    slab.close()
+    out.close()

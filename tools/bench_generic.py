@@ -21,6 +21,9 @@ def main():
     ap.add_argument("--params", type=float, default=125e6)
     ap.add_argument("--dtype", choices=["float64", "float32"], default="float64")
     ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--layout", choices=["rows", "tiled"], default="rows",
+                    help="rows: K separate client buffers (fedavg_accumulate); tiled: the engine's fp64 slab "
+                         "(fedavg_accumulate_tiled64, float64 only)")
     args = ap.parse_args()
     import torch
 
@@ -33,14 +36,29 @@ def main():
     code = N.FEDAVG_F64 if args.dtype == "float64" else N.FEDAVG_F32
     g = torch.Generator(device="cuda:0")
     g.manual_seed(0)
-    rows = [torch.randn(P, dtype=tdt, device="cuda:0", generator=g) for _ in range(K)]
-    out = torch.empty(P, dtype=tdt, device="cuda:0")
-    torch.cuda.synchronize()
     ws = [float(1 + (37 * k) % 100) for k in range(K)]
+    if args.layout == "tiled":
+        from nvflare_amd.device import TiledLayout
 
-    def launch():
-        ctx.accumulate([r.data_ptr() for r in rows], ws, P, out.data_ptr(), code, code, N.FEDAVG_OP_NUMPY,
-                       N.FEDAVG_FIN_SCALE, sum(ws))
+        assert args.dtype == "float64", "the tiled layout here is the fp64 arena's"
+        lay = TiledLayout(4096, K)
+        slab = torch.randn(lay.slab_elems(P), dtype=tdt, device="cuda:0", generator=g)
+        rows = [slab]
+        bases = [slab.data_ptr() + lay.slot_offset_elems(k) * 8 for k in range(K)]
+        end = (P + 1) // 2 * 2
+        out = torch.empty(end, dtype=tdt, device="cuda:0")
+
+        def launch():
+            ctx.accumulate_tiled64(bases, ws, 4096, lay.tile_stride, 0, end, out.data_ptr(), N.FEDAVG_OP_NUMPY,
+                                   N.FEDAVG_FIN_SCALE, sum(ws))
+    else:
+        rows = [torch.randn(P, dtype=tdt, device="cuda:0", generator=g) for _ in range(K)]
+        out = torch.empty(P, dtype=tdt, device="cuda:0")
+
+        def launch():
+            ctx.accumulate([r.data_ptr() for r in rows], ws, P, out.data_ptr(), code, code, N.FEDAVG_OP_NUMPY,
+                           N.FEDAVG_FIN_SCALE, sum(ws))
+    torch.cuda.synchronize()
 
     launch()
     ctx.sync()
@@ -48,8 +66,8 @@ def main():
     for _ in range(args.steps):
         launch()
     ms = ctx.timing_end() / args.steps
-    nbytes = (K + 1) * P * rows[0].element_size()
-    print(json.dumps({"tool": "bench_generic", "dtype": args.dtype, "clients": K, "params": P, "kernel_ms": round(ms, 3),
+    nbytes = (K + 1) * P * out.element_size()
+    print(json.dumps({"tool": "bench_generic", "dtype": args.dtype, "layout": args.layout, "clients": K, "params": P, "kernel_ms": round(ms, 3),
                       "alg_GBs": round(nbytes / ms / 1e6, 1), "frac_of_8TBs": round(nbytes / ms / 1e6 / 8000, 4)}))
 
 
