@@ -148,3 +148,31 @@ def test_plain_numpy_fast_path_keeps_type_checks():
     res = eng.result()["w"]
     vals = [a, a + 1, a[::-1], a[::-1]]
     assert same_bits(res, _one_shot(vals, [1.0, 2.0, 4.0, 5.0], "numpy"))
+
+
+@pytest.mark.parametrize("budget,slab_slots", [(None, None), (1, None), (None, 4)])
+def test_fp64_arena_with_fp32_keys(budget, slab_slots):
+    """numpy float64 keys (numpy's default dtype) in their own arena beside fp32 keys: folding under a tiny
+    budget, slab chaining, a key missing from one client -- same bits as the one-shot numpy sequence."""
+    rng = np.random.default_rng(8)
+    K = 9
+    clients = []
+    for k in range(K):
+        c = {"w64": rng.standard_normal((37, 129)), "w32": rng.standard_normal(5000).astype(np.float32)}
+        if k != 4:
+            c["b64"] = rng.standard_normal(77)
+        clients.append(c)
+    ws = [float(1 + (37 * k) % 11) for k in range(K)]
+    e = fake_engine(max_resident_bytes=budget, slab_slots=slab_slots)
+    for c, w in zip(clients, ws):
+        e.add(list(c.items()), w, True)
+    out = e.result()
+    assert {a.np_dtype for a in e.arenas.values()} >= {np.dtype(np.float64), np.dtype(np.float32)}
+    for key in ("w64", "w32", "b64"):
+        seq = [(c[key], w) for c, w in zip(clients, ws) if key in c]
+        exp = FakeDeviceContext._agg([v.reshape(-1) for v, _ in seq], [w for _, w in seq], N.FEDAVG_OP_NUMPY,
+                                     N.FEDAVG_FIN_SCALE, _count([w for _, w in seq]), None)
+        assert out[key].dtype == seq[0][0].dtype
+        assert same_bits(out[key].reshape(-1), exp), (key, budget, slab_slots)
+    if budget == 1:
+        assert e.stats["folds"] > 0
