@@ -221,3 +221,17 @@ def test_sag_harness_known_answer_with_oracle():
 
     model, _ = run_sag(_OracleAggregator(), n_clients=2, num_rounds=3)
     np.testing.assert_equal(model[NUMPY_KEY], [[4, 5, 6], [7, 8, 9], [10, 11, 12]])
+
+
+def test_deprecated_accumulate_aggregator_path():
+    """accumulate_model_aggregator.py:20-22: the deprecated class path exists and is the InTime aggregator."""
+    import warnings
+
+    from nvflare_amd.app_common.aggregators.accumulate_model_aggregator import AccumulateWeightedAggregator
+    from nvflare_amd.app_common.aggregators.intime_accumulate_model_aggregator import InTimeAccumulateWeightedAggregator
+
+    with warnings.catch_warnings(record=True) as w:
+        warnings.simplefilter("always")
+        agg = AccumulateWeightedAggregator(expected_data_kind="WEIGHTS")
+    assert isinstance(agg, InTimeAccumulateWeightedAggregator)
+    assert any(issubclass(x.category, DeprecationWarning) for x in w)
