@@ -88,3 +88,45 @@ def test_fedopt_controller_update_model(opt_cls, kw, sched):
                 assert same_bits(got, ref), (rnd, k)
         assert ctl.optimizer.param_groups[-1]["lr"] == ref_opt.param_groups[-1]["lr"]
         g_dev, g_ref = out, exp
+
+
+@pytest.mark.parametrize("opt_cls,groups", [
+    (torch.optim.SGD, [dict(lr=0.5, momentum=0.9), dict(lr=0.1, momentum=0.5, weight_decay=1e-2, nesterov=True)]),
+    (torch.optim.Adam, [dict(lr=1e-2), dict(lr=3e-3, betas=(0.8, 0.99), weight_decay=1e-3, amsgrad=True)]),
+])
+def test_fedopt_controller_param_groups(opt_cls, groups):
+    """Two param groups with different hyperparameters: each parameter is stepped with its own group's
+    settings (launches split where the group changes), against torch CPU with the same groups."""
+    rng = np.random.default_rng(9)
+    model = fedopt_model()
+    ref_model = copy.deepcopy(model)
+
+    def split(m):
+        ps = dict(m.named_parameters())
+        return [{"params": [ps["lin1.weight"], ps["lin2.weight"]], **groups[0]},
+                {"params": [ps["lin1.bias"], ps["bn.weight"], ps["bn.bias"]], **groups[1]}]
+
+    ref_opt = opt_cls(split(ref_model), foreach=False)
+    ctl = object.__new__(DeviceFedOptUpdate)
+    ctl.device = torch.device("cuda:0")
+    ctl.torch_model = model.to(ctl.device)
+    ctl.optimizer = opt_cls(split(model))
+    ctl.lr_scheduler = None
+    ctl.current_round = 0
+    ctl.info = lambda msg: None
+    names = [n for n, _ in ref_model.named_parameters()]
+    params0 = {k: v.detach().cpu().numpy().copy() for k, v in ref_model.state_dict().items()}
+    g_dev = FLModel(params={k: v.copy() for k, v in params0.items()})
+    for rnd in range(3):
+        diff = {n: (rng.standard_normal(params0[n].shape) * 0.05).astype(np.float32) for n in names}
+        out = ctl.update_model(g_dev, FLModel(params=diff))
+        exp = _reference_update(ref_model, ref_opt, None, {}, diff)
+        for n in names:
+            got, ref = np.asarray(out.params[n]), exp[n]
+            if opt_cls is torch.optim.SGD:
+                assert same_bits(got, ref), (rnd, n)
+            else:
+                lr = max(g["lr"] for g in groups)
+                tol = adam_param_tolerance(params0[n], ref, lr, rnd + 1)
+                assert np.all(np.abs(got.astype(np.float64) - ref.astype(np.float64)) <= tol), (rnd, n)
+        g_dev = out
