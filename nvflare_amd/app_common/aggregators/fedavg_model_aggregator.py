@@ -26,14 +26,17 @@ from .weighted_aggregation_helper import AggregationStatsKey, WeightedAggregatio
 
 class DeviceFedAvgModelAggregator(ModelAggregator):
     def __init__(self, aggregation_weights: Optional[Dict[str, float]] = None, device: Optional[int] = None,
-                 devices: Optional[list] = None, max_resident_bytes: Optional[int] = None):
+                 devices: Optional[list] = None, max_resident_bytes: Optional[int] = None, defer_result: bool = False):
         """Args:
             aggregation_weights: per-client multipliers (FedAvg's ``aggregation_weights``), default 1.0.
             device / devices / max_resident_bytes: passed to the drop-in ``WeightedAggregationHelper``.
+            defer_result: fp32 params of the aggregate stay in HBM as ``DeferredAggregate`` values; the FedOpt
+                controller drop-in (app_opt/pt/fedopt_ctl.py) then aggregates and steps them in one launch.
         """
         super().__init__()
         self.aggregation_weights = dict(aggregation_weights or {})
-        self._helper = WeightedAggregationHelper(device=device, devices=devices, max_resident_bytes=max_resident_bytes)
+        self._helper = WeightedAggregationHelper(device=device, devices=devices, max_resident_bytes=max_resident_bytes,
+                                                 defer_result=defer_result)
         self._lock = threading.Lock()
         self.reset_stats()
 

@@ -130,3 +130,46 @@ def test_fedopt_controller_param_groups(opt_cls, groups):
                 tol = adam_param_tolerance(params0[n], ref, lr, rnd + 1)
                 assert np.all(np.abs(got.astype(np.float64) - ref.astype(np.float64)) <= tol), (rnd, n)
         g_dev = out
+
+
+@pytest.mark.parametrize("opt_cls,kw", [(torch.optim.SGD, dict(lr=1.0, momentum=0.6)), (torch.optim.Adam, dict(lr=1e-2))])
+def test_fedopt_controller_with_deferred_aggregate(opt_cls, kw):
+    """FedAvg(aggregator=DeviceFedAvgModelAggregator(defer_result=True)) feeding the FedOpt controller: the
+    aggregate's params arrive as DeferredAggregate values and the controller aggregates and steps them in one
+    launch per run; results bit-identical to the eager aggregator + separate step, two rounds."""
+    from nvflare_amd.app_common.aggregators import DeviceFedAvgModelAggregator
+    from nvflare_amd.compat import FLMetaKey
+    from nvflare_amd.deferred import DeferredAggregate
+
+    rng = np.random.default_rng(13)
+    base = fedopt_model()
+    outs = {}
+    for defer in (False, True):
+        model = copy.deepcopy(base)
+        ctl = object.__new__(DeviceFedOptUpdate)
+        ctl.device = torch.device("cuda:0")
+        ctl.torch_model = model.to(ctl.device)
+        ctl.optimizer = opt_cls(model.parameters(), **kw)
+        ctl.lr_scheduler = None
+        ctl.current_round = 0
+        ctl.info = lambda msg: None
+        agg = DeviceFedAvgModelAggregator(device=0, defer_result=defer)
+        params0 = {k: v.detach().cpu().numpy().copy() for k, v in base.state_dict().items()}
+        g = FLModel(params={k: v.copy() for k, v in params0.items()})
+        crng = np.random.default_rng(13)
+        for rnd in range(2):
+            agg.reset_stats()
+            for c in range(4):
+                diff = {k: (crng.standard_normal(v.shape) * 0.05).astype(np.float32) for k, v in params0.items()
+                        if v.dtype == np.float32}
+                m = FLModel(params=diff, current_round=rnd, meta={FLMetaKey.NUM_STEPS_CURRENT_ROUND: 1 + c})
+                m.meta["client_name"] = f"site-{c}"
+                assert agg.accept_model(m)
+            res = agg.aggregate_model()
+            if defer:
+                assert isinstance(res.params["lin1.weight"], DeferredAggregate)
+            g = ctl.update_model(g, res)
+        outs[defer] = {k: np.asarray(v).copy() for k, v in g.params.items()}
+    assert set(outs[False]) == set(outs[True])
+    for k in outs[False]:
+        assert same_bits(outs[True][k], outs[False][k]), k
