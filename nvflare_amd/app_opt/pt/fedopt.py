@@ -225,6 +225,7 @@ class DeviceServerOptimizer:
         groups = self._group_of()
         present = []
         fused = self._fused_step(model_diff, groups)
+        host_pieces, keep = [], []  # host differences: one pass through the pinned ring, not a copy per tensor
         with torch.no_grad():
             for s in self.slots:
                 if s.name not in model_diff or s.name in fused:
@@ -237,11 +238,20 @@ class DeviceServerOptimizer:
                     raise RuntimeError(f"assigned grad has data of a different size for {s.name!r}")
                 if self.g is None:
                     self.g = torch.zeros_like(self.p)
-                self.g[s.offset:s.offset + s.n].copy_(t.reshape(-1), non_blocking=False)
+                if t.device.type == "cpu":
+                    t = t.contiguous()
+                    keep.append(t)
+                    host_pieces.append((s.offset * 4, t.data_ptr(), s.n * 4))
+                else:
+                    self.g[s.offset:s.offset + s.n].copy_(t.reshape(-1), non_blocking=False)
                 present.append(s)
         if not present:
             return [s.name for s in self.slots if s.name in fused]
         torch.cuda.synchronize(self.torch_device)
+        if host_pieces:  # the compute stream waits for these copies (fedavg_h2d_tiled_multi)
+            with self.ctx.lock:
+                self.ctx.h2d_tiled_multi(self.g.data_ptr(), 4096 * 4, 4096 * 4, sorted(host_pieces))
+        del keep
         # one launch per run of consecutive stepped parameters sharing group and per-parameter state
         runs: List[Tuple[tuple, List[_Slot]]] = []
         for s in present:
