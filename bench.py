@@ -150,8 +150,20 @@ def cpu_baseline_and_spot_check(args, ctx, K, out_buf, weights, count, P, col0, 
                       f"restatement of weighted_aggregation_helper.py:181-236, {reps} reps in {t_tot:.1f}s",
             "numpy_single_thread_GiBs": round(4.0 * K * Ps / t_np / 2**30, 3),
             "host_cpu_count": os.cpu_count(),
+            "host_cpu_model": _cpu_model(),
         }
     return res
+
+
+def _cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
 
 
 def pmc_traffic(args, K, P):
