@@ -72,6 +72,7 @@ enum fedavg_epi {
     FEDAVG_EPI_SGD = 2,      /* torch SGD on g = -d   app_opt/pt/fedopt.py:157-182 */
     FEDAVG_EPI_ADAM = 3,     /* torch Adam/AdamW on g = -d  (torch/optim/adam.py:347-551) */
     FEDAVG_EPI_ADAGRAD = 4,  /* torch Adagrad on g = -d  (torch/optim/adagrad.py _single_tensor_adagrad) */
+    FEDAVG_EPI_RMSPROP = 5,  /* torch RMSprop on g = -d  (torch/optim/rmsprop.py _single_tensor_rmsprop) */
 };
 
 typedef struct fedavg_epilogue {
@@ -90,6 +91,8 @@ typedef struct fedavg_epilogue {
     int amsgrad;                /* Adam: normalise by max_exp_avg_sq = max(max_exp_avg_sq, exp_avg_sq) */
     float* state3;              /* Adam amsgrad: max_exp_avg_sq (in place) */
     double lr_decay;            /* Adagrad: clr = lr / (1 + (step - 1) * lr_decay); state1 = sum, eps */
+    double alpha;               /* RMSprop: smoothing constant; state1 = square_avg, state2 = momentum_buffer */
+    int centered;               /* RMSprop: state3 = grad_avg */
 } fedavg_epilogue;
 
 /* Quantized payload formats (nvflare/app_opt/pt/quantization/dequantizer.py:47-185, row f4). */

@@ -169,6 +169,7 @@ FEDAVG_EPI_ADD_BASE = 1
 FEDAVG_EPI_SGD = 2
 FEDAVG_EPI_ADAM = 3
 FEDAVG_EPI_ADAGRAD = 4
+FEDAVG_EPI_RMSPROP = 5
 
 
 class Epilogue(ctypes.Structure):
@@ -195,6 +196,8 @@ class Epilogue(ctypes.Structure):
         ("amsgrad", c_int),
         ("state3", c_void_p),
         ("lr_decay", c_double),
+        ("alpha", c_double),
+        ("centered", c_int),
     ]
 
 

@@ -8,7 +8,7 @@ representation (torch tensors if the global model holds tensors, numpy otherwise
 
 What differs is where the step runs.  The reference sets ``param.grad`` and calls
 ``optimizer.step()``; here the model's parameters are re-pointed into ONE flat fp32 buffer in HBM and
-``torch.optim.SGD`` / ``Adam`` / ``AdamW`` / ``Adagrad`` steps are executed by the HIP fused-epilogue kernel
+``torch.optim.SGD`` / ``Adam`` / ``AdamW`` / ``Adagrad`` / ``RMSprop`` steps are executed by the HIP fused-epilogue kernel
 (``fedavg_accumulate_tiled_epi`` with the aggregated difference as ``acc_in``), with torch's
 single-tensor rounding sequence (``tests/test_fedopt_oracle.py``).  The torch optimizer object is kept
 for its ``param_groups`` (read every step, so lr schedulers work unchanged) and its ``state`` is filled
@@ -108,9 +108,11 @@ class DeviceServerOptimizer:
             return N.FEDAVG_EPI_ADAM
         if isinstance(optimizer, torch.optim.Adagrad):
             return N.FEDAVG_EPI_ADAGRAD
+        if isinstance(optimizer, torch.optim.RMSprop):
+            return N.FEDAVG_EPI_RMSPROP
         raise NotImplementedError(
             f"nvflare_amd: server optimizer {type(optimizer).__module__}.{type(optimizer).__name__} has no device "
-            "kernel (supported: torch.optim.SGD, Adam, AdamW, Adagrad)")
+            "kernel (supported: torch.optim.SGD, Adam, AdamW, Adagrad, RMSprop)")
 
     def _group_of(self) -> Dict[int, dict]:
         return {id(p): g for g in self.optimizer.param_groups for p in g["params"]}
@@ -130,7 +132,7 @@ class DeviceServerOptimizer:
         self.m = torch.zeros(total, dtype=torch.float32, device=dev)
         self.v = torch.zeros(total, dtype=torch.float32, device=dev)
         self.vmax = None  # Adam(amsgrad=True): max_exp_avg_sq, allocated with the first amsgrad group
-        if self.kind == N.FEDAVG_EPI_ADAM and any(g.get("amsgrad") for g in self.optimizer.param_groups):
+        if any(g.get("amsgrad") or g.get("centered") for g in self.optimizer.param_groups):  # Adam / RMSprop
             self.vmax = torch.zeros(total, dtype=torch.float32, device=dev)
         self.g = None
         self.host_pool = HostArenaPool()  # host copies of p returned by the generator, reused when released
@@ -142,7 +144,9 @@ class DeviceServerOptimizer:
                 s.param.data = view
                 st = self.optimizer.state.get(s.param) or {}
                 # resume from optimizer state present before binding (e.g. a loaded state_dict)
-                if "momentum_buffer" in st and st["momentum_buffer"] is not None:
+                if self.kind == N.FEDAVG_EPI_RMSPROP:
+                    self._resume_rmsprop(s, st, dev)
+                elif "momentum_buffer" in st and st["momentum_buffer"] is not None:
                     self.m[s.offset:s.offset + s.n].copy_(st["momentum_buffer"].reshape(-1).to(dev))
                     s.has_momentum_buffer = True
                 if "exp_avg" in st:
@@ -161,6 +165,14 @@ class DeviceServerOptimizer:
         self.by_name = {s.name: s for s in slots}
         torch.cuda.synchronize(dev)
 
+    def _resume_rmsprop(self, s: "_Slot", st: dict, dev) -> None:
+        """RMSprop state: square_avg -> m, momentum_buffer -> v, grad_avg -> vmax."""
+        for key, buf in (("square_avg", self.m), ("momentum_buffer", self.v), ("grad_avg", self.vmax)):
+            if st.get(key) is not None and buf is not None:
+                buf[s.offset:s.offset + s.n].copy_(st[key].reshape(-1).to(dev))
+        if "step" in st:
+            s.step = float(st["step"])
+
     def is_bound(self) -> bool:
         named = dict(self.model.named_parameters())
         if set(named) != set(self.by_name):
@@ -176,6 +188,14 @@ class DeviceServerOptimizer:
         elif self.kind == N.FEDAVG_EPI_ADAGRAD:
             st["step"] = torch.tensor(s.step, dtype=torch.float32)
             st["sum"] = self.m[s.offset:s.offset + s.n].view(s.param.shape)
+        elif self.kind == N.FEDAVG_EPI_RMSPROP:
+            g = self._group_of()[id(s.param)]
+            st["step"] = torch.tensor(s.step, dtype=torch.float32)
+            st["square_avg"] = self.m[s.offset:s.offset + s.n].view(s.param.shape)
+            if g.get("momentum", 0.0) > 0:
+                st["momentum_buffer"] = self.v[s.offset:s.offset + s.n].view(s.param.shape)
+            if g.get("centered"):
+                st["grad_avg"] = self._max_exp_avg_sq()[s.offset:s.offset + s.n].view(s.param.shape)
         else:
             st["step"] = torch.tensor(s.step, dtype=torch.float32)
             st["exp_avg"] = self.m[s.offset:s.offset + s.n].view(s.param.shape)
@@ -205,6 +225,15 @@ class DeviceServerOptimizer:
             e.lr_decay = float(group.get("lr_decay", 0.0))
             e.eps = float(group["eps"])
             e.step = s.step + 1.0
+        elif self.kind == N.FEDAVG_EPI_RMSPROP:
+            e.alpha = float(group["alpha"])
+            e.eps = float(group["eps"])
+            e.momentum = float(group.get("momentum", 0.0))
+            e.state2 = self.v.data_ptr()
+            e.step = s.step + 1.0
+            if group.get("centered"):
+                e.centered = 1
+                e.state3 = self._max_exp_avg_sq().data_ptr()
         else:
             b1, b2 = group["betas"]
             e.beta1, e.beta2, e.eps = float(b1), float(b2), float(group["eps"])

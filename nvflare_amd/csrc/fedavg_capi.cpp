@@ -409,6 +409,13 @@ fedavg::EpiParams make_epi(const fedavg_epilogue& e) {
     E.base = e.base;
     E.amsgrad = e.kind == FEDAVG_EPI_ADAM && e.amsgrad;
     E.state3 = e.state3;
+    if (e.kind == FEDAVG_EPI_RMSPROP) {  // rmsprop.py: square_avg.mul_(alpha).addcmul_(g, g, 1 - alpha), lerp(1 - alpha)
+        E.beta2 = (float)e.alpha;
+        E.one_minus_beta2 = (float)(1.0 - e.alpha);
+        E.one_minus_beta1 = E.one_minus_beta2;
+        E.one_minus_beta1_m1 = E.one_minus_beta1 - 1.0f;
+        E.centered = e.centered != 0;
+    }
     return E;
 }
 
@@ -1034,7 +1041,7 @@ int fedavg_accumulate_tiled_epi(fedavg_ctx* ctx, const void* const* bases, const
                 throw Error(g_last_error);
             return;
         }
-        if (epi->kind < FEDAVG_EPI_ADD_BASE || epi->kind > FEDAVG_EPI_ADAGRAD) throw Error("bad epilogue kind");
+        if (epi->kind < FEDAVG_EPI_ADD_BASE || epi->kind > FEDAVG_EPI_RMSPROP) throw Error("bad epilogue kind");
         if (k_rows < 0 || (k_rows == 0 && !acc_in)) throw Error("k_rows == 0 requires acc_in");
         check_op_fin(op, fin);
         if (tile_elems != (size_t)fedavg::kDefaultTile)
@@ -1054,6 +1061,9 @@ int fedavg_accumulate_tiled_epi(fedavg_ctx* ctx, const void* const* bases, const
         if (epi->kind == FEDAVG_EPI_ADAGRAD && (!epi->param || !epi->state1))
             throw Error("ADAGRAD needs param and state1 (sum)");
         if (epi->kind == FEDAVG_EPI_ADAGRAD && epi->step < 1.0) throw Error("ADAGRAD step must be >= 1");
+        if (epi->kind == FEDAVG_EPI_RMSPROP &&
+            (!epi->param || !epi->state1 || (epi->momentum != 0.0 && !epi->state2) || (epi->centered && !epi->state3)))
+            throw Error("RMSPROP needs param, state1 (square_avg), state2 with momentum, state3 when centered");
         for (const void* p : {(const void*)epi->param, (const void*)epi->state1, (const void*)epi->state2,
                               (const void*)epi->state3, (const void*)epi->base, (const void*)out, acc_in})
             if (misaligned(p)) throw Error("epilogue/out/acc_in pointers must be 16-byte aligned");

@@ -70,7 +70,8 @@ struct EpiParams {
     float* state2;  // Adam exp_avg_sq
     const float* base;
     int amsgrad;
-    float* state3;  // Adam amsgrad: max_exp_avg_sq
+    float* state3;  // Adam amsgrad: max_exp_avg_sq | RMSprop centered: grad_avg
+    int centered;   // RMSprop (alpha in beta2 / one_minus_beta2 / one_minus_beta1)
 };
 
 struct DequantLaunch {

@@ -195,6 +195,11 @@ __device__ __forceinline__ EpiIn epi_load(const EpiParams& E, const int64_t i) {
     } else if constexpr (EPI == FEDAVG_EPI_ADAGRAD) {
         in.a = load4<true>(reinterpret_cast<const f32x4*>(E.param) + i);
         in.b = load4<true>(reinterpret_cast<const f32x4*>(E.state1) + i);
+    } else if constexpr (EPI == FEDAVG_EPI_RMSPROP) {
+        in.a = load4<true>(reinterpret_cast<const f32x4*>(E.param) + i);
+        in.b = load4<true>(reinterpret_cast<const f32x4*>(E.state1) + i);
+        if (E.has_momentum) in.c = load4<true>(reinterpret_cast<const f32x4*>(E.state2) + i);
+        if (E.centered) in.d = load4<true>(reinterpret_cast<const f32x4*>(E.state3) + i);
     } else {
         in.a = load4<true>(reinterpret_cast<const f32x4*>(E.param) + i);
         in.b = load4<true>(reinterpret_cast<const f32x4*>(E.state1) + i);
@@ -239,6 +244,35 @@ __device__ __forceinline__ void epilogue4(const EpiParams& E, const int64_t i, c
         }
         store4<true>(p4, p);
         store4<true>(reinterpret_cast<f32x4*>(E.state1) + i, sum);
+    } else if constexpr (EPI == FEDAVG_EPI_RMSPROP) {
+        f32x4 p = in.a;
+        f32x4 sq = in.b;
+        f32x4 buf = in.c;
+        f32x4 ga = in.d;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            float g = E.maximize ? d[c] : -d[c];
+            if (E.has_weight_decay) g = __builtin_fmaf(p[c], E.weight_decay, g);       // grad.add(param, alpha=wd)
+            sq[c] = __builtin_fmaf(E.one_minus_beta2 * g, g, sq[c] * E.beta2);       // mul_(alpha).addcmul_(g, g, 1-alpha)
+            float avg;
+            if (E.centered) {
+                ga[c] = lerp_torch(ga[c], g, E.one_minus_beta1, E.one_minus_beta1_m1);  // grad_avg.lerp_(g, 1-alpha)
+                avg = __builtin_sqrtf(__builtin_fmaf(-ga[c], ga[c], sq[c]));          // addcmul(ga, ga, -1).sqrt_()
+            } else {
+                avg = __builtin_sqrtf(sq[c]);
+            }
+            avg = avg + E.eps;
+            if (E.has_momentum) {
+                buf[c] = buf[c] * E.momentum + g / avg;                               // buf.mul_(m).addcdiv_(g, avg)
+                p[c] = __builtin_fmaf(buf[c], E.neg_lr, p[c]);                        // param.add_(buf, alpha=-lr)
+            } else {
+                p[c] = p[c] + (E.neg_lr * g) / avg;                                   // param.addcdiv_(g, avg, -lr)
+            }
+        }
+        store4<true>(p4, p);
+        store4<true>(reinterpret_cast<f32x4*>(E.state1) + i, sq);
+        if (E.has_momentum) store4<true>(reinterpret_cast<f32x4*>(E.state2) + i, buf);
+        if (E.centered) store4<true>(reinterpret_cast<f32x4*>(E.state3) + i, ga);
     } else {  // EPI_ADAM
         f32x4 p = in.a;
         f32x4 m = in.b;
@@ -638,6 +672,10 @@ static hipError_t launch_epi_p(const TileLaunch& L, const EpiParams& E, hipStrea
             break;
         case FEDAVG_EPI_ADAGRAD:
             hipLaunchKernelGGL((fedavg_tiles_epi_f32x4<OP, FIN, ACC_IN, FEDAVG_EPI_ADAGRAD, PRE>), dim3(L.grid),
+                               dim3(kBlock), 0, s, L.tab, L.k, L.tstride4, ai, o, L.b4, L.e4, L.fin_val, E);
+            break;
+        case FEDAVG_EPI_RMSPROP:
+            hipLaunchKernelGGL((fedavg_tiles_epi_f32x4<OP, FIN, ACC_IN, FEDAVG_EPI_RMSPROP, PRE>), dim3(L.grid),
                                dim3(kBlock), 0, s, L.tab, L.k, L.tstride4, ai, o, L.b4, L.e4, L.fin_val, E);
             break;
         default:

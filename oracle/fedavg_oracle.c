@@ -116,6 +116,7 @@ void oracle_synth_fill_f32(uint64_t seed, uint64_t row, const uint64_t* cols, si
  *   ADD_BASE  w = base + d            full_model_shareable_generator.py:58-67 (WEIGHT_DIFF apply)
  *   SGD       torch/optim/sgd.py _single_tensor_sgd on grad g = -1.0 * d   (app_opt/pt/fedopt.py:175)
  *   ADAGRAD   torch/optim/adagrad.py _single_tensor_adagrad on g = -1.0 * d (m holds state_sum)
+ *   RMSPROP   torch/optim/rmsprop.py _single_tensor_rmsprop (m square_avg, v momentum_buffer, vmax grad_avg)
  *   ADAM      torch/optim/adam.py _single_tensor_adam (:347-551) on g = -1.0 * d; amsgrad divides by
  *             sqrt(vmax), vmax = torch.maximum(vmax, v) kept as a third state
  * Rounding sequence pinned against torch 2.10 CPU (tests/test_fedopt_oracle.py):
@@ -126,7 +127,8 @@ void oracle_synth_fill_f32(uint64_t seed, uint64_t row, const uint64_t* cols, si
  * Scalars follow torch: python-float hyperparameters and bias corrections computed in fp64, cast to
  * fp32 where they meet a tensor.
  * ------------------------------------------------------------------------------------------------ */
-enum { ORACLE_EPI_NONE = 0, ORACLE_EPI_ADD_BASE = 1, ORACLE_EPI_SGD = 2, ORACLE_EPI_ADAM = 3, ORACLE_EPI_ADAGRAD = 4 };
+enum { ORACLE_EPI_NONE = 0, ORACLE_EPI_ADD_BASE = 1, ORACLE_EPI_SGD = 2, ORACLE_EPI_ADAM = 3, ORACLE_EPI_ADAGRAD = 4,
+       ORACLE_EPI_RMSPROP = 5 };
 
 typedef struct {
     int kind;
@@ -138,6 +140,8 @@ typedef struct {
     double beta1, beta2, eps, step;               /* Adam: step after increment (1, 2, ...) */
     int amsgrad;                                  /* Adam: normalise by the running max of v (vmax) */
     double lr_decay;                              /* Adagrad: clr = lr / (1 + (step - 1) * lr_decay) */
+    double alpha;                                 /* RMSprop smoothing constant */
+    int centered;                                 /* RMSprop: vmax holds grad_avg */
 } oracle_epilogue;
 
 /* torch.maximum: a NaN operand is the result */
@@ -178,6 +182,26 @@ void oracle_epilogue_apply(const float* delta, size_t n, const oracle_epilogue* 
             m[i] = fmaf(g, g, m[i]);                                  /* state_sum.addcmul_(g, g, value=1) */
             const float std_ = sqrtf(m[i]) + (float)epi->eps;         /* state_sum.sqrt().add_(eps) */
             p[i] = p[i] + (neg_clr * g) / std_;                       /* param.addcdiv_(g, std, value=-clr) */
+        } else if (epi->kind == ORACLE_EPI_RMSPROP) { /* torch/optim/rmsprop.py _single_tensor_rmsprop */
+            /* m = square_avg, v = momentum_buffer, vmax = grad_avg */
+            float g = epi->maximize ? d : -d;
+            if (epi->weight_decay != 0.0) g = fmaf(p[i], (float)epi->weight_decay, g);
+            const float oma = (float)(1.0 - epi->alpha);
+            m[i] = fmaf(oma * g, g, m[i] * (float)epi->alpha);       /* mul_(alpha).addcmul_(g, g, 1 - alpha) */
+            float avg;
+            if (epi->centered) {
+                vmax[i] = lerp_torch(vmax[i], g, oma);                /* grad_avg.lerp_(g, 1 - alpha) */
+                avg = sqrtf(fmaf(-vmax[i], vmax[i], m[i]));          /* addcmul(ga, ga, value=-1).sqrt_() */
+            } else {
+                avg = sqrtf(m[i]);
+            }
+            avg = avg + (float)epi->eps;
+            if (epi->momentum > 0.0) {
+                v[i] = v[i] * (float)epi->momentum + g / avg;         /* buf.mul_(momentum).addcdiv_(g, avg) */
+                p[i] = fmaf(v[i], (float)(-epi->lr), p[i]);           /* param.add_(buf, alpha=-lr) */
+            } else {
+                p[i] = p[i] + ((float)(-epi->lr) * g) / avg;          /* param.addcdiv_(g, avg, value=-lr) */
+            }
         } else { /* ADAM */
             float g = epi->maximize ? d : -d;
             float pv = p[i];

@@ -244,7 +244,7 @@ def synth_weights(K: int):
 # ---------------------------------------------------------------------------------------------------
 # server-optimizer epilogues (rows a9/a10): see oracle_epilogue_apply in fedavg_oracle.c
 # ---------------------------------------------------------------------------------------------------
-EPI_NONE, EPI_ADD_BASE, EPI_SGD, EPI_ADAM, EPI_ADAGRAD = 0, 1, 2, 3, 4
+EPI_NONE, EPI_ADD_BASE, EPI_SGD, EPI_ADAM, EPI_ADAGRAD, EPI_RMSPROP = 0, 1, 2, 3, 4, 5
 
 
 class _Epi(ctypes.Structure):
@@ -264,6 +264,8 @@ class _Epi(ctypes.Structure):
         ("step", ctypes.c_double),
         ("amsgrad", ctypes.c_int),
         ("lr_decay", ctypes.c_double),
+        ("alpha", ctypes.c_double),
+        ("centered", ctypes.c_int),
     ]
 
 
@@ -284,8 +286,8 @@ def epilogue_apply(delta, kind, p=None, m=None, v=None, base=None, vmax=None, **
     def ptr(a):
         return None if a is None else a.ctypes.data
 
-    if e.amsgrad and vmax is None:
-        raise ValueError("amsgrad needs vmax")
+    if (e.amsgrad or e.centered) and vmax is None:
+        raise ValueError("amsgrad / centered need vmax")
     fn(delta.ctypes.data, delta.size, ctypes.byref(e), ptr(p), ptr(m), ptr(v), ptr(vmax), ptr(base), out.ctypes.data)
     return out if kind in (EPI_NONE, EPI_ADD_BASE) else p
 

@@ -135,6 +135,48 @@ def test_adagrad_vs_torch(oracle, kw):
     assert float((diff > 0).mean()) < 0.01
 
 
+@pytest.mark.parametrize("kw", [
+    dict(lr=1e-2),
+    dict(lr=1e-2, alpha=0.9, eps=1e-6, momentum=0.9),
+    dict(lr=1e-3, centered=True, weight_decay=1e-3),
+    dict(lr=1e-3, centered=True, momentum=0.5, maximize=True),
+])
+def test_rmsprop_vs_torch(oracle, kw):
+    """torch/optim/rmsprop.py _single_tensor_rmsprop: square_avg, momentum_buffer and grad_avg bit-exact
+    (without weight decay feeding p back); params within the sqrt bound, as for Adam."""
+    rng = np.random.default_rng(4)
+    n = 200_003
+    p0 = rng.standard_normal(n).astype(np.float32)
+    deltas = [(rng.standard_normal(n) * 0.01).astype(np.float32) for _ in range(5)]
+    tp, st = _torch_steps(torch.optim.RMSprop, kw, p0, deltas)
+    p, sq, buf, ga = p0.copy(), np.zeros(n, np.float32), np.zeros(n, np.float32), np.zeros(n, np.float32)
+    for k, d in enumerate(deltas):
+        oracle.epilogue_apply(d, oracle.EPI_RMSPROP, p=p, m=sq, v=buf, vmax=ga, lr=kw["lr"], alpha=kw.get("alpha", 0.99),
+                              eps=kw.get("eps", 1e-8), momentum=kw.get("momentum", 0.0),
+                              weight_decay=kw.get("weight_decay", 0.0), centered=int(kw.get("centered", False)),
+                              maximize=int(kw.get("maximize", False)), step=float(k + 1))
+    steps = len(deltas)
+    # every step adds a term g / avg with |g / avg| <= 1 / sqrt(1 - alpha) (square_avg >= (1 - alpha) g^2):
+    # torch's sqrt (1 ulp off on ~0.6 % of elements) perturbs such terms, which the momentum buffer sums
+    unit = np.float32(1.0 / np.sqrt(1.0 - kw.get("alpha", 0.99)))
+    states = [(sq, "square_avg")] + ([(buf, "momentum_buffer")] if kw.get("momentum") else []) + \
+             ([(ga, "grad_avg")] if kw.get("centered") else [])
+    for ours, key in states:
+        ref = st[key].numpy()
+        if kw.get("weight_decay") or key == "momentum_buffer":  # inputs carry torch's sqrt roundings
+            scale = np.maximum(np.abs(ref), unit if key == "momentum_buffer" else np.float32(0))
+            scale = np.maximum(scale, np.float32(kw.get("weight_decay", 0.0)) * np.abs(p0))
+            assert np.all(np.abs(ours.astype(np.float64) - ref) <= steps * 2 * np.spacing(scale)), key
+            assert float((ours != ref).mean()) < 0.02, key
+        else:
+            assert same_bits(ours, ref), key
+    tol = 2 * steps * np.spacing(np.maximum(np.maximum(np.abs(p0), np.abs(tp)), np.float32(kw["lr"]))).astype(np.float64)
+    tol += kw["lr"] * steps * steps * 2 * float(np.spacing(unit))
+    diff = np.abs(p.astype(np.float64) - tp.astype(np.float64))
+    assert np.all(diff <= tol), float((diff / tol).max())
+    assert float((diff > 0).mean()) < 0.02
+
+
 def test_add_base_matches_numpy_generator(oracle):
     """full_model_shareable_generator.py:58-67: weights[k] = weights[k] + diff[k] (numpy fp32 add)."""
     rng = np.random.default_rng(2)

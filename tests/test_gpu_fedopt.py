@@ -320,3 +320,34 @@ def test_adagrad_epilogue(ctx, oracle, K, hp):
             assert same_bits(dev.get("p"), p) and same_bits(dev.get("s"), s), step
         finally:
             dev.close()
+
+
+@pytest.mark.parametrize("K,hp", [(6, dict(lr=1e-2, alpha=0.99, eps=1e-8)),
+                                  (3, dict(lr=1e-2, alpha=0.9, eps=1e-6, momentum=0.9, weight_decay=1e-3)),
+                                  (2, dict(lr=1e-3, alpha=0.95, eps=1e-8, centered=1, momentum=0.5, maximize=1)),
+                                  (0, dict(lr=1e-3, alpha=0.99, eps=1e-8, centered=1))])
+def test_rmsprop_epilogue(ctx, oracle, K, hp):
+    """RMSprop: square_avg = fma((1-a) g, g, sq * a); centered grad_avg = lerp(ga, g, 1-a) and
+    avg = sqrt(fma(-ga, ga, sq)) + eps; momentum buf = buf * m + g / avg, p = fma(buf, -lr, p), else
+    p += (-lr g) / avg.  Three steps, bit-exact vs the oracle (pinned to torch CPU in test_fedopt_oracle)."""
+    rng = np.random.default_rng(90 + K)
+    n = 3 * TILE + 28
+    p = rng.standard_normal(n).astype(np.float32)
+    sq, buf, ga = (np.zeros(n, np.float32) for _ in range(3))
+    for step in range(3):
+        rows = [(rng.standard_normal(n) * 0.05).astype(np.float32) for _ in range(K)]
+        ws = [float(1 + (37 * k) % 100) for k in range(K)]
+        delta = (rng.standard_normal(n) * 0.05).astype(np.float32) if K == 0 else None
+        dev = _Dev(ctx, rows, n)
+        try:
+            e = _epi(5, param=dev.buf("p", p), state1=dev.buf("sq", sq), state2=dev.buf("buf", buf),
+                     state3=dev.buf("ga", ga), step=float(step + 1), **hp)
+            acc_ptr = dev.buf("acc", delta) if K == 0 else None
+            ctx.accumulate_tiled_epi(dev.bases, ws, TILE, dev.lay.tile_stride, 0, dev.n4, None, 1,
+                                     2 if K else 0, _sum(ws) if K else 1.0, e, acc_in_ptr=acc_ptr)
+            d = oracle.fedavg_c(rows, ws, oracle.MODE_TORCH, nthreads=8) if K else delta
+            oracle.epilogue_apply(d, oracle.EPI_RMSPROP, p=p, m=sq, v=buf, vmax=ga, step=float(step + 1), **hp)
+            assert same_bits(dev.get("p"), p) and same_bits(dev.get("sq"), sq), step
+            assert same_bits(dev.get("buf"), buf) and same_bits(dev.get("ga"), ga), step
+        finally:
+            dev.close()

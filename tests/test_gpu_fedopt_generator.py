@@ -101,14 +101,14 @@ def test_fedopt_generator_optimizer_state_views():
 
 def test_fedopt_generator_rejects_unsupported_optimizer():
     model = fedopt_model()
-    gen = PTFedOptModelShareableGenerator(optimizer_args={"path": "torch.optim.RMSprop", "args": {"lr": 1e-3}},
+    gen = PTFedOptModelShareableGenerator(optimizer_args={"path": "torch.optim.Adamax", "args": {"lr": 1e-3}},
                                           source_model=model, device=0)
     gen.handle_event(EventType.START_RUN, FLContext())
     w = {k: v.detach().cpu().numpy().copy() for k, v in model.state_dict().items()}
     fl_ctx = FLContext()
     fl_ctx.set_prop(AppConstants.GLOBAL_MODEL, make_model_learnable(w, {}))
     diff = {"lin1.weight": np.zeros((64, 7), np.float32)}
-    with pytest.raises(NotImplementedError, match="RMSprop"):
+    with pytest.raises(NotImplementedError, match="Adamax"):
         gen.shareable_to_learnable(DXO(DataKind.WEIGHT_DIFF, data=diff).to_shareable(), fl_ctx)
 
 
