@@ -73,6 +73,7 @@ enum fedavg_epi {
     FEDAVG_EPI_ADAM = 3,     /* torch Adam/AdamW on g = -d  (torch/optim/adam.py:347-551) */
     FEDAVG_EPI_ADAGRAD = 4,  /* torch Adagrad on g = -d  (torch/optim/adagrad.py _single_tensor_adagrad) */
     FEDAVG_EPI_RMSPROP = 5,  /* torch RMSprop on g = -d  (torch/optim/rmsprop.py _single_tensor_rmsprop) */
+    FEDAVG_EPI_ADAMAX = 6,   /* torch Adamax on g = -d  (torch/optim/adamax.py _single_tensor_adamax) */
 };
 
 typedef struct fedavg_epilogue {
@@ -86,7 +87,7 @@ typedef struct fedavg_epilogue {
     double step;                /* Adam: step count after this update (1, 2, ...) */
     float* param;               /* SGD/Adam: flat fp32 params, updated in place */
     float* state1;              /* SGD momentum buffer / Adam exp_avg (in place) */
-    float* state2;              /* Adam exp_avg_sq (in place) */
+    float* state2;              /* Adam exp_avg_sq / Adamax exp_inf (in place) */
     const float* base;          /* ADD_BASE: flat fp32 base weights (out may alias it) */
     int amsgrad;                /* Adam: normalise by max_exp_avg_sq = max(max_exp_avg_sq, exp_avg_sq) */
     float* state3;              /* Adam amsgrad: max_exp_avg_sq (in place) */

@@ -170,6 +170,7 @@ FEDAVG_EPI_SGD = 2
 FEDAVG_EPI_ADAM = 3
 FEDAVG_EPI_ADAGRAD = 4
 FEDAVG_EPI_RMSPROP = 5
+FEDAVG_EPI_ADAMAX = 6
 
 
 class Epilogue(ctypes.Structure):

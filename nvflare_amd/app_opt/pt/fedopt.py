@@ -8,12 +8,12 @@ representation (torch tensors if the global model holds tensors, numpy otherwise
 
 What differs is where the step runs.  The reference sets ``param.grad`` and calls
 ``optimizer.step()``; here the model's parameters are re-pointed into ONE flat fp32 buffer in HBM and
-``torch.optim.SGD`` / ``Adam`` / ``AdamW`` / ``Adagrad`` / ``RMSprop`` steps are executed by the HIP fused-epilogue kernel
+``torch.optim.SGD`` / ``Adam`` / ``AdamW`` / ``Adagrad`` / ``RMSprop`` / ``Adamax`` steps are executed by the HIP fused-epilogue kernel
 (``fedavg_accumulate_tiled_epi`` with the aggregated difference as ``acc_in``), with torch's
 single-tensor rounding sequence (``tests/test_fedopt_oracle.py``).  The torch optimizer object is kept
 for its ``param_groups`` (read every step, so lr schedulers work unchanged) and its ``state`` is filled
 with views of the device buffers (``momentum_buffer`` / ``exp_avg`` / ``exp_avg_sq`` / ``max_exp_avg_sq``
-with amsgrad / Adagrad's ``sum`` / ``step``), so ``optimizer.state_dict()`` checkpoints as before.  Other optimizers raise:
+with amsgrad / Adagrad's ``sum`` / Adamax's ``exp_inf`` / ``step``), so ``optimizer.state_dict()`` checkpoints as before.  Other optimizers raise:
 there is no CPU fallback.
 
 ``device`` names the HIP device ("cuda:N" or N); "cpu" (and None) select $NVFLARE_AMD_DEVICE / 0 --
@@ -110,9 +110,11 @@ class DeviceServerOptimizer:
             return N.FEDAVG_EPI_ADAGRAD
         if isinstance(optimizer, torch.optim.RMSprop):
             return N.FEDAVG_EPI_RMSPROP
+        if isinstance(optimizer, torch.optim.Adamax):
+            return N.FEDAVG_EPI_ADAMAX
         raise NotImplementedError(
             f"nvflare_amd: server optimizer {type(optimizer).__module__}.{type(optimizer).__name__} has no device "
-            "kernel (supported: torch.optim.SGD, Adam, AdamW, Adagrad, RMSprop)")
+            "kernel (supported: torch.optim.SGD, Adam, AdamW, Adagrad, RMSprop, Adamax)")
 
     def _group_of(self) -> Dict[int, dict]:
         return {id(p): g for g in self.optimizer.param_groups for p in g["params"]}
@@ -149,9 +151,10 @@ class DeviceServerOptimizer:
                 elif "momentum_buffer" in st and st["momentum_buffer"] is not None:
                     self.m[s.offset:s.offset + s.n].copy_(st["momentum_buffer"].reshape(-1).to(dev))
                     s.has_momentum_buffer = True
-                if "exp_avg" in st:
+                if "exp_avg" in st:  # Adam: exp_avg_sq, Adamax: exp_inf -> v
                     self.m[s.offset:s.offset + s.n].copy_(st["exp_avg"].reshape(-1).to(dev))
-                    self.v[s.offset:s.offset + s.n].copy_(st["exp_avg_sq"].reshape(-1).to(dev))
+                    second = st["exp_inf"] if self.kind == N.FEDAVG_EPI_ADAMAX else st["exp_avg_sq"]
+                    self.v[s.offset:s.offset + s.n].copy_(second.reshape(-1).to(dev))
                     s.step = float(st["step"])
                 if "sum" in st:  # Adagrad: state made at construction (initial_accumulator_value)
                     self.m[s.offset:s.offset + s.n].copy_(st["sum"].reshape(-1).to(dev))
@@ -196,6 +199,10 @@ class DeviceServerOptimizer:
                 st["momentum_buffer"] = self.v[s.offset:s.offset + s.n].view(s.param.shape)
             if g.get("centered"):
                 st["grad_avg"] = self._max_exp_avg_sq()[s.offset:s.offset + s.n].view(s.param.shape)
+        elif self.kind == N.FEDAVG_EPI_ADAMAX:
+            st["step"] = torch.tensor(s.step, dtype=torch.float32)
+            st["exp_avg"] = self.m[s.offset:s.offset + s.n].view(s.param.shape)
+            st["exp_inf"] = self.v[s.offset:s.offset + s.n].view(s.param.shape)
         else:
             st["step"] = torch.tensor(s.step, dtype=torch.float32)
             st["exp_avg"] = self.m[s.offset:s.offset + s.n].view(s.param.shape)
@@ -234,6 +241,11 @@ class DeviceServerOptimizer:
             if group.get("centered"):
                 e.centered = 1
                 e.state3 = self._max_exp_avg_sq().data_ptr()
+        elif self.kind == N.FEDAVG_EPI_ADAMAX:
+            b1, b2 = group["betas"]
+            e.beta1, e.beta2, e.eps = float(b1), float(b2), float(group["eps"])
+            e.state2 = self.v.data_ptr()
+            e.step = s.step + 1.0
         else:
             b1, b2 = group["betas"]
             e.beta1, e.beta2, e.eps = float(b1), float(b2), float(group["eps"])

@@ -1041,7 +1041,7 @@ int fedavg_accumulate_tiled_epi(fedavg_ctx* ctx, const void* const* bases, const
                 throw Error(g_last_error);
             return;
         }
-        if (epi->kind < FEDAVG_EPI_ADD_BASE || epi->kind > FEDAVG_EPI_RMSPROP) throw Error("bad epilogue kind");
+        if (epi->kind < FEDAVG_EPI_ADD_BASE || epi->kind > FEDAVG_EPI_ADAMAX) throw Error("bad epilogue kind");
         if (k_rows < 0 || (k_rows == 0 && !acc_in)) throw Error("k_rows == 0 requires acc_in");
         check_op_fin(op, fin);
         if (tile_elems != (size_t)fedavg::kDefaultTile)
@@ -1064,6 +1064,9 @@ int fedavg_accumulate_tiled_epi(fedavg_ctx* ctx, const void* const* bases, const
         if (epi->kind == FEDAVG_EPI_RMSPROP &&
             (!epi->param || !epi->state1 || (epi->momentum != 0.0 && !epi->state2) || (epi->centered && !epi->state3)))
             throw Error("RMSPROP needs param, state1 (square_avg), state2 with momentum, state3 when centered");
+        if (epi->kind == FEDAVG_EPI_ADAMAX && (!epi->param || !epi->state1 || !epi->state2))
+            throw Error("ADAMAX needs param, state1 (exp_avg), state2 (exp_inf)");
+        if (epi->kind == FEDAVG_EPI_ADAMAX && epi->step < 1.0) throw Error("ADAMAX step must be >= 1");
         for (const void* p : {(const void*)epi->param, (const void*)epi->state1, (const void*)epi->state2,
                               (const void*)epi->state3, (const void*)epi->base, (const void*)out, acc_in})
             if (misaligned(p)) throw Error("epilogue/out/acc_in pointers must be 16-byte aligned");

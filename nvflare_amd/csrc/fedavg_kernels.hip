@@ -161,6 +161,7 @@ __global__ void __launch_bounds__(kBlock) fedavg_tiles_f32x4(const RowTableF32 t
 //   EPI_ADD_BASE  w = base + d                          full_model_shareable_generator.py:58-67
 //   EPI_SGD       torch _single_tensor_sgd on g = -d     app_opt/pt/fedopt.py:157-182
 //   EPI_ADAM      torch _single_tensor_adam on g = -d    torch/optim/adam.py:347-551
+//   EPI_ADAGRAD / EPI_RMSPROP / EPI_ADAMAX   torch _single_tensor_{adagrad,rmsprop,adamax} on g = -d
 // Per parameter: 4K bytes of client reads + 12 B (p, m, v) read + 12 B written for Adam, so the
 // optimizer costs one pass instead of the reference's separate aggregate / H2D / step / D2H round trip.
 // Rounding sequence pinned against torch CPU by tests/test_fedopt_oracle.py (fma for add(alpha), lerp
@@ -200,6 +201,10 @@ __device__ __forceinline__ EpiIn epi_load(const EpiParams& E, const int64_t i) {
         in.b = load4<true>(reinterpret_cast<const f32x4*>(E.state1) + i);
         if (E.has_momentum) in.c = load4<true>(reinterpret_cast<const f32x4*>(E.state2) + i);
         if (E.centered) in.d = load4<true>(reinterpret_cast<const f32x4*>(E.state3) + i);
+    } else if constexpr (EPI == FEDAVG_EPI_ADAMAX) {
+        in.a = load4<true>(reinterpret_cast<const f32x4*>(E.param) + i);
+        in.b = load4<true>(reinterpret_cast<const f32x4*>(E.state1) + i);
+        in.c = load4<true>(reinterpret_cast<const f32x4*>(E.state2) + i);
     } else {
         in.a = load4<true>(reinterpret_cast<const f32x4*>(E.param) + i);
         in.b = load4<true>(reinterpret_cast<const f32x4*>(E.state1) + i);
@@ -273,6 +278,21 @@ __device__ __forceinline__ void epilogue4(const EpiParams& E, const int64_t i, c
         store4<true>(reinterpret_cast<f32x4*>(E.state1) + i, sq);
         if (E.has_momentum) store4<true>(reinterpret_cast<f32x4*>(E.state2) + i, buf);
         if (E.centered) store4<true>(reinterpret_cast<f32x4*>(E.state3) + i, ga);
+    } else if constexpr (EPI == FEDAVG_EPI_ADAMAX) {
+        f32x4 p = in.a;
+        f32x4 m = in.b;
+        f32x4 u = in.c;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            float g = E.maximize ? d[c] : -d[c];
+            if (E.has_weight_decay) g = __builtin_fmaf(p[c], E.weight_decay, g);     // grad.add(param, alpha=wd)
+            m[c] = lerp_torch(m[c], g, E.one_minus_beta1, E.one_minus_beta1_m1);      // exp_avg.lerp_(g, 1-beta1)
+            u[c] = max_torch(u[c] * E.beta2, fabsf(g) + E.eps);                      // maximum(exp_inf*b2, |g|+eps)
+            p[c] = p[c] + (E.step_size_neg * m[c]) / u[c];                            // addcdiv_(exp_avg, exp_inf, -clr)
+        }
+        store4<true>(p4, p);
+        store4<true>(reinterpret_cast<f32x4*>(E.state1) + i, m);
+        store4<true>(reinterpret_cast<f32x4*>(E.state2) + i, u);
     } else {  // EPI_ADAM
         f32x4 p = in.a;
         f32x4 m = in.b;
@@ -676,6 +696,10 @@ static hipError_t launch_epi_p(const TileLaunch& L, const EpiParams& E, hipStrea
             break;
         case FEDAVG_EPI_RMSPROP:
             hipLaunchKernelGGL((fedavg_tiles_epi_f32x4<OP, FIN, ACC_IN, FEDAVG_EPI_RMSPROP, PRE>), dim3(L.grid),
+                               dim3(kBlock), 0, s, L.tab, L.k, L.tstride4, ai, o, L.b4, L.e4, L.fin_val, E);
+            break;
+        case FEDAVG_EPI_ADAMAX:
+            hipLaunchKernelGGL((fedavg_tiles_epi_f32x4<OP, FIN, ACC_IN, FEDAVG_EPI_ADAMAX, PRE>), dim3(L.grid),
                                dim3(kBlock), 0, s, L.tab, L.k, L.tstride4, ai, o, L.b4, L.e4, L.fin_val, E);
             break;
         default:

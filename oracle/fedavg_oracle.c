@@ -117,6 +117,7 @@ void oracle_synth_fill_f32(uint64_t seed, uint64_t row, const uint64_t* cols, si
  *   SGD       torch/optim/sgd.py _single_tensor_sgd on grad g = -1.0 * d   (app_opt/pt/fedopt.py:175)
  *   ADAGRAD   torch/optim/adagrad.py _single_tensor_adagrad on g = -1.0 * d (m holds state_sum)
  *   RMSPROP   torch/optim/rmsprop.py _single_tensor_rmsprop (m square_avg, v momentum_buffer, vmax grad_avg)
+ *   ADAMAX    torch/optim/adamax.py _single_tensor_adamax on g = -1.0 * d (m exp_avg, v exp_inf)
  *   ADAM      torch/optim/adam.py _single_tensor_adam (:347-551) on g = -1.0 * d; amsgrad divides by
  *             sqrt(vmax), vmax = torch.maximum(vmax, v) kept as a third state
  * Rounding sequence pinned against torch 2.10 CPU (tests/test_fedopt_oracle.py):
@@ -128,7 +129,7 @@ void oracle_synth_fill_f32(uint64_t seed, uint64_t row, const uint64_t* cols, si
  * fp32 where they meet a tensor.
  * ------------------------------------------------------------------------------------------------ */
 enum { ORACLE_EPI_NONE = 0, ORACLE_EPI_ADD_BASE = 1, ORACLE_EPI_SGD = 2, ORACLE_EPI_ADAM = 3, ORACLE_EPI_ADAGRAD = 4,
-       ORACLE_EPI_RMSPROP = 5 };
+       ORACLE_EPI_RMSPROP = 5, ORACLE_EPI_ADAMAX = 6 };
 
 typedef struct {
     int kind;
@@ -202,6 +203,13 @@ void oracle_epilogue_apply(const float* delta, size_t n, const oracle_epilogue* 
             } else {
                 p[i] = p[i] + ((float)(-epi->lr) * g) / avg;          /* param.addcdiv_(g, avg, value=-lr) */
             }
+        } else if (epi->kind == ORACLE_EPI_ADAMAX) { /* torch/optim/adamax.py _single_tensor_adamax */
+            float g = epi->maximize ? d : -d;
+            if (epi->weight_decay != 0.0) g = fmaf(p[i], (float)epi->weight_decay, g); /* grad.add(param, alpha=wd) */
+            m[i] = lerp_torch(m[i], g, (float)(1.0 - epi->beta1));                    /* exp_avg.lerp_(g, 1 - beta1) */
+            v[i] = max_torch(v[i] * (float)epi->beta2, fabsf(g) + (float)epi->eps);    /* maximum(exp_inf.mul_(b2), |g|+eps) */
+            const float neg_clr = (float)(-(epi->lr / (1.0 - pow(epi->beta1, epi->step))));
+            p[i] = p[i] + (neg_clr * m[i]) / v[i];                                    /* addcdiv_(exp_avg, exp_inf, -clr) */
         } else { /* ADAM */
             float g = epi->maximize ? d : -d;
             float pv = p[i];

@@ -244,7 +244,7 @@ def synth_weights(K: int):
 # ---------------------------------------------------------------------------------------------------
 # server-optimizer epilogues (rows a9/a10): see oracle_epilogue_apply in fedavg_oracle.c
 # ---------------------------------------------------------------------------------------------------
-EPI_NONE, EPI_ADD_BASE, EPI_SGD, EPI_ADAM, EPI_ADAGRAD, EPI_RMSPROP = 0, 1, 2, 3, 4, 5
+EPI_NONE, EPI_ADD_BASE, EPI_SGD, EPI_ADAM, EPI_ADAGRAD, EPI_RMSPROP, EPI_ADAMAX = 0, 1, 2, 3, 4, 5, 6
 
 
 class _Epi(ctypes.Structure):

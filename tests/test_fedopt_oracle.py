@@ -183,3 +183,27 @@ def test_add_base_matches_numpy_generator(oracle):
     base = rng.standard_normal(10_001).astype(np.float32)
     d = rng.standard_normal(10_001).astype(np.float32)
     assert same_bits(oracle.epilogue_apply(d, oracle.EPI_ADD_BASE, base=base), base + d)
+
+
+@pytest.mark.parametrize("kw", [
+    dict(lr=2e-3),
+    dict(lr=1e-2, betas=(0.8, 0.95), eps=1e-6, weight_decay=1e-3),
+    dict(lr=1e-3, maximize=True),
+])
+def test_adamax_vs_torch(oracle, kw):
+    """torch/optim/adamax.py _single_tensor_adamax (no sqrt on the path): exp_avg, exp_inf and params
+    bit-exact against torch CPU."""
+    rng = np.random.default_rng(6)
+    n = 200_003
+    p0 = rng.standard_normal(n).astype(np.float32)
+    deltas = [(rng.standard_normal(n) * 0.01).astype(np.float32) for _ in range(5)]
+    tp, st = _torch_steps(torch.optim.Adamax, kw, p0, deltas)
+    p, m, u = p0.copy(), np.zeros(n, np.float32), np.zeros(n, np.float32)
+    b1, b2 = kw.get("betas", (0.9, 0.999))
+    for k, d in enumerate(deltas):
+        oracle.epilogue_apply(d, oracle.EPI_ADAMAX, p=p, m=m, v=u, lr=kw["lr"], beta1=b1, beta2=b2,
+                              eps=kw.get("eps", 1e-8), weight_decay=kw.get("weight_decay", 0.0),
+                              maximize=int(kw.get("maximize", False)), step=float(k + 1))
+    assert same_bits(m, st["exp_avg"].numpy()), "exp_avg"
+    assert same_bits(u, st["exp_inf"].numpy()), "exp_inf"
+    assert same_bits(p, tp), "param"

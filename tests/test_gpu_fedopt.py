@@ -322,6 +322,36 @@ def test_adagrad_epilogue(ctx, oracle, K, hp):
             dev.close()
 
 
+@pytest.mark.parametrize("K,hp", [(5, dict(lr=2e-3, beta1=0.9, beta2=0.999, eps=1e-8)),
+                                  (3, dict(lr=1e-2, beta1=0.8, beta2=0.95, eps=1e-6, weight_decay=1e-3, maximize=1)),
+                                  (0, dict(lr=1e-3, beta1=0.9, beta2=0.999, eps=1e-8))])
+def test_adamax_epilogue(ctx, oracle, K, hp):
+    """Adamax: exp_avg = lerp(m, g, 1-b1), exp_inf = maximum(u * b2, |g| + eps), p += (-clr * m) / u with
+    clr = lr / (1 - b1^step).  Three steps, bit-exact vs the oracle (itself bit-exact vs torch CPU,
+    tests/test_fedopt_oracle.py)."""
+    rng = np.random.default_rng(110 + K)
+    n = 3 * TILE + 36
+    p = rng.standard_normal(n).astype(np.float32)
+    m, u = np.zeros(n, np.float32), np.zeros(n, np.float32)
+    for step in range(3):
+        rows = [(rng.standard_normal(n) * 0.05).astype(np.float32) for _ in range(K)]
+        ws = [float(1 + (37 * k) % 100) for k in range(K)]
+        delta = (rng.standard_normal(n) * 0.05).astype(np.float32) if K == 0 else None
+        dev = _Dev(ctx, rows, n)
+        try:
+            e = _epi(6, param=dev.buf("p", p), state1=dev.buf("m", m), state2=dev.buf("u", u),
+                     step=float(step + 1), **hp)
+            acc_ptr = dev.buf("acc", delta) if K == 0 else None
+            ctx.accumulate_tiled_epi(dev.bases, ws, TILE, dev.lay.tile_stride, 0, dev.n4, None, 1,
+                                     2 if K else 0, _sum(ws) if K else 1.0, e, acc_in_ptr=acc_ptr)
+            d = oracle.fedavg_c(rows, ws, oracle.MODE_TORCH, nthreads=8) if K else delta
+            oracle.epilogue_apply(d, oracle.EPI_ADAMAX, p=p, m=m, v=u, step=float(step + 1), **hp)
+            assert same_bits(dev.get("p"), p) and same_bits(dev.get("m"), m), step
+            assert same_bits(dev.get("u"), u), step
+        finally:
+            dev.close()
+
+
 @pytest.mark.parametrize("K,hp", [(6, dict(lr=1e-2, alpha=0.99, eps=1e-8)),
                                   (3, dict(lr=1e-2, alpha=0.9, eps=1e-6, momentum=0.9, weight_decay=1e-3)),
                                   (2, dict(lr=1e-3, alpha=0.95, eps=1e-8, centered=1, momentum=0.5, maximize=1)),

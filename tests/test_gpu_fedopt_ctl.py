@@ -41,6 +41,7 @@ def _reference_update(model, opt, sched, global_params, diff):
     (torch.optim.AdamW, dict(lr=1e-2, weight_decay=0.1, amsgrad=True), None),
     (torch.optim.Adagrad, dict(lr=0.1, lr_decay=0.01, initial_accumulator_value=0.1), None),
     (torch.optim.RMSprop, dict(lr=1e-3, alpha=0.9, momentum=0.5, centered=True), None),
+    (torch.optim.Adamax, dict(lr=2e-3, weight_decay=1e-3), ("StepLR", dict(step_size=1, gamma=0.5))),
 ])
 def test_fedopt_controller_update_model(opt_cls, kw, sched):
     rng = np.random.default_rng(5)

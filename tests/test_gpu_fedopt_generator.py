@@ -99,16 +99,49 @@ def test_fedopt_generator_optimizer_state_views():
     assert len(sd["state"]) == len(list(model.parameters()))
 
 
+def test_fedopt_generator_adamax_state_matches_torch():
+    """Adamax (no sqrt on its path): params, exp_avg and exp_inf bit-exact against torch CPU stepping the same
+    -diff, over two rounds; optimizer.state holds views of the device buffers."""
+    import copy
+
+    model = fedopt_model()
+    ref_model = copy.deepcopy(model)
+    ref_opt = torch.optim.Adamax(ref_model.parameters(), lr=2e-3, weight_decay=1e-3, foreach=False)
+    gen = PTFedOptModelShareableGenerator(optimizer_args={"path": "torch.optim.Adamax",
+                                                          "args": {"lr": 2e-3, "weight_decay": 1e-3}},
+                                          source_model=model, device=0)
+    gen.handle_event(EventType.START_RUN, FLContext())
+    w = {k: v.detach().cpu().numpy().copy() for k, v in model.state_dict().items()}
+    rng = np.random.default_rng(12)
+    for rnd in range(2):
+        fl_ctx = FLContext()
+        fl_ctx.set_prop(AppConstants.GLOBAL_MODEL, make_model_learnable(w, {}))
+        diff = {k: (rng.standard_normal(v.shape) * 0.05).astype(np.float32) for k, v in w.items()
+                if v.dtype == np.float32}
+        w = gen.shareable_to_learnable(DXO(DataKind.WEIGHT_DIFF, data=diff).to_shareable(), fl_ctx)[
+            ModelLearnableKey.WEIGHTS]
+        ref_opt.zero_grad()
+        for n, p in ref_model.named_parameters():
+            p.grad = torch.tensor(-1.0 * diff[n])
+        ref_opt.step()
+    for (n, p), (_, rp) in zip(model.named_parameters(), ref_model.named_parameters()):
+        st, rst = gen.optimizer.state[p], ref_opt.state[rp]
+        assert st["exp_inf"].device.type == "cuda" and float(st["step"]) == 2.0
+        assert same_bits(_np(w[n]), rp.detach().numpy()), n
+        assert same_bits(st["exp_avg"].cpu().numpy(), rst["exp_avg"].numpy()), n
+        assert same_bits(st["exp_inf"].cpu().numpy(), rst["exp_inf"].numpy()), n
+
+
 def test_fedopt_generator_rejects_unsupported_optimizer():
     model = fedopt_model()
-    gen = PTFedOptModelShareableGenerator(optimizer_args={"path": "torch.optim.Adamax", "args": {"lr": 1e-3}},
+    gen = PTFedOptModelShareableGenerator(optimizer_args={"path": "torch.optim.NAdam", "args": {"lr": 1e-3}},
                                           source_model=model, device=0)
     gen.handle_event(EventType.START_RUN, FLContext())
     w = {k: v.detach().cpu().numpy().copy() for k, v in model.state_dict().items()}
     fl_ctx = FLContext()
     fl_ctx.set_prop(AppConstants.GLOBAL_MODEL, make_model_learnable(w, {}))
     diff = {"lin1.weight": np.zeros((64, 7), np.float32)}
-    with pytest.raises(NotImplementedError, match="Adamax"):
+    with pytest.raises(NotImplementedError, match="NAdam"):
         gen.shareable_to_learnable(DXO(DataKind.WEIGHT_DIFF, data=diff).to_shareable(), fl_ctx)
 
 
