@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define FEDAVG_ABI_VERSION 1
+#define FEDAVG_ABI_VERSION 2
 
 /* element types of client rows (in_dtype) and of the running sum / result (acc_dtype) */
 enum fedavg_dtype {
@@ -74,6 +74,8 @@ enum fedavg_epi {
     FEDAVG_EPI_ADAGRAD = 4,  /* torch Adagrad on g = -d  (torch/optim/adagrad.py _single_tensor_adagrad) */
     FEDAVG_EPI_RMSPROP = 5,  /* torch RMSprop on g = -d  (torch/optim/rmsprop.py _single_tensor_rmsprop) */
     FEDAVG_EPI_ADAMAX = 6,   /* torch Adamax on g = -d  (torch/optim/adamax.py _single_tensor_adamax) */
+    FEDAVG_EPI_NADAM = 7,    /* torch NAdam on g = -d  (torch/optim/nadam.py _single_tensor_nadam) */
+    FEDAVG_EPI_RADAM = 8,    /* torch RAdam on g = -d  (torch/optim/radam.py _single_tensor_radam) */
 };
 
 typedef struct fedavg_epilogue {
@@ -94,6 +96,8 @@ typedef struct fedavg_epilogue {
     double lr_decay;            /* Adagrad: clr = lr / (1 + (step - 1) * lr_decay); state1 = sum, eps */
     double alpha;               /* RMSprop: smoothing constant; state1 = square_avg, state2 = momentum_buffer */
     int centered;               /* RMSprop: state3 = grad_avg */
+    double momentum_decay;      /* NAdam: mu_t = beta1 * (1 - 0.5 * 0.96^(step * momentum_decay)) */
+    double mu_product;          /* NAdam: the fp32 mu_product state BEFORE this step (1.0 at the first) */
 } fedavg_epilogue;
 
 /* Quantized payload formats (nvflare/app_opt/pt/quantization/dequantizer.py:47-185, row f4). */

@@ -41,7 +41,7 @@ FEDAVG_FIN_NONE = 0
 FEDAVG_FIN_SCALE = 1
 FEDAVG_FIN_DIV = 2
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 c_void_p = ctypes.c_void_p
 c_int = ctypes.c_int
@@ -171,6 +171,8 @@ FEDAVG_EPI_ADAM = 3
 FEDAVG_EPI_ADAGRAD = 4
 FEDAVG_EPI_RMSPROP = 5
 FEDAVG_EPI_ADAMAX = 6
+FEDAVG_EPI_NADAM = 7
+FEDAVG_EPI_RADAM = 8
 
 
 class Epilogue(ctypes.Structure):
@@ -199,6 +201,8 @@ class Epilogue(ctypes.Structure):
         ("lr_decay", c_double),
         ("alpha", c_double),
         ("centered", c_int),
+        ("momentum_decay", c_double),
+        ("mu_product", c_double),
     ]
 
 

@@ -8,7 +8,7 @@ representation (torch tensors if the global model holds tensors, numpy otherwise
 
 What differs is where the step runs.  The reference sets ``param.grad`` and calls
 ``optimizer.step()``; here the model's parameters are re-pointed into ONE flat fp32 buffer in HBM and
-``torch.optim.SGD`` / ``Adam`` / ``AdamW`` / ``Adagrad`` / ``RMSprop`` / ``Adamax`` steps are executed by the HIP fused-epilogue kernel
+``torch.optim.SGD`` / ``Adam`` / ``AdamW`` / ``Adagrad`` / ``RMSprop`` / ``Adamax`` / ``NAdam`` / ``RAdam`` steps are executed by the HIP fused-epilogue kernel
 (``fedavg_accumulate_tiled_epi`` with the aggregated difference as ``acc_in``), with torch's
 single-tensor rounding sequence (``tests/test_fedopt_oracle.py``).  The torch optimizer object is kept
 for its ``param_groups`` (read every step, so lr schedulers work unchanged) and its ``state`` is filled
@@ -75,12 +75,13 @@ def build_component_from_args(args: dict):
 
 
 class _Slot:
-    __slots__ = ("name", "param", "offset", "n", "step", "has_momentum_buffer")
+    __slots__ = ("name", "param", "offset", "n", "step", "has_momentum_buffer", "mu_product")
 
     def __init__(self, name, param, offset, n):
         self.name, self.param, self.offset, self.n = name, param, offset, n
         self.step = 0.0
         self.has_momentum_buffer = False
+        self.mu_product = np.float32(1.0)  # NAdam's fp32 state tensor, kept on the host
 
 
 class DeviceServerOptimizer:
@@ -112,9 +113,13 @@ class DeviceServerOptimizer:
             return N.FEDAVG_EPI_RMSPROP
         if isinstance(optimizer, torch.optim.Adamax):
             return N.FEDAVG_EPI_ADAMAX
+        if isinstance(optimizer, torch.optim.NAdam):
+            return N.FEDAVG_EPI_NADAM
+        if isinstance(optimizer, torch.optim.RAdam):
+            return N.FEDAVG_EPI_RADAM
         raise NotImplementedError(
             f"nvflare_amd: server optimizer {type(optimizer).__module__}.{type(optimizer).__name__} has no device "
-            "kernel (supported: torch.optim.SGD, Adam, AdamW, Adagrad, RMSprop, Adamax)")
+            "kernel (supported: torch.optim.SGD, Adam, AdamW, Adagrad, RMSprop, Adamax, NAdam, RAdam)")
 
     def _group_of(self) -> Dict[int, dict]:
         return {id(p): g for g in self.optimizer.param_groups for p in g["params"]}
@@ -156,6 +161,8 @@ class DeviceServerOptimizer:
                     second = st["exp_inf"] if self.kind == N.FEDAVG_EPI_ADAMAX else st["exp_avg_sq"]
                     self.v[s.offset:s.offset + s.n].copy_(second.reshape(-1).to(dev))
                     s.step = float(st["step"])
+                if "mu_product" in st:  # NAdam
+                    s.mu_product = np.float32(float(st["mu_product"]))
                 if "sum" in st:  # Adagrad: state made at construction (initial_accumulator_value)
                     self.m[s.offset:s.offset + s.n].copy_(st["sum"].reshape(-1).to(dev))
                     s.step = float(st["step"])
@@ -207,6 +214,8 @@ class DeviceServerOptimizer:
             st["step"] = torch.tensor(s.step, dtype=torch.float32)
             st["exp_avg"] = self.m[s.offset:s.offset + s.n].view(s.param.shape)
             st["exp_avg_sq"] = self.v[s.offset:s.offset + s.n].view(s.param.shape)
+            if self.kind == N.FEDAVG_EPI_NADAM:
+                st["mu_product"] = torch.tensor(s.mu_product, dtype=torch.float32)
             if self._group_of()[id(s.param)].get("amsgrad"):
                 st["max_exp_avg_sq"] = self._max_exp_avg_sq()[s.offset:s.offset + s.n].view(s.param.shape)
 
@@ -252,6 +261,9 @@ class DeviceServerOptimizer:
             e.decoupled_weight_decay = int(bool(group.get("decoupled_weight_decay", False)))
             e.state2 = self.v.data_ptr()
             e.step = s.step + 1.0
+            if self.kind == N.FEDAVG_EPI_NADAM:
+                e.momentum_decay = float(group["momentum_decay"])
+                e.mu_product = float(s.mu_product)
             if group.get("amsgrad"):
                 e.amsgrad = 1
                 e.state3 = self._max_exp_avg_sq().data_ptr()
@@ -297,7 +309,7 @@ class DeviceServerOptimizer:
         runs: List[Tuple[tuple, List[_Slot]]] = []
         for s in present:
             g = groups[id(s.param)]
-            key = (id(g), s.step, s.has_momentum_buffer)
+            key = (id(g), s.step, s.has_momentum_buffer, float(s.mu_product))
             prev = runs[-1][1][-1] if runs else None
             contiguous = prev is not None and self.slots.index(s) == self.slots.index(prev) + 1
             if runs and runs[-1][0] == key and contiguous:
@@ -319,6 +331,10 @@ class DeviceServerOptimizer:
     def _advance(self, stepped: List[_Slot], groups: Dict[int, dict]) -> None:
         for s in stepped:
             s.step += 1.0
+            if self.kind == N.FEDAVG_EPI_NADAM:  # nadam.py: mu_product *= mu on an fp32 tensor
+                g = groups[id(s.param)]
+                mu = g["betas"][0] * (1.0 - 0.5 * (0.96 ** (s.step * g["momentum_decay"])))
+                s.mu_product = np.float32(np.float32(s.mu_product) * np.float32(mu))
             if self.kind == N.FEDAVG_EPI_SGD and groups[id(s.param)].get("momentum", 0.0) != 0.0:
                 s.has_momentum_buffer = True
             self._expose_state(s)
@@ -348,7 +364,8 @@ class DeviceServerOptimizer:
             entries = {}
             for key, s in by_key.items():
                 g = groups[id(s.param)]
-                entries[key] = FusedEntry(s.offset, self._epilogue(g, s), (id(g), s.step, s.has_momentum_buffer))
+                entries[key] = FusedEntry(s.offset, self._epilogue(g, s), (id(g), s.step, s.has_momentum_buffer,
+                                                                          float(s.mu_product)))
             names = set(rnd.fused_step(entries, egress_marks=egress))
             stepped = [s for key, s in by_key.items() if key in names]
             with self.ctx.lock:

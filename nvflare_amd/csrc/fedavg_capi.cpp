@@ -416,6 +416,23 @@ fedavg::EpiParams make_epi(const fedavg_epilogue& e) {
         E.one_minus_beta1_m1 = E.one_minus_beta1 - 1.0f;
         E.centered = e.centered != 0;
     }
+    if (e.kind == FEDAVG_EPI_NADAM) {  // nadam.py _single_tensor_nadam (python floats; mu_product is an fp32 tensor)
+        const double mu = e.beta1 * (1.0 - 0.5 * std::pow(0.96, e.step * e.momentum_decay));
+        const double mu_next = e.beta1 * (1.0 - 0.5 * std::pow(0.96, (e.step + 1.0) * e.momentum_decay));
+        const float mp = (float)e.mu_product * (float)mu;  // mu_product *= mu
+        E.bias_correction2 = (float)bc2;
+        E.coef_grad = (float)((-e.lr * (1.0 - mu)) / (1.0 - (double)mp));
+        E.coef_avg = (float)((-e.lr * mu_next) / (1.0 - (double)mp * mu_next));
+    }
+    if (e.kind == FEDAVG_EPI_RADAM) {  // radam.py _single_tensor_radam
+        const double rho_inf = 2.0 / (1.0 - e.beta2) - 1.0;
+        const double rho_t = rho_inf - 2.0 * e.step * std::pow(e.beta2, e.step) / bc2;
+        E.bias_correction1 = (float)bc1;
+        E.lr = (float)e.lr;
+        E.rectified = rho_t > 5.0;
+        if (E.rectified)
+            E.rect = (float)std::pow((rho_t - 4.0) * (rho_t - 2.0) * rho_inf / ((rho_inf - 4.0) * (rho_inf - 2.0) * rho_t), 0.5);
+    }
     return E;
 }
 
@@ -1041,7 +1058,7 @@ int fedavg_accumulate_tiled_epi(fedavg_ctx* ctx, const void* const* bases, const
                 throw Error(g_last_error);
             return;
         }
-        if (epi->kind < FEDAVG_EPI_ADD_BASE || epi->kind > FEDAVG_EPI_ADAMAX) throw Error("bad epilogue kind");
+        if (epi->kind < FEDAVG_EPI_ADD_BASE || epi->kind > FEDAVG_EPI_RADAM) throw Error("bad epilogue kind");
         if (k_rows < 0 || (k_rows == 0 && !acc_in)) throw Error("k_rows == 0 requires acc_in");
         check_op_fin(op, fin);
         if (tile_elems != (size_t)fedavg::kDefaultTile)
@@ -1067,6 +1084,9 @@ int fedavg_accumulate_tiled_epi(fedavg_ctx* ctx, const void* const* bases, const
         if (epi->kind == FEDAVG_EPI_ADAMAX && (!epi->param || !epi->state1 || !epi->state2))
             throw Error("ADAMAX needs param, state1 (exp_avg), state2 (exp_inf)");
         if (epi->kind == FEDAVG_EPI_ADAMAX && epi->step < 1.0) throw Error("ADAMAX step must be >= 1");
+        if ((epi->kind == FEDAVG_EPI_NADAM || epi->kind == FEDAVG_EPI_RADAM) &&
+            (!epi->param || !epi->state1 || !epi->state2 || epi->step < 1.0))
+            throw Error("NADAM/RADAM need param, state1 (exp_avg), state2 (exp_avg_sq) and step >= 1");
         for (const void* p : {(const void*)epi->param, (const void*)epi->state1, (const void*)epi->state2,
                               (const void*)epi->state3, (const void*)epi->base, (const void*)out, acc_in})
             if (misaligned(p)) throw Error("epilogue/out/acc_in pointers must be 16-byte aligned");

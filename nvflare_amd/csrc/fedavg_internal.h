@@ -72,6 +72,9 @@ struct EpiParams {
     int amsgrad;
     float* state3;  // Adam amsgrad: max_exp_avg_sq | RMSprop centered: grad_avg
     int centered;   // RMSprop (alpha in beta2 / one_minus_beta2 / one_minus_beta1)
+    float bias_correction2, coef_grad, coef_avg;  // NAdam: the two addcdiv values
+    float bias_correction1, lr, rect;             // RAdam
+    int rectified;                                // RAdam: rho_t > 5
 };
 
 struct DequantLaunch {

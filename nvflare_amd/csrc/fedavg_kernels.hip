@@ -161,7 +161,7 @@ __global__ void __launch_bounds__(kBlock) fedavg_tiles_f32x4(const RowTableF32 t
 //   EPI_ADD_BASE  w = base + d                          full_model_shareable_generator.py:58-67
 //   EPI_SGD       torch _single_tensor_sgd on g = -d     app_opt/pt/fedopt.py:157-182
 //   EPI_ADAM      torch _single_tensor_adam on g = -d    torch/optim/adam.py:347-551
-//   EPI_ADAGRAD / EPI_RMSPROP / EPI_ADAMAX   torch _single_tensor_{adagrad,rmsprop,adamax} on g = -d
+//   EPI_ADAGRAD / RMSPROP / ADAMAX / NADAM / RADAM   torch _single_tensor_{adagrad,rmsprop,adamax,nadam,radam}
 // Per parameter: 4K bytes of client reads + 12 B (p, m, v) read + 12 B written for Adam, so the
 // optimizer costs one pass instead of the reference's separate aggregate / H2D / step / D2H round trip.
 // Rounding sequence pinned against torch CPU by tests/test_fedopt_oracle.py (fma for add(alpha), lerp
@@ -293,6 +293,37 @@ __device__ __forceinline__ void epilogue4(const EpiParams& E, const int64_t i, c
         store4<true>(p4, p);
         store4<true>(reinterpret_cast<f32x4*>(E.state1) + i, m);
         store4<true>(reinterpret_cast<f32x4*>(E.state2) + i, u);
+    } else if constexpr (EPI == FEDAVG_EPI_NADAM || EPI == FEDAVG_EPI_RADAM) {
+        f32x4 p = in.a;
+        f32x4 m = in.b;
+        f32x4 v = in.c;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            float g = E.maximize ? d[c] : -d[c];
+            float pv = p[c];
+            if (E.has_weight_decay) {
+                if (E.decoupled_weight_decay) pv = pv * E.decoupled_scale;  // param.mul_(1 - lr * wd)
+                else g = __builtin_fmaf(pv, E.weight_decay, g);              // grad.add(param, alpha=wd)
+            }
+            m[c] = lerp_torch(m[c], g, E.one_minus_beta1, E.one_minus_beta1_m1);
+            v[c] = __builtin_fmaf(E.one_minus_beta2 * g, g, v[c] * E.beta2);
+            if constexpr (EPI == FEDAVG_EPI_NADAM) {
+                const float denom = __builtin_sqrtf(v[c] / E.bias_correction2) + E.eps;  // exp_avg_sq.div(bc2).sqrt().add_(eps)
+                pv = pv + (E.coef_grad * g) / denom;                                    // addcdiv_(grad, denom, value)
+                pv = pv + (E.coef_avg * m[c]) / denom;                                  // addcdiv_(exp_avg, denom, value)
+            } else {
+                float t = (m[c] / E.bias_correction1) * E.lr;                           // exp_avg / bc1 * lr
+                if (E.rectified) {
+                    const float a = (1.0f / (__builtin_sqrtf(v[c]) + E.eps)) * E.bias_correction2_sqrt;  // bc2**0.5 / (sqrt+eps)
+                    t = (t * a) * E.rect;
+                }
+                pv = __builtin_fmaf(t, -1.0f, pv);                                      // param.add_(..., alpha=-1)
+            }
+            p[c] = pv;
+        }
+        store4<true>(p4, p);
+        store4<true>(reinterpret_cast<f32x4*>(E.state1) + i, m);
+        store4<true>(reinterpret_cast<f32x4*>(E.state2) + i, v);
     } else {  // EPI_ADAM
         f32x4 p = in.a;
         f32x4 m = in.b;
@@ -700,6 +731,14 @@ static hipError_t launch_epi_p(const TileLaunch& L, const EpiParams& E, hipStrea
             break;
         case FEDAVG_EPI_ADAMAX:
             hipLaunchKernelGGL((fedavg_tiles_epi_f32x4<OP, FIN, ACC_IN, FEDAVG_EPI_ADAMAX, PRE>), dim3(L.grid),
+                               dim3(kBlock), 0, s, L.tab, L.k, L.tstride4, ai, o, L.b4, L.e4, L.fin_val, E);
+            break;
+        case FEDAVG_EPI_NADAM:
+            hipLaunchKernelGGL((fedavg_tiles_epi_f32x4<OP, FIN, ACC_IN, FEDAVG_EPI_NADAM, PRE>), dim3(L.grid),
+                               dim3(kBlock), 0, s, L.tab, L.k, L.tstride4, ai, o, L.b4, L.e4, L.fin_val, E);
+            break;
+        case FEDAVG_EPI_RADAM:
+            hipLaunchKernelGGL((fedavg_tiles_epi_f32x4<OP, FIN, ACC_IN, FEDAVG_EPI_RADAM, PRE>), dim3(L.grid),
                                dim3(kBlock), 0, s, L.tab, L.k, L.tstride4, ai, o, L.b4, L.e4, L.fin_val, E);
             break;
         default:

@@ -118,6 +118,8 @@ void oracle_synth_fill_f32(uint64_t seed, uint64_t row, const uint64_t* cols, si
  *   ADAGRAD   torch/optim/adagrad.py _single_tensor_adagrad on g = -1.0 * d (m holds state_sum)
  *   RMSPROP   torch/optim/rmsprop.py _single_tensor_rmsprop (m square_avg, v momentum_buffer, vmax grad_avg)
  *   ADAMAX    torch/optim/adamax.py _single_tensor_adamax on g = -1.0 * d (m exp_avg, v exp_inf)
+ *   NADAM     torch/optim/nadam.py _single_tensor_nadam (m exp_avg, v exp_avg_sq; mu_product passed in)
+ *   RADAM     torch/optim/radam.py _single_tensor_radam (m exp_avg, v exp_avg_sq)
  *   ADAM      torch/optim/adam.py _single_tensor_adam (:347-551) on g = -1.0 * d; amsgrad divides by
  *             sqrt(vmax), vmax = torch.maximum(vmax, v) kept as a third state
  * Rounding sequence pinned against torch 2.10 CPU (tests/test_fedopt_oracle.py):
@@ -129,7 +131,7 @@ void oracle_synth_fill_f32(uint64_t seed, uint64_t row, const uint64_t* cols, si
  * fp32 where they meet a tensor.
  * ------------------------------------------------------------------------------------------------ */
 enum { ORACLE_EPI_NONE = 0, ORACLE_EPI_ADD_BASE = 1, ORACLE_EPI_SGD = 2, ORACLE_EPI_ADAM = 3, ORACLE_EPI_ADAGRAD = 4,
-       ORACLE_EPI_RMSPROP = 5, ORACLE_EPI_ADAMAX = 6 };
+       ORACLE_EPI_RMSPROP = 5, ORACLE_EPI_ADAMAX = 6, ORACLE_EPI_NADAM = 7, ORACLE_EPI_RADAM = 8 };
 
 typedef struct {
     int kind;
@@ -143,6 +145,8 @@ typedef struct {
     double lr_decay;                              /* Adagrad: clr = lr / (1 + (step - 1) * lr_decay) */
     double alpha;                                 /* RMSprop smoothing constant */
     int centered;                                 /* RMSprop: vmax holds grad_avg */
+    double momentum_decay;                        /* NAdam */
+    double mu_product;                            /* NAdam: fp32 mu_product state before this step */
 } oracle_epilogue;
 
 /* torch.maximum: a NaN operand is the result */
@@ -210,6 +214,39 @@ void oracle_epilogue_apply(const float* delta, size_t n, const oracle_epilogue* 
             v[i] = max_torch(v[i] * (float)epi->beta2, fabsf(g) + (float)epi->eps);    /* maximum(exp_inf.mul_(b2), |g|+eps) */
             const float neg_clr = (float)(-(epi->lr / (1.0 - pow(epi->beta1, epi->step))));
             p[i] = p[i] + (neg_clr * m[i]) / v[i];                                    /* addcdiv_(exp_avg, exp_inf, -clr) */
+        } else if (epi->kind == ORACLE_EPI_NADAM || epi->kind == ORACLE_EPI_RADAM) {
+            float g = epi->maximize ? d : -d;
+            float pv = p[i];
+            if (epi->weight_decay != 0.0) {
+                if (epi->decoupled_weight_decay) pv = pv * (float)(1.0 - epi->lr * epi->weight_decay);
+                else g = fmaf(pv, (float)epi->weight_decay, g);
+            }
+            m[i] = lerp_torch(m[i], g, (float)(1.0 - epi->beta1));
+            v[i] = fmaf((float)(1.0 - epi->beta2) * g, g, v[i] * (float)epi->beta2);
+            const double bc1 = 1.0 - pow(epi->beta1, epi->step);
+            const double bc2 = 1.0 - pow(epi->beta2, epi->step);
+            if (epi->kind == ORACLE_EPI_NADAM) { /* nadam.py: two addcdiv_ on denom = sqrt(v / bc2) + eps */
+                const double mu = epi->beta1 * (1.0 - 0.5 * pow(0.96, epi->step * epi->momentum_decay));
+                const double mu_next = epi->beta1 * (1.0 - 0.5 * pow(0.96, (epi->step + 1.0) * epi->momentum_decay));
+                const float mp = (float)epi->mu_product * (float)mu;          /* mu_product *= mu (fp32 tensor) */
+                const float c_grad = (float)((-epi->lr * (1.0 - mu)) / (1.0 - (double)mp));
+                const float c_avg = (float)((-epi->lr * mu_next) / (1.0 - (double)mp * mu_next));
+                const float denom = sqrtf(v[i] / (float)bc2) + (float)epi->eps;
+                pv = pv + (c_grad * g) / denom;
+                pv = pv + (c_avg * m[i]) / denom;
+            } else { /* radam.py: rectified when rho_t > 5 */
+                const double rho_inf = 2.0 / (1.0 - epi->beta2) - 1.0;
+                const double rho_t = rho_inf - 2.0 * epi->step * pow(epi->beta2, epi->step) / bc2;
+                float t = (m[i] / (float)bc1) * (float)epi->lr;                /* exp_avg / bc1 * lr */
+                if (rho_t > 5.0) {
+                    const float rect = (float)pow((rho_t - 4.0) * (rho_t - 2.0) * rho_inf /
+                                                  ((rho_inf - 4.0) * (rho_inf - 2.0) * rho_t), 0.5);
+                    const float a = (1.0f / (sqrtf(v[i]) + (float)epi->eps)) * (float)pow(bc2, 0.5); /* bc2**.5 / x */
+                    t = (t * a) * rect;
+                }
+                pv = pv - t;                                                   /* param.add_(t, alpha=-1) */
+            }
+            p[i] = pv;
         } else { /* ADAM */
             float g = epi->maximize ? d : -d;
             float pv = p[i];

@@ -244,7 +244,7 @@ def synth_weights(K: int):
 # ---------------------------------------------------------------------------------------------------
 # server-optimizer epilogues (rows a9/a10): see oracle_epilogue_apply in fedavg_oracle.c
 # ---------------------------------------------------------------------------------------------------
-EPI_NONE, EPI_ADD_BASE, EPI_SGD, EPI_ADAM, EPI_ADAGRAD, EPI_RMSPROP, EPI_ADAMAX = 0, 1, 2, 3, 4, 5, 6
+EPI_NONE, EPI_ADD_BASE, EPI_SGD, EPI_ADAM, EPI_ADAGRAD, EPI_RMSPROP, EPI_ADAMAX, EPI_NADAM, EPI_RADAM = range(9)
 
 
 class _Epi(ctypes.Structure):
@@ -266,6 +266,8 @@ class _Epi(ctypes.Structure):
         ("lr_decay", ctypes.c_double),
         ("alpha", ctypes.c_double),
         ("centered", ctypes.c_int),
+        ("momentum_decay", ctypes.c_double),
+        ("mu_product", ctypes.c_double),
     ]
 
 

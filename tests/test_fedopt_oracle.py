@@ -207,3 +207,53 @@ def test_adamax_vs_torch(oracle, kw):
     assert same_bits(m, st["exp_avg"].numpy()), "exp_avg"
     assert same_bits(u, st["exp_inf"].numpy()), "exp_inf"
     assert same_bits(p, tp), "param"
+
+
+def nadam_mu_product(mu_product, beta1, momentum_decay, step):
+    """torch/optim/nadam.py: ``mu_product *= mu`` on the fp32 state tensor (what DeviceServerOptimizer keeps)."""
+    mu = beta1 * (1.0 - 0.5 * (0.96 ** (step * momentum_decay)))
+    return np.float32(np.float32(mu_product) * np.float32(mu))
+
+
+@pytest.mark.parametrize("opt_name,kw", [
+    ("NAdam", dict(lr=2e-3)),
+    ("NAdam", dict(lr=1e-2, betas=(0.8, 0.95), weight_decay=1e-3, momentum_decay=5e-3)),
+    ("NAdam", dict(lr=1e-3, weight_decay=1e-2, decoupled_weight_decay=True, maximize=True)),
+    ("RAdam", dict(lr=1e-3)),
+    ("RAdam", dict(lr=1e-2, betas=(0.8, 0.9), weight_decay=1e-3)),
+    ("RAdam", dict(lr=1e-3, weight_decay=1e-2, decoupled_weight_decay=True, maximize=True)),
+])
+def test_nadam_radam_vs_torch(oracle, opt_name, kw):
+    """torch/optim/nadam.py and radam.py single-tensor steps: exp_avg / exp_avg_sq bit-exact (without weight
+    decay feeding p back), NAdam's fp32 mu_product bit-exact, params within the Adam sqrt bound.  Eight steps,
+    so RAdam crosses from the unrectified (rho_t <= 5) to the rectified branch with betas (0.9, 0.999)."""
+    rng = np.random.default_rng(8)
+    n = 200_003
+    p0 = rng.standard_normal(n).astype(np.float32)
+    deltas = [(rng.standard_normal(n) * 0.01).astype(np.float32) for _ in range(8)]
+    tp, st = _torch_steps(getattr(torch.optim, opt_name), kw, p0, deltas)
+    p, m, v = p0.copy(), np.zeros(n, np.float32), np.zeros(n, np.float32)
+    b1, b2 = kw.get("betas", (0.9, 0.999))
+    md = kw.get("momentum_decay", 4e-3)
+    mp = np.float32(1.0)
+    kind = oracle.EPI_NADAM if opt_name == "NAdam" else oracle.EPI_RADAM
+    for k, d in enumerate(deltas):
+        oracle.epilogue_apply(d, kind, p=p, m=m, v=v, lr=kw["lr"], beta1=b1, beta2=b2, eps=kw.get("eps", 1e-8),
+                              weight_decay=kw.get("weight_decay", 0.0), maximize=int(kw.get("maximize", False)),
+                              decoupled_weight_decay=int(kw.get("decoupled_weight_decay", False)),
+                              momentum_decay=md, mu_product=float(mp), step=float(k + 1))
+        mp = nadam_mu_product(mp, b1, md, k + 1)
+    if opt_name == "NAdam":
+        assert same_bits(np.array(mp), st["mu_product"].numpy()), "mu_product"
+    steps = len(deltas)
+    for ours, key in ((m, "exp_avg"), (v, "exp_avg_sq")):
+        ref = st[key].numpy()
+        if kw.get("weight_decay") and not kw.get("decoupled_weight_decay"):
+            scale = np.maximum(np.abs(ref), np.float32(kw["weight_decay"]) * np.abs(p0))
+            assert np.all(np.abs(ours.astype(np.float64) - ref) <= steps * np.spacing(scale)), key
+        else:
+            assert same_bits(ours, ref), key
+    tol = 2 * steps * np.spacing(np.maximum(np.maximum(np.abs(p0), np.abs(tp)), np.float32(kw["lr"]))).astype(np.float64)
+    diff = np.abs(p.astype(np.float64) - tp.astype(np.float64))
+    assert np.all(diff <= tol), float((diff / tol).max())
+    assert float((diff > 0).mean()) < 0.02

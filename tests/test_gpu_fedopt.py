@@ -352,6 +352,46 @@ def test_adamax_epilogue(ctx, oracle, K, hp):
             dev.close()
 
 
+@pytest.mark.parametrize("kind,K,hp", [
+    (7, 5, dict(lr=2e-3, beta1=0.9, beta2=0.999, eps=1e-8, momentum_decay=4e-3)),
+    (7, 3, dict(lr=1e-2, beta1=0.8, beta2=0.95, eps=1e-6, weight_decay=1e-3, momentum_decay=5e-3, maximize=1)),
+    (7, 0, dict(lr=1e-3, beta1=0.9, beta2=0.999, eps=1e-8, weight_decay=1e-2, decoupled_weight_decay=1,
+                momentum_decay=4e-3)),
+    (8, 5, dict(lr=1e-3, beta1=0.9, beta2=0.999, eps=1e-8)),
+    (8, 2, dict(lr=1e-2, beta1=0.8, beta2=0.9, eps=1e-8, weight_decay=1e-3, maximize=1)),
+    (8, 0, dict(lr=1e-3, beta1=0.9, beta2=0.99, eps=1e-8, weight_decay=1e-2, decoupled_weight_decay=1)),
+])
+def test_nadam_radam_epilogue(ctx, oracle, kind, K, hp):
+    """NAdam (kind 7): denom = sqrt(v / bc2) + eps, two addcdiv_ with the mu / mu_product values; RAdam (kind 8):
+    t = exp_avg / bc1 * lr, rectified by (bc2^.5 / (sqrt(v) + eps)) * rect once rho_t > 5.  Seven steps (RAdam
+    crosses into the rectified branch), bit-exact vs the oracle (pinned to torch CPU in test_fedopt_oracle)."""
+    from test_fedopt_oracle import nadam_mu_product
+
+    rng = np.random.default_rng(130 + 10 * kind + K)
+    n = 2 * TILE + 44
+    p = rng.standard_normal(n).astype(np.float32)
+    m, v = np.zeros(n, np.float32), np.zeros(n, np.float32)
+    mp = np.float32(1.0)
+    for step in range(7):
+        rows = [(rng.standard_normal(n) * 0.05).astype(np.float32) for _ in range(K)]
+        ws = [float(1 + (37 * k) % 100) for k in range(K)]
+        delta = (rng.standard_normal(n) * 0.05).astype(np.float32) if K == 0 else None
+        dev = _Dev(ctx, rows, n)
+        try:
+            e = _epi(kind, param=dev.buf("p", p), state1=dev.buf("m", m), state2=dev.buf("v", v),
+                     step=float(step + 1), mu_product=float(mp), **hp)
+            acc_ptr = dev.buf("acc", delta) if K == 0 else None
+            ctx.accumulate_tiled_epi(dev.bases, ws, TILE, dev.lay.tile_stride, 0, dev.n4, None, 1,
+                                     2 if K else 0, _sum(ws) if K else 1.0, e, acc_in_ptr=acc_ptr)
+            d = oracle.fedavg_c(rows, ws, oracle.MODE_TORCH, nthreads=8) if K else delta
+            oracle.epilogue_apply(d, kind, p=p, m=m, v=v, step=float(step + 1), mu_product=float(mp), **hp)
+            assert same_bits(dev.get("p"), p) and same_bits(dev.get("m"), m), step
+            assert same_bits(dev.get("v"), v), step
+        finally:
+            dev.close()
+        mp = nadam_mu_product(mp, hp["beta1"], hp.get("momentum_decay", 4e-3), step + 1)
+
+
 @pytest.mark.parametrize("K,hp", [(6, dict(lr=1e-2, alpha=0.99, eps=1e-8)),
                                   (3, dict(lr=1e-2, alpha=0.9, eps=1e-6, momentum=0.9, weight_decay=1e-3)),
                                   (2, dict(lr=1e-3, alpha=0.95, eps=1e-8, centered=1, momentum=0.5, maximize=1)),

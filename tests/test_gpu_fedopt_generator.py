@@ -132,16 +132,55 @@ def test_fedopt_generator_adamax_state_matches_torch():
         assert same_bits(st["exp_inf"].cpu().numpy(), rst["exp_inf"].numpy()), n
 
 
+@pytest.mark.parametrize("opt_name", ["NAdam", "RAdam"])
+def test_fedopt_generator_nadam_radam_state(opt_name):
+    """NAdam / RAdam through the drop-in generator for three rounds: exp_avg / exp_avg_sq and NAdam's
+    mu_product match torch CPU stepping the same -diff (bit-exact), params within the Adam sqrt bound;
+    optimizer.state holds views of the device buffers."""
+    import copy
+
+    model = fedopt_model()
+    ref_model = copy.deepcopy(model)
+    ref_opt = getattr(torch.optim, opt_name)(ref_model.parameters(), lr=2e-3, foreach=False)
+    gen = PTFedOptModelShareableGenerator(optimizer_args={"path": f"torch.optim.{opt_name}", "args": {"lr": 2e-3}},
+                                          source_model=model, device=0)
+    gen.handle_event(EventType.START_RUN, FLContext())
+    w = {k: v.detach().cpu().numpy().copy() for k, v in model.state_dict().items()}
+    p0 = {n: p.detach().cpu().numpy().copy() for n, p in ref_model.named_parameters()}
+    rng = np.random.default_rng(13)
+    for rnd in range(3):
+        fl_ctx = FLContext()
+        fl_ctx.set_prop(AppConstants.GLOBAL_MODEL, make_model_learnable(w, {}))
+        diff = {k: (rng.standard_normal(v.shape) * 0.05).astype(np.float32) for k, v in w.items()
+                if v.dtype == np.float32}
+        w = gen.shareable_to_learnable(DXO(DataKind.WEIGHT_DIFF, data=diff).to_shareable(), fl_ctx)[
+            ModelLearnableKey.WEIGHTS]
+        ref_opt.zero_grad()
+        for n, p in ref_model.named_parameters():
+            p.grad = torch.tensor(-1.0 * diff[n])
+        ref_opt.step()
+    for (n, p), (_, rp) in zip(model.named_parameters(), ref_model.named_parameters()):
+        st, rst = gen.optimizer.state[p], ref_opt.state[rp]
+        assert st["exp_avg"].device.type == "cuda" and float(st["step"]) == 3.0
+        assert same_bits(st["exp_avg"].cpu().numpy(), rst["exp_avg"].numpy()), n
+        assert same_bits(st["exp_avg_sq"].cpu().numpy(), rst["exp_avg_sq"].numpy()), n
+        if opt_name == "NAdam":
+            assert same_bits(st["mu_product"].numpy(), rst["mu_product"].numpy()), n
+        ref = rp.detach().numpy()
+        tol = adam_param_tolerance(p0[n], ref, 2e-3, 3)
+        assert np.all(np.abs(_np(w[n]).astype(np.float64) - ref.astype(np.float64)) <= tol), n
+
+
 def test_fedopt_generator_rejects_unsupported_optimizer():
     model = fedopt_model()
-    gen = PTFedOptModelShareableGenerator(optimizer_args={"path": "torch.optim.NAdam", "args": {"lr": 1e-3}},
+    gen = PTFedOptModelShareableGenerator(optimizer_args={"path": "torch.optim.Rprop", "args": {"lr": 1e-3}},
                                           source_model=model, device=0)
     gen.handle_event(EventType.START_RUN, FLContext())
     w = {k: v.detach().cpu().numpy().copy() for k, v in model.state_dict().items()}
     fl_ctx = FLContext()
     fl_ctx.set_prop(AppConstants.GLOBAL_MODEL, make_model_learnable(w, {}))
     diff = {"lin1.weight": np.zeros((64, 7), np.float32)}
-    with pytest.raises(NotImplementedError, match="NAdam"):
+    with pytest.raises(NotImplementedError, match="Rprop"):
         gen.shareable_to_learnable(DXO(DataKind.WEIGHT_DIFF, data=diff).to_shareable(), fl_ctx)
 
 
