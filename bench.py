@@ -43,7 +43,7 @@ def parse():
     ap.add_argument("--unroll", type=int, default=0, help="0 = library default (4)")
     ap.add_argument("--variant", type=int, default=0, help="cache policy bits (0 = nontemporal loads+stores)")
     ap.add_argument("--tile", type=int, default=4096, help="slab tile width (elements)")
-    ap.add_argument("--epilogue", choices=["none", "add_base", "sgd", "adam"], default="none",
+    ap.add_argument("--epilogue", choices=["none", "add_base", "sgd", "adam", "adamax", "nadam", "radam"], default="none",
                     help="fused server update (config 5 = adam: FedOpt Adam on the aggregated deltas)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-params", type=int, default=16 * 1024 * 1024)
@@ -210,7 +210,7 @@ def main():
 
     end = (P + 3) // 4 * 4
     slab = ctx.alloc(lay.slab_elems(P) * 4)
-    epi_bufs = {"none": 1, "add_base": 1, "sgd": 2, "adam": 3}[args.epilogue]  # out | p+buf | p+m+v
+    epi_bufs = {"none": 1, "add_base": 1, "sgd": 2}.get(args.epilogue, 3)  # out | p+buf | p+m+v
     state = [ctx.alloc(end * 4) for _ in range(epi_bufs)]
     out = state[0]
     bases = [slab.ptr + lay.slot_offset_elems(k) * 4 for k in range(K)]
@@ -231,7 +231,8 @@ def main():
             else:
                 ctx.memset(b.ptr, 0, end * 4)
         epi = N.Epilogue()
-        epi.kind = {"add_base": N.FEDAVG_EPI_ADD_BASE, "sgd": N.FEDAVG_EPI_SGD, "adam": N.FEDAVG_EPI_ADAM}[args.epilogue]
+        epi.kind = {"add_base": N.FEDAVG_EPI_ADD_BASE, "sgd": N.FEDAVG_EPI_SGD, "adam": N.FEDAVG_EPI_ADAM,
+                    "adamax": N.FEDAVG_EPI_ADAMAX, "nadam": N.FEDAVG_EPI_NADAM, "radam": N.FEDAVG_EPI_RADAM}[args.epilogue]
         if args.epilogue == "add_base":
             epi.base = out.ptr
         elif args.epilogue == "sgd":
@@ -240,6 +241,7 @@ def main():
         else:
             epi.param, epi.state1, epi.state2 = state[0].ptr, state[1].ptr, state[2].ptr
             epi.lr, epi.beta1, epi.beta2, epi.eps = 1e-3, 0.9, 0.999, 1e-8
+            epi.momentum_decay, epi.mu_product = 4e-3, 1.0  # NAdam (mu_product held at its first-step value)
         ctx.sync()
     n_step = [0]
 
@@ -278,7 +280,7 @@ def main():
     if rank == 0:
         bytes_step = 4.0 * K * P * world  # aggregated client bytes per step, all ranks
         value = bytes_step * args.steps / wall / 2**30
-        epi_bytes = {"none": 4.0, "add_base": 8.0, "sgd": 16.0, "adam": 24.0}[args.epilogue]
+        epi_bytes = {"none": 4.0, "add_base": 8.0, "sgd": 16.0}.get(args.epilogue, 24.0)
         alg_bytes_launch = 4.0 * K * P + epi_bytes * P
         traffic, traffic_src = pmc_traffic(args, K, P)
         achieved = alg_bytes_launch / (kernel_ms / 1e3) / 1e9
