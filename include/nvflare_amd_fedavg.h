@@ -76,6 +76,7 @@ enum fedavg_epi {
     FEDAVG_EPI_ADAMAX = 6,   /* torch Adamax on g = -d  (torch/optim/adamax.py _single_tensor_adamax) */
     FEDAVG_EPI_NADAM = 7,    /* torch NAdam on g = -d  (torch/optim/nadam.py _single_tensor_nadam) */
     FEDAVG_EPI_RADAM = 8,    /* torch RAdam on g = -d  (torch/optim/radam.py _single_tensor_radam) */
+    FEDAVG_EPI_RPROP = 9,    /* torch Rprop on g = -d  (torch/optim/rprop.py _single_tensor_rprop) */
 };
 
 typedef struct fedavg_epilogue {
@@ -98,6 +99,8 @@ typedef struct fedavg_epilogue {
     int centered;               /* RMSprop: state3 = grad_avg */
     double momentum_decay;      /* NAdam: mu_t = beta1 * (1 - 0.5 * 0.96^(step * momentum_decay)) */
     double mu_product;          /* NAdam: the fp32 mu_product state BEFORE this step (1.0 at the first) */
+    double etaminus, etaplus;   /* Rprop: etas; state1 = prev, state2 = step_size (lr-filled before step 1) */
+    double step_size_min, step_size_max; /* Rprop: step_sizes */
 } fedavg_epilogue;
 
 /* Quantized payload formats (nvflare/app_opt/pt/quantization/dequantizer.py:47-185, row f4). */

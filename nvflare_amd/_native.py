@@ -173,6 +173,7 @@ FEDAVG_EPI_RMSPROP = 5
 FEDAVG_EPI_ADAMAX = 6
 FEDAVG_EPI_NADAM = 7
 FEDAVG_EPI_RADAM = 8
+FEDAVG_EPI_RPROP = 9
 
 
 class Epilogue(ctypes.Structure):
@@ -203,6 +204,10 @@ class Epilogue(ctypes.Structure):
         ("centered", c_int),
         ("momentum_decay", c_double),
         ("mu_product", c_double),
+        ("etaminus", c_double),
+        ("etaplus", c_double),
+        ("step_size_min", c_double),
+        ("step_size_max", c_double),
     ]
 
 

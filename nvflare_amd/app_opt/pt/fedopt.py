@@ -8,7 +8,7 @@ representation (torch tensors if the global model holds tensors, numpy otherwise
 
 What differs is where the step runs.  The reference sets ``param.grad`` and calls
 ``optimizer.step()``; here the model's parameters are re-pointed into ONE flat fp32 buffer in HBM and
-``torch.optim.SGD`` / ``Adam`` / ``AdamW`` / ``Adagrad`` / ``RMSprop`` / ``Adamax`` / ``NAdam`` / ``RAdam`` steps are executed by the HIP fused-epilogue kernel
+``torch.optim.SGD`` / ``Adam`` / ``AdamW`` / ``Adagrad`` / ``RMSprop`` / ``Adamax`` / ``NAdam`` / ``RAdam`` / ``Rprop`` steps are executed by the HIP fused-epilogue kernel
 (``fedavg_accumulate_tiled_epi`` with the aggregated difference as ``acc_in``), with torch's
 single-tensor rounding sequence (``tests/test_fedopt_oracle.py``).  The torch optimizer object is kept
 for its ``param_groups`` (read every step, so lr schedulers work unchanged) and its ``state`` is filled
@@ -117,9 +117,11 @@ class DeviceServerOptimizer:
             return N.FEDAVG_EPI_NADAM
         if isinstance(optimizer, torch.optim.RAdam):
             return N.FEDAVG_EPI_RADAM
+        if isinstance(optimizer, torch.optim.Rprop):
+            return N.FEDAVG_EPI_RPROP
         raise NotImplementedError(
             f"nvflare_amd: server optimizer {type(optimizer).__module__}.{type(optimizer).__name__} has no device "
-            "kernel (supported: torch.optim.SGD, Adam, AdamW, Adagrad, RMSprop, Adamax, NAdam, RAdam)")
+            "kernel (supported: torch.optim.SGD, Adam, AdamW, Adagrad, RMSprop, Adamax, NAdam, RAdam, Rprop)")
 
     def _group_of(self) -> Dict[int, dict]:
         return {id(p): g for g in self.optimizer.param_groups for p in g["params"]}
@@ -161,6 +163,11 @@ class DeviceServerOptimizer:
                     second = st["exp_inf"] if self.kind == N.FEDAVG_EPI_ADAMAX else st["exp_avg_sq"]
                     self.v[s.offset:s.offset + s.n].copy_(second.reshape(-1).to(dev))
                     s.step = float(st["step"])
+                if "step_size" in st:  # Rprop: prev -> m, step_size -> v
+                    self.m[s.offset:s.offset + s.n].copy_(st["prev"].reshape(-1).to(dev))
+                    self.v[s.offset:s.offset + s.n].copy_(st["step_size"].reshape(-1).to(dev))
+                    s.step = float(st["step"])
+                    s.has_momentum_buffer = True  # Rprop: state initialised
                 if "mu_product" in st:  # NAdam
                     s.mu_product = np.float32(float(st["mu_product"]))
                 if "sum" in st:  # Adagrad: state made at construction (initial_accumulator_value)
@@ -206,6 +213,10 @@ class DeviceServerOptimizer:
                 st["momentum_buffer"] = self.v[s.offset:s.offset + s.n].view(s.param.shape)
             if g.get("centered"):
                 st["grad_avg"] = self._max_exp_avg_sq()[s.offset:s.offset + s.n].view(s.param.shape)
+        elif self.kind == N.FEDAVG_EPI_RPROP:
+            st["step"] = torch.tensor(s.step, dtype=torch.float32)
+            st["prev"] = self.m[s.offset:s.offset + s.n].view(s.param.shape)
+            st["step_size"] = self.v[s.offset:s.offset + s.n].view(s.param.shape)
         elif self.kind == N.FEDAVG_EPI_ADAMAX:
             st["step"] = torch.tensor(s.step, dtype=torch.float32)
             st["exp_avg"] = self.m[s.offset:s.offset + s.n].view(s.param.shape)
@@ -250,6 +261,11 @@ class DeviceServerOptimizer:
             if group.get("centered"):
                 e.centered = 1
                 e.state3 = self._max_exp_avg_sq().data_ptr()
+        elif self.kind == N.FEDAVG_EPI_RPROP:
+            e.etaminus, e.etaplus = (float(x) for x in group["etas"])
+            e.step_size_min, e.step_size_max = (float(x) for x in group["step_sizes"])
+            e.state2 = self.v.data_ptr()
+            e.step = s.step + 1.0
         elif self.kind == N.FEDAVG_EPI_ADAMAX:
             b1, b2 = group["betas"]
             e.beta1, e.beta2, e.eps = float(b1), float(b2), float(group["eps"])
@@ -277,6 +293,7 @@ class DeviceServerOptimizer:
         with ``K = 0`` (the aggregated difference as ``acc_in``)."""
         groups = self._group_of()
         present = []
+        self._init_lazy_state(model_diff, groups)
         fused = self._fused_step(model_diff, groups)
         host_pieces, keep = [], []  # host differences: one pass through the pinned ring, not a copy per tensor
         with torch.no_grad():
@@ -327,6 +344,17 @@ class DeviceServerOptimizer:
             self.ctx.sync()
         self._advance(present, groups)
         return [s.name for s in self.slots if s.name in fused or s in present]
+
+    def _init_lazy_state(self, model_diff: Dict, groups: Dict[int, dict]) -> None:
+        """Rprop makes its state at the first step: prev = 0, step_size = full_like(grad, lr) (rprop.py _init_group)."""
+        if self.kind != N.FEDAVG_EPI_RPROP:
+            return
+        with torch.no_grad():
+            for s in self.slots:
+                if s.name in model_diff and not s.has_momentum_buffer:
+                    self.m[s.offset:s.offset + s.n].zero_()
+                    self.v[s.offset:s.offset + s.n].fill_(float(groups[id(s.param)]["lr"]))
+                    s.has_momentum_buffer = True
 
     def _advance(self, stepped: List[_Slot], groups: Dict[int, dict]) -> None:
         for s in stepped:

@@ -75,6 +75,7 @@ struct EpiParams {
     float bias_correction2, coef_grad, coef_avg;  // NAdam: the two addcdiv values
     float bias_correction1, lr, rect;             // RAdam
     int rectified;                                // RAdam: rho_t > 5
+    float etaminus, etaplus, ss_min, ss_max;      // Rprop
 };
 
 struct DequantLaunch {

@@ -161,7 +161,7 @@ __global__ void __launch_bounds__(kBlock) fedavg_tiles_f32x4(const RowTableF32 t
 //   EPI_ADD_BASE  w = base + d                          full_model_shareable_generator.py:58-67
 //   EPI_SGD       torch _single_tensor_sgd on g = -d     app_opt/pt/fedopt.py:157-182
 //   EPI_ADAM      torch _single_tensor_adam on g = -d    torch/optim/adam.py:347-551
-//   EPI_ADAGRAD / RMSPROP / ADAMAX / NADAM / RADAM   torch _single_tensor_{adagrad,rmsprop,adamax,nadam,radam}
+//   EPI_ADAGRAD / RMSPROP / ADAMAX / NADAM / RADAM / RPROP   torch _single_tensor_{adagrad,...,rprop} on g = -d
 // Per parameter: 4K bytes of client reads + 12 B (p, m, v) read + 12 B written for Adam, so the
 // optimizer costs one pass instead of the reference's separate aggregate / H2D / step / D2H round trip.
 // Rounding sequence pinned against torch CPU by tests/test_fedopt_oracle.py (fma for add(alpha), lerp
@@ -201,7 +201,7 @@ __device__ __forceinline__ EpiIn epi_load(const EpiParams& E, const int64_t i) {
         in.b = load4<true>(reinterpret_cast<const f32x4*>(E.state1) + i);
         if (E.has_momentum) in.c = load4<true>(reinterpret_cast<const f32x4*>(E.state2) + i);
         if (E.centered) in.d = load4<true>(reinterpret_cast<const f32x4*>(E.state3) + i);
-    } else if constexpr (EPI == FEDAVG_EPI_ADAMAX) {
+    } else if constexpr (EPI == FEDAVG_EPI_ADAMAX || EPI == FEDAVG_EPI_RPROP) {
         in.a = load4<true>(reinterpret_cast<const f32x4*>(E.param) + i);
         in.b = load4<true>(reinterpret_cast<const f32x4*>(E.state1) + i);
         in.c = load4<true>(reinterpret_cast<const f32x4*>(E.state2) + i);
@@ -293,6 +293,26 @@ __device__ __forceinline__ void epilogue4(const EpiParams& E, const int64_t i, c
         store4<true>(p4, p);
         store4<true>(reinterpret_cast<f32x4*>(E.state1) + i, m);
         store4<true>(reinterpret_cast<f32x4*>(E.state2) + i, u);
+    } else if constexpr (EPI == FEDAVG_EPI_RPROP) {
+        f32x4 p = in.a;
+        f32x4 prev = in.b;
+        f32x4 ss = in.c;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            float g = E.maximize ? d[c] : -d[c];
+            const float s = g * prev[c];                                   // grad.mul(prev).sign() -> etas / 1
+            const float sv = s > 0.0f ? E.etaplus : (s < 0.0f ? E.etaminus : (s == 0.0f ? 1.0f : s));
+            float st = ss[c] * sv;                                         // step_size.mul_(sign).clamp_(min, max)
+            st = st != st ? st : fminf(fmaxf(st, E.ss_min), E.ss_max);
+            if (sv == E.etaminus) g = 0.0f;                                // grad[sign.eq(etaminus)] = 0
+            const float sg = g > 0.0f ? 1.0f : (g < 0.0f ? -1.0f : (g == 0.0f ? 0.0f : g));
+            p[c] = __builtin_fmaf(-1.0f * sg, st, p[c]);                  // param.addcmul_(grad.sign(), step_size, -1)
+            prev[c] = g;                                                   // prev.copy_(grad)
+            ss[c] = st;
+        }
+        store4<true>(p4, p);
+        store4<true>(reinterpret_cast<f32x4*>(E.state1) + i, prev);
+        store4<true>(reinterpret_cast<f32x4*>(E.state2) + i, ss);
     } else if constexpr (EPI == FEDAVG_EPI_NADAM || EPI == FEDAVG_EPI_RADAM) {
         f32x4 p = in.a;
         f32x4 m = in.b;
@@ -739,6 +759,10 @@ static hipError_t launch_epi_p(const TileLaunch& L, const EpiParams& E, hipStrea
             break;
         case FEDAVG_EPI_RADAM:
             hipLaunchKernelGGL((fedavg_tiles_epi_f32x4<OP, FIN, ACC_IN, FEDAVG_EPI_RADAM, PRE>), dim3(L.grid),
+                               dim3(kBlock), 0, s, L.tab, L.k, L.tstride4, ai, o, L.b4, L.e4, L.fin_val, E);
+            break;
+        case FEDAVG_EPI_RPROP:
+            hipLaunchKernelGGL((fedavg_tiles_epi_f32x4<OP, FIN, ACC_IN, FEDAVG_EPI_RPROP, PRE>), dim3(L.grid),
                                dim3(kBlock), 0, s, L.tab, L.k, L.tstride4, ai, o, L.b4, L.e4, L.fin_val, E);
             break;
         default:

@@ -120,6 +120,7 @@ void oracle_synth_fill_f32(uint64_t seed, uint64_t row, const uint64_t* cols, si
  *   ADAMAX    torch/optim/adamax.py _single_tensor_adamax on g = -1.0 * d (m exp_avg, v exp_inf)
  *   NADAM     torch/optim/nadam.py _single_tensor_nadam (m exp_avg, v exp_avg_sq; mu_product passed in)
  *   RADAM     torch/optim/radam.py _single_tensor_radam (m exp_avg, v exp_avg_sq)
+ *   RPROP     torch/optim/rprop.py _single_tensor_rprop (m prev, v step_size filled with lr before step 1)
  *   ADAM      torch/optim/adam.py _single_tensor_adam (:347-551) on g = -1.0 * d; amsgrad divides by
  *             sqrt(vmax), vmax = torch.maximum(vmax, v) kept as a third state
  * Rounding sequence pinned against torch 2.10 CPU (tests/test_fedopt_oracle.py):
@@ -131,7 +132,8 @@ void oracle_synth_fill_f32(uint64_t seed, uint64_t row, const uint64_t* cols, si
  * fp32 where they meet a tensor.
  * ------------------------------------------------------------------------------------------------ */
 enum { ORACLE_EPI_NONE = 0, ORACLE_EPI_ADD_BASE = 1, ORACLE_EPI_SGD = 2, ORACLE_EPI_ADAM = 3, ORACLE_EPI_ADAGRAD = 4,
-       ORACLE_EPI_RMSPROP = 5, ORACLE_EPI_ADAMAX = 6, ORACLE_EPI_NADAM = 7, ORACLE_EPI_RADAM = 8 };
+       ORACLE_EPI_RMSPROP = 5, ORACLE_EPI_ADAMAX = 6, ORACLE_EPI_NADAM = 7, ORACLE_EPI_RADAM = 8,
+       ORACLE_EPI_RPROP = 9 };
 
 typedef struct {
     int kind;
@@ -147,6 +149,7 @@ typedef struct {
     int centered;                                 /* RMSprop: vmax holds grad_avg */
     double momentum_decay;                        /* NAdam */
     double mu_product;                            /* NAdam: fp32 mu_product state before this step */
+    double etaminus, etaplus, step_size_min, step_size_max; /* Rprop */
 } oracle_epilogue;
 
 /* torch.maximum: a NaN operand is the result */
@@ -214,6 +217,24 @@ void oracle_epilogue_apply(const float* delta, size_t n, const oracle_epilogue* 
             v[i] = max_torch(v[i] * (float)epi->beta2, fabsf(g) + (float)epi->eps);    /* maximum(exp_inf.mul_(b2), |g|+eps) */
             const float neg_clr = (float)(-(epi->lr / (1.0 - pow(epi->beta1, epi->step))));
             p[i] = p[i] + (neg_clr * m[i]) / v[i];                                    /* addcdiv_(exp_avg, exp_inf, -clr) */
+        } else if (epi->kind == ORACLE_EPI_RPROP) { /* torch/optim/rprop.py _single_tensor_rprop */
+            float g = epi->maximize ? d : -d;
+            const float s = g * m[i];
+            float sv;                                                     /* sign -> etaplus / etaminus / 1 */
+            if (s > 0.0f) sv = (float)epi->etaplus;
+            else if (s < 0.0f) sv = (float)epi->etaminus;
+            else if (s == 0.0f) sv = 1.0f;
+            else sv = s;                                                  /* NaN stays NaN */
+            float st = v[i] * sv;
+            if (st == st) {                                               /* clamp_(min, max); NaN propagates */
+                if (st < (float)epi->step_size_min) st = (float)epi->step_size_min;
+                if (st > (float)epi->step_size_max) st = (float)epi->step_size_max;
+            }
+            if (sv == (float)epi->etaminus) g = 0.0f;                     /* grad[sign.eq(etaminus)] = 0 */
+            float sg = g > 0.0f ? 1.0f : (g < 0.0f ? -1.0f : (g == 0.0f ? 0.0f : g));
+            p[i] = fmaf(-1.0f * sg, st, p[i]);                            /* addcmul_(grad.sign(), step_size, -1) */
+            m[i] = g;
+            v[i] = st;
         } else if (epi->kind == ORACLE_EPI_NADAM || epi->kind == ORACLE_EPI_RADAM) {
             float g = epi->maximize ? d : -d;
             float pv = p[i];

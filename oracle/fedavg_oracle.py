@@ -244,7 +244,7 @@ def synth_weights(K: int):
 # ---------------------------------------------------------------------------------------------------
 # server-optimizer epilogues (rows a9/a10): see oracle_epilogue_apply in fedavg_oracle.c
 # ---------------------------------------------------------------------------------------------------
-EPI_NONE, EPI_ADD_BASE, EPI_SGD, EPI_ADAM, EPI_ADAGRAD, EPI_RMSPROP, EPI_ADAMAX, EPI_NADAM, EPI_RADAM = range(9)
+EPI_NONE, EPI_ADD_BASE, EPI_SGD, EPI_ADAM, EPI_ADAGRAD, EPI_RMSPROP, EPI_ADAMAX, EPI_NADAM, EPI_RADAM, EPI_RPROP = range(10)
 
 
 class _Epi(ctypes.Structure):
@@ -268,6 +268,10 @@ class _Epi(ctypes.Structure):
         ("centered", ctypes.c_int),
         ("momentum_decay", ctypes.c_double),
         ("mu_product", ctypes.c_double),
+        ("etaminus", ctypes.c_double),
+        ("etaplus", ctypes.c_double),
+        ("step_size_min", ctypes.c_double),
+        ("step_size_max", ctypes.c_double),
     ]
 
 

@@ -257,3 +257,31 @@ def test_nadam_radam_vs_torch(oracle, opt_name, kw):
     diff = np.abs(p.astype(np.float64) - tp.astype(np.float64))
     assert np.all(diff <= tol), float((diff / tol).max())
     assert float((diff > 0).mean()) < 0.02
+
+
+@pytest.mark.parametrize("kw", [
+    dict(lr=1e-2),
+    dict(lr=5e-2, etas=(0.3, 1.5), step_sizes=(1e-3, 0.08)),
+    dict(lr=1e-3, maximize=True),
+])
+def test_rprop_vs_torch(oracle, kw):
+    """torch/optim/rprop.py _single_tensor_rprop: sign-driven step sizes, no rounding beyond one multiply per
+    state, so params, prev and step_size are bit-exact against torch CPU.  Deltas alternate in sign on part
+    of the elements so every branch (etaplus, etaminus with the gradient zeroed, 1) is taken."""
+    rng = np.random.default_rng(9)
+    n = 200_003
+    p0 = rng.standard_normal(n).astype(np.float32)
+    base = (rng.standard_normal(n) * 0.01).astype(np.float32)
+    deltas = [np.where(rng.random(n) < 0.3, -base, base).astype(np.float32) for _ in range(6)]
+    deltas[2][::7] = 0.0
+    tp, st = _torch_steps(torch.optim.Rprop, kw, p0, deltas)
+    p, prev, ss = p0.copy(), np.zeros(n, np.float32), np.full(n, kw["lr"], np.float32)
+    em, ep = kw.get("etas", (0.5, 1.2))
+    lo, hi = kw.get("step_sizes", (1e-6, 50))
+    for k, d in enumerate(deltas):
+        oracle.epilogue_apply(d, oracle.EPI_RPROP, p=p, m=prev, v=ss, lr=kw["lr"], etaminus=em, etaplus=ep,
+                              step_size_min=lo, step_size_max=hi, maximize=int(kw.get("maximize", False)),
+                              step=float(k + 1))
+    assert same_bits(prev, st["prev"].numpy()), "prev"
+    assert same_bits(ss, st["step_size"].numpy()), "step_size"
+    assert same_bits(p, tp), "param"

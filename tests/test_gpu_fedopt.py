@@ -392,6 +392,40 @@ def test_nadam_radam_epilogue(ctx, oracle, kind, K, hp):
         mp = nadam_mu_product(mp, hp["beta1"], hp.get("momentum_decay", 4e-3), step + 1)
 
 
+@pytest.mark.parametrize("K,hp", [(5, dict(etaminus=0.5, etaplus=1.2, step_size_min=1e-6, step_size_max=50.0)),
+                                  (2, dict(etaminus=0.3, etaplus=1.5, step_size_min=1e-3, step_size_max=0.08,
+                                           maximize=1)),
+                                  (0, dict(etaminus=0.5, etaplus=1.2, step_size_min=1e-6, step_size_max=50.0))])
+def test_rprop_epilogue(ctx, oracle, K, hp):
+    """Rprop: sign(g * prev) -> etaplus / etaminus / 1 scales the clamped step size, g is zeroed where the sign
+    flipped, p = fma(-sign(g), step_size, p), prev = g.  Four steps from step_size = lr, with aggregates that
+    flip sign on part of the elements, bit-exact vs the oracle (itself bit-exact vs torch CPU)."""
+    rng = np.random.default_rng(150 + K)
+    n = 3 * TILE + 52
+    p = rng.standard_normal(n).astype(np.float32)
+    prev, ss = np.zeros(n, np.float32), np.full(n, 0.01, np.float32)
+    for step in range(4):
+        rows = [(rng.standard_normal(n) * 0.05).astype(np.float32) for _ in range(K)]
+        ws = [float(1 + (37 * k) % 100) for k in range(K)]
+        delta = (rng.standard_normal(n) * 0.05).astype(np.float32) if K == 0 else None
+        if delta is not None and step == 2:
+            delta[::5] = 0.0
+        dev = _Dev(ctx, rows, n)
+        try:
+            e = _epi(9, param=dev.buf("p", p), state1=dev.buf("prev", prev), state2=dev.buf("ss", ss),
+                     step=float(step + 1), **hp)
+            acc_ptr = dev.buf("acc", delta) if K == 0 else None
+            ctx.accumulate_tiled_epi(dev.bases, ws, TILE, dev.lay.tile_stride, 0, dev.n4, None, 1,
+                                     2 if K else 0, _sum(ws) if K else 1.0, e, acc_in_ptr=acc_ptr)
+            d = oracle.fedavg_c(rows, ws, oracle.MODE_TORCH, nthreads=8) if K else delta
+            oracle.epilogue_apply(d, oracle.EPI_RPROP, p=p, m=prev, v=ss, step=float(step + 1), **hp)
+            assert same_bits(dev.get("p"), p) and same_bits(dev.get("prev"), prev), step
+            assert same_bits(dev.get("ss"), ss), step
+        finally:
+            dev.close()
+    assert len(np.unique(ss)) > 3  # several step-size histories were exercised
+
+
 @pytest.mark.parametrize("K,hp", [(6, dict(lr=1e-2, alpha=0.99, eps=1e-8)),
                                   (3, dict(lr=1e-2, alpha=0.9, eps=1e-6, momentum=0.9, weight_decay=1e-3)),
                                   (2, dict(lr=1e-3, alpha=0.95, eps=1e-8, centered=1, momentum=0.5, maximize=1)),

@@ -99,6 +99,38 @@ def test_fedopt_generator_optimizer_state_views():
     assert len(sd["state"]) == len(list(model.parameters()))
 
 
+def test_fedopt_generator_rprop_matches_torch():
+    """Rprop through the drop-in generator for four rounds, one parameter skipped in round 1 (its state is
+    made at its own first step, as torch's is): params, prev and step_size bit-exact against torch CPU."""
+    import copy
+
+    model = fedopt_model()
+    ref_model = copy.deepcopy(model)
+    ref_opt = torch.optim.Rprop(ref_model.parameters(), lr=1e-2, foreach=False)
+    gen = PTFedOptModelShareableGenerator(optimizer_args={"path": "torch.optim.Rprop", "args": {"lr": 1e-2}},
+                                          source_model=model, device=0)
+    gen.handle_event(EventType.START_RUN, FLContext())
+    w = {k: v.detach().cpu().numpy().copy() for k, v in model.state_dict().items()}
+    rng = np.random.default_rng(14)
+    for rnd in range(4):
+        fl_ctx = FLContext()
+        fl_ctx.set_prop(AppConstants.GLOBAL_MODEL, make_model_learnable(w, {}))
+        diff = {k: (rng.standard_normal(v.shape) * 0.05).astype(np.float32) for k, v in w.items()
+                if v.dtype == np.float32 and not (rnd == 0 and k == "lin2.weight")}
+        w = gen.shareable_to_learnable(DXO(DataKind.WEIGHT_DIFF, data=diff).to_shareable(), fl_ctx)[
+            ModelLearnableKey.WEIGHTS]
+        ref_opt.zero_grad()
+        for n, p in ref_model.named_parameters():
+            p.grad = torch.tensor(-1.0 * diff[n]) if n in diff else None
+        ref_opt.step()
+    for (n, p), (_, rp) in zip(model.named_parameters(), ref_model.named_parameters()):
+        st, rst = gen.optimizer.state[p], ref_opt.state[rp]
+        assert float(st["step"]) == float(rst["step"]), n
+        assert same_bits(_np(w[n]), rp.detach().numpy()), n
+        assert same_bits(st["prev"].cpu().numpy(), rst["prev"].numpy()), n
+        assert same_bits(st["step_size"].cpu().numpy(), rst["step_size"].numpy()), n
+
+
 def test_fedopt_generator_adamax_state_matches_torch():
     """Adamax (no sqrt on its path): params, exp_avg and exp_inf bit-exact against torch CPU stepping the same
     -diff, over two rounds; optimizer.state holds views of the device buffers."""
@@ -173,14 +205,14 @@ def test_fedopt_generator_nadam_radam_state(opt_name):
 
 def test_fedopt_generator_rejects_unsupported_optimizer():
     model = fedopt_model()
-    gen = PTFedOptModelShareableGenerator(optimizer_args={"path": "torch.optim.Rprop", "args": {"lr": 1e-3}},
+    gen = PTFedOptModelShareableGenerator(optimizer_args={"path": "torch.optim.ASGD", "args": {"lr": 1e-3}},
                                           source_model=model, device=0)
     gen.handle_event(EventType.START_RUN, FLContext())
     w = {k: v.detach().cpu().numpy().copy() for k, v in model.state_dict().items()}
     fl_ctx = FLContext()
     fl_ctx.set_prop(AppConstants.GLOBAL_MODEL, make_model_learnable(w, {}))
     diff = {"lin1.weight": np.zeros((64, 7), np.float32)}
-    with pytest.raises(NotImplementedError, match="Rprop"):
+    with pytest.raises(NotImplementedError, match="ASGD"):
         gen.shareable_to_learnable(DXO(DataKind.WEIGHT_DIFF, data=diff).to_shareable(), fl_ctx)
 
 
