@@ -77,6 +77,7 @@ enum fedavg_epi {
     FEDAVG_EPI_NADAM = 7,    /* torch NAdam on g = -d  (torch/optim/nadam.py _single_tensor_nadam) */
     FEDAVG_EPI_RADAM = 8,    /* torch RAdam on g = -d  (torch/optim/radam.py _single_tensor_radam) */
     FEDAVG_EPI_RPROP = 9,    /* torch Rprop on g = -d  (torch/optim/rprop.py _single_tensor_rprop) */
+    FEDAVG_EPI_ASGD = 10,    /* torch ASGD on g = -d  (torch/optim/asgd.py _single_tensor_asgd) */
 };
 
 typedef struct fedavg_epilogue {
@@ -101,6 +102,7 @@ typedef struct fedavg_epilogue {
     double mu_product;          /* NAdam: the fp32 mu_product state BEFORE this step (1.0 at the first) */
     double etaminus, etaplus;   /* Rprop: etas; state1 = prev, state2 = step_size (lr-filled before step 1) */
     double step_size_min, step_size_max; /* Rprop: step_sizes */
+    double eta, mu, lambd;      /* ASGD: fp32 eta / mu states before this step, lambd; state1 = ax */
 } fedavg_epilogue;
 
 /* Quantized payload formats (nvflare/app_opt/pt/quantization/dequantizer.py:47-185, row f4). */

@@ -174,6 +174,7 @@ FEDAVG_EPI_ADAMAX = 6
 FEDAVG_EPI_NADAM = 7
 FEDAVG_EPI_RADAM = 8
 FEDAVG_EPI_RPROP = 9
+FEDAVG_EPI_ASGD = 10
 
 
 class Epilogue(ctypes.Structure):
@@ -208,6 +209,9 @@ class Epilogue(ctypes.Structure):
         ("etaplus", c_double),
         ("step_size_min", c_double),
         ("step_size_max", c_double),
+        ("eta", c_double),
+        ("mu", c_double),
+        ("lambd", c_double),
     ]
 
 

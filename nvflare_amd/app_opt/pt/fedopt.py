@@ -8,7 +8,7 @@ representation (torch tensors if the global model holds tensors, numpy otherwise
 
 What differs is where the step runs.  The reference sets ``param.grad`` and calls
 ``optimizer.step()``; here the model's parameters are re-pointed into ONE flat fp32 buffer in HBM and
-``torch.optim.SGD`` / ``Adam`` / ``AdamW`` / ``Adagrad`` / ``RMSprop`` / ``Adamax`` / ``NAdam`` / ``RAdam`` / ``Rprop`` steps are executed by the HIP fused-epilogue kernel
+``torch.optim.SGD`` / ``Adam`` / ``AdamW`` / ``Adagrad`` / ``RMSprop`` / ``Adamax`` / ``NAdam`` / ``RAdam`` / ``Rprop`` / ``ASGD`` steps are executed by the HIP fused-epilogue kernel
 (``fedavg_accumulate_tiled_epi`` with the aggregated difference as ``acc_in``), with torch's
 single-tensor rounding sequence (``tests/test_fedopt_oracle.py``).  The torch optimizer object is kept
 for its ``param_groups`` (read every step, so lr schedulers work unchanged) and its ``state`` is filled
@@ -75,13 +75,19 @@ def build_component_from_args(args: dict):
 
 
 class _Slot:
-    __slots__ = ("name", "param", "offset", "n", "step", "has_momentum_buffer", "mu_product")
+    __slots__ = ("name", "param", "offset", "n", "step", "has_momentum_buffer", "mu_product", "eta", "mu")
 
     def __init__(self, name, param, offset, n):
         self.name, self.param, self.offset, self.n = name, param, offset, n
         self.step = 0.0
         self.has_momentum_buffer = False
         self.mu_product = np.float32(1.0)  # NAdam's fp32 state tensor, kept on the host
+        self.eta = np.float32(0.0)  # ASGD's fp32 eta / mu state tensors, kept on the host
+        self.mu = np.float32(1.0)
+
+    def host_key(self) -> tuple:
+        """Per-parameter host state a launch shares (runs group parameters whose keys are equal)."""
+        return (self.step, self.has_momentum_buffer, float(self.mu_product), float(self.eta), float(self.mu))
 
 
 class DeviceServerOptimizer:
@@ -119,9 +125,11 @@ class DeviceServerOptimizer:
             return N.FEDAVG_EPI_RADAM
         if isinstance(optimizer, torch.optim.Rprop):
             return N.FEDAVG_EPI_RPROP
+        if isinstance(optimizer, torch.optim.ASGD):
+            return N.FEDAVG_EPI_ASGD
         raise NotImplementedError(
             f"nvflare_amd: server optimizer {type(optimizer).__module__}.{type(optimizer).__name__} has no device "
-            "kernel (supported: torch.optim.SGD, Adam, AdamW, Adagrad, RMSprop, Adamax, NAdam, RAdam, Rprop)")
+            "kernel (supported: torch.optim.SGD, Adam, AdamW, Adagrad, RMSprop, Adamax, NAdam, RAdam, Rprop, ASGD)")
 
     def _group_of(self) -> Dict[int, dict]:
         return {id(p): g for g in self.optimizer.param_groups for p in g["params"]}
@@ -168,6 +176,11 @@ class DeviceServerOptimizer:
                     self.v[s.offset:s.offset + s.n].copy_(st["step_size"].reshape(-1).to(dev))
                     s.step = float(st["step"])
                     s.has_momentum_buffer = True  # Rprop: state initialised
+                if "ax" in st:  # ASGD: ax -> m, eta / mu host scalars
+                    self.m[s.offset:s.offset + s.n].copy_(st["ax"].reshape(-1).to(dev))
+                    s.eta, s.mu = np.float32(float(st["eta"])), np.float32(float(st["mu"]))
+                    s.step = float(st["step"])
+                    s.has_momentum_buffer = True  # ASGD: state initialised
                 if "mu_product" in st:  # NAdam
                     s.mu_product = np.float32(float(st["mu_product"]))
                 if "sum" in st:  # Adagrad: state made at construction (initial_accumulator_value)
@@ -213,6 +226,11 @@ class DeviceServerOptimizer:
                 st["momentum_buffer"] = self.v[s.offset:s.offset + s.n].view(s.param.shape)
             if g.get("centered"):
                 st["grad_avg"] = self._max_exp_avg_sq()[s.offset:s.offset + s.n].view(s.param.shape)
+        elif self.kind == N.FEDAVG_EPI_ASGD:
+            st["step"] = torch.tensor(s.step, dtype=torch.float32)
+            st["eta"] = torch.tensor(s.eta, dtype=torch.float32)
+            st["mu"] = torch.tensor(s.mu, dtype=torch.float32)
+            st["ax"] = self.m[s.offset:s.offset + s.n].view(s.param.shape)
         elif self.kind == N.FEDAVG_EPI_RPROP:
             st["step"] = torch.tensor(s.step, dtype=torch.float32)
             st["prev"] = self.m[s.offset:s.offset + s.n].view(s.param.shape)
@@ -261,6 +279,9 @@ class DeviceServerOptimizer:
             if group.get("centered"):
                 e.centered = 1
                 e.state3 = self._max_exp_avg_sq().data_ptr()
+        elif self.kind == N.FEDAVG_EPI_ASGD:
+            e.eta, e.mu, e.lambd = float(s.eta), float(s.mu), float(group["lambd"])
+            e.step = s.step + 1.0
         elif self.kind == N.FEDAVG_EPI_RPROP:
             e.etaminus, e.etaplus = (float(x) for x in group["etas"])
             e.step_size_min, e.step_size_max = (float(x) for x in group["step_sizes"])
@@ -326,7 +347,7 @@ class DeviceServerOptimizer:
         runs: List[Tuple[tuple, List[_Slot]]] = []
         for s in present:
             g = groups[id(s.param)]
-            key = (id(g), s.step, s.has_momentum_buffer, float(s.mu_product))
+            key = (id(g),) + s.host_key()
             prev = runs[-1][1][-1] if runs else None
             contiguous = prev is not None and self.slots.index(s) == self.slots.index(prev) + 1
             if runs and runs[-1][0] == key and contiguous:
@@ -346,19 +367,28 @@ class DeviceServerOptimizer:
         return [s.name for s in self.slots if s.name in fused or s in present]
 
     def _init_lazy_state(self, model_diff: Dict, groups: Dict[int, dict]) -> None:
-        """Rprop makes its state at the first step: prev = 0, step_size = full_like(grad, lr) (rprop.py _init_group)."""
-        if self.kind != N.FEDAVG_EPI_RPROP:
+        """Rprop and ASGD make their state at the first step (rprop.py / asgd.py ``_init_group``): Rprop prev = 0,
+        step_size = full_like(grad, lr); ASGD ax = 0, eta = lr (fp32), mu = 1."""
+        if self.kind not in (N.FEDAVG_EPI_RPROP, N.FEDAVG_EPI_ASGD):
             return
         with torch.no_grad():
             for s in self.slots:
                 if s.name in model_diff and not s.has_momentum_buffer:
+                    lr = float(groups[id(s.param)]["lr"])
                     self.m[s.offset:s.offset + s.n].zero_()
-                    self.v[s.offset:s.offset + s.n].fill_(float(groups[id(s.param)]["lr"]))
+                    if self.kind == N.FEDAVG_EPI_RPROP:
+                        self.v[s.offset:s.offset + s.n].fill_(lr)
+                    else:
+                        s.eta, s.mu = np.float32(lr), np.float32(1.0)
                     s.has_momentum_buffer = True
 
     def _advance(self, stepped: List[_Slot], groups: Dict[int, dict]) -> None:
         for s in stepped:
             s.step += 1.0
+            if self.kind == N.FEDAVG_EPI_ASGD:  # asgd.py: new eta / mu from the python-float formulas
+                g = groups[id(s.param)]
+                s.eta = np.float32(g["lr"] / ((1 + g["lambd"] * g["lr"] * s.step) ** g["alpha"]))
+                s.mu = np.float32(1 / max(1, s.step - g["t0"]))
             if self.kind == N.FEDAVG_EPI_NADAM:  # nadam.py: mu_product *= mu on an fp32 tensor
                 g = groups[id(s.param)]
                 mu = g["betas"][0] * (1.0 - 0.5 * (0.96 ** (s.step * g["momentum_decay"])))
@@ -392,8 +422,7 @@ class DeviceServerOptimizer:
             entries = {}
             for key, s in by_key.items():
                 g = groups[id(s.param)]
-                entries[key] = FusedEntry(s.offset, self._epilogue(g, s), (id(g), s.step, s.has_momentum_buffer,
-                                                                          float(s.mu_product)))
+                entries[key] = FusedEntry(s.offset, self._epilogue(g, s), (id(g),) + s.host_key())
             names = set(rnd.fused_step(entries, egress_marks=egress))
             stepped = [s for key, s in by_key.items() if key in names]
             with self.ctx.lock:

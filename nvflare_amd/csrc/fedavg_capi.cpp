@@ -430,6 +430,11 @@ fedavg::EpiParams make_epi(const fedavg_epilogue& e) {
         E.ss_min = (float)e.step_size_min;
         E.ss_max = (float)e.step_size_max;
     }
+    if (e.kind == FEDAVG_EPI_ASGD) {  // asgd.py: eta_value = _get_value(eta) (fp32 state), python-float math
+        E.decay = (float)(1.0 - e.lambd * e.eta);
+        E.neg_eta = (float)(-e.eta);
+        E.mu = (float)e.mu;
+    }
     if (e.kind == FEDAVG_EPI_RADAM) {  // radam.py _single_tensor_radam
         const double rho_inf = 2.0 / (1.0 - e.beta2) - 1.0;
         const double rho_t = rho_inf - 2.0 * e.step * std::pow(e.beta2, e.step) / bc2;
@@ -1064,7 +1069,7 @@ int fedavg_accumulate_tiled_epi(fedavg_ctx* ctx, const void* const* bases, const
                 throw Error(g_last_error);
             return;
         }
-        if (epi->kind < FEDAVG_EPI_ADD_BASE || epi->kind > FEDAVG_EPI_RPROP) throw Error("bad epilogue kind");
+        if (epi->kind < FEDAVG_EPI_ADD_BASE || epi->kind > FEDAVG_EPI_ASGD) throw Error("bad epilogue kind");
         if (k_rows < 0 || (k_rows == 0 && !acc_in)) throw Error("k_rows == 0 requires acc_in");
         check_op_fin(op, fin);
         if (tile_elems != (size_t)fedavg::kDefaultTile)
@@ -1095,6 +1100,8 @@ int fedavg_accumulate_tiled_epi(fedavg_ctx* ctx, const void* const* bases, const
             throw Error("NADAM/RADAM need param, state1 (exp_avg), state2 (exp_avg_sq) and step >= 1");
         if (epi->kind == FEDAVG_EPI_RPROP && (!epi->param || !epi->state1 || !epi->state2))
             throw Error("RPROP needs param, state1 (prev), state2 (step_size)");
+        if (epi->kind == FEDAVG_EPI_ASGD && (!epi->param || !epi->state1))
+            throw Error("ASGD needs param and state1 (ax)");
         for (const void* p : {(const void*)epi->param, (const void*)epi->state1, (const void*)epi->state2,
                               (const void*)epi->state3, (const void*)epi->base, (const void*)out, acc_in})
             if (misaligned(p)) throw Error("epilogue/out/acc_in pointers must be 16-byte aligned");

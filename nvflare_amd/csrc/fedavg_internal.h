@@ -76,6 +76,7 @@ struct EpiParams {
     float bias_correction1, lr, rect;             // RAdam
     int rectified;                                // RAdam: rho_t > 5
     float etaminus, etaplus, ss_min, ss_max;      // Rprop
+    float decay, neg_eta, mu;                     // ASGD: 1 - lambd * eta, -eta, mu (averaging when != 1)
 };
 
 struct DequantLaunch {

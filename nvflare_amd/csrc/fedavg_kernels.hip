@@ -161,7 +161,7 @@ __global__ void __launch_bounds__(kBlock) fedavg_tiles_f32x4(const RowTableF32 t
 //   EPI_ADD_BASE  w = base + d                          full_model_shareable_generator.py:58-67
 //   EPI_SGD       torch _single_tensor_sgd on g = -d     app_opt/pt/fedopt.py:157-182
 //   EPI_ADAM      torch _single_tensor_adam on g = -d    torch/optim/adam.py:347-551
-//   EPI_ADAGRAD / RMSPROP / ADAMAX / NADAM / RADAM / RPROP   torch _single_tensor_{adagrad,...,rprop} on g = -d
+//   EPI_ADAGRAD / RMSPROP / ADAMAX / NADAM / RADAM / RPROP / ASGD   torch _single_tensor_{adagrad,...,asgd} on g = -d
 // Per parameter: 4K bytes of client reads + 12 B (p, m, v) read + 12 B written for Adam, so the
 // optimizer costs one pass instead of the reference's separate aggregate / H2D / step / D2H round trip.
 // Rounding sequence pinned against torch CPU by tests/test_fedopt_oracle.py (fma for add(alpha), lerp
@@ -193,7 +193,7 @@ __device__ __forceinline__ EpiIn epi_load(const EpiParams& E, const int64_t i) {
     } else if constexpr (EPI == FEDAVG_EPI_SGD) {
         in.a = load4<true>(reinterpret_cast<const f32x4*>(E.param) + i);
         if (E.has_momentum && !E.first_step) in.b = load4<true>(reinterpret_cast<const f32x4*>(E.state1) + i);
-    } else if constexpr (EPI == FEDAVG_EPI_ADAGRAD) {
+    } else if constexpr (EPI == FEDAVG_EPI_ADAGRAD || EPI == FEDAVG_EPI_ASGD) {
         in.a = load4<true>(reinterpret_cast<const f32x4*>(E.param) + i);
         in.b = load4<true>(reinterpret_cast<const f32x4*>(E.state1) + i);
     } else if constexpr (EPI == FEDAVG_EPI_RMSPROP) {
@@ -293,6 +293,20 @@ __device__ __forceinline__ void epilogue4(const EpiParams& E, const int64_t i, c
         store4<true>(p4, p);
         store4<true>(reinterpret_cast<f32x4*>(E.state1) + i, m);
         store4<true>(reinterpret_cast<f32x4*>(E.state2) + i, u);
+    } else if constexpr (EPI == FEDAVG_EPI_ASGD) {
+        f32x4 p = in.a;
+        f32x4 ax = in.b;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            float g = E.maximize ? d[c] : -d[c];
+            if (E.has_weight_decay) g = __builtin_fmaf(p[c], E.weight_decay, g);  // grad.add(param, alpha=wd)
+            float pv = p[c] * E.decay;                                             // param.mul_(1 - lambd * eta)
+            pv = __builtin_fmaf(g, E.neg_eta, pv);                                 // param.add_(grad, alpha=-eta)
+            ax[c] = E.mu != 1.0f ? ax[c] + (pv - ax[c]) * E.mu : pv;               // ax.add_(p.sub(ax).mul_(mu)) | copy_
+            p[c] = pv;
+        }
+        store4<true>(p4, p);
+        store4<true>(reinterpret_cast<f32x4*>(E.state1) + i, ax);
     } else if constexpr (EPI == FEDAVG_EPI_RPROP) {
         f32x4 p = in.a;
         f32x4 prev = in.b;
@@ -763,6 +777,10 @@ static hipError_t launch_epi_p(const TileLaunch& L, const EpiParams& E, hipStrea
             break;
         case FEDAVG_EPI_RPROP:
             hipLaunchKernelGGL((fedavg_tiles_epi_f32x4<OP, FIN, ACC_IN, FEDAVG_EPI_RPROP, PRE>), dim3(L.grid),
+                               dim3(kBlock), 0, s, L.tab, L.k, L.tstride4, ai, o, L.b4, L.e4, L.fin_val, E);
+            break;
+        case FEDAVG_EPI_ASGD:
+            hipLaunchKernelGGL((fedavg_tiles_epi_f32x4<OP, FIN, ACC_IN, FEDAVG_EPI_ASGD, PRE>), dim3(L.grid),
                                dim3(kBlock), 0, s, L.tab, L.k, L.tstride4, ai, o, L.b4, L.e4, L.fin_val, E);
             break;
         default:

@@ -121,6 +121,7 @@ void oracle_synth_fill_f32(uint64_t seed, uint64_t row, const uint64_t* cols, si
  *   NADAM     torch/optim/nadam.py _single_tensor_nadam (m exp_avg, v exp_avg_sq; mu_product passed in)
  *   RADAM     torch/optim/radam.py _single_tensor_radam (m exp_avg, v exp_avg_sq)
  *   RPROP     torch/optim/rprop.py _single_tensor_rprop (m prev, v step_size filled with lr before step 1)
+ *   ASGD      torch/optim/asgd.py _single_tensor_asgd (m ax; eta and mu passed in)
  *   ADAM      torch/optim/adam.py _single_tensor_adam (:347-551) on g = -1.0 * d; amsgrad divides by
  *             sqrt(vmax), vmax = torch.maximum(vmax, v) kept as a third state
  * Rounding sequence pinned against torch 2.10 CPU (tests/test_fedopt_oracle.py):
@@ -133,7 +134,7 @@ void oracle_synth_fill_f32(uint64_t seed, uint64_t row, const uint64_t* cols, si
  * ------------------------------------------------------------------------------------------------ */
 enum { ORACLE_EPI_NONE = 0, ORACLE_EPI_ADD_BASE = 1, ORACLE_EPI_SGD = 2, ORACLE_EPI_ADAM = 3, ORACLE_EPI_ADAGRAD = 4,
        ORACLE_EPI_RMSPROP = 5, ORACLE_EPI_ADAMAX = 6, ORACLE_EPI_NADAM = 7, ORACLE_EPI_RADAM = 8,
-       ORACLE_EPI_RPROP = 9 };
+       ORACLE_EPI_RPROP = 9, ORACLE_EPI_ASGD = 10 };
 
 typedef struct {
     int kind;
@@ -150,6 +151,7 @@ typedef struct {
     double momentum_decay;                        /* NAdam */
     double mu_product;                            /* NAdam: fp32 mu_product state before this step */
     double etaminus, etaplus, step_size_min, step_size_max; /* Rprop */
+    double eta, mu, lambd;                        /* ASGD: fp32 eta / mu states before this step */
 } oracle_epilogue;
 
 /* torch.maximum: a NaN operand is the result */
@@ -217,6 +219,14 @@ void oracle_epilogue_apply(const float* delta, size_t n, const oracle_epilogue* 
             v[i] = max_torch(v[i] * (float)epi->beta2, fabsf(g) + (float)epi->eps);    /* maximum(exp_inf.mul_(b2), |g|+eps) */
             const float neg_clr = (float)(-(epi->lr / (1.0 - pow(epi->beta1, epi->step))));
             p[i] = p[i] + (neg_clr * m[i]) / v[i];                                    /* addcdiv_(exp_avg, exp_inf, -clr) */
+        } else if (epi->kind == ORACLE_EPI_ASGD) { /* torch/optim/asgd.py _single_tensor_asgd, m = ax */
+            float g = epi->maximize ? d : -d;
+            if (epi->weight_decay != 0.0) g = fmaf(p[i], (float)epi->weight_decay, g);
+            float pv = p[i] * (float)(1.0 - epi->lambd * epi->eta);       /* param.mul_(1 - lambd * eta) */
+            pv = fmaf(g, (float)(-epi->eta), pv);                          /* param.add_(grad, alpha=-eta) */
+            const float mu = (float)epi->mu;
+            m[i] = mu != 1.0f ? m[i] + (pv - m[i]) * mu : pv;             /* ax.add_(p.sub(ax).mul_(mu)) / copy_ */
+            p[i] = pv;
         } else if (epi->kind == ORACLE_EPI_RPROP) { /* torch/optim/rprop.py _single_tensor_rprop */
             float g = epi->maximize ? d : -d;
             const float s = g * m[i];

@@ -244,7 +244,7 @@ def synth_weights(K: int):
 # ---------------------------------------------------------------------------------------------------
 # server-optimizer epilogues (rows a9/a10): see oracle_epilogue_apply in fedavg_oracle.c
 # ---------------------------------------------------------------------------------------------------
-EPI_NONE, EPI_ADD_BASE, EPI_SGD, EPI_ADAM, EPI_ADAGRAD, EPI_RMSPROP, EPI_ADAMAX, EPI_NADAM, EPI_RADAM, EPI_RPROP = range(10)
+EPI_NONE, EPI_ADD_BASE, EPI_SGD, EPI_ADAM, EPI_ADAGRAD, EPI_RMSPROP, EPI_ADAMAX, EPI_NADAM, EPI_RADAM, EPI_RPROP, EPI_ASGD = range(11)
 
 
 class _Epi(ctypes.Structure):
@@ -272,6 +272,9 @@ class _Epi(ctypes.Structure):
         ("etaplus", ctypes.c_double),
         ("step_size_min", ctypes.c_double),
         ("step_size_max", ctypes.c_double),
+        ("eta", ctypes.c_double),
+        ("mu", ctypes.c_double),
+        ("lambd", ctypes.c_double),
     ]
 
 

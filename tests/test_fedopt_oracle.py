@@ -285,3 +285,36 @@ def test_rprop_vs_torch(oracle, kw):
     assert same_bits(prev, st["prev"].numpy()), "prev"
     assert same_bits(ss, st["step_size"].numpy()), "step_size"
     assert same_bits(p, tp), "param"
+
+
+def asgd_host_states(lr, lambd, alpha, t0, step):
+    """torch/optim/asgd.py: eta and mu after step ``step`` (fp32 state tensors)."""
+    eta = np.float32(lr / ((1 + lambd * lr * step) ** alpha))
+    mu = np.float32(1 / max(1, step - t0))
+    return eta, mu
+
+
+@pytest.mark.parametrize("kw", [
+    dict(lr=1e-2),
+    dict(lr=5e-2, lambd=1e-2, alpha=0.5, t0=2, weight_decay=1e-3),
+    dict(lr=1e-2, t0=0, maximize=True),
+])
+def test_asgd_vs_torch(oracle, kw):
+    """torch/optim/asgd.py _single_tensor_asgd (no sqrt): params and ax bit-exact against torch CPU, eta / mu
+    host states too; t0 small enough that the averaging branch (mu != 1) is taken."""
+    rng = np.random.default_rng(10)
+    n = 200_003
+    p0 = rng.standard_normal(n).astype(np.float32)
+    deltas = [(rng.standard_normal(n) * 0.01).astype(np.float32) for _ in range(6)]
+    tp, st = _torch_steps(torch.optim.ASGD, kw, p0, deltas)
+    p, ax = p0.copy(), np.zeros(n, np.float32)
+    lr, lambd, alpha, t0 = kw["lr"], kw.get("lambd", 1e-4), kw.get("alpha", 0.75), kw.get("t0", 1e6)
+    eta, mu = np.float32(lr), np.float32(1.0)
+    for k, d in enumerate(deltas):
+        oracle.epilogue_apply(d, oracle.EPI_ASGD, p=p, m=ax, eta=float(eta), mu=float(mu), lambd=lambd,
+                              weight_decay=kw.get("weight_decay", 0.0), maximize=int(kw.get("maximize", False)),
+                              step=float(k + 1))
+        eta, mu = asgd_host_states(lr, lambd, alpha, t0, k + 1)
+    assert same_bits(np.array(eta), st["eta"].numpy()) and same_bits(np.array(mu), st["mu"].numpy())
+    assert same_bits(ax, st["ax"].numpy()), "ax"
+    assert same_bits(p, tp), "param"

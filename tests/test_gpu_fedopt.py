@@ -426,6 +426,41 @@ def test_rprop_epilogue(ctx, oracle, K, hp):
     assert len(np.unique(ss)) > 3  # several step-size histories were exercised
 
 
+@pytest.mark.parametrize("K,hp", [(5, dict(lambd=1e-4, alpha=0.75, t0=1e6)),
+                                  (3, dict(lambd=1e-2, alpha=0.5, t0=1, weight_decay=1e-3, maximize=1)),
+                                  (0, dict(lambd=1e-4, alpha=0.75, t0=0))])
+def test_asgd_epilogue(ctx, oracle, K, hp):
+    """ASGD: p = fma(g, -eta, p * (1 - lambd * eta)); ax = ax + (p - ax) * mu (or p when mu == 1).  Four steps
+    with the host eta / mu sequence, bit-exact vs the oracle (itself bit-exact vs torch CPU)."""
+    from test_fedopt_oracle import asgd_host_states
+
+    rng = np.random.default_rng(170 + K)
+    n = 3 * TILE + 12
+    p = rng.standard_normal(n).astype(np.float32)
+    ax = np.zeros(n, np.float32)
+    lr = 1e-2
+    eta, mu = np.float32(lr), np.float32(1.0)
+    for step in range(4):
+        rows = [(rng.standard_normal(n) * 0.05).astype(np.float32) for _ in range(K)]
+        ws = [float(1 + (37 * k) % 100) for k in range(K)]
+        delta = (rng.standard_normal(n) * 0.05).astype(np.float32) if K == 0 else None
+        dev = _Dev(ctx, rows, n)
+        kw = dict(lambd=hp["lambd"], weight_decay=hp.get("weight_decay", 0.0), maximize=hp.get("maximize", 0))
+        try:
+            e = _epi(10, param=dev.buf("p", p), state1=dev.buf("ax", ax), eta=float(eta), mu=float(mu),
+                     step=float(step + 1), **kw)
+            acc_ptr = dev.buf("acc", delta) if K == 0 else None
+            ctx.accumulate_tiled_epi(dev.bases, ws, TILE, dev.lay.tile_stride, 0, dev.n4, None, 1,
+                                     2 if K else 0, _sum(ws) if K else 1.0, e, acc_in_ptr=acc_ptr)
+            d = oracle.fedavg_c(rows, ws, oracle.MODE_TORCH, nthreads=8) if K else delta
+            oracle.epilogue_apply(d, oracle.EPI_ASGD, p=p, m=ax, eta=float(eta), mu=float(mu),
+                                  step=float(step + 1), **kw)
+            assert same_bits(dev.get("p"), p) and same_bits(dev.get("ax"), ax), step
+        finally:
+            dev.close()
+        eta, mu = asgd_host_states(lr, hp["lambd"], hp["alpha"], hp["t0"], step + 1)
+
+
 @pytest.mark.parametrize("K,hp", [(6, dict(lr=1e-2, alpha=0.99, eps=1e-8)),
                                   (3, dict(lr=1e-2, alpha=0.9, eps=1e-6, momentum=0.9, weight_decay=1e-3)),
                                   (2, dict(lr=1e-3, alpha=0.95, eps=1e-8, centered=1, momentum=0.5, maximize=1)),

@@ -44,6 +44,7 @@ def _reference_update(model, opt, sched, global_params, diff):
     (torch.optim.Adamax, dict(lr=2e-3, weight_decay=1e-3), ("StepLR", dict(step_size=1, gamma=0.5))),
     (torch.optim.NAdam, dict(lr=2e-3, weight_decay=1e-3, momentum_decay=5e-3), None),
     (torch.optim.Rprop, dict(lr=1e-2, etas=(0.4, 1.3)), None),
+    (torch.optim.ASGD, dict(lr=1e-2, lambd=1e-2, t0=1, weight_decay=1e-3), ("StepLR", dict(step_size=1, gamma=0.5))),
     (torch.optim.RAdam, dict(lr=1e-2, betas=(0.8, 0.9), decoupled_weight_decay=True, weight_decay=1e-2),
      ("StepLR", dict(step_size=1, gamma=0.5))),
 ])

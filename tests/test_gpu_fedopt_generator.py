@@ -205,14 +205,14 @@ def test_fedopt_generator_nadam_radam_state(opt_name):
 
 def test_fedopt_generator_rejects_unsupported_optimizer():
     model = fedopt_model()
-    gen = PTFedOptModelShareableGenerator(optimizer_args={"path": "torch.optim.ASGD", "args": {"lr": 1e-3}},
+    gen = PTFedOptModelShareableGenerator(optimizer_args={"path": "torch.optim.LBFGS", "args": {"lr": 1e-3}},
                                           source_model=model, device=0)
     gen.handle_event(EventType.START_RUN, FLContext())
     w = {k: v.detach().cpu().numpy().copy() for k, v in model.state_dict().items()}
     fl_ctx = FLContext()
     fl_ctx.set_prop(AppConstants.GLOBAL_MODEL, make_model_learnable(w, {}))
     diff = {"lin1.weight": np.zeros((64, 7), np.float32)}
-    with pytest.raises(NotImplementedError, match="ASGD"):
+    with pytest.raises(NotImplementedError, match="LBFGS"):
         gen.shareable_to_learnable(DXO(DataKind.WEIGHT_DIFF, data=diff).to_shareable(), fl_ctx)
 
 
