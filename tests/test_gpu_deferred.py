@@ -40,6 +40,12 @@ OPTS = {
                                                           "weight_decay": 1e-3}},
     "adam": {"path": "torch.optim.Adam", "args": {"lr": 1e-2, "betas": [0.8, 0.95], "eps": 1e-6}},
     "adamw": {"path": "torch.optim.AdamW", "args": {"lr": 1e-2, "weight_decay": 0.05}},
+    # optimizers with host-side per-parameter state (NAdam mu_product, ASGD eta / mu) or lazily made state (Rprop)
+    "nadam": {"path": "torch.optim.NAdam", "args": {"lr": 1e-2, "momentum_decay": 5e-3}},
+    "radam": {"path": "torch.optim.RAdam", "args": {"lr": 1e-2, "betas": [0.8, 0.9]}},
+    "adamax": {"path": "torch.optim.Adamax", "args": {"lr": 1e-2}},
+    "rprop": {"path": "torch.optim.Rprop", "args": {"lr": 1e-2}},
+    "asgd": {"path": "torch.optim.ASGD", "args": {"lr": 1e-2, "t0": 1}},
 }
 
 
