@@ -26,7 +26,9 @@
 extern "C" {
 #endif
 
-#define FEDAVG_ABI_VERSION 2
+/* Bumped whenever a struct layout or an entry point's signature changes (v3: Rprop / ASGD fields appended
+ * to struct fedavg_epilogue).  fedavg_struct_size() lets a binding check each struct's size as well. */
+#define FEDAVG_ABI_VERSION 3
 
 /* element types of client rows (in_dtype) and of the running sum / result (acc_dtype) */
 enum fedavg_dtype {
@@ -130,6 +132,9 @@ typedef struct fedavg_ctx fedavg_ctx;
 /* Last error message of the calling thread ("" if none). */
 const char* fedavg_last_error(void);
 int fedavg_abi_version(void);
+/* sizeof the ABI's structs as this library was compiled: which = 0 struct fedavg_epilogue,
+ * 1 struct fedavg_quant; 0 for any other value. */
+size_t fedavg_struct_size(int which);
 int fedavg_device_count(int* n);
 
 /* Handle bound to one HIP device: owns a compute stream, a copy stream, timing events and a pinned

@@ -41,7 +41,7 @@ FEDAVG_FIN_NONE = 0
 FEDAVG_FIN_SCALE = 1
 FEDAVG_FIN_DIV = 2
 
-ABI_VERSION = 2
+ABI_VERSION = 3  # include/nvflare_amd_fedavg.h FEDAVG_ABI_VERSION
 
 c_void_p = ctypes.c_void_p
 c_int = ctypes.c_int
@@ -161,7 +161,7 @@ _SIGNATURES = {
     "fedavg_gather_f32": [c_void_p, c_void_p, c_void_p, c_size_t, c_void_p],
     "fedavg_dequantize": [c_void_p, c_void_p, c_void_p, c_size_t, c_void_p, c_size_t, c_size_t, c_size_t],
 }
-EXPORTED = ["fedavg_last_error", "fedavg_abi_version", *_SIGNATURES.keys()]
+EXPORTED = ["fedavg_last_error", "fedavg_abi_version", "fedavg_struct_size", *_SIGNATURES.keys()]
 
 
 FEDAVG_EPI_NONE = 0
@@ -276,6 +276,12 @@ def load():
             fn.argtypes = argtypes
         if lib.fedavg_abi_version() != ABI_VERSION:
             raise FedAvgError(f"ABI mismatch: library {lib.fedavg_abi_version()} != python {ABI_VERSION}")
+        lib.fedavg_struct_size.restype = c_size_t
+        lib.fedavg_struct_size.argtypes = [c_int]
+        for which, struct in enumerate((Epilogue, Quant)):
+            if lib.fedavg_struct_size(which) != ctypes.sizeof(struct):
+                raise FedAvgError(f"ABI mismatch: library sizeof({struct.__name__}) = "
+                                  f"{lib.fedavg_struct_size(which)} != python {ctypes.sizeof(struct)}")
         _lib = lib
         return lib
 

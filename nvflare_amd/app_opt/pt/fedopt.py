@@ -75,19 +75,22 @@ def build_component_from_args(args: dict):
 
 
 class _Slot:
-    __slots__ = ("name", "param", "offset", "n", "step", "has_momentum_buffer", "mu_product", "eta", "mu")
+    __slots__ = ("name", "param", "offset", "n", "step", "has_momentum_buffer", "state_initialised", "mu_product",
+                 "eta", "mu")
 
     def __init__(self, name, param, offset, n):
         self.name, self.param, self.offset, self.n = name, param, offset, n
         self.step = 0.0
-        self.has_momentum_buffer = False
+        self.has_momentum_buffer = False  # SGD: torch holds a momentum_buffer for this parameter
+        self.state_initialised = False  # Rprop / ASGD: the state _init_group makes at the first step exists
         self.mu_product = np.float32(1.0)  # NAdam's fp32 state tensor, kept on the host
         self.eta = np.float32(0.0)  # ASGD's fp32 eta / mu state tensors, kept on the host
         self.mu = np.float32(1.0)
 
     def host_key(self) -> tuple:
         """Per-parameter host state a launch shares (runs group parameters whose keys are equal)."""
-        return (self.step, self.has_momentum_buffer, float(self.mu_product), float(self.eta), float(self.mu))
+        return (self.step, self.has_momentum_buffer, self.state_initialised, float(self.mu_product), float(self.eta),
+                float(self.mu))
 
 
 class DeviceServerOptimizer:
@@ -175,12 +178,12 @@ class DeviceServerOptimizer:
                     self.m[s.offset:s.offset + s.n].copy_(st["prev"].reshape(-1).to(dev))
                     self.v[s.offset:s.offset + s.n].copy_(st["step_size"].reshape(-1).to(dev))
                     s.step = float(st["step"])
-                    s.has_momentum_buffer = True  # Rprop: state initialised
+                    s.state_initialised = True
                 if "ax" in st:  # ASGD: ax -> m, eta / mu host scalars
                     self.m[s.offset:s.offset + s.n].copy_(st["ax"].reshape(-1).to(dev))
                     s.eta, s.mu = np.float32(float(st["eta"])), np.float32(float(st["mu"]))
                     s.step = float(st["step"])
-                    s.has_momentum_buffer = True  # ASGD: state initialised
+                    s.state_initialised = True
                 if "mu_product" in st:  # NAdam
                     s.mu_product = np.float32(float(st["mu_product"]))
                 if "sum" in st:  # Adagrad: state made at construction (initial_accumulator_value)
@@ -314,6 +317,7 @@ class DeviceServerOptimizer:
         with ``K = 0`` (the aggregated difference as ``acc_in``)."""
         groups = self._group_of()
         present = []
+        self._check_diffs(model_diff)  # before any state is made or any launch, as torch fails at param.grad = ...
         self._init_lazy_state(model_diff, groups)
         fused = self._fused_step(model_diff, groups)
         host_pieces, keep = [], []  # host differences: one pass through the pinned ring, not a copy per tensor
@@ -366,21 +370,38 @@ class DeviceServerOptimizer:
         self._advance(present, groups)
         return [s.name for s in self.slots if s.name in fused or s in present]
 
+    def _check_diffs(self, model_diff: Dict) -> None:
+        """The reference assigns every difference to ``param.grad`` before ``optimizer.step()``
+        (fedopt.py:157-182); torch refuses a grad of another dtype or size there, so a bad difference fails
+        the round before any optimizer state is made.  Checked on shape / dtype attributes (a deferred
+        aggregate is not materialised for it)."""
+        for s in self.slots:
+            if s.name not in model_diff:
+                continue
+            d = model_diff[s.name]
+            if not hasattr(d, "shape") or not hasattr(d, "dtype"):
+                d = np.asarray(d)
+            dt = d.dtype
+            if dt not in (torch.float32, np.dtype(np.float32)):
+                raise RuntimeError(f"assigned grad has data of a different type ({dt}) for {s.name!r}")
+            if tuple(d.shape) != tuple(s.param.shape):
+                raise RuntimeError(f"assigned grad has data of a different size for {s.name!r}")
+
     def _init_lazy_state(self, model_diff: Dict, groups: Dict[int, dict]) -> None:
         """Rprop and ASGD make their state at the first step (rprop.py / asgd.py ``_init_group``): Rprop prev = 0,
-        step_size = full_like(grad, lr); ASGD ax = 0, eta = lr (fp32), mu = 1."""
+        step_size = full_like(grad, lr); ASGD ax = 0, eta = lr (fp32), mu = 1.  Runs after ``_check_diffs``."""
         if self.kind not in (N.FEDAVG_EPI_RPROP, N.FEDAVG_EPI_ASGD):
             return
         with torch.no_grad():
             for s in self.slots:
-                if s.name in model_diff and not s.has_momentum_buffer:
+                if s.name in model_diff and not s.state_initialised:
                     lr = float(groups[id(s.param)]["lr"])
                     self.m[s.offset:s.offset + s.n].zero_()
                     if self.kind == N.FEDAVG_EPI_RPROP:
                         self.v[s.offset:s.offset + s.n].fill_(lr)
                     else:
                         s.eta, s.mu = np.float32(lr), np.float32(1.0)
-                    s.has_momentum_buffer = True
+                    s.state_initialised = True
 
     def _advance(self, stepped: List[_Slot], groups: Dict[int, dict]) -> None:
         for s in stepped:

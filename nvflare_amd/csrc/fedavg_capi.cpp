@@ -565,6 +565,17 @@ const char* fedavg_last_error(void) { return g_last_error.c_str(); }
 
 int fedavg_abi_version(void) { return FEDAVG_ABI_VERSION; }
 
+size_t fedavg_struct_size(int which) {
+    switch (which) {
+        case 0:
+            return sizeof(fedavg_epilogue);
+        case 1:
+            return sizeof(fedavg_quant);
+        default:
+            return 0;
+    }
+}
+
 int fedavg_device_count(int* n) {
     return guarded([&] {
         if (!n) throw Error("n is NULL");

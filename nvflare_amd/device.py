@@ -66,6 +66,19 @@ class TiledLayout:
         return f"TiledLayout(tile={self.tile}, slots={self.slots}, tile_stride={self.tile_stride})"
 
 
+class _Lease:
+    """Buffer owner of one ``HostArenaPool.take``: the handed-out array is made over this non-array object,
+    so numpy's collapse of a view's ``base`` chain stops at that array (it never skips to the pooled
+    storage).  Every slice, reshape and ``torch.from_numpy`` of it therefore references the handed-out
+    array, which dies exactly when the last of them does."""
+
+    __slots__ = ("storage", "__array_interface__")
+
+    def __init__(self, storage: np.ndarray):
+        self.storage = storage
+        self.__array_interface__ = storage.__array_interface__
+
+
 class HostArenaPool:
     """Host result arrays reused across rounds once nothing else references them.
 
@@ -73,12 +86,16 @@ class HostArenaPool:
     new arrays).  A fresh array costs a page fault per 4 KiB page during the D2H (≈150 ms single-threaded
     for 500 MB); the pool keeps the last ``depth`` arrays and hands one out again only when no view of it
     is alive.  In scatter-and-gather the previous round's result is still referenced while the next one is
-    computed, so ``depth`` = 3 lets round r reuse the array of round r - 2."""
+    computed, so ``depth`` = 3 lets round r reuse the array of round r - 2.
+
+    Liveness is tracked explicitly, not by reference-count arithmetic: every take() hands out a fresh
+    array over the pooled storage (through a ``_Lease``), and the storage is free again once that array's
+    weak reference is dead."""
 
     PIN_MIN_BYTES = 16 << 20  # smaller results are cheaper through the pinned ring than to register
 
     def __init__(self, depth: int = 3):
-        self._arrs: list = []
+        self._arrs: list = []  # [storage ndarray, weakref to the array last handed out over it]
         self._depth = depth
         self._lock = threading.Lock()
 
@@ -87,26 +104,29 @@ class HostArenaPool:
         through that context (once; it stays registered while the pool reuses it), so D2H copies into it
         run at the PCIe rate without the pinned ring's extra host copy; it is unregistered just before
         its memory is freed (when the pool has dropped it and no view of it is left)."""
-        import sys
-
         dtype = np.dtype(dtype)
         with self._lock:
             for i in range(len(self._arrs)):
-                a = self._arrs[i]
-                # references: the list, the local `a`, getrefcount's argument -> 3 = nobody else
-                if a.size == n and a.dtype == dtype and sys.getrefcount(a) <= 3:
-                    self._arrs.append(self._arrs.pop(i))  # most recently used last
-                    return a
-            a = np.empty(n, dtype=dtype)
-            if pin is not None and a.nbytes >= self.PIN_MIN_BYTES:
+                storage, ref = self._arrs[i]
+                if storage.size == n and storage.dtype == dtype and ref() is None:
+                    self._arrs.pop(i)
+                    return self._lease(storage)  # most recently used last
+            storage = np.empty(n, dtype=dtype)
+            if pin is not None and storage.nbytes >= self.PIN_MIN_BYTES:
                 try:
-                    pin.host_register(a)
+                    pin.host_register(storage)
                 except N.FedAvgError:  # e.g. a locked-memory limit: the copies go through the pinned ring
                     pass
-            self._arrs.append(a)
+            out = self._lease(storage)
             if len(self._arrs) > self._depth:
                 self._arrs.pop(0)
-            return a
+            return out
+
+    def _lease(self, storage: np.ndarray) -> np.ndarray:
+        arr = np.asarray(_Lease(storage))
+        assert isinstance(arr.base, _Lease) and arr.ctypes.data == storage.ctypes.data
+        self._arrs.append([storage, weakref.ref(arr)])
+        return arr
 
 
 class DeviceBuffer:

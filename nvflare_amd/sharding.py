@@ -75,8 +75,18 @@ class ShardedFedAvg:
 
     def add(self, items: List[Tuple[str, Any]], weight, weighted: bool) -> None:
         with self.lock:
+            # Each engine sees only flat slices, so a reshaped contribution with the same element count
+            # would pass every shard: check the shape here, for every item before any shard is staged,
+            # with the single-device engine's message (engine.py DeviceFedAvg._register_key).
+            new = {}
             for k, v in items:
-                self._shapes.setdefault(k, tuple(v.shape))
+                shape = tuple(v.shape)
+                first = self._shapes.get(k, new.get(k))
+                if first is not None and first != shape:
+                    raise ValueError(f"nvflare_amd: key {k!r} shape {shape} != first contribution's {first}")
+                new.setdefault(k, shape)
+            for k, shape in new.items():
+                self._shapes.setdefault(k, shape)
             futs = [self._pool.submit(eng.add, self._pieces(b, items), weight, weighted)
                     for b, eng in enumerate(self.engines)]
             for f in futs:

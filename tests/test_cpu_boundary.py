@@ -31,6 +31,10 @@ def test_library_builds_and_exports_header_symbols():
         assert hasattr(lib, name), name
     assert set(declared) == set(_native.EXPORTED)
     assert _native.load().fedavg_abi_version() == _native.ABI_VERSION
+    # struct layouts: the library's sizeof matches the ctypes mirrors (load() refuses a mismatch)
+    assert _native.load().fedavg_struct_size(0) == ctypes.sizeof(_native.Epilogue)
+    assert _native.load().fedavg_struct_size(1) == ctypes.sizeof(_native.Quant)
+    assert _native.load().fedavg_struct_size(7) == 0
 
 
 def test_library_is_gfx950_code_object():

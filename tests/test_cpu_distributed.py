@@ -109,3 +109,44 @@ def test_sharded_pieces_reassemble(oracle):
             if hi > lo:
                 parts.append(oracle.fedavg_c([d[k].reshape(-1)[lo:hi] for d in data], ws, oracle.MODE_NUMPY))
         assert np.array_equal(np.concatenate(parts).view(np.uint32), whole.view(np.uint32))
+
+
+def _fake_sharded(n_dev=3):
+    import threading
+    from concurrent.futures import ThreadPoolExecutor
+
+    from fake_device import fake_engine
+    from nvflare_amd.sharding import ShardedFedAvg
+
+    sh = ShardedFedAvg.__new__(ShardedFedAvg)  # engines on tests/fake_device (host memory)
+    sh.devices = list(range(n_dev))
+    sh.engines = [fake_engine() for _ in range(n_dev)]
+    sh.lock = threading.RLock()
+    sh._pool = ThreadPoolExecutor(max_workers=n_dev)
+    sh._shapes = {}
+    return sh
+
+
+def test_sharded_rejects_reshaped_contribution(oracle):
+    """A later contribution with the first one's element count but another shape raises the single-device
+    engine's ValueError, and stages nothing on any shard (sharding.py shape check)."""
+    sh = _fake_sharded()
+    rng = np.random.default_rng(1)
+    a0 = rng.standard_normal((64, 7)).astype(np.float32)
+    b0 = rng.standard_normal(9000).astype(np.float32)
+    sh.add([("a", a0), ("b", b0)], 1.0, True)
+    staged = [len(e.ctx.launches) for e in sh.engines], [dict(e.stats) for e in sh.engines]
+    bad = rng.standard_normal((7, 64)).astype(np.float32)
+    with pytest.raises(ValueError, match="shape"):
+        sh.add([("b", b0), ("a", bad)], 2.0, True)  # the good item first: it must not be staged either
+    assert ([len(e.ctx.launches) for e in sh.engines], [dict(e.stats) for e in sh.engines]) == staged
+    with pytest.raises(ValueError, match="shape"):
+        sh.add([("c", b0), ("c", b0.reshape(90, 100))], 2.0, True)  # two shapes for a new key in one call
+    assert "c" not in sh._shapes
+    sh.add([("a", a0 * 2), ("b", b0)], 3.0, True)
+    res = sh.result()
+    assert res["a"].shape == (64, 7)
+    exp = oracle.fedavg_c([a0.reshape(-1), (a0 * 2).reshape(-1)], [1.0, 3.0], oracle.MODE_NUMPY)
+    assert np.array_equal(res["a"].reshape(-1).view(np.uint32), exp.view(np.uint32))
+    sh._pool.shutdown()
+

@@ -65,3 +65,30 @@ def test_shareable_checks_panic_before_any_device_work():
     g.shareable_to_learnable(DXO(DataKind.WEIGHT_DIFF, data={}).to_shareable(), ctx)
     assert p.reasons[-1] == "No global base model!"
     ctx.set_prop(AppConstants.GLOBAL_MODEL, make_model_learnable({}, {}))
+
+
+@pytest.mark.parametrize("kind", ["Rprop", "ASGD"])
+def test_bad_difference_fails_before_lazy_state(kind):
+    """A difference torch would refuse at ``param.grad = ...`` (other dtype / size) fails the step before
+    Rprop / ASGD state is made (fedopt.py lazy init ran ahead of the checks)."""
+    from nvflare_amd import _native as N
+    from nvflare_amd.app_opt.pt.fedopt import DeviceServerOptimizer, _Slot
+
+    a = torch.nn.Parameter(torch.zeros(3, 4))
+    b = torch.nn.Parameter(torch.zeros(5))
+    opt = getattr(torch.optim, kind)([a, b], lr=0.1)
+    so = DeviceServerOptimizer.__new__(DeviceServerOptimizer)  # host logic only: no device buffers
+    so.optimizer = opt
+    so.kind = N.FEDAVG_EPI_RPROP if kind == "Rprop" else N.FEDAVG_EPI_ASGD
+    so.slots = [_Slot("a", a, 0, 12), _Slot("b", b, 64, 5)]
+    so.by_name = {s.name: s for s in so.slots}
+    bad_cases = [
+        {"a": np.zeros((3, 4), np.float32), "b": np.zeros(5, np.float64)},  # dtype
+        {"a": np.zeros((4, 3), np.float32), "b": np.zeros(5, np.float32)},  # size
+        {"a": torch.zeros(3, 4, dtype=torch.float16)},
+    ]
+    for diff in bad_cases:
+        with pytest.raises(RuntimeError, match="assigned grad has data of a different"):
+            so.step(diff)
+        assert not any(s.state_initialised for s in so.slots)
+        assert all(s.step == 0.0 for s in so.slots)

@@ -2,7 +2,7 @@
 # line and a rocprofv3 kernel-trace of the same bench command.  Every GPU step has its own time limit and
 # `set -e` ends the script at the first failure.
 set -e
-OUT=gpurun_out/full_check
+OUT=${1:-gpurun_out/full_check}
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > "$OUT/pytest_gpu.log" 2>&1
