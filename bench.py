@@ -10,11 +10,12 @@ torch-mode arithmetic by default).  Inputs are resident in HBM before the timed 
                                                            # 1e9-param bucket, no data-path collective
 
 Prints ONE JSON line (rank 0).  value = GiB/s aggregated = 4*K*P*N*steps / t / 2^30 with t the max over
-ranks of the barrier+synchronize bracketed wall time.  roofline.achieved uses the algorithmic bytes
-(4*K*P + 4*P per launch) over the average kernel duration measured with HIP events on the stream the
-kernel runs on.  cpu_baseline times the oracle restatement (torch CPU ops, all threads) on a bounded
-sample of the same workload, and the same leg spot-checks sampled device outputs bit-exactly against
-the oracle (test infrastructure; never the measured path).
+ranks of the barrier+synchronize bracketed wall time.  roofline.achieved uses the algorithmic bytes of one
+aggregation (4*K*P + 4*P) over its device time measured with HIP events on the stream the kernels run on
+(one aggregation = roofline.launches_per_step launches of the burst kernel; launch_us_avg is the
+per-launch time a rocprofv3 --stats average compares with).  cpu_baseline times the oracle restatement
+(torch CPU ops, all threads) on a bounded sample of the same workload, and the same leg spot-checks
+sampled device outputs bit-exactly against the oracle (test infrastructure; never the measured path).
 """
 
 from __future__ import annotations
@@ -39,9 +40,11 @@ def parse():
     ap.add_argument("--clients", type=int, default=64)
     ap.add_argument("--params", type=float, default=1e9, help="fp32 params per GPU bucket")
     ap.add_argument("--mode", choices=["torch", "numpy"], default="torch")
-    ap.add_argument("--blocks-per-cu", type=int, default=0, help="0 = library default (2)")
+    ap.add_argument("--blocks-per-cu", type=int, default=0,
+                    help="0 = library default (burst kernel: 1 at >= 16 clients, else 2; others 2)")
     ap.add_argument("--unroll", type=int, default=0, help="0 = library default (4)")
-    ap.add_argument("--variant", type=int, default=0, help="cache policy bits (0 = nontemporal loads+stores)")
+    ap.add_argument("--variant", type=int, default=0,
+                    help="kernel variant bits (include/nvflare_amd_fedavg.h fedavg_set_variant; 0 = burst kernel)")
     ap.add_argument("--tile", type=int, default=4096, help="slab tile width (elements)")
     ap.add_argument("--epilogue", choices=["none", "add_base", "sgd", "adam", "adamax", "nadam", "radam"], default="none",
                     help="fused server update (config 5 = adam: FedOpt Adam on the aggregated deltas)")
@@ -259,6 +262,7 @@ def main():
         step()
     barrier_sync(world, ctx)
 
+    n_launch0 = ctx.launch_count()
     ctx.timing_begin()
     t0 = time.perf_counter()
     for _ in range(args.steps):
@@ -266,6 +270,7 @@ def main():
     barrier_sync(world, ctx)
     t1 = time.perf_counter()
     ev_ms = ctx.timing_end()
+    launches_per_step = (ctx.launch_count() - n_launch0) / args.steps
 
     wall = max_over_ranks(world, t1 - t0)
     kernel_ms = ev_ms / args.steps
@@ -306,6 +311,9 @@ def main():
                 "mode": args.mode,
                 "parallelism": f"param-bucket shards x{world}, no data-path collective",
                 "layout": f"tiled slab, {lay.tile}-element tiles x {K} slots",
+                "kernel": ("fedavg_tiles_burst_f32x4 (results staged in registers, stored as chip-wide bursts; "
+                           "8 tiles per block per launch)" if epi is None and args.variant & 11 == 0
+                           else "fedavg_tiles_epi_f32x4" if epi is not None else "fedavg_tiles_f32x4"),
             },
             "pct_hbm_peak": round(100.0 * achieved / HBM_PEAK_GBS, 2),
             "roofline": {
@@ -319,6 +327,11 @@ def main():
                 "kernel_ms_avg": round(kernel_ms, 4),
                 "kernel_ms_avg_max_rank": round(kernel_ms_max, 4),
                 "alg_bytes_per_launch": alg_bytes_launch,
+                # one aggregation = launches_per_step kernel launches (the burst kernel: one per 8 tiles per
+                # block); kernel_ms_avg and alg_bytes_per_launch are per aggregation, launch_us_avg is the
+                # per-launch figure a rocprofv3 --stats average compares with
+                "launches_per_step": launches_per_step,
+                "launch_us_avg": round(kernel_ms * 1e3 / max(launches_per_step, 1), 2),
             },
         }
         if "cpu_baseline" in extra:

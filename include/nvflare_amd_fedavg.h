@@ -26,9 +26,9 @@
 extern "C" {
 #endif
 
-/* Bumped whenever a struct layout or an entry point's signature changes (v3: Rprop / ASGD fields appended
- * to struct fedavg_epilogue).  fedavg_struct_size() lets a binding check each struct's size as well. */
-#define FEDAVG_ABI_VERSION 3
+/* Bumped whenever a struct layout or an entry point changes (v3: Rprop / ASGD fields appended to struct
+ * fedavg_epilogue; v4: fedavg_launch_count).  fedavg_struct_size() lets a binding check each struct's size as well. */
+#define FEDAVG_ABI_VERSION 4
 
 /* element types of client rows (in_dtype) and of the running sum / result (acc_dtype) */
 enum fedavg_dtype {
@@ -266,12 +266,19 @@ int fedavg_last_kernel_ms(fedavg_ctx* ctx, float* ms);
 int fedavg_timing_begin(fedavg_ctx* ctx);
 int fedavg_timing_end(fedavg_ctx* ctx, float* ms);
 
-/* Launch tuning (0 = default): blocks per CU of the streaming kernel (default 2), clients whose loads
- * are issued together (4 or 8, default 4). */
+/* Aggregation / epilogue / dequantization kernel launches issued on the context's compute stream so far.
+ * One fedavg_accumulate* call may issue several (the burst kernel: one per 8 tiles per block); relates a
+ * profiler's per-launch durations to per-call times. */
+int fedavg_launch_count(fedavg_ctx* ctx, uint64_t* n);
+/* Launch tuning (0 = default): blocks per CU (default: each kernel's own -- 1 for the burst aggregation
+ * kernel at >= 16 clients, 2 otherwise), clients whose loads are issued together (4 or 8, default 4). */
 int fedavg_set_launch(fedavg_ctx* ctx, int blocks_per_cu, int unroll);
-/* Streaming-kernel cache policy: bit 0 = temporal (cached) client loads, bit 1 = temporal result stores
- * (default 0: both nontemporal -- every byte is touched once); bit 2 = epilogue kernel software-pipelined
- * across tiles (the next tile's first client loads overlap the epilogue). */
+/* Kernel variants (default 0: the plain aggregation stages each block's results in registers and stores
+ * them as chip-wide bursts, one launch per 8 tiles per block; every load and store nontemporal).
+ * bit 3 = plain aggregation with each tile's results stored as it finishes (the round-1 kernel);
+ * bit 0 / bit 1 = that kernel with temporal client loads / temporal result stores (imply bit 3);
+ * bit 2 = epilogue kernel software-pipelined across tiles (the next tile's first client loads overlap
+ * the epilogue).  Results are bit-identical in every variant. */
 int fedavg_set_variant(fedavg_ctx* ctx, int variant);
 /* Tile width used by fedavg_accumulate for contiguous rows (default 4096 elements). */
 int fedavg_set_tile(fedavg_ctx* ctx, int tile_elems);

@@ -7,6 +7,7 @@ from __future__ import annotations
 
 import os
 import subprocess
+from concurrent.futures import ThreadPoolExecutor
 
 PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG)
@@ -14,14 +15,19 @@ CSRC = os.path.join(PKG, "csrc")
 LIB_DIR = os.path.join(PKG, "lib")
 LIB_NAME = "libnvflare_amd_fedavg.so"
 LIB_PATH = os.path.join(LIB_DIR, LIB_NAME)
-SOURCES = ["fedavg_kernels.hip", "fedavg_narrow.hip", "fedavg_dequant.hip", "fedavg_capi.cpp"]
-HEADERS = ["fedavg_internal.h"]
+# the fp32 tile kernels are instantiated per arithmetic mode in their own translation units so that the
+# objects compile in parallel (one hipcc per source), then link into one shared library
+SOURCES = ["fedavg_tiles_numpy.hip", "fedavg_tiles_torch.hip", "fedavg_tiles_unweighted.hip",
+           "fedavg_epi_numpy.hip", "fedavg_epi_torch.hip", "fedavg_epi_unweighted.hip",
+           "fedavg_kernels.hip", "fedavg_narrow.hip", "fedavg_dequant.hip", "fedavg_capi.cpp"]
+HEADERS = ["fedavg_internal.h", "fedavg_arith.h", "fedavg_tiles.h", "fedavg_epi.h"]
+OBJ_DIR = os.path.join(PKG, "lib", "obj")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 
 # -ffp-contract=off: the numpy-mode multiply and add must round separately (bit parity with the
 # reference); the torch mode uses explicit fma builtins.  No fast-math: IEEE division, denormals kept.
-FLAGS = ["-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off", "-fno-fast-math", f"--offload-arch={ARCH}",
+FLAGS = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-fast-math", f"--offload-arch={ARCH}",
          "-Wall", "-Wno-unused-command-line-argument"]
 
 
@@ -38,15 +44,27 @@ def needs_build() -> bool:
     return any(os.path.getmtime(f) > t for f in _inputs())
 
 
-def build_library(force: bool = False, verbose: bool = False) -> str:
+def build_library(force: bool = False, verbose: bool = False, jobs: int = 0) -> str:
     if not force and not needs_build():
         return LIB_PATH
-    os.makedirs(LIB_DIR, exist_ok=True)
+    os.makedirs(OBJ_DIR, exist_ok=True)
+    inc = [f"-I{os.path.join(ROOT, 'include')}", f"-I{CSRC}"]
+
+    def compile_one(src: str) -> str:
+        obj = os.path.join(OBJ_DIR, src + ".o")
+        cmd = [HIPCC, *FLAGS, *inc, "-c", os.path.join(CSRC, src), "-o", obj]
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        subprocess.run(cmd, check=True)
+        return obj
+
+    jobs = jobs or min(len(SOURCES), max(1, min(16, os.cpu_count() or 1)))
+    with ThreadPoolExecutor(max_workers=jobs) as pool:
+        objs = list(pool.map(compile_one, SOURCES))
     tmp = LIB_PATH + ".tmp"
-    cmd = [HIPCC, *FLAGS, f"-I{os.path.join(ROOT, 'include')}", f"-I{CSRC}",
-           *[os.path.join(CSRC, s) for s in SOURCES], "-o", tmp, "-lpthread"]
+    cmd = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-o", tmp, "-lpthread"]
     if verbose:
-        print(" ".join(cmd))
+        print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)
     os.replace(tmp, LIB_PATH)
     return LIB_PATH

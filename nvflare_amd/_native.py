@@ -41,7 +41,7 @@ FEDAVG_FIN_NONE = 0
 FEDAVG_FIN_SCALE = 1
 FEDAVG_FIN_DIV = 2
 
-ABI_VERSION = 3  # include/nvflare_amd_fedavg.h FEDAVG_ABI_VERSION
+ABI_VERSION = 4  # include/nvflare_amd_fedavg.h FEDAVG_ABI_VERSION
 
 c_void_p = ctypes.c_void_p
 c_int = ctypes.c_int
@@ -155,6 +155,7 @@ _SIGNATURES = {
     "fedavg_timing_begin": [c_void_p],
     "fedavg_timing_end": [c_void_p, ctypes.POINTER(c_float)],
     "fedavg_set_launch": [c_void_p, c_int, c_int],
+    "fedavg_launch_count": [c_void_p, ctypes.POINTER(ctypes.c_uint64)],
     "fedavg_set_variant": [c_void_p, c_int],
     "fedavg_set_tile": [c_void_p, c_int],
     "fedavg_fill_synthetic_f32": [c_void_p, c_void_p, c_size_t, c_size_t, c_size_t, c_u64, c_u64, c_u64],

@@ -1,0 +1,82 @@
+// fedavg_arith.h -- per-element arithmetic of the reference, shared by the fp32 kernels (not installed).
+// numpy / torch / unweighted steps and finalisations of weighted_aggregation_helper.py:181-236, the
+// f32x4 forms, and the cache-policy load / store helpers.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "fedavg_internal.h"
+
+namespace fedavg {
+
+// ---------------------------------------------------------------------------------------------
+// per-element arithmetic
+// ---------------------------------------------------------------------------------------------
+template <int OP, typename T>
+__device__ __forceinline__ T first_op(T v, T w) {
+    if constexpr (OP == FEDAVG_OP_UNWEIGHTED) {
+        return v;
+    } else {
+        return v * w;  // one rounding (fp-contract off)
+    }
+}
+
+__device__ __forceinline__ float fma_t(float a, float b, float c) { return __builtin_fmaf(a, b, c); }
+__device__ __forceinline__ double fma_t(double a, double b, double c) { return __builtin_fma(a, b, c); }
+
+template <int OP, typename T>
+__device__ __forceinline__ T step_op(T acc, T v, T w) {
+    if constexpr (OP == FEDAVG_OP_TORCH) {
+        return fma_t(v, w, acc);  // torch CPU add_(v, alpha=w): vec::fmadd, one rounding
+    } else if constexpr (OP == FEDAVG_OP_NUMPY) {
+        const T p = v * w;  // numpy: tmp = v * w (rounded) ...
+        return acc + p;     // ... then total + tmp (rounded)
+    } else {
+        return acc + v;
+    }
+}
+
+template <int FIN, typename T>
+__device__ __forceinline__ T fin_op(T acc, T s) {
+    if constexpr (FIN == FEDAVG_FIN_SCALE) {
+        return acc * s;  // numpy: total * (1.0 / count), s = acc_t(1.0 / count)
+    } else if constexpr (FIN == FEDAVG_FIN_DIV) {
+        return acc / s;  // torch: total.div_(count), correctly rounded IEEE division
+    } else {
+        return acc;
+    }
+}
+
+template <int OP>
+__device__ __forceinline__ f32x4 first4(f32x4 v, float w) {
+    return f32x4{first_op<OP>(v[0], w), first_op<OP>(v[1], w), first_op<OP>(v[2], w), first_op<OP>(v[3], w)};
+}
+template <int OP>
+__device__ __forceinline__ f32x4 step4(f32x4 a, f32x4 v, float w) {
+    return f32x4{step_op<OP>(a[0], v[0], w), step_op<OP>(a[1], v[1], w), step_op<OP>(a[2], v[2], w),
+                 step_op<OP>(a[3], v[3], w)};
+}
+template <int FIN>
+__device__ __forceinline__ f32x4 fin4(f32x4 a, float s) {
+    return f32x4{fin_op<FIN>(a[0], s), fin_op<FIN>(a[1], s), fin_op<FIN>(a[2], s), fin_op<FIN>(a[3], s)};
+}
+
+template <bool NT>
+__device__ __forceinline__ f32x4 load4(const f32x4* p) {
+    if constexpr (NT) {
+        return __builtin_nontemporal_load(p);
+    } else {
+        return *p;
+    }
+}
+template <bool NT>
+__device__ __forceinline__ void store4(f32x4* p, f32x4 v) {
+    if constexpr (NT) {
+        __builtin_nontemporal_store(v, p);
+    } else {
+        *p = v;
+    }
+}
+
+}  // namespace fedavg

@@ -191,7 +191,8 @@ struct fedavg_ctx {
     hipEvent_t ring_ev[kRingSlots] = {};
     bool ring_used[kRingSlots] = {};
     int ring_next = 0;
-    int blocks_per_cu = fedavg::kDefaultBlocksPerCu;
+    int blocks_per_cu = 0;  // 0: each kernel's own default (bpc())
+    uint64_t launches = 0;  // kernel launches issued on the compute stream (fedavg_launch_count)
     int unroll = fedavg::kDefaultUnroll;
     int variant = 0;
     int tile = fedavg::kDefaultTile;  // tile width of the contiguous-rows entry point
@@ -200,6 +201,7 @@ struct fedavg_ctx {
     std::vector<hipEvent_t> mark_pool;
 
     hipStream_t compute() const { return ext_stream ? ext_stream : own_stream; }
+    int bpc(int dflt = fedavg::kDefaultBlocksPerCu) const { return blocks_per_cu ? blocks_per_cu : dflt; }
     void activate() const { HIP_CHECK(hipSetDevice(device)); }
 };
 
@@ -353,7 +355,10 @@ void run_tiles(fedavg_ctx* ctx, const void* const* bases, const double* weights,
     L.b4 = b / 4;
     L.e4 = e / 4;
     const int64_t n_tiles = (L.e4 - 1) / L.tile4 - L.b4 / L.tile4 + 1;
-    L.grid = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)ctx->num_cus * ctx->blocks_per_cu, n_tiles));
+    const int bpc = fedavg::tiles_use_burst(L.tile4, L.unroll, L.variant)
+                        ? ctx->bpc(k_rows >= fedavg::kBurstOneBlockMinK ? 1 : 2)
+                        : ctx->bpc();
+    L.grid = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)ctx->num_cus * bpc, n_tiles));
     const float fv = (float)fin_scalar(fin, count);
     int k0 = 0;
     const float* cur_in = acc_in;
@@ -369,7 +374,7 @@ void run_tiles(fedavg_ctx* ctx, const void* const* bases, const double* weights,
         L.fin_val = fv;
         L.acc_in = cur_in;
         L.out = out;
-        HIP_CHECK(fedavg::launch_tiles_f32x4(L, s));
+        HIP_CHECK(fedavg::launch_tiles_f32x4(L, s, &ctx->launches));
         cur_in = out;
         k0 += kc;
     } while (k0 < k_rows);
@@ -469,6 +474,7 @@ void run_generic(fedavg_ctx* ctx, const void* const* rows, const double* weights
         const double fv = acc_dtype == FEDAVG_F32 ? (double)(float)fd : fd;
         HIP_CHECK(fedavg::launch_rows_generic(gt, kc, cur_in, o, n, in_dtype, acc_dtype, op,
                                               last ? fin : FEDAVG_FIN_NONE, fv, stream_grid(ctx, n), s));
+        ++ctx->launches;
         cur_in = o;
         k0 += kc;
     } while (k0 < k_rows);
@@ -514,8 +520,9 @@ void run_narrow(fedavg_ctx* ctx, const void* const* rows, const double* weights,
         // (4 by default: +2 % over 2, flat above -- profiles/r01/narrow_sweep.jsonl)
         const int64_t need = (n / 8 + fedavg::kBlock) / fedavg::kBlock;
         const int grid =
-            (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)ctx->num_cus * 2 * ctx->blocks_per_cu, need));
+            (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)ctx->num_cus * 2 * ctx->bpc(), need));
         HIP_CHECK(fedavg::launch_rows_narrow(t, kc, cur_in, out, n, fmt, op, last ? fin : FEDAVG_FIN_NONE, fv, grid, s));
+        ++ctx->launches;
         cur_in = out;
         k0 += kc;
     } while (k0 < k_rows);
@@ -528,7 +535,7 @@ void run_tiles_narrow(fedavg_ctx* ctx, const void* const* bases, const double* w
     const float fv = narrow_fin_value(fmt, fin, count);
     const int64_t T = fedavg::kTile16Elems;
     const int64_t n_tiles = (end - 1) / T - begin / T + 1;
-    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)ctx->num_cus * ctx->blocks_per_cu, n_tiles));
+    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)ctx->num_cus * ctx->bpc(), n_tiles));
     int k0 = 0;
     const void* cur_in = acc_in;
     do {
@@ -538,6 +545,7 @@ void run_tiles_narrow(fedavg_ctx* ctx, const void* const* bases, const double* w
         const bool last = k0 + kc >= k_rows;
         HIP_CHECK(fedavg::launch_tiles_narrow(t, kc, tstride, cur_in, out, begin, end, fmt, op,
                                               last ? fin : FEDAVG_FIN_NONE, fv, grid, s));
+        ++ctx->launches;
         cur_in = out;
         k0 += kc;
     } while (k0 < k_rows);
@@ -1047,7 +1055,7 @@ int fedavg_accumulate_tiled64(fedavg_ctx* ctx, const void* const* bases, const d
         TimingScope ts(ctx, s);
         const int64_t T = fedavg::kTile64Elems;
         const int64_t n_tiles = ((int64_t)end - 1) / T - (int64_t)begin / T + 1;
-        const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)ctx->num_cus * ctx->blocks_per_cu, n_tiles));
+        const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)ctx->num_cus * ctx->bpc(), n_tiles));
         const double fv = fin_scalar(fin, count);
         int k0 = 0;
         const void* cur_in = acc_in;
@@ -1062,6 +1070,7 @@ int fedavg_accumulate_tiled64(fedavg_ctx* ctx, const void* const* bases, const d
             const bool last = k0 + kc >= k_rows;
             HIP_CHECK(fedavg::launch_tiles_f64(t, kc, (int64_t)tile_stride, cur_in, out, (int64_t)begin, (int64_t)end,
                                                op, last ? fin : FEDAVG_FIN_NONE, fv, grid, s));
+            ++ctx->launches;
             cur_in = out;
             k0 += kc;
         } while (k0 < k_rows);
@@ -1156,11 +1165,11 @@ int fedavg_accumulate_tiled_epi(fedavg_ctx* ctx, const void* const* bases, const
         L.b4 = (int64_t)begin / 4;
         L.e4 = (int64_t)end / 4;
         const int64_t n_tiles = (L.e4 - 1) / L.tile4 - L.b4 / L.tile4 + 1;
-        L.grid = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)ctx->num_cus * ctx->blocks_per_cu, n_tiles));
+        L.grid = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)ctx->num_cus * ctx->bpc(), n_tiles));
         L.fin_val = (float)fin_scalar(fin, count);
         L.acc_in = cur_in;
         L.out = static_cast<float*>(out);
-        const hipError_t rc = fedavg::launch_tiles_epi_f32x4(L, make_epi(*epi), s);
+        const hipError_t rc = fedavg::launch_tiles_epi_f32x4(L, make_epi(*epi), s, &ctx->launches);
         if (scratch) HIP_CHECK(hipFreeAsync(scratch, s));
         HIP_CHECK(rc);
         ts.done();
@@ -1206,12 +1215,19 @@ int fedavg_timing_end(fedavg_ctx* ctx, float* ms) {
     });
 }
 
+int fedavg_launch_count(fedavg_ctx* ctx, uint64_t* n) {
+    return guarded([&] {
+        if (!ctx || !n) throw Error("NULL argument");
+        *n = ctx->launches;
+    });
+}
+
 int fedavg_set_launch(fedavg_ctx* ctx, int blocks_per_cu, int unroll) {
     return guarded([&] {
         if (!ctx) throw Error("ctx is NULL");
         if (blocks_per_cu < 0 || blocks_per_cu > 32) throw Error("blocks_per_cu out of range");
         if (unroll != 0 && unroll != 4 && unroll != 8) throw Error("unroll must be 0, 4 or 8");
-        ctx->blocks_per_cu = blocks_per_cu ? blocks_per_cu : fedavg::kDefaultBlocksPerCu;
+        ctx->blocks_per_cu = blocks_per_cu;
         ctx->unroll = unroll ? unroll : fedavg::kDefaultUnroll;
     });
 }
@@ -1219,7 +1235,7 @@ int fedavg_set_launch(fedavg_ctx* ctx, int blocks_per_cu, int unroll) {
 int fedavg_set_variant(fedavg_ctx* ctx, int variant) {
     return guarded([&] {
         if (!ctx) throw Error("ctx is NULL");
-        if (variant < 0 || variant > 7) throw Error("variant must be 0..7");
+        if (variant < 0 || variant > 15) throw Error("variant must be 0..15");
         ctx->variant = variant;
     });
 }
@@ -1267,6 +1283,7 @@ int fedavg_dequantize(fedavg_ctx* ctx, const fedavg_quant* qs, const void* q, si
         L.elem0 = (int64_t)logical_offset;
         L.grid = stream_grid(ctx, ((int64_t)n + 3) / 4);
         HIP_CHECK(fedavg::launch_dequant_f32(L, ctx->compute()));
+        ++ctx->launches;
     });
 }
 

@@ -1,0 +1,421 @@
+// fedavg_epi.h -- the fp32 tiled aggregation kernel with a fused server-optimizer epilogue (SURVEY.md section 8
+// rows a9 / a10) and its launch templates; included by fedavg_epi_{numpy,torch,unweighted}.hip.
+#pragma once
+
+#include "fedavg_arith.h"
+
+namespace fedavg {
+
+// ---------------------------------------------------------------------------------------------
+// The hot kernel with a server-optimizer EPILOGUE fused behind the finalisation (SURVEY.md section 8
+// rows a9/a10): d = fin(acc) is not stored but consumed per element by
+//   EPI_ADD_BASE  w = base + d                          full_model_shareable_generator.py:58-67
+//   EPI_SGD       torch _single_tensor_sgd on g = -d     app_opt/pt/fedopt.py:157-182
+//   EPI_ADAM      torch _single_tensor_adam on g = -d    torch/optim/adam.py:347-551
+//   EPI_ADAGRAD / RMSPROP / ADAMAX / NADAM / RADAM / RPROP / ASGD   torch _single_tensor_{adagrad,...,asgd} on g = -d
+// Per parameter: 4K bytes of client reads + 12 B (p, m, v) read + 12 B written for Adam, so the
+// optimizer costs one pass instead of the reference's separate aggregate / H2D / step / D2H round trip.
+// Rounding sequence pinned against torch CPU by tests/test_fedopt_oracle.py (fma for add(alpha), lerp
+// and addcmul; IEEE sqrt).  Geometry fixed at the tuned default (T = 4096, unroll 4, nontemporal).
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ float lerp_torch(float s, float e, float w, float w_m1) {
+    const float d = e - s;
+    return fabsf(w) < 0.5f ? __builtin_fmaf(w, d, s) : __builtin_fmaf(w_m1, d, e);
+}
+
+// Epilogue operands of one f32x4 column group, loaded at the START of the tile so their HBM latency
+// hides behind the client stream instead of stalling the wave after the last client.
+struct EpiIn {
+    f32x4 a, b, c, d;  // ADD_BASE: base | SGD: p, momentum buffer | ADAM: p, exp_avg, exp_avg_sq (, max_exp_avg_sq)
+};
+
+// torch.maximum: a NaN operand is the result
+__device__ __forceinline__ float max_torch(float a, float b) {
+    if (a != a) return a;
+    if (b != b) return b;
+    return a > b ? a : b;
+}
+
+template <int EPI>
+__device__ __forceinline__ EpiIn epi_load(const EpiParams& E, const int64_t i) {
+    EpiIn in;
+    if constexpr (EPI == FEDAVG_EPI_ADD_BASE) {
+        in.a = load4<true>(reinterpret_cast<const f32x4*>(E.base) + i);
+    } else if constexpr (EPI == FEDAVG_EPI_SGD) {
+        in.a = load4<true>(reinterpret_cast<const f32x4*>(E.param) + i);
+        if (E.has_momentum && !E.first_step) in.b = load4<true>(reinterpret_cast<const f32x4*>(E.state1) + i);
+    } else if constexpr (EPI == FEDAVG_EPI_ADAGRAD || EPI == FEDAVG_EPI_ASGD) {
+        in.a = load4<true>(reinterpret_cast<const f32x4*>(E.param) + i);
+        in.b = load4<true>(reinterpret_cast<const f32x4*>(E.state1) + i);
+    } else if constexpr (EPI == FEDAVG_EPI_RMSPROP) {
+        in.a = load4<true>(reinterpret_cast<const f32x4*>(E.param) + i);
+        in.b = load4<true>(reinterpret_cast<const f32x4*>(E.state1) + i);
+        if (E.has_momentum) in.c = load4<true>(reinterpret_cast<const f32x4*>(E.state2) + i);
+        if (E.centered) in.d = load4<true>(reinterpret_cast<const f32x4*>(E.state3) + i);
+    } else if constexpr (EPI == FEDAVG_EPI_ADAMAX || EPI == FEDAVG_EPI_RPROP) {
+        in.a = load4<true>(reinterpret_cast<const f32x4*>(E.param) + i);
+        in.b = load4<true>(reinterpret_cast<const f32x4*>(E.state1) + i);
+        in.c = load4<true>(reinterpret_cast<const f32x4*>(E.state2) + i);
+    } else {
+        in.a = load4<true>(reinterpret_cast<const f32x4*>(E.param) + i);
+        in.b = load4<true>(reinterpret_cast<const f32x4*>(E.state1) + i);
+        in.c = load4<true>(reinterpret_cast<const f32x4*>(E.state2) + i);
+        if (E.amsgrad) in.d = load4<true>(reinterpret_cast<const f32x4*>(E.state3) + i);
+    }
+    return in;
+}
+
+template <int EPI>
+__device__ __forceinline__ void epilogue4(const EpiParams& E, const int64_t i, const f32x4 d, const EpiIn& in,
+                                          f32x4* out) {
+    f32x4* p4 = reinterpret_cast<f32x4*>(E.param) + i;
+    if constexpr (EPI == FEDAVG_EPI_ADD_BASE) {
+        store4<true>(out + i, in.a + d);
+    } else if constexpr (EPI == FEDAVG_EPI_SGD) {
+        f32x4 p = in.a;
+        f32x4 buf = in.b;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            float g = E.maximize ? d[c] : -d[c];
+            if (E.has_weight_decay) g = __builtin_fmaf(p[c], E.weight_decay, g);
+            if (E.has_momentum) {
+                const float b = E.first_step ? g : __builtin_fmaf(g, E.one_minus_dampening, buf[c] * E.momentum);
+                buf[c] = b;
+                g = E.nesterov ? __builtin_fmaf(b, E.momentum, g) : b;
+            }
+            p[c] = __builtin_fmaf(g, E.neg_lr, p[c]);
+        }
+        store4<true>(p4, p);
+        if (E.has_momentum) store4<true>(reinterpret_cast<f32x4*>(E.state1) + i, buf);
+    } else if constexpr (EPI == FEDAVG_EPI_ADAGRAD) {
+        f32x4 p = in.a;
+        f32x4 sum = in.b;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            float g = E.maximize ? d[c] : -d[c];
+            if (E.has_weight_decay) g = __builtin_fmaf(p[c], E.weight_decay, g);  // grad.add(param, alpha=wd)
+            sum[c] = __builtin_fmaf(g, g, sum[c]);                                 // state_sum.addcmul_(g, g, value=1)
+            const float std_ = __builtin_sqrtf(sum[c]) + E.eps;                    // state_sum.sqrt().add_(eps)
+            p[c] = p[c] + (E.step_size_neg * g) / std_;                            // param.addcdiv_(g, std, value=-clr)
+        }
+        store4<true>(p4, p);
+        store4<true>(reinterpret_cast<f32x4*>(E.state1) + i, sum);
+    } else if constexpr (EPI == FEDAVG_EPI_RMSPROP) {
+        f32x4 p = in.a;
+        f32x4 sq = in.b;
+        f32x4 buf = in.c;
+        f32x4 ga = in.d;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            float g = E.maximize ? d[c] : -d[c];
+            if (E.has_weight_decay) g = __builtin_fmaf(p[c], E.weight_decay, g);       // grad.add(param, alpha=wd)
+            sq[c] = __builtin_fmaf(E.one_minus_beta2 * g, g, sq[c] * E.beta2);       // mul_(alpha).addcmul_(g, g, 1-alpha)
+            float avg;
+            if (E.centered) {
+                ga[c] = lerp_torch(ga[c], g, E.one_minus_beta1, E.one_minus_beta1_m1);  // grad_avg.lerp_(g, 1-alpha)
+                avg = __builtin_sqrtf(__builtin_fmaf(-ga[c], ga[c], sq[c]));          // addcmul(ga, ga, -1).sqrt_()
+            } else {
+                avg = __builtin_sqrtf(sq[c]);
+            }
+            avg = avg + E.eps;
+            if (E.has_momentum) {
+                buf[c] = buf[c] * E.momentum + g / avg;                               // buf.mul_(m).addcdiv_(g, avg)
+                p[c] = __builtin_fmaf(buf[c], E.neg_lr, p[c]);                        // param.add_(buf, alpha=-lr)
+            } else {
+                p[c] = p[c] + (E.neg_lr * g) / avg;                                   // param.addcdiv_(g, avg, -lr)
+            }
+        }
+        store4<true>(p4, p);
+        store4<true>(reinterpret_cast<f32x4*>(E.state1) + i, sq);
+        if (E.has_momentum) store4<true>(reinterpret_cast<f32x4*>(E.state2) + i, buf);
+        if (E.centered) store4<true>(reinterpret_cast<f32x4*>(E.state3) + i, ga);
+    } else if constexpr (EPI == FEDAVG_EPI_ADAMAX) {
+        f32x4 p = in.a;
+        f32x4 m = in.b;
+        f32x4 u = in.c;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            float g = E.maximize ? d[c] : -d[c];
+            if (E.has_weight_decay) g = __builtin_fmaf(p[c], E.weight_decay, g);     // grad.add(param, alpha=wd)
+            m[c] = lerp_torch(m[c], g, E.one_minus_beta1, E.one_minus_beta1_m1);      // exp_avg.lerp_(g, 1-beta1)
+            u[c] = max_torch(u[c] * E.beta2, fabsf(g) + E.eps);                      // maximum(exp_inf*b2, |g|+eps)
+            p[c] = p[c] + (E.step_size_neg * m[c]) / u[c];                            // addcdiv_(exp_avg, exp_inf, -clr)
+        }
+        store4<true>(p4, p);
+        store4<true>(reinterpret_cast<f32x4*>(E.state1) + i, m);
+        store4<true>(reinterpret_cast<f32x4*>(E.state2) + i, u);
+    } else if constexpr (EPI == FEDAVG_EPI_ASGD) {
+        f32x4 p = in.a;
+        f32x4 ax = in.b;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            float g = E.maximize ? d[c] : -d[c];
+            if (E.has_weight_decay) g = __builtin_fmaf(p[c], E.weight_decay, g);  // grad.add(param, alpha=wd)
+            float pv = p[c] * E.decay;                                             // param.mul_(1 - lambd * eta)
+            pv = __builtin_fmaf(g, E.neg_eta, pv);                                 // param.add_(grad, alpha=-eta)
+            ax[c] = E.mu != 1.0f ? ax[c] + (pv - ax[c]) * E.mu : pv;               // ax.add_(p.sub(ax).mul_(mu)) | copy_
+            p[c] = pv;
+        }
+        store4<true>(p4, p);
+        store4<true>(reinterpret_cast<f32x4*>(E.state1) + i, ax);
+    } else if constexpr (EPI == FEDAVG_EPI_RPROP) {
+        f32x4 p = in.a;
+        f32x4 prev = in.b;
+        f32x4 ss = in.c;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            float g = E.maximize ? d[c] : -d[c];
+            const float s = g * prev[c];                                   // grad.mul(prev).sign() -> etas / 1
+            const float sv = s > 0.0f ? E.etaplus : (s < 0.0f ? E.etaminus : (s == 0.0f ? 1.0f : s));
+            float st = ss[c] * sv;                                         // step_size.mul_(sign).clamp_(min, max)
+            st = st != st ? st : fminf(fmaxf(st, E.ss_min), E.ss_max);
+            if (sv == E.etaminus) g = 0.0f;                                // grad[sign.eq(etaminus)] = 0
+            const float sg = g > 0.0f ? 1.0f : (g < 0.0f ? -1.0f : (g == 0.0f ? 0.0f : g));
+            p[c] = __builtin_fmaf(-1.0f * sg, st, p[c]);                  // param.addcmul_(grad.sign(), step_size, -1)
+            prev[c] = g;                                                   // prev.copy_(grad)
+            ss[c] = st;
+        }
+        store4<true>(p4, p);
+        store4<true>(reinterpret_cast<f32x4*>(E.state1) + i, prev);
+        store4<true>(reinterpret_cast<f32x4*>(E.state2) + i, ss);
+    } else if constexpr (EPI == FEDAVG_EPI_NADAM || EPI == FEDAVG_EPI_RADAM) {
+        f32x4 p = in.a;
+        f32x4 m = in.b;
+        f32x4 v = in.c;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            float g = E.maximize ? d[c] : -d[c];
+            float pv = p[c];
+            if (E.has_weight_decay) {
+                if (E.decoupled_weight_decay) pv = pv * E.decoupled_scale;  // param.mul_(1 - lr * wd)
+                else g = __builtin_fmaf(pv, E.weight_decay, g);              // grad.add(param, alpha=wd)
+            }
+            m[c] = lerp_torch(m[c], g, E.one_minus_beta1, E.one_minus_beta1_m1);
+            v[c] = __builtin_fmaf(E.one_minus_beta2 * g, g, v[c] * E.beta2);
+            if constexpr (EPI == FEDAVG_EPI_NADAM) {
+                const float denom = __builtin_sqrtf(v[c] / E.bias_correction2) + E.eps;  // exp_avg_sq.div(bc2).sqrt().add_(eps)
+                pv = pv + (E.coef_grad * g) / denom;                                    // addcdiv_(grad, denom, value)
+                pv = pv + (E.coef_avg * m[c]) / denom;                                  // addcdiv_(exp_avg, denom, value)
+            } else {
+                float t = (m[c] / E.bias_correction1) * E.lr;                           // exp_avg / bc1 * lr
+                if (E.rectified) {
+                    const float a = (1.0f / (__builtin_sqrtf(v[c]) + E.eps)) * E.bias_correction2_sqrt;  // bc2**0.5 / (sqrt+eps)
+                    t = (t * a) * E.rect;
+                }
+                pv = __builtin_fmaf(t, -1.0f, pv);                                      // param.add_(..., alpha=-1)
+            }
+            p[c] = pv;
+        }
+        store4<true>(p4, p);
+        store4<true>(reinterpret_cast<f32x4*>(E.state1) + i, m);
+        store4<true>(reinterpret_cast<f32x4*>(E.state2) + i, v);
+    } else {  // EPI_ADAM
+        f32x4 p = in.a;
+        f32x4 m = in.b;
+        f32x4 v = in.c;
+        f32x4 vmax = in.d;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            float g = E.maximize ? d[c] : -d[c];
+            float pv = p[c];
+            if (E.has_weight_decay) {
+                if (E.decoupled_weight_decay) pv = pv * E.decoupled_scale;
+                else g = __builtin_fmaf(pv, E.weight_decay, g);
+            }
+            const float mm = lerp_torch(m[c], g, E.one_minus_beta1, E.one_minus_beta1_m1);
+            const float vv = __builtin_fmaf(E.one_minus_beta2 * g, g, v[c] * E.beta2);
+            float vden = vv;
+            if (E.amsgrad) {  // adam.py: torch.maximum(max_exp_avg_sq, exp_avg_sq, out=max_exp_avg_sq)
+                vmax[c] = max_torch(vmax[c], vv);
+                vden = vmax[c];
+            }
+            const float denom = __builtin_sqrtf(vden) / E.bias_correction2_sqrt + E.eps;
+            pv = pv + (E.step_size_neg * mm) / denom;
+            m[c] = mm;
+            v[c] = vv;
+            p[c] = pv;
+        }
+        store4<true>(p4, p);
+        store4<true>(reinterpret_cast<f32x4*>(E.state1) + i, m);
+        store4<true>(reinterpret_cast<f32x4*>(E.state2) + i, v);
+        if (E.amsgrad) store4<true>(reinterpret_cast<f32x4*>(E.state3) + i, vmax);
+    }
+}
+
+// PIPE: software-pipelined across tiles -- after the client loop of tile t the lane issues the epilogue
+// operand loads of t, then the first UNROLL client loads of its next tile, and only then waits for the
+// operands and runs the epilogue (ALU, three store streams) while the next tile's loads are in flight.
+template <int OP, int FIN, bool ACC_IN, int EPI, bool PIPE>
+__global__ void __launch_bounds__(kBlock) fedavg_tiles_epi_f32x4(const RowTableF32 tab, const int K,
+                                                                  const int64_t tstride4, const f32x4* acc_in,
+                                                                  f32x4* out, const int64_t b4, const int64_t e4,
+                                                                  const float fin_val, const EpiParams E) {
+    constexpr int UNROLL = kDefaultUnroll;
+    constexpr int CPL = kDefaultTile / (4 * kBlock);
+    constexpr int64_t T4 = (int64_t)CPL * kBlock;
+    const int64_t t_last = (e4 - 1) / T4;
+    const int g0 = PIPE ? (K < UNROLL ? K : UNROLL) : 0;  // clients carried over from the previous tile
+    f32x4 nxt[UNROLL][CPL];
+    int64_t t = b4 / T4 + blockIdx.x;
+    if constexpr (PIPE) {
+        if (t <= t_last) {
+            const int64_t off = t * tstride4 + threadIdx.x;
+#pragma unroll
+            for (int j = 0; j < UNROLL; ++j)
+                if (j < g0)
+#pragma unroll
+                    for (int c = 0; c < CPL; ++c) nxt[j][c] = load4<true>(tab.rows[j] + off + c * kBlock);
+        }
+    }
+    for (; t <= t_last; t += gridDim.x) {
+        const int64_t off = t * tstride4 + threadIdx.x;
+        const int64_t col = t * T4 + threadIdx.x;
+        f32x4 acc[CPL];
+        int k = 0;
+        if constexpr (ACC_IN) {
+#pragma unroll
+            for (int c = 0; c < CPL; ++c) {
+                const int64_t i = col + c * kBlock;
+                acc[c] = (i >= b4 && i < e4) ? load4<false>(acc_in + i) : f32x4{0, 0, 0, 0};
+            }
+        } else if constexpr (!PIPE) {
+            const f32x4* r = tab.rows[0] + off;
+#pragma unroll
+            for (int c = 0; c < CPL; ++c) acc[c] = first4<OP>(load4<true>(r + c * kBlock), tab.w[0]);
+            k = 1;
+        }
+        if constexpr (PIPE) {  // consume the carried group (clients 0 .. g0-1)
+#pragma unroll
+            for (int j = 0; j < UNROLL; ++j) {
+                if (j < g0) {
+#pragma unroll
+                    for (int c = 0; c < CPL; ++c) {
+                        if (!ACC_IN && j == 0) acc[c] = first4<OP>(nxt[0][c], tab.w[0]);
+                        else acc[c] = step4<OP>(acc[c], nxt[j][c], tab.w[j]);
+                    }
+                }
+            }
+            k = g0;
+        }
+        for (; k + UNROLL <= K; k += UNROLL) {
+            f32x4 v[UNROLL][CPL];
+#pragma unroll
+            for (int j = 0; j < UNROLL; ++j) {
+                const f32x4* r = tab.rows[k + j] + off;
+#pragma unroll
+                for (int c = 0; c < CPL; ++c) v[j][c] = load4<true>(r + c * kBlock);
+            }
+#pragma unroll
+            for (int j = 0; j < UNROLL; ++j)
+#pragma unroll
+                for (int c = 0; c < CPL; ++c) acc[c] = step4<OP>(acc[c], v[j][c], tab.w[k + j]);
+        }
+        for (; k < K; ++k) {
+            const f32x4* r = tab.rows[k] + off;
+#pragma unroll
+            for (int c = 0; c < CPL; ++c) acc[c] = step4<OP>(acc[c], load4<true>(r + c * kBlock), tab.w[k]);
+        }
+        EpiIn pre[CPL];
+#pragma unroll
+        for (int c = 0; c < CPL; ++c) {
+            const int64_t i = col + c * kBlock;
+            if (i >= b4 && i < e4) pre[c] = epi_load<EPI>(E, i);
+        }
+        if constexpr (PIPE) {
+            const int64_t tn = t + gridDim.x;
+            if (tn <= t_last) {
+                const int64_t offn = tn * tstride4 + threadIdx.x;
+#pragma unroll
+                for (int j = 0; j < UNROLL; ++j)
+                    if (j < g0)
+#pragma unroll
+                        for (int c = 0; c < CPL; ++c) nxt[j][c] = load4<true>(tab.rows[j] + offn + c * kBlock);
+            }
+        }
+#pragma unroll
+        for (int c = 0; c < CPL; ++c) {
+            const int64_t i = col + c * kBlock;
+            if (i >= b4 && i < e4) {
+                const f32x4 d = fin4<FIN>(acc[c], fin_val);
+                if (out != nullptr && EPI != FEDAVG_EPI_ADD_BASE) store4<true>(out + i, d);
+                epilogue4<EPI>(E, i, d, pre[c], out);
+            }
+        }
+    }
+}
+
+template <int OP, int FIN, bool ACC_IN, bool PRE>
+inline hipError_t launch_epi_p(const TileLaunch& L, const EpiParams& E, hipStream_t s) {
+    const f32x4* ai = reinterpret_cast<const f32x4*>(L.acc_in);
+    f32x4* o = reinterpret_cast<f32x4*>(L.out);
+    switch (E.kind) {
+        case FEDAVG_EPI_ADD_BASE:
+            hipLaunchKernelGGL((fedavg_tiles_epi_f32x4<OP, FIN, ACC_IN, FEDAVG_EPI_ADD_BASE, PRE>), dim3(L.grid),
+                               dim3(kBlock), 0, s, L.tab, L.k, L.tstride4, ai, o, L.b4, L.e4, L.fin_val, E);
+            break;
+        case FEDAVG_EPI_SGD:
+            hipLaunchKernelGGL((fedavg_tiles_epi_f32x4<OP, FIN, ACC_IN, FEDAVG_EPI_SGD, PRE>), dim3(L.grid), dim3(kBlock),
+                               0, s, L.tab, L.k, L.tstride4, ai, o, L.b4, L.e4, L.fin_val, E);
+            break;
+        case FEDAVG_EPI_ADAM:
+            hipLaunchKernelGGL((fedavg_tiles_epi_f32x4<OP, FIN, ACC_IN, FEDAVG_EPI_ADAM, PRE>), dim3(L.grid), dim3(kBlock),
+                               0, s, L.tab, L.k, L.tstride4, ai, o, L.b4, L.e4, L.fin_val, E);
+            break;
+        case FEDAVG_EPI_ADAGRAD:
+            hipLaunchKernelGGL((fedavg_tiles_epi_f32x4<OP, FIN, ACC_IN, FEDAVG_EPI_ADAGRAD, PRE>), dim3(L.grid),
+                               dim3(kBlock), 0, s, L.tab, L.k, L.tstride4, ai, o, L.b4, L.e4, L.fin_val, E);
+            break;
+        case FEDAVG_EPI_RMSPROP:
+            hipLaunchKernelGGL((fedavg_tiles_epi_f32x4<OP, FIN, ACC_IN, FEDAVG_EPI_RMSPROP, PRE>), dim3(L.grid),
+                               dim3(kBlock), 0, s, L.tab, L.k, L.tstride4, ai, o, L.b4, L.e4, L.fin_val, E);
+            break;
+        case FEDAVG_EPI_ADAMAX:
+            hipLaunchKernelGGL((fedavg_tiles_epi_f32x4<OP, FIN, ACC_IN, FEDAVG_EPI_ADAMAX, PRE>), dim3(L.grid),
+                               dim3(kBlock), 0, s, L.tab, L.k, L.tstride4, ai, o, L.b4, L.e4, L.fin_val, E);
+            break;
+        case FEDAVG_EPI_NADAM:
+            hipLaunchKernelGGL((fedavg_tiles_epi_f32x4<OP, FIN, ACC_IN, FEDAVG_EPI_NADAM, PRE>), dim3(L.grid),
+                               dim3(kBlock), 0, s, L.tab, L.k, L.tstride4, ai, o, L.b4, L.e4, L.fin_val, E);
+            break;
+        case FEDAVG_EPI_RADAM:
+            hipLaunchKernelGGL((fedavg_tiles_epi_f32x4<OP, FIN, ACC_IN, FEDAVG_EPI_RADAM, PRE>), dim3(L.grid),
+                               dim3(kBlock), 0, s, L.tab, L.k, L.tstride4, ai, o, L.b4, L.e4, L.fin_val, E);
+            break;
+        case FEDAVG_EPI_RPROP:
+            hipLaunchKernelGGL((fedavg_tiles_epi_f32x4<OP, FIN, ACC_IN, FEDAVG_EPI_RPROP, PRE>), dim3(L.grid),
+                               dim3(kBlock), 0, s, L.tab, L.k, L.tstride4, ai, o, L.b4, L.e4, L.fin_val, E);
+            break;
+        case FEDAVG_EPI_ASGD:
+            hipLaunchKernelGGL((fedavg_tiles_epi_f32x4<OP, FIN, ACC_IN, FEDAVG_EPI_ASGD, PRE>), dim3(L.grid),
+                               dim3(kBlock), 0, s, L.tab, L.k, L.tstride4, ai, o, L.b4, L.e4, L.fin_val, E);
+            break;
+        default:
+            return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+template <int OP, int FIN, bool ACC_IN>
+inline hipError_t launch_epi_a(const TileLaunch& L, const EpiParams& E, hipStream_t s) {
+    return (L.variant & kVariantEpiPrefetch) ? launch_epi_p<OP, FIN, ACC_IN, true>(L, E, s)
+                                             : launch_epi_p<OP, FIN, ACC_IN, false>(L, E, s);
+}
+
+template <int OP, int FIN>
+inline hipError_t launch_epi_f(const TileLaunch& L, const EpiParams& E, hipStream_t s) {
+    return L.acc_in ? launch_epi_a<OP, FIN, true>(L, E, s) : launch_epi_a<OP, FIN, false>(L, E, s);
+}
+
+template <int OP>
+inline hipError_t launch_epi_o(const TileLaunch& L, const EpiParams& E, hipStream_t s) {
+    switch (L.fin) {
+        case FEDAVG_FIN_SCALE:
+            return launch_epi_f<OP, FEDAVG_FIN_SCALE>(L, E, s);
+        case FEDAVG_FIN_DIV:
+            return launch_epi_f<OP, FEDAVG_FIN_DIV>(L, E, s);
+        default:
+            return launch_epi_f<OP, FEDAVG_FIN_NONE>(L, E, s);
+    }
+}
+
+}  // namespace fedavg

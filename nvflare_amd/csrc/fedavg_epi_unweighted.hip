@@ -1,0 +1,11 @@
+// fedavg_epi_unweighted.hip -- instantiations of the fp32 aggregation + server-optimizer epilogue kernels for the
+// unweighted arithmetic (one translation unit per mode: the three compile in parallel).
+#include "fedavg_epi.h"
+
+namespace fedavg {
+
+hipError_t launch_tiles_epi_f32x4_unweighted(const TileLaunch& L, const EpiParams& E, hipStream_t s) {
+    return launch_epi_o<FEDAVG_OP_UNWEIGHTED>(L, E, s);
+}
+
+}  // namespace fedavg

@@ -15,13 +15,16 @@ constexpr int kMaxRowsPerLaunch = 128;  // clients per launch carried in the ker
 
 // launch defaults, from the MI355X sweeps recorded in profiles/r01
 constexpr int kDefaultTile = 4096;      // elements per client segment per tile (16 KiB)
-constexpr int kDefaultBlocksPerCu = 2;  // 8 waves per CU
+constexpr int kDefaultBlocksPerCu = 2;  // 8 waves per CU (per-tile-store, epilogue, fp64 and 16-bit kernels)
 constexpr int kDefaultUnroll = 4;       // clients whose loads are in flight together per lane
 
-// variant bits (fedavg_set_variant)
-constexpr int kVariantTemporalLoads = 1;
-constexpr int kVariantTemporalStores = 2;
-constexpr int kVariantEpiPrefetch = 4;  // epilogue kernel: software-pipelined across tiles (see fedavg_tiles_epi_f32x4)
+// variant bits (fedavg_set_variant).  Default (0): the plain aggregation runs fedavg_tiles_burst_f32x4.
+constexpr int kVariantTemporalLoads = 1;   // per-tile-store kernel with temporal (cached) client loads
+constexpr int kVariantTemporalStores = 2;  // per-tile-store kernel with temporal result stores
+constexpr int kVariantEpiPrefetch = 4;     // epilogue kernel: software-pipelined across tiles (see fedavg_tiles_epi_f32x4)
+constexpr int kVariantTileStores = 8;      // plain aggregation on fedavg_tiles_f32x4 (each tile's results stored
+                                           // when it finishes; implied by bits 0 and 1)
+constexpr int kBurstTiles = 8;             // tiles per block per burst launch (results held in registers)
 
 // Per-launch client table passed BY VALUE in the kernarg segment: wave-uniform base pointers and
 // weights are loaded with s_load into SGPRs.
@@ -93,9 +96,22 @@ struct DequantLaunch {
     int grid;
 };
 
-hipError_t launch_tiles_f32x4(const TileLaunch& L, hipStream_t s);
+// launch_count (optional): incremented by the number of kernel launches issued
+hipError_t launch_tiles_f32x4(const TileLaunch& L, hipStream_t s, uint64_t* launch_count = nullptr);
+// per-mode instantiations (fedavg_tiles_*.hip, fedavg_epi_*.hip), dispatched on L.op by the two above
+hipError_t launch_tiles_f32x4_numpy(const TileLaunch& L, hipStream_t s, uint64_t* launch_count);
+hipError_t launch_tiles_f32x4_torch(const TileLaunch& L, hipStream_t s, uint64_t* launch_count);
+hipError_t launch_tiles_f32x4_unweighted(const TileLaunch& L, hipStream_t s, uint64_t* launch_count);
+hipError_t launch_tiles_epi_f32x4_numpy(const TileLaunch& L, const EpiParams& E, hipStream_t s);
+hipError_t launch_tiles_epi_f32x4_torch(const TileLaunch& L, const EpiParams& E, hipStream_t s);
+hipError_t launch_tiles_epi_f32x4_unweighted(const TileLaunch& L, const EpiParams& E, hipStream_t s);
+// whether launch_tiles_f32x4 takes the burst kernel for this geometry (it then wants one block per CU at
+// K >= kBurstOneBlockMinK clients, two below: profiles/r02/ab_burst_*.jsonl)
+bool tiles_use_burst(int64_t tile4, int unroll, int variant);
+constexpr int kBurstOneBlockMinK = 16;
 hipError_t launch_dequant_f32(const DequantLaunch& L, hipStream_t s);
-hipError_t launch_tiles_epi_f32x4(const TileLaunch& L, const EpiParams& E, hipStream_t s);
+hipError_t launch_tiles_epi_f32x4(const TileLaunch& L, const EpiParams& E, hipStream_t s,
+                                  uint64_t* launch_count = nullptr);
 hipError_t launch_rows_generic(const RowTableGeneric& tab, int K, const void* acc_in, void* out, int64_t n,
                                int in_dtype, int acc_dtype, int op, int fin, double fin_val, int grid,
                                hipStream_t s);

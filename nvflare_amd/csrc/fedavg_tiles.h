@@ -1,0 +1,233 @@
+// fedavg_tiles.h -- the fp32 tiled aggregation kernels (the hot path) and their launch templates; included by
+// one translation unit per arithmetic mode (fedavg_tiles_{numpy,torch,unweighted}.hip) so the instantiations
+// compile in parallel.  Design notes: fedavg_kernels.hip header, DESIGN.md section 3.
+#pragma once
+
+#include "fedavg_arith.h"
+
+namespace fedavg {
+
+// ---------------------------------------------------------------------------------------------
+// THE HOT KERNEL.  Global f32x4 index range [b4, e4); tiles t = b4/T4 .. (e4-1)/T4 are dealt to blocks
+// round-robin.  For every column of a tile:
+//     acc = ACC_IN ? acc_in[i] : first(client 0);  acc = step(acc, client k) for k = 1..K-1 in order;
+//     out[i] = fin(acc)                  (only for i in [b4, e4): partial edge tiles are masked at store)
+// Client loads are unconditional: the caller guarantees every client's tiled storage covers whole
+// tiles (slabs are allocated in whole tiles; the pointer-list entry point sends ragged tails elsewhere).
+// ---------------------------------------------------------------------------------------------
+template <int OP, int FIN, bool ACC_IN, int UNROLL, int CPL, bool NTL, bool NTS>
+__global__ void __launch_bounds__(kBlock) fedavg_tiles_f32x4(const RowTableF32 tab, const int K,
+                                                              const int64_t tstride4, const f32x4* acc_in,
+                                                              f32x4* out, const int64_t b4, const int64_t e4,
+                                                              const float fin_val) {
+    constexpr int64_t T4 = (int64_t)CPL * kBlock;
+    const int64_t t_last = (e4 - 1) / T4;
+    for (int64_t t = b4 / T4 + blockIdx.x; t <= t_last; t += gridDim.x) {
+        const int64_t off = t * tstride4 + threadIdx.x;  // offset inside each client's tiled storage
+        const int64_t col = t * T4 + threadIdx.x;        // global f32x4 index of column group 0
+        f32x4 acc[CPL];
+        int k = 0;
+        if constexpr (ACC_IN) {
+#pragma unroll
+            for (int c = 0; c < CPL; ++c) {
+                const int64_t i = col + c * kBlock;
+                acc[c] = (i >= b4 && i < e4) ? load4<false>(acc_in + i) : f32x4{0, 0, 0, 0};
+            }
+        } else {
+            const f32x4* r = tab.rows[0] + off;
+#pragma unroll
+            for (int c = 0; c < CPL; ++c) acc[c] = first4<OP>(load4<NTL>(r + c * kBlock), tab.w[0]);
+            k = 1;
+        }
+        // groups of UNROLL clients: issue all their loads, then the arrival-ordered arithmetic
+        for (; k + UNROLL <= K; k += UNROLL) {
+            f32x4 v[UNROLL][CPL];
+#pragma unroll
+            for (int j = 0; j < UNROLL; ++j) {
+                const f32x4* r = tab.rows[k + j] + off;
+#pragma unroll
+                for (int c = 0; c < CPL; ++c) v[j][c] = load4<NTL>(r + c * kBlock);
+            }
+#pragma unroll
+            for (int j = 0; j < UNROLL; ++j)
+#pragma unroll
+                for (int c = 0; c < CPL; ++c) acc[c] = step4<OP>(acc[c], v[j][c], tab.w[k + j]);
+        }
+        for (; k < K; ++k) {
+            const f32x4* r = tab.rows[k] + off;
+#pragma unroll
+            for (int c = 0; c < CPL; ++c) acc[c] = step4<OP>(acc[c], load4<NTL>(r + c * kBlock), tab.w[k]);
+        }
+#pragma unroll
+        for (int c = 0; c < CPL; ++c) {
+            const int64_t i = col + c * kBlock;
+            if (i >= b4 && i < e4) store4<NTS>(out + i, fin4<FIN>(acc[c], fin_val));
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// BURST form of the hot kernel (launch variant bit 5).  Measured on MI355X (profiles/r02/pattern_probe):
+// a 1 MiB-chunk read stream reaches 88 % of spec alone, but adding the result stream (1/64 of the bytes,
+// 16 KiB per tile, written as each tile finishes) drops it to 74-81 % whatever the store cache policy --
+// small writes scattered in time through a read stream are expensive.  Written as chip-wide bursts
+// instead (every block holds its results and all blocks store at about the same moment, at the end of a
+// short launch whose start re-aligns them) the same stream ran at 88.6 %.  So: each launch gives every
+// block TPB tiles (dealt round-robin, so the concurrently-read tiles stay adjacent), the results stay in
+// registers (TPB x CPL float4 per lane), and the stores are issued after the block's last tile; the host
+// issues one launch per grid x TPB tiles.  One block per CU (one wave per SIMD, registers for the staged
+// results and a whole client group's loads in flight).
+// ---------------------------------------------------------------------------------------------
+template <int OP, bool ACC_IN, int UNROLL, int CPL>
+__device__ __forceinline__ void tile_sum(f32x4 (&acc)[CPL], const RowTableF32& tab, const int K, const int64_t off,
+                                         const int64_t col, const f32x4* acc_in, const int64_t b4, const int64_t e4) {
+    int k = 0;
+    if constexpr (ACC_IN) {
+#pragma unroll
+        for (int c = 0; c < CPL; ++c) {
+            const int64_t i = col + c * kBlock;
+            acc[c] = (i >= b4 && i < e4) ? acc_in[i] : f32x4{0, 0, 0, 0};
+        }
+    } else {
+        const f32x4* r = tab.rows[0] + off;
+#pragma unroll
+        for (int c = 0; c < CPL; ++c) acc[c] = first4<OP>(__builtin_nontemporal_load(r + c * kBlock), tab.w[0]);
+        k = 1;
+    }
+    for (; k + UNROLL <= K; k += UNROLL) {
+        f32x4 v[UNROLL][CPL];
+#pragma unroll
+        for (int j = 0; j < UNROLL; ++j) {
+            const f32x4* r = tab.rows[k + j] + off;
+#pragma unroll
+            for (int c = 0; c < CPL; ++c) v[j][c] = __builtin_nontemporal_load(r + c * kBlock);
+        }
+#pragma unroll
+        for (int j = 0; j < UNROLL; ++j)
+#pragma unroll
+            for (int c = 0; c < CPL; ++c) acc[c] = step4<OP>(acc[c], v[j][c], tab.w[k + j]);
+    }
+    for (; k < K; ++k) {
+        const f32x4* r = tab.rows[k] + off;
+#pragma unroll
+        for (int c = 0; c < CPL; ++c) acc[c] = step4<OP>(acc[c], __builtin_nontemporal_load(r + c * kBlock), tab.w[k]);
+    }
+}
+
+template <int OP, int FIN, bool ACC_IN, int UNROLL, int CPL, int TPB>
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, 1)))
+fedavg_tiles_burst_f32x4(const RowTableF32 tab, const int K, const int64_t tstride4, const f32x4* acc_in, f32x4* out,
+                         const int64_t b4, const int64_t e4, const float fin_val, const int64_t t0, const int64_t t_end) {
+    constexpr int64_t T4 = (int64_t)CPL * kBlock;
+    f32x4 res[TPB][CPL];
+#pragma unroll
+    for (int m = 0; m < TPB; ++m) {
+        const int64_t t = t0 + blockIdx.x + (int64_t)m * gridDim.x;
+        if (t < t_end) {
+            f32x4 acc[CPL];
+            tile_sum<OP, ACC_IN, UNROLL, CPL>(acc, tab, K, t * tstride4 + threadIdx.x, t * T4 + threadIdx.x, acc_in, b4,
+                                              e4);
+#pragma unroll
+            for (int c = 0; c < CPL; ++c) res[m][c] = fin4<FIN>(acc[c], fin_val);
+        }
+    }
+#pragma unroll
+    for (int m = 0; m < TPB; ++m) {
+        const int64_t t = t0 + blockIdx.x + (int64_t)m * gridDim.x;
+        if (t < t_end) {
+#pragma unroll
+            for (int c = 0; c < CPL; ++c) {
+                const int64_t i = t * T4 + threadIdx.x + c * kBlock;
+                if (i >= b4 && i < e4) __builtin_nontemporal_store(res[m][c], out + i);
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// launchers
+// ---------------------------------------------------------------------------------------------
+// one launch per grid x TPB tiles (fedavg_tiles_burst_f32x4)
+template <int OP, int FIN, bool ACC_IN, int UNROLL, int CPL, int TPB>
+inline hipError_t launch_burst(const TileLaunch& L, hipStream_t s, uint64_t* nl) {
+    const f32x4* ai = reinterpret_cast<const f32x4*>(L.acc_in);
+    f32x4* o = reinterpret_cast<f32x4*>(L.out);
+    const int64_t t_first = L.b4 / L.tile4, t_stop = (L.e4 - 1) / L.tile4 + 1;
+    const int64_t per = (int64_t)L.grid * TPB;
+    for (int64_t t0 = t_first; t0 < t_stop; t0 += per) {
+        const int64_t t_end = t0 + per < t_stop ? t0 + per : t_stop;
+        const int64_t nb = t_end - t0 < L.grid ? t_end - t0 : L.grid;
+        hipLaunchKernelGGL((fedavg_tiles_burst_f32x4<OP, FIN, ACC_IN, UNROLL, CPL, TPB>), dim3(nb), dim3(kBlock), 0, s,
+                           L.tab, L.k, L.tstride4, ai, o, L.b4, L.e4, L.fin_val, t0, t_end);
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+        if (nl) ++*nl;
+    }
+    return hipSuccess;
+}
+
+template <int OP, int FIN, bool ACC_IN, int UNROLL, int CPL>
+inline hipError_t launch_tiles_v(const TileLaunch& L, hipStream_t s, uint64_t* nl) {
+    const f32x4* ai = reinterpret_cast<const f32x4*>(L.acc_in);
+    f32x4* o = reinterpret_cast<f32x4*>(L.out);
+    if constexpr (CPL * (UNROLL + kBurstTiles) <= 64) {  // staged results + a group's loads within 256 VGPRs
+        if (!(L.variant & (kVariantTileStores | kVariantTemporalLoads | kVariantTemporalStores)))
+            return launch_burst<OP, FIN, ACC_IN, UNROLL, CPL, kBurstTiles>(L, s, nl);
+    }
+    const bool ntl = !(L.variant & kVariantTemporalLoads);
+    const bool nts = !(L.variant & kVariantTemporalStores);
+#define FEDAVG_LAUNCH_TILES(NTL, NTS)                                                                                \
+    hipLaunchKernelGGL((fedavg_tiles_f32x4<OP, FIN, ACC_IN, UNROLL, CPL, NTL, NTS>), dim3(L.grid), dim3(kBlock), 0, \
+                       s, L.tab, L.k, L.tstride4, ai, o, L.b4, L.e4, L.fin_val)
+    if (ntl && nts) {
+        FEDAVG_LAUNCH_TILES(true, true);
+    } else if (ntl) {
+        FEDAVG_LAUNCH_TILES(true, false);
+    } else if (nts) {
+        FEDAVG_LAUNCH_TILES(false, true);
+    } else {
+        FEDAVG_LAUNCH_TILES(false, false);
+    }
+#undef FEDAVG_LAUNCH_TILES
+    if (nl) ++*nl;
+    return hipGetLastError();
+}
+
+template <int OP, int FIN, bool ACC_IN>
+inline hipError_t launch_tiles_a(const TileLaunch& L, hipStream_t s, uint64_t* nl) {
+    const int64_t cpl = L.tile4 / kBlock;
+#define FEDAVG_TILES_CPL(C) \
+    return L.unroll == 8 ? launch_tiles_v<OP, FIN, ACC_IN, 8, C>(L, s, nl) : launch_tiles_v<OP, FIN, ACC_IN, 4, C>(L, s, nl);
+    switch (cpl) {
+        case 1:
+            FEDAVG_TILES_CPL(1)
+        case 2:
+            FEDAVG_TILES_CPL(2)
+        case 4:
+            FEDAVG_TILES_CPL(4)
+        case 8:
+            FEDAVG_TILES_CPL(8)
+        default:
+            return hipErrorInvalidValue;
+    }
+#undef FEDAVG_TILES_CPL
+}
+
+template <int OP, int FIN>
+inline hipError_t launch_tiles_f(const TileLaunch& L, hipStream_t s, uint64_t* nl) {
+    return L.acc_in ? launch_tiles_a<OP, FIN, true>(L, s, nl) : launch_tiles_a<OP, FIN, false>(L, s, nl);
+}
+
+template <int OP>
+inline hipError_t launch_tiles_o(const TileLaunch& L, hipStream_t s, uint64_t* nl) {
+    switch (L.fin) {
+        case FEDAVG_FIN_SCALE:
+            return launch_tiles_f<OP, FEDAVG_FIN_SCALE>(L, s, nl);
+        case FEDAVG_FIN_DIV:
+            return launch_tiles_f<OP, FEDAVG_FIN_DIV>(L, s, nl);
+        default:
+            return launch_tiles_f<OP, FEDAVG_FIN_NONE>(L, s, nl);
+    }
+}
+
+}  // namespace fedavg

@@ -395,6 +395,12 @@ class DeviceContext:
         N.call("fedavg_timing_end", self.handle, ctypes.byref(ms))
         return float(ms.value)
 
+    def launch_count(self) -> int:
+        """Kernel launches issued on this context's compute stream so far (fedavg_launch_count)."""
+        n = ctypes.c_uint64(0)
+        N.call("fedavg_launch_count", self.handle, ctypes.byref(n))
+        return int(n.value)
+
     def set_launch(self, blocks_per_cu: int = 0, unroll: int = 0) -> None:
         N.call("fedavg_set_launch", self.handle, ctypes.c_int(blocks_per_cu), ctypes.c_int(unroll))
 

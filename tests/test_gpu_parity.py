@@ -250,8 +250,9 @@ def test_kernel_generic_dtypes(ctx, oracle, in_dt, acc_dt):
         assert same_bits(got, exp)
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3])
-@pytest.mark.parametrize("bpc,unroll,tile", [(1, 4, 1024), (2, 8, 2048), (4, 4, 4096), (8, 8, 8192), (2, 4, 4096)])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 8])
+@pytest.mark.parametrize("bpc,unroll,tile", [(1, 4, 1024), (2, 8, 2048), (4, 4, 4096), (8, 8, 8192), (2, 4, 4096),
+                                             (0, 0, 4096), (1, 8, 4096)])
 def test_launch_variants_same_bits(ctx, oracle, bpc, unroll, tile, variant):
     rng = np.random.default_rng(21)
     n = 300_001 + variant  # whole tiles on the streaming kernel + a ragged tail on the scalar kernel
@@ -269,6 +270,42 @@ def test_launch_variants_same_bits(ctx, oracle, bpc, unroll, tile, variant):
             ctx.set_variant(0)
             ctx.set_tile(0)
         assert same_bits(got, exp)
+
+
+@pytest.mark.parametrize("K,bpc", [(20, 0), (7, 0), (20, 3), (131, 0)])
+def test_burst_many_launches(ctx, oracle, K, bpc):
+    """The default (burst) kernel issues one launch per grid x 8 tiles: more tiles than one launch covers,
+    a last launch with fewer tiles than blocks, a sub-range starting and ending inside tiles, more than
+    128 clients (chained through the output), against the oracle bit for bit."""
+    n = 2048 * 4096 * 2 + 12345
+    rows = [oracle.synth_values(5, k, np.arange(n, dtype=np.uint64)) for k in range(K)]
+    ws = oracle.synth_weights(K)
+    ctx.set_launch(bpc, 0)
+    try:
+        for op, fin, mode in ((1, 2, oracle.MODE_TORCH), (0, 1, oracle.MODE_NUMPY)):
+            exp = oracle.fedavg_c(rows, ws, mode, fin=fin, nthreads=8)
+            got = _run_kernel(ctx, rows, ws, op, fin, _sum(ws))
+            assert same_bits(got, exp)
+        # a sub-range [lo, hi) through the tiled entry point (contiguous rows: tile stride == tile): only it
+        # is written, the sentinel around it stays
+        lo, hi = 4096 * 3 + 100, (n - 4096 * 5 - 36) // 4 * 4
+        n_alloc = (n + 4095) // 4096 * 4096
+        bufs = [ctx.alloc(n_alloc * 4) for _ in rows]
+        for b, r in zip(bufs, rows):
+            ctx.h2d_ptr(b.ptr, r.ctypes.data, r.nbytes)
+        out = ctx.alloc(n_alloc * 4)
+        sentinel = np.full(n, -7.0, np.float32)
+        ctx.h2d_ptr(out.ptr, sentinel.ctypes.data, sentinel.nbytes)
+        ctx.accumulate_tiled([b.ptr for b in bufs], ws, 4096, 4096, lo, hi, out.ptr, 1, 2, _sum(ws))
+        got = np.empty(n, np.float32)
+        ctx.d2h(got, out.ptr)
+        exp = oracle.fedavg_c([r[lo:hi] for r in rows], ws, oracle.MODE_TORCH, fin=2, nthreads=8)
+        assert same_bits(got[lo:hi], exp)
+        assert np.all(got[:lo] == -7.0) and np.all(got[hi:] == -7.0)
+        for b in bufs + [out]:
+            b.close()
+    finally:
+        ctx.set_launch(0, 0)
 
 
 def test_large_k64(ctx, oracle):

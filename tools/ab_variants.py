@@ -7,6 +7,8 @@ cancel.  Prints one JSON line per measurement and a median summary line per (epi
 
 import argparse
 import json
+
+import numpy as np
 import os
 import statistics
 import sys
@@ -22,8 +24,10 @@ def main():
     ap.add_argument("--params", type=float, default=1e9)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--rounds", type=int, default=3)
-    ap.add_argument("--variants", default="0,4")
+    ap.add_argument("--variants", default="0,4", help="variant bits, or variant:unroll:blocks_per_cu triples")
     ap.add_argument("--epilogues", default="none,adam")
+    ap.add_argument("--check", action="store_true",
+                    help="plain epilogue: every config's output must equal the first config's bit for bit")
     a = ap.parse_args()
     from nvflare_amd import _native as N
     from nvflare_amd.device import DeviceContext, TiledLayout
@@ -58,29 +62,44 @@ def main():
             o = None
         return lambda: ctx.accumulate_tiled_epi(bases, ws, lay.tile, lay.tile_stride, 0, end, o, 1, 2, cnt, e)
 
-    variants = [int(v) for v in a.variants.split(",")]
+    variants = [tuple(int(x) for x in (v.split(":") + ["0", "0"])[:3]) for v in a.variants.split(",")]
     epis = a.epilogues.split(",")
     res = {}
+    ref_out = None
     for rnd in range(a.rounds):
         for epi in epis:
             fn = launcher(epi)
             for v in variants:
-                ctx.set_variant(v)
+                ctx.set_variant(v[0])
+                ctx.set_launch(v[2], v[1])
                 fn()
+                if a.check and epi == "none" and rnd == 0:
+                    host = np.empty(end, dtype=np.float32)
+                    ctx.sync()
+                    ctx.d2h(host, out.ptr)
+                    if ref_out is None:
+                        ref_out = host
+                    else:
+                        bad = int(np.count_nonzero(host.view(np.uint32) != ref_out.view(np.uint32)))
+                        print(json.dumps({"check": ":".join(map(str, v)), "mismatches": bad}), flush=True)
+                        if bad:
+                            raise SystemExit(f"config {v}: {bad} outputs differ from config {variants[0]}")
+                    ctx.memset(out.ptr, 0xFF, end * 4)
                 ctx.timing_begin()
                 for _ in range(a.reps):
                     fn()
                 ms = ctx.timing_end() / a.reps
                 gbs = (4.0 * K * P + EXTRA[epi] * P) / ms / 1e6
                 res.setdefault((epi, v), []).append(ms)
-                print(json.dumps({"round": rnd, "epilogue": epi, "variant": v, "clients": K, "params": P,
+                print(json.dumps({"round": rnd, "epilogue": epi, "variant": ":".join(map(str, v)), "clients": K, "params": P,
                                   "ms": round(ms, 4), "GBps": round(gbs, 1), "frac_8TBps": round(gbs / 8000, 4)}),
                       flush=True)
     ctx.set_variant(0)
+    ctx.set_launch(0, 0)
     for (epi, v), xs in res.items():
         ms = statistics.median(xs)
         gbs = (4.0 * K * P + EXTRA[epi] * P) / ms / 1e6
-        print(json.dumps({"summary": True, "epilogue": epi, "variant": v, "clients": K, "params": P,
+        print(json.dumps({"summary": True, "epilogue": epi, "variant": ":".join(map(str, v)), "clients": K, "params": P,
                           "median_ms": round(ms, 4), "GBps": round(gbs, 1), "frac_8TBps": round(gbs / 8000, 4)}),
               flush=True)
 

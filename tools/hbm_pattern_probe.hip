@@ -1,0 +1,265 @@
+// hbm_pattern_probe.hip -- diagnostic only (not part of the product library): which HBM READ PATTERN
+// sustains the most bandwidth on this chip, to tell how far the slab kernel's access pattern (every block
+// streams its own 1 MiB tile; tiles dealt round-robin) sits from a chip-wide sequential sweep.
+//   mode 0  grid:   grid-stride float4 sweep, U loads in flight per lane (the whole chip reads one window)
+//   mode 1  chunk:  block b reads chunks b, b+G, ... of CH bytes sequentially (the slab kernel's pattern)
+//   mode 2  chunk_lds: mode 1 through LDS-DMA (global_load_lds_dwordx4, 1 KiB per wave-instruction),
+//                   16 in flight per wave, nothing read back (the DMA is the consumer)
+//   mode 3  chunk_pair: block b reads TWO chunks (b and b + n_chunks/2) alternately, U/2 loads each
+//   mode 4  chunk_w: mode 1 plus 4 nontemporal float4 stores per lane per chunk (the slab kernel's
+//                   result stream: 16 KiB per 1 MiB chunk) into the buffer's last 1/64
+//   mode 6/7/8 chunk_w with buffer stores of cache policy sc1 / sc0 sc1 / plain (instead of nt)
+//   mode 9  chunk_wb: results staged in LDS and written as a burst of 8 chunks' results (128 KiB) per block
+//   mode 10 chunk_wb_sliced: mode 9 as a sequence of launches of blocks x 8 chunks each, so every launch's
+//                   write burst starts chip-wide at about the same time (launch boundaries re-align the blocks)
+//   mode 5  chunk_wd: mode 4 with each chunk's stores issued AFTER the next chunk's first load group, so the
+//                   wait for those loads (vmcnt counts loads and stores in issue order) never waits on a store
+// Build: hipcc --offload-arch=gfx950 -O3 -shared -fPIC tools/hbm_pattern_probe.hip -o tools/build/libhbm_pattern_probe.so
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+template <int U>
+__global__ void __launch_bounds__(256) p_grid(const f32x4* __restrict__ src, int64_t n4, f32x4* __restrict__ sink) {
+    f32x4 acc = {0, 0, 0, 0};
+    const int64_t stride = (int64_t)gridDim.x * 256;
+    int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    for (; i + (U - 1) * stride < n4; i += U * stride) {
+        f32x4 v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) v[u] = __builtin_nontemporal_load(src + i + u * stride);
+#pragma unroll
+        for (int u = 0; u < U; ++u) acc += v[u];
+    }
+    sink[(int64_t)blockIdx.x * 256 + threadIdx.x] = acc;
+}
+
+// chunk4 = chunk size in float4 (multiple of 256 * U)
+template <int U>
+__global__ void __launch_bounds__(256) p_chunk(const f32x4* __restrict__ src, int64_t n_chunks, int64_t chunk4,
+                                               f32x4* __restrict__ sink) {
+    f32x4 acc = {0, 0, 0, 0};
+    for (int64_t c = blockIdx.x; c < n_chunks; c += gridDim.x) {
+        const f32x4* p = src + c * chunk4 + threadIdx.x;
+        for (int64_t j = 0; j < chunk4; j += 256 * U) {
+            f32x4 v[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) v[u] = __builtin_nontemporal_load(p + j + u * 256);
+#pragma unroll
+            for (int u = 0; u < U; ++u) acc += v[u];
+        }
+    }
+    sink[(int64_t)blockIdx.x * 256 + threadIdx.x] = acc;
+}
+
+template <int U>
+__global__ void __launch_bounds__(256) p_chunk_w(const f32x4* __restrict__ src, int64_t n_chunks, int64_t chunk4,
+                                                 f32x4* __restrict__ dst) {
+    for (int64_t c = blockIdx.x; c < n_chunks; c += gridDim.x) {
+        const f32x4* p = src + c * chunk4 + threadIdx.x;
+        f32x4 acc[4] = {};
+        for (int64_t j = 0; j < chunk4; j += 256 * U) {
+            f32x4 v[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) v[u] = __builtin_nontemporal_load(p + j + u * 256);
+#pragma unroll
+            for (int u = 0; u < U; ++u) acc[u % 4] += v[u];
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) __builtin_nontemporal_store(acc[q], dst + c * 1024 + q * 256 + threadIdx.x);
+    }
+}
+
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+
+template <int U, int AUX>
+__global__ void __launch_bounds__(256) p_chunk_wp(const f32x4* __restrict__ src, int64_t n_chunks, int64_t chunk4,
+                                                  f32x4* __restrict__ dst) {
+    for (int64_t c = blockIdx.x; c < n_chunks; c += gridDim.x) {
+        const f32x4* p = src + c * chunk4 + threadIdx.x;
+        f32x4 acc[4] = {};
+        for (int64_t j = 0; j < chunk4; j += 256 * U) {
+            f32x4 v[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) v[u] = __builtin_nontemporal_load(p + j + u * 256);
+#pragma unroll
+            for (int u = 0; u < U; ++u) acc[u % 4] += v[u];
+        }
+        __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(dst + c * 1024, 0, 16384, 0x00020000);
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, acc[q]), r, (q * 256 + threadIdx.x) * 16, 0, AUX);
+    }
+}
+
+template <int U>
+__global__ void __launch_bounds__(256) p_chunk_wb(const f32x4* __restrict__ src, int64_t n_chunks, int64_t chunk4,
+                                                  f32x4* __restrict__ dst) {
+    __shared__ f32x4 stage[8][1024];  // 8 chunks x 16 KiB
+    int n = 0;
+    int64_t first = blockIdx.x;
+    for (int64_t c = blockIdx.x; c < n_chunks; c += gridDim.x) {
+        const f32x4* p = src + c * chunk4 + threadIdx.x;
+        f32x4 acc[4] = {};
+        for (int64_t j = 0; j < chunk4; j += 256 * U) {
+            f32x4 v[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) v[u] = __builtin_nontemporal_load(p + j + u * 256);
+#pragma unroll
+            for (int u = 0; u < U; ++u) acc[u % 4] += v[u];
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) stage[n][q * 256 + threadIdx.x] = acc[q];  // own lanes only: no barrier
+        if (++n == 8 || c + gridDim.x >= n_chunks) {
+            for (int m = 0; m < n; ++m)
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    __builtin_nontemporal_store(stage[m][q * 256 + threadIdx.x],
+                                                dst + (first + (int64_t)m * gridDim.x) * 1024 + q * 256 + threadIdx.x);
+            n = 0;
+            first = c + gridDim.x;
+        }
+    }
+}
+
+template <int U>
+__global__ void __launch_bounds__(256) p_chunk_wd(const f32x4* __restrict__ src, int64_t n_chunks, int64_t chunk4,
+                                                  f32x4* __restrict__ dst) {
+    f32x4 res[4] = {};
+    int64_t prev = -1;
+    for (int64_t c = blockIdx.x; c < n_chunks; c += gridDim.x) {
+        const f32x4* p = src + c * chunk4 + threadIdx.x;
+        f32x4 acc[4] = {};
+        for (int64_t j = 0; j < chunk4; j += 256 * U) {
+            f32x4 v[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) v[u] = __builtin_nontemporal_load(p + j + u * 256);
+            if (j == 0) {  // branch-free stores (the first chunk writes its own slot early; rewritten later)
+                asm volatile("" ::: "memory");  // keep the stores behind this group's loads
+                const int64_t tgt = prev >= 0 ? prev : c;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) __builtin_nontemporal_store(res[q], dst + tgt * 1024 + q * 256 + threadIdx.x);
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) acc[u % 4] += v[u];
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) res[q] = acc[q];
+        prev = c;
+    }
+    if (prev >= 0)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) __builtin_nontemporal_store(res[q], dst + prev * 1024 + q * 256 + threadIdx.x);
+}
+
+template <int U>
+__global__ void __launch_bounds__(256) p_chunk_pair(const f32x4* __restrict__ src, int64_t n_chunks, int64_t chunk4,
+                                                    f32x4* __restrict__ sink) {
+    f32x4 acc = {0, 0, 0, 0};
+    const int64_t half = n_chunks / 2;
+    for (int64_t c = blockIdx.x; c < half; c += gridDim.x) {
+        const f32x4* p = src + c * chunk4 + threadIdx.x;
+        const f32x4* q = src + (c + half) * chunk4 + threadIdx.x;
+        for (int64_t j = 0; j < chunk4; j += 256 * (U / 2)) {
+            f32x4 v[U];
+#pragma unroll
+            for (int u = 0; u < U / 2; ++u) {
+                v[2 * u] = __builtin_nontemporal_load(p + j + u * 256);
+                v[2 * u + 1] = __builtin_nontemporal_load(q + j + u * 256);
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) acc += v[u];
+        }
+    }
+    sink[(int64_t)blockIdx.x * 256 + threadIdx.x] = acc;
+}
+
+// LDS-DMA: each wave owns a 16 KiB ring of 16 x 1 KiB slots; issue 16 DMAs, wait for the oldest 8, repeat.
+__global__ void __launch_bounds__(256) p_chunk_lds(const f32x4* __restrict__ src, int64_t n_chunks, int64_t chunk4,
+                                                   f32x4* __restrict__ sink) {
+    __shared__ f32x4 ring[4][16][64];
+    const int wave = threadIdx.x / 64, lane = threadIdx.x % 64;
+    for (int64_t c = blockIdx.x; c < n_chunks; c += gridDim.x) {
+        // wave w reads quarter w of the chunk as a sequential run of 1 KiB pieces
+        const int64_t q4 = chunk4 / 4;
+        const f32x4* p = src + c * chunk4 + wave * q4 + lane;
+        for (int64_t j = 0; j < q4; j += 64 * 8) {
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+                __builtin_amdgcn_global_load_lds(p + j + u * 64, &ring[wave][((j / 512) & 1) * 8 + u][0], 16, 0, 2);
+            asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+    sink[(int64_t)blockIdx.x * 256 + threadIdx.x] = ring[wave][lane % 16][lane];
+}
+
+extern "C" {
+// returns 0 on success; ms_out = average over reps
+int pattern_run(int mode, int unroll, void* buf, size_t bytes, size_t chunk_bytes, int blocks, int reps, float* ms_out) {
+    hipStream_t s;
+    if (hipStreamCreate(&s) != hipSuccess) return 1;
+    hipEvent_t a, b;
+    (void)hipEventCreate(&a);
+    (void)hipEventCreate(&b);
+    f32x4* sink = nullptr;
+    if (hipMalloc(&sink, (size_t)blocks * 256 * sizeof(f32x4)) != hipSuccess) return 2;
+    const int64_t n4 = (int64_t)(bytes / 16);
+    const int64_t chunk4 = (int64_t)(chunk_bytes / 16);
+    const int64_t n_chunks = n4 / chunk4;
+    const f32x4* src = (const f32x4*)buf;
+    auto launch = [&]() {
+        if (mode == 0) {
+            if (unroll == 16) hipLaunchKernelGGL(p_grid<16>, dim3(blocks), dim3(256), 0, s, src, n4, sink);
+            else if (unroll == 4) hipLaunchKernelGGL(p_grid<4>, dim3(blocks), dim3(256), 0, s, src, n4, sink);
+            else hipLaunchKernelGGL(p_grid<8>, dim3(blocks), dim3(256), 0, s, src, n4, sink);
+        } else if (mode == 1) {
+            if (unroll == 16) hipLaunchKernelGGL(p_chunk<16>, dim3(blocks), dim3(256), 0, s, src, n_chunks, chunk4, sink);
+            else if (unroll == 4) hipLaunchKernelGGL(p_chunk<4>, dim3(blocks), dim3(256), 0, s, src, n_chunks, chunk4, sink);
+            else hipLaunchKernelGGL(p_chunk<8>, dim3(blocks), dim3(256), 0, s, src, n_chunks, chunk4, sink);
+        } else if (mode == 4) {
+            const int64_t nc = n_chunks * 63 / 64;  // the last 1/64 of the buffer takes the results
+            hipLaunchKernelGGL(p_chunk_w<16>, dim3(blocks), dim3(256), 0, s, src, nc, chunk4, (f32x4*)buf + nc * chunk4);
+        } else if (mode >= 6 && mode <= 9) {
+            const int64_t nc = n_chunks * 63 / 64;
+            f32x4* d = (f32x4*)buf + nc * chunk4;
+            if (mode == 6) hipLaunchKernelGGL((p_chunk_wp<16, 16>), dim3(blocks), dim3(256), 0, s, src, nc, chunk4, d);
+            if (mode == 7) hipLaunchKernelGGL((p_chunk_wp<16, 17>), dim3(blocks), dim3(256), 0, s, src, nc, chunk4, d);
+            if (mode == 8) hipLaunchKernelGGL((p_chunk_wp<16, 0>), dim3(blocks), dim3(256), 0, s, src, nc, chunk4, d);
+            if (mode == 9) hipLaunchKernelGGL(p_chunk_wb<16>, dim3(blocks), dim3(256), 0, s, src, nc, chunk4, d);
+        } else if (mode == 10) {
+            const int64_t nc = n_chunks * 63 / 64;
+            f32x4* d = (f32x4*)buf + nc * chunk4;
+            const int64_t per = (int64_t)blocks * 8;
+            for (int64_t c0 = 0; c0 < nc; c0 += per) {
+                const int64_t m = nc - c0 < per ? nc - c0 : per;
+                hipLaunchKernelGGL(p_chunk_wb<16>, dim3(blocks), dim3(256), 0, s, src + c0 * chunk4, m, chunk4,
+                                   d + c0 * 1024);
+            }
+        } else if (mode == 5) {
+            const int64_t nc = n_chunks * 63 / 64;
+            hipLaunchKernelGGL(p_chunk_wd<16>, dim3(blocks), dim3(256), 0, s, src, nc, chunk4, (f32x4*)buf + nc * chunk4);
+        } else if (mode == 2) {
+            hipLaunchKernelGGL(p_chunk_lds, dim3(blocks), dim3(256), 0, s, src, n_chunks, chunk4, sink);
+        } else {
+            if (unroll == 16) hipLaunchKernelGGL(p_chunk_pair<16>, dim3(blocks), dim3(256), 0, s, src, n_chunks, chunk4, sink);
+            else hipLaunchKernelGGL(p_chunk_pair<8>, dim3(blocks), dim3(256), 0, s, src, n_chunks, chunk4, sink);
+        }
+    };
+    launch();
+    hipEventRecord(a, s);
+    for (int r = 0; r < reps; ++r) launch();
+    hipEventRecord(b, s);
+    hipEventSynchronize(b);
+    float ms = 0;
+    hipEventElapsedTime(&ms, a, b);
+    *ms_out = ms / reps;
+    hipFree(sink);
+    hipEventDestroy(a);
+    hipEventDestroy(b);
+    hipStreamDestroy(s);
+    return hipGetLastError() == hipSuccess ? 0 : 3;
+}
+}
