@@ -273,12 +273,13 @@ int fedavg_launch_count(fedavg_ctx* ctx, uint64_t* n);
 /* Launch tuning (0 = default): blocks per CU (default: each kernel's own -- 1 for the burst aggregation
  * kernel at >= 16 clients, 2 otherwise), clients whose loads are issued together (4 or 8, default 4). */
 int fedavg_set_launch(fedavg_ctx* ctx, int blocks_per_cu, int unroll);
-/* Kernel variants (default 0: the plain aggregation stages each block's results in registers and stores
- * them as chip-wide bursts, one launch per 8 tiles per block; every load and store nontemporal).
- * bit 3 = plain aggregation with each tile's results stored as it finishes (the round-1 kernel);
- * bit 0 / bit 1 = that kernel with temporal client loads / temporal result stores (imply bit 3);
- * bit 2 = epilogue kernel software-pipelined across tiles (the next tile's first client loads overlap
- * the epilogue).  Results are bit-identical in every variant. */
+/* Kernel variants (default 0: the aggregation -- plain or with a fused epilogue -- holds each block's
+ * results in registers and stores them (runs the epilogue) as chip-wide bursts, one launch per 8 tiles per
+ * block; every load and store nontemporal).
+ * bit 3 = each tile's results stored (epilogue run) as the tile finishes (the round-1 kernels);
+ * bit 0 / bit 1 = the plain one with temporal client loads / temporal result stores (imply bit 3);
+ * bit 2 = the per-tile epilogue kernel software-pipelined across tiles (the next tile's first client loads
+ * overlap the epilogue; implies bit 3 for the epilogue).  Results are bit-identical in every variant. */
 int fedavg_set_variant(fedavg_ctx* ctx, int variant);
 /* Tile width used by fedavg_accumulate for contiguous rows (default 4096 elements). */
 int fedavg_set_tile(fedavg_ctx* ctx, int tile_elems);

@@ -79,4 +79,44 @@ __device__ __forceinline__ void store4(f32x4* p, f32x4 v) {
     }
 }
 
+// One tile's arrival-ordered sum for the CPL float4 columns this lane owns: acc = ACC_IN ? acc_in : first(client
+// 0), then step(client k) for every later client, UNROLL clients' loads issued before their arithmetic.  Client
+// rows are tiled (row + off is this lane's first column of the tile); acc_in is indexed by global column and
+// masked to [b4, e4).
+template <int OP, bool ACC_IN, int UNROLL, int CPL>
+__device__ __forceinline__ void tile_sum(f32x4 (&acc)[CPL], const RowTableF32& tab, const int K, const int64_t off,
+                                         const int64_t col, const f32x4* acc_in, const int64_t b4, const int64_t e4) {
+    int k = 0;
+    if constexpr (ACC_IN) {
+#pragma unroll
+        for (int c = 0; c < CPL; ++c) {
+            const int64_t i = col + c * kBlock;
+            acc[c] = (i >= b4 && i < e4) ? acc_in[i] : f32x4{0, 0, 0, 0};
+        }
+    } else {
+        const f32x4* r = tab.rows[0] + off;
+#pragma unroll
+        for (int c = 0; c < CPL; ++c) acc[c] = first4<OP>(__builtin_nontemporal_load(r + c * kBlock), tab.w[0]);
+        k = 1;
+    }
+    for (; k + UNROLL <= K; k += UNROLL) {
+        f32x4 v[UNROLL][CPL];
+#pragma unroll
+        for (int j = 0; j < UNROLL; ++j) {
+            const f32x4* r = tab.rows[k + j] + off;
+#pragma unroll
+            for (int c = 0; c < CPL; ++c) v[j][c] = __builtin_nontemporal_load(r + c * kBlock);
+        }
+#pragma unroll
+        for (int j = 0; j < UNROLL; ++j)
+#pragma unroll
+            for (int c = 0; c < CPL; ++c) acc[c] = step4<OP>(acc[c], v[j][c], tab.w[k + j]);
+    }
+    for (; k < K; ++k) {
+        const f32x4* r = tab.rows[k] + off;
+#pragma unroll
+        for (int c = 0; c < CPL; ++c) acc[c] = step4<OP>(acc[c], __builtin_nontemporal_load(r + c * kBlock), tab.w[k]);
+    }
+}
+
 }  // namespace fedavg

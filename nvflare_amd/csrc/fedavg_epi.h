@@ -245,6 +245,66 @@ __device__ __forceinline__ void epilogue4(const EpiParams& E, const int64_t i, c
 // PIPE: software-pipelined across tiles -- after the client loop of tile t the lane issues the epilogue
 // operand loads of t, then the first UNROLL client loads of its next tile, and only then waits for the
 // operands and runs the epilogue (ALU, three store streams) while the next tile's loads are in flight.
+// BURST form (the default; see fedavg_tiles.h fedavg_tiles_burst_f32x4): each launch gives every block TPB
+// tiles; the aggregated differences d of all of them stay in registers while the client stream runs, and
+// the epilogue (operand loads, optimizer arithmetic, the state / parameter stores) runs for all TPB tiles
+// at the end of the launch -- the client-read phase carries no writes, and every block's epilogue phase
+// falls at about the same time.  `out` (when given) also receives d, as in the per-tile kernel.
+template <int OP, int FIN, bool ACC_IN, int EPI, int TPB>
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, 1)))
+fedavg_tiles_epi_burst_f32x4(const RowTableF32 tab, const int K, const int64_t tstride4, const f32x4* acc_in,
+                             f32x4* out, const int64_t b4, const int64_t e4, const float fin_val, const EpiParams E,
+                             const int64_t t0, const int64_t t_end) {
+    constexpr int UNROLL = kDefaultUnroll;
+    constexpr int CPL = kDefaultTile / (4 * kBlock);
+    constexpr int64_t T4 = (int64_t)CPL * kBlock;
+    f32x4 dd[TPB][CPL];
+#pragma unroll
+    for (int m = 0; m < TPB; ++m) {
+        const int64_t t = t0 + blockIdx.x + (int64_t)m * gridDim.x;
+        if (t < t_end) {
+            f32x4 acc[CPL];
+            tile_sum<OP, ACC_IN, UNROLL, CPL>(acc, tab, K, t * tstride4 + threadIdx.x, t * T4 + threadIdx.x, acc_in, b4,
+                                              e4);
+#pragma unroll
+            for (int c = 0; c < CPL; ++c) dd[m][c] = fin4<FIN>(acc[c], fin_val);
+        }
+    }
+    // Epilogue phase, double-buffered: tile m+1's operand loads are issued before tile m's arithmetic and
+    // stores (program order keeps them ahead of those stores, which may alias nothing they read but the
+    // compiler cannot know).  Loads are unconditional at a clamped in-range address so the waits count
+    // exactly one tile's loads; only in-range columns of real tiles are computed and stored.
+    const int64_t t_base = t0 + blockIdx.x;
+    const int64_t t_cap = t_end - 1;
+    auto operands = [&](EpiIn (&in)[CPL], const int m) {
+        const int64_t t = t_base + (int64_t)m * gridDim.x;
+        const int64_t tc = t < t_cap ? t : t_cap;
+#pragma unroll
+        for (int c = 0; c < CPL; ++c) {
+            int64_t i = tc * T4 + threadIdx.x + c * kBlock;
+            i = i < b4 ? b4 : (i >= e4 ? e4 - 1 : i);
+            in[c] = epi_load<EPI>(E, i);
+        }
+    };
+    EpiIn pre[2][CPL];
+    operands(pre[0], 0);
+#pragma unroll
+    for (int m = 0; m < TPB; ++m) {
+        if (m + 1 < TPB) operands(pre[(m + 1) & 1], m + 1);
+        const int64_t t = t_base + (int64_t)m * gridDim.x;
+        if (t < t_end) {
+#pragma unroll
+            for (int c = 0; c < CPL; ++c) {
+                const int64_t i = t * T4 + threadIdx.x + c * kBlock;
+                if (i >= b4 && i < e4) {
+                    if (out != nullptr && EPI != FEDAVG_EPI_ADD_BASE) store4<true>(out + i, dd[m][c]);
+                    epilogue4<EPI>(E, i, dd[m][c], pre[m & 1][c], out);
+                }
+            }
+        }
+    }
+}
+
 template <int OP, int FIN, bool ACC_IN, int EPI, bool PIPE>
 __global__ void __launch_bounds__(kBlock) fedavg_tiles_epi_f32x4(const RowTableF32 tab, const int K,
                                                                   const int64_t tstride4, const f32x4* acc_in,
@@ -344,77 +404,78 @@ __global__ void __launch_bounds__(kBlock) fedavg_tiles_epi_f32x4(const RowTableF
     }
 }
 
-template <int OP, int FIN, bool ACC_IN, bool PRE>
-inline hipError_t launch_epi_p(const TileLaunch& L, const EpiParams& E, hipStream_t s) {
+// one kernel instantiation per optimizer kind: K(EPI) launches the per-tile (PRE) or the burst form
+template <int OP, int FIN, bool ACC_IN, int EPI>
+inline hipError_t launch_epi_k(const TileLaunch& L, const EpiParams& E, hipStream_t s, uint64_t* nl) {
     const f32x4* ai = reinterpret_cast<const f32x4*>(L.acc_in);
     f32x4* o = reinterpret_cast<f32x4*>(L.out);
-    switch (E.kind) {
-        case FEDAVG_EPI_ADD_BASE:
-            hipLaunchKernelGGL((fedavg_tiles_epi_f32x4<OP, FIN, ACC_IN, FEDAVG_EPI_ADD_BASE, PRE>), dim3(L.grid),
-                               dim3(kBlock), 0, s, L.tab, L.k, L.tstride4, ai, o, L.b4, L.e4, L.fin_val, E);
-            break;
-        case FEDAVG_EPI_SGD:
-            hipLaunchKernelGGL((fedavg_tiles_epi_f32x4<OP, FIN, ACC_IN, FEDAVG_EPI_SGD, PRE>), dim3(L.grid), dim3(kBlock),
-                               0, s, L.tab, L.k, L.tstride4, ai, o, L.b4, L.e4, L.fin_val, E);
-            break;
-        case FEDAVG_EPI_ADAM:
-            hipLaunchKernelGGL((fedavg_tiles_epi_f32x4<OP, FIN, ACC_IN, FEDAVG_EPI_ADAM, PRE>), dim3(L.grid), dim3(kBlock),
-                               0, s, L.tab, L.k, L.tstride4, ai, o, L.b4, L.e4, L.fin_val, E);
-            break;
-        case FEDAVG_EPI_ADAGRAD:
-            hipLaunchKernelGGL((fedavg_tiles_epi_f32x4<OP, FIN, ACC_IN, FEDAVG_EPI_ADAGRAD, PRE>), dim3(L.grid),
-                               dim3(kBlock), 0, s, L.tab, L.k, L.tstride4, ai, o, L.b4, L.e4, L.fin_val, E);
-            break;
-        case FEDAVG_EPI_RMSPROP:
-            hipLaunchKernelGGL((fedavg_tiles_epi_f32x4<OP, FIN, ACC_IN, FEDAVG_EPI_RMSPROP, PRE>), dim3(L.grid),
-                               dim3(kBlock), 0, s, L.tab, L.k, L.tstride4, ai, o, L.b4, L.e4, L.fin_val, E);
-            break;
-        case FEDAVG_EPI_ADAMAX:
-            hipLaunchKernelGGL((fedavg_tiles_epi_f32x4<OP, FIN, ACC_IN, FEDAVG_EPI_ADAMAX, PRE>), dim3(L.grid),
-                               dim3(kBlock), 0, s, L.tab, L.k, L.tstride4, ai, o, L.b4, L.e4, L.fin_val, E);
-            break;
-        case FEDAVG_EPI_NADAM:
-            hipLaunchKernelGGL((fedavg_tiles_epi_f32x4<OP, FIN, ACC_IN, FEDAVG_EPI_NADAM, PRE>), dim3(L.grid),
-                               dim3(kBlock), 0, s, L.tab, L.k, L.tstride4, ai, o, L.b4, L.e4, L.fin_val, E);
-            break;
-        case FEDAVG_EPI_RADAM:
-            hipLaunchKernelGGL((fedavg_tiles_epi_f32x4<OP, FIN, ACC_IN, FEDAVG_EPI_RADAM, PRE>), dim3(L.grid),
-                               dim3(kBlock), 0, s, L.tab, L.k, L.tstride4, ai, o, L.b4, L.e4, L.fin_val, E);
-            break;
-        case FEDAVG_EPI_RPROP:
-            hipLaunchKernelGGL((fedavg_tiles_epi_f32x4<OP, FIN, ACC_IN, FEDAVG_EPI_RPROP, PRE>), dim3(L.grid),
-                               dim3(kBlock), 0, s, L.tab, L.k, L.tstride4, ai, o, L.b4, L.e4, L.fin_val, E);
-            break;
-        case FEDAVG_EPI_ASGD:
-            hipLaunchKernelGGL((fedavg_tiles_epi_f32x4<OP, FIN, ACC_IN, FEDAVG_EPI_ASGD, PRE>), dim3(L.grid),
-                               dim3(kBlock), 0, s, L.tab, L.k, L.tstride4, ai, o, L.b4, L.e4, L.fin_val, E);
-            break;
-        default:
-            return hipErrorInvalidValue;
+    if (!(L.variant & (kVariantTileStores | kVariantEpiPrefetch))) {  // burst: one launch per grid x TPB tiles
+        const int64_t t_first = L.b4 / L.tile4, t_stop = (L.e4 - 1) / L.tile4 + 1;
+        const int64_t per = (int64_t)L.grid * kBurstTiles;
+        for (int64_t t0 = t_first; t0 < t_stop; t0 += per) {
+            const int64_t t_end = t0 + per < t_stop ? t0 + per : t_stop;
+            const int64_t nb = t_end - t0 < L.grid ? t_end - t0 : L.grid;
+            hipLaunchKernelGGL((fedavg_tiles_epi_burst_f32x4<OP, FIN, ACC_IN, EPI, kBurstTiles>), dim3(nb), dim3(kBlock),
+                               0, s, L.tab, L.k, L.tstride4, ai, o, L.b4, L.e4, L.fin_val, E, t0, t_end);
+            const hipError_t e = hipGetLastError();
+            if (e != hipSuccess) return e;
+            if (nl) ++*nl;
+        }
+        return hipSuccess;
     }
+    if (L.variant & kVariantEpiPrefetch) {
+        hipLaunchKernelGGL((fedavg_tiles_epi_f32x4<OP, FIN, ACC_IN, EPI, true>), dim3(L.grid), dim3(kBlock), 0, s, L.tab,
+                           L.k, L.tstride4, ai, o, L.b4, L.e4, L.fin_val, E);
+    } else {
+        hipLaunchKernelGGL((fedavg_tiles_epi_f32x4<OP, FIN, ACC_IN, EPI, false>), dim3(L.grid), dim3(kBlock), 0, s, L.tab,
+                           L.k, L.tstride4, ai, o, L.b4, L.e4, L.fin_val, E);
+    }
+    if (nl) ++*nl;
     return hipGetLastError();
 }
 
 template <int OP, int FIN, bool ACC_IN>
-inline hipError_t launch_epi_a(const TileLaunch& L, const EpiParams& E, hipStream_t s) {
-    return (L.variant & kVariantEpiPrefetch) ? launch_epi_p<OP, FIN, ACC_IN, true>(L, E, s)
-                                             : launch_epi_p<OP, FIN, ACC_IN, false>(L, E, s);
+inline hipError_t launch_epi_a(const TileLaunch& L, const EpiParams& E, hipStream_t s, uint64_t* nl) {
+    switch (E.kind) {
+        case FEDAVG_EPI_ADD_BASE:
+            return launch_epi_k<OP, FIN, ACC_IN, FEDAVG_EPI_ADD_BASE>(L, E, s, nl);
+        case FEDAVG_EPI_SGD:
+            return launch_epi_k<OP, FIN, ACC_IN, FEDAVG_EPI_SGD>(L, E, s, nl);
+        case FEDAVG_EPI_ADAM:
+            return launch_epi_k<OP, FIN, ACC_IN, FEDAVG_EPI_ADAM>(L, E, s, nl);
+        case FEDAVG_EPI_ADAGRAD:
+            return launch_epi_k<OP, FIN, ACC_IN, FEDAVG_EPI_ADAGRAD>(L, E, s, nl);
+        case FEDAVG_EPI_RMSPROP:
+            return launch_epi_k<OP, FIN, ACC_IN, FEDAVG_EPI_RMSPROP>(L, E, s, nl);
+        case FEDAVG_EPI_ADAMAX:
+            return launch_epi_k<OP, FIN, ACC_IN, FEDAVG_EPI_ADAMAX>(L, E, s, nl);
+        case FEDAVG_EPI_NADAM:
+            return launch_epi_k<OP, FIN, ACC_IN, FEDAVG_EPI_NADAM>(L, E, s, nl);
+        case FEDAVG_EPI_RADAM:
+            return launch_epi_k<OP, FIN, ACC_IN, FEDAVG_EPI_RADAM>(L, E, s, nl);
+        case FEDAVG_EPI_RPROP:
+            return launch_epi_k<OP, FIN, ACC_IN, FEDAVG_EPI_RPROP>(L, E, s, nl);
+        case FEDAVG_EPI_ASGD:
+            return launch_epi_k<OP, FIN, ACC_IN, FEDAVG_EPI_ASGD>(L, E, s, nl);
+        default:
+            return hipErrorInvalidValue;
+    }
 }
 
 template <int OP, int FIN>
-inline hipError_t launch_epi_f(const TileLaunch& L, const EpiParams& E, hipStream_t s) {
-    return L.acc_in ? launch_epi_a<OP, FIN, true>(L, E, s) : launch_epi_a<OP, FIN, false>(L, E, s);
+inline hipError_t launch_epi_f(const TileLaunch& L, const EpiParams& E, hipStream_t s, uint64_t* nl) {
+    return L.acc_in ? launch_epi_a<OP, FIN, true>(L, E, s, nl) : launch_epi_a<OP, FIN, false>(L, E, s, nl);
 }
 
 template <int OP>
-inline hipError_t launch_epi_o(const TileLaunch& L, const EpiParams& E, hipStream_t s) {
+inline hipError_t launch_epi_o(const TileLaunch& L, const EpiParams& E, hipStream_t s, uint64_t* nl) {
     switch (L.fin) {
         case FEDAVG_FIN_SCALE:
-            return launch_epi_f<OP, FEDAVG_FIN_SCALE>(L, E, s);
+            return launch_epi_f<OP, FEDAVG_FIN_SCALE>(L, E, s, nl);
         case FEDAVG_FIN_DIV:
-            return launch_epi_f<OP, FEDAVG_FIN_DIV>(L, E, s);
+            return launch_epi_f<OP, FEDAVG_FIN_DIV>(L, E, s, nl);
         default:
-            return launch_epi_f<OP, FEDAVG_FIN_NONE>(L, E, s);
+            return launch_epi_f<OP, FEDAVG_FIN_NONE>(L, E, s, nl);
     }
 }
 

@@ -4,8 +4,8 @@
 
 namespace fedavg {
 
-hipError_t launch_tiles_epi_f32x4_torch(const TileLaunch& L, const EpiParams& E, hipStream_t s) {
-    return launch_epi_o<FEDAVG_OP_TORCH>(L, E, s);
+hipError_t launch_tiles_epi_f32x4_torch(const TileLaunch& L, const EpiParams& E, hipStream_t s, uint64_t* nl) {
+    return launch_epi_o<FEDAVG_OP_TORCH>(L, E, s, nl);
 }
 
 }  // namespace fedavg

@@ -102,9 +102,9 @@ hipError_t launch_tiles_f32x4(const TileLaunch& L, hipStream_t s, uint64_t* laun
 hipError_t launch_tiles_f32x4_numpy(const TileLaunch& L, hipStream_t s, uint64_t* launch_count);
 hipError_t launch_tiles_f32x4_torch(const TileLaunch& L, hipStream_t s, uint64_t* launch_count);
 hipError_t launch_tiles_f32x4_unweighted(const TileLaunch& L, hipStream_t s, uint64_t* launch_count);
-hipError_t launch_tiles_epi_f32x4_numpy(const TileLaunch& L, const EpiParams& E, hipStream_t s);
-hipError_t launch_tiles_epi_f32x4_torch(const TileLaunch& L, const EpiParams& E, hipStream_t s);
-hipError_t launch_tiles_epi_f32x4_unweighted(const TileLaunch& L, const EpiParams& E, hipStream_t s);
+hipError_t launch_tiles_epi_f32x4_numpy(const TileLaunch& L, const EpiParams& E, hipStream_t s, uint64_t* nl);
+hipError_t launch_tiles_epi_f32x4_torch(const TileLaunch& L, const EpiParams& E, hipStream_t s, uint64_t* nl);
+hipError_t launch_tiles_epi_f32x4_unweighted(const TileLaunch& L, const EpiParams& E, hipStream_t s, uint64_t* nl);
 // whether launch_tiles_f32x4 takes the burst kernel for this geometry (it then wants one block per CU at
 // K >= kBurstOneBlockMinK clients, two below: profiles/r02/ab_burst_*.jsonl)
 bool tiles_use_burst(int64_t tile4, int unroll, int variant);

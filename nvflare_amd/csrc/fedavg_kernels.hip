@@ -224,14 +224,13 @@ hipError_t launch_tiles_f32x4(const TileLaunch& L, hipStream_t s, uint64_t* nl) 
 }
 
 hipError_t launch_tiles_epi_f32x4(const TileLaunch& L, const EpiParams& E, hipStream_t s, uint64_t* nl) {
-    if (nl) ++*nl;
     switch (L.op) {
         case FEDAVG_OP_TORCH:
-            return launch_tiles_epi_f32x4_torch(L, E, s);
+            return launch_tiles_epi_f32x4_torch(L, E, s, nl);
         case FEDAVG_OP_UNWEIGHTED:
-            return launch_tiles_epi_f32x4_unweighted(L, E, s);
+            return launch_tiles_epi_f32x4_unweighted(L, E, s, nl);
         default:
-            return launch_tiles_epi_f32x4_numpy(L, E, s);
+            return launch_tiles_epi_f32x4_numpy(L, E, s, nl);
     }
 }
 

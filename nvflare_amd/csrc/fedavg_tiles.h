@@ -78,42 +78,6 @@ __global__ void __launch_bounds__(kBlock) fedavg_tiles_f32x4(const RowTableF32 t
 // issues one launch per grid x TPB tiles.  One block per CU (one wave per SIMD, registers for the staged
 // results and a whole client group's loads in flight).
 // ---------------------------------------------------------------------------------------------
-template <int OP, bool ACC_IN, int UNROLL, int CPL>
-__device__ __forceinline__ void tile_sum(f32x4 (&acc)[CPL], const RowTableF32& tab, const int K, const int64_t off,
-                                         const int64_t col, const f32x4* acc_in, const int64_t b4, const int64_t e4) {
-    int k = 0;
-    if constexpr (ACC_IN) {
-#pragma unroll
-        for (int c = 0; c < CPL; ++c) {
-            const int64_t i = col + c * kBlock;
-            acc[c] = (i >= b4 && i < e4) ? acc_in[i] : f32x4{0, 0, 0, 0};
-        }
-    } else {
-        const f32x4* r = tab.rows[0] + off;
-#pragma unroll
-        for (int c = 0; c < CPL; ++c) acc[c] = first4<OP>(__builtin_nontemporal_load(r + c * kBlock), tab.w[0]);
-        k = 1;
-    }
-    for (; k + UNROLL <= K; k += UNROLL) {
-        f32x4 v[UNROLL][CPL];
-#pragma unroll
-        for (int j = 0; j < UNROLL; ++j) {
-            const f32x4* r = tab.rows[k + j] + off;
-#pragma unroll
-            for (int c = 0; c < CPL; ++c) v[j][c] = __builtin_nontemporal_load(r + c * kBlock);
-        }
-#pragma unroll
-        for (int j = 0; j < UNROLL; ++j)
-#pragma unroll
-            for (int c = 0; c < CPL; ++c) acc[c] = step4<OP>(acc[c], v[j][c], tab.w[k + j]);
-    }
-    for (; k < K; ++k) {
-        const f32x4* r = tab.rows[k] + off;
-#pragma unroll
-        for (int c = 0; c < CPL; ++c) acc[c] = step4<OP>(acc[c], __builtin_nontemporal_load(r + c * kBlock), tab.w[k]);
-    }
-}
-
 template <int OP, int FIN, bool ACC_IN, int UNROLL, int CPL, int TPB>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, 1)))
 fedavg_tiles_burst_f32x4(const RowTableF32 tab, const int K, const int64_t tstride4, const f32x4* acc_in, f32x4* out,
