@@ -535,6 +535,9 @@ void run_tiles_narrow(fedavg_ctx* ctx, const void* const* bases, const double* w
     const float fv = narrow_fin_value(fmt, fin, count);
     const int64_t T = fedavg::kTile16Elems;
     const int64_t n_tiles = (end - 1) / T - begin / T + 1;
+    // the 16-bit burst kernel keeps two blocks per CU at every K: it rounds after every operation, and one
+    // wave per SIMD does not issue that VALU work fast enough (profiles/r02/ab/narrow_burst_bpc.jsonl)
+    const bool burst = !(ctx->variant & fedavg::kVariantTileStores);
     const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)ctx->num_cus * ctx->bpc(), n_tiles));
     int k0 = 0;
     const void* cur_in = acc_in;
@@ -544,8 +547,7 @@ void run_tiles_narrow(fedavg_ctx* ctx, const void* const* bases, const double* w
         fill_narrow_table(t, bases, weights, k0, kc, fmt, op);
         const bool last = k0 + kc >= k_rows;
         HIP_CHECK(fedavg::launch_tiles_narrow(t, kc, tstride, cur_in, out, begin, end, fmt, op,
-                                              last ? fin : FEDAVG_FIN_NONE, fv, grid, s));
-        ++ctx->launches;
+                                              last ? fin : FEDAVG_FIN_NONE, fv, grid, burst, s, &ctx->launches));
         cur_in = out;
         k0 += kc;
     } while (k0 < k_rows);
@@ -1055,7 +1057,9 @@ int fedavg_accumulate_tiled64(fedavg_ctx* ctx, const void* const* bases, const d
         TimingScope ts(ctx, s);
         const int64_t T = fedavg::kTile64Elems;
         const int64_t n_tiles = ((int64_t)end - 1) / T - (int64_t)begin / T + 1;
-        const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)ctx->num_cus * ctx->bpc(), n_tiles));
+        const bool burst = !(ctx->variant & fedavg::kVariantTileStores);
+        const int bpc = burst ? ctx->bpc(k_rows >= fedavg::kBurstOneBlockMinK ? 1 : 2) : ctx->bpc();
+        const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)ctx->num_cus * bpc, n_tiles));
         const double fv = fin_scalar(fin, count);
         int k0 = 0;
         const void* cur_in = acc_in;
@@ -1069,8 +1073,7 @@ int fedavg_accumulate_tiled64(fedavg_ctx* ctx, const void* const* bases, const d
             }
             const bool last = k0 + kc >= k_rows;
             HIP_CHECK(fedavg::launch_tiles_f64(t, kc, (int64_t)tile_stride, cur_in, out, (int64_t)begin, (int64_t)end,
-                                               op, last ? fin : FEDAVG_FIN_NONE, fv, grid, s));
-            ++ctx->launches;
+                                               op, last ? fin : FEDAVG_FIN_NONE, fv, grid, burst, s, &ctx->launches));
             cur_in = out;
             k0 += kc;
         } while (k0 < k_rows);

@@ -410,18 +410,12 @@ inline hipError_t launch_epi_k(const TileLaunch& L, const EpiParams& E, hipStrea
     const f32x4* ai = reinterpret_cast<const f32x4*>(L.acc_in);
     f32x4* o = reinterpret_cast<f32x4*>(L.out);
     if (!(L.variant & (kVariantTileStores | kVariantEpiPrefetch))) {  // burst: one launch per grid x TPB tiles
-        const int64_t t_first = L.b4 / L.tile4, t_stop = (L.e4 - 1) / L.tile4 + 1;
-        const int64_t per = (int64_t)L.grid * kBurstTiles;
-        for (int64_t t0 = t_first; t0 < t_stop; t0 += per) {
-            const int64_t t_end = t0 + per < t_stop ? t0 + per : t_stop;
-            const int64_t nb = t_end - t0 < L.grid ? t_end - t0 : L.grid;
-            hipLaunchKernelGGL((fedavg_tiles_epi_burst_f32x4<OP, FIN, ACC_IN, EPI, kBurstTiles>), dim3(nb), dim3(kBlock),
-                               0, s, L.tab, L.k, L.tstride4, ai, o, L.b4, L.e4, L.fin_val, E, t0, t_end);
-            const hipError_t e = hipGetLastError();
-            if (e != hipSuccess) return e;
-            if (nl) ++*nl;
-        }
-        return hipSuccess;
+        return burst_launches(L.b4 / L.tile4, (L.e4 - 1) / L.tile4 + 1, L.grid, kBurstTiles, nl,
+                              [&](int nb, int64_t t0, int64_t t_end) {
+                                  hipLaunchKernelGGL((fedavg_tiles_epi_burst_f32x4<OP, FIN, ACC_IN, EPI, kBurstTiles>),
+                                                     dim3(nb), dim3(kBlock), 0, s, L.tab, L.k, L.tstride4, ai, o, L.b4,
+                                                     L.e4, L.fin_val, E, t0, t_end);
+                              });
     }
     if (L.variant & kVariantEpiPrefetch) {
         hipLaunchKernelGGL((fedavg_tiles_epi_f32x4<OP, FIN, ACC_IN, EPI, true>), dim3(L.grid), dim3(kBlock), 0, s, L.tab,

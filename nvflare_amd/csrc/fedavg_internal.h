@@ -98,6 +98,22 @@ struct DequantLaunch {
 
 // launch_count (optional): incremented by the number of kernel launches issued
 hipError_t launch_tiles_f32x4(const TileLaunch& L, hipStream_t s, uint64_t* launch_count = nullptr);
+
+// Host loop of a BURST kernel (fedavg_tiles.h): one launch per grid x tpb tiles of [t_first, t_stop), every
+// block holding its tpb tiles' results until the end of its launch; launch(blocks, t0, t_end) issues one.
+template <typename Launch>
+inline hipError_t burst_launches(int64_t t_first, int64_t t_stop, int grid, int tpb, uint64_t* launch_count,
+                                 Launch&& launch) {
+    const int64_t per = (int64_t)grid * tpb;
+    for (int64_t t0 = t_first; t0 < t_stop; t0 += per) {
+        const int64_t t_end = t0 + per < t_stop ? t0 + per : t_stop;
+        launch((int)(t_end - t0 < grid ? t_end - t0 : grid), t0, t_end);
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+        if (launch_count) ++*launch_count;
+    }
+    return hipSuccess;
+}
 // per-mode instantiations (fedavg_tiles_*.hip, fedavg_epi_*.hip), dispatched on L.op by the two above
 hipError_t launch_tiles_f32x4_numpy(const TileLaunch& L, hipStream_t s, uint64_t* launch_count);
 hipError_t launch_tiles_f32x4_torch(const TileLaunch& L, hipStream_t s, uint64_t* launch_count);
@@ -117,13 +133,16 @@ hipError_t launch_rows_generic(const RowTableGeneric& tab, int K, const void* ac
                                hipStream_t s);
 hipError_t launch_rows_narrow(const RowTableNarrow& tab, int K, const void* acc_in, void* out, int64_t n, int fmt,
                               int op, int fin, float fin_val, int grid, hipStream_t s);
+// burst: the burst form (results held per block, stored at the end of each short launch); otherwise one
+// launch of the per-tile-store kernel.  launch_count is incremented per launch.
 hipError_t launch_tiles_narrow(const RowTableNarrow& tab, int K, int64_t tstride_elems, const void* acc_in, void* out,
                                int64_t begin, int64_t end, int fmt, int op, int fin, float fin_val, int grid,
-                               hipStream_t s);
+                               bool burst, hipStream_t s, uint64_t* launch_count);
 constexpr int kTile16Elems = 4096;  // the only tile width of the 16-bit tiled kernel
 constexpr int kTile64Elems = 4096;  // the only tile width of the fp64 tiled kernel
 hipError_t launch_tiles_f64(const RowTableGeneric& tab, int K, int64_t tstride_elems, const void* acc_in, void* out,
-                            int64_t begin, int64_t end, int op, int fin, double fin_val, int grid, hipStream_t s);
+                            int64_t begin, int64_t end, int op, int fin, double fin_val, int grid, bool burst,
+                            hipStream_t s, uint64_t* launch_count);
 hipError_t launch_fill_synthetic_f32(float* dst, int64_t n, int64_t tile, int64_t tstride, uint64_t seed, uint64_t row,
                                      uint64_t col0, int grid, hipStream_t s);
 hipError_t launch_gather_f32(const float* src, const uint64_t* idx, float* dst, int64_t m, hipStream_t s);

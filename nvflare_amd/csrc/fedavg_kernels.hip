@@ -107,63 +107,101 @@ constexpr int kCpl64 = kTile64Elems / (2 * kBlock);  // 8
 #ifndef FEDAVG_F64_UNROLL
 #define FEDAVG_F64_UNROLL 2  // clients whose loads are in flight together (16 x 16 B per lane)
 #endif
+constexpr int kBurstTiles64 = 4;  // tiles per block per burst launch: 4 x kCpl64 staged pairs = 128 VGPRs
 
+// One tile's arrival-ordered sum for this lane's kCpl64 pairs, finalised.
+template <int OP, int FIN, bool ACC_IN>
+__device__ __forceinline__ void tile_sum64(f64x2 (&res)[kCpl64], const RowTableGeneric& tab, const int K,
+                                           const int64_t off, const int64_t col, const f64x2* acc_in, const int64_t b2,
+                                           const int64_t e2, const double fin_val) {
+    constexpr int UNROLL = FEDAVG_F64_UNROLL;
+    f64x2 acc[kCpl64];
+    int k = 0;
+    if constexpr (ACC_IN) {
+#pragma unroll
+        for (int c = 0; c < kCpl64; ++c) {
+            const int64_t i = col + c * kBlock;
+            acc[c] = (i >= b2 && i < e2) ? acc_in[i] : f64x2{0, 0};
+        }
+    } else {
+        const f64x2* r = static_cast<const f64x2*>(tab.rows[0]) + off;
+#pragma unroll
+        for (int c = 0; c < kCpl64; ++c) {
+            const f64x2 v = __builtin_nontemporal_load(r + c * kBlock);
+            acc[c] = f64x2{first_op<OP>(v[0], tab.w[0]), first_op<OP>(v[1], tab.w[0])};
+        }
+        k = 1;
+    }
+    for (; k + UNROLL <= K; k += UNROLL) {
+        f64x2 v[UNROLL][kCpl64];
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u) {
+            const f64x2* r = static_cast<const f64x2*>(tab.rows[k + u]) + off;
+#pragma unroll
+            for (int c = 0; c < kCpl64; ++c) v[u][c] = __builtin_nontemporal_load(r + c * kBlock);
+        }
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u)
+#pragma unroll
+            for (int c = 0; c < kCpl64; ++c)
+                acc[c] = f64x2{step_op<OP>(acc[c][0], v[u][c][0], tab.w[k + u]),
+                               step_op<OP>(acc[c][1], v[u][c][1], tab.w[k + u])};
+    }
+    for (; k < K; ++k) {
+        const f64x2* r = static_cast<const f64x2*>(tab.rows[k]) + off;
+#pragma unroll
+        for (int c = 0; c < kCpl64; ++c) {
+            const f64x2 v = __builtin_nontemporal_load(r + c * kBlock);
+            acc[c] = f64x2{step_op<OP>(acc[c][0], v[0], tab.w[k]), step_op<OP>(acc[c][1], v[1], tab.w[k])};
+        }
+    }
+#pragma unroll
+    for (int c = 0; c < kCpl64; ++c) res[c] = f64x2{fin_op<FIN>(acc[c][0], fin_val), fin_op<FIN>(acc[c][1], fin_val)};
+}
+
+// per-tile-store form (launch variant bit 3)
 template <int OP, int FIN, bool ACC_IN>
 __global__ void __launch_bounds__(kBlock) fedavg_tiles_f64x2(const RowTableGeneric tab, const int K,
                                                               const int64_t tstride2, const f64x2* acc_in, f64x2* out,
                                                               const int64_t b2, const int64_t e2, const double fin_val) {
     constexpr int64_t T2 = (int64_t)kCpl64 * kBlock;
-    constexpr int UNROLL = FEDAVG_F64_UNROLL;
     const int64_t t_last = (e2 - 1) / T2;
     for (int64_t t = b2 / T2 + blockIdx.x; t <= t_last; t += gridDim.x) {
-        const int64_t off = t * tstride2 + threadIdx.x;
-        const int64_t col = t * T2 + threadIdx.x;
-        f64x2 acc[kCpl64];
-        int k = 0;
-        if constexpr (ACC_IN) {
-#pragma unroll
-            for (int c = 0; c < kCpl64; ++c) {
-                const int64_t i = col + c * kBlock;
-                acc[c] = (i >= b2 && i < e2) ? acc_in[i] : f64x2{0, 0};
-            }
-        } else {
-            const f64x2* r = static_cast<const f64x2*>(tab.rows[0]) + off;
-#pragma unroll
-            for (int c = 0; c < kCpl64; ++c) {
-                const f64x2 v = __builtin_nontemporal_load(r + c * kBlock);
-                acc[c] = f64x2{first_op<OP>(v[0], tab.w[0]), first_op<OP>(v[1], tab.w[0])};
-            }
-            k = 1;
-        }
-        for (; k + UNROLL <= K; k += UNROLL) {
-            f64x2 v[UNROLL][kCpl64];
-#pragma unroll
-            for (int u = 0; u < UNROLL; ++u) {
-                const f64x2* r = static_cast<const f64x2*>(tab.rows[k + u]) + off;
-#pragma unroll
-                for (int c = 0; c < kCpl64; ++c) v[u][c] = __builtin_nontemporal_load(r + c * kBlock);
-            }
-#pragma unroll
-            for (int u = 0; u < UNROLL; ++u)
-#pragma unroll
-                for (int c = 0; c < kCpl64; ++c)
-                    acc[c] = f64x2{step_op<OP>(acc[c][0], v[u][c][0], tab.w[k + u]),
-                                   step_op<OP>(acc[c][1], v[u][c][1], tab.w[k + u])};
-        }
-        for (; k < K; ++k) {
-            const f64x2* r = static_cast<const f64x2*>(tab.rows[k]) + off;
-#pragma unroll
-            for (int c = 0; c < kCpl64; ++c) {
-                const f64x2 v = __builtin_nontemporal_load(r + c * kBlock);
-                acc[c] = f64x2{step_op<OP>(acc[c][0], v[0], tab.w[k]), step_op<OP>(acc[c][1], v[1], tab.w[k])};
-            }
-        }
+        f64x2 res[kCpl64];
+        tile_sum64<OP, FIN, ACC_IN>(res, tab, K, t * tstride2 + threadIdx.x, t * T2 + threadIdx.x, acc_in, b2, e2, fin_val);
 #pragma unroll
         for (int c = 0; c < kCpl64; ++c) {
-            const int64_t i = col + c * kBlock;
-            if (i >= b2 && i < e2)
-                __builtin_nontemporal_store(f64x2{fin_op<FIN>(acc[c][0], fin_val), fin_op<FIN>(acc[c][1], fin_val)},
-                                            out + i);
+            const int64_t i = t * T2 + threadIdx.x + c * kBlock;
+            if (i >= b2 && i < e2) __builtin_nontemporal_store(res[c], out + i);
+        }
+    }
+}
+
+// BURST form (the default; fedavg_tiles.h fedavg_tiles_burst_f32x4): TPB tiles per block per launch, results
+// held in registers (kCpl64 pairs per tile) and stored after the block's last tile.
+template <int OP, int FIN, bool ACC_IN, int TPB>
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, 1)))
+fedavg_tiles_f64x2_burst(const RowTableGeneric tab, const int K, const int64_t tstride2, const f64x2* acc_in,
+                         f64x2* out, const int64_t b2, const int64_t e2, const double fin_val, const int64_t t0,
+                         const int64_t t_end) {
+    constexpr int64_t T2 = (int64_t)kCpl64 * kBlock;
+    f64x2 res[TPB][kCpl64];
+#pragma unroll
+    for (int m = 0; m < TPB; ++m) {
+        const int64_t t = t0 + blockIdx.x + (int64_t)m * gridDim.x;
+        if (t < t_end)
+            tile_sum64<OP, FIN, ACC_IN>(res[m], tab, K, t * tstride2 + threadIdx.x, t * T2 + threadIdx.x, acc_in, b2, e2,
+                                        fin_val);
+    }
+#pragma unroll
+    for (int m = 0; m < TPB; ++m) {
+        const int64_t t = t0 + blockIdx.x + (int64_t)m * gridDim.x;
+        if (t < t_end) {
+#pragma unroll
+            for (int c = 0; c < kCpl64; ++c) {
+                const int64_t i = t * T2 + threadIdx.x + c * kBlock;
+                if (i >= b2 && i < e2) __builtin_nontemporal_store(res[m][c], out + i);
+            }
         }
     }
 }
@@ -328,40 +366,55 @@ static hipError_t launch_rows_f64x2(const RowTableGeneric& tab, int K, const voi
 
 template <int OP, int FIN>
 static hipError_t launch_t64_f(const RowTableGeneric& tab, int K, int64_t ts2, const void* acc_in, void* out, int64_t b2,
-                               int64_t e2, double fin_val, int grid, hipStream_t s) {
-    if (acc_in) {
-        hipLaunchKernelGGL((fedavg_tiles_f64x2<OP, FIN, true>), dim3(grid), dim3(kBlock), 0, s, tab, K, ts2,
-                           static_cast<const f64x2*>(acc_in), static_cast<f64x2*>(out), b2, e2, fin_val);
-    } else {
-        hipLaunchKernelGGL((fedavg_tiles_f64x2<OP, FIN, false>), dim3(grid), dim3(kBlock), 0, s, tab, K, ts2,
-                           static_cast<const f64x2*>(acc_in), static_cast<f64x2*>(out), b2, e2, fin_val);
+                               int64_t e2, double fin_val, int grid, bool burst, hipStream_t s, uint64_t* nl) {
+    const f64x2* ai = static_cast<const f64x2*>(acc_in);
+    f64x2* o = static_cast<f64x2*>(out);
+    constexpr int64_t T2 = (int64_t)kCpl64 * kBlock;
+    if (burst) {
+        return burst_launches(b2 / T2, (e2 - 1) / T2 + 1, grid, kBurstTiles64, nl, [&](int nb, int64_t t0, int64_t t_end) {
+            if (acc_in)
+                hipLaunchKernelGGL((fedavg_tiles_f64x2_burst<OP, FIN, true, kBurstTiles64>), dim3(nb), dim3(kBlock), 0, s,
+                                   tab, K, ts2, ai, o, b2, e2, fin_val, t0, t_end);
+            else
+                hipLaunchKernelGGL((fedavg_tiles_f64x2_burst<OP, FIN, false, kBurstTiles64>), dim3(nb), dim3(kBlock), 0,
+                                   s, tab, K, ts2, ai, o, b2, e2, fin_val, t0, t_end);
+        });
     }
+    if (acc_in) {
+        hipLaunchKernelGGL((fedavg_tiles_f64x2<OP, FIN, true>), dim3(grid), dim3(kBlock), 0, s, tab, K, ts2, ai, o, b2, e2,
+                           fin_val);
+    } else {
+        hipLaunchKernelGGL((fedavg_tiles_f64x2<OP, FIN, false>), dim3(grid), dim3(kBlock), 0, s, tab, K, ts2, ai, o, b2,
+                           e2, fin_val);
+    }
+    if (nl) ++*nl;
     return hipGetLastError();
 }
 
 template <int OP>
 static hipError_t launch_t64_o(const RowTableGeneric& tab, int K, int64_t ts2, const void* acc_in, void* out, int64_t b2,
-                               int64_t e2, int fin, double fin_val, int grid, hipStream_t s) {
+                               int64_t e2, int fin, double fin_val, int grid, bool burst, hipStream_t s, uint64_t* nl) {
     switch (fin) {
         case FEDAVG_FIN_SCALE:
-            return launch_t64_f<OP, FEDAVG_FIN_SCALE>(tab, K, ts2, acc_in, out, b2, e2, fin_val, grid, s);
+            return launch_t64_f<OP, FEDAVG_FIN_SCALE>(tab, K, ts2, acc_in, out, b2, e2, fin_val, grid, burst, s, nl);
         case FEDAVG_FIN_DIV:
-            return launch_t64_f<OP, FEDAVG_FIN_DIV>(tab, K, ts2, acc_in, out, b2, e2, fin_val, grid, s);
+            return launch_t64_f<OP, FEDAVG_FIN_DIV>(tab, K, ts2, acc_in, out, b2, e2, fin_val, grid, burst, s, nl);
         default:
-            return launch_t64_f<OP, FEDAVG_FIN_NONE>(tab, K, ts2, acc_in, out, b2, e2, fin_val, grid, s);
+            return launch_t64_f<OP, FEDAVG_FIN_NONE>(tab, K, ts2, acc_in, out, b2, e2, fin_val, grid, burst, s, nl);
     }
 }
 
 hipError_t launch_tiles_f64(const RowTableGeneric& tab, int K, int64_t tstride_elems, const void* acc_in, void* out,
-                            int64_t begin, int64_t end, int op, int fin, double fin_val, int grid, hipStream_t s) {
+                            int64_t begin, int64_t end, int op, int fin, double fin_val, int grid, bool burst,
+                            hipStream_t s, uint64_t* nl) {
     const int64_t ts2 = tstride_elems / 2, b2 = begin / 2, e2 = end / 2;
     switch (op) {
         case FEDAVG_OP_TORCH:
-            return launch_t64_o<FEDAVG_OP_TORCH>(tab, K, ts2, acc_in, out, b2, e2, fin, fin_val, grid, s);
+            return launch_t64_o<FEDAVG_OP_TORCH>(tab, K, ts2, acc_in, out, b2, e2, fin, fin_val, grid, burst, s, nl);
         case FEDAVG_OP_UNWEIGHTED:
-            return launch_t64_o<FEDAVG_OP_UNWEIGHTED>(tab, K, ts2, acc_in, out, b2, e2, fin, fin_val, grid, s);
+            return launch_t64_o<FEDAVG_OP_UNWEIGHTED>(tab, K, ts2, acc_in, out, b2, e2, fin, fin_val, grid, burst, s, nl);
         default:
-            return launch_t64_o<FEDAVG_OP_NUMPY>(tab, K, ts2, acc_in, out, b2, e2, fin, fin_val, grid, s);
+            return launch_t64_o<FEDAVG_OP_NUMPY>(tab, K, ts2, acc_in, out, b2, e2, fin, fin_val, grid, burst, s, nl);
     }
 }
 

@@ -181,75 +181,109 @@ constexpr int kCpl16 = kTile16 / (8 * kBlock);  // 2
 #define FEDAVG_NARROW_UNROLL 6  // clients whose loads are in flight together (A/B: profiles/r01/narrow_unroll_ab.jsonl)
 #endif
 
+// One tile's arrival-ordered sum for this lane's kCpl16 8-element groups, packed to the output format.
+template <int FMT, int OP, int FIN, bool ACC_IN>
+__device__ __forceinline__ void tile_sum16(u32x4 (&res)[kCpl16], const RowTableNarrow& tab, const int K,
+                                           const int64_t off, const int64_t col, const u32x4* acc_in, const int64_t b8,
+                                           const int64_t e8, const float fv) {
+    constexpr int UNROLL = FEDAVG_NARROW_UNROLL;
+    float acc[kCpl16][8];
+    int k = 0;
+    if constexpr (ACC_IN) {
+#pragma unroll
+        for (int c = 0; c < kCpl16; ++c) {
+            const int64_t i = col + c * kBlock;
+            const u32x4 a = (i >= b8 && i < e8) ? acc_in[i] : u32x4{0, 0, 0, 0};
+#pragma unroll
+            for (int j = 0; j < 8; ++j) acc[c][j] = load16<FMT>(half_of(a, j));
+        }
+    } else {
+        const u32x4* r = static_cast<const u32x4*>(tab.rows[0]) + off;
+#pragma unroll
+        for (int c = 0; c < kCpl16; ++c) {
+            const u32x4 a = __builtin_nontemporal_load(r + c * kBlock);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) acc[c][j] = first16<FMT, OP>(load16<FMT>(half_of(a, j)), tab.w_first[0]);
+        }
+        k = 1;
+    }
+    for (; k + UNROLL <= K; k += UNROLL) {
+        u32x4 v[UNROLL][kCpl16];
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u) {
+            const u32x4* r = static_cast<const u32x4*>(tab.rows[k + u]) + off;
+#pragma unroll
+            for (int c = 0; c < kCpl16; ++c) v[u][c] = __builtin_nontemporal_load(r + c * kBlock);
+        }
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u) {
+            const float w = tab.w_step[k + u];
+#pragma unroll
+            for (int c = 0; c < kCpl16; ++c)
+#pragma unroll
+                for (int j = 0; j < 8; ++j) acc[c][j] = step16<FMT, OP>(acc[c][j], load16<FMT>(half_of(v[u][c], j)), w);
+        }
+    }
+    for (; k < K; ++k) {
+        const u32x4* r = static_cast<const u32x4*>(tab.rows[k]) + off;
+        const float w = tab.w_step[k];
+#pragma unroll
+        for (int c = 0; c < kCpl16; ++c) {
+            const u32x4 v = __builtin_nontemporal_load(r + c * kBlock);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) acc[c][j] = step16<FMT, OP>(acc[c][j], load16<FMT>(half_of(v, j)), w);
+        }
+    }
+#pragma unroll
+    for (int c = 0; c < kCpl16; ++c)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            res[c][j] = (uint32_t)bits16<FMT>(fin16<FMT, FIN>(acc[c][2 * j], fv)) |
+                        ((uint32_t)bits16<FMT>(fin16<FMT, FIN>(acc[c][2 * j + 1], fv)) << 16);
+}
+
+// per-tile-store form (launch variant bit 3): each tile's results stored as it finishes
 template <int FMT, int OP, int FIN, bool ACC_IN>
 __global__ void __launch_bounds__(kBlock) fedavg_tiles_narrow(const RowTableNarrow tab, const int K,
                                                                const int64_t tstride8, const u32x4* acc_in,
                                                                u32x4* out, const int64_t b8, const int64_t e8,
                                                                const float fv) {
     constexpr int64_t T8 = (int64_t)kCpl16 * kBlock;
-    constexpr int UNROLL = FEDAVG_NARROW_UNROLL;
     const int64_t t_last = (e8 - 1) / T8;
     for (int64_t t = b8 / T8 + blockIdx.x; t <= t_last; t += gridDim.x) {
-        const int64_t off = t * tstride8 + threadIdx.x;
-        const int64_t col = t * T8 + threadIdx.x;
-        float acc[kCpl16][8];
-        int k = 0;
-        if constexpr (ACC_IN) {
-#pragma unroll
-            for (int c = 0; c < kCpl16; ++c) {
-                const int64_t i = col + c * kBlock;
-                const u32x4 a = (i >= b8 && i < e8) ? acc_in[i] : u32x4{0, 0, 0, 0};
-#pragma unroll
-                for (int j = 0; j < 8; ++j) acc[c][j] = load16<FMT>(half_of(a, j));
-            }
-        } else {
-            const u32x4* r = static_cast<const u32x4*>(tab.rows[0]) + off;
-#pragma unroll
-            for (int c = 0; c < kCpl16; ++c) {
-                const u32x4 a = __builtin_nontemporal_load(r + c * kBlock);
-#pragma unroll
-                for (int j = 0; j < 8; ++j) acc[c][j] = first16<FMT, OP>(load16<FMT>(half_of(a, j)), tab.w_first[0]);
-            }
-            k = 1;
-        }
-        for (; k + UNROLL <= K; k += UNROLL) {
-            u32x4 v[UNROLL][kCpl16];
-#pragma unroll
-            for (int u = 0; u < UNROLL; ++u) {
-                const u32x4* r = static_cast<const u32x4*>(tab.rows[k + u]) + off;
-#pragma unroll
-                for (int c = 0; c < kCpl16; ++c) v[u][c] = __builtin_nontemporal_load(r + c * kBlock);
-            }
-#pragma unroll
-            for (int u = 0; u < UNROLL; ++u) {
-                const float w = tab.w_step[k + u];
-#pragma unroll
-                for (int c = 0; c < kCpl16; ++c)
-#pragma unroll
-                    for (int j = 0; j < 8; ++j) acc[c][j] = step16<FMT, OP>(acc[c][j], load16<FMT>(half_of(v[u][c], j)), w);
-            }
-        }
-        for (; k < K; ++k) {
-            const u32x4* r = static_cast<const u32x4*>(tab.rows[k]) + off;
-            const float w = tab.w_step[k];
-#pragma unroll
-            for (int c = 0; c < kCpl16; ++c) {
-                const u32x4 v = __builtin_nontemporal_load(r + c * kBlock);
-#pragma unroll
-                for (int j = 0; j < 8; ++j) acc[c][j] = step16<FMT, OP>(acc[c][j], load16<FMT>(half_of(v, j)), w);
-            }
-        }
+        u32x4 res[kCpl16];
+        tile_sum16<FMT, OP, FIN, ACC_IN>(res, tab, K, t * tstride8 + threadIdx.x, t * T8 + threadIdx.x, acc_in, b8, e8, fv);
 #pragma unroll
         for (int c = 0; c < kCpl16; ++c) {
-            const int64_t i = col + c * kBlock;
-            if (i >= b8 && i < e8) {
-                u32x4 o;
+            const int64_t i = t * T8 + threadIdx.x + c * kBlock;
+            if (i >= b8 && i < e8) __builtin_nontemporal_store(res[c], out + i);
+        }
+    }
+}
+
+// BURST form (the default; fedavg_tiles.h fedavg_tiles_burst_f32x4 has the measurements): TPB tiles per
+// block per launch, their packed results held in registers and stored after the block's last tile.
+template <int FMT, int OP, int FIN, bool ACC_IN, int TPB>
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2, 2)))
+fedavg_tiles_narrow_burst(const RowTableNarrow tab, const int K, const int64_t tstride8, const u32x4* acc_in, u32x4* out,
+                          const int64_t b8, const int64_t e8, const float fv, const int64_t t0, const int64_t t_end) {
+    constexpr int64_t T8 = (int64_t)kCpl16 * kBlock;
+    u32x4 res[TPB][kCpl16];
 #pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    o[j] = (uint32_t)bits16<FMT>(fin16<FMT, FIN>(acc[c][2 * j], fv)) |
-                           ((uint32_t)bits16<FMT>(fin16<FMT, FIN>(acc[c][2 * j + 1], fv)) << 16);
-                }
-                __builtin_nontemporal_store(o, out + i);
+    for (int m = 0; m < TPB; ++m) {
+        const int64_t t = t0 + blockIdx.x + (int64_t)m * gridDim.x;
+        if (t < t_end)
+            tile_sum16<FMT, OP, FIN, ACC_IN>(res[m], tab, K, t * tstride8 + threadIdx.x, t * T8 + threadIdx.x, acc_in, b8,
+                                             e8, fv);
+    }
+#pragma unroll
+    for (int m = 0; m < TPB; ++m) {
+        const int64_t t = t0 + blockIdx.x + (int64_t)m * gridDim.x;
+        if (t < t_end) {
+#pragma unroll
+            for (int c = 0; c < kCpl16; ++c) {
+                const int64_t i = t * T8 + threadIdx.x + c * kBlock;
+                if (i >= b8 && i < e8) __builtin_nontemporal_store(res[m][c], out + i);
             }
         }
     }
@@ -257,49 +291,68 @@ __global__ void __launch_bounds__(kBlock) fedavg_tiles_narrow(const RowTableNarr
 
 template <int FMT, int OP, int FIN>
 static hipError_t launch_t16_a(const RowTableNarrow& tab, int K, int64_t tstride8, const void* acc_in, void* out,
-                               int64_t b8, int64_t e8, float fv, int grid, hipStream_t s) {
+                               int64_t b8, int64_t e8, float fv, int grid, bool burst, hipStream_t s, uint64_t* nl) {
+    const u32x4* ai = static_cast<const u32x4*>(acc_in);
+    u32x4* o = static_cast<u32x4*>(out);
+    constexpr int64_t T8 = (int64_t)kCpl16 * kBlock;
+    if (burst) {
+        return burst_launches(b8 / T8, (e8 - 1) / T8 + 1, grid, kBurstTiles, nl, [&](int nb, int64_t t0, int64_t t_end) {
+            if (acc_in)
+                hipLaunchKernelGGL((fedavg_tiles_narrow_burst<FMT, OP, FIN, true, kBurstTiles>), dim3(nb), dim3(kBlock), 0,
+                                   s, tab, K, tstride8, ai, o, b8, e8, fv, t0, t_end);
+            else
+                hipLaunchKernelGGL((fedavg_tiles_narrow_burst<FMT, OP, FIN, false, kBurstTiles>), dim3(nb), dim3(kBlock),
+                                   0, s, tab, K, tstride8, ai, o, b8, e8, fv, t0, t_end);
+        });
+    }
     if (acc_in) {
-        hipLaunchKernelGGL((fedavg_tiles_narrow<FMT, OP, FIN, true>), dim3(grid), dim3(kBlock), 0, s, tab, K, tstride8,
-                           static_cast<const u32x4*>(acc_in), static_cast<u32x4*>(out), b8, e8, fv);
+        hipLaunchKernelGGL((fedavg_tiles_narrow<FMT, OP, FIN, true>), dim3(grid), dim3(kBlock), 0, s, tab, K, tstride8, ai,
+                           o, b8, e8, fv);
     } else {
         hipLaunchKernelGGL((fedavg_tiles_narrow<FMT, OP, FIN, false>), dim3(grid), dim3(kBlock), 0, s, tab, K, tstride8,
-                           static_cast<const u32x4*>(acc_in), static_cast<u32x4*>(out), b8, e8, fv);
+                           ai, o, b8, e8, fv);
     }
+    if (nl) ++*nl;
     return hipGetLastError();
 }
 
 template <int FMT, int OP>
 static hipError_t launch_t16_f(const RowTableNarrow& tab, int K, int64_t tstride8, const void* acc_in, void* out,
-                               int64_t b8, int64_t e8, int fin, float fv, int grid, hipStream_t s) {
+                               int64_t b8, int64_t e8, int fin, float fv, int grid, bool burst, hipStream_t s,
+                               uint64_t* nl) {
     switch (fin) {
         case FEDAVG_FIN_SCALE:
-            return launch_t16_a<FMT, OP, FEDAVG_FIN_SCALE>(tab, K, tstride8, acc_in, out, b8, e8, fv, grid, s);
+            return launch_t16_a<FMT, OP, FEDAVG_FIN_SCALE>(tab, K, tstride8, acc_in, out, b8, e8, fv, grid, burst, s, nl);
         case FEDAVG_FIN_DIV:
-            return launch_t16_a<FMT, OP, FEDAVG_FIN_DIV>(tab, K, tstride8, acc_in, out, b8, e8, fv, grid, s);
+            return launch_t16_a<FMT, OP, FEDAVG_FIN_DIV>(tab, K, tstride8, acc_in, out, b8, e8, fv, grid, burst, s, nl);
         default:
-            return launch_t16_a<FMT, OP, FEDAVG_FIN_NONE>(tab, K, tstride8, acc_in, out, b8, e8, fv, grid, s);
+            return launch_t16_a<FMT, OP, FEDAVG_FIN_NONE>(tab, K, tstride8, acc_in, out, b8, e8, fv, grid, burst, s, nl);
     }
 }
 
 template <int FMT>
 static hipError_t launch_t16_o(const RowTableNarrow& tab, int K, int64_t tstride8, const void* acc_in, void* out,
-                               int64_t b8, int64_t e8, int op, int fin, float fv, int grid, hipStream_t s) {
+                               int64_t b8, int64_t e8, int op, int fin, float fv, int grid, bool burst, hipStream_t s,
+                               uint64_t* nl) {
     switch (op) {
         case FEDAVG_OP_TORCH:
-            return launch_t16_f<FMT, FEDAVG_OP_TORCH>(tab, K, tstride8, acc_in, out, b8, e8, fin, fv, grid, s);
+            return launch_t16_f<FMT, FEDAVG_OP_TORCH>(tab, K, tstride8, acc_in, out, b8, e8, fin, fv, grid, burst, s, nl);
         case FEDAVG_OP_UNWEIGHTED:
-            return launch_t16_f<FMT, FEDAVG_OP_UNWEIGHTED>(tab, K, tstride8, acc_in, out, b8, e8, fin, fv, grid, s);
+            return launch_t16_f<FMT, FEDAVG_OP_UNWEIGHTED>(tab, K, tstride8, acc_in, out, b8, e8, fin, fv, grid, burst, s,
+                                                            nl);
         default:
-            return launch_t16_f<FMT, FEDAVG_OP_NUMPY>(tab, K, tstride8, acc_in, out, b8, e8, fin, fv, grid, s);
+            return launch_t16_f<FMT, FEDAVG_OP_NUMPY>(tab, K, tstride8, acc_in, out, b8, e8, fin, fv, grid, burst, s, nl);
     }
 }
 
 hipError_t launch_tiles_narrow(const RowTableNarrow& tab, int K, int64_t tstride_elems, const void* acc_in, void* out,
                                int64_t begin, int64_t end, int fmt, int op, int fin, float fin_val, int grid,
-                               hipStream_t s) {
+                               bool burst, hipStream_t s, uint64_t* nl) {
     const int64_t ts8 = tstride_elems / 8, b8 = begin / 8, e8 = end / 8;
-    if (fmt == FEDAVG_BF16) return launch_t16_o<FEDAVG_BF16>(tab, K, ts8, acc_in, out, b8, e8, op, fin, fin_val, grid, s);
-    if (fmt == FEDAVG_F16) return launch_t16_o<FEDAVG_F16>(tab, K, ts8, acc_in, out, b8, e8, op, fin, fin_val, grid, s);
+    if (fmt == FEDAVG_BF16)
+        return launch_t16_o<FEDAVG_BF16>(tab, K, ts8, acc_in, out, b8, e8, op, fin, fin_val, grid, burst, s, nl);
+    if (fmt == FEDAVG_F16)
+        return launch_t16_o<FEDAVG_F16>(tab, K, ts8, acc_in, out, b8, e8, op, fin, fin_val, grid, burst, s, nl);
     return hipErrorInvalidValue;
 }
 

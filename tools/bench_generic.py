@@ -21,6 +21,7 @@ def main():
     ap.add_argument("--params", type=float, default=125e6)
     ap.add_argument("--dtype", choices=["float64", "float32"], default="float64")
     ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--variants", default="0", help="comma list of fedavg_set_variant values, interleaved rounds")
     ap.add_argument("--layout", choices=["rows", "tiled"], default="rows",
                     help="rows: K separate client buffers (fedavg_accumulate); tiled: the engine's fp64 slab "
                          "(fedavg_accumulate_tiled64, float64 only)")
@@ -60,15 +61,24 @@ def main():
                            N.FEDAVG_FIN_SCALE, sum(ws))
     torch.cuda.synchronize()
 
-    launch()
-    ctx.sync()
-    ctx.timing_begin()
-    for _ in range(args.steps):
-        launch()
-    ms = ctx.timing_end() / args.steps
+    variants = [int(v) for v in args.variants.split(",")]
+    res = {v: [] for v in variants}
+    for rep in range(3):
+        for v in variants:
+            ctx.set_variant(v)
+            launch()
+            ctx.sync()
+            ctx.timing_begin()
+            for _ in range(args.steps):
+                launch()
+            res[v].append(ctx.timing_end() / args.steps)
+    ctx.set_variant(0)
     nbytes = (K + 1) * P * out.element_size()
-    print(json.dumps({"tool": "bench_generic", "dtype": args.dtype, "layout": args.layout, "clients": K, "params": P, "kernel_ms": round(ms, 3),
-                      "alg_GBs": round(nbytes / ms / 1e6, 1), "frac_of_8TBs": round(nbytes / ms / 1e6 / 8000, 4)}))
+    for v in variants:
+        ms = sorted(res[v])[len(res[v]) // 2]
+        print(json.dumps({"tool": "bench_generic", "dtype": args.dtype, "layout": args.layout, "clients": K, "params": P,
+                          "variant": v, "kernel_ms": round(ms, 3), "alg_GBs": round(nbytes / ms / 1e6, 1),
+                          "frac_of_8TBs": round(nbytes / ms / 1e6 / 8000, 4)}), flush=True)
 
 
 if __name__ == "__main__":

@@ -20,7 +20,9 @@ def main():
     ap.add_argument("--fmt", choices=["bfloat16", "float16"], default="bfloat16")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--mode", choices=["torch", "numpy"], default="torch")
-    ap.add_argument("--blocks-per-cu", default="2", help="comma list: interleaved same-process sweep")
+    ap.add_argument("--blocks-per-cu", default="0", help="comma list: interleaved same-process sweep (0 = default)")
+    ap.add_argument("--variants", default="0", help="comma list of fedavg_set_variant values (0 = burst kernel, "
+                                                      "8 = per-tile stores), swept with every blocks-per-cu value")
     ap.add_argument("--layout", choices=["rows", "tiled"], default="tiled",
                     help="rows: K separate client buffers (fedavg_accumulate); tiled: the engine's slab "
                          "(fedavg_accumulate_tiled16)")
@@ -59,21 +61,25 @@ def main():
         else:
             ctx.accumulate(bases, ws, P, out.data_ptr(), code, code, op, fin, sum(ws))
     alg = 2.0 * K * P + 2.0 * P
-    bpcs = [int(b) for b in args.blocks_per_cu.split(",")]
-    res = {b: [] for b in bpcs}
+    cfgs = [(int(v), int(b)) for v in args.variants.split(",") for b in args.blocks_per_cu.split(",")]
+    res = {c: [] for c in cfgs}
     for rep in range(3):
-        for b in bpcs:
-            ctx.set_launch(b, 0)
+        for c in cfgs:
+            ctx.set_variant(c[0])
+            ctx.set_launch(c[1], 0)
             launch()
             ctx.sync()
             ctx.timing_begin()
             for _ in range(args.steps):
                 launch()
-            res[b].append(ctx.timing_end() / args.steps)
-    for b in bpcs:
-        ms = sorted(res[b])[len(res[b]) // 2]
+            res[c].append(ctx.timing_end() / args.steps)
+    ctx.set_variant(0)
+    ctx.set_launch(0, 0)
+    for c in cfgs:
+        ms = sorted(res[c])[len(res[c]) // 2]
         print(json.dumps({"tool": "bench_narrow", "fmt": args.fmt, "mode": args.mode, "clients": K, "params": P,
-                          "blocks_per_cu": b, "layout": args.layout, "kernel_ms": round(ms, 3), "alg_GBs": round(alg / ms / 1e6, 1),
+                          "variant": c[0], "blocks_per_cu": c[1], "layout": args.layout, "kernel_ms": round(ms, 3),
+                          "alg_GBs": round(alg / ms / 1e6, 1),
                           "frac_of_8TBs": round(alg / ms / 1e6 / 8000.0, 4),
                           "GiBs_aggregated": round(2.0 * K * P / (ms / 1e3) / 2 ** 30, 1)}), flush=True)
 
