@@ -83,9 +83,45 @@ __device__ __forceinline__ void store4(f32x4* p, f32x4 v) {
 // 0), then step(client k) for every later client, UNROLL clients' loads issued before their arithmetic.  Client
 // rows are tiled (row + off is this lane's first column of the tile); acc_in is indexed by global column and
 // masked to [b4, e4).
-template <int OP, bool ACC_IN, int UNROLL, int CPL>
+// GROUPED: every load group holds UNROLL clients from client 0 on (the first client's operation applied in
+// the first group; a partial last group re-loads its last client in the missing slots, branch-free, and skips
+// their arithmetic), so a tile takes ceil(K / UNROLL) load round trips instead of 1 + (K-1) / UNROLL + the
+// remainder.
+template <int OP, bool ACC_IN, int UNROLL, int CPL, bool GROUPED = false>
 __device__ __forceinline__ void tile_sum(f32x4 (&acc)[CPL], const RowTableF32& tab, const int K, const int64_t off,
                                          const int64_t col, const f32x4* acc_in, const int64_t b4, const int64_t e4) {
+    if constexpr (GROUPED) {
+        if constexpr (ACC_IN) {
+#pragma unroll
+            for (int c = 0; c < CPL; ++c) {
+                const int64_t i = col + c * kBlock;
+                acc[c] = (i >= b4 && i < e4) ? acc_in[i] : f32x4{0, 0, 0, 0};
+            }
+        }
+        for (int k = 0; k < K; k += UNROLL) {
+            f32x4 v[UNROLL][CPL];
+#pragma unroll
+            for (int j = 0; j < UNROLL; ++j) {
+                const f32x4* r = tab.rows[k + j < K ? k + j : K - 1] + off;
+#pragma unroll
+                for (int c = 0; c < CPL; ++c) v[j][c] = __builtin_nontemporal_load(r + c * kBlock);
+            }
+#pragma unroll
+            for (int j = 0; j < UNROLL; ++j) {
+                if (k + j < K) {
+                    const float w = tab.w[k + j];
+                    if (!ACC_IN && k + j == 0) {
+#pragma unroll
+                        for (int c = 0; c < CPL; ++c) acc[c] = first4<OP>(v[j][c], w);
+                    } else {
+#pragma unroll
+                        for (int c = 0; c < CPL; ++c) acc[c] = step4<OP>(acc[c], v[j][c], w);
+                    }
+                }
+            }
+        }
+        return;
+    }
     int k = 0;
     if constexpr (ACC_IN) {
 #pragma unroll

@@ -264,8 +264,8 @@ fedavg_tiles_epi_burst_f32x4(const RowTableF32 tab, const int K, const int64_t t
         const int64_t t = t0 + blockIdx.x + (int64_t)m * gridDim.x;
         if (t < t_end) {
             f32x4 acc[CPL];
-            tile_sum<OP, ACC_IN, UNROLL, CPL>(acc, tab, K, t * tstride4 + threadIdx.x, t * T4 + threadIdx.x, acc_in, b4,
-                                              e4);
+            tile_sum<OP, ACC_IN, UNROLL, CPL, true>(acc, tab, K, t * tstride4 + threadIdx.x, t * T4 + threadIdx.x, acc_in,
+                                                    b4, e4);
 #pragma unroll
             for (int c = 0; c < CPL; ++c) dd[m][c] = fin4<FIN>(acc[c], fin_val);
         }
