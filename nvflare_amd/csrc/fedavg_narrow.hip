@@ -182,7 +182,8 @@ constexpr int kCpl16 = kTile16 / (8 * kBlock);  // 2
 #endif
 
 // One tile's arrival-ordered sum for this lane's kCpl16 8-element groups, packed to the output format.
-template <int FMT, int OP, int FIN, bool ACC_IN>
+// GROUPED (the burst form): load groups of UNROLL clients from client 0 on, as fedavg_arith.h tile_sum.
+template <int FMT, int OP, int FIN, bool ACC_IN, bool GROUPED = false>
 __device__ __forceinline__ void tile_sum16(u32x4 (&res)[kCpl16], const RowTableNarrow& tab, const int K,
                                            const int64_t off, const int64_t col, const u32x4* acc_in, const int64_t b8,
                                            const int64_t e8, const float fv) {
@@ -197,7 +198,38 @@ __device__ __forceinline__ void tile_sum16(u32x4 (&res)[kCpl16], const RowTableN
 #pragma unroll
             for (int j = 0; j < 8; ++j) acc[c][j] = load16<FMT>(half_of(a, j));
         }
-    } else {
+    }
+    if constexpr (GROUPED) {
+        for (; k < K; k += UNROLL) {
+            u32x4 v[UNROLL][kCpl16];
+#pragma unroll
+            for (int u = 0; u < UNROLL; ++u) {
+                const u32x4* r = static_cast<const u32x4*>(tab.rows[k + u < K ? k + u : K - 1]) + off;
+#pragma unroll
+                for (int c = 0; c < kCpl16; ++c) v[u][c] = __builtin_nontemporal_load(r + c * kBlock);
+            }
+#pragma unroll
+            for (int u = 0; u < UNROLL; ++u) {
+                if (k + u < K) {
+                    if (!ACC_IN && k + u == 0) {
+                        const float w = tab.w_first[0];
+#pragma unroll
+                        for (int c = 0; c < kCpl16; ++c)
+#pragma unroll
+                            for (int j = 0; j < 8; ++j) acc[c][j] = first16<FMT, OP>(load16<FMT>(half_of(v[u][c], j)), w);
+                    } else {
+                        const float w = tab.w_step[k + u];
+#pragma unroll
+                        for (int c = 0; c < kCpl16; ++c)
+#pragma unroll
+                            for (int j = 0; j < 8; ++j)
+                                acc[c][j] = step16<FMT, OP>(acc[c][j], load16<FMT>(half_of(v[u][c], j)), w);
+                    }
+                }
+            }
+        }
+        k = K;
+    } else if constexpr (!ACC_IN) {
         const u32x4* r = static_cast<const u32x4*>(tab.rows[0]) + off;
 #pragma unroll
         for (int c = 0; c < kCpl16; ++c) {
@@ -262,7 +294,9 @@ __global__ void __launch_bounds__(kBlock) fedavg_tiles_narrow(const RowTableNarr
 }
 
 // BURST form (the default; fedavg_tiles.h fedavg_tiles_burst_f32x4 has the measurements): TPB tiles per
-// block per launch, their packed results held in registers and stored after the block's last tile.
+// block per launch, their packed results held in registers and stored after the block's last tile; client
+// loads grouped from client 0 on (bf16 64 x 1e9: 85.6 % against 84.4 % ungrouped and 82.0 % for the per-tile
+// form, profiles/r02/ab/narrow_burst_grouped.jsonl).
 template <int FMT, int OP, int FIN, bool ACC_IN, int TPB>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2, 2)))
 fedavg_tiles_narrow_burst(const RowTableNarrow tab, const int K, const int64_t tstride8, const u32x4* acc_in, u32x4* out,
@@ -273,8 +307,8 @@ fedavg_tiles_narrow_burst(const RowTableNarrow tab, const int K, const int64_t t
     for (int m = 0; m < TPB; ++m) {
         const int64_t t = t0 + blockIdx.x + (int64_t)m * gridDim.x;
         if (t < t_end)
-            tile_sum16<FMT, OP, FIN, ACC_IN>(res[m], tab, K, t * tstride8 + threadIdx.x, t * T8 + threadIdx.x, acc_in, b8,
-                                             e8, fv);
+            tile_sum16<FMT, OP, FIN, ACC_IN, true>(res[m], tab, K, t * tstride8 + threadIdx.x, t * T8 + threadIdx.x,
+                                                   acc_in, b8, e8, fv);
     }
 #pragma unroll
     for (int m = 0; m < TPB; ++m) {
