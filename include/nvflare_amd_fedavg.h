@@ -27,8 +27,8 @@ extern "C" {
 #endif
 
 /* Bumped whenever a struct layout or an entry point changes (v3: Rprop / ASGD fields appended to struct
- * fedavg_epilogue; v4: fedavg_launch_count).  fedavg_struct_size() lets a binding check each struct's size as well. */
-#define FEDAVG_ABI_VERSION 4
+ * fedavg_epilogue; v4: fedavg_launch_count; v5: fedavg_d2h_multi).  fedavg_struct_size() lets a binding check each struct's size as well. */
+#define FEDAVG_ABI_VERSION 5
 
 /* element types of client rows (in_dtype) and of the running sum / result (acc_dtype) */
 enum fedavg_dtype {
@@ -173,6 +173,12 @@ int fedavg_d2d_tiled(fedavg_ctx* ctx, void* base, size_t tile_bytes, size_t tile
 /* Device -> host; returns when the bytes are in `dst` (waits for prior compute on the handle).  Large
  * pageable destinations are drained through the pinned ring by the host copy threads. */
 int fedavg_d2h(fedavg_ctx* ctx, void* dst, const void* src, size_t nbytes);
+/* n device -> host copies in one call: piece i is nbytes[i] bytes from dev_base + dev_offsets[i] to
+ * host_base + host_offsets[i], after the work queued on the context so far; returns when the host holds them.
+ * A page-locked host_base (fedavg_host_register) takes one DMA per piece and one synchronisation.  Serves
+ * the sharded server optimizer's egress (every parameter's bucket on this device into the host weights). */
+int fedavg_d2h_multi(fedavg_ctx* ctx, void* host_base, const void* dev_base, int n, const size_t* host_offsets,
+                     const size_t* dev_offsets, const size_t* nbytes);
 /* Page-lock caller-owned host memory for direct DMA (hipHostRegister, portable across devices): copies to
  * and from it skip the pinned ring.  The caller unregisters it before the memory is freed. */
 int fedavg_host_register(fedavg_ctx* ctx, void* p, size_t nbytes);

@@ -50,8 +50,14 @@ def build_library(force: bool = False, verbose: bool = False, jobs: int = 0) -> 
     os.makedirs(OBJ_DIR, exist_ok=True)
     inc = [f"-I{os.path.join(ROOT, 'include')}", f"-I{CSRC}"]
 
+    headers = [os.path.join(CSRC, h) for h in HEADERS] + [os.path.join(ROOT, "include", "nvflare_amd_fedavg.h")]
+    newest_header = max(os.path.getmtime(h) for h in headers)
+
     def compile_one(src: str) -> str:
         obj = os.path.join(OBJ_DIR, src + ".o")
+        if not force and os.path.exists(obj) and os.path.getmtime(obj) > max(
+                os.path.getmtime(os.path.join(CSRC, src)), newest_header):
+            return obj  # up to date: only changed sources (or any header change) recompile
         cmd = [HIPCC, *FLAGS, *inc, "-c", os.path.join(CSRC, src), "-o", obj]
         if verbose:
             print(" ".join(cmd), flush=True)

@@ -41,7 +41,7 @@ FEDAVG_FIN_NONE = 0
 FEDAVG_FIN_SCALE = 1
 FEDAVG_FIN_DIV = 2
 
-ABI_VERSION = 4  # include/nvflare_amd_fedavg.h FEDAVG_ABI_VERSION
+ABI_VERSION = 5  # include/nvflare_amd_fedavg.h FEDAVG_ABI_VERSION
 
 c_void_p = ctypes.c_void_p
 c_int = ctypes.c_int
@@ -66,6 +66,8 @@ _SIGNATURES = {
     "fedavg_h2d_tiled_multi": [c_void_p, c_void_p, c_size_t, c_size_t, c_int, ctypes.POINTER(c_size_t),
                                ctypes.POINTER(c_void_p), ctypes.POINTER(c_size_t)],
     "fedavg_d2h": [c_void_p, c_void_p, c_void_p, c_size_t],
+    "fedavg_d2h_multi": [c_void_p, c_void_p, c_void_p, c_int, ctypes.POINTER(c_size_t), ctypes.POINTER(c_size_t),
+                         ctypes.POINTER(c_size_t)],
     "fedavg_host_register": [c_void_p, c_void_p, c_size_t],
     "fedavg_host_unregister": [c_void_p, c_void_p],
     "fedavg_d2d": [c_void_p, c_void_p, c_void_p, c_size_t],

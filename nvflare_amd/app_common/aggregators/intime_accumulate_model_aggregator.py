@@ -67,7 +67,8 @@ class InTimeAccumulateWeightedAggregator(Aggregator):
         the aggregated fp32 values stay in HBM as ``DeferredAggregate`` objects until read, so the device
         FedOpt generator steps the model in the same launch as the aggregation (nvflare_amd/deferred.py),
         and ``devices``: several HIP devices, every key split into per-device parameter buckets
-        (nvflare_amd/sharding.py; results are eager, ``defer_result`` applies to one device only).
+        (nvflare_amd/sharding.py; with ``defer_result`` the values are ``ShardedDeferredAggregate`` objects whose
+        bucket pieces stay on their devices).
         """
         super().__init__()
         self._single_dxo_key = ""

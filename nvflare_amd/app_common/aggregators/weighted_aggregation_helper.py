@@ -131,9 +131,10 @@ class WeightedAggregationHelper(object):
             max_resident_bytes: HBM budget for staged contributions before they are folded.
             devices: several HIP devices: every key is split into per-device parameter buckets
                 (sharding.ShardedFedAvg; host arrays only), bit-identical to one device.
-            defer_result: ``get_result`` returns the fp32 keys as ``DeferredAggregate`` values that stay
-                in HBM until read (``materialize()`` / ``np.asarray``) or consumed by the device FedOpt
-                generator in the same launch as its optimizer step (nvflare_amd/deferred.py).
+            defer_result: ``get_result`` returns the fp32 keys as ``DeferredAggregate`` values
+                (``ShardedDeferredAggregate`` with ``devices``) that stay in HBM until read
+                (``materialize()`` / ``np.asarray``) or consumed by the device FedOpt generator in the same
+                launch as its optimizer step (nvflare_amd/deferred.py).
         """
         super().__init__()
         self.lock = threading.Lock()
@@ -239,7 +240,7 @@ class WeightedAggregationHelper(object):
         with self.lock:
             if not self._engine.keys:
                 device_results = {}
-            elif self.defer_result and isinstance(self._engine, DeviceFedAvg):
+            elif self.defer_result:
                 device_results = self._engine.result_deferred()
             else:
                 device_results = self._engine.result()

@@ -48,7 +48,7 @@ from ...compat import (
     from_shareable,
     make_model_learnable,
 )
-from ...deferred import DeferredAggregate, FusedEntry, materialize_deferred
+from ...deferred import DeferredAggregate, DeferredValue, FusedEntry, materialize_deferred
 from ...device import DeviceContext, HostArenaPool
 
 _ALIGN = 64  # elements per parameter slot boundary (256 B), as in the aggregation engine
@@ -157,6 +157,7 @@ class DeviceServerOptimizer:
         self.g = None
         self.host_pool = HostArenaPool()  # host copies of p returned by the generator, reused when released
         self.egress_pending = False  # the last fused step left readiness marks for a pipelined D2H of p
+        self.pipelined_egress = True  # fused steps may leave such marks (off for the shards of a sharded step)
         with torch.no_grad():
             for s in slots:
                 view = self.p[s.offset:s.offset + s.n].view(s.param.shape)
@@ -433,7 +434,7 @@ class DeviceServerOptimizer:
         # pipelined egress of the new weights: only when this one round steps every parameter, in a launch order
         # whose parameter offsets increase (then "bytes [0, X) of p are final" is a true statement per mark)
         egress = False
-        if len(cand) == 1:
+        if len(cand) == 1 and self.pipelined_egress:
             rnd, by_key = next(iter(cand.values()))
             if len(by_key) == len(self.slots):
                 order = sorted(by_key.items(), key=lambda kv: rnd.keys[kv[0]].offset)
@@ -460,9 +461,14 @@ class DeviceServerOptimizer:
 
 
 class PTFedOptModelShareableGenerator(FullModelShareableGenerator):
-    def __init__(self, optimizer_args: dict = None, lr_scheduler_args: dict = None, source_model="model", device=None):
-        """Same arguments as the reference (fedopt.py:30-81); ``device`` picks the HIP device."""
+    def __init__(self, optimizer_args: dict = None, lr_scheduler_args: dict = None, source_model="model", device=None,
+                 devices: Optional[list] = None):
+        """Same arguments as the reference (fedopt.py:30-81); ``device`` picks the HIP device.  ``devices``
+        (two or more HIP devices, the aggregator's ``devices`` in the same order): the optimizer state is
+        split by parameter bucket over them and each bucket is stepped on its device, in the launch that
+        aggregates it when the aggregator defers its result (``sharded_fedopt.ShardedServerOptimizer``)."""
         super().__init__(device=hip_device_index(device) if device not in (None, "cpu") else None)
+        self.devices = [int(d) for d in devices] if devices and len(devices) > 1 else None
         if not optimizer_args:
             self.logger.warning("No optimizer_args provided. Using FedOpt with SGD and lr 1.0")
             optimizer_args = {"path": "torch.optim.SGD", "args": {"lr": 1.0}}
@@ -507,7 +513,8 @@ class PTFedOptModelShareableGenerator(FullModelShareableGenerator):
         if not isinstance(self.model, torch.nn.Module):
             self.system_panic(f"Expected model to be a torch.nn.Module but got {type(self.model)}", fl_ctx)
             return
-        self.model.to(self.device)
+        if self.devices is None:  # sharded: the model stays on the host (its parameters view the host weights)
+            self.model.to(self.device)
         build = getattr(engine, "build_component", None) or build_component_from_args
         try:
             self.optimizer_args.setdefault("args", {})
@@ -527,11 +534,17 @@ class PTFedOptModelShareableGenerator(FullModelShareableGenerator):
                 self.system_panic(f"Exception while parsing `lr_scheduler_args`({self.lr_scheduler_args}): {e}", fl_ctx)
                 return
 
-    def device_optimizer(self) -> DeviceServerOptimizer:
-        """The HBM image of (model, optimizer); (re)bound when either changed since the last step."""
+    def device_optimizer(self):
+        """The HBM image of (model, optimizer) -- one device, or sharded over ``devices``; (re)bound when
+        either changed since the last step."""
         d = self._dev_opt
         if d is None or d.model is not self.model or d.optimizer is not self.optimizer or not d.is_bound():
-            self._dev_opt = DeviceServerOptimizer(self.model, self.optimizer, hip_device_index(self.device))
+            if self.devices is not None:
+                from .sharded_fedopt import ShardedServerOptimizer
+
+                self._dev_opt = ShardedServerOptimizer(self.model, self.optimizer, self.devices)
+            else:
+                self._dev_opt = DeviceServerOptimizer(self.model, self.optimizer, hip_device_index(self.device))
         return self._dev_opt
 
     def server_update(self, model_diff):
@@ -564,7 +577,7 @@ class PTFedOptModelShareableGenerator(FullModelShareableGenerator):
         if base_model_weights:
             preserve_torch = any(isinstance(v, torch.Tensor) for v in base_model_weights.values())
         else:
-            preserve_torch = any(isinstance(v, torch.Tensor) or (isinstance(v, DeferredAggregate) and v.container == "torch")
+            preserve_torch = any(isinstance(v, torch.Tensor) or (isinstance(v, DeferredValue) and v.container == "torch")
                                  for v in model_diff.values())
 
         start = time.time()
@@ -572,7 +585,10 @@ class PTFedOptModelShareableGenerator(FullModelShareableGenerator):
         secs = time.time() - start
 
         start = time.time()
-        weights = self._to_host(weights, preserve_torch, self._dev_opt)
+        if isinstance(self._dev_opt, DeviceServerOptimizer):
+            weights = self._to_host(weights, preserve_torch, self._dev_opt)
+        else:  # sharded: the parameters already are host views of the new weights
+            weights = self._dev_opt.to_host(weights, preserve_torch)
         secs_detach = time.time() - start
 
         # FedAvg for the keys the optimizer does not own (e.g. batch-norm statistics), fedopt.py:247-263
@@ -596,7 +612,7 @@ class PTFedOptModelShareableGenerator(FullModelShareableGenerator):
 
         self.log_info(
             fl_ctx,
-            f"FedOpt ({self.optimizer_name}, {self.device}) server model update "
+            f"FedOpt ({self.optimizer_name}, {self.devices or self.device}) server model update "
             f"round {fl_ctx.get_prop(AppConstants.CURRENT_ROUND)}, "
             f"{self.lr_scheduler_name if self.lr_scheduler_name else ''} "
             f"lr: {self.optimizer.param_groups[-1]['lr']}, "

@@ -745,12 +745,43 @@ int fedavg_d2d_tiled(fedavg_ctx* ctx, void* base, size_t tile_bytes, size_t tile
     });
 }
 
+static void d2h_impl(fedavg_ctx* ctx, void* dst, const void* src, size_t nbytes);
+
 int fedavg_d2h(fedavg_ctx* ctx, void* dst, const void* src, size_t nbytes) {
     return guarded([&] {
         if (!ctx) throw Error("ctx is NULL");
         if (nbytes == 0) return;
         if (!dst || !src) throw Error("NULL pointer");
         ctx->activate();
+        d2h_impl(ctx, dst, src, nbytes);
+    });
+}
+
+int fedavg_d2h_multi(fedavg_ctx* ctx, void* host_base, const void* dev_base, int n, const size_t* host_offsets,
+                     const size_t* dev_offsets, const size_t* nbytes) {
+    return guarded([&] {
+        if (!ctx) throw Error("ctx is NULL");
+        if (n < 0) throw Error("negative piece count");
+        if (n == 0) return;
+        if (!host_base || !dev_base || !host_offsets || !dev_offsets || !nbytes) throw Error("NULL pointer");
+        ctx->activate();
+        hipStream_t s = ctx->compute();
+        char* h = static_cast<char*>(host_base);
+        const char* d = static_cast<const char*>(dev_base);
+        if (is_pinned_host(host_base)) {  // every piece straight into the page-locked destination, one sync
+            for (int i = 0; i < n; ++i)
+                if (nbytes[i]) HIP_CHECK(hipMemcpyAsync(h + host_offsets[i], d + dev_offsets[i], nbytes[i], hipMemcpyDeviceToHost, s));
+            HIP_CHECK(hipStreamSynchronize(s));
+            return;
+        }
+        for (int i = 0; i < n; ++i)
+            if (nbytes[i]) d2h_impl(ctx, h + host_offsets[i], d + dev_offsets[i], nbytes[i]);
+    });
+}
+
+// D2H on the compute stream (after the work queued on it), returning when dst holds the bytes
+static void d2h_impl(fedavg_ctx* ctx, void* dst, const void* src, size_t nbytes) {
+    {
         hipStream_t s = ctx->compute();
         if (nbytes < kParallelCopyMin || is_pinned_host(dst)) {
             HIP_CHECK(hipMemcpyAsync(dst, src, nbytes, hipMemcpyDeviceToHost, s));
@@ -776,7 +807,7 @@ int fedavg_d2h(fedavg_ctx* ctx, void* dst, const void* src, size_t nbytes) {
             parallel_memcpy(static_cast<char*>(dst) + off, ctx->ring[slot], len);
             if (c + kRingSlots < nchunks) issue(c + kRingSlots);
         }
-    });
+    }
 }
 
 int fedavg_host_register(fedavg_ctx* ctx, void* p, size_t nbytes) {

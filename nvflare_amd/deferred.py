@@ -228,27 +228,18 @@ class _Locks:
         return False
 
 
-class DeferredAggregate:
-    """The aggregated value of one key, still in HBM.  ``materialize()`` returns what the eager path
-    returns (numpy array / torch tensor of the key's container and shape)."""
+class DeferredValue:
+    """An aggregated value still in HBM (one key of a deferred round).  ``materialize()`` returns what the
+    eager path returns (numpy array / torch tensor of the key's container and shape); reading it any other
+    way (``np.asarray``, arithmetic) materialises it first."""
 
-    __slots__ = ("round", "name", "__weakref__")
+    __slots__ = ()
 
-    def __init__(self, rnd: DeferredRound, name: str):
-        self.round = rnd
-        self.name = name
+    shape: tuple
+    container: str
 
-    @property
-    def _state(self):
-        return self.round.keys[self.name]
-
-    @property
-    def shape(self):
-        return self._state.shape
-
-    @property
-    def container(self) -> str:
-        return self._state.container
+    def materialize(self):  # pragma: no cover - abstract
+        raise NotImplementedError
 
     @property
     def dtype(self):
@@ -257,16 +248,6 @@ class DeferredAggregate:
     @property
     def ndim(self) -> int:
         return len(self.shape)
-
-    @property
-    def size(self) -> int:
-        return self._state.n
-
-    def fusable(self, device: int) -> bool:
-        return self.round.device == device and self.round.fusable(self.name)
-
-    def materialize(self):
-        return self.round.value(self.name)
 
     def __array__(self, dtype=None, copy=None):
         v = self.materialize()
@@ -300,10 +281,79 @@ class DeferredAggregate:
     def __neg__(self):
         return -self.materialize()
 
+
+class DeferredAggregate(DeferredValue):
+    """The aggregated value of one key of a ``DeferredRound`` on one device."""
+
+    __slots__ = ("round", "name", "__weakref__")
+
+    def __init__(self, rnd: DeferredRound, name: str):
+        self.round = rnd
+        self.name = name
+
+    @property
+    def _state(self):
+        return self.round.keys[self.name]
+
+    @property
+    def shape(self):
+        return self._state.shape
+
+    @property
+    def container(self) -> str:
+        return self._state.container
+
+    @property
+    def size(self) -> int:
+        return self._state.n
+
+    def fusable(self, device: int) -> bool:
+        return self.round.device == device and self.round.fusable(self.name)
+
+    def materialize(self):
+        return self.round.value(self.name)
+
     def __repr__(self) -> str:
         return f"DeferredAggregate({self.name!r}, shape={self.shape}, {self.container}, device={self.round.device})"
 
 
+class ShardedDeferredAggregate(DeferredValue):
+    """One key aggregated in parameter buckets over several devices (``sharding.ShardedFedAvg``), still in
+    HBM: ``pieces`` = [(lo, hi, DeferredAggregate)] over the flattened key, in bucket order.  A sharded
+    device optimizer steps each piece on its own device (``fusable``); ``materialize()`` assembles the
+    pieces as the eager sharded result does."""
+
+    __slots__ = ("name", "shape", "container", "pieces", "_value", "__weakref__")
+
+    def __init__(self, name: str, shape: tuple, container: str, pieces: List[Tuple[int, int, DeferredAggregate]]):
+        self.name = name
+        self.shape = tuple(shape)
+        self.container = container
+        self.pieces = list(pieces)
+        self._value = None
+
+    @property
+    def size(self) -> int:
+        return int(np.prod(self.shape, dtype=np.int64)) if self.shape else 1
+
+    def materialize(self):
+        if self._value is None:
+            vals = [d.materialize() for _, _, d in self.pieces]
+            if torch is not None and isinstance(vals[0], torch.Tensor):
+                flat = torch.cat([v.reshape(-1) for v in vals]) if len(vals) > 1 else vals[0].reshape(-1)
+                self._value = flat.reshape(self.shape)
+            else:
+                flat = np.concatenate([np.asarray(v).reshape(-1) for v in vals]) if len(vals) > 1 \
+                    else np.asarray(vals[0]).reshape(-1)
+                res = flat.reshape(self.shape)
+                self._value = res[()] if res.ndim == 0 else res
+        return self._value
+
+    def __repr__(self) -> str:
+        devs = [d.round.device for _, _, d in self.pieces]
+        return f"ShardedDeferredAggregate({self.name!r}, shape={self.shape}, {self.container}, devices={devs})"
+
+
 def materialize_deferred(v):
-    """``v.materialize()`` for a DeferredAggregate, ``v`` otherwise."""
-    return v.materialize() if isinstance(v, DeferredAggregate) else v
+    """``v.materialize()`` for a deferred value (one device or sharded), ``v`` otherwise."""
+    return v.materialize() if isinstance(v, DeferredValue) else v

@@ -247,6 +247,22 @@ class DeviceContext:
         """Drop recorded marks (start of a new marked sequence, or a copy that will not happen)."""
         N.call("fedavg_marks_reset", self.handle)
 
+    def d2h_multi(self, host: np.ndarray, dev_ptr: int, pieces) -> None:
+        """Device -> host copies in one call: ``pieces`` = [(host byte offset, device byte offset, nbytes)]
+        from ``dev_ptr`` into ``host`` (C-contiguous); returns when the host holds them (fedavg_d2h_multi)."""
+        if not host.flags.c_contiguous:
+            raise ValueError("d2h destination must be C-contiguous")
+        pieces = [p for p in pieces if p[2]]
+        for ho, _, nb in pieces:
+            if ho < 0 or ho + nb > host.nbytes:
+                raise ValueError("d2h_multi piece outside the host array")
+        n = len(pieces)
+        if not n:
+            return
+        arr = (ctypes.c_size_t * n)
+        N.call("fedavg_d2h_multi", self.handle, ctypes.c_void_p(host.ctypes.data), ctypes.c_void_p(dev_ptr),
+               ctypes.c_int(n), arr(*[p[0] for p in pieces]), arr(*[p[1] for p in pieces]), arr(*[p[2] for p in pieces]))
+
     def d2h_marked(self, host: np.ndarray, src_ptr: int) -> None:
         """D2H overlapping the launches still producing src (see mark); returns when host is filled."""
         if not host.flags.c_contiguous:

@@ -92,28 +92,48 @@ class ShardedFedAvg:
             for f in futs:
                 f.result()
 
+    def _assemble(self, k: str, plist: List[Tuple[int, Any]]):
+        """The whole key from its bucket results (plist sorted by offset)."""
+        shape = self._shapes[k]
+        arrs = [a for _, a in plist]
+        if is_torch_tensor(arrs[0]):
+            import torch
+
+            flat = torch.cat([a.reshape(-1) for a in arrs]) if len(arrs) > 1 else arrs[0].reshape(-1)
+            return flat.reshape(shape)
+        flat = np.concatenate([np.asarray(a).reshape(-1) for a in arrs]) if len(arrs) > 1 else np.asarray(arrs[0]).reshape(-1)
+        res = flat.reshape(shape)
+        return res[()] if res.ndim == 0 else res
+
+    def _bucket_results(self, deferred: bool) -> Dict[str, List[Tuple[int, Any]]]:
+        fn = (lambda e: e.result_deferred() if e.keys else {}) if deferred else (lambda e: e.result() if e.keys else {})
+        pieces: Dict[str, List[Tuple[int, Any]]] = {}
+        for res in self._pool.map(fn, self.engines):
+            for sub, arr in res.items():
+                k, off = sub.split("\x00")
+                pieces.setdefault(k, []).append((int(off), arr))
+        for plist in pieces.values():
+            plist.sort(key=lambda x: x[0])
+        return pieces
+
     def result(self) -> Dict[str, Any]:
         with self.lock:
-            parts = list(self._pool.map(lambda e: e.result() if e.keys else {}, self.engines))
-            pieces: Dict[str, List[Tuple[int, Any]]] = {}
-            for res in parts:
-                for sub, arr in res.items():
-                    k, off = sub.split("\x00")
-                    pieces.setdefault(k, []).append((int(off), arr))
-            out = {}
-            for k, plist in pieces.items():
-                plist.sort(key=lambda x: x[0])
-                shape = self._shapes[k]
-                arrs = [a for _, a in plist]
-                if is_torch_tensor(arrs[0]):
-                    import torch
+            return {k: self._assemble(k, plist) for k, plist in self._bucket_results(False).items()}
 
-                    flat = torch.cat([a.reshape(-1) for a in arrs]) if len(arrs) > 1 else arrs[0].reshape(-1)
-                    out[k] = flat.reshape(shape)
+    def result_deferred(self) -> Dict[str, Any]:
+        """``result()`` with every fp32 key left on the devices, one ``ShardedDeferredAggregate`` per key whose
+        bucket pieces are ``DeferredAggregate`` values of each device's round (engine.result_deferred); other
+        keys come back eagerly, assembled."""
+        from .deferred import DeferredAggregate, ShardedDeferredAggregate
+
+        with self.lock:
+            out = {}
+            for k, plist in self._bucket_results(True).items():
+                if all(isinstance(v, DeferredAggregate) for _, v in plist):
+                    spans = [(lo, lo + v.size, v) for lo, v in plist]
+                    out[k] = ShardedDeferredAggregate(k, self._shapes[k], plist[0][1].container, spans)
                 else:
-                    flat = np.concatenate([np.asarray(a).reshape(-1) for a in arrs]) if len(arrs) > 1 else np.asarray(arrs[0]).reshape(-1)
-                    res = flat.reshape(shape)
-                    out[k] = res[()] if res.ndim == 0 else res
+                    out[k] = self._assemble(k, [(lo, getattr(v, "materialize", lambda v=v: v)()) for lo, v in plist])
             return out
 
     @property

@@ -150,3 +150,45 @@ def test_sharded_rejects_reshaped_contribution(oracle):
     assert np.array_equal(res["a"].reshape(-1).view(np.uint32), exp.view(np.uint32))
     sh._pool.shutdown()
 
+
+
+def test_sharded_deferred_rounds_match_eager():
+    """ShardedFedAvg.result_deferred: every fp32 key comes back as a ShardedDeferredAggregate whose pieces are
+    the buckets' DeferredAggregates (one per engine); materialised, it equals the eager sharded result bit
+    for bit, also after the next round has settled the previous one; fp64 keys stay eager."""
+    import torch
+
+    from nvflare_amd.deferred import DeferredAggregate, ShardedDeferredAggregate, materialize_deferred
+
+    rng = np.random.default_rng(7)
+    shapes = {"a": (3, 5000), "b": (7,), "c": (), "e": (2, 4096), "big": (3 * 4096 + 5,)}
+    sh_def, sh_eager = _fake_sharded(3), _fake_sharded(3)
+    kept = []
+    for rnd in range(2):
+        ws = [1.0 + rnd, 2.5, 0.75, 3.0]
+        for k, w in enumerate(ws):
+            items = [(n, rng.standard_normal(s).astype(np.float32)) for n, s in shapes.items()]
+            items.append(("d64", rng.standard_normal(10)))  # numpy's default fp64: the fp64 arena, eager
+            items.append(("t", torch.from_numpy(rng.standard_normal(9000).astype(np.float32))))
+            sh_def.add(items, w, True)
+            sh_eager.add(items, w, True)
+        got, exp = sh_def.result_deferred(), sh_eager.result()
+        sh_def.reset()
+        sh_eager.reset()
+        assert isinstance(got["d64"], np.ndarray)
+        for n in list(shapes) + ["t"]:
+            v = got[n]
+            assert isinstance(v, ShardedDeferredAggregate), n
+            assert v.shape == tuple(exp[n].shape) and v.container == ("torch" if n == "t" else "numpy")
+            assert all(isinstance(d, DeferredAggregate) for _, _, d in v.pieces)
+            assert sum(hi - lo for lo, hi, _ in v.pieces) == v.size
+        kept.append((got, exp))
+    for got, exp in kept:  # round 0's values materialise after round 1 settled them
+        for n in exp:
+            g = materialize_deferred(got[n])
+            g = g.numpy() if isinstance(g, torch.Tensor) else np.asarray(g)
+            e_ = exp[n].numpy() if isinstance(exp[n], torch.Tensor) else np.asarray(exp[n])
+            assert g.shape == e_.shape and g.dtype == e_.dtype
+            assert np.array_equal(g.reshape(-1).view(np.uint8), e_.reshape(-1).view(np.uint8)), n
+    for s_ in (sh_def, sh_eager):
+        s_._pool.shutdown()

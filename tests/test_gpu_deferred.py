@@ -31,7 +31,7 @@ from nvflare_amd.compat import (
     from_shareable,
     make_model_learnable,
 )
-from nvflare_amd.deferred import DeferredAggregate
+from nvflare_amd.deferred import DeferredAggregate, DeferredValue, materialize_deferred
 
 pytestmark = pytest.mark.gpu
 
@@ -69,16 +69,19 @@ def _client_diff(rng, weights, k, rnd, container, drop_key=None):
     return out
 
 
-def run_fedopt_sag(defer, container, opt, n_clients, rounds=3, drop=None, seed=0):
+def run_fedopt_sag(defer, container, opt, n_clients, rounds=3, drop=None, seed=0, devices=None, model_fn=None,
+                   opt_args=None, sched_args=None, between_rounds=None):
     """ScatterAndGather's accept -> aggregate -> shareable_to_learnable -> reset loop (scatter_and_gather.py:
     224-349) with the drop-in aggregator and FedOpt generator; returns per-round weights, aggregated
-    differences, optimizer state and the generator."""
+    differences, optimizer state (one device) and the generator.  ``devices``: both sharded over them."""
     torch.manual_seed(seed)
-    model = fedopt_model()
-    gen = PTFedOptModelShareableGenerator(optimizer_args=copy.deepcopy(OPTS[opt]), source_model=model, device=0)
+    model = (model_fn or fedopt_model)()
+    gen = PTFedOptModelShareableGenerator(optimizer_args=copy.deepcopy(opt_args or OPTS[opt]), source_model=model,
+                                          device=0, devices=devices, lr_scheduler_args=copy.deepcopy(sched_args))
     fl_ctx = FLContext()
     gen.handle_event(EventType.START_RUN, fl_ctx)
-    agg = InTimeAccumulateWeightedAggregator(expected_data_kind=DataKind.WEIGHT_DIFF, defer_result=defer)
+    agg = InTimeAccumulateWeightedAggregator(expected_data_kind=DataKind.WEIGHT_DIFF, defer_result=defer,
+                                             devices=devices)
     agg.handle_event(EventType.START_RUN, fl_ctx)
     weights = {k: v.detach().cpu().clone() if container == "torch" else v.detach().cpu().numpy().copy()
                for k, v in model.state_dict().items()}
@@ -97,14 +100,19 @@ def run_fedopt_sag(defer, container, opt, n_clients, rounds=3, drop=None, seed=0
         aggr = agg.aggregate(fl_ctx)
         diff = from_shareable(aggr).data
         if defer:
-            assert any(isinstance(v, DeferredAggregate) for v in diff.values())
+            assert any(isinstance(v, DeferredValue) for v in diff.values())
         learnable = gen.shareable_to_learnable(aggr, fl_ctx)
         weights = learnable[ModelLearnableKey.WEIGHTS]
         agg.reset(fl_ctx)
-        diff_host = {k: _np(v.materialize() if isinstance(v, DeferredAggregate) else v).copy() for k, v in diff.items()}
+        diff_host = {k: _np(materialize_deferred(v)).copy() for k, v in diff.items()}
         hist.append(({k: _np(v).copy() for k, v in weights.items()}, diff_host))
+        if between_rounds is not None:  # may load new weights into the model; they become the global model
+            new = between_rounds(rnd, model, gen)
+            if new is not None:
+                weights = {k: v.detach().cpu().clone() if container == "torch" else v.detach().cpu().numpy().copy()
+                           for k, v in new.items()}
     dev = gen._dev_opt
-    state = (dev.p.cpu().numpy().copy(), dev.m.cpu().numpy().copy(), dev.v.cpu().numpy().copy())
+    state = (dev.p.cpu().numpy().copy(), dev.m.cpu().numpy().copy(), dev.v.cpu().numpy().copy()) if devices is None else None
     return hist, state, gen
 
 

@@ -234,8 +234,8 @@ def test_aggregate_random(shape, n_clients, oracle):
 @pytest.mark.parametrize("defer", [False, True])
 def test_intime_devices_shards_parameter_buckets(oracle, defer):
     """``devices=[...]`` on the InTime aggregator: every key split into parameter buckets over several engines
-    (here three on device 0), fp32 results bit-exact with the oracle; ``defer_result`` falls back to eager
-    results when sharded."""
+    (here three on device 0), fp32 results bit-exact with the oracle; with ``defer_result`` they are
+    ``ShardedDeferredAggregate`` values (one piece per engine) that materialise to the same bits."""
     from nvflare_amd.compat import DXO, AppConstants, DataKind, FLContext, MetaKey, from_shareable
     from nvflare_amd.sharding import ShardedFedAvg
 
@@ -252,6 +252,11 @@ def test_intime_devices_shards_parameter_buckets(oracle, defer):
         assert _submit(agg, fl_ctx, f"site-{i}", dxo)
     assert isinstance(agg.dxo_aggregators[""].aggregation_helper.engine, ShardedFedAvg)
     out = from_shareable(agg.aggregate(fl_ctx)).data
+    if defer:
+        from nvflare_amd.deferred import ShardedDeferredAggregate
+
+        assert isinstance(out["w"], ShardedDeferredAggregate) and len(out["w"].pieces) == 3
+        out = {k: np.asarray(v) for k, v in out.items()}
     assert isinstance(out["w"], np.ndarray)
     assert same_bits(out["w"], oracle.fedavg_c(rows, ws, oracle.MODE_NUMPY))
     assert same_bits(out["b"], oracle.fedavg_c([r[:10].copy() for r in rows], ws, oracle.MODE_NUMPY))
