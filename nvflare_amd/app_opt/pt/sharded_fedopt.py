@@ -25,6 +25,7 @@ Layout:
 from __future__ import annotations
 
 import threading
+import weakref
 from concurrent.futures import ThreadPoolExecutor
 from typing import Dict, List, Optional, Sequence, Tuple
 
@@ -133,6 +134,7 @@ class ShardedServerOptimizer:
         self.total = max(off, _HOST_ALIGN)
         self.host_pool = HostArenaPool()
         self._pool = ThreadPoolExecutor(max_workers=len(self.devices), thread_name_prefix="nvflare-amd-fedopt-shard")
+        self._pool_fin = weakref.finalize(self, self._pool.shutdown, wait=False)  # a re-bound generator drops us
         self._lock = threading.Lock()
         model.to("cpu")  # buffers (batch-norm statistics) stay with the model; parameters are re-pointed below
         host = self.host_pool.take(self.total, pin=self.shards[0].ctx)
@@ -267,4 +269,5 @@ class ShardedServerOptimizer:
         return out
 
     def release(self) -> None:
+        self._pool_fin.detach()
         self._pool.shutdown(wait=True)

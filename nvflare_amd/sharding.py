@@ -15,6 +15,7 @@ client-sharded RCCL reduce would not be (it re-associates the sums).
 from __future__ import annotations
 
 import threading
+import weakref
 from concurrent.futures import ThreadPoolExecutor
 from typing import Any, Dict, List, Optional, Sequence, Tuple
 
@@ -61,6 +62,7 @@ class ShardedFedAvg:
         self.engines = [DeviceFedAvg(device=d, max_resident_bytes=max_resident_bytes) for d in self.devices]
         self.lock = threading.RLock()
         self._pool = ThreadPoolExecutor(max_workers=len(self.devices), thread_name_prefix="nvflare-amd-shard")
+        self._pool_fin = weakref.finalize(self, self._pool.shutdown, wait=False)  # threads end with the engine
         self._shapes: Dict[str, tuple] = {}
 
     def _pieces(self, bucket: int, items):
@@ -157,4 +159,5 @@ class ShardedFedAvg:
     def release(self) -> None:
         for e in self.engines:
             e.release()
+        self._pool_fin.detach()
         self._pool.shutdown(wait=True)
