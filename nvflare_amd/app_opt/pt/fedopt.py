@@ -214,7 +214,7 @@ class DeviceServerOptimizer:
         base = self.p.data_ptr()
         return all(named[s.name] is s.param and s.param.data_ptr() == base + 4 * s.offset for s in self.slots)
 
-    def _expose_state(self, s: _Slot) -> None:
+    def _expose_state(self, s: _Slot, group: dict) -> None:
         st = self.optimizer.state[s.param]
         if self.kind == N.FEDAVG_EPI_SGD:
             if s.has_momentum_buffer:  # torch stores the buffer only when momentum != 0
@@ -223,7 +223,7 @@ class DeviceServerOptimizer:
             st["step"] = torch.tensor(s.step, dtype=torch.float32)
             st["sum"] = self.m[s.offset:s.offset + s.n].view(s.param.shape)
         elif self.kind == N.FEDAVG_EPI_RMSPROP:
-            g = self._group_of()[id(s.param)]
+            g = group
             st["step"] = torch.tensor(s.step, dtype=torch.float32)
             st["square_avg"] = self.m[s.offset:s.offset + s.n].view(s.param.shape)
             if g.get("momentum", 0.0) > 0:
@@ -249,7 +249,7 @@ class DeviceServerOptimizer:
             st["exp_avg_sq"] = self.v[s.offset:s.offset + s.n].view(s.param.shape)
             if self.kind == N.FEDAVG_EPI_NADAM:
                 st["mu_product"] = torch.tensor(s.mu_product, dtype=torch.float32)
-            if self._group_of()[id(s.param)].get("amsgrad"):
+            if group.get("amsgrad"):
                 st["max_exp_avg_sq"] = self._max_exp_avg_sq()[s.offset:s.offset + s.n].view(s.param.shape)
 
     def _max_exp_avg_sq(self) -> torch.Tensor:
@@ -350,11 +350,12 @@ class DeviceServerOptimizer:
         del keep
         # one launch per run of consecutive stepped parameters sharing group and per-parameter state
         runs: List[Tuple[tuple, List[_Slot]]] = []
+        pos = {id(s): i for i, s in enumerate(self.slots)}
         for s in present:
             g = groups[id(s.param)]
             key = (id(g),) + s.host_key()
             prev = runs[-1][1][-1] if runs else None
-            contiguous = prev is not None and self.slots.index(s) == self.slots.index(prev) + 1
+            contiguous = prev is not None and pos[id(s)] == pos[id(prev)] + 1
             if runs and runs[-1][0] == key and contiguous:
                 runs[-1][1].append(s)
             else:
@@ -417,7 +418,7 @@ class DeviceServerOptimizer:
                 s.mu_product = np.float32(np.float32(s.mu_product) * np.float32(mu))
             if self.kind == N.FEDAVG_EPI_SGD and groups[id(s.param)].get("momentum", 0.0) != 0.0:
                 s.has_momentum_buffer = True
-            self._expose_state(s)
+            self._expose_state(s, groups[id(s.param)])
 
     def _fused_step(self, model_diff: Dict, groups: Dict[int, dict]) -> set:
         """Aggregation + optimizer step in one launch for the parameters whose difference is a deferred
