@@ -34,6 +34,7 @@ FLAGS = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-fast-math", f"
 def _inputs():
     files = [os.path.join(CSRC, s) for s in SOURCES + HEADERS]
     files.append(os.path.join(ROOT, "include", "nvflare_amd_fedavg.h"))
+    files.append(os.path.abspath(__file__))  # flags and the source list live here
     return files
 
 
@@ -50,8 +51,9 @@ def build_library(force: bool = False, verbose: bool = False, jobs: int = 0) -> 
     os.makedirs(OBJ_DIR, exist_ok=True)
     inc = [f"-I{os.path.join(ROOT, 'include')}", f"-I{CSRC}"]
 
-    headers = [os.path.join(CSRC, h) for h in HEADERS] + [os.path.join(ROOT, "include", "nvflare_amd_fedavg.h")]
-    newest_header = max(os.path.getmtime(h) for h in headers)
+    headers = [os.path.join(CSRC, h) for h in HEADERS] + [os.path.join(ROOT, "include", "nvflare_amd_fedavg.h"),
+                                                          os.path.abspath(__file__)]
+    newest_header = max(os.path.getmtime(h) for h in headers)  # any header (or a flag change) rebuilds all
 
     def compile_one(src: str) -> str:
         obj = os.path.join(OBJ_DIR, src + ".o")
