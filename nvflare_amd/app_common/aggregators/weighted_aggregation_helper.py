@@ -245,7 +245,13 @@ class WeightedAggregationHelper(object):
             else:
                 device_results = self._engine.result()
             aggregated = {}
-            for k, v in self.total.items():
+            total = self.total
+            # key_contribution_counts holds the keys in first-arrival order (the reference's ``total`` order);
+            # ``total`` itself lists a contribution's device keys before its host keys
+            for k in self.key_contribution_counts:
+                v = total.get(k)
+                if v is None:
+                    continue
                 if isinstance(v, _HostValue):
                     t = v.total
                     aggregated[k] = t.div_(self.counts[k]) if self._is_pytorch_tensor(t) else t * (1.0 / self.counts[k])

@@ -16,7 +16,7 @@ if os.environ.get("NVFLARE_AMD_FORCE_STANDINS", "0") != "1":
         from nvflare.apis.fl_context import FLContext  # noqa: F401
         from nvflare.apis.shareable import Shareable  # noqa: F401
         from nvflare.app_common.abstract.aggregator import Aggregator  # noqa: F401
-        from nvflare.app_common.app_constant import AppConstants  # noqa: F401
+        from nvflare.app_common.app_constant import AlgorithmConstants, AppConstants  # noqa: F401
         from nvflare.fuel.utils.log_utils import get_module_logger  # noqa: F401
         from nvflare.apis.fl_constant import FLMetaKey  # noqa: F401
         from nvflare.app_common.abstract.fl_model import FLModel, ParamsType  # noqa: F401
@@ -40,6 +40,7 @@ if not HAVE_NVFLARE:
     from ._standins import (  # noqa: F401
         DXO,
         Aggregator,
+        AlgorithmConstants,
         DXOFilter,
         AppConstants,
         DataKind,
@@ -70,6 +71,7 @@ __all__ = [
     "DXO",
     "DXOFilter",
     "Aggregator",
+    "AlgorithmConstants",
     "AppConstants",
     "DataKind",
     "EventType",

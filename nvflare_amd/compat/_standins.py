@@ -16,7 +16,8 @@ repository's tests).  They reproduce the behaviour the aggregation path relies o
 * ``ShareableGenerator``, ``Learnable``, ``ModelLearnable`` helpers  app_common/abstract/shareable_generator.py,
                                                   learnable.py, model.py:25-71
 * constants: ``ReservedKey`` (fl_constant.py:69-80), ``ReturnCode`` (:26-36),
-  ``AppConstants`` (app_common/app_constant.py:33-79), ``EventType.START_RUN`` (apis/event_type.py:22)
+  ``AppConstants`` (app_common/app_constant.py:33-79), ``AlgorithmConstants`` (:156-160),
+  ``EventType.START_RUN`` (apis/event_type.py:22)
 """
 
 from __future__ import annotations
@@ -83,6 +84,11 @@ class AppConstants:
     NUM_ROUNDS = "num_rounds"
     CONTRIBUTION_ROUND = "contribution_round"
     AGGREGATION_STATS = "_aggregation_stats"
+
+
+class AlgorithmConstants:
+    SCAFFOLD_CTRL_DIFF = "scaffold_c_diff"
+    SCAFFOLD_CTRL_GLOBAL = "scaffold_c_global"
 
 
 class EventType:

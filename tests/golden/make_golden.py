@@ -14,14 +14,15 @@ Reference code exercised:
   nvflare/app_common/aggregators/weighted_aggregation_helper.py:153-240  (helper cases)
   nvflare/app_common/workflows/base_fedavg.py:93-230  (``--set fedavg``: aggregate_fn cases)
   nvflare/app_common/workflows/fedavg.py:268-366      (``--set fedavg``: built-in in-time FedAvg cases)
+  nvflare/app_common/workflows/scaffold.py:149-189    (``--set scaffold``: scaffold_aggregate_fn cases)
   nvflare/app_opt/pt/fedopt.py:157-270                 (``--set fedopt``: PTFedOptModelShareableGenerator, CPU)
   nvflare/app_common/shareablegenerators/full_model_shareable_generator.py:37-83  (``--set fedopt``)
   nvflare/app_opt/pt/quantization/ada_quant.py:39-87  (``--set quant``: AdaQuantizer quantize / dequantized)
   nvflare/app_common/aggregators/intime_accumulate_model_aggregator.py   (intime cases)
   nvflare/app_common/aggregators/dxo_aggregator.py:71-191
 
-Usage:  python tests/golden/make_golden.py [--ref /root/reference] [--set helper|fedavg|fedopt|quant|dtypes]
-        (helper -> helper_cases.{npz,json}; fedavg -> fedavg_cases.{npz,json};
+Usage:  python tests/golden/make_golden.py [--ref /root/reference] [--set helper|fedavg|scaffold|fedopt|quant|dtypes]
+        (helper -> helper_cases.{npz,json}; fedavg -> fedavg_cases.{npz,json}; scaffold -> scaffold_cases.{npz,json};
          fedopt -> fedopt_cases.{npz,json}; quant -> quant_cases.{npz,json};
          dtypes -> dtype_cases.{npz,json}: float16 / bfloat16 / integer / bool client arrays)
 """
@@ -275,6 +276,95 @@ def main_fedavg():
     print(f"wrote {len(cases)} fedavg cases, {len(store.arrays)} arrays")
 
 
+def run_scaffold_case(store, cases, name, clients):
+    """clients: [(name, num_steps, params, ctrl_diff, metrics, params_container, ctrl_container)]; ctrl None:
+    the client omits SCAFFOLD_CTRL_DIFF (the reference raises)."""
+    from nvflare.apis.fl_constant import FLMetaKey
+    from nvflare.app_common.abstract.fl_model import FLModel
+    from nvflare.app_common.app_constant import AlgorithmConstants
+    from nvflare.app_common.workflows.scaffold import scaffold_aggregate_fn
+
+    models, rec = [], []
+    for cname, steps, params, ctrl, metrics, pc, cc in clients:
+        meta = {"client_name": cname}
+        if steps is not None:
+            meta[FLMetaKey.NUM_STEPS_CURRENT_ROUND] = steps
+        if ctrl is not None:
+            meta[AlgorithmConstants.SCAFFOLD_CTRL_DIFF] = {k: to_container(v, cc) for k, v in ctrl.items()}
+        models.append(FLModel(params={k: to_container(v, pc) for k, v in params.items()}, metrics=metrics,
+                              current_round=3, meta=meta))
+        rec.append({"name": cname, "num_steps": _jsonable_steps(steps), "metrics": metrics,
+                    "params_container": pc, "ctrl_container": cc,
+                    "params": {k: store.put(v, "in") for k, v in params.items()},
+                    "ctrl": None if ctrl is None else {k: store.put(v, "in") for k, v in ctrl.items()}})
+    try:
+        out = scaffold_aggregate_fn(models)
+    except ValueError as e:
+        cases.append({"kind": "scaffold", "name": name, "clients": rec, "error": str(e)})
+        return
+    ctrl_out = out.meta[AlgorithmConstants.SCAFFOLD_CTRL_DIFF]
+
+    def dt(v):
+        return str(v.dtype).replace("torch.", "") if isinstance(v, torch.Tensor) else str(np.asarray(v).dtype)
+
+    expected = _result_record(store, out)
+    expected["meta"] = {k: v for k, v in out.meta.items() if k != AlgorithmConstants.SCAFFOLD_CTRL_DIFF}
+    expected["params_order"] = list(out.params)
+    expected["params_kind"] = {k: "torch" if isinstance(v, torch.Tensor) else "numpy" for k, v in out.params.items()}
+    expected["ctrl"] = {k: store.put(v, "out") for k, v in ctrl_out.items()}
+    expected["ctrl_order"] = list(ctrl_out)
+    expected["ctrl_dtype"] = {k: dt(v) for k, v in ctrl_out.items()}
+    expected["ctrl_kind"] = {k: "torch" if isinstance(v, torch.Tensor) else "numpy" for k, v in ctrl_out.items()}
+    cases.append({"kind": "scaffold", "name": name, "clients": rec, "expected": expected})
+
+
+def main_scaffold():
+    rng = np.random.default_rng(20261017)
+    store = Store()
+    cases = []
+    shapes = {"conv.weight": (8, 3, 3, 3), "conv.bias": (8,), "fc.weight": (10, 72), "fc.bias": (10,)}
+
+    def arr(shape, dtype=np.float32):
+        return rng.standard_normal(shape).astype(dtype)
+
+    def metrics(i):
+        return {"loss": float(rng.random()), "acc": float(rng.random()), "tag": "s", "flag": bool(i % 2)}
+
+    steps = [12, None, 3.5, "9", -1, True, 40]
+    for pc, cc in (("numpy", "numpy"), ("torch", "torch"), ("torch", "numpy")):
+        tag = pc if pc == cc else f"{pc}_{cc}"
+        # every client sends every key; the FedAvg weight rule on odd NUM_STEPS values
+        clients = [(f"site-{i+1}", steps[i], {k: arr(v) for k, v in shapes.items()},
+                    {k: arr(v) * 1e-2 for k, v in shapes.items()}, metrics(i), pc, cc) for i in range(len(steps))]
+        run_scaffold_case(store, cases, f"{tag}_full", clients)
+        # ragged keys: params and controls each miss keys on some clients; a control for a key no client
+        # sends as a param (a buffer); arrival order of new keys differs between params and controls
+        ragged = []
+        for i in range(5):
+            pk = [k for j, k in enumerate(shapes) if (i + j) % 4 != 3]
+            ck = [k for j, k in enumerate(reversed(list(shapes))) if (i * 3 + j) % 5 != 1]
+            ctrl = {k: arr(shapes[k]) for k in ck}
+            if i >= 2:
+                ctrl["bn.running_mean"] = arr(8)
+            ragged.append((f"site-{i+1}" if i != 3 else "", int(rng.integers(1, 50)), {k: arr(shapes[k]) for k in pk},
+                           ctrl, None if i == 4 else metrics(i), pc, cc))
+        run_scaffold_case(store, cases, f"{tag}_ragged", ragged)
+    # more clients, larger ragged tiles, special values in the controls, an fp64 control key
+    K, P = 20, 4099
+    clients = [(f"site-{i+1}", float(rng.integers(1, 100)), {"w": arr(P), "b": arr(33)},
+                {"w": special_values(rng, P) * np.float32(1e-3), "b": arr(33), "scale": rng.random(5)},
+                metrics(i), "numpy", "numpy") for i in range(K)]
+    run_scaffold_case(store, cases, "numpy_k20_special", clients)
+    # a client without SCAFFOLD_CTRL_DIFF: the reference's ValueError
+    bad = [(f"site-{i+1}", 2, {"w": arr(5)}, None if i == 1 else {"w": arr(5)}, None, "numpy", "numpy") for i in range(3)]
+    run_scaffold_case(store, cases, "missing_ctrl", bad)
+    np.savez_compressed(os.path.join(HERE, "scaffold_cases.npz"), **store.arrays)
+    with open(os.path.join(HERE, "scaffold_cases.json"), "w") as f:
+        json.dump({"generator": "tests/golden/make_golden.py --set scaffold", "reference": "NVFlare (/root/reference, ~2.9.0-dev)",
+                   "numpy": np.__version__, "torch": torch.__version__, "cases": cases}, f, indent=1, default=str)
+    print(f"wrote {len(cases)} scaffold cases, {len(store.arrays)} arrays")
+
+
 FEDOPT_CONFIGS = [
     # (name, optimizer_args, lr_scheduler_args)
     ("sgd_default", {"path": "torch.optim.SGD", "args": {"lr": 1.0}}, None),
@@ -519,12 +609,14 @@ def main_dtypes():
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ref", default="/root/reference")
-    ap.add_argument("--set", choices=["helper", "fedavg", "fedopt", "quant", "dtypes"], default="helper")
+    ap.add_argument("--set", choices=["helper", "fedavg", "scaffold", "fedopt", "quant", "dtypes"], default="helper")
     args = ap.parse_args()
     install_shim(args.ref)
     torch.set_num_threads(8)
     if args.set == "fedavg":
         return main_fedavg()
+    if args.set == "scaffold":
+        return main_scaffold()
     if args.set == "fedopt":
         return main_fedopt()
     if args.set == "quant":

@@ -99,6 +99,61 @@ def fl_models_from_case(case, arrays, FLModel, container):
     return models
 
 
+def load_scaffold_golden():
+    """SCAFFOLD cases (make_golden.py --set scaffold): the reference's scaffold_aggregate_fn."""
+    if "s" not in _cache:
+        with open(os.path.join(GOLDEN_DIR, "scaffold_cases.json")) as f:
+            meta = json.load(f)
+        arrays = dict(np.load(os.path.join(GOLDEN_DIR, "scaffold_cases.npz"), allow_pickle=False))
+        _cache["s"] = (meta, arrays)
+    return _cache["s"]
+
+
+def scaffold_models_from_case(case, arrays, FLModel):
+    """The case's clients as FLModels: params and SCAFFOLD_CTRL_DIFF in their recorded containers."""
+    import torch
+
+    def box(name, container):
+        a = np.array(arrays[name], copy=True)
+        return torch.from_numpy(a) if container == "torch" else a
+
+    models = []
+    for c in case["clients"]:
+        meta = {"client_name": c["name"]}
+        if c["num_steps"]["t"] != "none":
+            meta["NUM_STEPS_CURRENT_ROUND"] = decode_steps(c["num_steps"])
+        if c["ctrl"] is not None:
+            meta["scaffold_c_diff"] = {k: box(n, c["ctrl_container"]) for k, n in c["ctrl"].items()}
+        models.append(FLModel(params={k: box(n, c["params_container"]) for k, n in c["params"].items()},
+                              metrics=c["metrics"], current_round=3, meta=meta))
+    return models
+
+
+def check_scaffold_result(case, arrays, out):
+    """Params, controls (values, dtypes, containers, key order), metrics and meta as the reference made them."""
+    import torch
+
+    exp = case["expected"]
+
+    def same(got, name, kind, dtype, what):
+        assert isinstance(got, torch.Tensor if kind == "torch" else np.ndarray), (case["name"], what)
+        if isinstance(got, torch.Tensor):
+            assert str(got.dtype).replace("torch.", "") == dtype, (case["name"], what)
+            got = got.numpy()
+        assert str(got.dtype) == dtype and same_bits(got, arrays[name]), (case["name"], what)
+
+    assert list(out.params) == exp["params_order"]
+    for k, name in exp["params"].items():
+        same(out.params[k], name, exp["params_kind"][k], exp["params_dtype"][k], k)
+    ctrl = out.meta["scaffold_c_diff"]
+    assert list(ctrl) == exp["ctrl_order"]
+    for k, name in exp["ctrl"].items():
+        same(ctrl[k], name, exp["ctrl_kind"][k], exp["ctrl_dtype"][k], "ctrl " + k)
+    assert str(out.params_type.value if out.params_type is not None else None) == exp["params_type"]
+    assert same_metrics(out.metrics, exp["metrics"]), (out.metrics, exp["metrics"])
+    assert {k: v for k, v in out.meta.items() if k != "scaffold_c_diff"} == exp["meta"]
+
+
 def same_metrics(a, b) -> bool:
     """Exact equality of metric dicts (python floats; NaN == NaN)."""
     import math

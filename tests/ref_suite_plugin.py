@@ -73,6 +73,18 @@ def pytest_collection_modifyitems(session, config, items):
             if hasattr(mod, name):
                 setattr(mod, name, obj)
                 config._fedavg_swapped.append(f"{mod.__name__}.{name}")
+    # the reference's SCAFFOLD tests import ``Scaffold`` / ``scaffold_aggregate_fn`` from the workflow module
+    # inside each test (fedavg_test.py:1098-1700): swap the module's names for the drop-in's
+    try:
+        import nvflare.app_common.workflows.scaffold as ref_scaffold
+    except Exception:  # a reference without the FLModel SCAFFOLD workflow
+        ref_scaffold = None
+    if ref_scaffold is not None:
+        from nvflare_amd.app_common.workflows import scaffold as dropin_scaffold
+
+        for name in ("Scaffold", "scaffold_aggregate_fn"):
+            setattr(ref_scaffold, name, getattr(dropin_scaffold, name))
+            config._fedavg_swapped.append(f"{ref_scaffold.__name__}.{name}")
 
 
 def pytest_sessionfinish(session, exitstatus):

@@ -63,6 +63,9 @@ def test_reference_fedavg_workflow_tests_same_outcome(tmp_path):
     _, _, ref = _run(tmp_path, [FEDAVG_WORKFLOW], False, "ref")
     _, rep, ours = _run(tmp_path, [FEDAVG_WORKFLOW], True, "dropin")
     assert any("workflows.fedavg.WeightedAggregationHelper" in s for s in rep["swapped"]), rep
+    assert "nvflare.app_common.workflows.scaffold.scaffold_aggregate_fn" in rep["swapped"], rep
+    assert "nvflare.app_common.workflows.scaffold.Scaffold" in rep["swapped"], rep
+    assert sum("TestScaffold" in k and v == "passed" for k, v in ours.items()) >= 8, ours
     assert ours == ref
     assert sum(v == "passed" for v in ours.values()) >= 100
 
@@ -82,6 +85,21 @@ assert issubclass(FedOpt, Ref) and issubclass(FedOpt, DeviceFedOptUpdate)
 assert FedOpt.update_model is DeviceFedOptUpdate.update_model
 assert FedOpt.optimizer_update is DeviceFedOptUpdate.optimizer_update
 assert FedOpt.run is Ref.run
+from nvflare.app_common.workflows import scaffold as ref_scaffold
+from nvflare_amd.app_common.workflows import scaffold as dropin_scaffold
+assert issubclass(dropin_scaffold.Scaffold, ref_scaffold.Scaffold)
+assert dropin_scaffold._reference_scaffold_fn is ref_scaffold.scaffold_aggregate_fn
+ctl = dropin_scaffold.Scaffold(num_clients=2, num_rounds=1, aggregation_device=0)
+seen = []
+ctl._device_scaffold_fn = lambda results: seen.append("scaffold")
+ctl._device_fedavg_fn = lambda results: seen.append("fedavg")
+import nvflare.app_common.workflows.base_fedavg as bf
+bf.BaseFedAvg.aggregate = lambda self, results, aggregate_fn=None: aggregate_fn(results)
+ctl.aggregate([], aggregate_fn=ref_scaffold.scaffold_aggregate_fn)
+ctl.aggregate([])
+mine = lambda results: seen.append("own")
+ctl.aggregate([], aggregate_fn=mine)
+assert seen == ["scaffold", "fedavg", "own"], seen
 print("composed")
 """
 
@@ -89,7 +107,8 @@ print("composed")
 @pytest.mark.skipif(not os.path.exists(FEDOPT_CTL), reason="reference tree not mounted")
 def test_fedopt_controller_composes_with_reference_controller():
     """With the real nvflare importable, the drop-in FedOpt controller IS the reference controller (its run(),
-    FedAvg rounds, constructor) with the device server step in place of optimizer_update / update_model."""
+    FedAvg rounds, constructor) with the device server step in place of optimizer_update / update_model; the
+    drop-in Scaffold controller routes the reference's aggregation functions (and only those) to the device."""
     env = dict(os.environ, NVFLARE_REF_ROOT=REF, PYTHONDONTWRITEBYTECODE="1",
                PYTHONPATH=os.pathsep.join([HERE, os.path.dirname(HERE)]))
     env.pop("NVFLARE_AMD_FORCE_STANDINS", None)
