@@ -112,7 +112,7 @@ class ShardedFedAvg:
         pieces: Dict[str, List[Tuple[int, Any]]] = {}
         for res in self._pool.map(fn, self.engines):
             for sub, arr in res.items():
-                k, off = sub.split("\x00")
+                k, off = sub.rsplit("\x00", 1)  # a key may itself hold NULs (SCAFFOLD control prefix)
                 pieces.setdefault(k, []).append((int(off), arr))
         for plist in pieces.values():
             plist.sort(key=lambda x: x[0])
@@ -140,7 +140,7 @@ class ShardedFedAvg:
 
     @property
     def keys(self):
-        return {s.split("\x00")[0] for e in self.engines for s in e.keys}
+        return {s.rsplit("\x00", 1)[0] for e in self.engines for s in e.keys}
 
     @property
     def stats(self):

@@ -151,6 +151,23 @@ def test_sharded_rejects_reshaped_contribution(oracle):
     sh._pool.shutdown()
 
 
+def test_sharded_keys_with_nul_bytes(oracle):
+    """Keys holding NUL bytes (the SCAFFOLD control prefix) survive the bucket sub-key round trip."""
+    sh = _fake_sharded()
+    rng = np.random.default_rng(2)
+    keys = ["w", "\x00scaffold_ctrl\x00w", "a\x00b\x001"]
+    rows = [{k: rng.standard_normal(9000).astype(np.float32) for k in keys} for _ in range(3)]
+    for i, r in enumerate(rows):
+        sh.add(list(r.items()), 1.0 + i, True)
+    assert sh.keys == set(keys)
+    res = sh.result()
+    assert set(res) == set(keys)
+    for k in keys:
+        exp = oracle.fedavg_c([r[k] for r in rows], [1.0, 2.0, 3.0], oracle.MODE_NUMPY)
+        assert np.array_equal(res[k].view(np.uint32), exp.view(np.uint32))
+    sh._pool.shutdown()
+
+
 
 def test_sharded_deferred_rounds_match_eager():
     """ShardedFedAvg.result_deferred: every fp32 key comes back as a ShardedDeferredAggregate whose pieces are
