@@ -73,6 +73,16 @@ def pytest_collection_modifyitems(session, config, items):
             if hasattr(mod, name):
                 setattr(mod, name, obj)
                 config._fedavg_swapped.append(f"{mod.__name__}.{name}")
+    # FedAvgLR takes its helper as a constructor default built at import (lr/fedavg.py:45): the drop-in
+    # usage is ``FedAvgLR(aggregator=WeightedAggregationHelper(...))``; here the default itself is swapped
+    lr = sys.modules.get("nvflare.app_common.workflows.lr.fedavg")
+    if lr is not None:
+        init = lr.FedAvgLR.__init__
+        defaults = tuple(wah.WeightedAggregationHelper() if type(d).__name__ == "WeightedAggregationHelper" else d
+                         for d in init.__defaults__)
+        if defaults != init.__defaults__:
+            init.__defaults__ = defaults
+            config._fedavg_swapped.append("nvflare.app_common.workflows.lr.fedavg.FedAvgLR(aggregator=)")
     # the reference's SCAFFOLD tests import ``Scaffold`` / ``scaffold_aggregate_fn`` from the workflow module
     # inside each test (fedavg_test.py:1098-1700): swap the module's names for the drop-in's
     try:

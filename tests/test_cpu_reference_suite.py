@@ -70,6 +70,22 @@ def test_reference_fedavg_workflow_tests_same_outcome(tmp_path):
     assert sum(v == "passed" for v in ours.values()) >= 100
 
 
+FEDAVG_LR = os.path.join(REF, "tests/unit_test/app_common/workflow/fedavg_lr_test.py")
+
+
+@pytest.mark.skipif(not os.path.exists(FEDAVG_LR), reason="reference tree not mounted")
+def test_reference_fedavg_lr_tests_same_outcome(tmp_path):
+    """workflow/fedavg_lr_test.py with the drop-in helper as FedAvgLR's aggregator (lr/fedavg.py:45,157-164;
+    fp64 gradient / Hessian keys through the engine's fp64 arena): every test ends as it does for the
+    reference."""
+    _, _, ref = _run(tmp_path, [FEDAVG_LR], False, "ref")
+    _, rep, ours = _run(tmp_path, [FEDAVG_LR], True, "dropin")
+    assert "nvflare.app_common.workflows.lr.fedavg.FedAvgLR(aggregator=)" in rep["swapped"], rep
+    assert rep["launches"] > 0, rep
+    assert ours == ref
+    assert sum(v == "passed" for v in ours.values()) >= 20, ours
+
+
 FEDOPT_CTL = os.path.join(REF, "nvflare/app_opt/pt/fedopt_ctl.py")
 
 _COMPOSE = r"""
