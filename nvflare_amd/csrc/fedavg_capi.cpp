@@ -535,14 +535,14 @@ void run_tiles_narrow(fedavg_ctx* ctx, const void* const* bases, const double* w
     const float fv = narrow_fin_value(fmt, fin, count);
     const int64_t T = fedavg::kTile16Elems;
     const int64_t n_tiles = (end - 1) / T - begin / T + 1;
-    // the 16-bit burst kernel keeps two blocks per CU at every K: it rounds after every operation, and one
-    // wave per SIMD does not issue that VALU work fast enough (profiles/r02/ab/narrow_burst_bpc.jsonl)
+    // blocks per CU of the 16-bit burst kernel: fedavg_internal.h kNarrowOneBlockMinK
     const bool burst = !(ctx->variant & fedavg::kVariantTileStores);
-    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)ctx->num_cus * ctx->bpc(), n_tiles));
     int k0 = 0;
     const void* cur_in = acc_in;
     do {
         const int kc = std::min(k_rows - k0, fedavg::kMaxRowsPerLaunch);
+        const int dflt = burst && op != FEDAVG_OP_NUMPY && kc >= fedavg::kNarrowOneBlockMinK ? 1 : 2;
+        const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)ctx->num_cus * ctx->bpc(dflt), n_tiles));
         fedavg::RowTableNarrow t;
         fill_narrow_table(t, bases, weights, k0, kc, fmt, op);
         const bool last = k0 + kc >= k_rows;
@@ -1089,8 +1089,9 @@ int fedavg_accumulate_tiled64(fedavg_ctx* ctx, const void* const* bases, const d
         const int64_t T = fedavg::kTile64Elems;
         const int64_t n_tiles = ((int64_t)end - 1) / T - (int64_t)begin / T + 1;
         const bool burst = !(ctx->variant & fedavg::kVariantTileStores);
-        const int bpc = burst ? ctx->bpc(k_rows >= fedavg::kBurstOneBlockMinK ? 1 : 2) : ctx->bpc();
-        const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)ctx->num_cus * bpc, n_tiles));
+        // two blocks per CU at every K (198 VGPRs: both resident): 1 block at 16 / 32 / 64 clients runs 1.4 /
+        // 0.8 / 0.1 points slower (profiles/r02/ab/bpc_check/f64_k*.jsonl)
+        const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)ctx->num_cus * ctx->bpc(), n_tiles));
         const double fv = fin_scalar(fin, count);
         int k0 = 0;
         const void* cur_in = acc_in;

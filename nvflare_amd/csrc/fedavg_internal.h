@@ -125,6 +125,11 @@ hipError_t launch_tiles_epi_f32x4_unweighted(const TileLaunch& L, const EpiParam
 // K >= kBurstOneBlockMinK clients, two below: profiles/r02/ab_burst_*.jsonl)
 bool tiles_use_burst(int64_t tile4, int unroll, int variant);
 constexpr int kBurstOneBlockMinK = 16;
+// The 16-bit burst kernel: one block per CU from 48 clients on in torch / unweighted mode (bf16 / fp16 at 64
+// clients 89.6-89.9 % against 85.6 % with two; 128 clients 87.7-88.1 vs 84.3 %), two below and always in numpy
+// mode, whose two roundings per step leave one wave per SIMD short of VALU issue (K = 32: 83.3-84.1 vs 84.2-84.3 %;
+// numpy fp16 at 64: 74.3 vs 85.4 %) -- profiles/r02/ab/narrow_bpc/.
+constexpr int kNarrowOneBlockMinK = 48;
 hipError_t launch_dequant_f32(const DequantLaunch& L, hipStream_t s);
 hipError_t launch_tiles_epi_f32x4(const TileLaunch& L, const EpiParams& E, hipStream_t s,
                                   uint64_t* launch_count = nullptr);

@@ -22,6 +22,7 @@ def main():
     ap.add_argument("--dtype", choices=["float64", "float32"], default="float64")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--variants", default="0", help="comma list of fedavg_set_variant values, interleaved rounds")
+    ap.add_argument("--blocks-per-cu", default="0", help="comma list, swept with every variant (0 = library default)")
     ap.add_argument("--layout", choices=["rows", "tiled"], default="rows",
                     help="rows: K separate client buffers (fedavg_accumulate); tiled: the engine's fp64 slab "
                          "(fedavg_accumulate_tiled64, float64 only)")
@@ -61,11 +62,12 @@ def main():
                            N.FEDAVG_FIN_SCALE, sum(ws))
     torch.cuda.synchronize()
 
-    variants = [int(v) for v in args.variants.split(",")]
+    variants = [(int(v), int(b)) for v in args.variants.split(",") for b in args.blocks_per_cu.split(",")]
     res = {v: [] for v in variants}
     for rep in range(3):
         for v in variants:
-            ctx.set_variant(v)
+            ctx.set_variant(v[0])
+            ctx.set_launch(v[1], 0)
             launch()
             ctx.sync()
             ctx.timing_begin()
@@ -73,11 +75,12 @@ def main():
                 launch()
             res[v].append(ctx.timing_end() / args.steps)
     ctx.set_variant(0)
+    ctx.set_launch(0, 0)
     nbytes = (K + 1) * P * out.element_size()
     for v in variants:
         ms = sorted(res[v])[len(res[v]) // 2]
         print(json.dumps({"tool": "bench_generic", "dtype": args.dtype, "layout": args.layout, "clients": K, "params": P,
-                          "variant": v, "kernel_ms": round(ms, 3), "alg_GBs": round(nbytes / ms / 1e6, 1),
+                          "variant": v[0], "blocks_per_cu": v[1], "kernel_ms": round(ms, 3), "alg_GBs": round(nbytes / ms / 1e6, 1),
                           "frac_of_8TBs": round(nbytes / ms / 1e6 / 8000, 4)}), flush=True)
 
 

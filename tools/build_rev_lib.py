@@ -1,0 +1,60 @@
+#!/usr/bin/env python3
+"""Build the HIP library from the sources of another git revision into a side path, for same-box A/B runs
+(``NVFLARE_AMD_FEDAVG_LIB=<out> python tools/bench_narrow.py ...`` against the in-tree library).
+
+  python tools/build_rev_lib.py --rev HEAD --out nvflare_amd/lib/ab/libnvflare_amd_fedavg_head.so
+
+The revision's csrc/ and include/ are exported to a temporary directory with ``git show``; the flags and
+source list are the current nvflare_amd/_build.py's (the A/B compares kernels, not build settings)."""
+
+import argparse
+import os
+import subprocess
+import sys
+import tempfile
+from concurrent.futures import ThreadPoolExecutor
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+from nvflare_amd import _build as B  # noqa: E402
+
+
+def _export(rev: str, path: str, dst: str) -> None:
+    files = subprocess.run(["git", "-C", ROOT, "ls-tree", "-r", "--name-only", rev, path], check=True,
+                           capture_output=True, text=True).stdout.split()
+    for f in files:
+        blob = subprocess.run(["git", "-C", ROOT, "show", f"{rev}:{f}"], check=True, capture_output=True).stdout
+        out = os.path.join(dst, f)
+        os.makedirs(os.path.dirname(out), exist_ok=True)
+        with open(out, "wb") as fh:
+            fh.write(blob)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rev", default="HEAD")
+    ap.add_argument("--out", required=True)
+    args = ap.parse_args()
+    with tempfile.TemporaryDirectory() as tmp:
+        _export(args.rev, "nvflare_amd/csrc", tmp)
+        _export(args.rev, "include", tmp)
+        csrc = os.path.join(tmp, "nvflare_amd", "csrc")
+        inc = [f"-I{os.path.join(tmp, 'include')}", f"-I{csrc}"]
+        srcs = [s for s in B.SOURCES if os.path.exists(os.path.join(csrc, s))]
+
+        def compile_one(src):
+            obj = os.path.join(tmp, src + ".o")
+            subprocess.run([B.HIPCC, *B.FLAGS, *inc, "-c", os.path.join(csrc, src), "-o", obj], check=True)
+            return obj
+
+        with ThreadPoolExecutor(max_workers=min(8, len(srcs))) as pool:
+            objs = list(pool.map(compile_one, srcs))
+        os.makedirs(os.path.dirname(os.path.abspath(args.out)), exist_ok=True)
+        subprocess.run([B.HIPCC, "-shared", "-fPIC", f"--offload-arch={B.ARCH}", *objs, "-o", args.out, "-lpthread"],
+                       check=True)
+    print(args.out)
+
+
+if __name__ == "__main__":
+    main()
