@@ -67,8 +67,15 @@ def dist_setup(args):
     if world > 1:
         import torch.distributed as dist
 
-        torch.cuda.set_device(local)
-        dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
+        if os.environ.get("NVFLARE_AMD_BENCH_SHARED_DEVICE") == "1":
+            # rehearsal of the multi-rank flow on a one-GPU box: every rank on cuda:0, barriers and the
+            # max-over-ranks timing over gloo (RCCL refuses two ranks on one device); never a measurement
+            local = 0
+            torch.cuda.set_device(0)
+            dist.init_process_group(backend="gloo")
+        else:
+            torch.cuda.set_device(local)
+            dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
     if world != args.gpus and rank == 0:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
     return world, rank, local
@@ -98,15 +105,29 @@ def max_over_ranks(world, value: float) -> float:
     return float(t.item())
 
 
+def sum_over_ranks(world, values):
+    """Element-wise SUM over ranks of a few host integers (spot-check counts)."""
+    if world == 1:
+        return list(values)
+    import torch
+    import torch.distributed as dist
+
+    dev = "cuda" if dist.get_backend() == "nccl" else "cpu"
+    t = torch.tensor(list(values), dtype=torch.int64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return [int(x) for x in t.tolist()]
+
+
 def rank_bucket(rank: int, P: int):
     """Weak scaling: rank r aggregates global params [r*P, (r+1)*P) of every client (sharding.bucket_ranges
     with equal per-GPU buckets); returns the generator column offset of the bucket."""
     return rank * P
 
 
-def cpu_baseline_and_spot_check(args, ctx, K, out_buf, weights, count, P, col0, op):
-    """Oracle leg (test infrastructure): time the reference restatement on the host, then check sampled
-    device outputs bit-for-bit against the oracle computed from the host twin of the generator."""
+def cpu_baseline_and_spot_check(args, ctx, K, out_buf, weights, count, P, col0, op, baseline=True):
+    """Oracle leg (test infrastructure): time the reference restatement on the host (``baseline``: rank 0 at
+    N=1 only), then check sampled device outputs of this rank's bucket bit-for-bit against the oracle computed
+    from the host twin of the generator."""
     import torch
 
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
@@ -124,7 +145,7 @@ def cpu_baseline_and_spot_check(args, ctx, K, out_buf, weights, count, P, col0, 
         mism = int(np.count_nonzero(exp.view(np.uint32) != got.view(np.uint32)))
         res["spot_check"] = {"sampled": int(idx.size), "mismatches": mism, "oracle": "oracle/fedavg_oracle.c"}
     # -- CPU baseline: the reference's torch CPU op sequence on a bounded sample ------------------
-    if not args.no_cpu_baseline:
+    if baseline and not args.no_cpu_baseline:
         Ps = int(min(args.cpu_sample_params, P))
         gen = [np.random.default_rng(1000 + k).standard_normal(Ps, dtype=np.float32) for k in range(K)]
         trows = [torch.from_numpy(g) for g in gen]
@@ -277,10 +298,15 @@ def main():
     kernel_ms_max = max_over_ranks(world, kernel_ms)
 
     extra = {}
-    if rank == 0 and world == 1:
-        if args.epilogue != "none":
-            args.spot_check = 0  # the spot check covers the plain aggregation output only
+    if args.epilogue != "none":
+        args.spot_check = 0  # the spot check covers the plain aggregation output only
+    if world == 1:
         extra = cpu_baseline_and_spot_check(args, ctx, K, out, weights, count, P, col0, op)
+    else:  # every rank checks its own bucket; the counts are summed (no CPU baseline at N > 1)
+        extra = cpu_baseline_and_spot_check(args, ctx, K, out, weights, count, P, col0, op, baseline=False)
+        if "spot_check" in extra:
+            sampled, mism = sum_over_ranks(world, [extra["spot_check"]["sampled"], extra["spot_check"]["mismatches"]])
+            extra["spot_check"].update(sampled=sampled, mismatches=mism, ranks=world)
 
     if rank == 0:
         bytes_step = 4.0 * K * P * world  # aggregated client bytes per step, all ranks
@@ -341,14 +367,16 @@ def main():
         if "spot_check" in extra:
             line["spot_check"] = extra["spot_check"]
         print(json.dumps(line), flush=True)
-        if "spot_check" in extra and extra["spot_check"]["mismatches"]:
-            print("SPOT CHECK FAILED", file=sys.stderr)
-            sys.exit(3)
+    failed = bool(extra.get("spot_check", {}).get("mismatches"))  # summed over ranks: every rank agrees
+    if failed and rank == 0:
+        print("SPOT CHECK FAILED", file=sys.stderr)
     if world > 1:
         import torch.distributed as dist
 
         dist.barrier()
         dist.destroy_process_group()
+    if failed:
+        sys.exit(3)
 
 
 if __name__ == "__main__":

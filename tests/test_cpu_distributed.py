@@ -53,8 +53,9 @@ def _worker(rank, world, port, P, K, q):
         gathered = [None] * world if rank == 0 else None
         dist.gather_object(part, gathered, dst=0)
         t = bench.max_over_ranks(world, float(rank + 1))
+        sums = bench.sum_over_ranks(world, [rank, 1])  # the spot-check counts' reduction
         if rank == 0:
-            q.put((np.concatenate(gathered), t))
+            q.put((np.concatenate(gathered), (t, sums)))
     finally:
         dist.destroy_process_group()
 
@@ -67,7 +68,7 @@ def test_weak_scaling_buckets_gloo(oracle):
     procs = [ctx.Process(target=_worker, args=(r, world, port, P, K, q)) for r in range(world)]
     for p in procs:
         p.start()
-    res, tmax = q.get(timeout=120)
+    res, (tmax, sums) = q.get(timeout=120)
     for p in procs:
         p.join(60)
         assert p.exitcode == 0
@@ -75,6 +76,7 @@ def test_weak_scaling_buckets_gloo(oracle):
     full = oracle.fedavg_c(rows, oracle.synth_weights(K), oracle.MODE_TORCH)
     assert np.array_equal(res.view(np.uint32), full.view(np.uint32))
     assert tmax == 2.0  # max over ranks
+    assert sums == [1, 2]  # sum over ranks
 
 
 def test_sharded_pieces_reassemble(oracle):
