@@ -177,6 +177,9 @@ __global__ void __launch_bounds__(kBlock) fedavg_rows_narrow(const RowTableNarro
 // ---------------------------------------------------------------------------------------------
 constexpr int kTile16 = 4096;
 constexpr int kCpl16 = kTile16 / (8 * kBlock);  // 2
+#ifndef FEDAVG_NARROW_BURST_WAVES
+#define FEDAVG_NARROW_BURST_WAVES 2  // waves per SIMD the burst kernel is compiled for (register budget)
+#endif
 #ifndef FEDAVG_NARROW_UNROLL
 #define FEDAVG_NARROW_UNROLL 6  // clients whose loads are in flight together (A/B: profiles/r01/narrow_unroll_ab.jsonl)
 #endif
@@ -298,8 +301,8 @@ __global__ void __launch_bounds__(kBlock) fedavg_tiles_narrow(const RowTableNarr
 // loads grouped from client 0 on (bf16 64 x 1e9: 85.6 % against 84.4 % ungrouped and 82.0 % for the per-tile
 // form, profiles/r02/ab/narrow_burst_grouped.jsonl).
 template <int FMT, int OP, int FIN, bool ACC_IN, int TPB>
-__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2, 2)))
-fedavg_tiles_narrow_burst(const RowTableNarrow tab, const int K, const int64_t tstride8, const u32x4* acc_in, u32x4* out,
+__global__ void __launch_bounds__(kBlock)
+__attribute__((amdgpu_waves_per_eu(FEDAVG_NARROW_BURST_WAVES, FEDAVG_NARROW_BURST_WAVES))) fedavg_tiles_narrow_burst(const RowTableNarrow tab, const int K, const int64_t tstride8, const u32x4* acc_in, u32x4* out,
                           const int64_t b8, const int64_t e8, const float fv, const int64_t t0, const int64_t t_end) {
     constexpr int64_t T8 = (int64_t)kCpl16 * kBlock;
     u32x4 res[TPB][kCpl16];

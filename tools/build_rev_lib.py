@@ -3,6 +3,7 @@
 (``NVFLARE_AMD_FEDAVG_LIB=<out> python tools/bench_narrow.py ...`` against the in-tree library).
 
   python tools/build_rev_lib.py --rev HEAD --out nvflare_amd/lib/ab/libnvflare_amd_fedavg_head.so
+  python tools/build_rev_lib.py --rev WORKTREE -D FEDAVG_NARROW_UNROLL=8 --out nvflare_amd/lib/ab/u8.so
 
 The revision's csrc/ and include/ are exported to a temporary directory with ``git show``; the flags and
 source list are the current nvflare_amd/_build.py's (the A/B compares kernels, not build settings)."""
@@ -35,17 +36,25 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rev", default="HEAD")
     ap.add_argument("--out", required=True)
+    ap.add_argument("-D", dest="defines", action="append", default=[], help="extra preprocessor definitions")
     args = ap.parse_args()
     with tempfile.TemporaryDirectory() as tmp:
-        _export(args.rev, "nvflare_amd/csrc", tmp)
-        _export(args.rev, "include", tmp)
+        if args.rev == "WORKTREE":  # the working tree's sources as they are
+            import shutil
+
+            shutil.copytree(os.path.join(ROOT, "nvflare_amd", "csrc"), os.path.join(tmp, "nvflare_amd", "csrc"))
+            shutil.copytree(os.path.join(ROOT, "include"), os.path.join(tmp, "include"))
+        else:
+            _export(args.rev, "nvflare_amd/csrc", tmp)
+            _export(args.rev, "include", tmp)
         csrc = os.path.join(tmp, "nvflare_amd", "csrc")
         inc = [f"-I{os.path.join(tmp, 'include')}", f"-I{csrc}"]
         srcs = [s for s in B.SOURCES if os.path.exists(os.path.join(csrc, s))]
 
         def compile_one(src):
             obj = os.path.join(tmp, src + ".o")
-            subprocess.run([B.HIPCC, *B.FLAGS, *inc, "-c", os.path.join(csrc, src), "-o", obj], check=True)
+            defs = [f"-D{d}" for d in args.defines]
+            subprocess.run([B.HIPCC, *B.FLAGS, *defs, *inc, "-c", os.path.join(csrc, src), "-o", obj], check=True)
             return obj
 
         with ThreadPoolExecutor(max_workers=min(8, len(srcs))) as pool:
