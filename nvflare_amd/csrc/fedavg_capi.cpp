@@ -1201,7 +1201,7 @@ int fedavg_accumulate_tiled_epi(fedavg_ctx* ctx, const void* const* bases, const
         L.e4 = (int64_t)end / 4;
         const int64_t n_tiles = (L.e4 - 1) / L.tile4 - L.b4 / L.tile4 + 1;
         const bool burst = !(L.variant & (fedavg::kVariantEpiPrefetch | fedavg::kVariantTileStores));
-        const int bpc = burst ? ctx->bpc(L.k >= fedavg::kBurstOneBlockMinK ? 1 : 2) : ctx->bpc();
+        const int bpc = burst ? ctx->bpc(L.k >= fedavg::kEpiOneBlockMinK ? 1 : 2) : ctx->bpc();
         L.grid = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)ctx->num_cus * bpc, n_tiles));
         L.fin_val = (float)fin_scalar(fin, count);
         L.acc_in = cur_in;

@@ -122,9 +122,13 @@ hipError_t launch_tiles_epi_f32x4_numpy(const TileLaunch& L, const EpiParams& E,
 hipError_t launch_tiles_epi_f32x4_torch(const TileLaunch& L, const EpiParams& E, hipStream_t s, uint64_t* nl);
 hipError_t launch_tiles_epi_f32x4_unweighted(const TileLaunch& L, const EpiParams& E, hipStream_t s, uint64_t* nl);
 // whether launch_tiles_f32x4 takes the burst kernel for this geometry (it then wants one block per CU at
-// K >= kBurstOneBlockMinK clients, two below: profiles/r02/ab_burst_*.jsonl)
+// K >= kBurstOneBlockMinK clients, two below)
 bool tiles_use_burst(int64_t tile4, int unroll, int variant);
-constexpr int kBurstOneBlockMinK = 16;
+// Blocks per CU of the fp32 burst kernels by client count (profiles/r02/ab/epi_bpc/, interleaved in one
+// process, 1e9 params): plain kernel 1 vs 2 blocks at 8 / 16 / 32 / 64 clients 77.6/82.1, 85.0/87.2,
+// 87.7/87.3, 89.5/88.7 %; fused Adam 77.8/80.3, 81.6/83.1, 84.8/85.5, 87.2/87.2 %.
+constexpr int kBurstOneBlockMinK = 32;
+constexpr int kEpiOneBlockMinK = 64;
 // The 16-bit burst kernel: one block per CU from 48 clients on in torch / unweighted mode (bf16 / fp16 at 64
 // clients 89.6-89.9 % against 85.6 % with two; 128 clients 87.7-88.1 vs 84.3 %), two below and always in numpy
 // mode, whose two roundings per step leave one wave per SIMD short of VALU issue (K = 32: 83.3-84.1 vs 84.2-84.3 %;
