@@ -27,8 +27,9 @@ extern "C" {
 #endif
 
 /* Bumped whenever a struct layout or an entry point changes (v3: Rprop / ASGD fields appended to struct
- * fedavg_epilogue; v4: fedavg_launch_count; v5: fedavg_d2h_multi).  fedavg_struct_size() lets a binding check each struct's size as well. */
-#define FEDAVG_ABI_VERSION 5
+ * fedavg_epilogue; v4: fedavg_launch_count; v5: fedavg_d2h_multi; v6: fedavg_accumulate_tiled16_tails and
+ * integer accumulators in fedavg_accumulate).  fedavg_struct_size() lets a binding check each struct's size as well. */
+#define FEDAVG_ABI_VERSION 6
 
 /* element types of client rows (in_dtype) and of the running sum / result (acc_dtype) */
 enum fedavg_dtype {
@@ -213,7 +214,12 @@ int fedavg_sync(fedavg_ctx* ctx);
  *   TORCH (CPU vectorised path: mul/div in fp32 with the scalar as float, add_ alpha rounded to the format):
  *                                   first r(v*float(w))   step r(fma(v, r(w), T))   DIV r(T/float(count))
  *   UNWEIGHTED                      first v               step r(T + v)
- * (weighted_aggregation_helper.py:181-236 with float16 / bfloat16 values). */
+ * (weighted_aggregation_helper.py:181-236 with float16 / bfloat16 values).
+ * Integer / bool accumulators, (X,X) for X in I8, I16, I32, I64, U8, U16, U32, U64, BOOL, with
+ * FEDAVG_OP_UNWEIGHTED and FEDAVG_FIN_NONE only: numpy's integer sum of weigh_by_local_iter=False arrays
+ * (:195-199, :214-215) -- two's-complement wraparound in the array's dtype, logical OR for BOOL; weights and
+ * count unused.  The caller finalises it as numpy does (:236) with a (X, F64) call: one row (the sum), weight
+ * 1.0 / count, FEDAVG_OP_NUMPY, FEDAVG_FIN_NONE, which computes float64(T) * (1.0 / count). */
 int fedavg_accumulate(fedavg_ctx* ctx, const void* const* rows, const double* weights, int k_rows,
                       const void* acc_in, void* out, size_t n, int in_dtype, int acc_dtype, int op,
                       int fin, double count);
@@ -236,6 +242,19 @@ int fedavg_accumulate_tiled(fedavg_ctx* ctx, const void* const* bases, const dou
 int fedavg_accumulate_tiled16(fedavg_ctx* ctx, int fmt, const void* const* bases, const double* weights, int k_rows,
                               size_t tile_elems, size_t tile_stride, size_t begin, size_t end, const void* acc_in,
                               void* out, int op, int fin, double count);
+
+/* fedavg_accumulate_tiled16 with torch's scalar remainder.  torch CPU runs T.add_(v, alpha=w) on float16 /
+ * bfloat16 tensors (weighted_aggregation_helper.py:207) over the element ranges at::parallel_for gives its
+ * threads, each through a vectorised loop (the TORCH step above, one fp32 fma) and, for the last
+ * (range length mod 32) elements of the range, a scalar loop whose c10::Half / c10::BFloat16 operators round
+ * twice: step p = r(v * r(w)), T = r(T + p).  tails: n_tails strictly increasing flat element indices (host
+ * memory) that take that step; those outside [begin, end) are ignored, as are all of them for an op other
+ * than FEDAVG_OP_TORCH.  The listed elements are recomputed into a side buffer before the tile kernel (acc_in
+ * may alias out) and written over its results after it: two small extra launches when any lies in the range. */
+int fedavg_accumulate_tiled16_tails(fedavg_ctx* ctx, int fmt, const void* const* bases, const double* weights,
+                                    int k_rows, size_t tile_elems, size_t tile_stride, size_t begin, size_t end,
+                                    const void* acc_in, void* out, int op, int fin, double count,
+                                    const int64_t* tails, size_t n_tails);
 
 /* fedavg_accumulate_tiled for fp64 client storage and totals (numpy's default dtype; the engine's fp64 arena):
  * tile_elems = 4096, begin/end multiples of 2, every pointer 16-byte aligned.  fp64 arithmetic in arrival

@@ -41,7 +41,7 @@ FEDAVG_FIN_NONE = 0
 FEDAVG_FIN_SCALE = 1
 FEDAVG_FIN_DIV = 2
 
-ABI_VERSION = 5  # include/nvflare_amd_fedavg.h FEDAVG_ABI_VERSION
+ABI_VERSION = 6  # include/nvflare_amd_fedavg.h FEDAVG_ABI_VERSION
 
 c_void_p = ctypes.c_void_p
 c_int = ctypes.c_int
@@ -120,6 +120,24 @@ _SIGNATURES = {
         c_int,  # op
         c_int,  # fin
         c_double,  # count
+    ],
+    "fedavg_accumulate_tiled16_tails": [
+        c_void_p,  # ctx
+        c_int,  # fmt
+        ctypes.POINTER(c_void_p),  # bases
+        ctypes.POINTER(c_double),  # weights
+        c_int,  # k_rows
+        c_size_t,  # tile_elems
+        c_size_t,  # tile_stride
+        c_size_t,  # begin
+        c_size_t,  # end
+        c_void_p,  # acc_in
+        c_void_p,  # out
+        c_int,  # op
+        c_int,  # fin
+        c_double,  # count
+        c_void_p,  # tails (int64, host)
+        c_size_t,  # n_tails
     ],
     "fedavg_accumulate_tiled64": [
         c_void_p,  # ctx

@@ -199,6 +199,9 @@ struct fedavg_ctx {
     // readiness marks for fedavg_d2h_marked: (event on the compute stream, bytes of the source final by then)
     std::vector<std::pair<hipEvent_t, size_t>> marks;
     std::vector<hipEvent_t> mark_pool;
+    // torch scalar-remainder elements of a 16-bit launch: their indices and recomputed values (device)
+    void* tails_buf = nullptr;
+    size_t tails_bytes = 0;
 
     hipStream_t compute() const { return ext_stream ? ext_stream : own_stream; }
     int bpc(int dflt = fedavg::kDefaultBlocksPerCu) const { return blocks_per_cu ? blocks_per_cu : dflt; }
@@ -480,6 +483,23 @@ void run_generic(fedavg_ctx* ctx, const void* const* rows, const double* weights
     } while (k0 < k_rows);
 }
 
+// integer / bool sums (weigh_by_local_iter=False numpy arrays), chained through out past 128 rows
+void run_intsum(fedavg_ctx* ctx, const void* const* rows, int k_rows, const void* acc_in, void* out, int64_t n,
+                int dtype, hipStream_t s) {
+    int k0 = 0;
+    const void* cur_in = acc_in;
+    do {
+        const int kc = std::min(k_rows - k0, fedavg::kMaxRowsPerLaunch);
+        fedavg::RowTableGeneric gt;
+        memset(&gt, 0, sizeof(gt));
+        for (int j = 0; j < kc; ++j) gt.rows[j] = rows[k0 + j];
+        HIP_CHECK(fedavg::launch_rows_intsum(gt, kc, cur_in, out, n, dtype, stream_grid(ctx, n), s));
+        ++ctx->launches;
+        cur_in = out;
+        k0 += kc;
+    } while (k0 < k_rows);
+}
+
 // 16-bit accumulators: the weights and the finalisation scalar are rounded here exactly as the reference
 // library rounds them (see fedavg_narrow.hip).
 float narrow_fin_value(int fmt, int fin, double count) {
@@ -529,9 +549,11 @@ void run_narrow(fedavg_ctx* ctx, const void* const* rows, const double* weights,
 }
 
 // Tiled 16-bit client storage over [begin, end) (multiples of 8): chunks of 128 clients chained through out.
+// tails / n_tails: sorted flat indices inside [begin, end) that take torch's scalar-remainder step (op TORCH
+// only; fedavg_narrow.hip fedavg_torch16_tails), already on the device.
 void run_tiles_narrow(fedavg_ctx* ctx, const void* const* bases, const double* weights, int k_rows, int64_t tstride,
                       int64_t begin, int64_t end, const void* acc_in, void* out, int fmt, int op, int fin, double count,
-                      hipStream_t s) {
+                      hipStream_t s, const int64_t* tails = nullptr, int64_t n_tails = 0, void* tail_vals = nullptr) {
     const float fv = narrow_fin_value(fmt, fin, count);
     const int64_t T = fedavg::kTile16Elems;
     const int64_t n_tiles = (end - 1) / T - begin / T + 1;
@@ -546,8 +568,17 @@ void run_tiles_narrow(fedavg_ctx* ctx, const void* const* bases, const double* w
         fedavg::RowTableNarrow t;
         fill_narrow_table(t, bases, weights, k0, kc, fmt, op);
         const bool last = k0 + kc >= k_rows;
+        if (n_tails) {  // before the tile kernel: cur_in may be out
+            HIP_CHECK(fedavg::launch_torch16_tails(t, kc, T, tstride, tails, n_tails, cur_in, tail_vals, fmt,
+                                                   last ? fin : FEDAVG_FIN_NONE, fv, s));
+            ++ctx->launches;
+        }
         HIP_CHECK(fedavg::launch_tiles_narrow(t, kc, tstride, cur_in, out, begin, end, fmt, op,
                                               last ? fin : FEDAVG_FIN_NONE, fv, grid, burst, s, &ctx->launches));
+        if (n_tails) {
+            HIP_CHECK(fedavg::launch_scatter16(tails, tail_vals, n_tails, out, s));
+            ++ctx->launches;
+        }
         cur_in = out;
         k0 += kc;
     } while (k0 < k_rows);
@@ -643,6 +674,7 @@ int fedavg_destroy(fedavg_ctx* ctx) {
             if (ev) (void)hipEventDestroy(ev);
         for (auto& m : ctx->marks) (void)hipEventDestroy(m.first);
         for (hipEvent_t ev : ctx->mark_pool) (void)hipEventDestroy(ev);
+        if (ctx->tails_buf) (void)hipFree(ctx->tails_buf);
         if (ctx->own_stream) (void)hipStreamDestroy(ctx->own_stream);
         if (ctx->copy_stream) (void)hipStreamDestroy(ctx->copy_stream);
     });
@@ -957,10 +989,13 @@ int fedavg_accumulate(fedavg_ctx* ctx, const void* const* rows, const double* we
         check_dtype(in_dtype);
         check_dtype(acc_dtype);
         const bool narrow = acc_dtype == FEDAVG_F16 || acc_dtype == FEDAVG_BF16;
+        const bool int_acc = acc_dtype != FEDAVG_F32 && acc_dtype != FEDAVG_F64 && !narrow;
         if (narrow) {
             if (in_dtype != acc_dtype) throw Error("a 16-bit accumulator needs inputs of the same dtype");
-        } else if (acc_dtype != FEDAVG_F32 && acc_dtype != FEDAVG_F64) {
-            throw Error("acc_dtype must be F32, F64, F16 or BF16");
+        } else if (int_acc) {
+            if (in_dtype != acc_dtype || op != FEDAVG_OP_UNWEIGHTED || fin != FEDAVG_FIN_NONE)
+                throw Error("an integer / bool accumulator needs inputs of its dtype, FEDAVG_OP_UNWEIGHTED and "
+                            "FEDAVG_FIN_NONE");
         } else if (in_dtype == FEDAVG_BF16 ||
                    (acc_dtype == FEDAVG_F32 && (in_dtype == FEDAVG_F64 || in_dtype == FEDAVG_U16 ||
                                                 in_dtype == FEDAVG_U32 || in_dtype == FEDAVG_U64))) {
@@ -979,6 +1014,11 @@ int fedavg_accumulate(fedavg_ctx* ctx, const void* const* rows, const double* we
         TimingScope ts(ctx, s);
         if (narrow) {
             run_narrow(ctx, rows, weights, k_rows, acc_in, out, (int64_t)n, acc_dtype, op, fin, count, s);
+            ts.done();
+            return;
+        }
+        if (int_acc) {
+            run_intsum(ctx, rows, k_rows, acc_in, out, (int64_t)n, acc_dtype, s);
             ts.done();
             return;
         }
@@ -1034,6 +1074,14 @@ int fedavg_accumulate_tiled(fedavg_ctx* ctx, const void* const* bases, const dou
 int fedavg_accumulate_tiled16(fedavg_ctx* ctx, int fmt, const void* const* bases, const double* weights, int k_rows,
                               size_t tile_elems, size_t tile_stride, size_t begin, size_t end, const void* acc_in,
                               void* out, int op, int fin, double count) {
+    return fedavg_accumulate_tiled16_tails(ctx, fmt, bases, weights, k_rows, tile_elems, tile_stride, begin, end, acc_in,
+                                           out, op, fin, count, nullptr, 0);
+}
+
+int fedavg_accumulate_tiled16_tails(fedavg_ctx* ctx, int fmt, const void* const* bases, const double* weights,
+                                    int k_rows, size_t tile_elems, size_t tile_stride, size_t begin, size_t end,
+                                    const void* acc_in, void* out, int op, int fin, double count,
+                                    const int64_t* tails, size_t n_tails) {
     return guarded([&] {
         if (!ctx) throw Error("ctx is NULL");
         if (fmt != FEDAVG_F16 && fmt != FEDAVG_BF16) throw Error("fmt must be FEDAVG_F16 or FEDAVG_BF16");
@@ -1053,11 +1101,38 @@ int fedavg_accumulate_tiled16(fedavg_ctx* ctx, int fmt, const void* const* bases
         for (int k = 0; k < k_rows; ++k)
             if (!bases[k] || reinterpret_cast<uintptr_t>(bases[k]) % 16)
                 throw Error("base " + std::to_string(k) + " is NULL or not 16-byte aligned");
+        if (n_tails && !tails) throw Error("tails is NULL");
+        for (size_t j = 1; j < n_tails; ++j)
+            if (tails[j] <= tails[j - 1]) throw Error("tails must be strictly increasing");
         ctx->activate();
         hipStream_t s = ctx->compute();
+        // the scalar remainder exists only in torch's add_ with alpha (FEDAVG_OP_TORCH)
+        const int64_t* lo = tails;
+        const int64_t* hi = tails;
+        if (op == FEDAVG_OP_TORCH && n_tails) {
+            lo = std::lower_bound(tails, tails + n_tails, (int64_t)begin);
+            hi = std::lower_bound(lo, tails + n_tails, (int64_t)end);
+        }
+        const int64_t m = hi - lo;
+        int64_t* d_idx = nullptr;
+        void* d_vals = nullptr;
+        if (m) {
+            const size_t need = (size_t)m * (sizeof(int64_t) + sizeof(uint16_t));
+            HIP_CHECK(hipStreamSynchronize(s));  // earlier launches may still read the side buffer
+            if (ctx->tails_bytes < need) {
+                if (ctx->tails_buf) HIP_CHECK(hipFree(ctx->tails_buf));
+                ctx->tails_buf = nullptr;
+                ctx->tails_bytes = 0;
+                HIP_CHECK(hipMalloc(&ctx->tails_buf, need));
+                ctx->tails_bytes = need;
+            }
+            d_idx = static_cast<int64_t*>(ctx->tails_buf);
+            d_vals = d_idx + m;
+            HIP_CHECK(hipMemcpy(d_idx, lo, (size_t)m * sizeof(int64_t), hipMemcpyHostToDevice));
+        }
         TimingScope ts(ctx, s);
         run_tiles_narrow(ctx, bases, weights, k_rows, (int64_t)tile_stride, (int64_t)begin, (int64_t)end, acc_in, out,
-                         fmt, op, fin, count, s);
+                         fmt, op, fin, count, s, d_idx, m, d_vals);
         ts.done();
     });
 }

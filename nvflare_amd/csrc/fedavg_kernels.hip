@@ -418,6 +418,67 @@ hipError_t launch_tiles_f64(const RowTableGeneric& tab, int K, int64_t tstride_e
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// integer / bool totals of numpy arrays with weigh_by_local_iter=False (weighted_aggregation_helper.py:195-199,
+// :214-215): first T = v.copy(), step T = T + v in the array's own dtype -- two's-complement wraparound as
+// numpy's integer add, logical OR for bool (numpy's add on bool arrays).  The caller finalises the sum as
+// float64(T) * (1.0 / count) (:236) with a generic (int -> F64) launch.
+// ---------------------------------------------------------------------------------------------
+template <typename U, bool IS_BOOL, bool ACC_IN>
+__global__ void __launch_bounds__(kBlock) fedavg_rows_intsum(const RowTableGeneric tab, const int K, const U* acc_in,
+                                                              U* out, const int64_t n) {
+    const int64_t stride = (int64_t)gridDim.x * kBlock;
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
+        U acc;
+        int k = 0;
+        if constexpr (ACC_IN) {
+            acc = acc_in[i];
+        } else {
+            acc = static_cast<const U*>(tab.rows[0])[i];
+            k = 1;
+        }
+        for (; k < K; ++k) {
+            const U v = static_cast<const U*>(tab.rows[k])[i];
+            acc = IS_BOOL ? (U)(acc | v) : (U)(acc + v);  // unsigned arithmetic: defined wraparound
+        }
+        out[i] = acc;
+    }
+}
+
+template <typename U, bool IS_BOOL>
+static hipError_t launch_intsum_t(const RowTableGeneric& tab, int K, const void* acc_in, void* out, int64_t n, int grid,
+                                  hipStream_t s) {
+    if (acc_in)
+        hipLaunchKernelGGL((fedavg_rows_intsum<U, IS_BOOL, true>), dim3(grid), dim3(kBlock), 0, s, tab, K,
+                           static_cast<const U*>(acc_in), static_cast<U*>(out), n);
+    else
+        hipLaunchKernelGGL((fedavg_rows_intsum<U, IS_BOOL, false>), dim3(grid), dim3(kBlock), 0, s, tab, K,
+                           static_cast<const U*>(acc_in), static_cast<U*>(out), n);
+    return hipGetLastError();
+}
+
+hipError_t launch_rows_intsum(const RowTableGeneric& tab, int K, const void* acc_in, void* out, int64_t n, int dtype,
+                              int grid, hipStream_t s) {
+    switch (dtype) {
+        case FEDAVG_I8:
+        case FEDAVG_U8:
+            return launch_intsum_t<uint8_t, false>(tab, K, acc_in, out, n, grid, s);
+        case FEDAVG_BOOL:
+            return launch_intsum_t<uint8_t, true>(tab, K, acc_in, out, n, grid, s);
+        case FEDAVG_I16:
+        case FEDAVG_U16:
+            return launch_intsum_t<uint16_t, false>(tab, K, acc_in, out, n, grid, s);
+        case FEDAVG_I32:
+        case FEDAVG_U32:
+            return launch_intsum_t<uint32_t, false>(tab, K, acc_in, out, n, grid, s);
+        case FEDAVG_I64:
+        case FEDAVG_U64:
+            return launch_intsum_t<uint64_t, false>(tab, K, acc_in, out, n, grid, s);
+        default:
+            return hipErrorInvalidValue;
+    }
+}
+
 hipError_t launch_rows_generic(const RowTableGeneric& tab, int K, const void* acc_in, void* out, int64_t n,
                                int in_dtype, int acc_dtype, int op, int fin, double fin_val, int grid,
                                hipStream_t s) {

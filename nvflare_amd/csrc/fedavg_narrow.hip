@@ -393,6 +393,93 @@ hipError_t launch_tiles_narrow(const RowTableNarrow& tab, int K, int64_t tstride
     return hipErrorInvalidValue;
 }
 
+// ---------------------------------------------------------------------------------------------
+// torch's scalar remainder.  torch CPU runs T.add_(v, alpha=w) on float16 / bfloat16 tensors
+// (weighted_aggregation_helper.py:207) over the ranges at::parallel_for gives its threads (one range below
+// 32768 elements), each through cpu_kernel_vec's vectorized loop -- one fp32 fma, the TORCH step above --
+// and, for the last (range length mod 32) elements of the range, through the scalar remainder loop, whose
+// c10::Half / c10::BFloat16 operators round the product and the sum separately:  p = r(v * r(w)), T = r(T + p).
+// (The first v.mul(w) and the final div_ compute the same in both loops.)  The engine lists those elements;
+// fedavg_torch16_tails recomputes them from the same inputs into a side buffer before the tile kernel runs
+// (acc_in may alias out), and fedavg_scatter16 writes them over the tile kernel's results after it.
+// ---------------------------------------------------------------------------------------------
+template <int FMT, int FIN, bool ACC_IN>
+__global__ void __launch_bounds__(kBlock) fedavg_torch16_tails(const RowTableNarrow tab, const int K, const int64_t tile,
+                                                                const int64_t tstride, const int64_t* idx,
+                                                                const int64_t m, const uint16_t* acc_in,
+                                                                uint16_t* vals, const float fv) {
+    const int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (j >= m) return;
+    const int64_t i = idx[j];
+    const int64_t off = (i / tile) * tstride + i % tile;
+    float t;
+    int k = 0;
+    if constexpr (ACC_IN) {
+        t = load16<FMT>(acc_in[i]);
+    } else {
+        t = first16<FMT, FEDAVG_OP_TORCH>(load16<FMT>(static_cast<const uint16_t*>(tab.rows[0])[off]), tab.w_first[0]);
+        k = 1;
+    }
+    for (; k < K; ++k) {
+        const float v = load16<FMT>(static_cast<const uint16_t*>(tab.rows[k])[off]);
+        t = rnd<FMT>(t + rnd<FMT>(v * tab.w_step[k]));  // tab.w_step[k] = r(w): c10 casts alpha to the dtype
+    }
+    vals[j] = bits16<FMT>(fin16<FMT, FIN>(t, fv));
+}
+
+__global__ void __launch_bounds__(kBlock) fedavg_scatter16(const int64_t* idx, const uint16_t* vals, const int64_t m,
+                                                            uint16_t* out) {
+    const int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (j < m) out[idx[j]] = vals[j];
+}
+
+template <int FMT, int FIN>
+static hipError_t launch_tails_a(const RowTableNarrow& tab, int K, int64_t tile, int64_t tstride, const int64_t* idx,
+                                 int64_t m, const void* acc_in, void* vals, float fv, int grid, hipStream_t s) {
+    const uint16_t* ai = static_cast<const uint16_t*>(acc_in);
+    uint16_t* v = static_cast<uint16_t*>(vals);
+    if (acc_in)
+        hipLaunchKernelGGL((fedavg_torch16_tails<FMT, FIN, true>), dim3(grid), dim3(kBlock), 0, s, tab, K, tile, tstride,
+                           idx, m, ai, v, fv);
+    else
+        hipLaunchKernelGGL((fedavg_torch16_tails<FMT, FIN, false>), dim3(grid), dim3(kBlock), 0, s, tab, K, tile, tstride,
+                           idx, m, ai, v, fv);
+    return hipGetLastError();
+}
+
+template <int FMT>
+static hipError_t launch_tails_f(const RowTableNarrow& tab, int K, int64_t tile, int64_t tstride, const int64_t* idx,
+                                 int64_t m, const void* acc_in, void* vals, int fin, float fv, int grid, hipStream_t s) {
+    switch (fin) {
+        case FEDAVG_FIN_SCALE:
+            return launch_tails_a<FMT, FEDAVG_FIN_SCALE>(tab, K, tile, tstride, idx, m, acc_in, vals, fv, grid, s);
+        case FEDAVG_FIN_DIV:
+            return launch_tails_a<FMT, FEDAVG_FIN_DIV>(tab, K, tile, tstride, idx, m, acc_in, vals, fv, grid, s);
+        default:
+            return launch_tails_a<FMT, FEDAVG_FIN_NONE>(tab, K, tile, tstride, idx, m, acc_in, vals, fv, grid, s);
+    }
+}
+
+hipError_t launch_torch16_tails(const RowTableNarrow& tab, int K, int64_t tile, int64_t tstride, const int64_t* idx,
+                                int64_t m, const void* acc_in, void* vals, int fmt, int fin, float fin_val,
+                                hipStream_t s) {
+    const int grid = (int)((m + kBlock - 1) / kBlock);
+    if (grid == 0) return hipSuccess;
+    if (fmt == FEDAVG_BF16)
+        return launch_tails_f<FEDAVG_BF16>(tab, K, tile, tstride, idx, m, acc_in, vals, fin, fin_val, grid, s);
+    if (fmt == FEDAVG_F16)
+        return launch_tails_f<FEDAVG_F16>(tab, K, tile, tstride, idx, m, acc_in, vals, fin, fin_val, grid, s);
+    return hipErrorInvalidValue;
+}
+
+hipError_t launch_scatter16(const int64_t* idx, const void* vals, int64_t m, void* out, hipStream_t s) {
+    const int grid = (int)((m + kBlock - 1) / kBlock);
+    if (grid == 0) return hipSuccess;
+    hipLaunchKernelGGL(fedavg_scatter16, dim3(grid), dim3(kBlock), 0, s, idx, static_cast<const uint16_t*>(vals), m,
+                       static_cast<uint16_t*>(out));
+    return hipGetLastError();
+}
+
 template <int FMT, int OP, int FIN, bool ACC_IN>
 static hipError_t launch_n_v(const RowTableNarrow& tab, int K, const void* acc_in, void* out, int64_t n, float fv,
                              int grid, bool vec, hipStream_t s) {

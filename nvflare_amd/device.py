@@ -339,14 +339,21 @@ class DeviceContext:
 
     def accumulate_tiled16(self, fmt: int, bases: Sequence[int], weights: Sequence[float], tile: int, tile_stride: int,
                            begin: int, end: int, out_ptr: int, op: int, fin: int, count: float = 1.0,
-                           acc_in_ptr: Optional[int] = None) -> None:
+                           acc_in_ptr: Optional[int] = None, tails: Optional[np.ndarray] = None) -> None:
+        """fedavg_accumulate_tiled16(_tails): ``tails`` = sorted int64 flat indices taking torch's scalar-remainder
+        step (torch16.scalar_tail_indices), or None."""
         k = len(bases)
         b_arr = (ctypes.c_void_p * max(k, 1))(*bases)
         w_arr = (ctypes.c_double * max(k, 1))(*[float(w) for w in weights])
-        N.call("fedavg_accumulate_tiled16", self.handle, ctypes.c_int(fmt), b_arr, w_arr, ctypes.c_int(k),
-               ctypes.c_size_t(tile), ctypes.c_size_t(tile_stride), ctypes.c_size_t(begin), ctypes.c_size_t(end),
-               ctypes.c_void_p(acc_in_ptr or 0), ctypes.c_void_p(out_ptr), ctypes.c_int(op), ctypes.c_int(fin),
-               ctypes.c_double(float(count)))
+        args = (self.handle, ctypes.c_int(fmt), b_arr, w_arr, ctypes.c_int(k), ctypes.c_size_t(tile),
+                ctypes.c_size_t(tile_stride), ctypes.c_size_t(begin), ctypes.c_size_t(end),
+                ctypes.c_void_p(acc_in_ptr or 0), ctypes.c_void_p(out_ptr), ctypes.c_int(op), ctypes.c_int(fin),
+                ctypes.c_double(float(count)))
+        if tails is None or len(tails) == 0:
+            N.call("fedavg_accumulate_tiled16", *args)
+            return
+        t = np.ascontiguousarray(tails, dtype=np.int64)
+        N.call("fedavg_accumulate_tiled16_tails", *args, ctypes.c_void_p(t.ctypes.data), ctypes.c_size_t(t.size))
 
     def accumulate_tiled64(self, bases: Sequence[int], weights: Sequence[float], tile: int, tile_stride: int,
                            begin: int, end: int, out_ptr: int, op: int, fin: int, count: float = 1.0,

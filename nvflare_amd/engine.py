@@ -37,6 +37,7 @@ from typing import Any, Dict, List, Optional, Tuple
 import numpy as np
 
 from . import _native as N
+from . import torch16
 from .device import BF16_NP, DeviceBuffer, DeviceContext, HostArenaPool, TiledLayout, fedavg_dtype
 from .ingest import MappedTensor
 from .quantized import QuantizedPayload, stager
@@ -113,8 +114,9 @@ def _resolve_types(v, weight, weighted: bool) -> Tuple[str, np.dtype, np.dtype, 
         in_np = _TORCH_TO_NP[tdt]
         if in_np.kind in "iub":
             if not weighted:
-                # reference: v.clone() stays integer and div_(count) raises on an integer tensor
-                raise TypeError("nvflare_amd: integer tensors need weigh_by_local_iter=True (reference raises in div_)")
+                # reference: v.clone() stays integer, add_ keeps it, and get_result's div_(count) raises
+                # (weighted_aggregation_helper.py:186-187, :208-209, :233): the key is marked, not staged
+                return "torch", in_np, in_np, N.FEDAVG_OP_UNWEIGHTED, N.FEDAVG_FIN_DIV
             acc_np = _TORCH_TO_NP[torch.get_default_dtype()]
         else:
             acc_np = in_np
@@ -132,11 +134,11 @@ def _resolve_types(v, weight, weighted: bool) -> Tuple[str, np.dtype, np.dtype, 
             acc_np = np.result_type(in_np, 1.0)  # NEP 50: python float is weak
         op = N.FEDAVG_OP_NUMPY
     else:
-        if in_np.kind in "iub":
-            raise TypeError("nvflare_amd: integer arrays need weigh_by_local_iter=True")
         if isinstance(weight, np.generic):
             raise TypeError("nvflare_amd: numpy-scalar weights with weigh_by_local_iter=False change the result dtype; unsupported")
-        acc_np = in_np
+        # integer / bool arrays: an integer (bool: OR) sum in the array's dtype, float64 after the scaling
+        # (weighted_aggregation_helper.py:195-199, :214-215, :236)
+        acc_np = _F64 if in_np.kind in "iub" else in_np
         op = N.FEDAVG_OP_UNWEIGHTED
     acc_np = np.dtype(acc_np)
     ok = (acc_np == _F64 or (acc_np == _F32 and in_np in _ACC_F32_INPUTS) or (acc_np == _F16 and in_np == _F16))
@@ -225,13 +227,22 @@ class _Staged:
 
 
 _FLT_MAX = float(np.finfo(np.float32).max)
+_HALF_MAX = 65504.0
+# c10 scalar type names in torch's "result type Float can't be cast to the desired output type X"
+_TORCH_C10_NAMES = {np.dtype(np.int8): "Char", np.dtype(np.int16): "Short", np.dtype(np.int32): "Int",
+                    np.dtype(np.int64): "Long", np.dtype(np.uint8): "Byte", np.dtype(np.bool_): "Bool"}
+# torch totals whose add_ alpha c10 range-checks: (largest finite value, c10's type name in the message)
+_TORCH_ALPHA_LIMITS = {np.dtype(np.float32): (_FLT_MAX, "float"), np.dtype(np.float16): (_HALF_MAX, "c10::Half"),
+                       BF16_NP: (3.3895313892515355e38, "c10::BFloat16")}
 
 
 class _KeyState:
     __slots__ = ("name", "shape", "container", "torch_device", "in_np", "acc_np", "op", "fin", "n", "arena",
-                 "offset", "pending", "acc_valid", "acc_buf", "count", "done", "sig")
+                 "offset", "pending", "acc_valid", "acc_buf", "count", "done", "sig", "int_sum", "doomed")
 
     def __init__(self):
+        self.int_sum = False  # numpy integer / bool sum (weigh_by_local_iter=False): acc_buf holds in_np values
+        self.doomed = None  # torch integer total the reference's div_ rejects: c10 type name, nothing staged
         self.sig = None  # (dtype, type(weight), weighted) of plain numpy contributions already type-checked
         self.pending: List[_Staged] = []
         self.acc_valid = False
@@ -268,6 +279,7 @@ class DeviceFedAvg:
         self._round_clients = 0
         self.peak_clients = 0
         self._deferred = None  # DeferredRound still holding fp32 slots (result_deferred)
+        self._tails_cache: Dict[tuple, np.ndarray] = {}  # torch16 scalar-loop elements per run layout
         self.stats = {"h2d_bytes": 0, "folds": 0, "launches": 0, "slabs_allocated": 0}
 
     @property
@@ -380,17 +392,21 @@ class DeviceFedAvg:
     # ------------------------------------------------------------------ layout
     def _check_torch_alpha(self, items, weight, weighted: bool) -> None:
         """torch's ``T.add_(v, alpha=w)`` (weighted_aggregation_helper.py:205-207) refuses a finite alpha
-        outside the fp32 range for an fp32 total.  Raise the same RuntimeError, before anything of this
-        contribution is staged (the reference fails part-way through the keys instead)."""
+        outside the total's range (c10 ``checked_convert``: fp32, float16 65504, bfloat16).  Raise the same
+        RuntimeError, before anything of this contribution is staged (the reference fails part-way through the
+        keys instead)."""
         if not weighted:
             return
         w = float(weight)
-        if not (math.isfinite(w) and abs(w) > _FLT_MAX):
+        if not (math.isfinite(w) and abs(w) > _HALF_MAX):
             return
         for k, _ in items:
             st = self.keys.get(k)
-            if st is not None and st.container == "torch" and st.acc_np == np.dtype(np.float32):
-                raise RuntimeError("value cannot be converted to type float without overflow")
+            if st is None or st.container != "torch":
+                continue
+            limit = _TORCH_ALPHA_LIMITS.get(st.acc_np)
+            if limit is not None and abs(w) > limit[0]:
+                raise RuntimeError(f"value cannot be converted to type {limit[1]} without overflow")
 
     def _register_key(self, name: str, v, weight, weighted: bool) -> _KeyState:
         st = self.keys.get(name)
@@ -423,6 +439,11 @@ class DeviceFedAvg:
         st.n = int(np.prod(shape, dtype=np.int64)) if shape else 1
         if plain:
             st.sig = (v.dtype, type(weight), weighted)
+        if op == N.FEDAVG_OP_UNWEIGHTED and in_np.kind in "iub":
+            if container == "torch":
+                st.doomed = _TORCH_C10_NAMES[in_np]
+            else:
+                st.int_sum = True
         if in_np == acc_np and in_np in _ARENA_FORMATS:
             st.arena = self._arena(in_np)
             st.offset = st.arena.layout_elems
@@ -520,8 +541,8 @@ class DeviceFedAvg:
             for arena, arena_items in by_arena.values():
                 self._stage_arena(arena, arena_items, weight)
             for st, v in states:
-                if st.arena is not None or st.n == 0:
-                    if st.n == 0:
+                if st.arena is not None or st.n == 0 or st.doomed:
+                    if st.n == 0 and not st.doomed:
                         st.pending.append(_Staged(weight))
                     continue
                 buf = self.ctx.alloc(st.n * st.in_np.itemsize)
@@ -574,13 +595,16 @@ class DeviceFedAvg:
         count = float(first.count) if first.count is not None else 1.0
         if epi is not None and arena.fmt != N.FEDAVG_F32:
             raise TypeError("nvflare_amd: server-optimizer epilogues run on fp32 keys only")
+        tails = None
+        if first.op == N.FEDAVG_OP_TORCH and arena.fmt in (N.FEDAVG_F16, N.FEDAVG_BF16):
+            tails = self._torch16_tails(group)
 
         def launch(bases, weights, tile, stride, fin_, last_launch):
             if arena.fmt == N.FEDAVG_F64:
                 self.ctx.accumulate_tiled64(bases, weights, tile, stride, begin, end, out, first.op, fin_, count, acc_in)
             elif arena.fmt != N.FEDAVG_F32:
                 self.ctx.accumulate_tiled16(arena.fmt, bases, weights, tile, stride, begin, end, out, first.op, fin_,
-                                            count, acc_in)
+                                            count, acc_in, tails=tails)
             elif epi is not None and last_launch:
                 self.ctx.accumulate_tiled_epi(bases, weights, tile, stride, begin, end, out, first.op, fin_, count,
                                               epi, acc_in)
@@ -606,6 +630,15 @@ class DeviceFedAvg:
             launch([p.slot.base for p in seg], [p.weight for p in seg], lay.tile, lay.tile_stride,
                    fin if last_launch else N.FEDAVG_FIN_NONE, last_launch)
             acc_in = out
+
+    def _torch16_tails(self, group: List[_KeyState]) -> np.ndarray:
+        """Flat indices of the group's elements that torch's add_ runs through its scalar loop (torch16.py),
+        for the thread count and vector build of this process -- where the reference would run."""
+        sig = (tuple((st.offset, st.n) for st in group), torch16.torch_threads(), torch16.vector_block())
+        hit = self._tails_cache.get(sig)
+        if hit is None:
+            hit = self._tails_cache[sig] = torch16.scalar_tail_indices(sig[0], sig[1], sig[2])
+        return hit
 
     def _launch_arena(self, final: bool, keys: Optional[Dict[str, _KeyState]] = None,
                       out: Optional[int] = None, arenas: Optional[List[_Arena]] = None) -> None:
@@ -644,9 +677,12 @@ class DeviceFedAvg:
 
     def _launch_side(self, final: bool) -> None:
         for st in self.keys.values():
-            if st.arena is not None or st.n == 0:
+            if st.arena is not None or st.n == 0 or st.doomed or st.done:
                 continue
             if not st.pending and not (final and st.acc_valid):
+                continue
+            if st.int_sum:
+                self._launch_int_sum(st, final)
                 continue
             if st.acc_buf is None:
                 st.acc_buf = self.ctx.alloc(st.n * st.acc_np.itemsize)
@@ -665,6 +701,27 @@ class DeviceFedAvg:
             self.stats["launches"] += 1
             st.pending = []
             st.acc_valid = True
+
+    def _launch_int_sum(self, st: _KeyState, final: bool) -> None:
+        """numpy integer / bool arrays with weigh_by_local_iter=False: the running sum stays in the array's
+        dtype (wraparound; OR for bool); the final launch turns it into float64(T) * (1.0 / count) (:236)."""
+        if st.acc_buf is None:
+            st.acc_buf = self.ctx.alloc(st.n * st.in_np.itemsize)
+        if st.pending or not st.acc_valid:
+            self.ctx.accumulate([p.buf.ptr for p in st.pending], [p.weight for p in st.pending], st.n, st.acc_buf.ptr,
+                                st.in_dt, st.in_dt, N.FEDAVG_OP_UNWEIGHTED, N.FEDAVG_FIN_NONE, 1.0,
+                                acc_in_ptr=st.acc_buf.ptr if st.acc_valid else None)
+            self.stats["launches"] += 1
+            st.pending = []
+            st.acc_valid = True
+        if final:
+            ints, st.acc_buf = st.acc_buf, self.ctx.alloc(st.n * 8)
+            self.ctx.accumulate([ints.ptr], [1.0 / float(st.count)], st.n, st.acc_buf.ptr, st.in_dt, N.FEDAVG_F64,
+                                N.FEDAVG_OP_NUMPY, N.FEDAVG_FIN_NONE, 1.0)
+            self.ctx.sync()
+            ints.close()
+            st.done = True
+            self.stats["launches"] += 1
 
     def _fold(self) -> None:
         """Fold pending contributions into the device accumulators (bitwise-neutral) and free slots."""
@@ -713,8 +770,16 @@ class DeviceFedAvg:
         return bool(a.layout_elems) and any(st.arena is a and st.n > 0 and st.torch_device is None
                                             for st in self.keys.values())
 
+    def _check_doomed(self) -> None:
+        """torch integer totals under weigh_by_local_iter=False: the reference's get_result fails at the first
+        such key's ``div_`` (weighted_aggregation_helper.py:233); so does this one, before any launch."""
+        for st in self.keys.values():
+            if st.doomed:
+                raise RuntimeError(f"result type Float can't be cast to the desired output type {st.doomed}")
+
     def result(self) -> Dict[str, Any]:
         """Finalise every key on the device and return host (or device-tensor) results."""
+        self._check_doomed()
         with self.lock, self.ctx.lock:
             self._settle()
             # the largest host-bound arena leaves in a pipelined D2H that overlaps its own launches
@@ -737,6 +802,7 @@ class DeviceFedAvg:
         settled: by the fused step, by a materialisation, or by the next ``add`` / ``result``."""
         from .deferred import DeferredAggregate, DeferredRound
 
+        self._check_doomed()
         with self.lock, self.ctx.lock:
             self._settle()
             others = [a for a in self.arenas.values() if a.fmt != N.FEDAVG_F32]
@@ -823,6 +889,7 @@ class DeviceFedAvg:
                     st.acc_buf.close()
             self._consolidate()
             self.keys.clear()
+            self._tails_cache.clear()
             for a in self.arenas.values():
                 a.layout_elems = 0
 

@@ -197,6 +197,58 @@ def f32_to_bf16_bits(x) -> np.ndarray:
     return (bf16_round(x).view(np.uint32) >> 16).astype(np.uint16)
 
 
+def torch16_scalar_mask(n: int, threads: int = 1, grain: int = 32768, block: int = 32) -> np.ndarray:
+    """Elements of an n-element float16 / bfloat16 ``add_`` that torch CPU runs through its scalar loop
+    (third-party torch 2.x, restated): TensorIteratorBase::for_each keeps tensors below ``grain`` (and
+    single-thread runs) in one range, else at::parallel_for (ATen/ParallelOpenMP.h) cuts [0, n) into ranges of
+    ceil(n / min(threads, ceil(n / grain))) elements; cpu_kernel_vec's vectorized_loop (ATen/native/cpu/Loops.h)
+    covers each range in blocks of ``block`` elements (2 vectors; 32 on the AVX2 / AVX512 builds) and leaves
+    the last (length mod block) to basic_loop.  block 0: no vector kernel (every element scalar)."""
+    mask = np.zeros(n, dtype=bool)
+    if n <= 0:
+        return mask
+    if n < grain or threads <= 1:
+        ranges = [(0, n)]
+    else:
+        nt = min(threads, -(-n // grain))
+        chunk = -(-n // nt)
+        ranges = [(b, min(b + chunk, n)) for b in range(0, n, chunk)]
+    for b, e in ranges:
+        mask[(b if block <= 0 else b + (e - b) // block * block):e] = True
+    return mask
+
+
+def torch16_reference(rows, weights, fmt: str, weighted: bool = True, count: Optional[float] = None,
+                      threads: int = 1, block: int = 32, mask: Optional[np.ndarray] = None):
+    """torch branch for ``fmt`` tensors (weighted_aggregation_helper.py:181-187, :203-209, :233) as torch CPU
+    computes it, both loops: ``torch16_vector_reference`` on the vectorised elements, and on the elements of
+    ``torch16_scalar_mask`` the scalar loop's c10::Half / c10::BFloat16 add_ step
+        T = r(T + r(v * r(float32(w))))        (operator* and operator+ round to the format)
+    (mul and div_ compute the same in both loops).  ``mask`` overrides the scalar elements."""
+    rows = [np.asarray(v, dtype=np.float32) for v in rows]
+    if mask is None:
+        mask = torch16_scalar_mask(rows[0].size if rows else 0, threads, block=block)
+    with np.errstate(over="ignore", invalid="ignore"):
+        total, c = None, None
+        for v, w in zip(rows, weights):
+            if total is None:
+                total = round16(v * np.float32(w), fmt) if weighted else v.copy()
+                c = w
+            else:
+                if weighted:
+                    a = round16(np.float32(w), fmt)
+                    vec = round16((v.astype(np.float64) * np.float64(a) + total.astype(np.float64)).astype(np.float32),
+                                  fmt)
+                    sc = round16(total + round16(v * np.float32(a), fmt), fmt)
+                    total = np.where(mask, sc, vec)
+                else:
+                    total = round16(total + v, fmt)
+                c = c + w
+        if count is not None:
+            c = count
+        return round16(total / np.float32(c), fmt)
+
+
 def torch16_vector_reference(rows, weights, fmt: str, weighted: bool = True, count: Optional[float] = None):
     """torch branch for ``fmt`` tensors (weighted_aggregation_helper.py:181-187, :203-209, :233), as torch
     CPU's vectorised kernels compute it.  ``rows``: fp32 arrays holding ``fmt`` values; returns fp32 values

@@ -139,8 +139,9 @@ class FakeDeviceContext:
 
     # -- compute --------------------------------------------------------------------------------------
     @staticmethod
-    def _agg(rows, weights, op, fin, count, acc_in, fmt=None):
-        """The kernels' per-element sequence (oracle restatements).  rows: fp32 / fp16 / fp64 arrays."""
+    def _agg(rows, weights, op, fin, count, acc_in, fmt=None, scalar=None):
+        """The kernels' per-element sequence (oracle restatements).  rows: fp32 / fp16 / fp64 arrays.
+        ``scalar``: bool mask of 16-bit elements that take torch's scalar-loop step (torch mode)."""
         if fmt is not None:  # 16-bit totals (fmt "float16" | "bfloat16"); rows/acc_in are fp32 values
             if op == N.FEDAVG_OP_NUMPY:
                 t = None if acc_in is None else acc_in.astype(np.float16)
@@ -157,7 +158,11 @@ class FakeDeviceContext:
                     t = orc.round16(r * np.float32(w), fmt) if weighted else r.copy()
                 elif weighted:
                     a = np.float64(orc.round16(np.float32(w), fmt))
-                    t = orc.round16((r.astype(np.float64) * a + t.astype(np.float64)).astype(np.float32), fmt)
+                    vec = orc.round16((r.astype(np.float64) * a + t.astype(np.float64)).astype(np.float32), fmt)
+                    if scalar is not None:
+                        sc = orc.round16(t + orc.round16(r * np.float32(a), fmt), fmt)
+                        vec = np.where(scalar, sc, vec)
+                    t = vec
                 else:
                     t = orc.round16(t + r, fmt)
             if fin == N.FEDAVG_FIN_DIV:
@@ -167,10 +172,16 @@ class FakeDeviceContext:
             return t
         mode = orc.MODE_TORCH if op == N.FEDAVG_OP_TORCH else orc.MODE_NUMPY
         acc_t = rows[0].dtype if rows else acc_in.dtype
+        if acc_t in (np.float32, np.float64):  # the C restatement: torch steps are one correctly rounded fma
+            fin_c = {N.FEDAVG_FIN_SCALE: orc.FIN_NUMPY_SCALE, N.FEDAVG_FIN_DIV: orc.FIN_TORCH_DIV}.get(fin, orc.FIN_NONE)
+            if not rows:
+                return orc.fedavg_c([], [], mode, fin=fin_c, count=count, acc_in=acc_in)
+            return orc.fedavg_c([np.ascontiguousarray(r, dtype=acc_t) for r in rows], weights, mode,
+                                weighted=op != N.FEDAVG_OP_UNWEIGHTED, fin=fin_c, count=count, acc_in=acc_in)
         t = None if acc_in is None else acc_in.copy()
         with np.errstate(all="ignore"):
             for r, w in zip(rows, weights):
-                wv = acc_t.type(w)
+                wv = acc_t.type(w) if op != N.FEDAVG_OP_UNWEIGHTED else None
                 r = r.astype(acc_t)
                 if t is None:
                     t = r * wv if op != N.FEDAVG_OP_UNWEIGHTED else r.copy()
@@ -207,7 +218,7 @@ class FakeDeviceContext:
         self._view(out_ptr + begin * 4, (end - begin) * 4)[:] = res.astype(np.float32).view(np.uint8)
 
     def accumulate_tiled16(self, fmt, bases, weights, tile, stride, begin, end, out_ptr, op, fin, count=1.0,
-                           acc_in_ptr=None):
+                           acc_in_ptr=None, tails=None):
         self.launches.append(("tiled16", len(bases), begin, end))
         name = "bfloat16" if fmt == N.FEDAVG_BF16 else "float16"
 
@@ -216,7 +227,14 @@ class FakeDeviceContext:
 
         rows = [vals(self._read_tiled(b, tile, stride, begin, end, 2, np.uint16)) for b in bases]
         acc = None if acc_in_ptr is None else vals(self._view(acc_in_ptr + begin * 2, (end - begin) * 2).view(np.uint16).copy())
-        res = self._agg(rows, weights, op, fin, count, acc, fmt=name)
+        scalar = None
+        if tails is not None and op == N.FEDAVG_OP_TORCH:
+            t = np.asarray(tails, dtype=np.int64)
+            t = t[(t >= begin) & (t < end)]
+            if t.size:
+                scalar = np.zeros(end - begin, dtype=bool)
+                scalar[t - begin] = True
+        res = self._agg(rows, weights, op, fin, count, acc, fmt=name, scalar=scalar)
         bits = orc.f32_to_bf16_bits(res) if name == "bfloat16" else res.astype(np.float16).view(np.uint16)
         self._view(out_ptr + begin * 2, (end - begin) * 2)[:] = bits.view(np.uint8)
 

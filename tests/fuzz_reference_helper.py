@@ -1,0 +1,212 @@
+"""Randomised parity of the drop-in ``WeightedAggregationHelper`` against the REFERENCE helper itself --
+TEST INFRASTRUCTURE, run as a subprocess by tests/test_cpu_fuzz_reference.py in the build container (the
+reference tree mounted at NVFLARE_REF_ROOT; nothing of it is copied).
+
+The reference helper (weighted_aggregation_helper.py:117-240, imported through the same namespace shim as
+tests/ref_suite_plugin.py) and the drop-in helper on tests/fake_device.FakeDeviceContext (the kernels'
+per-element sequences restated by the oracle) get the same random contributions: client counts, key subsets
+per client, 0-d / empty / ragged / tile-crossing shapes, numpy and torch containers, float32 / float64 /
+float16 / bfloat16 / integer / bool values, odd weights, ``weigh_by_local_iter``, ``exclude_vars``, tiny HBM
+budgets (folding) and small slabs (chaining), two rounds per helper.  Every result must match the reference's:
+keys and their order, container, dtype, shape and bits (NaN payloads aside).
+
+  python tests/fuzz_reference_helper.py --cases 300 --seed 1
+"""
+
+import argparse
+import json
+import os
+import sys
+
+sys.dont_write_bytecode = True
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+sys.path.insert(0, os.path.dirname(HERE))
+
+import numpy as np  # noqa: E402
+
+
+def _setup():
+    from ref_suite_plugin import _install_shim
+
+    _install_shim(os.environ["NVFLARE_REF_ROOT"])
+    import nvflare_amd.compat as compat
+    import nvflare_amd.device as device
+    from fake_device import FakeDeviceContext
+
+    assert compat.HAVE_NVFLARE
+    fake = FakeDeviceContext()
+    device.DeviceContext.get = classmethod(lambda cls, d=None: fake)
+    from nvflare.app_common.aggregators.weighted_aggregation_helper import WeightedAggregationHelper as Ref
+
+    from nvflare_amd.app_common.aggregators.weighted_aggregation_helper import WeightedAggregationHelper as Mine
+
+    return Ref, Mine, fake
+
+
+SHAPES = [(), (0,), (1,), (3,), (7, 5), (4095,), (4096,), (4097,), (2, 4100), (9000,), (70001,)]
+NP_DTYPES = ["float32", "float32", "float32", "float64", "float16", "int32", "int64", "uint8", "bool"]
+TORCH_DTYPES = ["float32", "float32", "float32", "float64", "float16", "bfloat16", "int32", "int64", "bool"]
+
+
+def _value(rng, shape, dt, container):
+    import torch
+
+    if dt == "bool":
+        a = rng.random(shape) < 0.5
+    elif dt in ("int32", "int64", "uint8"):
+        lo = 0 if dt == "uint8" else -1000
+        a = rng.integers(lo, 1000 if dt != "uint8" else 256, size=shape).astype(dt)
+    else:
+        a = rng.standard_normal(shape) * float(rng.choice([1.0, 1e-3, 1e3]))
+        if rng.random() < 0.2 and a.size:
+            flat = a.reshape(-1)
+            flat[rng.integers(0, flat.size)] = rng.choice([0.0, -0.0, 1e-40, np.inf, -np.inf, np.nan, 6e4])
+        a = a.astype("float32" if dt == "bfloat16" else dt)
+    if container == "torch":
+        t = torch.from_numpy(np.array(a, copy=True))
+        return t.to(torch.bfloat16) if dt == "bfloat16" else t
+    return np.array(a, copy=True)
+
+
+def _weight(rng):
+    kind = rng.integers(0, 4)
+    if kind == 0:
+        return float(rng.integers(1, 100))
+    if kind == 1:
+        return float(rng.random() * 10)
+    if kind == 2:
+        return float(rng.choice([1e-6, 0.5, 3.0, 1e6]))
+    return float(rng.random()) * float(rng.integers(1, 50))
+
+
+def _copy(v):
+    import torch
+
+    return v.clone() if isinstance(v, torch.Tensor) else np.array(v, copy=True)
+
+
+def _same(a, b) -> str:
+    import torch
+
+    if type(a) is not type(b) and not (isinstance(a, np.generic) or isinstance(b, np.generic)):
+        if not (isinstance(a, torch.Tensor) and isinstance(b, torch.Tensor)):
+            return f"type {type(a).__name__} vs {type(b).__name__}"
+    if isinstance(a, torch.Tensor):
+        if a.dtype != b.dtype or tuple(a.shape) != tuple(b.shape):
+            return f"torch {a.dtype}{tuple(a.shape)} vs {b.dtype}{tuple(b.shape)}"
+        if a.dtype == torch.bfloat16:  # bits as int16, NaNs (any payload) from the float values
+            an, bn = torch.isnan(a).numpy(), torch.isnan(b).numpy()
+            if not np.array_equal(an, bn):
+                return "nan positions"
+            a, b = a.view(torch.int16).numpy()[~an], b.view(torch.int16).numpy()[~bn]
+        else:
+            a, b = a.numpy(), b.numpy()
+    a, b = np.asarray(a), np.asarray(b)
+    if a.dtype != b.dtype or a.shape != b.shape:
+        return f"numpy {a.dtype}{a.shape} vs {b.dtype}{b.shape}"
+    if a.dtype.kind == "f":
+        an, bn = np.isnan(a), np.isnan(b)
+        if not np.array_equal(an, bn):
+            return "nan positions"
+        a, b = a[~an], b[~bn]
+    fa, fb = a.reshape(-1), b.reshape(-1)
+    if not np.array_equal(fa.view(np.uint8), fb.view(np.uint8)):
+        diff = np.nonzero(fa != fb)[0] if fa.dtype.kind != "b" else np.nonzero(fa ^ fb)[0]
+        i = int(diff[0]) if diff.size else -1
+        return f"bits ({diff.size} of {fa.size} differ; first at {i}: {fa[i]!r} vs {fb[i]!r})"
+    return ""
+
+
+def run(cases: int, seed: int, threads: int) -> dict:
+    import torch
+
+    torch.set_num_threads(threads)  # torch's 16-bit add_ splits tensors of 32768+ elements over the threads
+    Ref, Mine, fake = _setup()
+    rng = np.random.default_rng(seed)
+    stats = {"cases": 0, "rounds": 0, "keys": 0, "errors": 0, "mismatches": [], "launches": 0}
+    for case in range(cases):
+        container = "torch" if rng.random() < 0.5 else "numpy"
+        nkeys = int(rng.integers(1, 6))
+        keys = {}
+        for j in range(nkeys):
+            dt = str(rng.choice(TORCH_DTYPES if container == "torch" else NP_DTYPES))
+            keys[f"layer{j}.{dt}"] = (SHAPES[int(rng.integers(0, len(SHAPES)))], dt)
+        weigh = bool(rng.random() < 0.85)
+        exclude = str(rng.choice(["", "layer1", "bool|int"])) if rng.random() < 0.3 else None
+        budget = int(rng.choice([0, 1, 50_000])) if rng.random() < 0.3 else None
+        slots = str(int(rng.choice([2, 3]))) if rng.random() < 0.3 else None
+        if slots:
+            os.environ["NVFLARE_AMD_SLAB_SLOTS"] = slots
+        else:
+            os.environ.pop("NVFLARE_AMD_SLAB_SLOTS", None)
+        ref = Ref(exclude_vars=exclude, weigh_by_local_iter=weigh)
+        mine = Mine(exclude_vars=exclude, weigh_by_local_iter=weigh, max_resident_bytes=budget)
+        for rnd in range(2):
+            K = int(rng.integers(1, 13))
+            for k in range(K):
+                data = {n: _value(rng, s, dt, container) for n, (s, dt) in keys.items() if rng.random() < 0.8}
+                w = _weight(rng)
+                try:
+                    ref.add(data={n: _copy(v) for n, v in data.items()}, weight=w, contributor_name=f"c{k}",
+                            contribution_round=rnd)
+                except Exception as e:  # e.g. torch refusing alpha=1e6 for a float16 total
+                    err = e
+                else:
+                    err = None
+                try:
+                    mine.add(data=data, weight=w, contributor_name=f"c{k}", contribution_round=rnd)
+                except Exception as e:
+                    if err is None or type(e) is not type(err):
+                        stats["mismatches"].append(f"case {case}: drop-in raised {e!r}, reference {err!r}")
+                    stats["errors"] += 1
+                    break  # the reference fails part-way through a contribution: states differ from here
+                if err is not None:
+                    stats["mismatches"].append(f"case {case}: reference raised {err!r}, drop-in did not")
+                    break
+            else:
+                err = None
+            if err is not None:
+                break
+            tag = f"case {case} round {rnd} ({container}, weigh={weigh}, exclude={exclude!r}, budget={budget}, slots={slots})"
+            try:
+                r_ref = ref.get_result()
+            except Exception as e:  # e.g. torch's div_ refusing an integer total (weigh_by_local_iter=False)
+                err = e
+            try:
+                r_mine = mine.get_result()
+            except Exception as e:
+                if err is None or type(e) is not type(err):
+                    stats["mismatches"].append(f"{tag}: drop-in get_result raised {e!r}, reference {err!r}")
+                stats["errors"] += 1
+                break
+            if err is not None:
+                stats["mismatches"].append(f"{tag}: reference get_result raised {err!r}, drop-in did not")
+                break
+            if list(r_ref) != list(r_mine):
+                stats["mismatches"].append(f"{tag}: keys {list(r_ref)} vs {list(r_mine)}")
+                continue
+            for n in r_ref:
+                why = _same(r_ref[n], r_mine[n])
+                if why:
+                    stats["mismatches"].append(f"{tag} key {n}: {why}")
+            stats["keys"] += len(r_ref)
+            stats["rounds"] += 1
+        stats["cases"] += 1
+    stats["launches"] = len(fake.launches)
+    return stats
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--cases", type=int, default=200)
+    ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--threads", type=int, default=3)
+    a = ap.parse_args()
+    stats = run(a.cases, a.seed, a.threads)
+    print(json.dumps({**stats, "mismatches": stats["mismatches"][:20], "n_mismatches": len(stats["mismatches"])}))
+    sys.exit(1 if stats["mismatches"] else 0)
+
+
+if __name__ == "__main__":
+    main()

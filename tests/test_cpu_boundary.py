@@ -167,8 +167,38 @@ def test_unsupported_dtypes_raise():
         _resolve_types(np.ones(3, np.complex64), 1.0, True)
     with pytest.raises(TypeError):
         _resolve_types(torch.ones(3, dtype=torch.complex64), 1.0, True)
-    with pytest.raises(TypeError):
-        _resolve_types(torch.ones(3, dtype=torch.int64), 1.0, False)
+    # weigh_by_local_iter=False integer values: numpy sums in the array dtype then scales to float64; torch keeps
+    # an integer total whose div_ raises at get_result (the engine raises the same RuntimeError there)
+    from nvflare_amd import _native as N
+
+    assert _resolve_types(np.ones(3, np.int32), 1.0, False)[2:4] == (np.dtype(np.float64), N.FEDAVG_OP_UNWEIGHTED)
+    assert _resolve_types(torch.ones(3, dtype=torch.int64), 1.0, False)[2] == np.dtype(np.int64)
+
+
+def test_unweighted_integers_on_the_fake_device():
+    """numpy integer / bool sums wrap (bool: OR) and scale to float64 as numpy does; a torch integer key makes
+    result() raise torch's div_ RuntimeError, as the reference's get_result does."""
+    from fake_device import fake_engine
+
+    e = fake_engine(max_resident_bytes=1)  # folds after every contribution: the sum continues through acc_in
+    vals = {"i8": [np.array([100, -100, 7], np.int8), np.array([100, -100, 9], np.int8), np.array([1, 2, 3], np.int8)],
+            "b": [np.array([True, False, False]), np.array([True, True, False]), np.array([False, False, False])],
+            "u64": [np.array([2**63, 5], np.uint64)] * 3}
+    ws = [1.0, 2.5, 0.25]
+    for k in range(3):
+        e.add([(n, v[k]) for n, v in vals.items()], ws[k], False)
+    out = e.result()
+    c = ws[0] + ws[1] + ws[2]
+    for n, v in vals.items():
+        t = v[0].copy()
+        for x in v[1:]:
+            t = t + x
+        exp = t * (1.0 / c)
+        assert out[n].dtype == np.float64 and np.array_equal(out[n], exp), n
+    e2 = fake_engine()
+    e2.add([("f", torch.ones(3)), ("n", torch.ones(2, dtype=torch.int32))], 1.0, False)
+    with pytest.raises(RuntimeError, match="desired output type Int"):
+        e2.result()
 
 
 # --- compat stand-ins ----------------------------------------------------------------------------------------

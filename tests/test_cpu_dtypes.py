@@ -4,10 +4,10 @@ produced by running weighted_aggregation_helper.py:153-240 itself, make_golden.p
 * numpy containers (float16 and every integer / bool dtype; python-float and numpy-scalar weights): the
   numpy-op restatement is bit-exact everywhere.
 * torch integer / bool tensors: the torch-op restatement is bit-exact.
-* torch float16 / bfloat16: ``torch16_vector_reference`` (fp32 ops with a 16-bit rounding after each
-  library operation) is bit-exact on every element torch computes on its vectorised path; on torch's
-  scalar tail (``vector_end`` .. n) the reference rounds the add_ product separately, and the restatement
-  stays within ``torch16_tail_tolerance``."""
+* torch float16 / bfloat16: ``torch16_reference`` (fp32 ops with a 16-bit rounding after each library
+  operation on the vectorised elements; on torch's scalar tail -- ``vector_end`` .. n at the one torch thread
+  the fixtures were made with -- the add_ product and sum rounded separately) is bit-exact on every element.
+  The vector-only restatement stays within ``torch16_tail_tolerance`` on that tail."""
 
 import numpy as np
 import pytest
@@ -44,9 +44,12 @@ def test_oracle_matches_reference_dtypes(name, case):
         assert same_bits(got.numpy(), exp_bits)
         return
     rows_f32 = [as_f32_values(r, dt) for r in rows]
-    got = orc.torch16_vector_reference(rows_f32, ws, dt, weighted=case["weighted"])
     exp = as_f32_values(exp_bits, dt)
     ve = case["vector_end"]
+    if case["weighted"]:
+        assert ve == orc.torch16_scalar_mask(exp.size).argmax() or not orc.torch16_scalar_mask(exp.size).any(), name
+    assert same_bits(orc.torch16_reference(rows_f32, ws, dt, weighted=case["weighted"]), exp), name
+    got = orc.torch16_vector_reference(rows_f32, ws, dt, weighted=case["weighted"])
     assert same_bits(got[:ve], exp[:ve]), name
     tol = torch16_tail_tolerance([r[ve:] for r in rows_f32], ws, exp[ve:], dt)
     d = np.abs(got[ve:].astype(np.float64) - exp[ve:].astype(np.float64))

@@ -1,0 +1,32 @@
+"""Randomised parity against the REFERENCE helper itself (tests/fuzz_reference_helper.py, in a subprocess with
+the reference tree mounted): the drop-in WeightedAggregationHelper on the fake device -- the engine's host logic
+with the kernels' per-element sequences restated by the oracle -- gives the reference's keys, key order,
+containers, dtypes, shapes and bits on random rounds (client counts, partial keys, 0-d / empty / ragged /
+multi-tile / 70001-element shapes, numpy and torch, float32 / float64 / float16 / bfloat16 / integer / bool,
+odd weights, weigh_by_local_iter, exclude_vars, HBM budgets that force folds, small slabs, torch threads 1 and
+4), and raises the reference's exception type where the reference raises.  Skipped where the reference tree
+is absent (the GPU box)."""
+
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+REF = os.environ.get("NVFLARE_REF_ROOT", "/root/reference")
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+@pytest.mark.skipif(not os.path.exists(os.path.join(REF, "nvflare")), reason="reference tree not mounted")
+@pytest.mark.parametrize("seed,threads", [(11, 1), (12, 4)])
+def test_random_rounds_match_reference(tmp_path, seed, threads):
+    env = dict(os.environ, NVFLARE_REF_ROOT=REF, PYTHONDONTWRITEBYTECODE="1")
+    env.pop("NVFLARE_AMD_FORCE_STANDINS", None)
+    proc = subprocess.run([sys.executable, os.path.join(HERE, "fuzz_reference_helper.py"), "--cases", "120",
+                           "--seed", str(seed), "--threads", str(threads)], cwd=str(tmp_path), env=env,
+                          capture_output=True, text=True, timeout=600)
+    line = proc.stdout.strip().splitlines()[-1] if proc.stdout.strip() else "{}"
+    stats = json.loads(line)
+    assert proc.returncode == 0 and stats.get("n_mismatches") == 0, (stats, proc.stderr[-2000:])
+    assert stats["cases"] == 120 and stats["rounds"] > 150 and stats["keys"] > 400 and stats["launches"] > 0

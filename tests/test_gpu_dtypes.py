@@ -1,9 +1,10 @@
 """GPU parity for float16 / bfloat16 / integer / bool client arrays.
 
-1. The drop-in helper on the reference's own outputs (tests/golden/dtype_cases.*): bit-exact for numpy
-   float16 and every integer / bool case (numpy and torch); torch float16 / bfloat16 bit-exact on the
-   elements torch computes on its vectorised path, within ``torch16_tail_tolerance`` on torch's scalar tail
-   (see tests/test_cpu_dtypes.py -- the oracle shows the same split).
+1. The drop-in helper on the reference's own outputs (tests/golden/dtype_cases.*): bit-exact on every element
+   of every case -- numpy float16, every integer / bool case (numpy and torch), and torch float16 / bfloat16
+   including torch's scalar-loop tail, which the engine recomputes with that loop's two roundings
+   (nvflare_amd/torch16.py, fedavg_accumulate_tiled16_tails) for the one torch thread the fixtures were made
+   with.
 2. The 16-bit kernel through the C-ABI against the oracle, bit-exact on EVERY element: both formats, all
    ops, K up to 131 (chained launches), ragged n, unaligned rows (per-element path), acc_in continuation.
 3. Device-resident bfloat16 tensors in, device tensor out."""
@@ -18,7 +19,6 @@ from golden_util import (
     dtype_case_weights,
     load_dtype_golden,
     same_bits,
-    torch16_tail_tolerance,
 )
 from oracle import fedavg_oracle as orc
 
@@ -37,7 +37,12 @@ def test_helper_dtype_golden(name, case):
     h = WeightedAggregationHelper(weigh_by_local_iter=case["weighted"])
     for k, (r, w) in enumerate(zip(rows, ws)):
         h.add({"w": r}, w, f"site-{k}", 0)
-    got = h.get_result()["w"]
+    threads = torch.get_num_threads()
+    torch.set_num_threads(1)  # the fixtures' torch thread count (the tails follow this process's setting)
+    try:
+        got = h.get_result()["w"]
+    finally:
+        torch.set_num_threads(threads)
     dt = case["dtype"]
     exp_bits = ARRAYS[case["expected"]]
     if case["container"] == "torch":
@@ -50,12 +55,7 @@ def test_helper_dtype_golden(name, case):
         assert same_bits(g, exp_bits), name
         return
     g, exp = as_f32_values(got, dt), as_f32_values(exp_bits, dt)
-    ve = case["vector_end"]
-    assert same_bits(g[:ve], exp[:ve]), name
-    rows_f32 = [as_f32_values(r, dt)[ve:] for r in rows]
-    tol = torch16_tail_tolerance(rows_f32, ws, exp[ve:], dt)
-    d = np.abs(g[ve:].astype(np.float64) - exp[ve:].astype(np.float64))
-    assert np.all((d <= tol) | (np.isnan(g[ve:]) & np.isnan(exp[ve:])) | (g[ve:] == exp[ve:])), name
+    assert same_bits(g, exp), name
 
 
 @pytest.fixture(scope="module")
@@ -206,6 +206,79 @@ def test_tiled16_vs_oracle(ctx, fmt, mode, K, slots, begin, end):
         assert same_bits(_vals(got[begin:end], fmt), exp)
     slab.close()
     out.close()
+
+
+@pytest.mark.parametrize("fmt", ["bfloat16", "float16"])
+@pytest.mark.parametrize("K", [5, 131])
+def test_tiled16_tails_vs_oracle(ctx, fmt, K):
+    """fedavg_accumulate_tiled16_tails: listed elements take torch's scalar-loop step (recomputed before the
+    tile kernel, written over its results after it), chained past 128 clients and through acc_in in place."""
+    from nvflare_amd import _native as N
+    from nvflare_amd.device import TiledLayout
+
+    begin, end = 8 * 37, 3 * 4096 + 8 * 11
+    n = (end + 4095) // 4096 * 4096
+    rng = np.random.default_rng(K)
+    rows = [_bits((rng.standard_normal(n) * 40).astype(np.float32), fmt) for _ in range(K)]
+    ws = [float(rng.random() * 20 + 1e-3) for _ in range(K)]
+    vals = [_vals(r[begin:end], fmt) for r in rows]
+    mask = np.zeros(end - begin, bool)
+    mask[rng.choice(end - begin, 200, replace=False)] = True
+    mask[-31:] = True
+    mask[4096 - begin - 5:4096 - begin + 9] = True  # across a tile boundary
+    tails = np.concatenate([[0, begin - 8], np.nonzero(mask)[0] + begin, [end, n - 1]]).astype(np.int64)  # out of range ignored
+    exp = orc.torch16_reference(vals, ws, fmt, mask=mask)
+    assert not same_bits(exp, orc.torch16_vector_reference(vals, ws, fmt))  # the tails matter here
+    code = N.FEDAVG_BF16 if fmt == "bfloat16" else N.FEDAVG_F16
+    lay = TiledLayout(4096, 8)
+    slab = ctx.alloc(lay.slab_elems(n) * 2 * -(-K // 8))
+    per = lay.slab_elems(n)
+    bases = [slab.ptr + ((k // 8) * per + lay.slot_offset_elems(k % 8)) * 2 for k in range(K)]
+    for b, r in zip(bases, rows):
+        ctx.h2d_tiled(b, 4096 * 2, lay.tile_stride * 2, 0, r.ctypes.data, r.nbytes)
+    out = ctx.alloc(n * 2)
+    ctx.accumulate_tiled16(code, bases, ws, 4096, lay.tile_stride, begin, end, out.ptr, N.FEDAVG_OP_TORCH,
+                           N.FEDAVG_FIN_DIV, _count(ws), tails=tails)
+    got = np.empty(n, np.uint16)
+    ctx.d2h(got, out.ptr)
+    assert same_bits(_vals(got[begin:end], fmt), exp)
+    ctx.accumulate_tiled16(code, bases[:2], ws[:2], 4096, lay.tile_stride, begin, end, out.ptr, N.FEDAVG_OP_TORCH,
+                           N.FEDAVG_FIN_NONE, 1.0, tails=tails)
+    ctx.accumulate_tiled16(code, bases[2:], ws[2:], 4096, lay.tile_stride, begin, end, out.ptr, N.FEDAVG_OP_TORCH,
+                           N.FEDAVG_FIN_DIV, _count(ws), acc_in_ptr=out.ptr, tails=tails)
+    ctx.d2h(got, out.ptr)
+    assert same_bits(_vals(got[begin:end], fmt), exp)
+    slab.close()
+    out.close()
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("threads", [1, 3, 8])
+def test_helper_torch16_matches_torch_cpu(dt, threads):
+    """The drop-in helper against torch CPU itself (mul / add_(alpha) / div_ run by torch, as the reference's
+    helper runs them) on 16-bit tensors whose scalar-loop elements depend on torch's thread ranges: sizes
+    below and above the 32768-element grain, ragged against the 32-element vector blocks."""
+    from nvflare_amd.app_common.aggregators.weighted_aggregation_helper import WeightedAggregationHelper
+
+    old = torch.get_num_threads()
+    torch.set_num_threads(threads)
+    try:
+        rng = np.random.default_rng(threads)
+        sizes = {"a": (33000 + 7,), "b": (3, 23339), "c": (1031,), "d": (100003,), "e": (64, 512)}
+        K = 6
+        clients = [{k: torch.from_numpy((rng.standard_normal(s) * 30).astype(np.float32)).to(dt) for k, s in sizes.items()}
+                   for _ in range(K)]
+        ws = [float(rng.random() * 5 + 0.1) for _ in range(K)]
+        h = WeightedAggregationHelper()
+        for k, (c, w) in enumerate(zip(clients, ws)):
+            h.add(c, w, f"site-{k}", 0)
+        got = h.get_result()
+        for key in sizes:
+            exp = orc.torch_mode_reference([c[key].clone() for c in clients], ws)
+            assert got[key].dtype == dt and got[key].shape == exp.shape
+            assert torch.equal(got[key].view(torch.int16), exp.view(torch.int16)), (key, threads)
+    finally:
+        torch.set_num_threads(old)
 
 
 @pytest.mark.parametrize("budget", [None, 1])
