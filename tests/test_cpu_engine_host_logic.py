@@ -13,13 +13,17 @@ import torch
 from fake_device import FakeDeviceContext, fake_engine
 from golden_util import as_f32_values, same_bits
 from nvflare_amd import _native as N
+from oracle import fedavg_oracle as orc
 
 
 def _one_shot(values, ws, container, fmt=None):
     """The per-element sequence over one key's contributions, computed directly."""
     if fmt is not None:
         rows = [as_f32_values(v, fmt).reshape(-1) for v in values]
-        res = FakeDeviceContext._agg(rows, ws, N.FEDAVG_OP_TORCH, N.FEDAVG_FIN_DIV, _count(ws), None, fmt=fmt)
+        # torch's scalar-loop elements of the add_ (nvflare_amd/torch16.py), as the engine reproduces them
+        scalar = orc.torch16_scalar_mask(rows[0].size, torch.get_num_threads())
+        res = FakeDeviceContext._agg(rows, ws, N.FEDAVG_OP_TORCH, N.FEDAVG_FIN_DIV, _count(ws), None, fmt=fmt,
+                                     scalar=scalar)
         return res
     op, fin = ((N.FEDAVG_OP_TORCH, N.FEDAVG_FIN_DIV) if container == "torch" else (N.FEDAVG_OP_NUMPY, N.FEDAVG_FIN_SCALE))
     rows = [np.asarray(v.numpy() if isinstance(v, torch.Tensor) else v, dtype=np.float32).reshape(-1) for v in values]
