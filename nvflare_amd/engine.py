@@ -634,7 +634,9 @@ class DeviceFedAvg:
     def _torch16_tails(self, group: List[_KeyState]) -> np.ndarray:
         """Flat indices of the group's elements that torch's add_ runs through its scalar loop (torch16.py),
         for the thread count and vector build of this process -- where the reference would run."""
-        sig = (tuple((st.offset, st.n) for st in group), torch16.torch_threads(), torch16.vector_block())
+        # host tensors only: the reference adds device-resident tensors with torch's GPU kernel (no CPU loops)
+        sig = (tuple((st.offset, st.n) for st in group if st.torch_device is None), torch16.torch_threads(),
+               torch16.vector_block())
         hit = self._tails_cache.get(sig)
         if hit is None:
             hit = self._tails_cache[sig] = torch16.scalar_tail_indices(sig[0], sig[1], sig[2])
