@@ -147,6 +147,20 @@ def _resolve_types(v, weight, weighted: bool) -> Tuple[str, np.dtype, np.dtype, 
     return "numpy", in_np, acc_np, op, N.FEDAVG_FIN_SCALE
 
 
+def _numpy_scale_override(st) -> Optional[float]:
+    """numpy's finalisation ``T * (1.0 / count)`` (weighted_aggregation_helper.py:236) when the weight sum is a
+    numpy scalar narrower than the total (np.float32 / np.float16 weights on a float64 total, np.float16 on
+    float32): ``1.0 / count`` is then that scalar type's correctly rounded quotient, not the total type's.
+    Returns the scale to multiply by in a separate launch, or None when the library's fin value is exact."""
+    c = st.count
+    if st.fin != N.FEDAVG_FIN_SCALE or not isinstance(c, np.floating):
+        return None
+    if np.dtype(type(c)).itemsize >= np.dtype(st.acc_np).itemsize or st.acc_np not in (_F32, _F64):
+        return None
+    with np.errstate(all="ignore"):
+        return float(1.0 / c)
+
+
 def _default_budget(ctx: DeviceContext) -> int:
     """HBM the engine may hold: everything but an 8 GiB reserve (torch, the runtime, other helpers)."""
     env = os.environ.get("NVFLARE_AMD_MAX_RESIDENT_BYTES")
@@ -590,6 +604,12 @@ class DeviceFedAvg:
         out = arena.acc.ptr if out is None else out
         acc_in = out if first.acc_valid else None
         fin = first.fin if final else N.FEDAVG_FIN_NONE
+        scale = _numpy_scale_override(first) if final else None
+        if scale is not None:
+            if epi is not None:
+                raise TypeError("nvflare_amd: a server-optimizer epilogue on a numpy total with narrower numpy-scalar "
+                                "weights is unsupported")
+            fin = N.FEDAVG_FIN_NONE  # the scaling runs as its own launch below
         # a fold can happen while a contribution is being staged (its second arena needs room), before the
         # contribution's weight is counted: the count only matters to the finalisation
         count = float(first.count) if first.count is not None else 1.0
@@ -615,6 +635,7 @@ class DeviceFedAvg:
 
         if not pend:  # finalise an already folded sum
             launch([], [], TILE, TILE, fin, True)
+            self._scale_range(arena, out, begin, end, scale)
             return
         # consecutive contributions staged in slabs of the same geometry go in one launch; a change of
         # geometry chains the next launch through the accumulator (arrival order is preserved)
@@ -630,6 +651,15 @@ class DeviceFedAvg:
             launch([p.slot.base for p in seg], [p.weight for p in seg], lay.tile, lay.tile_stride,
                    fin if last_launch else N.FEDAVG_FIN_NONE, last_launch)
             acc_in = out
+        self._scale_range(arena, out, begin, end, scale)
+
+    def _scale_range(self, arena: _Arena, out: int, begin: int, end: int, scale: Optional[float]) -> None:
+        """out[begin:end] *= scale in the total's dtype (the (X, X) rows entry, first step v * w)."""
+        if scale is None or end <= begin:
+            return
+        p = out + begin * arena.esize
+        self.ctx.accumulate([p], [scale], end - begin, p, arena.fmt, arena.fmt, N.FEDAVG_OP_NUMPY, N.FEDAVG_FIN_NONE, 1.0)
+        self.stats["launches"] += 1
 
     def _torch16_tails(self, group: List[_KeyState]) -> np.ndarray:
         """Flat indices of the group's elements that torch's add_ runs through its scalar loop (torch16.py),
@@ -688,19 +718,26 @@ class DeviceFedAvg:
                 continue
             if st.acc_buf is None:
                 st.acc_buf = self.ctx.alloc(st.n * st.acc_np.itemsize)
-            self.ctx.accumulate(
-                [p.buf.ptr for p in st.pending],
-                [p.weight for p in st.pending],
-                st.n,
-                st.acc_buf.ptr,
-                st.in_dt,
-                st.acc_dt,
-                st.op,
-                st.fin if final else N.FEDAVG_FIN_NONE,
-                float(st.count) if st.count is not None else 1.0,
-                acc_in_ptr=st.acc_buf.ptr if st.acc_valid else None,
-            )
-            self.stats["launches"] += 1
+            scale = _numpy_scale_override(st) if final else None
+            if st.pending or scale is None:
+                self.ctx.accumulate(
+                    [p.buf.ptr for p in st.pending],
+                    [p.weight for p in st.pending],
+                    st.n,
+                    st.acc_buf.ptr,
+                    st.in_dt,
+                    st.acc_dt,
+                    st.op,
+                    st.fin if final and scale is None else N.FEDAVG_FIN_NONE,
+                    float(st.count) if st.count is not None else 1.0,
+                    acc_in_ptr=st.acc_buf.ptr if st.acc_valid else None,
+                )
+                self.stats["launches"] += 1
+            if scale is not None:
+                self.ctx.accumulate([st.acc_buf.ptr], [scale], st.n, st.acc_buf.ptr, st.acc_dt, st.acc_dt,
+                                    N.FEDAVG_OP_NUMPY, N.FEDAVG_FIN_NONE, 1.0)
+                self.stats["launches"] += 1
+                st.done = True
             st.pending = []
             st.acc_valid = True
 
@@ -773,11 +810,15 @@ class DeviceFedAvg:
                                             for st in self.keys.values())
 
     def _check_doomed(self) -> None:
-        """torch integer totals under weigh_by_local_iter=False: the reference's get_result fails at the first
-        such key's ``div_`` (weighted_aggregation_helper.py:233); so does this one, before any launch."""
+        """Keys the reference's get_result (weighted_aggregation_helper.py:226-240) fails on, in its key order,
+        raised before any launch: a torch integer total under weigh_by_local_iter=False (``div_`` refuses it),
+        and a numpy key whose python-number weight sum is 0 (``1.0 / count`` -- e.g. every contribution with
+        NUM_STEPS_CURRENT_ROUND = 0)."""
         for st in self.keys.values():
             if st.doomed:
                 raise RuntimeError(f"result type Float can't be cast to the desired output type {st.doomed}")
+            if st.fin == N.FEDAVG_FIN_SCALE and type(st.count) in (int, float, bool) and st.count == 0:  # not numpy scalars
+                raise ZeroDivisionError("float division by zero")
 
     def result(self) -> Dict[str, Any]:
         """Finalise every key on the device and return host (or device-tensor) results."""

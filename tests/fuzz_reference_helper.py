@@ -69,15 +69,19 @@ def _value(rng, shape, dt, container):
     return np.array(a, copy=True)
 
 
-def _weight(rng):
-    kind = rng.integers(0, 4)
+def _weight(rng, wtype=float):
+    """One weight; ``wtype`` is the case's weight type: python float, or a numpy scalar type (NEP 50: it then
+    sets the result dtype -- a round mixing both changes a key's dtype mid-round, a documented gap)."""
+    kind = rng.integers(0, 5)
     if kind == 0:
-        return float(rng.integers(1, 100))
-    if kind == 1:
-        return float(rng.random() * 10)
-    if kind == 2:
-        return float(rng.choice([1e-6, 0.5, 3.0, 1e6]))
-    return float(rng.random()) * float(rng.integers(1, 50))
+        w = float(rng.integers(1, 100))
+    elif kind == 1:
+        w = float(rng.random() * 10)
+    elif kind == 2:
+        w = float(rng.choice([1e-6, 0.5, 3.0, 1e6, 0.0]))
+    else:
+        w = float(rng.random()) * float(rng.integers(1, 50))
+    return wtype(w)
 
 
 def _copy(v):
@@ -133,6 +137,7 @@ def run(cases: int, seed: int, threads: int) -> dict:
             dt = str(rng.choice(TORCH_DTYPES if container == "torch" else NP_DTYPES))
             keys[f"layer{j}.{dt}"] = (SHAPES[int(rng.integers(0, len(SHAPES)))], dt)
         weigh = bool(rng.random() < 0.85)
+        wtype = [float, np.float64, np.float32][int(rng.integers(0, 3))] if weigh and rng.random() < 0.3 else float
         exclude = str(rng.choice(["", "layer1", "bool|int"])) if rng.random() < 0.3 else None
         budget = int(rng.choice([0, 1, 50_000])) if rng.random() < 0.3 else None
         slots = str(int(rng.choice([2, 3]))) if rng.random() < 0.3 else None
@@ -146,7 +151,7 @@ def run(cases: int, seed: int, threads: int) -> dict:
             K = int(rng.integers(1, 13))
             for k in range(K):
                 data = {n: _value(rng, s, dt, container) for n, (s, dt) in keys.items() if rng.random() < 0.8}
-                w = _weight(rng)
+                w = _weight(rng, wtype)
                 try:
                     ref.add(data={n: _copy(v) for n, v in data.items()}, weight=w, contributor_name=f"c{k}",
                             contribution_round=rnd)
@@ -197,13 +202,174 @@ def run(cases: int, seed: int, threads: int) -> dict:
     return stats
 
 
+def _intime_classes():
+    from nvflare.app_common.aggregators.intime_accumulate_model_aggregator import InTimeAccumulateWeightedAggregator as R
+
+    from nvflare_amd.app_common.aggregators.intime_accumulate_model_aggregator import (
+        InTimeAccumulateWeightedAggregator as M,
+    )
+
+    return R, M
+
+
+def _same_dxo(a, b, tag, out):
+    """Compare two DXOs (data kind, meta, data; COLLECTION recursively)."""
+    if a.data_kind != b.data_kind:
+        out.append(f"{tag}: kind {a.data_kind} vs {b.data_kind}")
+        return
+    ma, mb = dict(a.meta or {}), dict(b.meta or {})
+    if set(ma) != set(mb) or any(repr(ma[k]) != repr(mb[k]) for k in ma):
+        out.append(f"{tag}: meta {ma} vs {mb}")
+    if a.data_kind == "COLLECTION":
+        if set(a.data) != set(b.data):
+            out.append(f"{tag}: collection keys {sorted(a.data)} vs {sorted(b.data)}")
+            return
+        for k in a.data:
+            _same_dxo(a.data[k], b.data[k], f"{tag}/{k}", out)
+        return
+    if list(a.data) != list(b.data):
+        out.append(f"{tag}: keys {list(a.data)} vs {list(b.data)}")
+        return
+    for k in a.data:
+        why = _same(a.data[k], b.data[k])
+        if why:
+            out.append(f"{tag} key {k}: {why}")
+
+
+def run_intime(cases: int, seed: int) -> dict:
+    """InTimeAccumulateWeightedAggregator (intime_accumulate_model_aggregator.py:47-288 with dxo_aggregator.py:
+    71-191) against the reference on random accept sequences: single and COLLECTION DXOs, per-client and
+    per-DXO aggregation weights, exclude_vars, weigh_by_local_iter, contributions from a wrong round, repeated
+    contributors, wrong data kinds, failed return codes, missing / odd NUM_STEPS, missing sub-DXOs; accept's
+    return values, the aggregated DXO and the published AGGREGATION_STATS must match, over two rounds."""
+    from nvflare.apis.dxo import DXO, DataKind, MetaKey, from_shareable
+    from nvflare.apis.fl_constant import ReservedKey, ReturnCode
+    from nvflare.apis.fl_context import FLContext
+    from nvflare.apis.shareable import Shareable
+    from nvflare.app_common.app_constant import AppConstants
+
+    R, M = _intime_classes()
+    rng = np.random.default_rng(seed)
+    stats = {"cases": 0, "accepts": 0, "rejected": 0, "aggregates": 0, "mismatches": [], "errors": 0}
+    for case in range(cases):
+        container = "torch" if rng.random() < 0.4 else "numpy"
+        collection = rng.random() < 0.35
+        subkeys = ["dxo_a", "dxo_b"] if collection else [""]
+        kinds = {k: [DataKind.WEIGHT_DIFF, DataKind.WEIGHTS][int(rng.integers(0, 2))] for k in subkeys}
+        edk = kinds if collection else kinds[""]
+        names = [f"site-{i}" for i in range(int(rng.integers(1, 7)))]
+        aw = None
+        if rng.random() < 0.5:
+            per = {n: float(rng.random() * 3) for n in names if rng.random() < 0.8}
+            aw = {k: dict(per) for k in subkeys} if collection and rng.random() < 0.5 else per
+        ex = None
+        if rng.random() < 0.3:
+            ex = {k: str(rng.choice(["", "bias", "w1"])) for k in subkeys} if collection else "bias"
+        weigh = bool(rng.random() < 0.85)
+        keys = {"w0": (int(rng.integers(1, 5000)),), "w1": (3, 7), "bias": (5,)}
+        kw = dict(exclude_vars=ex, aggregation_weights=aw, expected_data_kind=edk, weigh_by_local_iter=weigh)
+        try:
+            ref = R(**kw)
+            ref._initialize(ref.aggregation_weights, ref.exclude_vars, ref.expected_data_kind)
+        except Exception as e:
+            try:
+                mine = M(**kw)
+                mine._initialize(mine.aggregation_weights, mine.exclude_vars, mine.expected_data_kind)
+                stats["mismatches"].append(f"case {case}: reference init raised {e!r}, drop-in did not")
+            except Exception as e2:
+                if type(e2) is not type(e):
+                    stats["mismatches"].append(f"case {case}: init {e2!r} vs {e!r}")
+            continue
+        mine = M(**kw)
+        mine._initialize(mine.aggregation_weights, mine.exclude_vars, mine.expected_data_kind)
+        for rnd in range(2):
+            ctx_r, ctx_m = FLContext(), FLContext()
+            for c in (ctx_r, ctx_m):
+                c.set_prop(AppConstants.CURRENT_ROUND, rnd)
+            order = list(names) + [str(rng.choice(names)) for _ in range(int(rng.integers(0, 3)))]  # repeats
+            rng.shuffle(order)
+            for name in order:
+                odd = rng.random()
+                steps = [1, 3, 7.5, None, 0, -2, 20][int(rng.integers(0, 7))]
+
+                def make():
+                    sub = {}
+                    for k in subkeys:
+                        if collection and odd < 0.05:
+                            continue  # a COLLECTION missing a sub-DXO
+                        data = {n: _value(rng, s, "float32", container) for n, s in keys.items() if rng.random() < 0.85}
+                        kind = kinds[k] if odd >= 0.1 else DataKind.METRICS
+                        meta = {} if steps is None else {MetaKey.NUM_STEPS_CURRENT_ROUND: steps}
+                        sub[k] = DXO(kind, data=data, meta=meta)
+                    return sub
+
+                sub = make()
+                pair = []
+                for _ in range(2):
+                    d = (DXO(DataKind.COLLECTION, data={k: DXO(v.data_kind, data={n: _copy(x) for n, x in v.data.items()},
+                                                                 meta=dict(v.meta)) for k, v in sub.items()})
+                         if collection else DXO(sub[""].data_kind, data={n: _copy(x) for n, x in sub[""].data.items()},
+                                                meta=dict(sub[""].meta)))
+                    sh = d.to_shareable()
+                    sh.set_peer_props({ReservedKey.IDENTITY_NAME: name})
+                    sh.add_cookie(AppConstants.CONTRIBUTION_ROUND, rnd if odd < 0.9 else rnd + 1)
+                    if 0.15 <= odd < 0.2:
+                        sh.set_return_code(ReturnCode.EXECUTION_EXCEPTION)
+                    pair.append(sh)
+                try:
+                    a = ref.accept(pair[0], ctx_r)
+                except Exception as e:
+                    a = e
+                try:
+                    b = mine.accept(pair[1], ctx_m)
+                except Exception as e:
+                    b = e
+                stats["accepts"] += 1
+                if isinstance(a, Exception) or isinstance(b, Exception):
+                    if type(a) is not type(b):
+                        stats["mismatches"].append(f"case {case} round {rnd}: accept {b!r} vs {a!r}")
+                    stats["errors"] += 1
+                elif a != b:
+                    stats["mismatches"].append(f"case {case} round {rnd} {name}: accept {b} vs reference {a}")
+                elif not a:
+                    stats["rejected"] += 1
+            try:
+                ra = from_shareable(ref.aggregate(ctx_r))
+            except Exception as e:
+                ra = e
+            try:
+                ma = from_shareable(mine.aggregate(ctx_m))
+            except Exception as e:
+                ma = e
+            tag = f"case {case} round {rnd} ({container}, collection={collection}, weigh={weigh}, aw={aw is not None}, ex={ex!r})"
+            if isinstance(ra, Exception) or isinstance(ma, Exception):
+                if type(ra) is not type(ma):
+                    stats["mismatches"].append(f"{tag}: aggregate {ma!r} vs {ra!r}")
+                stats["errors"] += 1
+                break
+            _same_dxo(ra, ma, tag, stats["mismatches"])
+            sr, sm = ctx_r.get_prop(AppConstants.AGGREGATION_STATS), ctx_m.get_prop(AppConstants.AGGREGATION_STATS)
+            if repr(sr) != repr(sm):
+                stats["mismatches"].append(f"{tag}: stats {sm} vs {sr}")
+            stats["aggregates"] += 1
+            ref.reset(ctx_r)
+            mine.reset(ctx_m)
+        stats["cases"] += 1
+    return stats
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--cases", type=int, default=200)
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--threads", type=int, default=3)
+    ap.add_argument("--mode", choices=["helper", "intime"], default="helper")
     a = ap.parse_args()
-    stats = run(a.cases, a.seed, a.threads)
+    if a.mode == "intime":
+        _setup()
+        stats = run_intime(a.cases, a.seed)
+    else:
+        stats = run(a.cases, a.seed, a.threads)
     print(json.dumps({**stats, "mismatches": stats["mismatches"][:20], "n_mismatches": len(stats["mismatches"])}))
     sys.exit(1 if stats["mismatches"] else 0)
 

@@ -4,8 +4,11 @@ with the kernels' per-element sequences restated by the oracle -- gives the refe
 containers, dtypes, shapes and bits on random rounds (client counts, partial keys, 0-d / empty / ragged /
 multi-tile / 70001-element shapes, numpy and torch, float32 / float64 / float16 / bfloat16 / integer / bool,
 odd weights, weigh_by_local_iter, exclude_vars, HBM budgets that force folds, small slabs, torch threads 1 and
-4), and raises the reference's exception type where the reference raises.  Skipped where the reference tree
-is absent (the GPU box)."""
+4), and raises the reference's exception type where the reference raises.  The same for the
+InTimeAccumulateWeightedAggregator on random accept sequences (single and COLLECTION DXOs, aggregation weights,
+exclude_vars, wrong rounds, repeated contributors, wrong kinds, failed return codes, odd NUM_STEPS): accept's
+answers, the aggregated DXO and the published stats.  Skipped where the reference tree is absent (the GPU
+box)."""
 
 import json
 import os
@@ -19,14 +22,17 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 
 
 @pytest.mark.skipif(not os.path.exists(os.path.join(REF, "nvflare")), reason="reference tree not mounted")
-@pytest.mark.parametrize("seed,threads", [(11, 1), (12, 4)])
-def test_random_rounds_match_reference(tmp_path, seed, threads):
+@pytest.mark.parametrize("mode,seed,threads", [("helper", 11, 1), ("helper", 12, 4), ("intime", 13, 2)])
+def test_random_rounds_match_reference(tmp_path, mode, seed, threads):
     env = dict(os.environ, NVFLARE_REF_ROOT=REF, PYTHONDONTWRITEBYTECODE="1")
     env.pop("NVFLARE_AMD_FORCE_STANDINS", None)
     proc = subprocess.run([sys.executable, os.path.join(HERE, "fuzz_reference_helper.py"), "--cases", "120",
-                           "--seed", str(seed), "--threads", str(threads)], cwd=str(tmp_path), env=env,
+                           "--seed", str(seed), "--threads", str(threads), "--mode", mode], cwd=str(tmp_path), env=env,
                           capture_output=True, text=True, timeout=600)
     line = proc.stdout.strip().splitlines()[-1] if proc.stdout.strip() else "{}"
     stats = json.loads(line)
     assert proc.returncode == 0 and stats.get("n_mismatches") == 0, (stats, proc.stderr[-2000:])
-    assert stats["cases"] == 120 and stats["rounds"] > 150 and stats["keys"] > 400 and stats["launches"] > 0
+    if mode == "helper":
+        assert stats["cases"] == 120 and stats["rounds"] > 150 and stats["keys"] > 400 and stats["launches"] > 0
+    else:
+        assert stats["cases"] == 120 and stats["aggregates"] > 150 and stats["rejected"] > 100
