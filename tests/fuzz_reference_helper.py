@@ -122,7 +122,73 @@ def _same(a, b) -> str:
     return ""
 
 
-def run(cases: int, seed: int, threads: int) -> dict:
+def gen_helper_case(rng, big: bool = True) -> dict:
+    """One random helper case, every input drawn up front (replayable from the seed without the reference)."""
+    container = "torch" if rng.random() < 0.5 else "numpy"
+    shapes = SHAPES if big else SHAPES[:-1]
+    keys = {}
+    for j in range(int(rng.integers(1, 6))):
+        dt = str(rng.choice(TORCH_DTYPES if container == "torch" else NP_DTYPES))
+        keys[f"layer{j}.{dt}"] = (shapes[int(rng.integers(0, len(shapes)))], dt)
+    weigh = bool(rng.random() < 0.85)
+    wtype = [float, np.float64, np.float32][int(rng.integers(0, 3))] if weigh and rng.random() < 0.3 else float
+    exclude = str(rng.choice(["", "layer1", "bool|int"])) if rng.random() < 0.3 else None
+    budget = int(rng.choice([0, 1, 50_000])) if rng.random() < 0.3 else None
+    slots = str(int(rng.choice([2, 3]))) if rng.random() < 0.3 else None
+    rounds = []
+    for _ in range(2):
+        contribs = []
+        for k in range(int(rng.integers(1, 13))):
+            data = {n: _value(rng, s, dt, container) for n, (s, dt) in keys.items() if rng.random() < 0.8}
+            contribs.append((data, _weight(rng, wtype), f"c{k}"))
+        rounds.append(contribs)
+    return dict(container=container, weigh=weigh, exclude=exclude, budget=budget, slots=slots, rounds=rounds)
+
+
+def play_helper_case(helper, spec, rnd: int):
+    """Feed one round to a helper: (results, None) or (None, exception) -- the first exception ends the case."""
+    try:
+        for data, w, name in spec["rounds"][rnd]:
+            helper.add(data={n: _copy(v) for n, v in data.items()}, weight=w, contributor_name=name,
+                       contribution_round=rnd)
+        return helper.get_result(), None
+    except Exception as e:  # e.g. torch refusing alpha=1e6 for a float16 total, div_ on an integer total
+        return None, e
+
+
+def _canonical_bytes(v) -> bytes:
+    """A result's bits with every NaN replaced by one canonical NaN (payloads are unspecified)."""
+    import torch
+
+    if isinstance(v, torch.Tensor):
+        if v.dtype == torch.bfloat16:
+            bits = v.view(torch.int16).numpy().copy()
+            bits[torch.isnan(v).numpy()] = 0x7FC0
+            return bits.tobytes()
+        v = v.numpy()
+    a = np.array(np.asarray(v), copy=True)
+    if a.dtype.kind == "f":
+        a[np.isnan(a)] = np.nan
+    return a.tobytes()
+
+
+def describe_result(res) -> list:
+    """[(key, container, dtype, shape, sha256 of the canonical bits)] in result order."""
+    import hashlib
+
+    import torch
+
+    out = []
+    for k, v in res.items():
+        if isinstance(v, torch.Tensor):
+            cont, dt, shape = "torch", str(v.dtype).replace("torch.", ""), list(v.shape)
+        else:
+            cont, dt, shape = "numpy", str(np.asarray(v).dtype), list(np.asarray(v).shape)
+        out.append([k, cont, dt, shape, hashlib.sha256(_canonical_bytes(v)).hexdigest()])
+    return out
+
+
+def run(cases: int, seed: int, threads: int, record=None, big: bool = True) -> dict:
     import torch
 
     torch.set_num_threads(threads)  # torch's 16-bit add_ splits tensors of 32768+ elements over the threads
@@ -130,64 +196,26 @@ def run(cases: int, seed: int, threads: int) -> dict:
     rng = np.random.default_rng(seed)
     stats = {"cases": 0, "rounds": 0, "keys": 0, "errors": 0, "mismatches": [], "launches": 0}
     for case in range(cases):
-        container = "torch" if rng.random() < 0.5 else "numpy"
-        nkeys = int(rng.integers(1, 6))
-        keys = {}
-        for j in range(nkeys):
-            dt = str(rng.choice(TORCH_DTYPES if container == "torch" else NP_DTYPES))
-            keys[f"layer{j}.{dt}"] = (SHAPES[int(rng.integers(0, len(SHAPES)))], dt)
-        weigh = bool(rng.random() < 0.85)
-        wtype = [float, np.float64, np.float32][int(rng.integers(0, 3))] if weigh and rng.random() < 0.3 else float
-        exclude = str(rng.choice(["", "layer1", "bool|int"])) if rng.random() < 0.3 else None
-        budget = int(rng.choice([0, 1, 50_000])) if rng.random() < 0.3 else None
-        slots = str(int(rng.choice([2, 3]))) if rng.random() < 0.3 else None
-        if slots:
-            os.environ["NVFLARE_AMD_SLAB_SLOTS"] = slots
+        spec = gen_helper_case(rng, big)
+        if spec["slots"]:
+            os.environ["NVFLARE_AMD_SLAB_SLOTS"] = spec["slots"]
         else:
             os.environ.pop("NVFLARE_AMD_SLAB_SLOTS", None)
-        ref = Ref(exclude_vars=exclude, weigh_by_local_iter=weigh)
-        mine = Mine(exclude_vars=exclude, weigh_by_local_iter=weigh, max_resident_bytes=budget)
+        ref = Ref(exclude_vars=spec["exclude"], weigh_by_local_iter=spec["weigh"])
+        mine = Mine(exclude_vars=spec["exclude"], weigh_by_local_iter=spec["weigh"], max_resident_bytes=spec["budget"])
+        rec = []
         for rnd in range(2):
-            K = int(rng.integers(1, 13))
-            for k in range(K):
-                data = {n: _value(rng, s, dt, container) for n, (s, dt) in keys.items() if rng.random() < 0.8}
-                w = _weight(rng, wtype)
-                try:
-                    ref.add(data={n: _copy(v) for n, v in data.items()}, weight=w, contributor_name=f"c{k}",
-                            contribution_round=rnd)
-                except Exception as e:  # e.g. torch refusing alpha=1e6 for a float16 total
-                    err = e
-                else:
-                    err = None
-                try:
-                    mine.add(data=data, weight=w, contributor_name=f"c{k}", contribution_round=rnd)
-                except Exception as e:
-                    if err is None or type(e) is not type(err):
-                        stats["mismatches"].append(f"case {case}: drop-in raised {e!r}, reference {err!r}")
-                    stats["errors"] += 1
-                    break  # the reference fails part-way through a contribution: states differ from here
-                if err is not None:
-                    stats["mismatches"].append(f"case {case}: reference raised {err!r}, drop-in did not")
-                    break
-            else:
-                err = None
-            if err is not None:
-                break
-            tag = f"case {case} round {rnd} ({container}, weigh={weigh}, exclude={exclude!r}, budget={budget}, slots={slots})"
-            try:
-                r_ref = ref.get_result()
-            except Exception as e:  # e.g. torch's div_ refusing an integer total (weigh_by_local_iter=False)
-                err = e
-            try:
-                r_mine = mine.get_result()
-            except Exception as e:
-                if err is None or type(e) is not type(err):
-                    stats["mismatches"].append(f"{tag}: drop-in get_result raised {e!r}, reference {err!r}")
+            tag = (f"case {case} round {rnd} ({spec['container']}, weigh={spec['weigh']}, exclude={spec['exclude']!r}, "
+                   f"budget={spec['budget']}, slots={spec['slots']})")
+            r_ref, e_ref = play_helper_case(ref, spec, rnd)
+            r_mine, e_mine = play_helper_case(mine, spec, rnd)
+            if e_ref is not None or e_mine is not None:
+                if type(e_ref) is not type(e_mine):
+                    stats["mismatches"].append(f"{tag}: drop-in raised {e_mine!r}, reference {e_ref!r}")
                 stats["errors"] += 1
-                break
-            if err is not None:
-                stats["mismatches"].append(f"{tag}: reference get_result raised {err!r}, drop-in did not")
-                break
+                rec.append({"error": type(e_ref).__name__ if e_ref is not None else None})
+                break  # the reference fails part-way through a contribution: states differ from here
+            rec.append({"keys": describe_result(r_ref)})
             if list(r_ref) != list(r_mine):
                 stats["mismatches"].append(f"{tag}: keys {list(r_ref)} vs {list(r_mine)}")
                 continue
@@ -197,6 +225,8 @@ def run(cases: int, seed: int, threads: int) -> dict:
                     stats["mismatches"].append(f"{tag} key {n}: {why}")
             stats["keys"] += len(r_ref)
             stats["rounds"] += 1
+        if record is not None:
+            record.append({"case": case, "slots": spec["slots"], "budget": spec["budget"], "rounds": rec})
         stats["cases"] += 1
     stats["launches"] = len(fake.launches)
     return stats
@@ -358,18 +388,146 @@ def run_intime(cases: int, seed: int) -> dict:
     return stats
 
 
+def _same_flmodel(a, b, tag, out):
+    if type(a) is not type(b) or (a is None) != (b is None):
+        out.append(f"{tag}: {type(b).__name__} vs {type(a).__name__}")
+        return
+    if list(a.params or {}) != list(b.params or {}):
+        out.append(f"{tag}: params keys {list(b.params or {})} vs {list(a.params or {})}")
+    else:
+        for k in a.params or {}:
+            why = _same(a.params[k], b.params[k])
+            if why:
+                out.append(f"{tag} param {k}: {why}")
+    for field in ("params_type", "current_round", "metrics", "meta"):
+        va, vb = getattr(a, field), getattr(b, field)
+        if repr(va) != repr(vb):
+            out.append(f"{tag} {field}: {vb!r} vs {va!r}")
+
+
+def run_fedavg(cases: int, seed: int) -> dict:
+    """FedAvg-workflow aggregation (base_fedavg.py:93-230, fedavg.py:268-366) against the reference on random
+    FLModel lists: ``aggregate_fn`` vs ``BaseFedAvg.aggregate_fn`` and DeviceFedAvgModelAggregator vs FedAvg's
+    built-in in-time path (with aggregation_weights) -- odd NUM_STEPS values, missing / empty client names,
+    partial params, numpy and torch, metrics of every kind (numbers, bools, strings, nested dicts, NaN, None)."""
+    from nvflare.app_common.abstract.fl_model import FLModel
+    from nvflare.app_common.aggregators.weighted_aggregation_helper import WeightedAggregationHelper as RefHelper
+    from nvflare.app_common.workflows.base_fedavg import BaseFedAvg
+    from nvflare.app_common.workflows.fedavg import FedAvg
+
+    from nvflare_amd.app_common.aggregators import DeviceFedAvgModelAggregator
+    from nvflare_amd.app_common.workflows import aggregate_fn
+
+    rng = np.random.default_rng(seed)
+    stats = {"cases": 0, "mismatches": [], "errors": 0, "accepted": 0}
+    odd_steps = [None, True, False, 3, "7", "abc", 0, -1, float("nan"), float("inf"), 2.5, 40, [1]]
+    for case in range(cases):
+        container = "torch" if rng.random() < 0.5 else "numpy"
+        K = int(rng.integers(1, 7))
+        keys = {"w": (int(rng.integers(1, 3000)),), "b": (7,), "c": ()}
+        names = [f"site-{i}" for i in range(K)]
+        models = []
+        for i in range(K):
+            meta = {}
+            r = rng.random()
+            if r < 0.8:
+                meta["client_name"] = names[i] if r < 0.7 else ""
+            st = odd_steps[int(rng.integers(0, len(odd_steps)))]
+            if not (container == "torch" and st is not None and not isinstance(st, (bool, list)) and
+                    isinstance(st, (int, float)) and abs(float(st)) > 1e30):
+                if st is not None:
+                    meta["NUM_STEPS_CURRENT_ROUND"] = st
+            params = {n: _value(rng, sh, "float32", container) for n, sh in keys.items() if rng.random() < 0.85}
+            if not params:
+                params = {"w": _value(rng, keys["w"], "float32", container)}
+            m = rng.random()
+            metrics = None if m < 0.1 else {"acc": float(rng.random()), "n": int(rng.integers(0, 9)),
+                                            "flag": bool(m < 0.5), "tag": "x", "nested": {"a": 1},
+                                            "bad": float("nan") if m > 0.9 else 0.5}
+            models.append(FLModel(params=params, metrics=metrics, current_round=int(rng.integers(0, 3)), meta=meta))
+
+        def clone(ms):
+            return [FLModel(params={k: _copy(v) for k, v in x.params.items()}, metrics=None if x.metrics is None else
+                            dict(x.metrics), current_round=x.current_round, meta=dict(x.meta)) for x in ms]
+
+        tag = f"case {case} ({container}, K={K})"
+        try:
+            ra = BaseFedAvg.aggregate_fn(clone(models))
+        except Exception as e:
+            ra = e
+        try:
+            ma = aggregate_fn(clone(models))
+        except Exception as e:
+            ma = e
+        if isinstance(ra, Exception) or isinstance(ma, Exception):
+            if type(ra) is not type(ma):
+                stats["mismatches"].append(f"{tag} aggregate_fn: {ma!r} vs {ra!r}")
+            stats["errors"] += 1
+        else:
+            _same_flmodel(ra, ma, f"{tag} aggregate_fn", stats["mismatches"])
+        # FedAvg's built-in in-time path vs the FedAvg(aggregator=...) drop-in
+        aw = {n: float(rng.random() * 2) for n in names if rng.random() < 0.6} if rng.random() < 0.5 else None
+        wf = FedAvg(num_clients=K, num_rounds=1, aggregation_weights=aw)
+        wf.info = wf.warning = wf.debug = lambda *a, **k: None
+        wf.fl_ctx = None
+        wf.current_round = models[0].current_round
+        wf._aggr_helper = RefHelper()
+        wf._aggr_metrics_helper = RefHelper()
+        wf._expected_count = K
+        agg = DeviceFedAvgModelAggregator(aggregation_weights=aw)
+        from nvflare.apis.fl_context import FLContext
+
+        agg.handle_event("_start_run", FLContext())
+        acc_r, acc_m = [], []
+        try:
+            for x in clone(models):
+                acc_r.append(bool(wf._aggregate_one_result(x)))
+            rr = wf._get_aggregated_result()
+        except Exception as e:
+            rr = e
+        try:
+            for x in clone(models):
+                acc_m.append(bool(agg.accept_model(x)))
+            mr = agg.aggregate_model()
+        except Exception as e:
+            mr = e
+        if isinstance(rr, Exception) or isinstance(mr, Exception):
+            if type(rr) is not type(mr):
+                stats["mismatches"].append(f"{tag} in-time: {mr!r} vs {rr!r}")
+            stats["errors"] += 1
+        else:
+            if acc_r != acc_m:
+                stats["mismatches"].append(f"{tag} in-time accepted {acc_m} vs {acc_r}")
+            _same_flmodel(rr, mr, f"{tag} in-time", stats["mismatches"])
+            stats["accepted"] += sum(acc_r)
+        stats["cases"] += 1
+    return stats
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--cases", type=int, default=200)
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--threads", type=int, default=3)
-    ap.add_argument("--mode", choices=["helper", "intime"], default="helper")
+    ap.add_argument("--mode", choices=["helper", "intime", "fedavg"], default="helper")
+    ap.add_argument("--record", default=None, help="helper mode: write the reference's result hashes (GPU replay)")
+    ap.add_argument("--small", action="store_true", help="helper mode: no 70001-element shapes")
     a = ap.parse_args()
     if a.mode == "intime":
         _setup()
         stats = run_intime(a.cases, a.seed)
+    elif a.mode == "fedavg":
+        _setup()
+        stats = run_fedavg(a.cases, a.seed)
     else:
-        stats = run(a.cases, a.seed, a.threads)
+        record = [] if a.record else None
+        stats = run(a.cases, a.seed, a.threads, record, big=not a.small)
+        if a.record:
+            with open(a.record, "w") as f:
+                json.dump({"generator": "tests/fuzz_reference_helper.py --mode helper --record",
+                           "reference": "NVFlare weighted_aggregation_helper.py (/root/reference)", "seed": a.seed,
+                           "cases": a.cases, "threads": a.threads, "big": not a.small, "numpy": np.__version__,
+                           "torch": __import__("torch").__version__, "records": record}, f, indent=0)
     print(json.dumps({**stats, "mismatches": stats["mismatches"][:20], "n_mismatches": len(stats["mismatches"])}))
     sys.exit(1 if stats["mismatches"] else 0)
 

@@ -36,3 +36,16 @@ def test_random_rounds_match_reference(tmp_path, mode, seed, threads):
         assert stats["cases"] == 120 and stats["rounds"] > 150 and stats["keys"] > 400 and stats["launches"] > 0
     else:
         assert stats["cases"] == 120 and stats["aggregates"] > 150 and stats["rejected"] > 100
+
+
+def test_recorded_reference_rounds_replay_on_the_fake_device(monkeypatch):
+    """tests/golden/fuzz_helper_s21.json (the reference's result hashes for 200 random cases) replayed through
+    the drop-in on the fake device -- the same check tests/test_gpu_fuzz_replay.py runs on the MI355X; this one
+    needs no reference tree."""
+    import test_gpu_fuzz_replay as replay
+    from fake_device import FakeDeviceContext
+    from nvflare_amd.device import DeviceContext
+
+    fake = FakeDeviceContext()
+    monkeypatch.setattr(DeviceContext, "get", classmethod(lambda cls, d=None: fake))
+    replay.test_fuzz_cases_match_reference_on_the_gpu(monkeypatch)
