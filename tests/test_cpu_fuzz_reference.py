@@ -22,7 +22,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 
 
 @pytest.mark.skipif(not os.path.exists(os.path.join(REF, "nvflare")), reason="reference tree not mounted")
-@pytest.mark.parametrize("mode,seed,threads", [("helper", 11, 1), ("helper", 12, 4), ("intime", 13, 2)])
+@pytest.mark.parametrize("mode,seed,threads", [("helper", 11, 1), ("helper", 12, 4), ("intime", 13, 2), ("fedavg", 14, 1)])
 def test_random_rounds_match_reference(tmp_path, mode, seed, threads):
     env = dict(os.environ, NVFLARE_REF_ROOT=REF, PYTHONDONTWRITEBYTECODE="1")
     env.pop("NVFLARE_AMD_FORCE_STANDINS", None)
@@ -34,8 +34,10 @@ def test_random_rounds_match_reference(tmp_path, mode, seed, threads):
     assert proc.returncode == 0 and stats.get("n_mismatches") == 0, (stats, proc.stderr[-2000:])
     if mode == "helper":
         assert stats["cases"] == 120 and stats["rounds"] > 150 and stats["keys"] > 400 and stats["launches"] > 0
-    else:
+    elif mode == "intime":
         assert stats["cases"] == 120 and stats["aggregates"] > 150 and stats["rejected"] > 100
+    else:
+        assert stats["cases"] == 120 and stats["accepted"] > 200
 
 
 def test_recorded_reference_rounds_replay_on_the_fake_device(monkeypatch):
