@@ -294,6 +294,9 @@ class DeviceFedAvg:
         self.peak_clients = 0
         self._deferred = None  # DeferredRound still holding fp32 slots (result_deferred)
         self._tails_cache: Dict[tuple, np.ndarray] = {}  # torch16 scalar-loop elements per run layout
+        # key -> (first element within its whole tensor, the whole tensor's size) for keys that are a bucket of a
+        # larger tensor (sharding.ShardedFedAvg); other keys are whole tensors
+        self.key_spans: Dict[str, Tuple[int, int]] = {}
         self.stats = {"h2d_bytes": 0, "folds": 0, "launches": 0, "slabs_allocated": 0}
 
     @property
@@ -665,8 +668,8 @@ class DeviceFedAvg:
         """Flat indices of the group's elements that torch's add_ runs through its scalar loop (torch16.py),
         for the thread count and vector build of this process -- where the reference would run."""
         # host tensors only: the reference adds device-resident tensors with torch's GPU kernel (no CPU loops)
-        sig = (tuple((st.offset, st.n) for st in group if st.torch_device is None), torch16.torch_threads(),
-               torch16.vector_block())
+        sig = (tuple((st.offset, st.n) + self.key_spans.get(st.name, (0, st.n)) for st in group
+                     if st.torch_device is None), torch16.torch_threads(), torch16.vector_block())
         hit = self._tails_cache.get(sig)
         if hit is None:
             hit = self._tails_cache[sig] = torch16.scalar_tail_indices(sig[0], sig[1], sig[2])
@@ -933,6 +936,7 @@ class DeviceFedAvg:
             self._consolidate()
             self.keys.clear()
             self._tails_cache.clear()
+            self.key_spans.clear()
             for a in self.arenas.values():
                 a.layout_elems = 0
 

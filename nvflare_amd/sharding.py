@@ -66,13 +66,18 @@ class ShardedFedAvg:
         self._shapes: Dict[str, tuple] = {}
 
     def _pieces(self, bucket: int, items):
-        """(subkey, 1-D slice view) of every key overlapping `bucket`."""
+        """(subkey, 1-D slice view) of every key overlapping `bucket`; each subkey's place in its whole key goes
+        to the bucket's engine (``key_spans``: torch's 16-bit scalar-loop elements are those of the whole
+        tensor, engine.py ``_torch16_tails``)."""
         out = []
+        spans = self.engines[bucket].key_spans
         for k, v in items:
             n = int(np.prod(v.shape, dtype=np.int64)) if v.shape else 1
             lo, hi = bucket_ranges(n, len(self.engines))[bucket]
             if lo < hi or (n == 0 and bucket == 0):
-                out.append((f"{k}\x00{lo}", _flat_view(v)[lo:hi]))
+                sub = f"{k}\x00{lo}"
+                spans[sub] = (lo, n)
+                out.append((sub, _flat_view(v)[lo:hi]))
         return out
 
     def add(self, items: List[Tuple[str, Any]], weight, weighted: bool) -> None:

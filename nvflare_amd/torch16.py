@@ -63,12 +63,18 @@ def scalar_ranges(n: int, threads: int, block: int) -> List[Tuple[int, int]]:
     return out
 
 
-def scalar_tail_indices(keys: Sequence[Tuple[int, int]], threads: int, block: int) -> np.ndarray:
-    """Sorted flat indices, over keys given as (flat offset, n), of the elements torch's scalar loop adds."""
+def scalar_tail_indices(keys: Sequence[Tuple[int, ...]], threads: int, block: int) -> np.ndarray:
+    """Sorted flat indices of the elements torch's scalar loop adds, over keys given as (flat offset, n) -- a
+    whole tensor -- or (flat offset, n, lo, n_whole): elements [lo, lo + n) of an n_whole-element tensor (a
+    parameter bucket; the loops run over the whole tensor)."""
     parts = []
-    for off, n in keys:
-        for s, e in scalar_ranges(int(n), threads, block):
-            parts.append(np.arange(off + s, off + e, dtype=np.int64))
+    for key in keys:
+        off, n = int(key[0]), int(key[1])
+        lo, whole = (int(key[2]), int(key[3])) if len(key) > 2 else (0, n)
+        for s, e in scalar_ranges(whole, threads, block):
+            s, e = max(s, lo), min(e, lo + n)
+            if s < e:
+                parts.append(np.arange(off + s - lo, off + e - lo, dtype=np.int64))
     if not parts:
         return np.empty(0, dtype=np.int64)
     idx = np.concatenate(parts)

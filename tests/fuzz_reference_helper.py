@@ -146,14 +146,24 @@ def gen_helper_case(rng, big: bool = True) -> dict:
 
 
 def play_helper_case(helper, spec, rnd: int):
-    """Feed one round to a helper: (results, None) or (None, exception) -- the first exception ends the case."""
+    """Feed one round to a helper: (results, None) or (None, exception) -- the first exception ends the case.
+    Deferred values (a drop-in helper with defer_result=True) are materialised here, as a consumer would."""
     try:
         for data, w, name in spec["rounds"][rnd]:
             helper.add(data={n: _copy(v) for n, v in data.items()}, weight=w, contributor_name=name,
                        contribution_round=rnd)
-        return helper.get_result(), None
+        res = helper.get_result()
+        return {k: (v.materialize() if hasattr(v, "materialize") and hasattr(v, "container") else v)
+                for k, v in res.items()}, None
     except Exception as e:  # e.g. torch refusing alpha=1e6 for a float16 total, div_ on an integer total
         return None, e
+
+
+def dropin_variant(case: int) -> dict:
+    """Drop-in constructor options by case index (no RNG draw, so recorded seeds stay valid): every third case
+    defers its fp32 results (DeferredAggregate, materialised by the consumer), every fifth splits every key
+    into three parameter buckets (ShardedFedAvg, three engines on one device)."""
+    return dict(defer_result=case % 3 == 1, devices=[0, 0, 0] if case % 5 == 2 else None)
 
 
 def _canonical_bytes(v) -> bytes:
@@ -202,7 +212,8 @@ def run(cases: int, seed: int, threads: int, record=None, big: bool = True) -> d
         else:
             os.environ.pop("NVFLARE_AMD_SLAB_SLOTS", None)
         ref = Ref(exclude_vars=spec["exclude"], weigh_by_local_iter=spec["weigh"])
-        mine = Mine(exclude_vars=spec["exclude"], weigh_by_local_iter=spec["weigh"], max_resident_bytes=spec["budget"])
+        mine = Mine(exclude_vars=spec["exclude"], weigh_by_local_iter=spec["weigh"], max_resident_bytes=spec["budget"],
+                    **dropin_variant(case))
         rec = []
         for rnd in range(2):
             tag = (f"case {case} round {rnd} ({spec['container']}, weigh={spec['weigh']}, exclude={spec['exclude']!r}, "

@@ -9,6 +9,8 @@ and the bits cannot change."""
 import os
 import socket
 
+import types
+
 import numpy as np
 import pytest
 import torch
@@ -89,8 +91,12 @@ def test_sharded_pieces_reassemble(oracle):
     data = [{k: rng.standard_normal(s).astype(np.float32) for k, s in shapes.items()} for _ in range(K)]
     ws = [1.0, 2.0, 0.5, 3.0]
     sh = ShardedFedAvg.__new__(ShardedFedAvg)  # host-side methods only (no device engines)
-    sh.engines = [None, None, None]
+    sh.engines = [types.SimpleNamespace(key_spans={}) for _ in range(3)]
     pieces = [dict(sh._pieces(b, list(data[0].items()))) for b in range(3)]
+    for b, eng in enumerate(sh.engines):  # each bucket's place in its whole key, for the 16-bit torch loops
+        assert set(eng.key_spans) == set(pieces[b])
+        for sub, (lo, n) in eng.key_spans.items():
+            assert sub.endswith(f"\x00{lo}") and n == (int(np.prod(shapes[sub.split(chr(0))[0]])) or 0)
     covered = {}
     for b, pc in enumerate(pieces):
         for sub, arr in pc.items():

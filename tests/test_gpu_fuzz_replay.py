@@ -2,7 +2,8 @@
 
 tests/golden/fuzz_helper_s21.json holds, for 200 random helper cases (seed 21, torch at 4 threads), the
 REFERENCE helper's result per round -- keys in order, container, dtype, shape and a SHA-256 of the bits (NaNs
-canonicalised) -- or the exception type it raised.  The inputs are not stored: the same generator regenerates
+canonicalised) -- or the exception type it raised.  Every third case runs the drop-in with deferred results,
+every fifth sharded over three parameter buckets (fuzz_reference_helper.dropin_variant).  The inputs are not stored: the same generator regenerates
 them from the seed here (numpy's generator is bit-stable for a given version).  The drop-in helper on the
 MI355X must give the same keys, containers, dtypes, shapes and bits, and the same exception types."""
 
@@ -38,7 +39,7 @@ def test_fuzz_cases_match_reference_on_the_gpu(monkeypatch):
             else:
                 monkeypatch.delenv("NVFLARE_AMD_SLAB_SLOTS", raising=False)
             h = WeightedAggregationHelper(exclude_vars=spec["exclude"], weigh_by_local_iter=spec["weigh"],
-                                          max_resident_bytes=spec["budget"])
+                                          max_resident_bytes=spec["budget"], **F.dropin_variant(r["case"]))
             for rnd, exp in enumerate(r["rounds"]):
                 res, err = F.play_helper_case(h, spec, rnd)
                 if "error" in exp:
