@@ -56,6 +56,10 @@ enum fedavg_op {
     FEDAVG_OP_NUMPY = 0,
     FEDAVG_OP_TORCH = 1,
     FEDAVG_OP_UNWEIGHTED = 2,
+    /* torch-ROCm's GPU kernels, for device-resident tensors: the steps of FEDAVG_OP_TORCH, except that a
+     * float16 / bfloat16 total keeps alpha in fp32 (the GPU add_ converts alpha to its fp32 opmath type, the
+     * CPU kernel to the tensor dtype):  first r(v*float(w))  step r(fma(v, float(w), T))  (v6) */
+    FEDAVG_OP_TORCH_DEVICE = 3,
 };
 
 /* finalisation after the last row, reference get_result (:226-240):
@@ -66,6 +70,10 @@ enum fedavg_fin {
     FEDAVG_FIN_NONE = 0,
     FEDAVG_FIN_SCALE = 1,
     FEDAVG_FIN_DIV = 2,
+    /* torch-ROCm's div_ by a CPU scalar on device-resident tensors: a multiplication by the opmath reciprocal,
+     * T * (1.0f / float(count)) for fp32 / float16 / bfloat16 totals (rounded to the total's format),
+     * T * (1.0 / count) for fp64 (v6) */
+    FEDAVG_FIN_RECIP = 3,
 };
 
 /* server-optimizer epilogue fused behind the finalisation (fedavg_accumulate_tiled_epi) */

@@ -36,10 +36,12 @@ FEDAVG_U64 = 12
 FEDAVG_OP_NUMPY = 0
 FEDAVG_OP_TORCH = 1
 FEDAVG_OP_UNWEIGHTED = 2
+FEDAVG_OP_TORCH_DEVICE = 3  # torch-ROCm arithmetic of device-resident tensors
 
 FEDAVG_FIN_NONE = 0
 FEDAVG_FIN_SCALE = 1
 FEDAVG_FIN_DIV = 2
+FEDAVG_FIN_RECIP = 3  # torch-ROCm div_ by a CPU scalar: multiply by the opmath reciprocal
 
 ABI_VERSION = 6  # include/nvflare_amd_fedavg.h FEDAVG_ABI_VERSION
 

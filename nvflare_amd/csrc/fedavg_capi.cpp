@@ -335,8 +335,21 @@ void h2d_multi_impl(fedavg_ctx* ctx, char* dst, size_t tile_b, size_t tstride_b,
 }
 
 void check_op_fin(int op, int fin) {
-    if (op < FEDAVG_OP_NUMPY || op > FEDAVG_OP_UNWEIGHTED) throw Error("bad op " + std::to_string(op));
-    if (fin < FEDAVG_FIN_NONE || fin > FEDAVG_FIN_DIV) throw Error("bad fin " + std::to_string(fin));
+    if (op < FEDAVG_OP_NUMPY || op > FEDAVG_OP_TORCH_DEVICE) throw Error("bad op " + std::to_string(op));
+    if (fin < FEDAVG_FIN_NONE || fin > FEDAVG_FIN_RECIP) throw Error("bad fin " + std::to_string(fin));
+}
+
+// The fp32 / fp64 kernels know three steps and two finalisations; torch-ROCm's device-tensor arithmetic
+// (FEDAVG_OP_TORCH_DEVICE, FEDAVG_FIN_RECIP) maps onto them: the steps are FEDAVG_OP_TORCH's at these widths,
+// and the reciprocal becomes FEDAVG_FIN_SCALE with a count whose library scale -- acc_t(1.0 / count) -- is
+// torch's: for fp32, count' = 1 / (double)(1.0f / (float)count), so that (float)(1.0 / count') is exactly
+// 1.0f / (float)count (a double quotient within 2^-52 of a float cannot round to another float).
+void normalize_wide(int& op, int& fin, double& count, bool acc_f32) {
+    if (op == FEDAVG_OP_TORCH_DEVICE) op = FEDAVG_OP_TORCH;
+    if (fin == FEDAVG_FIN_RECIP) {
+        fin = FEDAVG_FIN_SCALE;
+        if (acc_f32) count = 1.0 / (double)(1.0f / (float)count);
+    }
 }
 
 // finalisation scalar, computed on the host exactly as the reference computes it:
@@ -507,8 +520,14 @@ float narrow_fin_value(int fmt, int fin, double count) {
         return fmt == FEDAVG_F16 ? half_value(1.0 / count) : bf16_value((float)(1.0 / count));
     if (fin == FEDAVG_FIN_DIV)  // torch: div_ by a CPU scalar in fp32
         return (float)count;
+    if (fin == FEDAVG_FIN_RECIP)  // torch-ROCm: multiply by the fp32 reciprocal (the kernel's SCALE form)
+        return 1.0f / (float)count;
     return 0.0f;
 }
+
+// the narrow kernels' own op / fin for a C-ABI op / fin (device-tensor modes: see the enums)
+int narrow_kernel_op(int op) { return op == FEDAVG_OP_TORCH_DEVICE ? FEDAVG_OP_TORCH : op; }
+int narrow_kernel_fin(int fin) { return fin == FEDAVG_FIN_RECIP ? FEDAVG_FIN_SCALE : fin; }
 
 void fill_narrow_table(fedavg::RowTableNarrow& t, const void* const* rows, const double* weights, int k0, int kc,
                        int fmt, int op) {
@@ -518,6 +537,8 @@ void fill_narrow_table(fedavg::RowTableNarrow& t, const void* const* rows, const
         t.rows[j] = rows[k0 + j];
         if (op == FEDAVG_OP_NUMPY) {
             t.w_first[j] = t.w_step[j] = fmt == FEDAVG_F16 ? half_value(w) : bf16_value((float)w);
+        } else if (op == FEDAVG_OP_TORCH_DEVICE) {  // torch-ROCm: mul and add_ keep the scalar in fp32
+            t.w_first[j] = t.w_step[j] = (float)w;
         } else {  // torch: mul keeps the scalar in fp32, add_ casts alpha to the tensor dtype
             t.w_first[j] = (float)w;
             t.w_step[j] = torch16_value(fmt, w);
@@ -541,7 +562,8 @@ void run_narrow(fedavg_ctx* ctx, const void* const* rows, const double* weights,
         const int64_t need = (n / 8 + fedavg::kBlock) / fedavg::kBlock;
         const int grid =
             (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)ctx->num_cus * 2 * ctx->bpc(), need));
-        HIP_CHECK(fedavg::launch_rows_narrow(t, kc, cur_in, out, n, fmt, op, last ? fin : FEDAVG_FIN_NONE, fv, grid, s));
+        HIP_CHECK(fedavg::launch_rows_narrow(t, kc, cur_in, out, n, fmt, narrow_kernel_op(op),
+                                             last ? narrow_kernel_fin(fin) : FEDAVG_FIN_NONE, fv, grid, s));
         ++ctx->launches;
         cur_in = out;
         k0 += kc;
@@ -573,8 +595,9 @@ void run_tiles_narrow(fedavg_ctx* ctx, const void* const* bases, const double* w
                                                    last ? fin : FEDAVG_FIN_NONE, fv, s));
             ++ctx->launches;
         }
-        HIP_CHECK(fedavg::launch_tiles_narrow(t, kc, tstride, cur_in, out, begin, end, fmt, op,
-                                              last ? fin : FEDAVG_FIN_NONE, fv, grid, burst, s, &ctx->launches));
+        HIP_CHECK(fedavg::launch_tiles_narrow(t, kc, tstride, cur_in, out, begin, end, fmt, narrow_kernel_op(op),
+                                              last ? narrow_kernel_fin(fin) : FEDAVG_FIN_NONE, fv, grid, burst, s,
+                                              &ctx->launches));
         if (n_tails) {
             HIP_CHECK(fedavg::launch_scatter16(tails, tail_vals, n_tails, out, s));
             ++ctx->launches;
@@ -1001,6 +1024,7 @@ int fedavg_accumulate(fedavg_ctx* ctx, const void* const* rows, const double* we
                                                 in_dtype == FEDAVG_U32 || in_dtype == FEDAVG_U64))) {
             throw Error("unsupported (in_dtype, acc_dtype) pair");
         }
+        if (!narrow && !int_acc) normalize_wide(op, fin, count, acc_dtype == FEDAVG_F32);
         if (n == 0) {
             ctx->timed_valid = false;
             return;
@@ -1048,6 +1072,7 @@ int fedavg_accumulate_tiled(fedavg_ctx* ctx, const void* const* bases, const dou
         if (!ctx) throw Error("ctx is NULL");
         if (k_rows < 0 || (k_rows == 0 && !acc_in)) throw Error("k_rows == 0 requires acc_in");
         check_op_fin(op, fin);
+        normalize_wide(op, fin, count, true);
         if (!valid_tile(tile_elems)) throw Error("tile_elems must be 1024, 2048, 4096 or 8192");
         if (tile_stride < tile_elems || tile_stride % 4) throw Error("tile_stride must be >= tile_elems, multiple of 4");
         if (begin % 4 || end % 4 || end < begin) throw Error("begin/end must be multiples of 4 with begin <= end");
@@ -1144,6 +1169,7 @@ int fedavg_accumulate_tiled64(fedavg_ctx* ctx, const void* const* bases, const d
         if (!ctx) throw Error("ctx is NULL");
         if (k_rows < 0 || (k_rows == 0 && !acc_in)) throw Error("k_rows == 0 requires acc_in");
         check_op_fin(op, fin);
+        normalize_wide(op, fin, count, false);
         if (tile_elems != (size_t)fedavg::kTile64Elems) throw Error("tile_elems must be 4096");
         if (tile_stride < tile_elems || tile_stride % 2) throw Error("tile_stride must be >= tile_elems, multiple of 2");
         if (begin % 2 || end % 2 || end < begin) throw Error("begin/end must be multiples of 2 with begin <= end");
@@ -1202,6 +1228,7 @@ int fedavg_accumulate_tiled_epi(fedavg_ctx* ctx, const void* const* bases, const
         if (epi->kind < FEDAVG_EPI_ADD_BASE || epi->kind > FEDAVG_EPI_ASGD) throw Error("bad epilogue kind");
         if (k_rows < 0 || (k_rows == 0 && !acc_in)) throw Error("k_rows == 0 requires acc_in");
         check_op_fin(op, fin);
+        normalize_wide(op, fin, count, true);
         if (tile_elems != (size_t)fedavg::kDefaultTile)
             throw Error("the epilogue kernel runs the default tile (" + std::to_string(fedavg::kDefaultTile) + ")");
         if (tile_stride < tile_elems || tile_stride % 4) throw Error("tile_stride must be >= tile_elems, multiple of 4");

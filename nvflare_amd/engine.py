@@ -112,16 +112,21 @@ def _resolve_types(v, weight, weighted: bool) -> Tuple[str, np.dtype, np.dtype, 
         if tdt not in _TORCH_TO_NP:
             raise TypeError(f"nvflare_amd: torch dtype {tdt} is not supported by the device kernels")
         in_np = _TORCH_TO_NP[tdt]
+        # the reference's torch ops run where the tensors are: torch CPU kernels for host tensors, torch-ROCm's
+        # GPU kernels for device-resident ones (alpha kept in fp32, div_ by a scalar as a reciprocal product;
+        # include/nvflare_amd_fedavg.h FEDAVG_OP_TORCH_DEVICE / FEDAVG_FIN_RECIP, probed against torch on the GPU)
+        on_device = v.device.type != "cpu"
+        fin = N.FEDAVG_FIN_RECIP if on_device else N.FEDAVG_FIN_DIV
         if in_np.kind in "iub":
             if not weighted:
                 # reference: v.clone() stays integer, add_ keeps it, and get_result's div_(count) raises
                 # (weighted_aggregation_helper.py:186-187, :208-209, :233): the key is marked, not staged
-                return "torch", in_np, in_np, N.FEDAVG_OP_UNWEIGHTED, N.FEDAVG_FIN_DIV
+                return "torch", in_np, in_np, N.FEDAVG_OP_UNWEIGHTED, fin
             acc_np = _TORCH_TO_NP[torch.get_default_dtype()]
         else:
             acc_np = in_np
-        op = N.FEDAVG_OP_TORCH if weighted else N.FEDAVG_OP_UNWEIGHTED
-        return "torch", in_np, acc_np, op, N.FEDAVG_FIN_DIV
+        op = (N.FEDAVG_OP_TORCH_DEVICE if on_device else N.FEDAVG_OP_TORCH) if weighted else N.FEDAVG_OP_UNWEIGHTED
+        return "torch", in_np, acc_np, op, fin
     in_np = np.dtype(v.dtype)
     if in_np not in _NUMPY_INPUTS:
         raise TypeError(f"nvflare_amd: numpy dtype {in_np} is not supported by the device kernels")
@@ -421,7 +426,9 @@ class DeviceFedAvg:
             st = self.keys.get(k)
             if st is None or st.container != "torch":
                 continue
-            limit = _TORCH_ALPHA_LIMITS.get(st.acc_np)
+            # device tensors: torch-ROCm converts alpha to its fp32 opmath type whatever the tensor dtype
+            limit = (_TORCH_ALPHA_LIMITS.get(st.acc_np) if st.torch_device is None
+                     else (_FLT_MAX, "float") if st.acc_np != _F64 else None)
             if limit is not None and abs(w) > limit[0]:
                 raise RuntimeError(f"value cannot be converted to type {limit[1]} without overflow")
 

@@ -156,10 +156,15 @@ def test_device_bf16_tensors_through_helper():
     out = h.get_result()
     assert out["w"].device.type == "cuda" and out["w"].dtype == torch.bfloat16
     assert out["h"].device.type == "cuda" and out["h"].dtype == torch.float16
-    exp = orc.torch16_vector_reference([as_f32_values(r, "bfloat16") for r in rows], ws, "bfloat16")
-    assert same_bits(as_f32_values(out["w"].cpu(), "bfloat16"), exp)
-    exp_h = orc.torch16_vector_reference([r.to(torch.float16).numpy().astype(np.float32) for r in rows], ws, "float16")
-    assert same_bits(out["h"].cpu().numpy().astype(np.float32), exp_h)
+    # the reference's ops as torch-ROCm runs them on device tensors: alpha kept in fp32, div_ as a product with
+    # the fp32 reciprocal (FEDAVG_OP_TORCH_DEVICE / FEDAVG_FIN_RECIP)
+    exp = orc.torch_mode_reference([r.to("cuda:0") for r in rows], ws)
+    assert torch.equal(out["w"].view(torch.int16), exp.view(torch.int16))
+    exp_h = orc.torch_mode_reference([r.to(torch.float16).to("cuda:0") for r in rows], ws)
+    assert torch.equal(out["h"].view(torch.int16), exp_h.view(torch.int16))
+    # and it differs from torch CPU's arithmetic on the same values (alpha rounded, true division)
+    cpu = orc.torch_mode_reference([r.clone() for r in rows], ws)
+    assert not torch.equal(out["w"].cpu().view(torch.int16), cpu.view(torch.int16))
 
 
 # ---------------------------------------------------------------------------------------------------
@@ -250,6 +255,40 @@ def test_tiled16_tails_vs_oracle(ctx, fmt, K):
     assert same_bits(_vals(got[begin:end], fmt), exp)
     slab.close()
     out.close()
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.float64, torch.bfloat16, torch.float16, torch.int32])
+@pytest.mark.parametrize("weighted", [True, False])
+def test_device_tensors_match_torch_rocm(dt, weighted):
+    """Device-resident tensors: the helper's torch ops as torch-ROCm runs them on the GPU (probe:
+    tools/torch_gpu_semantics_probe.py) -- alpha in fp32 for every dtype, div_ by a scalar as a product with the
+    opmath reciprocal -- bit for bit, for ragged sizes, a 0-d key and 130 clients (chained launches)."""
+    from nvflare_amd.app_common.aggregators.weighted_aggregation_helper import WeightedAggregationHelper
+
+    if dt == torch.int32 and not weighted:
+        pytest.skip("an integer total's div_ raises (tests/test_cpu_boundary.py)")
+    rng = np.random.default_rng(5)
+    sizes = {"a": (4097 * 3 + 5,), "b": (33, 7), "c": ()}
+    for K in (6, 130):
+        clients = []
+        for _ in range(K):
+            c = {}
+            for k, s in sizes.items():
+                x = torch.from_numpy((rng.standard_normal(s) * 20).astype(np.float32))
+                c[k] = (x.round() if dt == torch.int32 else x).to(dt).to("cuda:0")
+            clients.append(c)
+        ws = [float(rng.random() * 4 + 0.05) for _ in range(K)]
+        h = WeightedAggregationHelper(weigh_by_local_iter=weighted)
+        for k, (c, w) in enumerate(zip(clients, ws)):
+            h.add(c, w, f"s{k}", 0)
+        out = h.get_result()
+        for key in sizes:
+            exp = orc.torch_mode_reference([c[key].clone() for c in clients], ws, weighted=weighted)
+            got = out[key]
+            assert got.device.type == "cuda" and got.dtype == exp.dtype and got.shape == exp.shape, key
+            if got.dtype in (torch.bfloat16, torch.float16):
+                got, exp = got.view(torch.int16), exp.view(torch.int16)
+            assert torch.equal(got, exp), (key, K)
 
 
 @pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])

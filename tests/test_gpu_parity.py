@@ -97,19 +97,37 @@ def test_helper_golden_bitexact_sharded(case):
     h.engine.release()
 
 
+def oracle_mod():
+    from oracle import fedavg_oracle
+
+    return fedavg_oracle
+
+
 @pytest.mark.parametrize("case", [c for c in HCASES if c["container"] == "torch"][:4],
                          ids=[c["name"] for c in HCASES if c["container"] == "torch"][:4])
 def test_helper_device_tensors(case):
-    """torch tensors already on the GPU: staged D2D, result returned as a device tensor."""
+    """torch tensors already on the GPU: staged D2D, result returned as a device tensor -- bit for bit what the
+    reference helper's torch ops (mul / add_(alpha) / div_) give when torch-ROCm runs them on those tensors
+    (FEDAVG_OP_TORCH_DEVICE / FEDAVG_FIN_RECIP: div_ by a scalar is a product with the fp32 reciprocal there)."""
+    import re
+
     from nvflare_amd.app_common.aggregators.weighted_aggregation_helper import WeightedAggregationHelper
 
     h = WeightedAggregationHelper(exclude_vars=case["exclude_vars"], weigh_by_local_iter=case["weigh_by_local_iter"])
+    seqs = {}
     for c in case["contributions"]:
-        h.add({k: _container(ARRAYS[n], "torch", "cuda:0") for k, n in c["data"].items()}, c["weight"], c["name"], 0)
+        data = {k: _container(ARRAYS[n], "torch", "cuda:0") for k, n in c["data"].items()}
+        h.add(data, c["weight"], c["name"], 0)
+        for k, v in data.items():
+            if not (case["exclude_vars"] and re.search(case["exclude_vars"], k)):
+                seqs.setdefault(k, []).append((v.clone(), c["weight"]))
     out = h.get_result()
-    for k, name in case["expected"].items():
-        assert out[k].device.type == "cuda"
-        assert same_bits(_as_numpy(out[k]).reshape(ARRAYS[name].shape), ARRAYS[name]), k
+    assert set(out) == set(seqs)
+    for k, seq in seqs.items():
+        exp = oracle_mod().torch_mode_reference([v for v, _ in seq], [w for _, w in seq],
+                                                weighted=case["weigh_by_local_iter"])
+        assert out[k].device.type == "cuda" and out[k].dtype == exp.dtype
+        assert same_bits(_as_numpy(out[k]), _as_numpy(exp)), k
 
 
 @pytest.mark.parametrize("case", ICASES, ids=[c["name"] for c in ICASES])
