@@ -274,7 +274,7 @@ def test_device_tensors_match_torch_rocm(dt, weighted):
         for _ in range(K):
             c = {}
             for k, s in sizes.items():
-                x = torch.from_numpy((rng.standard_normal(s) * 20).astype(np.float32))
+                x = torch.from_numpy(np.asarray(rng.standard_normal(s) * 20, dtype=np.float32))
                 c[k] = (x.round() if dt == torch.int32 else x).to(dt).to("cuda:0")
             clients.append(c)
         ws = [float(rng.random() * 4 + 0.05) for _ in range(K)]
