@@ -58,7 +58,8 @@ enum fedavg_op {
     FEDAVG_OP_UNWEIGHTED = 2,
     /* torch-ROCm's GPU kernels, for device-resident tensors: the steps of FEDAVG_OP_TORCH, except that a
      * float16 / bfloat16 total keeps alpha in fp32 (the GPU add_ converts alpha to its fp32 opmath type, the
-     * CPU kernel to the tensor dtype):  first r(v*float(w))  step r(fma(v, float(w), T))  (v6) */
+     * CPU kernel to the tensor dtype):  first r(v*float(w))  step r(fma(v, float(w), T)); for float16 the fma
+     * is rounded once, straight to fp16 (torch-ROCm's kernel uses v_fma_mixlo_f16)  (v6) */
     FEDAVG_OP_TORCH_DEVICE = 3,
 };
 

@@ -525,8 +525,9 @@ float narrow_fin_value(int fmt, int fin, double count) {
     return 0.0f;
 }
 
-// the narrow kernels' own op / fin for a C-ABI op / fin (device-tensor modes: see the enums)
-int narrow_kernel_op(int op) { return op == FEDAVG_OP_TORCH_DEVICE ? FEDAVG_OP_TORCH : op; }
+// the narrow kernels' own fin for a C-ABI fin (the device reciprocal is their SCALE form with an fp32 scale);
+// FEDAVG_OP_TORCH_DEVICE reaches them as is (float16: one rounding per add_ step; bfloat16: FEDAVG_OP_TORCH)
+int narrow_kernel_op(int op) { return op; }
 int narrow_kernel_fin(int fin) { return fin == FEDAVG_FIN_RECIP ? FEDAVG_FIN_SCALE : fin; }
 
 void fill_narrow_table(fedavg::RowTableNarrow& t, const void* const* rows, const double* weights, int k0, int kc,

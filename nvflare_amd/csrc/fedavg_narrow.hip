@@ -75,9 +75,22 @@ __device__ __forceinline__ float first16(float v, float w) {
     }
 }
 
+// torch-ROCm's float16 add_(v, alpha) on device-resident tensors (FEDAVG_OP_TORCH_DEVICE): its compiled
+// kernel rounds the exact fma once, straight to fp16 (v_fma_mixlo_f16; established against torch on the GPU:
+// tools/debug_fp16_device.py), where the CPU kernel rounds to fp32 first.  Explicit, so that no compiler choice
+// decides it; all three sources are fp32 (op_sel_hi 0), the result lands in the low half.
+__device__ __forceinline__ float fma_f16_once(float a, float b, float c) {
+    uint32_t d = 0;
+    asm volatile("v_fma_mixlo_f16 %0, %1, %2, %3" : "+v"(d) : "v"(a), "v"(b), "v"(c));
+    return load16<FEDAVG_F16>((uint16_t)(d & 0xffffu));
+}
+
 template <int FMT, int OP>
 __device__ __forceinline__ float step16(float t, float v, float w) {
-    if constexpr (OP == FEDAVG_OP_TORCH) {
+    if constexpr (OP == FEDAVG_OP_TORCH_DEVICE) {  // float16 only (bfloat16 device totals take FEDAVG_OP_TORCH)
+        static_assert(FMT == FEDAVG_F16, "FEDAVG_OP_TORCH_DEVICE kernels exist for float16 only");
+        return fma_f16_once(v, w, t);
+    } else if constexpr (OP == FEDAVG_OP_TORCH) {
         return rnd<FMT>(__builtin_fmaf(v, w, t));
     } else if constexpr (OP == FEDAVG_OP_NUMPY) {
         return rnd<FMT>(t + rnd<FMT>(v * w));
@@ -372,6 +385,13 @@ static hipError_t launch_t16_o(const RowTableNarrow& tab, int K, int64_t tstride
                                int64_t b8, int64_t e8, int op, int fin, float fv, int grid, bool burst, hipStream_t s,
                                uint64_t* nl) {
     switch (op) {
+        case FEDAVG_OP_TORCH_DEVICE:
+            if constexpr (FMT == FEDAVG_F16)
+                return launch_t16_f<FMT, FEDAVG_OP_TORCH_DEVICE>(tab, K, tstride8, acc_in, out, b8, e8, fin, fv, grid, burst,
+                                                                 s, nl);
+            else
+                return launch_t16_f<FMT, FEDAVG_OP_TORCH>(tab, K, tstride8, acc_in, out, b8, e8, fin, fv, grid, burst, s,
+                                                          nl);
         case FEDAVG_OP_TORCH:
             return launch_t16_f<FMT, FEDAVG_OP_TORCH>(tab, K, tstride8, acc_in, out, b8, e8, fin, fv, grid, burst, s, nl);
         case FEDAVG_OP_UNWEIGHTED:
@@ -517,6 +537,11 @@ template <int FMT>
 static hipError_t launch_n_o(const RowTableNarrow& tab, int K, const void* acc_in, void* out, int64_t n, int op, int fin,
                              float fv, int grid, bool vec, hipStream_t s) {
     switch (op) {
+        case FEDAVG_OP_TORCH_DEVICE:
+            if constexpr (FMT == FEDAVG_F16)
+                return launch_n_f<FMT, FEDAVG_OP_TORCH_DEVICE>(tab, K, acc_in, out, n, fin, fv, grid, vec, s);
+            else
+                return launch_n_f<FMT, FEDAVG_OP_TORCH>(tab, K, acc_in, out, n, fin, fv, grid, vec, s);
         case FEDAVG_OP_TORCH:
             return launch_n_f<FMT, FEDAVG_OP_TORCH>(tab, K, acc_in, out, n, fin, fv, grid, vec, s);
         case FEDAVG_OP_UNWEIGHTED:
