@@ -58,8 +58,9 @@ enum fedavg_op {
     FEDAVG_OP_UNWEIGHTED = 2,
     /* torch-ROCm's GPU kernels, for device-resident tensors: the steps of FEDAVG_OP_TORCH, except that a
      * float16 / bfloat16 total keeps alpha in fp32 (the GPU add_ converts alpha to its fp32 opmath type, the
-     * CPU kernel to the tensor dtype):  first r(v*float(w))  step r(fma(v, float(w), T)); for float16 the fma
-     * is rounded once, straight to fp16 (torch-ROCm's kernel uses v_fma_mixlo_f16)  (v6) */
+     * CPU kernel to the tensor dtype):  first r(v*float(w))  step r(fma(v, float(w), T)).  Elements listed to
+     * fedavg_accumulate_tiled16_tails (float16 only) take torch-ROCm's unrolled path instead, where the fma is
+     * rounded once, straight to fp16 (v_fma_mixlo_f16)  (v6) */
     FEDAVG_OP_TORCH_DEVICE = 3,
 };
 
@@ -258,7 +259,8 @@ int fedavg_accumulate_tiled16(fedavg_ctx* ctx, int fmt, const void* const* bases
  * (range length mod 32) elements of the range, a scalar loop whose c10::Half / c10::BFloat16 operators round
  * twice: step p = r(v * r(w)), T = r(T + p).  tails: n_tails strictly increasing flat element indices (host
  * memory) that take that step; those outside [begin, end) are ignored, as are all of them for an op other
- * than FEDAVG_OP_TORCH.  The listed elements are recomputed into a side buffer before the tile kernel (acc_in
+ * than FEDAVG_OP_TORCH -- except FEDAVG_OP_TORCH_DEVICE on float16, where the listed elements take torch-ROCm's
+ * unrolled step instead, T = fp16(exact fma(v, float(w), T)).  The listed elements are recomputed into a side buffer before the tile kernel (acc_in
  * may alias out) and written over its results after it: two small extra launches when any lies in the range. */
 int fedavg_accumulate_tiled16_tails(fedavg_ctx* ctx, int fmt, const void* const* bases, const double* weights,
                                     int k_rows, size_t tile_elems, size_t tile_stride, size_t begin, size_t end,

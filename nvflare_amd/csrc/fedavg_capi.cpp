@@ -592,8 +592,8 @@ void run_tiles_narrow(fedavg_ctx* ctx, const void* const* bases, const double* w
         fill_narrow_table(t, bases, weights, k0, kc, fmt, op);
         const bool last = k0 + kc >= k_rows;
         if (n_tails) {  // before the tile kernel: cur_in may be out
-            HIP_CHECK(fedavg::launch_torch16_tails(t, kc, T, tstride, tails, n_tails, cur_in, tail_vals, fmt,
-                                                   last ? fin : FEDAVG_FIN_NONE, fv, s));
+            HIP_CHECK(fedavg::launch_torch16_tails(t, kc, T, tstride, tails, n_tails, cur_in, tail_vals, fmt, op,
+                                                   last ? narrow_kernel_fin(fin) : FEDAVG_FIN_NONE, fv, s));
             ++ctx->launches;
         }
         HIP_CHECK(fedavg::launch_tiles_narrow(t, kc, tstride, cur_in, out, begin, end, fmt, narrow_kernel_op(op),
@@ -1132,10 +1132,11 @@ int fedavg_accumulate_tiled16_tails(fedavg_ctx* ctx, int fmt, const void* const*
             if (tails[j] <= tails[j - 1]) throw Error("tails must be strictly increasing");
         ctx->activate();
         hipStream_t s = ctx->compute();
-        // the scalar remainder exists only in torch's add_ with alpha (FEDAVG_OP_TORCH)
+        // the second path exists only in torch's add_ with alpha: the CPU scalar remainder (FEDAVG_OP_TORCH) and
+        // torch-ROCm's unrolled float16 path (FEDAVG_OP_TORCH_DEVICE)
         const int64_t* lo = tails;
         const int64_t* hi = tails;
-        if (op == FEDAVG_OP_TORCH && n_tails) {
+        if ((op == FEDAVG_OP_TORCH || (op == FEDAVG_OP_TORCH_DEVICE && fmt == FEDAVG_F16)) && n_tails) {
             lo = std::lower_bound(tails, tails + n_tails, (int64_t)begin);
             hi = std::lower_bound(lo, tails + n_tails, (int64_t)end);
         }

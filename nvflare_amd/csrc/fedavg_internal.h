@@ -138,7 +138,7 @@ hipError_t launch_dequant_f32(const DequantLaunch& L, hipStream_t s);
 hipError_t launch_tiles_epi_f32x4(const TileLaunch& L, const EpiParams& E, hipStream_t s,
                                   uint64_t* launch_count = nullptr);
 hipError_t launch_torch16_tails(const RowTableNarrow& tab, int K, int64_t tile, int64_t tstride, const int64_t* idx,
-                                int64_t m, const void* acc_in, void* vals, int fmt, int fin, float fin_val,
+                                int64_t m, const void* acc_in, void* vals, int fmt, int op, int fin, float fin_val,
                                 hipStream_t s);
 hipError_t launch_scatter16(const int64_t* idx, const void* vals, int64_t m, void* out, hipStream_t s);
 hipError_t launch_rows_intsum(const RowTableGeneric& tab, int K, const void* acc_in, void* out, int64_t n, int dtype,

@@ -75,10 +75,11 @@ __device__ __forceinline__ float first16(float v, float w) {
     }
 }
 
-// torch-ROCm's float16 add_(v, alpha) on device-resident tensors (FEDAVG_OP_TORCH_DEVICE): its compiled
-// kernel rounds the exact fma once, straight to fp16 (v_fma_mixlo_f16; established against torch on the GPU:
-// tools/debug_fp16_device.py), where the CPU kernel rounds to fp32 first.  Explicit, so that no compiler choice
-// decides it; all three sources are fp32 (op_sel_hi 0), the result lands in the low half.
+// torch-ROCm's float16 add_(v, alpha) on device-resident tensors (FEDAVG_OP_TORCH_DEVICE) in its unrolled
+// (non-vector) path: the exact fma rounded once, straight to fp16 (v_fma_mixlo_f16; established against torch
+// on the GPU: tools/debug_fp16_device.py), where its vector path and the CPU kernel round to fp32 first.
+// Explicit, so that no compiler choice decides it; all three sources are fp32 (op_sel_hi 0), result in the low
+// half.
 __device__ __forceinline__ float fma_f16_once(float a, float b, float c) {
     uint32_t d = 0;
     asm volatile("v_fma_mixlo_f16 %0, %1, %2, %3" : "+v"(d) : "v"(a), "v"(b), "v"(c));
@@ -87,10 +88,7 @@ __device__ __forceinline__ float fma_f16_once(float a, float b, float c) {
 
 template <int FMT, int OP>
 __device__ __forceinline__ float step16(float t, float v, float w) {
-    if constexpr (OP == FEDAVG_OP_TORCH_DEVICE) {  // float16 only (bfloat16 device totals take FEDAVG_OP_TORCH)
-        static_assert(FMT == FEDAVG_F16, "FEDAVG_OP_TORCH_DEVICE kernels exist for float16 only");
-        return fma_f16_once(v, w, t);
-    } else if constexpr (OP == FEDAVG_OP_TORCH) {
+    if constexpr (OP == FEDAVG_OP_TORCH) {
         return rnd<FMT>(__builtin_fmaf(v, w, t));
     } else if constexpr (OP == FEDAVG_OP_NUMPY) {
         return rnd<FMT>(t + rnd<FMT>(v * w));
@@ -385,13 +383,7 @@ static hipError_t launch_t16_o(const RowTableNarrow& tab, int K, int64_t tstride
                                int64_t b8, int64_t e8, int op, int fin, float fv, int grid, bool burst, hipStream_t s,
                                uint64_t* nl) {
     switch (op) {
-        case FEDAVG_OP_TORCH_DEVICE:
-            if constexpr (FMT == FEDAVG_F16)
-                return launch_t16_f<FMT, FEDAVG_OP_TORCH_DEVICE>(tab, K, tstride8, acc_in, out, b8, e8, fin, fv, grid, burst,
-                                                                 s, nl);
-            else
-                return launch_t16_f<FMT, FEDAVG_OP_TORCH>(tab, K, tstride8, acc_in, out, b8, e8, fin, fv, grid, burst, s,
-                                                          nl);
+        case FEDAVG_OP_TORCH_DEVICE:  // same steps; the host keeps alpha in fp32 in the table
         case FEDAVG_OP_TORCH:
             return launch_t16_f<FMT, FEDAVG_OP_TORCH>(tab, K, tstride8, acc_in, out, b8, e8, fin, fv, grid, burst, s, nl);
         case FEDAVG_OP_UNWEIGHTED:
@@ -423,7 +415,9 @@ hipError_t launch_tiles_narrow(const RowTableNarrow& tab, int K, int64_t tstride
 // fedavg_torch16_tails recomputes them from the same inputs into a side buffer before the tile kernel runs
 // (acc_in may alias out), and fedavg_scatter16 writes them over the tile kernel's results after it.
 // ---------------------------------------------------------------------------------------------
-template <int FMT, int FIN, bool ACC_IN>
+// DEVICE: the listed elements are those torch-ROCm's float16 add_ runs through its unrolled path (the last
+// partial block of its vectorized kernel): one rounding of the exact fma, fma_f16_once.
+template <int FMT, int FIN, bool ACC_IN, bool DEVICE>
 __global__ void __launch_bounds__(kBlock) fedavg_torch16_tails(const RowTableNarrow tab, const int K, const int64_t tile,
                                                                 const int64_t tstride, const int64_t* idx,
                                                                 const int64_t m, const uint16_t* acc_in,
@@ -442,7 +436,10 @@ __global__ void __launch_bounds__(kBlock) fedavg_torch16_tails(const RowTableNar
     }
     for (; k < K; ++k) {
         const float v = load16<FMT>(static_cast<const uint16_t*>(tab.rows[k])[off]);
-        t = rnd<FMT>(t + rnd<FMT>(v * tab.w_step[k]));  // tab.w_step[k] = r(w): c10 casts alpha to the dtype
+        if constexpr (DEVICE)
+            t = fma_f16_once(v, tab.w_step[k], t);  // tab.w_step[k] = float(w): torch-ROCm's fp32 opmath alpha
+        else
+            t = rnd<FMT>(t + rnd<FMT>(v * tab.w_step[k]));  // tab.w_step[k] = r(w): c10 casts alpha to the dtype
     }
     vals[j] = bits16<FMT>(fin16<FMT, FIN>(t, fv));
 }
@@ -453,42 +450,46 @@ __global__ void __launch_bounds__(kBlock) fedavg_scatter16(const int64_t* idx, c
     if (j < m) out[idx[j]] = vals[j];
 }
 
-template <int FMT, int FIN>
+template <int FMT, int FIN, bool DEVICE>
 static hipError_t launch_tails_a(const RowTableNarrow& tab, int K, int64_t tile, int64_t tstride, const int64_t* idx,
                                  int64_t m, const void* acc_in, void* vals, float fv, int grid, hipStream_t s) {
     const uint16_t* ai = static_cast<const uint16_t*>(acc_in);
     uint16_t* v = static_cast<uint16_t*>(vals);
     if (acc_in)
-        hipLaunchKernelGGL((fedavg_torch16_tails<FMT, FIN, true>), dim3(grid), dim3(kBlock), 0, s, tab, K, tile, tstride,
-                           idx, m, ai, v, fv);
+        hipLaunchKernelGGL((fedavg_torch16_tails<FMT, FIN, true, DEVICE>), dim3(grid), dim3(kBlock), 0, s, tab, K, tile,
+                           tstride, idx, m, ai, v, fv);
     else
-        hipLaunchKernelGGL((fedavg_torch16_tails<FMT, FIN, false>), dim3(grid), dim3(kBlock), 0, s, tab, K, tile, tstride,
-                           idx, m, ai, v, fv);
+        hipLaunchKernelGGL((fedavg_torch16_tails<FMT, FIN, false, DEVICE>), dim3(grid), dim3(kBlock), 0, s, tab, K, tile,
+                           tstride, idx, m, ai, v, fv);
     return hipGetLastError();
 }
 
-template <int FMT>
+template <int FMT, bool DEVICE>
 static hipError_t launch_tails_f(const RowTableNarrow& tab, int K, int64_t tile, int64_t tstride, const int64_t* idx,
                                  int64_t m, const void* acc_in, void* vals, int fin, float fv, int grid, hipStream_t s) {
-    switch (fin) {
+    switch (fin) {  // (FEDAVG_FIN_RECIP arrives as its SCALE form)
         case FEDAVG_FIN_SCALE:
-            return launch_tails_a<FMT, FEDAVG_FIN_SCALE>(tab, K, tile, tstride, idx, m, acc_in, vals, fv, grid, s);
+            return launch_tails_a<FMT, FEDAVG_FIN_SCALE, DEVICE>(tab, K, tile, tstride, idx, m, acc_in, vals, fv, grid, s);
         case FEDAVG_FIN_DIV:
-            return launch_tails_a<FMT, FEDAVG_FIN_DIV>(tab, K, tile, tstride, idx, m, acc_in, vals, fv, grid, s);
+            return launch_tails_a<FMT, FEDAVG_FIN_DIV, DEVICE>(tab, K, tile, tstride, idx, m, acc_in, vals, fv, grid, s);
         default:
-            return launch_tails_a<FMT, FEDAVG_FIN_NONE>(tab, K, tile, tstride, idx, m, acc_in, vals, fv, grid, s);
+            return launch_tails_a<FMT, FEDAVG_FIN_NONE, DEVICE>(tab, K, tile, tstride, idx, m, acc_in, vals, fv, grid, s);
     }
 }
 
 hipError_t launch_torch16_tails(const RowTableNarrow& tab, int K, int64_t tile, int64_t tstride, const int64_t* idx,
-                                int64_t m, const void* acc_in, void* vals, int fmt, int fin, float fin_val,
+                                int64_t m, const void* acc_in, void* vals, int fmt, int op, int fin, float fin_val,
                                 hipStream_t s) {
     const int grid = (int)((m + kBlock - 1) / kBlock);
     if (grid == 0) return hipSuccess;
+    if (op == FEDAVG_OP_TORCH_DEVICE) {  // float16 only: bfloat16 has no single-rounding path in torch-ROCm
+        if (fmt != FEDAVG_F16) return hipErrorInvalidValue;
+        return launch_tails_f<FEDAVG_F16, true>(tab, K, tile, tstride, idx, m, acc_in, vals, fin, fin_val, grid, s);
+    }
     if (fmt == FEDAVG_BF16)
-        return launch_tails_f<FEDAVG_BF16>(tab, K, tile, tstride, idx, m, acc_in, vals, fin, fin_val, grid, s);
+        return launch_tails_f<FEDAVG_BF16, false>(tab, K, tile, tstride, idx, m, acc_in, vals, fin, fin_val, grid, s);
     if (fmt == FEDAVG_F16)
-        return launch_tails_f<FEDAVG_F16>(tab, K, tile, tstride, idx, m, acc_in, vals, fin, fin_val, grid, s);
+        return launch_tails_f<FEDAVG_F16, false>(tab, K, tile, tstride, idx, m, acc_in, vals, fin, fin_val, grid, s);
     return hipErrorInvalidValue;
 }
 
@@ -538,10 +539,6 @@ static hipError_t launch_n_o(const RowTableNarrow& tab, int K, const void* acc_i
                              float fv, int grid, bool vec, hipStream_t s) {
     switch (op) {
         case FEDAVG_OP_TORCH_DEVICE:
-            if constexpr (FMT == FEDAVG_F16)
-                return launch_n_f<FMT, FEDAVG_OP_TORCH_DEVICE>(tab, K, acc_in, out, n, fin, fv, grid, vec, s);
-            else
-                return launch_n_f<FMT, FEDAVG_OP_TORCH>(tab, K, acc_in, out, n, fin, fv, grid, vec, s);
         case FEDAVG_OP_TORCH:
             return launch_n_f<FMT, FEDAVG_OP_TORCH>(tab, K, acc_in, out, n, fin, fv, grid, vec, s);
         case FEDAVG_OP_UNWEIGHTED:

@@ -628,6 +628,8 @@ class DeviceFedAvg:
         tails = None
         if first.op == N.FEDAVG_OP_TORCH and arena.fmt in (N.FEDAVG_F16, N.FEDAVG_BF16):
             tails = self._torch16_tails(group)
+        elif first.op == N.FEDAVG_OP_TORCH_DEVICE and arena.fmt == N.FEDAVG_F16:
+            tails = self._rocm16_tails(group)
 
         def launch(bases, weights, tile, stride, fin_, last_launch):
             if arena.fmt == N.FEDAVG_F64:
@@ -680,6 +682,14 @@ class DeviceFedAvg:
         hit = self._tails_cache.get(sig)
         if hit is None:
             hit = self._tails_cache[sig] = torch16.scalar_tail_indices(sig[0], sig[1], sig[2])
+        return hit
+
+    def _rocm16_tails(self, group: List[_KeyState]) -> np.ndarray:
+        """Flat indices of the group's float16 device-tensor elements torch-ROCm adds in its unrolled path."""
+        sig = ("rocm",) + tuple((st.offset, st.n) + self.key_spans.get(st.name, (0, st.n)) for st in group)
+        hit = self._tails_cache.get(sig)
+        if hit is None:
+            hit = self._tails_cache[sig] = torch16.rocm_f16_unrolled_indices(sig[1:])
         return hit
 
     def _launch_arena(self, final: bool, keys: Optional[Dict[str, _KeyState]] = None,

@@ -80,3 +80,31 @@ def scalar_tail_indices(keys: Sequence[Tuple[int, ...]], threads: int, block: in
     idx = np.concatenate(parts)
     idx.sort()
     return idx
+
+
+# torch-ROCm (device-resident float16 tensors): its vectorized elementwise kernel gives every block of 256
+# threads x 8 halves (16-byte vectors) = 2048 elements; blocks run the vector path (fp32 fma, then fp16: two
+# roundings, like the CPU vector loop), the last partial block runs the unrolled path, where the compiler fuses
+# the fma and the fp16 conversion (v_fma_mixlo_f16: one rounding).  Measured on MI355X with torch 2.10+rocm7.0
+# (tools/debug_fp16_device.py): 1500 / 2047 elements all single-rounded, 2048 / 4096 / 10240 all double,
+# 3072: elements 2048.. single.  Assumes 16-byte aligned tensors (torch's fresh allocations; a misaligned
+# client tensor would take narrower vectors).  bfloat16 has no fused path: both round twice.
+ROCM_F16_BLOCK = int(os.environ.get("NVFLARE_AMD_ROCM_F16_BLOCK", "2048"))
+
+
+def rocm_f16_unrolled_indices(keys: Sequence[Tuple[int, ...]], block: int = 0) -> np.ndarray:
+    """Sorted flat indices of the float16 elements torch-ROCm's add_ runs through its unrolled path, over keys
+    given as (flat offset, n[, lo, n_whole]) like scalar_tail_indices."""
+    block = block or ROCM_F16_BLOCK
+    parts = []
+    for key in keys:
+        off, n = int(key[0]), int(key[1])
+        lo, whole = (int(key[2]), int(key[3])) if len(key) > 2 else (0, n)
+        s, e = max(whole - whole % block, lo), min(whole, lo + n)
+        if s < e:
+            parts.append(np.arange(off + s - lo, off + e - lo, dtype=np.int64))
+    if not parts:
+        return np.empty(0, dtype=np.int64)
+    idx = np.concatenate(parts)
+    idx.sort()
+    return idx

@@ -45,3 +45,12 @@ def test_keys_at_offsets_and_build_without_vectors(monkeypatch):
     monkeypatch.setenv("NVFLARE_AMD_TORCH16_VEC_BLOCK", "0")
     assert torch16.vector_block() == 0
     assert torch16.scalar_tail_indices([(8, 5)], 1, 0).tolist() == [8, 9, 10, 11, 12]
+
+
+def test_rocm_f16_unrolled_elements():
+    """torch-ROCm's float16 add_: the last partial 2048-element block (all of a smaller tensor) is unrolled."""
+    assert torch16.rocm_f16_unrolled_indices([(0, 1500)]).tolist() == list(range(1500))
+    assert torch16.rocm_f16_unrolled_indices([(0, 2048)]).size == 0
+    assert torch16.rocm_f16_unrolled_indices([(16, 3072)]).tolist() == list(range(16 + 2048, 16 + 3072))
+    # a bucket [4096, 6149) of a 6149-element tensor: only the whole tensor's tail 6144.. is unrolled
+    assert torch16.rocm_f16_unrolled_indices([(0, 2053, 4096, 6149)]).tolist() == list(range(2048, 2053))
