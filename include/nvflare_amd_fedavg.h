@@ -72,9 +72,9 @@ enum fedavg_fin {
     FEDAVG_FIN_NONE = 0,
     FEDAVG_FIN_SCALE = 1,
     FEDAVG_FIN_DIV = 2,
-    /* torch-ROCm's div_ by a CPU scalar on device-resident tensors: a multiplication by the opmath reciprocal,
-     * T * (1.0f / float(count)) for fp32 / float16 / bfloat16 totals (rounded to the total's format),
-     * T * (1.0 / count) for fp64 (v6) */
+    /* torch-ROCm's div_ by a CPU scalar on device-resident tensors: a multiplication by the reciprocal, the
+     * fp64 quotient cast to the opmath type: T * (float)(1.0 / count) for fp32 / float16 / bfloat16 totals
+     * (rounded to the total's format), T * (1.0 / count) for fp64 (v6) */
     FEDAVG_FIN_RECIP = 3,
 };
 

@@ -341,15 +341,13 @@ void check_op_fin(int op, int fin) {
 
 // The fp32 / fp64 kernels know three steps and two finalisations; torch-ROCm's device-tensor arithmetic
 // (FEDAVG_OP_TORCH_DEVICE, FEDAVG_FIN_RECIP) maps onto them: the steps are FEDAVG_OP_TORCH's at these widths,
-// and the reciprocal becomes FEDAVG_FIN_SCALE with a count whose library scale -- acc_t(1.0 / count) -- is
-// torch's: for fp32, count' = 1 / (double)(1.0f / (float)count), so that (float)(1.0 / count') is exactly
-// 1.0f / (float)count (a double quotient within 2^-52 of a float cannot round to another float).
+// and torch's reciprocal -- the fp64 quotient 1.0 / count cast to the opmath type (measured against torch on the
+// GPU: tools/debug_device_f32.py) -- is exactly the library's FEDAVG_FIN_SCALE value acc_t(1.0 / count).
 void normalize_wide(int& op, int& fin, double& count, bool acc_f32) {
+    (void)count;
+    (void)acc_f32;
     if (op == FEDAVG_OP_TORCH_DEVICE) op = FEDAVG_OP_TORCH;
-    if (fin == FEDAVG_FIN_RECIP) {
-        fin = FEDAVG_FIN_SCALE;
-        if (acc_f32) count = 1.0 / (double)(1.0f / (float)count);
-    }
+    if (fin == FEDAVG_FIN_RECIP) fin = FEDAVG_FIN_SCALE;
 }
 
 // finalisation scalar, computed on the host exactly as the reference computes it:
@@ -520,8 +518,8 @@ float narrow_fin_value(int fmt, int fin, double count) {
         return fmt == FEDAVG_F16 ? half_value(1.0 / count) : bf16_value((float)(1.0 / count));
     if (fin == FEDAVG_FIN_DIV)  // torch: div_ by a CPU scalar in fp32
         return (float)count;
-    if (fin == FEDAVG_FIN_RECIP)  // torch-ROCm: multiply by the fp32 reciprocal (the kernel's SCALE form)
-        return 1.0f / (float)count;
+    if (fin == FEDAVG_FIN_RECIP)  // torch-ROCm: multiply by (float)(1.0 / count) (the kernel's SCALE form)
+        return (float)(1.0 / count);
     return 0.0f;
 }
 
