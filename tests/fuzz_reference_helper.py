@@ -308,6 +308,7 @@ def run_intime(cases: int, seed: int) -> dict:
             ex = {k: str(rng.choice(["", "bias", "w1"])) for k in subkeys} if collection else "bias"
         weigh = bool(rng.random() < 0.85)
         keys = {"w0": (int(rng.integers(1, 5000)),), "w1": (3, 7), "bias": (5,)}
+        vdt = str(rng.choice(["float32", "float32", "float64", "float16"] + (["bfloat16"] if container == "torch" else [])))
         kw = dict(exclude_vars=ex, aggregation_weights=aw, expected_data_kind=edk, weigh_by_local_iter=weigh)
         try:
             ref = R(**kw)
@@ -338,7 +339,7 @@ def run_intime(cases: int, seed: int) -> dict:
                     for k in subkeys:
                         if collection and odd < 0.05:
                             continue  # a COLLECTION missing a sub-DXO
-                        data = {n: _value(rng, s, "float32", container) for n, s in keys.items() if rng.random() < 0.85}
+                        data = {n: _value(rng, s, vdt, container) for n, s in keys.items() if rng.random() < 0.85}
                         kind = kinds[k] if odd >= 0.1 else DataKind.METRICS
                         meta = {} if steps is None else {MetaKey.NUM_STEPS_CURRENT_ROUND: steps}
                         sub[k] = DXO(kind, data=data, meta=meta)
