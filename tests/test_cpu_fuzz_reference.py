@@ -40,6 +40,28 @@ def test_random_rounds_match_reference(tmp_path, mode, seed, threads):
         assert stats["cases"] == 120 and stats["accepted"] > 200
 
 
+def test_recorded_fedopt_cases_regenerate():
+    """tests/golden/fuzz_fedopt_s31.json's inputs regenerate from its seed here: each case's optimizer,
+    container and per-round key sets (the reference's outputs carry every state key, the rounds' diffs a subset)
+    come out of fuzz_reference_fedopt.gen_case as recorded."""
+    import numpy as np
+
+    import fuzz_reference_fedopt as F
+
+    with open(os.path.join(HERE, "golden", "fuzz_fedopt_s31.json")) as f:
+        rec = json.load(f)
+    rng = np.random.default_rng(rec["seed"])
+    n_missing = 0
+    for r in rec["records"]:
+        spec = F.gen_case(rng)
+        assert spec["optimizer_args"]["path"] == r["optimizer"] and spec["container"] == r["container"]
+        state_keys = list(F.build_model(spec).state_dict())
+        for diff, exp in zip(spec["rounds"], r["rounds"]):
+            assert list(exp["weights"]) == state_keys
+            n_missing += len(state_keys) - len(diff)
+    assert n_missing > 10
+
+
 def test_recorded_reference_rounds_replay_on_the_fake_device(monkeypatch):
     """tests/golden/fuzz_helper_s21.json (the reference's result hashes for 200 random cases) replayed through
     the drop-in on the fake device -- the same check tests/test_gpu_fuzz_replay.py runs on the MI355X; this one
