@@ -315,7 +315,9 @@ int fedavg_set_launch(fedavg_ctx* ctx, int blocks_per_cu, int unroll);
  * bit 3 = each tile's results stored (epilogue run) as the tile finishes (the round-1 kernels);
  * bit 0 / bit 1 = the plain one with temporal client loads / temporal result stores (imply bit 3);
  * bit 2 = the per-tile epilogue kernel software-pipelined across tiles (the next tile's first client loads
- * overlap the epilogue; implies bit 3 for the epilogue).  Results are bit-identical in every variant. */
+ * overlap the epilogue; implies bit 3 for the epilogue);
+ * bit 4 = burst launches after the first of a call go out without the AQL barrier bit (hipExtAnyOrderLaunch),
+ * so one launch's blocks start as the previous launch drains.  Results are bit-identical in every variant. */
 int fedavg_set_variant(fedavg_ctx* ctx, int variant);
 /* Tile width used by fedavg_accumulate for contiguous rows (default 4096 elements). */
 int fedavg_set_tile(fedavg_ctx* ctx, int tile_elems);

@@ -1296,7 +1296,7 @@ int fedavg_accumulate_tiled_epi(fedavg_ctx* ctx, const void* const* bases, const
         L.op = op;
         L.fin = fin;
         L.unroll = fedavg::kDefaultUnroll;
-        L.variant = ctx->variant & (fedavg::kVariantEpiPrefetch | fedavg::kVariantTileStores);
+        L.variant = ctx->variant & (fedavg::kVariantEpiPrefetch | fedavg::kVariantTileStores | fedavg::kVariantAnyOrder);
         L.tile4 = (int64_t)tile_elems / 4;
         L.tstride4 = (int64_t)tile_stride / 4;
         L.b4 = (int64_t)begin / 4;
@@ -1374,7 +1374,7 @@ int fedavg_set_launch(fedavg_ctx* ctx, int blocks_per_cu, int unroll) {
 int fedavg_set_variant(fedavg_ctx* ctx, int variant) {
     return guarded([&] {
         if (!ctx) throw Error("ctx is NULL");
-        if (variant < 0 || variant > 15) throw Error("variant must be 0..15");
+        if (variant < 0 || variant > 31) throw Error("variant must be 0..31");
         ctx->variant = variant;
     });
 }

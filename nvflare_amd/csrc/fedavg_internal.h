@@ -1,6 +1,7 @@
 // fedavg_internal.h -- shared between the HIP kernels and the C-ABI layer (not installed).
 #pragma once
 
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -24,6 +25,9 @@ constexpr int kVariantTemporalStores = 2;  // per-tile-store kernel with tempora
 constexpr int kVariantEpiPrefetch = 4;     // epilogue kernel: software-pipelined across tiles (see fedavg_tiles_epi_f32x4)
 constexpr int kVariantTileStores = 8;      // plain aggregation on fedavg_tiles_f32x4 (each tile's results stored
                                            // when it finishes; implied by bits 0 and 1)
+constexpr int kVariantAnyOrder = 16;       // burst launches after an aggregation's first go without the AQL barrier
+                                           // bit (hipExtAnyOrderLaunch): launch i+1's blocks fill CUs as launch i
+                                           // drains; they touch disjoint tiles, and the next ordinary packet waits
 constexpr int kBurstTiles = 8;             // tiles per block per burst launch (results held in registers)
 
 // Per-launch client table passed BY VALUE in the kernarg segment: wave-uniform base pointers and
@@ -100,14 +104,17 @@ struct DequantLaunch {
 hipError_t launch_tiles_f32x4(const TileLaunch& L, hipStream_t s, uint64_t* launch_count = nullptr);
 
 // Host loop of a BURST kernel (fedavg_tiles.h): one launch per grid x tpb tiles of [t_first, t_stop), every
-// block holding its tpb tiles' results until the end of its launch; launch(blocks, t0, t_end) issues one.
+// block holding its tpb tiles' results until the end of its launch; launch(blocks, t0, t_end, flags) issues
+// one with hipExtLaunchKernel flags: 0 for the first, hipExtAnyOrderLaunch for the rest when any_order (the
+// first keeps the barrier bit, so it waits for the staging copies; the launches of one call touch disjoint tiles).
 template <typename Launch>
 inline hipError_t burst_launches(int64_t t_first, int64_t t_stop, int grid, int tpb, uint64_t* launch_count,
-                                 Launch&& launch) {
+                                 bool any_order, Launch&& launch) {
     const int64_t per = (int64_t)grid * tpb;
     for (int64_t t0 = t_first; t0 < t_stop; t0 += per) {
         const int64_t t_end = t0 + per < t_stop ? t0 + per : t_stop;
-        launch((int)(t_end - t0 < grid ? t_end - t0 : grid), t0, t_end);
+        launch((int)(t_end - t0 < grid ? t_end - t0 : grid), t0, t_end,
+               (any_order && t0 != t_first) ? (uint32_t)hipExtAnyOrderLaunch : 0u);
         const hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
         if (launch_count) ++*launch_count;

@@ -371,7 +371,7 @@ static hipError_t launch_t64_f(const RowTableGeneric& tab, int K, int64_t ts2, c
     f64x2* o = static_cast<f64x2*>(out);
     constexpr int64_t T2 = (int64_t)kCpl64 * kBlock;
     if (burst) {
-        return burst_launches(b2 / T2, (e2 - 1) / T2 + 1, grid, kBurstTiles64, nl, [&](int nb, int64_t t0, int64_t t_end) {
+        return burst_launches(b2 / T2, (e2 - 1) / T2 + 1, grid, kBurstTiles64, nl, false, [&](int nb, int64_t t0, int64_t t_end, uint32_t) {
             if (acc_in)
                 hipLaunchKernelGGL((fedavg_tiles_f64x2_burst<OP, FIN, true, kBurstTiles64>), dim3(nb), dim3(kBlock), 0, s,
                                    tab, K, ts2, ai, o, b2, e2, fin_val, t0, t_end);

@@ -344,7 +344,7 @@ static hipError_t launch_t16_a(const RowTableNarrow& tab, int K, int64_t tstride
     u32x4* o = static_cast<u32x4*>(out);
     constexpr int64_t T8 = (int64_t)kCpl16 * kBlock;
     if (burst) {
-        return burst_launches(b8 / T8, (e8 - 1) / T8 + 1, grid, kBurstTiles, nl, [&](int nb, int64_t t0, int64_t t_end) {
+        return burst_launches(b8 / T8, (e8 - 1) / T8 + 1, grid, kBurstTiles, nl, false, [&](int nb, int64_t t0, int64_t t_end, uint32_t) {
             if (acc_in)
                 hipLaunchKernelGGL((fedavg_tiles_narrow_burst<FMT, OP, FIN, true, kBurstTiles>), dim3(nb), dim3(kBlock), 0,
                                    s, tab, K, tstride8, ai, o, b8, e8, fv, t0, t_end);

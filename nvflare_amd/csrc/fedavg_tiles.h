@@ -116,10 +116,12 @@ template <int OP, int FIN, bool ACC_IN, int UNROLL, int CPL, int TPB>
 inline hipError_t launch_burst(const TileLaunch& L, hipStream_t s, uint64_t* nl) {
     const f32x4* ai = reinterpret_cast<const f32x4*>(L.acc_in);
     f32x4* o = reinterpret_cast<f32x4*>(L.out);
-    return burst_launches(L.b4 / L.tile4, (L.e4 - 1) / L.tile4 + 1, L.grid, TPB, nl, [&](int nb, int64_t t0, int64_t t_end) {
-        hipLaunchKernelGGL((fedavg_tiles_burst_f32x4<OP, FIN, ACC_IN, UNROLL, CPL, TPB>), dim3(nb), dim3(kBlock), 0, s,
-                           L.tab, L.k, L.tstride4, ai, o, L.b4, L.e4, L.fin_val, t0, t_end);
-    });
+    return burst_launches(L.b4 / L.tile4, (L.e4 - 1) / L.tile4 + 1, L.grid, TPB, nl, L.variant & kVariantAnyOrder,
+                          [&](int nb, int64_t t0, int64_t t_end, uint32_t flags) {
+                              hipExtLaunchKernelGGL((fedavg_tiles_burst_f32x4<OP, FIN, ACC_IN, UNROLL, CPL, TPB>),
+                                                    dim3(nb), dim3(kBlock), 0, s, nullptr, nullptr, flags, L.tab, L.k,
+                                                    L.tstride4, ai, o, L.b4, L.e4, L.fin_val, t0, t_end);
+                          });
 }
 
 template <int OP, int FIN, bool ACC_IN, int UNROLL, int CPL>
