@@ -317,7 +317,10 @@ int fedavg_set_launch(fedavg_ctx* ctx, int blocks_per_cu, int unroll);
  * bit 2 = the per-tile epilogue kernel software-pipelined across tiles (the next tile's first client loads
  * overlap the epilogue; implies bit 3 for the epilogue);
  * bit 4 = burst launches after the first of a call go out without the AQL barrier bit (hipExtAnyOrderLaunch),
- * so one launch's blocks start as the previous launch drains.  Results are bit-identical in every variant. */
+ * so one launch's blocks start as the previous launch drains;
+ * bit 5 = the plain burst kernel WITHOUT its 4 LDS-held tiles per block (default: 8 tiles' results in registers
+ * and 4 in LDS, 12 tiles per block per launch; with bit 5, 8).
+ * Results are bit-identical in every variant. */
 int fedavg_set_variant(fedavg_ctx* ctx, int variant);
 /* Tile width used by fedavg_accumulate for contiguous rows (default 4096 elements). */
 int fedavg_set_tile(fedavg_ctx* ctx, int tile_elems);

@@ -1374,7 +1374,7 @@ int fedavg_set_launch(fedavg_ctx* ctx, int blocks_per_cu, int unroll) {
 int fedavg_set_variant(fedavg_ctx* ctx, int variant) {
     return guarded([&] {
         if (!ctx) throw Error("ctx is NULL");
-        if (variant < 0 || variant > 31) throw Error("variant must be 0..31");
+        if (variant < 0 || variant > 63) throw Error("variant must be 0..63");
         ctx->variant = variant;
     });
 }

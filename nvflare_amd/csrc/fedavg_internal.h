@@ -28,7 +28,11 @@ constexpr int kVariantTileStores = 8;      // plain aggregation on fedavg_tiles_
 constexpr int kVariantAnyOrder = 16;       // burst launches after an aggregation's first go without the AQL barrier
                                            // bit (hipExtAnyOrderLaunch): launch i+1's blocks fill CUs as launch i
                                            // drains; they touch disjoint tiles, and the next ordinary packet waits
+constexpr int kVariantRegisterTiles = 32;  // plain burst kernel without its kBurstLdsTiles LDS-held tiles (by default
+                                           // each block also holds 4 tiles' results in LDS: 1.5x longer launches,
+                                           // +0.3 to +1.5 points at 8-64 clients, profiles/r02/ab/lds_tiles/)
 constexpr int kBurstTiles = 8;             // tiles per block per burst launch (results held in registers)
+constexpr int kBurstLdsTiles = 4;          // 4 x 16 KiB of LDS per block (2 blocks fit a CU)
 
 // Per-launch client table passed BY VALUE in the kernarg segment: wave-uniform base pointers and
 // weights are loaded with s_load into SGPRs.

@@ -78,21 +78,41 @@ __global__ void __launch_bounds__(kBlock) fedavg_tiles_f32x4(const RowTableF32 t
 // issues one launch per grid x TPB tiles.  One block per CU (one wave per SIMD, registers for the staged
 // results and a whole client group's loads in flight).
 // ---------------------------------------------------------------------------------------------
-template <int OP, int FIN, bool ACC_IN, int UNROLL, int CPL, int TPB>
+// TPB_LDS > 0 (the default; launch variant bit 5 turns it off): TPB_LDS more tiles per block whose results wait in LDS (each lane
+// reads back only what it wrote, so no barrier), making each launch (TPB + TPB_LDS) / TPB times longer.
+template <int OP, int FIN, bool ACC_IN, int UNROLL, int CPL, int TPB, int TPB_LDS = 0>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, 1)))
 fedavg_tiles_burst_f32x4(const RowTableF32 tab, const int K, const int64_t tstride4, const f32x4* acc_in, f32x4* out,
                          const int64_t b4, const int64_t e4, const float fin_val, const int64_t t0, const int64_t t_end) {
     constexpr int64_t T4 = (int64_t)CPL * kBlock;
     f32x4 res[TPB][CPL];
+    __shared__ f32x4 staged[TPB_LDS > 0 ? TPB_LDS * CPL * kBlock : 1];
 #pragma unroll
-    for (int m = 0; m < TPB; ++m) {
+    for (int m = 0; m < TPB + TPB_LDS; ++m) {
         const int64_t t = t0 + blockIdx.x + (int64_t)m * gridDim.x;
         if (t < t_end) {
             f32x4 acc[CPL];
             tile_sum<OP, ACC_IN, UNROLL, CPL, true>(acc, tab, K, t * tstride4 + threadIdx.x, t * T4 + threadIdx.x,
                                                     acc_in, b4, e4);
 #pragma unroll
-            for (int c = 0; c < CPL; ++c) res[m][c] = fin4<FIN>(acc[c], fin_val);
+            for (int c = 0; c < CPL; ++c) {
+                if (m < TPB)
+                    res[m < TPB ? m : 0][c] = fin4<FIN>(acc[c], fin_val);
+                else
+                    staged[((m - TPB) * CPL + c) * kBlock + threadIdx.x] = fin4<FIN>(acc[c], fin_val);
+            }
+        }
+    }
+#pragma unroll
+    for (int m = TPB; m < TPB + TPB_LDS; ++m) {
+        const int64_t t = t0 + blockIdx.x + (int64_t)m * gridDim.x;
+        if (t < t_end) {
+#pragma unroll
+            for (int c = 0; c < CPL; ++c) {
+                const int64_t i = t * T4 + threadIdx.x + c * kBlock;
+                if (i >= b4 && i < e4)
+                    __builtin_nontemporal_store(staged[((m - TPB) * CPL + c) * kBlock + threadIdx.x], out + i);
+            }
         }
     }
 #pragma unroll
@@ -111,14 +131,14 @@ fedavg_tiles_burst_f32x4(const RowTableF32 tab, const int K, const int64_t tstri
 // ---------------------------------------------------------------------------------------------
 // launchers
 // ---------------------------------------------------------------------------------------------
-// one launch per grid x TPB tiles (fedavg_tiles_burst_f32x4)
-template <int OP, int FIN, bool ACC_IN, int UNROLL, int CPL, int TPB>
+// one launch per grid x (TPB + TPB_LDS) tiles (fedavg_tiles_burst_f32x4)
+template <int OP, int FIN, bool ACC_IN, int UNROLL, int CPL, int TPB, int TPB_LDS = 0>
 inline hipError_t launch_burst(const TileLaunch& L, hipStream_t s, uint64_t* nl) {
     const f32x4* ai = reinterpret_cast<const f32x4*>(L.acc_in);
     f32x4* o = reinterpret_cast<f32x4*>(L.out);
-    return burst_launches(L.b4 / L.tile4, (L.e4 - 1) / L.tile4 + 1, L.grid, TPB, nl, L.variant & kVariantAnyOrder,
-                          [&](int nb, int64_t t0, int64_t t_end, uint32_t flags) {
-                              hipExtLaunchKernelGGL((fedavg_tiles_burst_f32x4<OP, FIN, ACC_IN, UNROLL, CPL, TPB>),
+    return burst_launches(L.b4 / L.tile4, (L.e4 - 1) / L.tile4 + 1, L.grid, TPB + TPB_LDS, nl,
+                          L.variant & kVariantAnyOrder, [&](int nb, int64_t t0, int64_t t_end, uint32_t flags) {
+                              hipExtLaunchKernelGGL((fedavg_tiles_burst_f32x4<OP, FIN, ACC_IN, UNROLL, CPL, TPB, TPB_LDS>),
                                                     dim3(nb), dim3(kBlock), 0, s, nullptr, nullptr, flags, L.tab, L.k,
                                                     L.tstride4, ai, o, L.b4, L.e4, L.fin_val, t0, t_end);
                           });
@@ -129,8 +149,13 @@ inline hipError_t launch_tiles_v(const TileLaunch& L, hipStream_t s, uint64_t* n
     const f32x4* ai = reinterpret_cast<const f32x4*>(L.acc_in);
     f32x4* o = reinterpret_cast<f32x4*>(L.out);
     if constexpr (CPL * (UNROLL + kBurstTiles) <= 64) {  // staged results + a group's loads within 256 VGPRs
-        if (!(L.variant & (kVariantTileStores | kVariantTemporalLoads | kVariantTemporalStores)))
+        if (!(L.variant & (kVariantTileStores | kVariantTemporalLoads | kVariantTemporalStores))) {
+            if constexpr (CPL == 4 && UNROLL == 4) {  // the default geometry only (build time)
+                if (!(L.variant & kVariantRegisterTiles))
+                    return launch_burst<OP, FIN, ACC_IN, UNROLL, CPL, kBurstTiles, kBurstLdsTiles>(L, s, nl);
+            }
             return launch_burst<OP, FIN, ACC_IN, UNROLL, CPL, kBurstTiles>(L, s, nl);
+        }
     }
     const bool ntl = !(L.variant & kVariantTemporalLoads);
     const bool nts = !(L.variant & kVariantTemporalStores);

@@ -268,7 +268,7 @@ def test_kernel_generic_dtypes(ctx, oracle, in_dt, acc_dt):
         assert same_bits(got, exp)
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 8])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 8, 16, 32])
 @pytest.mark.parametrize("bpc,unroll,tile", [(1, 4, 1024), (2, 8, 2048), (4, 4, 4096), (8, 8, 8192), (2, 4, 4096),
                                              (0, 0, 4096), (1, 8, 4096)])
 def test_launch_variants_same_bits(ctx, oracle, bpc, unroll, tile, variant):
