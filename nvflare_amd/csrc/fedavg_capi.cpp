@@ -1296,7 +1296,8 @@ int fedavg_accumulate_tiled_epi(fedavg_ctx* ctx, const void* const* bases, const
         L.op = op;
         L.fin = fin;
         L.unroll = fedavg::kDefaultUnroll;
-        L.variant = ctx->variant & (fedavg::kVariantEpiPrefetch | fedavg::kVariantTileStores | fedavg::kVariantAnyOrder);
+        L.variant = ctx->variant & (fedavg::kVariantEpiPrefetch | fedavg::kVariantTileStores | fedavg::kVariantAnyOrder |
+                                    fedavg::kVariantRegisterTiles);
         L.tile4 = (int64_t)tile_elems / 4;
         L.tstride4 = (int64_t)tile_stride / 4;
         L.b4 = (int64_t)begin / 4;

@@ -249,8 +249,9 @@ __device__ __forceinline__ void epilogue4(const EpiParams& E, const int64_t i, c
 // tiles; the aggregated differences d of all of them stay in registers while the client stream runs, and
 // the epilogue (operand loads, optimizer arithmetic, the state / parameter stores) runs for all TPB tiles
 // at the end of the launch -- the client-read phase carries no writes, and every block's epilogue phase
-// falls at about the same time.  `out` (when given) also receives d, as in the per-tile kernel.
-template <int OP, int FIN, bool ACC_IN, int EPI, int TPB>
+// falls at about the same time.  `out` (when given) also receives d, as in the per-tile kernel.  TPB_LDS > 0:
+// that many more tiles per block, their d held in LDS (each lane reads back only what it wrote).
+template <int OP, int FIN, bool ACC_IN, int EPI, int TPB, int TPB_LDS = 0>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, 1)))
 fedavg_tiles_epi_burst_f32x4(const RowTableF32 tab, const int K, const int64_t tstride4, const f32x4* acc_in,
                              f32x4* out, const int64_t b4, const int64_t e4, const float fin_val, const EpiParams E,
@@ -258,16 +259,23 @@ fedavg_tiles_epi_burst_f32x4(const RowTableF32 tab, const int K, const int64_t t
     constexpr int UNROLL = kDefaultUnroll;
     constexpr int CPL = kDefaultTile / (4 * kBlock);
     constexpr int64_t T4 = (int64_t)CPL * kBlock;
+    constexpr int NT = TPB + TPB_LDS;
     f32x4 dd[TPB][CPL];
+    __shared__ f32x4 staged[TPB_LDS > 0 ? TPB_LDS * CPL * kBlock : 1];
 #pragma unroll
-    for (int m = 0; m < TPB; ++m) {
+    for (int m = 0; m < NT; ++m) {
         const int64_t t = t0 + blockIdx.x + (int64_t)m * gridDim.x;
         if (t < t_end) {
             f32x4 acc[CPL];
             tile_sum<OP, ACC_IN, UNROLL, CPL, true>(acc, tab, K, t * tstride4 + threadIdx.x, t * T4 + threadIdx.x, acc_in,
                                                     b4, e4);
 #pragma unroll
-            for (int c = 0; c < CPL; ++c) dd[m][c] = fin4<FIN>(acc[c], fin_val);
+            for (int c = 0; c < CPL; ++c) {
+                if (m < TPB)
+                    dd[m < TPB ? m : 0][c] = fin4<FIN>(acc[c], fin_val);
+                else
+                    staged[((m - TPB) * CPL + c) * kBlock + threadIdx.x] = fin4<FIN>(acc[c], fin_val);
+            }
         }
     }
     // Epilogue phase, double-buffered: tile m+1's operand loads are issued before tile m's arithmetic and
@@ -289,16 +297,17 @@ fedavg_tiles_epi_burst_f32x4(const RowTableF32 tab, const int K, const int64_t t
     EpiIn pre[2][CPL];
     operands(pre[0], 0);
 #pragma unroll
-    for (int m = 0; m < TPB; ++m) {
-        if (m + 1 < TPB) operands(pre[(m + 1) & 1], m + 1);
+    for (int m = 0; m < NT; ++m) {
+        if (m + 1 < NT) operands(pre[(m + 1) & 1], m + 1);
         const int64_t t = t_base + (int64_t)m * gridDim.x;
         if (t < t_end) {
 #pragma unroll
             for (int c = 0; c < CPL; ++c) {
                 const int64_t i = t * T4 + threadIdx.x + c * kBlock;
                 if (i >= b4 && i < e4) {
-                    if (out != nullptr && EPI != FEDAVG_EPI_ADD_BASE) store4<true>(out + i, dd[m][c]);
-                    epilogue4<EPI>(E, i, dd[m][c], pre[m & 1][c], out);
+                    const f32x4 d = m < TPB ? dd[m < TPB ? m : 0][c] : staged[((m - TPB) * CPL + c) * kBlock + threadIdx.x];
+                    if (out != nullptr && EPI != FEDAVG_EPI_ADD_BASE) store4<true>(out + i, d);
+                    epilogue4<EPI>(E, i, d, pre[m & 1][c], out);
                 }
             }
         }
@@ -410,6 +419,14 @@ inline hipError_t launch_epi_k(const TileLaunch& L, const EpiParams& E, hipStrea
     const f32x4* ai = reinterpret_cast<const f32x4*>(L.acc_in);
     f32x4* o = reinterpret_cast<f32x4*>(L.out);
     if (!(L.variant & (kVariantTileStores | kVariantEpiPrefetch))) {  // burst: one launch per grid x TPB tiles
+        if (!(L.variant & kVariantRegisterTiles))  // default: 4 more tiles per block with d held in LDS
+            return burst_launches(L.b4 / L.tile4, (L.e4 - 1) / L.tile4 + 1, L.grid, kBurstTiles + kBurstLdsTiles, nl,
+                                  L.variant & kVariantAnyOrder, [&](int nb, int64_t t0, int64_t t_end, uint32_t flags) {
+                                      hipExtLaunchKernelGGL(
+                                          (fedavg_tiles_epi_burst_f32x4<OP, FIN, ACC_IN, EPI, kBurstTiles, kBurstLdsTiles>),
+                                          dim3(nb), dim3(kBlock), 0, s, nullptr, nullptr, flags, L.tab, L.k, L.tstride4,
+                                          ai, o, L.b4, L.e4, L.fin_val, E, t0, t_end);
+                                  });
         return burst_launches(L.b4 / L.tile4, (L.e4 - 1) / L.tile4 + 1, L.grid, kBurstTiles, nl,
                               L.variant & kVariantAnyOrder, [&](int nb, int64_t t0, int64_t t_end, uint32_t flags) {
                                   hipExtLaunchKernelGGL(
