@@ -595,7 +595,8 @@ void run_tiles_narrow(fedavg_ctx* ctx, const void* const* bases, const double* w
             ++ctx->launches;
         }
         HIP_CHECK(fedavg::launch_tiles_narrow(t, kc, tstride, cur_in, out, begin, end, fmt, narrow_kernel_op(op),
-                                              last ? narrow_kernel_fin(fin) : FEDAVG_FIN_NONE, fv, grid, burst, s,
+                                              last ? narrow_kernel_fin(fin) : FEDAVG_FIN_NONE, fv, grid,
+                                              burst ? ((ctx->variant & fedavg::kVariantRegisterTiles) ? 1 : 2) : 0, s,
                                               &ctx->launches));
         if (n_tails) {
             HIP_CHECK(fedavg::launch_scatter16(tails, tail_vals, n_tails, out, s));
@@ -1206,7 +1207,9 @@ int fedavg_accumulate_tiled64(fedavg_ctx* ctx, const void* const* bases, const d
             }
             const bool last = k0 + kc >= k_rows;
             HIP_CHECK(fedavg::launch_tiles_f64(t, kc, (int64_t)tile_stride, cur_in, out, (int64_t)begin, (int64_t)end,
-                                               op, last ? fin : FEDAVG_FIN_NONE, fv, grid, burst, s, &ctx->launches));
+                                               op, last ? fin : FEDAVG_FIN_NONE, fv, grid,
+                                               burst ? ((ctx->variant & fedavg::kVariantRegisterTiles) ? 1 : 2) : 0, s,
+                                               &ctx->launches));
             cur_in = out;
             k0 += kc;
         } while (k0 < k_rows);

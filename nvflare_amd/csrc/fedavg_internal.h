@@ -159,15 +159,17 @@ hipError_t launch_rows_generic(const RowTableGeneric& tab, int K, const void* ac
                                hipStream_t s);
 hipError_t launch_rows_narrow(const RowTableNarrow& tab, int K, const void* acc_in, void* out, int64_t n, int fmt,
                               int op, int fin, float fin_val, int grid, hipStream_t s);
-// burst: the burst form (results held per block, stored at the end of each short launch); otherwise one
-// launch of the per-tile-store kernel.  launch_count is incremented per launch.
+// burst: 2 = the burst form with LDS-held tiles (the default), 1 = the burst form with register-held tiles only
+// (results held per block, stored at the end of each short launch), 0 = one launch of the per-tile-store kernel.
+// launch_count is incremented per launch.
 hipError_t launch_tiles_narrow(const RowTableNarrow& tab, int K, int64_t tstride_elems, const void* acc_in, void* out,
                                int64_t begin, int64_t end, int fmt, int op, int fin, float fin_val, int grid,
-                               bool burst, hipStream_t s, uint64_t* launch_count);
+                               int burst, hipStream_t s, uint64_t* launch_count);
+constexpr int kBurstLdsTiles16 = 8;  // 16-bit burst kernel: 8 x 8 KiB of LDS per block (2 blocks fit a CU)
 constexpr int kTile16Elems = 4096;  // the only tile width of the 16-bit tiled kernel
 constexpr int kTile64Elems = 4096;  // the only tile width of the fp64 tiled kernel
 hipError_t launch_tiles_f64(const RowTableGeneric& tab, int K, int64_t tstride_elems, const void* acc_in, void* out,
-                            int64_t begin, int64_t end, int op, int fin, double fin_val, int grid, bool burst,
+                            int64_t begin, int64_t end, int op, int fin, double fin_val, int grid, int burst,
                             hipStream_t s, uint64_t* launch_count);
 hipError_t launch_fill_synthetic_f32(float* dst, int64_t n, int64_t tile, int64_t tstride, uint64_t seed, uint64_t row,
                                      uint64_t col0, int grid, hipStream_t s);

@@ -108,6 +108,7 @@ constexpr int kCpl64 = kTile64Elems / (2 * kBlock);  // 8
 #define FEDAVG_F64_UNROLL 2  // clients whose loads are in flight together (16 x 16 B per lane)
 #endif
 constexpr int kBurstTiles64 = 4;  // tiles per block per burst launch: 4 x kCpl64 staged pairs = 128 VGPRs
+constexpr int kBurstLdsTiles64 = 2;  // and 2 more in LDS: 2 x 32 KiB per block (2 blocks fit a CU)
 
 // One tile's arrival-ordered sum for this lane's kCpl64 pairs, finalised.
 template <int OP, int FIN, bool ACC_IN>
@@ -179,19 +180,45 @@ __global__ void __launch_bounds__(kBlock) fedavg_tiles_f64x2(const RowTableGener
 
 // BURST form (the default; fedavg_tiles.h fedavg_tiles_burst_f32x4): TPB tiles per block per launch, results
 // held in registers (kCpl64 pairs per tile) and stored after the block's last tile.
-template <int OP, int FIN, bool ACC_IN, int TPB>
+// TPB_LDS > 0 (the default, burst mode 2): that many more tiles per block, results held in LDS (32 KiB per tile;
+// each lane reads back only what it wrote), in rolled loops so the tile body is not copied TPB_LDS more times.
+template <int OP, int FIN, bool ACC_IN, int TPB, int TPB_LDS = 0>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, 1)))
 fedavg_tiles_f64x2_burst(const RowTableGeneric tab, const int K, const int64_t tstride2, const f64x2* acc_in,
                          f64x2* out, const int64_t b2, const int64_t e2, const double fin_val, const int64_t t0,
                          const int64_t t_end) {
     constexpr int64_t T2 = (int64_t)kCpl64 * kBlock;
     f64x2 res[TPB][kCpl64];
+    __shared__ f64x2 staged[TPB_LDS > 0 ? TPB_LDS * kCpl64 * kBlock : 1];
 #pragma unroll
     for (int m = 0; m < TPB; ++m) {
         const int64_t t = t0 + blockIdx.x + (int64_t)m * gridDim.x;
         if (t < t_end)
             tile_sum64<OP, FIN, ACC_IN>(res[m], tab, K, t * tstride2 + threadIdx.x, t * T2 + threadIdx.x, acc_in, b2, e2,
                                         fin_val);
+    }
+#pragma unroll 1
+    for (int m = TPB; m < TPB + TPB_LDS; ++m) {
+        const int64_t t = t0 + blockIdx.x + (int64_t)m * gridDim.x;
+        if (t < t_end) {
+            f64x2 r[kCpl64];
+            tile_sum64<OP, FIN, ACC_IN>(r, tab, K, t * tstride2 + threadIdx.x, t * T2 + threadIdx.x, acc_in, b2, e2,
+                                        fin_val);
+#pragma unroll
+            for (int c = 0; c < kCpl64; ++c) staged[((m - TPB) * kCpl64 + c) * kBlock + threadIdx.x] = r[c];
+        }
+    }
+#pragma unroll 1
+    for (int m = TPB; m < TPB + TPB_LDS; ++m) {
+        const int64_t t = t0 + blockIdx.x + (int64_t)m * gridDim.x;
+        if (t < t_end) {
+#pragma unroll
+            for (int c = 0; c < kCpl64; ++c) {
+                const int64_t i = t * T2 + threadIdx.x + c * kBlock;
+                if (i >= b2 && i < e2)
+                    __builtin_nontemporal_store(staged[((m - TPB) * kCpl64 + c) * kBlock + threadIdx.x], out + i);
+            }
+        }
     }
 #pragma unroll
     for (int m = 0; m < TPB; ++m) {
@@ -366,10 +393,21 @@ static hipError_t launch_rows_f64x2(const RowTableGeneric& tab, int K, const voi
 
 template <int OP, int FIN>
 static hipError_t launch_t64_f(const RowTableGeneric& tab, int K, int64_t ts2, const void* acc_in, void* out, int64_t b2,
-                               int64_t e2, double fin_val, int grid, bool burst, hipStream_t s, uint64_t* nl) {
+                               int64_t e2, double fin_val, int grid, int burst, hipStream_t s, uint64_t* nl) {
     const f64x2* ai = static_cast<const f64x2*>(acc_in);
     f64x2* o = static_cast<f64x2*>(out);
     constexpr int64_t T2 = (int64_t)kCpl64 * kBlock;
+    if (burst == 2) {  // default: kBurstTiles64 in registers + kBurstLdsTiles64 in LDS per block and launch
+        return burst_launches(b2 / T2, (e2 - 1) / T2 + 1, grid, kBurstTiles64 + kBurstLdsTiles64, nl, false,
+                              [&](int nb, int64_t t0, int64_t t_end, uint32_t) {
+            if (acc_in)
+                hipLaunchKernelGGL((fedavg_tiles_f64x2_burst<OP, FIN, true, kBurstTiles64, kBurstLdsTiles64>), dim3(nb),
+                                   dim3(kBlock), 0, s, tab, K, ts2, ai, o, b2, e2, fin_val, t0, t_end);
+            else
+                hipLaunchKernelGGL((fedavg_tiles_f64x2_burst<OP, FIN, false, kBurstTiles64, kBurstLdsTiles64>), dim3(nb),
+                                   dim3(kBlock), 0, s, tab, K, ts2, ai, o, b2, e2, fin_val, t0, t_end);
+        });
+    }
     if (burst) {
         return burst_launches(b2 / T2, (e2 - 1) / T2 + 1, grid, kBurstTiles64, nl, false, [&](int nb, int64_t t0, int64_t t_end, uint32_t) {
             if (acc_in)
@@ -393,7 +431,7 @@ static hipError_t launch_t64_f(const RowTableGeneric& tab, int K, int64_t ts2, c
 
 template <int OP>
 static hipError_t launch_t64_o(const RowTableGeneric& tab, int K, int64_t ts2, const void* acc_in, void* out, int64_t b2,
-                               int64_t e2, int fin, double fin_val, int grid, bool burst, hipStream_t s, uint64_t* nl) {
+                               int64_t e2, int fin, double fin_val, int grid, int burst, hipStream_t s, uint64_t* nl) {
     switch (fin) {
         case FEDAVG_FIN_SCALE:
             return launch_t64_f<OP, FEDAVG_FIN_SCALE>(tab, K, ts2, acc_in, out, b2, e2, fin_val, grid, burst, s, nl);
@@ -405,7 +443,7 @@ static hipError_t launch_t64_o(const RowTableGeneric& tab, int K, int64_t ts2, c
 }
 
 hipError_t launch_tiles_f64(const RowTableGeneric& tab, int K, int64_t tstride_elems, const void* acc_in, void* out,
-                            int64_t begin, int64_t end, int op, int fin, double fin_val, int grid, bool burst,
+                            int64_t begin, int64_t end, int op, int fin, double fin_val, int grid, int burst,
                             hipStream_t s, uint64_t* nl) {
     const int64_t ts2 = tstride_elems / 2, b2 = begin / 2, e2 = end / 2;
     switch (op) {

@@ -311,18 +311,45 @@ __global__ void __launch_bounds__(kBlock) fedavg_tiles_narrow(const RowTableNarr
 // block per launch, their packed results held in registers and stored after the block's last tile; client
 // loads grouped from client 0 on (bf16 64 x 1e9: 85.6 % against 84.4 % ungrouped and 82.0 % for the per-tile
 // form, profiles/r02/ab/narrow_burst_grouped.jsonl).
-template <int FMT, int OP, int FIN, bool ACC_IN, int TPB>
+// TPB_LDS > 0 (the default; burst mode 2): that many more tiles per block, their packed results held in LDS
+// (8 KiB per tile; each lane reads back only what it wrote) -- launches (TPB + TPB_LDS) / TPB times longer.
+template <int FMT, int OP, int FIN, bool ACC_IN, int TPB, int TPB_LDS = 0>
 __global__ void __launch_bounds__(kBlock)
 __attribute__((amdgpu_waves_per_eu(FEDAVG_NARROW_BURST_WAVES, FEDAVG_NARROW_BURST_WAVES))) fedavg_tiles_narrow_burst(const RowTableNarrow tab, const int K, const int64_t tstride8, const u32x4* acc_in, u32x4* out,
                           const int64_t b8, const int64_t e8, const float fv, const int64_t t0, const int64_t t_end) {
     constexpr int64_t T8 = (int64_t)kCpl16 * kBlock;
     u32x4 res[TPB][kCpl16];
+    __shared__ u32x4 staged[TPB_LDS > 0 ? TPB_LDS * kCpl16 * kBlock : 1];
 #pragma unroll
     for (int m = 0; m < TPB; ++m) {
         const int64_t t = t0 + blockIdx.x + (int64_t)m * gridDim.x;
         if (t < t_end)
             tile_sum16<FMT, OP, FIN, ACC_IN, true>(res[m], tab, K, t * tstride8 + threadIdx.x, t * T8 + threadIdx.x,
                                                    acc_in, b8, e8, fv);
+    }
+    // the LDS-held tiles in a rolled loop: one more copy of the (long) tile body, not TPB_LDS of them
+#pragma unroll 1
+    for (int m = TPB; m < TPB + TPB_LDS; ++m) {
+        const int64_t t = t0 + blockIdx.x + (int64_t)m * gridDim.x;
+        if (t < t_end) {
+            u32x4 r[kCpl16];
+            tile_sum16<FMT, OP, FIN, ACC_IN, true>(r, tab, K, t * tstride8 + threadIdx.x, t * T8 + threadIdx.x, acc_in,
+                                                   b8, e8, fv);
+#pragma unroll
+            for (int c = 0; c < kCpl16; ++c) staged[((m - TPB) * kCpl16 + c) * kBlock + threadIdx.x] = r[c];
+        }
+    }
+#pragma unroll 1
+    for (int m = TPB; m < TPB + TPB_LDS; ++m) {
+        const int64_t t = t0 + blockIdx.x + (int64_t)m * gridDim.x;
+        if (t < t_end) {
+#pragma unroll
+            for (int c = 0; c < kCpl16; ++c) {
+                const int64_t i = t * T8 + threadIdx.x + c * kBlock;
+                if (i >= b8 && i < e8)
+                    __builtin_nontemporal_store(staged[((m - TPB) * kCpl16 + c) * kBlock + threadIdx.x], out + i);
+            }
+        }
     }
 #pragma unroll
     for (int m = 0; m < TPB; ++m) {
@@ -339,10 +366,21 @@ __attribute__((amdgpu_waves_per_eu(FEDAVG_NARROW_BURST_WAVES, FEDAVG_NARROW_BURS
 
 template <int FMT, int OP, int FIN>
 static hipError_t launch_t16_a(const RowTableNarrow& tab, int K, int64_t tstride8, const void* acc_in, void* out,
-                               int64_t b8, int64_t e8, float fv, int grid, bool burst, hipStream_t s, uint64_t* nl) {
+                               int64_t b8, int64_t e8, float fv, int grid, int burst, hipStream_t s, uint64_t* nl) {
     const u32x4* ai = static_cast<const u32x4*>(acc_in);
     u32x4* o = static_cast<u32x4*>(out);
     constexpr int64_t T8 = (int64_t)kCpl16 * kBlock;
+    if (burst == 2) {  // default: kBurstTiles in registers + kBurstLdsTiles16 in LDS per block and launch
+        return burst_launches(b8 / T8, (e8 - 1) / T8 + 1, grid, kBurstTiles + kBurstLdsTiles16, nl, false,
+                              [&](int nb, int64_t t0, int64_t t_end, uint32_t) {
+            if (acc_in)
+                hipLaunchKernelGGL((fedavg_tiles_narrow_burst<FMT, OP, FIN, true, kBurstTiles, kBurstLdsTiles16>), dim3(nb),
+                                   dim3(kBlock), 0, s, tab, K, tstride8, ai, o, b8, e8, fv, t0, t_end);
+            else
+                hipLaunchKernelGGL((fedavg_tiles_narrow_burst<FMT, OP, FIN, false, kBurstTiles, kBurstLdsTiles16>), dim3(nb),
+                                   dim3(kBlock), 0, s, tab, K, tstride8, ai, o, b8, e8, fv, t0, t_end);
+        });
+    }
     if (burst) {
         return burst_launches(b8 / T8, (e8 - 1) / T8 + 1, grid, kBurstTiles, nl, false, [&](int nb, int64_t t0, int64_t t_end, uint32_t) {
             if (acc_in)
@@ -366,7 +404,7 @@ static hipError_t launch_t16_a(const RowTableNarrow& tab, int K, int64_t tstride
 
 template <int FMT, int OP>
 static hipError_t launch_t16_f(const RowTableNarrow& tab, int K, int64_t tstride8, const void* acc_in, void* out,
-                               int64_t b8, int64_t e8, int fin, float fv, int grid, bool burst, hipStream_t s,
+                               int64_t b8, int64_t e8, int fin, float fv, int grid, int burst, hipStream_t s,
                                uint64_t* nl) {
     switch (fin) {
         case FEDAVG_FIN_SCALE:
@@ -380,7 +418,7 @@ static hipError_t launch_t16_f(const RowTableNarrow& tab, int K, int64_t tstride
 
 template <int FMT>
 static hipError_t launch_t16_o(const RowTableNarrow& tab, int K, int64_t tstride8, const void* acc_in, void* out,
-                               int64_t b8, int64_t e8, int op, int fin, float fv, int grid, bool burst, hipStream_t s,
+                               int64_t b8, int64_t e8, int op, int fin, float fv, int grid, int burst, hipStream_t s,
                                uint64_t* nl) {
     switch (op) {
         case FEDAVG_OP_TORCH_DEVICE:  // same steps; the host keeps alpha in fp32 in the table
@@ -396,7 +434,7 @@ static hipError_t launch_t16_o(const RowTableNarrow& tab, int K, int64_t tstride
 
 hipError_t launch_tiles_narrow(const RowTableNarrow& tab, int K, int64_t tstride_elems, const void* acc_in, void* out,
                                int64_t begin, int64_t end, int fmt, int op, int fin, float fin_val, int grid,
-                               bool burst, hipStream_t s, uint64_t* nl) {
+                               int burst, hipStream_t s, uint64_t* nl) {
     const int64_t ts8 = tstride_elems / 8, b8 = begin / 8, e8 = end / 8;
     if (fmt == FEDAVG_BF16)
         return launch_t16_o<FEDAVG_BF16>(tab, K, ts8, acc_in, out, b8, e8, op, fin, fin_val, grid, burst, s, nl);
