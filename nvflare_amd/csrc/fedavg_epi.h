@@ -263,19 +263,25 @@ fedavg_tiles_epi_burst_f32x4(const RowTableF32 tab, const int K, const int64_t t
     f32x4 dd[TPB][CPL];
     __shared__ f32x4 staged[TPB_LDS > 0 ? TPB_LDS * CPL * kBlock : 1];
 #pragma unroll
-    for (int m = 0; m < NT; ++m) {
+    for (int m = 0; m < TPB; ++m) {
         const int64_t t = t0 + blockIdx.x + (int64_t)m * gridDim.x;
         if (t < t_end) {
             f32x4 acc[CPL];
             tile_sum<OP, ACC_IN, UNROLL, CPL, true>(acc, tab, K, t * tstride4 + threadIdx.x, t * T4 + threadIdx.x, acc_in,
                                                     b4, e4);
 #pragma unroll
-            for (int c = 0; c < CPL; ++c) {
-                if (m < TPB)
-                    dd[m < TPB ? m : 0][c] = fin4<FIN>(acc[c], fin_val);
-                else
-                    staged[((m - TPB) * CPL + c) * kBlock + threadIdx.x] = fin4<FIN>(acc[c], fin_val);
-            }
+            for (int c = 0; c < CPL; ++c) dd[m][c] = fin4<FIN>(acc[c], fin_val);
+        }
+    }
+#pragma unroll 1
+    for (int m = TPB; m < NT; ++m) {  // rolled: one more copy of the client loop, not TPB_LDS of them
+        const int64_t t = t0 + blockIdx.x + (int64_t)m * gridDim.x;
+        if (t < t_end) {
+            f32x4 acc[CPL];
+            tile_sum<OP, ACC_IN, UNROLL, CPL, true>(acc, tab, K, t * tstride4 + threadIdx.x, t * T4 + threadIdx.x, acc_in,
+                                                    b4, e4);
+#pragma unroll
+            for (int c = 0; c < CPL; ++c) staged[((m - TPB) * CPL + c) * kBlock + threadIdx.x] = fin4<FIN>(acc[c], fin_val);
         }
     }
     // Epilogue phase, double-buffered: tile m+1's operand loads are issued before tile m's arithmetic and
