@@ -151,7 +151,8 @@ def test_exchange_chunks_cover_the_splits():
 @pytest.mark.parametrize("chunk", [1 << 28, 1])
 @pytest.mark.parametrize("mode", ["torch", "numpy"])
 @pytest.mark.parametrize("clients,P", [([2, 2], 5 * TILE + 1000), ([3, 1], 2 * TILE), ([2, 0, 3], 7 * TILE + 8),
-                                       ([1, 1, 1], 2 * TILE + 4)])
+                                       ([1, 1, 1], 2 * TILE + 4),
+                                       ([3, 0, 2, 1, 4, 1, 1, 2], 13 * TILE + 52)])  # eight ranks, one empty
 def test_exchange_gloo_matches_oracle(clients, P, mode, chunk):
     world = len(clients)
     order = [(s, j) for s in range(world) for j in range(clients[s])]

@@ -88,7 +88,8 @@ def _cases(world, seed):
     cases = []
     shapes = {1: [([5], 3 * TILE + 100), ([131], 2 * TILE + 8)],
               2: [([3, 2], 5 * TILE + 1000), ([2, 2], 64 * TILE), ([4, 0], TILE + 4), ([130, 3], 2 * TILE)],
-              3: [([2, 1, 3], 9 * TILE + 12), ([1, 1, 1], 3 * TILE)]}[world]
+              3: [([2, 1, 3], 9 * TILE + 12), ([1, 1, 1], 3 * TILE)],
+              4: [([2, 1, 0, 3], 10 * TILE + 4)]}[world]
     for clients, P in shapes:
         for mode in ("torch", "numpy"):
             order = [(s, j) for s in range(world) for j in range(clients[s])]
@@ -98,7 +99,7 @@ def _cases(world, seed):
     return cases
 
 
-@pytest.mark.parametrize("world", [1, 2, 3])
+@pytest.mark.parametrize("world", [1, 2, 3, 4])
 def test_client_sharded_exchange_exact_reduce_bounded(world):
     import torch.multiprocessing as mp
 
