@@ -337,8 +337,11 @@ def main():
                 "mode": args.mode,
                 "parallelism": f"param-bucket shards x{world}, no data-path collective",
                 "layout": f"tiled slab, {lay.tile}-element tiles x {K} slots",
-                "kernel": ("fedavg_tiles_burst_f32x4 (results staged in registers, stored as chip-wide bursts; "
-                           "8 tiles per block per launch)" if epi is None and args.variant & 11 == 0
+                "kernel": (("fedavg_tiles_burst_f32x4 (results staged on chip, stored as chip-wide bursts; "
+                            + ("8 register-held tiles per block per launch)" if args.variant & 32
+                               else "8 register- + 4 LDS-held tiles per block per launch)"))
+                           if epi is None and args.variant & 11 == 0
+                           else "fedavg_tiles_epi_burst_f32x4" if epi is not None and args.variant & 12 == 0
                            else "fedavg_tiles_epi_f32x4" if epi is not None else "fedavg_tiles_f32x4"),
             },
             "pct_hbm_peak": round(100.0 * achieved / HBM_PEAK_GBS, 2),
