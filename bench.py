@@ -41,7 +41,7 @@ def parse():
     ap.add_argument("--params", type=float, default=1e9, help="fp32 params per GPU bucket")
     ap.add_argument("--mode", choices=["torch", "numpy"], default="torch")
     ap.add_argument("--blocks-per-cu", type=int, default=0,
-                    help="0 = library default (burst kernel: 1 at >= 16 clients, else 2; others 2)")
+                    help="0 = library default (burst kernel: 1 at >= 32 clients, else 2; fused: 1 at >= 64)")
     ap.add_argument("--unroll", type=int, default=0, help="0 = library default (4)")
     ap.add_argument("--variant", type=int, default=0,
                     help="kernel variant bits (include/nvflare_amd_fedavg.h fedavg_set_variant; 0 = burst kernel)")

@@ -303,11 +303,12 @@ int fedavg_timing_begin(fedavg_ctx* ctx);
 int fedavg_timing_end(fedavg_ctx* ctx, float* ms);
 
 /* Aggregation / epilogue / dequantization kernel launches issued on the context's compute stream so far.
- * One fedavg_accumulate* call may issue several (the burst kernel: one per 8 tiles per block); relates a
+ * One fedavg_accumulate* call may issue several (the fp32 burst kernel: one per 12 tiles per block); relates a
  * profiler's per-launch durations to per-call times. */
 int fedavg_launch_count(fedavg_ctx* ctx, uint64_t* n);
 /* Launch tuning (0 = default): blocks per CU (default: each kernel's own -- 1 for the burst aggregation
- * kernel at >= 16 clients, 2 otherwise), clients whose loads are issued together (4 or 8, default 4). */
+ * kernel at >= 32 clients, the fused one at >= 64, the 16-bit one at >= 48 in torch mode, 2 otherwise),
+ * clients whose loads are issued together (4 or 8, default 4). */
 int fedavg_set_launch(fedavg_ctx* ctx, int blocks_per_cu, int unroll);
 /* Kernel variants (default 0: the aggregation -- plain or with a fused epilogue -- holds each block's
  * results in registers and stores them (runs the epilogue) as chip-wide bursts, one launch per 8 tiles per
