@@ -39,14 +39,65 @@ _SUMMED_STATS = (
 )
 
 
-def _is_nested_aggregation_weights(aggregation_weights) -> bool:
-    if not aggregation_weights or not isinstance(aggregation_weights, dict):
-        return False
-    return isinstance(next(iter(aggregation_weights.values())), dict)
+def _kind_error(label: str, kind) -> ValueError:
+    allowed = " or ".join(f"{k}" for k in _KINDS)
+    return ValueError(f"{label} = {kind} is not {allowed}")
 
 
-def _get_missing_keys(ref_dict: dict, dict_to_check: dict):
-    return [k for k in ref_dict if k not in dict_to_check]
+def _absent(required, given: dict) -> list:
+    """Keys of ``required`` that ``given`` lacks, in ``required``'s order."""
+    return [name for name in required if name not in given]
+
+
+def _kinds_by_dxo(expected_data_kind, single_key: str) -> dict:
+    """{dxo name: DataKind}; one bare DataKind means the single unnamed DXO (reference :101-113)."""
+    table = expected_data_kind if isinstance(expected_data_kind, dict) else {single_key: expected_data_kind}
+    for name, kind in table.items():
+        if kind not in _KINDS:
+            raise _kind_error(f"expected_data_kind[{name}]" if table is expected_data_kind else "expected_data_kind", kind)
+    return table
+
+
+def _excludes_by_dxo(exclude_vars, raw_kinds, kinds: dict, single_key: str) -> dict:
+    """{dxo name: regex or None} (reference :114-141): a dict must name every DXO, a string applies to all."""
+    per_dxo = isinstance(exclude_vars, dict)
+    if exclude_vars and not (per_dxo or isinstance(exclude_vars, str)):
+        raise ValueError(f"exclude_vars = {exclude_vars} should be a regex string but got {type(exclude_vars)}.")
+    if exclude_vars and per_dxo:
+        gaps = _absent(raw_kinds, exclude_vars)
+        if gaps:
+            raise ValueError(
+                "A dict exclude_vars should specify exclude_vars for every key in expected_data_kind. "
+                f"But missed these keys: {gaps}"
+            )
+    table = {}
+    for name in kinds:
+        if not per_dxo:
+            table[name] = exclude_vars
+        elif name in exclude_vars:
+            regex = exclude_vars[name]
+            if not isinstance(regex, str):
+                raise ValueError(f"exclude_vars[{name}] = {regex} should be a regex string but got {type(regex)}.")
+            table[name] = regex
+    if single_key in kinds:
+        table[single_key] = exclude_vars
+    return table
+
+
+def _weights_by_dxo(aggregation_weights, raw_kinds, kinds: dict) -> dict:
+    """{dxo name: {contributor: weight}} (reference :142-158); a dict of dicts must name every DXO."""
+    nested = bool(aggregation_weights) and isinstance(aggregation_weights, dict) and isinstance(
+        next(iter(aggregation_weights.values())), dict
+    )
+    if nested:
+        gaps = _absent(raw_kinds, aggregation_weights)
+        if gaps:
+            raise ValueError(
+                "A dict of dict aggregation_weights should specify aggregation_weights "
+                f"for every key in expected_data_kind. But missed these keys: {gaps}"
+            )
+    shared = aggregation_weights or {}
+    return {name: shared[name] if name in shared else shared for name in kinds}
 
 
 class InTimeAccumulateWeightedAggregator(Aggregator):
@@ -86,70 +137,18 @@ class InTimeAccumulateWeightedAggregator(Aggregator):
             self._initialize(self.aggregation_weights, self.exclude_vars, self.expected_data_kind)
 
     def _initialize(self, aggregation_weights, exclude_vars, expected_data_kind):
-        if isinstance(expected_data_kind, dict):
-            for k, v in expected_data_kind.items():
-                if v not in _KINDS:
-                    raise ValueError(
-                        f"expected_data_kind[{k}] = {v} is not {DataKind.WEIGHT_DIFF} or {DataKind.WEIGHTS} or {DataKind.METRICS}"
-                    )
-            self.expected_data_kind = expected_data_kind
-        else:
-            if expected_data_kind not in _KINDS:
-                raise ValueError(
-                    f"expected_data_kind = {expected_data_kind} is not {DataKind.WEIGHT_DIFF} or {DataKind.WEIGHTS} or {DataKind.METRICS}"
-                )
-            self.expected_data_kind = {self._single_dxo_key: expected_data_kind}
-
-        if exclude_vars:
-            if not isinstance(exclude_vars, (dict, str)):
-                raise ValueError(f"exclude_vars = {exclude_vars} should be a regex string but got {type(exclude_vars)}.")
-            if isinstance(exclude_vars, dict):
-                missing = _get_missing_keys(expected_data_kind, exclude_vars)
-                if missing:
-                    raise ValueError(
-                        "A dict exclude_vars should specify exclude_vars for every key in expected_data_kind. "
-                        f"But missed these keys: {missing}"
-                    )
-        exclude_by_key = {}
-        for k in self.expected_data_kind:
-            if isinstance(exclude_vars, dict):
-                if k in exclude_vars:
-                    if not isinstance(exclude_vars[k], str):
-                        raise ValueError(
-                            f"exclude_vars[{k}] = {exclude_vars[k]} should be a regex string but got {type(exclude_vars[k])}."
-                        )
-                    exclude_by_key[k] = exclude_vars[k]
-            else:
-                exclude_by_key[k] = exclude_vars  # same regex for every DXO of a collection
-        if self._single_dxo_key in self.expected_data_kind:
-            exclude_by_key[self._single_dxo_key] = exclude_vars
-        self.exclude_vars = exclude_by_key
-
-        if _is_nested_aggregation_weights(aggregation_weights):
-            missing = _get_missing_keys(expected_data_kind, aggregation_weights)
-            if missing:
-                raise ValueError(
-                    "A dict of dict aggregation_weights should specify aggregation_weights "
-                    f"for every key in expected_data_kind. But missed these keys: {missing}"
-                )
-        aggregation_weights = aggregation_weights or {}
-        self.aggregation_weights = {
-            k: aggregation_weights[k] if k in aggregation_weights else aggregation_weights for k in self.expected_data_kind
-        }
-
-        self.dxo_aggregators = {
-            k: DXOAggregator(
-                exclude_vars=self.exclude_vars[k],
-                aggregation_weights=self.aggregation_weights[k],
-                expected_data_kind=self.expected_data_kind[k],
-                name_postfix=k,
-                weigh_by_local_iter=self._weigh_by_local_iter,
-                device=self._device,
-                defer_result=self._defer_result,
-                devices=self._devices,
-            )
-            for k in self.expected_data_kind
-        }
+        # validation order and messages as intime_accumulate_model_aggregator.py:99-172
+        kinds = _kinds_by_dxo(expected_data_kind, self._single_dxo_key)
+        self.expected_data_kind = kinds
+        self.exclude_vars = _excludes_by_dxo(exclude_vars, expected_data_kind, kinds, self._single_dxo_key)
+        self.aggregation_weights = _weights_by_dxo(aggregation_weights, expected_data_kind, kinds)
+        engine_kwargs = dict(device=self._device, defer_result=self._defer_result, devices=self._devices,
+                             weigh_by_local_iter=self._weigh_by_local_iter)
+        self.dxo_aggregators = {}
+        for name, kind in kinds.items():
+            self.dxo_aggregators[name] = DXOAggregator(
+                exclude_vars=self.exclude_vars[name], aggregation_weights=self.aggregation_weights[name],
+                expected_data_kind=kind, name_postfix=name, **engine_kwargs)
 
     def accept(self, shareable: Shareable, fl_ctx: FLContext) -> bool:
         """Stage one client's result; False on any rejection (intime_accumulate_model_aggregator.py:174-230)."""
@@ -175,53 +174,49 @@ class InTimeAccumulateWeightedAggregator(Aggregator):
             self.log_warning(fl_ctx, f"Contributor {contributor_name} returned rc: {rc}. Disregarding contribution.")
             return False
 
-        n_accepted = 0
-        for key in self.expected_data_kind:
-            sub_dxo = dxo if key == self._single_dxo_key else dxo.data.get(key)
-            if not isinstance(sub_dxo, DXO):
-                self.log_warning(fl_ctx, f"Collection does not contain DXO for key {key} but {type(sub_dxo)}.")
+        taken = 0
+        for name, agg in self.dxo_aggregators.items():
+            part = dxo if name == self._single_dxo_key else dxo.data.get(name)
+            if not isinstance(part, DXO):
+                self.log_warning(fl_ctx, f"Collection does not contain DXO for key {name} but {type(part)}.")
                 continue
-            if not self.dxo_aggregators[key].accept(
-                dxo=sub_dxo, contributor_name=contributor_name, contribution_round=contribution_round, fl_ctx=fl_ctx
-            ):
-                return False
-            n_accepted += 1
-
-        if n_accepted > 0:
-            return True
-        self.log_warning(fl_ctx, f"Did not accept any DXOs from {contributor_name} in round {contribution_round}!")
-        return False
+            ok = agg.accept(dxo=part, contributor_name=contributor_name, contribution_round=contribution_round,
+                            fl_ctx=fl_ctx)
+            if not ok:
+                return False  # one rejected DXO rejects the whole contribution
+            taken += 1
+        if not taken:
+            self.log_warning(fl_ctx, f"Did not accept any DXOs from {contributor_name} in round {contribution_round}!")
+        return taken > 0
 
     def aggregate(self, fl_ctx: FLContext) -> Shareable:
         """Weighted mean of the accepted results (intime_accumulate_model_aggregator.py:232-255)."""
-        results = {}
-        for key in self.expected_data_kind:
-            aggregated_dxo = self.dxo_aggregators[key].aggregate(fl_ctx)
-            if key == self._single_dxo_key:
+        parts = {}
+        for name, agg in self.dxo_aggregators.items():
+            out = agg.aggregate(fl_ctx)
+            if name == self._single_dxo_key:  # the unnamed DXO is returned as it is, stats published first
                 self._publish_aggregation_stats(fl_ctx)
-                return aggregated_dxo.to_shareable()
-            self.log_info(fl_ctx, f"Aggregated contributions matching key '{key}'.")
-            results[key] = aggregated_dxo
+                return out.to_shareable()
+            self.log_info(fl_ctx, f"Aggregated contributions matching key '{name}'.")
+            parts[name] = out
         self._publish_aggregation_stats(fl_ctx)
-        return DXO(data_kind=DataKind.COLLECTION, data=results).to_shareable()
+        return DXO(data_kind=DataKind.COLLECTION, data=parts).to_shareable()
 
     # reset(): inherited no-op, as in the reference (abstract/aggregator.py:23-32); get_result() already
     # resets each helper, and a late accept between aggregate() and reset() carries over exactly as there.
 
     def _publish_aggregation_stats(self, fl_ctx: FLContext):
         """Merge per-DXO stats and post them (intime_accumulate_model_aggregator.py:257-288)."""
-        combined = None
-        for agg in self.dxo_aggregators.values():
-            stats = agg.last_aggregation_stats
+        merged: Optional[dict] = None
+        for stats in (agg.last_aggregation_stats for agg in self.dxo_aggregators.values()):
             if not stats:
                 continue
-            if combined is None:
-                combined = dict(stats)
+            if merged is None:
+                merged = dict(stats)
                 continue
-            for key in _SUMMED_STATS:
-                combined[key] += stats[key]
-            contributors = set(combined[AggregationStatsKey.CONTRIBUTORS]) | set(stats[AggregationStatsKey.CONTRIBUTORS])
-            combined[AggregationStatsKey.CONTRIBUTORS] = sorted(contributors)
-            combined[AggregationStatsKey.ACCEPTED_CONTRIBUTIONS] = len(contributors)
-        if combined:
-            fl_ctx.set_prop(AppConstants.AGGREGATION_STATS, combined, private=True, sticky=False)
+            merged.update({key: merged[key] + stats[key] for key in _SUMMED_STATS})
+            everyone = sorted(set(merged[AggregationStatsKey.CONTRIBUTORS]).union(stats[AggregationStatsKey.CONTRIBUTORS]))
+            merged[AggregationStatsKey.CONTRIBUTORS] = everyone
+            merged[AggregationStatsKey.ACCEPTED_CONTRIBUTIONS] = len(everyone)
+        if merged:
+            fl_ctx.set_prop(AppConstants.AGGREGATION_STATS, merged, private=True, sticky=False)
