@@ -339,6 +339,8 @@ def main():
                 "layout": f"tiled slab, {lay.tile}-element tiles x {K} slots",
                 "kernel": (("fedavg_tiles_burst_f32x4 (results staged on chip, stored as chip-wide bursts; "
                             + ("8 register-held tiles per block per launch)" if args.variant & 32
+                               else "8 register- + 10 LDS-held tiles per block per launch, one block per CU)"
+                               if K >= 32 and not args.variant & 64
                                else "8 register- + 4 LDS-held tiles per block per launch)"))
                            if epi is None and args.variant & 11 == 0
                            else "fedavg_tiles_epi_burst_f32x4" if epi is not None and args.variant & 12 == 0

@@ -369,9 +369,11 @@ void run_tiles(fedavg_ctx* ctx, const void* const* bases, const double* weights,
     L.b4 = b / 4;
     L.e4 = e / 4;
     const int64_t n_tiles = (L.e4 - 1) / L.tile4 - L.b4 / L.tile4 + 1;
-    const int bpc = fedavg::tiles_use_burst(L.tile4, L.unroll, L.variant)
-                        ? ctx->bpc(k_rows >= fedavg::kBurstOneBlockMinK ? 1 : 2)
-                        : ctx->bpc();
+    const bool burst = fedavg::tiles_use_burst(L.tile4, L.unroll, L.variant);
+    const int bpc = burst ? ctx->bpc(k_rows >= fedavg::kBurstOneBlockMinK ? 1 : 2) : ctx->bpc();
+    // one block per CU: the burst kernel holds 10 tiles in LDS (all 160 KiB); public bit 6 keeps the 4-tile form
+    const bool wide = burst && bpc == 1 && !(ctx->variant & fedavg::kVariantWideLds);
+    L.variant = (ctx->variant & ~fedavg::kVariantWideLds) | (wide ? fedavg::kVariantWideLds : 0);
     L.grid = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)ctx->num_cus * bpc, n_tiles));
     const float fv = (float)fin_scalar(fin, count);
     int k0 = 0;
@@ -1378,7 +1380,7 @@ int fedavg_set_launch(fedavg_ctx* ctx, int blocks_per_cu, int unroll) {
 int fedavg_set_variant(fedavg_ctx* ctx, int variant) {
     return guarded([&] {
         if (!ctx) throw Error("ctx is NULL");
-        if (variant < 0 || variant > 63) throw Error("variant must be 0..63");
+        if (variant < 0 || variant > 127) throw Error("variant must be 0..127");
         ctx->variant = variant;
     });
 }

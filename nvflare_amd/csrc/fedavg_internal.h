@@ -31,6 +31,11 @@ constexpr int kVariantAnyOrder = 16;       // burst launches after an aggregatio
 constexpr int kVariantRegisterTiles = 32;  // plain burst kernel without its kBurstLdsTiles LDS-held tiles (by default
                                            // each block also holds 4 tiles' results in LDS: 1.5x longer launches,
                                            // +0.3 to +1.5 points at 8-64 clients, profiles/r02/ab/lds_tiles/)
+constexpr int kVariantWideLds = 64;       // inside TileLaunch: plain burst kernel with kBurstLdsTilesWide LDS-held tiles
+                                           // (160 KiB, one block per CU); run_tiles sets it for one-block-per-CU grids
+                                           // unless the public variant has bit 6, which keeps the 4-tile form there
+                                           // (32 clients 88.4 -> 88.9 %, 64: 89.7 -> 89.9 %, profiles/r02/ab/wide_lds/)
+constexpr int kBurstLdsTilesWide = 10;     // 10 x 16 KiB = all of a CU's LDS
 constexpr int kBurstTiles = 8;             // tiles per block per burst launch (results held in registers)
 constexpr int kBurstLdsTiles = 4;          // 4 x 16 KiB of LDS per block (2 blocks fit a CU)
 

@@ -158,6 +158,8 @@ inline hipError_t launch_tiles_v(const TileLaunch& L, hipStream_t s, uint64_t* n
     if constexpr (CPL * (UNROLL + kBurstTiles) <= 64) {  // staged results + a group's loads within 256 VGPRs
         if (!(L.variant & (kVariantTileStores | kVariantTemporalLoads | kVariantTemporalStores))) {
             if constexpr (CPL == 4 && UNROLL == 4) {  // the default geometry only (build time)
+                if (L.variant & kVariantWideLds)
+                    return launch_burst<OP, FIN, ACC_IN, UNROLL, CPL, kBurstTiles, kBurstLdsTilesWide>(L, s, nl);
                 if (!(L.variant & kVariantRegisterTiles))
                     return launch_burst<OP, FIN, ACC_IN, UNROLL, CPL, kBurstTiles, kBurstLdsTiles>(L, s, nl);
             }
