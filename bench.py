@@ -5,17 +5,26 @@ One step = one aggregation: the arrival-ordered weighted accumulate-and-finalise
 device-resident client rows of P fp32 params -> P fp32 results (weighted_aggregation_helper.py:153-240,
 torch-mode arithmetic by default).  Inputs are resident in HBM before the timed region starts.
 
-  python bench.py [--gpus N --steps K --warmup W]          # default: 64 clients x 1e9 params, 1 GPU
-  torchrun --nproc-per-node N bench.py --gpus N ...        # weak scaling: each GPU aggregates its own
-                                                           # 1e9-param bucket, no data-path collective
+  python bench.py [--gpus N --steps K --warmup W]          # default: BASELINE config 3, 64 clients x 1e9 params
+  torchrun --nproc-per-node N bench.py --gpus N ...        # N ranks, one GPU each, no data-path collective
+  python bench.py --config {2,3,4,5}                       # BASELINE.json configs[1..4] (presets below)
 
-Prints ONE JSON line (rank 0).  value = GiB/s aggregated = 4*K*P*N*steps / t / 2^30 with t the max over
-ranks of the barrier+synchronize bracketed wall time.  roofline.achieved uses the algorithmic bytes of one
-aggregation (4*K*P + 4*P) over its device time measured with HIP events on the stream the kernels run on
-(one aggregation = roofline.launches_per_step launches of the burst kernel; launch_us_avg is the
-per-launch time a rocprofv3 --stats average compares with).  cpu_baseline times the oracle restatement
-(torch CPU ops, all threads) on a bounded sample of the same workload, and the same leg spot-checks
-sampled device outputs bit-exactly against the oracle (test infrastructure; never the measured path).
+Scaling.  The path shards by parameter bucket:
+  weak   (configs 2, 3 -- single-GPU configs): every rank aggregates its own P-param bucket of the K clients
+  strong (configs 4, 5 -- "sharded across 8", "1->8 GPUs"): a fixed global model of P params is split by
+         sharding.bucket_ranges(P, N); rank r aggregates bucket r of every client.
+After the main measurement the default run also measures, in the same process, BASELINE configs 5 and 4 under
+strong scaling (``--also``; config 4 needs >= 2 GPUs: 358 GB of client updates do not fit one 288 GB HBM), and
+embeds them in the line's ``also`` list -- so one N-GPU run records configs 3, 4 and 5 at that N.
+
+Prints ONE JSON line (rank 0).  value = GiB/s aggregated = 4*K*P_total*steps / t / 2^30 with t the max over
+ranks of the barrier+synchronize bracketed wall time (P_total = P*N weak, P strong).  roofline.achieved uses the
+algorithmic bytes of one aggregation on one GPU (4*K*P_gpu + 4*P_gpu, or + the epilogue's state bytes) over
+its device time measured with HIP events on the stream the kernels run on (one aggregation =
+roofline.launches_per_step launches of the burst kernel; launch_us_avg is the per-launch time a rocprofv3
+--stats average compares with).  cpu_baseline times the oracle restatement (torch CPU ops) on a bounded
+sample of the same workload, and the same leg spot-checks sampled device outputs bit-exactly against the
+oracle (test infrastructure; never the measured path).
 """
 
 from __future__ import annotations
@@ -31,14 +40,38 @@ import numpy as np
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 METRIC = "GiB/s aggregated (device-resident FedAvg, K clients × P fp32 params); % HBM peak"
 
+# BASELINE.json configs[1..4] (configs[0] is the CPU plumbing job, tests/sag_harness.py)
+PRESETS = {
+    2: dict(clients=8, params=125_000_000, epilogue="none", scaling="weak"),
+    3: dict(clients=64, params=1_000_000_000, epilogue="none", scaling="weak"),
+    4: dict(clients=256, params=350_000_000, epilogue="none", scaling="strong"),
+    5: dict(clients=64, params=1_000_000_000, epilogue="adam", scaling="strong"),
+}
+PRESET_NAMES = {
+    2: "BASELINE config 2: 8 clients x 125M fp32 params, weighted FedAvg on 1 MI355X",
+    3: "BASELINE config 3: 64 clients x 1B fp32 params, single-GPU HBM-resident aggregation",
+    4: "BASELINE config 4: 256 clients x 350M fp32 params, param buckets sharded across the GPUs",
+    5: "BASELINE config 5: FedOpt server optimizer (Adam on aggregated deltas), 64 clients x 1B params",
+}
+EPI_STATE_BYTES = {"none": 4.0, "add_base": 8.0, "sgd": 16.0}  # per param beyond the 4*K client reads; else 24
+HEADROOM = 2 << 30  # device bytes left free beside a workload (runtime, gather buffers)
 
-def parse():
+
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--clients", type=int, default=64)
-    ap.add_argument("--params", type=float, default=1e9, help="fp32 params per GPU bucket")
+    ap.add_argument("--config", type=int, choices=sorted(PRESETS), default=3,
+                    help="BASELINE.json workload preset (clients, params, epilogue, scaling); flags below override")
+    ap.add_argument("--clients", type=int, default=None)
+    ap.add_argument("--params", type=float, default=None,
+                    help="fp32 params: per GPU under weak scaling, of the whole model under strong scaling")
+    ap.add_argument("--global-params", type=float, default=None, help="--scaling strong --params N")
+    ap.add_argument("--scaling", choices=["weak", "strong"], default=None)
+    ap.add_argument("--also", default="auto",
+                    help="extra strong-scaling BASELINE configs measured after the main one, in the same line "
+                         "(comma list of 4/5; 'auto' = 5,4 for the default config 3 run; 'none')")
     ap.add_argument("--mode", choices=["torch", "numpy"], default="torch")
     ap.add_argument("--blocks-per-cu", type=int, default=0,
                     help="0 = library default (burst kernel: 1 at >= 32 clients, else 2; fused: 1 at >= 64)")
@@ -46,16 +79,30 @@ def parse():
     ap.add_argument("--variant", type=int, default=0,
                     help="kernel variant bits (include/nvflare_amd_fedavg.h fedavg_set_variant; 0 = burst kernel)")
     ap.add_argument("--tile", type=int, default=4096, help="slab tile width (elements)")
-    ap.add_argument("--epilogue", choices=["none", "add_base", "sgd", "adam", "adamax", "nadam", "radam"], default="none",
+    ap.add_argument("--epilogue", choices=["none", "add_base", "sgd", "adam", "adamax", "nadam", "radam"], default=None,
                     help="fused server update (config 5 = adam: FedOpt Adam on the aggregated deltas)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-params", type=int, default=16 * 1024 * 1024)
     ap.add_argument("--spot-check", type=int, default=4096, help="sampled outputs checked against the oracle")
     ap.add_argument("--traffic-bytes", type=float, default=None,
-                    help="HBM bytes per launch from a separate rocprofv3 --pmc pass (default: profiles/pmc_traffic.json "
-                         "when its config matches this run)")
+                    help="HBM bytes per aggregation from a separate rocprofv3 --pmc pass (default: "
+                         "profiles/pmc_traffic.json when its config matches this run)")
     ap.add_argument("--seed", type=int, default=1000)
-    return ap.parse_args()
+    args = ap.parse_args(argv)
+    preset = PRESETS[args.config]
+    if args.global_params is not None:
+        args.params, args.scaling = args.global_params, "strong"
+    for k in ("clients", "params", "epilogue", "scaling"):
+        if getattr(args, k) is None:
+            setattr(args, k, preset[k])
+    args.clients, args.params = int(args.clients), int(args.params)
+    explicit = any(f in (argv if argv is not None else sys.argv[1:])
+                   for f in ("--clients", "--params", "--global-params", "--scaling", "--epilogue"))
+    args.preset_exact = not explicit
+    if args.also == "auto":
+        args.also = "5,4" if (args.config == 3 and not explicit) else "none"
+    args.also = [] if args.also in ("", "none") else [int(x) for x in args.also.split(",")]
+    return args
 
 
 def dist_setup(args):
@@ -106,7 +153,7 @@ def max_over_ranks(world, value: float) -> float:
 
 
 def sum_over_ranks(world, values):
-    """Element-wise SUM over ranks of a few host integers (spot-check counts)."""
+    """Element-wise SUM over ranks of a few host integers (spot-check counts, feasibility votes)."""
     if world == 1:
         return list(values)
     import torch
@@ -124,59 +171,113 @@ def rank_bucket(rank: int, P: int):
     return rank * P
 
 
-def cpu_baseline_and_spot_check(args, ctx, K, out_buf, weights, count, P, col0, op, baseline=True):
-    """Oracle leg (test infrastructure): time the reference restatement on the host (``baseline``: rank 0 at
-    N=1 only), then check sampled device outputs of this rank's bucket bit-for-bit against the oracle computed
-    from the host twin of the generator."""
+def rank_span(scaling: str, rank: int, world: int, P: int):
+    """(first global param, params) of rank r's bucket: weak -- its own P; strong -- bucket r of a P-param
+    model split by sharding.bucket_ranges (whole 4096-element tiles, sizes within one tile of each other)."""
+    if scaling == "weak":
+        return rank_bucket(rank, P), P
+    from nvflare_amd.sharding import bucket_ranges
+
+    lo, hi = bucket_ranges(P, world)[rank]
+    return lo, hi - lo
+
+
+def synth_weights(K):
+    """aggregation_weight 1.0 x NUM_STEPS_CURRENT_ROUND = 1 + (37k mod 100)."""
+    return [1.0 * float(1 + (37 * k) % 100) for k in range(K)]
+
+
+def arrival_count(weights):
+    count = None
+    for w in weights:
+        count = w if count is None else count + w
+    return count
+
+
+ADAM_HP = dict(lr=1e-3, beta1=0.9, beta2=0.999, eps=1e-8)
+
+
+def spot_check(args, ctx, K, P, col0, op, epilogue, bufs, n_steps, seed):
+    """Sampled device outputs of this rank's bucket against the oracle computed from the host twin of the
+    generator (test infrastructure): the plain aggregation's output, or for the fused Adam step the parameter and
+    both moments after every step the run made."""
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from oracle import fedavg_oracle as orc
+
+    if args.spot_check <= 0 or epilogue not in ("none", "adam"):
+        return None
+    rng = np.random.default_rng(7)
+    idx = np.unique(np.concatenate([rng.integers(0, P, args.spot_check, dtype=np.int64), [0, P - 1]]))
+    cols = (idx + col0).astype(np.uint64)
+    weights = synth_weights(K)
+    mode = orc.MODE_TORCH if op == 1 else orc.MODE_NUMPY
+    d = orc.fedavg_c([orc.synth_values(seed, k, cols) for k in range(K)], weights, mode)
+    if epilogue == "none":
+        got = ctx.gather_f32(bufs[0].ptr, idx.astype(np.uint64))
+        mism = int(np.count_nonzero(d.view(np.uint32) != got.view(np.uint32)))
+        return {"sampled": int(idx.size), "mismatches": mism, "oracle": "oracle/fedavg_oracle.c"}
+    p = orc.synth_values(seed + 7, 0, cols)
+    m = np.zeros_like(p)
+    v = np.zeros_like(p)
+    for s in range(1, n_steps + 1):
+        orc.epilogue_apply(d, orc.EPI_ADAM, p=p, m=m, v=v, step=float(s), **ADAM_HP)
+    mism = 0
+    for buf, host in zip(bufs, (p, m, v)):
+        got = ctx.gather_f32(buf.ptr, idx.astype(np.uint64))
+        mism += int(np.count_nonzero(host.view(np.uint32) != got.view(np.uint32)))
+    return {"sampled": int(idx.size) * 3, "mismatches": mism,
+            "oracle": f"oracle/fedavg_oracle.c (aggregation + {n_steps} Adam steps; p, exp_avg, exp_avg_sq)"}
+
+
+def cpu_baseline(args, K, P, op):
+    """The reference's op sequence restated on the host (oracle, test infrastructure) on a bounded sample of the
+    workload: torch CPU mul / add_(alpha) / div_ with torch's intra-op threads, and numpy single-threaded."""
     import torch
 
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     from oracle import fedavg_oracle as orc
 
-    res = {}
-    # -- spot check at full size -----------------------------------------------------------------
-    if args.spot_check > 0:
-        rng = np.random.default_rng(7)
-        idx = np.unique(np.concatenate([rng.integers(0, P, args.spot_check, dtype=np.int64), [0, P - 1]]))
-        host_rows = [orc.synth_values(args.seed, k, (idx + col0).astype(np.uint64)) for k in range(K)]
-        mode = orc.MODE_TORCH if op == 1 else orc.MODE_NUMPY
-        exp = orc.fedavg_c(host_rows, weights, mode)
-        got = ctx.gather_f32(out_buf.ptr, idx.astype(np.uint64))
-        mism = int(np.count_nonzero(exp.view(np.uint32) != got.view(np.uint32)))
-        res["spot_check"] = {"sampled": int(idx.size), "mismatches": mism, "oracle": "oracle/fedavg_oracle.c"}
-    # -- CPU baseline: the reference's torch CPU op sequence on a bounded sample ------------------
-    if baseline and not args.no_cpu_baseline:
-        Ps = int(min(args.cpu_sample_params, P))
-        gen = [np.random.default_rng(1000 + k).standard_normal(Ps, dtype=np.float32) for k in range(K)]
-        trows = [torch.from_numpy(g) for g in gen]
-        threads = torch.get_num_threads()
-        reps, t_tot = 0, 0.0
-        while t_tot < 10.0 and reps < 2000:
-            t0 = time.perf_counter()
-            if op == 1:
-                orc.torch_mode_reference(trows, weights)
-            else:
-                orc.numpy_mode_reference(gen, weights)
-            t_tot += time.perf_counter() - t0
-            reps += 1
-        gibs = 4.0 * K * Ps * reps / t_tot / 2**30
-        # single-thread numpy restatement (the numpy-job path) for context
+    weights = synth_weights(K)
+    Ps = int(min(args.cpu_sample_params, P))
+    gen = [np.random.default_rng(1000 + k).standard_normal(Ps, dtype=np.float32) for k in range(K)]
+    trows = [torch.from_numpy(g) for g in gen]
+    threads = torch.get_num_threads()
+    reps, t_tot = 0, 0.0
+    while t_tot < 10.0 and reps < 2000:
         t0 = time.perf_counter()
-        orc.numpy_mode_reference(gen, weights)
-        t_np = time.perf_counter() - t0
-        res["cpu_baseline"] = {
-            "value": round(gibs, 3),
-            "unit": "GiB/s",
-            "cores": threads if op == 1 else 1,
-            "kind": "port",
-            "sample": f"{K} clients x {Ps} fp32 params (numpy default_rng(1000+k) N(0,1)), "
-                      f"{'torch CPU mul/add_(alpha)/div_' if op == 1 else 'numpy v*w / t+v*w / t*(1/c)'} "
-                      f"restatement of weighted_aggregation_helper.py:181-236, {reps} reps in {t_tot:.1f}s",
-            "numpy_single_thread_GiBs": round(4.0 * K * Ps / t_np / 2**30, 3),
-            "host_cpu_count": os.cpu_count(),
-            "host_cpu_model": _cpu_model(),
-        }
-    return res
+        if op == 1:
+            orc.torch_mode_reference(trows, weights)
+        else:
+            orc.numpy_mode_reference(gen, weights)
+        t_tot += time.perf_counter() - t0
+        reps += 1
+    gibs = 4.0 * K * Ps * reps / t_tot / 2**30
+    t0 = time.perf_counter()  # single-thread numpy restatement (the numpy-job path) for context
+    orc.numpy_mode_reference(gen, weights)
+    t_np = time.perf_counter() - t0
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        affinity = None
+    omp = os.environ.get("OMP_NUM_THREADS")
+    return {
+        "value": round(gibs, 3),
+        "unit": "GiB/s",
+        "cores": threads if op == 1 else 1,
+        "kind": "port",
+        "sample": f"{K} clients x {Ps} fp32 params (numpy default_rng(1000+k) N(0,1)), "
+                  f"{'torch CPU mul/add_(alpha)/div_' if op == 1 else 'numpy v*w / t+v*w / t*(1/c)'} "
+                  f"restatement of weighted_aggregation_helper.py:181-236, {reps} reps in {t_tot:.1f}s",
+        "numpy_single_thread_GiBs": round(4.0 * K * Ps / t_np / 2**30, 3),
+        "torch_threads": threads,
+        "host_cpu_count": os.cpu_count(),
+        "affinity_cpus": affinity,
+        "omp_num_threads_env": omp,
+        "cores_reason": (f"torch uses OMP_NUM_THREADS={omp} threads: the GPU pool's CPU share per GPU (the pool sets "
+                         f"it; {affinity} CPUs are in this process's affinity mask, {os.cpu_count()} on the host)"
+                         if omp else f"torch.get_num_threads() = {threads} ({affinity} CPUs in the affinity mask)"),
+        "host_cpu_model": _cpu_model(),
+    }
 
 
 def _cpu_model() -> str:
@@ -190,9 +291,9 @@ def _cpu_model() -> str:
     return "unknown"
 
 
-def pmc_traffic(args, K, P):
-    """HBM bytes per launch measured by rocprofv3 PMC passes of this same command (profiles/pmc_traffic.json),
-    only when that measurement's configuration is this run's."""
+def pmc_traffic(args, K, P, epilogue):
+    """HBM bytes per aggregation measured by rocprofv3 PMC passes of this same command
+    (profiles/pmc_traffic.json), only when that measurement's configuration is this run's."""
     if args.traffic_bytes is not None:
         return args.traffic_bytes, "--traffic-bytes"
     path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "pmc_traffic.json")
@@ -201,7 +302,7 @@ def pmc_traffic(args, K, P):
             rec = json.load(f)
     except (OSError, ValueError):
         return None, None
-    want = {"clients": K, "params": P, "tile": args.tile, "mode": args.mode, "epilogue": args.epilogue}
+    want = {"clients": K, "params": P, "tile": args.tile, "mode": args.mode, "epilogue": epilogue}
     for r in rec.get("records", []):
         cfg = dict(r.get("config", {}))
         cfg.setdefault("epilogue", "none")
@@ -210,171 +311,218 @@ def pmc_traffic(args, K, P):
     return None, None
 
 
-def main():
-    args = parse()
+def kernel_name(K, epilogue, variant):
+    if epilogue != "none":
+        return "fedavg_tiles_epi_burst_f32x4" if variant & 12 == 0 else "fedavg_tiles_epi_f32x4"
+    if variant & 11:
+        return "fedavg_tiles_f32x4"
+    return ("fedavg_tiles_burst_f32x4 (results staged on chip, stored as chip-wide bursts; "
+            + ("8 register-held tiles per block per launch)" if variant & 32
+               else "8 register- + 10 LDS-held tiles per block per launch, one block per CU)"
+               if K >= 32 and not variant & 64 else "8 register- + 4 LDS-held tiles per block per launch)"))
+
+
+def run_workload(args, ctx, world, rank, K, P_spec, scaling, epilogue, baseline, seed):
+    """Stage one workload in HBM, time args.steps aggregations after args.warmup, spot-check, free it.
+
+    Returns a dict (every rank) or, when the workload does not fit every rank's device, {"skipped": reason}."""
+    from nvflare_amd import _native as N
+    from nvflare_amd.device import TiledLayout
+
+    col0, P = rank_span(scaling, rank, world, P_spec)
+    op = N.FEDAVG_OP_TORCH if args.mode == "torch" else N.FEDAVG_OP_NUMPY
+    fin = N.FEDAVG_FIN_DIV if args.mode == "torch" else N.FEDAVG_FIN_SCALE
+    lay = TiledLayout(args.tile, K)  # the engine's slab layout: K client slots interleaved per tile
+    end = (P + 3) // 4 * 4
+    epi_bufs = {"none": 1, "add_base": 1, "sgd": 2}.get(epilogue, 3)  # out | p+buf | p+m+v
+    need = lay.slab_elems(P) * 4 + epi_bufs * end * 4
+    free, total = ctx.mem_info()
+    fits = need + HEADROOM <= free
+    if sum_over_ranks(world, [0 if fits else 1])[0]:
+        return {"skipped": f"needs {need / 1e9:.1f} GB of HBM per GPU at {world} GPU(s) "
+                           f"(this device: {free / 1e9:.1f} GB free of {total / 1e9:.1f})"}
+    slab = ctx.alloc(lay.slab_elems(P) * 4)
+    state = [ctx.alloc(end * 4) for _ in range(epi_bufs)]
+    try:
+        out = state[0]
+        bases = [slab.ptr + lay.slot_offset_elems(k) * 4 for k in range(K)]
+        for k, base in enumerate(bases):
+            ctx.fill_synthetic_f32(base, P, seed, k, col0, lay.tile, lay.tile_stride)
+        weights = synth_weights(K)
+        count = arrival_count(weights)
+        epi = None
+        if epilogue != "none":
+            for j, b in enumerate(state):  # initial params (or base weights), zero optimizer state
+                if j == 0:
+                    ctx.fill_synthetic_f32(b.ptr, end, seed + 7, 0, col0)
+                else:
+                    ctx.memset(b.ptr, 0, end * 4)
+            epi = N.Epilogue()
+            epi.kind = {"add_base": N.FEDAVG_EPI_ADD_BASE, "sgd": N.FEDAVG_EPI_SGD, "adam": N.FEDAVG_EPI_ADAM,
+                        "adamax": N.FEDAVG_EPI_ADAMAX, "nadam": N.FEDAVG_EPI_NADAM,
+                        "radam": N.FEDAVG_EPI_RADAM}[epilogue]
+            if epilogue == "add_base":
+                epi.base = out.ptr
+            elif epilogue == "sgd":
+                epi.param, epi.state1 = state[0].ptr, state[1].ptr
+                epi.lr, epi.momentum = 1.0, 0.9
+            else:
+                epi.param, epi.state1, epi.state2 = state[0].ptr, state[1].ptr, state[2].ptr
+                for k, v in ADAM_HP.items():
+                    setattr(epi, k, v)
+                epi.momentum_decay, epi.mu_product = 4e-3, 1.0  # NAdam (mu_product held at its first-step value)
+        ctx.sync()
+        n_step = [0]
+
+        def step():
+            if epi is None:
+                ctx.accumulate_tiled(bases, weights, lay.tile, lay.tile_stride, 0, end, out.ptr, op, fin, count)
+                return
+            n_step[0] += 1
+            epi.step = float(n_step[0])
+            epi.first_step = int(n_step[0] == 1)
+            ctx.accumulate_tiled_epi(bases, weights, lay.tile, lay.tile_stride, 0, end,
+                                     out.ptr if epilogue == "add_base" else None, op, fin, count, epi)
+
+        for _ in range(args.warmup):
+            step()
+        barrier_sync(world, ctx)
+        n_launch0 = ctx.launch_count()
+        ctx.timing_begin()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            step()
+        barrier_sync(world, ctx)
+        t1 = time.perf_counter()
+        ev_ms = ctx.timing_end()
+        launches_per_step = (ctx.launch_count() - n_launch0) / args.steps
+        wall = max_over_ranks(world, t1 - t0)
+        kernel_ms = ev_ms / args.steps
+        kernel_ms_max = max_over_ranks(world, kernel_ms)
+        sc = spot_check(args, ctx, K, P, col0, op, epilogue, state if epi is not None else [out], n_step[0], seed)
+        if sc is not None and world > 1:  # every rank checks its own bucket; the counts are summed
+            sampled, mism = sum_over_ranks(world, [sc["sampled"], sc["mismatches"]])
+            sc.update(sampled=sampled, mismatches=mism, ranks=world)
+        res = {"K": K, "P": P, "P_total": P_spec * world if scaling == "weak" else P_spec, "col0": col0,
+               "wall": wall, "kernel_ms": kernel_ms, "kernel_ms_max": kernel_ms_max,
+               "launches_per_step": launches_per_step, "spot_check": sc, "op": op}
+    finally:
+        slab.close()
+        for b in state:
+            b.close()
+    if baseline:
+        res["cpu_baseline"] = cpu_baseline(args, K, P, op)
+    return res
+
+
+def summarize(args, world, res, K, scaling, epilogue, label):
+    """The JSON fields of one measured workload (rank 0)."""
+    P = res["P"]
+    bytes_step = 4.0 * K * res["P_total"]  # aggregated client bytes per step, all ranks
+    value = bytes_step * args.steps / res["wall"] / 2**30
+    alg_bytes = 4.0 * K * P + EPI_STATE_BYTES.get(epilogue, 24.0) * P
+    kernel_ms = res["kernel_ms"]
+    achieved = alg_bytes / (kernel_ms / 1e3) / 1e9
+    traffic, traffic_src = pmc_traffic(args, K, P, epilogue)
+    per_gpu = "per GPU" if scaling == "weak" else f"in all (model split over {world} GPU(s): {P} on GPU 0)"
+    return {
+        "value": round(value, 2),
+        "ms_per_step": round(res["wall"] / args.steps * 1e3, 4),
+        "scaling": scaling,
+        "config": {
+            "workload": f"{K} clients x {res['P_total'] if scaling == 'strong' else P} fp32 params {per_gpu}, weighted "
+                        f"FedAvg, {args.mode}-mode arithmetic"
+                        + ("" if epilogue == "none" else f", fused {epilogue} server update"),
+            "baseline_config": label,
+            "epilogue": epilogue,
+            "clients": K,
+            "params_per_gpu": P,
+            "params_total": res["P_total"],
+            "mode": args.mode,
+            "parallelism": (f"param-bucket shards x{world}, no data-path collective"
+                            + (" (each GPU its own bucket)" if scaling == "weak" else " (one model split in buckets)")),
+            "layout": f"tiled slab, {args.tile}-element tiles x {K} slots",
+            "kernel": kernel_name(K, epilogue, args.variant),
+        },
+        "pct_hbm_peak": round(100.0 * achieved / HBM_PEAK_GBS, 2),
+        "roofline": {
+            "bound": "hbm",
+            "achieved": round(achieved, 1),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "traffic": traffic,
+            "traffic_source": traffic_src,
+            "kernel_ms_avg": round(kernel_ms, 4),
+            "kernel_ms_avg_max_rank": round(res["kernel_ms_max"], 4),
+            "alg_bytes_per_launch": alg_bytes,
+            # one aggregation = launches_per_step kernel launches (the burst kernel: one per grid x tiles-per-block);
+            # kernel_ms_avg, alg_bytes_per_launch and traffic are per aggregation (rank 0's GPU), launch_us_avg is the
+            # per-launch figure a rocprofv3 --stats average compares with
+            "launches_per_step": res["launches_per_step"],
+            "launch_us_avg": round(kernel_ms * 1e3 / max(res["launches_per_step"], 1), 2),
+        },
+    }
+
+
+def main(argv=None):
+    args = parse(argv)
     world, rank, local = dist_setup(args)
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
-    from nvflare_amd import _native as N
-    from nvflare_amd.device import DeviceContext, TiledLayout
+    from nvflare_amd.device import DeviceContext
 
     ctx = DeviceContext.get(local)
     ctx.set_launch(args.blocks_per_cu, args.unroll)
     ctx.set_variant(args.variant)
-    K = int(args.clients)
-    P = int(args.params)
-    op = N.FEDAVG_OP_TORCH if args.mode == "torch" else N.FEDAVG_OP_NUMPY
-    fin = N.FEDAVG_FIN_DIV if args.mode == "torch" else N.FEDAVG_FIN_SCALE
-    col0 = rank_bucket(rank, P)  # weak scaling: rank r owns param bucket [r*P, (r+1)*P)
-
-    free, total = ctx.mem_info()
-    lay = TiledLayout(args.tile, K)  # the engine's slab layout: K client slots interleaved per tile
-    need = lay.slab_elems(P) * 4 + P * 4
-    if need > free:
-        raise SystemExit(f"rank {rank}: workload needs {need / 2**30:.1f} GiB, device has {free / 2**30:.1f} GiB free")
-
-    end = (P + 3) // 4 * 4
-    slab = ctx.alloc(lay.slab_elems(P) * 4)
-    epi_bufs = {"none": 1, "add_base": 1, "sgd": 2}.get(args.epilogue, 3)  # out | p+buf | p+m+v
-    state = [ctx.alloc(end * 4) for _ in range(epi_bufs)]
-    out = state[0]
-    bases = [slab.ptr + lay.slot_offset_elems(k) * 4 for k in range(K)]
-    for k, base in enumerate(bases):
-        ctx.fill_synthetic_f32(base, P, args.seed, k, col0, lay.tile, lay.tile_stride)
-    ctx.sync()
-    # per-client weights: aggregation_weight 1.0 x NUM_STEPS_CURRENT_ROUND = 1 + (37k mod 100)
-    weights = [1.0 * float(1 + (37 * k) % 100) for k in range(K)]
-    count = None
-    for w in weights:
-        count = w if count is None else count + w
-
-    epi = None
-    if args.epilogue != "none":
-        for j, b in enumerate(state):  # initial params (or base weights), zero optimizer state
-            if j == 0:
-                ctx.fill_synthetic_f32(b.ptr, end, args.seed + 7, 0, col0)
+    K = args.clients
+    label = (PRESET_NAMES[args.config] if args.preset_exact
+             else f"custom (preset {args.config} overridden: {K} clients x {args.params} params, {args.epilogue})")
+    main_res = run_workload(args, ctx, world, rank, K, args.params, args.scaling, args.epilogue,
+                            baseline=(world == 1 and rank == 0 and not args.no_cpu_baseline), seed=args.seed)
+    if "skipped" in main_res:
+        raise SystemExit(f"rank {rank}: workload {main_res['skipped']}")
+    also = []
+    failed = bool((main_res.get("spot_check") or {}).get("mismatches"))  # counts summed over ranks: all agree
+    for cfg in args.also:
+        p = PRESETS[cfg]
+        r = run_workload(args, ctx, world, rank, p["clients"], p["params"], p["scaling"], p["epilogue"],
+                         baseline=False, seed=args.seed)
+        failed = failed or bool((r.get("spot_check") or {}).get("mismatches"))
+        if rank == 0:
+            if "skipped" in r:
+                also.append({"baseline_config": PRESET_NAMES[cfg], "n_gpus": world, "skipped": r["skipped"]})
             else:
-                ctx.memset(b.ptr, 0, end * 4)
-        epi = N.Epilogue()
-        epi.kind = {"add_base": N.FEDAVG_EPI_ADD_BASE, "sgd": N.FEDAVG_EPI_SGD, "adam": N.FEDAVG_EPI_ADAM,
-                    "adamax": N.FEDAVG_EPI_ADAMAX, "nadam": N.FEDAVG_EPI_NADAM, "radam": N.FEDAVG_EPI_RADAM}[args.epilogue]
-        if args.epilogue == "add_base":
-            epi.base = out.ptr
-        elif args.epilogue == "sgd":
-            epi.param, epi.state1 = state[0].ptr, state[1].ptr
-            epi.lr, epi.momentum = 1.0, 0.9
-        else:
-            epi.param, epi.state1, epi.state2 = state[0].ptr, state[1].ptr, state[2].ptr
-            epi.lr, epi.beta1, epi.beta2, epi.eps = 1e-3, 0.9, 0.999, 1e-8
-            epi.momentum_decay, epi.mu_product = 4e-3, 1.0  # NAdam (mu_product held at its first-step value)
-        ctx.sync()
-    n_step = [0]
-
-    def step():
-        if epi is None:
-            ctx.accumulate_tiled(bases, weights, lay.tile, lay.tile_stride, 0, end, out.ptr, op, fin, count)
-            return
-        n_step[0] += 1
-        epi.step = float(n_step[0])
-        epi.first_step = int(n_step[0] == 1)
-        ctx.accumulate_tiled_epi(bases, weights, lay.tile, lay.tile_stride, 0, end,
-                                 out.ptr if args.epilogue == "add_base" else None, op, fin, count, epi)
-
-    for _ in range(args.warmup):
-        step()
-    barrier_sync(world, ctx)
-
-    n_launch0 = ctx.launch_count()
-    ctx.timing_begin()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    barrier_sync(world, ctx)
-    t1 = time.perf_counter()
-    ev_ms = ctx.timing_end()
-    launches_per_step = (ctx.launch_count() - n_launch0) / args.steps
-
-    wall = max_over_ranks(world, t1 - t0)
-    kernel_ms = ev_ms / args.steps
-    kernel_ms_max = max_over_ranks(world, kernel_ms)
-
-    extra = {}
-    if args.epilogue != "none":
-        args.spot_check = 0  # the spot check covers the plain aggregation output only
-    if world == 1:
-        extra = cpu_baseline_and_spot_check(args, ctx, K, out, weights, count, P, col0, op)
-    else:  # every rank checks its own bucket; the counts are summed (no CPU baseline at N > 1)
-        extra = cpu_baseline_and_spot_check(args, ctx, K, out, weights, count, P, col0, op, baseline=False)
-        if "spot_check" in extra:
-            sampled, mism = sum_over_ranks(world, [extra["spot_check"]["sampled"], extra["spot_check"]["mismatches"]])
-            extra["spot_check"].update(sampled=sampled, mismatches=mism, ranks=world)
-
+                entry = summarize(args, world, r, p["clients"], p["scaling"], p["epilogue"], PRESET_NAMES[cfg])
+                entry["n_gpus"] = world
+                entry["spot_check"] = r["spot_check"]
+                also.append(entry)
     if rank == 0:
-        bytes_step = 4.0 * K * P * world  # aggregated client bytes per step, all ranks
-        value = bytes_step * args.steps / wall / 2**30
-        epi_bytes = {"none": 4.0, "add_base": 8.0, "sgd": 16.0}.get(args.epilogue, 24.0)
-        alg_bytes_launch = 4.0 * K * P + epi_bytes * P
-        traffic, traffic_src = pmc_traffic(args, K, P)
-        achieved = alg_bytes_launch / (kernel_ms / 1e3) / 1e9
+        s = summarize(args, world, main_res, K, args.scaling, args.epilogue, label)
         line = {
             "metric": METRIC,
-            "value": round(value, 2),
+            "value": s["value"],
             "unit": "GiB/s",
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": round(wall / args.steps * 1e3, 4),
+            "ms_per_step": s["ms_per_step"],
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": s["scaling"],
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic: device counter-hash generator (Irwin-Hall(4) ~N(0,1)), host twin in oracle/",
-            "config": {
-                "workload": f"{K} clients x {P} fp32 params per GPU, weighted FedAvg, {args.mode}-mode arithmetic"
-                            + ("" if args.epilogue == "none" else f", fused {args.epilogue} server update"),
-                "epilogue": args.epilogue,
-                "clients": K,
-                "params_per_gpu": P,
-                "mode": args.mode,
-                "parallelism": f"param-bucket shards x{world}, no data-path collective",
-                "layout": f"tiled slab, {lay.tile}-element tiles x {K} slots",
-                "kernel": (("fedavg_tiles_burst_f32x4 (results staged on chip, stored as chip-wide bursts; "
-                            + ("8 register-held tiles per block per launch)" if args.variant & 32
-                               else "8 register- + 10 LDS-held tiles per block per launch, one block per CU)"
-                               if K >= 32 and not args.variant & 64
-                               else "8 register- + 4 LDS-held tiles per block per launch)"))
-                           if epi is None and args.variant & 11 == 0
-                           else "fedavg_tiles_epi_burst_f32x4" if epi is not None and args.variant & 12 == 0
-                           else "fedavg_tiles_epi_f32x4" if epi is not None else "fedavg_tiles_f32x4"),
-            },
-            "pct_hbm_peak": round(100.0 * achieved / HBM_PEAK_GBS, 2),
-            "roofline": {
-                "bound": "hbm",
-                "achieved": round(achieved, 1),
-                "peak": HBM_PEAK_GBS,
-                "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": traffic,
-                "traffic_source": traffic_src,
-                "kernel_ms_avg": round(kernel_ms, 4),
-                "kernel_ms_avg_max_rank": round(kernel_ms_max, 4),
-                "alg_bytes_per_launch": alg_bytes_launch,
-                # one aggregation = launches_per_step kernel launches (the burst kernel: one per 8 tiles per
-                # block); kernel_ms_avg and alg_bytes_per_launch are per aggregation, launch_us_avg is the
-                # per-launch figure a rocprofv3 --stats average compares with
-                "launches_per_step": launches_per_step,
-                "launch_us_avg": round(kernel_ms * 1e3 / max(launches_per_step, 1), 2),
-            },
+            "config": s["config"],
+            "pct_hbm_peak": s["pct_hbm_peak"],
+            "roofline": s["roofline"],
+            "cpu_baseline": main_res.get("cpu_baseline"),
         }
-        if "cpu_baseline" in extra:
-            line["cpu_baseline"] = extra["cpu_baseline"]
-        else:
-            line["cpu_baseline"] = None
-        if "spot_check" in extra:
-            line["spot_check"] = extra["spot_check"]
+        if main_res.get("spot_check") is not None:
+            line["spot_check"] = main_res["spot_check"]
+        if also:
+            line["also"] = also
         print(json.dumps(line), flush=True)
-    failed = bool(extra.get("spot_check", {}).get("mismatches"))  # summed over ranks: every rank agrees
-    if failed and rank == 0:
-        print("SPOT CHECK FAILED", file=sys.stderr)
+        if failed:
+            print("SPOT CHECK FAILED", file=sys.stderr)
     if world > 1:
         import torch.distributed as dist
 

@@ -172,12 +172,12 @@ class WeightedAggregationHelper(object):
             host_items = []
             sharded = isinstance(self._engine, ShardedFedAvg)
             total = self.total
-            kcc = self.key_contribution_counts
+            skipped, counted = [], []  # committed once the device has staged the contribution
             for k, v in data.items():
                 if self.exclude_vars is not None and self.exclude_vars.search(k):
-                    self.skipped_keys.add(k)
+                    skipped.append(k)
                     continue
-                kcc[k] = kcc.get(k, 0) + 1
+                counted.append(k)
                 if type(v) is np.ndarray:  # plain array: no lazy ref, no quantized payload -> device unless host key
                     (host_items if isinstance(total.get(k), _HostValue) else device_items).append((k, v))
                     continue
@@ -200,9 +200,14 @@ class WeightedAggregationHelper(object):
                 else:
                     host_items.append((k, v))
             if device_items:
+                # all or nothing (engine.DeviceFedAvg.add): a failed staging leaves no trace of this contribution
                 self._engine.add(device_items, weight, self.weigh_by_local_iter)
                 for k, _ in device_items:
                     self.total[k] = _ON_DEVICE
+            self.skipped_keys.update(skipped)
+            kcc = self.key_contribution_counts
+            for k in counted:
+                kcc[k] = kcc.get(k, 0) + 1
             for k, v in host_items:
                 self._add_host(k, v, weight)
             for k, _ in device_items:

@@ -255,6 +255,22 @@ _TORCH_ALPHA_LIMITS = {np.dtype(np.float32): (_FLT_MAX, "float"), np.dtype(np.fl
                        BF16_NP: (3.3895313892515355e38, "c10::BFloat16")}
 
 
+class _AddTx:
+    """What one ``DeviceFedAvg.add`` took (engine.py): rolled back if the add fails, kept for ``undo_add``."""
+
+    __slots__ = ("n_keys", "layout", "slots", "bufs", "staged", "counts", "moved", "committed")
+
+    def __init__(self, n_keys: int, layout: Dict[int, int]):
+        self.n_keys = n_keys  # keys registered before this add (the ones after it are its own)
+        self.layout = layout  # arena flat-layout sizes before this add
+        self.slots: List[_Slot] = []
+        self.bufs: List[DeviceBuffer] = []
+        self.staged: List[Tuple["_KeyState", _Staged]] = []
+        self.counts: List[tuple] = []  # (key state, count before, count after)
+        self.moved = 0
+        self.committed = False
+
+
 class _KeyState:
     __slots__ = ("name", "shape", "container", "torch_device", "in_np", "acc_np", "op", "fin", "n", "arena",
                  "offset", "pending", "acc_valid", "acc_buf", "count", "done", "sig", "int_sum", "doomed")
@@ -298,6 +314,7 @@ class DeviceFedAvg:
         self._round_clients = 0
         self.peak_clients = 0
         self._deferred = None  # DeferredRound still holding fp32 slots (result_deferred)
+        self._last_add: Optional[_AddTx] = None  # the last committed add, while undo_add may take it back
         self._tails_cache: Dict[tuple, np.ndarray] = {}  # torch16 scalar-loop elements per run layout
         # key -> (first element within its whole tensor, the whole tensor's size) for keys that are a bucket of a
         # larger tensor (sharding.ShardedFedAvg); other keys are whole tensors
@@ -509,14 +526,18 @@ class DeviceFedAvg:
         if is_torch_tensor(v) and v.device.type != "cpu" and v.device.index != self.ctx.device:
             raise ValueError(f"nvflare_amd: tensor on {v.device}, engine on device {self.ctx.device}")
 
-    def _stage_arena(self, arena: _Arena, items, weight) -> None:
-        """One contribution's keys of one arena into one slot (the slot base + logical offsets)."""
+    def _stage_arena(self, arena: _Arena, items, weight, tx: "_AddTx") -> None:
+        """One contribution's keys of one arena into one slot (the slot base + logical offsets).  The staged
+        records go to ``tx``; the keys' ``pending`` lists only see them when the whole contribution commits."""
         extent = max(st.offset + st.n for st, _ in items)
         slot = self._acquire_slot(arena, extent)
+        tx.slots.append(slot)
+        slot.refs += len(items)  # held by this contribution: a fold while its other arenas stage keeps it live
         lay = slot.slab.layout
         es = arena.esize
         host_pieces, keep = [], []
         quantized = []
+        device_src = False
         staged = _Staged(weight, slot=slot)  # immutable: shared by every key of this contribution in this slot
         moved = 0
         for st, v in sorted(items, key=lambda x: x[0].offset):
@@ -531,56 +552,123 @@ class DeviceFedAvg:
                 src, ptr, nbytes, on_dev = self._source(v)
                 if on_dev:
                     self.ctx.d2d_tiled(slot.base, lay.tile * es, lay.tile_stride * es, st.offset * es, ptr, nbytes)
+                    keep.append(src)
+                    device_src = True
                 else:
                     host_pieces.append((st.offset * es, ptr, nbytes))
                     keep.append(src)
-            st.pending.append(staged)
+            tx.staged.append((st, staged))
             moved += nbytes
-        slot.refs += len(items)
-        self.stats["h2d_bytes"] += moved
         # every host key of this client in one pass through the pinned ring (one DMA per 64 MiB)
         self.ctx.h2d_tiled_multi(slot.base, lay.tile * es, lay.tile_stride * es, host_pieces)
-        del keep
         for st, v in quantized:  # compressed bytes over PCIe, fp32 written into the slot by the GPU
             stager().dequantize_into(self.ctx, v, slot.base, lay.tile, lay.tile_stride, st.offset)
+        tx.moved += moved
+        if device_src:
+            # the device-to-device copies run on the library's stream: finish them before the caller (or torch's
+            # allocator, for a contiguous() temporary) may reuse the source memory -- accept must not alias
+            self.ctx.sync()
+        del keep
 
-    def add(self, items: List[Tuple[str, Any]], weight, weighted: bool) -> None:
-        """Stage one contribution's device-path arrays (already filtered by exclude_vars)."""
+    def add(self, items: List[Tuple[str, Any]], weight, weighted: bool) -> "_AddTx":
+        """Stage one contribution's device-path arrays (already filtered by exclude_vars).
+
+        All or nothing: the contribution's slots, side buffers and keys it introduces are taken inside a
+        transaction; only when every arena and side buffer is staged do its records join the keys' pending
+        lists and its weight their counts (the reference's per-key ``counts[k] += w`` next to the key's sum,
+        weighted_aggregation_helper.py:201,216).  On any exception (an allocation, a copy) everything is given
+        back and the next aggregation is the one over the contributions accepted so far.  Returns the
+        committed transaction, which ``undo_add`` can take back while it is the engine's last operation (a
+        sharded contribution whose other buckets failed, sharding.ShardedFedAvg.add)."""
         # quantized payloads dequantize on the device straight into their fp32 slot; other dtypes take
         # the generic path from their (device-dequantized) host values
         items = [(k, v.materialize() if isinstance(v, QuantizedPayload) and v.out_dtype != np.float32 else v)
                  for k, v in items]
         with self.lock, self.ctx.lock:
+            self._last_add = None
             self._settle()
             self._check_torch_alpha(items, weight, weighted)
-            states = [(self._register_key(k, v, weight, weighted), v) for k, v in items]
-            for _, v in states:
-                if type(v) is not np.ndarray:
-                    self._check_device(v)
+            tx = _AddTx(len(self.keys), {fmt: a.layout_elems for fmt, a in self.arenas.items()})
+            try:
+                states = [(self._register_key(k, v, weight, weighted), v) for k, v in items]
+                for _, v in states:
+                    if type(v) is not np.ndarray:
+                        self._check_device(v)
+                by_arena: Dict[int, Tuple[_Arena, list]] = {}
+                for st, v in states:
+                    if st.arena is not None and st.n > 0:
+                        by_arena.setdefault(st.arena.fmt, (st.arena, []))[1].append((st, v))
+                for arena, arena_items in by_arena.values():
+                    self._stage_arena(arena, arena_items, weight, tx)
+                for st, v in states:
+                    if st.arena is not None or st.n == 0 or st.doomed:
+                        if st.n == 0 and not st.doomed:
+                            tx.staged.append((st, _Staged(weight)))
+                        continue
+                    buf = self.ctx.alloc(st.n * st.in_np.itemsize)
+                    tx.bufs.append(buf)
+                    self._side_bufs.append(buf)
+                    keep, ptr, nbytes, on_dev = self._source(v)
+                    if on_dev:
+                        self.ctx.d2d(buf.ptr, ptr, nbytes)
+                        self.ctx.sync()  # as in _stage_arena: the source may be reused once we return
+                    else:
+                        self.ctx.h2d_ptr(buf.ptr, ptr, nbytes)
+                    del keep
+                    tx.staged.append((st, _Staged(weight, buf=buf)))
+                    tx.moved += nbytes
+                tx.counts = [(st, st.count, weight if st.count is None else st.count + weight) for st, _ in states]
+            except BaseException:
+                self._give_back(tx)
+                raise
+            # commit (nothing below raises)
+            for st, p in tx.staged:
+                st.pending.append(p)
+            for st, _, new in tx.counts:
+                st.count = new
             self._round_clients += 1
-            by_arena: Dict[int, Tuple[_Arena, list]] = {}
-            for st, v in states:
-                if st.arena is not None and st.n > 0:
-                    by_arena.setdefault(st.arena.fmt, (st.arena, []))[1].append((st, v))
-            for arena, arena_items in by_arena.values():
-                self._stage_arena(arena, arena_items, weight)
-            for st, v in states:
-                if st.arena is not None or st.n == 0 or st.doomed:
-                    if st.n == 0 and not st.doomed:
-                        st.pending.append(_Staged(weight))
-                    continue
-                buf = self.ctx.alloc(st.n * st.in_np.itemsize)
-                self._side_bufs.append(buf)
-                keep, ptr, nbytes, on_dev = self._source(v)
-                if on_dev:
-                    self.ctx.d2d(buf.ptr, ptr, nbytes)
-                else:
-                    self.ctx.h2d_ptr(buf.ptr, ptr, nbytes)
-                del keep
-                st.pending.append(_Staged(weight, buf=buf))
-                self.stats["h2d_bytes"] += nbytes
-            for st, _ in states:
-                st.count = weight if st.count is None else st.count + weight
+            self.stats["h2d_bytes"] += tx.moved
+            tx.committed = True
+            self._last_add = tx
+            return tx
+
+    def _give_back(self, tx: "_AddTx") -> None:
+        """Return what an uncommitted (or undone) contribution took: slots, side buffers, the keys it
+        introduced and their place in the arenas' flat layouts."""
+        try:
+            self.ctx.sync()  # copies into the slots / buffers may still be in flight
+        except Exception:  # pragma: no cover - the device error is the one being raised
+            pass
+        for slot in tx.slots:
+            slot.refs = 0
+            self._release_slot(slot)
+        for buf in tx.bufs:
+            if buf in self._side_bufs:
+                self._side_bufs.remove(buf)
+            buf.close()
+        for name in list(self.keys)[tx.n_keys:]:  # dicts keep insertion order: the keys this add registered
+            del self.keys[name]
+        for fmt, a in self.arenas.items():
+            a.layout_elems = tx.layout.get(fmt, 0)
+
+    def undo_add(self, tx: "_AddTx") -> None:
+        """Take back a committed contribution, which must be this engine's last operation (nothing was added,
+        folded, aggregated or reset since): its pending records, its weight in the counts, its slots and side
+        buffers and the keys it introduced."""
+        with self.lock, self.ctx.lock:
+            if tx is None or not tx.committed or tx is not self._last_add:
+                raise RuntimeError("nvflare_amd: only the engine's last contribution can be taken back")
+            for st, p in reversed(tx.staged):
+                if not st.pending or st.pending[-1] is not p:
+                    raise RuntimeError("nvflare_amd: contribution already consumed; cannot take it back")
+                st.pending.pop()
+            for st, old, _ in tx.counts:
+                st.count = old
+            self._round_clients -= 1
+            self.stats["h2d_bytes"] -= tx.moved
+            tx.committed = False
+            self._last_add = None
+            self._give_back(tx)
 
     # ------------------------------------------------------------------ compute
     def _runs(self, keys: Optional[Dict[str, _KeyState]] = None, arena: Optional[_Arena] = None):
@@ -812,11 +900,12 @@ class DeviceFedAvg:
                 st.done = True
         self.ctx.mark(arena.layout_elems * arena.esize)
 
-    def _host_arenas(self, arenas, pipelined: Optional[_Arena] = None) -> Dict[int, np.ndarray]:
-        """One D2H per arena holding host-container keys (results are views of these arrays)."""
+    def _host_arenas(self, arenas, pipelined: Optional[_Arena] = None, skip=()) -> Dict[int, np.ndarray]:
+        """One D2H per arena holding host-container keys (results are views of these arrays); keys in ``skip`` go
+        to destinations of their own (``result(host_dest=...)``)."""
         hosts = {}
         for a in sorted(arenas, key=lambda x: x is not pipelined):  # the pipelined D2H first
-            if self._has_host_keys(a):
+            if self._has_host_keys(a, skip):
                 host = a.host_pool.take(a.layout_elems, a.np_dtype, pin=self.ctx)
                 if a is pipelined:
                     self.ctx.d2h_marked(host, a.acc.ptr)
@@ -825,9 +914,9 @@ class DeviceFedAvg:
                 hosts[a.fmt] = host
         return hosts
 
-    def _has_host_keys(self, a: _Arena) -> bool:
+    def _has_host_keys(self, a: _Arena, skip=()) -> bool:
         return bool(a.layout_elems) and any(st.arena is a and st.n > 0 and st.torch_device is None
-                                            for st in self.keys.values())
+                                            and st.name not in skip for st in self.keys.values())
 
     def _check_doomed(self) -> None:
         """Keys the reference's get_result (weighted_aggregation_helper.py:226-240) fails on, in its key order,
@@ -840,22 +929,43 @@ class DeviceFedAvg:
             if st.fin == N.FEDAVG_FIN_SCALE and type(st.count) in (int, float, bool) and st.count == 0:  # not numpy scalars
                 raise ZeroDivisionError("float division by zero")
 
-    def result(self) -> Dict[str, Any]:
-        """Finalise every key on the device and return host (or device-tensor) results."""
+    def result(self, host_dest: Optional[Dict[str, Tuple[np.ndarray, int]]] = None) -> Dict[str, Any]:
+        """Finalise every key on the device and return host (or device-tensor) results.
+
+        ``host_dest`` ({key: (host array, element offset)}): those of the keys that are host-container arena keys
+        are copied straight into the caller's array (one ``fedavg_d2h_multi`` per array and arena, page-locked
+        destinations written by the DMA) and come back as None -- sharding.ShardedFedAvg assembles whole keys
+        from its buckets this way, without a host-side concatenation."""
         self._check_doomed()
         with self.lock, self.ctx.lock:
+            self._last_add = None
             self._settle()
+            direct = {}
+            for n, d in (host_dest or {}).items():
+                st = self.keys.get(n)
+                if st is not None and st.arena is not None and st.n > 0 and st.torch_device is None:
+                    if np.dtype(d[0].dtype) != st.arena.np_dtype:
+                        raise TypeError(f"nvflare_amd: host destination of {n!r} is {d[0].dtype}, not {st.arena.np_dtype}")
+                    direct[n] = d
             # the largest host-bound arena leaves in a pipelined D2H that overlaps its own launches
             big = [a for a in self.arenas.values()
-                   if a.layout_elems * a.esize >= 2 * EGRESS_CHUNK and self._has_host_keys(a)]
+                   if a.layout_elems * a.esize >= 2 * EGRESS_CHUNK and self._has_host_keys(a, direct)]
             pipelined = max(big, key=lambda a: a.layout_elems * a.esize) if big else None
             if pipelined is not None:
                 self._launch_arena_chunked(pipelined)
             self._launch_arena(final=True, arenas=[a for a in self.arenas.values() if a is not pipelined])
             self._launch_side(final=True)
-            hosts = self._host_arenas(self.arenas.values(), pipelined)
+            hosts = self._host_arenas(self.arenas.values(), pipelined, direct)
+            groups: Dict[tuple, tuple] = {}
+            for n, (host, off) in direct.items():
+                st = self.keys[n]
+                es = st.arena.esize
+                g = groups.setdefault((id(host), st.arena.fmt), (host, st.arena, []))
+                g[2].append((off * es, st.offset * es, st.n * es))
+            for host, arena, pieces in groups.values():
+                self.ctx.d2h_multi(host, arena.acc.ptr, pieces)
             self.ctx.sync()
-            return {name: self._materialize(st, hosts) for name, st in self.keys.items()}
+            return {name: None if name in direct else self._materialize(st, hosts) for name, st in self.keys.items()}
 
     def result_deferred(self) -> Dict[str, Any]:
         """``result()`` with the fp32 arena keys left on the device: they come back as ``DeferredAggregate``
@@ -867,6 +977,7 @@ class DeviceFedAvg:
 
         self._check_doomed()
         with self.lock, self.ctx.lock:
+            self._last_add = None
             self._settle()
             others = [a for a in self.arenas.values() if a.fmt != N.FEDAVG_F32]
             self._launch_arena(final=True, arenas=others)
@@ -933,6 +1044,7 @@ class DeviceFedAvg:
         """Drop the round's state; slabs are kept (and consolidated) for the next round."""
         self.peak_clients = max(self.peak_clients, self._round_clients)
         self._round_clients = 0
+        self._last_add = None
         if self._ctx is None:
             self.keys.clear()
             for a in self.arenas.values():

@@ -21,6 +21,7 @@ from typing import Any, Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
 
+from .device import BF16_NP, HostArenaPool
 from .engine import DeviceFedAvg, is_torch_tensor
 
 BUCKET_ALIGN = 4096  # elements: a bucket boundary never splits a kernel tile
@@ -55,6 +56,8 @@ class ShardedFedAvg:
     `len(devices)` contiguous, tile-aligned pieces (keys shorter than one tile stay whole on one
     device).  Partial keys and keys first seen late work exactly as on one device, bucket by bucket."""
 
+    direct_egress = True  # False: round 2's per-key concatenation of the bucket results (A/B tools only)
+
     def __init__(self, devices: Sequence[int], max_resident_bytes: Optional[int] = None):
         self.devices = list(devices)
         if not self.devices:
@@ -81,6 +84,7 @@ class ShardedFedAvg:
         return out
 
     def add(self, items: List[Tuple[str, Any]], weight, weighted: bool) -> None:
+        """Stage one contribution's pieces on every device in parallel; all or nothing (engine.DeviceFedAvg.add)."""
         with self.lock:
             # Each engine sees only flat slices, so a reshaped contribution with the same element count
             # would pass every shard: check the shape here, for every item before any shard is staged,
@@ -92,12 +96,27 @@ class ShardedFedAvg:
                 if first is not None and first != shape:
                     raise ValueError(f"nvflare_amd: key {k!r} shape {shape} != first contribution's {first}")
                 new.setdefault(k, shape)
+            introduced = [k for k in new if k not in self._shapes]
             for k, shape in new.items():
                 self._shapes.setdefault(k, shape)
             futs = [self._pool.submit(eng.add, self._pieces(b, items), weight, weighted)
                     for b, eng in enumerate(self.engines)]
+            txs, err = [], None
             for f in futs:
-                f.result()
+                try:
+                    txs.append(f.result())
+                except BaseException as e:  # noqa: B036 - re-raised below, after the other buckets are undone
+                    txs.append(None)
+                    err = err or e
+            if err is not None:
+                # all or nothing across buckets too: the buckets that staged give their piece back (each engine's
+                # add is already atomic), so no bucket counts a weight the others do not
+                for eng, tx in zip(self.engines, txs):
+                    if tx is not None:
+                        eng.undo_add(tx)
+                for k in introduced:
+                    self._shapes.pop(k, None)
+                raise err
 
     def _assemble(self, k: str, plist: List[Tuple[int, Any]]):
         """The whole key from its bucket results (plist sorted by offset)."""
@@ -112,10 +131,15 @@ class ShardedFedAvg:
         res = flat.reshape(shape)
         return res[()] if res.ndim == 0 else res
 
-    def _bucket_results(self, deferred: bool) -> Dict[str, List[Tuple[int, Any]]]:
-        fn = (lambda e: e.result_deferred() if e.keys else {}) if deferred else (lambda e: e.result() if e.keys else {})
+    def _bucket_results(self, deferred: bool, dests=None) -> Dict[str, List[Tuple[int, Any]]]:
+        if deferred:
+            def fn(b):
+                return self.engines[b].result_deferred() if self.engines[b].keys else {}
+        else:
+            def fn(b):
+                return self.engines[b].result(host_dest=dests[b] if dests else None) if self.engines[b].keys else {}
         pieces: Dict[str, List[Tuple[int, Any]]] = {}
-        for res in self._pool.map(fn, self.engines):
+        for res in self._pool.map(fn, range(len(self.engines))):
             for sub, arr in res.items():
                 k, off = sub.rsplit("\x00", 1)  # a key may itself hold NULs (SCAFFOLD control prefix)
                 pieces.setdefault(k, []).append((int(off), arr))
@@ -123,9 +147,64 @@ class ShardedFedAvg:
             plist.sort(key=lambda x: x[0])
         return pieces
 
+    def _direct_plan(self):
+        """Whole-key host destinations for the keys whose every bucket is a host-container arena key: one host
+        array per element format (page-locked once, reused across rounds by a HostArenaPool), each such key at its
+        own offset.  Returns ({key: (array, element offset, container)}, per-engine {subkey: (array, offset)})."""
+        fmt: Dict[str, Any] = {}
+        for e in self.engines:
+            for sub, st in e.keys.items():
+                k = sub.rsplit("\x00", 1)[0]
+                ok = st.arena is not None and st.n > 0 and st.torch_device is None
+                tag = (st.arena.np_dtype, st.container) if ok else None
+                fmt[k] = tag if fmt.get(k, tag) == tag and tag is not None else False
+        sizes: Dict[Any, int] = {}
+        offsets: Dict[str, Tuple[Any, int]] = {}
+        for k, tag in fmt.items():
+            if not tag:
+                continue
+            n = int(np.prod(self._shapes[k], dtype=np.int64)) if self._shapes[k] else 1
+            offsets[k] = (tag[0], sizes.get(tag[0], 0))
+            sizes[tag[0]] = sizes.get(tag[0], 0) + n
+        hosts = {dt: self._host_pool(dt).take(n, dt, pin=self.engines[0].ctx) for dt, n in sizes.items()}
+        plan = {k: (hosts[dt], off, fmt[k][1]) for k, (dt, off) in offsets.items()}
+        dests = []
+        for e in self.engines:
+            d = {}
+            for sub in e.keys:
+                k, lo = sub.rsplit("\x00", 1)
+                if k in plan:
+                    d[sub] = (plan[k][0], plan[k][1] + int(lo))
+            dests.append(d)
+        return plan, dests
+
+    def _host_pool(self, dt):
+        pools = self.__dict__.setdefault("_host_pools", {})
+        if dt not in pools:
+            pools[dt] = HostArenaPool()
+        return pools[dt]
+
+    def _view(self, k: str, host: np.ndarray, off: int, container: str):
+        """Key k as a view of the host array its buckets were copied into (the engine's _materialize rules)."""
+        shape = self._shapes[k]
+        n = int(np.prod(shape, dtype=np.int64)) if shape else 1
+        arr = host[off: off + n].reshape(shape)
+        if container == "torch":
+            import torch
+
+            if arr.dtype == BF16_NP:
+                return torch.from_numpy(arr.view(np.uint16)).view(torch.bfloat16)
+            return torch.from_numpy(arr)
+        return arr[()] if arr.ndim == 0 else arr
+
     def result(self) -> Dict[str, Any]:
+        """Every bucket finalised on its device; keys whose buckets are all host-container arena keys are copied by
+        each device straight to their place in one page-locked host array (each GPU over its own PCIe link, no
+        host-side concatenation); others (device tensors, side-buffer keys) are reassembled per key."""
         with self.lock:
-            return {k: self._assemble(k, plist) for k, plist in self._bucket_results(False).items()}
+            plan, dests = self._direct_plan() if self.direct_egress else ({}, None)
+            pieces = self._bucket_results(False, dests)
+            return {k: self._view(k, *plan[k]) if k in plan else self._assemble(k, plist) for k, plist in pieces.items()}
 
     def result_deferred(self) -> Dict[str, Any]:
         """``result()`` with every fp32 key left on the devices, one ``ShardedDeferredAggregate`` per key whose

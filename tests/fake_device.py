@@ -117,6 +117,14 @@ class FakeDeviceContext:
     def d2h(self, host, src):
         host.reshape(-1).view(np.uint8)[:] = self._view(src, host.nbytes)
 
+    def d2h_multi(self, host, src, pieces):
+        assert host.flags.c_contiguous
+        flat = host.reshape(-1).view(np.uint8)
+        for ho, do, nb in pieces:
+            assert 0 <= ho and ho + nb <= flat.size, "d2h_multi piece outside the host array"
+            flat[ho:ho + nb] = self._view(src + do, nb)
+        self.d2h_multi_calls = getattr(self, "d2h_multi_calls", 0) + 1
+
     def mark(self, ready_bytes):
         marks = self.__dict__.setdefault("marks", [])
         assert not marks or ready_bytes >= marks[-1], "marks must be non-decreasing"

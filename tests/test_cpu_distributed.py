@@ -41,15 +41,15 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, P, K, q):
+def _worker(rank, world, port, P, K, q, scaling="weak"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         import bench
         from oracle import fedavg_oracle as orc
 
-        col0 = bench.rank_bucket(rank, P)
-        rows = [orc.synth_values(1000, k, np.arange(col0, col0 + P, dtype=np.uint64)) for k in range(K)]
+        col0, n = bench.rank_span(scaling, rank, world, P)
+        rows = [orc.synth_values(1000, k, np.arange(col0, col0 + n, dtype=np.uint64)) for k in range(K)]
         ws = orc.synth_weights(K)
         part = orc.fedavg_c(rows, ws, orc.MODE_TORCH)
         gathered = [None] * world if rank == 0 else None
@@ -79,6 +79,50 @@ def test_weak_scaling_buckets_gloo(oracle):
     assert np.array_equal(res.view(np.uint32), full.view(np.uint32))
     assert tmax == 2.0  # max over ranks
     assert sums == [1, 2]  # sum over ranks
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_strong_scaling_buckets_gloo(oracle, world):
+    """bench.py --scaling strong (BASELINE configs 4 and 5): one P-param model split by bucket_ranges over the
+    ranks; the ranks' buckets, reassembled, are the one-process aggregation of the whole model, bit for bit."""
+    P, K = 3 * 4096 * 5 + 77, 7
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, P, K, q, "strong")) for r in range(world)]
+    for p in procs:
+        p.start()
+    res, (tmax, sums) = q.get(timeout=120)
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    rows = [oracle.synth_values(1000, k, np.arange(P, dtype=np.uint64)) for k in range(K)]
+    full = oracle.fedavg_c(rows, oracle.synth_weights(K), oracle.MODE_TORCH)
+    assert res.size == P and np.array_equal(res.view(np.uint32), full.view(np.uint32))
+    assert tmax == float(world) and sums == [sum(range(world)), world]
+
+
+def test_bench_presets_follow_baseline():
+    """bench.py --config N fills K, P, the epilogue and the scaling from BASELINE.json configs[1..4]; the default run
+    (config 3) also measures configs 5 and 4 under strong scaling, explicit overrides turn that off."""
+    import bench
+
+    a = bench.parse([])
+    assert (a.clients, a.params, a.epilogue, a.scaling, a.also) == (64, 10**9, "none", "weak", [5, 4])
+    assert (lambda c: (c.clients, c.params, c.epilogue, c.scaling))(bench.parse(["--config", "2"])) == \
+        (8, 125_000_000, "none", "weak")
+    assert (lambda c: (c.clients, c.params, c.epilogue, c.scaling))(bench.parse(["--config", "4"])) == \
+        (256, 350_000_000, "none", "strong")
+    assert (lambda c: (c.clients, c.params, c.epilogue, c.scaling))(bench.parse(["--config", "5"])) == \
+        (64, 10**9, "adam", "strong")
+    b = bench.parse(["--clients", "8", "--params", "1.25e8"])
+    assert b.also == [] and not b.preset_exact and b.scaling == "weak"
+    c = bench.parse(["--global-params", "3.5e8", "--clients", "256"])
+    assert c.scaling == "strong" and c.params == 350_000_000
+    # config 4 per GPU at 8 GPUs: 256 clients x 43.75 M (bucket_ranges in whole tiles)
+    spans = [bench.rank_span("strong", r, 8, 350_000_000) for r in range(8)]
+    assert sum(n for _, n in spans) == 350_000_000 and all(abs(n - 43_750_000) < 4096 for _, n in spans)
+    assert spans[0][0] == 0 and all(spans[i][0] + spans[i][1] == spans[i + 1][0] for i in range(7))
 
 
 def test_sharded_pieces_reassemble(oracle):
@@ -217,3 +261,40 @@ def test_sharded_deferred_rounds_match_eager():
             assert np.array_equal(g.reshape(-1).view(np.uint8), e_.reshape(-1).view(np.uint8)), n
     for s_ in (sh_def, sh_eager):
         s_._pool.shutdown()
+
+
+def test_sharded_result_lands_in_one_host_array(oracle):
+    """ShardedFedAvg.result: every device copies its buckets straight to their place in one host array per
+    element format (fedavg_d2h_multi, one call per device and format) -- no host concatenation; keys with a
+    bucket outside an arena (integer side buffers, empty keys) are still reassembled per key.  Same bits."""
+    import torch
+
+    sh = _fake_sharded(3)
+    rng = np.random.default_rng(9)
+    shapes = {"a": (3, 5000), "b": (7,), "c": (), "e": (2, 4096), "z": (0,)}
+    rows = []
+    for i in range(4):
+        r = {k: rng.standard_normal(s).astype(np.float32) for k, s in shapes.items()}
+        r["d64"] = rng.standard_normal(9000)
+        r["n"] = np.arange(5000, dtype=np.int64) * i
+        rows.append(r)
+        sh.add(list(r.items()), 1.0 + i, True)
+    res = sh.result()
+    ws = [1.0, 2.0, 3.0, 4.0]
+    base32 = None
+    for k in ("a", "b", "c", "e"):
+        v = res[k]
+        assert np.shape(v) == shapes[k]
+        exp = oracle.fedavg_c([r[k].reshape(-1) for r in rows], ws, oracle.MODE_NUMPY)
+        assert np.array_equal(np.asarray(v, dtype=np.float32).reshape(-1).view(np.uint32), exp.view(np.uint32)), k
+        if k != "c":  # 0-d results are numpy scalars, as the reference's
+            owner = v.base if v.base is not None else v
+            while getattr(owner, "base", None) is not None and isinstance(owner.base, np.ndarray):
+                owner = owner.base
+            base32 = base32 if base32 is not None else owner
+            assert np.shares_memory(v, base32), k  # one host array for every fp32 key
+    exp64 = oracle.fedavg_c([r["d64"] for r in rows], ws, oracle.MODE_NUMPY)
+    assert res["d64"].dtype == np.float64 and np.array_equal(res["d64"].view(np.uint64), exp64.view(np.uint64))
+    assert res["z"].shape == (0,) and res["n"].dtype == np.float64
+    assert sum(getattr(e.ctx, "d2h_multi_calls", 0) for e in sh.engines) >= 3
+    sh._pool.shutdown()

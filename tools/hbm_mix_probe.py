@@ -1,0 +1,112 @@
+#!/usr/bin/env python3
+"""R:1 read/write mix probe (diagnostic; tools/hbm_pattern_probe.hip ``mix_run``): the chip's ceiling for the
+traffic shape of a K-client aggregation (K reads per result write; config 2 = 8 clients: 8:1), next to the
+real burst kernel on the same footprint, interleaved rounds in one process, medians.  Prints JSON lines.
+
+  python tools/hbm_mix_probe.py [--ratio 8] [--params 1.25e8] [--rounds 5]
+"""
+
+import argparse
+import ctypes
+import json
+import os
+import statistics
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+sys.path.insert(0, ROOT)
+
+
+def lib_path():
+    path = os.path.join(HERE, "build", "libhbm_pattern_probe.so")
+    src = os.path.join(HERE, "hbm_pattern_probe.hip")
+    if not os.path.exists(path) or os.path.getmtime(path) < os.path.getmtime(src):
+        os.makedirs(os.path.dirname(path), exist_ok=True)
+        subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-shared", "-fPIC", src, "-o", path],
+                       check=True)
+    return path
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--ratio", type=int, default=8)
+    ap.add_argument("--params", type=float, default=1.25e8, help="results (fp32) per pass: footprint (R+1) x 4 x this")
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--build-only", action="store_true")
+    a = ap.parse_args()
+    lp = lib_path()
+    if a.build_only:
+        return
+    from nvflare_amd import _native as N
+    from nvflare_amd.device import DeviceContext, TiledLayout
+
+    ctx = DeviceContext.get(0)
+    lib = ctypes.CDLL(lp)
+    lib.mix_run.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t,
+                            ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_double),
+                            ctypes.POINTER(ctypes.c_int)]
+    R = a.ratio
+    P = int(a.params)
+    n_tiles = (P + 4095) // 4096
+    nbytes = n_tiles * (R + 1) * 16384
+    buf = ctx.alloc(nbytes)
+    ctx.fill_synthetic_f32(buf.ptr, nbytes // 4, 1, 0)
+    # the real kernel on a slab of R clients x P params (torch mode, library defaults)
+    lay = TiledLayout(4096, R)
+    slab = ctx.alloc(lay.slab_elems(P) * 4)
+    bases = [slab.ptr + lay.slot_offset_elems(k) * 4 for k in range(R)]
+    for k, b in enumerate(bases):
+        ctx.fill_synthetic_f32(b, P, 1000, k, 0, lay.tile, lay.tile_stride)
+    end = (P + 3) // 4 * 4
+    out = ctx.alloc(end * 4)
+    ws = [float(1 + (37 * k) % 100) for k in range(R)]
+    cnt = sum(ws)
+    ctx.sync()
+    ncu = ctx.num_cus
+    cases = [("grid", 0, 0, 0, 4), ("grid", 0, 0, 0, 8), ("read", 1, 0, 0, 1), ("read", 1, 0, 0, 2),
+             ("tile", 2, 0, 0, 1), ("tile", 2, 0, 0, 2),
+             ("burst_r8_l4", 3, 8, 4, 2), ("burst_r8_l5", 3, 8, 5, 2), ("burst_r8_l0", 3, 8, 0, 2),
+             ("burst_r4_l4", 3, 4, 4, 2), ("burst_r8_l10", 3, 8, 10, 1), ("burst_r0_l8", 3, 0, 8, 1),
+             ("write", 4, 0, 0, 1), ("write", 4, 0, 0, 2), ("write_grid", 5, 0, 0, 2),
+             ("kernel", -1, 0, 0, 0)]
+    res = {c: [] for c in cases}
+    info = {}
+    for _ in range(a.rounds):
+        for c in cases:
+            name, mode, reg, lds, bpc = c
+            if mode < 0:
+                ctx.timing_begin()
+                n0 = ctx.launch_count()
+                for _ in range(a.reps):
+                    ctx.accumulate_tiled(bases, ws, lay.tile, lay.tile_stride, 0, end, out.ptr, N.FEDAVG_OP_TORCH,
+                                         N.FEDAVG_FIN_DIV, cnt)
+                ctx.sync()
+                ms = ctx.timing_end() / a.reps
+                info[c] = (4.0 * R * P + 4.0 * P, (ctx.launch_count() - n0) / a.reps)
+                res[c].append(ms)
+                continue
+            ms = ctypes.c_float(0)
+            moved = ctypes.c_double(0)
+            nl = ctypes.c_int(0)
+            rc = lib.mix_run(mode, R, reg, lds, ctypes.c_void_p(buf.ptr), nbytes, ncu * bpc, a.reps, ctypes.byref(ms),
+                             ctypes.byref(moved), ctypes.byref(nl))
+            if rc != 0:
+                raise SystemExit(f"mix probe {c} rc={rc}")
+            info[c] = (moved.value, nl.value)
+            res[c].append(ms.value)
+    for c, v in res.items():
+        name, mode, reg, lds, bpc = c
+        med = statistics.median(v)
+        moved, nl = info[c]
+        print(json.dumps({"probe": name, "ratio": R, "params": P, "blocks_per_cu": bpc, "reg_tiles": reg,
+                          "lds_tiles": lds, "launches": nl, "ms_median": round(med, 4),
+                          "ms_all": [round(x, 4) for x in v], "bytes": moved,
+                          "GBps": round(moved / (med / 1e3) / 1e9, 1), "frac_spec": round(moved / (med / 1e3) / 8e12, 4)}),
+              flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -196,7 +196,194 @@ __global__ void __launch_bounds__(256) p_chunk_lds(const f32x4* __restrict__ src
     sink[(int64_t)blockIdx.x * 256 + threadIdx.x] = ring[wave][lane % 16][lane];
 }
 
+// ---------------------------------------------------------------------------------------------------------
+// R:1 read/write MIXES (round 3): the shape of a K-client aggregation is K reads per write (config 2: 8:1).
+// The buffer is split into a read region of n_chunks chunks of R x 16 KiB and a write region of n_chunks x
+// 16 KiB; chunk c's "result" (the sum of its R segments, 16 KiB) goes to write slot c.
+//   mix 0  grid:      out[i] = sum_r in_r[i] over R separate arrays, grid-stride (a STREAM-style R-input triad)
+//   mix 1  read:      the chunk stream alone (no writes): the read ceiling of this footprint
+//   mix 2  tile:      chunk stream, each chunk's 16 KiB stored when it finishes (scattered small writes)
+//   mix 3  burst:     REG chunks' results in registers + LDS chunks' results in LDS per block, stored at the end
+//                     of a launch of blocks x (REG + LDS) chunks (the burst kernel's pattern, no arithmetic)
+//   mix 4  write:     the write region alone, 16 KiB per chunk per block (mix 5: grid-stride) -- with mix 1 the
+//                     additive bound t_read + t_write of a mix whose reads and writes share the HBM data bus
+// ---------------------------------------------------------------------------------------------------------
+template <int R>
+__global__ void __launch_bounds__(256) m_grid(const f32x4* __restrict__ src, int64_t n4, f32x4* __restrict__ dst) {
+    const int64_t stride = (int64_t)gridDim.x * 256;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += stride) {
+        f32x4 v[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) v[r] = __builtin_nontemporal_load(src + r * n4 + i);
+        f32x4 acc = v[0];
+#pragma unroll
+        for (int r = 1; r < R; ++r) acc += v[r];
+        __builtin_nontemporal_store(acc, dst + i);
+    }
+}
+
+// one chunk of R x 1024 float4: 16 loads in flight per lane, 4 float4 of result per lane
+template <int R>
+__device__ inline void m_chunk_sum(const f32x4* __restrict__ p, f32x4 (&acc)[4]) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) acc[q] = f32x4{0, 0, 0, 0};
+#pragma unroll 1
+    for (int g = 0; g < R; g += 4) {
+        f32x4 v[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) v[u] = __builtin_nontemporal_load(p + (int64_t)(g + u / 4) * 1024 + (u % 4) * 256);
+#pragma unroll
+        for (int u = 0; u < 16; ++u) acc[u % 4] += v[u];
+    }
+}
+
+template <int R, bool STORE>
+__global__ void __launch_bounds__(256) m_tile(const f32x4* __restrict__ src, int64_t n_chunks, f32x4* __restrict__ dst,
+                                              f32x4* __restrict__ sink) {
+    f32x4 tot = {0, 0, 0, 0};
+    for (int64_t c = blockIdx.x; c < n_chunks; c += gridDim.x) {
+        f32x4 acc[4];
+        m_chunk_sum<R>(src + c * R * 1024 + threadIdx.x, acc);
+        if constexpr (STORE) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) __builtin_nontemporal_store(acc[q], dst + c * 1024 + q * 256 + threadIdx.x);
+        } else {
+            tot += acc[0] + acc[1] + acc[2] + acc[3];
+        }
+    }
+    if constexpr (!STORE) sink[(int64_t)blockIdx.x * 256 + threadIdx.x] = tot;
+}
+
+template <int R, int REG, int LDS>
+__global__ void __launch_bounds__(256) m_burst(const f32x4* __restrict__ src, int64_t c0, int64_t c_end,
+                                               f32x4* __restrict__ dst) {
+    f32x4 res[REG > 0 ? REG : 1][4];
+    __shared__ f32x4 stage[LDS > 0 ? LDS * 1024 : 1];
+#pragma unroll
+    for (int m = 0; m < REG; ++m) {
+        const int64_t c = c0 + blockIdx.x + (int64_t)m * gridDim.x;
+        if (c < c_end) m_chunk_sum<R>(src + c * R * 1024 + threadIdx.x, res[m]);
+    }
+#pragma unroll 1
+    for (int m = 0; m < LDS; ++m) {
+        const int64_t c = c0 + blockIdx.x + (int64_t)(REG + m) * gridDim.x;
+        if (c < c_end) {
+            f32x4 acc[4];
+            m_chunk_sum<R>(src + c * R * 1024 + threadIdx.x, acc);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) stage[m * 1024 + q * 256 + threadIdx.x] = acc[q];  // own lanes: no barrier
+        }
+    }
+#pragma unroll 1
+    for (int m = 0; m < LDS; ++m) {
+        const int64_t c = c0 + blockIdx.x + (int64_t)(REG + m) * gridDim.x;
+        if (c < c_end)
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                __builtin_nontemporal_store(stage[m * 1024 + q * 256 + threadIdx.x], dst + c * 1024 + q * 256 + threadIdx.x);
+    }
+#pragma unroll
+    for (int m = 0; m < REG; ++m) {
+        const int64_t c = c0 + blockIdx.x + (int64_t)m * gridDim.x;
+        if (c < c_end)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) __builtin_nontemporal_store(res[m][q], dst + c * 1024 + q * 256 + threadIdx.x);
+    }
+}
+
+// write-only streams of the same write region (the other half of an additive read + write bound)
+__global__ void __launch_bounds__(256) m_write_chunks(int64_t n_chunks, f32x4* __restrict__ dst) {
+    const f32x4 v = {1.0f, 2.0f, 3.0f, (float)blockIdx.x};
+    for (int64_t c = blockIdx.x; c < n_chunks; c += gridDim.x)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) __builtin_nontemporal_store(v, dst + c * 1024 + q * 256 + threadIdx.x);
+}
+
+__global__ void __launch_bounds__(256) m_write_grid(int64_t n4, f32x4* __restrict__ dst) {
+    const f32x4 v = {1.0f, 2.0f, 3.0f, (float)blockIdx.x};
+    const int64_t stride = (int64_t)gridDim.x * 256;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += stride) __builtin_nontemporal_store(v, dst + i);
+}
+
+template <int R>
+static int mix_launch(int mode, int reg, int lds, const f32x4* src, int64_t n_chunks, f32x4* dst, f32x4* sink,
+                      int blocks, hipStream_t s, int* n_launch) {
+    *n_launch = 0;
+    if (mode == 0) {
+        hipLaunchKernelGGL(m_grid<R>, dim3(blocks), dim3(256), 0, s, src, n_chunks * 1024, dst);
+        *n_launch = 1;
+    } else if (mode == 4) {
+        hipLaunchKernelGGL(m_write_chunks, dim3(blocks), dim3(256), 0, s, n_chunks, dst);
+        *n_launch = 1;
+    } else if (mode == 5) {
+        hipLaunchKernelGGL(m_write_grid, dim3(blocks), dim3(256), 0, s, n_chunks * 1024, dst);
+        *n_launch = 1;
+    } else if (mode == 1 || mode == 2) {
+        if (mode == 1) hipLaunchKernelGGL((m_tile<R, false>), dim3(blocks), dim3(256), 0, s, src, n_chunks, dst, sink);
+        else hipLaunchKernelGGL((m_tile<R, true>), dim3(blocks), dim3(256), 0, s, src, n_chunks, dst, sink);
+        *n_launch = 1;
+    } else {
+        const int64_t per = (int64_t)blocks * (reg + lds);
+        for (int64_t c0 = 0; c0 < n_chunks; c0 += per) {
+            const int64_t ce = c0 + per < n_chunks ? c0 + per : n_chunks;
+            const int nb = (int)(ce - c0 < blocks ? ce - c0 : blocks);
+#define M_BURST(RG, LD) \
+    if (reg == RG && lds == LD) hipLaunchKernelGGL((m_burst<R, RG, LD>), dim3(nb), dim3(256), 0, s, src, c0, ce, dst)
+            M_BURST(8, 4);
+            else M_BURST(8, 5);
+            else M_BURST(8, 10);
+            else M_BURST(8, 0);
+            else M_BURST(0, 8);
+            else M_BURST(4, 4);
+            else return 4;
+#undef M_BURST
+            ++*n_launch;
+        }
+    }
+    return 0;
+}
+
 extern "C" {
+// R:1 mix over `bytes` of buf (see above); R in {4, 8, 16}; returns 0 on success, ms_out = average over reps,
+// bytes_out = bytes moved per rep (reads + writes), launches_out = kernel launches per rep
+int mix_run(int mode, int R, int reg, int lds, void* buf, size_t bytes, int blocks, int reps, float* ms_out,
+            double* bytes_out, int* launches_out) {
+    hipStream_t s;
+    if (hipStreamCreate(&s) != hipSuccess) return 1;
+    hipEvent_t a, b;
+    (void)hipEventCreate(&a);
+    (void)hipEventCreate(&b);
+    f32x4* sink = nullptr;
+    if (hipMalloc(&sink, (size_t)blocks * 256 * sizeof(f32x4)) != hipSuccess) return 2;
+    const int64_t unit = (int64_t)(R + 1) * 16384;  // one chunk's reads + its result
+    const int64_t n_chunks = (int64_t)bytes / unit;
+    const f32x4* src = (const f32x4*)buf;
+    f32x4* dst = (f32x4*)buf + n_chunks * R * 1024;
+    int rc = 0, nl = 0;
+    auto launch = [&]() {
+        if (R == 4) rc = mix_launch<4>(mode, reg, lds, src, n_chunks, dst, sink, blocks, s, &nl);
+        else if (R == 8) rc = mix_launch<8>(mode, reg, lds, src, n_chunks, dst, sink, blocks, s, &nl);
+        else if (R == 16) rc = mix_launch<16>(mode, reg, lds, src, n_chunks, dst, sink, blocks, s, &nl);
+        else rc = 5;
+    };
+    launch();
+    hipEventRecord(a, s);
+    for (int r = 0; r < reps && rc == 0; ++r) launch();
+    hipEventRecord(b, s);
+    hipEventSynchronize(b);
+    float ms = 0;
+    hipEventElapsedTime(&ms, a, b);
+    *ms_out = ms / reps;
+    *bytes_out = (double)n_chunks * (mode == 1 ? R * 16384.0 : mode >= 4 ? 16384.0 : (R + 1) * 16384.0);
+    *launches_out = nl;
+    hipFree(sink);
+    hipEventDestroy(a);
+    hipEventDestroy(b);
+    hipStreamDestroy(s);
+    if (rc != 0) return 10 + rc;
+    return hipGetLastError() == hipSuccess ? 0 : 3;
+}
+
 // returns 0 on success; ms_out = average over reps
 int pattern_run(int mode, int unroll, void* buf, size_t bytes, size_t chunk_bytes, int blocks, int reps, float* ms_out) {
     hipStream_t s;
