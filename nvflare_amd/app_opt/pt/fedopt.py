@@ -543,6 +543,10 @@ class PTFedOptModelShareableGenerator(FullModelShareableGenerator):
             if self.devices is not None:
                 from .sharded_fedopt import ShardedServerOptimizer
 
+                if isinstance(d, ShardedServerOptimizer):
+                    if d.optimizer is self.optimizer:
+                        d.export_state()  # the new image starts from the shards' moments, not stale state
+                    d.release()
                 self._dev_opt = ShardedServerOptimizer(self.model, self.optimizer, self.devices)
             else:
                 self._dev_opt = DeviceServerOptimizer(self.model, self.optimizer, hip_device_index(self.device))

@@ -19,7 +19,10 @@ Layout:
 * the original model lives on the host: its parameters are views of the latest host weights.  A parameter
   the caller modifies in place (``load_state_dict``, ``param.copy_``: its ``_version`` moves) is uploaded to
   its shards before the next step.  Per-parameter optimizer state lives in the shard optimizers
-  (``shards[b].optimizer.state``, views of each device's buffers).
+  (``shards[b].optimizer.state``, views of each device's buffers); ``export_state`` assembles it into the
+  original optimizer's ``state`` (host tensors of the parameters' shapes) whenever the original is asked for
+  its ``state_dict()`` (a pre-hook) and before the generator re-binds a new sharded image of the same
+  optimizer, so neither sees stale or empty moments.
 """
 
 from __future__ import annotations
@@ -135,6 +138,15 @@ class ShardedServerOptimizer:
         self.host_pool = HostArenaPool()
         self._pool = ThreadPoolExecutor(max_workers=len(self.devices), thread_name_prefix="nvflare-amd-fedopt-shard")
         self._pool_fin = weakref.finalize(self, self._pool.shutdown, wait=False)  # a re-bound generator drops us
+        me = weakref.ref(self)
+
+        def _export(opt, _me=me):  # optimizer.state_dict() sees the shards' current state
+            obj = _me()
+            if obj is not None and obj.optimizer is opt:
+                obj.export_state()
+
+        self._hook = optimizer.register_state_dict_pre_hook(_export) \
+            if hasattr(optimizer, "register_state_dict_pre_hook") else None
         self._lock = threading.Lock()
         model.to("cpu")  # buffers (batch-norm statistics) stay with the model; parameters are re-pointed below
         host = self.host_pool.take(self.total, pin=self.shards[0].ctx)
@@ -268,6 +280,32 @@ class ShardedServerOptimizer:
             out[k] = h.clone() if preserve_torch else h.numpy()
         return out
 
+    def export_state(self) -> None:
+        """Every parameter's optimizer state, assembled from its shards into the original optimizer's ``state``:
+        per-element tensors (exp_avg, momentum_buffer, ...) as host tensors of the parameter's shape, the shard
+        slices in bucket order; scalar entries (step, mu_product, eta, ...) from the first shard holding the
+        parameter (every shard of a parameter steps it together).  A parameter no shard has stepped keeps its
+        original state."""
+        with self._lock:
+            for shard in self.shards:
+                torch.cuda.synchronize(shard.torch_device)
+            for name, p in self.params.items():
+                holders = [b for b in range(len(self.shards)) if name in self.spans[b]]
+                sts = [self.shards[b].optimizer.state.get(self.shards[b].by_name[name].param) for b in holders]
+                if not holders or not all(sts):
+                    continue
+                out = {}
+                for key, v0 in sts[0].items():
+                    if isinstance(v0, torch.Tensor) and v0.dim() >= 1:
+                        parts = [st[key].detach().reshape(-1).cpu() for st in sts]
+                        out[key] = torch.cat(parts).reshape(p.shape) if len(parts) > 1 else parts[0].clone().reshape(p.shape)
+                    else:
+                        out[key] = v0.clone() if isinstance(v0, torch.Tensor) else v0
+                self.optimizer.state[p] = out
+
     def release(self) -> None:
+        if self._hook is not None:
+            self._hook.remove()
+            self._hook = None
         self._pool_fin.detach()
         self._pool.shutdown(wait=True)

@@ -141,16 +141,26 @@ def _backend(group) -> str:
 # all_to_all_single of 4.1 GB per peer returned with only the first half of the output written, no error
 # (tools/debug_client_shards_nccl.py, profiles/r02/client_shards/) -- so the exchange goes in chunks.
 MAX_PEER_CHUNK_BYTES = 256 << 20
+# Smallest tile range the overlapped exchange hands to the kernel: 2048 tiles (8 Mi params) keep every block of
+# a burst launch busy for several tiles; smaller pieces would be launch-ramp bound (fedavg_tiles.h)
+MIN_KERNEL_TILES = 2048
+
+
+def chunk_tiles(plan: ExchangePlan, max_peer_bytes: int = MAX_PEER_CHUNK_BYTES) -> int:
+    """Tiles of a bucket per all-to-all call: at most ``max_peer_bytes`` per peer from the rank with the most
+    clients (the same count on every rank, so every peer's chunk c is the same tile sub-range)."""
+    kmax = max(max(plan.clients), 1)
+    return max(1, max_peer_bytes // (plan.tile * 4 * kmax))
 
 
 def exchange_chunks(plan: ExchangePlan, rank: int, max_peer_bytes: int = MAX_PEER_CHUNK_BYTES):
     """The exchange as a list of all-to-all calls, each moving at most ``max_peer_bytes`` per peer:
     [(send ranges, recv ranges)] with one (element offset, length) per peer, into rank ``rank``'s slab and
     receive buffer.  A sub-range of a bucket's tiles is contiguous on both sides (the slab is tile-major,
-    and the chunk from rank s keeps its [tile][K_s][TILE] order), so no call repacks anything."""
+    and the chunk from rank s keeps its [tile][K_s][TILE] order), so no call repacks anything.  Call c
+    carries tiles [c * chunk_tiles, (c + 1) * chunk_tiles) of every bucket."""
     T, W = plan.tile, plan.world
-    kmax = max(max(plan.clients), 1)
-    ct = max(1, max_peer_bytes // (T * 4 * kmax))  # tiles per chunk
+    ct = chunk_tiles(plan, max_peer_bytes)
     span = [t1 - t0 for t0, t1 in (plan.tile_range(b) for b in range(W))]
     n_chunks = max(1, -(-max(span) // ct))
     roffs = plan.recv_offsets(rank)
@@ -198,27 +208,58 @@ def exchange(plan: ExchangePlan, rank: int, send, recv, group=None, max_peer_byt
         all_to_all([recv[o: o + n] for o, n in recvs], [send[o: o + n] for o, n in sends], group)
 
 
-def reduce_scatter(out, inp, group=None) -> None:
-    """SUM reduce-scatter of equal chunks; gloo with device tensors goes through host copies."""
+def _pieces(n: int, max_peer_bytes: int):
+    """[lo, hi) element ranges of an n-element per-peer message, each at most ``max_peer_bytes`` (fp32)."""
+    step = max(1, int(max_peer_bytes) // 4)
+    return [(lo, min(n, lo + step)) for lo in range(0, max(n, 1), step)] if n else [(0, 0)]
+
+
+def reduce_scatter(out, inp, group=None, max_peer_bytes: int = MAX_PEER_CHUNK_BYTES) -> None:
+    """SUM reduce-scatter of equal chunks (``inp`` = W rank-major chunks of ``out.numel()``), in calls of at
+    most ``max_peer_bytes`` per peer (the all-to-all's limit: RCCL was seen to truncate a 4.1 GB message
+    silently); gloo with device tensors goes through host copies."""
+    import torch
     import torch.distributed as dist
 
-    if inp.device.type == "cpu" or _backend(group) == "nccl":
-        dist.reduce_scatter_tensor(out, inp, op=dist.ReduceOp.SUM, group=group)
-        return
-    o = out.new_empty(out.shape, device="cpu")
-    dist.reduce_scatter_tensor(o, inp.cpu(), op=dist.ReduceOp.SUM, group=group)
-    out.copy_(o)
+    n = out.numel()
+    W = inp.numel() // max(n, 1) if n else 1
+    pieces = _pieces(n, max_peer_bytes)
+    for lo, hi in pieces:
+        if len(pieces) == 1:
+            o_v, i_v = out, inp
+        else:
+            o_v = out[lo:hi]
+            i_v = torch.cat([inp[b * n + lo: b * n + hi] for b in range(W)])  # rank-major piece
+        if i_v.device.type == "cpu" or _backend(group) == "nccl":
+            dist.reduce_scatter_tensor(o_v, i_v, op=dist.ReduceOp.SUM, group=group)
+            continue
+        o = o_v.new_empty(o_v.shape, device="cpu")
+        dist.reduce_scatter_tensor(o, i_v.cpu(), op=dist.ReduceOp.SUM, group=group)
+        o_v.copy_(o)
 
 
-def all_gather(out, inp, group=None) -> None:
+def all_gather(out, inp, group=None, max_peer_bytes: int = MAX_PEER_CHUNK_BYTES) -> None:
+    """All-gather of equal chunks (``out`` = W rank-major copies of ``inp``), in calls of at most
+    ``max_peer_bytes`` per peer; gloo with device tensors goes through host copies."""
+    import torch
     import torch.distributed as dist
 
-    if inp.device.type == "cpu" or _backend(group) == "nccl":
-        dist.all_gather_into_tensor(out, inp, group=group)
-        return
-    o = out.new_empty(out.shape, device="cpu")
-    dist.all_gather_into_tensor(o, inp.cpu(), group=group)
-    out.copy_(o)
+    n = inp.numel()
+    W = out.numel() // max(n, 1) if n else 1
+    pieces = _pieces(n, max_peer_bytes)
+    for lo, hi in pieces:
+        whole = len(pieces) == 1
+        i_v = inp if whole else inp[lo:hi]
+        o_v = out if whole else torch.empty(W * (hi - lo), dtype=out.dtype, device=out.device)
+        if i_v.device.type == "cpu" or _backend(group) == "nccl":
+            dist.all_gather_into_tensor(o_v, i_v, group=group)
+        else:
+            o = o_v.new_empty(o_v.shape, device="cpu")
+            dist.all_gather_into_tensor(o, i_v.cpu(), group=group)
+            o_v.copy_(o)
+        if not whole:
+            for b in range(W):
+                out[b * n + lo: b * n + hi].copy_(o_v[b * (hi - lo): (b + 1) * (hi - lo)])
 
 
 class ClientShardedFedAvg:
@@ -259,6 +300,8 @@ class ClientShardedFedAvg:
         self.device = torch.device("cuda", dev)
         self.ctx = DeviceContext.get(dev)
         self._stream = torch.cuda.Stream(self.device)  # collectives + kernels (see _torch_stream)
+        self._kstream = torch.cuda.Stream(self.device)  # kernels overlapping the chunked all-to-all
+        self.min_kernel_tiles = MIN_KERNEL_TILES
         f32 = torch.float32
         self.slab = torch.empty(max(self.plan.slab_elems(self.rank), 4), dtype=f32, device=self.device)
         self._recv = None  # allocated on the first exchange
@@ -336,11 +379,65 @@ class ClientShardedFedAvg:
         order, weights = self._checked(order, weights)
         with self._torch_stream():
             if strategy == "exchange":
-                self.exchange()
-                self._exchange_and_aggregate(order, weights)
+                self._exchange_overlapped(order, weights)
             else:
                 self._reduce(order, weights)
         return self.out[: self.plan.bucket_len(self.rank)]
+
+    def _exchange_overlapped(self, order, weights) -> None:
+        """The exchange strategy with the kernels overlapping the all-to-all: the exchange goes in tile chunks
+        (``exchange_chunks``) on the collectives' stream; as soon as the chunks received so far hold at least
+        ``min_kernel_tiles`` tiles of this rank's bucket (or the last chunk is in), the arrival-ordered kernels
+        over those tiles are launched on a second stream, fenced by an event after the chunk's all-to-all, while
+        the next chunks are in flight.  Every element still sees the same launches (the runs chained through the
+        accumulator over its tile), so the bits are those of ``exchange()`` + ``aggregate_exchanged``."""
+        import torch
+
+        p, r = self.plan, self.rank
+        if self._recv is None:
+            self._recv = torch.empty(max(p.recv_elems(r), 4), dtype=torch.float32, device=self.device)
+        comm = torch.cuda.current_stream(self.device)
+        kst = self._kstream
+        kst.wait_stream(comm)
+        prev = self.ctx.stream()
+        self.ctx.set_stream(kst.cuda_stream)
+        try:
+            t0, t1 = p.tile_range(r)
+            my_tiles = t1 - t0
+            ct = chunk_tiles(p, self.max_peer_bytes)
+            chunks = exchange_chunks(p, r, self.max_peer_bytes) if p.world > 1 else [None]
+            end = (p.bucket_len(r) + 3) // 4 * 4
+            done = 0
+            for c, ch in enumerate(chunks):
+                if ch is not None:
+                    sends, recvs = ch
+                    all_to_all([self._recv[o: o + n] for o, n in recvs], [self.slab[o: o + n] for o, n in sends],
+                               self.group)
+                arrived = my_tiles if c == len(chunks) - 1 else min(my_tiles, (c + 1) * ct)
+                if arrived > done and (arrived - done >= self.min_kernel_tiles or arrived == my_tiles):
+                    ev = torch.cuda.Event()
+                    ev.record(comm)
+                    kst.wait_event(ev)
+                    self._launch_runs(order, weights, done * p.tile, min(arrived * p.tile, end))
+                    done = arrived
+            comm.wait_stream(kst)  # the caller's fence (``_torch_stream``) covers the kernels too
+        finally:
+            self.ctx.set_stream(prev)
+
+    def _launch_runs(self, order, weights, begin: int, end: int) -> None:
+        """The arrival-ordered kernels over bucket elements [begin, end) (after the exchange delivered them)."""
+        if end <= begin:
+            return
+        p, r = self.plan, self.rank
+        base = (self._recv.data_ptr(), self.slab.data_ptr())
+        out = self.out.data_ptr()
+        count = self._count(weights)
+        runs = p.exchange_runs(r, order)
+        for i, (ts, rows, pos) in enumerate(runs):
+            last = i == len(runs) - 1
+            self.ctx.accumulate_tiled([base[own] + o * 4 for own, o in rows], [weights[q] for q in pos], TILE, ts, begin,
+                                      end, out, self.op, self.fin if last else self._fin_none, count,
+                                      acc_in_ptr=out if i else None)
 
     def aggregate_exchanged(self, order: Sequence[Tuple[int, int]], weights: Sequence[float]):
         """The kernel half of the exchange strategy, after ``exchange()`` (timed apart by the bench)."""
@@ -363,19 +460,7 @@ class ClientShardedFedAvg:
         p, r = self.plan, self.rank
         if self._recv is None:
             raise RuntimeError("exchange() has not run")
-        end = (p.bucket_len(r) + 3) // 4 * 4
-        if end == 0:
-            return
-        base = (self._recv.data_ptr(), self.slab.data_ptr())
-        out = self.out.data_ptr()
-        count = self._count(weights)
-        runs = p.exchange_runs(r, order)
-        for i, (ts, rows, pos) in enumerate(runs):
-            last = i == len(runs) - 1
-            self.ctx.accumulate_tiled([base[own] + o * 4 for own, o in rows], [weights[q] for q in pos], TILE, ts, 0,
-                                      end, out,
-                                      self.op, self.fin if last else self._fin_none, count,
-                                      acc_in_ptr=out if i else None)
+        self._launch_runs(order, weights, 0, (p.bucket_len(r) + 3) // 4 * 4)
 
     def _reduce(self, order, weights) -> None:
         import torch
@@ -401,7 +486,7 @@ class ClientShardedFedAvg:
             self._partial.zero_()
         chunk = self.out[:pad]
         # the local kernels ran on torch's stream (set above), so the collective follows them in order
-        reduce_scatter(chunk, self._partial[: pad * self.world], self.group)
+        reduce_scatter(chunk, self._partial[: pad * self.world], self.group, self.max_peer_bytes)
         end = (p.bucket_len(r) + 3) // 4 * 4
         if end:
             # finalise in place: K = 0 clients, acc_in = the reduced partial (fin only)
@@ -415,5 +500,6 @@ class ClientShardedFedAvg:
         p = self.plan
         pad = p.bucket_pad()
         full = torch.empty(pad * self.world, dtype=torch.float32, device=self.device)
-        all_gather(full, self.out[:pad], self.group)
+        with self._torch_stream():
+            all_gather(full, self.out[:pad], self.group, self.max_peer_bytes)
         return torch.cat([full[b * pad: b * pad + p.bucket_len(b)] for b in range(self.world)])

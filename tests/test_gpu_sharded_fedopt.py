@@ -118,3 +118,31 @@ def test_d2h_multi_pieces(ctx):
             exp[ho // 4:(ho + nb) // 4] = src[do // 4:(do + nb) // 4]
         assert same_bits(host[:80_000], exp)
     buf.close()
+
+
+def test_sharded_fedopt_rebind_keeps_state():
+    """A re-bind after a few Adam rounds (a parameter re-pointed, so is_bound() is false) starts the new sharded
+    image from the shards' moments (ShardedServerOptimizer.export_state), and the original optimizer's
+    state_dict() shows them: same bits as the one-device flow, every round and every state entry."""
+    def repoint(rnd, model, gen):
+        if rnd == 1:
+            p = dict(model.named_parameters())["lin1.weight"]
+            p.data = p.data.clone()  # same values, new storage: the device image must be re-bound
+        return None
+
+    runs = []
+    for devices in (None, DEVS):
+        hist, _, gen = run_fedopt_sag(True, "numpy", "adam", 4, rounds=4, model_fn=wide_model, devices=devices,
+                                      between_rounds=repoint)
+        runs.append((hist, gen))
+    _compare(runs[0][0], runs[1][0])
+    sd_ref = runs[0][1].optimizer.state_dict()["state"]
+    sd_got = runs[1][1].optimizer.state_dict()["state"]
+    assert set(sd_ref) == set(sd_got) and sd_ref
+    for i, st in sd_ref.items():
+        assert set(st) == set(sd_got[i]), i
+        for k, v in st.items():
+            a = v.detach().cpu().numpy() if isinstance(v, torch.Tensor) else np.asarray(v)
+            b = sd_got[i][k]
+            b = b.detach().cpu().numpy() if isinstance(b, torch.Tensor) else np.asarray(b)
+            assert a.shape == b.shape and same_bits(a, b), (i, k)

@@ -45,6 +45,7 @@ def main():
 
     ctx = DeviceContext.get(0)
     lib = ctypes.CDLL(lp)
+    lib.mix_set_dyn.argtypes = [ctypes.c_int]
     lib.mix_run.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t,
                             ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_double),
                             ctypes.POINTER(ctypes.c_int)]
@@ -71,12 +72,18 @@ def main():
              ("burst_r8_l4", 3, 8, 4, 2), ("burst_r8_l5", 3, 8, 5, 2), ("burst_r8_l0", 3, 8, 0, 2),
              ("burst_r4_l4", 3, 4, 4, 2), ("burst_r8_l10", 3, 8, 10, 1), ("burst_r0_l8", 3, 0, 8, 1),
              ("write", 4, 0, 0, 1), ("write", 4, 0, 0, 2), ("write_grid", 5, 0, 0, 2),
+             ("dyn_r8_l9_avg12", 6, 8, 9, 1, 12), ("dyn_r8_l9_avg15", 6, 8, 9, 1, 15),
+             ("dyn_r8_l4_avg11", 6, 8, 4, 2, 11), ("dyn_r8_l4_avg12", 6, 8, 4, 2, 12),
              ("kernel", -1, 0, 0, 0)]
+    if os.environ.get("MIX_CASES"):  # comma list of probe names to run
+        keep = set(os.environ["MIX_CASES"].split(","))
+        cases = [c for c in cases if c[0] in keep]
     res = {c: [] for c in cases}
     info = {}
     for _ in range(a.rounds):
         for c in cases:
-            name, mode, reg, lds, bpc = c
+            name, mode, reg, lds, bpc = c[:5]
+            lib.mix_set_dyn(c[5] if len(c) > 5 else 12)
             if mode < 0:
                 ctx.timing_begin()
                 n0 = ctx.launch_count()
@@ -98,7 +105,7 @@ def main():
             info[c] = (moved.value, nl.value)
             res[c].append(ms.value)
     for c, v in res.items():
-        name, mode, reg, lds, bpc = c
+        name, mode, reg, lds, bpc = c[:5]
         med = statistics.median(v)
         moved, nl = info[c]
         print(json.dumps({"probe": name, "ratio": R, "params": P, "blocks_per_cu": bpc, "reg_tiles": reg,

@@ -291,6 +291,69 @@ __global__ void __launch_bounds__(256) m_burst(const f32x4* __restrict__ src, in
     }
 }
 
+// mix 6  burst_dyn: mix 3 with the chunks of a launch handed out DYNAMICALLY (one atomic counter per launch, one
+//                     vector atomic per chunk by lane 0): a block takes chunks until the launch's are gone or it
+//                     holds REG + LDS results, so blocks that stream faster take more and the launch's blocks
+//                     finish closer together (a launch of static round-robin chunks ends with its slowest block)
+template <int R, int REG, int LDS>
+__global__ void __launch_bounds__(256) m_burst_dyn(const f32x4* __restrict__ src, int64_t c0, int64_t n,
+                                                   f32x4* __restrict__ dst, int* __restrict__ ctr) {
+    f32x4 res[REG > 0 ? REG : 1][4];
+    int64_t held[REG > 0 ? REG : 1];
+    __shared__ f32x4 stage[LDS > 0 ? LDS * 1024 : 1];
+    __shared__ int64_t lds_tile[LDS > 0 ? LDS : 1];
+    __shared__ int grab;
+    int nreg = 0, nlds = 0;
+    bool more = true;
+#pragma unroll
+    for (int m = 0; m < REG; ++m) {
+        held[m] = -1;
+        if (more) {
+            if (threadIdx.x == 0) grab = atomicAdd(ctr, 1);
+            __syncthreads();
+            const int64_t t = grab;
+            __syncthreads();
+            if (t < n) {
+                held[m] = c0 + t;
+                m_chunk_sum<R>(src + (c0 + t) * R * 1024 + threadIdx.x, res[m]);
+                nreg = m + 1;
+            } else {
+                more = false;
+            }
+        }
+    }
+#pragma unroll 1
+    for (int m = 0; m < LDS && more; ++m) {
+        if (threadIdx.x == 0) grab = atomicAdd(ctr, 1);
+        __syncthreads();
+        const int64_t t = grab;
+        __syncthreads();
+        if (t >= n) break;
+        f32x4 acc[4];
+        m_chunk_sum<R>(src + (c0 + t) * R * 1024 + threadIdx.x, acc);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) stage[m * 1024 + q * 256 + threadIdx.x] = acc[q];
+        if (threadIdx.x == 0) lds_tile[m] = c0 + t;
+        nlds = m + 1;
+    }
+    __syncthreads();
+#pragma unroll 1
+    for (int m = 0; m < nlds; ++m) {
+        const int64_t c = lds_tile[m];
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            __builtin_nontemporal_store(stage[m * 1024 + q * 256 + threadIdx.x], dst + c * 1024 + q * 256 + threadIdx.x);
+    }
+#pragma unroll
+    for (int m = 0; m < REG; ++m) {
+        if (m < nreg)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) __builtin_nontemporal_store(res[m][q], dst + held[m] * 1024 + q * 256 + threadIdx.x);
+    }
+}
+
+static int g_dyn_avg = 12;  // chunks per block per launch of mix 6 (the blocks' average; capacity REG + LDS)
+
 // write-only streams of the same write region (the other half of an additive read + write bound)
 __global__ void __launch_bounds__(256) m_write_chunks(int64_t n_chunks, f32x4* __restrict__ dst) {
     const f32x4 v = {1.0f, 2.0f, 3.0f, (float)blockIdx.x};
@@ -322,6 +385,26 @@ static int mix_launch(int mode, int reg, int lds, const f32x4* src, int64_t n_ch
         if (mode == 1) hipLaunchKernelGGL((m_tile<R, false>), dim3(blocks), dim3(256), 0, s, src, n_chunks, dst, sink);
         else hipLaunchKernelGGL((m_tile<R, true>), dim3(blocks), dim3(256), 0, s, src, n_chunks, dst, sink);
         *n_launch = 1;
+    } else if (mode == 6) {
+        const int64_t per = (int64_t)blocks * g_dyn_avg;
+        const int64_t n_l = (n_chunks + per - 1) / per;
+        int* ctr = nullptr;
+        if (hipMalloc(&ctr, n_l * sizeof(int)) != hipSuccess) return 6;
+        if (hipMemsetAsync(ctr, 0, n_l * sizeof(int), s) != hipSuccess) return 7;
+        for (int64_t l = 0; l < n_l; ++l) {
+            const int64_t c0 = l * per;
+            const int64_t n = c0 + per < n_chunks ? per : n_chunks - c0;
+            const int nb = (int)(n < blocks ? n : blocks);
+#define M_DYN(RG, LD) \
+    if (reg == RG && lds == LD) hipLaunchKernelGGL((m_burst_dyn<R, RG, LD>), dim3(nb), dim3(256), 0, s, src, c0, n, dst, ctr + l)
+            M_DYN(8, 9);
+            else M_DYN(8, 4);
+            else return 8;
+#undef M_DYN
+            ++*n_launch;
+        }
+        (void)hipStreamSynchronize(s);
+        (void)hipFree(ctr);
     } else {
         const int64_t per = (int64_t)blocks * (reg + lds);
         for (int64_t c0 = 0; c0 < n_chunks; c0 += per) {
@@ -344,6 +427,8 @@ static int mix_launch(int mode, int reg, int lds, const f32x4* src, int64_t n_ch
 }
 
 extern "C" {
+void mix_set_dyn(int avg) { g_dyn_avg = avg > 0 ? avg : 12; }
+
 // R:1 mix over `bytes` of buf (see above); R in {4, 8, 16}; returns 0 on success, ms_out = average over reps,
 // bytes_out = bytes moved per rep (reads + writes), launches_out = kernel launches per rep
 int mix_run(int mode, int R, int reg, int lds, void* buf, size_t bytes, int blocks, int reps, float* ms_out,
