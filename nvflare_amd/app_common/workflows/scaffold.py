@@ -83,12 +83,17 @@ def make_scaffold_aggregate_fn(device: Optional[int] = None, devices: Optional[l
 
 _ReferenceScaffold = None
 _reference_scaffold_fn = None
+_ReferenceBaseFedAvg = None
 if HAVE_NVFLARE:
     try:
         from nvflare.app_common.workflows.scaffold import Scaffold as _ReferenceScaffold
         from nvflare.app_common.workflows.scaffold import scaffold_aggregate_fn as _reference_scaffold_fn
     except Exception:  # the workflow package needs more of nvflare than the API types
         _ReferenceScaffold = None
+    try:
+        from nvflare.app_common.workflows.base_fedavg import BaseFedAvg as _ReferenceBaseFedAvg
+    except Exception:
+        _ReferenceBaseFedAvg = None
 
 if _ReferenceScaffold is not None:
 
@@ -111,8 +116,12 @@ if _ReferenceScaffold is not None:
             any other caller-supplied function runs as given."""
             if aggregate_fn is _reference_scaffold_fn:
                 aggregate_fn = self._device_scaffold_fn
-            elif aggregate_fn is None:
-                aggregate_fn = self._device_fedavg_fn
+            elif not aggregate_fn:
+                # the reference falls back to self.aggregate_fn (base_fedavg.py:251-252): a subclass's own override
+                # runs as given; only the reference's BaseFedAvg.aggregate_fn moves to the device
+                own = getattr(type(self), "aggregate_fn", None)
+                ref = getattr(_ReferenceBaseFedAvg, "aggregate_fn", None) if _ReferenceBaseFedAvg is not None else None
+                aggregate_fn = self._device_fedavg_fn if own is ref else self.aggregate_fn
             return super().aggregate(results, aggregate_fn=aggregate_fn)
 
 else:

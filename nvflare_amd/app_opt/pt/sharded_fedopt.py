@@ -266,15 +266,26 @@ class ShardedServerOptimizer:
 
     def to_host(self, state: Dict, preserve_torch: bool) -> Dict:
         """state_dict -> host values (fedopt.py:238-244): parameters are already views of the host weights
-        (returned as they are, like the reference's CPU model returns views of its parameters); other entries
-        are copied as the single-device path copies them."""
+        (returned without a copy, like the reference's CPU model returns views of its parameters); other entries
+        are copied as the single-device path copies them.
+
+        The device shards only learn about in-place edits of a parameter through its ``_version`` counter
+        (``_upload_modified``), so the views handed out must not let an edit slip past it: torch values are
+        ``detach()``-ed parameters (they share the parameter's version counter, so an in-place torch op on them
+        is uploaded before the next step), numpy values are READ-ONLY views (an in-place numpy write would not
+        move any counter; it raises instead of leaving the host model and the shards disagreeing)."""
         out = {}
         base = self.host.ctypes.data
         for k, v in state.items():
             lay = self.layout.get(k)
             if lay is not None and v.dtype == torch.float32 and v.data_ptr() == base + 4 * lay[0]:
+                p = self.params.get(k)
+                if preserve_torch and p is not None and p.data_ptr() == v.data_ptr():
+                    out[k] = p.detach()
+                    continue
                 h = self.host[lay[0]:lay[0] + lay[1]].reshape(tuple(v.shape))
-                out[k] = torch.from_numpy(h) if preserve_torch else h
+                h.flags.writeable = False
+                out[k] = torch.from_numpy(h.copy()) if preserve_torch else h
                 continue
             h = v.detach().cpu()
             out[k] = h.clone() if preserve_torch else h.numpy()

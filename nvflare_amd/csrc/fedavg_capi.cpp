@@ -371,8 +371,9 @@ void run_tiles(fedavg_ctx* ctx, const void* const* bases, const double* weights,
     const int64_t n_tiles = (L.e4 - 1) / L.tile4 - L.b4 / L.tile4 + 1;
     const bool burst = fedavg::tiles_use_burst(L.tile4, L.unroll, L.variant);
     const int bpc = burst ? ctx->bpc(k_rows >= fedavg::kBurstOneBlockMinK ? 1 : 2) : ctx->bpc();
-    // one block per CU: the burst kernel holds 10 tiles in LDS (all 160 KiB); public bit 6 keeps the 4-tile form
-    const bool wide = burst && bpc == 1 && !(ctx->variant & fedavg::kVariantWideLds);
+    // one block per CU: the burst kernel holds 10 tiles in LDS (all 160 KiB); public bit 6 keeps the 4-tile form,
+    // public bit 5 (register-held tiles only) keeps no LDS tiles at all
+    const bool wide = burst && bpc == 1 && !(ctx->variant & (fedavg::kVariantWideLds | fedavg::kVariantRegisterTiles));
     L.variant = (ctx->variant & ~fedavg::kVariantWideLds) | (wide ? fedavg::kVariantWideLds : 0);
     L.grid = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)ctx->num_cus * bpc, n_tiles));
     const float fv = (float)fin_scalar(fin, count);

@@ -459,7 +459,7 @@ int mix_run(int mode, int R, int reg, int lds, void* buf, size_t bytes, int bloc
     float ms = 0;
     hipEventElapsedTime(&ms, a, b);
     *ms_out = ms / reps;
-    *bytes_out = (double)n_chunks * (mode == 1 ? R * 16384.0 : mode >= 4 ? 16384.0 : (R + 1) * 16384.0);
+    *bytes_out = (double)n_chunks * (mode == 1 ? R * 16384.0 : (mode == 4 || mode == 5) ? 16384.0 : (R + 1) * 16384.0);
     *launches_out = nl;
     hipFree(sink);
     hipEventDestroy(a);
