@@ -88,6 +88,9 @@ def parse(argv=None):
                     help="HBM bytes per aggregation from a separate rocprofv3 --pmc pass (default: "
                          "profiles/pmc_traffic.json when its config matches this run)")
     ap.add_argument("--seed", type=int, default=1000)
+    ap.add_argument("--sqrt", choices=["auto", "torch_cpu", "ieee"], default="auto",
+                    help="sqrt of the fused optimizer step: the product default (auto: the sqrt this host's torch "
+                         "computes, nvflare_amd/torch_sqrt.py), torch CPU's restated vsSqrt, or the correctly rounded one")
     args = ap.parse_args(argv)
     preset = PRESETS[args.config]
     if args.global_params is not None:
@@ -197,6 +200,13 @@ def arrival_count(weights):
 ADAM_HP = dict(lr=1e-3, beta1=0.9, beta2=0.999, eps=1e-8)
 
 
+def sqrt_mode(args) -> str:
+    """The fused optimizer step's sqrt (nvflare_amd/torch_sqrt.py): the product default unless --sqrt says."""
+    from nvflare_amd import torch_sqrt
+
+    return torch_sqrt.mode() if args.sqrt == "auto" else args.sqrt
+
+
 def spot_check(args, ctx, K, P, col0, op, epilogue, bufs, n_steps, seed):
     """Sampled device outputs of this rank's bucket against the oracle computed from the host twin of the
     generator (test infrastructure): the plain aggregation's output, or for the fused Adam step the parameter and
@@ -219,14 +229,16 @@ def spot_check(args, ctx, K, P, col0, op, epilogue, bufs, n_steps, seed):
     p = orc.synth_values(seed + 7, 0, cols)
     m = np.zeros_like(p)
     v = np.zeros_like(p)
+    torch_cpu = sqrt_mode(args) == "torch_cpu"
     for s in range(1, n_steps + 1):
-        orc.epilogue_apply(d, orc.EPI_ADAM, p=p, m=m, v=v, step=float(s), **ADAM_HP)
+        orc.epilogue_apply(d, orc.EPI_ADAM, p=p, m=m, v=v, step=float(s), torch_cpu_sqrt=torch_cpu, **ADAM_HP)
     mism = 0
     for buf, host in zip(bufs, (p, m, v)):
         got = ctx.gather_f32(buf.ptr, idx.astype(np.uint64))
         mism += int(np.count_nonzero(host.view(np.uint32) != got.view(np.uint32)))
     return {"sampled": int(idx.size) * 3, "mismatches": mism,
-            "oracle": f"oracle/fedavg_oracle.c (aggregation + {n_steps} Adam steps; p, exp_avg, exp_avg_sq)"}
+            "oracle": f"oracle/fedavg_oracle.c (aggregation + {n_steps} Adam steps; p, exp_avg, exp_avg_sq; "
+                      f"{'torch CPU' if torch_cpu else 'correctly rounded'} sqrt)"}
 
 
 def cpu_baseline(args, K, P, op):
@@ -367,10 +379,13 @@ def run_workload(args, ctx, world, rank, K, P_spec, scaling, epilogue, baseline,
                 epi.param, epi.state1 = state[0].ptr, state[1].ptr
                 epi.lr, epi.momentum = 1.0, 0.9
             else:
+                from nvflare_amd import torch_sqrt
+
                 epi.param, epi.state1, epi.state2 = state[0].ptr, state[1].ptr, state[2].ptr
                 for k, v in ADAM_HP.items():
                     setattr(epi, k, v)
                 epi.momentum_decay, epi.mu_product = 4e-3, 1.0  # NAdam (mu_product held at its first-step value)
+                epi.sqrt_table = torch_sqrt.epilogue_table(ctx, sqrt_mode(args))
         ctx.sync()
         n_step = [0]
 
@@ -443,6 +458,7 @@ def summarize(args, world, res, K, scaling, epilogue, label):
                             + (" (each GPU its own bucket)" if scaling == "weak" else " (one model split in buckets)")),
             "layout": f"tiled slab, {args.tile}-element tiles x {K} slots",
             "kernel": kernel_name(K, epilogue, args.variant),
+            **({"sqrt": sqrt_mode(args)} if epilogue in ("adam", "nadam", "radam") else {}),
         },
         "pct_hbm_peak": round(100.0 * achieved / HBM_PEAK_GBS, 2),
         "roofline": {

@@ -43,7 +43,7 @@ FEDAVG_FIN_SCALE = 1
 FEDAVG_FIN_DIV = 2
 FEDAVG_FIN_RECIP = 3  # torch-ROCm div_ by a CPU scalar: multiply by the opmath reciprocal
 
-ABI_VERSION = 6  # include/nvflare_amd_fedavg.h FEDAVG_ABI_VERSION
+ABI_VERSION = 7  # include/nvflare_amd_fedavg.h FEDAVG_ABI_VERSION
 
 c_void_p = ctypes.c_void_p
 c_int = ctypes.c_int
@@ -182,6 +182,7 @@ _SIGNATURES = {
     "fedavg_set_tile": [c_void_p, c_int],
     "fedavg_fill_synthetic_f32": [c_void_p, c_void_p, c_size_t, c_size_t, c_size_t, c_u64, c_u64, c_u64],
     "fedavg_gather_f32": [c_void_p, c_void_p, c_void_p, c_size_t, c_void_p],
+    "fedavg_sqrt_f32": [c_void_p, c_void_p, c_void_p, c_size_t, c_void_p],
     "fedavg_dequantize": [c_void_p, c_void_p, c_void_p, c_size_t, c_void_p, c_size_t, c_size_t, c_size_t],
 }
 EXPORTED = ["fedavg_last_error", "fedavg_abi_version", "fedavg_struct_size", *_SIGNATURES.keys()]
@@ -235,9 +236,11 @@ class Epilogue(ctypes.Structure):
         ("eta", c_double),
         ("mu", c_double),
         ("lambd", c_double),
+        ("sqrt_table", c_void_p),  # v7: device table of torch CPU's sqrt (nvflare_amd/torch_sqrt.py) or NULL
     ]
 
 
+FEDAVG_SQRT_TABLE_ENTRIES = 65536
 FEDAVG_Q_F16 = 1
 FEDAVG_Q_BF16 = 2
 FEDAVG_Q_BLOCKWISE8 = 3

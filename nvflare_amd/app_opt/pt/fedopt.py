@@ -49,6 +49,7 @@ from ...compat import (
     make_model_learnable,
 )
 from ...deferred import DeferredAggregate, DeferredValue, FusedEntry, materialize_deferred
+from ... import torch_sqrt
 from ...device import DeviceContext, HostArenaPool
 
 _ALIGN = 64  # elements per parameter slot boundary (256 B), as in the aggregation engine
@@ -73,6 +74,9 @@ def build_component_from_args(args: dict):
     mod, _, cls = path.rpartition(".")
     return getattr(importlib.import_module(mod), cls)(**args.get("args", {}))
 
+
+# server optimizers whose torch step takes a sqrt (exp_avg_sq.sqrt(), state_sum.sqrt(), square_avg.sqrt())
+_SQRT_KINDS = (N.FEDAVG_EPI_ADAM, N.FEDAVG_EPI_ADAGRAD, N.FEDAVG_EPI_RMSPROP, N.FEDAVG_EPI_NADAM, N.FEDAVG_EPI_RADAM)
 
 class _Slot:
     __slots__ = ("name", "param", "offset", "n", "step", "has_momentum_buffer", "state_initialised", "mu_product",
@@ -108,6 +112,7 @@ class DeviceServerOptimizer:
         self.model = model
         self.optimizer = optimizer
         self.kind = self._kind(optimizer)
+        self.sqrt_mode = torch_sqrt.mode()  # "torch_cpu" | "ieee": the sqrt of the reference's step (torch_sqrt.py)
         self._bind()
 
     @staticmethod
@@ -308,6 +313,9 @@ class DeviceServerOptimizer:
             if group.get("amsgrad"):
                 e.amsgrad = 1
                 e.state3 = self._max_exp_avg_sq().data_ptr()
+        if self.kind in _SQRT_KINDS:
+            # the reference's sqrt is torch CPU's on the server (vsSqrt, not correctly rounded; torch_sqrt.py)
+            e.sqrt_table = torch_sqrt.epilogue_table(self.ctx, self.sqrt_mode)
         return e
 
     def step(self, model_diff: Dict) -> List[str]:

@@ -155,4 +155,30 @@ __device__ __forceinline__ void tile_sum(f32x4 (&acc)[CPL], const RowTableF32& t
     }
 }
 
+// torch CPU's fp32 Tensor.sqrt (the epilogues' sqrt when EpiParams.sqrt_tab != NULL, fedavg_epi.h sqrt_e): MKL VML
+// vsSqrt on AVX-512 (ATen vml.h IMPLEMENT_VML_MKL(sqrt, Sqrt), VML_HA), which is not correctly rounded but one Newton step from the VRSQRT14PS estimate (measured
+// bit-exact against torch over every mantissa of [1, 4), every subnormal and a sample of every binade:
+// tools/sqrt_probe.py; restated in oracle_sqrt_torch_cpu):
+//     y = rsqrt14(x);  s = x * y;  r = fma(-s, s, x);  sqrt = fma(r, 0.5 * y, s)
+// rsqrt14 depends on the exponent parity and the top 15 mantissa bits: tab[parity << 15 | m >> 8] = mantissa bits
+// 22..7 of the estimate for x in [1, 4) (exponent 126), a power of four giving its exact root.  Inputs below 2^-96
+// run at x * 2^64 and are scaled back by 2^-32 (no subnormal residual); 0, inf, NaN and negatives are IEEE.  The
+// table (128 KiB) stays in L2; one 2-byte gather per sqrt.
+__device__ __forceinline__ float sqrt_torch_cpu(const uint16_t* __restrict__ tab, const float x) {
+    if (!(x > 0.0f) || x == __builtin_inff()) return __builtin_sqrtf(x);
+    const bool tiny = x < 0x1p-96f;
+    const float xs = tiny ? x * 0x1p64f : x;
+    const uint32_t b = __float_as_uint(xs);
+    const int e = (int)(b >> 23) - 127;
+    const uint32_t m = b & 0x7FFFFFu;
+    const int p = e & 1;
+    const int k = (e - p) / 2;
+    const uint32_t yb = (p == 0 && m == 0) ? 0x3F800000u : (0x3F000000u | ((uint32_t)tab[(p << 15) | (m >> 8)] << 7));
+    const float y = __uint_as_float((uint32_t)((int32_t)yb - k * 8388608));
+    const float s = xs * y;
+    const float r = __builtin_fmaf(-s, s, xs);
+    const float res = __builtin_fmaf(r, 0.5f * y, s);
+    return tiny ? res * 0x1p-32f : res;
+}
+
 }  // namespace fedavg

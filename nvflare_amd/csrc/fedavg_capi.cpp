@@ -431,6 +431,7 @@ fedavg::EpiParams make_epi(const fedavg_epilogue& e) {
     E.base = e.base;
     E.amsgrad = e.kind == FEDAVG_EPI_ADAM && e.amsgrad;
     E.state3 = e.state3;
+    E.sqrt_tab = e.sqrt_table;
     if (e.kind == FEDAVG_EPI_RMSPROP) {  // rmsprop.py: square_avg.mul_(alpha).addcmul_(g, g, 1 - alpha), lerp(1 - alpha)
         E.beta2 = (float)e.alpha;
         E.one_minus_beta2 = (float)(1.0 - e.alpha);
@@ -1444,6 +1445,17 @@ int fedavg_fill_synthetic_f32(fedavg_ctx* ctx, float* dst, size_t n, size_t tile
         ctx->activate();
         HIP_CHECK(fedavg::launch_fill_synthetic_f32(dst, (int64_t)n, (int64_t)tile_elems, (int64_t)tile_stride, seed,
                                                     row, col0, stream_grid(ctx, (int64_t)n), ctx->compute()));
+    });
+}
+
+int fedavg_sqrt_f32(fedavg_ctx* ctx, const float* x, float* out, size_t n, const uint16_t* sqrt_table) {
+    return guarded([&] {
+        if (!ctx) throw Error("ctx is NULL");
+        if (n == 0) return;
+        if (!x || !out) throw Error("NULL pointer");
+        ctx->activate();
+        const int grid = (int)std::min<size_t>((size_t)ctx->num_cus * 8, (n + fedavg::kBlock - 1) / fedavg::kBlock);
+        HIP_CHECK(fedavg::launch_sqrt_f32(x, out, (int64_t)n, sqrt_table, grid, ctx->compute()));
     });
 }
 

@@ -16,7 +16,7 @@ namespace fedavg {
 // Per parameter: 4K bytes of client reads + 12 B (p, m, v) read + 12 B written for Adam, so the
 // optimizer costs one pass instead of the reference's separate aggregate / H2D / step / D2H round trip.
 // Rounding sequence pinned against torch CPU by tests/test_fedopt_oracle.py (fma for add(alpha), lerp
-// and addcmul; IEEE sqrt).  Geometry fixed at the tuned default (T = 4096, unroll 4, nontemporal).
+// and addcmul; torch CPU's sqrt or IEEE: sqrt_e).  Geometry fixed at the tuned default (T = 4096, unroll 4, nontemporal).
 // ---------------------------------------------------------------------------------------------
 __device__ __forceinline__ float lerp_torch(float s, float e, float w, float w_m1) {
     const float d = e - s;
@@ -28,6 +28,10 @@ __device__ __forceinline__ float lerp_torch(float s, float e, float w, float w_m
 struct EpiIn {
     f32x4 a, b, c, d;  // ADD_BASE: base | SGD: p, momentum buffer | ADAM: p, exp_avg, exp_avg_sq (, max_exp_avg_sq)
 };
+
+__device__ __forceinline__ float sqrt_e(const EpiParams& E, const float x) {
+    return E.sqrt_tab != nullptr ? sqrt_torch_cpu(E.sqrt_tab, x) : __builtin_sqrtf(x);
+}
 
 // torch.maximum: a NaN operand is the result
 __device__ __forceinline__ float max_torch(float a, float b) {
@@ -95,7 +99,7 @@ __device__ __forceinline__ void epilogue4(const EpiParams& E, const int64_t i, c
             float g = E.maximize ? d[c] : -d[c];
             if (E.has_weight_decay) g = __builtin_fmaf(p[c], E.weight_decay, g);  // grad.add(param, alpha=wd)
             sum[c] = __builtin_fmaf(g, g, sum[c]);                                 // state_sum.addcmul_(g, g, value=1)
-            const float std_ = __builtin_sqrtf(sum[c]) + E.eps;                    // state_sum.sqrt().add_(eps)
+            const float std_ = sqrt_e(E, sum[c]) + E.eps;                    // state_sum.sqrt().add_(eps)
             p[c] = p[c] + (E.step_size_neg * g) / std_;                            // param.addcdiv_(g, std, value=-clr)
         }
         store4<true>(p4, p);
@@ -113,9 +117,9 @@ __device__ __forceinline__ void epilogue4(const EpiParams& E, const int64_t i, c
             float avg;
             if (E.centered) {
                 ga[c] = lerp_torch(ga[c], g, E.one_minus_beta1, E.one_minus_beta1_m1);  // grad_avg.lerp_(g, 1-alpha)
-                avg = __builtin_sqrtf(__builtin_fmaf(-ga[c], ga[c], sq[c]));          // addcmul(ga, ga, -1).sqrt_()
+                avg = sqrt_e(E, __builtin_fmaf(-ga[c], ga[c], sq[c]));          // addcmul(ga, ga, -1).sqrt_()
             } else {
-                avg = __builtin_sqrtf(sq[c]);
+                avg = sqrt_e(E, sq[c]);
             }
             avg = avg + E.eps;
             if (E.has_momentum) {
@@ -193,13 +197,13 @@ __device__ __forceinline__ void epilogue4(const EpiParams& E, const int64_t i, c
             m[c] = lerp_torch(m[c], g, E.one_minus_beta1, E.one_minus_beta1_m1);
             v[c] = __builtin_fmaf(E.one_minus_beta2 * g, g, v[c] * E.beta2);
             if constexpr (EPI == FEDAVG_EPI_NADAM) {
-                const float denom = __builtin_sqrtf(v[c] / E.bias_correction2) + E.eps;  // exp_avg_sq.div(bc2).sqrt().add_(eps)
+                const float denom = sqrt_e(E, v[c] / E.bias_correction2) + E.eps;  // exp_avg_sq.div(bc2).sqrt().add_(eps)
                 pv = pv + (E.coef_grad * g) / denom;                                    // addcdiv_(grad, denom, value)
                 pv = pv + (E.coef_avg * m[c]) / denom;                                  // addcdiv_(exp_avg, denom, value)
             } else {
                 float t = (m[c] / E.bias_correction1) * E.lr;                           // exp_avg / bc1 * lr
                 if (E.rectified) {
-                    const float a = (1.0f / (__builtin_sqrtf(v[c]) + E.eps)) * E.bias_correction2_sqrt;  // bc2**0.5 / (sqrt+eps)
+                    const float a = (1.0f / (sqrt_e(E, v[c]) + E.eps)) * E.bias_correction2_sqrt;  // bc2**0.5 / (sqrt+eps)
                     t = (t * a) * E.rect;
                 }
                 pv = __builtin_fmaf(t, -1.0f, pv);                                      // param.add_(..., alpha=-1)
@@ -229,7 +233,7 @@ __device__ __forceinline__ void epilogue4(const EpiParams& E, const int64_t i, c
                 vmax[c] = max_torch(vmax[c], vv);
                 vden = vmax[c];
             }
-            const float denom = __builtin_sqrtf(vden) / E.bias_correction2_sqrt + E.eps;
+            const float denom = sqrt_e(E, vden) / E.bias_correction2_sqrt + E.eps;
             pv = pv + (E.step_size_neg * mm) / denom;
             m[c] = mm;
             v[c] = vv;

@@ -93,6 +93,7 @@ struct EpiParams {
     int rectified;                                // RAdam: rho_t > 5
     float etaminus, etaplus, ss_min, ss_max;      // Rprop
     float decay, neg_eta, mu;                     // ASGD: 1 - lambd * eta, -eta, mu (averaging when != 1)
+    const uint16_t* sqrt_tab;                     // torch CPU's sqrt (VRSQRT14 mantissa table) or NULL: IEEE
 };
 
 struct DequantLaunch {
@@ -179,5 +180,6 @@ hipError_t launch_tiles_f64(const RowTableGeneric& tab, int K, int64_t tstride_e
 hipError_t launch_fill_synthetic_f32(float* dst, int64_t n, int64_t tile, int64_t tstride, uint64_t seed, uint64_t row,
                                      uint64_t col0, int grid, hipStream_t s);
 hipError_t launch_gather_f32(const float* src, const uint64_t* idx, float* dst, int64_t m, hipStream_t s);
+hipError_t launch_sqrt_f32(const float* x, float* out, int64_t n, const uint16_t* tab, int grid, hipStream_t s);
 
 }  // namespace fedavg

@@ -127,8 +127,10 @@ void oracle_synth_fill_f32(uint64_t seed, uint64_t row, const uint64_t* cols, si
  * Rounding sequence pinned against torch 2.10 CPU (tests/test_fedopt_oracle.py):
  *   add(alpha)  fma(b, alpha, a);   lerp  |w| < .5 ? fma(w, e - s, s) : fma(w - 1, e - s, e)
  *   addcmul     fma(val * t1, t2, self);   addcdiv  self + (val * t1) / t2
- *   sqrt        IEEE (correctly rounded).  torch CPU's MKL sqrt is not: ~0.6 % of its results are 1 ulp
- *               off, so Adam params are compared within 1 ulp, m and v bit-exactly.
+ *   sqrt        IEEE (correctly rounded) when sqrt_table is NULL; with the table, torch CPU's own sqrt:
+ *               MKL VML vsSqrt on the AVX-512 path (ATen vml.h IMPLEMENT_VML_MKL(sqrt, Sqrt)), which is
+ *               one Newton step from the VRSQRT14PS estimate, restated in oracle_sqrt_torch_cpu below
+ *               (~0.5 % of its results are 1 ulp below the correctly rounded value; tools/sqrt_probe.c).
  * Scalars follow torch: python-float hyperparameters and bias corrections computed in fp64, cast to
  * fp32 where they meet a tensor.
  * ------------------------------------------------------------------------------------------------ */
@@ -152,7 +154,44 @@ typedef struct {
     double mu_product;                            /* NAdam: fp32 mu_product state before this step */
     double etaminus, etaplus, step_size_min, step_size_max; /* Rprop */
     double eta, mu, lambd;                        /* ASGD: fp32 eta / mu states before this step */
+    const uint16_t* sqrt_table;                   /* NULL: IEEE sqrt; else the VRSQRT14 mantissa table */
 } oracle_epilogue;
+
+/* torch CPU's fp32 Tensor.sqrt, restated (torch 2.10 + MKL 2024.2 on AVX-512; measured bit-exact against torch
+ * over every fp32 mantissa of [1, 4), every subnormal and 1 in 61 of every other binade -- tools/sqrt_probe.py):
+ *   y = rsqrt14(x); s = x * y; r = fma(-s, s, x); sqrt = fma(r, 0.5 * y, s)
+ * rsqrt14 (VRSQRT14PS) depends on the exponent parity and the top 15 mantissa bits only: tab[parity << 15 | m >> 8]
+ * holds mantissa bits 22..7 of its result for x in [1, 4) (exponent 126 throughout), a power of four giving its
+ * exact reciprocal root.  Inputs below 2^-96 are computed at x * 2^64 and scaled back by 2^-32 (vsSqrt keeps the
+ * Newton residual out of the subnormal range; every scale from 2^32 to 2^200 gives the same bits).  Zero, inf,
+ * NaN and negative inputs take the IEEE results. */
+float oracle_sqrt_torch_cpu(const uint16_t* tab, float x) {
+    if (!(x > 0.0f) || isinf(x)) return sqrtf(x);
+    const int tiny = x < 0x1p-96f;
+    const float xs = tiny ? x * 0x1p64f : x;
+    uint32_t b;
+    memcpy(&b, &xs, 4);
+    const int e = (int)(b >> 23) - 127;
+    const uint32_t m = b & 0x7FFFFFu;
+    const int p = e & 1;
+    const int k = (e - p) / 2;
+    const uint32_t yb = (p == 0 && m == 0) ? 0x3F800000u : (0x3F000000u | ((uint32_t)tab[(p << 15) | (m >> 8)] << 7));
+    const uint32_t yk = (uint32_t)((int32_t)yb - k * 8388608);
+    float y;
+    memcpy(&y, &yk, 4);
+    const float s = xs * y;
+    const float r = fmaf(-s, s, xs);
+    const float res = fmaf(r, 0.5f * y, s);
+    return tiny ? res * 0x1p-32f : res;
+}
+
+void oracle_sqrt_torch_cpu_n(const uint16_t* tab, const float* x, size_t n, float* out) {
+    for (size_t i = 0; i < n; ++i) out[i] = oracle_sqrt_torch_cpu(tab, x[i]);
+}
+
+static inline float sqrt_e(const oracle_epilogue* epi, float x) {
+    return epi->sqrt_table ? oracle_sqrt_torch_cpu(epi->sqrt_table, x) : sqrtf(x);
+}
 
 /* torch.maximum: a NaN operand is the result */
 static inline float max_torch(float a, float b) {
@@ -190,7 +229,7 @@ void oracle_epilogue_apply(const float* delta, size_t n, const oracle_epilogue* 
             if (epi->weight_decay != 0.0) g = fmaf(p[i], (float)epi->weight_decay, g);
             const float neg_clr = (float)(-(epi->lr / (1.0 + (epi->step - 1.0) * epi->lr_decay)));
             m[i] = fmaf(g, g, m[i]);                                  /* state_sum.addcmul_(g, g, value=1) */
-            const float std_ = sqrtf(m[i]) + (float)epi->eps;         /* state_sum.sqrt().add_(eps) */
+            const float std_ = sqrt_e(epi, m[i]) + (float)epi->eps;         /* state_sum.sqrt().add_(eps) */
             p[i] = p[i] + (neg_clr * g) / std_;                       /* param.addcdiv_(g, std, value=-clr) */
         } else if (epi->kind == ORACLE_EPI_RMSPROP) { /* torch/optim/rmsprop.py _single_tensor_rmsprop */
             /* m = square_avg, v = momentum_buffer, vmax = grad_avg */
@@ -201,9 +240,9 @@ void oracle_epilogue_apply(const float* delta, size_t n, const oracle_epilogue* 
             float avg;
             if (epi->centered) {
                 vmax[i] = lerp_torch(vmax[i], g, oma);                /* grad_avg.lerp_(g, 1 - alpha) */
-                avg = sqrtf(fmaf(-vmax[i], vmax[i], m[i]));          /* addcmul(ga, ga, value=-1).sqrt_() */
+                avg = sqrt_e(epi, fmaf(-vmax[i], vmax[i], m[i]));          /* addcmul(ga, ga, value=-1).sqrt_() */
             } else {
-                avg = sqrtf(m[i]);
+                avg = sqrt_e(epi, m[i]);
             }
             avg = avg + (float)epi->eps;
             if (epi->momentum > 0.0) {
@@ -262,7 +301,7 @@ void oracle_epilogue_apply(const float* delta, size_t n, const oracle_epilogue* 
                 const float mp = (float)epi->mu_product * (float)mu;          /* mu_product *= mu (fp32 tensor) */
                 const float c_grad = (float)((-epi->lr * (1.0 - mu)) / (1.0 - (double)mp));
                 const float c_avg = (float)((-epi->lr * mu_next) / (1.0 - (double)mp * mu_next));
-                const float denom = sqrtf(v[i] / (float)bc2) + (float)epi->eps;
+                const float denom = sqrt_e(epi, v[i] / (float)bc2) + (float)epi->eps;
                 pv = pv + (c_grad * g) / denom;
                 pv = pv + (c_avg * m[i]) / denom;
             } else { /* radam.py: rectified when rho_t > 5 */
@@ -272,7 +311,7 @@ void oracle_epilogue_apply(const float* delta, size_t n, const oracle_epilogue* 
                 if (rho_t > 5.0) {
                     const float rect = (float)pow((rho_t - 4.0) * (rho_t - 2.0) * rho_inf /
                                                   ((rho_inf - 4.0) * (rho_inf - 2.0) * rho_t), 0.5);
-                    const float a = (1.0f / (sqrtf(v[i]) + (float)epi->eps)) * (float)pow(bc2, 0.5); /* bc2**.5 / x */
+                    const float a = (1.0f / (sqrt_e(epi, v[i]) + (float)epi->eps)) * (float)pow(bc2, 0.5); /* bc2**.5 / x */
                     t = (t * a) * rect;
                 }
                 pv = pv - t;                                                   /* param.add_(t, alpha=-1) */
@@ -296,7 +335,7 @@ void oracle_epilogue_apply(const float* delta, size_t n, const oracle_epilogue* 
                 vmax[i] = max_torch(vmax[i], vv);
                 vden = vmax[i];
             }
-            const float denom = sqrtf(vden) / bc2s + (float)epi->eps;
+            const float denom = sqrt_e(epi, vden) / bc2s + (float)epi->eps;
             pv = pv + (step_size_neg * mm) / denom;
             m[i] = mm;
             v[i] = vv;

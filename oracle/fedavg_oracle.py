@@ -327,12 +327,45 @@ class _Epi(ctypes.Structure):
         ("eta", ctypes.c_double),
         ("mu", ctypes.c_double),
         ("lambd", ctypes.c_double),
+        ("sqrt_table", ctypes.c_void_p),
     ]
 
 
-def epilogue_apply(delta, kind, p=None, m=None, v=None, base=None, vmax=None, **hp):
+_SQRT_TABLE_FILE = os.path.join(os.path.dirname(_HERE), "nvflare_amd", "data", "rsqrt14_avx512.bin")
+_sqrt_table = None
+
+
+def sqrt_table() -> np.ndarray:
+    """The VRSQRT14PS estimates behind torch CPU's sqrt (captured by tools/sqrt_probe.c where the golden FedOpt
+    fixtures were generated): 2 x 2^15 uint32 results for x in [1, 2) then [2, 4), one per top-15-bit mantissa,
+    as the uint16 mantissa bits 22..7 oracle_sqrt_torch_cpu indexes (every entry has exponent 126 and its low 7
+    mantissa bits clear -- checked here)."""
+    global _sqrt_table
+    if _sqrt_table is None:
+        raw = np.fromfile(_SQRT_TABLE_FILE, dtype=np.uint32)
+        if raw.size != 65536 or np.any((raw >> 23) != 126) or np.any(raw & 0x7F):
+            raise ValueError(f"{_SQRT_TABLE_FILE}: not a VRSQRT14 table")
+        _sqrt_table = np.ascontiguousarray(((raw >> 7) & 0xFFFF).astype(np.uint16))
+    return _sqrt_table
+
+
+def sqrt_torch_cpu(x) -> np.ndarray:
+    """torch CPU's fp32 sqrt restated (oracle_sqrt_torch_cpu in fedavg_oracle.c), elementwise."""
+    lib = load()
+    fn = lib.oracle_sqrt_torch_cpu_n
+    fn.restype = None
+    fn.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]
+    tab = sqrt_table()
+    x = np.ascontiguousarray(x, dtype=np.float32)
+    out = np.empty_like(x)
+    fn(tab.ctypes.data, x.ctypes.data, x.size, out.ctypes.data)
+    return out
+
+
+def epilogue_apply(delta, kind, p=None, m=None, v=None, base=None, vmax=None, torch_cpu_sqrt=False, **hp):
     """Apply an epilogue to the aggregated update `delta` (fp32).  p/m/v (and vmax with amsgrad=1) are
-    updated IN PLACE (copies are the caller's business); returns `out` for NONE/ADD_BASE and p otherwise."""
+    updated IN PLACE (copies are the caller's business); returns `out` for NONE/ADD_BASE and p otherwise.
+    ``torch_cpu_sqrt``: torch CPU's sqrt (oracle_sqrt_torch_cpu) instead of the correctly rounded one."""
     lib = load()
     fn = lib.oracle_epilogue_apply
     fn.restype = None
@@ -342,6 +375,8 @@ def epilogue_apply(delta, kind, p=None, m=None, v=None, base=None, vmax=None, **
     e.kind = kind
     for k, val in hp.items():
         setattr(e, k, val)
+    if torch_cpu_sqrt:
+        e.sqrt_table = sqrt_table().ctypes.data
     out = np.empty_like(delta)
 
     def ptr(a):

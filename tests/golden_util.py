@@ -194,6 +194,28 @@ def fedopt_model():
     return Net()
 
 
+def fedopt_params_exact(reference_sqrt: str) -> bool:
+    """Whether a FedOpt step with a sqrt must reproduce the reference's parameters bit for bit: the device
+    epilogue runs torch CPU's restated sqrt (nvflare_amd.torch_sqrt.mode()) and the reference computed that same
+    sqrt -- ``reference_sqrt`` is "torch_cpu" for the golden fixtures (generated where torch's vsSqrt is the
+    restated one, tests/test_torch_sqrt.py), or "live" for torch running on this host (torch_sqrt.detect())."""
+    from nvflare_amd import torch_sqrt
+
+    ref = torch_sqrt.detect() if reference_sqrt == "live" else reference_sqrt
+    return ref in torch_sqrt.MODES and torch_sqrt.mode() == ref
+
+
+def assert_fedopt_param(got, ref, p0, lr, steps, reference_sqrt, msg=""):
+    """Bit-exact when fedopt_params_exact(reference_sqrt), else within adam_param_tolerance (a device sqrt that is
+    not the reference's: e.g. NVFLARE_AMD_TORCH_SQRT=ieee, or a host whose torch sqrt matches neither)."""
+    if fedopt_params_exact(reference_sqrt):
+        assert same_bits(got, ref), (msg, int(np.count_nonzero(np.asarray(got).view(np.uint32) != np.asarray(ref).view(np.uint32))))
+        return
+    tol = adam_param_tolerance(p0, ref, lr, max(steps, 1))
+    d = np.abs(np.asarray(got, np.float64) - np.asarray(ref, np.float64))
+    assert np.all(d <= tol), (msg, float((d / tol).max()))
+
+
 def adam_param_tolerance(p0, p_ref, lr, steps):
     """|p - p_torch| bound for Adam params: torch CPU's MKL sqrt is not correctly rounded (see
     tests/test_fedopt_oracle.py); its error passes through the two divisions into the update and the

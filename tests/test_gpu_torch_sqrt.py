@@ -1,0 +1,153 @@
+"""The device epilogues' torch-CPU sqrt (fedavg_arith.h sqrt_torch_cpu; nvflare_amd/torch_sqrt.py) on the GPU.
+
+* elementwise (fedavg_sqrt_f32), against the oracle's restatement (oracle_sqrt_torch_cpu, itself pinned against
+  torch CPU by tests/test_torch_sqrt.py) over every mantissa of [1, 4), every subnormal and 1 in 61 of every
+  other binade (tools/sqrt_probe.py's set, 59.8 M values) -- and against this host's torch.sqrt when
+  torch_sqrt.detect() finds the restated vsSqrt here;
+* inside every epilogue that takes a sqrt (Adam, AdamW + amsgrad, Adagrad, RMSprop centered + momentum, NAdam,
+  RAdam), kernel against oracle with the same sqrt, several rounds, bit-exact;
+* the table-driven and the correctly rounded sqrt really differ (the mode switch reaches the kernel)."""
+
+import os
+import sys
+
+import numpy as np
+import pytest
+
+from golden_util import same_bits
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    from nvflare_amd.device import DeviceContext
+
+    return DeviceContext.get(0)
+
+
+def _probe_set():
+    sys.path.insert(0, os.path.join(os.path.dirname(HERE), "tools"))
+    import sqrt_probe
+
+    return sqrt_probe.probe_set().view(np.float32)
+
+
+def _device_sqrt(ctx, x, table):
+    buf = ctx.alloc(x.nbytes)
+    out = ctx.alloc(x.nbytes)
+    ctx.h2d_ptr(buf.ptr, x.ctypes.data, x.nbytes)
+    ctx.sqrt_f32(buf.ptr, out.ptr, x.size, table)
+    got = np.empty_like(x)
+    ctx.d2h(got, out.ptr)
+    buf.close()
+    out.close()
+    return got
+
+
+def _same(a, b):
+    return np.count_nonzero(~((a.view(np.uint32) == b.view(np.uint32)) | (np.isnan(a) & np.isnan(b))))
+
+
+def test_device_sqrt_matches_restatement_everywhere(ctx, oracle):
+    import torch
+
+    from nvflare_amd import torch_sqrt
+
+    x = _probe_set()
+    got = _device_sqrt(ctx, x, torch_sqrt.device_table(ctx))
+    exp = oracle.sqrt_torch_cpu(x)
+    assert _same(got, exp) == 0
+    ieee = _device_sqrt(ctx, x, None)
+    with np.errstate(invalid="ignore"):
+        assert _same(ieee, np.sqrt(x)) == 0
+    assert _same(got, ieee) > 300_000  # the two sqrt modes are different functions
+    if torch_sqrt.detect() == "torch_cpu":  # this host's torch computes the restated vsSqrt: compare with it too
+        with np.errstate(invalid="ignore"):
+            assert _same(got, torch.from_numpy(x.copy()).sqrt().numpy()) == 0
+
+
+class _Dev:
+    def __init__(self, ctx, rows, n):
+        from nvflare_amd.device import TiledLayout
+
+        self.ctx, self.n = ctx, n
+        self.lay = TiledLayout(4096, len(rows))
+        self.slab = ctx.alloc(self.lay.slab_elems(n) * 4)
+        self.bases = [self.slab.ptr + self.lay.slot_offset_elems(k) * 4 for k in range(len(rows))]
+        for b, r in zip(self.bases, rows):
+            ctx.h2d_tiled(b, 4096 * 4, self.lay.tile_stride * 4, 0, r.ctypes.data, r.nbytes)
+        self.n4 = (n + 3) // 4 * 4
+        self.bufs = {}
+
+    def buf(self, name, host):
+        if name not in self.bufs:
+            self.bufs[name] = self.ctx.alloc(self.n4 * 4 + 16)
+        self.ctx.h2d_ptr(self.bufs[name].ptr, host.ctypes.data, host.nbytes)
+        return self.bufs[name].ptr
+
+    def get(self, name):
+        out = np.empty(self.n, np.float32)
+        self.ctx.d2h(out, self.bufs[name].ptr)
+        return out
+
+    def close(self):
+        self.slab.close()
+        for b in self.bufs.values():
+            b.close()
+
+
+KINDS = [
+    ("adam", dict(lr=1e-3, beta1=0.9, beta2=0.999, eps=1e-8)),
+    ("adamw_amsgrad", dict(lr=1e-3, beta1=0.5, beta2=0.9, eps=1e-8, weight_decay=1e-2, decoupled_weight_decay=1, amsgrad=1)),
+    ("adagrad", dict(lr=1e-2, lr_decay=0.05, eps=1e-10, weight_decay=1e-3)),
+    ("rmsprop", dict(lr=1e-3, alpha=0.99, eps=1e-8, momentum=0.5, centered=1)),
+    ("nadam", dict(lr=2e-3, beta1=0.9, beta2=0.999, eps=1e-8, momentum_decay=4e-3)),
+    ("radam", dict(lr=1e-3, beta1=0.9, beta2=0.999, eps=1e-8)),
+]
+
+
+@pytest.mark.parametrize("K", [5, 70])
+@pytest.mark.parametrize("name,hp", KINDS, ids=[k for k, _ in KINDS])
+def test_epilogues_with_torch_cpu_sqrt(ctx, oracle, name, hp, K):
+    from nvflare_amd import _native as N
+    from nvflare_amd import torch_sqrt
+
+    kind = {"adam": oracle.EPI_ADAM, "adamw_amsgrad": oracle.EPI_ADAM, "adagrad": oracle.EPI_ADAGRAD,
+            "rmsprop": oracle.EPI_RMSPROP, "nadam": oracle.EPI_NADAM, "radam": oracle.EPI_RADAM}[name]
+    rng = np.random.default_rng(31 + K)
+    n = 3 * 4096 + 77
+    p = rng.standard_normal(n).astype(np.float32)
+    m, v, x3 = (np.zeros(n, np.float32) for _ in range(3))
+    dev_p = dev_m = dev_v = dev_3 = None
+    table = torch_sqrt.device_table(ctx)
+    ws = [float(1 + (37 * k) % 100) for k in range(K)]
+    count = None
+    for w in ws:
+        count = w if count is None else count + w
+    mp = 1.0
+    for step in range(1, 9):  # RAdam crosses into its rectified branch
+        rows = [(rng.standard_normal(n) * 0.01 * (1.0 if step % 3 else 0.05)).astype(np.float32) for _ in range(K)]
+        d = oracle.fedavg_c(rows, ws, oracle.MODE_TORCH)
+        dev = _Dev(ctx, rows, n)
+        if dev_p is None:
+            dev_p, dev_m, dev_v, dev_3 = p.copy(), m.copy(), v.copy(), x3.copy()
+        e = N.Epilogue()
+        e.kind = kind
+        for k_, val in hp.items():
+            setattr(e, k_, val)
+        e.step, e.mu_product, e.sqrt_table = float(step), mp, table
+        e.param, e.state1 = dev.buf("p", dev_p), dev.buf("m", dev_m)
+        e.state2, e.state3 = dev.buf("v", dev_v), dev.buf("x3", dev_3)
+        ctx.accumulate_tiled_epi(dev.bases, ws, 4096, dev.lay.tile_stride, 0, dev.n4, None, N.FEDAVG_OP_TORCH,
+                                 N.FEDAVG_FIN_DIV, count, e)
+        dev_p, dev_m, dev_v, dev_3 = dev.get("p"), dev.get("m"), dev.get("v"), dev.get("x3")
+        dev.close()
+        oracle.epilogue_apply(d, kind, p=p, m=m, v=v, vmax=x3, step=float(step), mu_product=mp, torch_cpu_sqrt=True, **hp)
+        for nm, a, b in (("p", dev_p, p), ("m", dev_m, m), ("v", dev_v, v), ("x3", dev_3, x3)):
+            assert same_bits(a, b), (name, step, nm, int(np.count_nonzero(a.view(np.uint32) != b.view(np.uint32))))
+        if kind == oracle.EPI_NADAM:
+            mu = hp["beta1"] * (1.0 - 0.5 * (0.96 ** (step * hp["momentum_decay"])))
+            mp = float(np.float32(np.float32(mp) * np.float32(mu)))
