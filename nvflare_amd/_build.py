@@ -27,8 +27,11 @@ ARCH = "gfx950"
 
 # -ffp-contract=off: the numpy-mode multiply and add must round separately (bit parity with the
 # reference); the torch mode uses explicit fma builtins.  No fast-math: IEEE division, denormals kept.
+# -pragma-unroll-threshold: the burst epilogue's `#pragma unroll` over its register-held tiles must unroll fully
+# (tile m's results live in dd[m]); at LLVM's default threshold the largest epilogue (RMSprop with torch CPU's
+# restated sqrt) stayed rolled and dd went to 528 bytes of scratch per lane.
 FLAGS = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-fast-math", f"--offload-arch={ARCH}",
-         "-Wall", "-Wno-unused-command-line-argument"]
+         "-mllvm", "-pragma-unroll-threshold=200000", "-Wall", "-Wno-unused-command-line-argument"]
 
 
 def _inputs():

@@ -29,8 +29,10 @@ struct EpiIn {
     f32x4 a, b, c, d;  // ADD_BASE: base | SGD: p, momentum buffer | ADAM: p, exp_avg, exp_avg_sq (, max_exp_avg_sq)
 };
 
+template <bool TSQ>
 __device__ __forceinline__ float sqrt_e(const EpiParams& E, const float x) {
-    return E.sqrt_tab != nullptr ? sqrt_torch_cpu(E.sqrt_tab, x) : __builtin_sqrtf(x);
+    if constexpr (TSQ) return sqrt_torch_cpu(E.sqrt_tab, x);
+    return __builtin_sqrtf(x);
 }
 
 // torch.maximum: a NaN operand is the result
@@ -42,21 +44,22 @@ __device__ __forceinline__ float max_torch(float a, float b) {
 
 template <int EPI>
 __device__ __forceinline__ EpiIn epi_load(const EpiParams& E, const int64_t i) {
+    constexpr int KIND = EPI & 0xFF;
     EpiIn in;
-    if constexpr (EPI == FEDAVG_EPI_ADD_BASE) {
+    if constexpr (KIND == FEDAVG_EPI_ADD_BASE) {
         in.a = load4<true>(reinterpret_cast<const f32x4*>(E.base) + i);
-    } else if constexpr (EPI == FEDAVG_EPI_SGD) {
+    } else if constexpr (KIND == FEDAVG_EPI_SGD) {
         in.a = load4<true>(reinterpret_cast<const f32x4*>(E.param) + i);
         if (E.has_momentum && !E.first_step) in.b = load4<true>(reinterpret_cast<const f32x4*>(E.state1) + i);
-    } else if constexpr (EPI == FEDAVG_EPI_ADAGRAD || EPI == FEDAVG_EPI_ASGD) {
+    } else if constexpr (KIND == FEDAVG_EPI_ADAGRAD || KIND == FEDAVG_EPI_ASGD) {
         in.a = load4<true>(reinterpret_cast<const f32x4*>(E.param) + i);
         in.b = load4<true>(reinterpret_cast<const f32x4*>(E.state1) + i);
-    } else if constexpr (EPI == FEDAVG_EPI_RMSPROP) {
+    } else if constexpr (KIND == FEDAVG_EPI_RMSPROP) {
         in.a = load4<true>(reinterpret_cast<const f32x4*>(E.param) + i);
         in.b = load4<true>(reinterpret_cast<const f32x4*>(E.state1) + i);
         if (E.has_momentum) in.c = load4<true>(reinterpret_cast<const f32x4*>(E.state2) + i);
         if (E.centered) in.d = load4<true>(reinterpret_cast<const f32x4*>(E.state3) + i);
-    } else if constexpr (EPI == FEDAVG_EPI_ADAMAX || EPI == FEDAVG_EPI_RPROP) {
+    } else if constexpr (KIND == FEDAVG_EPI_ADAMAX || KIND == FEDAVG_EPI_RPROP) {
         in.a = load4<true>(reinterpret_cast<const f32x4*>(E.param) + i);
         in.b = load4<true>(reinterpret_cast<const f32x4*>(E.state1) + i);
         in.c = load4<true>(reinterpret_cast<const f32x4*>(E.state2) + i);
@@ -72,10 +75,12 @@ __device__ __forceinline__ EpiIn epi_load(const EpiParams& E, const int64_t i) {
 template <int EPI>
 __device__ __forceinline__ void epilogue4(const EpiParams& E, const int64_t i, const f32x4 d, const EpiIn& in,
                                           f32x4* out) {
+    constexpr int KIND = EPI & 0xFF;
+    constexpr bool TSQ = (EPI & kEpiTorchSqrt) != 0;
     f32x4* p4 = reinterpret_cast<f32x4*>(E.param) + i;
-    if constexpr (EPI == FEDAVG_EPI_ADD_BASE) {
+    if constexpr (KIND == FEDAVG_EPI_ADD_BASE) {
         store4<true>(out + i, in.a + d);
-    } else if constexpr (EPI == FEDAVG_EPI_SGD) {
+    } else if constexpr (KIND == FEDAVG_EPI_SGD) {
         f32x4 p = in.a;
         f32x4 buf = in.b;
 #pragma unroll
@@ -91,7 +96,7 @@ __device__ __forceinline__ void epilogue4(const EpiParams& E, const int64_t i, c
         }
         store4<true>(p4, p);
         if (E.has_momentum) store4<true>(reinterpret_cast<f32x4*>(E.state1) + i, buf);
-    } else if constexpr (EPI == FEDAVG_EPI_ADAGRAD) {
+    } else if constexpr (KIND == FEDAVG_EPI_ADAGRAD) {
         f32x4 p = in.a;
         f32x4 sum = in.b;
 #pragma unroll
@@ -99,12 +104,12 @@ __device__ __forceinline__ void epilogue4(const EpiParams& E, const int64_t i, c
             float g = E.maximize ? d[c] : -d[c];
             if (E.has_weight_decay) g = __builtin_fmaf(p[c], E.weight_decay, g);  // grad.add(param, alpha=wd)
             sum[c] = __builtin_fmaf(g, g, sum[c]);                                 // state_sum.addcmul_(g, g, value=1)
-            const float std_ = sqrt_e(E, sum[c]) + E.eps;                    // state_sum.sqrt().add_(eps)
+            const float std_ = sqrt_e<TSQ>(E, sum[c]) + E.eps;                    // state_sum.sqrt().add_(eps)
             p[c] = p[c] + (E.step_size_neg * g) / std_;                            // param.addcdiv_(g, std, value=-clr)
         }
         store4<true>(p4, p);
         store4<true>(reinterpret_cast<f32x4*>(E.state1) + i, sum);
-    } else if constexpr (EPI == FEDAVG_EPI_RMSPROP) {
+    } else if constexpr (KIND == FEDAVG_EPI_RMSPROP) {
         f32x4 p = in.a;
         f32x4 sq = in.b;
         f32x4 buf = in.c;
@@ -117,9 +122,9 @@ __device__ __forceinline__ void epilogue4(const EpiParams& E, const int64_t i, c
             float avg;
             if (E.centered) {
                 ga[c] = lerp_torch(ga[c], g, E.one_minus_beta1, E.one_minus_beta1_m1);  // grad_avg.lerp_(g, 1-alpha)
-                avg = sqrt_e(E, __builtin_fmaf(-ga[c], ga[c], sq[c]));          // addcmul(ga, ga, -1).sqrt_()
+                avg = sqrt_e<TSQ>(E, __builtin_fmaf(-ga[c], ga[c], sq[c]));          // addcmul(ga, ga, -1).sqrt_()
             } else {
-                avg = sqrt_e(E, sq[c]);
+                avg = sqrt_e<TSQ>(E, sq[c]);
             }
             avg = avg + E.eps;
             if (E.has_momentum) {
@@ -133,7 +138,7 @@ __device__ __forceinline__ void epilogue4(const EpiParams& E, const int64_t i, c
         store4<true>(reinterpret_cast<f32x4*>(E.state1) + i, sq);
         if (E.has_momentum) store4<true>(reinterpret_cast<f32x4*>(E.state2) + i, buf);
         if (E.centered) store4<true>(reinterpret_cast<f32x4*>(E.state3) + i, ga);
-    } else if constexpr (EPI == FEDAVG_EPI_ADAMAX) {
+    } else if constexpr (KIND == FEDAVG_EPI_ADAMAX) {
         f32x4 p = in.a;
         f32x4 m = in.b;
         f32x4 u = in.c;
@@ -148,7 +153,7 @@ __device__ __forceinline__ void epilogue4(const EpiParams& E, const int64_t i, c
         store4<true>(p4, p);
         store4<true>(reinterpret_cast<f32x4*>(E.state1) + i, m);
         store4<true>(reinterpret_cast<f32x4*>(E.state2) + i, u);
-    } else if constexpr (EPI == FEDAVG_EPI_ASGD) {
+    } else if constexpr (KIND == FEDAVG_EPI_ASGD) {
         f32x4 p = in.a;
         f32x4 ax = in.b;
 #pragma unroll
@@ -162,7 +167,7 @@ __device__ __forceinline__ void epilogue4(const EpiParams& E, const int64_t i, c
         }
         store4<true>(p4, p);
         store4<true>(reinterpret_cast<f32x4*>(E.state1) + i, ax);
-    } else if constexpr (EPI == FEDAVG_EPI_RPROP) {
+    } else if constexpr (KIND == FEDAVG_EPI_RPROP) {
         f32x4 p = in.a;
         f32x4 prev = in.b;
         f32x4 ss = in.c;
@@ -182,7 +187,7 @@ __device__ __forceinline__ void epilogue4(const EpiParams& E, const int64_t i, c
         store4<true>(p4, p);
         store4<true>(reinterpret_cast<f32x4*>(E.state1) + i, prev);
         store4<true>(reinterpret_cast<f32x4*>(E.state2) + i, ss);
-    } else if constexpr (EPI == FEDAVG_EPI_NADAM || EPI == FEDAVG_EPI_RADAM) {
+    } else if constexpr (KIND == FEDAVG_EPI_NADAM || KIND == FEDAVG_EPI_RADAM) {
         f32x4 p = in.a;
         f32x4 m = in.b;
         f32x4 v = in.c;
@@ -196,14 +201,14 @@ __device__ __forceinline__ void epilogue4(const EpiParams& E, const int64_t i, c
             }
             m[c] = lerp_torch(m[c], g, E.one_minus_beta1, E.one_minus_beta1_m1);
             v[c] = __builtin_fmaf(E.one_minus_beta2 * g, g, v[c] * E.beta2);
-            if constexpr (EPI == FEDAVG_EPI_NADAM) {
-                const float denom = sqrt_e(E, v[c] / E.bias_correction2) + E.eps;  // exp_avg_sq.div(bc2).sqrt().add_(eps)
+            if constexpr (KIND == FEDAVG_EPI_NADAM) {
+                const float denom = sqrt_e<TSQ>(E, v[c] / E.bias_correction2) + E.eps;  // exp_avg_sq.div(bc2).sqrt().add_(eps)
                 pv = pv + (E.coef_grad * g) / denom;                                    // addcdiv_(grad, denom, value)
                 pv = pv + (E.coef_avg * m[c]) / denom;                                  // addcdiv_(exp_avg, denom, value)
             } else {
                 float t = (m[c] / E.bias_correction1) * E.lr;                           // exp_avg / bc1 * lr
                 if (E.rectified) {
-                    const float a = (1.0f / (sqrt_e(E, v[c]) + E.eps)) * E.bias_correction2_sqrt;  // bc2**0.5 / (sqrt+eps)
+                    const float a = (1.0f / (sqrt_e<TSQ>(E, v[c]) + E.eps)) * E.bias_correction2_sqrt;  // bc2**0.5 / (sqrt+eps)
                     t = (t * a) * E.rect;
                 }
                 pv = __builtin_fmaf(t, -1.0f, pv);                                      // param.add_(..., alpha=-1)
@@ -233,7 +238,7 @@ __device__ __forceinline__ void epilogue4(const EpiParams& E, const int64_t i, c
                 vmax[c] = max_torch(vmax[c], vv);
                 vden = vmax[c];
             }
-            const float denom = sqrt_e(E, vden) / E.bias_correction2_sqrt + E.eps;
+            const float denom = sqrt_e<TSQ>(E, vden) / E.bias_correction2_sqrt + E.eps;
             pv = pv + (E.step_size_neg * mm) / denom;
             m[c] = mm;
             v[c] = vv;
@@ -294,7 +299,7 @@ fedavg_tiles_epi_burst_f32x4(const RowTableF32 tab, const int K, const int64_t t
     // exactly one tile's loads; only in-range columns of real tiles are computed and stored.
     const int64_t t_base = t0 + blockIdx.x;
     const int64_t t_cap = t_end - 1;
-    auto operands = [&](EpiIn (&in)[CPL], const int m) {
+    auto operands = [&](EpiIn (&in)[CPL], const int m) __attribute__((always_inline)) {
         const int64_t t = t_base + (int64_t)m * gridDim.x;
         const int64_t tc = t < t_cap ? t : t_cap;
 #pragma unroll
@@ -304,23 +309,40 @@ fedavg_tiles_epi_burst_f32x4(const RowTableF32 tab, const int K, const int64_t t
             in[c] = epi_load<EPI>(E, i);
         }
     };
-    EpiIn pre[2][CPL];
-    operands(pre[0], 0);
-#pragma unroll
-    for (int m = 0; m < NT; ++m) {
-        if (m + 1 < NT) operands(pre[(m + 1) & 1], m + 1);
-        const int64_t t = t_base + (int64_t)m * gridDim.x;
+    // cur / nxt with static indices only (a pre[m & 1] buffer in the rolled LDS-tile loop, or in an epilogue too
+    // large for the compiler to unroll fully, went to scratch memory: 528 bytes per lane for Adam with the restated
+    // torch sqrt)
+    EpiIn cur[CPL], nxt[CPL];
+    operands(cur, 0);
+    auto tile_epilogue = [&](const int m, const int64_t t, auto&& d_of) __attribute__((always_inline)) {
         if (t < t_end) {
 #pragma unroll
             for (int c = 0; c < CPL; ++c) {
                 const int64_t i = t * T4 + threadIdx.x + c * kBlock;
                 if (i >= b4 && i < e4) {
-                    const f32x4 d = m < TPB ? dd[m < TPB ? m : 0][c] : staged[((m - TPB) * CPL + c) * kBlock + threadIdx.x];
-                    if (out != nullptr && EPI != FEDAVG_EPI_ADD_BASE) store4<true>(out + i, d);
-                    epilogue4<EPI>(E, i, d, pre[m & 1][c], out);
+                    const f32x4 d = d_of(c);
+                    if (out != nullptr && (EPI & 0xFF) != FEDAVG_EPI_ADD_BASE) store4<true>(out + i, d);
+                    epilogue4<EPI>(E, i, d, cur[c], out);
                 }
             }
         }
+    };
+#pragma unroll
+    for (int m = 0; m < TPB; ++m) {
+        if (m + 1 < NT) operands(nxt, m + 1);
+        tile_epilogue(m, t_base + (int64_t)m * gridDim.x, [&](int c) __attribute__((always_inline)) { return dd[m][c]; });
+#pragma unroll
+        for (int c = 0; c < CPL; ++c) cur[c] = nxt[c];
+    }
+#pragma unroll 1
+    for (int m = TPB; m < NT; ++m) {
+        if (m + 1 < NT) operands(nxt, m + 1);
+        tile_epilogue(m, t_base + (int64_t)m * gridDim.x,
+                      [&](int c) __attribute__((always_inline)) {
+                          return staged[((m - TPB) * CPL + c) * kBlock + threadIdx.x];
+                      });
+#pragma unroll
+        for (int c = 0; c < CPL; ++c) cur[c] = nxt[c];
     }
 }
 
@@ -416,7 +438,7 @@ __global__ void __launch_bounds__(kBlock) fedavg_tiles_epi_f32x4(const RowTableF
             const int64_t i = col + c * kBlock;
             if (i >= b4 && i < e4) {
                 const f32x4 d = fin4<FIN>(acc[c], fin_val);
-                if (out != nullptr && EPI != FEDAVG_EPI_ADD_BASE) store4<true>(out + i, d);
+                if (out != nullptr && (EPI & 0xFF) != FEDAVG_EPI_ADD_BASE) store4<true>(out + i, d);
                 epilogue4<EPI>(E, i, d, pre[c], out);
             }
         }
@@ -464,17 +486,22 @@ inline hipError_t launch_epi_a(const TileLaunch& L, const EpiParams& E, hipStrea
         case FEDAVG_EPI_SGD:
             return launch_epi_k<OP, FIN, ACC_IN, FEDAVG_EPI_SGD>(L, E, s, nl);
         case FEDAVG_EPI_ADAM:
-            return launch_epi_k<OP, FIN, ACC_IN, FEDAVG_EPI_ADAM>(L, E, s, nl);
+            return E.sqrt_tab ? launch_epi_k<OP, FIN, ACC_IN, FEDAVG_EPI_ADAM | kEpiTorchSqrt>(L, E, s, nl)
+                              : launch_epi_k<OP, FIN, ACC_IN, FEDAVG_EPI_ADAM>(L, E, s, nl);
         case FEDAVG_EPI_ADAGRAD:
-            return launch_epi_k<OP, FIN, ACC_IN, FEDAVG_EPI_ADAGRAD>(L, E, s, nl);
+            return E.sqrt_tab ? launch_epi_k<OP, FIN, ACC_IN, FEDAVG_EPI_ADAGRAD | kEpiTorchSqrt>(L, E, s, nl)
+                              : launch_epi_k<OP, FIN, ACC_IN, FEDAVG_EPI_ADAGRAD>(L, E, s, nl);
         case FEDAVG_EPI_RMSPROP:
-            return launch_epi_k<OP, FIN, ACC_IN, FEDAVG_EPI_RMSPROP>(L, E, s, nl);
+            return E.sqrt_tab ? launch_epi_k<OP, FIN, ACC_IN, FEDAVG_EPI_RMSPROP | kEpiTorchSqrt>(L, E, s, nl)
+                              : launch_epi_k<OP, FIN, ACC_IN, FEDAVG_EPI_RMSPROP>(L, E, s, nl);
         case FEDAVG_EPI_ADAMAX:
             return launch_epi_k<OP, FIN, ACC_IN, FEDAVG_EPI_ADAMAX>(L, E, s, nl);
         case FEDAVG_EPI_NADAM:
-            return launch_epi_k<OP, FIN, ACC_IN, FEDAVG_EPI_NADAM>(L, E, s, nl);
+            return E.sqrt_tab ? launch_epi_k<OP, FIN, ACC_IN, FEDAVG_EPI_NADAM | kEpiTorchSqrt>(L, E, s, nl)
+                              : launch_epi_k<OP, FIN, ACC_IN, FEDAVG_EPI_NADAM>(L, E, s, nl);
         case FEDAVG_EPI_RADAM:
-            return launch_epi_k<OP, FIN, ACC_IN, FEDAVG_EPI_RADAM>(L, E, s, nl);
+            return E.sqrt_tab ? launch_epi_k<OP, FIN, ACC_IN, FEDAVG_EPI_RADAM | kEpiTorchSqrt>(L, E, s, nl)
+                              : launch_epi_k<OP, FIN, ACC_IN, FEDAVG_EPI_RADAM>(L, E, s, nl);
         case FEDAVG_EPI_RPROP:
             return launch_epi_k<OP, FIN, ACC_IN, FEDAVG_EPI_RPROP>(L, E, s, nl);
         case FEDAVG_EPI_ASGD:

@@ -35,6 +35,10 @@ constexpr int kVariantWideLds = 64;       // inside TileLaunch: plain burst kern
                                            // (160 KiB, one block per CU); run_tiles sets it for one-block-per-CU grids
                                            // unless the public variant has bit 6, which keeps the 4-tile form there
                                            // (32 clients 88.4 -> 88.9 %, 64: 89.7 -> 89.9 %, profiles/r02/ab/wide_lds/)
+// epilogue template value: the optimizer kind | kEpiTorchSqrt when the step's sqrt is torch CPU's restated vsSqrt
+// (EpiParams.sqrt_tab; fedavg_arith.h sqrt_torch_cpu) -- a compile-time choice, so the correctly rounded path
+// keeps its own code (a runtime branch cost the fused Adam kernel 9 points, profiles/r03/s3/)
+constexpr int kEpiTorchSqrt = 0x100;
 constexpr int kBurstLdsTilesWide = 10;     // 10 x 16 KiB = all of a CU's LDS
 constexpr int kBurstTiles = 8;             // tiles per block per burst launch (results held in registers)
 constexpr int kBurstLdsTiles = 4;          // 4 x 16 KiB of LDS per block (2 blocks fit a CU)

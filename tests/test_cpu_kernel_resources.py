@@ -1,0 +1,38 @@
+"""Resource guard on the built library (CPU, no GPU): every gfx950 kernel of the in-tree objects keeps its data in
+registers and LDS -- no scratch (private segment) memory, LDS within a CU's 160 KiB -- read from the code
+objects' metadata (tools/kernel_resources.py).  Scratch in a streaming kernel is an HBM round trip per spilled
+value: the burst epilogue with torch CPU's restated sqrt once spilled its register-held tiles (528 bytes per lane)
+and lost 9 points of HBM bandwidth before the build raised LLVM's pragma-unroll threshold (nvflare_amd/_build.py)."""
+
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+
+import kernel_resources as kr  # noqa: E402
+
+
+@pytest.fixture(scope="module")
+def ks():
+    if not os.path.isdir(kr.OBJ) or not os.path.exists(os.path.join(kr.LLVM, "clang-offload-bundler")):
+        pytest.skip("library objects or the ROCm LLVM tools are absent")
+    res = kr.all_kernels()
+    if not res:
+        pytest.skip("no kernel metadata found")
+    return res
+
+
+def test_no_kernel_uses_scratch(ks):
+    bad = [(k["object"], k["name"], k["scratch"]) for k in ks if k["scratch"]]
+    assert not bad, bad[:10]
+
+
+def test_lds_and_registers_fit_a_cu(ks):
+    assert all(k["lds"] <= 160 * 1024 for k in ks)
+    assert all(k["vgpr"] + k["agpr"] <= 512 for k in ks)
+    names = [k["name"] for k in ks]
+    for needed in ("fedavg_tiles_burst_f32x4", "fedavg_tiles_epi_burst_f32x4", "fedavg_sqrt_f32"):
+        assert any(needed in n for n in names), needed

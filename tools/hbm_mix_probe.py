@@ -72,6 +72,8 @@ def main():
              ("burst_r8_l4", 3, 8, 4, 2), ("burst_r8_l5", 3, 8, 5, 2), ("burst_r8_l0", 3, 8, 0, 2),
              ("burst_r4_l4", 3, 4, 4, 2), ("burst_r8_l10", 3, 8, 10, 1), ("burst_r0_l8", 3, 0, 8, 1),
              ("write", 4, 0, 0, 1), ("write", 4, 0, 0, 2), ("write_grid", 5, 0, 0, 2),
+             ("write_aux0", 7, 0, 0, 1), ("write_aux2", 7, 2, 0, 1), ("write_aux16", 7, 16, 0, 1),
+             ("write_aux17", 7, 17, 0, 1), ("write_aux0", 7, 0, 0, 2),
              ("dyn_r8_l9_avg12", 6, 8, 9, 1, 12), ("dyn_r8_l9_avg15", 6, 8, 9, 1, 15),
              ("dyn_r8_l4_avg11", 6, 8, 4, 2, 11), ("dyn_r8_l4_avg12", 6, 8, 4, 2, 12),
              ("kernel", -1, 0, 0, 0)]

@@ -205,6 +205,7 @@ __global__ void __launch_bounds__(256) p_chunk_lds(const f32x4* __restrict__ src
 //   mix 2  tile:      chunk stream, each chunk's 16 KiB stored when it finishes (scattered small writes)
 //   mix 3  burst:     REG chunks' results in registers + LDS chunks' results in LDS per block, stored at the end
 //                     of a launch of blocks x (REG + LDS) chunks (the burst kernel's pattern, no arithmetic)
+//   mix 7  write_aux: mix 4 through buffer stores with cache-policy bits (reg = 0 plain, 2 nt, 16 sc1, 17 sc0 sc1)
 //   mix 4  write:     the write region alone, 16 KiB per chunk per block (mix 5: grid-stride) -- with mix 1 the
 //                     additive bound t_read + t_write of a mix whose reads and writes share the HBM data bus
 // ---------------------------------------------------------------------------------------------------------
@@ -362,6 +363,18 @@ __global__ void __launch_bounds__(256) m_write_chunks(int64_t n_chunks, f32x4* _
         for (int q = 0; q < 4; ++q) __builtin_nontemporal_store(v, dst + c * 1024 + q * 256 + threadIdx.x);
 }
 
+// mix 7: the write region through buffer stores with cache-policy bits AUX (0 plain, 2 nt, 16 sc1, 17 sc0 sc1)
+template <int AUX>
+__global__ void __launch_bounds__(256) m_write_chunks_aux(int64_t n_chunks, f32x4* __restrict__ dst) {
+    const f32x4 v = {1.0f, 2.0f, 3.0f, (float)blockIdx.x};
+    for (int64_t c = blockIdx.x; c < n_chunks; c += gridDim.x) {
+        __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(dst + c * 1024, 0, 16384, 0x00020000);
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, v), r, (q * 256 + threadIdx.x) * 16, 0, AUX);
+    }
+}
+
 __global__ void __launch_bounds__(256) m_write_grid(int64_t n4, f32x4* __restrict__ dst) {
     const f32x4 v = {1.0f, 2.0f, 3.0f, (float)blockIdx.x};
     const int64_t stride = (int64_t)gridDim.x * 256;
@@ -380,6 +393,13 @@ static int mix_launch(int mode, int reg, int lds, const f32x4* src, int64_t n_ch
         *n_launch = 1;
     } else if (mode == 5) {
         hipLaunchKernelGGL(m_write_grid, dim3(blocks), dim3(256), 0, s, n_chunks * 1024, dst);
+        *n_launch = 1;
+    } else if (mode == 7) {  // reg = cache-policy bits of the buffer stores
+        if (reg == 0) hipLaunchKernelGGL(m_write_chunks_aux<0>, dim3(blocks), dim3(256), 0, s, n_chunks, dst);
+        else if (reg == 2) hipLaunchKernelGGL(m_write_chunks_aux<2>, dim3(blocks), dim3(256), 0, s, n_chunks, dst);
+        else if (reg == 16) hipLaunchKernelGGL(m_write_chunks_aux<16>, dim3(blocks), dim3(256), 0, s, n_chunks, dst);
+        else if (reg == 17) hipLaunchKernelGGL(m_write_chunks_aux<17>, dim3(blocks), dim3(256), 0, s, n_chunks, dst);
+        else return 9;
         *n_launch = 1;
     } else if (mode == 1 || mode == 2) {
         if (mode == 1) hipLaunchKernelGGL((m_tile<R, false>), dim3(blocks), dim3(256), 0, s, src, n_chunks, dst, sink);
@@ -459,7 +479,7 @@ int mix_run(int mode, int R, int reg, int lds, void* buf, size_t bytes, int bloc
     float ms = 0;
     hipEventElapsedTime(&ms, a, b);
     *ms_out = ms / reps;
-    *bytes_out = (double)n_chunks * (mode == 1 ? R * 16384.0 : (mode == 4 || mode == 5) ? 16384.0 : (R + 1) * 16384.0);
+    *bytes_out = (double)n_chunks * (mode == 1 ? R * 16384.0 : (mode == 4 || mode == 5 || mode == 7) ? 16384.0 : (R + 1) * 16384.0);
     *launches_out = nl;
     hipFree(sink);
     hipEventDestroy(a);

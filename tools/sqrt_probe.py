@@ -77,6 +77,16 @@ def main():
         assert r.size == x.size
         res[f"torch_vs_restated_{name}_table"] = diff(t, r)
         res[f"{name}_table_restatement_vs_this_cpu_instruction"] = chk
+    # which candidate sequence reproduces this host's torch (tools/sqrt_probe2.c: rsqrt14 / rsqrtps estimates,
+    # Newton forms, small-input scaling)
+    exe2 = os.path.join(tmp, "sqrt_probe2")
+    subprocess.run(["gcc", "-O2", "-mavx512f", "-mavx2", "-mfma", "-o", exe2, os.path.join(HERE, "sqrt_probe2.c"), "-lm"],
+                   check=True)
+    xin, tin = os.path.join(tmp, "x.bin"), os.path.join(tmp, "torch.bin")
+    x.tofile(xin)
+    t.tofile(tin)
+    p2 = subprocess.run([exe2, xin, tin], check=True, capture_output=True, text=True)
+    res["candidates"] = json.loads(p2.stdout)
     with open(local_tab, "rb") as f:
         lt = f.read()
     res["local_table_sha256"] = hashlib.sha256(lt).hexdigest()
