@@ -8,11 +8,13 @@ Nothing else is stored: tests/test_gpu_fuzz_fedopt.py regenerates every input fr
 architecture, its initial weights, the optimizer and scheduler settings, the per-round
 differences and the keys each round leaves out) and replays them through the drop-in generator on the GPU.
 
-Only optimizers whose device step is bit-exact with torch CPU are drawn (SGD with momentum / dampening /
-nesterov / weight decay / maximize, Adamax, Rprop, ASGD): for Adam-family steps torch's
-MKL sqrt is not correctly rounded and the fixed golden cases (tests/golden/fedopt_cases.*) hold the bound.
+Two families of cases: ``plain`` (SGD with momentum / dampening / nesterov / weight decay / maximize, Adamax,
+Rprop, ASGD: no sqrt on the path) and ``sqrt`` (round 3: Adam, AdamW, amsgrad, NAdam, RAdam, RMSprop, Adagrad,
+whose steps take torch CPU's sqrt -- MKL vsSqrt, not correctly rounded -- which the drop-in restates,
+DESIGN.md section 5.1; replayed with NVFLARE_AMD_TORCH_SQRT=torch_cpu, the sqrt this container's torch computes).
 
-  python tests/fuzz_reference_fedopt.py --record tests/golden/fuzz_fedopt_s31.json --cases 40 --seed 31
+  python tests/fuzz_reference_fedopt.py --record tests/golden/fuzz_fedopt_s31.json --cases 60 --seed 31
+  python tests/fuzz_reference_fedopt.py --record tests/golden/fuzz_fedopt_sqrt_s41.json --cases 60 --seed 41 --family sqrt
 """
 
 import argparse
@@ -46,14 +48,54 @@ def build_model(spec):
     return model
 
 
-def gen_case(rng) -> dict:
+def sqrt_optimizer(rng) -> dict:
+    """A torch optimizer whose step takes a sqrt, with random hyperparameters (family "sqrt")."""
+    kind = int(rng.integers(0, 6))
+    lr = float(rng.choice([1e-3, 2e-3, 1e-2]))
+    if kind in (0, 1):  # Adam / AdamW
+        args = {"lr": lr, "betas": [float(rng.choice([0.9, 0.8, 0.3])), float(rng.choice([0.999, 0.99, 0.9]))],
+                "eps": float(rng.choice([1e-8, 1e-6]))}
+        if rng.random() < 0.4:
+            args["weight_decay"] = float(rng.choice([1e-3, 1e-2]))
+        if rng.random() < 0.3:
+            args["amsgrad"] = True
+        if rng.random() < 0.15:
+            args["maximize"] = True
+        return {"path": "torch.optim.AdamW" if kind == 1 else "torch.optim.Adam", "args": args}
+    if kind == 2:
+        args = {"lr": lr, "momentum_decay": float(rng.choice([4e-3, 5e-3]))}
+        if rng.random() < 0.4:
+            args["weight_decay"] = float(rng.choice([1e-3, 1e-2]))
+            args["decoupled_weight_decay"] = bool(rng.random() < 0.5)
+        return {"path": "torch.optim.NAdam", "args": args}
+    if kind == 3:
+        args = {"lr": lr}
+        if rng.random() < 0.4:
+            args["weight_decay"] = float(rng.choice([1e-3, 1e-2]))
+        return {"path": "torch.optim.RAdam", "args": args}
+    if kind == 4:
+        args = {"lr": lr, "alpha": float(rng.choice([0.99, 0.9]))}
+        if rng.random() < 0.5:
+            args["centered"] = True
+        if rng.random() < 0.5:
+            args["momentum"] = float(rng.choice([0.5, 0.9]))
+        return {"path": "torch.optim.RMSprop", "args": args}
+    args = {"lr": float(rng.choice([1e-2, 0.1])), "lr_decay": float(rng.choice([0.0, 0.05]))}
+    if rng.random() < 0.4:
+        args["weight_decay"] = 1e-3
+    return {"path": "torch.optim.Adagrad", "args": args}
+
+
+def gen_case(rng, family: str = "plain") -> dict:
     container = "torch" if rng.random() < 0.5 else "numpy"
     depth = int(rng.integers(1, 4))
     dims = [int(rng.integers(1, 200)) for _ in range(depth + 1)]
     spec = {"container": container, "dims": dims, "bias": [bool(rng.random() < 0.7) for _ in range(depth)],
             "bn": [bool(rng.random() < 0.4) for _ in range(depth)]}
-    kind = int(rng.integers(0, 4))
-    if kind == 0:
+    kind = int(rng.integers(0, 4)) if family == "plain" else -1
+    if family == "sqrt":
+        opt = sqrt_optimizer(rng)
+    elif kind == 0:
         args = {"lr": float(rng.choice([1.0, 0.5, 0.05]))}
         if rng.random() < 0.7:
             args["momentum"] = float(rng.choice([0.5, 0.9]))
@@ -130,7 +172,7 @@ def play(gen, spec, FLContext, AppConstants, make_model_learnable, DXO, DataKind
     return out
 
 
-def record(path: str, cases: int, seed: int) -> None:
+def record(path: str, cases: int, seed: int, family: str = "plain") -> None:
     from ref_suite_plugin import _install_shim
 
     _install_shim(os.environ.get("NVFLARE_REF_ROOT", "/root/reference"))
@@ -149,7 +191,7 @@ def record(path: str, cases: int, seed: int) -> None:
     rng = np.random.default_rng(seed)
     recs = []
     for case in range(cases):
-        spec = gen_case(rng)
+        spec = gen_case(rng, family)
         model = build_model(spec)
         opt_args = json.loads(json.dumps(spec["optimizer_args"]))
         gen = PTFedOptModelShareableGenerator(optimizer_args=opt_args, device="cpu")
@@ -165,6 +207,7 @@ def record(path: str, cases: int, seed: int) -> None:
         recs.append({"case": case, "optimizer": opt_args["path"], "container": spec["container"], "rounds": rounds})
     with open(path, "w") as f:
         json.dump({"generator": "tests/fuzz_reference_fedopt.py --record", "seed": seed, "cases": cases,
+                   "family": family,
                    "reference": "NVFlare app_opt/pt/fedopt.py (/root/reference), torch CPU",
                    "numpy": np.__version__, "torch": torch.__version__, "torch_threads": torch.get_num_threads(),
                    "records": recs}, f, indent=0)
@@ -176,8 +219,9 @@ def main():
     ap.add_argument("--record", required=True)
     ap.add_argument("--cases", type=int, default=40)
     ap.add_argument("--seed", type=int, default=31)
+    ap.add_argument("--family", choices=["plain", "sqrt"], default="plain")
     a = ap.parse_args()
-    record(a.record, a.cases, a.seed)
+    record(a.record, a.cases, a.seed, a.family)
 
 
 if __name__ == "__main__":

@@ -6,8 +6,10 @@ keys in order, each value's container, dtype, shape and a SHA-256 of its bits, t
 meta.  Cases draw a 1-3 layer Linear model with optional biases and BatchNorm layers (fp32 running stats and
 an int64 ``num_batches_tracked`` take the ``base + diff`` branch), numpy or torch containers, keys missing
 from later rounds, SGD (momentum, dampening, nesterov, weight decay, maximize), Adamax, Rprop and ASGD, with or
-without a StepLR schedule.  The drop-in generator steps every parameter with the HIP kernels on cuda:0 and
-must give the same bits."""
+without a StepLR schedule; tests/golden/fuzz_fedopt_sqrt_s41.json (round 3) the same for 60 cases of the
+optimizers that take a sqrt (Adam, AdamW, amsgrad, maximize, NAdam, RAdam, RMSprop centered / momentum,
+Adagrad).  The drop-in generator steps every parameter with the HIP kernels on cuda:0 and must give the same
+bits."""
 
 import copy
 import json
@@ -23,18 +25,24 @@ pytestmark = pytest.mark.gpu
 HERE = os.path.dirname(os.path.abspath(__file__))
 
 
-def test_fuzz_fedopt_cases_match_reference_on_the_gpu():
+@pytest.mark.parametrize("fixture,family,n_kinds", [("fuzz_fedopt_s31.json", "plain", 4),
+                                                     ("fuzz_fedopt_sqrt_s41.json", "sqrt", 6)])
+def test_fuzz_fedopt_cases_match_reference_on_the_gpu(fixture, family, n_kinds, monkeypatch):
+    """The sqrt family (Adam, AdamW, amsgrad, NAdam, RAdam, RMSprop, Adagrad) replays with torch CPU's restated
+    sqrt, the one the recording container's torch computed (nvflare_amd/torch_sqrt.py)."""
     from nvflare_amd.app_opt.pt import PTFedOptModelShareableGenerator
     from nvflare_amd.compat import (DXO, AppConstants, DataKind, EventType, FLContext, ModelLearnableKey,
                                     make_model_learnable)
 
-    with open(os.path.join(HERE, "golden", "fuzz_fedopt_s31.json")) as f:
+    monkeypatch.setenv("NVFLARE_AMD_TORCH_SQRT", "torch_cpu")
+    with open(os.path.join(HERE, "golden", fixture)) as f:
         rec = json.load(f)
+    assert rec.get("family", "plain") == family
     assert rec["numpy"].split(".")[:2] == np.__version__.split(".")[:2], "the inputs regenerate only on this numpy"
     rng = np.random.default_rng(rec["seed"])
     bad, rounds, keys, kinds = [], 0, 0, set()
     for r in rec["records"]:
-        spec = F.gen_case(rng)
+        spec = F.gen_case(rng, family)
         assert spec["optimizer_args"]["path"] == r["optimizer"] and spec["container"] == r["container"]
         gen = PTFedOptModelShareableGenerator(optimizer_args=copy.deepcopy(spec["optimizer_args"]),
                                               lr_scheduler_args=copy.deepcopy(spec["lr_scheduler_args"]),
@@ -51,4 +59,4 @@ def test_fuzz_fedopt_cases_match_reference_on_the_gpu():
             keys += len(g["weights"])
         kinds.add(r["optimizer"])
     assert not bad, bad[:10]
-    assert rounds == 3 * len(rec["records"]) and keys > 500 and len(kinds) == 4
+    assert rounds == 3 * len(rec["records"]) and keys > 500 and len(kinds) == n_kinds
