@@ -40,20 +40,22 @@ def test_random_rounds_match_reference(tmp_path, mode, seed, threads):
         assert stats["cases"] == 120 and stats["accepted"] > 200
 
 
-def test_recorded_fedopt_cases_regenerate():
-    """tests/golden/fuzz_fedopt_s31.json's inputs regenerate from its seed here: each case's optimizer,
-    container and per-round key sets (the reference's outputs carry every state key, the rounds' diffs a subset)
-    come out of fuzz_reference_fedopt.gen_case as recorded."""
+@pytest.mark.parametrize("fixture,family", [("fuzz_fedopt_s31.json", "plain"), ("fuzz_fedopt_sqrt_s41.json", "sqrt")])
+def test_recorded_fedopt_cases_regenerate(fixture, family):
+    """tests/golden/fuzz_fedopt_s31.json's (and the sqrt family's fuzz_fedopt_sqrt_s41.json) inputs regenerate from
+    the seed here: each case's optimizer, container and per-round key sets (the reference's outputs carry every
+    state key, the rounds' diffs a subset) come out of fuzz_reference_fedopt.gen_case as recorded."""
     import numpy as np
 
     import fuzz_reference_fedopt as F
 
-    with open(os.path.join(HERE, "golden", "fuzz_fedopt_s31.json")) as f:
+    with open(os.path.join(HERE, "golden", fixture)) as f:
         rec = json.load(f)
+    assert rec.get("family", "plain") == family
     rng = np.random.default_rng(rec["seed"])
     n_missing = 0
     for r in rec["records"]:
-        spec = F.gen_case(rng)
+        spec = F.gen_case(rng, family)
         assert spec["optimizer_args"]["path"] == r["optimizer"] and spec["container"] == r["container"]
         state_keys = list(F.build_model(spec).state_dict())
         for diff, exp in zip(spec["rounds"], r["rounds"]):
