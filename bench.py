@@ -385,7 +385,7 @@ def run_workload(args, ctx, world, rank, K, P_spec, scaling, epilogue, baseline,
                 for k, v in ADAM_HP.items():
                     setattr(epi, k, v)
                 epi.momentum_decay, epi.mu_product = 4e-3, 1.0  # NAdam (mu_product held at its first-step value)
-                epi.sqrt_table = torch_sqrt.epilogue_table(ctx, sqrt_mode(args))
+                epi.torch_sqrt = torch_sqrt.epilogue_flag(sqrt_mode(args))
         ctx.sync()
         n_step = [0]
 

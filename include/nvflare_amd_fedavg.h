@@ -28,7 +28,7 @@ extern "C" {
 
 /* Bumped whenever a struct layout or an entry point changes (v3: Rprop / ASGD fields appended to struct
  * fedavg_epilogue; v4: fedavg_launch_count; v5: fedavg_d2h_multi; v6: fedavg_accumulate_tiled16_tails and
- * integer accumulators in fedavg_accumulate; v7: fedavg_epilogue.sqrt_table).  fedavg_struct_size() lets a binding
+ * integer accumulators in fedavg_accumulate; v7: fedavg_epilogue.torch_sqrt).  fedavg_struct_size() lets a binding
  * check each struct's size as well. */
 #define FEDAVG_ABI_VERSION 7
 
@@ -117,13 +117,11 @@ typedef struct fedavg_epilogue {
     double etaminus, etaplus;   /* Rprop: etas; state1 = prev, state2 = step_size (lr-filled before step 1) */
     double step_size_min, step_size_max; /* Rprop: step_sizes */
     double eta, mu, lambd;      /* ASGD: fp32 eta / mu states before this step, lambd; state1 = ax */
-    /* v7: NULL = correctly rounded sqrt; else a DEVICE pointer to FEDAVG_SQRT_TABLE_ENTRIES uint16 entries, and every
-     * sqrt of the step is torch CPU's (MKL vsSqrt on AVX-512: one Newton step from the VRSQRT14PS estimate, entry
-     * [parity << 15 | mantissa >> 8] holding mantissa bits 22..7 of the estimate for x in [1, 4); see
-     * tools/sqrt_probe.c and nvflare_amd/torch_sqrt.py) */
-    const uint16_t* sqrt_table;
+    /* v7: 0 = correctly rounded sqrt; nonzero = every sqrt of the step is torch CPU's (MKL vsSqrt on AVX-512: one
+     * Newton step from the VRSQRT14PS estimate, restated exactly; see tools/sqrt_probe.c and
+     * nvflare_amd/torch_sqrt.py) */
+    int torch_sqrt;
 } fedavg_epilogue;
-#define FEDAVG_SQRT_TABLE_ENTRIES 65536
 
 /* Quantized payload formats (nvflare/app_opt/pt/quantization/dequantizer.py:47-185, row f4). */
 enum fedavg_qtype {
@@ -343,8 +341,8 @@ int fedavg_fill_synthetic_f32(fedavg_ctx* ctx, float* dst, size_t n, size_t tile
 /* Gather m fp32 elements src[idx[j]] (idx: host array) into host_out (spot checks at full size). */
 int fedavg_gather_f32(fedavg_ctx* ctx, const float* src, const uint64_t* idx, size_t m, float* host_out);
 /* Test entry (v7): out[i] = the epilogues' sqrt of x[i] on the compute stream (device pointers): torch CPU's vsSqrt
- * restated from sqrt_table (struct fedavg_epilogue.sqrt_table), or the correctly rounded sqrt when it is NULL. */
-int fedavg_sqrt_f32(fedavg_ctx* ctx, const float* x, float* out, size_t n, const uint16_t* sqrt_table);
+ * restated (torch_sqrt nonzero, as struct fedavg_epilogue.torch_sqrt), or the correctly rounded sqrt. */
+int fedavg_sqrt_f32(fedavg_ctx* ctx, const float* x, float* out, size_t n, int torch_sqrt);
 
 #ifdef __cplusplus
 }

@@ -20,7 +20,7 @@ LIB_PATH = os.path.join(LIB_DIR, LIB_NAME)
 SOURCES = ["fedavg_tiles_numpy.hip", "fedavg_tiles_torch.hip", "fedavg_tiles_unweighted.hip",
            "fedavg_epi_numpy.hip", "fedavg_epi_torch.hip", "fedavg_epi_unweighted.hip",
            "fedavg_kernels.hip", "fedavg_narrow.hip", "fedavg_dequant.hip", "fedavg_capi.cpp"]
-HEADERS = ["fedavg_internal.h", "fedavg_arith.h", "fedavg_tiles.h", "fedavg_epi.h"]
+HEADERS = ["fedavg_internal.h", "fedavg_rsqrt14.h", "fedavg_arith.h", "fedavg_tiles.h", "fedavg_epi.h"]
 OBJ_DIR = os.path.join(PKG, "lib", "obj")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"

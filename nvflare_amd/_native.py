@@ -182,7 +182,7 @@ _SIGNATURES = {
     "fedavg_set_tile": [c_void_p, c_int],
     "fedavg_fill_synthetic_f32": [c_void_p, c_void_p, c_size_t, c_size_t, c_size_t, c_u64, c_u64, c_u64],
     "fedavg_gather_f32": [c_void_p, c_void_p, c_void_p, c_size_t, c_void_p],
-    "fedavg_sqrt_f32": [c_void_p, c_void_p, c_void_p, c_size_t, c_void_p],
+    "fedavg_sqrt_f32": [c_void_p, c_void_p, c_void_p, c_size_t, c_int],
     "fedavg_dequantize": [c_void_p, c_void_p, c_void_p, c_size_t, c_void_p, c_size_t, c_size_t, c_size_t],
 }
 EXPORTED = ["fedavg_last_error", "fedavg_abi_version", "fedavg_struct_size", *_SIGNATURES.keys()]
@@ -236,11 +236,10 @@ class Epilogue(ctypes.Structure):
         ("eta", c_double),
         ("mu", c_double),
         ("lambd", c_double),
-        ("sqrt_table", c_void_p),  # v7: device table of torch CPU's sqrt (nvflare_amd/torch_sqrt.py) or NULL
+        ("torch_sqrt", c_int),  # v7: torch CPU's sqrt (nvflare_amd/torch_sqrt.py) when nonzero, else IEEE
     ]
 
 
-FEDAVG_SQRT_TABLE_ENTRIES = 65536
 FEDAVG_Q_F16 = 1
 FEDAVG_Q_BF16 = 2
 FEDAVG_Q_BLOCKWISE8 = 3

@@ -315,7 +315,7 @@ class DeviceServerOptimizer:
                 e.state3 = self._max_exp_avg_sq().data_ptr()
         if self.kind in _SQRT_KINDS:
             # the reference's sqrt is torch CPU's on the server (vsSqrt, not correctly rounded; torch_sqrt.py)
-            e.sqrt_table = torch_sqrt.epilogue_table(self.ctx, self.sqrt_mode)
+            e.torch_sqrt = torch_sqrt.epilogue_flag(self.sqrt_mode)
         return e
 
     def step(self, model_diff: Dict) -> List[str]:

@@ -7,6 +7,7 @@
 #include <stdint.h>
 
 #include "fedavg_internal.h"
+#include "fedavg_rsqrt14.h"
 
 namespace fedavg {
 
@@ -155,17 +156,29 @@ __device__ __forceinline__ void tile_sum(f32x4 (&acc)[CPL], const RowTableF32& t
     }
 }
 
-// torch CPU's fp32 Tensor.sqrt (the epilogues' sqrt when EpiParams.sqrt_tab != NULL, fedavg_epi.h sqrt_e): MKL VML
-// vsSqrt on AVX-512 (ATen vml.h IMPLEMENT_VML_MKL(sqrt, Sqrt), VML_HA), which is not correctly rounded but one Newton step from the VRSQRT14PS estimate (measured
-// bit-exact against torch over every mantissa of [1, 4), every subnormal and a sample of every binade:
-// tools/sqrt_probe.py; restated in oracle_sqrt_torch_cpu):
+// torch CPU's fp32 Tensor.sqrt (the epilogues' sqrt when EpiParams.torch_sqrt is set, fedavg_epi.h sqrt_e): MKL VML
+// vsSqrt on AVX-512 (ATen vml.h IMPLEMENT_VML_MKL(sqrt, Sqrt), VML_HA), which is not correctly rounded but one Newton
+// step from the VRSQRT14PS estimate (measured bit-exact against torch over every mantissa of [1, 4), every subnormal
+// and a sample of every binade: tools/sqrt_probe.py; restated in oracle_sqrt_torch_cpu):
 //     y = rsqrt14(x);  s = x * y;  r = fma(-s, s, x);  sqrt = fma(r, 0.5 * y, s)
-// rsqrt14 depends on the exponent parity and the top 15 mantissa bits: tab[parity << 15 | m >> 8] = mantissa bits
-// 22..7 of the estimate for x in [1, 4) (exponent 126), a power of four giving its exact root.  Inputs below 2^-96
-// run at x * 2^64 and are scaled back by 2^-32 (no subnormal residual); 0, inf, NaN and negatives are IEEE.  The
-// table (128 KiB) stays in L2; one 2-byte gather per sqrt.
-__device__ __forceinline__ float sqrt_torch_cpu(const uint16_t* __restrict__ tab, const float x) {
-    if (!(x > 0.0f) || x == __builtin_inff()) return __builtin_sqrtf(x);
+// rsqrt14 depends on the exponent parity and the top 15 mantissa bits; mantissa bits 22..7 of the estimate for x in
+// [1, 4) are 32 exact fixed-point lines per parity (fedavg_rsqrt14.h, generated from the captured instruction table
+// nvflare_amd/data/rsqrt14_avx512.bin), a power of four giving its exact root.  Inputs below 2^-96 run at x * 2^64
+// and are scaled back by 2^-32 (no subnormal residual); 0, inf, NaN and negatives are IEEE (v_sqrt_f32 is exact
+// on them).  Branch-free; per sqrt one 8-byte LDS read of the staged segment table (rsqrt14_stage) and one integer
+// multiply-add.  (The first form gathered 2 bytes per sqrt from a 128 KiB device table: fused Adam at config 5 ran
+// 81.3 % of HBM peak against 87.3 % with the correctly rounded sqrt; the same segments read from global memory,
+// 83.3 %: profiles/r03/s4, s5.)
+__shared__ uint2 g_rsqrt14_lds[64];  // {kRsqrt14Base, kRsqrt14Slope}[segment]
+
+// every kernel that computes sqrt_torch_cpu calls this first, with the whole block (one barrier)
+__device__ __forceinline__ void rsqrt14_stage() {
+    if (threadIdx.x < 64) g_rsqrt14_lds[threadIdx.x] = uint2{kRsqrt14Base[threadIdx.x], kRsqrt14Slope[threadIdx.x]};
+    __syncthreads();
+}
+
+__device__ __forceinline__ float sqrt_torch_cpu(const float x) {
+    const bool special = !(x > 0.0f) || x == __builtin_inff();
     const bool tiny = x < 0x1p-96f;
     const float xs = tiny ? x * 0x1p64f : x;
     const uint32_t b = __float_as_uint(xs);
@@ -173,12 +186,14 @@ __device__ __forceinline__ float sqrt_torch_cpu(const uint16_t* __restrict__ tab
     const uint32_t m = b & 0x7FFFFFu;
     const int p = e & 1;
     const int k = (e - p) / 2;
-    const uint32_t yb = (p == 0 && m == 0) ? 0x3F800000u : (0x3F000000u | ((uint32_t)tab[(p << 15) | (m >> 8)] << 7));
+    const uint2 ab = g_rsqrt14_lds[(((uint32_t)p << 5) | (m >> 18)) & 63u];
+    const uint32_t y16 = (ab.x - ab.y * ((m >> 8) & 1023u)) >> 10;
+    const uint32_t yb = (p == 0 && m == 0) ? 0x3F800000u : (0x3F000000u | (y16 << 7));
     const float y = __uint_as_float((uint32_t)((int32_t)yb - k * 8388608));
     const float s = xs * y;
     const float r = __builtin_fmaf(-s, s, xs);
     const float res = __builtin_fmaf(r, 0.5f * y, s);
-    return tiny ? res * 0x1p-32f : res;
+    return special ? __builtin_amdgcn_sqrtf(x) : (tiny ? res * 0x1p-32f : res);
 }
 
 }  // namespace fedavg

@@ -431,7 +431,7 @@ fedavg::EpiParams make_epi(const fedavg_epilogue& e) {
     E.base = e.base;
     E.amsgrad = e.kind == FEDAVG_EPI_ADAM && e.amsgrad;
     E.state3 = e.state3;
-    E.sqrt_tab = e.sqrt_table;
+    E.torch_sqrt = e.torch_sqrt != 0;
     if (e.kind == FEDAVG_EPI_RMSPROP) {  // rmsprop.py: square_avg.mul_(alpha).addcmul_(g, g, 1 - alpha), lerp(1 - alpha)
         E.beta2 = (float)e.alpha;
         E.one_minus_beta2 = (float)(1.0 - e.alpha);
@@ -1448,14 +1448,14 @@ int fedavg_fill_synthetic_f32(fedavg_ctx* ctx, float* dst, size_t n, size_t tile
     });
 }
 
-int fedavg_sqrt_f32(fedavg_ctx* ctx, const float* x, float* out, size_t n, const uint16_t* sqrt_table) {
+int fedavg_sqrt_f32(fedavg_ctx* ctx, const float* x, float* out, size_t n, int torch_sqrt) {
     return guarded([&] {
         if (!ctx) throw Error("ctx is NULL");
         if (n == 0) return;
         if (!x || !out) throw Error("NULL pointer");
         ctx->activate();
         const int grid = (int)std::min<size_t>((size_t)ctx->num_cus * 8, (n + fedavg::kBlock - 1) / fedavg::kBlock);
-        HIP_CHECK(fedavg::launch_sqrt_f32(x, out, (int64_t)n, sqrt_table, grid, ctx->compute()));
+        HIP_CHECK(fedavg::launch_sqrt_f32(x, out, (int64_t)n, torch_sqrt != 0, grid, ctx->compute()));
     });
 }
 

@@ -31,7 +31,7 @@ struct EpiIn {
 
 template <bool TSQ>
 __device__ __forceinline__ float sqrt_e(const EpiParams& E, const float x) {
-    if constexpr (TSQ) return sqrt_torch_cpu(E.sqrt_tab, x);
+    if constexpr (TSQ) return sqrt_torch_cpu(x);
     return __builtin_sqrtf(x);
 }
 
@@ -271,6 +271,7 @@ fedavg_tiles_epi_burst_f32x4(const RowTableF32 tab, const int K, const int64_t t
     constexpr int NT = TPB + TPB_LDS;
     f32x4 dd[TPB][CPL];
     __shared__ f32x4 staged[TPB_LDS > 0 ? TPB_LDS * CPL * kBlock : 1];
+    if constexpr ((EPI & kEpiTorchSqrt) != 0) rsqrt14_stage();
 #pragma unroll
     for (int m = 0; m < TPB; ++m) {
         const int64_t t = t0 + blockIdx.x + (int64_t)m * gridDim.x;
@@ -356,6 +357,7 @@ __global__ void __launch_bounds__(kBlock) fedavg_tiles_epi_f32x4(const RowTableF
     constexpr int64_t T4 = (int64_t)CPL * kBlock;
     const int64_t t_last = (e4 - 1) / T4;
     const int g0 = PIPE ? (K < UNROLL ? K : UNROLL) : 0;  // clients carried over from the previous tile
+    if constexpr ((EPI & kEpiTorchSqrt) != 0) rsqrt14_stage();
     f32x4 nxt[UNROLL][CPL];
     int64_t t = b4 / T4 + blockIdx.x;
     if constexpr (PIPE) {
@@ -486,22 +488,22 @@ inline hipError_t launch_epi_a(const TileLaunch& L, const EpiParams& E, hipStrea
         case FEDAVG_EPI_SGD:
             return launch_epi_k<OP, FIN, ACC_IN, FEDAVG_EPI_SGD>(L, E, s, nl);
         case FEDAVG_EPI_ADAM:
-            return E.sqrt_tab ? launch_epi_k<OP, FIN, ACC_IN, FEDAVG_EPI_ADAM | kEpiTorchSqrt>(L, E, s, nl)
-                              : launch_epi_k<OP, FIN, ACC_IN, FEDAVG_EPI_ADAM>(L, E, s, nl);
+            return E.torch_sqrt ? launch_epi_k<OP, FIN, ACC_IN, FEDAVG_EPI_ADAM | kEpiTorchSqrt>(L, E, s, nl)
+                                : launch_epi_k<OP, FIN, ACC_IN, FEDAVG_EPI_ADAM>(L, E, s, nl);
         case FEDAVG_EPI_ADAGRAD:
-            return E.sqrt_tab ? launch_epi_k<OP, FIN, ACC_IN, FEDAVG_EPI_ADAGRAD | kEpiTorchSqrt>(L, E, s, nl)
-                              : launch_epi_k<OP, FIN, ACC_IN, FEDAVG_EPI_ADAGRAD>(L, E, s, nl);
+            return E.torch_sqrt ? launch_epi_k<OP, FIN, ACC_IN, FEDAVG_EPI_ADAGRAD | kEpiTorchSqrt>(L, E, s, nl)
+                                : launch_epi_k<OP, FIN, ACC_IN, FEDAVG_EPI_ADAGRAD>(L, E, s, nl);
         case FEDAVG_EPI_RMSPROP:
-            return E.sqrt_tab ? launch_epi_k<OP, FIN, ACC_IN, FEDAVG_EPI_RMSPROP | kEpiTorchSqrt>(L, E, s, nl)
-                              : launch_epi_k<OP, FIN, ACC_IN, FEDAVG_EPI_RMSPROP>(L, E, s, nl);
+            return E.torch_sqrt ? launch_epi_k<OP, FIN, ACC_IN, FEDAVG_EPI_RMSPROP | kEpiTorchSqrt>(L, E, s, nl)
+                                : launch_epi_k<OP, FIN, ACC_IN, FEDAVG_EPI_RMSPROP>(L, E, s, nl);
         case FEDAVG_EPI_ADAMAX:
             return launch_epi_k<OP, FIN, ACC_IN, FEDAVG_EPI_ADAMAX>(L, E, s, nl);
         case FEDAVG_EPI_NADAM:
-            return E.sqrt_tab ? launch_epi_k<OP, FIN, ACC_IN, FEDAVG_EPI_NADAM | kEpiTorchSqrt>(L, E, s, nl)
-                              : launch_epi_k<OP, FIN, ACC_IN, FEDAVG_EPI_NADAM>(L, E, s, nl);
+            return E.torch_sqrt ? launch_epi_k<OP, FIN, ACC_IN, FEDAVG_EPI_NADAM | kEpiTorchSqrt>(L, E, s, nl)
+                                : launch_epi_k<OP, FIN, ACC_IN, FEDAVG_EPI_NADAM>(L, E, s, nl);
         case FEDAVG_EPI_RADAM:
-            return E.sqrt_tab ? launch_epi_k<OP, FIN, ACC_IN, FEDAVG_EPI_RADAM | kEpiTorchSqrt>(L, E, s, nl)
-                              : launch_epi_k<OP, FIN, ACC_IN, FEDAVG_EPI_RADAM>(L, E, s, nl);
+            return E.torch_sqrt ? launch_epi_k<OP, FIN, ACC_IN, FEDAVG_EPI_RADAM | kEpiTorchSqrt>(L, E, s, nl)
+                                : launch_epi_k<OP, FIN, ACC_IN, FEDAVG_EPI_RADAM>(L, E, s, nl);
         case FEDAVG_EPI_RPROP:
             return launch_epi_k<OP, FIN, ACC_IN, FEDAVG_EPI_RPROP>(L, E, s, nl);
         case FEDAVG_EPI_ASGD:

@@ -36,7 +36,7 @@ constexpr int kVariantWideLds = 64;       // inside TileLaunch: plain burst kern
                                            // unless the public variant has bit 6, which keeps the 4-tile form there
                                            // (32 clients 88.4 -> 88.9 %, 64: 89.7 -> 89.9 %, profiles/r02/ab/wide_lds/)
 // epilogue template value: the optimizer kind | kEpiTorchSqrt when the step's sqrt is torch CPU's restated vsSqrt
-// (EpiParams.sqrt_tab; fedavg_arith.h sqrt_torch_cpu) -- a compile-time choice, so the correctly rounded path
+// (EpiParams.torch_sqrt; fedavg_arith.h sqrt_torch_cpu) -- a compile-time choice, so the correctly rounded path
 // keeps its own code (a runtime branch cost the fused Adam kernel 9 points, profiles/r03/s3/)
 constexpr int kEpiTorchSqrt = 0x100;
 constexpr int kBurstLdsTilesWide = 10;     // 10 x 16 KiB = all of a CU's LDS
@@ -97,7 +97,7 @@ struct EpiParams {
     int rectified;                                // RAdam: rho_t > 5
     float etaminus, etaplus, ss_min, ss_max;      // Rprop
     float decay, neg_eta, mu;                     // ASGD: 1 - lambd * eta, -eta, mu (averaging when != 1)
-    const uint16_t* sqrt_tab;                     // torch CPU's sqrt (VRSQRT14 mantissa table) or NULL: IEEE
+    int torch_sqrt;                               // torch CPU's sqrt (fedavg_arith.h sqrt_torch_cpu), else IEEE
 };
 
 struct DequantLaunch {
@@ -184,6 +184,6 @@ hipError_t launch_tiles_f64(const RowTableGeneric& tab, int K, int64_t tstride_e
 hipError_t launch_fill_synthetic_f32(float* dst, int64_t n, int64_t tile, int64_t tstride, uint64_t seed, uint64_t row,
                                      uint64_t col0, int grid, hipStream_t s);
 hipError_t launch_gather_f32(const float* src, const uint64_t* idx, float* dst, int64_t m, hipStream_t s);
-hipError_t launch_sqrt_f32(const float* x, float* out, int64_t n, const uint16_t* tab, int grid, hipStream_t s);
+hipError_t launch_sqrt_f32(const float* x, float* out, int64_t n, int torch_sqrt, int grid, hipStream_t s);
 
 }  // namespace fedavg

@@ -585,17 +585,18 @@ hipError_t launch_fill_synthetic_f32(float* dst, int64_t n, int64_t tile, int64_
     return hipGetLastError();
 }
 
-// test kernel: the epilogues' sqrt elementwise (tab: torch CPU's restated vsSqrt; NULL: the correctly rounded one)
+// test kernel: the epilogues' sqrt elementwise (torch_sqrt: torch CPU's restated vsSqrt; 0: the correctly rounded one)
 __global__ void __launch_bounds__(kBlock) fedavg_sqrt_f32(const float* __restrict__ x, float* __restrict__ out, int64_t n,
-                                                          const uint16_t* __restrict__ tab) {
+                                                          int torch_sqrt) {
     const int64_t stride = (int64_t)gridDim.x * kBlock;
+    rsqrt14_stage();
     for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride)
-        out[i] = tab != nullptr ? sqrt_torch_cpu(tab, x[i]) : __builtin_sqrtf(x[i]);
+        out[i] = torch_sqrt ? sqrt_torch_cpu(x[i]) : __builtin_sqrtf(x[i]);
 }
 
-hipError_t launch_sqrt_f32(const float* x, float* out, int64_t n, const uint16_t* tab, int grid, hipStream_t s) {
+hipError_t launch_sqrt_f32(const float* x, float* out, int64_t n, int torch_sqrt, int grid, hipStream_t s) {
     if (n <= 0) return hipSuccess;
-    hipLaunchKernelGGL(fedavg_sqrt_f32, dim3(grid), dim3(kBlock), 0, s, x, out, n, tab);
+    hipLaunchKernelGGL(fedavg_sqrt_f32, dim3(grid), dim3(kBlock), 0, s, x, out, n, torch_sqrt);
     return hipGetLastError();
 }
 

@@ -6,8 +6,9 @@ kernel.  torch 2.10 with MKL computes it with MKL VML vsSqrt (ATen vml.h, IMPLEM
 on the AVX-512 path is NOT the correctly rounded vsqrtps: it is one Newton step from the VRSQRT14PS estimate
 (tools/sqrt_probe.c; ~0.5 % of results 1 ulp low).  The device epilogue reproduces either:
 
-* ``"torch_cpu"`` -- the restated vsSqrt (fedavg_epi.h ``sqrt_torch_cpu``) from the estimate table captured where
-  the golden FedOpt fixtures were generated (``data/rsqrt14_avx512.bin``, 2 x 2^15 estimates);
+* ``"torch_cpu"`` -- the restated vsSqrt (fedavg_arith.h ``sqrt_torch_cpu``) with the estimate table captured where
+  the golden FedOpt fixtures were generated (``data/rsqrt14_avx512.bin``, 2 x 2^15 estimates), which the kernel
+  evaluates as 64 exact line segments (fedavg_rsqrt14.h, tools/make_rsqrt14_segments.py);
 * ``"ieee"`` -- the correctly rounded sqrt (torch builds / CPUs whose vsSqrt rounds correctly).
 
 ``mode()`` follows ``$NVFLARE_AMD_TORCH_SQRT`` (``torch_cpu`` | ``ieee`` | ``auto``, the default): ``auto`` asks this
@@ -19,7 +20,7 @@ from __future__ import annotations
 
 import os
 import threading
-from typing import Dict, Optional
+from typing import Optional
 
 import numpy as np
 
@@ -31,7 +32,6 @@ MODES = ("torch_cpu", "ieee")
 _lock = threading.RLock()
 _detected: Optional[str] = None
 _table: Optional[np.ndarray] = None
-_device_tables: Dict[int, object] = {}  # id(DeviceContext) -> DeviceBuffer holding the table
 
 
 def table() -> np.ndarray:
@@ -77,22 +77,9 @@ def mode() -> str:
     return d if d in MODES else "ieee"
 
 
-def device_table(ctx) -> int:
-    """Device address of the estimate table on ``ctx``'s device (uploaded once per context)."""
-    with _lock:
-        buf = _device_tables.get(id(ctx))
-        if buf is None or getattr(buf, "ctx", None) is not ctx or not buf.ptr:
-            tab = table() if _table is None else _table
-            buf = ctx.alloc(tab.nbytes)
-            ctx.h2d_ptr(buf.ptr, tab.ctypes.data, tab.nbytes)
-            ctx.sync()
-            _device_tables[id(ctx)] = buf
-        return buf.ptr
-
-
-def epilogue_table(ctx, sqrt_mode: Optional[str] = None) -> Optional[int]:
-    """``fedavg_epilogue.sqrt_table`` for a step on ``ctx``: the device table in ``torch_cpu`` mode, else None."""
+def epilogue_flag(sqrt_mode: Optional[str] = None) -> int:
+    """``fedavg_epilogue.torch_sqrt`` for a step: 1 in ``torch_cpu`` mode, else 0 (the correctly rounded sqrt)."""
     m = sqrt_mode or mode()
     if m not in MODES:
         raise ValueError(f"sqrt mode {m!r}: expected one of {MODES}")
-    return device_table(ctx) if m == "torch_cpu" else None
+    return int(m == "torch_cpu")

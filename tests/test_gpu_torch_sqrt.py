@@ -6,7 +6,7 @@
   torch_sqrt.detect() finds the restated vsSqrt here;
 * inside every epilogue that takes a sqrt (Adam, AdamW + amsgrad, Adagrad, RMSprop centered + momentum, NAdam,
   RAdam), kernel against oracle with the same sqrt, several rounds, bit-exact;
-* the table-driven and the correctly rounded sqrt really differ (the mode switch reaches the kernel)."""
+* the restated and the correctly rounded sqrt really differ (the mode switch reaches the kernel)."""
 
 import os
 import sys
@@ -35,11 +35,11 @@ def _probe_set():
     return sqrt_probe.probe_set().view(np.float32)
 
 
-def _device_sqrt(ctx, x, table):
+def _device_sqrt(ctx, x, torch_sqrt):
     buf = ctx.alloc(x.nbytes)
     out = ctx.alloc(x.nbytes)
     ctx.h2d_ptr(buf.ptr, x.ctypes.data, x.nbytes)
-    ctx.sqrt_f32(buf.ptr, out.ptr, x.size, table)
+    ctx.sqrt_f32(buf.ptr, out.ptr, x.size, torch_sqrt)
     got = np.empty_like(x)
     ctx.d2h(got, out.ptr)
     buf.close()
@@ -57,10 +57,10 @@ def test_device_sqrt_matches_restatement_everywhere(ctx, oracle):
     from nvflare_amd import torch_sqrt
 
     x = _probe_set()
-    got = _device_sqrt(ctx, x, torch_sqrt.device_table(ctx))
+    got = _device_sqrt(ctx, x, True)
     exp = oracle.sqrt_torch_cpu(x)
     assert _same(got, exp) == 0
-    ieee = _device_sqrt(ctx, x, None)
+    ieee = _device_sqrt(ctx, x, False)
     with np.errstate(invalid="ignore"):
         assert _same(ieee, np.sqrt(x)) == 0
     assert _same(got, ieee) > 300_000  # the two sqrt modes are different functions
@@ -113,7 +113,6 @@ KINDS = [
 @pytest.mark.parametrize("name,hp", KINDS, ids=[k for k, _ in KINDS])
 def test_epilogues_with_torch_cpu_sqrt(ctx, oracle, name, hp, K):
     from nvflare_amd import _native as N
-    from nvflare_amd import torch_sqrt
 
     kind = {"adam": oracle.EPI_ADAM, "adamw_amsgrad": oracle.EPI_ADAM, "adagrad": oracle.EPI_ADAGRAD,
             "rmsprop": oracle.EPI_RMSPROP, "nadam": oracle.EPI_NADAM, "radam": oracle.EPI_RADAM}[name]
@@ -122,7 +121,6 @@ def test_epilogues_with_torch_cpu_sqrt(ctx, oracle, name, hp, K):
     p = rng.standard_normal(n).astype(np.float32)
     m, v, x3 = (np.zeros(n, np.float32) for _ in range(3))
     dev_p = dev_m = dev_v = dev_3 = None
-    table = torch_sqrt.device_table(ctx)
     ws = [float(1 + (37 * k) % 100) for k in range(K)]
     count = None
     for w in ws:
@@ -138,7 +136,7 @@ def test_epilogues_with_torch_cpu_sqrt(ctx, oracle, name, hp, K):
         e.kind = kind
         for k_, val in hp.items():
             setattr(e, k_, val)
-        e.step, e.mu_product, e.sqrt_table = float(step), mp, table
+        e.step, e.mu_product, e.torch_sqrt = float(step), mp, 1
         e.param, e.state1 = dev.buf("p", dev_p), dev.buf("m", dev_m)
         e.state2, e.state3 = dev.buf("v", dev_v), dev.buf("x3", dev_3)
         ctx.accumulate_tiled_epi(dev.bases, ws, 4096, dev.lay.tile_stride, 0, dev.n4, None, N.FEDAVG_OP_TORCH,

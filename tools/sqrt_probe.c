@@ -5,6 +5,7 @@
  * one Newton step from the CPU's reciprocal-square-root estimate (measured bit-exact in the container over every
  * mantissa of two binades, tools/sqrt_probe.py):
  *     y = rsqrt14(x);  s = x * y;  r = fma(-s, s, x);  sqrt(x) = fma(r, 0.5 * y, s)
+ * with inputs below 2^-96 computed at x * 2^64 and scaled back by 2^-32
  * so about 0.5 % of results sit 1 ulp below the correctly rounded one (Adam's exp_avg_sq.sqrt(), torch
  * optim/adam.py:545, and every other torch optimizer's sqrt).
  * The estimate (VRSQRT14PS) depends on the exponent parity and the top 15 mantissa bits only (measured),
@@ -95,12 +96,17 @@ int main(int argc, char** argv) {
         for (size_t i = 0; i < n; i += 16) {
             float xv[16], yv[16];
             const size_t c = n - i < 16 ? n - i : 16;
-            for (size_t j = 0; j < 16; ++j) xv[j] = f_of(xs[j < c ? i + j : i]);
+            float xo[16];
+            for (size_t j = 0; j < 16; ++j) {
+                xo[j] = f_of(xs[j < c ? i + j : i]);
+                xv[j] = (xo[j] > 0.0f && xo[j] < 0x1p-96f) ? xo[j] * 0x1p64f : xo[j];  /* the tiny-input scaling */
+            }
             _mm512_storeu_ps(yv, _mm512_rsqrt14_ps(_mm512_loadu_ps(xv)));
             for (size_t j = 0; j < c; ++j) {
                 const float yt = rsqrt14_table(tab, xv[j]);
                 if (b_of(yt) != b_of(yv[j]) && xv[j] > 0.0f && !isinf(xv[j])) ++est_mism;
-                const float a = sqrt_restated(xv[j], yt), b = sqrt_restated(xv[j], yv[j]);
+                const float sc = xv[j] != xo[j] ? 0x1p-32f : 1.0f;
+                const float a = sqrt_restated(xv[j], yt) * sc, b = sqrt_restated(xv[j], yv[j]) * sc;
                 if (b_of(a) != b_of(b)) ++sqrt_mism;
                 res[i + j] = a;
             }

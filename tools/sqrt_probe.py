@@ -77,6 +77,8 @@ def main():
         assert r.size == x.size
         res[f"torch_vs_restated_{name}_table"] = diff(t, r)
         res[f"{name}_table_restatement_vs_this_cpu_instruction"] = chk
+        if name == "local":
+            res["breakdown"] = _breakdown(x, xf, t, cr, r)
     # which candidate sequence reproduces this host's torch (tools/sqrt_probe2.c: rsqrt14 / rsqrtps estimates,
     # Newton forms, small-input scaling)
     exe2 = os.path.join(tmp, "sqrt_probe2")
@@ -96,6 +98,29 @@ def main():
         res["committed_table_sha256"] = hashlib.sha256(ct).hexdigest()
         res["local_table_equals_committed"] = lt == ct
     print(json.dumps(res), flush=True)
+
+
+def _breakdown(x, xf, t, cr, r):
+    """Where torch differs from the correctly rounded and the restated sqrt, by input class, with samples."""
+    tb, cb, rb = t.view(np.uint32), cr.view(np.uint32), r.view(np.uint32)
+    fin = np.isfinite(xf) & (xf > 0)
+    classes = {"subnormal": fin & (x < 0x00800000), "normal_lt_2m96": fin & (x >= 0x00800000) & (xf < 2.0 ** -96),
+               "normal_ge_2m96": fin & (xf >= 2.0 ** -96), "one_to_four": fin & (xf >= 1.0) & (xf < 4.0)}
+    out = {}
+    for name, sel in classes.items():
+        n = int(np.count_nonzero(sel))
+        d_cr = sel & (tb != cb)
+        d_r = sel & (tb != rb)
+        e = {"n": n, "vs_cr": int(np.count_nonzero(d_cr)), "vs_restated": int(np.count_nonzero(d_r)),
+             "torch_zero": int(np.count_nonzero(sel & (tb == 0)))}
+        # signed ulp distance torch - correctly rounded, histogram
+        ulp = tb[sel].astype(np.int64) - cb[sel].astype(np.int64)
+        vals, cnt = np.unique(np.clip(ulp, -4, 4), return_counts=True)
+        e["ulp_vs_cr"] = {int(v): int(c) for v, c in zip(vals, cnt)}
+        idx = np.flatnonzero(d_r)[:12]
+        e["samples"] = [[f"{int(x[i]):08x}", f"{int(tb[i]):08x}", f"{int(cb[i]):08x}", f"{int(rb[i]):08x}"] for i in idx]
+        out[name] = e
+    return out
 
 
 def _cpu_model() -> str:
