@@ -15,7 +15,10 @@ Scaling.  The path shards by parameter bucket:
          sharding.bucket_ranges(P, N); rank r aggregates bucket r of every client.
 After the main measurement the default run also measures, in the same process, BASELINE configs 5 and 4 under
 strong scaling (``--also``; config 4 needs >= 2 GPUs: 358 GB of client updates do not fit one 288 GB HBM), and
-embeds them in the line's ``also`` list -- so one N-GPU run records configs 3, 4 and 5 at that N.
+config 4 once more as a multi-GPU server would ingest it ("4x": client g's whole update on GPU g mod N, RCCL
+all-to-all of the buckets overlapped with the kernels, nvflare_amd/client_shards.py; serial and overlapped device
+times side by side, under a watchdog so a stuck collective cannot cost the line), and embeds them in the line's
+``also`` list -- so one N-GPU run records configs 3, 4 and 5 at that N.
 
 Prints ONE JSON line (rank 0).  value = GiB/s aggregated = 4*K*P_total*steps / t / 2^30 with t the max over
 ranks of the barrier+synchronize bracketed wall time (P_total = P*N weak, P strong).  roofline.achieved uses the
@@ -53,6 +56,8 @@ PRESET_NAMES = {
     4: "BASELINE config 4: 256 clients x 350M fp32 params, param buckets sharded across the GPUs",
     5: "BASELINE config 5: FedOpt server optimizer (Adam on aggregated deltas), 64 clients x 1B params",
 }
+CLIENT_SHARDED = 40  # --also token "4x": config 4 through the client-sharded exchange (run_client_sharded)
+WATCHDOG_S = 240.0  # the client-sharded entry's limit: a stuck collective must not cost the measured line
 EPI_STATE_BYTES = {"none": 4.0, "add_base": 8.0, "sgd": 16.0}  # per param beyond the 4*K client reads; else 24
 HEADROOM = 2 << 30  # device bytes left free beside a workload (runtime, gather buffers)
 
@@ -71,7 +76,11 @@ def parse(argv=None):
     ap.add_argument("--scaling", choices=["weak", "strong"], default=None)
     ap.add_argument("--also", default="auto",
                     help="extra strong-scaling BASELINE configs measured after the main one, in the same line "
-                         "(comma list of 4/5; 'auto' = 5,4 for the default config 3 run; 'none')")
+                         "(comma list of 4 / 5 / 4x = config 4 through the client-sharded RCCL exchange; "
+                         "'auto' = 5,4,4x for the default config 3 run; 'none')")
+    ap.add_argument("--client-sharded-params", type=float, default=None,
+                    help="model size of the 4x entry (default: config 4's 350M; smaller for one-GPU rehearsals)")
+    ap.add_argument("--watchdog-s", type=float, default=WATCHDOG_S, help="limit of the 4x entry")
     ap.add_argument("--mode", choices=["torch", "numpy"], default="torch")
     ap.add_argument("--blocks-per-cu", type=int, default=0,
                     help="0 = library default (burst kernel: 1 at >= 32 clients, else 2; fused: 1 at >= 64)")
@@ -103,8 +112,9 @@ def parse(argv=None):
                    for f in ("--clients", "--params", "--global-params", "--scaling", "--epilogue"))
     args.preset_exact = not explicit
     if args.also == "auto":
-        args.also = "5,4" if (args.config == 3 and not explicit) else "none"
-    args.also = [] if args.also in ("", "none") else [int(x) for x in args.also.split(",")]
+        args.also = "5,4,4x" if (args.config == 3 and not explicit) else "none"
+    args.also = [] if args.also in ("", "none") else [CLIENT_SHARDED if x.strip() == "4x" else int(x)
+                                                      for x in args.also.split(",")]
     return args
 
 
@@ -430,6 +440,117 @@ def run_workload(args, ctx, world, rank, K, P_spec, scaling, epilogue, baseline,
     return res
 
 
+def run_client_sharded(args, world, rank, local, K, P, seed):
+    """BASELINE config 4 ingested as a multi-GPU server receives it: client g's WHOLE update (P params) lands on
+    rank g mod N; RCCL all-to-alls move bucket b of every client to rank b, and each rank runs the arrival-ordered
+    kernel over its bucket (nvflare_amd/client_shards.py, the bit-exact "exchange" strategy).  Timed twice over
+    the same inputs: serial (all-to-all, then the kernels) and overlapped (the product path: chunked all-to-alls
+    on one stream, the kernels over the tiles received so far on another).  Strong scaling: value counts the
+    4*K*P client bytes once.  Returns {"skipped": ...} at N = 1 (nothing to exchange) or when it does not fit."""
+    if world < 2:
+        return {"skipped": "client-sharded ingest needs >= 2 GPUs (one rank has nothing to exchange)"}
+    import torch
+
+    from nvflare_amd.client_shards import ClientShardedFedAvg, ExchangePlan
+
+    clients = [len(range(s, K, world)) for s in range(world)]
+    plan = ExchangePlan(P, clients)
+    need = 4 * (plan.slab_elems(rank) + plan.recv_elems(rank) + plan.bucket_pad())
+    free, total = torch.cuda.mem_get_info(local)
+    if os.environ.get("NVFLARE_AMD_BENCH_SHARED_DEVICE") == "1":
+        free //= world  # the one-GPU rehearsal: every rank on cuda:0
+    if sum_over_ranks(world, [0 if need + HEADROOM <= free else 1])[0]:
+        return {"skipped": f"needs {need / 1e9:.1f} GB of HBM per GPU at {world} GPU(s) "
+                           f"(this device: {free / 1e9:.1f} GB free of {total / 1e9:.1f})"}
+    steps, warmup = max(1, min(args.steps, 5)), max(1, min(args.warmup, 1))
+    agg = ClientShardedFedAvg(P, clients, device=local, mode=args.mode)
+    try:
+        agg.fill_synthetic(seed, [j * world + rank for j in range(clients[rank])])
+        order = [(g % world, g // world) for g in range(K)]  # arrival order = global client id
+        weights = synth_weights(K)
+        nb = plan.bucket_len(rank)
+        stream = torch.cuda.current_stream()
+
+        def bracket(fn):
+            torch.cuda.synchronize()
+            dist_barrier(world)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            t0 = time.perf_counter()
+            e0.record(stream)
+            for _ in range(steps):
+                fn()
+            e1.record(stream)
+            torch.cuda.synchronize()
+            dist_barrier(world)
+            return max_over_ranks(world, time.perf_counter() - t0), max_over_ranks(world, e0.elapsed_time(e1) / steps)
+
+        for _ in range(warmup):
+            agg.aggregate(order, weights, "exchange")
+        # serial: the all-to-all alone, then the kernels alone (device times per phase)
+        a2a_wall, a2a_ms = bracket(agg.exchange)
+        kern_wall, kern_ms = bracket(lambda: agg.aggregate_exchanged(order, weights))
+        serial = agg.out[:nb].clone()
+        wall, ovl_ms = bracket(lambda: agg.aggregate(order, weights, "exchange"))
+        differ = int(not torch.equal(agg.out[:nb].view(torch.int32), serial.view(torch.int32)))
+        sc = None
+        if args.spot_check > 0 and nb:
+            sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+            from oracle import fedavg_oracle as orc
+
+            rng = np.random.default_rng(rank + 17)
+            idx = np.unique(np.concatenate([rng.integers(0, nb, min(args.spot_check, nb)), [0, nb - 1]]))
+            cols = (plan.buckets[rank][0] + idx).astype(np.uint64)
+            want = orc.fedavg_c([orc.synth_values(seed, g, cols) for g in range(K)], weights,
+                                orc.MODE_TORCH if args.mode == "torch" else orc.MODE_NUMPY)
+            got = agg.out[torch.from_numpy(idx).to(agg.out.device)].cpu().numpy()
+            sc = [int(idx.size), int(np.count_nonzero(got.view(np.uint32) != want.view(np.uint32)))]
+        sampled, mism, differ = sum_over_ranks(world, (sc or [0, 0]) + [differ])
+        a2a_out = 4.0 * (sum(plan.send_splits(rank)) - plan.send_splits(rank)[rank])
+        return {"K": K, "P": nb, "P_total": P, "wall": wall * steps, "steps": steps, "warmup": warmup,
+                "kernel_ms": kern_ms, "all_to_all_ms": a2a_ms, "overlapped_ms": ovl_ms,
+                "all_to_all_bytes_out_rank0": a2a_out if rank == 0 else None,
+                "bits_equal_serial": differ == 0,
+                "spot_check": {"sampled": sampled, "mismatches": mism + differ, "ranks": world,
+                               "oracle": "oracle/fedavg_oracle.c"} if sc is not None else None,
+                "clients_per_rank": clients, "max_peer_bytes": agg.max_peer_bytes,
+                "min_kernel_tiles": agg.min_kernel_tiles}
+    finally:
+        del agg
+        torch.cuda.empty_cache()
+
+
+def dist_barrier(world):
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.barrier()
+
+
+def summarize_client_sharded(args, world, r):
+    value = 4.0 * r["K"] * r["P_total"] * r["steps"] / r["wall"] / 2**30
+    kern_bytes = 4.0 * r["K"] * r["P"] + 4.0 * r["P"]
+    a2a_b = r["all_to_all_bytes_out_rank0"]
+    return {
+        "baseline_config": (PRESET_NAMES[4] if r["P_total"] == PRESETS[4]["params"]
+                            else f"custom (config 4 with {r['P_total']} params)")
+                           + " -- client-sharded ingest: client g's whole update on GPU g mod N, RCCL all-to-all of "
+                             "buckets, overlapped with the kernels",
+        "value": round(value, 2), "unit": "GiB/s", "n_gpus": world, "scaling": "strong",
+        "steps": r["steps"], "warmup": r["warmup"],
+        "ms_per_step": round(r["wall"] / r["steps"] * 1e3, 3),
+        "device_ms": {"overlapped": round(r["overlapped_ms"], 3), "serial_all_to_all": round(r["all_to_all_ms"], 3),
+                      "serial_kernels": round(r["kernel_ms"], 3),
+                      "hidden": round(r["all_to_all_ms"] + r["kernel_ms"] - r["overlapped_ms"], 3)},
+        "all_to_all_GBps_out_rank0": round(a2a_b / (r["all_to_all_ms"] / 1e3) / 1e9, 1) if r["all_to_all_ms"] else None,
+        "kernel_roofline_frac_rank0": round(kern_bytes / (r["kernel_ms"] / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+        "bits_equal_serial": r["bits_equal_serial"],
+        "spot_check": r["spot_check"],
+        "config": {"clients": r["K"], "params_total": r["P_total"], "params_bucket_rank0": r["P"],
+                   "clients_per_rank": r["clients_per_rank"], "mode": args.mode,
+                   "max_peer_bytes": r["max_peer_bytes"], "min_kernel_tiles": r["min_kernel_tiles"]},
+    }
+
+
 def summarize(args, world, res, K, scaling, epilogue, label):
     """The JSON fields of one measured workload (rank 0)."""
     P = res["P"]
@@ -481,6 +602,46 @@ def summarize(args, world, res, K, scaling, epilogue, label):
     }
 
 
+def client_sharded_entry(args, world, rank, local, line, also) -> bool:
+    """Run the client-sharded config-4 measurement and append its entry (rank 0).  A watchdog bounds it: if the
+    exchange has not finished after WATCHDOG_S, rank 0 prints the line measured so far (the entry marked timed
+    out) and every rank exits -- the main measurement is never lost to a stuck collective.  Returns True when its
+    spot check failed."""
+    import threading
+
+    def on_timeout():
+        if rank == 0:
+            also.append({"baseline_config": PRESET_NAMES[4] + " -- client-sharded ingest", "n_gpus": world,
+                         "error": f"did not finish within {args.watchdog_s:g} s (watchdog); measurement abandoned"})
+            line["also"] = also
+            print(json.dumps(line), flush=True)
+        sys.stdout.flush()
+        sys.stderr.flush()
+        os._exit(0)
+
+    dog = threading.Timer(args.watchdog_s, on_timeout)
+    dog.daemon = True
+    dog.start()
+    try:
+        p = PRESETS[4]
+        P = int(args.client_sharded_params) if args.client_sharded_params else p["params"]
+        r = run_client_sharded(args, world, rank, local, p["clients"], P, args.seed)
+    except Exception as e:  # noqa: BLE001 -- recorded in the line, the main measurement stands
+        dog.cancel()
+        if rank == 0:
+            also.append({"baseline_config": PRESET_NAMES[4] + " -- client-sharded ingest", "n_gpus": world,
+                         "error": f"{type(e).__name__}: {e}"})
+        return False
+    dog.cancel()
+    if rank == 0:
+        if "skipped" in r:
+            also.append({"baseline_config": PRESET_NAMES[4] + " -- client-sharded ingest", "n_gpus": world,
+                         "skipped": r["skipped"]})
+        else:
+            also.append(summarize_client_sharded(args, world, r))
+    return bool("skipped" not in r and (r.get("spot_check") or {}).get("mismatches"))
+
+
 def main(argv=None):
     args = parse(argv)
     world, rank, local = dist_setup(args)
@@ -500,6 +661,8 @@ def main(argv=None):
     also = []
     failed = bool((main_res.get("spot_check") or {}).get("mismatches"))  # counts summed over ranks: all agree
     for cfg in args.also:
+        if cfg == CLIENT_SHARDED:
+            continue  # last, under a watchdog (below)
         p = PRESETS[cfg]
         r = run_workload(args, ctx, world, rank, p["clients"], p["params"], p["scaling"], p["epilogue"],
                          baseline=False, seed=args.seed)
@@ -512,6 +675,7 @@ def main(argv=None):
                 entry["n_gpus"] = world
                 entry["spot_check"] = r["spot_check"]
                 also.append(entry)
+    line = None
     if rank == 0:
         s = summarize(args, world, main_res, K, args.scaling, args.epilogue, label)
         line = {
@@ -534,6 +698,9 @@ def main(argv=None):
         }
         if main_res.get("spot_check") is not None:
             line["spot_check"] = main_res["spot_check"]
+    if CLIENT_SHARDED in args.also:
+        failed = client_sharded_entry(args, world, rank, local, line, also) or failed
+    if rank == 0:
         if also:
             line["also"] = also
         print(json.dumps(line), flush=True)

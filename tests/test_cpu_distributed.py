@@ -104,11 +104,13 @@ def test_strong_scaling_buckets_gloo(oracle, world):
 
 def test_bench_presets_follow_baseline():
     """bench.py --config N fills K, P, the epilogue and the scaling from BASELINE.json configs[1..4]; the default run
-    (config 3) also measures configs 5 and 4 under strong scaling, explicit overrides turn that off."""
+    (config 3) also measures configs 5 and 4 under strong scaling and config 4 through the client-sharded exchange;
+    explicit overrides turn that off."""
     import bench
 
     a = bench.parse([])
-    assert (a.clients, a.params, a.epilogue, a.scaling, a.also) == (64, 10**9, "none", "weak", [5, 4])
+    assert (a.clients, a.params, a.epilogue, a.scaling, a.also) == (64, 10**9, "none", "weak", [5, 4, bench.CLIENT_SHARDED])
+    assert bench.parse(["--also", "4x,5"]).also == [bench.CLIENT_SHARDED, 5]
     assert (lambda c: (c.clients, c.params, c.epilogue, c.scaling))(bench.parse(["--config", "2"])) == \
         (8, 125_000_000, "none", "weak")
     assert (lambda c: (c.clients, c.params, c.epilogue, c.scaling))(bench.parse(["--config", "4"])) == \
