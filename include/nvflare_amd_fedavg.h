@@ -326,8 +326,8 @@ int fedavg_set_launch(fedavg_ctx* ctx, int blocks_per_cu, int unroll);
  * so one launch's blocks start as the previous launch drains;
  * bit 5 = the plain burst kernel WITHOUT its 4 LDS-held tiles per block (default: 8 tiles' results in registers
  * and 4 in LDS, 12 tiles per block per launch; with bit 5, 8);
- * bit 6 = one-block-per-CU grids (32+ clients) keep the 4-LDS-tile form (default there: 10 tiles' results in
- * LDS, all 160 KiB of the CU's LDS, 18 tiles per block per launch).
+ * bit 6 = one-block-per-CU grids (32+ clients; 64+ for the fused kernel) keep the 4-LDS-tile form (default there:
+ * 10 tiles' results in LDS, all 160 KiB of the CU's LDS, 18 tiles per block per launch; the fused kernel 9, 17).
  * Results are bit-identical in every variant. */
 int fedavg_set_variant(fedavg_ctx* ctx, int variant);
 /* Tile width used by fedavg_accumulate for contiguous rows (default 4096 elements). */

@@ -453,6 +453,15 @@ inline hipError_t launch_epi_k(const TileLaunch& L, const EpiParams& E, hipStrea
     const f32x4* ai = reinterpret_cast<const f32x4*>(L.acc_in);
     f32x4* o = reinterpret_cast<f32x4*>(L.out);
     if (!(L.variant & (kVariantTileStores | kVariantEpiPrefetch))) {  // burst: one launch per grid x TPB tiles
+        if (L.variant & kVariantWideLds)  // one block per CU: 9 more tiles with d in LDS (144 KiB)
+            return burst_launches(L.b4 / L.tile4, (L.e4 - 1) / L.tile4 + 1, L.grid, kBurstTiles + kBurstEpiLdsTilesWide,
+                                  nl, L.variant & kVariantAnyOrder, [&](int nb, int64_t t0, int64_t t_end, uint32_t flags) {
+                                      hipExtLaunchKernelGGL(
+                                          (fedavg_tiles_epi_burst_f32x4<OP, FIN, ACC_IN, EPI, kBurstTiles,
+                                                                        kBurstEpiLdsTilesWide>),
+                                          dim3(nb), dim3(kBlock), 0, s, nullptr, nullptr, flags, L.tab, L.k, L.tstride4,
+                                          ai, o, L.b4, L.e4, L.fin_val, E, t0, t_end);
+                                  });
         if (!(L.variant & kVariantRegisterTiles))  // default: 4 more tiles per block with d held in LDS
             return burst_launches(L.b4 / L.tile4, (L.e4 - 1) / L.tile4 + 1, L.grid, kBurstTiles + kBurstLdsTiles, nl,
                                   L.variant & kVariantAnyOrder, [&](int nb, int64_t t0, int64_t t_end, uint32_t flags) {

@@ -40,6 +40,7 @@ constexpr int kVariantWideLds = 64;       // inside TileLaunch: plain burst kern
 // keeps its own code (a runtime branch cost the fused Adam kernel 9 points, profiles/r03/s3/)
 constexpr int kEpiTorchSqrt = 0x100;
 constexpr int kBurstLdsTilesWide = 10;     // 10 x 16 KiB = all of a CU's LDS
+constexpr int kBurstEpiLdsTilesWide = 9;   // fused form at one block per CU: 9 x 16 KiB (+ the 512-byte sqrt table)
 constexpr int kBurstTiles = 8;             // tiles per block per burst launch (results held in registers)
 constexpr int kBurstLdsTiles = 4;          // 4 x 16 KiB of LDS per block (2 blocks fit a CU)
 
