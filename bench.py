@@ -602,15 +602,16 @@ def summarize(args, world, res, K, scaling, epilogue, label):
     }
 
 
-def client_sharded_entry(args, world, rank, local, line, also) -> bool:
-    """Run the client-sharded config-4 measurement and append its entry (rank 0).  A watchdog bounds it: if the
-    exchange has not finished after WATCHDOG_S, rank 0 prints the line measured so far (the entry marked timed
-    out) and every rank exits -- the main measurement is never lost to a stuck collective.  Returns True when its
-    spot check failed."""
+def client_sharded_entry(args, world, rank, local, line, also, state):
+    """Run the client-sharded config-4 measurement and append its entry (rank 0).  A watchdog bounds it and the
+    process teardown after it: if they have not finished after --watchdog-s, rank 0 prints the line measured so
+    far (the entry marked timed out) unless it already has, and every rank exits -- the main measurement is never
+    lost to a stuck collective or a rank that failed alone.  Returns (spot check failed, the watchdog), which the
+    caller cancels once the process group is down."""
     import threading
 
     def on_timeout():
-        if rank == 0:
+        if rank == 0 and not state.get("printed"):
             also.append({"baseline_config": PRESET_NAMES[4] + " -- client-sharded ingest", "n_gpus": world,
                          "error": f"did not finish within {args.watchdog_s:g} s (watchdog); measurement abandoned"})
             line["also"] = also
@@ -627,19 +628,17 @@ def client_sharded_entry(args, world, rank, local, line, also) -> bool:
         P = int(args.client_sharded_params) if args.client_sharded_params else p["params"]
         r = run_client_sharded(args, world, rank, local, p["clients"], P, args.seed)
     except Exception as e:  # noqa: BLE001 -- recorded in the line, the main measurement stands
-        dog.cancel()
         if rank == 0:
             also.append({"baseline_config": PRESET_NAMES[4] + " -- client-sharded ingest", "n_gpus": world,
                          "error": f"{type(e).__name__}: {e}"})
-        return False
-    dog.cancel()
+        return False, dog
     if rank == 0:
         if "skipped" in r:
             also.append({"baseline_config": PRESET_NAMES[4] + " -- client-sharded ingest", "n_gpus": world,
                          "skipped": r["skipped"]})
         else:
             also.append(summarize_client_sharded(args, world, r))
-    return bool("skipped" not in r and (r.get("spot_check") or {}).get("mismatches"))
+    return bool("skipped" not in r and (r.get("spot_check") or {}).get("mismatches")), dog
 
 
 def main(argv=None):
@@ -698,11 +697,14 @@ def main(argv=None):
         }
         if main_res.get("spot_check") is not None:
             line["spot_check"] = main_res["spot_check"]
+    state, dog = {}, None
     if CLIENT_SHARDED in args.also:
-        failed = client_sharded_entry(args, world, rank, local, line, also) or failed
+        cs_failed, dog = client_sharded_entry(args, world, rank, local, line, also, state)
+        failed = cs_failed or failed
     if rank == 0:
         if also:
             line["also"] = also
+        state["printed"] = True
         print(json.dumps(line), flush=True)
         if failed:
             print("SPOT CHECK FAILED", file=sys.stderr)
@@ -711,6 +713,8 @@ def main(argv=None):
 
         dist.barrier()
         dist.destroy_process_group()
+    if dog is not None:
+        dog.cancel()
     if failed:
         sys.exit(3)
 

@@ -1,0 +1,58 @@
+"""bench.py's client-sharded entry under its watchdog (CPU; the measurement itself is stubbed): a stuck exchange
+ends the process with the line measured so far printed once, an exception becomes an error entry, and a line
+already printed is not printed again."""
+
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+STUCK = r"""
+import sys, time
+sys.path.insert(0, {root!r})
+import bench
+bench.run_client_sharded = lambda *a, **k: time.sleep(30)
+args = bench.parse(["--also", "4x", "--watchdog-s", "0.3"])
+line, also, state = {{"metric": "m", "value": 1.0}}, [], {{"printed": {printed}}}
+bench.client_sharded_entry(args, 2, 0, 0, line, also, state)
+print("NOT REACHED")
+"""
+
+
+def _run(printed):
+    p = subprocess.run([sys.executable, "-c", STUCK.format(root=ROOT, printed=printed)], capture_output=True,
+                       text=True, timeout=60)
+    return p.returncode, [ln for ln in p.stdout.splitlines() if ln.strip()]
+
+
+def test_stuck_entry_prints_line_once_and_exits():
+    rc, out = _run(False)
+    assert rc == 0 and len(out) == 1, out
+    d = json.loads(out[0])
+    assert d["value"] == 1.0 and "watchdog" in d["also"][0]["error"]
+
+
+def test_stuck_teardown_after_print_does_not_print_again():
+    rc, out = _run(True)
+    assert rc == 0 and out == []
+
+
+def test_exception_becomes_error_entry():
+    sys.path.insert(0, ROOT)
+    import bench
+
+    def boom(*a, **k):
+        raise RuntimeError("exchange failed")
+
+    saved = bench.run_client_sharded
+    bench.run_client_sharded = boom
+    try:
+        args = bench.parse(["--also", "4x", "--watchdog-s", "30"])
+        also = []
+        failed, dog = bench.client_sharded_entry(args, 2, 0, 0, {}, also, {})
+        dog.cancel()
+    finally:
+        bench.run_client_sharded = saved
+    assert failed is False and "RuntimeError: exchange failed" in also[0]["error"]
