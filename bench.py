@@ -359,6 +359,8 @@ def run_workload(args, ctx, world, rank, K, P_spec, scaling, epilogue, baseline,
     epi_bufs = {"none": 1, "add_base": 1, "sgd": 2}.get(epilogue, 3)  # out | p+buf | p+m+v
     need = lay.slab_elems(P) * 4 + epi_bufs * end * 4
     free, total = ctx.mem_info()
+    if os.environ.get("NVFLARE_AMD_BENCH_SHARED_DEVICE") == "1":
+        free //= world  # the one-GPU rehearsal: every rank on cuda:0
     fits = need + HEADROOM <= free
     if sum_over_ranks(world, [0 if fits else 1])[0]:
         return {"skipped": f"needs {need / 1e9:.1f} GB of HBM per GPU at {world} GPU(s) "
