@@ -16,9 +16,13 @@ LIB_DIR = os.path.join(PKG, "lib")
 LIB_NAME = "libnvflare_amd_fedavg.so"
 LIB_PATH = os.path.join(LIB_DIR, LIB_NAME)
 # the fp32 tile kernels are instantiated per arithmetic mode in their own translation units so that the
-# objects compile in parallel (one hipcc per source), then link into one shared library
-SOURCES = ["fedavg_tiles_numpy.hip", "fedavg_tiles_torch.hip", "fedavg_tiles_unweighted.hip",
-           "fedavg_epi_numpy.hip", "fedavg_epi_torch.hip", "fedavg_epi_unweighted.hip",
+# objects compile in parallel (one hipcc per source), then link into one shared library; the fused kernels
+# (every optimizer kind x launch form) go further: fedavg_epi_inst.hip is compiled once per (mode,
+# finalisation), nine objects, the heaviest first in the queue
+EPI_SOURCE = "fedavg_epi_inst.hip"
+EPI_UNITS = [(f"{mode}_{fin}", op, fin_v) for mode, op in (("torch", 1), ("numpy", 0), ("unweighted", 2))
+             for fin, fin_v in (("div", 2), ("scale", 1), ("none", 0))]
+SOURCES = [EPI_SOURCE, "fedavg_tiles_numpy.hip", "fedavg_tiles_torch.hip", "fedavg_tiles_unweighted.hip",
            "fedavg_kernels.hip", "fedavg_narrow.hip", "fedavg_dequant.hip", "fedavg_capi.cpp"]
 HEADERS = ["fedavg_internal.h", "fedavg_rsqrt14.h", "fedavg_arith.h", "fedavg_tiles.h", "fedavg_epi.h"]
 OBJ_DIR = os.path.join(PKG, "lib", "obj")
@@ -58,20 +62,30 @@ def build_library(force: bool = False, verbose: bool = False, jobs: int = 0) -> 
                                                           os.path.abspath(__file__)]
     newest_header = max(os.path.getmtime(h) for h in headers)  # any header (or a flag change) rebuilds all
 
-    def compile_one(src: str) -> str:
-        obj = os.path.join(OBJ_DIR, src + ".o")
+    units = []  # (source, object, extra flags)
+    for src in SOURCES:
+        if src == EPI_SOURCE:
+            units += [(src, f"fedavg_epi_{name}.hip.o",
+                       [f"-DFEDAVG_EPI_OP={op}", f"-DFEDAVG_EPI_FIN={fin}", f"-DFEDAVG_EPI_FN=launch_epi_{name}"])
+                      for name, op, fin in EPI_UNITS]
+        else:
+            units.append((src, src + ".o", []))
+
+    def compile_one(unit) -> str:
+        src, obj_name, extra = unit
+        obj = os.path.join(OBJ_DIR, obj_name)
         if not force and os.path.exists(obj) and os.path.getmtime(obj) > max(
                 os.path.getmtime(os.path.join(CSRC, src)), newest_header):
             return obj  # up to date: only changed sources (or any header change) recompile
-        cmd = [HIPCC, *FLAGS, *inc, "-c", os.path.join(CSRC, src), "-o", obj]
+        cmd = [HIPCC, *FLAGS, *extra, *inc, "-c", os.path.join(CSRC, src), "-o", obj]
         if verbose:
             print(" ".join(cmd), flush=True)
         subprocess.run(cmd, check=True)
         return obj
 
-    jobs = jobs or min(len(SOURCES), max(1, min(16, os.cpu_count() or 1)))
+    jobs = jobs or min(len(units), max(1, min(16, os.cpu_count() or 1)))
     with ThreadPoolExecutor(max_workers=jobs) as pool:
-        objs = list(pool.map(compile_one, SOURCES))
+        objs = list(pool.map(compile_one, units))
     tmp = LIB_PATH + ".tmp"
     cmd = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-o", tmp, "-lpthread"]
     if verbose:

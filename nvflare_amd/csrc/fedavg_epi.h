@@ -527,16 +527,4 @@ inline hipError_t launch_epi_f(const TileLaunch& L, const EpiParams& E, hipStrea
     return L.acc_in ? launch_epi_a<OP, FIN, true>(L, E, s, nl) : launch_epi_a<OP, FIN, false>(L, E, s, nl);
 }
 
-template <int OP>
-inline hipError_t launch_epi_o(const TileLaunch& L, const EpiParams& E, hipStream_t s, uint64_t* nl) {
-    switch (L.fin) {
-        case FEDAVG_FIN_SCALE:
-            return launch_epi_f<OP, FEDAVG_FIN_SCALE>(L, E, s, nl);
-        case FEDAVG_FIN_DIV:
-            return launch_epi_f<OP, FEDAVG_FIN_DIV>(L, E, s, nl);
-        default:
-            return launch_epi_f<OP, FEDAVG_FIN_NONE>(L, E, s, nl);
-    }
-}
-
 }  // namespace fedavg

@@ -140,9 +140,19 @@ inline hipError_t burst_launches(int64_t t_first, int64_t t_stop, int grid, int 
 hipError_t launch_tiles_f32x4_numpy(const TileLaunch& L, hipStream_t s, uint64_t* launch_count);
 hipError_t launch_tiles_f32x4_torch(const TileLaunch& L, hipStream_t s, uint64_t* launch_count);
 hipError_t launch_tiles_f32x4_unweighted(const TileLaunch& L, hipStream_t s, uint64_t* launch_count);
-hipError_t launch_tiles_epi_f32x4_numpy(const TileLaunch& L, const EpiParams& E, hipStream_t s, uint64_t* nl);
-hipError_t launch_tiles_epi_f32x4_torch(const TileLaunch& L, const EpiParams& E, hipStream_t s, uint64_t* nl);
-hipError_t launch_tiles_epi_f32x4_unweighted(const TileLaunch& L, const EpiParams& E, hipStream_t s, uint64_t* nl);
+// fused kernels, one entry per (mode, finalisation): fedavg_epi_inst.hip compiled nine times
+#define FEDAVG_EPI_DECL(name) \
+    hipError_t name(const TileLaunch& L, const EpiParams& E, hipStream_t s, uint64_t* nl);
+FEDAVG_EPI_DECL(launch_epi_numpy_none)
+FEDAVG_EPI_DECL(launch_epi_numpy_scale)
+FEDAVG_EPI_DECL(launch_epi_numpy_div)
+FEDAVG_EPI_DECL(launch_epi_torch_none)
+FEDAVG_EPI_DECL(launch_epi_torch_scale)
+FEDAVG_EPI_DECL(launch_epi_torch_div)
+FEDAVG_EPI_DECL(launch_epi_unweighted_none)
+FEDAVG_EPI_DECL(launch_epi_unweighted_scale)
+FEDAVG_EPI_DECL(launch_epi_unweighted_div)
+#undef FEDAVG_EPI_DECL
 // whether launch_tiles_f32x4 takes the burst kernel for this geometry (it then wants one block per CU at
 // K >= kBurstOneBlockMinK clients, two below)
 bool tiles_use_burst(int64_t tile4, int unroll, int variant);

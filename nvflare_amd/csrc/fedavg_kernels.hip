@@ -289,14 +289,14 @@ hipError_t launch_tiles_f32x4(const TileLaunch& L, hipStream_t s, uint64_t* nl) 
 }
 
 hipError_t launch_tiles_epi_f32x4(const TileLaunch& L, const EpiParams& E, hipStream_t s, uint64_t* nl) {
-    switch (L.op) {
-        case FEDAVG_OP_TORCH:
-            return launch_tiles_epi_f32x4_torch(L, E, s, nl);
-        case FEDAVG_OP_UNWEIGHTED:
-            return launch_tiles_epi_f32x4_unweighted(L, E, s, nl);
-        default:
-            return launch_tiles_epi_f32x4_numpy(L, E, s, nl);
-    }
+    using Fn = hipError_t (*)(const TileLaunch&, const EpiParams&, hipStream_t, uint64_t*);
+    static constexpr Fn kFns[3][3] = {  // [mode][finalisation]: numpy (and any other op), torch, unweighted
+        {launch_epi_numpy_none, launch_epi_numpy_scale, launch_epi_numpy_div},
+        {launch_epi_torch_none, launch_epi_torch_scale, launch_epi_torch_div},
+        {launch_epi_unweighted_none, launch_epi_unweighted_scale, launch_epi_unweighted_div}};
+    const int o = L.op == FEDAVG_OP_TORCH ? 1 : (L.op == FEDAVG_OP_UNWEIGHTED ? 2 : 0);
+    const int f = L.fin == FEDAVG_FIN_SCALE ? 1 : (L.fin == FEDAVG_FIN_DIV ? 2 : 0);
+    return kFns[o][f](L, E, s, nl);
 }
 
 template <typename Tin, typename Tacc, int OP, int FIN>
