@@ -17,8 +17,10 @@ After the main measurement the default run also measures, in the same process, B
 strong scaling (``--also``; config 4 needs >= 2 GPUs: 358 GB of client updates do not fit one 288 GB HBM), and
 config 4 once more as a multi-GPU server would ingest it ("4x": client g's whole update on GPU g mod N, RCCL
 all-to-all of the buckets overlapped with the kernels, nvflare_amd/client_shards.py; serial and overlapped device
-times side by side, under a watchdog so a stuck collective cannot cost the line), and embeds them in the line's
-``also`` list -- so one N-GPU run records configs 3, 4 and 5 at that N.
+times side by side, under a watchdog so a stuck collective cannot cost the line), and config 2 once more as the
+server receives it ("2h": pageable host arrays through the drop-in helper's add / get_result, H2D and D2H included --
+north_star's PCIe-inclusive rate, each rank on its own GPU and PCIe link), and embeds them in the line's ``also``
+list -- so one N-GPU run records configs 2, 3, 4 and 5 at that N.
 
 Prints ONE JSON line (rank 0).  value = GiB/s aggregated = 4*K*P_total*steps / t / 2^30 with t the max over
 ranks of the barrier+synchronize bracketed wall time (P_total = P*N weak, P strong).  roofline.achieved uses the
@@ -57,7 +59,8 @@ PRESET_NAMES = {
     5: "BASELINE config 5: FedOpt server optimizer (Adam on aggregated deltas), 64 clients x 1B params",
 }
 CLIENT_SHARDED = 40  # --also token "4x": config 4 through the client-sharded exchange (run_client_sharded)
-WATCHDOG_S = 240.0  # the client-sharded entry's limit: a stuck collective must not cost the measured line
+HOST_RESIDENT = 20  # --also token "2h": config 2 with host-resident updates and result (run_host_resident)
+WATCHDOG_S = 240.0  # each guarded entry's limit: a stuck collective must not cost the measured line
 EPI_STATE_BYTES = {"none": 4.0, "add_base": 8.0, "sgd": 16.0}  # per param beyond the 4*K client reads; else 24
 HEADROOM = 2 << 30  # device bytes left free beside a workload (runtime, gather buffers)
 
@@ -76,11 +79,14 @@ def parse(argv=None):
     ap.add_argument("--scaling", choices=["weak", "strong"], default=None)
     ap.add_argument("--also", default="auto",
                     help="extra strong-scaling BASELINE configs measured after the main one, in the same line "
-                         "(comma list of 4 / 5 / 4x = config 4 through the client-sharded RCCL exchange; "
-                         "'auto' = 5,4,4x for the default config 3 run; 'none')")
+                         "(comma list of 4 / 5 / 4x = config 4 through the client-sharded RCCL exchange / "
+                         "2h = config 2 from host-resident updates to a host result, PCIe included; "
+                         "'auto' = 5,4,2h,4x for the default config 3 run; 'none')")
     ap.add_argument("--client-sharded-params", type=float, default=None,
                     help="model size of the 4x entry (default: config 4's 350M; smaller for one-GPU rehearsals)")
-    ap.add_argument("--watchdog-s", type=float, default=WATCHDOG_S, help="limit of the 4x entry")
+    ap.add_argument("--host-resident-params", type=float, default=None,
+                    help="params per GPU of the 2h entry (default: config 2's 125M)")
+    ap.add_argument("--watchdog-s", type=float, default=WATCHDOG_S, help="limit of the 4x and 2h entries")
     ap.add_argument("--mode", choices=["torch", "numpy"], default="torch")
     ap.add_argument("--blocks-per-cu", type=int, default=0,
                     help="0 = library default (burst kernel: 1 at >= 32 clients, else 2; fused: 1 at >= 64)")
@@ -97,9 +103,10 @@ def parse(argv=None):
                     help="HBM bytes per aggregation from a separate rocprofv3 --pmc pass (default: "
                          "profiles/pmc_traffic.json when its config matches this run)")
     ap.add_argument("--seed", type=int, default=1000)
-    ap.add_argument("--sqrt", choices=["auto", "torch_cpu", "ieee"], default="auto",
+    ap.add_argument("--sqrt", choices=["auto", "torch_cpu", "torch_cpu_sse2", "ieee"], default="auto",
                     help="sqrt of the fused optimizer step: the product default (auto: the sqrt this host's torch "
-                         "computes, nvflare_amd/torch_sqrt.py), torch CPU's restated vsSqrt, or the correctly rounded one")
+                         "computes, nvflare_amd/torch_sqrt.py), torch CPU's restated AVX-512 or SSE2 vsSqrt, or the "
+                         "correctly rounded one")
     args = ap.parse_args(argv)
     preset = PRESETS[args.config]
     if args.global_params is not None:
@@ -112,9 +119,9 @@ def parse(argv=None):
                    for f in ("--clients", "--params", "--global-params", "--scaling", "--epilogue"))
     args.preset_exact = not explicit
     if args.also == "auto":
-        args.also = "5,4,4x" if (args.config == 3 and not explicit) else "none"
-    args.also = [] if args.also in ("", "none") else [CLIENT_SHARDED if x.strip() == "4x" else int(x)
-                                                      for x in args.also.split(",")]
+        args.also = "5,4,2h,4x" if (args.config == 3 and not explicit) else "none"
+    tokens = {"4x": CLIENT_SHARDED, "2h": HOST_RESIDENT}
+    args.also = [] if args.also in ("", "none") else [tokens.get(x.strip()) or int(x) for x in args.also.split(",")]
     return args
 
 
@@ -239,16 +246,16 @@ def spot_check(args, ctx, K, P, col0, op, epilogue, bufs, n_steps, seed):
     p = orc.synth_values(seed + 7, 0, cols)
     m = np.zeros_like(p)
     v = np.zeros_like(p)
-    torch_cpu = sqrt_mode(args) == "torch_cpu"
+    sq = sqrt_mode(args)
     for s in range(1, n_steps + 1):
-        orc.epilogue_apply(d, orc.EPI_ADAM, p=p, m=m, v=v, step=float(s), torch_cpu_sqrt=torch_cpu, **ADAM_HP)
+        orc.epilogue_apply(d, orc.EPI_ADAM, p=p, m=m, v=v, step=float(s), torch_cpu_sqrt=sq, **ADAM_HP)
     mism = 0
     for buf, host in zip(bufs, (p, m, v)):
         got = ctx.gather_f32(buf.ptr, idx.astype(np.uint64))
         mism += int(np.count_nonzero(host.view(np.uint32) != got.view(np.uint32)))
     return {"sampled": int(idx.size) * 3, "mismatches": mism,
             "oracle": f"oracle/fedavg_oracle.c (aggregation + {n_steps} Adam steps; p, exp_avg, exp_avg_sq; "
-                      f"{'torch CPU' if torch_cpu else 'correctly rounded'} sqrt)"}
+                      f"{ {'torch_cpu': 'torch CPU AVX-512', 'torch_cpu_sse2': 'torch CPU SSE2'}.get(sq, 'correctly rounded')} sqrt)"}
 
 
 def cpu_baseline(args, K, P, op):
@@ -521,6 +528,95 @@ def run_client_sharded(args, world, rank, local, K, P, seed):
         torch.cuda.empty_cache()
 
 
+def run_host_resident(args, world, rank, local, K, P, seed):
+    """BASELINE config 2 as the server receives it (north_star's PCIe-inclusive rate): the K client updates are
+    pageable numpy arrays in HOST memory (what the comm layer's decoder hands over), each goes through the drop-in
+    WeightedAggregationHelper.add (weighted_aggregation_helper.py:153-224; the engine packs it through its pinned
+    ring and H2D-copies it into the tiled slab) and get_result (:226-240; kernel + D2H into a new host array).
+    One step = one round: K adds + get_result.  Weak scaling: every rank runs its own config-2 round on its own GPU
+    and PCIe link, so value = 4*K*P*N per step.  The whole result of the last step is compared with the oracle."""
+    import torch
+
+    steps, warmup = max(1, min(args.steps, 5)), max(1, min(args.warmup, 1))
+    rng = np.random.default_rng(seed + 101 * rank)
+    base = rng.standard_normal(P, dtype=np.float32)
+    clients = [base * np.float32(1.0 + 0.01 * k) for k in range(K)]  # K distinct pageable host updates
+    weights = synth_weights(K)
+    helper = make_host_helper(local)
+    t_accept, out = 0.0, None
+    try:
+        def one_round(r):
+            a0 = time.perf_counter()
+            for k in range(K):
+                helper.add({"w": clients[k]}, weights[k], f"site-{k}", r)
+            a1 = time.perf_counter()
+            res = helper.get_result()["w"]
+            return res, a1 - a0
+
+        for r in range(warmup):
+            one_round(r)
+        device_sync()
+        dist_barrier(world)
+        t0 = time.perf_counter()
+        for r in range(steps):
+            out, dt = one_round(warmup + r)
+            t_accept += dt
+        device_sync()
+        dist_barrier(world)
+        wall = max_over_ranks(world, time.perf_counter() - t0)
+        sc = None
+        if args.spot_check > 0:
+            sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+            from oracle import fedavg_oracle as orc
+
+            threads = max(1, min(16, len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else 1))
+            want = orc.fedavg_c(clients, weights, orc.MODE_NUMPY, nthreads=threads)
+            sc = [int(want.size), int(np.count_nonzero(np.asarray(out).view(np.uint32) != want.view(np.uint32)))]
+        sampled, mism = sum_over_ranks(world, sc or [0, 0])
+        return {"K": K, "P": P, "wall": wall, "steps": steps, "warmup": warmup,
+                "accept_s": max_over_ranks(world, t_accept / steps),
+                "result_type": type(out).__name__,
+                "spot_check": {"compared": sampled, "mismatches": mism, "ranks": world,
+                               "oracle": "oracle/fedavg_oracle.c (every element of the last round's result)"}
+                if sc is not None else None}
+    finally:
+        helper.reset_stats()
+        del helper, clients
+        if torch.cuda.is_available():
+            torch.cuda.empty_cache()
+
+
+def make_host_helper(local):
+    """The drop-in helper the 2h entry drives (a seam for the CPU tests' fake device)."""
+    from nvflare_amd.app_common.aggregators.weighted_aggregation_helper import WeightedAggregationHelper
+
+    return WeightedAggregationHelper(device=local)
+
+
+def device_sync():
+    import torch
+
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
+
+
+def summarize_host_resident(args, world, r):
+    step_s = r["wall"] / r["steps"]
+    exact = r["K"] == PRESETS[2]["clients"] and r["P"] == PRESETS[2]["params"]
+    return {
+        "baseline_config": (PRESET_NAMES[2] if exact else f"custom (config 2 with {r['K']} x {r['P']})")
+                           + " -- host-resident updates in, host result out (PCIe-inclusive, the drop-in helper)",
+        "value": round(4.0 * r["K"] * r["P"] * world / step_s / 2**30, 2), "unit": "GiB/s", "n_gpus": world,
+        "scaling": "weak", "steps": r["steps"], "warmup": r["warmup"], "ms_per_step": round(step_s * 1e3, 2),
+        "accept_ms_per_step": round(r["accept_s"] * 1e3, 2),
+        "h2d_GBps_per_gpu": round(4.0 * r["K"] * r["P"] / r["accept_s"] / 1e9, 2),
+        "get_result_ms": round((step_s - r["accept_s"]) * 1e3, 2),
+        "spot_check": r["spot_check"],
+        "config": {"clients": r["K"], "params_per_gpu": r["P"], "container": "numpy (pageable)", "keys": 1,
+                   "mode": "numpy", "result": r["result_type"]},
+    }
+
+
 def dist_barrier(world):
     if world > 1:
         import torch.distributed as dist
@@ -604,17 +700,22 @@ def summarize(args, world, res, K, scaling, epilogue, label):
     }
 
 
-def client_sharded_entry(args, world, rank, local, line, also, state):
-    """Run the client-sharded config-4 measurement and append its entry (rank 0).  A watchdog bounds it and the
-    process teardown after it: if they have not finished after --watchdog-s, rank 0 prints the line measured so
-    far (the entry marked timed out) unless it already has, and every rank exits -- the main measurement is never
-    lost to a stuck collective or a rank that failed alone.  Returns (spot check failed, the watchdog), which the
-    caller cancels once the process group is down."""
+def entry_name(token) -> str:
+    return (PRESET_NAMES[4] + " -- client-sharded ingest" if token == CLIENT_SHARDED
+            else PRESET_NAMES[2] + " -- host-resident")
+
+
+def guarded_entry(args, world, rank, local, line, also, state, token):
+    """Run one collective-bearing ``also`` entry (4x: client-sharded config 4; 2h: host-resident config 2) and
+    append it (rank 0).  A watchdog bounds it and whatever follows until the caller cancels it (the next entry, the
+    process-group teardown): if that has not finished after --watchdog-s, rank 0 prints the line measured so far
+    (the entry marked timed out) unless it already has, and every rank exits -- the main measurement is never lost
+    to a stuck collective or a rank that failed alone.  Returns (spot check failed, the watchdog)."""
     import threading
 
     def on_timeout():
         if rank == 0 and not state.get("printed"):
-            also.append({"baseline_config": PRESET_NAMES[4] + " -- client-sharded ingest", "n_gpus": world,
+            also.append({"baseline_config": entry_name(token), "n_gpus": world,
                          "error": f"did not finish within {args.watchdog_s:g} s (watchdog); measurement abandoned"})
             line["also"] = also
             print(json.dumps(line), flush=True)
@@ -626,21 +727,30 @@ def client_sharded_entry(args, world, rank, local, line, also, state):
     dog.daemon = True
     dog.start()
     try:
-        p = PRESETS[4]
-        P = int(args.client_sharded_params) if args.client_sharded_params else p["params"]
-        r = run_client_sharded(args, world, rank, local, p["clients"], P, args.seed)
+        if token == HOST_RESIDENT:
+            p = PRESETS[2]
+            P = int(args.host_resident_params) if args.host_resident_params else p["params"]
+            r = run_host_resident(args, world, rank, local, p["clients"], P, args.seed)
+        else:
+            p = PRESETS[4]
+            P = int(args.client_sharded_params) if args.client_sharded_params else p["params"]
+            r = run_client_sharded(args, world, rank, local, p["clients"], P, args.seed)
     except Exception as e:  # noqa: BLE001 -- recorded in the line, the main measurement stands
         if rank == 0:
-            also.append({"baseline_config": PRESET_NAMES[4] + " -- client-sharded ingest", "n_gpus": world,
-                         "error": f"{type(e).__name__}: {e}"})
+            also.append({"baseline_config": entry_name(token), "n_gpus": world, "error": f"{type(e).__name__}: {e}"})
         return False, dog
     if rank == 0:
         if "skipped" in r:
-            also.append({"baseline_config": PRESET_NAMES[4] + " -- client-sharded ingest", "n_gpus": world,
-                         "skipped": r["skipped"]})
+            also.append({"baseline_config": entry_name(token), "n_gpus": world, "skipped": r["skipped"]})
+        elif token == HOST_RESIDENT:
+            also.append(summarize_host_resident(args, world, r))
         else:
             also.append(summarize_client_sharded(args, world, r))
     return bool("skipped" not in r and (r.get("spot_check") or {}).get("mismatches")), dog
+
+
+def client_sharded_entry(args, world, rank, local, line, also, state):
+    return guarded_entry(args, world, rank, local, line, also, state, CLIENT_SHARDED)
 
 
 def main(argv=None):
@@ -662,8 +772,8 @@ def main(argv=None):
     also = []
     failed = bool((main_res.get("spot_check") or {}).get("mismatches"))  # counts summed over ranks: all agree
     for cfg in args.also:
-        if cfg == CLIENT_SHARDED:
-            continue  # last, under a watchdog (below)
+        if cfg in (CLIENT_SHARDED, HOST_RESIDENT):
+            continue  # last, each under a watchdog (below)
         p = PRESETS[cfg]
         r = run_workload(args, ctx, world, rank, p["clients"], p["params"], p["scaling"], p["epilogue"],
                          baseline=False, seed=args.seed)
@@ -700,9 +810,12 @@ def main(argv=None):
         if main_res.get("spot_check") is not None:
             line["spot_check"] = main_res["spot_check"]
     state, dog = {}, None
-    if CLIENT_SHARDED in args.also:
-        cs_failed, dog = client_sharded_entry(args, world, rank, local, line, also, state)
-        failed = cs_failed or failed
+    for token in (HOST_RESIDENT, CLIENT_SHARDED):
+        if token in args.also:
+            if dog is not None:
+                dog.cancel()
+            e_failed, dog = guarded_entry(args, world, rank, local, line, also, state, token)
+            failed = e_failed or failed
     if rank == 0:
         if also:
             line["also"] = also

@@ -28,9 +28,9 @@ extern "C" {
 
 /* Bumped whenever a struct layout or an entry point changes (v3: Rprop / ASGD fields appended to struct
  * fedavg_epilogue; v4: fedavg_launch_count; v5: fedavg_d2h_multi; v6: fedavg_accumulate_tiled16_tails and
- * integer accumulators in fedavg_accumulate; v7: fedavg_epilogue.torch_sqrt).  fedavg_struct_size() lets a binding
+ * integer accumulators in fedavg_accumulate; v7: fedavg_epilogue.torch_sqrt; v8: its FEDAVG_SQRT_* values).  fedavg_struct_size() lets a binding
  * check each struct's size as well. */
-#define FEDAVG_ABI_VERSION 7
+#define FEDAVG_ABI_VERSION 8
 
 /* element types of client rows (in_dtype) and of the running sum / result (acc_dtype) */
 enum fedavg_dtype {
@@ -94,6 +94,14 @@ enum fedavg_epi {
     FEDAVG_EPI_ASGD = 10,    /* torch ASGD on g = -d  (torch/optim/asgd.py _single_tensor_asgd) */
 };
 
+/* fedavg_epilogue.torch_sqrt (v8): the sqrt of the reference's server step, torch CPU's Tensor.sqrt on the host it runs
+ * on (nvflare_amd/torch_sqrt.py picks it by probing that host's torch) */
+enum fedavg_sqrt {
+    FEDAVG_SQRT_IEEE = 0,           /* correctly rounded */
+    FEDAVG_SQRT_TORCH_AVX512 = 1,   /* MKL vsSqrt, AVX-512 path (Intel): VRSQRT14PS estimate + one Newton step */
+    FEDAVG_SQRT_TORCH_SSE2 = 2,     /* MKL vsSqrt, SSE2 path (AMD): sqrtps refined by a truncated-reciprocal step */
+};
+
 typedef struct fedavg_epilogue {
     int kind;                   /* enum fedavg_epi */
     int first_step;             /* SGD: the momentum buffer starts as a clone of the gradient */
@@ -117,9 +125,10 @@ typedef struct fedavg_epilogue {
     double etaminus, etaplus;   /* Rprop: etas; state1 = prev, state2 = step_size (lr-filled before step 1) */
     double step_size_min, step_size_max; /* Rprop: step_sizes */
     double eta, mu, lambd;      /* ASGD: fp32 eta / mu states before this step, lambd; state1 = ax */
-    /* v7: 0 = correctly rounded sqrt; nonzero = every sqrt of the step is torch CPU's (MKL vsSqrt on AVX-512: one
-     * Newton step from the VRSQRT14PS estimate, restated exactly; see tools/sqrt_probe.c and
-     * nvflare_amd/torch_sqrt.py) */
+    /* v8: which sqrt every sqrt of the step computes -- FEDAVG_SQRT_IEEE (correctly rounded), FEDAVG_SQRT_TORCH_AVX512
+     * (torch CPU's on Intel AVX-512 hosts: MKL vsSqrt, one Newton step from the VRSQRT14PS estimate) or
+     * FEDAVG_SQRT_TORCH_SSE2 (torch CPU's where MKL takes its SSE2 path, as on AMD EPYC hosts); both restated
+     * exactly, see nvflare_amd/torch_sqrt.py.  Other values: error. */
     int torch_sqrt;
 } fedavg_epilogue;
 
@@ -340,8 +349,8 @@ int fedavg_fill_synthetic_f32(fedavg_ctx* ctx, float* dst, size_t n, size_t tile
                               uint64_t seed, uint64_t row, uint64_t col0);
 /* Gather m fp32 elements src[idx[j]] (idx: host array) into host_out (spot checks at full size). */
 int fedavg_gather_f32(fedavg_ctx* ctx, const float* src, const uint64_t* idx, size_t m, float* host_out);
-/* Test entry (v7): out[i] = the epilogues' sqrt of x[i] on the compute stream (device pointers): torch CPU's vsSqrt
- * restated (torch_sqrt nonzero, as struct fedavg_epilogue.torch_sqrt), or the correctly rounded sqrt. */
+/* Test entry (v8): out[i] = the epilogues' sqrt of x[i] on the compute stream (device pointers); torch_sqrt is a
+ * FEDAVG_SQRT_* value as in struct fedavg_epilogue. */
 int fedavg_sqrt_f32(fedavg_ctx* ctx, const float* x, float* out, size_t n, int torch_sqrt);
 
 #ifdef __cplusplus

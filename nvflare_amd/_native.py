@@ -43,7 +43,12 @@ FEDAVG_FIN_SCALE = 1
 FEDAVG_FIN_DIV = 2
 FEDAVG_FIN_RECIP = 3  # torch-ROCm div_ by a CPU scalar: multiply by the opmath reciprocal
 
-ABI_VERSION = 7  # include/nvflare_amd_fedavg.h FEDAVG_ABI_VERSION
+ABI_VERSION = 8  # include/nvflare_amd_fedavg.h FEDAVG_ABI_VERSION
+
+# fedavg_epilogue.torch_sqrt (enum fedavg_sqrt)
+FEDAVG_SQRT_IEEE = 0
+FEDAVG_SQRT_TORCH_AVX512 = 1
+FEDAVG_SQRT_TORCH_SSE2 = 2
 
 c_void_p = ctypes.c_void_p
 c_int = ctypes.c_int
@@ -236,7 +241,7 @@ class Epilogue(ctypes.Structure):
         ("eta", c_double),
         ("mu", c_double),
         ("lambd", c_double),
-        ("torch_sqrt", c_int),  # v7: torch CPU's sqrt (nvflare_amd/torch_sqrt.py) when nonzero, else IEEE
+        ("torch_sqrt", c_int),  # v8: FEDAVG_SQRT_* (nvflare_amd/torch_sqrt.py epilogue_flag)
     ]
 
 

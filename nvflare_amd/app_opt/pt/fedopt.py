@@ -112,7 +112,7 @@ class DeviceServerOptimizer:
         self.model = model
         self.optimizer = optimizer
         self.kind = self._kind(optimizer)
-        self.sqrt_mode = torch_sqrt.mode()  # "torch_cpu" | "ieee": the sqrt of the reference's step (torch_sqrt.py)
+        self.sqrt_mode = torch_sqrt.mode()  # torch_sqrt.MODES: the sqrt of the reference's step on this host
         self._bind()
 
     @staticmethod

@@ -196,4 +196,23 @@ __device__ __forceinline__ float sqrt_torch_cpu(const float x) {
     return special ? __builtin_amdgcn_sqrtf(x) : (tiny ? res * 0x1p-32f : res);
 }
 
+// torch CPU's fp32 Tensor.sqrt where MKL dispatches its SSE2 code path (mkl_vml_kernel_sSqrt_E2HAynn), as on the GPU
+// pool's AMD EPYC hosts (EpiParams.torch_sqrt == FEDAVG_SQRT_TORCH_SSE2).  The MKL kernel refines the correctly
+// rounded sqrtps with a coupled Newton step in plain fp32 -- every operation rounds, no FMA (-ffp-contract=off) --
+// from a reciprocal truncated to 12 significant bits; positive normals up to 0x7f7ff000 only, every other input
+// (zero, subnormals, the top 4095 finite values, inf, NaN, negatives) takes its scalar callout, the correctly rounded
+// sqrt.  Restated in oracle_sqrt_mkl_sse2, which equals the MKL kernel on all 2^32 inputs
+// (tools/sqrt_mkl_sse2_check.py).  Branch-free, no table: two IEEE operations (sqrt, 1/x) and eleven fp32 ops.
+__device__ __forceinline__ float sqrt_mkl_sse2(const float x) {
+    const float s0 = __builtin_sqrtf(x);
+    const float y = __uint_as_float(__float_as_uint(1.0f / s0) & 0xFFFFF800u);
+    const float s = x * y;
+    const float h = y * 0.5f;
+    const float r = 0.5f - s * h;
+    const float s1 = s * r + s;
+    const float h1 = h * r + h;
+    const float res = (x - s1 * s1) * h1 + s1;
+    return __float_as_uint(x) - 0x00800000u <= 0x7F7FF000u - 0x00800000u ? res : s0;
+}
+
 }  // namespace fedavg

@@ -29,9 +29,10 @@ struct EpiIn {
     f32x4 a, b, c, d;  // ADD_BASE: base | SGD: p, momentum buffer | ADAM: p, exp_avg, exp_avg_sq (, max_exp_avg_sq)
 };
 
-template <bool TSQ>
+template <int SQ>  // EPI & kEpiSqrtMask
 __device__ __forceinline__ float sqrt_e(const EpiParams& E, const float x) {
-    if constexpr (TSQ) return sqrt_torch_cpu(x);
+    if constexpr (SQ == kEpiTorchSqrt) return sqrt_torch_cpu(x);
+    if constexpr (SQ == kEpiTorchSqrtSse2) return sqrt_mkl_sse2(x);
     return __builtin_sqrtf(x);
 }
 
@@ -76,7 +77,7 @@ template <int EPI>
 __device__ __forceinline__ void epilogue4(const EpiParams& E, const int64_t i, const f32x4 d, const EpiIn& in,
                                           f32x4* out) {
     constexpr int KIND = EPI & 0xFF;
-    constexpr bool TSQ = (EPI & kEpiTorchSqrt) != 0;
+    constexpr int TSQ = EPI & kEpiSqrtMask;
     f32x4* p4 = reinterpret_cast<f32x4*>(E.param) + i;
     if constexpr (KIND == FEDAVG_EPI_ADD_BASE) {
         store4<true>(out + i, in.a + d);
@@ -489,6 +490,14 @@ inline hipError_t launch_epi_k(const TileLaunch& L, const EpiParams& E, hipStrea
     return hipGetLastError();
 }
 
+// the step's sqrt (EpiParams.torch_sqrt, FEDAVG_SQRT_*) as a compile-time epilogue variant
+template <int OP, int FIN, bool ACC_IN, int KIND>
+inline hipError_t sqrt_mode(const TileLaunch& L, const EpiParams& E, hipStream_t s, uint64_t* nl) {
+    if (E.torch_sqrt == FEDAVG_SQRT_TORCH_AVX512) return launch_epi_k<OP, FIN, ACC_IN, KIND | kEpiTorchSqrt>(L, E, s, nl);
+    if (E.torch_sqrt == FEDAVG_SQRT_TORCH_SSE2) return launch_epi_k<OP, FIN, ACC_IN, KIND | kEpiTorchSqrtSse2>(L, E, s, nl);
+    return launch_epi_k<OP, FIN, ACC_IN, KIND>(L, E, s, nl);
+}
+
 template <int OP, int FIN, bool ACC_IN>
 inline hipError_t launch_epi_a(const TileLaunch& L, const EpiParams& E, hipStream_t s, uint64_t* nl) {
     switch (E.kind) {
@@ -497,22 +506,17 @@ inline hipError_t launch_epi_a(const TileLaunch& L, const EpiParams& E, hipStrea
         case FEDAVG_EPI_SGD:
             return launch_epi_k<OP, FIN, ACC_IN, FEDAVG_EPI_SGD>(L, E, s, nl);
         case FEDAVG_EPI_ADAM:
-            return E.torch_sqrt ? launch_epi_k<OP, FIN, ACC_IN, FEDAVG_EPI_ADAM | kEpiTorchSqrt>(L, E, s, nl)
-                                : launch_epi_k<OP, FIN, ACC_IN, FEDAVG_EPI_ADAM>(L, E, s, nl);
+            return sqrt_mode<OP, FIN, ACC_IN, FEDAVG_EPI_ADAM>(L, E, s, nl);
         case FEDAVG_EPI_ADAGRAD:
-            return E.torch_sqrt ? launch_epi_k<OP, FIN, ACC_IN, FEDAVG_EPI_ADAGRAD | kEpiTorchSqrt>(L, E, s, nl)
-                                : launch_epi_k<OP, FIN, ACC_IN, FEDAVG_EPI_ADAGRAD>(L, E, s, nl);
+            return sqrt_mode<OP, FIN, ACC_IN, FEDAVG_EPI_ADAGRAD>(L, E, s, nl);
         case FEDAVG_EPI_RMSPROP:
-            return E.torch_sqrt ? launch_epi_k<OP, FIN, ACC_IN, FEDAVG_EPI_RMSPROP | kEpiTorchSqrt>(L, E, s, nl)
-                                : launch_epi_k<OP, FIN, ACC_IN, FEDAVG_EPI_RMSPROP>(L, E, s, nl);
+            return sqrt_mode<OP, FIN, ACC_IN, FEDAVG_EPI_RMSPROP>(L, E, s, nl);
         case FEDAVG_EPI_ADAMAX:
             return launch_epi_k<OP, FIN, ACC_IN, FEDAVG_EPI_ADAMAX>(L, E, s, nl);
         case FEDAVG_EPI_NADAM:
-            return E.torch_sqrt ? launch_epi_k<OP, FIN, ACC_IN, FEDAVG_EPI_NADAM | kEpiTorchSqrt>(L, E, s, nl)
-                                : launch_epi_k<OP, FIN, ACC_IN, FEDAVG_EPI_NADAM>(L, E, s, nl);
+            return sqrt_mode<OP, FIN, ACC_IN, FEDAVG_EPI_NADAM>(L, E, s, nl);
         case FEDAVG_EPI_RADAM:
-            return E.torch_sqrt ? launch_epi_k<OP, FIN, ACC_IN, FEDAVG_EPI_RADAM | kEpiTorchSqrt>(L, E, s, nl)
-                                : launch_epi_k<OP, FIN, ACC_IN, FEDAVG_EPI_RADAM>(L, E, s, nl);
+            return sqrt_mode<OP, FIN, ACC_IN, FEDAVG_EPI_RADAM>(L, E, s, nl);
         case FEDAVG_EPI_RPROP:
             return launch_epi_k<OP, FIN, ACC_IN, FEDAVG_EPI_RPROP>(L, E, s, nl);
         case FEDAVG_EPI_ASGD:

@@ -35,10 +35,13 @@ constexpr int kVariantWideLds = 64;       // inside TileLaunch: plain burst kern
                                            // (160 KiB, one block per CU); run_tiles sets it for one-block-per-CU grids
                                            // unless the public variant has bit 6, which keeps the 4-tile form there
                                            // (32 clients 88.4 -> 88.9 %, 64: 89.7 -> 89.9 %, profiles/r02/ab/wide_lds/)
-// epilogue template value: the optimizer kind | kEpiTorchSqrt when the step's sqrt is torch CPU's restated vsSqrt
-// (EpiParams.torch_sqrt; fedavg_arith.h sqrt_torch_cpu) -- a compile-time choice, so the correctly rounded path
-// keeps its own code (a runtime branch cost the fused Adam kernel 9 points, profiles/r03/s3/)
+// epilogue template value: the optimizer kind | kEpiTorchSqrt when the step's sqrt is torch CPU's restated AVX-512
+// vsSqrt (EpiParams.torch_sqrt == FEDAVG_SQRT_TORCH_AVX512; fedavg_arith.h sqrt_torch_cpu) | kEpiTorchSqrtSse2 for its
+// SSE2 path (FEDAVG_SQRT_TORCH_SSE2; sqrt_mkl_sse2) -- a compile-time choice, so the correctly rounded path keeps its
+// own code (a runtime branch cost the fused Adam kernel 9 points, profiles/r03/s3/)
 constexpr int kEpiTorchSqrt = 0x100;
+constexpr int kEpiTorchSqrtSse2 = 0x200;
+constexpr int kEpiSqrtMask = kEpiTorchSqrt | kEpiTorchSqrtSse2;
 constexpr int kBurstLdsTilesWide = 10;     // 10 x 16 KiB = all of a CU's LDS
 constexpr int kBurstEpiLdsTilesWide = 9;   // fused form at one block per CU: 9 x 16 KiB (+ the 512-byte sqrt table)
 constexpr int kBurstTiles = 8;             // tiles per block per burst launch (results held in registers)
@@ -98,7 +101,7 @@ struct EpiParams {
     int rectified;                                // RAdam: rho_t > 5
     float etaminus, etaplus, ss_min, ss_max;      // Rprop
     float decay, neg_eta, mu;                     // ASGD: 1 - lambd * eta, -eta, mu (averaging when != 1)
-    int torch_sqrt;                               // torch CPU's sqrt (fedavg_arith.h sqrt_torch_cpu), else IEEE
+    int torch_sqrt;                               // FEDAVG_SQRT_*: torch CPU's sqrt (AVX-512 / SSE2 path), or IEEE
 };
 
 struct DequantLaunch {

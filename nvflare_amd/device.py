@@ -447,11 +447,11 @@ class DeviceContext:
     def set_tile(self, tile: int = 0) -> None:
         N.call("fedavg_set_tile", self.handle, ctypes.c_int(tile))
 
-    def sqrt_f32(self, x_ptr: int, out_ptr: int, n: int, torch_sqrt: bool = False) -> None:
-        """out[i] = the epilogues' sqrt of x[i] (device pointers): torch CPU's restated vsSqrt when ``torch_sqrt``,
-        else the correctly rounded sqrt.  Test entry."""
+    def sqrt_f32(self, x_ptr: int, out_ptr: int, n: int, torch_sqrt=False) -> None:
+        """out[i] = the epilogues' sqrt of x[i] (device pointers).  ``torch_sqrt``: a FEDAVG_SQRT_* value, or a bool
+        (True: torch CPU's AVX-512 vsSqrt, False: the correctly rounded sqrt).  Test entry."""
         N.call("fedavg_sqrt_f32", self.handle, ctypes.c_void_p(x_ptr), ctypes.c_void_p(out_ptr), ctypes.c_size_t(n),
-               ctypes.c_int(1 if torch_sqrt else 0))
+               ctypes.c_int(int(torch_sqrt)))
 
     def gather_f32(self, src_ptr: int, idx: np.ndarray) -> np.ndarray:
         idx = np.ascontiguousarray(idx, dtype=np.uint64)

@@ -2,19 +2,24 @@
 
 The FedOpt server step (nvflare/app_opt/pt/fedopt.py:157-182) calls torch's single-tensor optimizers, whose
 ``exp_avg_sq.sqrt()`` (torch/optim/adam.py:545; NAdam, RAdam, RMSprop, Adagrad alike) is torch CPU's unary sqrt
-kernel.  torch 2.10 with MKL computes it with MKL VML vsSqrt (ATen vml.h, IMPLEMENT_VML_MKL(sqrt, Sqrt)), which
-on the AVX-512 path is NOT the correctly rounded vsqrtps: it is one Newton step from the VRSQRT14PS estimate
-(tools/sqrt_probe.c; ~0.5 % of results 1 ulp low).  The device epilogue reproduces either:
+kernel.  torch 2.10 with MKL computes it with MKL VML vsSqrt (ATen vml.h, IMPLEMENT_VML_MKL(sqrt, Sqrt)), which is
+NOT the correctly rounded sqrt, and MKL picks its code path by CPU.  The device epilogue reproduces:
 
-* ``"torch_cpu"`` -- the restated vsSqrt (fedavg_arith.h ``sqrt_torch_cpu``) with the estimate table captured where
-  the golden FedOpt fixtures were generated (``data/rsqrt14_avx512.bin``, 2 x 2^15 estimates), which the kernel
-  evaluates as 64 exact line segments (fedavg_rsqrt14.h, tools/make_rsqrt14_segments.py);
+* ``"torch_cpu"`` -- the AVX-512 path (Intel hosts; where the golden FedOpt fixtures were generated): one Newton step
+  from the VRSQRT14PS estimate (tools/sqrt_probe.c; ~0.5 % of results 1 ulp low), restated in fedavg_arith.h
+  ``sqrt_torch_cpu`` with the captured estimate table (``data/rsqrt14_avx512.bin``, 2 x 2^15 estimates) evaluated as
+  64 exact line segments (fedavg_rsqrt14.h, tools/make_rsqrt14_segments.py);
+* ``"torch_cpu_sse2"`` -- the SSE2 path MKL dispatches on AMD CPUs (the GPU pool's EPYC hosts): the correctly rounded
+  sqrtps refined by a Newton step from a truncated reciprocal in plain fp32 (~16 % of results +-1 ulp), restated in
+  fedavg_arith.h ``sqrt_mkl_sse2`` and checked equal to MKL's own kernel on all 2^32 inputs
+  (tools/sqrt_mkl_sse2_check.py);
 * ``"ieee"`` -- the correctly rounded sqrt (torch builds / CPUs whose vsSqrt rounds correctly).
 
-``mode()`` follows ``$NVFLARE_AMD_TORCH_SQRT`` (``torch_cpu`` | ``ieee`` | ``auto``, the default): ``auto`` asks this
-host's torch for the sqrt of ``data/sqrt_vectors.npz``'s probe values (8407 inputs, 6400 of them where the two
-differ) and picks the one it matches bit for bit, ``ieee`` when it matches neither (then the FedOpt parameters
-carry the documented sqrt bound)."""
+``mode()`` follows ``$NVFLARE_AMD_TORCH_SQRT`` (``torch_cpu`` | ``torch_cpu_sse2`` | ``ieee`` | ``auto``, the default):
+``auto`` asks this host's torch for the sqrt of ``data/sqrt_vectors.npz``'s probe values (11479 inputs: 6400 where
+the AVX-512 path and the correctly rounded sqrt differ, 3072 where the SSE2 path differs from both) and picks the one
+it matches bit for bit, ``ieee`` when it matches none (then the FedOpt parameters carry the documented sqrt bound,
+DESIGN.md section 8)."""
 
 from __future__ import annotations
 
@@ -27,7 +32,7 @@ import numpy as np
 DATA = os.path.join(os.path.dirname(os.path.abspath(__file__)), "data")
 TABLE_FILE = os.path.join(DATA, "rsqrt14_avx512.bin")
 VECTORS_FILE = os.path.join(DATA, "sqrt_vectors.npz")
-MODES = ("torch_cpu", "ieee")
+MODES = ("torch_cpu", "torch_cpu_sse2", "ieee")
 
 _lock = threading.RLock()
 _detected: Optional[str] = None
@@ -48,8 +53,7 @@ def table() -> np.ndarray:
 
 
 def detect() -> str:
-    """``"torch_cpu"`` if this host's torch.sqrt gives the restated vsSqrt on every probe value, ``"ieee"`` if it
-    gives the correctly rounded sqrt on every one, else ``"unmatched"``."""
+    """The mode (``MODES``) whose results this host's torch.sqrt gives on every probe value, else ``"unmatched"``."""
     global _detected
     with _lock:
         if _detected is None:
@@ -57,12 +61,7 @@ def detect() -> str:
 
             v = np.load(VECTORS_FILE, allow_pickle=False)
             got = torch.from_numpy(np.ascontiguousarray(v["x"])).sqrt().numpy().view(np.uint32)
-            if np.array_equal(got, v["torch_cpu"].view(np.uint32)):
-                _detected = "torch_cpu"
-            elif np.array_equal(got, v["ieee"].view(np.uint32)):
-                _detected = "ieee"
-            else:
-                _detected = "unmatched"
+            _detected = next((m for m in MODES if np.array_equal(got, v[m].view(np.uint32))), "unmatched")
         return _detected
 
 
@@ -72,14 +71,17 @@ def mode() -> str:
     if env in MODES:
         return env
     if env != "auto":
-        raise ValueError(f"NVFLARE_AMD_TORCH_SQRT={env!r}: expected torch_cpu, ieee or auto")
+        raise ValueError(f"NVFLARE_AMD_TORCH_SQRT={env!r}: expected torch_cpu, torch_cpu_sse2, ieee or auto")
     d = detect()
     return d if d in MODES else "ieee"
 
 
 def epilogue_flag(sqrt_mode: Optional[str] = None) -> int:
-    """``fedavg_epilogue.torch_sqrt`` for a step: 1 in ``torch_cpu`` mode, else 0 (the correctly rounded sqrt)."""
+    """``fedavg_epilogue.torch_sqrt`` (FEDAVG_SQRT_*) for a step in the given (default: this host's) mode."""
+    from nvflare_amd import _native as N
+
     m = sqrt_mode or mode()
     if m not in MODES:
         raise ValueError(f"sqrt mode {m!r}: expected one of {MODES}")
-    return int(m == "torch_cpu")
+    return {"torch_cpu": N.FEDAVG_SQRT_TORCH_AVX512, "torch_cpu_sse2": N.FEDAVG_SQRT_TORCH_SSE2,
+            "ieee": N.FEDAVG_SQRT_IEEE}[m]

@@ -127,10 +127,11 @@ void oracle_synth_fill_f32(uint64_t seed, uint64_t row, const uint64_t* cols, si
  * Rounding sequence pinned against torch 2.10 CPU (tests/test_fedopt_oracle.py):
  *   add(alpha)  fma(b, alpha, a);   lerp  |w| < .5 ? fma(w, e - s, s) : fma(w - 1, e - s, e)
  *   addcmul     fma(val * t1, t2, self);   addcdiv  self + (val * t1) / t2
- *   sqrt        IEEE (correctly rounded) when sqrt_table is NULL; with the table, torch CPU's own sqrt:
- *               MKL VML vsSqrt on the AVX-512 path (ATen vml.h IMPLEMENT_VML_MKL(sqrt, Sqrt)), which is
- *               one Newton step from the VRSQRT14PS estimate, restated in oracle_sqrt_torch_cpu below
- *               (~0.5 % of its results are 1 ulp below the correctly rounded value; tools/sqrt_probe.c).
+ *   sqrt        IEEE (correctly rounded) when sqrt_table is NULL and sqrt_sse2 is 0; with the table, torch CPU's
+ *               own sqrt: MKL VML vsSqrt on the AVX-512 path (ATen vml.h IMPLEMENT_VML_MKL(sqrt, Sqrt)), which
+ *               is one Newton step from the VRSQRT14PS estimate, restated in oracle_sqrt_torch_cpu below
+ *               (~0.5 % of its results are 1 ulp below the correctly rounded value; tools/sqrt_probe.c);
+ *               with sqrt_sse2, MKL's SSE2 path (AMD hosts), oracle_sqrt_mkl_sse2.
  * Scalars follow torch: python-float hyperparameters and bias corrections computed in fp64, cast to
  * fp32 where they meet a tensor.
  * ------------------------------------------------------------------------------------------------ */
@@ -155,6 +156,7 @@ typedef struct {
     double etaminus, etaplus, step_size_min, step_size_max; /* Rprop */
     double eta, mu, lambd;                        /* ASGD: fp32 eta / mu states before this step */
     const uint16_t* sqrt_table;                   /* NULL: IEEE sqrt; else the VRSQRT14 mantissa table */
+    int sqrt_sse2;                                /* nonzero: MKL's SSE2 vsSqrt (oracle_sqrt_mkl_sse2) */
 } oracle_epilogue;
 
 /* torch CPU's fp32 Tensor.sqrt, restated (torch 2.10 + MKL 2024.2 on AVX-512; measured bit-exact against torch
@@ -189,7 +191,44 @@ void oracle_sqrt_torch_cpu_n(const uint16_t* tab, const float* x, size_t n, floa
     for (size_t i = 0; i < n; ++i) out[i] = oracle_sqrt_torch_cpu(tab, x[i]);
 }
 
+/* torch CPU's fp32 Tensor.sqrt where MKL dispatches its SSE2 code path (mkl_vml_kernel_sSqrt_E2HAynn), as it does on
+ * the AMD EPYC hosts of the GPU pool (their torch.sqrt matched this kernel on every probe value; the AVX-512 path
+ * above is Intel-only).  The kernel refines the correctly rounded sqrtps result with a coupled Newton step in plain
+ * fp32 (SSE2: every operation rounds, no FMA), starting from a reciprocal truncated to 12 significant bits:
+ *   s0 = sqrt(x);  y = trunc12(1 / s0);  s = x * y;  h = y * 0.5;  r = 0.5 - s * h;
+ *   s1 = s * r + s;  h1 = h * r + h;  sqrt = (x - s1 * s1) * h1 + s1
+ * for positive normal x up to 0x7f7ff000; everything else (zero, subnormals, the top 4095 finite values, inf, NaN,
+ * negatives) takes the kernel's scalar callout, which returns the correctly rounded sqrt.  Checked equal to the MKL
+ * kernel itself (called from libtorch_cpu) on all 2^32 inputs, NaN payloads aside -- tools/sqrt_mkl_sse2_check.py. */
+float oracle_sqrt_mkl_sse2(float x) {
+    uint32_t b;
+    memcpy(&b, &x, 4);
+    if (b < 0x00800000u || b > 0x7F7FF000u) return sqrtf(x);
+    const float s0 = sqrtf(x);
+    float y = 1.0f / s0;
+    uint32_t yb;
+    memcpy(&yb, &y, 4);
+    yb &= 0xFFFFF800u;
+    memcpy(&y, &yb, 4);
+    const float s = x * y;
+    const float h = y * 0.5f;
+    const float t = s * h;
+    const float r = 0.5f - t;
+    const float sr = s * r, hr = h * r;
+    const float s1 = sr + s;
+    const float h1 = hr + h;
+    const float q = s1 * s1;
+    const float d = x - q;
+    const float dh = d * h1;
+    return dh + s1;
+}
+
+void oracle_sqrt_mkl_sse2_n(const float* x, size_t n, float* out) {
+    for (size_t i = 0; i < n; ++i) out[i] = oracle_sqrt_mkl_sse2(x[i]);
+}
+
 static inline float sqrt_e(const oracle_epilogue* epi, float x) {
+    if (epi->sqrt_sse2) return oracle_sqrt_mkl_sse2(x);
     return epi->sqrt_table ? oracle_sqrt_torch_cpu(epi->sqrt_table, x) : sqrtf(x);
 }
 

@@ -328,6 +328,7 @@ class _Epi(ctypes.Structure):
         ("mu", ctypes.c_double),
         ("lambd", ctypes.c_double),
         ("sqrt_table", ctypes.c_void_p),
+        ("sqrt_sse2", ctypes.c_int),
     ]
 
 
@@ -362,10 +363,26 @@ def sqrt_torch_cpu(x) -> np.ndarray:
     return out
 
 
+def sqrt_torch_cpu_sse2(x) -> np.ndarray:
+    """torch CPU's fp32 sqrt where MKL takes its SSE2 path (AMD hosts; oracle_sqrt_mkl_sse2), elementwise."""
+    lib = load()
+    fn = lib.oracle_sqrt_mkl_sse2_n
+    fn.restype = None
+    fn.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]
+    x = np.ascontiguousarray(x, dtype=np.float32)
+    out = np.empty_like(x)
+    fn(x.ctypes.data, x.size, out.ctypes.data)
+    return out
+
+
+SQRT_FUNCS = {"torch_cpu": sqrt_torch_cpu, "torch_cpu_sse2": sqrt_torch_cpu_sse2, "ieee": np.sqrt}
+
+
 def epilogue_apply(delta, kind, p=None, m=None, v=None, base=None, vmax=None, torch_cpu_sqrt=False, **hp):
     """Apply an epilogue to the aggregated update `delta` (fp32).  p/m/v (and vmax with amsgrad=1) are
     updated IN PLACE (copies are the caller's business); returns `out` for NONE/ADD_BASE and p otherwise.
-    ``torch_cpu_sqrt``: torch CPU's sqrt (oracle_sqrt_torch_cpu) instead of the correctly rounded one."""
+    ``torch_cpu_sqrt``: which sqrt -- False / "ieee" the correctly rounded one, True / "torch_cpu" torch CPU's
+    AVX-512 vsSqrt (oracle_sqrt_torch_cpu), "torch_cpu_sse2" its SSE2 path (oracle_sqrt_mkl_sse2)."""
     lib = load()
     fn = lib.oracle_epilogue_apply
     fn.restype = None
@@ -375,8 +392,12 @@ def epilogue_apply(delta, kind, p=None, m=None, v=None, base=None, vmax=None, to
     e.kind = kind
     for k, val in hp.items():
         setattr(e, k, val)
-    if torch_cpu_sqrt:
+    if torch_cpu_sqrt not in (False, True, "ieee", "torch_cpu", "torch_cpu_sse2"):
+        raise ValueError(f"torch_cpu_sqrt={torch_cpu_sqrt!r}")
+    if torch_cpu_sqrt is True or torch_cpu_sqrt == "torch_cpu":
         e.sqrt_table = sqrt_table().ctypes.data
+    elif torch_cpu_sqrt == "torch_cpu_sse2":
+        e.sqrt_sse2 = 1
     out = np.empty_like(delta)
 
     def ptr(a):

@@ -56,3 +56,31 @@ def test_exception_becomes_error_entry():
     finally:
         bench.run_client_sharded = saved
     assert failed is False and "RuntimeError: exchange failed" in also[0]["error"]
+
+
+def test_host_resident_entry_on_fake_device(monkeypatch):
+    """The 2h entry (config 2 from pageable host arrays to a host result through the drop-in helper) on the fake
+    device: every element of the result is compared with the oracle, and the summary carries the PCIe-inclusive
+    fields."""
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import bench
+    from fake_device import fake_engine
+
+    from nvflare_amd.app_common.aggregators.weighted_aggregation_helper import WeightedAggregationHelper
+
+    def helper(local):
+        h = WeightedAggregationHelper(device=local)
+        h._engine = fake_engine()
+        return h
+
+    monkeypatch.setattr(bench, "make_host_helper", helper)
+    args = bench.parse(["--also", "2h", "--host-resident-params", "10001", "--steps", "2", "--warmup", "1"])
+    also = []
+    failed, dog = bench.guarded_entry(args, 1, 0, 0, {}, also, {}, bench.HOST_RESIDENT)
+    dog.cancel()
+    e = also[0]
+    assert failed is False, e
+    assert e["spot_check"]["compared"] == 10001 and e["spot_check"]["mismatches"] == 0
+    assert e["steps"] == 2 and e["config"]["clients"] == 8 and e["value"] > 0
+    assert "host-resident" in e["baseline_config"] and "custom" in e["baseline_config"]

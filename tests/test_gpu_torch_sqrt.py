@@ -1,12 +1,14 @@
-"""The device epilogues' torch-CPU sqrt (fedavg_arith.h sqrt_torch_cpu; nvflare_amd/torch_sqrt.py) on the GPU.
+"""The device epilogues' torch-CPU sqrt (fedavg_arith.h sqrt_torch_cpu / sqrt_mkl_sse2; nvflare_amd/torch_sqrt.py) on
+the GPU, both restated MKL vsSqrt paths: AVX-512 (Intel hosts) and SSE2 (AMD hosts, e.g. this pool's).
 
-* elementwise (fedavg_sqrt_f32), against the oracle's restatement (oracle_sqrt_torch_cpu, itself pinned against
-  torch CPU by tests/test_torch_sqrt.py) over every mantissa of [1, 4), every subnormal and 1 in 61 of every
-  other binade (tools/sqrt_probe.py's set, 59.8 M values) -- and against this host's torch.sqrt when
-  torch_sqrt.detect() finds the restated vsSqrt here;
+* elementwise (fedavg_sqrt_f32), against the oracle's restatements (oracle_sqrt_torch_cpu, pinned against torch CPU
+  by tests/test_torch_sqrt.py; oracle_sqrt_mkl_sse2, pinned against MKL's SSE2 kernel by
+  tests/test_torch_sqrt_sse2.py) over every mantissa of [1, 4), every subnormal and 1 in 61 of every other binade
+  (tools/sqrt_probe.py's set, 59.8 M values) -- and against this host's torch.sqrt for whichever path
+  torch_sqrt.detect() finds here;
 * inside every epilogue that takes a sqrt (Adam, AdamW + amsgrad, Adagrad, RMSprop centered + momentum, NAdam,
   RAdam), kernel against oracle with the same sqrt, several rounds, bit-exact;
-* the restated and the correctly rounded sqrt really differ (the mode switch reaches the kernel)."""
+* the three sqrt modes really differ (the mode switch reaches the kernel)."""
 
 import os
 import sys
@@ -57,16 +59,21 @@ def test_device_sqrt_matches_restatement_everywhere(ctx, oracle):
     from nvflare_amd import torch_sqrt
 
     x = _probe_set()
-    got = _device_sqrt(ctx, x, True)
+    got = _device_sqrt(ctx, x, 1)
     exp = oracle.sqrt_torch_cpu(x)
     assert _same(got, exp) == 0
-    ieee = _device_sqrt(ctx, x, False)
+    sse2 = _device_sqrt(ctx, x, 2)
+    with np.errstate(invalid="ignore"):
+        assert _same(sse2, oracle.sqrt_torch_cpu_sse2(x)) == 0
+    ieee = _device_sqrt(ctx, x, 0)
     with np.errstate(invalid="ignore"):
         assert _same(ieee, np.sqrt(x)) == 0
-    assert _same(got, ieee) > 300_000  # the two sqrt modes are different functions
-    if torch_sqrt.detect() == "torch_cpu":  # this host's torch computes the restated vsSqrt: compare with it too
+    assert _same(got, ieee) > 300_000  # the three sqrt modes are different functions
+    assert _same(sse2, ieee) > 3_000_000 and _same(sse2, got) > 3_000_000
+    here = torch_sqrt.detect()
+    if here in ("torch_cpu", "torch_cpu_sse2"):  # this host's torch computes one of them: compare with it too
         with np.errstate(invalid="ignore"):
-            assert _same(got, torch.from_numpy(x.copy()).sqrt().numpy()) == 0
+            assert _same(got if here == "torch_cpu" else sse2, torch.from_numpy(x.copy()).sqrt().numpy()) == 0
 
 
 class _Dev:
@@ -109,9 +116,10 @@ KINDS = [
 ]
 
 
+@pytest.mark.parametrize("sqrt", ["torch_cpu", "torch_cpu_sse2"])
 @pytest.mark.parametrize("K", [5, 70])
 @pytest.mark.parametrize("name,hp", KINDS, ids=[k for k, _ in KINDS])
-def test_epilogues_with_torch_cpu_sqrt(ctx, oracle, name, hp, K):
+def test_epilogues_with_torch_cpu_sqrt(ctx, oracle, name, hp, K, sqrt):
     from nvflare_amd import _native as N
 
     kind = {"adam": oracle.EPI_ADAM, "adamw_amsgrad": oracle.EPI_ADAM, "adagrad": oracle.EPI_ADAGRAD,
@@ -136,14 +144,15 @@ def test_epilogues_with_torch_cpu_sqrt(ctx, oracle, name, hp, K):
         e.kind = kind
         for k_, val in hp.items():
             setattr(e, k_, val)
-        e.step, e.mu_product, e.torch_sqrt = float(step), mp, 1
+        e.step, e.mu_product = float(step), mp
+        e.torch_sqrt = {"torch_cpu": N.FEDAVG_SQRT_TORCH_AVX512, "torch_cpu_sse2": N.FEDAVG_SQRT_TORCH_SSE2}[sqrt]
         e.param, e.state1 = dev.buf("p", dev_p), dev.buf("m", dev_m)
         e.state2, e.state3 = dev.buf("v", dev_v), dev.buf("x3", dev_3)
         ctx.accumulate_tiled_epi(dev.bases, ws, 4096, dev.lay.tile_stride, 0, dev.n4, None, N.FEDAVG_OP_TORCH,
                                  N.FEDAVG_FIN_DIV, count, e)
         dev_p, dev_m, dev_v, dev_3 = dev.get("p"), dev.get("m"), dev.get("v"), dev.get("x3")
         dev.close()
-        oracle.epilogue_apply(d, kind, p=p, m=m, v=v, vmax=x3, step=float(step), mu_product=mp, torch_cpu_sqrt=True, **hp)
+        oracle.epilogue_apply(d, kind, p=p, m=m, v=v, vmax=x3, step=float(step), mu_product=mp, torch_cpu_sqrt=sqrt, **hp)
         for nm, a, b in (("p", dev_p, p), ("m", dev_m, m), ("v", dev_v, v), ("x3", dev_3, x3)):
             assert same_bits(a, b), (name, step, nm, int(np.count_nonzero(a.view(np.uint32) != b.view(np.uint32))))
         if kind == oracle.EPI_NADAM:

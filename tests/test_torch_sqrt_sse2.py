@@ -1,0 +1,160 @@
+"""torch CPU's fp32 sqrt on AMD hosts, restated (oracle_sqrt_mkl_sse2; the device epilogue's sqrt_mkl_sse2) -- CPU tests.
+
+On AMD CPUs (the GPU pool's EPYC hosts) MKL runs vsSqrt's SSE2 kernel, mkl_vml_kernel_sSqrt_E2HAynn, instead of the
+AVX-512 one the Intel container uses: torch.sqrt on the box matched it on every probe value recorded there
+(profiles/r03/s5/sqrt_probe_box.json).  The kernel ships inside the libtorch_cpu this torch loads, so it is called
+directly here, on any x86-64 host, and pins the restatement: every mantissa of several binades and a stride-61
+sample of all 2^32 bit patterns (tools/sqrt_mkl_sse2_check.py ran all 2^32: 0 mismatches).  Whole torch optimizer
+runs with torch's sqrt swapped for that kernel then check that the oracle's "torch_cpu_sse2" epilogues reproduce
+torch's single-tensor Adam / AdamW / amsgrad / NAdam / RAdam / Adagrad / RMSprop bit for bit with that sqrt."""
+
+import ctypes
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from golden_util import same_bits
+from nvflare_amd import torch_sqrt
+
+
+def _kernel():
+    try:
+        lib = ctypes.CDLL(os.path.join(os.path.dirname(torch.__file__), "lib", "libtorch_cpu.so"))
+        fn = lib.mkl_vml_kernel_sSqrt_E2HAynn
+    except (OSError, AttributeError):
+        return None
+    fn.restype = None
+    fn.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
+    return fn
+
+
+KERNEL = _kernel()
+pytestmark = pytest.mark.skipif(KERNEL is None, reason="this torch build has no MKL SSE2 vsSqrt kernel")
+
+
+def mkl_sse2(x: np.ndarray) -> np.ndarray:
+    x = np.ascontiguousarray(x, dtype=np.float32)
+    out = np.empty_like(x)
+    for i in range(0, x.size, 1 << 30):
+        n = min(1 << 30, x.size - i)
+        KERNEL(n, x[i:].ctypes.data, out[i:].ctypes.data)
+    return out
+
+
+def _same_nan(a, b):
+    return np.count_nonzero(~((a.view(np.uint32) == b.view(np.uint32)) | (np.isnan(a) & np.isnan(b))))
+
+
+@pytest.mark.parametrize("exp", [-127, -126, -100, -96, -30, -20, 0, 1, 77, 126, 127])
+def test_every_mantissa_of_a_binade(oracle, exp):
+    bits = np.arange(1 << 23, dtype=np.uint32)
+    bits = bits | np.uint32((exp + 127) << 23) if exp > -127 else bits
+    x = bits.view(np.float32)
+    got, ref = oracle.sqrt_torch_cpu_sse2(x), mkl_sse2(x)
+    assert same_bits(got, ref), int(np.count_nonzero(got.view(np.uint32) != ref.view(np.uint32)))
+    if exp in (0, 1):  # a different function from the correctly rounded sqrt and from the AVX-512 path
+        assert np.count_nonzero(ref.view(np.uint32) != np.sqrt(x).view(np.uint32)) > 500_000
+        assert np.count_nonzero(ref.view(np.uint32) != oracle.sqrt_torch_cpu(x).view(np.uint32)) > 500_000
+
+
+def test_all_bit_patterns_sampled(oracle):
+    bits = np.arange(0, 1 << 32, 61, dtype=np.uint64).astype(np.uint32)
+    x = bits.view(np.float32)
+    with np.errstate(invalid="ignore"):
+        assert _same_nan(oracle.sqrt_torch_cpu_sse2(x), mkl_sse2(x)) == 0
+
+
+def test_specials_and_callout_edges(oracle):
+    edge = np.array([0, 0x80000000, 1, 0x007FFFFF, 0x00800000, 0x7F7FF000, 0x7F7FF001, 0x7F7FFFFF, 0x7F800000,
+                     0xFF800000, 0x7FC00000, 0xBF800000, 0x3F800000, 0x40800000, 0x3E800000], np.uint32)
+    x = edge.view(np.float32)
+    with np.errstate(invalid="ignore"):
+        assert _same_nan(oracle.sqrt_torch_cpu_sse2(x), mkl_sse2(x)) == 0
+
+
+def test_probe_vectors_and_detection(oracle):
+    v = np.load(torch_sqrt.VECTORS_FILE, allow_pickle=False)
+    assert same_bits(oracle.sqrt_torch_cpu_sse2(v["x"]), v["torch_cpu_sse2"])
+    assert same_bits(mkl_sse2(v["x"]), v["torch_cpu_sse2"])
+    for other in ("torch_cpu", "ieee"):  # each mode is told apart from the others by thousands of probe values
+        assert np.count_nonzero(v["torch_cpu_sse2"].view(np.uint32) != v[other].view(np.uint32)) >= 3000
+    assert torch_sqrt.detect() in torch_sqrt.MODES + ("unmatched",)
+    assert torch_sqrt.epilogue_flag("torch_cpu_sse2") == 2 and torch_sqrt.epilogue_flag("torch_cpu") == 1
+    assert torch_sqrt.epilogue_flag("ieee") == 0
+
+
+@pytest.fixture
+def sse2_torch(monkeypatch):
+    """torch's CPU sqrt replaced by MKL's SSE2 kernel (what torch computes on an AMD host)."""
+
+    def sq(t, *a, **k):
+        return torch.from_numpy(mkl_sse2(t.detach().contiguous().numpy()).reshape(t.shape))
+
+    def sq_(t):
+        t.copy_(sq(t))
+        return t
+
+    monkeypatch.setattr(torch.Tensor, "sqrt", sq)
+    monkeypatch.setattr(torch.Tensor, "sqrt_", sq_)
+    monkeypatch.setattr(torch, "sqrt", sq)
+
+
+def _torch_steps(opt_cls, kw, p0, deltas):
+    p = torch.nn.Parameter(torch.from_numpy(p0.copy()))
+    opt = opt_cls([p], foreach=False, **kw)
+    for d in deltas:
+        opt.zero_grad()
+        p.grad = torch.tensor(-1.0 * d)  # fedopt.py:175
+        opt.step()
+    return p.detach().numpy().copy(), opt.state[p]
+
+
+@pytest.mark.parametrize("name,kw", [
+    ("Adam", dict(lr=1e-3)),
+    ("Adam", dict(lr=1e-3, amsgrad=True)),
+    ("AdamW", dict(lr=1e-3, weight_decay=1e-2)),
+    ("NAdam", dict(lr=2e-3)),
+    ("RAdam", dict(lr=1e-3)),
+    ("Adagrad", dict(lr=0.1, lr_decay=0.05, eps=1e-8)),
+    ("RMSprop", dict(lr=1e-3, centered=True, momentum=0.5)),
+])
+def test_optimizer_steps_bit_exact_with_sse2_sqrt(oracle, sse2_torch, name, kw):
+    from test_fedopt_oracle import nadam_mu_product
+
+    rng = np.random.default_rng(21)
+    n = 100_003
+    p0 = rng.standard_normal(n).astype(np.float32)
+    deltas = [(rng.standard_normal(n) * 0.01 * (0.05 if k == 2 else 1.0)).astype(np.float32) for k in range(7)]
+    tp, st = _torch_steps(getattr(torch.optim, name), kw, p0, deltas)
+    p, m, v, x3 = p0.copy(), np.zeros(n, np.float32), np.zeros(n, np.float32), np.zeros(n, np.float32)
+    b1, b2 = kw.get("betas", (0.9, 0.999))
+    mp = np.float32(1.0)
+    for k, d in enumerate(deltas):
+        common = dict(step=float(k + 1), torch_cpu_sqrt="torch_cpu_sse2", lr=kw["lr"])
+        if name in ("Adam", "AdamW"):
+            oracle.epilogue_apply(d, oracle.EPI_ADAM, p=p, m=m, v=v, vmax=x3, beta1=b1, beta2=b2, eps=1e-8,
+                                  weight_decay=kw.get("weight_decay", 0.0), decoupled_weight_decay=int(name == "AdamW"),
+                                  amsgrad=int(bool(kw.get("amsgrad"))), **common)
+        elif name in ("NAdam", "RAdam"):
+            oracle.epilogue_apply(d, oracle.EPI_NADAM if name == "NAdam" else oracle.EPI_RADAM, p=p, m=m, v=v,
+                                  beta1=b1, beta2=b2, eps=1e-8, momentum_decay=4e-3, mu_product=float(mp), **common)
+            mp = nadam_mu_product(mp, b1, 4e-3, k + 1)
+        elif name == "Adagrad":
+            oracle.epilogue_apply(d, oracle.EPI_ADAGRAD, p=p, m=m, lr_decay=kw["lr_decay"], eps=kw["eps"], **common)
+        else:
+            oracle.epilogue_apply(d, oracle.EPI_RMSPROP, p=p, m=m, v=v, vmax=x3, alpha=0.99, eps=1e-8,
+                                  momentum=kw["momentum"], centered=1, **common)
+    assert same_bits(p, tp), int(np.count_nonzero(p.view(np.uint32) != tp.view(np.uint32)))
+    state = {"Adagrad": "sum", "RMSprop": "square_avg"}.get(name, "exp_avg")
+    assert same_bits(m, st[state].numpy())
+    # with the other sqrt modes the same run differs (the swap reached torch's optimizer)
+    p2, m2, v2, x32 = p0.copy(), np.zeros(n, np.float32), np.zeros(n, np.float32), np.zeros(n, np.float32)
+    if name in ("Adam", "AdamW"):
+        for k, d in enumerate(deltas):
+            oracle.epilogue_apply(d, oracle.EPI_ADAM, p=p2, m=m2, v=v2, vmax=x32, beta1=b1, beta2=b2, eps=1e-8,
+                                  weight_decay=kw.get("weight_decay", 0.0), decoupled_weight_decay=int(name == "AdamW"),
+                                  amsgrad=int(bool(kw.get("amsgrad"))), step=float(k + 1), lr=kw["lr"],
+                                  torch_cpu_sqrt="ieee")
+        assert not same_bits(p2, tp)
