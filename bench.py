@@ -103,9 +103,9 @@ def parse(argv=None):
                     help="HBM bytes per aggregation from a separate rocprofv3 --pmc pass (default: "
                          "profiles/pmc_traffic.json when its config matches this run)")
     ap.add_argument("--seed", type=int, default=1000)
-    ap.add_argument("--sqrt", choices=["auto", "torch_cpu", "torch_cpu_sse2", "ieee"], default="auto",
+    ap.add_argument("--sqrt", choices=["auto", "torch_cpu", "torch_cpu_amd", "ieee"], default="auto",
                     help="sqrt of the fused optimizer step: the product default (auto: the sqrt this host's torch "
-                         "computes, nvflare_amd/torch_sqrt.py), torch CPU's restated AVX-512 or SSE2 vsSqrt, or the "
+                         "computes, nvflare_amd/torch_sqrt.py), torch CPU's restated vsSqrt of the Intel or the AMD hosts, or the "
                          "correctly rounded one")
     args = ap.parse_args(argv)
     preset = PRESETS[args.config]
@@ -255,7 +255,7 @@ def spot_check(args, ctx, K, P, col0, op, epilogue, bufs, n_steps, seed):
         mism += int(np.count_nonzero(host.view(np.uint32) != got.view(np.uint32)))
     return {"sampled": int(idx.size) * 3, "mismatches": mism,
             "oracle": f"oracle/fedavg_oracle.c (aggregation + {n_steps} Adam steps; p, exp_avg, exp_avg_sq; "
-                      f"{ {'torch_cpu': 'torch CPU AVX-512', 'torch_cpu_sse2': 'torch CPU SSE2'}.get(sq, 'correctly rounded')} sqrt)"}
+                      f"{ {'torch_cpu': 'torch CPU (Intel host)', 'torch_cpu_amd': 'torch CPU (AMD host)'}.get(sq, 'correctly rounded')} sqrt)"}
 
 
 def cpu_baseline(args, K, P, op):

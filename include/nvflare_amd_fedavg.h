@@ -99,7 +99,7 @@ enum fedavg_epi {
 enum fedavg_sqrt {
     FEDAVG_SQRT_IEEE = 0,           /* correctly rounded */
     FEDAVG_SQRT_TORCH_AVX512 = 1,   /* MKL vsSqrt, AVX-512 path (Intel): VRSQRT14PS estimate + one Newton step */
-    FEDAVG_SQRT_TORCH_SSE2 = 2,     /* MKL vsSqrt, SSE2 path (AMD): sqrtps refined by a truncated-reciprocal step */
+    FEDAVG_SQRT_TORCH_AMD = 2,      /* MKL vsSqrt, SSE4.2 / AVX path (AMD EPYC): the host's RSQRTPS + a Newton step */
 };
 
 typedef struct fedavg_epilogue {
@@ -127,8 +127,8 @@ typedef struct fedavg_epilogue {
     double eta, mu, lambd;      /* ASGD: fp32 eta / mu states before this step, lambd; state1 = ax */
     /* v8: which sqrt every sqrt of the step computes -- FEDAVG_SQRT_IEEE (correctly rounded), FEDAVG_SQRT_TORCH_AVX512
      * (torch CPU's on Intel AVX-512 hosts: MKL vsSqrt, one Newton step from the VRSQRT14PS estimate) or
-     * FEDAVG_SQRT_TORCH_SSE2 (torch CPU's where MKL takes its SSE2 path, as on AMD EPYC hosts); both restated
-     * exactly, see nvflare_amd/torch_sqrt.py.  Other values: error. */
+     * FEDAVG_SQRT_TORCH_AMD (torch CPU's on AMD EPYC hosts: MKL's SSE4.2 / AVX kernel, a Newton step from that CPU's
+     * RSQRTPS estimate); both restated exactly, see nvflare_amd/torch_sqrt.py.  Other values: error. */
     int torch_sqrt;
 } fedavg_epilogue;
 

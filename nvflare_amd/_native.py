@@ -48,7 +48,7 @@ ABI_VERSION = 8  # include/nvflare_amd_fedavg.h FEDAVG_ABI_VERSION
 # fedavg_epilogue.torch_sqrt (enum fedavg_sqrt)
 FEDAVG_SQRT_IEEE = 0
 FEDAVG_SQRT_TORCH_AVX512 = 1
-FEDAVG_SQRT_TORCH_SSE2 = 2
+FEDAVG_SQRT_TORCH_AMD = 2
 
 c_void_p = ctypes.c_void_p
 c_int = ctypes.c_int

@@ -8,6 +8,7 @@
 
 #include "fedavg_internal.h"
 #include "fedavg_rsqrt14.h"
+#include "fedavg_rsqrtps_amd.h"
 
 namespace fedavg {
 
@@ -196,23 +197,42 @@ __device__ __forceinline__ float sqrt_torch_cpu(const float x) {
     return special ? __builtin_amdgcn_sqrtf(x) : (tiny ? res * 0x1p-32f : res);
 }
 
-// torch CPU's fp32 Tensor.sqrt where MKL dispatches its SSE2 code path (mkl_vml_kernel_sSqrt_E2HAynn), as on the GPU
-// pool's AMD EPYC hosts (EpiParams.torch_sqrt == FEDAVG_SQRT_TORCH_SSE2).  The MKL kernel refines the correctly
-// rounded sqrtps with a coupled Newton step in plain fp32 -- every operation rounds, no FMA (-ffp-contract=off) --
-// from a reciprocal truncated to 12 significant bits; positive normals up to 0x7f7ff000 only, every other input
-// (zero, subnormals, the top 4095 finite values, inf, NaN, negatives) takes its scalar callout, the correctly rounded
-// sqrt.  Restated in oracle_sqrt_mkl_sse2, which equals the MKL kernel on all 2^32 inputs
-// (tools/sqrt_mkl_sse2_check.py).  Branch-free, no table: two IEEE operations (sqrt, 1/x) and eleven fp32 ops.
-__device__ __forceinline__ float sqrt_mkl_sse2(const float x) {
-    const float s0 = __builtin_sqrtf(x);
-    const float y = __uint_as_float(__float_as_uint(1.0f / s0) & 0xFFFFF800u);
+// torch CPU's fp32 Tensor.sqrt on the GPU pool's AMD EPYC hosts (EpiParams.torch_sqrt == FEDAVG_SQRT_TORCH_AMD): MKL
+// runs vsSqrt's SSE4.2 / AVX kernel there (mkl_vml_kernel_sSqrt_EXHAynn, equal to torch.sqrt on all 59.8 M probe
+// inputs on the box, tools/sqrt_box_kernels.py), which starts a coupled Newton step in plain fp32 -- every operation
+// rounds, no FMA (-ffp-contract=off) -- from the RSQRTPS estimate:
+//     y = rsqrtps(x);  s = x * y;  h = y * 0.5;  r = 0.5 - s * h;  s1 = s * r + s;  h1 = h * r + h;
+//     sqrt = (x - s1 * s1) * h1 + s1
+// on positive normals up to 0x7f7ff000; every other input takes the kernel's correctly rounded scalar callout.
+// RSQRTPS is vendor-specific: the host CPU's estimates (12 bits, a function of the exponent parity and the top 12
+// mantissa bits) are the 8192-entry table fedavg_rsqrtps_amd.h, staged in LDS once per block (rsqrtps_stage, 16 KiB);
+// each sqrt reads one 16-bit entry.  Restated in oracle_sqrt_mkl_rsqrtps: with this container's RSQRTPS it equals
+// MKL's EX kernel on all 2^32 inputs, with the AMD table the box's torch.sqrt on every fp32 in [1, 4)
+// (tools/sqrt_mkl_sse_check.py).
+__shared__ uint32_t g_rsqrtps_lds[4096];  // kRsqrtpsAmd: two 12-bit estimates per word
+
+// every kernel that computes sqrt_mkl_rsqrtps calls this first, with the whole block (one barrier)
+__device__ __forceinline__ void rsqrtps_stage() {
+    const uint4* src = reinterpret_cast<const uint4*>(kRsqrtpsAmd);
+    uint4* dst = reinterpret_cast<uint4*>(g_rsqrtps_lds);
+    for (int i = threadIdx.x; i < 1024; i += kBlock) dst[i] = src[i];
+    __syncthreads();
+}
+
+__device__ __forceinline__ float sqrt_mkl_rsqrtps(const float x) {
+    const uint32_t b = __float_as_uint(x);
+    const int e = (int)((b >> 23) & 0xFFu) - 127;
+    const int p = e & 1;
+    const int k = (e - p) / 2;
+    const uint32_t t = reinterpret_cast<const uint16_t*>(g_rsqrtps_lds)[((uint32_t)p << 12) | ((b & 0x7FFFFFu) >> 11)];
+    const float y = __uint_as_float((0x3F000000u | (t << 11)) - (uint32_t)(k * 8388608));
     const float s = x * y;
     const float h = y * 0.5f;
     const float r = 0.5f - s * h;
     const float s1 = s * r + s;
     const float h1 = h * r + h;
     const float res = (x - s1 * s1) * h1 + s1;
-    return __float_as_uint(x) - 0x00800000u <= 0x7F7FF000u - 0x00800000u ? res : s0;
+    return b - 0x00800000u <= 0x7F7FF000u - 0x00800000u ? res : __builtin_sqrtf(x);
 }
 
 }  // namespace fedavg

@@ -431,8 +431,8 @@ fedavg::EpiParams make_epi(const fedavg_epilogue& e) {
     E.base = e.base;
     E.amsgrad = e.kind == FEDAVG_EPI_ADAM && e.amsgrad;
     E.state3 = e.state3;
-    if (e.torch_sqrt != FEDAVG_SQRT_IEEE && e.torch_sqrt != FEDAVG_SQRT_TORCH_AVX512 && e.torch_sqrt != FEDAVG_SQRT_TORCH_SSE2)
-        throw Error("epilogue torch_sqrt must be FEDAVG_SQRT_IEEE, _TORCH_AVX512 or _TORCH_SSE2");
+    if (e.torch_sqrt != FEDAVG_SQRT_IEEE && e.torch_sqrt != FEDAVG_SQRT_TORCH_AVX512 && e.torch_sqrt != FEDAVG_SQRT_TORCH_AMD)
+        throw Error("epilogue torch_sqrt must be FEDAVG_SQRT_IEEE, _TORCH_AVX512 or _TORCH_AMD");
     E.torch_sqrt = e.torch_sqrt;
     if (e.kind == FEDAVG_EPI_RMSPROP) {  // rmsprop.py: square_avg.mul_(alpha).addcmul_(g, g, 1 - alpha), lerp(1 - alpha)
         E.beta2 = (float)e.alpha;
@@ -1460,8 +1460,8 @@ int fedavg_sqrt_f32(fedavg_ctx* ctx, const float* x, float* out, size_t n, int t
         if (!x || !out) throw Error("NULL pointer");
         ctx->activate();
         const int grid = (int)std::min<size_t>((size_t)ctx->num_cus * 8, (n + fedavg::kBlock - 1) / fedavg::kBlock);
-        if (torch_sqrt != FEDAVG_SQRT_IEEE && torch_sqrt != FEDAVG_SQRT_TORCH_AVX512 && torch_sqrt != FEDAVG_SQRT_TORCH_SSE2)
-            throw Error("torch_sqrt must be FEDAVG_SQRT_IEEE, _TORCH_AVX512 or _TORCH_SSE2");
+        if (torch_sqrt != FEDAVG_SQRT_IEEE && torch_sqrt != FEDAVG_SQRT_TORCH_AVX512 && torch_sqrt != FEDAVG_SQRT_TORCH_AMD)
+            throw Error("torch_sqrt must be FEDAVG_SQRT_IEEE, _TORCH_AVX512 or _TORCH_AMD");
         HIP_CHECK(fedavg::launch_sqrt_f32(x, out, (int64_t)n, torch_sqrt, grid, ctx->compute()));
     });
 }

@@ -32,7 +32,7 @@ struct EpiIn {
 template <int SQ>  // EPI & kEpiSqrtMask
 __device__ __forceinline__ float sqrt_e(const EpiParams& E, const float x) {
     if constexpr (SQ == kEpiTorchSqrt) return sqrt_torch_cpu(x);
-    if constexpr (SQ == kEpiTorchSqrtSse2) return sqrt_mkl_sse2(x);
+    if constexpr (SQ == kEpiTorchSqrtAmd) return sqrt_mkl_rsqrtps(x);
     return __builtin_sqrtf(x);
 }
 
@@ -273,6 +273,7 @@ fedavg_tiles_epi_burst_f32x4(const RowTableF32 tab, const int K, const int64_t t
     f32x4 dd[TPB][CPL];
     __shared__ f32x4 staged[TPB_LDS > 0 ? TPB_LDS * CPL * kBlock : 1];
     if constexpr ((EPI & kEpiTorchSqrt) != 0) rsqrt14_stage();
+    if constexpr ((EPI & kEpiTorchSqrtAmd) != 0) rsqrtps_stage();
 #pragma unroll
     for (int m = 0; m < TPB; ++m) {
         const int64_t t = t0 + blockIdx.x + (int64_t)m * gridDim.x;
@@ -359,6 +360,7 @@ __global__ void __launch_bounds__(kBlock) fedavg_tiles_epi_f32x4(const RowTableF
     const int64_t t_last = (e4 - 1) / T4;
     const int g0 = PIPE ? (K < UNROLL ? K : UNROLL) : 0;  // clients carried over from the previous tile
     if constexpr ((EPI & kEpiTorchSqrt) != 0) rsqrt14_stage();
+    if constexpr ((EPI & kEpiTorchSqrtAmd) != 0) rsqrtps_stage();
     f32x4 nxt[UNROLL][CPL];
     int64_t t = b4 / T4 + blockIdx.x;
     if constexpr (PIPE) {
@@ -494,7 +496,7 @@ inline hipError_t launch_epi_k(const TileLaunch& L, const EpiParams& E, hipStrea
 template <int OP, int FIN, bool ACC_IN, int KIND>
 inline hipError_t sqrt_mode(const TileLaunch& L, const EpiParams& E, hipStream_t s, uint64_t* nl) {
     if (E.torch_sqrt == FEDAVG_SQRT_TORCH_AVX512) return launch_epi_k<OP, FIN, ACC_IN, KIND | kEpiTorchSqrt>(L, E, s, nl);
-    if (E.torch_sqrt == FEDAVG_SQRT_TORCH_SSE2) return launch_epi_k<OP, FIN, ACC_IN, KIND | kEpiTorchSqrtSse2>(L, E, s, nl);
+    if (E.torch_sqrt == FEDAVG_SQRT_TORCH_AMD) return launch_epi_k<OP, FIN, ACC_IN, KIND | kEpiTorchSqrtAmd>(L, E, s, nl);
     return launch_epi_k<OP, FIN, ACC_IN, KIND>(L, E, s, nl);
 }
 

@@ -36,14 +36,14 @@ constexpr int kVariantWideLds = 64;       // inside TileLaunch: plain burst kern
                                            // unless the public variant has bit 6, which keeps the 4-tile form there
                                            // (32 clients 88.4 -> 88.9 %, 64: 89.7 -> 89.9 %, profiles/r02/ab/wide_lds/)
 // epilogue template value: the optimizer kind | kEpiTorchSqrt when the step's sqrt is torch CPU's restated AVX-512
-// vsSqrt (EpiParams.torch_sqrt == FEDAVG_SQRT_TORCH_AVX512; fedavg_arith.h sqrt_torch_cpu) | kEpiTorchSqrtSse2 for its
-// SSE2 path (FEDAVG_SQRT_TORCH_SSE2; sqrt_mkl_sse2) -- a compile-time choice, so the correctly rounded path keeps its
-// own code (a runtime branch cost the fused Adam kernel 9 points, profiles/r03/s3/)
+// vsSqrt (EpiParams.torch_sqrt == FEDAVG_SQRT_TORCH_AVX512; fedavg_arith.h sqrt_torch_cpu) | kEpiTorchSqrtAmd for the
+// AMD hosts' path (FEDAVG_SQRT_TORCH_AMD; sqrt_mkl_rsqrtps) -- a compile-time choice, so the correctly rounded path
+// keeps its own code (a runtime branch cost the fused Adam kernel 9 points, profiles/r03/s3/)
 constexpr int kEpiTorchSqrt = 0x100;
-constexpr int kEpiTorchSqrtSse2 = 0x200;
-constexpr int kEpiSqrtMask = kEpiTorchSqrt | kEpiTorchSqrtSse2;
+constexpr int kEpiTorchSqrtAmd = 0x200;
+constexpr int kEpiSqrtMask = kEpiTorchSqrt | kEpiTorchSqrtAmd;
 constexpr int kBurstLdsTilesWide = 10;     // 10 x 16 KiB = all of a CU's LDS
-constexpr int kBurstEpiLdsTilesWide = 9;   // fused form at one block per CU: 9 x 16 KiB (+ the 512-byte sqrt table)
+constexpr int kBurstEpiLdsTilesWide = 9;   // fused form at one block per CU: 9 x 16 KiB (+ a sqrt table: 512 B / 16 KiB)
 constexpr int kBurstTiles = 8;             // tiles per block per burst launch (results held in registers)
 constexpr int kBurstLdsTiles = 4;          // 4 x 16 KiB of LDS per block (2 blocks fit a CU)
 
@@ -101,7 +101,7 @@ struct EpiParams {
     int rectified;                                // RAdam: rho_t > 5
     float etaminus, etaplus, ss_min, ss_max;      // Rprop
     float decay, neg_eta, mu;                     // ASGD: 1 - lambd * eta, -eta, mu (averaging when != 1)
-    int torch_sqrt;                               // FEDAVG_SQRT_*: torch CPU's sqrt (AVX-512 / SSE2 path), or IEEE
+    int torch_sqrt;                               // FEDAVG_SQRT_*: torch CPU's sqrt (Intel / AMD host), or IEEE
 };
 
 struct DequantLaunch {

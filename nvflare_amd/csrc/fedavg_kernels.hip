@@ -585,15 +585,16 @@ hipError_t launch_fill_synthetic_f32(float* dst, int64_t n, int64_t tile, int64_
     return hipGetLastError();
 }
 
-// test kernel: the epilogues' sqrt elementwise (torch_sqrt: FEDAVG_SQRT_* -- torch CPU's restated AVX-512 / SSE2 vsSqrt,
-// or the correctly rounded one)
+// test kernel: the epilogues' sqrt elementwise (torch_sqrt: FEDAVG_SQRT_* -- torch CPU's restated vsSqrt of the Intel
+// or the AMD hosts, or the correctly rounded one)
 __global__ void __launch_bounds__(kBlock) fedavg_sqrt_f32(const float* __restrict__ x, float* __restrict__ out, int64_t n,
                                                           int torch_sqrt) {
     const int64_t stride = (int64_t)gridDim.x * kBlock;
     rsqrt14_stage();
+    rsqrtps_stage();
     for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride)
         out[i] = torch_sqrt == FEDAVG_SQRT_TORCH_AVX512 ? sqrt_torch_cpu(x[i])
-                 : torch_sqrt == FEDAVG_SQRT_TORCH_SSE2 ? sqrt_mkl_sse2(x[i])
+                 : torch_sqrt == FEDAVG_SQRT_TORCH_AMD ? sqrt_mkl_rsqrtps(x[i])
                                                         : __builtin_sqrtf(x[i]);
 }
 

@@ -9,17 +9,18 @@ NOT the correctly rounded sqrt, and MKL picks its code path by CPU.  The device 
   from the VRSQRT14PS estimate (tools/sqrt_probe.c; ~0.5 % of results 1 ulp low), restated in fedavg_arith.h
   ``sqrt_torch_cpu`` with the captured estimate table (``data/rsqrt14_avx512.bin``, 2 x 2^15 estimates) evaluated as
   64 exact line segments (fedavg_rsqrt14.h, tools/make_rsqrt14_segments.py);
-* ``"torch_cpu_sse2"`` -- the SSE2 path MKL dispatches on AMD CPUs (the GPU pool's EPYC hosts): the correctly rounded
-  sqrtps refined by a Newton step from a truncated reciprocal in plain fp32 (~16 % of results +-1 ulp), restated in
-  fedavg_arith.h ``sqrt_mkl_sse2`` and checked equal to MKL's own kernel on all 2^32 inputs
-  (tools/sqrt_mkl_sse2_check.py);
+* ``"torch_cpu_amd"`` -- the SSE4.2 / AVX path MKL runs on the GPU pool's AMD EPYC hosts: a coupled Newton step in
+  plain fp32 from that CPU's RSQRTPS estimate (~16 % of results +-1 ulp), restated in fedavg_arith.h
+  ``sqrt_mkl_rsqrtps`` with the estimate table captured on the box (``data/rsqrtps_amd.bin``, 2 x 4096 estimates,
+  tools/rsqrtps_dump.c); the sequence equals MKL's own kernel on all 2^32 inputs with this container's RSQRTPS and
+  the box's torch.sqrt on every fp32 in [1, 4) with the AMD table (tools/sqrt_mkl_sse_check.py);
 * ``"ieee"`` -- the correctly rounded sqrt (torch builds / CPUs whose vsSqrt rounds correctly).
 
-``mode()`` follows ``$NVFLARE_AMD_TORCH_SQRT`` (``torch_cpu`` | ``torch_cpu_sse2`` | ``ieee`` | ``auto``, the default):
-``auto`` asks this host's torch for the sqrt of ``data/sqrt_vectors.npz``'s probe values (11479 inputs: 6400 where
-the AVX-512 path and the correctly rounded sqrt differ, 3072 where the SSE2 path differs from both) and picks the one
-it matches bit for bit, ``ieee`` when it matches none (then the FedOpt parameters carry the documented sqrt bound,
-DESIGN.md section 8)."""
+``mode()`` follows ``$NVFLARE_AMD_TORCH_SQRT`` (``torch_cpu`` | ``torch_cpu_amd`` | ``ieee`` | ``auto``, the default):
+``auto`` asks this host's torch for the sqrt of ``data/sqrt_vectors.npz``'s probe values (6400 inputs where the AVX-512
+path and the correctly rounded sqrt differ, 3072 where the AMD path differs from both, and inputs where they agree)
+and picks the one it matches bit for bit, ``ieee`` when it matches none (then the FedOpt parameters carry the
+documented sqrt bound)."""
 
 from __future__ import annotations
 
@@ -32,7 +33,7 @@ import numpy as np
 DATA = os.path.join(os.path.dirname(os.path.abspath(__file__)), "data")
 TABLE_FILE = os.path.join(DATA, "rsqrt14_avx512.bin")
 VECTORS_FILE = os.path.join(DATA, "sqrt_vectors.npz")
-MODES = ("torch_cpu", "torch_cpu_sse2", "ieee")
+MODES = ("torch_cpu", "torch_cpu_amd", "ieee")
 
 _lock = threading.RLock()
 _detected: Optional[str] = None
@@ -71,7 +72,7 @@ def mode() -> str:
     if env in MODES:
         return env
     if env != "auto":
-        raise ValueError(f"NVFLARE_AMD_TORCH_SQRT={env!r}: expected torch_cpu, torch_cpu_sse2, ieee or auto")
+        raise ValueError(f"NVFLARE_AMD_TORCH_SQRT={env!r}: expected torch_cpu, torch_cpu_amd, ieee or auto")
     d = detect()
     return d if d in MODES else "ieee"
 
@@ -83,5 +84,5 @@ def epilogue_flag(sqrt_mode: Optional[str] = None) -> int:
     m = sqrt_mode or mode()
     if m not in MODES:
         raise ValueError(f"sqrt mode {m!r}: expected one of {MODES}")
-    return {"torch_cpu": N.FEDAVG_SQRT_TORCH_AVX512, "torch_cpu_sse2": N.FEDAVG_SQRT_TORCH_SSE2,
+    return {"torch_cpu": N.FEDAVG_SQRT_TORCH_AVX512, "torch_cpu_amd": N.FEDAVG_SQRT_TORCH_AMD,
             "ieee": N.FEDAVG_SQRT_IEEE}[m]

@@ -131,7 +131,7 @@ void oracle_synth_fill_f32(uint64_t seed, uint64_t row, const uint64_t* cols, si
  *               own sqrt: MKL VML vsSqrt on the AVX-512 path (ATen vml.h IMPLEMENT_VML_MKL(sqrt, Sqrt)), which
  *               is one Newton step from the VRSQRT14PS estimate, restated in oracle_sqrt_torch_cpu below
  *               (~0.5 % of its results are 1 ulp below the correctly rounded value; tools/sqrt_probe.c);
- *               with sqrt_sse2, MKL's SSE2 path (AMD hosts), oracle_sqrt_mkl_sse2.
+ *               with rsqrtps_table, MKL's SSE4.2 / AVX path (AMD hosts), oracle_sqrt_mkl_rsqrtps.
  * Scalars follow torch: python-float hyperparameters and bias corrections computed in fp64, cast to
  * fp32 where they meet a tensor.
  * ------------------------------------------------------------------------------------------------ */
@@ -156,7 +156,7 @@ typedef struct {
     double etaminus, etaplus, step_size_min, step_size_max; /* Rprop */
     double eta, mu, lambd;                        /* ASGD: fp32 eta / mu states before this step */
     const uint16_t* sqrt_table;                   /* NULL: IEEE sqrt; else the VRSQRT14 mantissa table */
-    int sqrt_sse2;                                /* nonzero: MKL's SSE2 vsSqrt (oracle_sqrt_mkl_sse2) */
+    const uint16_t* rsqrtps_table;                /* non-NULL: MKL's SSE4.2 / AVX vsSqrt (oracle_sqrt_mkl_rsqrtps) */
 } oracle_epilogue;
 
 /* torch CPU's fp32 Tensor.sqrt, restated (torch 2.10 + MKL 2024.2 on AVX-512; measured bit-exact against torch
@@ -191,10 +191,10 @@ void oracle_sqrt_torch_cpu_n(const uint16_t* tab, const float* x, size_t n, floa
     for (size_t i = 0; i < n; ++i) out[i] = oracle_sqrt_torch_cpu(tab, x[i]);
 }
 
-/* torch CPU's fp32 Tensor.sqrt where MKL dispatches its SSE2 code path (mkl_vml_kernel_sSqrt_E2HAynn), as it does on
- * the AMD EPYC hosts of the GPU pool (their torch.sqrt matched this kernel on every probe value; the AVX-512 path
- * above is Intel-only).  The kernel refines the correctly rounded sqrtps result with a coupled Newton step in plain
- * fp32 (SSE2: every operation rounds, no FMA), starting from a reciprocal truncated to 12 significant bits:
+/* MKL vsSqrt's SSE2 kernel (mkl_vml_kernel_sSqrt_E2HAynn): not what torch runs on the hosts seen so far, but the
+ * plain-fp32 refinement it shares with the SSE4.2 / AVX kernels below, pinned exhaustively on any x86-64 host because
+ * its estimate uses only IEEE operations.  It refines the correctly rounded sqrtps result with a coupled Newton step
+ * (SSE2: every operation rounds, no FMA), starting from a reciprocal truncated to 12 significant bits:
  *   s0 = sqrt(x);  y = trunc12(1 / s0);  s = x * y;  h = y * 0.5;  r = 0.5 - s * h;
  *   s1 = s * r + s;  h1 = h * r + h;  sqrt = (x - s1 * s1) * h1 + s1
  * for positive normal x up to 0x7f7ff000; everything else (zero, subnormals, the top 4095 finite values, inf, NaN,
@@ -227,8 +227,45 @@ void oracle_sqrt_mkl_sse2_n(const float* x, size_t n, float* out) {
     for (size_t i = 0; i < n; ++i) out[i] = oracle_sqrt_mkl_sse2(x[i]);
 }
 
+/* torch CPU's fp32 Tensor.sqrt on the GPU pool's AMD EPYC hosts: there MKL runs vsSqrt's SSE4.2 / AVX kernels
+ * (mkl_vml_kernel_sSqrt_EXHAynn / _H8HAynn, identical results), which start the same coupled Newton step as the SSE2
+ * kernel above from the RSQRTPS estimate instead:
+ *   y = rsqrtps(x);  s = x * y;  h = y * 0.5;  r = 0.5 - s * h;  s1 = s * r + s;  h1 = h * r + h;
+ *   sqrt = (x - s1 * s1) * h1 + s1
+ * (positive normals up to 0x7f7ff000; everything else the correctly rounded callout).  RSQRTPS differs between CPU
+ * vendors; it depends on the exponent parity and the top 12 mantissa bits only, so tab[parity << 12 | m >> 11] holds
+ * mantissa bits 22..11 of its result for x in [1, 4) (exponent 126 throughout; tools/rsqrtps_dump.c captures it) and
+ * y = that estimate * 2^-k for x = 4^k * x0.  With this CPU's table the sequence equals MKL's EX kernel on all 2^32
+ * inputs (tools/sqrt_mkl_sse2_check.py); with the AMD host's table, that host's torch.sqrt (tools/sqrt_box_kernels.py). */
+float oracle_sqrt_mkl_rsqrtps(const uint16_t* tab, float x) {
+    uint32_t b;
+    memcpy(&b, &x, 4);
+    if (b < 0x00800000u || b > 0x7F7FF000u) return sqrtf(x);
+    const int e = (int)(b >> 23) - 127;
+    const int p = e & 1;
+    const int k = (e - p) / 2;
+    const uint32_t yb = (0x3F000000u | ((uint32_t)tab[(p << 12) | ((b & 0x7FFFFFu) >> 11)] << 11)) - (uint32_t)(k * 8388608);
+    float y;
+    memcpy(&y, &yb, 4);
+    const float s = x * y;
+    const float h = y * 0.5f;
+    const float t = s * h;
+    const float r = 0.5f - t;
+    const float sr = s * r, hr = h * r;
+    const float s1 = sr + s;
+    const float h1 = hr + h;
+    const float q = s1 * s1;
+    const float d = x - q;
+    const float dh = d * h1;
+    return dh + s1;
+}
+
+void oracle_sqrt_mkl_rsqrtps_n(const uint16_t* tab, const float* x, size_t n, float* out) {
+    for (size_t i = 0; i < n; ++i) out[i] = oracle_sqrt_mkl_rsqrtps(tab, x[i]);
+}
+
 static inline float sqrt_e(const oracle_epilogue* epi, float x) {
-    if (epi->sqrt_sse2) return oracle_sqrt_mkl_sse2(x);
+    if (epi->rsqrtps_table) return oracle_sqrt_mkl_rsqrtps(epi->rsqrtps_table, x);
     return epi->sqrt_table ? oracle_sqrt_torch_cpu(epi->sqrt_table, x) : sqrtf(x);
 }
 

@@ -328,7 +328,7 @@ class _Epi(ctypes.Structure):
         ("mu", ctypes.c_double),
         ("lambd", ctypes.c_double),
         ("sqrt_table", ctypes.c_void_p),
-        ("sqrt_sse2", ctypes.c_int),
+        ("rsqrtps_table", ctypes.c_void_p),
     ]
 
 
@@ -375,14 +375,46 @@ def sqrt_torch_cpu_sse2(x) -> np.ndarray:
     return out
 
 
-SQRT_FUNCS = {"torch_cpu": sqrt_torch_cpu, "torch_cpu_sse2": sqrt_torch_cpu_sse2, "ieee": np.sqrt}
+_RSQRTPS_FILE = os.path.join(os.path.dirname(_HERE), "nvflare_amd", "data", "rsqrtps_amd.bin")
+_rsqrtps = None
 
 
-def epilogue_apply(delta, kind, p=None, m=None, v=None, base=None, vmax=None, torch_cpu_sqrt=False, **hp):
+def rsqrtps_table() -> np.ndarray:
+    """RSQRTPS of the GPU pool's AMD EPYC host CPU (tools/rsqrtps_dump.c, tools/make_rsqrtps_table.py): 2 x 4096
+    uint16, mantissa bits 22..11 of the estimate for x in [1, 2) then [2, 4), one per top-12-bit mantissa."""
+    global _rsqrtps
+    if _rsqrtps is None:
+        t = np.fromfile(_RSQRTPS_FILE, dtype=np.uint16)
+        if t.size != 8192 or np.any(t > 0xFFF):
+            raise ValueError(f"{_RSQRTPS_FILE}: not an RSQRTPS table")
+        _rsqrtps = np.ascontiguousarray(t)
+    return _rsqrtps
+
+
+def sqrt_torch_cpu_amd(x, table: Optional[np.ndarray] = None) -> np.ndarray:
+    """torch CPU's fp32 sqrt on the AMD hosts (MKL vsSqrt's SSE4.2 / AVX kernel, oracle_sqrt_mkl_rsqrtps) with that
+    CPU's RSQRTPS table, or ``table`` (another CPU's, e.g. this one's for a check against MKL's kernel here)."""
+    lib = load()
+    fn = lib.oracle_sqrt_mkl_rsqrtps_n
+    fn.restype = None
+    fn.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]
+    tab = np.ascontiguousarray(rsqrtps_table() if table is None else table, dtype=np.uint16)
+    x = np.ascontiguousarray(x, dtype=np.float32)
+    out = np.empty_like(x)
+    fn(tab.ctypes.data, x.ctypes.data, x.size, out.ctypes.data)
+    return out
+
+
+SQRT_FUNCS = {"torch_cpu": sqrt_torch_cpu, "torch_cpu_amd": sqrt_torch_cpu_amd, "ieee": np.sqrt}
+
+
+def epilogue_apply(delta, kind, p=None, m=None, v=None, base=None, vmax=None, torch_cpu_sqrt=False,
+                   rsqrtps=None, **hp):
     """Apply an epilogue to the aggregated update `delta` (fp32).  p/m/v (and vmax with amsgrad=1) are
     updated IN PLACE (copies are the caller's business); returns `out` for NONE/ADD_BASE and p otherwise.
     ``torch_cpu_sqrt``: which sqrt -- False / "ieee" the correctly rounded one, True / "torch_cpu" torch CPU's
-    AVX-512 vsSqrt (oracle_sqrt_torch_cpu), "torch_cpu_sse2" its SSE2 path (oracle_sqrt_mkl_sse2)."""
+    AVX-512 vsSqrt (oracle_sqrt_torch_cpu), "torch_cpu_amd" its SSE4.2 / AVX path on the AMD hosts
+    (oracle_sqrt_mkl_rsqrtps with ``rsqrtps`` or the AMD host's RSQRTPS table)."""
     lib = load()
     fn = lib.oracle_epilogue_apply
     fn.restype = None
@@ -392,12 +424,13 @@ def epilogue_apply(delta, kind, p=None, m=None, v=None, base=None, vmax=None, to
     e.kind = kind
     for k, val in hp.items():
         setattr(e, k, val)
-    if torch_cpu_sqrt not in (False, True, "ieee", "torch_cpu", "torch_cpu_sse2"):
+    if torch_cpu_sqrt not in (False, True, "ieee", "torch_cpu", "torch_cpu_amd"):
         raise ValueError(f"torch_cpu_sqrt={torch_cpu_sqrt!r}")
     if torch_cpu_sqrt is True or torch_cpu_sqrt == "torch_cpu":
         e.sqrt_table = sqrt_table().ctypes.data
-    elif torch_cpu_sqrt == "torch_cpu_sse2":
-        e.sqrt_sse2 = 1
+    elif torch_cpu_sqrt == "torch_cpu_amd":
+        tab = np.ascontiguousarray(rsqrtps_table() if rsqrtps is None else rsqrtps, dtype=np.uint16)
+        e.rsqrtps_table = tab.ctypes.data
     out = np.empty_like(delta)
 
     def ptr(a):

@@ -1,8 +1,8 @@
 """The fused burst kernel's launch forms at one block per CU (64+ clients), bit-exact against the oracle over
 more tiles than one launch holds (two launches, the second partial, ragged end): the default form (8 register-
 + 9 LDS-held tiles per block, round 3), the 4-LDS-tile form (variant bit 6) and the register-only form (bit 5),
-with the correctly rounded and both restated torch-CPU sqrts (the AVX-512 one stages its segment table in the
-same LDS; the SSE2 one needs no table).  64 and 70 clients read 4 distinct uploaded rows cyclically (the kernel sees 64 / 70 row pointers; the
+with the correctly rounded and both restated torch-CPU sqrts (each stages its table in the same LDS: the Intel
+hosts' 512-byte segments, the AMD hosts' 16 KiB RSQRTPS table -- 160 KiB in all at one block per CU).  64 and 70 clients read 4 distinct uploaded rows cyclically (the kernel sees 64 / 70 row pointers; the
 oracle the same list), which keeps the host side small at 18 M elements per row."""
 
 import numpy as np
@@ -81,6 +81,6 @@ def test_fused_adam_launch_forms(ctx, oracle, rows, K, variant, torch_sqrt):
     assert launches == -(-tiles // per_launch)  # the form that ran is the one asked for
     d = oracle.fedavg_c([rows[k % len(rows)] for k in range(K)], ws, oracle.MODE_TORCH, nthreads=8)
     oracle.epilogue_apply(d, oracle.EPI_ADAM, p=p, m=m, v=v, step=2.0, lr=1e-3, beta1=0.9, beta2=0.999, eps=1e-8,
-                          torch_cpu_sqrt=["ieee", "torch_cpu", "torch_cpu_sse2"][torch_sqrt])
+                          torch_cpu_sqrt=["ieee", "torch_cpu", "torch_cpu_amd"][torch_sqrt])
     for name, a, b in (("p", got[0], p), ("m", got[1], m), ("v", got[2], v)):
         assert same_bits(a, b), (name, int(np.count_nonzero(a.view(np.uint32) != b.view(np.uint32))))

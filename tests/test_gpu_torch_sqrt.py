@@ -1,9 +1,9 @@
-"""The device epilogues' torch-CPU sqrt (fedavg_arith.h sqrt_torch_cpu / sqrt_mkl_sse2; nvflare_amd/torch_sqrt.py) on
-the GPU, both restated MKL vsSqrt paths: AVX-512 (Intel hosts) and SSE2 (AMD hosts, e.g. this pool's).
+"""The device epilogues' torch-CPU sqrt (fedavg_arith.h sqrt_torch_cpu / sqrt_mkl_rsqrtps; nvflare_amd/torch_sqrt.py)
+on the GPU, both restated MKL vsSqrt paths: Intel hosts (AVX-512) and AMD hosts (SSE4.2 / AVX, e.g. this pool's).
 
 * elementwise (fedavg_sqrt_f32), against the oracle's restatements (oracle_sqrt_torch_cpu, pinned against torch CPU
-  by tests/test_torch_sqrt.py; oracle_sqrt_mkl_sse2, pinned against MKL's SSE2 kernel by
-  tests/test_torch_sqrt_sse2.py) over every mantissa of [1, 4), every subnormal and 1 in 61 of every other binade
+  by tests/test_torch_sqrt.py; oracle_sqrt_mkl_rsqrtps, pinned against MKL's kernel and the box's torch by
+  tests/test_torch_sqrt_amd.py) over every mantissa of [1, 4), every subnormal and 1 in 61 of every other binade
   (tools/sqrt_probe.py's set, 59.8 M values) -- and against this host's torch.sqrt for whichever path
   torch_sqrt.detect() finds here;
 * inside every epilogue that takes a sqrt (Adam, AdamW + amsgrad, Adagrad, RMSprop centered + momentum, NAdam,
@@ -62,18 +62,18 @@ def test_device_sqrt_matches_restatement_everywhere(ctx, oracle):
     got = _device_sqrt(ctx, x, 1)
     exp = oracle.sqrt_torch_cpu(x)
     assert _same(got, exp) == 0
-    sse2 = _device_sqrt(ctx, x, 2)
+    amd = _device_sqrt(ctx, x, 2)
     with np.errstate(invalid="ignore"):
-        assert _same(sse2, oracle.sqrt_torch_cpu_sse2(x)) == 0
+        assert _same(amd, oracle.sqrt_torch_cpu_amd(x)) == 0
     ieee = _device_sqrt(ctx, x, 0)
     with np.errstate(invalid="ignore"):
         assert _same(ieee, np.sqrt(x)) == 0
     assert _same(got, ieee) > 300_000  # the three sqrt modes are different functions
-    assert _same(sse2, ieee) > 3_000_000 and _same(sse2, got) > 3_000_000
+    assert _same(amd, ieee) > 3_000_000 and _same(amd, got) > 3_000_000
     here = torch_sqrt.detect()
-    if here in ("torch_cpu", "torch_cpu_sse2"):  # this host's torch computes one of them: compare with it too
+    if here in ("torch_cpu", "torch_cpu_amd"):  # this host's torch computes one of them: compare with it too
         with np.errstate(invalid="ignore"):
-            assert _same(got if here == "torch_cpu" else sse2, torch.from_numpy(x.copy()).sqrt().numpy()) == 0
+            assert _same(got if here == "torch_cpu" else amd, torch.from_numpy(x.copy()).sqrt().numpy()) == 0
 
 
 class _Dev:
@@ -116,7 +116,7 @@ KINDS = [
 ]
 
 
-@pytest.mark.parametrize("sqrt", ["torch_cpu", "torch_cpu_sse2"])
+@pytest.mark.parametrize("sqrt", ["torch_cpu", "torch_cpu_amd"])
 @pytest.mark.parametrize("K", [5, 70])
 @pytest.mark.parametrize("name,hp", KINDS, ids=[k for k, _ in KINDS])
 def test_epilogues_with_torch_cpu_sqrt(ctx, oracle, name, hp, K, sqrt):
@@ -145,7 +145,7 @@ def test_epilogues_with_torch_cpu_sqrt(ctx, oracle, name, hp, K, sqrt):
         for k_, val in hp.items():
             setattr(e, k_, val)
         e.step, e.mu_product = float(step), mp
-        e.torch_sqrt = {"torch_cpu": N.FEDAVG_SQRT_TORCH_AVX512, "torch_cpu_sse2": N.FEDAVG_SQRT_TORCH_SSE2}[sqrt]
+        e.torch_sqrt = {"torch_cpu": N.FEDAVG_SQRT_TORCH_AVX512, "torch_cpu_amd": N.FEDAVG_SQRT_TORCH_AMD}[sqrt]
         e.param, e.state1 = dev.buf("p", dev_p), dev.buf("m", dev_m)
         e.state2, e.state3 = dev.buf("v", dev_v), dev.buf("x3", dev_3)
         ctx.accumulate_tiled_epi(dev.bases, ws, 4096, dev.lay.tile_stride, 0, dev.n4, None, N.FEDAVG_OP_TORCH,

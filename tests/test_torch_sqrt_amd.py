@@ -1,15 +1,25 @@
-"""torch CPU's fp32 sqrt on AMD hosts, restated (oracle_sqrt_mkl_sse2; the device epilogue's sqrt_mkl_sse2) -- CPU tests.
+"""torch CPU's fp32 sqrt on the GPU pool's AMD hosts, restated (oracle_sqrt_mkl_rsqrtps; the device epilogue's
+sqrt_mkl_rsqrtps) -- CPU tests.
 
-On AMD CPUs (the GPU pool's EPYC hosts) MKL runs vsSqrt's SSE2 kernel, mkl_vml_kernel_sSqrt_E2HAynn, instead of the
-AVX-512 one the Intel container uses: torch.sqrt on the box matched it on every probe value recorded there
-(profiles/r03/s5/sqrt_probe_box.json).  The kernel ships inside the libtorch_cpu this torch loads, so it is called
-directly here, on any x86-64 host, and pins the restatement: every mantissa of several binades and a stride-61
-sample of all 2^32 bit patterns (tools/sqrt_mkl_sse2_check.py ran all 2^32: 0 mismatches).  Whole torch optimizer
-runs with torch's sqrt swapped for that kernel then check that the oracle's "torch_cpu_sse2" epilogues reproduce
-torch's single-tensor Adam / AdamW / amsgrad / NAdam / RAdam / Adagrad / RMSprop bit for bit with that sqrt."""
+On AMD EPYC (the GPU box host) MKL runs vsSqrt's SSE4.2 / AVX kernels (mkl_vml_kernel_sSqrt_EXHAynn / _H8HAynn): on
+the box torch.sqrt equalled them on all 59.8 M probe inputs (profiles/r03/s12/sqrt_box_kernels.json).  They start a
+coupled Newton step in plain fp32 from the RSQRTPS estimate, which differs between CPU vendors.  The pins:
+
+* the kernels ship inside the libtorch_cpu this torch loads, so they run HERE too: the restatement with THIS CPU's
+  RSQRTPS (captured by tools/rsqrtps_dump.c at test time) equals MKL's EX kernel on every mantissa of several
+  binades and a stride-61 sample of all 2^32 inputs (tools/sqrt_mkl_sse_check.py ran all 2^32: 0 mismatches);
+* the SSE2 kernel (E2HA) shares the refinement with an IEEE-only estimate: oracle_sqrt_mkl_sse2 equals it too;
+* with the AMD host's table (nvflare_amd/data/rsqrtps_amd.bin, captured on the box) the restatement reproduces the
+  box's own torch.sqrt: tests/golden/sqrt_amd_box.npz (100,000 inputs of [1, 4); all 2^24 matched offline);
+* whole torch optimizer runs with torch's sqrt swapped for MKL's EX kernel run here equal the oracle's
+  "torch_cpu_amd" epilogues given this CPU's table: single-tensor Adam / AdamW / amsgrad / NAdam / RAdam / Adagrad /
+  RMSprop, parameters and state bit for bit."""
 
 import ctypes
 import os
+import shutil
+import subprocess
+import sys
 
 import numpy as np
 import pytest
@@ -19,10 +29,14 @@ from golden_util import same_bits
 from nvflare_amd import torch_sqrt
 
 
-def _kernel():
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLDEN = os.path.join(ROOT, "tests", "golden", "sqrt_amd_box.npz")
+
+
+def _kernel(name):
     try:
         lib = ctypes.CDLL(os.path.join(os.path.dirname(torch.__file__), "lib", "libtorch_cpu.so"))
-        fn = lib.mkl_vml_kernel_sSqrt_E2HAynn
+        fn = getattr(lib, name)
     except (OSError, AttributeError):
         return None
     fn.restype = None
@@ -30,17 +44,40 @@ def _kernel():
     return fn
 
 
-KERNEL = _kernel()
-pytestmark = pytest.mark.skipif(KERNEL is None, reason="this torch build has no MKL SSE2 vsSqrt kernel")
+E2, EX = _kernel("mkl_vml_kernel_sSqrt_E2HAynn"), _kernel("mkl_vml_kernel_sSqrt_EXHAynn")
+pytestmark = pytest.mark.skipif(E2 is None or EX is None, reason="this torch build has no MKL SSE vsSqrt kernels")
 
 
-def mkl_sse2(x: np.ndarray) -> np.ndarray:
+def _run(kernel, x: np.ndarray) -> np.ndarray:
     x = np.ascontiguousarray(x, dtype=np.float32)
     out = np.empty_like(x)
     for i in range(0, x.size, 1 << 30):
         n = min(1 << 30, x.size - i)
-        KERNEL(n, x[i:].ctypes.data, out[i:].ctypes.data)
+        kernel(n, x[i:].ctypes.data, out[i:].ctypes.data)
     return out
+
+
+def mkl_sse2(x):
+    return _run(E2, x)
+
+
+def mkl_ex(x):
+    return _run(EX, x)
+
+
+@pytest.fixture(scope="module")
+def here_rsqrtps(tmp_path_factory):
+    """THIS CPU's RSQRTPS table (tools/rsqrtps_dump.c, tools/make_rsqrtps_table.py)."""
+    if shutil.which("gcc") is None:
+        pytest.skip("gcc is absent")
+    d = tmp_path_factory.mktemp("rsqrtps")
+    exe = str(d / "rsqrtps_dump")
+    subprocess.run(["gcc", "-O2", "-msse2", os.path.join(ROOT, "tools", "rsqrtps_dump.c"), "-o", exe], check=True)
+    subprocess.run([exe, str(d / "rsq.bin"), str(d / "rcp.bin")], check=True, capture_output=True)
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import make_rsqrtps_table
+
+    return make_rsqrtps_table.table_from_dump(str(d / "rsq.bin"))
 
 
 def _same_nan(a, b):
@@ -48,49 +85,62 @@ def _same_nan(a, b):
 
 
 @pytest.mark.parametrize("exp", [-127, -126, -100, -96, -30, -20, 0, 1, 77, 126, 127])
-def test_every_mantissa_of_a_binade(oracle, exp):
+def test_every_mantissa_of_a_binade(oracle, here_rsqrtps, exp):
     bits = np.arange(1 << 23, dtype=np.uint32)
     bits = bits | np.uint32((exp + 127) << 23) if exp > -127 else bits
     x = bits.view(np.float32)
-    got, ref = oracle.sqrt_torch_cpu_sse2(x), mkl_sse2(x)
+    got, ref = oracle.sqrt_torch_cpu_amd(x, here_rsqrtps), mkl_ex(x)
     assert same_bits(got, ref), int(np.count_nonzero(got.view(np.uint32) != ref.view(np.uint32)))
+    got2, ref2 = oracle.sqrt_torch_cpu_sse2(x), mkl_sse2(x)
+    assert same_bits(got2, ref2), int(np.count_nonzero(got2.view(np.uint32) != ref2.view(np.uint32)))
     if exp in (0, 1):  # a different function from the correctly rounded sqrt and from the AVX-512 path
-        assert np.count_nonzero(ref.view(np.uint32) != np.sqrt(x).view(np.uint32)) > 500_000
-        assert np.count_nonzero(ref.view(np.uint32) != oracle.sqrt_torch_cpu(x).view(np.uint32)) > 500_000
+        amd = oracle.sqrt_torch_cpu_amd(x)
+        assert np.count_nonzero(amd.view(np.uint32) != np.sqrt(x).view(np.uint32)) > 500_000
+        assert np.count_nonzero(amd.view(np.uint32) != oracle.sqrt_torch_cpu(x).view(np.uint32)) > 500_000
 
 
-def test_all_bit_patterns_sampled(oracle):
+def test_all_bit_patterns_sampled(oracle, here_rsqrtps):
     bits = np.arange(0, 1 << 32, 61, dtype=np.uint64).astype(np.uint32)
     x = bits.view(np.float32)
     with np.errstate(invalid="ignore"):
+        assert _same_nan(oracle.sqrt_torch_cpu_amd(x, here_rsqrtps), mkl_ex(x)) == 0
         assert _same_nan(oracle.sqrt_torch_cpu_sse2(x), mkl_sse2(x)) == 0
 
 
-def test_specials_and_callout_edges(oracle):
+def test_specials_and_callout_edges(oracle, here_rsqrtps):
     edge = np.array([0, 0x80000000, 1, 0x007FFFFF, 0x00800000, 0x7F7FF000, 0x7F7FF001, 0x7F7FFFFF, 0x7F800000,
                      0xFF800000, 0x7FC00000, 0xBF800000, 0x3F800000, 0x40800000, 0x3E800000], np.uint32)
     x = edge.view(np.float32)
     with np.errstate(invalid="ignore"):
-        assert _same_nan(oracle.sqrt_torch_cpu_sse2(x), mkl_sse2(x)) == 0
+        assert _same_nan(oracle.sqrt_torch_cpu_amd(x, here_rsqrtps), mkl_ex(x)) == 0
+        assert _same_nan(oracle.sqrt_torch_cpu_amd(x), mkl_ex(x)) == 0  # the callout does not depend on the table
+
+
+def test_amd_table_reproduces_the_box_torch(oracle):
+    g = np.load(GOLDEN, allow_pickle=False)
+    got = oracle.sqrt_torch_cpu_amd(g["x"].view(np.float32)).view(np.uint32)
+    assert np.array_equal(got, g["torch_sqrt"]), int(np.count_nonzero(got != g["torch_sqrt"]))
+    cr = np.sqrt(g["x"].view(np.float32)).view(np.uint32)
+    assert np.count_nonzero(cr != g["torch_sqrt"]) > 10_000  # the box's sqrt is not the correctly rounded one
 
 
 def test_probe_vectors_and_detection(oracle):
     v = np.load(torch_sqrt.VECTORS_FILE, allow_pickle=False)
-    assert same_bits(oracle.sqrt_torch_cpu_sse2(v["x"]), v["torch_cpu_sse2"])
-    assert same_bits(mkl_sse2(v["x"]), v["torch_cpu_sse2"])
+    assert same_bits(oracle.sqrt_torch_cpu_amd(v["x"]), v["torch_cpu_amd"])
     for other in ("torch_cpu", "ieee"):  # each mode is told apart from the others by thousands of probe values
-        assert np.count_nonzero(v["torch_cpu_sse2"].view(np.uint32) != v[other].view(np.uint32)) >= 3000
+        assert np.count_nonzero(v["torch_cpu_amd"].view(np.uint32) != v[other].view(np.uint32)) >= 3000
     assert torch_sqrt.detect() in torch_sqrt.MODES + ("unmatched",)
-    assert torch_sqrt.epilogue_flag("torch_cpu_sse2") == 2 and torch_sqrt.epilogue_flag("torch_cpu") == 1
+    assert torch_sqrt.epilogue_flag("torch_cpu_amd") == 2 and torch_sqrt.epilogue_flag("torch_cpu") == 1
     assert torch_sqrt.epilogue_flag("ieee") == 0
 
 
 @pytest.fixture
-def sse2_torch(monkeypatch):
-    """torch's CPU sqrt replaced by MKL's SSE2 kernel (what torch computes on an AMD host)."""
+def ex_torch(monkeypatch):
+    """torch's CPU sqrt replaced by MKL's EX kernel run here (what torch computes on the AMD host, with this CPU's
+    RSQRTPS)."""
 
     def sq(t, *a, **k):
-        return torch.from_numpy(mkl_sse2(t.detach().contiguous().numpy()).reshape(t.shape))
+        return torch.from_numpy(mkl_ex(t.detach().contiguous().numpy()).reshape(t.shape))
 
     def sq_(t):
         t.copy_(sq(t))
@@ -120,7 +170,7 @@ def _torch_steps(opt_cls, kw, p0, deltas):
     ("Adagrad", dict(lr=0.1, lr_decay=0.05, eps=1e-8)),
     ("RMSprop", dict(lr=1e-3, centered=True, momentum=0.5)),
 ])
-def test_optimizer_steps_bit_exact_with_sse2_sqrt(oracle, sse2_torch, name, kw):
+def test_optimizer_steps_bit_exact_with_amd_path_sqrt(oracle, ex_torch, here_rsqrtps, name, kw):
     from test_fedopt_oracle import nadam_mu_product
 
     rng = np.random.default_rng(21)
@@ -132,7 +182,7 @@ def test_optimizer_steps_bit_exact_with_sse2_sqrt(oracle, sse2_torch, name, kw):
     b1, b2 = kw.get("betas", (0.9, 0.999))
     mp = np.float32(1.0)
     for k, d in enumerate(deltas):
-        common = dict(step=float(k + 1), torch_cpu_sqrt="torch_cpu_sse2", lr=kw["lr"])
+        common = dict(step=float(k + 1), torch_cpu_sqrt="torch_cpu_amd", rsqrtps=here_rsqrtps, lr=kw["lr"])
         if name in ("Adam", "AdamW"):
             oracle.epilogue_apply(d, oracle.EPI_ADAM, p=p, m=m, v=v, vmax=x3, beta1=b1, beta2=b2, eps=1e-8,
                                   weight_decay=kw.get("weight_decay", 0.0), decoupled_weight_decay=int(name == "AdamW"),

@@ -2,9 +2,9 @@
 """Writes nvflare_amd/data/sqrt_vectors.npz: the probe nvflare_amd/torch_sqrt.py uses to tell which fp32 sqrt
 this host's torch CPU computes.  Inputs: 6144 fp32 values where torch CPU's AVX-512 vsSqrt (restated by the oracle,
 oracle_sqrt_torch_cpu, pinned against torch in tests/test_torch_sqrt.py) and the correctly rounded sqrt DIFFER
-(spread over 48 binades, subnormals included), plus 2048 where they agree, then 3072 where MKL's SSE2 vsSqrt (the AMD
-hosts' path, oracle_sqrt_mkl_sse2, pinned against MKL's kernel in tests/test_torch_sqrt_sse2.py) differs from both;
-outputs: the three results.
+(spread over 48 binades, subnormals included), plus 2048 where they agree, then 3072 where the AMD hosts' vsSqrt
+(oracle_sqrt_mkl_rsqrtps with the captured RSQRTPS table, tests/test_torch_sqrt_amd.py) differs from both; outputs:
+the three results.
 
   python tools/make_sqrt_vectors.py          (test infrastructure: run where the oracle is built)
 """
@@ -37,16 +37,16 @@ def main():
         picked_same.append(x[~d][:40])
     x = np.concatenate(picked_diff + picked_same + [np.array([0.0, 1.0, 4.0, 0.25, 2.0, 3.4e38, 1e-45], np.float32)])
     rng2 = np.random.default_rng(20261018)
-    picked_sse2 = []
+    picked_amd = []
     for e in range(-40, 8):
         bits = (np.uint32((e + 127) << 23) | rng2.integers(0, 1 << 23, 20_000, dtype=np.uint32)).astype(np.uint32)
         y = bits.view(np.float32)
-        c = orc.sqrt_torch_cpu_sse2(y).view(np.uint32)
+        c = orc.sqrt_torch_cpu_amd(y).view(np.uint32)
         d = (c != np.sqrt(y).view(np.uint32)) & (c != orc.sqrt_torch_cpu(y).view(np.uint32))
-        picked_sse2.append(y[d][:64])
-    x = np.concatenate([x] + picked_sse2)
+        picked_amd.append(y[d][:64])
+    x = np.concatenate([x] + picked_amd)
     out = os.path.join(ROOT, "nvflare_amd", "data", "sqrt_vectors.npz")
-    np.savez(out, x=x, torch_cpu=orc.sqrt_torch_cpu(x), torch_cpu_sse2=orc.sqrt_torch_cpu_sse2(x), ieee=np.sqrt(x))
+    np.savez(out, x=x, torch_cpu=orc.sqrt_torch_cpu(x), torch_cpu_amd=orc.sqrt_torch_cpu_amd(x), ieee=np.sqrt(x))
     print(out, x.size, int(np.count_nonzero(orc.sqrt_torch_cpu(x).view(np.uint32) != np.sqrt(x).view(np.uint32))))
 
 

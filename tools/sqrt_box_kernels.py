@@ -3,12 +3,14 @@
 
 Calls every single-precision vsSqrt kernel the libtorch_cpu of this torch exports (mkl_vml_kernel_sSqrt_{E2,EX,H8,
 L9,Z0}{HA,LA,EP}) on tools/sqrt_probe.py's 59.8 M inputs ON THIS HOST, and counts where each differs from this host's
-torch.sqrt; also the oracle's restatements (AVX-512: oracle_sqrt_torch_cpu, SSE2: oracle_sqrt_mkl_sse2) by input class.
+torch.sqrt; also the oracle's restatements (AVX-512: oracle_sqrt_torch_cpu, AMD: oracle_sqrt_mkl_rsqrtps with the
+captured table, SSE2: oracle_sqrt_mkl_sse2) by input class.
 Kernels built on approximate instructions (rcpps / rsqrtps) can give other bits on another CPU vendor, so this must
 run where the question is asked.
 
   python tools/sqrt_box_kernels.py OUT_DIR     writes OUT_DIR/sqrt_box_kernels.json and, for [1, 4), the inputs
                                                where torch differs from the SSE2 restatement (sse2_misses_1_4.npz)
+                                               and from the AMD one (amd_misses_1_4.npz)
 """
 
 import ctypes
@@ -64,16 +66,17 @@ def main():
     b = x.view(np.uint32)
     classes = {"subnormal": (b > 0) & (b < 0x00800000), "normal_lt_2m96": (b >= 0x00800000) & (x < 2.0 ** -96),
                "normal_ge_2m96": (x >= 2.0 ** -96) & (b < 0x7F800000), "one_to_four": (x >= 1) & (x < 4)}
-    for label, fn in (("sse2_restated", orc.sqrt_torch_cpu_sse2), ("avx512_restated", orc.sqrt_torch_cpu)):
+    for label, fn in (("sse2_restated", orc.sqrt_torch_cpu_sse2), ("amd_restated", orc.sqrt_torch_cpu_amd),
+                      ("avx512_restated", orc.sqrt_torch_cpu)):
         with np.errstate(invalid="ignore"):
             r = fn(x)
         d = differ(r, t)
         rec[label] = {"vs_torch": int(d.sum()), **{k: int((d & m).sum()) for k, m in classes.items()}}
         print(label, rec[label], flush=True)
-        if label == "sse2_restated":
+        if label in ("sse2_restated", "amd_restated"):
             sel = d & classes["one_to_four"]
-            np.savez_compressed(os.path.join(out_dir, "sse2_misses_1_4.npz"), x=b[sel], torch=t.view(np.uint32)[sel],
-                                restated=r.view(np.uint32)[sel])
+            np.savez_compressed(os.path.join(out_dir, f"{label[:-9]}_misses_1_4.npz"), x=b[sel],
+                                torch=t.view(np.uint32)[sel], restated=r.view(np.uint32)[sel])
     with open(os.path.join(out_dir, "sqrt_box_kernels.json"), "w") as f:
         json.dump(rec, f, indent=1)
 

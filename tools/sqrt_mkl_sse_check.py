@@ -1,11 +1,14 @@
 #!/usr/bin/env python3
-"""Check the oracle's restatement of MKL's SSE2 vsSqrt (oracle_sqrt_mkl_sse2, the sqrt torch CPU computes on the GPU
-pool's AMD hosts) exhaustively -- diagnostic, not part of the product.
+"""Check the oracle's restatements of MKL's SSE vsSqrt kernels exhaustively -- diagnostic, not part of the product.
 
-  python tools/sqrt_mkl_sse2_check.py kernel [--stride S]   against mkl_vml_kernel_sSqrt_E2HAynn itself, called from
-                                                            the libtorch_cpu this torch ships (any x86-64 host)
-  python tools/sqrt_mkl_sse2_check.py torch [--stride S]    against this host's torch.sqrt (the AMD box: which path
-                                                            MKL dispatches there)
+  python tools/sqrt_mkl_sse2_check.py kernel [--stride S]   oracle_sqrt_mkl_sse2 against mkl_vml_kernel_sSqrt_E2HAynn
+                                                            itself, called from the libtorch_cpu this torch ships
+  python tools/sqrt_mkl_sse2_check.py ex --rsqrtps DUMP     oracle_sqrt_mkl_rsqrtps with THIS CPU's RSQRTPS table
+                                                            (a tools/rsqrtps_dump.c dump made here) against
+                                                            mkl_vml_kernel_sSqrt_EXHAynn run here
+  python tools/sqrt_mkl_sse2_check.py torch [--stride S]    oracle_sqrt_mkl_rsqrtps with the AMD host's table
+                                                            (nvflare_amd/data/rsqrtps_amd.bin) against this host's
+                                                            torch.sqrt (run it on the AMD box)
 
 Every fp32 bit pattern (or every S-th) in chunks of 2^24; NaN results compare as NaN.  Prints one JSON line per
 input class and a summary.
@@ -22,14 +25,15 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tools"))
 CHUNK = 1 << 24
 
 
-def mkl_kernel():
+def mkl_kernel(name):
     import torch
 
     lib = ctypes.CDLL(os.path.join(os.path.dirname(torch.__file__), "lib", "libtorch_cpu.so"))
-    fn = lib.mkl_vml_kernel_sSqrt_E2HAynn
+    fn = getattr(lib, name)
     fn.restype = None
     fn.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
     return fn
@@ -44,7 +48,7 @@ def classify(bits):
 
 
 def work(job):
-    i, stride, against = job
+    i, stride, against, dump = job
     import torch
 
     from oracle import fedavg_oracle as orc
@@ -52,12 +56,18 @@ def work(job):
     torch.set_num_threads(1)
     bits = ((np.uint64(i) * CHUNK + np.arange(0, CHUNK, stride, dtype=np.uint64)) & 0xFFFFFFFF).astype(np.uint32)
     x = bits.view(np.float32)
-    if against == "kernel":
+    if against in ("kernel", "ex"):
         got = np.empty_like(x)
-        mkl_kernel()(x.size, x.ctypes.data, got.ctypes.data)
+        mkl_kernel("mkl_vml_kernel_sSqrt_E2HAynn" if against == "kernel" else "mkl_vml_kernel_sSqrt_EXHAynn")(
+            x.size, x.ctypes.data, got.ctypes.data)
     else:
         got = torch.from_numpy(x.copy()).sqrt().numpy()
-    want = orc.sqrt_torch_cpu_sse2(x)
+    if against == "kernel":
+        want = orc.sqrt_torch_cpu_sse2(x)
+    else:
+        import make_rsqrtps_table
+
+        want = orc.sqrt_torch_cpu_amd(x, make_rsqrtps_table.table_from_dump(dump) if dump else None)
     with np.errstate(invalid="ignore"):
         cr = np.sqrt(x)
     both_nan = np.isnan(got) & np.isnan(want)
@@ -75,7 +85,8 @@ def work(job):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("against", choices=["kernel", "torch"])
+    ap.add_argument("against", choices=["kernel", "ex", "torch"])
+    ap.add_argument("--rsqrtps", default=None, help="tools/rsqrtps_dump.c dump of this CPU (for 'ex')")
     ap.add_argument("--stride", type=int, default=1)
     ap.add_argument("--workers", type=int, default=8)
     args = ap.parse_args()
@@ -83,13 +94,16 @@ def main():
     tot = np.zeros((4, 3), np.int64)
     examples = []
     with Pool(args.workers) as pool:
-        for i, out, ex in pool.imap_unordered(work, [(i, args.stride, args.against) for i in range(256)]):
+        for i, out, ex in pool.imap_unordered(work, [(i, args.stride, args.against, args.rsqrtps) for i in range(256)]):
             tot += np.array(out)
             examples += ex
     for c, name in enumerate(names):
         print(json.dumps({"class": name, "inputs": int(tot[c, 0]), "mismatches_vs_restatement": int(tot[c, 1]),
                           "differ_from_correctly_rounded": int(tot[c, 2])}))
-    print(json.dumps({"summary": f"oracle_sqrt_mkl_sse2 vs {'MKL E2HA kernel' if args.against == 'kernel' else 'torch.sqrt'}",
+    what = {"kernel": "oracle_sqrt_mkl_sse2 vs MKL's E2HA kernel",
+            "ex": "oracle_sqrt_mkl_rsqrtps (this CPU's table) vs MKL's EXHA kernel",
+            "torch": "oracle_sqrt_mkl_rsqrtps (AMD table) vs torch.sqrt"}[args.against]
+    print(json.dumps({"summary": what,
                       "inputs": int(tot[:, 0].sum()), "mismatches": int(tot[:, 1].sum()), "stride": args.stride,
                       "examples": examples[:10]}), flush=True)
     return 1 if tot[:, 1].sum() else 0
