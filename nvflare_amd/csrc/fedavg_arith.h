@@ -231,8 +231,11 @@ __device__ __forceinline__ float sqrt_mkl_rsqrtps(const float x) {
     const float r = 0.5f - s * h;
     const float s1 = s * r + s;
     const float h1 = h * r + h;
-    const float res = (x - s1 * s1) * h1 + s1;
-    return b - 0x00800000u <= 0x7F7FF000u - 0x00800000u ? res : __builtin_sqrtf(x);
+    float res = (x - s1 * s1) * h1 + s1;
+    // the callout (zero, subnormals, the top 4095 finite values, inf, NaN, negatives) as a branch the waves skip
+    // unless one of their lanes needs it: the correctly rounded sqrt is more instructions than the refinement
+    if (__builtin_expect(b - 0x00800000u > 0x7F7FF000u - 0x00800000u, 0)) res = __builtin_sqrtf(x);
+    return res;
 }
 
 }  // namespace fedavg
