@@ -24,7 +24,8 @@ EPI_UNITS = [(f"{mode}_{fin}", op, fin_v) for mode, op in (("torch", 1), ("numpy
              for fin, fin_v in (("div", 2), ("scale", 1), ("none", 0))]
 SOURCES = [EPI_SOURCE, "fedavg_tiles_numpy.hip", "fedavg_tiles_torch.hip", "fedavg_tiles_unweighted.hip",
            "fedavg_kernels.hip", "fedavg_narrow.hip", "fedavg_dequant.hip", "fedavg_capi.cpp"]
-HEADERS = ["fedavg_internal.h", "fedavg_rsqrt14.h", "fedavg_arith.h", "fedavg_tiles.h", "fedavg_epi.h"]
+HEADERS = ["fedavg_internal.h", "fedavg_rsqrt14.h", "fedavg_rsqrtps_amd.h", "fedavg_arith.h", "fedavg_tiles.h",
+           "fedavg_epi.h"]
 OBJ_DIR = os.path.join(PKG, "lib", "obj")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
@@ -52,6 +53,25 @@ def needs_build() -> bool:
     return any(os.path.getmtime(f) > t for f in _inputs())
 
 
+def compile_units(sources=SOURCES):
+    """(source, object name, extra flags) of every translation unit: the fused kernels' source once per EPI_UNITS
+    entry, the others once each."""
+    units = []
+    for src in sources:
+        if src == EPI_SOURCE:
+            units += [(src, f"fedavg_epi_{name}.hip.o",
+                       [f"-DFEDAVG_EPI_OP={op}", f"-DFEDAVG_EPI_FIN={fin}", f"-DFEDAVG_EPI_FN=launch_epi_{name}"])
+                      for name, op, fin in EPI_UNITS]
+        else:
+            units.append((src, src + ".o", []))
+    return units
+
+
+# every symbol must resolve at link time: a translation unit missing from the link fails the build, not the first
+# dlopen on the GPU box
+LINK_FLAGS = ["-shared", "-fPIC", f"--offload-arch={ARCH}", "-Wl,--no-undefined"]
+
+
 def build_library(force: bool = False, verbose: bool = False, jobs: int = 0) -> str:
     if not force and not needs_build():
         return LIB_PATH
@@ -62,14 +82,7 @@ def build_library(force: bool = False, verbose: bool = False, jobs: int = 0) -> 
                                                           os.path.abspath(__file__)]
     newest_header = max(os.path.getmtime(h) for h in headers)  # any header (or a flag change) rebuilds all
 
-    units = []  # (source, object, extra flags)
-    for src in SOURCES:
-        if src == EPI_SOURCE:
-            units += [(src, f"fedavg_epi_{name}.hip.o",
-                       [f"-DFEDAVG_EPI_OP={op}", f"-DFEDAVG_EPI_FIN={fin}", f"-DFEDAVG_EPI_FN=launch_epi_{name}"])
-                      for name, op, fin in EPI_UNITS]
-        else:
-            units.append((src, src + ".o", []))
+    units = compile_units()
 
     def compile_one(unit) -> str:
         src, obj_name, extra = unit
@@ -87,7 +100,7 @@ def build_library(force: bool = False, verbose: bool = False, jobs: int = 0) -> 
     with ThreadPoolExecutor(max_workers=jobs) as pool:
         objs = list(pool.map(compile_one, units))
     tmp = LIB_PATH + ".tmp"
-    cmd = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-o", tmp, "-lpthread"]
+    cmd = [HIPCC, *LINK_FLAGS, *objs, "-o", tmp, "-lpthread"]
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)

@@ -6,7 +6,8 @@
   python tools/build_rev_lib.py --rev WORKTREE -D FEDAVG_NARROW_UNROLL=8 --out nvflare_amd/lib/ab/u8.so
 
 The revision's csrc/ and include/ are exported to a temporary directory with ``git show``; the flags and
-source list are the current nvflare_amd/_build.py's (the A/B compares kernels, not build settings)."""
+source list (with the fused kernels' per-unit definitions) are the current nvflare_amd/_build.py's (the A/B
+compares kernels, not build settings)."""
 
 import argparse
 import os
@@ -49,19 +50,19 @@ def main():
             _export(args.rev, "include", tmp)
         csrc = os.path.join(tmp, "nvflare_amd", "csrc")
         inc = [f"-I{os.path.join(tmp, 'include')}", f"-I{csrc}"]
-        srcs = [s for s in B.SOURCES if os.path.exists(os.path.join(csrc, s))]
+        units = B.compile_units([s for s in B.SOURCES if os.path.exists(os.path.join(csrc, s))])
 
-        def compile_one(src):
-            obj = os.path.join(tmp, src + ".o")
+        def compile_one(unit):
+            src, obj_name, extra = unit
+            obj = os.path.join(tmp, obj_name)
             defs = [f"-D{d}" for d in args.defines]
-            subprocess.run([B.HIPCC, *B.FLAGS, *defs, *inc, "-c", os.path.join(csrc, src), "-o", obj], check=True)
+            subprocess.run([B.HIPCC, *B.FLAGS, *extra, *defs, *inc, "-c", os.path.join(csrc, src), "-o", obj], check=True)
             return obj
 
-        with ThreadPoolExecutor(max_workers=min(8, len(srcs))) as pool:
-            objs = list(pool.map(compile_one, srcs))
+        with ThreadPoolExecutor(max_workers=min(8, len(units))) as pool:
+            objs = list(pool.map(compile_one, units))
         os.makedirs(os.path.dirname(os.path.abspath(args.out)), exist_ok=True)
-        subprocess.run([B.HIPCC, "-shared", "-fPIC", f"--offload-arch={B.ARCH}", *objs, "-o", args.out, "-lpthread"],
-                       check=True)
+        subprocess.run([B.HIPCC, *B.LINK_FLAGS, *objs, "-o", args.out, "-lpthread"], check=True)
     print(args.out)
 
 
