@@ -296,15 +296,10 @@ fedavg_tiles_epi_burst_f32x4(const RowTableF32 tab, const int K, const int64_t t
             for (int c = 0; c < CPL; ++c) staged[((m - TPB) * CPL + c) * kBlock + threadIdx.x] = fin4<FIN>(acc[c], fin_val);
         }
     }
-    // Epilogue phase, software-pipelined: the operand loads of the next AHEAD tiles are in flight while tile m's
-    // arithmetic and stores run (program order keeps them ahead of those stores, which may alias nothing they read
-    // but the compiler cannot know).  AHEAD = 2 in the one-block-per-CU form (9 LDS tiles): with one wave per SIMD,
-    // one tile of operands in flight per wave (48 KiB per CU for Adam) is below what HBM latency needs at the CU's
-    // share of the bandwidth.  AHEAD = 1 in the two-block forms, where the other block covers it and the extra
-    // registers (64 VGPRs for Adam) would cost the second block its place.  Loads are unconditional at a clamped
-    // in-range address so the waits count whole tiles' loads; only in-range columns of real tiles are computed
-    // and stored.
-    constexpr int AHEAD = TPB_LDS >= kBurstEpiLdsTilesWide ? 2 : 1;
+    // Epilogue phase, double-buffered: tile m+1's operand loads are issued before tile m's arithmetic and
+    // stores (program order keeps them ahead of those stores, which may alias nothing they read but the
+    // compiler cannot know).  Loads are unconditional at a clamped in-range address so the waits count
+    // exactly one tile's loads; only in-range columns of real tiles are computed and stored.
     const int64_t t_base = t0 + blockIdx.x;
     const int64_t t_cap = t_end - 1;
     auto operands = [&](EpiIn (&in)[CPL], const int m) __attribute__((always_inline)) {
@@ -320,24 +315,8 @@ fedavg_tiles_epi_burst_f32x4(const RowTableF32 tab, const int K, const int64_t t
     // cur / nxt with static indices only (a pre[m & 1] buffer in the rolled LDS-tile loop, or in an epilogue too
     // large for the compiler to unroll fully, went to scratch memory: 528 bytes per lane for Adam with the restated
     // torch sqrt)
-    EpiIn cur[CPL], nxt[CPL], nx2[CPL];
+    EpiIn cur[CPL], nxt[CPL];
     operands(cur, 0);
-    if (AHEAD == 2 && NT > 1) operands(nxt, 1);
-    // before tile m: issue tile m + AHEAD's loads; after it, shift the buffers
-    auto prefetch = [&](const int m) __attribute__((always_inline)) {
-        if constexpr (AHEAD == 2) {
-            if (m + 2 < NT) operands(nx2, m + 2);
-        } else {
-            if (m + 1 < NT) operands(nxt, m + 1);
-        }
-    };
-    auto shift = [&]() __attribute__((always_inline)) {
-#pragma unroll
-        for (int c = 0; c < CPL; ++c) {
-            cur[c] = nxt[c];
-            if constexpr (AHEAD == 2) nxt[c] = nx2[c];
-        }
-    };
     auto tile_epilogue = [&](const int m, const int64_t t, auto&& d_of) __attribute__((always_inline)) {
         if (t < t_end) {
 #pragma unroll
@@ -353,18 +332,20 @@ fedavg_tiles_epi_burst_f32x4(const RowTableF32 tab, const int K, const int64_t t
     };
 #pragma unroll
     for (int m = 0; m < TPB; ++m) {
-        prefetch(m);
+        if (m + 1 < NT) operands(nxt, m + 1);
         tile_epilogue(m, t_base + (int64_t)m * gridDim.x, [&](int c) __attribute__((always_inline)) { return dd[m][c]; });
-        shift();
+#pragma unroll
+        for (int c = 0; c < CPL; ++c) cur[c] = nxt[c];
     }
 #pragma unroll 1
     for (int m = TPB; m < NT; ++m) {
-        prefetch(m);
+        if (m + 1 < NT) operands(nxt, m + 1);
         tile_epilogue(m, t_base + (int64_t)m * gridDim.x,
                       [&](int c) __attribute__((always_inline)) {
                           return staged[((m - TPB) * CPL + c) * kBlock + threadIdx.x];
                       });
-        shift();
+#pragma unroll
+        for (int c = 0; c < CPL; ++c) cur[c] = nxt[c];
     }
 }
 
