@@ -24,6 +24,7 @@ documented sqrt bound)."""
 
 from __future__ import annotations
 
+import logging
 import os
 import threading
 from typing import Optional
@@ -37,6 +38,7 @@ MODES = ("torch_cpu", "torch_cpu_amd", "ieee")
 
 _lock = threading.RLock()
 _detected: Optional[str] = None
+_warned = False
 _table: Optional[np.ndarray] = None
 
 
@@ -74,7 +76,17 @@ def mode() -> str:
     if env != "auto":
         raise ValueError(f"NVFLARE_AMD_TORCH_SQRT={env!r}: expected torch_cpu, torch_cpu_amd, ieee or auto")
     d = detect()
-    return d if d in MODES else "ieee"
+    if d in MODES:
+        return d
+    global _warned
+    with _lock:
+        if not _warned:
+            _warned = True
+            logging.getLogger(__name__).warning(
+                "torch CPU's sqrt on this host matches none of the restated paths (%s); the device server optimizer "
+                "uses the correctly rounded sqrt, so Adam-family parameters can differ from torch's by a few ulp "
+                "(capture this CPU's RSQRTPS with tools/rsqrtps_dump.c to add its path)", ", ".join(MODES[:-1]))
+    return "ieee"
 
 
 def epilogue_flag(sqrt_mode: Optional[str] = None) -> int:
