@@ -165,9 +165,10 @@ __device__ __forceinline__ void tile_sum(f32x4 (&acc)[CPL], const RowTableF32& t
 // rsqrt14 depends on the exponent parity and the top 15 mantissa bits; mantissa bits 22..7 of the estimate for x in
 // [1, 4) are 32 exact fixed-point lines per parity (fedavg_rsqrt14.h, generated from the captured instruction table
 // nvflare_amd/data/rsqrt14_avx512.bin), a power of four giving its exact root.  Inputs below 2^-96 run at x * 2^64
-// and are scaled back by 2^-32 (no subnormal residual); 0, inf, NaN and negatives are IEEE (v_sqrt_f32 is exact
-// on them).  Branch-free; per sqrt one 8-byte LDS read of the staged segment table (rsqrt14_stage) and one integer
-// multiply-add.  (The first form gathered 2 bytes per sqrt from a 128 KiB device table: fused Adam at config 5 ran
+// and are scaled back by 2^-32 (no subnormal residual); 0, inf, NaN and negatives take the correctly rounded sqrt
+// (a branch the waves skip unless a lane needs it: the raw v_sqrt_f32 it replaced flushed negative subnormals to -0
+// where torch returns NaN -- tools/sqrt_device_exhaustive.py over all 2^32 inputs).  Per sqrt one 8-byte LDS read of
+// the staged segment table (rsqrt14_stage) and one integer multiply-add.  (The first form gathered 2 bytes per sqrt from a 128 KiB device table: fused Adam at config 5 ran
 // 81.3 % of HBM peak against 87.3 % with the correctly rounded sqrt; the same segments read from global memory,
 // 83.3 %: profiles/r03/s4, s5.)
 __shared__ uint2 g_rsqrt14_lds[64];  // {kRsqrt14Base, kRsqrt14Slope}[segment]
@@ -194,7 +195,9 @@ __device__ __forceinline__ float sqrt_torch_cpu(const float x) {
     const float s = xs * y;
     const float r = __builtin_fmaf(-s, s, xs);
     const float res = __builtin_fmaf(r, 0.5f * y, s);
-    return special ? __builtin_amdgcn_sqrtf(x) : (tiny ? res * 0x1p-32f : res);
+    float out = tiny ? res * 0x1p-32f : res;
+    if (__builtin_expect(special, 0)) out = __builtin_sqrtf(x);
+    return out;
 }
 
 // torch CPU's fp32 Tensor.sqrt on the GPU pool's AMD EPYC hosts (EpiParams.torch_sqrt == FEDAVG_SQRT_TORCH_AMD): MKL

@@ -76,6 +76,21 @@ def test_device_sqrt_matches_restatement_everywhere(ctx, oracle):
             assert _same(got if here == "torch_cpu" else amd, torch.from_numpy(x.copy()).sqrt().numpy()) == 0
 
 
+def test_device_sqrt_specials_every_mode(ctx, oracle):
+    """Every positive and negative subnormal, zeros, the top 4096 finite values, inf, NaN and negatives through each
+    mode's device sqrt against the oracle (NaN-aware).  Torch returns NaN for a negative subnormal (RMSprop's centered
+    ``square_avg - grad_avg**2`` can round to one) where the raw v_sqrt_f32 the Intel-host form once used for its
+    specials gave -0: tools/sqrt_device_exhaustive.py found those 8,388,607 inputs over all 2^32."""
+    neg_sub = np.uint32(0x80000000) | np.arange(1, 1 << 23, dtype=np.uint32)
+    pos_sub = np.arange(0, 1 << 23, dtype=np.uint32)
+    top = np.arange(0x7F7FF000, 0x7F800001, dtype=np.uint32)
+    misc = np.array([0x80000000, 0xFF800000, 0x7FC00000, 0xFFC00000, 0xBF800000, 0x80800000, 0xC0800000], np.uint32)
+    x = np.concatenate([neg_sub, pos_sub, top, misc]).view(np.float32)
+    for mode, fn in ((0, np.sqrt), (1, oracle.sqrt_torch_cpu), (2, oracle.sqrt_torch_cpu_amd)):
+        with np.errstate(invalid="ignore"):
+            assert _same(_device_sqrt(ctx, x, mode), fn(x)) == 0, mode
+
+
 class _Dev:
     def __init__(self, ctx, rows, n):
         from nvflare_amd.device import TiledLayout
