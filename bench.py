@@ -19,8 +19,9 @@ config 4 once more as a multi-GPU server would ingest it ("4x": client g's whole
 all-to-all of the buckets overlapped with the kernels, nvflare_amd/client_shards.py; serial and overlapped device
 times side by side, under a watchdog so a stuck collective cannot cost the line), and config 2 once more as the
 server receives it ("2h": pageable host arrays through the drop-in helper's add / get_result, H2D and D2H included --
-north_star's PCIe-inclusive rate, each rank on its own GPU and PCIe link), and embeds them in the line's ``also``
-list -- so one N-GPU run records configs 2, 3, 4 and 5 at that N.
+north_star's PCIe-inclusive rate, each rank on its own GPU and PCIe link; "2s": the same round in ONE process whose
+helper splits every key over all N GPUs, as a single NVFlare server process drives a node), and embeds them in the
+line's ``also`` list -- so one N-GPU run records configs 2, 3, 4 and 5 at that N.
 
 Prints ONE JSON line (rank 0).  value = GiB/s aggregated = 4*K*P_total*steps / t / 2^30 with t the max over
 ranks of the barrier+synchronize bracketed wall time (P_total = P*N weak, P strong).  roofline.achieved uses the
@@ -60,6 +61,7 @@ PRESET_NAMES = {
 }
 CLIENT_SHARDED = 40  # --also token "4x": config 4 through the client-sharded exchange (run_client_sharded)
 HOST_RESIDENT = 20  # --also token "2h": config 2 with host-resident updates and result (run_host_resident)
+HOST_SHARDED = 21  # --also token "2s": the same round in ONE process over all N GPUs' buckets (run_host_resident)
 WATCHDOG_S = 240.0  # each guarded entry's limit: a stuck collective must not cost the measured line
 EPI_STATE_BYTES = {"none": 4.0, "add_base": 8.0, "sgd": 16.0}  # per param beyond the 4*K client reads; else 24
 HEADROOM = 2 << 30  # device bytes left free beside a workload (runtime, gather buffers)
@@ -80,8 +82,9 @@ def parse(argv=None):
     ap.add_argument("--also", default="auto",
                     help="extra strong-scaling BASELINE configs measured after the main one, in the same line "
                          "(comma list of 4 / 5 / 4x = config 4 through the client-sharded RCCL exchange / "
-                         "2h = config 2 from host-resident updates to a host result, PCIe included; "
-                         "'auto' = 5,4,2h,4x for the default config 3 run; 'none')")
+                         "2h = config 2 from host-resident updates to a host result, PCIe included, every rank / "
+                         "2s = the same round in one process over all N GPUs' parameter buckets; "
+                         "'auto' = 5,4,2h,2s,4x for the default config 3 run; 'none')")
     ap.add_argument("--client-sharded-params", type=float, default=None,
                     help="model size of the 4x entry (default: config 4's 350M; smaller for one-GPU rehearsals)")
     ap.add_argument("--host-resident-params", type=float, default=None,
@@ -119,8 +122,8 @@ def parse(argv=None):
                    for f in ("--clients", "--params", "--global-params", "--scaling", "--epilogue"))
     args.preset_exact = not explicit
     if args.also == "auto":
-        args.also = "5,4,2h,4x" if (args.config == 3 and not explicit) else "none"
-    tokens = {"4x": CLIENT_SHARDED, "2h": HOST_RESIDENT}
+        args.also = "5,4,2h,2s,4x" if (args.config == 3 and not explicit) else "none"
+    tokens = {"4x": CLIENT_SHARDED, "2h": HOST_RESIDENT, "2s": HOST_SHARDED}
     args.also = [] if args.also in ("", "none") else [tokens.get(x.strip()) or int(x) for x in args.also.split(",")]
     return args
 
@@ -528,24 +531,39 @@ def run_client_sharded(args, world, rank, local, K, P, seed):
         torch.cuda.empty_cache()
 
 
-def run_host_resident(args, world, rank, local, K, P, seed):
+def run_host_resident(args, world, rank, local, K, P, seed, sharded=False):
     """BASELINE config 2 as the server receives it (north_star's PCIe-inclusive rate): the K client updates are
     pageable numpy arrays in HOST memory (what the comm layer's decoder hands over), each goes through the drop-in
     WeightedAggregationHelper.add (weighted_aggregation_helper.py:153-224; the engine packs it through its pinned
     ring and H2D-copies it into the tiled slab) and get_result (:226-240; kernel + D2H into a new host array).
-    One step = one round: K adds + get_result.  Weak scaling: every rank runs its own config-2 round on its own GPU
-    and PCIe link, so value = 4*K*P*N per step.  The whole result of the last step is compared with the oracle."""
+    One step = one round: K adds + get_result.  The whole result of the last step is compared with the oracle.
+
+    2h (sharded=False), weak scaling: every rank runs its own config-2 round on its own GPU and PCIe link, so
+    value = 4*K*P*N per step.  2s (sharded=True), strong scaling: rank 0 alone runs the round as ONE NVFlare server
+    process would on an N-GPU node -- WeightedAggregationHelper(devices=[0..N-1]), every key split into N parameter
+    buckets (sharding.ShardedFedAvg), bucket b of each client H2D-copied to GPU b over its own link by its own thread,
+    the result buckets D2H-copied straight into one host array -- while the other ranks wait; value = 4*K*P per step."""
     import torch
+
+    if sharded and world < 2:
+        return {"skipped": "one process over N GPUs' buckets needs >= 2 GPUs (at N = 1 it is the 2h entry)"}
+    active = rank == 0 or not sharded
 
     # three untimed rounds: the engine's page-locked result arrays are reused from round r - 2 on (the previous
     # round's result is still referenced by the caller, device.HostArenaPool), the steady state of a multi-round job
     steps, warmup = max(1, min(args.steps, 5)), 3
-    rng = np.random.default_rng(seed + 101 * rank)
-    base = rng.standard_normal(P, dtype=np.float32)
-    clients = [base * np.float32(1.0 + 0.01 * k) for k in range(K)]  # K distinct pageable host updates
     weights = synth_weights(K)
-    helper = make_host_helper(local)
-    t_accept, out = 0.0, None
+    clients, helper = [], None
+    if active:
+        rng = np.random.default_rng(seed + 101 * rank)
+        base = rng.standard_normal(P, dtype=np.float32)
+        clients = [base * np.float32(1.0 + 0.01 * k) for k in range(K)]  # K distinct pageable host updates
+        if sharded:
+            shared = os.environ.get("NVFLARE_AMD_BENCH_SHARED_DEVICE") == "1"  # the one-GPU rehearsal
+            helper = make_host_helper(local, devices=[0] * world if shared else list(range(world)))
+        else:
+            helper = make_host_helper(local)
+    t_accept, out, elapsed = 0.0, None, 0.0
     try:
         def one_round(r):
             a0 = time.perf_counter()
@@ -555,19 +573,20 @@ def run_host_resident(args, world, rank, local, K, P, seed):
             res = helper.get_result()["w"]
             return res, a1 - a0
 
-        for r in range(warmup):
+        for r in range(warmup if active else 0):
             one_round(r)
         device_sync()
         dist_barrier(world)
         t0 = time.perf_counter()
-        for r in range(steps):
+        for r in range(steps if active else 0):
             out, dt = one_round(warmup + r)
             t_accept += dt
         device_sync()
+        elapsed = time.perf_counter() - t0
         dist_barrier(world)
-        wall = max_over_ranks(world, time.perf_counter() - t0)
+        wall = max_over_ranks(world, elapsed)
         sc = None
-        if args.spot_check > 0:
+        if args.spot_check > 0 and active:
             sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
             from oracle import fedavg_oracle as orc
 
@@ -575,24 +594,26 @@ def run_host_resident(args, world, rank, local, K, P, seed):
             want = orc.fedavg_c(clients, weights, orc.MODE_NUMPY, nthreads=threads)
             sc = [int(want.size), int(np.count_nonzero(np.asarray(out).view(np.uint32) != want.view(np.uint32)))]
         sampled, mism = sum_over_ranks(world, sc or [0, 0])
-        return {"K": K, "P": P, "wall": wall, "steps": steps, "warmup": warmup,
+        return {"K": K, "P": P, "wall": wall, "steps": steps, "warmup": warmup, "sharded": sharded,
                 "accept_s": max_over_ranks(world, t_accept / steps),
-                "result_type": type(out).__name__,
-                "spot_check": {"compared": sampled, "mismatches": mism, "ranks": world,
+                "result_type": type(out).__name__ if active else None,
+                "devices": len(helper.engine.engines) if sharded and active else 1,
+                "spot_check": {"compared": sampled, "mismatches": mism, "ranks": 1 if sharded else world,
                                "oracle": "oracle/fedavg_oracle.c (every element of the last round's result)"}
-                if sc is not None else None}
+                if args.spot_check > 0 else None}
     finally:
-        helper.reset_stats()
+        if helper is not None:
+            helper.reset_stats()
         del helper, clients
         if torch.cuda.is_available():
             torch.cuda.empty_cache()
 
 
-def make_host_helper(local):
-    """The drop-in helper the 2h entry drives (a seam for the CPU tests' fake device)."""
+def make_host_helper(local, devices=None):
+    """The drop-in helper the 2h / 2s entries drive (a seam for the CPU tests' fake device)."""
     from nvflare_amd.app_common.aggregators.weighted_aggregation_helper import WeightedAggregationHelper
 
-    return WeightedAggregationHelper(device=local)
+    return WeightedAggregationHelper(devices=devices) if devices else WeightedAggregationHelper(device=local)
 
 
 def device_sync():
@@ -605,17 +626,23 @@ def device_sync():
 def summarize_host_resident(args, world, r):
     step_s = r["wall"] / r["steps"]
     exact = r["K"] == PRESETS[2]["clients"] and r["P"] == PRESETS[2]["params"]
+    sharded = r["sharded"]
+    per_step_bytes = 4.0 * r["K"] * r["P"] * (1 if sharded else world)
     return {
         "baseline_config": (PRESET_NAMES[2] if exact else f"custom (config 2 with {r['K']} x {r['P']})")
-                           + " -- host-resident updates in, host result out (PCIe-inclusive, the drop-in helper)",
-        "value": round(4.0 * r["K"] * r["P"] * world / step_s / 2**30, 2), "unit": "GiB/s", "n_gpus": world,
-        "scaling": "weak", "steps": r["steps"], "warmup": r["warmup"], "ms_per_step": round(step_s * 1e3, 2),
+                           + (" -- host-resident, ONE server process over all GPUs' parameter buckets (PCIe-inclusive, "
+                              "the drop-in helper with devices=[0..N-1])" if sharded else
+                              " -- host-resident updates in, host result out (PCIe-inclusive, the drop-in helper)"),
+        "value": round(per_step_bytes / step_s / 2**30, 2), "unit": "GiB/s", "n_gpus": world,
+        "scaling": "strong" if sharded else "weak", "steps": r["steps"], "warmup": r["warmup"],
+        "ms_per_step": round(step_s * 1e3, 2),
         "accept_ms_per_step": round(r["accept_s"] * 1e3, 2),
-        "h2d_GBps_per_gpu": round(4.0 * r["K"] * r["P"] / r["accept_s"] / 1e9, 2),
+        ("h2d_GBps_all_gpus" if sharded else "h2d_GBps_per_gpu"): round(4.0 * r["K"] * r["P"] / r["accept_s"] / 1e9, 2),
         "get_result_ms": round((step_s - r["accept_s"]) * 1e3, 2),
         "spot_check": r["spot_check"],
-        "config": {"clients": r["K"], "params_per_gpu": r["P"], "container": "numpy (pageable)", "keys": 1,
-                   "mode": "numpy", "result": r["result_type"]},
+        "config": {"clients": r["K"], ("params_total" if sharded else "params_per_gpu"): r["P"],
+                   "container": "numpy (pageable)", "keys": 1, "mode": "numpy", "result": r["result_type"],
+                   **({"devices": r["devices"], "process": "rank 0 alone; the other ranks wait"} if sharded else {})},
     }
 
 
@@ -703,8 +730,9 @@ def summarize(args, world, res, K, scaling, epilogue, label):
 
 
 def entry_name(token) -> str:
-    return (PRESET_NAMES[4] + " -- client-sharded ingest" if token == CLIENT_SHARDED
-            else PRESET_NAMES[2] + " -- host-resident")
+    return {CLIENT_SHARDED: PRESET_NAMES[4] + " -- client-sharded ingest",
+            HOST_RESIDENT: PRESET_NAMES[2] + " -- host-resident",
+            HOST_SHARDED: PRESET_NAMES[2] + " -- host-resident, one process over all GPUs"}[token]
 
 
 def guarded_entry(args, world, rank, local, line, also, state, token):
@@ -729,10 +757,10 @@ def guarded_entry(args, world, rank, local, line, also, state, token):
     dog.daemon = True
     dog.start()
     try:
-        if token == HOST_RESIDENT:
+        if token in (HOST_RESIDENT, HOST_SHARDED):
             p = PRESETS[2]
             P = int(args.host_resident_params) if args.host_resident_params else p["params"]
-            r = run_host_resident(args, world, rank, local, p["clients"], P, args.seed)
+            r = run_host_resident(args, world, rank, local, p["clients"], P, args.seed, sharded=token == HOST_SHARDED)
         else:
             p = PRESETS[4]
             P = int(args.client_sharded_params) if args.client_sharded_params else p["params"]
@@ -744,7 +772,7 @@ def guarded_entry(args, world, rank, local, line, also, state, token):
     if rank == 0:
         if "skipped" in r:
             also.append({"baseline_config": entry_name(token), "n_gpus": world, "skipped": r["skipped"]})
-        elif token == HOST_RESIDENT:
+        elif token in (HOST_RESIDENT, HOST_SHARDED):
             also.append(summarize_host_resident(args, world, r))
         else:
             also.append(summarize_client_sharded(args, world, r))
@@ -774,7 +802,7 @@ def main(argv=None):
     also = []
     failed = bool((main_res.get("spot_check") or {}).get("mismatches"))  # counts summed over ranks: all agree
     for cfg in args.also:
-        if cfg in (CLIENT_SHARDED, HOST_RESIDENT):
+        if cfg in (CLIENT_SHARDED, HOST_RESIDENT, HOST_SHARDED):
             continue  # last, each under a watchdog (below)
         p = PRESETS[cfg]
         r = run_workload(args, ctx, world, rank, p["clients"], p["params"], p["scaling"], p["epilogue"],
@@ -812,7 +840,7 @@ def main(argv=None):
         if main_res.get("spot_check") is not None:
             line["spot_check"] = main_res["spot_check"]
     state, dog = {}, None
-    for token in (HOST_RESIDENT, CLIENT_SHARDED):
+    for token in (HOST_RESIDENT, HOST_SHARDED, CLIENT_SHARDED):
         if token in args.also:
             if dog is not None:
                 dog.cancel()

@@ -84,3 +84,22 @@ def test_host_resident_entry_on_fake_device(monkeypatch):
     assert e["spot_check"]["compared"] == 10001 and e["spot_check"]["mismatches"] == 0
     assert e["steps"] == 2 and e["config"]["clients"] == 8 and e["value"] > 0
     assert "host-resident" in e["baseline_config"] and "custom" in e["baseline_config"]
+
+
+def test_host_sharded_entry_needs_two_gpus_and_summarises_strong():
+    """The 2s entry (one process over all N GPUs' buckets) skips at N = 1; its summary counts the model once."""
+    sys.path.insert(0, ROOT)
+    import bench
+
+    args = bench.parse(["--also", "2s", "--host-resident-params", "10001"])
+    also = []
+    failed, dog = bench.guarded_entry(args, 1, 0, 0, {}, also, {}, bench.HOST_SHARDED)
+    dog.cancel()
+    assert failed is False and "needs >= 2 GPUs" in also[0]["skipped"]
+    r = {"K": 8, "P": 1000, "wall": 0.5, "steps": 5, "warmup": 3, "sharded": True, "accept_s": 0.08,
+         "result_type": "ndarray", "devices": 4, "spot_check": None}
+    e = bench.summarize_host_resident(args, 4, r)
+    assert e["scaling"] == "strong" and e["config"]["devices"] == 4 and e["config"]["params_total"] == 1000
+    assert abs(e["value"] - 4.0 * 8 * 1000 / 0.1 / 2**30) < 0.01
+    r["sharded"] = False
+    assert abs(bench.summarize_host_resident(args, 4, r)["value"] - 4 * 4.0 * 8 * 1000 / 0.1 / 2**30) < 0.01

@@ -109,9 +109,10 @@ def test_bench_presets_follow_baseline():
     import bench
 
     a = bench.parse([])
-    assert (a.clients, a.params, a.epilogue, a.scaling, a.also) == (64, 10**9, "none", "weak", [5, 4, bench.HOST_RESIDENT, bench.CLIENT_SHARDED])
+    assert (a.clients, a.params, a.epilogue, a.scaling, a.also) == (64, 10**9, "none", "weak", [5, 4, bench.HOST_RESIDENT, bench.HOST_SHARDED, bench.CLIENT_SHARDED])
     assert bench.parse(["--also", "4x,5"]).also == [bench.CLIENT_SHARDED, 5]
     assert bench.parse(["--also", "2h"]).also == [bench.HOST_RESIDENT]
+    assert bench.parse(["--also", "2s,2h"]).also == [bench.HOST_SHARDED, bench.HOST_RESIDENT]
     assert (lambda c: (c.clients, c.params, c.epilogue, c.scaling))(bench.parse(["--config", "2"])) == \
         (8, 125_000_000, "none", "weak")
     assert (lambda c: (c.clients, c.params, c.epilogue, c.scaling))(bench.parse(["--config", "4"])) == \
