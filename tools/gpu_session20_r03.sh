@@ -6,4 +6,5 @@ mkdir -p "$OUT"
 export TMPDIR=/tmp
 cd "$GRAFT_REPO_ROOT"
 timeout -k 10 180 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > "$OUT/smoke.log" 2>&1
-/usr/bin/time -v timeout -k 10 400 python bench.py > "$OUT/bench.jsonl" 2> "$OUT/bench.err"
+timeout -k 10 400 python bench.py > "$OUT/bench.jsonl" 2> "$OUT/bench.err"
+echo "bench seconds: $SECONDS" > "$OUT/bench_seconds.txt"
