@@ -344,9 +344,11 @@ def pmc_traffic(args, K, P, epilogue):
 
 
 def kernel_name(K, epilogue, variant):
+    # fewer client reads per launch than fedavg_capi.cpp's kBurstMinClients / kEpiBurstMinClients take the
+    # per-tile-store kernels
     if epilogue != "none":
-        return "fedavg_tiles_epi_burst_f32x4" if variant & 12 == 0 else "fedavg_tiles_epi_f32x4"
-    if variant & 11:
+        return "fedavg_tiles_epi_burst_f32x4" if variant & 12 == 0 and K >= 4 else "fedavg_tiles_epi_f32x4"
+    if variant & 11 or K < 4:
         return "fedavg_tiles_f32x4"
     return ("fedavg_tiles_burst_f32x4 (results staged on chip, stored as chip-wide bursts; "
             + ("8 register-held tiles per block per launch)" if variant & 32

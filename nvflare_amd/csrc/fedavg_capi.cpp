@@ -355,6 +355,19 @@ void normalize_wide(int& op, int& fin, double& count, bool acc_f32) {
 //   torch  T.div_(count):     the scalar operand cast to the tensor dtype
 double fin_scalar(int fin, double count) { return fin == FEDAVG_FIN_SCALE ? 1.0 / count : count; }
 
+// Fewest row reads per launch (clients, plus the chained partial sum) that take the burst kernels; fewer go to the
+// per-tile-store kernels (same tile_sum and epilogue arithmetic, so the same bits).  With few reads per result the
+// burst kernel's read phase is too short to pay for holding the results (1e9 params, % of HBM peak, burst vs
+// per-tile, profiles/r03/s24/, s25/): 2 clients 50.7 vs 69.7 %, 3 clients 63.5 vs 71.6 %, 4 clients 70.5 vs 68.9 %
+// on one box and 71.7 vs 73.4 % on another.  The fused epilogue reads and writes its optimizer state in the same
+// launch, so its per-tile form wins further up (Adam, 5e8 params: 1 client 62 vs 73 %, 2: 63.6 vs 77.2 %, 4: 72.9
+// vs 76.2 %), and the burst form wins again from 5 clients on (s26/: Adam 5 / 8 / 16 clients 70.0 / 78.1 / 83.2 vs
+// 68.5 / 69.8 / 71.4 %, SGD 73.8 / 82.7 / 85.7 vs 69.5 / 70.4 / 68.6 %).  The epilogue threshold leaves 4 reads on
+// the burst form, where SGD's larger burst gain was not measured.  The stand-alone server step (no clients, the
+// aggregate as acc_in: one read) takes the per-tile form.
+constexpr int kBurstMinClients = 4;
+constexpr int kEpiBurstMinClients = 4;
+
 // Tile-kernel launches over [b, e) (elements, multiples of 4) for any number of clients: chunks of at
 // most kMaxRowsPerLaunch clients, later chunks continuing in place through `out`.
 void run_tiles(fedavg_ctx* ctx, const void* const* bases, const double* weights, int k_rows, int64_t tile,
@@ -363,24 +376,26 @@ void run_tiles(fedavg_ctx* ctx, const void* const* bases, const double* weights,
     fedavg::TileLaunch L;
     L.op = op;
     L.unroll = ctx->unroll;
-    L.variant = ctx->variant;
     L.tile4 = tile / 4;
     L.tstride4 = tstride / 4;
     L.b4 = b / 4;
     L.e4 = e / 4;
     const int64_t n_tiles = (L.e4 - 1) / L.tile4 - L.b4 / L.tile4 + 1;
-    const bool burst = fedavg::tiles_use_burst(L.tile4, L.unroll, L.variant);
-    const int bpc = burst ? ctx->bpc(k_rows >= fedavg::kBurstOneBlockMinK ? 1 : 2) : ctx->bpc();
-    // one block per CU: the burst kernel holds 10 tiles in LDS (all 160 KiB); public bit 6 keeps the 4-tile form,
-    // public bit 5 (register-held tiles only) keeps no LDS tiles at all
-    const bool wide = burst && bpc == 1 && !(ctx->variant & (fedavg::kVariantWideLds | fedavg::kVariantRegisterTiles));
-    L.variant = (ctx->variant & ~fedavg::kVariantWideLds) | (wide ? fedavg::kVariantWideLds : 0);
-    L.grid = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)ctx->num_cus * bpc, n_tiles));
     const float fv = (float)fin_scalar(fin, count);
     int k0 = 0;
     const float* cur_in = acc_in;
     do {
         const int kc = std::min(k_rows - k0, fedavg::kMaxRowsPerLaunch);
+        // the kernel form per launch: a chained chunk (acc_in + kc clients) reads kc + 1 rows
+        const int reads = kc + (cur_in ? 1 : 0);
+        const int variant = ctx->variant | (reads < kBurstMinClients ? fedavg::kVariantTileStores : 0);
+        const bool burst = fedavg::tiles_use_burst(L.tile4, L.unroll, variant);
+        const int bpc = burst ? ctx->bpc(k_rows >= fedavg::kBurstOneBlockMinK ? 1 : 2) : ctx->bpc();
+        // one block per CU: the burst kernel holds 10 tiles in LDS (all 160 KiB); public bit 6 keeps the 4-tile
+        // form, public bit 5 (register-held tiles only) keeps no LDS tiles at all
+        const bool wide = burst && bpc == 1 && !(variant & (fedavg::kVariantWideLds | fedavg::kVariantRegisterTiles));
+        L.variant = (variant & ~fedavg::kVariantWideLds) | (wide ? fedavg::kVariantWideLds : 0);
+        L.grid = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)ctx->num_cus * bpc, n_tiles));
         memset(&L.tab, 0, sizeof(L.tab));
         for (int j = 0; j < kc; ++j) {
             L.tab.rows[j] = static_cast<const fedavg::f32x4*>(bases[k0 + j]);
@@ -1312,6 +1327,7 @@ int fedavg_accumulate_tiled_epi(fedavg_ctx* ctx, const void* const* bases, const
         L.b4 = (int64_t)begin / 4;
         L.e4 = (int64_t)end / 4;
         const int64_t n_tiles = (L.e4 - 1) / L.tile4 - L.b4 / L.tile4 + 1;
+        if (L.k + (cur_in ? 1 : 0) < kEpiBurstMinClients) L.variant |= fedavg::kVariantTileStores;
         const bool burst = !(L.variant & (fedavg::kVariantEpiPrefetch | fedavg::kVariantTileStores));
         const int bpc = burst ? ctx->bpc(L.k >= fedavg::kEpiOneBlockMinK ? 1 : 2) : ctx->bpc();
         // one block per CU: the LDS-held tiles fill the CU (9 instead of 4), unless the public variant has bit 6

@@ -290,11 +290,12 @@ def test_launch_variants_same_bits(ctx, oracle, bpc, unroll, tile, variant):
         assert same_bits(got, exp)
 
 
-@pytest.mark.parametrize("K,bpc", [(20, 0), (7, 0), (20, 3), (131, 0)])
+@pytest.mark.parametrize("K,bpc", [(20, 0), (7, 0), (20, 3), (131, 0), (1, 0), (2, 0), (129, 0)])
 def test_burst_many_launches(ctx, oracle, K, bpc):
     """The default (burst) kernel issues one launch per grid x 8 tiles: more tiles than one launch covers,
     a last launch with fewer tiles than blocks, a sub-range starting and ending inside tiles, more than
-    128 clients (chained through the output), against the oracle bit for bit."""
+    128 clients (chained through the output), against the oracle bit for bit.  One and two clients, and a
+    chained last chunk of one client (129), take the per-tile-store kernel (fedavg_capi.cpp kBurstMinClients)."""
     n = 2048 * 4096 * 2 + 12345
     rows = [oracle.synth_values(5, k, np.arange(n, dtype=np.uint64)) for k in range(K)]
     ws = oracle.synth_weights(K)
