@@ -28,9 +28,10 @@ extern "C" {
 
 /* Bumped whenever a struct layout or an entry point changes (v3: Rprop / ASGD fields appended to struct
  * fedavg_epilogue; v4: fedavg_launch_count; v5: fedavg_d2h_multi; v6: fedavg_accumulate_tiled16_tails and
- * integer accumulators in fedavg_accumulate; v7: fedavg_epilogue.torch_sqrt; v8: its FEDAVG_SQRT_* values).  fedavg_struct_size() lets a binding
- * check each struct's size as well. */
-#define FEDAVG_ABI_VERSION 8
+ * integer accumulators in fedavg_accumulate; v7: fedavg_epilogue.torch_sqrt; v8: its FEDAVG_SQRT_* values; v9:
+ * fedavg_host_rsqrtps_table / fedavg_set_rsqrtps_table -- FEDAVG_SQRT_TORCH_AMD uses the host CPU's RSQRTPS captured at
+ * run time instead of a table compiled in).  fedavg_struct_size() lets a binding check each struct's size as well. */
+#define FEDAVG_ABI_VERSION 9
 
 /* element types of client rows (in_dtype) and of the running sum / result (acc_dtype) */
 enum fedavg_dtype {
@@ -99,7 +100,8 @@ enum fedavg_epi {
 enum fedavg_sqrt {
     FEDAVG_SQRT_IEEE = 0,           /* correctly rounded */
     FEDAVG_SQRT_TORCH_AVX512 = 1,   /* MKL vsSqrt, AVX-512 path (Intel): VRSQRT14PS estimate + one Newton step */
-    FEDAVG_SQRT_TORCH_AMD = 2,      /* MKL vsSqrt, SSE4.2 / AVX path (AMD EPYC): the host's RSQRTPS + a Newton step */
+    FEDAVG_SQRT_TORCH_AMD = 2,      /* MKL vsSqrt, SSE4.2 / AVX path (AMD EPYC): the host's RSQRTPS + a Newton step;
+                                       needs fedavg_set_rsqrtps_table on the handle first (v9) */
 };
 
 typedef struct fedavg_epilogue {
@@ -352,6 +354,16 @@ int fedavg_gather_f32(fedavg_ctx* ctx, const float* src, const uint64_t* idx, si
 /* Test entry (v8): out[i] = the epilogues' sqrt of x[i] on the compute stream (device pointers); torch_sqrt is a
  * FEDAVG_SQRT_* value as in struct fedavg_epilogue. */
 int fedavg_sqrt_f32(fedavg_ctx* ctx, const float* x, float* out, size_t n, int torch_sqrt);
+
+/* v9 -- torch CPU's sqrt on hosts where MKL runs vsSqrt's SSE4.2 / AVX kernel (FEDAVG_SQRT_TORCH_AMD) starts from the
+ * CPU's RSQRTPS estimate, which is vendor-specific.  fedavg_host_rsqrtps_table (host only, no device needed) captures
+ * THIS CPU's estimates: table[parity * 4096 + (m >> 11)] = mantissa bits 22..11 of RSQRTPS(x) for x = 2^parity * 1.m
+ * (n must be 8192); it fails if the CPU's estimate is not a function of the exponent parity and the top 12 mantissa
+ * bits (every fp32 of [1, 4) is checked).  fedavg_set_rsqrtps_table uploads such a table for the handle's kernels;
+ * until it is called, FEDAVG_SQRT_TORCH_AMD steps and sqrt calls fail.  (Replaces a table compiled in from one
+ * host; nvflare_amd/torch_sqrt.py verifies the restatement against the host's torch.sqrt before selecting it.) */
+int fedavg_host_rsqrtps_table(uint16_t* table, size_t n);
+int fedavg_set_rsqrtps_table(fedavg_ctx* ctx, const uint16_t* table, size_t n);
 
 #ifdef __cplusplus
 }

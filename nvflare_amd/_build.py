@@ -6,6 +6,7 @@ The library lands in nvflare_amd/lib/ so that it travels with the repository sna
 from __future__ import annotations
 
 import os
+import re
 import subprocess
 from concurrent.futures import ThreadPoolExecutor
 
@@ -24,7 +25,7 @@ EPI_UNITS = [(f"{mode}_{fin}", op, fin_v) for mode, op in (("torch", 1), ("numpy
              for fin, fin_v in (("div", 2), ("scale", 1), ("none", 0))]
 SOURCES = [EPI_SOURCE, "fedavg_tiles_numpy.hip", "fedavg_tiles_torch.hip", "fedavg_tiles_unweighted.hip",
            "fedavg_kernels.hip", "fedavg_narrow.hip", "fedavg_dequant.hip", "fedavg_capi.cpp"]
-HEADERS = ["fedavg_internal.h", "fedavg_rsqrt14.h", "fedavg_rsqrtps_amd.h", "fedavg_arith.h", "fedavg_tiles.h",
+HEADERS = ["fedavg_internal.h", "fedavg_rsqrt14.h", "fedavg_arith.h", "fedavg_tiles.h",
            "fedavg_epi.h"]
 OBJ_DIR = os.path.join(PKG, "lib", "obj")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
@@ -72,15 +73,32 @@ def compile_units(sources=SOURCES):
 LINK_FLAGS = ["-shared", "-fPIC", f"--offload-arch={ARCH}", "-Wl,--no-undefined"]
 
 
+_INCLUDE = re.compile(r'^\s*#\s*include\s+"([^"]+)"', re.M)
+
+
+def unit_deps(src: str) -> list:
+    """The source and every local header it includes, transitively (csrc/ and include/), plus this file (flags)."""
+    seen, todo = [], [os.path.join(CSRC, src)]
+    while todo:
+        f = todo.pop()
+        if f in seen:
+            continue
+        seen.append(f)
+        with open(f) as fh:
+            for name in _INCLUDE.findall(fh.read()):
+                for d in (CSRC, os.path.join(ROOT, "include")):
+                    cand = os.path.join(d, name)
+                    if os.path.exists(cand):
+                        todo.append(cand)
+                        break
+    return seen + [os.path.abspath(__file__)]
+
+
 def build_library(force: bool = False, verbose: bool = False, jobs: int = 0) -> str:
     if not force and not needs_build():
         return LIB_PATH
     os.makedirs(OBJ_DIR, exist_ok=True)
     inc = [f"-I{os.path.join(ROOT, 'include')}", f"-I{CSRC}"]
-
-    headers = [os.path.join(CSRC, h) for h in HEADERS] + [os.path.join(ROOT, "include", "nvflare_amd_fedavg.h"),
-                                                          os.path.abspath(__file__)]
-    newest_header = max(os.path.getmtime(h) for h in headers)  # any header (or a flag change) rebuilds all
 
     units = compile_units()
 
@@ -88,8 +106,8 @@ def build_library(force: bool = False, verbose: bool = False, jobs: int = 0) -> 
         src, obj_name, extra = unit
         obj = os.path.join(OBJ_DIR, obj_name)
         if not force and os.path.exists(obj) and os.path.getmtime(obj) > max(
-                os.path.getmtime(os.path.join(CSRC, src)), newest_header):
-            return obj  # up to date: only changed sources (or any header change) recompile
+                os.path.getmtime(f) for f in unit_deps(src)):
+            return obj  # up to date: a unit recompiles when its source or a header it includes changed
         cmd = [HIPCC, *FLAGS, *extra, *inc, "-c", os.path.join(CSRC, src), "-o", obj]
         if verbose:
             print(" ".join(cmd), flush=True)

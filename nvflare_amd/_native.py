@@ -43,7 +43,7 @@ FEDAVG_FIN_SCALE = 1
 FEDAVG_FIN_DIV = 2
 FEDAVG_FIN_RECIP = 3  # torch-ROCm div_ by a CPU scalar: multiply by the opmath reciprocal
 
-ABI_VERSION = 8  # include/nvflare_amd_fedavg.h FEDAVG_ABI_VERSION
+ABI_VERSION = 9  # include/nvflare_amd_fedavg.h FEDAVG_ABI_VERSION
 
 # fedavg_epilogue.torch_sqrt (enum fedavg_sqrt)
 FEDAVG_SQRT_IEEE = 0
@@ -188,6 +188,8 @@ _SIGNATURES = {
     "fedavg_fill_synthetic_f32": [c_void_p, c_void_p, c_size_t, c_size_t, c_size_t, c_u64, c_u64, c_u64],
     "fedavg_gather_f32": [c_void_p, c_void_p, c_void_p, c_size_t, c_void_p],
     "fedavg_sqrt_f32": [c_void_p, c_void_p, c_void_p, c_size_t, c_int],
+    "fedavg_host_rsqrtps_table": [c_void_p, c_size_t],  # v9: this CPU's RSQRTPS (host only)
+    "fedavg_set_rsqrtps_table": [c_void_p, c_void_p, c_size_t],  # v9: the table FEDAVG_SQRT_TORCH_AMD reads
     "fedavg_dequantize": [c_void_p, c_void_p, c_void_p, c_size_t, c_void_p, c_size_t, c_size_t, c_size_t],
 }
 EXPORTED = ["fedavg_last_error", "fedavg_abi_version", "fedavg_struct_size", *_SIGNATURES.keys()]

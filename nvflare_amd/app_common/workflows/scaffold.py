@@ -117,11 +117,15 @@ if _ReferenceScaffold is not None:
             if aggregate_fn is _reference_scaffold_fn:
                 aggregate_fn = self._device_scaffold_fn
             elif not aggregate_fn:
-                # the reference falls back to self.aggregate_fn (base_fedavg.py:251-252): a subclass's own override
-                # runs as given; only the reference's BaseFedAvg.aggregate_fn moves to the device
-                own = getattr(type(self), "aggregate_fn", None)
-                ref = getattr(_ReferenceBaseFedAvg, "aggregate_fn", None) if _ReferenceBaseFedAvg is not None else None
-                aggregate_fn = self._device_fedavg_fn if own is ref else self.aggregate_fn
+                # the reference falls back to self.aggregate_fn (base_fedavg.py:251-252): an instance attribute
+                # (self.aggregate_fn = fn, set in __init__ or by the caller) or a subclass's own override runs as
+                # given; only the reference's BaseFedAvg.aggregate_fn moves to the device
+                if "aggregate_fn" in self.__dict__:
+                    aggregate_fn = self.__dict__["aggregate_fn"]
+                else:
+                    own = getattr(type(self), "aggregate_fn", None)
+                    ref = getattr(_ReferenceBaseFedAvg, "aggregate_fn", None) if _ReferenceBaseFedAvg is not None else None
+                    aggregate_fn = self._device_fedavg_fn if own is ref else self.aggregate_fn
             return super().aggregate(results, aggregate_fn=aggregate_fn)
 
 else:

@@ -136,6 +136,7 @@ class ShardedServerOptimizer:
             off += (p.numel() + _HOST_ALIGN - 1) // _HOST_ALIGN * _HOST_ALIGN
         self.total = max(off, _HOST_ALIGN)
         self.host_pool = HostArenaPool()
+        self.out_pool = HostArenaPool()  # the weights handed out by to_host (independent of the live parameters)
         self._pool = ThreadPoolExecutor(max_workers=len(self.devices), thread_name_prefix="nvflare-amd-fedopt-shard")
         self._pool_fin = weakref.finalize(self, self._pool.shutdown, wait=False)  # a re-bound generator drops us
         me = weakref.ref(self)
@@ -247,9 +248,10 @@ class ShardedServerOptimizer:
             self._egress()
             return [n for n in self.params if n in stepped]
 
-    def _egress(self) -> None:
-        """Every device's buckets into one fresh host array (its own PCIe link, one fedavg_d2h_multi each)."""
-        host = self.host_pool.take(self.total, pin=self.shards[0].ctx)
+    def _pull(self, pool: HostArenaPool) -> np.ndarray:
+        """Every device's buckets into one fresh host array from ``pool`` (each device over its own PCIe link, one
+        fedavg_d2h_multi each, in parallel)."""
+        host = pool.take(self.total, pin=self.shards[0].ctx)
 
         def pull(b: int) -> None:
             shard = self.shards[b]
@@ -262,30 +264,30 @@ class ShardedServerOptimizer:
                 shard.ctx.d2h_multi(host, shard.p.data_ptr(), pieces)
 
         list(self._pool.map(pull, range(len(self.shards))))
-        self._point_params(host)
+        return host
+
+    def _egress(self) -> None:
+        """The new weights into a fresh host array that the model's parameters are re-pointed at."""
+        self._point_params(self._pull(self.host_pool))
 
     def to_host(self, state: Dict, preserve_torch: bool) -> Dict:
-        """state_dict -> host values (fedopt.py:238-244): parameters are already views of the host weights
-        (returned without a copy, like the reference's CPU model returns views of its parameters); other entries
-        are copied as the single-device path copies them.
-
-        The device shards only learn about in-place edits of a parameter through its ``_version`` counter
-        (``_upload_modified``), so the views handed out must not let an edit slip past it: torch values are
-        ``detach()``-ed parameters (they share the parameter's version counter, so an in-place torch op on them
-        is uploaded before the next step), numpy values are READ-ONLY views (an in-place numpy write would not
-        move any counter; it raises instead of leaving the host model and the shards disagreeing)."""
+        """state_dict -> host values as the reference hands them out (fedopt.py:232-236: ``detach().cpu().clone()``
+        for torch, ``detach().cpu().numpy()`` of its GPU model for numpy): independent, writable copies.  The
+        parameters' values are pulled from the devices a second time into an array of their own (``out_pool``;
+        every device over its own link, in parallel -- cheaper than a host copy of the weights), so nothing the
+        caller does to the returned weights reaches the live parameters or the shards' next step; other entries
+        are copied as the single-device path copies them."""
         out = {}
         base = self.host.ctypes.data
+        handout = None
         for k, v in state.items():
             lay = self.layout.get(k)
             if lay is not None and v.dtype == torch.float32 and v.data_ptr() == base + 4 * lay[0]:
-                p = self.params.get(k)
-                if preserve_torch and p is not None and p.data_ptr() == v.data_ptr():
-                    out[k] = p.detach()
-                    continue
-                h = self.host[lay[0]:lay[0] + lay[1]].reshape(tuple(v.shape))
-                h.flags.writeable = False
-                out[k] = torch.from_numpy(h.copy()) if preserve_torch else h
+                if handout is None:
+                    with self._lock:
+                        handout = self._pull(self.out_pool)
+                h = handout[lay[0]:lay[0] + lay[1]].reshape(tuple(v.shape))
+                out[k] = torch.from_numpy(h) if preserve_torch else h
                 continue
             h = v.detach().cpu()
             out[k] = h.clone() if preserve_torch else h.numpy()

@@ -8,7 +8,6 @@
 
 #include "fedavg_internal.h"
 #include "fedavg_rsqrt14.h"
-#include "fedavg_rsqrtps_amd.h"
 
 namespace fedavg {
 
@@ -200,23 +199,24 @@ __device__ __forceinline__ float sqrt_torch_cpu(const float x) {
     return out;
 }
 
-// torch CPU's fp32 Tensor.sqrt on the GPU pool's AMD EPYC hosts (EpiParams.torch_sqrt == FEDAVG_SQRT_TORCH_AMD): MKL
-// runs vsSqrt's SSE4.2 / AVX kernel there (mkl_vml_kernel_sSqrt_EXHAynn, equal to torch.sqrt on all 59.8 M probe
+// torch CPU's fp32 Tensor.sqrt on hosts where MKL takes vsSqrt's SSE4.2 / AVX kernel -- the GPU pool's AMD EPYC hosts
+// (EpiParams.torch_sqrt == FEDAVG_SQRT_TORCH_AMD; mkl_vml_kernel_sSqrt_EXHAynn, equal to torch.sqrt on all 59.8 M probe
 // inputs on the box, tools/sqrt_box_kernels.py), which starts a coupled Newton step in plain fp32 -- every operation
 // rounds, no FMA (-ffp-contract=off) -- from the RSQRTPS estimate:
 //     y = rsqrtps(x);  s = x * y;  h = y * 0.5;  r = 0.5 - s * h;  s1 = s * r + s;  h1 = h * r + h;
 //     sqrt = (x - s1 * s1) * h1 + s1
 // on positive normals up to 0x7f7ff000; every other input takes the kernel's correctly rounded scalar callout.
-// RSQRTPS is vendor-specific: the host CPU's estimates (12 bits, a function of the exponent parity and the top 12
-// mantissa bits) are the 8192-entry table fedavg_rsqrtps_amd.h, staged in LDS once per block (rsqrtps_stage, 16 KiB);
-// each sqrt reads one 16-bit entry.  Restated in oracle_sqrt_mkl_rsqrtps: with this container's RSQRTPS it equals
-// MKL's EX kernel on all 2^32 inputs, with the AMD table the box's torch.sqrt on every fp32 in [1, 4)
-// (tools/sqrt_mkl_sse_check.py).
-__shared__ uint32_t g_rsqrtps_lds[4096];  // kRsqrtpsAmd: two 12-bit estimates per word
+// RSQRTPS is vendor-specific: the HOST CPU's estimates (12 bits, a function of the exponent parity and the top 12
+// mantissa bits), captured at run time by fedavg_host_rsqrtps_table and uploaded by fedavg_set_rsqrtps_table (8192
+// entries, two per word, EpiParams.rsqrtps), are staged in LDS once per block (rsqrtps_stage, 16 KiB); each sqrt reads
+// one 16-bit entry.  Restated in oracle_sqrt_mkl_rsqrtps: with this container's RSQRTPS it equals MKL's EX kernel on
+// all 2^32 inputs, with the box's table the box's torch.sqrt on all 2^32 inputs (tools/sqrt_mkl_sse_check.py,
+// profiles/r03/final/sqrt_check_torch_all.log).
+__shared__ uint32_t g_rsqrtps_lds[4096];  // two 12-bit estimates per word (low half first)
 
 // every kernel that computes sqrt_mkl_rsqrtps calls this first, with the whole block (one barrier)
-__device__ __forceinline__ void rsqrtps_stage() {
-    const uint4* src = reinterpret_cast<const uint4*>(kRsqrtpsAmd);
+__device__ __forceinline__ void rsqrtps_stage(const uint32_t* table) {
+    const uint4* src = reinterpret_cast<const uint4*>(table);
     uint4* dst = reinterpret_cast<uint4*>(g_rsqrtps_lds);
     for (int i = threadIdx.x; i < 1024; i += kBlock) dst[i] = src[i];
     __syncthreads();

@@ -4,6 +4,7 @@
 // plugins/plugin_main.cc:24-111): opaque handle, int rc, thread-local last-error string, every entry
 // point wrapped so that no C++ exception crosses the boundary.
 #include <hip/hip_runtime.h>
+#include <immintrin.h>
 #include <stdint.h>
 #include <string.h>
 
@@ -54,6 +55,7 @@ int guarded(F&& f) {
     return 1;
 }
 
+constexpr size_t kRsqrtpsEntries = 8192;  // 2 exponent parities x 4096 top-12-bit mantissas
 constexpr int kRingSlots = 4;
 constexpr size_t kRingBytes = 64ull << 20;  // 64 MiB per pinned staging slot
 constexpr size_t kParallelCopyMin = 8ull << 20;
@@ -202,6 +204,9 @@ struct fedavg_ctx {
     // torch scalar-remainder elements of a 16-bit launch: their indices and recomputed values (device)
     void* tails_buf = nullptr;
     size_t tails_bytes = 0;
+    // this host's RSQRTPS estimates for FEDAVG_SQRT_TORCH_AMD (fedavg_set_rsqrtps_table): 8192 x 12 bits, two per
+    // word, in device memory; staged into LDS by every kernel that computes that sqrt
+    uint32_t* rsqrtps = nullptr;
 
     hipStream_t compute() const { return ext_stream ? ext_stream : own_stream; }
     int bpc(int dflt = fedavg::kDefaultBlocksPerCu) const { return blocks_per_cu ? blocks_per_cu : dflt; }
@@ -414,9 +419,14 @@ void run_tiles(fedavg_ctx* ctx, const void* const* bases, const double* weights,
 
 // Epilogue scalars as torch computes them: python-float (fp64) hyperparameters and bias corrections,
 // cast to fp32 where they meet a tensor (oracle/fedavg_oracle.c oracle_epilogue_apply mirrors this).
-fedavg::EpiParams make_epi(const fedavg_epilogue& e) {
+fedavg::EpiParams make_epi(const fedavg_ctx* ctx, const fedavg_epilogue& e) {
     fedavg::EpiParams E;
     memset(&E, 0, sizeof(E));
+    if (e.torch_sqrt == FEDAVG_SQRT_TORCH_AMD) {
+        if (!ctx->rsqrtps)
+            throw Error("FEDAVG_SQRT_TORCH_AMD needs this host's RSQRTPS table first (fedavg_set_rsqrtps_table)");
+        E.rsqrtps = ctx->rsqrtps;
+    }
     E.kind = e.kind;
     E.first_step = e.first_step;
     E.nesterov = e.nesterov;
@@ -719,6 +729,7 @@ int fedavg_destroy(fedavg_ctx* ctx) {
         for (auto& m : ctx->marks) (void)hipEventDestroy(m.first);
         for (hipEvent_t ev : ctx->mark_pool) (void)hipEventDestroy(ev);
         if (ctx->tails_buf) (void)hipFree(ctx->tails_buf);
+        if (ctx->rsqrtps) (void)hipFree(ctx->rsqrtps);
         if (ctx->own_stream) (void)hipStreamDestroy(ctx->own_stream);
         if (ctx->copy_stream) (void)hipStreamDestroy(ctx->copy_stream);
     });
@@ -1337,7 +1348,7 @@ int fedavg_accumulate_tiled_epi(fedavg_ctx* ctx, const void* const* bases, const
         L.fin_val = (float)fin_scalar(fin, count);
         L.acc_in = cur_in;
         L.out = static_cast<float*>(out);
-        const hipError_t rc = fedavg::launch_tiles_epi_f32x4(L, make_epi(*epi), s, &ctx->launches);
+        const hipError_t rc = fedavg::launch_tiles_epi_f32x4(L, make_epi(ctx, *epi), s, &ctx->launches);
         if (scratch) HIP_CHECK(hipFreeAsync(scratch, s));
         HIP_CHECK(rc);
         ts.done();
@@ -1478,7 +1489,56 @@ int fedavg_sqrt_f32(fedavg_ctx* ctx, const float* x, float* out, size_t n, int t
         const int grid = (int)std::min<size_t>((size_t)ctx->num_cus * 8, (n + fedavg::kBlock - 1) / fedavg::kBlock);
         if (torch_sqrt != FEDAVG_SQRT_IEEE && torch_sqrt != FEDAVG_SQRT_TORCH_AVX512 && torch_sqrt != FEDAVG_SQRT_TORCH_AMD)
             throw Error("torch_sqrt must be FEDAVG_SQRT_IEEE, _TORCH_AVX512 or _TORCH_AMD");
-        HIP_CHECK(fedavg::launch_sqrt_f32(x, out, (int64_t)n, torch_sqrt, grid, ctx->compute()));
+        if (torch_sqrt == FEDAVG_SQRT_TORCH_AMD && !ctx->rsqrtps)
+            throw Error("FEDAVG_SQRT_TORCH_AMD needs this host's RSQRTPS table first (fedavg_set_rsqrtps_table)");
+        HIP_CHECK(fedavg::launch_sqrt_f32(x, out, (int64_t)n, torch_sqrt, ctx->rsqrtps, grid, ctx->compute()));
+    });
+}
+
+int fedavg_host_rsqrtps_table(uint16_t* table, size_t n) {
+    return guarded([&] {
+        if (!table) throw Error("table is NULL");
+        if (n != kRsqrtpsEntries) throw Error("the RSQRTPS table has 8192 entries");
+        // every fp32 of [1, 4), four per RSQRTPS: the estimate must have exponent 126, 11 clear low bits and one
+        // value per 2^11-input block (a function of the exponent parity and the top 12 mantissa bits), which is the
+        // shape the device sqrt (fedavg_arith.h sqrt_mkl_rsqrtps) indexes
+        for (uint32_t b = 0x3F800000u; b < 0x40800000u; b += 4) {
+            alignas(16) uint32_t in[4] = {b, b + 1, b + 2, b + 3}, est[4];
+            __m128 v;
+            memcpy(&v, in, 16);
+            const __m128 r = _mm_rsqrt_ps(v);
+            memcpy(est, &r, 16);
+            for (int j = 0; j < 4; ++j) {
+                const uint32_t off = in[j] - 0x3F800000u;
+                if ((est[j] >> 23) != 126u || (est[j] & 0x7FFu) != 0u)
+                    throw Error("this CPU's RSQRTPS estimate of " + std::to_string(in[j]) +
+                                " is not a 12-bit estimate in [0.5, 1)");
+                const uint16_t e12 = (uint16_t)((est[j] >> 11) & 0xFFFu);
+                if ((off & 0x7FFu) == 0u) {
+                    table[off >> 11] = e12;
+                } else if (table[off >> 11] != e12) {
+                    throw Error("this CPU's RSQRTPS depends on more than the top 12 mantissa bits");
+                }
+            }
+        }
+    });
+}
+
+int fedavg_set_rsqrtps_table(fedavg_ctx* ctx, const uint16_t* table, size_t n) {
+    return guarded([&] {
+        if (!ctx) throw Error("ctx is NULL");
+        if (!table) throw Error("table is NULL");
+        if (n != kRsqrtpsEntries) throw Error("the RSQRTPS table has 8192 entries");
+        std::vector<uint32_t> words(kRsqrtpsEntries / 2);
+        for (size_t i = 0; i < words.size(); ++i) {
+            if (table[2 * i] > 0xFFFu || table[2 * i + 1] > 0xFFFu) throw Error("RSQRTPS table entries are 12-bit");
+            words[i] = (uint32_t)table[2 * i] | ((uint32_t)table[2 * i + 1] << 16);  // low half first
+        }
+        ctx->activate();
+        if (!ctx->rsqrtps) HIP_CHECK(hipMalloc(&ctx->rsqrtps, words.size() * sizeof(uint32_t)));
+        // ordered behind every earlier launch on the compute stream (one may be reading the old table)
+        HIP_CHECK(hipStreamSynchronize(ctx->compute()));
+        HIP_CHECK(hipMemcpy(ctx->rsqrtps, words.data(), words.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
     });
 }
 

@@ -273,7 +273,7 @@ fedavg_tiles_epi_burst_f32x4(const RowTableF32 tab, const int K, const int64_t t
     f32x4 dd[TPB][CPL];
     __shared__ f32x4 staged[TPB_LDS > 0 ? TPB_LDS * CPL * kBlock : 1];
     if constexpr ((EPI & kEpiTorchSqrt) != 0) rsqrt14_stage();
-    if constexpr ((EPI & kEpiTorchSqrtAmd) != 0) rsqrtps_stage();
+    if constexpr ((EPI & kEpiTorchSqrtAmd) != 0) rsqrtps_stage(E.rsqrtps);
 #pragma unroll
     for (int m = 0; m < TPB; ++m) {
         const int64_t t = t0 + blockIdx.x + (int64_t)m * gridDim.x;
@@ -360,7 +360,7 @@ __global__ void __launch_bounds__(kBlock) fedavg_tiles_epi_f32x4(const RowTableF
     const int64_t t_last = (e4 - 1) / T4;
     const int g0 = PIPE ? (K < UNROLL ? K : UNROLL) : 0;  // clients carried over from the previous tile
     if constexpr ((EPI & kEpiTorchSqrt) != 0) rsqrt14_stage();
-    if constexpr ((EPI & kEpiTorchSqrtAmd) != 0) rsqrtps_stage();
+    if constexpr ((EPI & kEpiTorchSqrtAmd) != 0) rsqrtps_stage(E.rsqrtps);
     f32x4 nxt[UNROLL][CPL];
     int64_t t = b4 / T4 + blockIdx.x;
     if constexpr (PIPE) {

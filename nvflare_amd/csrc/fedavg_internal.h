@@ -102,6 +102,7 @@ struct EpiParams {
     float etaminus, etaplus, ss_min, ss_max;      // Rprop
     float decay, neg_eta, mu;                     // ASGD: 1 - lambd * eta, -eta, mu (averaging when != 1)
     int torch_sqrt;                               // FEDAVG_SQRT_*: torch CPU's sqrt (Intel / AMD host), or IEEE
+    const uint32_t* rsqrtps;                      // FEDAVG_SQRT_TORCH_AMD: this host's RSQRTPS table (device, 16 KiB)
 };
 
 struct DequantLaunch {
@@ -198,6 +199,7 @@ hipError_t launch_tiles_f64(const RowTableGeneric& tab, int K, int64_t tstride_e
 hipError_t launch_fill_synthetic_f32(float* dst, int64_t n, int64_t tile, int64_t tstride, uint64_t seed, uint64_t row,
                                      uint64_t col0, int grid, hipStream_t s);
 hipError_t launch_gather_f32(const float* src, const uint64_t* idx, float* dst, int64_t m, hipStream_t s);
-hipError_t launch_sqrt_f32(const float* x, float* out, int64_t n, int torch_sqrt, int grid, hipStream_t s);
+hipError_t launch_sqrt_f32(const float* x, float* out, int64_t n, int torch_sqrt, const uint32_t* rsqrtps, int grid,
+                           hipStream_t s);
 
 }  // namespace fedavg

@@ -586,21 +586,22 @@ hipError_t launch_fill_synthetic_f32(float* dst, int64_t n, int64_t tile, int64_
 }
 
 // test kernel: the epilogues' sqrt elementwise (torch_sqrt: FEDAVG_SQRT_* -- torch CPU's restated vsSqrt of the Intel
-// or the AMD hosts, or the correctly rounded one)
+// or the AMD hosts, or the correctly rounded one; rsqrtps: the host's RSQRTPS table for FEDAVG_SQRT_TORCH_AMD)
 __global__ void __launch_bounds__(kBlock) fedavg_sqrt_f32(const float* __restrict__ x, float* __restrict__ out, int64_t n,
-                                                          int torch_sqrt) {
+                                                          int torch_sqrt, const uint32_t* __restrict__ rsqrtps) {
     const int64_t stride = (int64_t)gridDim.x * kBlock;
     rsqrt14_stage();
-    rsqrtps_stage();
+    if (torch_sqrt == FEDAVG_SQRT_TORCH_AMD) rsqrtps_stage(rsqrtps);  // block-uniform: the barrier is safe
     for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride)
         out[i] = torch_sqrt == FEDAVG_SQRT_TORCH_AVX512 ? sqrt_torch_cpu(x[i])
                  : torch_sqrt == FEDAVG_SQRT_TORCH_AMD ? sqrt_mkl_rsqrtps(x[i])
                                                         : __builtin_sqrtf(x[i]);
 }
 
-hipError_t launch_sqrt_f32(const float* x, float* out, int64_t n, int torch_sqrt, int grid, hipStream_t s) {
+hipError_t launch_sqrt_f32(const float* x, float* out, int64_t n, int torch_sqrt, const uint32_t* rsqrtps, int grid,
+                           hipStream_t s) {
     if (n <= 0) return hipSuccess;
-    hipLaunchKernelGGL(fedavg_sqrt_f32, dim3(grid), dim3(kBlock), 0, s, x, out, n, torch_sqrt);
+    hipLaunchKernelGGL(fedavg_sqrt_f32, dim3(grid), dim3(kBlock), 0, s, x, out, n, torch_sqrt, rsqrtps);
     return hipGetLastError();
 }
 

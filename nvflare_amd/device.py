@@ -369,6 +369,8 @@ class DeviceContext:
     def accumulate_tiled_epi(self, bases: Sequence[int], weights: Sequence[float], tile: int, tile_stride: int,
                              begin: int, end: int, out_ptr: Optional[int], op: int, fin: int, count: float,
                              epilogue: "N.Epilogue", acc_in_ptr: Optional[int] = None) -> None:
+        if epilogue.torch_sqrt == N.FEDAVG_SQRT_TORCH_AMD:
+            self.load_rsqrtps()
         k = len(bases)
         b_arr = (ctypes.c_void_p * max(k, 1))(*bases)
         w_arr = (ctypes.c_double * max(k, 1))(*[float(w) for w in weights])
@@ -450,8 +452,22 @@ class DeviceContext:
     def sqrt_f32(self, x_ptr: int, out_ptr: int, n: int, torch_sqrt=False) -> None:
         """out[i] = the epilogues' sqrt of x[i] (device pointers).  ``torch_sqrt``: a FEDAVG_SQRT_* value, or a bool
         (True: torch CPU's AVX-512 vsSqrt, False: the correctly rounded sqrt).  Test entry."""
+        if int(torch_sqrt) == N.FEDAVG_SQRT_TORCH_AMD:
+            self.load_rsqrtps()
         N.call("fedavg_sqrt_f32", self.handle, ctypes.c_void_p(x_ptr), ctypes.c_void_p(out_ptr), ctypes.c_size_t(n),
                ctypes.c_int(int(torch_sqrt)))
+
+    def load_rsqrtps(self, table: Optional[np.ndarray] = None) -> None:
+        """Upload the RSQRTPS table FEDAVG_SQRT_TORCH_AMD reads (fedavg_set_rsqrtps_table): ``table``, or -- once per
+        context -- THIS host CPU's estimates captured at run time (torch_sqrt.host_rsqrtps_table)."""
+        if table is None and getattr(self, "_rsqrtps_loaded", False):
+            return
+        from . import torch_sqrt
+
+        t = np.ascontiguousarray(torch_sqrt.host_rsqrtps_table() if table is None else table, dtype=np.uint16)
+        with self.lock:
+            N.call("fedavg_set_rsqrtps_table", self.handle, ctypes.c_void_p(t.ctypes.data), ctypes.c_size_t(t.size))
+            self._rsqrtps_loaded = table is None
 
     def gather_f32(self, src_ptr: int, idx: np.ndarray) -> np.ndarray:
         idx = np.ascontiguousarray(idx, dtype=np.uint64)

@@ -110,12 +110,20 @@ class ShardedFedAvg:
                     err = err or e
             if err is not None:
                 # all or nothing across buckets too: the buckets that staged give their piece back (each engine's
-                # add is already atomic), so no bucket counts a weight the others do not
-                for eng, tx in zip(self.engines, txs):
+                # add is already atomic), so no bucket counts a weight the others do not.  Every bucket is undone
+                # even when one undo fails; the staging error is the one raised, the undo failures chained to it.
+                undo_errs = []
+                for b, (eng, tx) in enumerate(zip(self.engines, txs)):
                     if tx is not None:
-                        eng.undo_add(tx)
+                        try:
+                            eng.undo_add(tx)
+                        except BaseException as e:  # noqa: B036 - reported with the staging error below
+                            undo_errs.append((b, e))
                 for k in introduced:
                     self._shapes.pop(k, None)
+                if undo_errs:
+                    msg = "; ".join(f"bucket {b}: {type(e).__name__}: {e}" for b, e in undo_errs)
+                    raise err from RuntimeError(f"nvflare_amd: undoing the other buckets also failed ({msg})")
                 raise err
 
     def _assemble(self, k: str, plist: List[Tuple[int, Any]]):

@@ -24,6 +24,7 @@
  * vectors in tests/golden/, which were produced by running the reference helper itself
  * (tests/golden/make_golden.py).
  */
+#include <immintrin.h>
 #include <math.h>
 #include <stddef.h>
 #include <stdint.h>
@@ -262,6 +263,24 @@ float oracle_sqrt_mkl_rsqrtps(const uint16_t* tab, float x) {
 
 void oracle_sqrt_mkl_rsqrtps_n(const uint16_t* tab, const float* x, size_t n, float* out) {
     for (size_t i = 0; i < n; ++i) out[i] = oracle_sqrt_mkl_rsqrtps(tab, x[i]);
+}
+
+/* THIS CPU's RSQRTPS table in the layout above: the estimate of the first fp32 of each top-12-bit-mantissa block of
+ * [1, 2) and [2, 4) (tools/rsqrtps_dump.c dumps every input; tests compare).  Returns the number of blocks whose
+ * estimate is not a 12-bit value with exponent 126 (0 on the CPUs the restatement covers). */
+int oracle_host_rsqrtps_table(uint16_t* tab) {
+    int bad = 0;
+    for (uint32_t i = 0; i < 8192; ++i) {
+        const uint32_t bits = 0x3F800000u + (i << 11);
+        float x, y;
+        memcpy(&x, &bits, 4);
+        _mm_store_ss(&y, _mm_rsqrt_ss(_mm_set_ss(x)));
+        uint32_t e;
+        memcpy(&e, &y, 4);
+        bad += (e >> 23) != 126u || (e & 0x7FFu) != 0u;
+        tab[i] = (uint16_t)((e >> 11) & 0xFFFu);
+    }
+    return bad;
 }
 
 static inline float sqrt_e(const oracle_epilogue* epi, float x) {

@@ -375,25 +375,44 @@ def sqrt_torch_cpu_sse2(x) -> np.ndarray:
     return out
 
 
-_RSQRTPS_FILE = os.path.join(os.path.dirname(_HERE), "nvflare_amd", "data", "rsqrtps_amd.bin")
+_RSQRTPS_BOX_FILE = os.path.join(os.path.dirname(_HERE), "tests", "golden", "rsqrtps_amd_epyc9575f.bin")
 _rsqrtps = None
+_rsqrtps_box = None
 
 
 def rsqrtps_table() -> np.ndarray:
-    """RSQRTPS of the GPU pool's AMD EPYC host CPU (tools/rsqrtps_dump.c, tools/make_rsqrtps_table.py): 2 x 4096
-    uint16, mantissa bits 22..11 of the estimate for x in [1, 2) then [2, 4), one per top-12-bit mantissa."""
+    """RSQRTPS of THIS host CPU (oracle_host_rsqrtps_table; the product captures its own, fedavg_host_rsqrtps_table):
+    2 x 4096 uint16, mantissa bits 22..11 of the estimate for x in [1, 2) then [2, 4), one per top-12-bit mantissa."""
     global _rsqrtps
     if _rsqrtps is None:
-        t = np.fromfile(_RSQRTPS_FILE, dtype=np.uint16)
-        if t.size != 8192 or np.any(t > 0xFFF):
-            raise ValueError(f"{_RSQRTPS_FILE}: not an RSQRTPS table")
-        _rsqrtps = np.ascontiguousarray(t)
+        lib = load()
+        fn = lib.oracle_host_rsqrtps_table
+        fn.restype = ctypes.c_int
+        fn.argtypes = [ctypes.c_void_p]
+        t = np.zeros(8192, np.uint16)
+        bad = fn(t.ctypes.data)
+        if bad:
+            raise ValueError(f"this CPU's RSQRTPS is not a 12-bit estimate in [0.5, 1) ({bad} blocks)")
+        _rsqrtps = t
     return _rsqrtps
 
 
+def rsqrtps_table_box() -> np.ndarray:
+    """RSQRTPS of the GPU pool's AMD EPYC 9575F hosts, captured there in round 3 (tools/rsqrtps_dump.c,
+    tools/make_rsqrtps_table.py): the fixture tests/golden/rsqrtps_amd_epyc9575f.bin, which pins the restatement to
+    that host's torch.sqrt (tests/golden/sqrt_amd_box.npz)."""
+    global _rsqrtps_box
+    if _rsqrtps_box is None:
+        t = np.fromfile(_RSQRTPS_BOX_FILE, dtype=np.uint16)
+        if t.size != 8192 or np.any(t > 0xFFF):
+            raise ValueError(f"{_RSQRTPS_BOX_FILE}: not an RSQRTPS table")
+        _rsqrtps_box = np.ascontiguousarray(t)
+    return _rsqrtps_box
+
+
 def sqrt_torch_cpu_amd(x, table: Optional[np.ndarray] = None) -> np.ndarray:
-    """torch CPU's fp32 sqrt on the AMD hosts (MKL vsSqrt's SSE4.2 / AVX kernel, oracle_sqrt_mkl_rsqrtps) with that
-    CPU's RSQRTPS table, or ``table`` (another CPU's, e.g. this one's for a check against MKL's kernel here)."""
+    """torch CPU's fp32 sqrt where MKL takes vsSqrt's SSE4.2 / AVX kernel (the AMD hosts; oracle_sqrt_mkl_rsqrtps) with
+    THIS CPU's RSQRTPS table, or ``table`` (another CPU's, e.g. the AMD box's fixture rsqrtps_table_box())."""
     lib = load()
     fn = lib.oracle_sqrt_mkl_rsqrtps_n
     fn.restype = None
@@ -414,7 +433,7 @@ def epilogue_apply(delta, kind, p=None, m=None, v=None, base=None, vmax=None, to
     updated IN PLACE (copies are the caller's business); returns `out` for NONE/ADD_BASE and p otherwise.
     ``torch_cpu_sqrt``: which sqrt -- False / "ieee" the correctly rounded one, True / "torch_cpu" torch CPU's
     AVX-512 vsSqrt (oracle_sqrt_torch_cpu), "torch_cpu_amd" its SSE4.2 / AVX path on the AMD hosts
-    (oracle_sqrt_mkl_rsqrtps with ``rsqrtps`` or the AMD host's RSQRTPS table)."""
+    (oracle_sqrt_mkl_rsqrtps with ``rsqrtps`` or THIS host's RSQRTPS table)."""
     lib = load()
     fn = lib.oracle_epilogue_apply
     fn.restype = None

@@ -282,3 +282,60 @@ def fake_engine(max_resident_bytes=None, slab_slots=None):
     e = DeviceFedAvg(device=0, max_resident_bytes=max_resident_bytes, slab_slots=slab_slots)
     e._ctx = FakeDeviceContext()
     return e
+
+
+class FakeBenchContext(FakeDeviceContext):
+    """FakeDeviceContext with the entry points bench.py drives (launch tuning, synthetic fill, the fused Adam step,
+    timing, launch counts, gathers): bench.main() runs on it in the CPU suite (tests/test_cpu_bench_world8.py)."""
+
+    _SQRT = {0: "ieee", 1: "torch_cpu", 2: "torch_cpu_amd"}
+
+    def __init__(self, device=0, total_bytes=1 << 34):
+        super().__init__(device, total_bytes)
+        self._t0 = None
+
+    def set_launch(self, blocks_per_cu=0, unroll=0):
+        pass
+
+    def set_variant(self, variant=0):
+        pass
+
+    def launch_count(self):
+        return len(self.launches)
+
+    def timing_begin(self):
+        import time
+
+        self._t0 = time.perf_counter()
+
+    def timing_end(self):
+        import time
+
+        return (time.perf_counter() - self._t0) * 1e3
+
+    def fill_synthetic_f32(self, dst_ptr, n, seed, row, col0=0, tile=0, tile_stride=0):
+        vals = orc.synth_values(seed, row, np.arange(col0, col0 + n, dtype=np.uint64)).astype(np.float32)
+        if tile:
+            self._tiled_write(dst_ptr, tile * 4, tile_stride * 4, 0, vals.view(np.uint8))
+        else:
+            self._view(dst_ptr, n * 4)[:] = vals.view(np.uint8)
+
+    def gather_f32(self, src_ptr, idx):
+        idx = np.asarray(idx, dtype=np.uint64)
+        return np.array([self._view(src_ptr + 4 * int(i), 4).view(np.float32)[0] for i in idx], dtype=np.float32)
+
+    def accumulate_tiled_epi(self, bases, weights, tile, stride, begin, end, out_ptr, op, fin, count, epilogue,
+                             acc_in_ptr=None):
+        """Aggregation + the fused Adam step (the only epilogue bench.py's spot check replays), by the oracle."""
+        assert epilogue.kind == N.FEDAVG_EPI_ADAM, "the fake bench context restates the Adam epilogue only"
+        self.launches.append(("tiled_epi", len(bases), begin, end))
+        rows = [self._read_tiled(b, tile, stride, begin, end, 4, np.float32) for b in bases]
+        d = np.asarray(self._agg(rows, weights, op, fin, count, None), dtype=np.float32)
+        n = end - begin
+        p, m, v = (self._view(ptr + begin * 4, n * 4).view(np.float32)
+                   for ptr in (epilogue.param, epilogue.state1, epilogue.state2))
+        hp = dict(lr=epilogue.lr, beta1=epilogue.beta1, beta2=epilogue.beta2, eps=epilogue.eps)
+        orc.epilogue_apply(d, orc.EPI_ADAM, p=p, m=m, v=v, step=float(epilogue.step),
+                           torch_cpu_sqrt=self._SQRT[epilogue.torch_sqrt], **hp)
+        if out_ptr:
+            self._view(out_ptr + begin * 4, n * 4)[:] = d.view(np.uint8)

@@ -37,6 +37,22 @@ def test_subclass_aggregate_fn_is_kept():
     assert np.array_equal(out.params["w"], np.zeros(3, np.float32))
 
 
+def test_instance_aggregate_fn_is_kept():
+    """An instance-level override (``self.aggregate_fn = fn``) runs as given, as the reference's
+    ``self.aggregate_fn`` lookup would run it."""
+    calls = []
+
+    def fn(results):
+        calls.append(len(results))
+        return FLModel(params={"w": np.full(3, 7.0, np.float32)})
+
+    ctl = _ctl(Scaffold)
+    ctl.aggregate_fn = fn
+    out = ctl.aggregate(_results())
+    assert calls == [2]
+    assert np.array_equal(out.params["w"], np.full(3, 7.0, np.float32))
+
+
 def test_default_aggregate_fn_runs_on_the_device():
     ctl = _ctl(Scaffold)
     out = ctl.aggregate(_results())

@@ -171,6 +171,40 @@ def test_sharded_add_rolls_back_every_bucket(failing_bucket):
         sh.release()
 
 
+def test_sharded_add_undoes_every_bucket_when_an_undo_fails():
+    """bucket 1 fails to stage, bucket 0's undo raises too -- bucket 2 is still undone, and the error
+    raised is the staging error with the undo failure chained to it."""
+    rng = np.random.default_rng(15)
+    sh = ShardedFedAvg([0, 0, 0])
+    for eng in sh.engines:
+        eng._ctx = FakeDeviceContext()
+    try:
+        ok = _client(rng, 0)
+        sh.add(list(ok.items()), 2.0, True)
+        f = _Fail(sh.engines[1].ctx, "h2d_tiled_multi")
+        f.arm(1)
+        undone = []
+        orig0, orig2 = sh.engines[0].undo_add, sh.engines[2].undo_add
+
+        def undo0(tx):
+            raise RuntimeError("injected undo failure")
+
+        def undo2(tx):
+            undone.append(tx)
+            return orig2(tx)
+
+        sh.engines[0].undo_add, sh.engines[2].undo_add = undo0, undo2
+        with pytest.raises(N.FedAvgError, match="injected h2d_tiled_multi failure") as ei:
+            sh.add(list(_client(rng, 1, late=True).items()), 3.0, True)
+        assert len(undone) == 1, "bucket 2 must be undone although bucket 0's undo failed"
+        cause = ei.value.__cause__
+        assert isinstance(cause, RuntimeError) and "bucket 0" in str(cause) and "injected undo failure" in str(cause)
+        assert "late" not in sh._shapes
+        sh.engines[0].undo_add = orig0
+    finally:
+        sh.release()
+
+
 def test_helper_stats_skip_a_failed_contribution():
     """The drop-in helper counts a contribution (key_contribution_counts, history, counts) only once the device
     has staged it: a failed add leaves the stats and the next result as if it never arrived."""

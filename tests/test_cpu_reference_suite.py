@@ -137,8 +137,8 @@ SCAFFOLD_CHECK = os.path.join(HERE, "ref_scaffold_override_check.py")
 
 @pytest.mark.skipif(not os.path.exists(FEDAVG_WORKFLOW), reason="reference tree not mounted")
 def test_dropin_scaffold_keeps_subclass_aggregate_fn(tmp_path):
-    """The drop-in Scaffold under the real NVFlare classes: a subclass's own aggregate_fn runs as given, the
+    """The drop-in Scaffold under the real NVFlare classes: a subclass's own or an instance-level aggregate_fn runs as given, the
     reference's default goes to the device (tests/ref_scaffold_override_check.py)."""
     proc, _, outcomes = _run(tmp_path, [SCAFFOLD_CHECK], True, "scaffold_override")
     assert proc.returncode == 0, (proc.stdout + proc.stderr)[-3000:]
-    assert len(outcomes) == 2 and set(outcomes.values()) == {"passed"}, outcomes
+    assert len(outcomes) == 3 and set(outcomes.values()) == {"passed"}, outcomes

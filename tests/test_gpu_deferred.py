@@ -70,7 +70,7 @@ def _client_diff(rng, weights, k, rnd, container, drop_key=None):
 
 
 def run_fedopt_sag(defer, container, opt, n_clients, rounds=3, drop=None, seed=0, devices=None, model_fn=None,
-                   opt_args=None, sched_args=None, between_rounds=None):
+                   opt_args=None, sched_args=None, between_rounds=None, edit_weights=None):
     """ScatterAndGather's accept -> aggregate -> shareable_to_learnable -> reset loop (scatter_and_gather.py:
     224-349) with the drop-in aggregator and FedOpt generator; returns per-round weights, aggregated
     differences, optimizer state (one device) and the generator.  ``devices``: both sharded over them."""
@@ -106,6 +106,8 @@ def run_fedopt_sag(defer, container, opt, n_clients, rounds=3, drop=None, seed=0
         agg.reset(fl_ctx)
         diff_host = {k: _np(materialize_deferred(v)).copy() for k, v in diff.items()}
         hist.append(({k: _np(v).copy() for k, v in weights.items()}, diff_host))
+        if edit_weights is not None:  # a filter / persistor writing into the returned global model in place
+            edit_weights(rnd, weights)
         if between_rounds is not None:  # may load new weights into the model; they become the global model
             new = between_rounds(rnd, model, gen)
             if new is not None:

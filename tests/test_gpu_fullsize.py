@@ -77,10 +77,25 @@ def test_full_size_aggregation_sampled(full, oracle, mode):
     assert same_bits(got, exp), f"{np.count_nonzero(got.view(np.uint32) != exp.view(np.uint32))} of {idx.size} differ"
 
 
-def test_full_size_fused_adam_sampled(full, oracle):
+def _sqrt_modes():
+    """The product's sqrt first (``torch_sqrt.mode()``: on the GPU pool's AMD hosts ``torch_cpu_amd``), then the
+    other two restated forms."""
+    from nvflare_amd import torch_sqrt
+
+    first = torch_sqrt.mode()
+    return [first] + [m for m in torch_sqrt.MODES if m != first]
+
+
+@pytest.mark.parametrize("sqrt_idx", [0, 1, 2], ids=["product", "other1", "other2"])
+def test_full_size_fused_adam_sampled(full, oracle, sqrt_idx):
     """Config 5: aggregation + Adam (step 1 then step 2) in one launch per step, sampled against the oracle
-    aggregation followed by the oracle Adam epilogue."""
+    aggregation followed by the oracle Adam epilogue -- in every sqrt the epilogue knows, the one the product
+    ships on this host (``torch_sqrt.mode()``, the bench's config-5 line) first (nvflare/app_opt/pt/fedopt.py:157-182
+    steps with torch CPU's sqrt)."""
     from nvflare_amd import _native as N
+    from nvflare_amd import torch_sqrt
+
+    sqrt_mode = _sqrt_modes()[sqrt_idx]
 
     ctx, lay, slab, bases, P = full
     ws = oracle.synth_weights(K)
@@ -104,13 +119,15 @@ def test_full_size_fused_adam_sampled(full, oracle):
         e.kind = N.FEDAVG_EPI_ADAM
         e.step = float(step)
         e.param, e.state1, e.state2 = p.ptr, m.ptr, v.ptr
+        e.torch_sqrt = torch_sqrt.epilogue_flag(sqrt_mode)
         for k, val in hp.items():
             setattr(e, k, val)
         ctx.accumulate_tiled_epi(bases, ws, lay.tile, lay.tile_stride, 0, end, None, N.FEDAVG_OP_TORCH,
                                  N.FEDAVG_FIN_DIV, count, e)
-        oracle.epilogue_apply(d, oracle.EPI_ADAM, p=p_h, m=m_h, v=v_h, step=float(step), **hp)
+        oracle.epilogue_apply(d, oracle.EPI_ADAM, p=p_h, m=m_h, v=v_h, step=float(step), torch_cpu_sqrt=sqrt_mode,
+                              **hp)
         for name, buf, host in (("p", p, p_h), ("exp_avg", m, m_h), ("exp_avg_sq", v, v_h)):
             got = ctx.gather_f32(buf.ptr, idx)
-            assert same_bits(got, host), f"step {step} {name}"
+            assert same_bits(got, host), f"sqrt {sqrt_mode} step {step} {name}"
     for b in (p, m, v):
         b.close()

@@ -146,3 +146,35 @@ def test_sharded_fedopt_rebind_keeps_state():
             b = sd_got[i][k]
             b = b.detach().cpu().numpy() if isinstance(b, torch.Tensor) else np.asarray(b)
             assert a.shape == b.shape and same_bits(a, b), (i, k)
+
+
+@pytest.mark.parametrize("container", ["numpy", "torch"])
+def test_sharded_fedopt_returned_weights_are_independent(container):
+    """The weights a round returns are independent, writable copies (fedopt.py:232-236 hands out
+    ``detach().cpu().clone()`` / the ``.numpy()`` of its GPU model): a caller writing into them in place
+    changes neither the live parameters nor the next step.  Parameters of the next rounds equal those of a run
+    without the edits; every key equals the one-device flow under the same edits."""
+    def edit(rnd, weights):
+        for v in weights.values():
+            if container == "torch":
+                assert isinstance(v, torch.Tensor)
+                if v.dtype == torch.float32:
+                    v.mul_(3.0).add_(1.0)
+            else:
+                assert isinstance(v, np.ndarray) and v.flags.writeable
+                if v.dtype == np.float32:
+                    v *= 3.0
+                    v += 1.0
+
+    plain, _, _ = run_fedopt_sag(True, container, "adam", 4, rounds=3, model_fn=wide_model, devices=DEVS)
+    runs = []
+    for devices in (None, DEVS):
+        hist, _, gen = run_fedopt_sag(True, container, "adam", 4, rounds=3, model_fn=wide_model, devices=devices,
+                                      edit_weights=edit)
+        runs.append(hist)
+    _compare(runs[0], runs[1])
+    params = {n for n, _ in wide_model().named_parameters()}
+    for (w_plain, _), (w_edit, _) in zip(plain, runs[1]):
+        for k in params:
+            assert same_bits(w_plain[k], w_edit[k]), k
+    assert gen._dev_opt.is_bound()

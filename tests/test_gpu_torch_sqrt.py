@@ -173,3 +173,55 @@ def test_epilogues_with_torch_cpu_sqrt(ctx, oracle, name, hp, K, sqrt):
         if kind == oracle.EPI_NADAM:
             mu = hp["beta1"] * (1.0 - 0.5 * (0.96 ** (step * hp["momentum_decay"])))
             mp = float(np.float32(np.float32(mp) * np.float32(mu)))
+
+
+def test_runtime_rsqrtps_table_on_the_box(ctx, oracle):
+    """the RSQRTPS table FEDAVG_SQRT_TORCH_AMD uses is captured on the host at run time
+    (fedavg_host_rsqrtps_table) and uploaded per context; on the GPU pool's EPYC 9575F it equals the table captured
+    there in round 3 (tests/golden/rsqrtps_amd_epyc9575f.bin), and torch_sqrt.detect() must find the host's path --
+    on this pool a silent fall-back to the correctly rounded sqrt would break Adam's 1-ulp parity."""
+    from test_cpu_rsqrtps_table import BOX_CPU, cpu_model
+
+    from nvflare_amd import torch_sqrt
+
+    tab = torch_sqrt.host_rsqrtps_table()
+    assert np.array_equal(tab, oracle.rsqrtps_table())
+    if BOX_CPU in cpu_model():
+        assert np.array_equal(tab, oracle.rsqrtps_table_box())
+        assert torch_sqrt.detect() == "torch_cpu_amd"
+    assert torch_sqrt.detect() != "unmatched", f"torch.sqrt on {cpu_model()!r} matches no restated path"
+    # the device reads the uploaded table: a different table gives different roots, the host's gives the host's
+    x = (1.0 + np.arange(1 << 16, dtype=np.float32) / (1 << 16)) * np.float32(2.0)
+    ctx.load_rsqrtps(tab[::-1].copy())
+    other = _device_sqrt(ctx, x, 2)
+    ctx.load_rsqrtps(tab)
+    mine = _device_sqrt(ctx, x, 2)
+    assert _same(mine, oracle.sqrt_torch_cpu_amd(x, tab)) == 0
+    assert _same(other, mine) > 1000
+
+
+@pytest.mark.parametrize("threads", [1, 3, 16])
+def test_short_and_ragged_calls_match_the_hosts_torch(ctx, threads):
+    """torch.sqrt on short tensors (1..67 elements) and on lengths that leave ragged chunk tails under
+    at::parallel_for (grain 32768), at several intra-op thread counts, against the device sqrt in the mode this
+    host's torch was detected as -- MKL's short-call and remainder paths, not only its long batches."""
+    import torch
+
+    from nvflare_amd import torch_sqrt
+
+    mode = torch_sqrt.detect()
+    if mode == "unmatched":
+        pytest.fail("this host's torch.sqrt matches no restated path")
+    flag = {"torch_cpu": 1, "torch_cpu_amd": 2, "ieee": 0}[mode]
+    rng = np.random.default_rng(threads)
+    sizes = list(range(1, 68)) + [32767, 32768, 32769, 65536 + 13, 3 * 32768 + 5, 100_003]
+    saved = torch.get_num_threads()
+    torch.set_num_threads(threads)
+    try:
+        for n in sizes:
+            x = np.abs(rng.standard_normal(n)).astype(np.float32) * np.float32(10.0) ** rng.integers(-30, 30, n).astype(np.float32)
+            want = torch.from_numpy(x.copy()).sqrt().numpy()
+            got = _device_sqrt(ctx, x, flag)
+            assert _same(got, want) == 0, (n, threads, mode)
+    finally:
+        torch.set_num_threads(saved)

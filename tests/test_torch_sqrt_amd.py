@@ -9,7 +9,7 @@ coupled Newton step in plain fp32 from the RSQRTPS estimate, which differs betwe
   RSQRTPS (captured by tools/rsqrtps_dump.c at test time) equals MKL's EX kernel on every mantissa of several
   binades and a stride-61 sample of all 2^32 inputs (tools/sqrt_mkl_sse_check.py ran all 2^32: 0 mismatches);
 * the SSE2 kernel (E2HA) shares the refinement with an IEEE-only estimate: oracle_sqrt_mkl_sse2 equals it too;
-* with the AMD host's table (nvflare_amd/data/rsqrtps_amd.bin, captured on the box) the restatement reproduces the
+* with the AMD host's table (tests/golden/rsqrtps_amd_epyc9575f.bin, captured on the box) the restatement reproduces the
   box's own torch.sqrt: tests/golden/sqrt_amd_box.npz (100,000 inputs of [1, 4); all 2^24 matched offline);
 * whole torch optimizer runs with torch's sqrt swapped for MKL's EX kernel run here equal the oracle's
   "torch_cpu_amd" epilogues given this CPU's table: single-tensor Adam / AdamW / amsgrad / NAdam / RAdam / Adagrad /
@@ -94,7 +94,7 @@ def test_every_mantissa_of_a_binade(oracle, here_rsqrtps, exp):
     got2, ref2 = oracle.sqrt_torch_cpu_sse2(x), mkl_sse2(x)
     assert same_bits(got2, ref2), int(np.count_nonzero(got2.view(np.uint32) != ref2.view(np.uint32)))
     if exp in (0, 1):  # a different function from the correctly rounded sqrt and from the AVX-512 path
-        amd = oracle.sqrt_torch_cpu_amd(x)
+        amd = oracle.sqrt_torch_cpu_amd(x, oracle.rsqrtps_table_box())
         assert np.count_nonzero(amd.view(np.uint32) != np.sqrt(x).view(np.uint32)) > 500_000
         assert np.count_nonzero(amd.view(np.uint32) != oracle.sqrt_torch_cpu(x).view(np.uint32)) > 500_000
 
@@ -118,7 +118,7 @@ def test_specials_and_callout_edges(oracle, here_rsqrtps):
 
 def test_amd_table_reproduces_the_box_torch(oracle):
     g = np.load(GOLDEN, allow_pickle=False)
-    got = oracle.sqrt_torch_cpu_amd(g["x"].view(np.float32)).view(np.uint32)
+    got = oracle.sqrt_torch_cpu_amd(g["x"].view(np.float32), oracle.rsqrtps_table_box()).view(np.uint32)
     assert np.array_equal(got, g["torch_sqrt"]), int(np.count_nonzero(got != g["torch_sqrt"]))
     cr = np.sqrt(g["x"].view(np.float32)).view(np.uint32)
     assert np.count_nonzero(cr != g["torch_sqrt"]) > 10_000  # the box's sqrt is not the correctly rounded one
@@ -126,12 +126,26 @@ def test_amd_table_reproduces_the_box_torch(oracle):
 
 def test_probe_vectors_and_detection(oracle):
     v = np.load(torch_sqrt.VECTORS_FILE, allow_pickle=False)
-    assert same_bits(oracle.sqrt_torch_cpu_amd(v["x"]), v["torch_cpu_amd"])
+    assert same_bits(oracle.sqrt_torch_cpu_amd(v["x"], oracle.rsqrtps_table_box()), v["torch_cpu_amd"])
     for other in ("torch_cpu", "ieee"):  # each mode is told apart from the others by thousands of probe values
         assert np.count_nonzero(v["torch_cpu_amd"].view(np.uint32) != v[other].view(np.uint32)) >= 3000
     assert torch_sqrt.detect() in torch_sqrt.MODES + ("unmatched",)
     assert torch_sqrt.epilogue_flag("torch_cpu_amd") == 2 and torch_sqrt.epilogue_flag("torch_cpu") == 1
     assert torch_sqrt.epilogue_flag("ieee") == 0
+
+
+def test_detection_selects_the_sse_path_with_this_cpus_table(oracle):
+    """MKL's SSE4.2 / AVX kernel run HERE (this CPU's RSQRTPS, not the box's: 4000+ of the 8192
+    estimates differ on an Intel host) is identified as "torch_cpu_amd" through the run-time table; with the box's
+    fixture table that identification would fail, and the correctly rounded sqrt is still told apart."""
+    from nvflare_amd import torch_sqrt as ts
+
+    assert ts.detect(host_sqrt=mkl_ex) == "torch_cpu_amd"
+    assert ts.detect(host_sqrt=np.sqrt) == "ieee"
+    x = np.load(ts.VECTORS_FILE, allow_pickle=False)["x"]
+    here, box = ts.host_rsqrtps_table(), oracle.rsqrtps_table_box()
+    if not np.array_equal(here, box):
+        assert not np.array_equal(mkl_ex(x).view(np.uint32), ts.sqrt_sse_restated(x, box).view(np.uint32))
 
 
 @pytest.fixture

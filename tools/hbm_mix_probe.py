@@ -36,6 +36,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--build-only", action="store_true")
+    ap.add_argument("--preset", choices=["default", "few"], default="default")
     a = ap.parse_args()
     lp = lib_path()
     if a.build_only:
@@ -77,6 +78,18 @@ def main():
              ("dyn_r8_l9_avg12", 6, 8, 9, 1, 12), ("dyn_r8_l9_avg15", 6, 8, 9, 1, 15),
              ("dyn_r8_l4_avg11", 6, 8, 4, 2, 11), ("dyn_r8_l4_avg12", 6, 8, 4, 2, 12),
              ("kernel", -1, 0, 0, 0)]
+    if a.preset == "few":  # few-client shapes (R = 1..4): the additive bound's halves, the per-chunk store forms at
+        # several occupancies, and the multi forms (G chunks' loads in flight per lane, stores immediate / deferred)
+        cases = [("read", 1, 0, 0, 1), ("read", 1, 0, 0, 2), ("read", 1, 0, 0, 4),
+                 ("write", 4, 0, 0, 1), ("write", 4, 0, 0, 2), ("write", 4, 0, 0, 4),
+                 ("grid", 0, 0, 0, 2), ("grid", 0, 0, 0, 4), ("grid", 0, 0, 0, 8),
+                 ("tile", 2, 0, 0, 1), ("tile", 2, 0, 0, 2), ("tile", 2, 0, 0, 4),
+                 ("burst_r8_l4", 3, 8, 4, 2)]
+        for g in (1, 2, 4):
+            for bpc in (1, 2, 4):
+                cases.append((f"multi_g{g}", 8, g, 0, bpc))
+                cases.append((f"multi_defer_g{g}", 9, g, 0, bpc))
+        cases.append(("kernel", -1, 0, 0, 0))
     if os.environ.get("MIX_CASES"):  # comma list of probe names to run
         keep = set(os.environ["MIX_CASES"].split(","))
         cases = [c for c in cases if c[0] in keep]

@@ -206,6 +206,7 @@ __global__ void __launch_bounds__(256) p_chunk_lds(const f32x4* __restrict__ src
 //   mix 3  burst:     REG chunks' results in registers + LDS chunks' results in LDS per block, stored at the end
 //                     of a launch of blocks x (REG + LDS) chunks (the burst kernel's pattern, no arithmetic)
 //   mix 7  write_aux: mix 4 through buffer stores with cache-policy bits (reg = 0 plain, 2 nt, 16 sc1, 17 sc0 sc1)
+//   mix 8 / 9 multi:  G chunks per block per iteration, all their loads in flight, stores immediate / deferred (below)
 //   mix 4  write:     the write region alone, 16 KiB per chunk per block (mix 5: grid-stride) -- with mix 1 the
 //                     additive bound t_read + t_write of a mix whose reads and writes share the HBM data bus
 // ---------------------------------------------------------------------------------------------------------
@@ -223,18 +224,88 @@ __global__ void __launch_bounds__(256) m_grid(const f32x4* __restrict__ src, int
     }
 }
 
-// one chunk of R x 1024 float4: 16 loads in flight per lane, 4 float4 of result per lane
+// one chunk of R x 1024 float4: min(R, 4) segments' loads in flight per lane (16 from R = 4 on), 4 float4 of
+// result per lane
 template <int R>
 __device__ inline void m_chunk_sum(const f32x4* __restrict__ p, f32x4 (&acc)[4]) {
+    constexpr int GR = R < 4 ? R : 4;
+    static_assert(R % GR == 0, "R must be 1, 2, 3 or a multiple of 4");
 #pragma unroll
     for (int q = 0; q < 4; ++q) acc[q] = f32x4{0, 0, 0, 0};
 #pragma unroll 1
-    for (int g = 0; g < R; g += 4) {
-        f32x4 v[16];
+    for (int g = 0; g < R; g += GR) {
+        f32x4 v[GR * 4];
 #pragma unroll
-        for (int u = 0; u < 16; ++u) v[u] = __builtin_nontemporal_load(p + (int64_t)(g + u / 4) * 1024 + (u % 4) * 256);
+        for (int u = 0; u < GR * 4; ++u) v[u] = __builtin_nontemporal_load(p + (int64_t)(g + u / 4) * 1024 + (u % 4) * 256);
 #pragma unroll
-        for (int u = 0; u < 16; ++u) acc[u % 4] += v[u];
+        for (int u = 0; u < GR * 4; ++u) acc[u % 4] += v[u];
+    }
+}
+
+// mix 8 / 9  multi (few-client shapes, round 4): every block takes G chunks per iteration (chunks base + j * grid,
+// round-robin as the slab kernels deal tiles) and issues ALL their R x 4 x G loads per lane before any arithmetic --
+// G x R x 64 B in flight per lane -- then stores the G results (mix 8), or holds them and stores them after the NEXT
+// iteration's loads are issued (mix 9, DEFER: the stores never sit in front of loads the lane waits for)
+template <int R, int G, bool DEFER>
+__global__ void __launch_bounds__(256) m_multi(const f32x4* __restrict__ src, int64_t n_chunks, f32x4* __restrict__ dst) {
+    f32x4 pend[G][4];
+    int64_t pend_base = -1;
+    const int64_t step = (int64_t)G * gridDim.x;
+    for (int64_t base = blockIdx.x; base < n_chunks; base += step) {
+        f32x4 v[G][R][4];
+#pragma unroll
+        for (int j = 0; j < G; ++j) {
+            int64_t c = base + (int64_t)j * gridDim.x;
+            c = c < n_chunks ? c : n_chunks - 1;  // clamped: loads unconditional, stores masked
+#pragma unroll
+            for (int r = 0; r < R; ++r)
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    v[j][r][q] = __builtin_nontemporal_load(src + (c * R + r) * 1024 + q * 256 + threadIdx.x);
+        }
+        if constexpr (DEFER) {
+            asm volatile("" ::: "memory");  // keep the held stores behind this iteration's loads
+            if (pend_base >= 0) {
+#pragma unroll
+                for (int j = 0; j < G; ++j) {
+                    const int64_t c = pend_base + (int64_t)j * gridDim.x;
+                    if (c < n_chunks)
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) __builtin_nontemporal_store(pend[j][q], dst + c * 1024 + q * 256 + threadIdx.x);
+                }
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < G; ++j) {
+            f32x4 acc[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                acc[q] = v[j][0][q];
+#pragma unroll
+                for (int r = 1; r < R; ++r) acc[q] += v[j][r][q];
+            }
+            if constexpr (DEFER) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) pend[j][q] = acc[q];
+            } else {
+                const int64_t c = base + (int64_t)j * gridDim.x;
+                if (c < n_chunks)
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) __builtin_nontemporal_store(acc[q], dst + c * 1024 + q * 256 + threadIdx.x);
+            }
+        }
+        if constexpr (DEFER) pend_base = base;
+    }
+    if constexpr (DEFER) {
+        if (pend_base >= 0) {
+#pragma unroll
+            for (int j = 0; j < G; ++j) {
+                const int64_t c = pend_base + (int64_t)j * gridDim.x;
+                if (c < n_chunks)
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) __builtin_nontemporal_store(pend[j][q], dst + c * 1024 + q * 256 + threadIdx.x);
+            }
+        }
     }
 }
 
@@ -401,6 +472,21 @@ static int mix_launch(int mode, int reg, int lds, const f32x4* src, int64_t n_ch
         else if (reg == 17) hipLaunchKernelGGL(m_write_chunks_aux<17>, dim3(blocks), dim3(256), 0, s, n_chunks, dst);
         else return 9;
         *n_launch = 1;
+    } else if (mode == 8 || mode == 9) {  // reg = G chunks per iteration
+#define M_MULTI(GG)                                                                                                   \
+    if (reg == GG) {                                                                                                  \
+        if (mode == 8) hipLaunchKernelGGL((m_multi<R, GG, false>), dim3(blocks), dim3(256), 0, s, src, n_chunks, dst); \
+        else hipLaunchKernelGGL((m_multi<R, GG, true>), dim3(blocks), dim3(256), 0, s, src, n_chunks, dst);           \
+    }
+        if constexpr (R <= 4) {
+            M_MULTI(1)
+            else M_MULTI(2) else M_MULTI(4) else return 11;
+        } else {
+            M_MULTI(1)
+            else return 11;
+        }
+#undef M_MULTI
+        *n_launch = 1;
     } else if (mode == 1 || mode == 2) {
         if (mode == 1) hipLaunchKernelGGL((m_tile<R, false>), dim3(blocks), dim3(256), 0, s, src, n_chunks, dst, sink);
         else hipLaunchKernelGGL((m_tile<R, true>), dim3(blocks), dim3(256), 0, s, src, n_chunks, dst, sink);
@@ -449,7 +535,7 @@ static int mix_launch(int mode, int reg, int lds, const f32x4* src, int64_t n_ch
 extern "C" {
 void mix_set_dyn(int avg) { g_dyn_avg = avg > 0 ? avg : 12; }
 
-// R:1 mix over `bytes` of buf (see above); R in {4, 8, 16}; returns 0 on success, ms_out = average over reps,
+// R:1 mix over `bytes` of buf (see above); R in {1, 2, 3, 4, 8, 16} (mix 8 / 9: G in {1, 2, 4} up to R = 4, 1 above); returns 0 on success, ms_out = average over reps,
 // bytes_out = bytes moved per rep (reads + writes), launches_out = kernel launches per rep
 int mix_run(int mode, int R, int reg, int lds, void* buf, size_t bytes, int blocks, int reps, float* ms_out,
             double* bytes_out, int* launches_out) {
@@ -466,7 +552,10 @@ int mix_run(int mode, int R, int reg, int lds, void* buf, size_t bytes, int bloc
     f32x4* dst = (f32x4*)buf + n_chunks * R * 1024;
     int rc = 0, nl = 0;
     auto launch = [&]() {
-        if (R == 4) rc = mix_launch<4>(mode, reg, lds, src, n_chunks, dst, sink, blocks, s, &nl);
+        if (R == 1) rc = mix_launch<1>(mode, reg, lds, src, n_chunks, dst, sink, blocks, s, &nl);
+        else if (R == 2) rc = mix_launch<2>(mode, reg, lds, src, n_chunks, dst, sink, blocks, s, &nl);
+        else if (R == 3) rc = mix_launch<3>(mode, reg, lds, src, n_chunks, dst, sink, blocks, s, &nl);
+        else if (R == 4) rc = mix_launch<4>(mode, reg, lds, src, n_chunks, dst, sink, blocks, s, &nl);
         else if (R == 8) rc = mix_launch<8>(mode, reg, lds, src, n_chunks, dst, sink, blocks, s, &nl);
         else if (R == 16) rc = mix_launch<16>(mode, reg, lds, src, n_chunks, dst, sink, blocks, s, &nl);
         else rc = 5;
