@@ -580,15 +580,25 @@ def run_host_resident(args, world, rank, local, K, P, seed, sharded=False):
             helper = make_host_helper(local, devices=[0] * world if shared else list(range(world)))
         else:
             helper = make_host_helper(local)
-    t_accept, out, elapsed = 0.0, None, 0.0
+    t_accept, t_drain, out, elapsed = 0.0, 0.0, None, 0.0
     try:
+        def drain():
+            """Wait until the staged client bytes are on the device(s): ``add`` returns once a client's bytes are in
+            the pinned ring (the caller may reuse its array), with up to 4 x 64 MiB still crossing PCIe, and those
+            DMAs would otherwise be counted in get_result."""
+            eng = helper.engine
+            for e in getattr(eng, "engines", [eng]):
+                e.ctx.sync()
+
         def one_round(r):
             a0 = time.perf_counter()
             for k in range(K):
                 helper.add({"w": clients[k]}, weights[k], f"site-{k}", r)
             a1 = time.perf_counter()
+            drain()
+            a2 = time.perf_counter()
             res = helper.get_result()["w"]
-            return res, a1 - a0
+            return res, a1 - a0, a2 - a1
 
         for r in range(warmup if active else 0):
             one_round(r)
@@ -596,8 +606,9 @@ def run_host_resident(args, world, rank, local, K, P, seed, sharded=False):
         dist_barrier(world)
         t0 = time.perf_counter()
         for r in range(steps if active else 0):
-            out, dt = one_round(warmup + r)
+            out, dt, dd = one_round(warmup + r)
             t_accept += dt
+            t_drain += dd
         device_sync()
         elapsed = time.perf_counter() - t0
         dist_barrier(world)
@@ -613,6 +624,7 @@ def run_host_resident(args, world, rank, local, K, P, seed, sharded=False):
         sampled, mism = sum_over_ranks(world, sc or [0, 0])
         return {"K": K, "P": P, "wall": wall, "steps": steps, "warmup": warmup, "sharded": sharded,
                 "accept_s": max_over_ranks(world, t_accept / steps),
+                "drain_s": max_over_ranks(world, t_drain / steps),
                 "result_type": type(out).__name__ if active else None,
                 "devices": len(helper.engine.engines) if sharded and active else 1,
                 "spot_check": {"compared": sampled, "mismatches": mism, "ranks": 1 if sharded else world,
@@ -654,8 +666,11 @@ def summarize_host_resident(args, world, r):
         "scaling": "strong" if sharded else "weak", "steps": r["steps"], "warmup": r["warmup"],
         "ms_per_step": round(step_s * 1e3, 2),
         "accept_ms_per_step": round(r["accept_s"] * 1e3, 2),
-        ("h2d_GBps_all_gpus" if sharded else "h2d_GBps_per_gpu"): round(4.0 * r["K"] * r["P"] / r["accept_s"] / 1e9, 2),
-        "get_result_ms": round((step_s - r["accept_s"]) * 1e3, 2),
+        # the staging DMAs still in flight when the last add returned (the pinned ring's last slots)
+        "staging_drain_ms": round(r["drain_s"] * 1e3, 2),
+        ("h2d_GBps_all_gpus" if sharded else "h2d_GBps_per_gpu"):
+            round(4.0 * r["K"] * r["P"] / (r["accept_s"] + r["drain_s"]) / 1e9, 2),
+        "get_result_ms": round((step_s - r["accept_s"] - r["drain_s"]) * 1e3, 2),
         "spot_check": r["spot_check"],
         "config": {"clients": r["K"], ("params_total" if sharded else "params_per_gpu"): r["P"],
                    "container": "numpy (pageable)", "keys": 1, "mode": "numpy", "result": r["result_type"],
@@ -773,6 +788,7 @@ def guarded_entry(args, world, rank, local, line, also, state, token):
     dog = threading.Timer(args.watchdog_s, on_timeout)
     dog.daemon = True
     dog.start()
+    t_entry = time.perf_counter()
     try:
         if token in (HOST_RESIDENT, HOST_SHARDED):
             p = PRESETS[2]
@@ -793,6 +809,7 @@ def guarded_entry(args, world, rank, local, line, also, state, token):
             also.append(summarize_host_resident(args, world, r))
         else:
             also.append(summarize_client_sharded(args, world, r))
+        also[-1]["elapsed_s"] = round(time.perf_counter() - t_entry, 2)  # the entry's whole wall time
     return bool("skipped" not in r and (r.get("spot_check") or {}).get("mismatches")), dog
 
 
@@ -812,8 +829,10 @@ def main(argv=None):
     K = args.clients
     label = (PRESET_NAMES[args.config] if args.preset_exact
              else f"custom (preset {args.config} overridden: {K} clients x {args.params} params, {args.epilogue})")
+    t_main = time.perf_counter()
     main_res = run_workload(args, ctx, world, rank, K, args.params, args.scaling, args.epilogue,
                             baseline=(world == 1 and rank == 0 and not args.no_cpu_baseline), seed=args.seed)
+    main_s = time.perf_counter() - t_main
     if "skipped" in main_res:
         raise SystemExit(f"rank {rank}: workload {main_res['skipped']}")
     also = []
@@ -822,6 +841,7 @@ def main(argv=None):
         if cfg in (CLIENT_SHARDED, HOST_RESIDENT, HOST_SHARDED):
             continue  # last, each under a watchdog (below)
         p = PRESETS[cfg]
+        t_entry = time.perf_counter()
         r = run_workload(args, ctx, world, rank, p["clients"], p["params"], p["scaling"], p["epilogue"],
                          baseline=False, seed=args.seed)
         failed = failed or bool((r.get("spot_check") or {}).get("mismatches"))
@@ -832,6 +852,7 @@ def main(argv=None):
                 entry = summarize(args, world, r, p["clients"], p["scaling"], p["epilogue"], PRESET_NAMES[cfg])
                 entry["n_gpus"] = world
                 entry["spot_check"] = r["spot_check"]
+                entry["elapsed_s"] = round(time.perf_counter() - t_entry, 2)  # fill, warmup, steps, spot check
                 also.append(entry)
     line = None
     if rank == 0:
@@ -853,6 +874,7 @@ def main(argv=None):
             "pct_hbm_peak": s["pct_hbm_peak"],
             "roofline": s["roofline"],
             "cpu_baseline": main_res.get("cpu_baseline"),
+            "elapsed_s": round(main_s, 2),  # the main entry's wall time: fill, warmup, steps, spot check, CPU baseline
         }
         if main_res.get("spot_check") is not None:
             line["spot_check"] = main_res["spot_check"]

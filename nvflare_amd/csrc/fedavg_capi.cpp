@@ -371,6 +371,7 @@ double fin_scalar(int fin, double count) { return fin == FEDAVG_FIN_SCALE ? 1.0 
 // the burst form, where SGD's larger burst gain was not measured.  The stand-alone server step (no clients, the
 // aggregate as acc_in: one read) takes the per-tile form.
 constexpr int kBurstMinClients = 4;
+constexpr int kVariantFewBurst = 256;  // public variant bit 8: launches under kBurstMinClients reads keep the burst form
 constexpr int kEpiBurstMinClients = 4;
 
 // Tile-kernel launches over [b, e) (elements, multiples of 4) for any number of clients: chunks of at
@@ -393,7 +394,8 @@ void run_tiles(fedavg_ctx* ctx, const void* const* bases, const double* weights,
         const int kc = std::min(k_rows - k0, fedavg::kMaxRowsPerLaunch);
         // the kernel form per launch: a chained chunk (acc_in + kc clients) reads kc + 1 rows
         const int reads = kc + (cur_in ? 1 : 0);
-        const int variant = ctx->variant | (reads < kBurstMinClients ? fedavg::kVariantTileStores : 0);
+        const int variant =
+            ctx->variant | (reads < kBurstMinClients && !(ctx->variant & kVariantFewBurst) ? fedavg::kVariantTileStores : 0);
         const bool burst = fedavg::tiles_use_burst(L.tile4, L.unroll, variant);
         const int bpc = burst ? ctx->bpc(k_rows >= fedavg::kBurstOneBlockMinK ? 1 : 2) : ctx->bpc();
         // one block per CU: the burst kernel holds 10 tiles in LDS (all 160 KiB); public bit 6 keeps the 4-tile
@@ -1414,7 +1416,7 @@ int fedavg_set_launch(fedavg_ctx* ctx, int blocks_per_cu, int unroll) {
 int fedavg_set_variant(fedavg_ctx* ctx, int variant) {
     return guarded([&] {
         if (!ctx) throw Error("ctx is NULL");
-        if (variant < 0 || variant > 127) throw Error("variant must be 0..127");
+        if (variant < 0 || variant > 511) throw Error("variant must be 0..511");
         ctx->variant = variant;
     });
 }

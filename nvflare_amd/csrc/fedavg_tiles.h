@@ -7,6 +7,9 @@
 
 namespace fedavg {
 
+constexpr int kVariantRuntimeK = 128;  // burst kernels: the runtime-K tile loop even where the launch's client count
+                                       // (1 .. 8) has a build-time specialisation (tile_sum_kc, round 4)
+
 // ---------------------------------------------------------------------------------------------
 // THE HOT KERNEL.  Global f32x4 index range [b4, e4); tiles t = b4/T4 .. (e4-1)/T4 are dealt to blocks
 // round-robin.  For every column of a tile:
@@ -66,6 +69,55 @@ __global__ void __launch_bounds__(kBlock) fedavg_tiles_f32x4(const RowTableF32 t
     }
 }
 
+// tile_sum with the launch's client count KC known at build time (round 4; fedavg_arith.h tile_sum is the runtime-K
+// form): groups of min(KC - g, 4) clients -- exactly the launch's rows, where the runtime form's last group re-loads
+// its last client in the missing slots (at K = 2 half of a tile's loads were such repeats) -- and every row pointer
+// and weight at a fixed kernarg offset, loaded once per kernel into SGPRs instead of per group and tile.
+template <int OP, bool ACC_IN, int KC, int CPL>
+__device__ __forceinline__ void tile_sum_kc(f32x4 (&acc)[CPL], const RowTableF32& tab, const int64_t off, const int64_t col,
+                                            const f32x4* acc_in, const int64_t b4, const int64_t e4) {
+    if constexpr (ACC_IN) {
+#pragma unroll
+        for (int c = 0; c < CPL; ++c) {
+            const int64_t i = col + c * kBlock;
+            acc[c] = (i >= b4 && i < e4) ? __builtin_nontemporal_load(acc_in + i) : f32x4{0, 0, 0, 0};
+        }
+    }
+#pragma unroll
+    for (int g = 0; g < KC; g += 4) {
+        f32x4 v[4][CPL];
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            if (g + j < KC)
+#pragma unroll
+                for (int c = 0; c < CPL; ++c) v[j][c] = __builtin_nontemporal_load(tab.rows[g + j] + off + c * kBlock);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            if (g + j < KC) {
+                const float w = tab.w[g + j];
+                if (!ACC_IN && g + j == 0) {
+#pragma unroll
+                    for (int c = 0; c < CPL; ++c) acc[c] = first4<OP>(v[j][c], w);
+                } else {
+#pragma unroll
+                    for (int c = 0; c < CPL; ++c) acc[c] = step4<OP>(acc[c], v[j][c], w);
+                }
+            }
+        }
+    }
+}
+
+// one tile's sum: the KC form above when the client count is a build-time constant (KC > 0), else the runtime form
+template <int OP, bool ACC_IN, int UNROLL, int CPL, int KC>
+__device__ __forceinline__ void tile_sum_any(f32x4 (&acc)[CPL], const RowTableF32& tab, const int K, const int64_t off,
+                                             const int64_t col, const f32x4* acc_in, const int64_t b4, const int64_t e4) {
+    if constexpr (KC > 0) {
+        tile_sum_kc<OP, ACC_IN, KC, CPL>(acc, tab, off, col, acc_in, b4, e4);
+    } else {
+        tile_sum<OP, ACC_IN, UNROLL, CPL, true>(acc, tab, K, off, col, acc_in, b4, e4);
+    }
+}
+
 // ---------------------------------------------------------------------------------------------
 // BURST form of the hot kernel (launch variant bit 5).  Measured on MI355X (profiles/r02/pattern_probe):
 // a 1 MiB-chunk read stream reaches 88 % of spec alone, but adding the result stream (1/64 of the bytes,
@@ -80,7 +132,7 @@ __global__ void __launch_bounds__(kBlock) fedavg_tiles_f32x4(const RowTableF32 t
 // ---------------------------------------------------------------------------------------------
 // TPB_LDS > 0 (the default; launch variant bit 5 turns it off): TPB_LDS more tiles per block whose results wait in LDS (each lane
 // reads back only what it wrote, so no barrier), making each launch (TPB + TPB_LDS) / TPB times longer.
-template <int OP, int FIN, bool ACC_IN, int UNROLL, int CPL, int TPB, int TPB_LDS = 0>
+template <int OP, int FIN, bool ACC_IN, int UNROLL, int CPL, int TPB, int TPB_LDS = 0, int KC = 0>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, 1)))
 fedavg_tiles_burst_f32x4(const RowTableF32 tab, const int K, const int64_t tstride4, const f32x4* acc_in, f32x4* out,
                          const int64_t b4, const int64_t e4, const float fin_val, const int64_t t0, const int64_t t_end) {
@@ -92,8 +144,8 @@ fedavg_tiles_burst_f32x4(const RowTableF32 tab, const int K, const int64_t tstri
         const int64_t t = t0 + blockIdx.x + (int64_t)m * gridDim.x;
         if (t < t_end) {
             f32x4 acc[CPL];
-            tile_sum<OP, ACC_IN, UNROLL, CPL, true>(acc, tab, K, t * tstride4 + threadIdx.x, t * T4 + threadIdx.x,
-                                                    acc_in, b4, e4);
+            tile_sum_any<OP, ACC_IN, UNROLL, CPL, KC>(acc, tab, K, t * tstride4 + threadIdx.x, t * T4 + threadIdx.x,
+                                                      acc_in, b4, e4);
 #pragma unroll
             for (int c = 0; c < CPL; ++c) res[m][c] = fin4<FIN>(acc[c], fin_val);
         }
@@ -104,8 +156,8 @@ fedavg_tiles_burst_f32x4(const RowTableF32 tab, const int K, const int64_t tstri
         const int64_t t = t0 + blockIdx.x + (int64_t)m * gridDim.x;
         if (t < t_end) {
             f32x4 acc[CPL];
-            tile_sum<OP, ACC_IN, UNROLL, CPL, true>(acc, tab, K, t * tstride4 + threadIdx.x, t * T4 + threadIdx.x,
-                                                    acc_in, b4, e4);
+            tile_sum_any<OP, ACC_IN, UNROLL, CPL, KC>(acc, tab, K, t * tstride4 + threadIdx.x, t * T4 + threadIdx.x,
+                                                      acc_in, b4, e4);
 #pragma unroll
             for (int c = 0; c < CPL; ++c) staged[((m - TPB) * CPL + c) * kBlock + threadIdx.x] = fin4<FIN>(acc[c], fin_val);
         }
@@ -139,16 +191,44 @@ fedavg_tiles_burst_f32x4(const RowTableF32 tab, const int K, const int64_t tstri
 // launchers
 // ---------------------------------------------------------------------------------------------
 // one launch per grid x (TPB + TPB_LDS) tiles (fedavg_tiles_burst_f32x4)
-template <int OP, int FIN, bool ACC_IN, int UNROLL, int CPL, int TPB, int TPB_LDS = 0>
-inline hipError_t launch_burst(const TileLaunch& L, hipStream_t s, uint64_t* nl) {
+template <int OP, int FIN, bool ACC_IN, int UNROLL, int CPL, int TPB, int TPB_LDS, int KC>
+inline hipError_t launch_burst_kc(const TileLaunch& L, hipStream_t s, uint64_t* nl) {
     const f32x4* ai = reinterpret_cast<const f32x4*>(L.acc_in);
     f32x4* o = reinterpret_cast<f32x4*>(L.out);
     return burst_launches(L.b4 / L.tile4, (L.e4 - 1) / L.tile4 + 1, L.grid, TPB + TPB_LDS, nl,
                           L.variant & kVariantAnyOrder, [&](int nb, int64_t t0, int64_t t_end, uint32_t flags) {
-                              hipExtLaunchKernelGGL((fedavg_tiles_burst_f32x4<OP, FIN, ACC_IN, UNROLL, CPL, TPB, TPB_LDS>),
-                                                    dim3(nb), dim3(kBlock), 0, s, nullptr, nullptr, flags, L.tab, L.k,
-                                                    L.tstride4, ai, o, L.b4, L.e4, L.fin_val, t0, t_end);
+                              hipExtLaunchKernelGGL(
+                                  (fedavg_tiles_burst_f32x4<OP, FIN, ACC_IN, UNROLL, CPL, TPB, TPB_LDS, KC>), dim3(nb),
+                                  dim3(kBlock), 0, s, nullptr, nullptr, flags, L.tab, L.k, L.tstride4, ai, o, L.b4, L.e4,
+                                  L.fin_val, t0, t_end);
                           });
+}
+
+// the burst kernel with the launch's client count built in (KC, up to kBurstKcMax) unless variant bit 7 asks for the
+// runtime-K form; more clients take the runtime form
+template <int OP, int FIN, bool ACC_IN, int UNROLL, int CPL, int TPB, int TPB_LDS = 0>
+inline hipError_t launch_burst(const TileLaunch& L, hipStream_t s, uint64_t* nl) {
+    if constexpr (CPL == 4 && UNROLL == 4) {
+        if (!(L.variant & kVariantRuntimeK)) {
+            switch (L.k) {
+#define FEDAVG_KC(N) \
+    case N:          \
+        return launch_burst_kc<OP, FIN, ACC_IN, UNROLL, CPL, TPB, TPB_LDS, N>(L, s, nl);
+                FEDAVG_KC(1)
+                FEDAVG_KC(2)
+                FEDAVG_KC(3)
+                FEDAVG_KC(4)
+                FEDAVG_KC(5)
+                FEDAVG_KC(6)
+                FEDAVG_KC(7)
+                FEDAVG_KC(8)
+#undef FEDAVG_KC
+                default:
+                    break;
+            }
+        }
+    }
+    return launch_burst_kc<OP, FIN, ACC_IN, UNROLL, CPL, TPB, TPB_LDS, 0>(L, s, nl);
 }
 
 template <int OP, int FIN, bool ACC_IN, int UNROLL, int CPL>

@@ -458,8 +458,9 @@ class DeviceContext:
                ctypes.c_int(int(torch_sqrt)))
 
     def load_rsqrtps(self, table: Optional[np.ndarray] = None) -> None:
-        """Upload the RSQRTPS table FEDAVG_SQRT_TORCH_AMD reads (fedavg_set_rsqrtps_table): ``table``, or -- once per
-        context -- THIS host CPU's estimates captured at run time (torch_sqrt.host_rsqrtps_table)."""
+        """Upload the RSQRTPS table FEDAVG_SQRT_TORCH_AMD reads (fedavg_set_rsqrtps_table): ``table`` (kept until the
+        next upload), or -- when the context has none yet -- THIS host CPU's estimates captured at run time
+        (torch_sqrt.host_rsqrtps_table)."""
         if table is None and getattr(self, "_rsqrtps_loaded", False):
             return
         from . import torch_sqrt
@@ -467,7 +468,7 @@ class DeviceContext:
         t = np.ascontiguousarray(torch_sqrt.host_rsqrtps_table() if table is None else table, dtype=np.uint16)
         with self.lock:
             N.call("fedavg_set_rsqrtps_table", self.handle, ctypes.c_void_p(t.ctypes.data), ctypes.c_size_t(t.size))
-            self._rsqrtps_loaded = table is None
+            self._rsqrtps_loaded = True
 
     def gather_f32(self, src_ptr: int, idx: np.ndarray) -> np.ndarray:
         idx = np.ascontiguousarray(idx, dtype=np.uint64)

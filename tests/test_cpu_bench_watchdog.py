@@ -96,7 +96,7 @@ def test_host_sharded_entry_needs_two_gpus_and_summarises_strong():
     failed, dog = bench.guarded_entry(args, 1, 0, 0, {}, also, {}, bench.HOST_SHARDED)
     dog.cancel()
     assert failed is False and "needs >= 2 GPUs" in also[0]["skipped"]
-    r = {"K": 8, "P": 1000, "wall": 0.5, "steps": 5, "warmup": 3, "sharded": True, "accept_s": 0.08,
+    r = {"K": 8, "P": 1000, "wall": 0.5, "steps": 5, "warmup": 3, "sharded": True, "accept_s": 0.08, "drain_s": 0.005,
          "result_type": "ndarray", "devices": 4, "spot_check": None}
     e = bench.summarize_host_resident(args, 4, r)
     assert e["scaling"] == "strong" and e["config"]["devices"] == 4 and e["config"]["params_total"] == 1000

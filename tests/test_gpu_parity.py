@@ -290,16 +290,21 @@ def test_launch_variants_same_bits(ctx, oracle, bpc, unroll, tile, variant):
         assert same_bits(got, exp)
 
 
-@pytest.mark.parametrize("K,bpc", [(20, 0), (7, 0), (20, 3), (131, 0), (1, 0), (2, 0), (129, 0)])
-def test_burst_many_launches(ctx, oracle, K, bpc):
+@pytest.mark.parametrize("K,bpc,variant", [(20, 0, 0), (7, 0, 0), (20, 3, 0), (131, 0, 0), (1, 0, 0), (2, 0, 0),
+                                           (129, 0, 0), (1, 0, 256), (2, 0, 256), (3, 0, 256), (3, 0, 384), (4, 0, 0),
+                                           (5, 0, 0), (8, 0, 0), (8, 0, 128), (9, 0, 0), (130, 0, 256), (136, 0, 0)])
+def test_burst_many_launches(ctx, oracle, K, bpc, variant):
     """The default (burst) kernel issues one launch per grid x 8 tiles: more tiles than one launch covers,
     a last launch with fewer tiles than blocks, a sub-range starting and ending inside tiles, more than
     128 clients (chained through the output), against the oracle bit for bit.  One and two clients, and a
-    chained last chunk of one client (129), take the per-tile-store kernel (fedavg_capi.cpp kBurstMinClients)."""
+    chained last chunk of one client (129), take the per-tile-store kernel (fedavg_capi.cpp kBurstMinClients);
+    variant bit 8 keeps them on the burst form.  1-8 clients per launch (a chained last chunk of 1-8: 129-136) take
+    the burst kernel with the client count built in (tile_sum_kc, round 4); bit 7 the runtime-K loop."""
     n = 2048 * 4096 * 2 + 12345
     rows = [oracle.synth_values(5, k, np.arange(n, dtype=np.uint64)) for k in range(K)]
     ws = oracle.synth_weights(K)
     ctx.set_launch(bpc, 0)
+    ctx.set_variant(variant)
     try:
         for op, fin, mode in ((1, 2, oracle.MODE_TORCH), (0, 1, oracle.MODE_NUMPY)):
             exp = oracle.fedavg_c(rows, ws, mode, fin=fin, nthreads=8)
@@ -325,6 +330,7 @@ def test_burst_many_launches(ctx, oracle, K, bpc):
             b.close()
     finally:
         ctx.set_launch(0, 0)
+        ctx.set_variant(0)
 
 
 def test_large_k64(ctx, oracle):

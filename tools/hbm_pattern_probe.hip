@@ -424,6 +424,213 @@ __global__ void __launch_bounds__(256) m_burst_dyn(const f32x4* __restrict__ src
     }
 }
 
+// ---------------------------------------------------------------------------------------------------------
+// EPILOGUE-shaped mixes (round 4): the fused server step at few clients.  n chunks; chunk c reads R client
+// segments (16 KiB each, contiguous: the slab's tile) and three operand segments (p, m, v: three arrays of n x 16 KiB)
+// and writes the three operand segments back IN PLACE -- (R + 3) x 16 KiB read, 3 x 16 KiB written per chunk (Adam at
+// R clients; R = 2: 20:12).  The arithmetic is a stand-in (d = sum; p += d; m = 0.9 m + d; v += d d).
+//   epi 0  tile2:  per chunk the client loads, then the operand loads (the library's per-tile order), then the stores
+//   epi 1  tile1:  per chunk the client and the operand loads together, then the stores
+//   epi 2  burst:  REG chunks' new p, m, v held in registers and LDS chunks' in LDS, stored at the end of a launch of
+//                  blocks x (REG + LDS) chunks (reads and writes in chip-wide phases)
+//   epi 3  burst_d: the library's burst order: the client sums of REG + LDS chunks first (d in registers / LDS), then
+//                  per chunk the operand loads, arithmetic and stores (one chunk of operands ahead)
+// ---------------------------------------------------------------------------------------------------------
+struct EpiBufs {
+    const f32x4* cl;
+    f32x4* op[3];
+};
+
+__device__ inline void e_ops(const f32x4 d, f32x4& p, f32x4& m, f32x4& v) {
+    p += d;
+    m = m * 0.9f + d;
+    v += d * d;
+}
+
+template <int R>
+__device__ inline void e_sum(const f32x4* __restrict__ cl, int64_t c, f32x4 (&d)[4]) {
+    f32x4 x[R][4];
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) x[r][q] = __builtin_nontemporal_load(cl + (c * R + r) * 1024 + q * 256 + threadIdx.x);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        d[q] = x[0][q];
+#pragma unroll
+        for (int r = 1; r < R; ++r) d[q] += x[r][q];
+    }
+}
+
+template <int R, bool TOGETHER>
+__global__ void __launch_bounds__(256) e_tile(EpiBufs B, int64_t n) {
+    for (int64_t c = blockIdx.x; c < n; c += gridDim.x) {
+        f32x4 o[3][4];
+        f32x4 d[4];
+        if constexpr (TOGETHER) {
+#pragma unroll
+            for (int k = 0; k < 3; ++k)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) o[k][q] = __builtin_nontemporal_load(B.op[k] + c * 1024 + q * 256 + threadIdx.x);
+            e_sum<R>(B.cl, c, d);
+        } else {
+            e_sum<R>(B.cl, c, d);
+            asm volatile("" ::: "memory");  // the operand loads after the client sums, as the library orders them
+#pragma unroll
+            for (int k = 0; k < 3; ++k)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) o[k][q] = __builtin_nontemporal_load(B.op[k] + c * 1024 + q * 256 + threadIdx.x);
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) e_ops(d[q], o[0][q], o[1][q], o[2][q]);
+#pragma unroll
+        for (int k = 0; k < 3; ++k)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) __builtin_nontemporal_store(o[k][q], B.op[k] + c * 1024 + q * 256 + threadIdx.x);
+    }
+}
+
+template <int R, int REG, int LDS>
+__global__ void __launch_bounds__(256) e_burst(EpiBufs B, int64_t c0, int64_t c_end) {
+    f32x4 res[REG > 0 ? REG : 1][3][4];
+    __shared__ f32x4 stage[LDS > 0 ? LDS * 3 * 1024 : 1];
+#pragma unroll
+    for (int m = 0; m < REG; ++m) {
+        const int64_t c = c0 + blockIdx.x + (int64_t)m * gridDim.x;
+        if (c < c_end) {
+            f32x4 d[4];
+#pragma unroll
+            for (int k = 0; k < 3; ++k)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) res[m][k][q] = __builtin_nontemporal_load(B.op[k] + c * 1024 + q * 256 + threadIdx.x);
+            e_sum<R>(B.cl, c, d);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) e_ops(d[q], res[m][0][q], res[m][1][q], res[m][2][q]);
+        }
+    }
+#pragma unroll 1
+    for (int m = 0; m < LDS; ++m) {
+        const int64_t c = c0 + blockIdx.x + (int64_t)(REG + m) * gridDim.x;
+        if (c < c_end) {
+            f32x4 o[3][4], d[4];
+#pragma unroll
+            for (int k = 0; k < 3; ++k)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) o[k][q] = __builtin_nontemporal_load(B.op[k] + c * 1024 + q * 256 + threadIdx.x);
+            e_sum<R>(B.cl, c, d);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                e_ops(d[q], o[0][q], o[1][q], o[2][q]);
+#pragma unroll
+                for (int k = 0; k < 3; ++k) stage[(m * 3 + k) * 1024 + q * 256 + threadIdx.x] = o[k][q];
+            }
+        }
+    }
+#pragma unroll 1
+    for (int m = 0; m < LDS; ++m) {
+        const int64_t c = c0 + blockIdx.x + (int64_t)(REG + m) * gridDim.x;
+        if (c < c_end)
+#pragma unroll
+            for (int k = 0; k < 3; ++k)
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    __builtin_nontemporal_store(stage[(m * 3 + k) * 1024 + q * 256 + threadIdx.x], B.op[k] + c * 1024 + q * 256 + threadIdx.x);
+    }
+#pragma unroll
+    for (int m = 0; m < REG; ++m) {
+        const int64_t c = c0 + blockIdx.x + (int64_t)m * gridDim.x;
+        if (c < c_end)
+#pragma unroll
+            for (int k = 0; k < 3; ++k)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) __builtin_nontemporal_store(res[m][k][q], B.op[k] + c * 1024 + q * 256 + threadIdx.x);
+    }
+}
+
+template <int R, int REG, int LDS>
+__global__ void __launch_bounds__(256) e_burst_d(EpiBufs B, int64_t c0, int64_t c_end) {
+    f32x4 dd[REG > 0 ? REG : 1][4];
+    __shared__ f32x4 stage[LDS > 0 ? LDS * 1024 : 1];
+#pragma unroll
+    for (int m = 0; m < REG; ++m) {
+        const int64_t c = c0 + blockIdx.x + (int64_t)m * gridDim.x;
+        if (c < c_end) e_sum<R>(B.cl, c, dd[m]);
+    }
+#pragma unroll 1
+    for (int m = 0; m < LDS; ++m) {
+        const int64_t c = c0 + blockIdx.x + (int64_t)(REG + m) * gridDim.x;
+        if (c < c_end) {
+            f32x4 d[4];
+            e_sum<R>(B.cl, c, d);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) stage[m * 1024 + q * 256 + threadIdx.x] = d[q];
+        }
+    }
+    constexpr int NT = REG + LDS;
+    auto load_ops = [&](f32x4 (&o)[3][4], int m) __attribute__((always_inline)) {
+        int64_t c = c0 + blockIdx.x + (int64_t)m * gridDim.x;
+        c = c < c_end ? c : c_end - 1;
+#pragma unroll
+        for (int k = 0; k < 3; ++k)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) o[k][q] = __builtin_nontemporal_load(B.op[k] + c * 1024 + q * 256 + threadIdx.x);
+    };
+    f32x4 cur[3][4], nxt[3][4];
+    load_ops(cur, 0);
+#pragma unroll
+    for (int m = 0; m < NT; ++m) {
+        if (m + 1 < NT) load_ops(nxt, m + 1);
+        const int64_t c = c0 + blockIdx.x + (int64_t)m * gridDim.x;
+        if (c < c_end) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const f32x4 d = m < REG ? dd[m < REG ? m : 0][q] : stage[(m - REG) * 1024 + q * 256 + threadIdx.x];
+                e_ops(d, cur[0][q], cur[1][q], cur[2][q]);
+            }
+#pragma unroll
+            for (int k = 0; k < 3; ++k)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) __builtin_nontemporal_store(cur[k][q], B.op[k] + c * 1024 + q * 256 + threadIdx.x);
+        }
+#pragma unroll
+        for (int k = 0; k < 3; ++k)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) cur[k][q] = nxt[k][q];
+    }
+}
+
+template <int R>
+static int epi_launch(int mode, int reg, int lds, EpiBufs B, int64_t n, int blocks, hipStream_t s, int* n_launch) {
+    *n_launch = 0;
+    if (mode == 0 || mode == 1) {
+        if (mode == 0) hipLaunchKernelGGL((e_tile<R, false>), dim3(blocks), dim3(256), 0, s, B, n);
+        else hipLaunchKernelGGL((e_tile<R, true>), dim3(blocks), dim3(256), 0, s, B, n);
+        *n_launch = 1;
+        return 0;
+    }
+    const int64_t per = (int64_t)blocks * (reg + lds);
+    for (int64_t c0 = 0; c0 < n; c0 += per) {
+        const int64_t ce = c0 + per < n ? c0 + per : n;
+        const int nb = (int)(ce - c0 < blocks ? ce - c0 : blocks);
+#define E_B(KERN, RG, LD) \
+    if (reg == RG && lds == LD) hipLaunchKernelGGL((KERN<R, RG, LD>), dim3(nb), dim3(256), 0, s, B, c0, ce)
+        if (mode == 2) {
+            E_B(e_burst, 4, 0);
+            else E_B(e_burst, 4, 3);
+            else E_B(e_burst, 2, 1);
+            else E_B(e_burst, 3, 0);
+            else return 4;
+        } else {
+            E_B(e_burst_d, 8, 4);
+            else E_B(e_burst_d, 8, 9);
+            else return 4;
+        }
+#undef E_B
+        ++*n_launch;
+    }
+    return 0;
+}
+
 static int g_dyn_avg = 12;  // chunks per block per launch of mix 6 (the blocks' average; capacity REG + LDS)
 
 // write-only streams of the same write region (the other half of an additive read + write bound)
@@ -571,6 +778,43 @@ int mix_run(int mode, int R, int reg, int lds, void* buf, size_t bytes, int bloc
     *bytes_out = (double)n_chunks * (mode == 1 ? R * 16384.0 : (mode == 4 || mode == 5 || mode == 7) ? 16384.0 : (R + 1) * 16384.0);
     *launches_out = nl;
     hipFree(sink);
+    hipEventDestroy(a);
+    hipEventDestroy(b);
+    hipStreamDestroy(s);
+    if (rc != 0) return 10 + rc;
+    return hipGetLastError() == hipSuccess ? 0 : 3;
+}
+
+// the epilogue-shaped mixes (above) over `bytes` of buf; R in {1, 2, 3}; bytes_out = bytes moved per rep
+int epi_run(int mode, int R, int reg, int lds, void* buf, size_t bytes, int blocks, int reps, float* ms_out,
+            double* bytes_out, int* launches_out) {
+    hipStream_t s;
+    if (hipStreamCreate(&s) != hipSuccess) return 1;
+    hipEvent_t a, b;
+    (void)hipEventCreate(&a);
+    (void)hipEventCreate(&b);
+    const int64_t unit = (int64_t)(R + 3) * 16384;
+    const int64_t n = (int64_t)bytes / unit;
+    EpiBufs B;
+    B.cl = (const f32x4*)buf;
+    for (int k = 0; k < 3; ++k) B.op[k] = (f32x4*)buf + n * R * 1024 + (int64_t)k * n * 1024;
+    int rc = 0, nl = 0;
+    auto launch = [&]() {
+        if (R == 1) rc = epi_launch<1>(mode, reg, lds, B, n, blocks, s, &nl);
+        else if (R == 2) rc = epi_launch<2>(mode, reg, lds, B, n, blocks, s, &nl);
+        else if (R == 3) rc = epi_launch<3>(mode, reg, lds, B, n, blocks, s, &nl);
+        else rc = 5;
+    };
+    launch();
+    hipEventRecord(a, s);
+    for (int r = 0; r < reps && rc == 0; ++r) launch();
+    hipEventRecord(b, s);
+    hipEventSynchronize(b);
+    float ms = 0;
+    hipEventElapsedTime(&ms, a, b);
+    *ms_out = ms / reps;
+    *bytes_out = (double)n * (R + 6) * 16384.0;
+    *launches_out = nl;
     hipEventDestroy(a);
     hipEventDestroy(b);
     hipStreamDestroy(s);
