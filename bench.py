@@ -36,6 +36,7 @@ oracle (test infrastructure; never the measured path).
 from __future__ import annotations
 
 import argparse
+import gc
 import json
 import os
 import sys
@@ -602,11 +603,19 @@ def run_host_resident(args, world, rank, local, K, P, seed, sharded=False):
 
         for r in range(warmup if active else 0):
             one_round(r)
+        # Python's cyclic collector would otherwise scan the whole heap (torch's objects included) at some point
+        # inside a timed round -- a 20 ms pause in one round of five seen on the box; a long-running server freezes
+        # its startup objects the same way
+        gc.collect()
+        gc.freeze()
         device_sync()
         dist_barrier(world)
+        rounds_ms = []
         t0 = time.perf_counter()
         for r in range(steps if active else 0):
+            r0 = time.perf_counter()
             out, dt, dd = one_round(warmup + r)
+            rounds_ms.append(((time.perf_counter() - r0) - dt - dd) * 1e3)
             t_accept += dt
             t_drain += dd
         device_sync()
@@ -625,12 +634,14 @@ def run_host_resident(args, world, rank, local, K, P, seed, sharded=False):
         return {"K": K, "P": P, "wall": wall, "steps": steps, "warmup": warmup, "sharded": sharded,
                 "accept_s": max_over_ranks(world, t_accept / steps),
                 "drain_s": max_over_ranks(world, t_drain / steps),
+                "get_result_ms_rounds": [round(x, 2) for x in rounds_ms],
                 "result_type": type(out).__name__ if active else None,
                 "devices": len(helper.engine.engines) if sharded and active else 1,
                 "spot_check": {"compared": sampled, "mismatches": mism, "ranks": 1 if sharded else world,
                                "oracle": "oracle/fedavg_oracle.c (every element of the last round's result)"}
                 if args.spot_check > 0 else None}
     finally:
+        gc.unfreeze()
         if helper is not None:
             helper.reset_stats()
         del helper, clients
@@ -671,6 +682,7 @@ def summarize_host_resident(args, world, r):
         ("h2d_GBps_all_gpus" if sharded else "h2d_GBps_per_gpu"):
             round(4.0 * r["K"] * r["P"] / (r["accept_s"] + r["drain_s"]) / 1e9, 2),
         "get_result_ms": round((step_s - r["accept_s"] - r["drain_s"]) * 1e3, 2),
+        "get_result_ms_rounds": r.get("get_result_ms_rounds"),  # rank 0's rounds (kernel + D2H + host work)
         "spot_check": r["spot_check"],
         "config": {"clients": r["K"], ("params_total" if sharded else "params_per_gpu"): r["P"],
                    "container": "numpy (pageable)", "keys": 1, "mode": "numpy", "result": r["result_type"],

@@ -319,27 +319,34 @@ int fedavg_timing_begin(fedavg_ctx* ctx);
 int fedavg_timing_end(fedavg_ctx* ctx, float* ms);
 
 /* Aggregation / epilogue / dequantization kernel launches issued on the context's compute stream so far.
- * One fedavg_accumulate* call may issue several (the fp32 burst kernel: one per 12 tiles per block); relates a
- * profiler's per-launch durations to per-call times. */
+ * One fedavg_accumulate* call may issue several (the fp32 burst kernels: one per grid x tiles-per-block tiles --
+ * 18 tiles per block on the one-block-per-CU grids of the plain kernel at 32+ clients (17 for the fused kernel at
+ * 64+), 12 on two-block grids); relates a profiler's per-launch durations to per-call times. */
 int fedavg_launch_count(fedavg_ctx* ctx, uint64_t* n);
 /* Launch tuning (0 = default): blocks per CU (default: each kernel's own -- 1 for the burst aggregation
  * kernel at >= 32 clients, the fused one at >= 64, the 16-bit one at >= 48 in torch mode, 2 otherwise),
  * clients whose loads are issued together (4 or 8, default 4). */
 int fedavg_set_launch(fedavg_ctx* ctx, int blocks_per_cu, int unroll);
-/* Kernel variants (default 0: the aggregation -- plain or with a fused epilogue -- holds each block's
- * results in registers and stores them (runs the epilogue) as chip-wide bursts, one launch per 8 tiles per
- * block; every load and store nontemporal).
- * bit 3 = each tile's results stored (epilogue run) as the tile finishes (the round-1 kernels);
- * bit 0 / bit 1 = the plain one with temporal client loads / temporal result stores (imply bit 3);
+/* Kernel variants (default 0).  By default a launch with 4 or more row reads (its clients, plus the chained partial
+ * sum of a launch after the first 128 clients) runs the BURST form: each block holds its tiles' results (the fused
+ * kernel: its differences) in registers and LDS and stores them (runs the epilogue) as chip-wide bursts at the end of
+ * a short launch -- per launch 8 register-held tiles per block plus 4 LDS-held ones on two-block-per-CU grids, or 10
+ * (fused: 9) on the one-block-per-CU grids of the plain kernel at 32+ clients (fused: 64+); a launch with fewer row
+ * reads (1-3: most NVFlare jobs run 2 clients) runs the PER-TILE-STORE form, which stores each tile's results as it
+ * finishes; every load and store is nontemporal.  The plain burst kernel has the launch's client count built in for
+ * 1-6 clients and the count's remainder mod 4 from 7 on (no repeated loads).  The bits (results are bit-identical in
+ * every variant):
+ * bit 0 / bit 1 = the per-tile-store plain kernel with temporal client loads / temporal result stores (imply bit 3);
  * bit 2 = the per-tile epilogue kernel software-pipelined across tiles (the next tile's first client loads
- * overlap the epilogue; implies bit 3 for the epilogue);
- * bit 4 = burst launches after the first of a call go out without the AQL barrier bit (hipExtAnyOrderLaunch),
- * so one launch's blocks start as the previous launch drains;
- * bit 5 = the plain burst kernel WITHOUT its 4 LDS-held tiles per block (default: 8 tiles' results in registers
- * and 4 in LDS, 12 tiles per block per launch; with bit 5, 8);
- * bit 6 = one-block-per-CU grids (32+ clients; 64+ for the fused kernel) keep the 4-LDS-tile form (default there:
- * 10 tiles' results in LDS, all 160 KiB of the CU's LDS, 18 tiles per block per launch; the fused kernel 9, 17).
- * Results are bit-identical in every variant. */
+ *         overlap the epilogue; implies bit 3 for the epilogue);
+ * bit 3 = every launch on the per-tile-store form;
+ * bit 4 = burst launches after the first of a call go out without the AQL barrier bit (hipExtAnyOrderLaunch), so
+ *         one launch's blocks start as the previous launch drains;
+ * bit 5 = the burst kernels without their LDS-held tiles (register-held tiles only: 8 per block per launch);
+ * bit 6 = one-block-per-CU grids keep the 4-LDS-tile form (12 tiles per block per launch);
+ * bit 7 = the plain burst kernel's round-3 runtime client loop (its last group of 4 re-loads the last client in the
+ *         missing slots when the count is not a multiple of 4);
+ * bit 8 = plain launches with fewer than 4 row reads keep the burst form. */
 int fedavg_set_variant(fedavg_ctx* ctx, int variant);
 /* Tile width used by fedavg_accumulate for contiguous rows (default 4096 elements). */
 int fedavg_set_tile(fedavg_ctx* ctx, int tile_elems);

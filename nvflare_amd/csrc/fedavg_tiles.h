@@ -7,8 +7,53 @@
 
 namespace fedavg {
 
-constexpr int kVariantRuntimeK = 128;  // burst kernels: the runtime-K tile loop even where the launch's client count
-                                       // (1 .. 8) has a build-time specialisation (tile_sum_kc, round 4)
+constexpr int kVariantRuntimeK = 128;  // burst kernels: round 3's runtime-K tile loop (tile_sum GROUPED) instead of the
+                                       // built-in client count (1-6) or remainder (7+) forms (tile_sum_kc / _rem, round 4)
+
+// ---------------------------------------------------------------------------------------------
+// The finalisation of the plain kernels.  FIN_DIV is torch's total.div_(count) -- the correctly rounded quotient by
+// one launch-constant count b.  Instead of the IEEE division sequence per element (v_div_scale x 2, v_rcp, four FMAs,
+// v_div_fmas, v_div_fixup) it takes Markstein's correction from the correctly rounded reciprocal, computed once per
+// thread:  r = RN(1 / b);  q = RN(a r);  e = fma(-q, b, a) (exact);  a / b = RN(q + e r).  Checked against the IEEE
+// division for every pair of significands (2^23 dividends x 2^23 divisors, tools/div_const_probe.py); away from
+// underflow and overflow the result depends on the significands only, so the fast path runs where 2^-20 <= b <= 2^20
+// (every weight sum of a FedAvg round in practice; a uniform flag) and |a| in [2^-100, 2^100) (exponent field 27..226),
+// which keeps q, e r and every intermediate normal; zeros, subnormals, huge values, inf and NaN take the IEEE division,
+// a branch the waves skip unless one of their lanes needs it.
+// ---------------------------------------------------------------------------------------------
+struct FinConst {
+    float v;     // the finalisation scalar (FIN_SCALE: 1 / count as the reference rounds it; FIN_DIV: count)
+    float r;     // FIN_DIV: RN(1 / count)
+    bool fast;   // FIN_DIV: count in [2^-20, 2^20]
+};
+
+template <int FIN>
+__device__ __forceinline__ FinConst fin_const(const float v) {
+    FinConst f{v, 0.0f, false};
+    if constexpr (FIN == FEDAVG_FIN_DIV) {
+        f.r = 1.0f / v;
+        f.fast = v >= 0x1p-20f && v <= 0x1p20f;
+    }
+    return f;
+}
+
+__device__ __forceinline__ float div_const(const float a, const FinConst& f) {
+    const float q = a * f.r;
+    const float e = __builtin_fmaf(-q, f.v, a);
+    float res = __builtin_fmaf(e, f.r, q);
+    const uint32_t ea = (__float_as_uint(a) >> 23) & 0xFFu;
+    if (__builtin_expect(!f.fast || ea - 27u >= 200u, 0)) res = a / f.v;
+    return res;
+}
+
+template <int FIN>
+__device__ __forceinline__ f32x4 fin4c(const f32x4 a, const FinConst& f) {
+    if constexpr (FIN == FEDAVG_FIN_DIV) {
+        return f32x4{div_const(a[0], f), div_const(a[1], f), div_const(a[2], f), div_const(a[3], f)};
+    } else {
+        return fin4<FIN>(a, f.v);
+    }
+}
 
 // ---------------------------------------------------------------------------------------------
 // THE HOT KERNEL.  Global f32x4 index range [b4, e4); tiles t = b4/T4 .. (e4-1)/T4 are dealt to blocks
@@ -25,6 +70,7 @@ __global__ void __launch_bounds__(kBlock) fedavg_tiles_f32x4(const RowTableF32 t
                                                               const float fin_val) {
     constexpr int64_t T4 = (int64_t)CPL * kBlock;
     const int64_t t_last = (e4 - 1) / T4;
+    const FinConst fc = fin_const<FIN>(fin_val);
     for (int64_t t = b4 / T4 + blockIdx.x; t <= t_last; t += gridDim.x) {
         const int64_t off = t * tstride4 + threadIdx.x;  // offset inside each client's tiled storage
         const int64_t col = t * T4 + threadIdx.x;        // global f32x4 index of column group 0
@@ -64,7 +110,7 @@ __global__ void __launch_bounds__(kBlock) fedavg_tiles_f32x4(const RowTableF32 t
 #pragma unroll
         for (int c = 0; c < CPL; ++c) {
             const int64_t i = col + c * kBlock;
-            if (i >= b4 && i < e4) store4<NTS>(out + i, fin4<FIN>(acc[c], fin_val));
+            if (i >= b4 && i < e4) store4<NTS>(out + i, fin4c<FIN>(acc[c], fc));
         }
     }
 }
@@ -107,12 +153,67 @@ __device__ __forceinline__ void tile_sum_kc(f32x4 (&acc)[CPL], const RowTableF32
     }
 }
 
-// one tile's sum: the KC form above when the client count is a build-time constant (KC > 0), else the runtime form
+// The runtime-K form with the remainder REM = K mod 4 built in: full groups of 4 clients in a loop, then one group of
+// exactly REM clients -- no repeated loads for any K (fedavg_arith.h tile_sum's GROUPED form re-loads the last client
+// 4 - K mod 4 times per tile).
+template <int OP, bool ACC_IN, int REM, int CPL>
+__device__ __forceinline__ void tile_sum_rem(f32x4 (&acc)[CPL], const RowTableF32& tab, const int K, const int64_t off,
+                                             const int64_t col, const f32x4* acc_in, const int64_t b4, const int64_t e4) {
+    if constexpr (ACC_IN) {
+#pragma unroll
+        for (int c = 0; c < CPL; ++c) {
+            const int64_t i = col + c * kBlock;
+            acc[c] = (i >= b4 && i < e4) ? __builtin_nontemporal_load(acc_in + i) : f32x4{0, 0, 0, 0};
+        }
+    }
+    const int k_full = K - REM;
+    for (int k = 0; k < k_full; k += 4) {
+        f32x4 v[4][CPL];
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int c = 0; c < CPL; ++c) v[j][c] = __builtin_nontemporal_load(tab.rows[k + j] + off + c * kBlock);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const float w = tab.w[k + j];
+            if (!ACC_IN && k + j == 0) {
+#pragma unroll
+                for (int c = 0; c < CPL; ++c) acc[c] = first4<OP>(v[j][c], w);
+            } else {
+#pragma unroll
+                for (int c = 0; c < CPL; ++c) acc[c] = step4<OP>(acc[c], v[j][c], w);
+            }
+        }
+    }
+    if constexpr (REM > 0) {
+        f32x4 v[REM][CPL];
+#pragma unroll
+        for (int j = 0; j < REM; ++j)
+#pragma unroll
+            for (int c = 0; c < CPL; ++c) v[j][c] = __builtin_nontemporal_load(tab.rows[k_full + j] + off + c * kBlock);
+#pragma unroll
+        for (int j = 0; j < REM; ++j) {
+            const float w = tab.w[k_full + j];
+            if (!ACC_IN && k_full + j == 0) {
+#pragma unroll
+                for (int c = 0; c < CPL; ++c) acc[c] = first4<OP>(v[j][c], w);
+            } else {
+#pragma unroll
+                for (int c = 0; c < CPL; ++c) acc[c] = step4<OP>(acc[c], v[j][c], w);
+            }
+        }
+    }
+}
+
+// one tile's sum: KC > 0 -- the client count built in (tile_sum_kc); KC = -1 - REM -- the runtime count with its
+// remainder mod 4 built in (tile_sum_rem); KC = 0 -- fedavg_arith.h tile_sum's GROUPED form (variant bit 7, for A/Bs)
 template <int OP, bool ACC_IN, int UNROLL, int CPL, int KC>
 __device__ __forceinline__ void tile_sum_any(f32x4 (&acc)[CPL], const RowTableF32& tab, const int K, const int64_t off,
                                              const int64_t col, const f32x4* acc_in, const int64_t b4, const int64_t e4) {
     if constexpr (KC > 0) {
         tile_sum_kc<OP, ACC_IN, KC, CPL>(acc, tab, off, col, acc_in, b4, e4);
+    } else if constexpr (KC < 0) {
+        tile_sum_rem<OP, ACC_IN, -1 - KC, CPL>(acc, tab, K, off, col, acc_in, b4, e4);
     } else {
         tile_sum<OP, ACC_IN, UNROLL, CPL, true>(acc, tab, K, off, col, acc_in, b4, e4);
     }
@@ -137,6 +238,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, 
 fedavg_tiles_burst_f32x4(const RowTableF32 tab, const int K, const int64_t tstride4, const f32x4* acc_in, f32x4* out,
                          const int64_t b4, const int64_t e4, const float fin_val, const int64_t t0, const int64_t t_end) {
     constexpr int64_t T4 = (int64_t)CPL * kBlock;
+    const FinConst fc = fin_const<FIN>(fin_val);
     f32x4 res[TPB][CPL];
     __shared__ f32x4 staged[TPB_LDS > 0 ? TPB_LDS * CPL * kBlock : 1];
 #pragma unroll
@@ -147,7 +249,7 @@ fedavg_tiles_burst_f32x4(const RowTableF32 tab, const int K, const int64_t tstri
             tile_sum_any<OP, ACC_IN, UNROLL, CPL, KC>(acc, tab, K, t * tstride4 + threadIdx.x, t * T4 + threadIdx.x,
                                                       acc_in, b4, e4);
 #pragma unroll
-            for (int c = 0; c < CPL; ++c) res[m][c] = fin4<FIN>(acc[c], fin_val);
+            for (int c = 0; c < CPL; ++c) res[m][c] = fin4c<FIN>(acc[c], fc);
         }
     }
     // the LDS-held tiles in a rolled loop: one more copy of the tile body, not TPB_LDS of them
@@ -159,7 +261,7 @@ fedavg_tiles_burst_f32x4(const RowTableF32 tab, const int K, const int64_t tstri
             tile_sum_any<OP, ACC_IN, UNROLL, CPL, KC>(acc, tab, K, t * tstride4 + threadIdx.x, t * T4 + threadIdx.x,
                                                       acc_in, b4, e4);
 #pragma unroll
-            for (int c = 0; c < CPL; ++c) staged[((m - TPB) * CPL + c) * kBlock + threadIdx.x] = fin4<FIN>(acc[c], fin_val);
+            for (int c = 0; c < CPL; ++c) staged[((m - TPB) * CPL + c) * kBlock + threadIdx.x] = fin4c<FIN>(acc[c], fc);
         }
     }
 #pragma unroll 1
@@ -204,8 +306,10 @@ inline hipError_t launch_burst_kc(const TileLaunch& L, hipStream_t s, uint64_t* 
                           });
 }
 
-// the burst kernel with the launch's client count built in (KC, up to kBurstKcMax) unless variant bit 7 asks for the
-// runtime-K form; more clients take the runtime form
+// the burst kernel with the launch's client count built in (1-6 clients: every row pointer and weight in SGPRs, every
+// load a real client's; from 7 on -- 7 with a chained partial sum, 8 -- both groups' loads are hoisted together past
+// 256 VGPRs, one wave per SIMD), or from 7 clients on the runtime count with its remainder mod 4 built in; variant bit
+// 7 takes the round-3 runtime form everywhere (A/Bs)
 template <int OP, int FIN, bool ACC_IN, int UNROLL, int CPL, int TPB, int TPB_LDS = 0>
 inline hipError_t launch_burst(const TileLaunch& L, hipStream_t s, uint64_t* nl) {
     if constexpr (CPL == 4 && UNROLL == 4) {
@@ -220,11 +324,19 @@ inline hipError_t launch_burst(const TileLaunch& L, hipStream_t s, uint64_t* nl)
                 FEDAVG_KC(4)
                 FEDAVG_KC(5)
                 FEDAVG_KC(6)
-                FEDAVG_KC(7)
-                FEDAVG_KC(8)
 #undef FEDAVG_KC
                 default:
                     break;
+            }
+            switch (L.k % 4) {
+                case 1:
+                    return launch_burst_kc<OP, FIN, ACC_IN, UNROLL, CPL, TPB, TPB_LDS, -2>(L, s, nl);
+                case 2:
+                    return launch_burst_kc<OP, FIN, ACC_IN, UNROLL, CPL, TPB, TPB_LDS, -3>(L, s, nl);
+                case 3:
+                    return launch_burst_kc<OP, FIN, ACC_IN, UNROLL, CPL, TPB, TPB_LDS, -4>(L, s, nl);
+                default:
+                    return launch_burst_kc<OP, FIN, ACC_IN, UNROLL, CPL, TPB, TPB_LDS, -1>(L, s, nl);
             }
         }
     }

@@ -161,6 +161,8 @@ def test_sharded_fedopt_returned_weights_are_independent(container):
                 if v.dtype == torch.float32:
                     v.mul_(3.0).add_(1.0)
             else:
+                if isinstance(v, np.generic):  # a 0-d key's base + diff is a numpy scalar, as in the reference
+                    continue
                 assert isinstance(v, np.ndarray) and v.flags.writeable
                 if v.dtype == np.float32:
                     v *= 3.0

@@ -26,6 +26,10 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--variants", default="0,4", help="variant bits, or variant:unroll:blocks_per_cu triples")
     ap.add_argument("--epilogues", default="none,adam")
+    ap.add_argument("--pads", default="0", help="tile-stride pads in elements (multiples of 64): one slab each, "
+                                                "interleaved -- DRAM channel mapping of power-of-two strides")
+    ap.add_argument("--mode", choices=["torch", "numpy"], default="torch",
+                    help="torch: fma steps, IEEE division at the end; numpy: mul + add, multiply by 1/count")
     ap.add_argument("--check", action="store_true",
                     help="plain epilogue: every config's output must equal the first config's bit for bit")
     a = ap.parse_args()
@@ -36,10 +40,18 @@ def main():
     K, P = a.clients, int(a.params)
     lay = TiledLayout(4096, K)
     end = (P + 3) // 4 * 4
-    slab = ctx.alloc(lay.slab_elems(P) * 4)
-    bases = [slab.ptr + lay.slot_offset_elems(k) * 4 for k in range(K)]
-    for k in range(K):
-        ctx.fill_synthetic_f32(bases[k], P, 1234, k, 0, lay.tile, lay.tile_stride)
+    pads = [int(x) for x in a.pads.split(",")]
+    slabs = {}
+    for pad in pads:
+        assert pad % 64 == 0
+        stride = lay.tile_stride + pad
+        n_tiles = (P + lay.tile - 1) // lay.tile
+        slab = ctx.alloc(n_tiles * stride * 4)
+        bases = [slab.ptr + k * lay.tile * 4 for k in range(K)]
+        for k in range(K):
+            ctx.fill_synthetic_f32(bases[k], P, 1234, k, 0, lay.tile, stride)
+        slabs[pad] = (slab, bases, stride)
+    op, fin = (1, 2) if a.mode == "torch" else (0, 1)
     ws = [float(1 + (37 * k) % 100) for k in range(K)]
     cnt = sum(ws)
     bufs = [ctx.alloc(end * 4) for _ in range(3)]
@@ -49,9 +61,10 @@ def main():
     ctx.sync()
     kinds = {"add_base": N.FEDAVG_EPI_ADD_BASE, "sgd": N.FEDAVG_EPI_SGD, "adam": N.FEDAVG_EPI_ADAM}
 
-    def launcher(epi):
+    def launcher(epi, pad):
+        _, bases, stride = slabs[pad]
         if epi == "none":
-            return lambda: ctx.accumulate_tiled(bases, ws, lay.tile, lay.tile_stride, 0, end, out.ptr, 1, 2, cnt)
+            return lambda: ctx.accumulate_tiled(bases, ws, lay.tile, stride, 0, end, out.ptr, op, fin, cnt)
         e = N.Epilogue()
         e.kind = kinds[epi]
         e.lr, e.momentum, e.beta1, e.beta2, e.eps, e.step = 1e-3, 0.9, 0.9, 0.999, 1e-8, 1.0
@@ -60,20 +73,20 @@ def main():
         else:
             e.param, e.state1, e.state2 = bufs[0].ptr, bufs[1].ptr, bufs[2].ptr
             o = None
-        return lambda: ctx.accumulate_tiled_epi(bases, ws, lay.tile, lay.tile_stride, 0, end, o, 1, 2, cnt, e)
+        return lambda: ctx.accumulate_tiled_epi(bases, ws, lay.tile, stride, 0, end, o, op, fin, cnt, e)
 
     variants = [tuple(int(x) for x in (v.split(":") + ["0", "0"])[:3]) for v in a.variants.split(",")]
     epis = a.epilogues.split(",")
     res = {}
     ref_out = None
     for rnd in range(a.rounds):
-        for epi in epis:
-            fn = launcher(epi)
+        for epi, pad in [(e_, p_) for e_ in epis for p_ in pads]:
+            fn = launcher(epi, pad)
             for v in variants:
                 ctx.set_variant(v[0])
                 ctx.set_launch(v[2], v[1])
                 fn()
-                if a.check and epi == "none" and rnd == 0:
+                if a.check and epi == "none" and rnd == 0 and pad == pads[0]:
                     host = np.empty(end, dtype=np.float32)
                     ctx.sync()
                     ctx.d2h(host, out.ptr)
@@ -90,16 +103,18 @@ def main():
                     fn()
                 ms = ctx.timing_end() / a.reps
                 gbs = (4.0 * K * P + EXTRA[epi] * P) / ms / 1e6
-                res.setdefault((epi, v), []).append(ms)
-                print(json.dumps({"round": rnd, "epilogue": epi, "variant": ":".join(map(str, v)), "clients": K, "params": P,
+                res.setdefault((epi, pad, v), []).append(ms)
+                print(json.dumps({"round": rnd, "epilogue": epi, "pad": pad, "mode": a.mode,
+                                  "variant": ":".join(map(str, v)), "clients": K, "params": P,
                                   "ms": round(ms, 4), "GBps": round(gbs, 1), "frac_8TBps": round(gbs / 8000, 4)}),
                       flush=True)
     ctx.set_variant(0)
     ctx.set_launch(0, 0)
-    for (epi, v), xs in res.items():
+    for (epi, pad, v), xs in res.items():
         ms = statistics.median(xs)
         gbs = (4.0 * K * P + EXTRA[epi] * P) / ms / 1e6
-        print(json.dumps({"summary": True, "epilogue": epi, "variant": ":".join(map(str, v)), "clients": K, "params": P,
+        print(json.dumps({"summary": True, "epilogue": epi, "pad": pad, "mode": a.mode,
+                          "variant": ":".join(map(str, v)), "clients": K, "params": P,
                           "median_ms": round(ms, 4), "GBps": round(gbs, 1), "frac_8TBps": round(gbs / 8000, 4)}),
               flush=True)
 
