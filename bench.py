@@ -364,7 +364,7 @@ def kernel_name(K, epilogue, variant):
     # per-tile-store kernels
     if epilogue != "none":
         return "fedavg_tiles_epi_burst_f32x4" if variant & 12 == 0 and K >= 4 else "fedavg_tiles_epi_f32x4"
-    if variant & 11 or K < 4:
+    if (variant & 11 or K < 3) and not (K < 3 and variant & 256 and not variant & 11):
         return "fedavg_tiles_f32x4"
     return ("fedavg_tiles_burst_f32x4 (results staged on chip, stored as chip-wide bursts; "
             + ("8 register-held tiles per block per launch)" if variant & 32
@@ -601,8 +601,8 @@ def run_host_resident(args, world, rank, local, K, P, seed, sharded=False):
             res = helper.get_result()["w"]
             return res, a1 - a0, a2 - a1
 
-        for r in range(warmup if active else 0):
-            one_round(r)
+        for r in range(warmup if active else 0):  # holding the previous round's result, as the timed rounds do (a
+            out = one_round(r)[0]                # server keeps the last global model): the pool's steady state
         # Python's cyclic collector would otherwise scan the whole heap (torch's objects included) at some point
         # inside a timed round -- a 20 ms pause in one round of five seen on the box; a long-running server freezes
         # its startup objects the same way

@@ -361,16 +361,17 @@ void normalize_wide(int& op, int& fin, double& count, bool acc_f32) {
 double fin_scalar(int fin, double count) { return fin == FEDAVG_FIN_SCALE ? 1.0 / count : count; }
 
 // Fewest row reads per launch (clients, plus the chained partial sum) that take the burst kernels; fewer go to the
-// per-tile-store kernels (same tile_sum and epilogue arithmetic, so the same bits).  With few reads per result the
-// burst kernel's read phase is too short to pay for holding the results (1e9 params, % of HBM peak, burst vs
-// per-tile, profiles/r03/s24/, s25/): 2 clients 50.7 vs 69.7 %, 3 clients 63.5 vs 71.6 %, 4 clients 70.5 vs 68.9 %
-// on one box and 71.7 vs 73.4 % on another.  The fused epilogue reads and writes its optimizer state in the same
-// launch, so its per-tile form wins further up (Adam, 5e8 params: 1 client 62 vs 73 %, 2: 63.6 vs 77.2 %, 4: 72.9
-// vs 76.2 %), and the burst form wins again from 5 clients on (s26/: Adam 5 / 8 / 16 clients 70.0 / 78.1 / 83.2 vs
-// 68.5 / 69.8 / 71.4 %, SGD 73.8 / 82.7 / 85.7 vs 69.5 / 70.4 / 68.6 %).  The epilogue threshold leaves 4 reads on
-// the burst form, where SGD's larger burst gain was not measured.  The stand-alone server step (no clients, the
-// aggregate as acc_in: one read) takes the per-tile form.
-constexpr int kBurstMinClients = 4;
+// per-tile-store kernels (same tile_sum and epilogue arithmetic, so the same bits).  With one or two row reads per
+// result the burst kernel's read phase is too short to pay for holding the results.  Round 4, with the client count
+// built into the burst kernel (no repeated loads) and the division-free FIN_DIV, same box, % of HBM peak, per-tile vs
+// burst (profiles/r04/s4/divc_k*.jsonl; s2/ab_k*.jsonl on another box): 1 client 63.7 vs 53.9 (74.4 vs 54.7), 2
+// clients 71.1 vs 69.2 (75.4 vs 71.6), 3 clients 70.2 vs 74.8 (71.7 vs 74.5), 4 clients 71.3 vs 72.2.  Round 3 (the
+// burst kernel re-loading clients to fill its groups of four) had the switch at 4.  The fused epilogue keeps 4: its
+// per-tile form wins further up, because its optimizer-state reads and writes fall in the same launch (Adam, 5e8
+// params, per-tile vs burst: 1 client 73 vs 62 %, 2: 77.2 vs 63.6 %, 4: 76.2 vs 72.9 %; from 5 clients on the burst
+// form wins by 1.5-14 points, profiles/r03/s25/, s26/).  The stand-alone server step (no clients, the aggregate as
+// acc_in: one read) takes the per-tile form.
+constexpr int kBurstMinClients = 3;
 constexpr int kVariantFewBurst = 256;  // public variant bit 8: launches under kBurstMinClients reads keep the burst form
 constexpr int kEpiBurstMinClients = 4;
 
