@@ -36,7 +36,6 @@ oracle (test infrastructure; never the measured path).
 from __future__ import annotations
 
 import argparse
-import gc
 import json
 import os
 import sys
@@ -601,13 +600,12 @@ def run_host_resident(args, world, rank, local, K, P, seed, sharded=False):
             res = helper.get_result()["w"]
             return res, a1 - a0, a2 - a1
 
-        for r in range(warmup if active else 0):  # holding the previous round's result, as the timed rounds do (a
-            out = one_round(r)[0]                # server keeps the last global model): the pool's steady state
-        # Python's cyclic collector would otherwise scan the whole heap (torch's objects included) at some point
-        # inside a timed round -- a 20 ms pause in one round of five seen on the box; a long-running server freezes
-        # its startup objects the same way
-        gc.collect()
-        gc.freeze()
+        # the warmup rounds hold the previous round's result, as the timed rounds do (a server keeps the last global
+        # model): the result-array pool then alternates two page-locked arrays from the first timed round on.  Round
+        # 3's warmup dropped its results, so the first timed round that held one paid the page-locking of a second
+        # 500 MB array inside get_result (hipHostRegister, ~20 ms: profiles/r04/s3/trace2h_summary.json)
+        for r in range(warmup if active else 0):
+            out = one_round(r)[0]
         device_sync()
         dist_barrier(world)
         rounds_ms = []
@@ -641,7 +639,6 @@ def run_host_resident(args, world, rank, local, K, P, seed, sharded=False):
                                "oracle": "oracle/fedavg_oracle.c (every element of the last round's result)"}
                 if args.spot_check > 0 else None}
     finally:
-        gc.unfreeze()
         if helper is not None:
             helper.reset_stats()
         del helper, clients

@@ -85,9 +85,9 @@ __device__ __forceinline__ void store4(f32x4* p, f32x4 v) {
 // rows are tiled (row + off is this lane's first column of the tile); acc_in is indexed by global column and
 // masked to [b4, e4).
 // GROUPED: every load group holds UNROLL clients from client 0 on (the first client's operation applied in
-// the first group; a partial last group re-loads its last client in the missing slots, branch-free, and skips
-// their arithmetic), so a tile takes ceil(K / UNROLL) load round trips instead of 1 + (K-1) / UNROLL + the
-// remainder.
+// the first group), so a tile takes ceil(K / UNROLL) load round trips instead of 1 + (K-1) / UNROLL + the
+// remainder.  A partial last group loads only its real clients (wave-uniform branches; round 3 re-loaded the last
+// client in the missing slots, branch-free: at 5 or 6 clients a third of a tile's loads were such repeats).
 template <int OP, bool ACC_IN, int UNROLL, int CPL, bool GROUPED = false>
 __device__ __forceinline__ void tile_sum(f32x4 (&acc)[CPL], const RowTableF32& tab, const int K, const int64_t off,
                                          const int64_t col, const f32x4* acc_in, const int64_t b4, const int64_t e4) {
@@ -103,9 +103,11 @@ __device__ __forceinline__ void tile_sum(f32x4 (&acc)[CPL], const RowTableF32& t
             f32x4 v[UNROLL][CPL];
 #pragma unroll
             for (int j = 0; j < UNROLL; ++j) {
-                const f32x4* r = tab.rows[k + j < K ? k + j : K - 1] + off;
+                if (j == 0 || k + j < K) {  // uniform: only a partial last group skips slots
+                    const f32x4* r = tab.rows[k + j] + off;
 #pragma unroll
-                for (int c = 0; c < CPL; ++c) v[j][c] = __builtin_nontemporal_load(r + c * kBlock);
+                    for (int c = 0; c < CPL; ++c) v[j][c] = __builtin_nontemporal_load(r + c * kBlock);
+                }
             }
 #pragma unroll
             for (int j = 0; j < UNROLL; ++j) {
