@@ -80,6 +80,52 @@ __device__ __forceinline__ void store4(f32x4* p, f32x4 v) {
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Division by a launch constant b: the plain and fused kernels' FIN_DIV (torch's total.div_(count), the correctly
+// rounded quotient by the weight sum) and the fused optimizers' divisions by a bias correction (Adam's
+// sqrt(v) / sqrt(bc2), NAdam's v / bc2, RAdam's m / bc1).  Instead of the IEEE division sequence per element (v_div_scale x 2, v_rcp, four FMAs,
+// v_div_fmas, v_div_fixup) it takes Markstein's correction from the correctly rounded reciprocal, computed once per
+// thread:  r = RN(1 / b);  q = RN(a r);  e = fma(-q, b, a) (exact);  a / b = RN(q + e r).  Checked against the IEEE
+// division for every pair of significands (2^23 dividends x 2^23 divisors, tools/div_const_probe.py); away from
+// underflow and overflow the result depends on the significands only, so the fast path runs where 2^-20 <= b <= 2^20
+// (every weight sum of a FedAvg round in practice; a uniform flag) and |a| in [2^-100, 2^100) (exponent field 27..226),
+// which keeps q, e r and every intermediate normal; zeros, subnormals, huge values, inf and NaN take the IEEE division,
+// a branch the waves skip unless one of their lanes needs it.
+// ---------------------------------------------------------------------------------------------
+struct FinConst {
+    float v;     // the finalisation scalar (FIN_SCALE: 1 / count as the reference rounds it; FIN_DIV: count), or divisor
+    float r;     // divisor: RN(1 / v)
+    bool fast;   // divisor in [2^-20, 2^20]
+};
+
+__device__ __forceinline__ FinConst div_const_init(const float v) {
+    return FinConst{v, 1.0f / v, v >= 0x1p-20f && v <= 0x1p20f};
+}
+
+template <int FIN>
+__device__ __forceinline__ FinConst fin_const(const float v) {
+    if constexpr (FIN == FEDAVG_FIN_DIV) return div_const_init(v);
+    return FinConst{v, 0.0f, false};
+}
+
+__device__ __forceinline__ float div_const(const float a, const FinConst& f) {
+    const float q = a * f.r;
+    const float e = __builtin_fmaf(-q, f.v, a);
+    float res = __builtin_fmaf(e, f.r, q);
+    const uint32_t ea = (__float_as_uint(a) >> 23) & 0xFFu;
+    if (__builtin_expect(!f.fast || ea - 27u >= 200u, 0)) res = a / f.v;
+    return res;
+}
+
+template <int FIN>
+__device__ __forceinline__ f32x4 fin4c(const f32x4 a, const FinConst& f) {
+    if constexpr (FIN == FEDAVG_FIN_DIV) {
+        return f32x4{div_const(a[0], f), div_const(a[1], f), div_const(a[2], f), div_const(a[3], f)};
+    } else {
+        return fin4<FIN>(a, f.v);
+    }
+}
+
 // One tile's arrival-ordered sum for the CPL float4 columns this lane owns: acc = ACC_IN ? acc_in : first(client
 // 0), then step(client k) for every later client, UNROLL clients' loads issued before their arithmetic.  Client
 // rows are tiled (row + off is this lane's first column of the tile); acc_in is indexed by global column and

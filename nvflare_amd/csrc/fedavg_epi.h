@@ -43,6 +43,23 @@ __device__ __forceinline__ float max_torch(float a, float b) {
     return a > b ? a : b;
 }
 
+// the epilogues' launch-constant divisors, prepared once per thread (fedavg_arith.h div_const)
+struct EpiConsts {
+    FinConst bc2s;  // Adam: sqrt(bias_correction2)
+    FinConst bc2;   // NAdam: bias_correction2
+    FinConst bc1;   // RAdam: bias_correction1
+};
+
+template <int EPI>
+__device__ __forceinline__ EpiConsts epi_consts(const EpiParams& E) {
+    constexpr int KIND = EPI & 0xFF;
+    EpiConsts C{};
+    if constexpr (KIND == FEDAVG_EPI_ADAM) C.bc2s = div_const_init(E.bias_correction2_sqrt);
+    if constexpr (KIND == FEDAVG_EPI_NADAM) C.bc2 = div_const_init(E.bias_correction2);
+    if constexpr (KIND == FEDAVG_EPI_RADAM) C.bc1 = div_const_init(E.bias_correction1);
+    return C;
+}
+
 template <int EPI>
 __device__ __forceinline__ EpiIn epi_load(const EpiParams& E, const int64_t i) {
     constexpr int KIND = EPI & 0xFF;
@@ -74,8 +91,8 @@ __device__ __forceinline__ EpiIn epi_load(const EpiParams& E, const int64_t i) {
 }
 
 template <int EPI>
-__device__ __forceinline__ void epilogue4(const EpiParams& E, const int64_t i, const f32x4 d, const EpiIn& in,
-                                          f32x4* out) {
+__device__ __forceinline__ void epilogue4(const EpiParams& E, const EpiConsts& C, const int64_t i, const f32x4 d,
+                                          const EpiIn& in, f32x4* out) {
     constexpr int KIND = EPI & 0xFF;
     constexpr int TSQ = EPI & kEpiSqrtMask;
     f32x4* p4 = reinterpret_cast<f32x4*>(E.param) + i;
@@ -203,11 +220,11 @@ __device__ __forceinline__ void epilogue4(const EpiParams& E, const int64_t i, c
             m[c] = lerp_torch(m[c], g, E.one_minus_beta1, E.one_minus_beta1_m1);
             v[c] = __builtin_fmaf(E.one_minus_beta2 * g, g, v[c] * E.beta2);
             if constexpr (KIND == FEDAVG_EPI_NADAM) {
-                const float denom = sqrt_e<TSQ>(E, v[c] / E.bias_correction2) + E.eps;  // exp_avg_sq.div(bc2).sqrt().add_(eps)
+                const float denom = sqrt_e<TSQ>(E, div_const(v[c], C.bc2)) + E.eps;  // exp_avg_sq.div(bc2).sqrt().add_(eps)
                 pv = pv + (E.coef_grad * g) / denom;                                    // addcdiv_(grad, denom, value)
                 pv = pv + (E.coef_avg * m[c]) / denom;                                  // addcdiv_(exp_avg, denom, value)
             } else {
-                float t = (m[c] / E.bias_correction1) * E.lr;                           // exp_avg / bc1 * lr
+                float t = div_const(m[c], C.bc1) * E.lr;                                // exp_avg / bc1 * lr
                 if (E.rectified) {
                     const float a = (1.0f / (sqrt_e<TSQ>(E, v[c]) + E.eps)) * E.bias_correction2_sqrt;  // bc2**0.5 / (sqrt+eps)
                     t = (t * a) * E.rect;
@@ -239,7 +256,7 @@ __device__ __forceinline__ void epilogue4(const EpiParams& E, const int64_t i, c
                 vmax[c] = max_torch(vmax[c], vv);
                 vden = vmax[c];
             }
-            const float denom = sqrt_e<TSQ>(E, vden) / E.bias_correction2_sqrt + E.eps;
+            const float denom = div_const(sqrt_e<TSQ>(E, vden), C.bc2s) + E.eps;  // sqrt(v) / sqrt(bc2) + eps
             pv = pv + (E.step_size_neg * mm) / denom;
             m[c] = mm;
             v[c] = vv;
@@ -272,6 +289,8 @@ fedavg_tiles_epi_burst_f32x4(const RowTableF32 tab, const int K, const int64_t t
     constexpr int NT = TPB + TPB_LDS;
     f32x4 dd[TPB][CPL];
     __shared__ f32x4 staged[TPB_LDS > 0 ? TPB_LDS * CPL * kBlock : 1];
+    const FinConst fc = fin_const<FIN>(fin_val);
+    const EpiConsts C = epi_consts<EPI>(E);
     if constexpr ((EPI & kEpiTorchSqrt) != 0) rsqrt14_stage();
     if constexpr ((EPI & kEpiTorchSqrtAmd) != 0) rsqrtps_stage(E.rsqrtps);
 #pragma unroll
@@ -282,7 +301,7 @@ fedavg_tiles_epi_burst_f32x4(const RowTableF32 tab, const int K, const int64_t t
             tile_sum<OP, ACC_IN, UNROLL, CPL, true>(acc, tab, K, t * tstride4 + threadIdx.x, t * T4 + threadIdx.x, acc_in,
                                                     b4, e4);
 #pragma unroll
-            for (int c = 0; c < CPL; ++c) dd[m][c] = fin4<FIN>(acc[c], fin_val);
+            for (int c = 0; c < CPL; ++c) dd[m][c] = fin4c<FIN>(acc[c], fc);
         }
     }
 #pragma unroll 1
@@ -293,7 +312,7 @@ fedavg_tiles_epi_burst_f32x4(const RowTableF32 tab, const int K, const int64_t t
             tile_sum<OP, ACC_IN, UNROLL, CPL, true>(acc, tab, K, t * tstride4 + threadIdx.x, t * T4 + threadIdx.x, acc_in,
                                                     b4, e4);
 #pragma unroll
-            for (int c = 0; c < CPL; ++c) staged[((m - TPB) * CPL + c) * kBlock + threadIdx.x] = fin4<FIN>(acc[c], fin_val);
+            for (int c = 0; c < CPL; ++c) staged[((m - TPB) * CPL + c) * kBlock + threadIdx.x] = fin4c<FIN>(acc[c], fc);
         }
     }
     // Epilogue phase, double-buffered: tile m+1's operand loads are issued before tile m's arithmetic and
@@ -325,7 +344,7 @@ fedavg_tiles_epi_burst_f32x4(const RowTableF32 tab, const int K, const int64_t t
                 if (i >= b4 && i < e4) {
                     const f32x4 d = d_of(c);
                     if (out != nullptr && (EPI & 0xFF) != FEDAVG_EPI_ADD_BASE) store4<true>(out + i, d);
-                    epilogue4<EPI>(E, i, d, cur[c], out);
+                    epilogue4<EPI>(E, C, i, d, cur[c], out);
                 }
             }
         }
@@ -359,6 +378,8 @@ __global__ void __launch_bounds__(kBlock) fedavg_tiles_epi_f32x4(const RowTableF
     constexpr int64_t T4 = (int64_t)CPL * kBlock;
     const int64_t t_last = (e4 - 1) / T4;
     const int g0 = PIPE ? (K < UNROLL ? K : UNROLL) : 0;  // clients carried over from the previous tile
+    const FinConst fc = fin_const<FIN>(fin_val);
+    const EpiConsts C = epi_consts<EPI>(E);
     if constexpr ((EPI & kEpiTorchSqrt) != 0) rsqrt14_stage();
     if constexpr ((EPI & kEpiTorchSqrtAmd) != 0) rsqrtps_stage(E.rsqrtps);
     f32x4 nxt[UNROLL][CPL];
@@ -442,9 +463,9 @@ __global__ void __launch_bounds__(kBlock) fedavg_tiles_epi_f32x4(const RowTableF
         for (int c = 0; c < CPL; ++c) {
             const int64_t i = col + c * kBlock;
             if (i >= b4 && i < e4) {
-                const f32x4 d = fin4<FIN>(acc[c], fin_val);
+                const f32x4 d = fin4c<FIN>(acc[c], fc);
                 if (out != nullptr && (EPI & 0xFF) != FEDAVG_EPI_ADD_BASE) store4<true>(out + i, d);
-                epilogue4<EPI>(E, i, d, pre[c], out);
+                epilogue4<EPI>(E, C, i, d, pre[c], out);
             }
         }
     }

@@ -11,51 +11,6 @@ constexpr int kVariantRuntimeK = 128;  // burst kernels: round 3's runtime-K til
                                        // built-in client count (1-6) or remainder (7+) forms (tile_sum_kc / _rem, round 4)
 
 // ---------------------------------------------------------------------------------------------
-// The finalisation of the plain kernels.  FIN_DIV is torch's total.div_(count) -- the correctly rounded quotient by
-// one launch-constant count b.  Instead of the IEEE division sequence per element (v_div_scale x 2, v_rcp, four FMAs,
-// v_div_fmas, v_div_fixup) it takes Markstein's correction from the correctly rounded reciprocal, computed once per
-// thread:  r = RN(1 / b);  q = RN(a r);  e = fma(-q, b, a) (exact);  a / b = RN(q + e r).  Checked against the IEEE
-// division for every pair of significands (2^23 dividends x 2^23 divisors, tools/div_const_probe.py); away from
-// underflow and overflow the result depends on the significands only, so the fast path runs where 2^-20 <= b <= 2^20
-// (every weight sum of a FedAvg round in practice; a uniform flag) and |a| in [2^-100, 2^100) (exponent field 27..226),
-// which keeps q, e r and every intermediate normal; zeros, subnormals, huge values, inf and NaN take the IEEE division,
-// a branch the waves skip unless one of their lanes needs it.
-// ---------------------------------------------------------------------------------------------
-struct FinConst {
-    float v;     // the finalisation scalar (FIN_SCALE: 1 / count as the reference rounds it; FIN_DIV: count)
-    float r;     // FIN_DIV: RN(1 / count)
-    bool fast;   // FIN_DIV: count in [2^-20, 2^20]
-};
-
-template <int FIN>
-__device__ __forceinline__ FinConst fin_const(const float v) {
-    FinConst f{v, 0.0f, false};
-    if constexpr (FIN == FEDAVG_FIN_DIV) {
-        f.r = 1.0f / v;
-        f.fast = v >= 0x1p-20f && v <= 0x1p20f;
-    }
-    return f;
-}
-
-__device__ __forceinline__ float div_const(const float a, const FinConst& f) {
-    const float q = a * f.r;
-    const float e = __builtin_fmaf(-q, f.v, a);
-    float res = __builtin_fmaf(e, f.r, q);
-    const uint32_t ea = (__float_as_uint(a) >> 23) & 0xFFu;
-    if (__builtin_expect(!f.fast || ea - 27u >= 200u, 0)) res = a / f.v;
-    return res;
-}
-
-template <int FIN>
-__device__ __forceinline__ f32x4 fin4c(const f32x4 a, const FinConst& f) {
-    if constexpr (FIN == FEDAVG_FIN_DIV) {
-        return f32x4{div_const(a[0], f), div_const(a[1], f), div_const(a[2], f), div_const(a[3], f)};
-    } else {
-        return fin4<FIN>(a, f.v);
-    }
-}
-
-// ---------------------------------------------------------------------------------------------
 // THE HOT KERNEL.  Global f32x4 index range [b4, e4); tiles t = b4/T4 .. (e4-1)/T4 are dealt to blocks
 // round-robin.  For every column of a tile:
 //     acc = ACC_IN ? acc_in[i] : first(client 0);  acc = step(acc, client k) for k = 1..K-1 in order;

@@ -23,12 +23,15 @@ for C in FETCH_SIZE WRITE_SIZE; do
   timeout -s KILL 180 rocprofv3 --pmc $C --output-format csv -d "$OUT/pmc/adam_$C" -o pmc -- $B --config 5 --also none --steps 2 --warmup 1 --no-cpu-baseline --spot-check 0 > "$OUT/pmc_adam_$C.log" 2>&1 || exit $?
   timeout -s KILL 180 rocprofv3 --pmc $C --output-format csv -d "$OUT/pmc/k2_$C" -o pmc -- $B --clients 2 --params 1e9 --also none --steps 2 --warmup 1 --no-cpu-baseline --spot-check 0 > "$OUT/pmc_k2_$C.log" 2>&1 || exit $?
 done
-# the fused kernel's partial last client group without repeated loads (fedavg_arith.h tile_sum, round 4) against the
-# previous commit's library, Adam at 5 / 6 / 7 / 10 clients and 8 (no partial group) as the control, interleaved twice
+# the fused kernel's partial last client group without repeated loads (fedavg_arith.h tile_sum) and its constant
+# divisions by Markstein's correction (FIN_DIV, Adam's sqrt(bc2)) against the library of commit 4f8a188: Adam at
+# 5 / 6 / 7 / 10 clients, 8 (no partial group), 2 (per-tile form) and config 5, interleaved twice
 cd "$GRAFT_REPO_ROOT"
 HEADLIB=$GRAFT_REPO_ROOT/nvflare_amd/lib/ab/libnvflare_amd_fedavg_head.so
 for i in 1 2; do
-  for K in 5 6 7 10 8; do
+  NVFLARE_AMD_FEDAVG_LIB=$HEADLIB timeout -k 10 300 $B --config 5 --also none --no-cpu-baseline > "$OUT/epi_head_c5_$i.jsonl" 2> "$OUT/epi_head_c5_$i.err" || exit $?
+  timeout -k 10 300 $B --config 5 --also none --no-cpu-baseline > "$OUT/epi_new_c5_$i.jsonl" 2> "$OUT/epi_new_c5_$i.err" || exit $?
+  for K in 5 6 7 10 8 2; do
     timeout -k 10 300 $B --clients $K --params 5e8 --epilogue adam --also none --no-cpu-baseline --steps 10 > "$OUT/epi_new_k${K}_$i.jsonl" 2> "$OUT/epi_new_k${K}_$i.err" || exit $?
     NVFLARE_AMD_FEDAVG_LIB=$HEADLIB timeout -k 10 300 $B --clients $K --params 5e8 --epilogue adam --also none --no-cpu-baseline --steps 10 > "$OUT/epi_head_k${K}_$i.jsonl" 2> "$OUT/epi_head_k${K}_$i.err" || exit $?
   done
