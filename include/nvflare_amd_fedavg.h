@@ -346,7 +346,9 @@ int fedavg_set_launch(fedavg_ctx* ctx, int blocks_per_cu, int unroll);
  * bit 6 = one-block-per-CU grids keep the 4-LDS-tile form (12 tiles per block per launch);
  * bit 7 = the plain burst kernel's round-3 runtime client loop (its last group of 4 re-loads the last client in the
  *         missing slots when the count is not a multiple of 4);
- * bit 8 = plain launches with fewer than 4 row reads keep the burst form. */
+ * bit 8 = plain launches with fewer than 3 row reads keep the burst form;
+ * bits 9-11 = A/B only: the fused burst kernel's client loop in shape 1-4 (fedavg_epi.h launch_epi_loop_ab; built for
+ *         torch-mode FIN_DIV Adam with the AMD-host sqrt and no chained partial sum, ignored elsewhere). */
 int fedavg_set_variant(fedavg_ctx* ctx, int variant);
 /* Tile width used by fedavg_accumulate for contiguous rows (default 4096 elements). */
 int fedavg_set_tile(fedavg_ctx* ctx, int tile_elems);

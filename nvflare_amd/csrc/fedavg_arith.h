@@ -109,6 +109,9 @@ __device__ __forceinline__ FinConst fin_const(const float v) {
 }
 
 __device__ __forceinline__ float div_const(const float a, const FinConst& f) {
+#if defined(FEDAVG_AB_IEEE_DIV)  // A/B builds only (tools/build_rev_lib.py -D): the IEEE division everywhere
+    return a / f.v;
+#endif
     const float q = a * f.r;
     const float e = __builtin_fmaf(-q, f.v, a);
     float res = __builtin_fmaf(e, f.r, q);
@@ -130,14 +133,15 @@ __device__ __forceinline__ f32x4 fin4c(const f32x4 a, const FinConst& f) {
 // 0), then step(client k) for every later client, UNROLL clients' loads issued before their arithmetic.  Client
 // rows are tiled (row + off is this lane's first column of the tile); acc_in is indexed by global column and
 // masked to [b4, e4).
-// GROUPED: every load group holds UNROLL clients from client 0 on (the first client's operation applied in
+// GROUPED (1 or 2): every load group holds UNROLL clients from client 0 on (the first client's operation applied in
 // the first group), so a tile takes ceil(K / UNROLL) load round trips instead of 1 + (K-1) / UNROLL + the
-// remainder.  A partial last group loads only its real clients (wave-uniform branches; round 3 re-loaded the last
-// client in the missing slots, branch-free: at 5 or 6 clients a third of a tile's loads were such repeats).
-template <int OP, bool ACC_IN, int UNROLL, int CPL, bool GROUPED = false>
+// remainder.  GROUPED = 1: a partial last group loads only its real clients (wave-uniform branches per slot);
+// GROUPED = 2 (round 3): the missing slots re-load the last client, branch-free (at 5 or 6 clients a third of a
+// tile's loads are such repeats).
+template <int OP, bool ACC_IN, int UNROLL, int CPL, int GROUPED = 0>
 __device__ __forceinline__ void tile_sum(f32x4 (&acc)[CPL], const RowTableF32& tab, const int K, const int64_t off,
                                          const int64_t col, const f32x4* acc_in, const int64_t b4, const int64_t e4) {
-    if constexpr (GROUPED) {
+    if constexpr (GROUPED != 0) {
         if constexpr (ACC_IN) {
 #pragma unroll
             for (int c = 0; c < CPL; ++c) {
@@ -149,7 +153,11 @@ __device__ __forceinline__ void tile_sum(f32x4 (&acc)[CPL], const RowTableF32& t
             f32x4 v[UNROLL][CPL];
 #pragma unroll
             for (int j = 0; j < UNROLL; ++j) {
-                if (j == 0 || k + j < K) {  // uniform: only a partial last group skips slots
+                if constexpr (GROUPED == 2) {
+                    const f32x4* r = tab.rows[k + j < K ? k + j : K - 1] + off;
+#pragma unroll
+                    for (int c = 0; c < CPL; ++c) v[j][c] = __builtin_nontemporal_load(r + c * kBlock);
+                } else if (j == 0 || k + j < K) {  // uniform: only a partial last group skips slots
                     const f32x4* r = tab.rows[k + j] + off;
 #pragma unroll
                     for (int c = 0; c < CPL; ++c) v[j][c] = __builtin_nontemporal_load(r + c * kBlock);
@@ -201,6 +209,113 @@ __device__ __forceinline__ void tile_sum(f32x4 (&acc)[CPL], const RowTableF32& t
         const f32x4* r = tab.rows[k] + off;
 #pragma unroll
         for (int c = 0; c < CPL; ++c) acc[c] = step4<OP>(acc[c], __builtin_nontemporal_load(r + c * kBlock), tab.w[k]);
+    }
+}
+
+// a chained partial sum's column i, or zero outside [b4, e4): the load is unconditional (an in-range clamped address),
+// so it adds no control flow to the tile loop
+__device__ __forceinline__ f32x4 load_acc_in(const f32x4* acc_in, const int64_t i, const int64_t b4, const int64_t e4) {
+    const int64_t j = i < b4 ? b4 : (i >= e4 ? e4 - 1 : i);
+    const f32x4 v = __builtin_nontemporal_load(acc_in + j);
+    return (i >= b4 && i < e4) ? v : f32x4{0, 0, 0, 0};
+}
+
+// client k's operation on this lane's columns: first4 for client 0 unless ACC_IN, step4 otherwise
+template <int OP, bool ACC_IN, int CPL>
+__device__ __forceinline__ void client_apply(f32x4 (&acc)[CPL], const RowTableF32& tab, const int k, const f32x4 (&v)[CPL]) {
+    const float w = tab.w[k];
+    if (!ACC_IN && k == 0) {
+#pragma unroll
+        for (int c = 0; c < CPL; ++c) acc[c] = first4<OP>(v[c], w);
+    } else {
+#pragma unroll
+        for (int c = 0; c < CPL; ++c) acc[c] = step4<OP>(acc[c], v[c], w);
+    }
+}
+
+// N clients from client k on: the N rows' loads issued together, then their arithmetic in arrival order (client 0's
+// operation is first4 unless ACC_IN)
+template <int OP, bool ACC_IN, int N, int CPL>
+__device__ __forceinline__ void client_group(f32x4 (&acc)[CPL], const RowTableF32& tab, const int k, const int64_t off) {
+    f32x4 v[N][CPL];
+#pragma unroll
+    for (int j = 0; j < N; ++j)
+#pragma unroll
+        for (int c = 0; c < CPL; ++c) v[j][c] = __builtin_nontemporal_load(tab.rows[k + j] + off + c * kBlock);
+#pragma unroll
+    for (int j = 0; j < N; ++j) client_apply<OP, ACC_IN>(acc, tab, k + j, v[j]);
+}
+
+// Shapes of the fused kernels' four-client group (A/B only: launch variant bits 9-11, fedavg_epi.h): 0 -- the four
+// clients' loads together (client_group<4>, the default); 2 -- two pairs, the second pair's loads issued after the
+// first pair's arithmetic; 3 -- clients 0, 2 and 3 of the group, then client 1 after client 0's arithmetic (the order
+// round 3's GROUPED loop compiled to); 4 -- one client at a time.  fence(): a value the next loads must wait for.
+template <int CPL>
+__device__ __forceinline__ void fence_on(const f32x4 (&acc)[CPL]) {
+#pragma unroll
+    for (int c = 0; c < CPL; ++c) asm volatile("" ::"v"(acc[c]) : "memory");  // every column: no arithmetic deferred past it
+}
+
+template <int OP, bool ACC_IN, int SHAPE, int CPL>
+__device__ __forceinline__ void client_group4(f32x4 (&acc)[CPL], const RowTableF32& tab, const int k, const int64_t off) {
+    if constexpr (SHAPE == 2) {
+        client_group<OP, ACC_IN, 2, CPL>(acc, tab, k, off);
+        fence_on(acc);
+        client_group<OP, ACC_IN, 2, CPL>(acc, tab, k + 2, off);
+    } else if constexpr (SHAPE == 3) {
+        f32x4 v0[CPL], v1[CPL], v2[CPL], v3[CPL];
+#pragma unroll
+        for (int c = 0; c < CPL; ++c) {
+            v0[c] = __builtin_nontemporal_load(tab.rows[k] + off + c * kBlock);
+            v2[c] = __builtin_nontemporal_load(tab.rows[k + 2] + off + c * kBlock);
+            v3[c] = __builtin_nontemporal_load(tab.rows[k + 3] + off + c * kBlock);
+        }
+        client_apply<OP, ACC_IN>(acc, tab, k, v0);
+        fence_on(acc);
+#pragma unroll
+        for (int c = 0; c < CPL; ++c) v1[c] = __builtin_nontemporal_load(tab.rows[k + 1] + off + c * kBlock);
+        client_apply<OP, ACC_IN>(acc, tab, k + 1, v1);
+        client_apply<OP, ACC_IN>(acc, tab, k + 2, v2);
+        client_apply<OP, ACC_IN>(acc, tab, k + 3, v3);
+    } else if constexpr (SHAPE == 4) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            client_group<OP, ACC_IN, 1, CPL>(acc, tab, k + j, off);
+            if (j < 3) fence_on(acc);
+        }
+    } else {
+        client_group<OP, ACC_IN, 4, CPL>(acc, tab, k, off);
+    }
+}
+
+// The fused kernels' tile sum (round 4): groups of 4 clients in a loop with unconditional loads, then the K mod 4
+// remainder as one group of exactly that many clients, chosen by a wave-uniform branch per tile -- no repeated loads
+// for any K, in one instantiation (the plain kernels build the client count or its remainder into the kernel
+// instead: fedavg_tiles.h tile_sum_kc / tile_sum_rem).  SHAPE -1 (default): the groups' loads as two pairs from two
+// full groups on, four together below (fedavg_tiles.h tile_sum_rem has the measurements); SHAPE >= 0 forces
+// client_group4's shape (A/B).
+template <int OP, bool ACC_IN, int CPL, int SHAPE = -1>
+__device__ __forceinline__ void tile_sum_rrem(f32x4 (&acc)[CPL], const RowTableF32& tab, const int K, const int64_t off,
+                                              const int64_t col, const f32x4* acc_in, const int64_t b4, const int64_t e4) {
+    if constexpr (ACC_IN) {
+#pragma unroll
+        for (int c = 0; c < CPL; ++c) acc[c] = load_acc_in(acc_in, col + c * kBlock, b4, e4);
+    }
+    const int rem = K & 3;
+    const int k_full = K - rem;
+    if constexpr (SHAPE >= 0) {
+        for (int k = 0; k < k_full; k += 4) client_group4<OP, ACC_IN, SHAPE, CPL>(acc, tab, k, off);
+    } else if (k_full >= 8) {  // uniform
+        for (int k = 0; k < k_full; k += 4) client_group4<OP, ACC_IN, 2, CPL>(acc, tab, k, off);
+    } else {
+        for (int k = 0; k < k_full; k += 4) client_group4<OP, ACC_IN, 0, CPL>(acc, tab, k, off);
+    }
+    if (rem == 3) {
+        client_group<OP, ACC_IN, 3, CPL>(acc, tab, k_full, off);
+    } else if (rem == 2) {
+        client_group<OP, ACC_IN, 2, CPL>(acc, tab, k_full, off);
+    } else if (rem == 1) {
+        client_group<OP, ACC_IN, 1, CPL>(acc, tab, k_full, off);
     }
 }
 

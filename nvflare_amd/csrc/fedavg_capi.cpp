@@ -1335,7 +1335,7 @@ int fedavg_accumulate_tiled_epi(fedavg_ctx* ctx, const void* const* bases, const
         L.fin = fin;
         L.unroll = fedavg::kDefaultUnroll;
         L.variant = ctx->variant & (fedavg::kVariantEpiPrefetch | fedavg::kVariantTileStores | fedavg::kVariantAnyOrder |
-                                    fedavg::kVariantRegisterTiles);
+                                    fedavg::kVariantRegisterTiles | (7 << fedavg::kVariantLoopShift));
         L.tile4 = (int64_t)tile_elems / 4;
         L.tstride4 = (int64_t)tile_stride / 4;
         L.b4 = (int64_t)begin / 4;
@@ -1417,7 +1417,7 @@ int fedavg_set_launch(fedavg_ctx* ctx, int blocks_per_cu, int unroll) {
 int fedavg_set_variant(fedavg_ctx* ctx, int variant) {
     return guarded([&] {
         if (!ctx) throw Error("ctx is NULL");
-        if (variant < 0 || variant > 511) throw Error("variant must be 0..511");
+        if (variant < 0 || variant > 4095) throw Error("variant must be 0..4095");
         ctx->variant = variant;
     });
 }

@@ -278,7 +278,14 @@ __device__ __forceinline__ void epilogue4(const EpiParams& E, const EpiConsts& C
 // at the end of the launch -- the client-read phase carries no writes, and every block's epilogue phase
 // falls at about the same time.  `out` (when given) also receives d, as in the per-tile kernel.  TPB_LDS > 0:
 // that many more tiles per block, their d held in LDS (each lane reads back only what it wrote).
-template <int OP, int FIN, bool ACC_IN, int EPI, int TPB, int TPB_LDS = 0>
+// LOOP: 0 -- the default, tile_sum_rrem (four-client groups as two pairs from 8 clients on, client_group4 shape 2;
+// four together below); A/B only (launch variant bits 9-11): 1 -- tile_sum's GROUPED loop with round 3's repeats;
+// 2-4 -- tile_sum_rrem with client_group4 shape LOOP; 5 -- shape 0 (four clients' loads together) everywhere.  Fused Adam, % of 8 TB/s, shapes 0 / 1 / 2 /
+// 3 / 4 in one process (profiles/r04/s6/loop_k*.jsonl): 64 clients 83.2 / 85.6 / 85.4 / 83.8 / 80.4, 32: 80.1 / 82.3 /
+// 81.3 / 80.5 / 78.3, 8: 73.5 / 76.6 / 76.4 / 75.9 / 74.0, 10: 75.7 / 75.5 / 75.0 / 75.6 / 76.8, 6: 74.2 / 70.4 /
+// 73.6 / 73.7 / 75.7 -- fewer loads in flight per wave stream better once a tile holds two groups or more; the pairs
+// are within about a point of the best everywhere and re-load nothing.
+template <int OP, int FIN, bool ACC_IN, int EPI, int TPB, int TPB_LDS = 0, int LOOP = 0>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, 1)))
 fedavg_tiles_epi_burst_f32x4(const RowTableF32 tab, const int K, const int64_t tstride4, const f32x4* acc_in,
                              f32x4* out, const int64_t b4, const int64_t e4, const float fin_val, const EpiParams E,
@@ -293,13 +300,20 @@ fedavg_tiles_epi_burst_f32x4(const RowTableF32 tab, const int K, const int64_t t
     const EpiConsts C = epi_consts<EPI>(E);
     if constexpr ((EPI & kEpiTorchSqrt) != 0) rsqrt14_stage();
     if constexpr ((EPI & kEpiTorchSqrtAmd) != 0) rsqrtps_stage(E.rsqrtps);
+    auto sum = [&](f32x4 (&acc)[CPL], const int64_t t) __attribute__((always_inline)) {
+        if constexpr (LOOP == 1)
+            tile_sum<OP, ACC_IN, UNROLL, CPL, 2>(acc, tab, K, t * tstride4 + threadIdx.x, t * T4 + threadIdx.x, acc_in,
+                                                 b4, e4);
+        else
+            tile_sum_rrem<OP, ACC_IN, CPL, LOOP == 0 ? -1 : LOOP == 5 ? 0 : LOOP>(
+                acc, tab, K, t * tstride4 + threadIdx.x, t * T4 + threadIdx.x, acc_in, b4, e4);
+    };
 #pragma unroll
     for (int m = 0; m < TPB; ++m) {
         const int64_t t = t0 + blockIdx.x + (int64_t)m * gridDim.x;
         if (t < t_end) {
             f32x4 acc[CPL];
-            tile_sum<OP, ACC_IN, UNROLL, CPL, true>(acc, tab, K, t * tstride4 + threadIdx.x, t * T4 + threadIdx.x, acc_in,
-                                                    b4, e4);
+            sum(acc, t);
 #pragma unroll
             for (int c = 0; c < CPL; ++c) dd[m][c] = fin4c<FIN>(acc[c], fc);
         }
@@ -309,8 +323,7 @@ fedavg_tiles_epi_burst_f32x4(const RowTableF32 tab, const int K, const int64_t t
         const int64_t t = t0 + blockIdx.x + (int64_t)m * gridDim.x;
         if (t < t_end) {
             f32x4 acc[CPL];
-            tile_sum<OP, ACC_IN, UNROLL, CPL, true>(acc, tab, K, t * tstride4 + threadIdx.x, t * T4 + threadIdx.x, acc_in,
-                                                    b4, e4);
+            sum(acc, t);
 #pragma unroll
             for (int c = 0; c < CPL; ++c) staged[((m - TPB) * CPL + c) * kBlock + threadIdx.x] = fin4c<FIN>(acc[c], fc);
         }
@@ -471,12 +484,48 @@ __global__ void __launch_bounds__(kBlock) fedavg_tiles_epi_f32x4(const RowTableF
     }
 }
 
+// A/B of the burst kernel's client loop (launch variant bits 9-11 = LOOP 1-4), instantiated for one configuration only:
+// torch-mode FIN_DIV Adam with the AMD-host sqrt, no chained partial sum (bench.py --epilogue adam on the pool's boxes)
+template <int OP, int FIN, bool ACC_IN, int EPI, int TPB_LDS, int LOOP>
+inline hipError_t launch_epi_loop_ab(const TileLaunch& L, const EpiParams& E, hipStream_t s, uint64_t* nl) {
+    const f32x4* ai = reinterpret_cast<const f32x4*>(L.acc_in);
+    f32x4* o = reinterpret_cast<f32x4*>(L.out);
+    return burst_launches(L.b4 / L.tile4, (L.e4 - 1) / L.tile4 + 1, L.grid, kBurstTiles + TPB_LDS, nl,
+                          L.variant & kVariantAnyOrder, [&](int nb, int64_t t0, int64_t t_end, uint32_t flags) {
+                              hipExtLaunchKernelGGL(
+                                  (fedavg_tiles_epi_burst_f32x4<OP, FIN, ACC_IN, EPI, kBurstTiles, TPB_LDS, LOOP>),
+                                  dim3(nb), dim3(kBlock), 0, s, nullptr, nullptr, flags, L.tab, L.k, L.tstride4, ai, o,
+                                  L.b4, L.e4, L.fin_val, E, t0, t_end);
+                          });
+}
+
+template <int OP, int FIN, bool ACC_IN, int EPI, int TPB_LDS>
+inline bool epi_loop_ab(const TileLaunch& L, const EpiParams& E, hipStream_t s, uint64_t* nl, hipError_t* err) {
+    if constexpr (OP == FEDAVG_OP_TORCH && FIN == FEDAVG_FIN_DIV && !ACC_IN && EPI == (FEDAVG_EPI_ADAM | kEpiTorchSqrtAmd)) {
+        switch ((L.variant >> kVariantLoopShift) & 7) {
+            case 1: *err = launch_epi_loop_ab<OP, FIN, ACC_IN, EPI, TPB_LDS, 1>(L, E, s, nl); return true;
+            case 2: *err = launch_epi_loop_ab<OP, FIN, ACC_IN, EPI, TPB_LDS, 2>(L, E, s, nl); return true;
+            case 3: *err = launch_epi_loop_ab<OP, FIN, ACC_IN, EPI, TPB_LDS, 3>(L, E, s, nl); return true;
+            case 4: *err = launch_epi_loop_ab<OP, FIN, ACC_IN, EPI, TPB_LDS, 4>(L, E, s, nl); return true;
+            case 5: *err = launch_epi_loop_ab<OP, FIN, ACC_IN, EPI, TPB_LDS, 5>(L, E, s, nl); return true;
+            default: return false;
+        }
+    }
+    return false;
+}
+
 // one kernel instantiation per optimizer kind: K(EPI) launches the per-tile (PRE) or the burst form
 template <int OP, int FIN, bool ACC_IN, int EPI>
 inline hipError_t launch_epi_k(const TileLaunch& L, const EpiParams& E, hipStream_t s, uint64_t* nl) {
     const f32x4* ai = reinterpret_cast<const f32x4*>(L.acc_in);
     f32x4* o = reinterpret_cast<f32x4*>(L.out);
     if (!(L.variant & (kVariantTileStores | kVariantEpiPrefetch))) {  // burst: one launch per grid x TPB tiles
+        hipError_t ab_err = hipSuccess;
+        if ((L.variant & kVariantWideLds) && epi_loop_ab<OP, FIN, ACC_IN, EPI, kBurstEpiLdsTilesWide>(L, E, s, nl, &ab_err))
+            return ab_err;
+        if (!(L.variant & (kVariantWideLds | kVariantRegisterTiles)) &&
+            epi_loop_ab<OP, FIN, ACC_IN, EPI, kBurstLdsTiles>(L, E, s, nl, &ab_err))
+            return ab_err;
         if (L.variant & kVariantWideLds)  // one block per CU: 9 more tiles with d in LDS (144 KiB)
             return burst_launches(L.b4 / L.tile4, (L.e4 - 1) / L.tile4 + 1, L.grid, kBurstTiles + kBurstEpiLdsTilesWide,
                                   nl, L.variant & kVariantAnyOrder, [&](int nb, int64_t t0, int64_t t_end, uint32_t flags) {

@@ -35,6 +35,8 @@ constexpr int kVariantWideLds = 64;       // inside TileLaunch: plain burst kern
                                            // (160 KiB, one block per CU); run_tiles sets it for one-block-per-CU grids
                                            // unless the public variant has bit 6, which keeps the 4-tile form there
                                            // (32 clients 88.4 -> 88.9 %, 64: 89.7 -> 89.9 %, profiles/r02/ab/wide_lds/)
+constexpr int kVariantLoopShift = 9;       // bits 9-11: A/B shapes of the burst kernels' client loop
+                                           // (fedavg_epi.h launch_epi_loop_ab, fedavg_tiles.h launch_burst)
 // epilogue template value: the optimizer kind | kEpiTorchSqrt when the step's sqrt is torch CPU's restated AVX-512
 // vsSqrt (EpiParams.torch_sqrt == FEDAVG_SQRT_TORCH_AVX512; fedavg_arith.h sqrt_torch_cpu) | kEpiTorchSqrtAmd for the
 // AMD hosts' path (FEDAVG_SQRT_TORCH_AMD; sqrt_mkl_rsqrtps) -- a compile-time choice, so the correctly rounded path

@@ -110,8 +110,14 @@ __device__ __forceinline__ void tile_sum_kc(f32x4 (&acc)[CPL], const RowTableF32
 
 // The runtime-K form with the remainder REM = K mod 4 built in: full groups of 4 clients in a loop, then one group of
 // exactly REM clients -- no repeated loads for any K (fedavg_arith.h tile_sum's GROUPED form re-loads the last client
-// 4 - K mod 4 times per tile).
-template <int OP, bool ACC_IN, int REM, int CPL>
+// 4 - K mod 4 times per tile).  SHAPE: how a full group's loads are issued (fedavg_arith.h client_group4).  -1, the
+// default: from two full groups on (8+ clients) as two pairs, the second pair's loads after the first pair's
+// arithmetic; a single group, four together (pairs cost fused Adam 3 points at 5 clients, profiles/r04/s7/).
+// 0: always four together (round 4 until session 7); 2-4: the other shapes (A/B, launch variant bits 9-11).  Plain
+// burst, % of 8 TB/s, four together / round 3's GROUPED loop / pairs, one process each (profiles/r04/s7/plain_k*):
+// 64 clients 87.8 / 90.3 / 90.0, 32: 86.9 / 89.0 / 88.2, 16: 80.7 / 84.9 / 84.9, 8: 77.0 / 79.9 / 83.9 -- fewer
+// loads in flight per wave (one wave per SIMD) stream better.
+template <int OP, bool ACC_IN, int REM, int CPL, int SHAPE = -1>
 __device__ __forceinline__ void tile_sum_rem(f32x4 (&acc)[CPL], const RowTableF32& tab, const int K, const int64_t off,
                                              const int64_t col, const f32x4* acc_in, const int64_t b4, const int64_t e4) {
     if constexpr (ACC_IN) {
@@ -122,6 +128,11 @@ __device__ __forceinline__ void tile_sum_rem(f32x4 (&acc)[CPL], const RowTableF3
         }
     }
     const int k_full = K - REM;
+    if constexpr (SHAPE > 0) {
+        for (int k = 0; k < k_full; k += 4) client_group4<OP, ACC_IN, SHAPE, CPL>(acc, tab, k, off);
+    } else if (SHAPE < 0 && k_full >= 8) {  // the default from two full groups on: pairs (uniform branch)
+        for (int k = 0; k < k_full; k += 4) client_group4<OP, ACC_IN, 2, CPL>(acc, tab, k, off);
+    } else {
     for (int k = 0; k < k_full; k += 4) {
         f32x4 v[4][CPL];
 #pragma unroll
@@ -139,6 +150,7 @@ __device__ __forceinline__ void tile_sum_rem(f32x4 (&acc)[CPL], const RowTableF3
                 for (int c = 0; c < CPL; ++c) acc[c] = step4<OP>(acc[c], v[j][c], w);
             }
         }
+    }
     }
     if constexpr (REM > 0) {
         f32x4 v[REM][CPL];
@@ -162,13 +174,17 @@ __device__ __forceinline__ void tile_sum_rem(f32x4 (&acc)[CPL], const RowTableF3
 
 // one tile's sum: KC > 0 -- the client count built in (tile_sum_kc); KC = -1 - REM -- the runtime count with its
 // remainder mod 4 built in (tile_sum_rem); KC = 0 -- fedavg_arith.h tile_sum's GROUPED form (variant bit 7, for A/Bs)
-template <int OP, bool ACC_IN, int UNROLL, int CPL, int KC>
+// SHAPE (remainder forms): -1 -- tile_sum_rem's default; A/B only (launch variant bits 9-11): 1 -- tile_sum's GROUPED
+// loop with round 3's repeats; 0, 2-4 -- tile_sum_rem with that shape
+template <int OP, bool ACC_IN, int UNROLL, int CPL, int KC, int SHAPE = -1>
 __device__ __forceinline__ void tile_sum_any(f32x4 (&acc)[CPL], const RowTableF32& tab, const int K, const int64_t off,
                                              const int64_t col, const f32x4* acc_in, const int64_t b4, const int64_t e4) {
     if constexpr (KC > 0) {
         tile_sum_kc<OP, ACC_IN, KC, CPL>(acc, tab, off, col, acc_in, b4, e4);
+    } else if constexpr (KC < 0 && SHAPE == 1) {
+        tile_sum<OP, ACC_IN, UNROLL, CPL, 2>(acc, tab, K, off, col, acc_in, b4, e4);
     } else if constexpr (KC < 0) {
-        tile_sum_rem<OP, ACC_IN, -1 - KC, CPL>(acc, tab, K, off, col, acc_in, b4, e4);
+        tile_sum_rem<OP, ACC_IN, -1 - KC, CPL, SHAPE>(acc, tab, K, off, col, acc_in, b4, e4);
     } else {
         tile_sum<OP, ACC_IN, UNROLL, CPL, true>(acc, tab, K, off, col, acc_in, b4, e4);
     }
@@ -188,7 +204,7 @@ __device__ __forceinline__ void tile_sum_any(f32x4 (&acc)[CPL], const RowTableF3
 // ---------------------------------------------------------------------------------------------
 // TPB_LDS > 0 (the default; launch variant bit 5 turns it off): TPB_LDS more tiles per block whose results wait in LDS (each lane
 // reads back only what it wrote, so no barrier), making each launch (TPB + TPB_LDS) / TPB times longer.
-template <int OP, int FIN, bool ACC_IN, int UNROLL, int CPL, int TPB, int TPB_LDS = 0, int KC = 0>
+template <int OP, int FIN, bool ACC_IN, int UNROLL, int CPL, int TPB, int TPB_LDS = 0, int KC = 0, int SHAPE = -1>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, 1)))
 fedavg_tiles_burst_f32x4(const RowTableF32 tab, const int K, const int64_t tstride4, const f32x4* acc_in, f32x4* out,
                          const int64_t b4, const int64_t e4, const float fin_val, const int64_t t0, const int64_t t_end) {
@@ -201,7 +217,7 @@ fedavg_tiles_burst_f32x4(const RowTableF32 tab, const int K, const int64_t tstri
         const int64_t t = t0 + blockIdx.x + (int64_t)m * gridDim.x;
         if (t < t_end) {
             f32x4 acc[CPL];
-            tile_sum_any<OP, ACC_IN, UNROLL, CPL, KC>(acc, tab, K, t * tstride4 + threadIdx.x, t * T4 + threadIdx.x,
+            tile_sum_any<OP, ACC_IN, UNROLL, CPL, KC, SHAPE>(acc, tab, K, t * tstride4 + threadIdx.x, t * T4 + threadIdx.x,
                                                       acc_in, b4, e4);
 #pragma unroll
             for (int c = 0; c < CPL; ++c) res[m][c] = fin4c<FIN>(acc[c], fc);
@@ -213,7 +229,7 @@ fedavg_tiles_burst_f32x4(const RowTableF32 tab, const int K, const int64_t tstri
         const int64_t t = t0 + blockIdx.x + (int64_t)m * gridDim.x;
         if (t < t_end) {
             f32x4 acc[CPL];
-            tile_sum_any<OP, ACC_IN, UNROLL, CPL, KC>(acc, tab, K, t * tstride4 + threadIdx.x, t * T4 + threadIdx.x,
+            tile_sum_any<OP, ACC_IN, UNROLL, CPL, KC, SHAPE>(acc, tab, K, t * tstride4 + threadIdx.x, t * T4 + threadIdx.x,
                                                       acc_in, b4, e4);
 #pragma unroll
             for (int c = 0; c < CPL; ++c) staged[((m - TPB) * CPL + c) * kBlock + threadIdx.x] = fin4c<FIN>(acc[c], fc);
@@ -248,14 +264,14 @@ fedavg_tiles_burst_f32x4(const RowTableF32 tab, const int K, const int64_t tstri
 // launchers
 // ---------------------------------------------------------------------------------------------
 // one launch per grid x (TPB + TPB_LDS) tiles (fedavg_tiles_burst_f32x4)
-template <int OP, int FIN, bool ACC_IN, int UNROLL, int CPL, int TPB, int TPB_LDS, int KC>
+template <int OP, int FIN, bool ACC_IN, int UNROLL, int CPL, int TPB, int TPB_LDS, int KC, int SHAPE = -1>
 inline hipError_t launch_burst_kc(const TileLaunch& L, hipStream_t s, uint64_t* nl) {
     const f32x4* ai = reinterpret_cast<const f32x4*>(L.acc_in);
     f32x4* o = reinterpret_cast<f32x4*>(L.out);
     return burst_launches(L.b4 / L.tile4, (L.e4 - 1) / L.tile4 + 1, L.grid, TPB + TPB_LDS, nl,
                           L.variant & kVariantAnyOrder, [&](int nb, int64_t t0, int64_t t_end, uint32_t flags) {
                               hipExtLaunchKernelGGL(
-                                  (fedavg_tiles_burst_f32x4<OP, FIN, ACC_IN, UNROLL, CPL, TPB, TPB_LDS, KC>), dim3(nb),
+                                  (fedavg_tiles_burst_f32x4<OP, FIN, ACC_IN, UNROLL, CPL, TPB, TPB_LDS, KC, SHAPE>), dim3(nb),
                                   dim3(kBlock), 0, s, nullptr, nullptr, flags, L.tab, L.k, L.tstride4, ai, o, L.b4, L.e4,
                                   L.fin_val, t0, t_end);
                           });
@@ -268,6 +284,18 @@ inline hipError_t launch_burst_kc(const TileLaunch& L, hipStream_t s, uint64_t* 
 template <int OP, int FIN, bool ACC_IN, int UNROLL, int CPL, int TPB, int TPB_LDS = 0>
 inline hipError_t launch_burst(const TileLaunch& L, hipStream_t s, uint64_t* nl) {
     if constexpr (CPL == 4 && UNROLL == 4) {
+        if constexpr (OP == FEDAVG_OP_TORCH && FIN == FEDAVG_FIN_DIV && !ACC_IN) {  // A/B: client-loop shapes, K % 4 == 0
+            if (L.k >= 8 && L.k % 4 == 0) {
+                switch ((L.variant >> kVariantLoopShift) & 7) {
+                    case 1: return launch_burst_kc<OP, FIN, ACC_IN, UNROLL, CPL, TPB, TPB_LDS, -1, 1>(L, s, nl);
+                    case 2: return launch_burst_kc<OP, FIN, ACC_IN, UNROLL, CPL, TPB, TPB_LDS, -1, 2>(L, s, nl);
+                    case 3: return launch_burst_kc<OP, FIN, ACC_IN, UNROLL, CPL, TPB, TPB_LDS, -1, 3>(L, s, nl);
+                    case 4: return launch_burst_kc<OP, FIN, ACC_IN, UNROLL, CPL, TPB, TPB_LDS, -1, 4>(L, s, nl);
+                    case 5: return launch_burst_kc<OP, FIN, ACC_IN, UNROLL, CPL, TPB, TPB_LDS, -1, 0>(L, s, nl);
+                    default: break;
+                }
+            }
+        }
         if (!(L.variant & kVariantRuntimeK)) {
             switch (L.k) {
 #define FEDAVG_KC(N) \

@@ -253,6 +253,34 @@ def test_epilogue_variants_multi_tile_per_block(ctx, oracle, variant, K, kind):
         dev.close()
 
 
+@pytest.mark.parametrize("K", [4, 5, 6, 7, 8, 9, 10, 11, 131, 133, 134])
+def test_adam_burst_remainders(ctx, oracle, K):
+    """The fused burst kernel's client loop (fedavg_arith.h tile_sum_rrem, round 4): groups of four, then the K mod 4
+    remainder as one group chosen per tile; every remainder, one and two full groups before it, and chained launches
+    (131 / 133 / 134: 128 clients, then 3 / 5 / 6 more on top of the partial sum, ACC_IN); more tiles than one launch
+    covers (several launches, a short last one; the chained cases at one launch, 3.3 GB of rows), a ragged end; p, m
+    and v bit for bit against the oracle."""
+    n = (7000 if K <= 128 else 1500) * TILE + 12345
+    cols = np.arange(n, dtype=np.uint64)
+    rows = [oracle.synth_values(9, k, cols) for k in range(K)]
+    ws = oracle.synth_weights(K)
+    rng = np.random.default_rng(K)
+    p = rng.standard_normal(n).astype(np.float32)
+    m = (rng.standard_normal(n) * 0.1).astype(np.float32)
+    v = (rng.random(n) * 0.01).astype(np.float32)
+    hp = dict(lr=1e-3, beta1=0.9, beta2=0.999, eps=1e-8, step=2.0)
+    dev = _Dev(ctx, rows, n)
+    try:
+        e = _epi(3, param=dev.buf("p", p), state1=dev.buf("m", m), state2=dev.buf("v", v), **hp)
+        out = dev.buf("d") if K > 128 else None
+        ctx.accumulate_tiled_epi(dev.bases, ws, TILE, dev.lay.tile_stride, 0, dev.n4, out, 1, 2, _sum(ws), e)
+        d = oracle.fedavg_c(rows, ws, oracle.MODE_TORCH, nthreads=8)
+        oracle.epilogue_apply(d, oracle.EPI_ADAM, p=p, m=m, v=v, **hp)
+        assert same_bits(dev.get("p"), p) and same_bits(dev.get("m"), m) and same_bits(dev.get("v"), v)
+    finally:
+        dev.close()
+
+
 @pytest.mark.parametrize("K,decoupled", [(7, 0), (3, 1), (0, 0)])
 def test_adam_amsgrad_epilogue(ctx, oracle, K, decoupled):
     """Adam / AdamW with amsgrad: max_exp_avg_sq (state3) = torch.maximum(max_exp_avg_sq, exp_avg_sq) and the

@@ -31,7 +31,10 @@ def main():
     ap.add_argument("--mode", choices=["torch", "numpy"], default="torch",
                     help="torch: fma steps, IEEE division at the end; numpy: mul + add, multiply by 1/count")
     ap.add_argument("--check", action="store_true",
-                    help="plain epilogue: every config's output must equal the first config's bit for bit")
+                    help="every config's output (the fused epilogues: p and the last state, from zeroed state) must "
+                         "equal the first config's bit for bit")
+    ap.add_argument("--sqrt", choices=["ieee", "torch_cpu", "torch_cpu_amd"], default="ieee",
+                    help="the fused epilogues' sqrt (EpiParams.torch_sqrt)")
     a = ap.parse_args()
     from nvflare_amd import _native as N
     from nvflare_amd.device import DeviceContext, TiledLayout
@@ -68,6 +71,8 @@ def main():
         e = N.Epilogue()
         e.kind = kinds[epi]
         e.lr, e.momentum, e.beta1, e.beta2, e.eps, e.step = 1e-3, 0.9, 0.9, 0.999, 1e-8, 1.0
+        e.torch_sqrt = {"ieee": N.FEDAVG_SQRT_IEEE, "torch_cpu": N.FEDAVG_SQRT_TORCH_AVX512,
+                        "torch_cpu_amd": N.FEDAVG_SQRT_TORCH_AMD}[a.sqrt]
         if epi == "add_base":
             e.base, o = bufs[0].ptr, out.ptr
         else:
@@ -78,23 +83,30 @@ def main():
     variants = [tuple(int(x) for x in (v.split(":") + ["0", "0"])[:3]) for v in a.variants.split(",")]
     epis = a.epilogues.split(",")
     res = {}
-    ref_out = None
+    ref_out = {}
     for rnd in range(a.rounds):
         for epi, pad in [(e_, p_) for e_ in epis for p_ in pads]:
             fn = launcher(epi, pad)
             for v in variants:
                 ctx.set_variant(v[0])
                 ctx.set_launch(v[2], v[1])
+                if a.check and epi != "none" and rnd == 0 and pad == pads[0]:
+                    for b in bufs:  # the same state in for every config
+                        ctx.memset(b.ptr, 0, end * 4)
                 fn()
-                if a.check and epi == "none" and rnd == 0 and pad == pads[0]:
+                if a.check and rnd == 0 and pad == pads[0]:
                     host = np.empty(end, dtype=np.float32)
                     ctx.sync()
-                    ctx.d2h(host, out.ptr)
-                    if ref_out is None:
-                        ref_out = host
+                    ctx.d2h(host, out.ptr if epi in ("none", "add_base") else bufs[0].ptr)
+                    if epi not in ("none", "add_base"):
+                        last = np.empty(end, dtype=np.float32)
+                        ctx.d2h(last, bufs[2 if epi == "adam" else 1].ptr)
+                        host = np.concatenate([host, last])
+                    if epi not in ref_out:
+                        ref_out[epi] = host
                     else:
-                        bad = int(np.count_nonzero(host.view(np.uint32) != ref_out.view(np.uint32)))
-                        print(json.dumps({"check": ":".join(map(str, v)), "mismatches": bad}), flush=True)
+                        bad = int(np.count_nonzero(host.view(np.uint32) != ref_out[epi].view(np.uint32)))
+                        print(json.dumps({"check": ":".join(map(str, v)), "epilogue": epi, "mismatches": bad}), flush=True)
                         if bad:
                             raise SystemExit(f"config {v}: {bad} outputs differ from config {variants[0]}")
                     ctx.memset(out.ptr, 0xFF, end * 4)
