@@ -38,6 +38,9 @@ def main():
     ap.add_argument("--rev", default="HEAD")
     ap.add_argument("--out", required=True)
     ap.add_argument("-D", dest="defines", action="append", default=[], help="extra preprocessor definitions")
+    ap.add_argument("--only", default="",
+                    help="with --rev WORKTREE: comma list of sources to compile (with -D); every other unit's object "
+                         "is the in-tree build's (nvflare_amd/lib/obj, same sources), so a one-file A/B links in minutes")
     args = ap.parse_args()
     with tempfile.TemporaryDirectory() as tmp:
         if args.rev == "WORKTREE":  # the working tree's sources as they are
@@ -51,9 +54,16 @@ def main():
         csrc = os.path.join(tmp, "nvflare_amd", "csrc")
         inc = [f"-I{os.path.join(tmp, 'include')}", f"-I{csrc}"]
         units = B.compile_units([s for s in B.SOURCES if os.path.exists(os.path.join(csrc, s))])
+        only = [x for x in args.only.split(",") if x]
+        if only and args.rev != "WORKTREE":
+            raise SystemExit("--only needs --rev WORKTREE (the reused objects are the working tree's)")
+        if only and B.needs_build():
+            raise SystemExit("--only reuses the in-tree objects: build the in-tree library first")
 
         def compile_one(unit):
             src, obj_name, extra = unit
+            if only and src not in only:
+                return os.path.join(B.OBJ_DIR, obj_name)
             obj = os.path.join(tmp, obj_name)
             defs = [f"-D{d}" for d in args.defines]
             subprocess.run([B.HIPCC, *B.FLAGS, *extra, *defs, *inc, "-c", os.path.join(csrc, src), "-o", obj], check=True)
