@@ -7,7 +7,7 @@ mkdir -p "$OUT"
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
 for i in 1 2; do
-  for u in 6 3 4; do
+  for u in 6 3; do
     lib=nvflare_amd/lib/libnvflare_amd_fedavg.so
     [ "$u" != 6 ] && lib=nvflare_amd/lib/ab/libnvflare_amd_fedavg_nu$u.so
     for fmt in bfloat16 float16; do
