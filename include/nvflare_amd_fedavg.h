@@ -327,15 +327,16 @@ int fedavg_launch_count(fedavg_ctx* ctx, uint64_t* n);
  * kernel at >= 32 clients, the fused one at >= 64, the 16-bit one at >= 48 in torch mode, 2 otherwise),
  * clients whose loads are issued together (4 or 8, default 4). */
 int fedavg_set_launch(fedavg_ctx* ctx, int blocks_per_cu, int unroll);
-/* Kernel variants (default 0).  By default a launch with 4 or more row reads (its clients, plus the chained partial
- * sum of a launch after the first 128 clients) runs the BURST form: each block holds its tiles' results (the fused
- * kernel: its differences) in registers and LDS and stores them (runs the epilogue) as chip-wide bursts at the end of
- * a short launch -- per launch 8 register-held tiles per block plus 4 LDS-held ones on two-block-per-CU grids, or 10
- * (fused: 9) on the one-block-per-CU grids of the plain kernel at 32+ clients (fused: 64+); a launch with fewer row
- * reads (1-3: most NVFlare jobs run 2 clients) runs the PER-TILE-STORE form, which stores each tile's results as it
- * finishes; every load and store is nontemporal.  The plain burst kernel has the launch's client count built in for
- * 1-6 clients and the count's remainder mod 4 from 7 on (no repeated loads).  The bits (results are bit-identical in
- * every variant):
+/* Kernel variants (default 0).  By default a launch with 3 or more row reads (plain; fused: 4 or more -- its clients,
+ * plus the chained partial sum of a launch after the first 128 clients) runs the BURST form: each block holds its
+ * tiles' results (the fused kernel: its differences) in registers and LDS and stores them (runs the epilogue) as
+ * chip-wide bursts at the end of a short launch -- per launch 8 register-held tiles per block plus 4 LDS-held ones on
+ * two-block-per-CU grids, or 10 (fused: 9) on the one-block-per-CU grids of the plain kernel at 32+ clients (fused:
+ * 64+); a launch with fewer row reads (most NVFlare jobs run 2 clients) runs the PER-TILE-STORE form, which stores
+ * each tile's results as it finishes (fused, 2-3 reads: its cross-tile pipelined variant, bit 2); every load and store
+ * is nontemporal.  The plain burst kernel has the launch's client count built in for 1-6 clients and the count's
+ * remainder mod 4 from 7 on (no repeated loads); from 8 clients on both burst kernels load each four-client group as
+ * two pairs.  The bits (results are bit-identical in every variant):
  * bit 0 / bit 1 = the per-tile-store plain kernel with temporal client loads / temporal result stores (imply bit 3);
  * bit 2 = the per-tile epilogue kernel software-pipelined across tiles (the next tile's first client loads
  *         overlap the epilogue; implies bit 3 for the epilogue);

@@ -1341,7 +1341,13 @@ int fedavg_accumulate_tiled_epi(fedavg_ctx* ctx, const void* const* bases, const
         L.b4 = (int64_t)begin / 4;
         L.e4 = (int64_t)end / 4;
         const int64_t n_tiles = (L.e4 - 1) / L.tile4 - L.b4 / L.tile4 + 1;
-        if (L.k + (cur_in ? 1 : 0) < kEpiBurstMinClients) L.variant |= fedavg::kVariantTileStores;
+        // under kEpiBurstMinClients row reads the per-tile form; from 2 reads on its cross-tile pipelined variant
+        // (Adam at 2 / 3 clients +1.8 / +1.4 and +0.9 / +1.0 points on two boxes, 1 client -1.5 / +0.1:
+        // profiles/r04/s9/epi_bpc_k*.jsonl, s10/epi_pipe_k*.jsonl), unless the public variant asks for tile stores
+        const int reads = L.k + (cur_in ? 1 : 0);
+        if (reads < kEpiBurstMinClients)
+            L.variant |= reads >= 2 && !(ctx->variant & fedavg::kVariantTileStores) ? fedavg::kVariantEpiPrefetch
+                                                                                    : fedavg::kVariantTileStores;
         const bool burst = !(L.variant & (fedavg::kVariantEpiPrefetch | fedavg::kVariantTileStores));
         const int bpc = burst ? ctx->bpc(L.k >= fedavg::kEpiOneBlockMinK ? 1 : 2) : ctx->bpc();
         // one block per CU: the LDS-held tiles fill the CU (9 instead of 4), unless the public variant has bit 6

@@ -280,7 +280,8 @@ __device__ __forceinline__ void epilogue4(const EpiParams& E, const EpiConsts& C
 // that many more tiles per block, their d held in LDS (each lane reads back only what it wrote).
 // LOOP: 0 -- the default, tile_sum_rrem (four-client groups as two pairs from 8 clients on, client_group4 shape 2;
 // four together below); A/B only (launch variant bits 9-11): 1 -- tile_sum's GROUPED loop with round 3's repeats;
-// 2-4 -- tile_sum_rrem with client_group4 shape LOOP; 5 -- shape 0 (four clients' loads together) everywhere.  Fused Adam, % of 8 TB/s, shapes 0 / 1 / 2 /
+// 2-4 -- tile_sum_rrem with client_group4 shape LOOP; 5 -- shape 0 (four clients' loads together) everywhere;
+// 6 -- the default loop, the epilogue phase without its operand prefetch.  Fused Adam, % of 8 TB/s, shapes 0 / 1 / 2 /
 // 3 / 4 in one process (profiles/r04/s6/loop_k*.jsonl): 64 clients 83.2 / 85.6 / 85.4 / 83.8 / 80.4, 32: 80.1 / 82.3 /
 // 81.3 / 80.5 / 78.3, 8: 73.5 / 76.6 / 76.4 / 75.9 / 74.0, 10: 75.7 / 75.5 / 75.0 / 75.6 / 76.8, 6: 74.2 / 70.4 /
 // 73.6 / 73.7 / 75.7 -- fewer loads in flight per wave stream better once a tile holds two groups or more; the pairs
@@ -305,7 +306,7 @@ fedavg_tiles_epi_burst_f32x4(const RowTableF32 tab, const int K, const int64_t t
             tile_sum<OP, ACC_IN, UNROLL, CPL, 2>(acc, tab, K, t * tstride4 + threadIdx.x, t * T4 + threadIdx.x, acc_in,
                                                  b4, e4);
         else
-            tile_sum_rrem<OP, ACC_IN, CPL, LOOP == 0 ? -1 : LOOP == 5 ? 0 : LOOP>(
+            tile_sum_rrem<OP, ACC_IN, CPL, LOOP == 0 || LOOP == 6 ? -1 : LOOP == 5 ? 0 : LOOP>(
                 acc, tab, K, t * tstride4 + threadIdx.x, t * T4 + threadIdx.x, acc_in, b4, e4);
     };
 #pragma unroll
@@ -362,20 +363,23 @@ fedavg_tiles_epi_burst_f32x4(const RowTableF32 tab, const int K, const int64_t t
             }
         }
     };
+    constexpr bool PREFETCH = LOOP != 6;  // A/B 6: tile m+1's operands loaded after tile m's stores
 #pragma unroll
     for (int m = 0; m < TPB; ++m) {
-        if (m + 1 < NT) operands(nxt, m + 1);
+        if (PREFETCH && m + 1 < NT) operands(nxt, m + 1);
         tile_epilogue(m, t_base + (int64_t)m * gridDim.x, [&](int c) __attribute__((always_inline)) { return dd[m][c]; });
+        if (!PREFETCH && m + 1 < NT) operands(nxt, m + 1);
 #pragma unroll
         for (int c = 0; c < CPL; ++c) cur[c] = nxt[c];
     }
 #pragma unroll 1
     for (int m = TPB; m < NT; ++m) {
-        if (m + 1 < NT) operands(nxt, m + 1);
+        if (PREFETCH && m + 1 < NT) operands(nxt, m + 1);
         tile_epilogue(m, t_base + (int64_t)m * gridDim.x,
                       [&](int c) __attribute__((always_inline)) {
                           return staged[((m - TPB) * CPL + c) * kBlock + threadIdx.x];
                       });
+        if (!PREFETCH && m + 1 < NT) operands(nxt, m + 1);
 #pragma unroll
         for (int c = 0; c < CPL; ++c) cur[c] = nxt[c];
     }
@@ -508,6 +512,7 @@ inline bool epi_loop_ab(const TileLaunch& L, const EpiParams& E, hipStream_t s, 
             case 3: *err = launch_epi_loop_ab<OP, FIN, ACC_IN, EPI, TPB_LDS, 3>(L, E, s, nl); return true;
             case 4: *err = launch_epi_loop_ab<OP, FIN, ACC_IN, EPI, TPB_LDS, 4>(L, E, s, nl); return true;
             case 5: *err = launch_epi_loop_ab<OP, FIN, ACC_IN, EPI, TPB_LDS, 5>(L, E, s, nl); return true;
+            case 6: *err = launch_epi_loop_ab<OP, FIN, ACC_IN, EPI, TPB_LDS, 6>(L, E, s, nl); return true;
             default: return false;
         }
     }
