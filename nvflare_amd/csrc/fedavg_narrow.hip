@@ -194,14 +194,16 @@ constexpr int kCpl16 = kTile16 / (8 * kBlock);  // 2
 #ifndef FEDAVG_NARROW_UNROLL
 #define FEDAVG_NARROW_UNROLL 6  // clients whose loads are in flight together (A/B: profiles/r01/narrow_unroll_ab.jsonl)
 #endif
+// Burst launches under this many clients take groups of 4 (round 4, bf16, groups of 4 against 6: 8 / 12 / 16 clients
+// 79.8 / 80.6 / 84.2 % against 77.8 / 77.5 / 82.0 %, but 64 clients 71.0 % against 89.4 %; profiles/r04/s13/)
+constexpr int kNarrowUnroll4MaxK = 32;
 
 // One tile's arrival-ordered sum for this lane's kCpl16 8-element groups, packed to the output format.
 // GROUPED (the burst form): load groups of UNROLL clients from client 0 on, as fedavg_arith.h tile_sum.
-template <int FMT, int OP, int FIN, bool ACC_IN, bool GROUPED = false>
+template <int FMT, int OP, int FIN, bool ACC_IN, bool GROUPED = false, int UNROLL = FEDAVG_NARROW_UNROLL>
 __device__ __forceinline__ void tile_sum16(u32x4 (&res)[kCpl16], const RowTableNarrow& tab, const int K,
                                            const int64_t off, const int64_t col, const u32x4* acc_in, const int64_t b8,
                                            const int64_t e8, const float fv) {
-    constexpr int UNROLL = FEDAVG_NARROW_UNROLL;
     float acc[kCpl16][8];
     int k = 0;
     if constexpr (ACC_IN) {
@@ -313,7 +315,7 @@ __global__ void __launch_bounds__(kBlock) fedavg_tiles_narrow(const RowTableNarr
 // form, profiles/r02/ab/narrow_burst_grouped.jsonl).
 // TPB_LDS > 0 (the default; burst mode 2): that many more tiles per block, their packed results held in LDS
 // (8 KiB per tile; each lane reads back only what it wrote) -- launches (TPB + TPB_LDS) / TPB times longer.
-template <int FMT, int OP, int FIN, bool ACC_IN, int TPB, int TPB_LDS = 0>
+template <int FMT, int OP, int FIN, bool ACC_IN, int TPB, int TPB_LDS = 0, int UNROLL = FEDAVG_NARROW_UNROLL>
 __global__ void __launch_bounds__(kBlock)
 __attribute__((amdgpu_waves_per_eu(FEDAVG_NARROW_BURST_WAVES, FEDAVG_NARROW_BURST_WAVES))) fedavg_tiles_narrow_burst(const RowTableNarrow tab, const int K, const int64_t tstride8, const u32x4* acc_in, u32x4* out,
                           const int64_t b8, const int64_t e8, const float fv, const int64_t t0, const int64_t t_end) {
@@ -324,7 +326,7 @@ __attribute__((amdgpu_waves_per_eu(FEDAVG_NARROW_BURST_WAVES, FEDAVG_NARROW_BURS
     for (int m = 0; m < TPB; ++m) {
         const int64_t t = t0 + blockIdx.x + (int64_t)m * gridDim.x;
         if (t < t_end)
-            tile_sum16<FMT, OP, FIN, ACC_IN, true>(res[m], tab, K, t * tstride8 + threadIdx.x, t * T8 + threadIdx.x,
+            tile_sum16<FMT, OP, FIN, ACC_IN, true, UNROLL>(res[m], tab, K, t * tstride8 + threadIdx.x, t * T8 + threadIdx.x,
                                                    acc_in, b8, e8, fv);
     }
     // the LDS-held tiles in a rolled loop: one more copy of the (long) tile body, not TPB_LDS of them
@@ -333,7 +335,7 @@ __attribute__((amdgpu_waves_per_eu(FEDAVG_NARROW_BURST_WAVES, FEDAVG_NARROW_BURS
         const int64_t t = t0 + blockIdx.x + (int64_t)m * gridDim.x;
         if (t < t_end) {
             u32x4 r[kCpl16];
-            tile_sum16<FMT, OP, FIN, ACC_IN, true>(r, tab, K, t * tstride8 + threadIdx.x, t * T8 + threadIdx.x, acc_in,
+            tile_sum16<FMT, OP, FIN, ACC_IN, true, UNROLL>(r, tab, K, t * tstride8 + threadIdx.x, t * T8 + threadIdx.x, acc_in,
                                                    b8, e8, fv);
 #pragma unroll
             for (int c = 0; c < kCpl16; ++c) staged[((m - TPB) * kCpl16 + c) * kBlock + threadIdx.x] = r[c];
@@ -371,14 +373,18 @@ static hipError_t launch_t16_a(const RowTableNarrow& tab, int K, int64_t tstride
     u32x4* o = static_cast<u32x4*>(out);
     constexpr int64_t T8 = (int64_t)kCpl16 * kBlock;
     if (burst == 2) {  // default: kBurstTiles in registers + kBurstLdsTiles16 in LDS per block and launch
+        // client groups of 4 under kNarrowUnroll4MaxK clients, of FEDAVG_NARROW_UNROLL (6) from there on
+        const bool u4 = K < kNarrowUnroll4MaxK;
         return burst_launches(b8 / T8, (e8 - 1) / T8 + 1, grid, kBurstTiles + kBurstLdsTiles16, nl, false,
                               [&](int nb, int64_t t0, int64_t t_end, uint32_t) {
-            if (acc_in)
-                hipLaunchKernelGGL((fedavg_tiles_narrow_burst<FMT, OP, FIN, true, kBurstTiles, kBurstLdsTiles16>), dim3(nb),
-                                   dim3(kBlock), 0, s, tab, K, tstride8, ai, o, b8, e8, fv, t0, t_end);
-            else
-                hipLaunchKernelGGL((fedavg_tiles_narrow_burst<FMT, OP, FIN, false, kBurstTiles, kBurstLdsTiles16>), dim3(nb),
-                                   dim3(kBlock), 0, s, tab, K, tstride8, ai, o, b8, e8, fv, t0, t_end);
+#define FEDAVG_T16_BURST(AI, U)                                                                                        \
+    hipLaunchKernelGGL((fedavg_tiles_narrow_burst<FMT, OP, FIN, AI, kBurstTiles, kBurstLdsTiles16, U>), dim3(nb),      \
+                       dim3(kBlock), 0, s, tab, K, tstride8, ai, o, b8, e8, fv, t0, t_end)
+            if (acc_in && u4) FEDAVG_T16_BURST(true, 4);
+            else if (acc_in) FEDAVG_T16_BURST(true, FEDAVG_NARROW_UNROLL);
+            else if (u4) FEDAVG_T16_BURST(false, 4);
+            else FEDAVG_T16_BURST(false, FEDAVG_NARROW_UNROLL);
+#undef FEDAVG_T16_BURST
         });
     }
     if (burst) {
