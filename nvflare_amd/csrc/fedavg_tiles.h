@@ -74,7 +74,10 @@ __global__ void __launch_bounds__(kBlock) fedavg_tiles_f32x4(const RowTableF32 t
 // form): groups of min(KC - g, 4) clients -- exactly the launch's rows, where the runtime form's last group re-loads
 // its last client in the missing slots (at K = 2 half of a tile's loads were such repeats) -- and every row pointer
 // and weight at a fixed kernarg offset, loaded once per kernel into SGPRs instead of per group and tile.
-template <int OP, bool ACC_IN, int KC, int CPL>
+// SHAPE: -1 (default) -- from 4 clients on the full group's loads as two pairs (fedavg_arith.h client_group4; plain
+// burst at 4 / 5 / 6 / 7 clients 71.9 / 73.7 / 73.7 / 77.0 % -> 76.9 / 75.7 / 75.1 / 83.3 %, profiles/r04/s15/, s16/),
+// together at 1-3; A/B only: 0 -- four together, 2 -- pairs (3 clients: a pair, then the third).
+template <int OP, bool ACC_IN, int KC, int CPL, int SHAPE = -1>
 __device__ __forceinline__ void tile_sum_kc(f32x4 (&acc)[CPL], const RowTableF32& tab, const int64_t off, const int64_t col,
                                             const f32x4* acc_in, const int64_t b4, const int64_t e4) {
     if constexpr (ACC_IN) {
@@ -86,6 +89,18 @@ __device__ __forceinline__ void tile_sum_kc(f32x4 (&acc)[CPL], const RowTableF32
     }
 #pragma unroll
     for (int g = 0; g < KC; g += 4) {
+        if constexpr (SHAPE == 2 || (SHAPE < 0 && KC >= 4)) {
+            if (g + 4 <= KC) {
+                client_group4<OP, ACC_IN, 2, CPL>(acc, tab, g, off);
+                continue;
+            }
+        }
+        if constexpr (SHAPE == 2 && KC == 3) {
+            client_group<OP, ACC_IN, 2, CPL>(acc, tab, 0, off);
+            fence_on(acc);
+            client_group<OP, ACC_IN, 1, CPL>(acc, tab, 2, off);
+            continue;
+        }
         f32x4 v[4][CPL];
 #pragma unroll
         for (int j = 0; j < 4; ++j)
@@ -111,9 +126,9 @@ __device__ __forceinline__ void tile_sum_kc(f32x4 (&acc)[CPL], const RowTableF32
 // The runtime-K form with the remainder REM = K mod 4 built in: full groups of 4 clients in a loop, then one group of
 // exactly REM clients -- no repeated loads for any K (fedavg_arith.h tile_sum's GROUPED form re-loads the last client
 // 4 - K mod 4 times per tile).  SHAPE: how a full group's loads are issued (fedavg_arith.h client_group4).  -1, the
-// default: from two full groups on (8+ clients) as two pairs, the second pair's loads after the first pair's
-// arithmetic; a single group, four together (pairs cost fused Adam 3 points at 5 clients, profiles/r04/s7/).
-// 0: always four together (round 4 until session 7); 2-4: the other shapes (A/B, launch variant bits 9-11).  Plain
+// default: as two pairs, the second pair's loads after the first pair's arithmetic (at 7 clients, one group plus 3:
+// 76.5 -> 82.8 %, profiles/r04/s15/).  0: four together (round 4 until session 7); 2-4: the other shapes (A/B,
+// launch variant bits 9-11).  Plain
 // burst, % of 8 TB/s, four together / round 3's GROUPED loop / pairs, one process each (profiles/r04/s7/plain_k*):
 // 64 clients 87.8 / 90.3 / 90.0, 32: 86.9 / 89.0 / 88.2, 16: 80.7 / 84.9 / 84.9, 8: 77.0 / 79.9 / 83.9 -- fewer
 // loads in flight per wave (one wave per SIMD) stream better.
@@ -130,7 +145,7 @@ __device__ __forceinline__ void tile_sum_rem(f32x4 (&acc)[CPL], const RowTableF3
     const int k_full = K - REM;
     if constexpr (SHAPE > 0) {
         for (int k = 0; k < k_full; k += 4) client_group4<OP, ACC_IN, SHAPE, CPL>(acc, tab, k, off);
-    } else if (SHAPE < 0 && k_full >= 8) {  // the default from two full groups on: pairs (uniform branch)
+    } else if constexpr (SHAPE < 0) {  // the default: pairs (these forms run from 7 clients on)
         for (int k = 0; k < k_full; k += 4) client_group4<OP, ACC_IN, 2, CPL>(acc, tab, k, off);
     } else {
     for (int k = 0; k < k_full; k += 4) {
@@ -180,7 +195,7 @@ template <int OP, bool ACC_IN, int UNROLL, int CPL, int KC, int SHAPE = -1>
 __device__ __forceinline__ void tile_sum_any(f32x4 (&acc)[CPL], const RowTableF32& tab, const int K, const int64_t off,
                                              const int64_t col, const f32x4* acc_in, const int64_t b4, const int64_t e4) {
     if constexpr (KC > 0) {
-        tile_sum_kc<OP, ACC_IN, KC, CPL>(acc, tab, off, col, acc_in, b4, e4);
+        tile_sum_kc<OP, ACC_IN, KC, CPL, SHAPE>(acc, tab, off, col, acc_in, b4, e4);
     } else if constexpr (KC < 0 && SHAPE == 1) {
         tile_sum<OP, ACC_IN, UNROLL, CPL, 2>(acc, tab, K, off, col, acc_in, b4, e4);
     } else if constexpr (KC < 0) {
@@ -285,6 +300,14 @@ template <int OP, int FIN, bool ACC_IN, int UNROLL, int CPL, int TPB, int TPB_LD
 inline hipError_t launch_burst(const TileLaunch& L, hipStream_t s, uint64_t* nl) {
     if constexpr (CPL == 4 && UNROLL == 4) {
         if constexpr (OP == FEDAVG_OP_TORCH && FIN == FEDAVG_FIN_DIV && !ACC_IN) {  // A/B: client-loop shapes, K % 4 == 0
+            const int shape = (L.variant >> kVariantLoopShift) & 7;
+            if (shape == 2 && L.k == 3) return launch_burst_kc<OP, FIN, ACC_IN, UNROLL, CPL, TPB, TPB_LDS, 3, 2>(L, s, nl);
+            if (shape == 5 && L.k == 4) return launch_burst_kc<OP, FIN, ACC_IN, UNROLL, CPL, TPB, TPB_LDS, 4, 0>(L, s, nl);
+            if (shape == 5 && L.k >= 5 && L.k <= 7) {  // one group plus a remainder, four together (before session 16)
+                if (L.k == 5) return launch_burst_kc<OP, FIN, ACC_IN, UNROLL, CPL, TPB, TPB_LDS, 5, 0>(L, s, nl);
+                if (L.k == 6) return launch_burst_kc<OP, FIN, ACC_IN, UNROLL, CPL, TPB, TPB_LDS, 6, 0>(L, s, nl);
+                return launch_burst_kc<OP, FIN, ACC_IN, UNROLL, CPL, TPB, TPB_LDS, -4, 0>(L, s, nl);
+            }
             if (L.k >= 8 && L.k % 4 == 0) {
                 switch ((L.variant >> kVariantLoopShift) & 7) {
                     case 1: return launch_burst_kc<OP, FIN, ACC_IN, UNROLL, CPL, TPB, TPB_LDS, -1, 1>(L, s, nl);
