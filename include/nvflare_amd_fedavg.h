@@ -335,8 +335,8 @@ int fedavg_set_launch(fedavg_ctx* ctx, int blocks_per_cu, int unroll);
  * 64+); a launch with fewer row reads (most NVFlare jobs run 2 clients) runs the PER-TILE-STORE form, which stores
  * each tile's results as it finishes (fused, 2-3 reads: its cross-tile pipelined variant, bit 2); every load and store
  * is nontemporal.  The plain burst kernel has the launch's client count built in for 1-6 clients and the count's
- * remainder mod 4 from 7 on (no repeated loads); from 8 clients on both burst kernels load each four-client group as
- * two pairs.  The bits (results are bit-identical in every variant):
+ * remainder mod 4 from 7 on (no repeated loads); each full four-client group's loads go out as two pairs (plain burst
+ * kernel from 4 clients on, fused from 8).  The bits (results are bit-identical in every variant):
  * bit 0 / bit 1 = the per-tile-store plain kernel with temporal client loads / temporal result stores (imply bit 3);
  * bit 2 = the per-tile epilogue kernel software-pipelined across tiles (the next tile's first client loads
  *         overlap the epilogue; implies bit 3 for the epilogue);
