@@ -5,8 +5,9 @@ One step = one aggregation: the arrival-ordered weighted accumulate-and-finalise
 device-resident client rows of P fp32 params -> P fp32 results (weighted_aggregation_helper.py:153-240,
 torch-mode arithmetic by default).  Inputs are resident in HBM before the timed region starts.
 
-  python bench.py [--gpus N --steps K --warmup W]          # default: BASELINE config 3, 64 clients x 1e9 params
-  torchrun --nproc-per-node N bench.py --gpus N ...        # N ranks, one GPU each, no data-path collective
+  python bench.py [--gpus N --steps K --warmup W]          # default: BASELINE config 3, 64 clients x 1e9 params;
+                                                           # N > 1: starts N rank processes itself (launch_ranks)
+  torchrun --nproc-per-node N bench.py --gpus N ...        # the same N ranks under torchrun (WORLD_SIZE set)
   python bench.py --config {2,3,4,5}                       # BASELINE.json configs[1..4] (presets below)
 
 Scaling.  The path shards by parameter bucket:
@@ -90,6 +91,8 @@ def parse(argv=None):
     ap.add_argument("--host-resident-params", type=float, default=None,
                     help="params per GPU of the 2h entry (default: config 2's 125M)")
     ap.add_argument("--watchdog-s", type=float, default=WATCHDOG_S, help="limit of the 4x and 2h entries")
+    ap.add_argument("--rank-timeout-s", type=float, default=RANK_TIMEOUT_S,
+                    help="--gpus N without torchrun: limit of the N rank processes this run starts")
     ap.add_argument("--mode", choices=["torch", "numpy"], default="torch")
     ap.add_argument("--blocks-per-cu", type=int, default=0,
                     help="0 = library default (burst kernel: 1 at >= 32 clients, else 2; fused: 1 at >= 64)")
@@ -126,6 +129,95 @@ def parse(argv=None):
     tokens = {"4x": CLIENT_SHARDED, "2h": HOST_RESIDENT, "2s": HOST_SHARDED}
     args.also = [] if args.also in ("", "none") else [tokens.get(x.strip()) or int(x) for x in args.also.split(",")]
     return args
+
+
+RANK_TIMEOUT_S = 1800.0  # the self-launched ranks' limit (python bench.py --gpus N without torchrun)
+RANK_GRACE_S = 60.0  # after one rank fails: how long the others get to end on their own before they are killed
+
+
+def _free_port() -> int:
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(args, argv) -> int:
+    """``python bench.py --gpus N`` with no WORLD_SIZE in the environment: start N rank
+    processes of this same script, one per GPU, the way ``torchrun --nproc-per-node N`` would (RANK / LOCAL_RANK /
+    WORLD_SIZE / MASTER_ADDR=127.0.0.1 / MASTER_PORT), and print rank 0's JSON line.  This process makes no GPU call
+    (it has not imported torch): it only starts the ranks, so nothing re-executes a process that touched the GPU.
+    The other ranks' stdout goes to stderr; every rank's stderr passes through (progress).  Returns the exit code: 0,
+    the first failing rank's code (the others then get RANK_GRACE_S to end before they are killed), or 124 when the
+    ranks have not finished within --rank-timeout-s (all killed)."""
+    import signal
+    import subprocess
+    import threading
+
+    world = args.gpus
+    script = os.environ.get("NVFLARE_AMD_BENCH_WORKER_SCRIPT") or os.path.abspath(__file__)  # a test seam
+    argv = list(sys.argv[1:] if argv is None else argv)
+    base_env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()), WORLD_SIZE=str(world),
+                    LOCAL_WORLD_SIZE=str(world), GROUP_RANK="0", NVFLARE_AMD_BENCH_LAUNCHED="1")
+    base_env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # RCCL over dmabuf IPC on this pool
+    procs, lines = [], []
+
+    def pump(p, rank):
+        for raw in p.stdout:
+            line = raw.decode(errors="replace")
+            if rank == 0 and line.startswith("{"):  # the result line; library chatter (gloo, RCCL) goes to stderr
+                lines.append(line)
+                sys.stdout.write(line)
+                sys.stdout.flush()
+            else:
+                sys.stderr.write(f"[rank {rank}] {line}")
+
+    for r in range(world):
+        env = dict(base_env, RANK=str(r), LOCAL_RANK=str(r))
+        p = subprocess.Popen([sys.executable, "-u", script, *argv], env=env, stdout=subprocess.PIPE,
+                             start_new_session=True)  # its own process group: killed as a whole on failure
+        t = threading.Thread(target=pump, args=(p, r), daemon=True)
+        t.start()
+        procs.append((p, t))
+
+    def kill_all():
+        for p, _ in procs:
+            if p.poll() is None:
+                try:
+                    os.killpg(p.pid, signal.SIGKILL)
+                except OSError:
+                    pass
+
+    deadline = time.monotonic() + args.rank_timeout_s
+    code, failed_at = 0, None
+    try:
+        while True:
+            states = [p.poll() for p, _ in procs]
+            bad = [(r, c) for r, c in enumerate(states) if c not in (None, 0)]
+            if bad and code == 0:
+                r, code = bad[0]
+                failed_at = time.monotonic()
+                print(f"bench: rank {r} exited with {code}; the other ranks get {RANK_GRACE_S:g} s", file=sys.stderr)
+            if all(c is not None for c in states):
+                break
+            now = time.monotonic()
+            if now > deadline or (failed_at is not None and now - failed_at > RANK_GRACE_S):
+                if failed_at is None:
+                    code = 124
+                    print(f"bench: the ranks did not finish within {args.rank_timeout_s:g} s; killed", file=sys.stderr)
+                kill_all()
+                break
+            time.sleep(0.2)
+    finally:
+        kill_all()
+        for p, t in procs:
+            p.wait()
+            t.join(timeout=5)
+    if code == 0 and len(lines) != 1:
+        print("bench: rank 0 printed no result line", file=sys.stderr)
+        code = 1
+    return code
 
 
 def dist_setup(args):
@@ -273,7 +365,8 @@ def cpu_baseline(args, K, P, op):
     Ps = int(min(args.cpu_sample_params, P))
     gen = [np.random.default_rng(1000 + k).standard_normal(Ps, dtype=np.float32) for k in range(K)]
     trows = [torch.from_numpy(g) for g in gen]
-    threads = torch.get_num_threads()
+    threads, cg_cpus, cg_file, affinity = baseline_threads()
+    prev_threads = torch.get_num_threads()
 
     def timed(limit_s):
         reps, t_tot = 0, 0.0
@@ -287,25 +380,22 @@ def cpu_baseline(args, K, P, op):
             reps += 1
         return reps, t_tot
 
-    reps, t_tot = timed(8.0)
+    torch.set_num_threads(threads)
+    try:
+        reps, t_tot = timed(8.0)
+    finally:
+        torch.set_num_threads(prev_threads)
     gibs = 4.0 * K * Ps * reps / t_tot / 2**30
     t0 = time.perf_counter()  # single-thread numpy restatement (the numpy-job path) for context
     orc.numpy_mode_reference(gen, weights)
     t_np = time.perf_counter() - t0
-    try:
-        affinity = len(os.sched_getaffinity(0))
-    except (AttributeError, OSError):
-        affinity = None
     omp = os.environ.get("OMP_NUM_THREADS")
-    full = None
-    if op == 1 and affinity and affinity > threads:  # the same timing on every CPU of the mask
-        torch.set_num_threads(affinity)
-        try:
-            reps_f, t_f = timed(8.0)
-        finally:
-            torch.set_num_threads(threads)
-        full = {"value": round(4.0 * K * Ps * reps_f / t_f / 2**30, 3), "unit": "GiB/s", "cores": affinity,
-                "sample": f"same sample, torch.set_num_threads({affinity}), {reps_f} reps in {t_f:.1f}s"}
+    if cg_cpus is not None:
+        reason = (f"min(affinity {affinity}, ceil(cgroup quota {cg_cpus:g} CPUs from {cg_file})): the CPUs this "
+                  f"process may use ({os.cpu_count()} on the host)")
+    else:
+        reason = (f"no cgroup CPU quota; min(affinity {affinity}, OMP_NUM_THREADS={omp} or torch's default "
+                  f"{prev_threads}) ({os.cpu_count()} on the host)")
     return {
         "value": round(gibs, 3),
         "unit": "GiB/s",
@@ -318,13 +408,87 @@ def cpu_baseline(args, K, P, op):
         "torch_threads": threads,
         "host_cpu_count": os.cpu_count(),
         "affinity_cpus": affinity,
+        "cgroup_cpus": round(cg_cpus, 3) if cg_cpus is not None else None,
+        "cgroup_quota_file": cg_file,
         "omp_num_threads_env": omp,
-        "cores_reason": (f"torch uses OMP_NUM_THREADS={omp} threads: the GPU pool's CPU share per GPU (the pool sets "
-                         f"it; {affinity} CPUs are in this process's affinity mask, {os.cpu_count()} on the host)"
-                         if omp else f"torch.get_num_threads() = {threads} ({affinity} CPUs in the affinity mask)"),
+        "cores_reason": reason,
         "host_cpu_model": _cpu_model(),
-        "full_affinity": full,
     }
+
+
+def cgroup_cpu_quota(root="/sys/fs/cgroup", proc_cgroup="/proc/self/cgroup"):
+    """CPUs this process's cgroup may use (quota / period, the smallest along its cgroup path), or None when no quota
+    is set.  cgroup v2: <root>/<path>/cpu.max ("max 100000" | "1600000 100000"); v1: cpu.cfs_quota_us and
+    cpu.cfs_period_us under the cpu (or cpu,cpuacct) hierarchy.  Returns (cpus as a float, the file it came from)."""
+    v2, v1 = None, None
+    try:
+        with open(proc_cgroup) as f:
+            for line in f:
+                parts = line.rstrip("\n").split(":", 2)
+                if len(parts) != 3:
+                    continue
+                if parts[0] == "0" and parts[1] == "":
+                    v2 = parts[2]
+                elif "cpu" in parts[1].split(","):
+                    v1 = (parts[1], parts[2])
+    except OSError:
+        pass
+
+    def walk(base, rel):
+        rel = rel.strip("/")
+        parts = rel.split("/") if rel else []
+        for i in range(len(parts), -1, -1):
+            yield os.path.join(base, *parts[:i])
+
+    best = None
+    if v2 is not None:
+        for d in walk(root, v2):
+            try:
+                with open(os.path.join(d, "cpu.max")) as f:
+                    q, p = f.read().split()[:2]
+            except (OSError, ValueError):
+                continue
+            if q != "max" and float(p) > 0:
+                c = float(q) / float(p)
+                if best is None or c < best[0]:
+                    best = (c, os.path.join(d, "cpu.max"))
+    if v1 is not None:
+        for ctrl in (v1[0], "cpu,cpuacct", "cpu"):
+            for d in walk(os.path.join(root, ctrl), v1[1]):
+                try:
+                    with open(os.path.join(d, "cpu.cfs_quota_us")) as f:
+                        q = int(f.read())
+                    with open(os.path.join(d, "cpu.cfs_period_us")) as f:
+                        p = int(f.read())
+                except (OSError, ValueError):
+                    continue
+                if q > 0 and p > 0:
+                    c = q / p
+                    if best is None or c < best[0]:
+                        best = (c, os.path.join(d, "cpu.cfs_quota_us"))
+            if best is not None:
+                break
+    return best
+
+
+def baseline_threads():
+    """Threads for the CPU baseline: min(affinity CPUs, ceil(cgroup quota)) when the cgroup sets a
+    quota -- a process that sees 256 CPUs but may use 16 thrashes at 256 threads -- else min(affinity,
+    OMP_NUM_THREADS or torch's default).  Returns (threads, cgroup cpus or None, quota file or None, affinity)."""
+    import math
+
+    import torch
+
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        affinity = os.cpu_count() or 1
+    quota = cgroup_cpu_quota()
+    if quota is not None:
+        return max(1, min(affinity, math.ceil(quota[0] - 1e-9))), quota[0], quota[1], affinity
+    omp = os.environ.get("OMP_NUM_THREADS")
+    want = int(omp) if omp and omp.isdigit() and int(omp) > 0 else torch.get_num_threads()
+    return max(1, min(affinity, want)), None, None, affinity
 
 
 def _cpu_model() -> str:
@@ -828,6 +992,12 @@ def client_sharded_entry(args, world, rank, local, line, also, state):
 
 def main(argv=None):
     args = parse(argv)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # one process per GPU, started here (no torchrun around us); nothing in this process touches the GPU
+        code = launch_ranks(args, argv)
+        if code:
+            sys.exit(code)
+        return
     world, rank, local = dist_setup(args)
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     from nvflare_amd.device import DeviceContext
