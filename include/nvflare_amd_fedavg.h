@@ -255,7 +255,7 @@ int fedavg_accumulate(fedavg_ctx* ctx, const void* const* rows, const double* we
  * so a slab of S clients with tile_stride = S * tile_elems keeps one tile's S client segments contiguous
  * in HBM.  Computes out[i] for begin <= i < end with the same per-element sequence as fedavg_accumulate;
  * out and acc_in are flat arrays indexed by i.  Every client's storage must cover the whole tiles that
- * [begin, end) touches.  tile_elems in {1024, 2048, 4096, 8192}; tile_stride, begin, end multiples of 4;
+ * [begin, end) touches.  tile_elems 4096 (A/B builds: 1024, 2048, 4096, 8192); tile_stride, begin, end multiples of 4;
  * pointers 16-byte aligned; any k_rows (more than 128 are chained through out). */
 int fedavg_accumulate_tiled(fedavg_ctx* ctx, const void* const* bases, const double* weights, int k_rows,
                             size_t tile_elems, size_t tile_stride, size_t begin, size_t end,
@@ -293,8 +293,12 @@ int fedavg_accumulate_tiled64(fedavg_ctx* ctx, const void* const* bases, const d
 
 /* fedavg_accumulate_tiled with a server-optimizer epilogue applied per element to d = fin(acc) in the
  * same launch (rows a9/a10): ADD_BASE writes base + d to out; SGD/ADAM update epi->param/state in place
- * and also store d to out when out != NULL.  More than 128 clients are chained through a partial sum
- * kept in out, or in a stream-ordered scratch when out is NULL or aliases an epilogue operand. */
+ * and also store d to out when out != NULL.  Product libraries fuse the (op, fin) pairs the drop-in produces
+ * (numpy * SCALE, torch * DIV | SCALE, unweighted * SCALE | DIV) for 1-128 clients, and the server step alone (k_rows
+ * == 0, acc_in = the aggregate, FEDAVG_FIN_NONE); any other call -- more than 128 clients, a chained acc_in with
+ * clients, numpy * DIV, FIN_NONE with clients -- runs the plain aggregation into a stream-ordered scratch and then that
+ * server step on it, the same per-element sequence.  (A/B libraries fuse every case: more than 128 clients chained
+ * through a partial sum kept in out, or in a scratch when out is NULL or aliases an epilogue operand.) */
 int fedavg_accumulate_tiled_epi(fedavg_ctx* ctx, const void* const* bases, const double* weights, int k_rows,
                                 size_t tile_elems, size_t tile_stride, size_t begin, size_t end,
                                 const void* acc_in, void* out, int op, int fin, double count,
@@ -325,33 +329,40 @@ int fedavg_timing_end(fedavg_ctx* ctx, float* ms);
 int fedavg_launch_count(fedavg_ctx* ctx, uint64_t* n);
 /* Launch tuning (0 = default): blocks per CU (default: each kernel's own -- 1 for the burst aggregation
  * kernel at >= 32 clients, the fused one at >= 64, the 16-bit one at >= 48 in torch mode, 2 otherwise),
- * clients whose loads are issued together (4 or 8, default 4). */
+ * clients whose loads are issued together (4; 8 in A/B builds only -- see below). */
 int fedavg_set_launch(fedavg_ctx* ctx, int blocks_per_cu, int unroll);
-/* Kernel variants (default 0).  By default a launch with 3 or more row reads (plain; fused: 4 or more -- its clients,
+/* Kernel variants (default 0).  By default a plain launch with 3 or more row reads (fused: 4 or more -- its clients,
  * plus the chained partial sum of a launch after the first 128 clients) runs the BURST form: each block holds its
  * tiles' results (the fused kernel: its differences) in registers and LDS and stores them (runs the epilogue) as
  * chip-wide bursts at the end of a short launch -- per launch 8 register-held tiles per block plus 4 LDS-held ones on
  * two-block-per-CU grids, or 10 (fused: 9) on the one-block-per-CU grids of the plain kernel at 32+ clients (fused:
- * 64+); a launch with fewer row reads (most NVFlare jobs run 2 clients) runs the PER-TILE-STORE form, which stores
- * each tile's results as it finishes (fused, 2-3 reads: its cross-tile pipelined variant, bit 2); every load and store
- * is nontemporal.  The plain burst kernel has the launch's client count built in for 1-6 clients and the count's
+ * 64+).  A plain launch with 1-2 client reads and no chained sum (most NVFlare jobs run 2 clients) runs the FEW-CLIENT
+ * burst form (round 5): every register-held tile's loads go out before any arithmetic, the results are stored as a
+ * burst; a chained sum with fewer than 3 reads runs the PER-TILE-STORE form, which stores each tile's results as it
+ * finishes; the fused kernel under 4 reads its per-tile form pipelined across tiles.  Every load and store is
+ * nontemporal.  The plain burst kernel has the launch's client count built in for 3-6 clients and the count's
  * remainder mod 4 from 7 on (no repeated loads); each full four-client group's loads go out as two pairs (plain burst
- * kernel from 4 clients on, fused from 8).  The bits (results are bit-identical in every variant):
- * bit 0 / bit 1 = the per-tile-store plain kernel with temporal client loads / temporal result stores (imply bit 3);
- * bit 2 = the per-tile epilogue kernel software-pipelined across tiles (the next tile's first client loads
- *         overlap the epilogue; implies bit 3 for the epilogue);
- * bit 3 = every launch on the per-tile-store form;
+ * kernel from 4 clients on, fused from 8).  Results are bit-identical in every variant.
+ * The PRODUCT library (nvflare_amd/_build.py) carries only the routed kernel forms and accepts:
+ * bit 2 = the fused per-tile form (pipelined across tiles: the next tile's first client loads overlap the epilogue) at
+ *         every read count;
  * bit 4 = burst launches after the first of a call go out without the AQL barrier bit (hipExtAnyOrderLaunch), so
  *         one launch's blocks start as the previous launch drains;
+ * bit 6 = one-block-per-CU grids keep the 4-LDS-tile form (12 tiles per block per launch).
+ * A/B libraries (tools/build_rev_lib.py, -DFEDAVG_AB) also carry, and accept:
+ * bit 0 / bit 1 = the per-tile-store plain kernel with temporal client loads / temporal result stores (imply bit 3);
+ * bit 3 = every launch on the per-tile-store form (fused: unpipelined);
  * bit 5 = the burst kernels without their LDS-held tiles (register-held tiles only: 8 per block per launch);
- * bit 6 = one-block-per-CU grids keep the 4-LDS-tile form (12 tiles per block per launch);
  * bit 7 = the plain burst kernel's round-3 runtime client loop (its last group of 4 re-loads the last client in the
  *         missing slots when the count is not a multiple of 4);
- * bit 8 = plain launches with fewer than 3 row reads keep the burst form;
- * bits 9-11 = A/B only: the fused burst kernel's client loop in shape 1-4 (fedavg_epi.h launch_epi_loop_ab; built for
- *         torch-mode FIN_DIV Adam with the AMD-host sqrt and no chained partial sum, ignored elsewhere). */
+ * bit 8 = plain launches with fewer than 3 row reads on the general burst form;
+ * bits 9-11 = the fused burst kernel's client loop in shape 1-6 (fedavg_epi.h launch_epi_loop_ab; built for torch-mode
+ *         FIN_DIV Adam with the AMD-host sqrt and no chained partial sum), the plain burst kernel's (fedavg_tiles.h
+ *         launch_burst), and for 1-2 reads the few-client form's geometry 1-6 (fedavg_internal.h kFewAB);
+ * and unroll 8 (fedavg_set_launch) and tile widths 1024 / 2048 / 8192 (fedavg_set_tile, fedavg_accumulate_tiled).
+ * A product library refuses those with an error ("... A/B form ..."), never running another form in their place. */
 int fedavg_set_variant(fedavg_ctx* ctx, int variant);
-/* Tile width used by fedavg_accumulate for contiguous rows (default 4096 elements). */
+/* Tile width used by fedavg_accumulate for contiguous rows (default 4096 elements; other widths in A/B builds). */
 int fedavg_set_tile(fedavg_ctx* ctx, int tile_elems);
 
 /* Synthetic inputs for benchmarks/tests: logical element j of a client row (tiled like

@@ -21,8 +21,12 @@ LIB_PATH = os.path.join(LIB_DIR, LIB_NAME)
 # (every optimizer kind x launch form) go further: fedavg_epi_inst.hip is compiled once per (mode,
 # finalisation), nine objects, the heaviest first in the queue
 EPI_SOURCE = "fedavg_epi_inst.hip"
-EPI_UNITS = [(f"{mode}_{fin}", op, fin_v) for mode, op in (("torch", 1), ("numpy", 0), ("unweighted", 2))
-             for fin, fin_v in (("div", 2), ("scale", 1), ("none", 0))]
+# A/B builds (-DFEDAVG_AB, tools/build_rev_lib.py): every (mode, finalisation) pair.  Product builds: the pairs the
+# drop-in's callers produce plus the server step alone (csrc/fedavg_internal.h epi_direct; "step" = -DFEDAVG_EPI_STEP)
+EPI_UNITS_AB = [(f"{mode}_{fin}", op, fin_v) for mode, op in (("torch", 1), ("numpy", 0), ("unweighted", 2))
+                for fin, fin_v in (("div", 2), ("scale", 1), ("none", 0))]
+EPI_UNITS = [u for u in EPI_UNITS_AB if u[0] in ("torch_div", "torch_scale", "numpy_scale", "unweighted_scale",
+                                                  "unweighted_div")] + [("step", None, None)]
 SOURCES = [EPI_SOURCE, "fedavg_tiles_numpy.hip", "fedavg_tiles_torch.hip", "fedavg_tiles_unweighted.hip",
            "fedavg_kernels.hip", "fedavg_narrow.hip", "fedavg_dequant.hip", "fedavg_capi.cpp"]
 HEADERS = ["fedavg_internal.h", "fedavg_rsqrt14.h", "fedavg_arith.h", "fedavg_tiles.h",
@@ -54,15 +58,16 @@ def needs_build() -> bool:
     return any(os.path.getmtime(f) > t for f in _inputs())
 
 
-def compile_units(sources=SOURCES):
+def compile_units(sources=SOURCES, ab=False):
     """(source, object name, extra flags) of every translation unit: the fused kernels' source once per EPI_UNITS
-    entry, the others once each."""
+    entry (EPI_UNITS_AB for an A/B build), the others once each."""
     units = []
     for src in sources:
         if src == EPI_SOURCE:
             units += [(src, f"fedavg_epi_{name}.hip.o",
+                       ["-DFEDAVG_EPI_STEP"] if op is None else
                        [f"-DFEDAVG_EPI_OP={op}", f"-DFEDAVG_EPI_FIN={fin}", f"-DFEDAVG_EPI_FN=launch_epi_{name}"])
-                      for name, op, fin in EPI_UNITS]
+                      for name, op, fin in (EPI_UNITS_AB if ab else EPI_UNITS)]
         else:
             units.append((src, src + ".o", []))
     return units
@@ -117,6 +122,9 @@ def build_library(force: bool = False, verbose: bool = False, jobs: int = 0) -> 
     jobs = jobs or min(len(units), max(1, min(16, os.cpu_count() or 1)))
     with ThreadPoolExecutor(max_workers=jobs) as pool:
         objs = list(pool.map(compile_one, units))
+    for f in os.listdir(OBJ_DIR):  # objects of units this build no longer has (an earlier unit list)
+        if f.endswith(".o") and os.path.join(OBJ_DIR, f) not in objs:
+            os.remove(os.path.join(OBJ_DIR, f))
     tmp = LIB_PATH + ".tmp"
     cmd = [HIPCC, *LINK_FLAGS, *objs, "-o", tmp, "-lpthread"]
     if verbose:

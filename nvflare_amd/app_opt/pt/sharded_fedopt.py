@@ -136,7 +136,10 @@ class ShardedServerOptimizer:
             off += (p.numel() + _HOST_ALIGN - 1) // _HOST_ALIGN * _HOST_ALIGN
         self.total = max(off, _HOST_ALIGN)
         self.host_pool = HostArenaPool()
-        self.out_pool = HostArenaPool()  # the weights handed out by to_host (independent of the live parameters)
+        # the weights handed out by to_host (independent of the live parameters); depth 2: the caller holds last
+        # round's hand-out while this round's is pulled, so two page-locked arrays suffice (depth 3 here
+        # beside host_pool's 3 page-locked five full-model arrays)
+        self.out_pool = HostArenaPool(depth=2)
         self._pool = ThreadPoolExecutor(max_workers=len(self.devices), thread_name_prefix="nvflare-amd-fedopt-shard")
         self._pool_fin = weakref.finalize(self, self._pool.shutdown, wait=False)  # a re-bound generator drops us
         me = weakref.ref(self)
@@ -285,6 +288,9 @@ class ShardedServerOptimizer:
             if lay is not None and v.dtype == torch.float32 and v.data_ptr() == base + 4 * lay[0]:
                 if handout is None:
                     with self._lock:
+                        # a parameter written in place on the host since the last step (load_state_dict, copy_) is
+                        # on the host only: upload it first, or the pull below would hand out the stale shard value
+                        self._upload_modified()
                         handout = self._pull(self.out_pool)
                 h = handout[lay[0]:lay[0] + lay[1]].reshape(tuple(v.shape))
                 out[k] = torch.from_numpy(h) if preserve_torch else h

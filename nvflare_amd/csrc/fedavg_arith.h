@@ -129,6 +129,41 @@ __device__ __forceinline__ f32x4 fin4c(const f32x4 a, const FinConst& f) {
     }
 }
 
+// div_const's fast path with its range check folded into `slow` (non-zero: some input left [2^-100, 2^100) or the
+// divisor is not fast); the caller recomputes a whole group with the exact form when it is set, so a group of
+// quotients is straight-line code with one branch after it instead of one per element (round 5: a branch is a
+// basic-block boundary the scheduler does not hoist loads across)
+__device__ __forceinline__ float div_const_fast(const float a, const FinConst& f, uint32_t& slow) {
+#if defined(FEDAVG_AB_IEEE_DIV)
+    return a / f.v;
+#endif
+    const float q = a * f.r;
+    const float e = __builtin_fmaf(-q, f.v, a);
+    slow |= (uint32_t)(((__float_as_uint(a) >> 23) & 0xFFu) - 27u >= 200u);
+    return __builtin_fmaf(e, f.r, q);
+}
+
+// fin4c over a lane's CPL columns of one tile, with one rare-case branch for all of them (div_const_fast)
+template <int FIN, int CPL>
+__device__ __forceinline__ void fin_tile(f32x4 (&r)[CPL], const f32x4 (&a)[CPL], const FinConst& f) {
+    if constexpr (FIN == FEDAVG_FIN_DIV) {
+        uint32_t slow = f.fast ? 0u : 1u;
+#pragma unroll
+        for (int c = 0; c < CPL; ++c)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) r[c][j] = div_const_fast(a[c][j], f, slow);
+        if (__builtin_expect(slow != 0u, 0)) {
+#pragma unroll
+            for (int c = 0; c < CPL; ++c)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) r[c][j] = a[c][j] / f.v;
+        }
+    } else {
+#pragma unroll
+        for (int c = 0; c < CPL; ++c) r[c] = fin4<FIN>(a[c], f.v);
+    }
+}
+
 // One tile's arrival-ordered sum for the CPL float4 columns this lane owns: acc = ACC_IN ? acc_in : first(client
 // 0), then step(client k) for every later client, UNROLL clients' loads issued before their arithmetic.  Client
 // rows are tiled (row + off is this lane's first column of the tile); acc_in is indexed by global column and
@@ -362,6 +397,27 @@ __device__ __forceinline__ float sqrt_torch_cpu(const float x) {
     return out;
 }
 
+// sqrt_torch_cpu without its special-input branch: `slow` set where it would have taken the callout (the caller then
+// recomputes the group with sqrt_torch_cpu)
+__device__ __forceinline__ float sqrt_torch_cpu_fast(const float x, uint32_t& slow) {
+    slow |= (uint32_t)(!(x > 0.0f) || x == __builtin_inff());
+    const bool tiny = x < 0x1p-96f;
+    const float xs = tiny ? x * 0x1p64f : x;
+    const uint32_t b = __float_as_uint(xs);
+    const int e = (int)(b >> 23) - 127;
+    const uint32_t m = b & 0x7FFFFFu;
+    const int p = e & 1;
+    const int k = (e - p) / 2;
+    const uint2 ab = g_rsqrt14_lds[(((uint32_t)p << 5) | (m >> 18)) & 63u];
+    const uint32_t y16 = (ab.x - ab.y * ((m >> 8) & 1023u)) >> 10;
+    const uint32_t yb = (p == 0 && m == 0) ? 0x3F800000u : (0x3F000000u | (y16 << 7));
+    const float y = __uint_as_float((uint32_t)((int32_t)yb - k * 8388608));
+    const float s = xs * y;
+    const float r = __builtin_fmaf(-s, s, xs);
+    const float res = __builtin_fmaf(r, 0.5f * y, s);
+    return tiny ? res * 0x1p-32f : res;
+}
+
 // torch CPU's fp32 Tensor.sqrt on hosts where MKL takes vsSqrt's SSE4.2 / AVX kernel -- the GPU pool's AMD EPYC hosts
 // (EpiParams.torch_sqrt == FEDAVG_SQRT_TORCH_AMD; mkl_vml_kernel_sSqrt_EXHAynn, equal to torch.sqrt on all 59.8 M probe
 // inputs on the box, tools/sqrt_box_kernels.py), which starts a coupled Newton step in plain fp32 -- every operation
@@ -402,6 +458,24 @@ __device__ __forceinline__ float sqrt_mkl_rsqrtps(const float x) {
     // unless one of their lanes needs it: the correctly rounded sqrt is more instructions than the refinement
     if (__builtin_expect(b - 0x00800000u > 0x7F7FF000u - 0x00800000u, 0)) res = __builtin_sqrtf(x);
     return res;
+}
+
+// sqrt_mkl_rsqrtps without its callout branch: `slow` set where it would have been taken (the caller then recomputes
+// the group with sqrt_mkl_rsqrtps)
+__device__ __forceinline__ float sqrt_mkl_rsqrtps_fast(const float x, uint32_t& slow) {
+    const uint32_t b = __float_as_uint(x);
+    slow |= (uint32_t)(b - 0x00800000u > 0x7F7FF000u - 0x00800000u);
+    const int e = (int)((b >> 23) & 0xFFu) - 127;
+    const int p = e & 1;
+    const int k = (e - p) / 2;
+    const uint32_t t = reinterpret_cast<const uint16_t*>(g_rsqrtps_lds)[((uint32_t)p << 12) | ((b & 0x7FFFFFu) >> 11)];
+    const float y = __uint_as_float((0x3F000000u | (t << 11)) - (uint32_t)(k * 8388608));
+    const float s = x * y;
+    const float h = y * 0.5f;
+    const float r = 0.5f - s * h;
+    const float s1 = s * r + s;
+    const float h1 = h * r + h;
+    return (x - s1 * s1) * h1 + s1;
 }
 
 }  // namespace fedavg

@@ -395,14 +395,22 @@ void run_tiles(fedavg_ctx* ctx, const void* const* bases, const double* weights,
         const int kc = std::min(k_rows - k0, fedavg::kMaxRowsPerLaunch);
         // the kernel form per launch: a chained chunk (acc_in + kc clients) reads kc + 1 rows
         const int reads = kc + (cur_in ? 1 : 0);
+        // 1-2 client reads without a chained sum: the few-client burst kernel (round 5) at the default geometry,
+        // unless the public variant asks for the per-tile form (bit 3) or the general burst form (bit 8; A/B builds)
+        const bool few = reads < kBurstMinClients && !cur_in && kc >= 1 && L.tile4 == fedavg::kDefaultTile / 4 &&
+                         L.unroll == fedavg::kDefaultUnroll &&
+                         !(ctx->variant & (fedavg::kVariantTileStores | fedavg::kVariantTemporalLoads |
+                                           fedavg::kVariantTemporalStores | kVariantFewBurst));
         const int variant =
-            ctx->variant | (reads < kBurstMinClients && !(ctx->variant & kVariantFewBurst) ? fedavg::kVariantTileStores : 0);
+            ctx->variant | (reads < kBurstMinClients && !few && !(ctx->variant & kVariantFewBurst) ? fedavg::kVariantTileStores
+                                                                                                  : 0);
         const bool burst = fedavg::tiles_use_burst(L.tile4, L.unroll, variant);
-        const int bpc = burst ? ctx->bpc(k_rows >= fedavg::kBurstOneBlockMinK ? 1 : 2) : ctx->bpc();
+        int bpc = burst ? ctx->bpc(k_rows >= fedavg::kBurstOneBlockMinK ? 1 : 2) : ctx->bpc();
+        if (few) bpc = ctx->bpc(fedavg::few_form(kc, ctx->variant).bpc);
         // one block per CU: the burst kernel holds 10 tiles in LDS (all 160 KiB); public bit 6 keeps the 4-tile
         // form, public bit 5 (register-held tiles only) keeps no LDS tiles at all
-        const bool wide = burst && bpc == 1 && !(variant & (fedavg::kVariantWideLds | fedavg::kVariantRegisterTiles));
-        L.variant = (variant & ~fedavg::kVariantWideLds) | (wide ? fedavg::kVariantWideLds : 0);
+        const bool wide = !few && burst && bpc == 1 && !(variant & (fedavg::kVariantWideLds | fedavg::kVariantRegisterTiles));
+        L.variant = (variant & ~fedavg::kVariantWideLds) | (wide ? fedavg::kVariantWideLds : 0) | (few ? fedavg::kVariantFew : 0);
         L.grid = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)ctx->num_cus * bpc, n_tiles));
         memset(&L.tab, 0, sizeof(L.tab));
         for (int j = 0; j < kc; ++j) {
@@ -1109,6 +1117,8 @@ int fedavg_accumulate_tiled(fedavg_ctx* ctx, const void* const* bases, const dou
         check_op_fin(op, fin);
         normalize_wide(op, fin, count, true);
         if (!valid_tile(tile_elems)) throw Error("tile_elems must be 1024, 2048, 4096 or 8192");
+        if (!fedavg::kAB && tile_elems != (size_t)fedavg::kDefaultTile)
+            throw Error("tile_elems " + std::to_string(tile_elems) + " is an A/B form (this product library carries 4096)");
         if (tile_stride < tile_elems || tile_stride % 4) throw Error("tile_stride must be >= tile_elems, multiple of 4");
         if (begin % 4 || end % 4 || end < begin) throw Error("begin/end must be multiples of 4 with begin <= end");
         if (end == begin) {
@@ -1311,7 +1321,20 @@ int fedavg_accumulate_tiled_epi(fedavg_ctx* ctx, const void* const* bases, const
         int head = k_rows > fedavg::kMaxRowsPerLaunch ? (k_rows - 1) / fedavg::kMaxRowsPerLaunch * fedavg::kMaxRowsPerLaunch : 0;
         const float* cur_in = static_cast<const float*>(acc_in);
         void* scratch = nullptr;
-        if (head > 0) {
+        if (!fedavg::epi_direct(op, fin, k_rows, acc_in != nullptr)) {
+            // A fused form the product library does not carry (fedavg_internal.h epi_direct: a chained partial sum,
+            // more than 128 clients, a finalisation with no clients, numpy mode with FIN_DIV, FIN_NONE with clients):
+            // the plain kernels finalise d = fin(acc) into a scratch, then the server step reads it as its chained sum
+            // (no clients, FIN_NONE).  The per-element sequence is the fused one, so the bits are the same.
+            HIP_CHECK(hipMallocAsync(&scratch, (end - begin) * sizeof(float), s));
+            float* d = static_cast<float*>(scratch) - begin;  // indexed by global element, touched on [begin, end)
+            run_tiles(ctx, bases, weights, k_rows, (int64_t)tile_elems, (int64_t)tile_stride, (int64_t)begin,
+                      (int64_t)end, cur_in, d, op, fin, count, s);
+            cur_in = d;
+            head = k_rows;
+            op = FEDAVG_OP_TORCH;
+            fin = FEDAVG_FIN_NONE;
+        } else if (head > 0) {
             float* partial = static_cast<float*>(out);
             const void* operands[] = {epi->base, epi->param, epi->state1, epi->state2, epi->state3};
             bool alias = !out;
@@ -1344,10 +1367,13 @@ int fedavg_accumulate_tiled_epi(fedavg_ctx* ctx, const void* const* bases, const
         // under kEpiBurstMinClients row reads the per-tile form; from 2 reads on its cross-tile pipelined variant
         // (Adam at 2 / 3 clients +1.8 / +1.4 and +0.9 / +1.0 points on two boxes, 1 client -1.5 / +0.1:
         // profiles/r04/s9/epi_bpc_k*.jsonl, s10/epi_pipe_k*.jsonl), unless the public variant asks for tile stores
+        // (product builds: the pipelined per-tile form at every read count under kEpiBurstMinClients -- at one read it
+        // carries client 0, or nothing for the server step -- and for a chained sum; the unpipelined one is A/B only)
         const int reads = L.k + (cur_in ? 1 : 0);
-        if (reads < kEpiBurstMinClients)
-            L.variant |= reads >= 2 && !(ctx->variant & fedavg::kVariantTileStores) ? fedavg::kVariantEpiPrefetch
-                                                                                    : fedavg::kVariantTileStores;
+        if (reads < kEpiBurstMinClients || (!fedavg::kAB && cur_in))
+            L.variant |= (reads >= 2 || !fedavg::kAB) && !(ctx->variant & fedavg::kVariantTileStores)
+                             ? fedavg::kVariantEpiPrefetch
+                             : fedavg::kVariantTileStores;
         const bool burst = !(L.variant & (fedavg::kVariantEpiPrefetch | fedavg::kVariantTileStores));
         const int bpc = burst ? ctx->bpc(L.k >= fedavg::kEpiOneBlockMinK ? 1 : 2) : ctx->bpc();
         // one block per CU: the LDS-held tiles fill the CU (9 instead of 4), unless the public variant has bit 6
@@ -1415,6 +1441,8 @@ int fedavg_set_launch(fedavg_ctx* ctx, int blocks_per_cu, int unroll) {
         if (!ctx) throw Error("ctx is NULL");
         if (blocks_per_cu < 0 || blocks_per_cu > 32) throw Error("blocks_per_cu out of range");
         if (unroll != 0 && unroll != 4 && unroll != 8) throw Error("unroll must be 0, 4 or 8");
+        if (!fedavg::kAB && unroll == 8)
+            throw Error("unroll 8 is an A/B form (this product library carries unroll 4; tools/build_rev_lib.py builds A/B libraries)");
         ctx->blocks_per_cu = blocks_per_cu;
         ctx->unroll = unroll ? unroll : fedavg::kDefaultUnroll;
     });
@@ -1424,6 +1452,10 @@ int fedavg_set_variant(fedavg_ctx* ctx, int variant) {
     return guarded([&] {
         if (!ctx) throw Error("ctx is NULL");
         if (variant < 0 || variant > 4095) throw Error("variant must be 0..4095");
+        if (!fedavg::kAB && (variant & ~fedavg::kVariantProductMask))
+            throw Error("variant bits " + std::to_string(variant & ~fedavg::kVariantProductMask) +
+                        " are A/B forms this product library does not carry (it accepts bits 2, 4 and 6; "
+                        "tools/build_rev_lib.py builds A/B libraries)");
         ctx->variant = variant;
     });
 }
@@ -1433,6 +1465,9 @@ int fedavg_set_tile(fedavg_ctx* ctx, int tile_elems) {
         if (!ctx) throw Error("ctx is NULL");
         if (tile_elems == 0) tile_elems = fedavg::kDefaultTile;
         if (!valid_tile((size_t)tile_elems)) throw Error("tile_elems must be 1024, 2048, 4096 or 8192");
+        if (!fedavg::kAB && tile_elems != fedavg::kDefaultTile)
+            throw Error("tile_elems " + std::to_string(tile_elems) +
+                        " is an A/B form (this product library carries 4096; tools/build_rev_lib.py builds A/B libraries)");
         ctx->tile = tile_elems;
     });
 }

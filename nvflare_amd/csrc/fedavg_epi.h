@@ -90,14 +90,42 @@ __device__ __forceinline__ EpiIn epi_load(const EpiParams& E, const int64_t i) {
     return in;
 }
 
+// The epilogues' sqrt and constant-divisor quotient in two forms (round 5): FAST -- straight-line, each rare input
+// (sqrt_torch_cpu / sqrt_mkl_rsqrtps callouts, div_const outside its checked range) only noted in `slow`; exact -- the
+// per-element forms with their branches.  epilogue4 computes a column group FAST and recomputes it exactly when any
+// lane noted a rare input, so the common case has one branch per column group instead of one per sqrt and quotient.
+template <int SQ, bool FAST>
+__device__ __forceinline__ float sqrt_x(const EpiParams& E, const float x, uint32_t& slow) {
+    if constexpr (FAST && SQ == kEpiTorchSqrt) return sqrt_torch_cpu_fast(x, slow);
+    if constexpr (FAST && SQ == kEpiTorchSqrtAmd) return sqrt_mkl_rsqrtps_fast(x, slow);
+    return sqrt_e<SQ>(E, x);
+}
+
+template <bool FAST>
+__device__ __forceinline__ float div_x(const float a, const FinConst& f, uint32_t& slow) {
+    if constexpr (FAST) return div_const_fast(a, f, slow);
+    return div_const(a, f);
+}
+
+// whether the optimizer kind has a rare-input path at all (a restated sqrt, or a constant-divisor quotient)
 template <int EPI>
-__device__ __forceinline__ void epilogue4(const EpiParams& E, const EpiConsts& C, const int64_t i, const f32x4 d,
-                                          const EpiIn& in, f32x4* out) {
+constexpr bool epi_has_rare() {
+    constexpr int KIND = EPI & 0xFF;
+    constexpr bool sq = (EPI & kEpiSqrtMask) != 0 &&
+                        (KIND == FEDAVG_EPI_ADAM || KIND == FEDAVG_EPI_ADAGRAD || KIND == FEDAVG_EPI_RMSPROP ||
+                         KIND == FEDAVG_EPI_NADAM || KIND == FEDAVG_EPI_RADAM);
+    return sq || KIND == FEDAVG_EPI_ADAM || KIND == FEDAVG_EPI_NADAM || KIND == FEDAVG_EPI_RADAM;
+}
+
+// one column group's optimizer step: the new parameter (ADD_BASE: the result) in .a, the new states in .b / .c / .d
+template <int EPI, bool FAST>
+__device__ __forceinline__ EpiIn epi_compute(const EpiParams& E, const EpiConsts& C, const f32x4 d, const EpiIn& in,
+                                             uint32_t& slow) {
     constexpr int KIND = EPI & 0xFF;
     constexpr int TSQ = EPI & kEpiSqrtMask;
-    f32x4* p4 = reinterpret_cast<f32x4*>(E.param) + i;
+    EpiIn o = in;
     if constexpr (KIND == FEDAVG_EPI_ADD_BASE) {
-        store4<true>(out + i, in.a + d);
+        o.a = in.a + d;
     } else if constexpr (KIND == FEDAVG_EPI_SGD) {
         f32x4 p = in.a;
         f32x4 buf = in.b;
@@ -112,8 +140,8 @@ __device__ __forceinline__ void epilogue4(const EpiParams& E, const EpiConsts& C
             }
             p[c] = __builtin_fmaf(g, E.neg_lr, p[c]);
         }
-        store4<true>(p4, p);
-        if (E.has_momentum) store4<true>(reinterpret_cast<f32x4*>(E.state1) + i, buf);
+        o.a = p;
+        o.b = buf;
     } else if constexpr (KIND == FEDAVG_EPI_ADAGRAD) {
         f32x4 p = in.a;
         f32x4 sum = in.b;
@@ -122,11 +150,11 @@ __device__ __forceinline__ void epilogue4(const EpiParams& E, const EpiConsts& C
             float g = E.maximize ? d[c] : -d[c];
             if (E.has_weight_decay) g = __builtin_fmaf(p[c], E.weight_decay, g);  // grad.add(param, alpha=wd)
             sum[c] = __builtin_fmaf(g, g, sum[c]);                                 // state_sum.addcmul_(g, g, value=1)
-            const float std_ = sqrt_e<TSQ>(E, sum[c]) + E.eps;                    // state_sum.sqrt().add_(eps)
+            const float std_ = sqrt_x<TSQ, FAST>(E, sum[c], slow) + E.eps;        // state_sum.sqrt().add_(eps)
             p[c] = p[c] + (E.step_size_neg * g) / std_;                            // param.addcdiv_(g, std, value=-clr)
         }
-        store4<true>(p4, p);
-        store4<true>(reinterpret_cast<f32x4*>(E.state1) + i, sum);
+        o.a = p;
+        o.b = sum;
     } else if constexpr (KIND == FEDAVG_EPI_RMSPROP) {
         f32x4 p = in.a;
         f32x4 sq = in.b;
@@ -140,9 +168,9 @@ __device__ __forceinline__ void epilogue4(const EpiParams& E, const EpiConsts& C
             float avg;
             if (E.centered) {
                 ga[c] = lerp_torch(ga[c], g, E.one_minus_beta1, E.one_minus_beta1_m1);  // grad_avg.lerp_(g, 1-alpha)
-                avg = sqrt_e<TSQ>(E, __builtin_fmaf(-ga[c], ga[c], sq[c]));          // addcmul(ga, ga, -1).sqrt_()
+                avg = sqrt_x<TSQ, FAST>(E, __builtin_fmaf(-ga[c], ga[c], sq[c]), slow);  // addcmul(ga, ga, -1).sqrt_()
             } else {
-                avg = sqrt_e<TSQ>(E, sq[c]);
+                avg = sqrt_x<TSQ, FAST>(E, sq[c], slow);
             }
             avg = avg + E.eps;
             if (E.has_momentum) {
@@ -152,10 +180,10 @@ __device__ __forceinline__ void epilogue4(const EpiParams& E, const EpiConsts& C
                 p[c] = p[c] + (E.neg_lr * g) / avg;                                   // param.addcdiv_(g, avg, -lr)
             }
         }
-        store4<true>(p4, p);
-        store4<true>(reinterpret_cast<f32x4*>(E.state1) + i, sq);
-        if (E.has_momentum) store4<true>(reinterpret_cast<f32x4*>(E.state2) + i, buf);
-        if (E.centered) store4<true>(reinterpret_cast<f32x4*>(E.state3) + i, ga);
+        o.a = p;
+        o.b = sq;
+        o.c = buf;
+        o.d = ga;
     } else if constexpr (KIND == FEDAVG_EPI_ADAMAX) {
         f32x4 p = in.a;
         f32x4 m = in.b;
@@ -168,9 +196,9 @@ __device__ __forceinline__ void epilogue4(const EpiParams& E, const EpiConsts& C
             u[c] = max_torch(u[c] * E.beta2, fabsf(g) + E.eps);                      // maximum(exp_inf*b2, |g|+eps)
             p[c] = p[c] + (E.step_size_neg * m[c]) / u[c];                            // addcdiv_(exp_avg, exp_inf, -clr)
         }
-        store4<true>(p4, p);
-        store4<true>(reinterpret_cast<f32x4*>(E.state1) + i, m);
-        store4<true>(reinterpret_cast<f32x4*>(E.state2) + i, u);
+        o.a = p;
+        o.b = m;
+        o.c = u;
     } else if constexpr (KIND == FEDAVG_EPI_ASGD) {
         f32x4 p = in.a;
         f32x4 ax = in.b;
@@ -183,8 +211,8 @@ __device__ __forceinline__ void epilogue4(const EpiParams& E, const EpiConsts& C
             ax[c] = E.mu != 1.0f ? ax[c] + (pv - ax[c]) * E.mu : pv;               // ax.add_(p.sub(ax).mul_(mu)) | copy_
             p[c] = pv;
         }
-        store4<true>(p4, p);
-        store4<true>(reinterpret_cast<f32x4*>(E.state1) + i, ax);
+        o.a = p;
+        o.b = ax;
     } else if constexpr (KIND == FEDAVG_EPI_RPROP) {
         f32x4 p = in.a;
         f32x4 prev = in.b;
@@ -202,9 +230,9 @@ __device__ __forceinline__ void epilogue4(const EpiParams& E, const EpiConsts& C
             prev[c] = g;                                                   // prev.copy_(grad)
             ss[c] = st;
         }
-        store4<true>(p4, p);
-        store4<true>(reinterpret_cast<f32x4*>(E.state1) + i, prev);
-        store4<true>(reinterpret_cast<f32x4*>(E.state2) + i, ss);
+        o.a = p;
+        o.b = prev;
+        o.c = ss;
     } else if constexpr (KIND == FEDAVG_EPI_NADAM || KIND == FEDAVG_EPI_RADAM) {
         f32x4 p = in.a;
         f32x4 m = in.b;
@@ -220,22 +248,23 @@ __device__ __forceinline__ void epilogue4(const EpiParams& E, const EpiConsts& C
             m[c] = lerp_torch(m[c], g, E.one_minus_beta1, E.one_minus_beta1_m1);
             v[c] = __builtin_fmaf(E.one_minus_beta2 * g, g, v[c] * E.beta2);
             if constexpr (KIND == FEDAVG_EPI_NADAM) {
-                const float denom = sqrt_e<TSQ>(E, div_const(v[c], C.bc2)) + E.eps;  // exp_avg_sq.div(bc2).sqrt().add_(eps)
+                // exp_avg_sq.div(bc2).sqrt().add_(eps)
+                const float denom = sqrt_x<TSQ, FAST>(E, div_x<FAST>(v[c], C.bc2, slow), slow) + E.eps;
                 pv = pv + (E.coef_grad * g) / denom;                                    // addcdiv_(grad, denom, value)
                 pv = pv + (E.coef_avg * m[c]) / denom;                                  // addcdiv_(exp_avg, denom, value)
             } else {
-                float t = div_const(m[c], C.bc1) * E.lr;                                // exp_avg / bc1 * lr
+                float t = div_x<FAST>(m[c], C.bc1, slow) * E.lr;                        // exp_avg / bc1 * lr
                 if (E.rectified) {
-                    const float a = (1.0f / (sqrt_e<TSQ>(E, v[c]) + E.eps)) * E.bias_correction2_sqrt;  // bc2**0.5 / (sqrt+eps)
-                    t = (t * a) * E.rect;
+                    const float a = (1.0f / (sqrt_x<TSQ, FAST>(E, v[c], slow) + E.eps)) * E.bias_correction2_sqrt;
+                    t = (t * a) * E.rect;                                               // bc2**0.5 / (sqrt+eps)
                 }
                 pv = __builtin_fmaf(t, -1.0f, pv);                                      // param.add_(..., alpha=-1)
             }
             p[c] = pv;
         }
-        store4<true>(p4, p);
-        store4<true>(reinterpret_cast<f32x4*>(E.state1) + i, m);
-        store4<true>(reinterpret_cast<f32x4*>(E.state2) + i, v);
+        o.a = p;
+        o.b = m;
+        o.c = v;
     } else {  // EPI_ADAM
         f32x4 p = in.a;
         f32x4 m = in.b;
@@ -256,17 +285,65 @@ __device__ __forceinline__ void epilogue4(const EpiParams& E, const EpiConsts& C
                 vmax[c] = max_torch(vmax[c], vv);
                 vden = vmax[c];
             }
-            const float denom = div_const(sqrt_e<TSQ>(E, vden), C.bc2s) + E.eps;  // sqrt(v) / sqrt(bc2) + eps
+            const float denom = div_x<FAST>(sqrt_x<TSQ, FAST>(E, vden, slow), C.bc2s, slow) + E.eps;  // sqrt(v)/sqrt(bc2)+eps
             pv = pv + (E.step_size_neg * mm) / denom;
             m[c] = mm;
             v[c] = vv;
             p[c] = pv;
         }
-        store4<true>(p4, p);
-        store4<true>(reinterpret_cast<f32x4*>(E.state1) + i, m);
-        store4<true>(reinterpret_cast<f32x4*>(E.state2) + i, v);
-        if (E.amsgrad) store4<true>(reinterpret_cast<f32x4*>(E.state3) + i, vmax);
+        o.a = p;
+        o.b = m;
+        o.c = v;
+        o.d = vmax;
     }
+    return o;
+}
+
+template <int EPI>
+__device__ __forceinline__ void epi_store(const EpiParams& E, const int64_t i, const EpiIn& o, f32x4* out) {
+    constexpr int KIND = EPI & 0xFF;
+    if constexpr (KIND == FEDAVG_EPI_ADD_BASE) {
+        store4<true>(out + i, o.a);
+        return;
+    }
+    store4<true>(reinterpret_cast<f32x4*>(E.param) + i, o.a);
+    f32x4* s1 = reinterpret_cast<f32x4*>(E.state1) + i;
+    f32x4* s2 = reinterpret_cast<f32x4*>(E.state2) + i;
+    f32x4* s3 = reinterpret_cast<f32x4*>(E.state3) + i;
+    if constexpr (KIND == FEDAVG_EPI_SGD) {
+        if (E.has_momentum) store4<true>(s1, o.b);
+    } else if constexpr (KIND == FEDAVG_EPI_ADAGRAD || KIND == FEDAVG_EPI_ASGD) {
+        store4<true>(s1, o.b);
+    } else if constexpr (KIND == FEDAVG_EPI_RMSPROP) {
+        store4<true>(s1, o.b);
+        if (E.has_momentum) store4<true>(s2, o.c);
+        if (E.centered) store4<true>(s3, o.d);
+    } else if constexpr (KIND == FEDAVG_EPI_ADAMAX || KIND == FEDAVG_EPI_RPROP || KIND == FEDAVG_EPI_NADAM ||
+                         KIND == FEDAVG_EPI_RADAM) {
+        store4<true>(s1, o.b);
+        store4<true>(s2, o.c);
+    } else {  // ADAM
+        store4<true>(s1, o.b);
+        store4<true>(s2, o.c);
+        if (E.amsgrad) store4<true>(s3, o.d);
+    }
+}
+
+template <int EPI>
+__device__ __forceinline__ void epilogue4(const EpiParams& E, const EpiConsts& C, const int64_t i, const f32x4 d,
+                                          const EpiIn& in, f32x4* out) {
+    uint32_t slow = 0;
+    if constexpr ((EPI & 0xFF) == FEDAVG_EPI_ADAM) slow = C.bc2s.fast ? 0u : 1u;
+    if constexpr ((EPI & 0xFF) == FEDAVG_EPI_NADAM) slow = C.bc2.fast ? 0u : 1u;
+    if constexpr ((EPI & 0xFF) == FEDAVG_EPI_RADAM) slow = C.bc1.fast ? 0u : 1u;
+    EpiIn o = epi_compute<EPI, epi_has_rare<EPI>()>(E, C, d, in, slow);
+    if constexpr (epi_has_rare<EPI>()) {
+        if (__builtin_expect(slow != 0u, 0)) {
+            uint32_t unused = 0;
+            o = epi_compute<EPI, false>(E, C, d, in, unused);
+        }
+    }
+    epi_store<EPI>(E, i, o, out);
 }
 
 // PIPE: software-pipelined across tiles -- after the client loop of tile t the lane issues the epilogue
@@ -315,18 +392,18 @@ fedavg_tiles_epi_burst_f32x4(const RowTableF32 tab, const int K, const int64_t t
         if (t < t_end) {
             f32x4 acc[CPL];
             sum(acc, t);
-#pragma unroll
-            for (int c = 0; c < CPL; ++c) dd[m][c] = fin4c<FIN>(acc[c], fc);
+            fin_tile<FIN, CPL>(dd[m], acc, fc);
         }
     }
 #pragma unroll 1
     for (int m = TPB; m < NT; ++m) {  // rolled: one more copy of the client loop, not TPB_LDS of them
         const int64_t t = t0 + blockIdx.x + (int64_t)m * gridDim.x;
         if (t < t_end) {
-            f32x4 acc[CPL];
+            f32x4 acc[CPL], r[CPL];
             sum(acc, t);
+            fin_tile<FIN, CPL>(r, acc, fc);
 #pragma unroll
-            for (int c = 0; c < CPL; ++c) staged[((m - TPB) * CPL + c) * kBlock + threadIdx.x] = fin4c<FIN>(acc[c], fc);
+            for (int c = 0; c < CPL; ++c) staged[((m - TPB) * CPL + c) * kBlock + threadIdx.x] = r[c];
         }
     }
     // Epilogue phase, double-buffered: tile m+1's operand loads are issued before tile m's arithmetic and
@@ -476,13 +553,14 @@ __global__ void __launch_bounds__(kBlock) fedavg_tiles_epi_f32x4(const RowTableF
                         for (int c = 0; c < CPL; ++c) nxt[j][c] = load4<true>(tab.rows[j] + offn + c * kBlock);
             }
         }
+        f32x4 dv[CPL];
+        fin_tile<FIN, CPL>(dv, acc, fc);
 #pragma unroll
         for (int c = 0; c < CPL; ++c) {
             const int64_t i = col + c * kBlock;
             if (i >= b4 && i < e4) {
-                const f32x4 d = fin4c<FIN>(acc[c], fc);
-                if (out != nullptr && (EPI & 0xFF) != FEDAVG_EPI_ADD_BASE) store4<true>(out + i, d);
-                epilogue4<EPI>(E, C, i, d, pre[c], out);
+                if (out != nullptr && (EPI & 0xFF) != FEDAVG_EPI_ADD_BASE) store4<true>(out + i, dv[c]);
+                epilogue4<EPI>(E, C, i, dv[c], pre[c], out);
             }
         }
     }
@@ -519,48 +597,61 @@ inline bool epi_loop_ab(const TileLaunch& L, const EpiParams& E, hipStream_t s, 
     return false;
 }
 
-// one kernel instantiation per optimizer kind: K(EPI) launches the per-tile (PRE) or the burst form
+// one kernel instantiation per optimizer kind: K(EPI) launches the per-tile (PRE) or the burst form.  Product builds
+// (fedavg_internal.h kAB): the burst form with 4 (two blocks per CU) or 9 (one block per CU) LDS-held tiles without a
+// chained sum, the pipelined per-tile form; A/B builds also the register-only burst form, the burst form over a
+// chained sum, the unpipelined per-tile form and the client-loop shapes.
 template <int OP, int FIN, bool ACC_IN, int EPI>
 inline hipError_t launch_epi_k(const TileLaunch& L, const EpiParams& E, hipStream_t s, uint64_t* nl) {
     const f32x4* ai = reinterpret_cast<const f32x4*>(L.acc_in);
     f32x4* o = reinterpret_cast<f32x4*>(L.out);
-    if (!(L.variant & (kVariantTileStores | kVariantEpiPrefetch))) {  // burst: one launch per grid x TPB tiles
-        hipError_t ab_err = hipSuccess;
-        if ((L.variant & kVariantWideLds) && epi_loop_ab<OP, FIN, ACC_IN, EPI, kBurstEpiLdsTilesWide>(L, E, s, nl, &ab_err))
-            return ab_err;
-        if (!(L.variant & (kVariantWideLds | kVariantRegisterTiles)) &&
-            epi_loop_ab<OP, FIN, ACC_IN, EPI, kBurstLdsTiles>(L, E, s, nl, &ab_err))
-            return ab_err;
-        if (L.variant & kVariantWideLds)  // one block per CU: 9 more tiles with d in LDS (144 KiB)
-            return burst_launches(L.b4 / L.tile4, (L.e4 - 1) / L.tile4 + 1, L.grid, kBurstTiles + kBurstEpiLdsTilesWide,
-                                  nl, L.variant & kVariantAnyOrder, [&](int nb, int64_t t0, int64_t t_end, uint32_t flags) {
-                                      hipExtLaunchKernelGGL(
-                                          (fedavg_tiles_epi_burst_f32x4<OP, FIN, ACC_IN, EPI, kBurstTiles,
-                                                                        kBurstEpiLdsTilesWide>),
-                                          dim3(nb), dim3(kBlock), 0, s, nullptr, nullptr, flags, L.tab, L.k, L.tstride4,
-                                          ai, o, L.b4, L.e4, L.fin_val, E, t0, t_end);
-                                  });
-        if (!(L.variant & kVariantRegisterTiles))  // default: 4 more tiles per block with d held in LDS
-            return burst_launches(L.b4 / L.tile4, (L.e4 - 1) / L.tile4 + 1, L.grid, kBurstTiles + kBurstLdsTiles, nl,
-                                  L.variant & kVariantAnyOrder, [&](int nb, int64_t t0, int64_t t_end, uint32_t flags) {
-                                      hipExtLaunchKernelGGL(
-                                          (fedavg_tiles_epi_burst_f32x4<OP, FIN, ACC_IN, EPI, kBurstTiles, kBurstLdsTiles>),
-                                          dim3(nb), dim3(kBlock), 0, s, nullptr, nullptr, flags, L.tab, L.k, L.tstride4,
-                                          ai, o, L.b4, L.e4, L.fin_val, E, t0, t_end);
-                                  });
-        return burst_launches(L.b4 / L.tile4, (L.e4 - 1) / L.tile4 + 1, L.grid, kBurstTiles, nl,
-                              L.variant & kVariantAnyOrder, [&](int nb, int64_t t0, int64_t t_end, uint32_t flags) {
-                                  hipExtLaunchKernelGGL(
-                                      (fedavg_tiles_epi_burst_f32x4<OP, FIN, ACC_IN, EPI, kBurstTiles>), dim3(nb),
-                                      dim3(kBlock), 0, s, nullptr, nullptr, flags, L.tab, L.k, L.tstride4, ai, o, L.b4,
-                                      L.e4, L.fin_val, E, t0, t_end);
-                              });
+    if constexpr (kAB || !ACC_IN) {
+        if (!(L.variant & (kVariantTileStores | kVariantEpiPrefetch))) {  // burst: one launch per grid x TPB tiles
+            if constexpr (kAB) {
+                hipError_t ab_err = hipSuccess;
+                if ((L.variant & kVariantWideLds) &&
+                    epi_loop_ab<OP, FIN, ACC_IN, EPI, kBurstEpiLdsTilesWide>(L, E, s, nl, &ab_err))
+                    return ab_err;
+                if (!(L.variant & (kVariantWideLds | kVariantRegisterTiles)) &&
+                    epi_loop_ab<OP, FIN, ACC_IN, EPI, kBurstLdsTiles>(L, E, s, nl, &ab_err))
+                    return ab_err;
+            }
+            if (L.variant & kVariantWideLds)  // one block per CU: 9 more tiles with d in LDS (144 KiB)
+                return burst_launches(L.b4 / L.tile4, (L.e4 - 1) / L.tile4 + 1, L.grid,
+                                      kBurstTiles + kBurstEpiLdsTilesWide, nl, L.variant & kVariantAnyOrder,
+                                      [&](int nb, int64_t t0, int64_t t_end, uint32_t flags) {
+                                          hipExtLaunchKernelGGL(
+                                              (fedavg_tiles_epi_burst_f32x4<OP, FIN, ACC_IN, EPI, kBurstTiles,
+                                                                            kBurstEpiLdsTilesWide>),
+                                              dim3(nb), dim3(kBlock), 0, s, nullptr, nullptr, flags, L.tab, L.k,
+                                              L.tstride4, ai, o, L.b4, L.e4, L.fin_val, E, t0, t_end);
+                                      });
+            if (!kAB || !(L.variant & kVariantRegisterTiles))  // default: 4 more tiles per block with d held in LDS
+                return burst_launches(L.b4 / L.tile4, (L.e4 - 1) / L.tile4 + 1, L.grid, kBurstTiles + kBurstLdsTiles,
+                                      nl, L.variant & kVariantAnyOrder,
+                                      [&](int nb, int64_t t0, int64_t t_end, uint32_t flags) {
+                                          hipExtLaunchKernelGGL(
+                                              (fedavg_tiles_epi_burst_f32x4<OP, FIN, ACC_IN, EPI, kBurstTiles,
+                                                                            kBurstLdsTiles>),
+                                              dim3(nb), dim3(kBlock), 0, s, nullptr, nullptr, flags, L.tab, L.k,
+                                              L.tstride4, ai, o, L.b4, L.e4, L.fin_val, E, t0, t_end);
+                                      });
+            if constexpr (kAB)
+                return burst_launches(L.b4 / L.tile4, (L.e4 - 1) / L.tile4 + 1, L.grid, kBurstTiles, nl,
+                                      L.variant & kVariantAnyOrder, [&](int nb, int64_t t0, int64_t t_end, uint32_t flags) {
+                                          hipExtLaunchKernelGGL(
+                                              (fedavg_tiles_epi_burst_f32x4<OP, FIN, ACC_IN, EPI, kBurstTiles>), dim3(nb),
+                                              dim3(kBlock), 0, s, nullptr, nullptr, flags, L.tab, L.k, L.tstride4, ai, o,
+                                              L.b4, L.e4, L.fin_val, E, t0, t_end);
+                                      });
+        }
     }
-    if (L.variant & kVariantEpiPrefetch) {
-        hipLaunchKernelGGL((fedavg_tiles_epi_f32x4<OP, FIN, ACC_IN, EPI, true>), dim3(L.grid), dim3(kBlock), 0, s, L.tab,
-                           L.k, L.tstride4, ai, o, L.b4, L.e4, L.fin_val, E);
+    if (kAB && !(L.variant & kVariantEpiPrefetch)) {
+        if constexpr (kAB)
+            hipLaunchKernelGGL((fedavg_tiles_epi_f32x4<OP, FIN, ACC_IN, EPI, false>), dim3(L.grid), dim3(kBlock), 0, s,
+                               L.tab, L.k, L.tstride4, ai, o, L.b4, L.e4, L.fin_val, E);
     } else {
-        hipLaunchKernelGGL((fedavg_tiles_epi_f32x4<OP, FIN, ACC_IN, EPI, false>), dim3(L.grid), dim3(kBlock), 0, s, L.tab,
+        hipLaunchKernelGGL((fedavg_tiles_epi_f32x4<OP, FIN, ACC_IN, EPI, true>), dim3(L.grid), dim3(kBlock), 0, s, L.tab,
                            L.k, L.tstride4, ai, o, L.b4, L.e4, L.fin_val, E);
     }
     if (nl) ++*nl;
@@ -603,9 +694,12 @@ inline hipError_t launch_epi_a(const TileLaunch& L, const EpiParams& E, hipStrea
     }
 }
 
+// one (mode, finalisation) pair's entry; product builds carry no chained-sum forms here (launch_epi_step has the
+// server step's, fedavg_internal.h epi_direct)
 template <int OP, int FIN>
 inline hipError_t launch_epi_f(const TileLaunch& L, const EpiParams& E, hipStream_t s, uint64_t* nl) {
-    return L.acc_in ? launch_epi_a<OP, FIN, true>(L, E, s, nl) : launch_epi_a<OP, FIN, false>(L, E, s, nl);
+    if constexpr (kAB) return L.acc_in ? launch_epi_a<OP, FIN, true>(L, E, s, nl) : launch_epi_a<OP, FIN, false>(L, E, s, nl);
+    return L.acc_in ? hipErrorNotSupported : launch_epi_a<OP, FIN, false>(L, E, s, nl);
 }
 
 }  // namespace fedavg

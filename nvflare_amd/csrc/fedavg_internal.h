@@ -19,6 +19,16 @@ constexpr int kDefaultTile = 4096;      // elements per client segment per tile 
 constexpr int kDefaultBlocksPerCu = 2;  // 8 waves per CU (per-tile-store, epilogue, fp64 and 16-bit kernels)
 constexpr int kDefaultUnroll = 4;       // clients whose loads are in flight together per lane
 
+// The product library carries only the kernel forms the launchers route to (round 5); the A/B
+// forms -- other tile widths and unrolls, temporal loads / stores, register-only burst forms, the round-3 client loop,
+// client-loop shapes, the per-tile forms of the 16-bit and fp64 kernels -- are compiled only with -DFEDAVG_AB
+// (tools/build_rev_lib.py), where fedavg_set_variant / set_launch / set_tile accept them.
+#if defined(FEDAVG_AB)
+constexpr bool kAB = true;
+#else
+constexpr bool kAB = false;
+#endif
+
 // variant bits (fedavg_set_variant).  Default (0): the plain aggregation runs fedavg_tiles_burst_f32x4.
 constexpr int kVariantTemporalLoads = 1;   // per-tile-store kernel with temporal (cached) client loads
 constexpr int kVariantTemporalStores = 2;  // per-tile-store kernel with temporal result stores
@@ -37,6 +47,11 @@ constexpr int kVariantWideLds = 64;       // inside TileLaunch: plain burst kern
                                            // (32 clients 88.4 -> 88.9 %, 64: 89.7 -> 89.9 %, profiles/r02/ab/wide_lds/)
 constexpr int kVariantLoopShift = 9;       // bits 9-11: A/B shapes of the burst kernels' client loop
                                            // (fedavg_epi.h launch_epi_loop_ab, fedavg_tiles.h launch_burst)
+constexpr int kVariantFew = 1 << 12;      // inside TileLaunch: the few-client burst kernel (fedavg_tiles.h
+                                           // fedavg_tiles_few_f32x4), set by run_tiles for 1-2 reads, no chained sum
+// public variant bits a product build accepts (fedavg_set_variant): the fused per-tile pipelined form (2), burst
+// launches without the barrier bit (16), the 4-LDS-tile form on one-block-per-CU grids (64) -- each a routed form
+constexpr int kVariantProductMask = kVariantEpiPrefetch | kVariantAnyOrder | kVariantWideLds;
 // epilogue template value: the optimizer kind | kEpiTorchSqrt when the step's sqrt is torch CPU's restated AVX-512
 // vsSqrt (EpiParams.torch_sqrt == FEDAVG_SQRT_TORCH_AVX512; fedavg_arith.h sqrt_torch_cpu) | kEpiTorchSqrtAmd for the
 // AMD hosts' path (FEDAVG_SQRT_TORCH_AMD; sqrt_mkl_rsqrtps) -- a compile-time choice, so the correctly rounded path
@@ -146,9 +161,11 @@ inline hipError_t burst_launches(int64_t t_first, int64_t t_stop, int grid, int 
 hipError_t launch_tiles_f32x4_numpy(const TileLaunch& L, hipStream_t s, uint64_t* launch_count);
 hipError_t launch_tiles_f32x4_torch(const TileLaunch& L, hipStream_t s, uint64_t* launch_count);
 hipError_t launch_tiles_f32x4_unweighted(const TileLaunch& L, hipStream_t s, uint64_t* launch_count);
-// fused kernels, one entry per (mode, finalisation): fedavg_epi_inst.hip compiled nine times
+// fused kernels, one entry per (mode, finalisation): fedavg_epi_inst.hip compiled once per pair (nine A/B builds, the
+// five of epi_direct in product builds, plus launch_epi_step there: the server step alone, no clients, FIN_NONE)
 #define FEDAVG_EPI_DECL(name) \
     hipError_t name(const TileLaunch& L, const EpiParams& E, hipStream_t s, uint64_t* nl);
+FEDAVG_EPI_DECL(launch_epi_step)
 FEDAVG_EPI_DECL(launch_epi_numpy_none)
 FEDAVG_EPI_DECL(launch_epi_numpy_scale)
 FEDAVG_EPI_DECL(launch_epi_numpy_div)
@@ -159,6 +176,38 @@ FEDAVG_EPI_DECL(launch_epi_unweighted_none)
 FEDAVG_EPI_DECL(launch_epi_unweighted_scale)
 FEDAVG_EPI_DECL(launch_epi_unweighted_div)
 #undef FEDAVG_EPI_DECL
+// Whether a fused launch (clients + epilogue in one kernel) is in this build.  Product builds carry, per optimizer kind
+// and sqrt, the forms without a chained sum for the (mode, finalisation) pairs the drop-in's callers produce -- numpy
+// * SCALE, torch * DIV, torch device tensors * SCALE (FEDAVG_FIN_RECIP), unweighted * SCALE | DIV -- and the server step
+// alone (no clients, the aggregate as the chained sum, FIN_NONE: the FedOpt generator's step, fedopt.py:157-182).
+// Anything else (a chained sum with clients, more than 128 clients, numpy with FIN_DIV, FIN_NONE with clients) runs as
+// the plain aggregation into a scratch followed by that server step (fedavg_capi.cpp): the same per-element sequence.
+inline bool epi_direct(int op, int fin, int k, bool acc_in) {
+    if (kAB) return true;
+    if (acc_in || k == 0) return acc_in && k == 0 && fin == FEDAVG_FIN_NONE;
+    if (k > kMaxRowsPerLaunch) return false;
+    if (fin == FEDAVG_FIN_SCALE) return true;
+    return fin == FEDAVG_FIN_DIV && op != FEDAVG_OP_NUMPY;
+}
+// the few-client forms' geometry: blocks per CU, register-held tiles R, LDS-held tiles L, LDS tiles per load group G
+struct FewForm {
+    int bpc, r, l, g;
+};
+// the product's form per read count (profiles/r05: A/B sweep of the forms below, interleaved in one process)
+constexpr FewForm kFewDefault[3] = {{0, 0, 0, 0}, {2, 8, 4, 4}, {2, 4, 4, 2}};
+// A/B builds: launch variant bits 9-11 pick one of these per read count (1-6; 0 = the default)
+constexpr FewForm kFewAB[2][6] = {
+    {{2, 8, 4, 4}, {2, 8, 4, 2}, {1, 8, 10, 5}, {2, 8, 0, 1}, {2, 4, 4, 4}, {1, 8, 8, 4}},
+    {{2, 4, 4, 2}, {2, 4, 4, 4}, {1, 4, 10, 2}, {1, 6, 9, 3}, {2, 6, 4, 2}, {2, 4, 0, 1}}};
+
+// the few-client form of a launch with `reads` (1 or 2) client reads
+inline FewForm few_form(int reads, int variant) {
+    if (kAB) {
+        const int ix = (variant >> kVariantLoopShift) & 7;
+        if (ix >= 1 && ix <= 6) return kFewAB[reads - 1][ix - 1];
+    }
+    return kFewDefault[reads];
+}
 // whether launch_tiles_f32x4 takes the burst kernel for this geometry (it then wants one block per CU at
 // K >= kBurstOneBlockMinK clients, two below)
 bool tiles_use_burst(int64_t tile4, int unroll, int variant);

@@ -35,10 +35,18 @@ namespace fedavg {
 // ---------------------------------------------------------------------------------------------
 // generic scalar kernel: any (Tin, Tacc) pair, contiguous rows, any alignment (ragged tails, fp64, ints)
 // ---------------------------------------------------------------------------------------------
-template <typename Tin, typename Tacc, int OP, int FIN, bool ACC_IN>
+// The step and the finalisation are launch arguments here (round 5: one instantiation per (Tin, Tacc, ACC_IN) instead
+// of nine -- this is the path for odd dtypes, unaligned rows and ragged tails, not the streaming one); the per-element
+// sequence is fedavg_arith.h's first_op / step_op / fin_op for that op and fin.
+template <int OP, typename Tacc>
+__device__ __forceinline__ Tacc step_any(const Tacc acc, const Tacc v, const Tacc w) {
+    return step_op<OP>(acc, v, w);
+}
+
+template <typename Tin, typename Tacc, bool ACC_IN>
 __global__ void __launch_bounds__(kBlock) fedavg_rows_generic(const RowTableGeneric tab, const int K,
                                                                const Tacc* acc_in, Tacc* out, const int64_t n,
-                                                               const double fin_val_d) {
+                                                               const double fin_val_d, const int op, const int fin) {
     const Tacc fin_val = (Tacc)fin_val_d;
     const int64_t stride = (int64_t)gridDim.x * kBlock;
     for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
@@ -47,14 +55,21 @@ __global__ void __launch_bounds__(kBlock) fedavg_rows_generic(const RowTableGene
         if constexpr (ACC_IN) {
             acc = acc_in[i];
         } else {
-            acc = first_op<OP>((Tacc)(static_cast<const Tin*>(tab.rows[0])[i]), (Tacc)tab.w[0]);
+            const Tacc v = (Tacc)(static_cast<const Tin*>(tab.rows[0])[i]);
+            acc = op == FEDAVG_OP_UNWEIGHTED ? first_op<FEDAVG_OP_UNWEIGHTED>(v, (Tacc)tab.w[0])
+                                             : first_op<FEDAVG_OP_NUMPY>(v, (Tacc)tab.w[0]);
             k = 1;
         }
         for (; k < K; ++k) {
             const Tacc v = (Tacc)(static_cast<const Tin*>(tab.rows[k])[i]);
-            acc = step_op<OP>(acc, v, (Tacc)tab.w[k]);
+            const Tacc w = (Tacc)tab.w[k];
+            acc = op == FEDAVG_OP_TORCH        ? step_any<FEDAVG_OP_TORCH>(acc, v, w)
+                  : op == FEDAVG_OP_UNWEIGHTED ? step_any<FEDAVG_OP_UNWEIGHTED>(acc, v, w)
+                                               : step_any<FEDAVG_OP_NUMPY>(acc, v, w);
         }
-        out[i] = fin_op<FIN>(acc, fin_val);
+        out[i] = fin == FEDAVG_FIN_SCALE ? fin_op<FEDAVG_FIN_SCALE>(acc, fin_val)
+                 : fin == FEDAVG_FIN_DIV ? fin_op<FEDAVG_FIN_DIV>(acc, fin_val)
+                                         : acc;
     }
 }
 
@@ -290,52 +305,37 @@ hipError_t launch_tiles_f32x4(const TileLaunch& L, hipStream_t s, uint64_t* nl) 
 
 hipError_t launch_tiles_epi_f32x4(const TileLaunch& L, const EpiParams& E, hipStream_t s, uint64_t* nl) {
     using Fn = hipError_t (*)(const TileLaunch&, const EpiParams&, hipStream_t, uint64_t*);
+    if (!epi_direct(L.op, L.fin, L.k, L.acc_in != nullptr)) return hipErrorNotSupported;  // fedavg_capi.cpp splits it
+#if defined(FEDAVG_AB)
     static constexpr Fn kFns[3][3] = {  // [mode][finalisation]: numpy (and any other op), torch, unweighted
         {launch_epi_numpy_none, launch_epi_numpy_scale, launch_epi_numpy_div},
         {launch_epi_torch_none, launch_epi_torch_scale, launch_epi_torch_div},
         {launch_epi_unweighted_none, launch_epi_unweighted_scale, launch_epi_unweighted_div}};
+#else
+    if (L.acc_in) return launch_epi_step(L, E, s, nl);  // the server step alone (no clients, FIN_NONE)
+    static constexpr Fn kFns[3][3] = {  // the product's (mode, finalisation) pairs (epi_direct)
+        {nullptr, launch_epi_numpy_scale, nullptr},
+        {nullptr, launch_epi_torch_scale, launch_epi_torch_div},
+        {nullptr, launch_epi_unweighted_scale, launch_epi_unweighted_div}};
+#endif
     const int o = L.op == FEDAVG_OP_TORCH ? 1 : (L.op == FEDAVG_OP_UNWEIGHTED ? 2 : 0);
     const int f = L.fin == FEDAVG_FIN_SCALE ? 1 : (L.fin == FEDAVG_FIN_DIV ? 2 : 0);
-    return kFns[o][f](L, E, s, nl);
-}
-
-template <typename Tin, typename Tacc, int OP, int FIN>
-static hipError_t launch_generic_f(const RowTableGeneric& tab, int K, const void* acc_in, void* out, int64_t n,
-                                   double fin_val, int grid, hipStream_t s) {
-    if (acc_in) {
-        hipLaunchKernelGGL((fedavg_rows_generic<Tin, Tacc, OP, FIN, true>), dim3(grid), dim3(kBlock), 0, s, tab, K,
-                           static_cast<const Tacc*>(acc_in), static_cast<Tacc*>(out), n, fin_val);
-    } else {
-        hipLaunchKernelGGL((fedavg_rows_generic<Tin, Tacc, OP, FIN, false>), dim3(grid), dim3(kBlock), 0, s, tab, K,
-                           static_cast<const Tacc*>(acc_in), static_cast<Tacc*>(out), n, fin_val);
-    }
-    return hipGetLastError();
-}
-
-template <typename Tin, typename Tacc, int OP>
-static hipError_t launch_generic_o(const RowTableGeneric& tab, int K, const void* acc_in, void* out, int64_t n, int fin,
-                                   double fin_val, int grid, hipStream_t s) {
-    switch (fin) {
-        case FEDAVG_FIN_SCALE:
-            return launch_generic_f<Tin, Tacc, OP, FEDAVG_FIN_SCALE>(tab, K, acc_in, out, n, fin_val, grid, s);
-        case FEDAVG_FIN_DIV:
-            return launch_generic_f<Tin, Tacc, OP, FEDAVG_FIN_DIV>(tab, K, acc_in, out, n, fin_val, grid, s);
-        default:
-            return launch_generic_f<Tin, Tacc, OP, FEDAVG_FIN_NONE>(tab, K, acc_in, out, n, fin_val, grid, s);
-    }
+    return kFns[o][f] ? kFns[o][f](L, E, s, nl) : hipErrorNotSupported;
 }
 
 template <typename Tin, typename Tacc>
 static hipError_t launch_generic_t(const RowTableGeneric& tab, int K, const void* acc_in, void* out, int64_t n, int op,
                                    int fin, double fin_val, int grid, hipStream_t s) {
-    switch (op) {
-        case FEDAVG_OP_TORCH:
-            return launch_generic_o<Tin, Tacc, FEDAVG_OP_TORCH>(tab, K, acc_in, out, n, fin, fin_val, grid, s);
-        case FEDAVG_OP_UNWEIGHTED:
-            return launch_generic_o<Tin, Tacc, FEDAVG_OP_UNWEIGHTED>(tab, K, acc_in, out, n, fin, fin_val, grid, s);
-        default:
-            return launch_generic_o<Tin, Tacc, FEDAVG_OP_NUMPY>(tab, K, acc_in, out, n, fin, fin_val, grid, s);
+    if (fin != FEDAVG_FIN_SCALE && fin != FEDAVG_FIN_DIV) fin = FEDAVG_FIN_NONE;
+    if (op != FEDAVG_OP_TORCH && op != FEDAVG_OP_UNWEIGHTED) op = FEDAVG_OP_NUMPY;
+    if (acc_in) {
+        hipLaunchKernelGGL((fedavg_rows_generic<Tin, Tacc, true>), dim3(grid), dim3(kBlock), 0, s, tab, K,
+                           static_cast<const Tacc*>(acc_in), static_cast<Tacc*>(out), n, fin_val, op, fin);
+    } else {
+        hipLaunchKernelGGL((fedavg_rows_generic<Tin, Tacc, false>), dim3(grid), dim3(kBlock), 0, s, tab, K,
+                           static_cast<const Tacc*>(acc_in), static_cast<Tacc*>(out), n, fin_val, op, fin);
     }
+    return hipGetLastError();
 }
 
 template <int OP, int FIN>
@@ -397,7 +397,7 @@ static hipError_t launch_t64_f(const RowTableGeneric& tab, int K, int64_t ts2, c
     const f64x2* ai = static_cast<const f64x2*>(acc_in);
     f64x2* o = static_cast<f64x2*>(out);
     constexpr int64_t T2 = (int64_t)kCpl64 * kBlock;
-    if (burst == 2) {  // default: kBurstTiles64 in registers + kBurstLdsTiles64 in LDS per block and launch
+    if (burst == 2 || !kAB) {  // default: kBurstTiles64 in registers + kBurstLdsTiles64 in LDS per block and launch
         return burst_launches(b2 / T2, (e2 - 1) / T2 + 1, grid, kBurstTiles64 + kBurstLdsTiles64, nl, false,
                               [&](int nb, int64_t t0, int64_t t_end, uint32_t) {
             if (acc_in)
@@ -408,25 +408,29 @@ static hipError_t launch_t64_f(const RowTableGeneric& tab, int K, int64_t ts2, c
                                    dim3(kBlock), 0, s, tab, K, ts2, ai, o, b2, e2, fin_val, t0, t_end);
         });
     }
-    if (burst) {
-        return burst_launches(b2 / T2, (e2 - 1) / T2 + 1, grid, kBurstTiles64, nl, false, [&](int nb, int64_t t0, int64_t t_end, uint32_t) {
-            if (acc_in)
-                hipLaunchKernelGGL((fedavg_tiles_f64x2_burst<OP, FIN, true, kBurstTiles64>), dim3(nb), dim3(kBlock), 0, s,
-                                   tab, K, ts2, ai, o, b2, e2, fin_val, t0, t_end);
-            else
-                hipLaunchKernelGGL((fedavg_tiles_f64x2_burst<OP, FIN, false, kBurstTiles64>), dim3(nb), dim3(kBlock), 0,
-                                   s, tab, K, ts2, ai, o, b2, e2, fin_val, t0, t_end);
-        });
-    }
-    if (acc_in) {
-        hipLaunchKernelGGL((fedavg_tiles_f64x2<OP, FIN, true>), dim3(grid), dim3(kBlock), 0, s, tab, K, ts2, ai, o, b2, e2,
-                           fin_val);
+    if constexpr (kAB) {  // A/B builds: the register-only burst form (variant bit 5) and the per-tile form (bit 3)
+        if (burst) {
+            return burst_launches(b2 / T2, (e2 - 1) / T2 + 1, grid, kBurstTiles64, nl, false, [&](int nb, int64_t t0, int64_t t_end, uint32_t) {
+                if (acc_in)
+                    hipLaunchKernelGGL((fedavg_tiles_f64x2_burst<OP, FIN, true, kBurstTiles64>), dim3(nb), dim3(kBlock), 0, s,
+                                       tab, K, ts2, ai, o, b2, e2, fin_val, t0, t_end);
+                else
+                    hipLaunchKernelGGL((fedavg_tiles_f64x2_burst<OP, FIN, false, kBurstTiles64>), dim3(nb), dim3(kBlock), 0,
+                                       s, tab, K, ts2, ai, o, b2, e2, fin_val, t0, t_end);
+            });
+        }
+        if (acc_in) {
+            hipLaunchKernelGGL((fedavg_tiles_f64x2<OP, FIN, true>), dim3(grid), dim3(kBlock), 0, s, tab, K, ts2, ai, o, b2, e2,
+                               fin_val);
+        } else {
+            hipLaunchKernelGGL((fedavg_tiles_f64x2<OP, FIN, false>), dim3(grid), dim3(kBlock), 0, s, tab, K, ts2, ai, o, b2,
+                               e2, fin_val);
+        }
+        if (nl) ++*nl;
+        return hipGetLastError();
     } else {
-        hipLaunchKernelGGL((fedavg_tiles_f64x2<OP, FIN, false>), dim3(grid), dim3(kBlock), 0, s, tab, K, ts2, ai, o, b2,
-                           e2, fin_val);
+        return hipErrorInvalidValue;
     }
-    if (nl) ++*nl;
-    return hipGetLastError();
 }
 
 template <int OP>

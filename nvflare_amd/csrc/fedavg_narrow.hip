@@ -372,7 +372,7 @@ static hipError_t launch_t16_a(const RowTableNarrow& tab, int K, int64_t tstride
     const u32x4* ai = static_cast<const u32x4*>(acc_in);
     u32x4* o = static_cast<u32x4*>(out);
     constexpr int64_t T8 = (int64_t)kCpl16 * kBlock;
-    if (burst == 2) {  // default: kBurstTiles in registers + kBurstLdsTiles16 in LDS per block and launch
+    if (burst == 2 || !kAB) {  // default: kBurstTiles in registers + kBurstLdsTiles16 in LDS per block and launch
         // client groups of 4 under kNarrowUnroll4MaxK clients, of FEDAVG_NARROW_UNROLL (6) from there on
         const bool u4 = K < kNarrowUnroll4MaxK;
         return burst_launches(b8 / T8, (e8 - 1) / T8 + 1, grid, kBurstTiles + kBurstLdsTiles16, nl, false,
@@ -387,25 +387,29 @@ static hipError_t launch_t16_a(const RowTableNarrow& tab, int K, int64_t tstride
 #undef FEDAVG_T16_BURST
         });
     }
-    if (burst) {
-        return burst_launches(b8 / T8, (e8 - 1) / T8 + 1, grid, kBurstTiles, nl, false, [&](int nb, int64_t t0, int64_t t_end, uint32_t) {
-            if (acc_in)
-                hipLaunchKernelGGL((fedavg_tiles_narrow_burst<FMT, OP, FIN, true, kBurstTiles>), dim3(nb), dim3(kBlock), 0,
-                                   s, tab, K, tstride8, ai, o, b8, e8, fv, t0, t_end);
-            else
-                hipLaunchKernelGGL((fedavg_tiles_narrow_burst<FMT, OP, FIN, false, kBurstTiles>), dim3(nb), dim3(kBlock),
-                                   0, s, tab, K, tstride8, ai, o, b8, e8, fv, t0, t_end);
-        });
-    }
-    if (acc_in) {
-        hipLaunchKernelGGL((fedavg_tiles_narrow<FMT, OP, FIN, true>), dim3(grid), dim3(kBlock), 0, s, tab, K, tstride8, ai,
-                           o, b8, e8, fv);
+    if constexpr (kAB) {  // A/B builds: the register-only burst form (variant bit 5) and the per-tile form (bit 3)
+        if (burst) {
+            return burst_launches(b8 / T8, (e8 - 1) / T8 + 1, grid, kBurstTiles, nl, false, [&](int nb, int64_t t0, int64_t t_end, uint32_t) {
+                if (acc_in)
+                    hipLaunchKernelGGL((fedavg_tiles_narrow_burst<FMT, OP, FIN, true, kBurstTiles>), dim3(nb), dim3(kBlock), 0,
+                                       s, tab, K, tstride8, ai, o, b8, e8, fv, t0, t_end);
+                else
+                    hipLaunchKernelGGL((fedavg_tiles_narrow_burst<FMT, OP, FIN, false, kBurstTiles>), dim3(nb), dim3(kBlock),
+                                       0, s, tab, K, tstride8, ai, o, b8, e8, fv, t0, t_end);
+            });
+        }
+        if (acc_in) {
+            hipLaunchKernelGGL((fedavg_tiles_narrow<FMT, OP, FIN, true>), dim3(grid), dim3(kBlock), 0, s, tab, K, tstride8, ai,
+                               o, b8, e8, fv);
+        } else {
+            hipLaunchKernelGGL((fedavg_tiles_narrow<FMT, OP, FIN, false>), dim3(grid), dim3(kBlock), 0, s, tab, K, tstride8,
+                               ai, o, b8, e8, fv);
+        }
+        if (nl) ++*nl;
+        return hipGetLastError();
     } else {
-        hipLaunchKernelGGL((fedavg_tiles_narrow<FMT, OP, FIN, false>), dim3(grid), dim3(kBlock), 0, s, tab, K, tstride8,
-                           ai, o, b8, e8, fv);
+        return hipErrorInvalidValue;
     }
-    if (nl) ++*nl;
-    return hipGetLastError();
 }
 
 template <int FMT, int OP>

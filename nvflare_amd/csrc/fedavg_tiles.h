@@ -7,8 +7,9 @@
 
 namespace fedavg {
 
-constexpr int kVariantRuntimeK = 128;  // burst kernels: round 3's runtime-K tile loop (tile_sum GROUPED) instead of the
-                                       // built-in client count (1-6) or remainder (7+) forms (tile_sum_kc / _rem, round 4)
+constexpr int kVariantRuntimeK = 128;  // A/B: burst kernels on round 3's runtime-K tile loop (tile_sum GROUPED = 2, the
+                                       // last group re-loading its last client) instead of the built-in client count
+                                       // (3-6) or remainder (7+) forms (tile_sum_kc / _rem, round 4)
 
 // ---------------------------------------------------------------------------------------------
 // THE HOT KERNEL.  Global f32x4 index range [b4, e4); tiles t = b4/T4 .. (e4-1)/T4 are dealt to blocks
@@ -62,10 +63,12 @@ __global__ void __launch_bounds__(kBlock) fedavg_tiles_f32x4(const RowTableF32 t
 #pragma unroll
             for (int c = 0; c < CPL; ++c) acc[c] = step4<OP>(acc[c], load4<NTL>(r + c * kBlock), tab.w[k]);
         }
+        f32x4 r[CPL];
+        fin_tile<FIN, CPL>(r, acc, fc);
 #pragma unroll
         for (int c = 0; c < CPL; ++c) {
             const int64_t i = col + c * kBlock;
-            if (i >= b4 && i < e4) store4<NTS>(out + i, fin4c<FIN>(acc[c], fc));
+            if (i >= b4 && i < e4) store4<NTS>(out + i, r[c]);
         }
     }
 }
@@ -188,7 +191,8 @@ __device__ __forceinline__ void tile_sum_rem(f32x4 (&acc)[CPL], const RowTableF3
 }
 
 // one tile's sum: KC > 0 -- the client count built in (tile_sum_kc); KC = -1 - REM -- the runtime count with its
-// remainder mod 4 built in (tile_sum_rem); KC = 0 -- fedavg_arith.h tile_sum's GROUPED form (variant bit 7, for A/Bs)
+// remainder mod 4 built in (tile_sum_rem); KC = 0 -- fedavg_arith.h tile_sum's GROUPED = 2 form, round 3's loop with
+// its repeated loads (A/B builds only: variant bit 7, and every launch of a non-default tile width or unroll)
 // SHAPE (remainder forms): -1 -- tile_sum_rem's default; A/B only (launch variant bits 9-11): 1 -- tile_sum's GROUPED
 // loop with round 3's repeats; 0, 2-4 -- tile_sum_rem with that shape
 template <int OP, bool ACC_IN, int UNROLL, int CPL, int KC, int SHAPE = -1>
@@ -200,8 +204,8 @@ __device__ __forceinline__ void tile_sum_any(f32x4 (&acc)[CPL], const RowTableF3
         tile_sum<OP, ACC_IN, UNROLL, CPL, 2>(acc, tab, K, off, col, acc_in, b4, e4);
     } else if constexpr (KC < 0) {
         tile_sum_rem<OP, ACC_IN, -1 - KC, CPL, SHAPE>(acc, tab, K, off, col, acc_in, b4, e4);
-    } else {
-        tile_sum<OP, ACC_IN, UNROLL, CPL, true>(acc, tab, K, off, col, acc_in, b4, e4);
+    } else {  // A/B builds: round 3's loop (variant bit 7, and the non-default tile widths and unrolls)
+        tile_sum<OP, ACC_IN, UNROLL, CPL, 2>(acc, tab, K, off, col, acc_in, b4, e4);
     }
 }
 
@@ -234,8 +238,7 @@ fedavg_tiles_burst_f32x4(const RowTableF32 tab, const int K, const int64_t tstri
             f32x4 acc[CPL];
             tile_sum_any<OP, ACC_IN, UNROLL, CPL, KC, SHAPE>(acc, tab, K, t * tstride4 + threadIdx.x, t * T4 + threadIdx.x,
                                                       acc_in, b4, e4);
-#pragma unroll
-            for (int c = 0; c < CPL; ++c) res[m][c] = fin4c<FIN>(acc[c], fc);
+            fin_tile<FIN, CPL>(res[m], acc, fc);
         }
     }
     // the LDS-held tiles in a rolled loop: one more copy of the tile body, not TPB_LDS of them
@@ -243,11 +246,12 @@ fedavg_tiles_burst_f32x4(const RowTableF32 tab, const int K, const int64_t tstri
     for (int m = TPB; m < TPB + TPB_LDS; ++m) {
         const int64_t t = t0 + blockIdx.x + (int64_t)m * gridDim.x;
         if (t < t_end) {
-            f32x4 acc[CPL];
+            f32x4 acc[CPL], r[CPL];
             tile_sum_any<OP, ACC_IN, UNROLL, CPL, KC, SHAPE>(acc, tab, K, t * tstride4 + threadIdx.x, t * T4 + threadIdx.x,
                                                       acc_in, b4, e4);
+            fin_tile<FIN, CPL>(r, acc, fc);
 #pragma unroll
-            for (int c = 0; c < CPL; ++c) staged[((m - TPB) * CPL + c) * kBlock + threadIdx.x] = fin4c<FIN>(acc[c], fc);
+            for (int c = 0; c < CPL; ++c) staged[((m - TPB) * CPL + c) * kBlock + threadIdx.x] = r[c];
         }
     }
 #pragma unroll 1
@@ -276,8 +280,136 @@ fedavg_tiles_burst_f32x4(const RowTableF32 tab, const int K, const int64_t tstri
 }
 
 // ---------------------------------------------------------------------------------------------
+// FEW-CLIENT burst form (round 5): launches with 1 or 2 row reads and no chained sum.  With one or
+// two reads per result the burst kernel above spends its launch in round trips: each register-held tile's loads sit
+// behind a guard (`t < t_end`) and the finalisation's rare-case branches, basic-block boundaries the scheduler does
+// not hoist loads across, so a wave has one tile's 4-8 KiB in flight where HBM wants ~64 KiB per CU.  Here every load
+// is unconditional (a slot past the launch's last tile re-reads that tile; only real tiles are stored), the
+// finalisation has one rare-case branch per tile (fin_tile), and the R register-held tiles' loads all go out first:
+//   1. R tiles' loads (KC x 4 float4 per lane each) issued together -- in flight while step 2 runs;
+//   2. the L LDS-held tiles in groups of G (a group's loads together), summed, finalised, written to LDS;
+//   3. the R register-held tiles summed and finalised;
+//   4. every result stored: the LDS-held tiles', then the register-held tiles' -- the launch's write burst.
+// Per-element sequence as tile_sum_kc's (first4, then step4 for client 1), so the bits are the burst kernel's.
+// ---------------------------------------------------------------------------------------------
+template <int OP, int FIN, int KC, int R, int L, int G>
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, 2)))
+fedavg_tiles_few_f32x4(const RowTableF32 tab, const int64_t tstride4, f32x4* out, const int64_t b4, const int64_t e4,
+                       const float fin_val, const int64_t t0, const int64_t t_end) {
+    static_assert(KC == 1 || KC == 2, "one or two row reads");
+    static_assert(L % G == 0 || L == 0, "whole LDS groups");
+    constexpr int CPL = 4;
+    constexpr int64_t T4 = (int64_t)CPL * kBlock;
+    const FinConst fc = fin_const<FIN>(fin_val);
+    __shared__ f32x4 staged[L > 0 ? L * CPL * kBlock : 1];
+    const int64_t t_first = t0 + blockIdx.x;
+    auto tile_of = [&](const int m) __attribute__((always_inline)) {
+        const int64_t t = t_first + (int64_t)m * gridDim.x;
+        return t < t_end ? t : t_end - 1;  // unconditional loads: a slot past the end re-reads the last tile
+    };
+    auto sum = [&](f32x4 (&acc)[CPL], const f32x4 (&v)[KC][CPL]) __attribute__((always_inline)) {
+#pragma unroll
+        for (int c = 0; c < CPL; ++c) {
+            acc[c] = first4<OP>(v[0][c], tab.w[0]);
+            if constexpr (KC == 2) acc[c] = step4<OP>(acc[c], v[1][c], tab.w[1]);
+        }
+    };
+    // 1. the register-held tiles' loads
+    f32x4 vr[R][KC][CPL];
+#pragma unroll
+    for (int m = 0; m < R; ++m) {
+        const int64_t off = tile_of(L + m) * tstride4 + threadIdx.x;
+#pragma unroll
+        for (int j = 0; j < KC; ++j)
+#pragma unroll
+            for (int c = 0; c < CPL; ++c) vr[m][j][c] = __builtin_nontemporal_load(tab.rows[j] + off + c * kBlock);
+    }
+    // 2. the LDS-held tiles (slots 0 .. L-1), G at a time
+#pragma unroll
+    for (int g = 0; g < L; g += G) {
+        f32x4 v[G][KC][CPL];
+#pragma unroll
+        for (int m = 0; m < G; ++m) {
+            const int64_t off = tile_of(g + m) * tstride4 + threadIdx.x;
+#pragma unroll
+            for (int j = 0; j < KC; ++j)
+#pragma unroll
+                for (int c = 0; c < CPL; ++c) v[m][j][c] = __builtin_nontemporal_load(tab.rows[j] + off + c * kBlock);
+        }
+#pragma unroll
+        for (int m = 0; m < G; ++m) {
+            f32x4 acc[CPL], r[CPL];
+            sum(acc, v[m]);
+            fin_tile<FIN, CPL>(r, acc, fc);
+#pragma unroll
+            for (int c = 0; c < CPL; ++c) staged[((g + m) * CPL + c) * kBlock + threadIdx.x] = r[c];
+        }
+    }
+    // 3. the register-held tiles (slots L .. L+R-1)
+    f32x4 res[R][CPL];
+#pragma unroll
+    for (int m = 0; m < R; ++m) {
+        f32x4 acc[CPL];
+        sum(acc, vr[m]);
+        fin_tile<FIN, CPL>(res[m], acc, fc);
+    }
+    // 4. the write burst
+#pragma unroll
+    for (int m = 0; m < L + R; ++m) {
+        const int64_t t = t_first + (int64_t)m * gridDim.x;
+        if (t < t_end) {
+#pragma unroll
+            for (int c = 0; c < CPL; ++c) {
+                const int64_t i = t * T4 + threadIdx.x + c * kBlock;
+                const f32x4 r = m < L ? staged[(m * CPL + c) * kBlock + threadIdx.x] : res[m < L ? 0 : m - L][c];
+                if (i >= b4 && i < e4) __builtin_nontemporal_store(r, out + i);
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
 // launchers
 // ---------------------------------------------------------------------------------------------
+template <int OP, int FIN, int KC, int R, int L, int G>
+inline hipError_t launch_few_form(const TileLaunch& L_, hipStream_t s, uint64_t* nl) {
+    f32x4* o = reinterpret_cast<f32x4*>(L_.out);
+    return burst_launches(L_.b4 / L_.tile4, (L_.e4 - 1) / L_.tile4 + 1, L_.grid, R + L, nl,
+                          L_.variant & kVariantAnyOrder, [&](int nb, int64_t t0, int64_t t_end, uint32_t flags) {
+                              hipExtLaunchKernelGGL((fedavg_tiles_few_f32x4<OP, FIN, KC, R, L, G>), dim3(nb), dim3(kBlock),
+                                                    0, s, nullptr, nullptr, flags, L_.tab, L_.tstride4, o, L_.b4, L_.e4,
+                                                    L_.fin_val, t0, t_end);
+                          });
+}
+
+// the few-client burst kernel (1-2 client reads, no chained sum): the host sets L.grid from few_form().bpc
+template <int OP, int FIN, int KC>
+inline hipError_t launch_few(const TileLaunch& L, hipStream_t s, uint64_t* nl) {
+    const FewForm f = few_form(KC, L.variant);
+#define FEDAVG_FEW(R, LL, G)                                                       \
+    if (f.r == R && f.l == LL && f.g == G) return launch_few_form<OP, FIN, KC, R, LL, G>(L, s, nl);
+    if constexpr (KC == 1) {
+        FEDAVG_FEW(8, 4, 4)
+        if constexpr (kAB) {
+            FEDAVG_FEW(8, 4, 2)
+            FEDAVG_FEW(8, 10, 5)
+            FEDAVG_FEW(8, 0, 1)
+            FEDAVG_FEW(4, 4, 4)
+            FEDAVG_FEW(8, 8, 4)
+        }
+    } else {
+        FEDAVG_FEW(4, 4, 2)
+        if constexpr (kAB) {
+            FEDAVG_FEW(4, 4, 4)
+            FEDAVG_FEW(4, 10, 2)
+            FEDAVG_FEW(6, 9, 3)
+            FEDAVG_FEW(6, 4, 2)
+            FEDAVG_FEW(4, 0, 1)
+        }
+    }
+#undef FEDAVG_FEW
+    return hipErrorInvalidValue;
+}
 // one launch per grid x (TPB + TPB_LDS) tiles (fedavg_tiles_burst_f32x4)
 template <int OP, int FIN, bool ACC_IN, int UNROLL, int CPL, int TPB, int TPB_LDS, int KC, int SHAPE = -1>
 inline hipError_t launch_burst_kc(const TileLaunch& L, hipStream_t s, uint64_t* nl) {
@@ -292,14 +424,17 @@ inline hipError_t launch_burst_kc(const TileLaunch& L, hipStream_t s, uint64_t* 
                           });
 }
 
-// the burst kernel with the launch's client count built in (1-6 clients: every row pointer and weight in SGPRs, every
-// load a real client's; from 7 on -- 7 with a chained partial sum, 8 -- both groups' loads are hoisted together past
-// 256 VGPRs, one wave per SIMD), or from 7 clients on the runtime count with its remainder mod 4 built in; variant bit
-// 7 takes the round-3 runtime form everywhere (A/Bs)
+// The burst kernel's client loop per launch: the client count built in for 3-6 clients (tile_sum_kc: every row pointer
+// and weight in SGPRs, every load a real client's), from 7 on the runtime count with its remainder mod 4 built in
+// (tile_sum_rem; 7 with a chained partial sum and 8 built in would hoist both groups' 32 loads past 256 VGPRs at one wave
+// per SIMD).  The built-in counts are instantiated only where the router sends them -- no chained sum, two blocks per
+// CU (fewer than kBurstOneBlockMinK clients); a chained sum or a one-block-per-CU grid takes the remainder forms, which
+// run the same per-element sequence.  A/B builds (kAB) add the built-in 1-2 client forms (public variant bit 8), the
+// round-3 runtime loop (bit 7: tile_sum's GROUPED form with its repeated loads) and the loop shapes (bits 9-11).
 template <int OP, int FIN, bool ACC_IN, int UNROLL, int CPL, int TPB, int TPB_LDS = 0>
 inline hipError_t launch_burst(const TileLaunch& L, hipStream_t s, uint64_t* nl) {
     if constexpr (CPL == 4 && UNROLL == 4) {
-        if constexpr (OP == FEDAVG_OP_TORCH && FIN == FEDAVG_FIN_DIV && !ACC_IN) {  // A/B: client-loop shapes, K % 4 == 0
+        if constexpr (kAB && OP == FEDAVG_OP_TORCH && FIN == FEDAVG_FIN_DIV && !ACC_IN) {  // A/B: client-loop shapes
             const int shape = (L.variant >> kVariantLoopShift) & 7;
             if (shape == 2 && L.k == 3) return launch_burst_kc<OP, FIN, ACC_IN, UNROLL, CPL, TPB, TPB_LDS, 3, 2>(L, s, nl);
             if (shape == 5 && L.k == 4) return launch_burst_kc<OP, FIN, ACC_IN, UNROLL, CPL, TPB, TPB_LDS, 4, 0>(L, s, nl);
@@ -319,49 +454,69 @@ inline hipError_t launch_burst(const TileLaunch& L, hipStream_t s, uint64_t* nl)
                 }
             }
         }
-        if (!(L.variant & kVariantRuntimeK)) {
+        if constexpr (kAB) {
+            if (L.variant & kVariantRuntimeK) return launch_burst_kc<OP, FIN, ACC_IN, UNROLL, CPL, TPB, TPB_LDS, 0>(L, s, nl);
+        }
+        if constexpr (kAB || (!ACC_IN && TPB_LDS != kBurstLdsTilesWide)) {
             switch (L.k) {
 #define FEDAVG_KC(N) \
     case N:          \
         return launch_burst_kc<OP, FIN, ACC_IN, UNROLL, CPL, TPB, TPB_LDS, N>(L, s, nl);
-                FEDAVG_KC(1)
-                FEDAVG_KC(2)
                 FEDAVG_KC(3)
                 FEDAVG_KC(4)
                 FEDAVG_KC(5)
                 FEDAVG_KC(6)
-#undef FEDAVG_KC
                 default:
                     break;
             }
-            switch (L.k % 4) {
-                case 1:
-                    return launch_burst_kc<OP, FIN, ACC_IN, UNROLL, CPL, TPB, TPB_LDS, -2>(L, s, nl);
-                case 2:
-                    return launch_burst_kc<OP, FIN, ACC_IN, UNROLL, CPL, TPB, TPB_LDS, -3>(L, s, nl);
-                case 3:
-                    return launch_burst_kc<OP, FIN, ACC_IN, UNROLL, CPL, TPB, TPB_LDS, -4>(L, s, nl);
-                default:
-                    return launch_burst_kc<OP, FIN, ACC_IN, UNROLL, CPL, TPB, TPB_LDS, -1>(L, s, nl);
+            if constexpr (kAB) {
+                switch (L.k) {
+                    FEDAVG_KC(1)
+                    FEDAVG_KC(2)
+                    default:
+                        break;
+                }
             }
+#undef FEDAVG_KC
+        }
+        switch (L.k % 4) {
+            case 1:
+                return launch_burst_kc<OP, FIN, ACC_IN, UNROLL, CPL, TPB, TPB_LDS, -2>(L, s, nl);
+            case 2:
+                return launch_burst_kc<OP, FIN, ACC_IN, UNROLL, CPL, TPB, TPB_LDS, -3>(L, s, nl);
+            case 3:
+                return launch_burst_kc<OP, FIN, ACC_IN, UNROLL, CPL, TPB, TPB_LDS, -4>(L, s, nl);
+            default:
+                return launch_burst_kc<OP, FIN, ACC_IN, UNROLL, CPL, TPB, TPB_LDS, -1>(L, s, nl);
         }
     }
-    return launch_burst_kc<OP, FIN, ACC_IN, UNROLL, CPL, TPB, TPB_LDS, 0>(L, s, nl);
+    if constexpr (kAB) return launch_burst_kc<OP, FIN, ACC_IN, UNROLL, CPL, TPB, TPB_LDS, 0>(L, s, nl);
+    return hipErrorInvalidValue;  // product builds: the default geometry only (launch_tiles_a)
 }
 
+// the per-tile-store kernel (each tile's results stored as it finishes) or the burst kernel; product builds carry the
+// default geometry's nontemporal per-tile form and the burst forms with LDS-held tiles (4 on two-block grids, 10 on
+// one-block grids)
 template <int OP, int FIN, bool ACC_IN, int UNROLL, int CPL>
 inline hipError_t launch_tiles_v(const TileLaunch& L, hipStream_t s, uint64_t* nl) {
     const f32x4* ai = reinterpret_cast<const f32x4*>(L.acc_in);
     f32x4* o = reinterpret_cast<f32x4*>(L.out);
+    if (L.variant & kVariantFew) {  // 1-2 client reads, no chained sum (fedavg_capi.cpp run_tiles)
+        if constexpr (!ACC_IN && CPL == 4 && UNROLL == 4) {
+            if (L.k == 1) return launch_few<OP, FIN, 1>(L, s, nl);
+            if (L.k == 2) return launch_few<OP, FIN, 2>(L, s, nl);
+        }
+        return hipErrorInvalidValue;
+    }
     if constexpr (CPL * (UNROLL + kBurstTiles) <= 64) {  // staged results + a group's loads within 256 VGPRs
         if (!(L.variant & (kVariantTileStores | kVariantTemporalLoads | kVariantTemporalStores))) {
             if constexpr (CPL == 4 && UNROLL == 4) {  // the default geometry only (build time)
                 if (L.variant & kVariantWideLds)
                     return launch_burst<OP, FIN, ACC_IN, UNROLL, CPL, kBurstTiles, kBurstLdsTilesWide>(L, s, nl);
-                if (!(L.variant & kVariantRegisterTiles))
+                if (!kAB || !(L.variant & kVariantRegisterTiles))
                     return launch_burst<OP, FIN, ACC_IN, UNROLL, CPL, kBurstTiles, kBurstLdsTiles>(L, s, nl);
             }
-            return launch_burst<OP, FIN, ACC_IN, UNROLL, CPL, kBurstTiles>(L, s, nl);
+            if constexpr (kAB) return launch_burst<OP, FIN, ACC_IN, UNROLL, CPL, kBurstTiles>(L, s, nl);
         }
     }
     const bool ntl = !(L.variant & kVariantTemporalLoads);
@@ -369,14 +524,16 @@ inline hipError_t launch_tiles_v(const TileLaunch& L, hipStream_t s, uint64_t* n
 #define FEDAVG_LAUNCH_TILES(NTL, NTS)                                                                                \
     hipLaunchKernelGGL((fedavg_tiles_f32x4<OP, FIN, ACC_IN, UNROLL, CPL, NTL, NTS>), dim3(L.grid), dim3(kBlock), 0, \
                        s, L.tab, L.k, L.tstride4, ai, o, L.b4, L.e4, L.fin_val)
-    if (ntl && nts) {
+    if (!kAB || (ntl && nts)) {
         FEDAVG_LAUNCH_TILES(true, true);
-    } else if (ntl) {
-        FEDAVG_LAUNCH_TILES(true, false);
-    } else if (nts) {
-        FEDAVG_LAUNCH_TILES(false, true);
-    } else {
-        FEDAVG_LAUNCH_TILES(false, false);
+    } else if constexpr (kAB) {
+        if (ntl) {
+            FEDAVG_LAUNCH_TILES(true, false);
+        } else if (nts) {
+            FEDAVG_LAUNCH_TILES(false, true);
+        } else {
+            FEDAVG_LAUNCH_TILES(false, false);
+        }
     }
 #undef FEDAVG_LAUNCH_TILES
     if (nl) ++*nl;
@@ -386,21 +543,26 @@ inline hipError_t launch_tiles_v(const TileLaunch& L, hipStream_t s, uint64_t* n
 template <int OP, int FIN, bool ACC_IN>
 inline hipError_t launch_tiles_a(const TileLaunch& L, hipStream_t s, uint64_t* nl) {
     const int64_t cpl = L.tile4 / kBlock;
+    if constexpr (!kAB) {  // product builds: the default tile (4096 elements) and unroll only (fedavg_set_tile / _launch)
+        if (cpl != 4 || L.unroll != 4) return hipErrorInvalidValue;
+        return launch_tiles_v<OP, FIN, ACC_IN, 4, 4>(L, s, nl);
+    } else {
 #define FEDAVG_TILES_CPL(C) \
     return L.unroll == 8 ? launch_tiles_v<OP, FIN, ACC_IN, 8, C>(L, s, nl) : launch_tiles_v<OP, FIN, ACC_IN, 4, C>(L, s, nl);
-    switch (cpl) {
-        case 1:
-            FEDAVG_TILES_CPL(1)
-        case 2:
-            FEDAVG_TILES_CPL(2)
-        case 4:
-            FEDAVG_TILES_CPL(4)
-        case 8:
-            FEDAVG_TILES_CPL(8)
-        default:
-            return hipErrorInvalidValue;
-    }
+        switch (cpl) {
+            case 1:
+                FEDAVG_TILES_CPL(1)
+            case 2:
+                FEDAVG_TILES_CPL(2)
+            case 4:
+                FEDAVG_TILES_CPL(4)
+            case 8:
+                FEDAVG_TILES_CPL(8)
+            default:
+                return hipErrorInvalidValue;
+        }
 #undef FEDAVG_TILES_CPL
+    }
 }
 
 template <int OP, int FIN>

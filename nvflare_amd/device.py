@@ -432,6 +432,17 @@ class DeviceContext:
     def set_variant(self, variant: int = 0) -> None:
         N.call("fedavg_set_variant", self.handle, ctypes.c_int(variant))
 
+    def ab_build(self) -> bool:
+        """Whether the loaded library is an A/B build (tools/build_rev_lib.py, -DFEDAVG_AB): it accepts the A/B-only
+        launch variants, tile widths and unrolls, which a product library refuses (round 5).  Probed with variant
+        bit 5, then the default is restored."""
+        try:
+            self.set_variant(32)
+        except N.FedAvgError:
+            return False
+        self.set_variant(0)
+        return True
+
     def dequantize(self, quant: "N.Quant", q_ptr: int, n: int, out_ptr: int, tile: int = 0, tile_stride: int = 0,
                    logical_offset: int = 0) -> None:
         """Dequantize n elements of the device payload at q_ptr into fp32 (fedavg_dequantize)."""

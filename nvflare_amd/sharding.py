@@ -14,6 +14,7 @@ client-sharded RCCL reduce would not be (it re-associates the sums).
 
 from __future__ import annotations
 
+import logging
 import threading
 import weakref
 from concurrent.futures import ThreadPoolExecutor
@@ -122,8 +123,15 @@ class ShardedFedAvg:
                 for k in introduced:
                     self._shapes.pop(k, None)
                 if undo_errs:
+                    # the undo failures came after the staging error: reported beside it (a note on 3.11+, and the
+                    # log), never as its cause -- err is re-raised with its own __cause__ unchanged
                     msg = "; ".join(f"bucket {b}: {type(e).__name__}: {e}" for b, e in undo_errs)
-                    raise err from RuntimeError(f"nvflare_amd: undoing the other buckets also failed ({msg})")
+                    note = f"nvflare_amd: undoing the other buckets also failed ({msg})"
+                    logging.getLogger(__name__).error(note)
+                    if hasattr(err, "add_note"):
+                        err.add_note(note)
+                    else:
+                        err.undo_failures = undo_errs
                 raise err
 
     def _assemble(self, k: str, plist: List[Tuple[int, Any]]):

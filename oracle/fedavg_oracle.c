@@ -265,20 +265,28 @@ void oracle_sqrt_mkl_rsqrtps_n(const uint16_t* tab, const float* x, size_t n, fl
     for (size_t i = 0; i < n; ++i) out[i] = oracle_sqrt_mkl_rsqrtps(tab, x[i]);
 }
 
-/* THIS CPU's RSQRTPS table in the layout above: the estimate of the first fp32 of each top-12-bit-mantissa block of
- * [1, 2) and [2, 4) (tools/rsqrtps_dump.c dumps every input; tests compare).  Returns the number of blocks whose
- * estimate is not a 12-bit value with exponent 126 (0 on the CPUs the restatement covers). */
+/* THIS CPU's RSQRTPS table in the layout above, from the packed instruction MKL's SSE kernel executes (RSQRTPS,
+ * _mm_rsqrt_ps; ADVICE r04: the scalar RSQRTSS is another instruction) over EVERY fp32 of [1, 4), four per
+ * instruction: entry i = the estimate of block i (2^11 consecutive inputs sharing the exponent parity and the top 12
+ * mantissa bits).  Returns the number of blocks whose inputs do not all give one 12-bit estimate with exponent 126 (0
+ * on the CPUs the restatement covers), independently of the product's own capture (fedavg_host_rsqrtps_table). */
 int oracle_host_rsqrtps_table(uint16_t* tab) {
     int bad = 0;
     for (uint32_t i = 0; i < 8192; ++i) {
-        const uint32_t bits = 0x3F800000u + (i << 11);
-        float x, y;
-        memcpy(&x, &bits, 4);
-        _mm_store_ss(&y, _mm_rsqrt_ss(_mm_set_ss(x)));
-        uint32_t e;
-        memcpy(&e, &y, 4);
-        bad += (e >> 23) != 126u || (e & 0x7FFu) != 0u;
-        tab[i] = (uint16_t)((e >> 11) & 0xFFFu);
+        uint32_t first = 0;
+        int block_bad = 0;
+        for (uint32_t j = 0; j < 2048; j += 4) {
+            uint32_t in[4], out[4];
+            for (int l = 0; l < 4; ++l) in[l] = 0x3F800000u + (i << 11) + j + (uint32_t)l;
+            __m128 x;
+            memcpy(&x, in, 16);
+            const __m128 y = _mm_rsqrt_ps(x);
+            memcpy(out, &y, 16);
+            if (j == 0) first = out[0];
+            for (int l = 0; l < 4; ++l) block_bad |= out[l] != first;
+        }
+        bad += block_bad || (first >> 23) != 126u || (first & 0x7FFu) != 0u;
+        tab[i] = (uint16_t)((first >> 11) & 0xFFFu);
     }
     return bad;
 }

@@ -268,10 +268,25 @@ def test_kernel_generic_dtypes(ctx, oracle, in_dt, acc_dt):
         assert same_bits(got, exp)
 
 
+PRODUCT_VARIANTS = (0, 4, 16, 64, 20, 80)  # fedavg_internal.h kVariantProductMask: bits 2, 4 and 6
+
+
+def _product_form(variant=0, unroll=0, tile=4096):
+    return (variant & ~84) == 0 and unroll in (0, 4) and tile == 4096
+
+
+@pytest.fixture(scope="module")
+def ab(ctx):
+    """Whether the library is an A/B build (tools/build_rev_lib.py): the product library carries only routed forms."""
+    return ctx.ab_build()
+
+
 @pytest.mark.parametrize("variant", [0, 1, 2, 3, 8, 16, 32])
 @pytest.mark.parametrize("bpc,unroll,tile", [(1, 4, 1024), (2, 8, 2048), (4, 4, 4096), (8, 8, 8192), (2, 4, 4096),
                                              (0, 0, 4096), (1, 8, 4096)])
-def test_launch_variants_same_bits(ctx, oracle, bpc, unroll, tile, variant):
+def test_launch_variants_same_bits(ctx, oracle, ab, bpc, unroll, tile, variant):
+    if not ab and not _product_form(variant, unroll, tile):
+        pytest.skip("an A/B form: tools/build_rev_lib.py builds the library that carries it")
     rng = np.random.default_rng(21)
     n = 300_001 + variant  # whole tiles on the streaming kernel + a ragged tail on the scalar kernel
     rows = [rng.standard_normal(n).astype(np.float32) for _ in range(33)]
@@ -293,13 +308,15 @@ def test_launch_variants_same_bits(ctx, oracle, bpc, unroll, tile, variant):
 @pytest.mark.parametrize("K,bpc,variant", [(20, 0, 0), (7, 0, 0), (20, 3, 0), (131, 0, 0), (1, 0, 0), (2, 0, 0),
                                            (129, 0, 0), (1, 0, 256), (2, 0, 256), (3, 0, 256), (3, 0, 384), (4, 0, 0),
                                            (5, 0, 0), (8, 0, 0), (8, 0, 128), (9, 0, 0), (130, 0, 256), (136, 0, 0)])
-def test_burst_many_launches(ctx, oracle, K, bpc, variant):
+def test_burst_many_launches(ctx, oracle, ab, K, bpc, variant):
     """The default (burst) kernel issues one launch per grid x 8 tiles: more tiles than one launch covers,
     a last launch with fewer tiles than blocks, a sub-range starting and ending inside tiles, more than
     128 clients (chained through the output), against the oracle bit for bit.  One and two clients, and a
     chained last chunk of one client (129), take the per-tile-store kernel (fedavg_capi.cpp kBurstMinClients);
     variant bit 8 keeps them on the burst form.  1-8 clients per launch (a chained last chunk of 1-8: 129-136) take
     the burst kernel with the client count built in (tile_sum_kc, round 4); bit 7 the runtime-K loop."""
+    if not ab and not _product_form(variant):
+        pytest.skip("an A/B form: tools/build_rev_lib.py builds the library that carries it")
     n = 2048 * 4096 * 2 + 12345
     rows = [oracle.synth_values(5, k, np.arange(n, dtype=np.uint64)) for k in range(K)]
     ws = oracle.synth_weights(K)
@@ -553,3 +570,68 @@ def test_h2d_tiled_multi_packs_keys(ctx, oracle):
             assert same_bits(got[o:o + n], exp), j
     slab.close()
     out.close()
+
+
+@pytest.mark.parametrize("K", [1, 2])
+@pytest.mark.parametrize("form", [0, 1, 2, 3, 4, 5, 6])
+def test_few_client_burst_forms(ctx, oracle, ab, K, form):
+    """The few-client burst kernel (fedavg_tiles.h fedavg_tiles_few_f32x4; 1-2 client reads, no chained sum): several
+    launches and a short last one (15 001 tiles against 6144 per launch at the default form), every load unconditional
+    (a launch's slots past its last tile re-read that tile, nothing past it is stored), a ragged end, a sub-range
+    starting and ending inside tiles with a sentinel around it; numpy and torch modes, bit for bit.  Forms 1-6 (launch
+    variant bits 9-11, A/B builds) are the sweep's geometries (fedavg_internal.h kFewAB)."""
+    if form and not ab:
+        pytest.skip("an A/B form: tools/build_rev_lib.py builds the library that carries it")
+    n = 15_001 * 4096 - 4092
+    cols = np.arange(n, dtype=np.uint64)
+    rows = [oracle.synth_values(17, k, cols) for k in range(K)]
+    ws = oracle.synth_weights(K)
+    n_alloc = (n + 4095) // 4096 * 4096
+    bufs = [ctx.alloc(n_alloc * 4) for _ in rows]
+    out = ctx.alloc(n_alloc * 4)
+    ctx.set_variant(form << 9)
+    try:
+        for b, r in zip(bufs, rows):
+            ctx.h2d_ptr(b.ptr, r.ctypes.data, r.nbytes)
+        got = np.empty(n, np.float32)
+        for op, fin, mode in ((1, 2, oracle.MODE_TORCH), (0, 1, oracle.MODE_NUMPY)):
+            exp = oracle.fedavg_c(rows, ws, mode, fin=fin, nthreads=8)
+            n0 = ctx.launch_count()
+            ctx.accumulate_tiled([b.ptr for b in bufs], ws, 4096, 4096, 0, (n + 3) // 4 * 4, out.ptr, op, fin, _sum(ws))
+            assert ctx.launch_count() - n0 >= 2
+            ctx.d2h(got, out.ptr)
+            assert same_bits(got, exp), (K, form, mode)
+        lo, hi = 4096 * 7 + 36, n - 4096 * 3 - 100
+        sentinel = np.full(n, -7.0, np.float32)
+        ctx.h2d_ptr(out.ptr, sentinel.ctypes.data, sentinel.nbytes)
+        ctx.accumulate_tiled([b.ptr for b in bufs], ws, 4096, 4096, lo, hi, out.ptr, 1, 2, _sum(ws))
+        ctx.d2h(got, out.ptr)
+        exp = oracle.fedavg_c([r[lo:hi] for r in rows], ws, oracle.MODE_TORCH, fin=2, nthreads=8)
+        assert same_bits(got[lo:hi], exp)
+        assert np.all(got[:lo] == -7.0) and np.all(got[hi:] == -7.0)
+    finally:
+        ctx.set_variant(0)
+        for b in bufs + [out]:
+            b.close()
+
+
+def test_product_library_refuses_ab_forms(ctx, ab):
+    """The product library carries only the routed kernel forms (round 5): the A/B launch variants, unroll 8 and other
+    tile widths are refused with an error, not run on some other form."""
+    from nvflare_amd._native import FedAvgError
+
+    if ab:
+        pytest.skip("an A/B build accepts them")
+    for v in (1, 2, 8, 32, 128, 256, 1 << 9, 3 << 9):
+        with pytest.raises(FedAvgError, match="A/B"):
+            ctx.set_variant(v)
+    for v in PRODUCT_VARIANTS:
+        ctx.set_variant(v)
+    ctx.set_variant(0)
+    with pytest.raises(FedAvgError, match="A/B"):
+        ctx.set_launch(0, 8)
+    for t in (1024, 2048, 8192):
+        with pytest.raises(FedAvgError, match="A/B"):
+            ctx.set_tile(t)
+    ctx.set_launch(0, 0)
+    ctx.set_tile(0)

@@ -180,3 +180,22 @@ def test_sharded_fedopt_returned_weights_are_independent(container):
         for k in params:
             assert same_bits(w_plain[k], w_edit[k]), k
     assert gen._dev_opt.is_bound()
+
+
+def test_sharded_to_host_uploads_host_edits_first():
+    """ShardedServerOptimizer.to_host pulls the weights it hands out from the device shards; a parameter
+    written in place on the host after the last step (load_state_dict, param.copy_) must reach the shards first, or
+    the hand-out is the stale shard value.  The hand-out equals the edited host parameters bit for bit, and the
+    next step starts from them."""
+    _, _, gen = run_fedopt_sag(True, "torch", "adam", 4, rounds=1, model_fn=wide_model, devices=DEVS)
+    dev = gen._dev_opt
+    assert dev.is_bound()
+    with torch.no_grad():
+        for p in gen.model.parameters():
+            p.mul_(2.0).add_(0.5)
+    want = {k: v.detach().clone() for k, v in gen.model.state_dict().items()}
+    got = dev.to_host(gen.model.state_dict(), True)
+    params = {n for n, _ in gen.model.named_parameters()}
+    assert params
+    for k in params:
+        assert same_bits(got[k].numpy(), want[k].numpy()), k

@@ -7,10 +7,12 @@
 
 The revision's csrc/ and include/ are exported to a temporary directory with ``git show``; the flags and
 source list (with the fused kernels' per-unit definitions) are the current nvflare_amd/_build.py's (the A/B
-compares kernels, not build settings)."""
+compares kernels, not build settings).  The library is an A/B build (-DFEDAVG_AB): it carries every kernel form,
+launch variant, tile width and unroll the sources know, which the product library (nvflare_amd/_build.py) leaves out."""
 
 import argparse
 import os
+import shutil
 import subprocess
 import sys
 import tempfile
@@ -20,6 +22,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 from nvflare_amd import _build as B  # noqa: E402
+
+AB_OBJ = os.path.join(B.PKG, "lib", "obj_ab")  # objects of the last full WORKTREE A/B build (no -D), for --only
 
 
 def _export(rev: str, path: str, dst: str) -> None:
@@ -40,12 +44,11 @@ def main():
     ap.add_argument("-D", dest="defines", action="append", default=[], help="extra preprocessor definitions")
     ap.add_argument("--only", default="",
                     help="with --rev WORKTREE: comma list of sources to compile (with -D); every other unit's object "
-                         "is the in-tree build's (nvflare_amd/lib/obj, same sources), so a one-file A/B links in minutes")
+                         "is the last full WORKTREE A/B build's (nvflare_amd/lib/obj_ab, same sources), so a one-file "
+                         "A/B links in minutes")
     args = ap.parse_args()
     with tempfile.TemporaryDirectory() as tmp:
         if args.rev == "WORKTREE":  # the working tree's sources as they are
-            import shutil
-
             shutil.copytree(os.path.join(ROOT, "nvflare_amd", "csrc"), os.path.join(tmp, "nvflare_amd", "csrc"))
             shutil.copytree(os.path.join(ROOT, "include"), os.path.join(tmp, "include"))
         else:
@@ -53,20 +56,24 @@ def main():
             _export(args.rev, "include", tmp)
         csrc = os.path.join(tmp, "nvflare_amd", "csrc")
         inc = [f"-I{os.path.join(tmp, 'include')}", f"-I{csrc}"]
-        units = B.compile_units([s for s in B.SOURCES if os.path.exists(os.path.join(csrc, s))])
+        # an A/B library: every kernel form the sources know (-DFEDAVG_AB; ignored by revisions before round 5)
+        units = B.compile_units([s for s in B.SOURCES if os.path.exists(os.path.join(csrc, s))], ab=True)
         only = [x for x in args.only.split(",") if x]
         if only and args.rev != "WORKTREE":
             raise SystemExit("--only needs --rev WORKTREE (the reused objects are the working tree's)")
-        if only and B.needs_build():
-            raise SystemExit("--only reuses the in-tree objects: build the in-tree library first")
+        if only and not os.path.isdir(AB_OBJ):
+            raise SystemExit(f"--only reuses the objects of a full --rev WORKTREE build ({AB_OBJ}): run one first")
 
         def compile_one(unit):
             src, obj_name, extra = unit
             if only and src not in only:
-                return os.path.join(B.OBJ_DIR, obj_name)
+                return os.path.join(AB_OBJ, obj_name)
             obj = os.path.join(tmp, obj_name)
-            defs = [f"-D{d}" for d in args.defines]
+            defs = [f"-D{d}" for d in ["FEDAVG_AB"] + args.defines]
             subprocess.run([B.HIPCC, *B.FLAGS, *extra, *defs, *inc, "-c", os.path.join(csrc, src), "-o", obj], check=True)
+            if args.rev == "WORKTREE" and not only and not args.defines:  # the objects a later --only run reuses
+                os.makedirs(AB_OBJ, exist_ok=True)
+                shutil.copy(obj, os.path.join(AB_OBJ, obj_name))
             return obj
 
         with ThreadPoolExecutor(max_workers=min(8, len(units))) as pool:
