@@ -1452,8 +1452,9 @@ int fedavg_set_variant(fedavg_ctx* ctx, int variant) {
     return guarded([&] {
         if (!ctx) throw Error("ctx is NULL");
         if (variant < 0 || variant > 4095) throw Error("variant must be 0..4095");
-        if (!fedavg::kAB && (variant & ~fedavg::kVariantProductMask))
-            throw Error("variant bits " + std::to_string(variant & ~fedavg::kVariantProductMask) +
+        const int accepted = fedavg::kVariantProductMask | (fedavg::kABFew ? 7 << fedavg::kVariantLoopShift : 0);
+        if (!fedavg::kAB && (variant & ~accepted))
+            throw Error("variant bits " + std::to_string(variant & ~accepted) +
                         " are A/B forms this product library does not carry (it accepts bits 2, 4 and 6; "
                         "tools/build_rev_lib.py builds A/B libraries)");
         ctx->variant = variant;

@@ -332,6 +332,13 @@ __device__ __forceinline__ void epi_store(const EpiParams& E, const int64_t i, c
 template <int EPI>
 __device__ __forceinline__ void epilogue4(const EpiParams& E, const EpiConsts& C, const int64_t i, const f32x4 d,
                                           const EpiIn& in, f32x4* out) {
+#if defined(FEDAVG_AB_EPI_EXACT)  // A/B builds only: round 4's per-element rare-case branches
+    {
+        uint32_t unused = 0;
+        epi_store<EPI>(E, i, epi_compute<EPI, false>(E, C, d, in, unused), out);
+        return;
+    }
+#endif
     uint32_t slow = 0;
     if constexpr ((EPI & 0xFF) == FEDAVG_EPI_ADAM) slow = C.bc2s.fast ? 0u : 1u;
     if constexpr ((EPI & 0xFF) == FEDAVG_EPI_NADAM) slow = C.bc2.fast ? 0u : 1u;
@@ -554,7 +561,12 @@ __global__ void __launch_bounds__(kBlock) fedavg_tiles_epi_f32x4(const RowTableF
             }
         }
         f32x4 dv[CPL];
+#if defined(FEDAVG_AB_EPI_EXACT)  // A/B builds only: round 4's per-element finalisation
+#pragma unroll
+        for (int c = 0; c < CPL; ++c) dv[c] = fin4c<FIN>(acc[c], fc);
+#else
         fin_tile<FIN, CPL>(dv, acc, fc);
+#endif
 #pragma unroll
         for (int c = 0; c < CPL; ++c) {
             const int64_t i = col + c * kBlock;

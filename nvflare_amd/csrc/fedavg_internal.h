@@ -28,6 +28,13 @@ constexpr bool kAB = true;
 #else
 constexpr bool kAB = false;
 #endif
+// -DFEDAVG_AB_FEW: a product library plus the few-client forms' geometry sweep only (launch variant bits 9-11 for 1-2
+// client reads, kFewAB) -- a product-sized A/B build (tools/build_rev_lib.py --product -D FEDAVG_AB_FEW)
+#if defined(FEDAVG_AB) || defined(FEDAVG_AB_FEW)
+constexpr bool kABFew = true;
+#else
+constexpr bool kABFew = false;
+#endif
 
 // variant bits (fedavg_set_variant).  Default (0): the plain aggregation runs fedavg_tiles_burst_f32x4.
 constexpr int kVariantTemporalLoads = 1;   // per-tile-store kernel with temporal (cached) client loads
@@ -202,7 +209,7 @@ constexpr FewForm kFewAB[2][6] = {
 
 // the few-client form of a launch with `reads` (1 or 2) client reads
 inline FewForm few_form(int reads, int variant) {
-    if (kAB) {
+    if (kABFew) {
         const int ix = (variant >> kVariantLoopShift) & 7;
         if (ix >= 1 && ix <= 6) return kFewAB[reads - 1][ix - 1];
     }

@@ -390,7 +390,7 @@ inline hipError_t launch_few(const TileLaunch& L, hipStream_t s, uint64_t* nl) {
     if (f.r == R && f.l == LL && f.g == G) return launch_few_form<OP, FIN, KC, R, LL, G>(L, s, nl);
     if constexpr (KC == 1) {
         FEDAVG_FEW(8, 4, 4)
-        if constexpr (kAB) {
+        if constexpr (kABFew) {
             FEDAVG_FEW(8, 4, 2)
             FEDAVG_FEW(8, 10, 5)
             FEDAVG_FEW(8, 0, 1)
@@ -399,7 +399,7 @@ inline hipError_t launch_few(const TileLaunch& L, hipStream_t s, uint64_t* nl) {
         }
     } else {
         FEDAVG_FEW(4, 4, 2)
-        if constexpr (kAB) {
+        if constexpr (kABFew) {
             FEDAVG_FEW(4, 4, 4)
             FEDAVG_FEW(4, 10, 2)
             FEDAVG_FEW(6, 9, 3)

@@ -393,10 +393,13 @@ def test_timing_events(ctx):
 @pytest.mark.parametrize("tile", [1024, 2048, 4096, 8192])
 @pytest.mark.parametrize("K,slots", [(13, 16), (16, 16), (24, 24), (130, 130)])
 @pytest.mark.parametrize("begin,end", [(0, None), (64, None), (4096 + 128, 3 * 4096 - 64), (8, 12)])
-def test_tiled_slab_vs_oracle(ctx, oracle, tile, K, slots, begin, end):
+def test_tiled_slab_vs_oracle(ctx, oracle, ab, tile, K, slots, begin, end):
     """Tiled slab (clients interleaved per tile), permuted arrival order, sub-ranges that start and end
     mid-tile (only [begin, end) of the flat output is written), >128 clients chained through the output."""
     from nvflare_amd.device import TiledLayout
+
+    if not ab and not _product_form(tile=tile):
+        pytest.skip("tile widths other than 4096 are A/B forms (tools/build_rev_lib.py)")
 
     n = 7 * 4096 + 1024 + 12  # ragged last tile
     end = n if end is None else end
@@ -426,9 +429,12 @@ def test_tiled_slab_vs_oracle(ctx, oracle, tile, K, slots, begin, end):
 
 
 @pytest.mark.parametrize("tile", [1024, 4096])
-def test_h2d_tiled_staging(ctx, oracle, tile):
+def test_h2d_tiled_staging(ctx, oracle, ab, tile):
     """Host arrays staged into tiled slots at arbitrary (4-aligned) logical offsets, pageable and pinned."""
     from nvflare_amd.device import TiledLayout
+
+    if not ab and not _product_form(tile=tile):
+        pytest.skip("tile widths other than 4096 are A/B forms (tools/build_rev_lib.py)")
 
     K, slots, n = 5, 8, 3 * tile + 100
     lay = TiledLayout(tile, slots)
@@ -458,7 +464,7 @@ def test_h2d_tiled_staging(ctx, oracle, tile):
 def test_d2d_tiled_staging_from_torch(ctx, oracle):
     from nvflare_amd.device import TiledLayout
 
-    tile, K, n = 2048, 3, 2 * 2048 + 8
+    tile, K, n = 4096, 3, 2 * 4096 + 8
     lay = TiledLayout(tile, K)
     slab = ctx.alloc(lay.slab_elems(n) * 4)
     rows = [torch.randn(n, generator=torch.Generator().manual_seed(k)) for k in range(K)]
@@ -580,8 +586,14 @@ def test_few_client_burst_forms(ctx, oracle, ab, K, form):
     (a launch's slots past its last tile re-read that tile, nothing past it is stored), a ragged end, a sub-range
     starting and ending inside tiles with a sentinel around it; numpy and torch modes, bit for bit.  Forms 1-6 (launch
     variant bits 9-11, A/B builds) are the sweep's geometries (fedavg_internal.h kFewAB)."""
-    if form and not ab:
-        pytest.skip("an A/B form: tools/build_rev_lib.py builds the library that carries it")
+    if form:
+        from nvflare_amd._native import FedAvgError
+
+        try:  # A/B builds, or a product build with -DFEDAVG_AB_FEW (tools/build_rev_lib.py --product)
+            ctx.set_variant(form << 9)
+        except FedAvgError:
+            pytest.skip("an A/B form: tools/build_rev_lib.py builds the library that carries it")
+        ctx.set_variant(0)
     n = 15_001 * 4096 - 4092
     cols = np.arange(n, dtype=np.uint64)
     rows = [oracle.synth_values(17, k, cols) for k in range(K)]

@@ -42,10 +42,14 @@ def main():
     ap.add_argument("--rev", default="HEAD")
     ap.add_argument("--out", required=True)
     ap.add_argument("-D", dest="defines", action="append", default=[], help="extra preprocessor definitions")
+    ap.add_argument("--product", action="store_true",
+                    help="a product-sized library (no -DFEDAVG_AB, the product unit list) plus the -D definitions, "
+                         "e.g. -D FEDAVG_AB_FEW for the few-client forms' sweep only")
     ap.add_argument("--only", default="",
-                    help="with --rev WORKTREE: comma list of sources to compile (with -D); every other unit's object "
-                         "is the last full WORKTREE A/B build's (nvflare_amd/lib/obj_ab, same sources), so a one-file "
-                         "A/B links in minutes")
+                    help="with --rev WORKTREE: comma list of sources or object names to compile (with -D); every "
+                         "other unit's object is the last full WORKTREE A/B build's (nvflare_amd/lib/obj_ab), or with "
+                         "--product the in-tree product build's (nvflare_amd/lib/obj), so a one-unit A/B links in "
+                         "minutes")
     args = ap.parse_args()
     with tempfile.TemporaryDirectory() as tmp:
         if args.rev == "WORKTREE":  # the working tree's sources as they are
@@ -57,21 +61,24 @@ def main():
         csrc = os.path.join(tmp, "nvflare_amd", "csrc")
         inc = [f"-I{os.path.join(tmp, 'include')}", f"-I{csrc}"]
         # an A/B library: every kernel form the sources know (-DFEDAVG_AB; ignored by revisions before round 5)
-        units = B.compile_units([s for s in B.SOURCES if os.path.exists(os.path.join(csrc, s))], ab=True)
+        units = B.compile_units([s for s in B.SOURCES if os.path.exists(os.path.join(csrc, s))], ab=not args.product)
         only = [x for x in args.only.split(",") if x]
         if only and args.rev != "WORKTREE":
             raise SystemExit("--only needs --rev WORKTREE (the reused objects are the working tree's)")
-        if only and not os.path.isdir(AB_OBJ):
-            raise SystemExit(f"--only reuses the objects of a full --rev WORKTREE build ({AB_OBJ}): run one first")
+        reuse = B.OBJ_DIR if args.product else AB_OBJ  # --product: the in-tree product build's objects
+        if only and not os.path.isdir(reuse):
+            raise SystemExit(f"--only reuses the objects of a full build ({reuse}): run one first")
+        if only and args.product and B.needs_build():
+            raise SystemExit("--only --product reuses the in-tree objects: build the in-tree library first")
 
         def compile_one(unit):
             src, obj_name, extra = unit
-            if only and src not in only:
-                return os.path.join(AB_OBJ, obj_name)
+            if only and src not in only and obj_name not in only:  # a source, or one object (fedavg_epi_torch_div.hip.o)
+                return os.path.join(reuse, obj_name)
             obj = os.path.join(tmp, obj_name)
-            defs = [f"-D{d}" for d in ["FEDAVG_AB"] + args.defines]
+            defs = [f"-D{d}" for d in ([] if args.product else ["FEDAVG_AB"]) + args.defines]
             subprocess.run([B.HIPCC, *B.FLAGS, *extra, *defs, *inc, "-c", os.path.join(csrc, src), "-o", obj], check=True)
-            if args.rev == "WORKTREE" and not only and not args.defines:  # the objects a later --only run reuses
+            if args.rev == "WORKTREE" and not only and not args.defines and not args.product:  # for a later --only
                 os.makedirs(AB_OBJ, exist_ok=True)
                 shutil.copy(obj, os.path.join(AB_OBJ, obj_name))
             return obj
