@@ -200,13 +200,16 @@ inline bool epi_direct(int op, int fin, int k, bool acc_in) {
 struct FewForm {
     int bpc, r, l, g;
 };
-// the product's form per read count (profiles/r05: A/B sweep of the forms below, interleaved in one process)
-constexpr FewForm kFewDefault[3] = {{0, 0, 0, 0}, {2, 8, 4, 4}, {2, 4, 4, 2}};
+// the product's form per read count: the best of the sweep (profiles/r05/s2/few_k*.jsonl, 1e9 params, interleaved in
+// one process, % of 8 TB/s): 1 read -- two blocks per CU, 8 register- + 4 LDS-held tiles, LDS tiles loaded two at a
+// time (75.2, against 74.4 four at a time, 71.5 with 10 LDS tiles at one block per CU); 2 reads -- one block per CU,
+// 4 register- + 10 LDS-held tiles, two at a time (77.2, against 74.1 at two blocks per CU with 4 LDS tiles, 76.7 with
+// 6 + 9, 71.2 loading 4 LDS tiles together)
+constexpr FewForm kFewDefault[3] = {{0, 0, 0, 0}, {2, 8, 4, 2}, {1, 4, 10, 2}};
 // A/B builds: launch variant bits 9-11 pick one of these per read count (1-6; 0 = the default)
 constexpr FewForm kFewAB[2][6] = {
-    {{2, 8, 4, 4}, {2, 8, 4, 2}, {1, 8, 10, 5}, {2, 8, 0, 1}, {2, 4, 4, 4}, {1, 8, 8, 4}},
-    {{2, 4, 4, 2}, {2, 4, 4, 4}, {1, 4, 10, 2}, {1, 6, 9, 3}, {2, 6, 4, 2}, {2, 4, 0, 1}}};
-
+    {{2, 8, 4, 2}, {2, 8, 4, 1}, {2, 6, 4, 2}, {1, 8, 10, 2}, {2, 8, 4, 4}, {2, 8, 2, 2}},
+    {{1, 4, 10, 2}, {1, 4, 10, 1}, {1, 4, 10, 5}, {1, 2, 10, 2}, {1, 6, 10, 2}, {2, 4, 4, 2}}};
 // the few-client form of a launch with `reads` (1 or 2) client reads
 inline FewForm few_form(int reads, int variant) {
     if (kABFew) {

@@ -389,22 +389,22 @@ inline hipError_t launch_few(const TileLaunch& L, hipStream_t s, uint64_t* nl) {
 #define FEDAVG_FEW(R, LL, G)                                                       \
     if (f.r == R && f.l == LL && f.g == G) return launch_few_form<OP, FIN, KC, R, LL, G>(L, s, nl);
     if constexpr (KC == 1) {
-        FEDAVG_FEW(8, 4, 4)
+        FEDAVG_FEW(8, 4, 2)
         if constexpr (kABFew) {
-            FEDAVG_FEW(8, 4, 2)
-            FEDAVG_FEW(8, 10, 5)
-            FEDAVG_FEW(8, 0, 1)
-            FEDAVG_FEW(4, 4, 4)
-            FEDAVG_FEW(8, 8, 4)
+            FEDAVG_FEW(8, 4, 1)
+            FEDAVG_FEW(6, 4, 2)
+            FEDAVG_FEW(8, 10, 2)
+            FEDAVG_FEW(8, 4, 4)
+            FEDAVG_FEW(8, 2, 2)
         }
     } else {
-        FEDAVG_FEW(4, 4, 2)
+        FEDAVG_FEW(4, 10, 2)
         if constexpr (kABFew) {
-            FEDAVG_FEW(4, 4, 4)
-            FEDAVG_FEW(4, 10, 2)
-            FEDAVG_FEW(6, 9, 3)
-            FEDAVG_FEW(6, 4, 2)
-            FEDAVG_FEW(4, 0, 1)
+            FEDAVG_FEW(4, 10, 1)
+            FEDAVG_FEW(4, 10, 5)
+            FEDAVG_FEW(2, 10, 2)
+            FEDAVG_FEW(6, 10, 2)
+            FEDAVG_FEW(4, 4, 2)
         }
     }
 #undef FEDAVG_FEW
