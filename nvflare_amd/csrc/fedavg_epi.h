@@ -90,20 +90,27 @@ __device__ __forceinline__ EpiIn epi_load(const EpiParams& E, const int64_t i) {
     return in;
 }
 
-// The epilogues' sqrt and constant-divisor quotient in two forms (round 5): FAST -- straight-line, each rare input
-// (sqrt_torch_cpu / sqrt_mkl_rsqrtps callouts, div_const outside its checked range) only noted in `slow`; exact -- the
-// per-element forms with their branches.  epilogue4 computes a column group FAST and recomputes it exactly when any
-// lane noted a rare input, so the common case has one branch per column group instead of one per sqrt and quotient.
-template <int SQ, bool FAST>
+// The epilogues' sqrt and constant-divisor quotient (round 5), in one of three forms EM, every one bit-identical:
+// kEmFast -- straight-line, each rare input (sqrt_torch_cpu / sqrt_mkl_rsqrtps callouts, div_const outside its checked
+// range) only noted in `slow`; epilogue4 recomputes the column group with kEmElem when any lane noted one, so the
+// common case has one branch per column group instead of one per sqrt and quotient; kEmElem -- the per-element forms
+// with their rare-case branches (round 4); kEmIeee -- the constant-divisor quotients as the IEEE division, branch-free
+// (round 3), the sqrt per element.
+constexpr int kEmFast = 0;
+constexpr int kEmElem = 1;
+constexpr int kEmIeee = 2;
+
+template <int SQ, int EM>
 __device__ __forceinline__ float sqrt_x(const EpiParams& E, const float x, uint32_t& slow) {
-    if constexpr (FAST && SQ == kEpiTorchSqrt) return sqrt_torch_cpu_fast(x, slow);
-    if constexpr (FAST && SQ == kEpiTorchSqrtAmd) return sqrt_mkl_rsqrtps_fast(x, slow);
+    if constexpr (EM == kEmFast && SQ == kEpiTorchSqrt) return sqrt_torch_cpu_fast(x, slow);
+    if constexpr (EM == kEmFast && SQ == kEpiTorchSqrtAmd) return sqrt_mkl_rsqrtps_fast(x, slow);
     return sqrt_e<SQ>(E, x);
 }
 
-template <bool FAST>
+template <int EM>
 __device__ __forceinline__ float div_x(const float a, const FinConst& f, uint32_t& slow) {
-    if constexpr (FAST) return div_const_fast(a, f, slow);
+    if constexpr (EM == kEmFast) return div_const_fast(a, f, slow);
+    if constexpr (EM == kEmIeee) return a / f.v;
     return div_const(a, f);
 }
 
@@ -118,7 +125,7 @@ constexpr bool epi_has_rare() {
 }
 
 // one column group's optimizer step: the new parameter (ADD_BASE: the result) in .a, the new states in .b / .c / .d
-template <int EPI, bool FAST>
+template <int EPI, int EM>
 __device__ __forceinline__ EpiIn epi_compute(const EpiParams& E, const EpiConsts& C, const f32x4 d, const EpiIn& in,
                                              uint32_t& slow) {
     constexpr int KIND = EPI & 0xFF;
@@ -150,7 +157,7 @@ __device__ __forceinline__ EpiIn epi_compute(const EpiParams& E, const EpiConsts
             float g = E.maximize ? d[c] : -d[c];
             if (E.has_weight_decay) g = __builtin_fmaf(p[c], E.weight_decay, g);  // grad.add(param, alpha=wd)
             sum[c] = __builtin_fmaf(g, g, sum[c]);                                 // state_sum.addcmul_(g, g, value=1)
-            const float std_ = sqrt_x<TSQ, FAST>(E, sum[c], slow) + E.eps;        // state_sum.sqrt().add_(eps)
+            const float std_ = sqrt_x<TSQ, EM>(E, sum[c], slow) + E.eps;        // state_sum.sqrt().add_(eps)
             p[c] = p[c] + (E.step_size_neg * g) / std_;                            // param.addcdiv_(g, std, value=-clr)
         }
         o.a = p;
@@ -168,9 +175,9 @@ __device__ __forceinline__ EpiIn epi_compute(const EpiParams& E, const EpiConsts
             float avg;
             if (E.centered) {
                 ga[c] = lerp_torch(ga[c], g, E.one_minus_beta1, E.one_minus_beta1_m1);  // grad_avg.lerp_(g, 1-alpha)
-                avg = sqrt_x<TSQ, FAST>(E, __builtin_fmaf(-ga[c], ga[c], sq[c]), slow);  // addcmul(ga, ga, -1).sqrt_()
+                avg = sqrt_x<TSQ, EM>(E, __builtin_fmaf(-ga[c], ga[c], sq[c]), slow);  // addcmul(ga, ga, -1).sqrt_()
             } else {
-                avg = sqrt_x<TSQ, FAST>(E, sq[c], slow);
+                avg = sqrt_x<TSQ, EM>(E, sq[c], slow);
             }
             avg = avg + E.eps;
             if (E.has_momentum) {
@@ -249,13 +256,13 @@ __device__ __forceinline__ EpiIn epi_compute(const EpiParams& E, const EpiConsts
             v[c] = __builtin_fmaf(E.one_minus_beta2 * g, g, v[c] * E.beta2);
             if constexpr (KIND == FEDAVG_EPI_NADAM) {
                 // exp_avg_sq.div(bc2).sqrt().add_(eps)
-                const float denom = sqrt_x<TSQ, FAST>(E, div_x<FAST>(v[c], C.bc2, slow), slow) + E.eps;
+                const float denom = sqrt_x<TSQ, EM>(E, div_x<EM>(v[c], C.bc2, slow), slow) + E.eps;
                 pv = pv + (E.coef_grad * g) / denom;                                    // addcdiv_(grad, denom, value)
                 pv = pv + (E.coef_avg * m[c]) / denom;                                  // addcdiv_(exp_avg, denom, value)
             } else {
-                float t = div_x<FAST>(m[c], C.bc1, slow) * E.lr;                        // exp_avg / bc1 * lr
+                float t = div_x<EM>(m[c], C.bc1, slow) * E.lr;                        // exp_avg / bc1 * lr
                 if (E.rectified) {
-                    const float a = (1.0f / (sqrt_x<TSQ, FAST>(E, v[c], slow) + E.eps)) * E.bias_correction2_sqrt;
+                    const float a = (1.0f / (sqrt_x<TSQ, EM>(E, v[c], slow) + E.eps)) * E.bias_correction2_sqrt;
                     t = (t * a) * E.rect;                                               // bc2**0.5 / (sqrt+eps)
                 }
                 pv = __builtin_fmaf(t, -1.0f, pv);                                      // param.add_(..., alpha=-1)
@@ -285,7 +292,7 @@ __device__ __forceinline__ EpiIn epi_compute(const EpiParams& E, const EpiConsts
                 vmax[c] = max_torch(vmax[c], vv);
                 vden = vmax[c];
             }
-            const float denom = div_x<FAST>(sqrt_x<TSQ, FAST>(E, vden, slow), C.bc2s, slow) + E.eps;  // sqrt(v)/sqrt(bc2)+eps
+            const float denom = div_x<EM>(sqrt_x<TSQ, EM>(E, vden, slow), C.bc2s, slow) + E.eps;  // sqrt(v)/sqrt(bc2)+eps
             pv = pv + (E.step_size_neg * mm) / denom;
             m[c] = mm;
             v[c] = vv;
@@ -329,29 +336,52 @@ __device__ __forceinline__ void epi_store(const EpiParams& E, const int64_t i, c
     }
 }
 
-template <int EPI>
+template <int EPI, int EM>
 __device__ __forceinline__ void epilogue4(const EpiParams& E, const EpiConsts& C, const int64_t i, const f32x4 d,
                                           const EpiIn& in, f32x4* out) {
-#if defined(FEDAVG_AB_EPI_EXACT)  // A/B builds only: round 4's per-element rare-case branches
-    {
+    if constexpr (EM != kEmFast || !epi_has_rare<EPI>()) {
         uint32_t unused = 0;
-        epi_store<EPI>(E, i, epi_compute<EPI, false>(E, C, d, in, unused), out);
-        return;
-    }
-#endif
-    uint32_t slow = 0;
-    if constexpr ((EPI & 0xFF) == FEDAVG_EPI_ADAM) slow = C.bc2s.fast ? 0u : 1u;
-    if constexpr ((EPI & 0xFF) == FEDAVG_EPI_NADAM) slow = C.bc2.fast ? 0u : 1u;
-    if constexpr ((EPI & 0xFF) == FEDAVG_EPI_RADAM) slow = C.bc1.fast ? 0u : 1u;
-    EpiIn o = epi_compute<EPI, epi_has_rare<EPI>()>(E, C, d, in, slow);
-    if constexpr (epi_has_rare<EPI>()) {
+        epi_store<EPI>(E, i, epi_compute<EPI, EM == kEmFast ? kEmElem : EM>(E, C, d, in, unused), out);
+    } else {
+        uint32_t slow = 0;
+        if constexpr ((EPI & 0xFF) == FEDAVG_EPI_ADAM) slow = C.bc2s.fast ? 0u : 1u;
+        if constexpr ((EPI & 0xFF) == FEDAVG_EPI_NADAM) slow = C.bc2.fast ? 0u : 1u;
+        if constexpr ((EPI & 0xFF) == FEDAVG_EPI_RADAM) slow = C.bc1.fast ? 0u : 1u;
+        EpiIn o = epi_compute<EPI, kEmFast>(E, C, d, in, slow);
         if (__builtin_expect(slow != 0u, 0)) {
             uint32_t unused = 0;
-            o = epi_compute<EPI, false>(E, C, d, in, unused);
+            o = epi_compute<EPI, kEmElem>(E, C, d, in, unused);
         }
+        epi_store<EPI>(E, i, o, out);
     }
-    epi_store<EPI>(E, i, o, out);
 }
+
+// the finalisation of one tile's CPL columns in the epilogue's form: one rare-case branch for the tile (kEmFast),
+// per element (kEmElem), or the IEEE division (kEmIeee)
+template <int FIN, int EM, int CPL>
+__device__ __forceinline__ void fin_tile_em(f32x4 (&r)[CPL], const f32x4 (&a)[CPL], const FinConst& f) {
+    if constexpr (EM == kEmFast) {
+        fin_tile<FIN, CPL>(r, a, f);
+    } else if constexpr (EM == kEmElem) {
+#pragma unroll
+        for (int c = 0; c < CPL; ++c) r[c] = fin4c<FIN>(a[c], f);
+    } else {
+#pragma unroll
+        for (int c = 0; c < CPL; ++c) r[c] = fin4<FIN>(a[c], f.v);
+    }
+}
+
+// the forms the kernels use (A/B builds: -DFEDAVG_EM_TILE=n / -DFEDAVG_EM_BURST=n)
+#if defined(FEDAVG_EM_TILE)
+constexpr int kEmTile = FEDAVG_EM_TILE;
+#else
+constexpr int kEmTile = kEmFast;
+#endif
+#if defined(FEDAVG_EM_BURST)
+constexpr int kEmBurst = FEDAVG_EM_BURST;
+#else
+constexpr int kEmBurst = kEmFast;
+#endif
 
 // PIPE: software-pipelined across tiles -- after the client loop of tile t the lane issues the epilogue
 // operand loads of t, then the first UNROLL client loads of its next tile, and only then waits for the
@@ -399,7 +429,7 @@ fedavg_tiles_epi_burst_f32x4(const RowTableF32 tab, const int K, const int64_t t
         if (t < t_end) {
             f32x4 acc[CPL];
             sum(acc, t);
-            fin_tile<FIN, CPL>(dd[m], acc, fc);
+            fin_tile_em<FIN, kEmBurst, CPL>(dd[m], acc, fc);
         }
     }
 #pragma unroll 1
@@ -408,7 +438,7 @@ fedavg_tiles_epi_burst_f32x4(const RowTableF32 tab, const int K, const int64_t t
         if (t < t_end) {
             f32x4 acc[CPL], r[CPL];
             sum(acc, t);
-            fin_tile<FIN, CPL>(r, acc, fc);
+            fin_tile_em<FIN, kEmBurst, CPL>(r, acc, fc);
 #pragma unroll
             for (int c = 0; c < CPL; ++c) staged[((m - TPB) * CPL + c) * kBlock + threadIdx.x] = r[c];
         }
@@ -442,7 +472,7 @@ fedavg_tiles_epi_burst_f32x4(const RowTableF32 tab, const int K, const int64_t t
                 if (i >= b4 && i < e4) {
                     const f32x4 d = d_of(c);
                     if (out != nullptr && (EPI & 0xFF) != FEDAVG_EPI_ADD_BASE) store4<true>(out + i, d);
-                    epilogue4<EPI>(E, C, i, d, cur[c], out);
+                    epilogue4<EPI, kEmBurst>(E, C, i, d, cur[c], out);
                 }
             }
         }
@@ -561,22 +591,90 @@ __global__ void __launch_bounds__(kBlock) fedavg_tiles_epi_f32x4(const RowTableF
             }
         }
         f32x4 dv[CPL];
-#if defined(FEDAVG_AB_EPI_EXACT)  // A/B builds only: round 4's per-element finalisation
-#pragma unroll
-        for (int c = 0; c < CPL; ++c) dv[c] = fin4c<FIN>(acc[c], fc);
-#else
-        fin_tile<FIN, CPL>(dv, acc, fc);
-#endif
+        fin_tile_em<FIN, kEmTile, CPL>(dv, acc, fc);
 #pragma unroll
         for (int c = 0; c < CPL; ++c) {
             const int64_t i = col + c * kBlock;
             if (i >= b4 && i < e4) {
                 if (out != nullptr && (EPI & 0xFF) != FEDAVG_EPI_ADD_BASE) store4<true>(out + i, dv[c]);
-                epilogue4<EPI>(E, C, i, dv[c], pre[c], out);
+                epilogue4<EPI, kEmTile>(E, C, i, dv[c], pre[c], out);
             }
         }
     }
 }
+
+// FEW-CLIENT fused form (round 5): 2-3 client reads, no chained sum.  The per-tile form above stores
+// each tile's new parameters and states as it finishes -- small writes scattered through the read stream, the shape
+// the HBM handles worst (profiles/r04/s2/epi_r2.jsonl: the library's per-tile form 70.6 % of 8 TB/s at 2 clients) --
+// while the epilogue-shaped burst probe that holds REG tiles' results on chip and stores them at the end of a short
+// launch measured 76.3 % (e_burst_r4: one block per CU, 4 register-held tiles).  This is that shape with the real
+// arithmetic: per tile its operands (p, m, v ...) and client rows are loaded, d = fin(sum) and the optimizer step
+// computed, the new values held in registers; after the block's REG tiles every result is stored.  K (2 or 3 here,
+// any count is correct) is a launch argument: groups of up to four clients' loads, then their arrival-ordered steps.
+template <int OP, int FIN, int EPI, int REG>
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, 1)))
+fedavg_tiles_epi_few_f32x4(const RowTableF32 tab, const int K, const int64_t tstride4, f32x4* out, const int64_t b4,
+                           const int64_t e4, const float fin_val, const EpiParams E, const int64_t t0, const int64_t t_end) {
+    constexpr int CPL = kDefaultTile / (4 * kBlock);
+    constexpr int64_t T4 = (int64_t)CPL * kBlock;
+    const FinConst fc = fin_const<FIN>(fin_val);
+    const EpiConsts C = epi_consts<EPI>(E);
+    if constexpr ((EPI & kEpiTorchSqrt) != 0) rsqrt14_stage();
+    if constexpr ((EPI & kEpiTorchSqrtAmd) != 0) rsqrtps_stage(E.rsqrtps);
+    EpiIn res[REG][CPL];
+#pragma unroll
+    for (int m = 0; m < REG; ++m) {
+        const int64_t t = t0 + blockIdx.x + (int64_t)m * gridDim.x;
+        if (t < t_end) {
+            EpiIn in[CPL];
+#pragma unroll
+            for (int c = 0; c < CPL; ++c) {
+                int64_t i = t * T4 + threadIdx.x + c * kBlock;
+                i = i < b4 ? b4 : (i >= e4 ? e4 - 1 : i);  // a partial edge tile: in-range operands, not stored
+                in[c] = epi_load<EPI>(E, i);
+            }
+            f32x4 acc[CPL];
+            const int64_t off = t * tstride4 + threadIdx.x;
+            tile_sum_rrem<OP, false, CPL>(acc, tab, K, off, t * T4 + threadIdx.x, nullptr, b4, e4);
+            f32x4 dv[CPL];
+            fin_tile_em<FIN, kEmBurst, CPL>(dv, acc, fc);
+#pragma unroll
+            for (int c = 0; c < CPL; ++c) {
+                const int64_t i = t * T4 + threadIdx.x + c * kBlock;
+                if (out != nullptr && (EPI & 0xFF) != FEDAVG_EPI_ADD_BASE && i >= b4 && i < e4)
+                    store4<true>(out + i, dv[c]);  // the aggregate itself, when asked for (not held: rare)
+                uint32_t slow = 0;
+                if constexpr ((EPI & 0xFF) == FEDAVG_EPI_ADAM) slow = C.bc2s.fast ? 0u : 1u;
+                if constexpr ((EPI & 0xFF) == FEDAVG_EPI_NADAM) slow = C.bc2.fast ? 0u : 1u;
+                if constexpr ((EPI & 0xFF) == FEDAVG_EPI_RADAM) slow = C.bc1.fast ? 0u : 1u;
+                if constexpr (epi_has_rare<EPI>()) {
+                    res[m][c] = epi_compute<EPI, kEmFast>(E, C, dv[c], in[c], slow);
+                    if (__builtin_expect(slow != 0u, 0)) {
+                        uint32_t unused = 0;
+                        res[m][c] = epi_compute<EPI, kEmElem>(E, C, dv[c], in[c], unused);
+                    }
+                } else {
+                    res[m][c] = epi_compute<EPI, kEmElem>(E, C, dv[c], in[c], slow);
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int m = 0; m < REG; ++m) {
+        const int64_t t = t0 + blockIdx.x + (int64_t)m * gridDim.x;
+        if (t < t_end) {
+#pragma unroll
+            for (int c = 0; c < CPL; ++c) {
+                const int64_t i = t * T4 + threadIdx.x + c * kBlock;
+                if (i >= b4 && i < e4) epi_store<EPI>(E, i, res[m][c], out);
+            }
+        }
+    }
+}
+
+// register-held tiles per block per launch of the few-client fused form (one block per CU); A/B builds with
+// -DFEDAVG_AB_FEW sweep others through launch variant bits 9-11 (torch-mode FIN_DIV Adam with the AMD-host sqrt only)
+constexpr int kEpiFewReg = 4;  // (fedavg_capi.cpp routes 2 .. kEpiFewMaxReads client reads without a chained sum here)
 
 // A/B of the burst kernel's client loop (launch variant bits 9-11 = LOOP 1-4), instantiated for one configuration only:
 // torch-mode FIN_DIV Adam with the AMD-host sqrt, no chained partial sum (bench.py --epilogue adam on the pool's boxes)
@@ -613,10 +711,41 @@ inline bool epi_loop_ab(const TileLaunch& L, const EpiParams& E, hipStream_t s, 
 // (fedavg_internal.h kAB): the burst form with 4 (two blocks per CU) or 9 (one block per CU) LDS-held tiles without a
 // chained sum, the pipelined per-tile form; A/B builds also the register-only burst form, the burst form over a
 // chained sum, the unpipelined per-tile form and the client-loop shapes.
+template <int OP, int FIN, int EPI, int REG>
+inline hipError_t launch_epi_few(const TileLaunch& L, const EpiParams& E, hipStream_t s, uint64_t* nl) {
+    f32x4* o = reinterpret_cast<f32x4*>(L.out);
+    return burst_launches(L.b4 / L.tile4, (L.e4 - 1) / L.tile4 + 1, L.grid, REG, nl, L.variant & kVariantAnyOrder,
+                          [&](int nb, int64_t t0, int64_t t_end, uint32_t flags) {
+                              hipExtLaunchKernelGGL((fedavg_tiles_epi_few_f32x4<OP, FIN, EPI, REG>), dim3(nb),
+                                                    dim3(kBlock), 0, s, nullptr, nullptr, flags, L.tab, L.k, L.tstride4,
+                                                    o, L.b4, L.e4, L.fin_val, E, t0, t_end);
+                          });
+}
+
+// the few-client fused form's register-held tiles: kEpiFewReg, or (A/B builds with -DFEDAVG_AB_FEW, torch-mode
+// FIN_DIV Adam with the AMD-host sqrt) launch variant bits 9-11: 1-5 = 2, 3, 5, 6, 8 tiles
+template <int OP, int FIN, int EPI>
+inline hipError_t launch_epi_few_any(const TileLaunch& L, const EpiParams& E, hipStream_t s, uint64_t* nl) {
+    if constexpr (kABFew && OP == FEDAVG_OP_TORCH && FIN == FEDAVG_FIN_DIV && EPI == (FEDAVG_EPI_ADAM | kEpiTorchSqrtAmd)) {
+        switch ((L.variant >> kVariantLoopShift) & 7) {
+            case 1: return launch_epi_few<OP, FIN, EPI, 2>(L, E, s, nl);
+            case 2: return launch_epi_few<OP, FIN, EPI, 3>(L, E, s, nl);
+            case 3: return launch_epi_few<OP, FIN, EPI, 5>(L, E, s, nl);
+            case 4: return launch_epi_few<OP, FIN, EPI, 6>(L, E, s, nl);
+            case 5: return launch_epi_few<OP, FIN, EPI, 8>(L, E, s, nl);
+            default: break;
+        }
+    }
+    return launch_epi_few<OP, FIN, EPI, kEpiFewReg>(L, E, s, nl);
+}
+
 template <int OP, int FIN, bool ACC_IN, int EPI>
 inline hipError_t launch_epi_k(const TileLaunch& L, const EpiParams& E, hipStream_t s, uint64_t* nl) {
     const f32x4* ai = reinterpret_cast<const f32x4*>(L.acc_in);
     f32x4* o = reinterpret_cast<f32x4*>(L.out);
+    if constexpr (!ACC_IN) {
+        if (L.variant & kVariantEpiFew) return launch_epi_few_any<OP, FIN, EPI>(L, E, s, nl);
+    }
     if constexpr (kAB || !ACC_IN) {
         if (!(L.variant & (kVariantTileStores | kVariantEpiPrefetch))) {  // burst: one launch per grid x TPB tiles
             if constexpr (kAB) {

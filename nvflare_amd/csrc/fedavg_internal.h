@@ -56,6 +56,8 @@ constexpr int kVariantLoopShift = 9;       // bits 9-11: A/B shapes of the burst
                                            // (fedavg_epi.h launch_epi_loop_ab, fedavg_tiles.h launch_burst)
 constexpr int kVariantFew = 1 << 12;      // inside TileLaunch: the few-client burst kernel (fedavg_tiles.h
                                            // fedavg_tiles_few_f32x4), set by run_tiles for 1-2 reads, no chained sum
+constexpr int kVariantEpiFew = 1 << 13;   // inside TileLaunch: the few-client fused kernel (fedavg_epi.h
+                                           // fedavg_tiles_epi_few_f32x4), 2-3 client reads, no chained sum
 // public variant bits a product build accepts (fedavg_set_variant): the fused per-tile pipelined form (2), burst
 // launches without the barrier bit (16), the 4-LDS-tile form on one-block-per-CU grids (64) -- each a routed form
 constexpr int kVariantProductMask = kVariantEpiPrefetch | kVariantAnyOrder | kVariantWideLds;
@@ -200,16 +202,17 @@ inline bool epi_direct(int op, int fin, int k, bool acc_in) {
 struct FewForm {
     int bpc, r, l, g;
 };
-// the product's form per read count: the best of the sweep (profiles/r05/s2/few_k*.jsonl, 1e9 params, interleaved in
-// one process, % of 8 TB/s): 1 read -- two blocks per CU, 8 register- + 4 LDS-held tiles, LDS tiles loaded two at a
-// time (75.2, against 74.4 four at a time, 71.5 with 10 LDS tiles at one block per CU); 2 reads -- one block per CU,
-// 4 register- + 10 LDS-held tiles, two at a time (77.2, against 74.1 at two blocks per CU with 4 LDS tiles, 76.7 with
-// 6 + 9, 71.2 loading 4 LDS tiles together)
-constexpr FewForm kFewDefault[3] = {{0, 0, 0, 0}, {2, 8, 4, 2}, {1, 4, 10, 2}};
+// the product's form per read count: the best of two sweeps (profiles/r05/s2/few_k*.jsonl, s3/few_k*.jsonl; 1e9
+// params, interleaved in one process, outputs bit-equal, % of 8 TB/s): 1 read -- two blocks per CU, 8 register- + 4
+// LDS-held tiles, LDS tiles loaded two at a time (75.2 / 74.6, against 74.4 / 73.8 four at a time, 72.2 one at a time,
+// 71.5 / 73.5 with 10 LDS tiles at one block per CU); 2 reads -- one block per CU, 4 register- + 10 LDS-held tiles, one
+// LDS tile's loads at a time (78.9, against 77.2 two at a time, 75.3 five, 77.5 with 6 register tiles, 74.1 / 73.8 at
+// two blocks per CU).  The same box's 1 : 1 and 2 : 1 burst patterns: 74.5 / 77.2 % (s3/mix_r*.jsonl).
+constexpr FewForm kFewDefault[3] = {{0, 0, 0, 0}, {2, 8, 4, 2}, {1, 4, 10, 1}};
 // A/B builds: launch variant bits 9-11 pick one of these per read count (1-6; 0 = the default)
 constexpr FewForm kFewAB[2][6] = {
-    {{2, 8, 4, 2}, {2, 8, 4, 1}, {2, 6, 4, 2}, {1, 8, 10, 2}, {2, 8, 4, 4}, {2, 8, 2, 2}},
-    {{1, 4, 10, 2}, {1, 4, 10, 1}, {1, 4, 10, 5}, {1, 2, 10, 2}, {1, 6, 10, 2}, {2, 4, 4, 2}}};
+    {{2, 8, 4, 2}, {1, 12, 10, 2}, {1, 8, 10, 1}, {2, 10, 4, 2}, {2, 8, 4, 4}, {1, 16, 10, 2}},
+    {{1, 4, 10, 1}, {1, 6, 10, 1}, {1, 5, 10, 1}, {1, 4, 9, 1}, {1, 3, 10, 1}, {1, 4, 10, 2}}};
 // the few-client form of a launch with `reads` (1 or 2) client reads
 inline FewForm few_form(int reads, int variant) {
     if (kABFew) {

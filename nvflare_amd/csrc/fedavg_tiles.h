@@ -391,20 +391,20 @@ inline hipError_t launch_few(const TileLaunch& L, hipStream_t s, uint64_t* nl) {
     if constexpr (KC == 1) {
         FEDAVG_FEW(8, 4, 2)
         if constexpr (kABFew) {
-            FEDAVG_FEW(8, 4, 1)
-            FEDAVG_FEW(6, 4, 2)
-            FEDAVG_FEW(8, 10, 2)
+            FEDAVG_FEW(12, 10, 2)
+            FEDAVG_FEW(8, 10, 1)
+            FEDAVG_FEW(10, 4, 2)
             FEDAVG_FEW(8, 4, 4)
-            FEDAVG_FEW(8, 2, 2)
+            FEDAVG_FEW(16, 10, 2)
         }
     } else {
-        FEDAVG_FEW(4, 10, 2)
+        FEDAVG_FEW(4, 10, 1)
         if constexpr (kABFew) {
-            FEDAVG_FEW(4, 10, 1)
-            FEDAVG_FEW(4, 10, 5)
-            FEDAVG_FEW(2, 10, 2)
-            FEDAVG_FEW(6, 10, 2)
-            FEDAVG_FEW(4, 4, 2)
+            FEDAVG_FEW(6, 10, 1)
+            FEDAVG_FEW(5, 10, 1)
+            FEDAVG_FEW(4, 9, 1)
+            FEDAVG_FEW(3, 10, 1)
+            FEDAVG_FEW(4, 10, 2)
         }
     }
 #undef FEDAVG_FEW

@@ -518,3 +518,90 @@ def test_rmsprop_epilogue(ctx, oracle, K, hp):
             assert same_bits(dev.get("buf"), buf) and same_bits(dev.get("ga"), ga), step
         finally:
             dev.close()
+
+
+FEW_CASES = [  # (kind, hp, state names): every optimizer kind through the few-client fused form
+    (1, dict(), ()),
+    (2, dict(lr=0.5, momentum=0.9, nesterov=1, weight_decay=1e-3, dampening=0.1), ("m",)),
+    (3, dict(lr=1e-3, beta1=0.9, beta2=0.999, eps=1e-8), ("m", "v")),
+    (3, dict(lr=1e-3, beta1=0.5, beta2=0.9, eps=1e-8, amsgrad=1, weight_decay=1e-2, decoupled_weight_decay=1),
+     ("m", "v", "vmax")),
+    (4, dict(lr=1e-2, weight_decay=1e-3, eps=1e-8, maximize=1), ("m",)),
+    (5, dict(lr=1e-3, alpha=0.95, eps=1e-8, centered=1, momentum=0.5, maximize=1), ("m", "v", "vmax")),
+    (6, dict(lr=1e-2, beta1=0.8, beta2=0.95, eps=1e-6, weight_decay=1e-3), ("m", "v")),
+    (7, dict(lr=2e-3, beta1=0.9, beta2=0.999, eps=1e-8, momentum_decay=4e-3), ("m", "v")),
+    (8, dict(lr=1e-2, beta1=0.8, beta2=0.9, eps=1e-8, weight_decay=1e-3), ("m", "v")),
+    (9, dict(etaminus=0.5, etaplus=1.2, step_size_min=1e-6, step_size_max=50.0), ("m", "v")),
+    (10, dict(lambd=1e-4, eta=1e-2, mu=0.5, weight_decay=1e-3), ("m",)),
+]
+
+
+@pytest.mark.parametrize("K", [2, 3])
+@pytest.mark.parametrize("case", range(len(FEW_CASES)))
+def test_few_client_fused_form(ctx, oracle, K, case):
+    """The few-client fused kernel (fedavg_epi.h fedavg_tiles_epi_few_f32x4, round 5: 2-3 client reads, no chained sum,
+    each tile's new parameters and states held in registers and stored at the end of a short launch) for every
+    optimizer kind: three launches of 4 tiles per block and CU (the last partial), a ragged end, states from a
+    non-zero start, two steps; every output and state bit for bit against the oracle.  ADD_BASE writes out; the Adam
+    case also asks for d in out."""
+    from nvflare_amd import _native as N_
+
+    kind, hp, names = FEW_CASES[case]
+    rng = np.random.default_rng(300 + 10 * case + K)
+    n = ctx.num_cus * 4 * 2 * TILE + 5 * TILE + 44
+    p = rng.standard_normal(n).astype(np.float32)
+    st = {"m": (rng.standard_normal(n) * 0.01).astype(np.float32),
+          "v": (rng.random(n) * 1e-4 + 1e-6).astype(np.float32),
+          "vmax": (rng.random(n) * 1e-4 + 1e-6).astype(np.float32)}
+    if kind == 9:  # Rprop: prev gradient, step sizes
+        st["v"] = np.full(n, 0.01, np.float32)
+    if kind == 4:  # Adagrad: a positive sum
+        st["m"] = np.abs(st["m"]) + np.float32(0.1)
+    if kind == 5:  # RMSprop centered: square_avg above grad_avg^2
+        st["m"] = (rng.random(n) * 1e-2 + 1e-3).astype(np.float32)
+        st["vmax"] = (rng.standard_normal(n) * 1e-3).astype(np.float32)
+    if kind == 10:  # ASGD: ax
+        st["m"] = p.copy()
+    base = rng.standard_normal(n).astype(np.float32)
+    sq = {"torch_sqrt": 2} if kind in (3, 4, 5, 7, 8) and case != 3 else {}
+    for step in (1, 2):
+        rows = [(rng.standard_normal(n) * 0.05).astype(np.float32) for _ in range(K)]
+        ws = [float(1 + (37 * k) % 100) for k in range(K)]
+        dev = _Dev(ctx, rows, n)
+        try:
+            ptr = {"p": dev.buf("p", p)}
+            for nm in names:
+                ptr[nm] = dev.buf(nm, st[nm])
+            out = None
+            if kind == 1:
+                e = _epi(1, base=dev.buf("base", base))
+                out = dev.buf("out")
+            else:
+                kw = dict(param=ptr["p"], step=float(step), **hp)
+                for nm, field in zip(names, ("state1", "state2", "state3")):
+                    kw[field] = ptr[nm]
+                if kind == 3 and case == 2:
+                    out = dev.buf("out")
+                if sq:
+                    ctx.load_rsqrtps(oracle.rsqrtps_table())
+                    kw.update(sq)
+                e = _epi(kind, **kw)
+            n_launch = ctx.launch_count()
+            ctx.accumulate_tiled_epi(dev.bases, ws, TILE, dev.lay.tile_stride, 0, dev.n4, out, N_.FEDAVG_OP_TORCH,
+                                     N_.FEDAVG_FIN_DIV, _sum(ws), e)
+            ctx.sync()
+            assert ctx.launch_count() - n_launch == 3  # the few-client form: grid x 4 tiles per launch
+            d = oracle.fedavg_c(rows, ws, oracle.MODE_TORCH, nthreads=8)
+            if kind == 1:
+                assert same_bits(dev.get("out"), oracle.epilogue_apply(d, oracle.EPI_ADD_BASE, base=base)), step
+                continue
+            if out is not None:
+                assert same_bits(dev.get("out"), d), step
+            kw = {k: st[nm] for k, nm in zip(("m", "v", "vmax"), names)}
+            oracle.epilogue_apply(d, kind, p=p, step=float(step), torch_cpu_sqrt="torch_cpu_amd" if sq else False,
+                                  **kw, **hp)
+            assert same_bits(dev.get("p"), p), (step, "p")
+            for nm in names:
+                assert same_bits(dev.get(nm), st[nm]), (step, nm)
+        finally:
+            dev.close()
