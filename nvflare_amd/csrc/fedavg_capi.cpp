@@ -374,7 +374,6 @@ double fin_scalar(int fin, double count) { return fin == FEDAVG_FIN_SCALE ? 1.0 
 constexpr int kBurstMinClients = 3;
 constexpr int kVariantFewBurst = 256;  // public variant bit 8: launches under kBurstMinClients reads keep the burst form
 constexpr int kEpiBurstMinClients = 4;
-constexpr int kEpiFewMaxReads = 3;  // fedavg_epi.h fedavg_tiles_epi_few_f32x4 takes 2-3 client reads
 
 // Tile-kernel launches over [b, e) (elements, multiples of 4) for any number of clients: chunks of at
 // most kMaxRowsPerLaunch clients, later chunks continuing in place through `out`.
@@ -1371,17 +1370,12 @@ int fedavg_accumulate_tiled_epi(fedavg_ctx* ctx, const void* const* bases, const
         // (product builds: the pipelined per-tile form at every read count under kEpiBurstMinClients -- at one read it
         // carries client 0, or nothing for the server step -- and for a chained sum; the unpipelined one is A/B only)
         const int reads = L.k + (cur_in ? 1 : 0);
-        // 2-3 client reads without a chained sum: the few-client fused form (round 5), unless the public variant asks
-        // for the per-tile form (bit 2, or bit 3 in A/B builds)
-        const bool few = !cur_in && reads >= 2 && reads <= kEpiFewMaxReads &&
-                         !(ctx->variant & (fedavg::kVariantEpiPrefetch | fedavg::kVariantTileStores));
-        if (!few && (reads < kEpiBurstMinClients || (!fedavg::kAB && cur_in)))
+        if (reads < kEpiBurstMinClients || (!fedavg::kAB && cur_in))
             L.variant |= (reads >= 2 || !fedavg::kAB) && !(ctx->variant & fedavg::kVariantTileStores)
                              ? fedavg::kVariantEpiPrefetch
                              : fedavg::kVariantTileStores;
-        if (few) L.variant |= fedavg::kVariantEpiFew;
-        const bool burst = !few && !(L.variant & (fedavg::kVariantEpiPrefetch | fedavg::kVariantTileStores));
-        const int bpc = few ? ctx->bpc(1) : burst ? ctx->bpc(L.k >= fedavg::kEpiOneBlockMinK ? 1 : 2) : ctx->bpc();
+        const bool burst = !(L.variant & (fedavg::kVariantEpiPrefetch | fedavg::kVariantTileStores));
+        const int bpc = burst ? ctx->bpc(L.k >= fedavg::kEpiOneBlockMinK ? 1 : 2) : ctx->bpc();
         // one block per CU: the LDS-held tiles fill the CU (9 instead of 4), unless the public variant has bit 6
         if (burst && bpc == 1 && !(ctx->variant & (fedavg::kVariantWideLds | fedavg::kVariantRegisterTiles)))
             L.variant |= fedavg::kVariantWideLds;

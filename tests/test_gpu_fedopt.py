@@ -538,12 +538,13 @@ FEW_CASES = [  # (kind, hp, state names): every optimizer kind through the few-c
 
 @pytest.mark.parametrize("K", [2, 3])
 @pytest.mark.parametrize("case", range(len(FEW_CASES)))
-def test_few_client_fused_form(ctx, oracle, K, case):
-    """The few-client fused kernel (fedavg_epi.h fedavg_tiles_epi_few_f32x4, round 5: 2-3 client reads, no chained sum,
-    each tile's new parameters and states held in registers and stored at the end of a short launch) for every
-    optimizer kind: three launches of 4 tiles per block and CU (the last partial), a ragged end, states from a
-    non-zero start, two steps; every output and state bit for bit against the oracle.  ADD_BASE writes out; the Adam
-    case also asks for d in out."""
+def test_few_client_fused_every_kind(ctx, oracle, K, case):
+    """2-3 client reads through the fused per-tile form (pipelined across tiles; the form most FedOpt jobs run) for
+    every optimizer kind and the Adam family's restated AMD-host sqrt: more tiles than blocks, a ragged end, states
+    from a non-zero start, two steps; every output and state bit for bit against the oracle.  ADD_BASE writes out;
+    one Adam case also asks for d in out.  (Round 5 also ran these against a register-held burst form of the fused
+    kernel, fedavg_tiles_epi_few_f32x4 -- bit-exact, but 53 % of HBM peak against the per-tile form's 69 %, so it
+    was dropped: DESIGN.md section 3.4.)"""
     from nvflare_amd import _native as N_
 
     kind, hp, names = FEW_CASES[case]
@@ -590,7 +591,7 @@ def test_few_client_fused_form(ctx, oracle, K, case):
             ctx.accumulate_tiled_epi(dev.bases, ws, TILE, dev.lay.tile_stride, 0, dev.n4, out, N_.FEDAVG_OP_TORCH,
                                      N_.FEDAVG_FIN_DIV, _sum(ws), e)
             ctx.sync()
-            assert ctx.launch_count() - n_launch == 3  # the few-client form: grid x 4 tiles per launch
+            assert ctx.launch_count() - n_launch == 1  # the per-tile form: one persistent launch
             d = oracle.fedavg_c(rows, ws, oracle.MODE_TORCH, nthreads=8)
             if kind == 1:
                 assert same_bits(dev.get("out"), oracle.epilogue_apply(d, oracle.EPI_ADD_BASE, base=base)), step
