@@ -1370,12 +1370,17 @@ int fedavg_accumulate_tiled_epi(fedavg_ctx* ctx, const void* const* bases, const
         // (product builds: the pipelined per-tile form at every read count under kEpiBurstMinClients -- at one read it
         // carries client 0, or nothing for the server step -- and for a chained sum; the unpipelined one is A/B only)
         const int reads = L.k + (cur_in ? 1 : 0);
-        if (reads < kEpiBurstMinClients || (!fedavg::kAB && cur_in))
+        // A/B builds with -DFEDAVG_AB_FEW: 2-3 client reads with launch variant bits 9-11 set take the register-held
+        // few-client fused form (one block per CU unless fedavg_set_launch says otherwise)
+        const bool few_ab = fedavg::kABFew && !cur_in && reads >= 2 && reads <= 3 &&
+                            ((ctx->variant >> fedavg::kVariantLoopShift) & 7) != 0;
+        if (few_ab) L.variant |= fedavg::kVariantEpiFew;
+        if (!few_ab && (reads < kEpiBurstMinClients || (!fedavg::kAB && cur_in)))
             L.variant |= (reads >= 2 || !fedavg::kAB) && !(ctx->variant & fedavg::kVariantTileStores)
                              ? fedavg::kVariantEpiPrefetch
                              : fedavg::kVariantTileStores;
-        const bool burst = !(L.variant & (fedavg::kVariantEpiPrefetch | fedavg::kVariantTileStores));
-        const int bpc = burst ? ctx->bpc(L.k >= fedavg::kEpiOneBlockMinK ? 1 : 2) : ctx->bpc();
+        const bool burst = !few_ab && !(L.variant & (fedavg::kVariantEpiPrefetch | fedavg::kVariantTileStores));
+        const int bpc = few_ab ? ctx->bpc(1) : burst ? ctx->bpc(L.k >= fedavg::kEpiOneBlockMinK ? 1 : 2) : ctx->bpc();
         // one block per CU: the LDS-held tiles fill the CU (9 instead of 4), unless the public variant has bit 6
         if (burst && bpc == 1 && !(ctx->variant & (fedavg::kVariantWideLds | fedavg::kVariantRegisterTiles)))
             L.variant |= fedavg::kVariantWideLds;

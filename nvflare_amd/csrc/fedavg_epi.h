@@ -651,6 +651,76 @@ __global__ void __launch_bounds__(kBlock) fedavg_tiles_epi_f32x4(const RowTableF
     }
 }
 
+// A/B ONLY (-DFEDAVG_AB_FEW): a register-held FEW-CLIENT fused form (round 5), 2-3 client reads.  The per-tile form above stores
+// each tile's new parameters and states as it finishes -- small writes scattered through the read stream, the shape
+// the HBM handles worst (profiles/r04/s2/epi_r2.jsonl: the library's per-tile form 70.6 % of 8 TB/s at 2 clients) --
+// while the epilogue-shaped burst probe that holds REG tiles' results on chip and stores them at the end of a short
+// launch measured 76.3 % (e_burst_r4: one block per CU, 4 register-held tiles).  This is that shape with the real
+// arithmetic: per tile its operands (p, m, v ...) and client rows are loaded, d = fin(sum) and the optimizer step
+// computed, the new values held in registers; after the block's REG tiles every result is stored.  K (2 or 3 here,
+// any count is correct) is a launch argument: groups of up to four clients' loads, then their arrival-ordered steps.
+template <int OP, int FIN, int EPI, int REG>
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, 2)))
+fedavg_tiles_epi_few_f32x4(const RowTableF32 tab, const int K, const int64_t tstride4, f32x4* out, const int64_t b4,
+                           const int64_t e4, const float fin_val, const EpiParams E, const int64_t t0, const int64_t t_end) {
+    constexpr int CPL = kDefaultTile / (4 * kBlock);
+    constexpr int64_t T4 = (int64_t)CPL * kBlock;
+    const FinConst fc = fin_const<FIN>(fin_val);
+    const EpiConsts C = epi_consts<EPI>(E);
+    if constexpr ((EPI & kEpiTorchSqrt) != 0) rsqrt14_stage();
+    if constexpr ((EPI & kEpiTorchSqrtAmd) != 0) rsqrtps_stage(E.rsqrtps);
+    EpiIn res[REG][CPL];
+#pragma unroll
+    for (int m = 0; m < REG; ++m) {
+        const int64_t t = t0 + blockIdx.x + (int64_t)m * gridDim.x;
+        if (t < t_end) {
+            EpiIn in[CPL];
+#pragma unroll
+            for (int c = 0; c < CPL; ++c) {
+                int64_t i = t * T4 + threadIdx.x + c * kBlock;
+                i = i < b4 ? b4 : (i >= e4 ? e4 - 1 : i);  // a partial edge tile: in-range operands, not stored
+                in[c] = epi_load<EPI>(E, i);
+            }
+            f32x4 acc[CPL];
+            const int64_t off = t * tstride4 + threadIdx.x;
+            tile_sum_rrem<OP, false, CPL>(acc, tab, K, off, t * T4 + threadIdx.x, nullptr, b4, e4);
+            f32x4 dv[CPL];
+            fin_tile_em<FIN, kEmBurst, CPL>(dv, acc, fc);
+#pragma unroll
+            for (int c = 0; c < CPL; ++c) {
+                const int64_t i = t * T4 + threadIdx.x + c * kBlock;
+                if (out != nullptr && (EPI & 0xFF) != FEDAVG_EPI_ADD_BASE && i >= b4 && i < e4)
+                    store4<true>(out + i, dv[c]);  // the aggregate itself, when asked for (not held: rare)
+                uint32_t slow = 0;
+                if constexpr ((EPI & 0xFF) == FEDAVG_EPI_ADAM) slow = C.bc2s.fast ? 0u : 1u;
+                if constexpr ((EPI & 0xFF) == FEDAVG_EPI_NADAM) slow = C.bc2.fast ? 0u : 1u;
+                if constexpr ((EPI & 0xFF) == FEDAVG_EPI_RADAM) slow = C.bc1.fast ? 0u : 1u;
+                if constexpr (epi_has_rare<EPI>()) {
+                    res[m][c] = epi_compute<EPI, kEmFast>(E, C, dv[c], in[c], slow);
+                    if (__builtin_expect(slow != 0u, 0)) {
+                        uint32_t unused = 0;
+                        res[m][c] = epi_compute<EPI, kEmElem>(E, C, dv[c], in[c], unused);
+                    }
+                } else {
+                    res[m][c] = epi_compute<EPI, kEmElem>(E, C, dv[c], in[c], slow);
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int m = 0; m < REG; ++m) {
+        const int64_t t = t0 + blockIdx.x + (int64_t)m * gridDim.x;
+        if (t < t_end) {
+#pragma unroll
+            for (int c = 0; c < CPL; ++c) {
+                const int64_t i = t * T4 + threadIdx.x + c * kBlock;
+                if (i >= b4 && i < e4) epi_store<EPI>(E, i, res[m][c], out);
+            }
+        }
+    }
+}
+
+
 // A/B of the burst kernel's client loop (launch variant bits 9-11 = LOOP 1-4), instantiated for one configuration only:
 // torch-mode FIN_DIV Adam with the AMD-host sqrt, no chained partial sum (bench.py --epilogue adam on the pool's boxes)
 template <int OP, int FIN, bool ACC_IN, int EPI, int TPB_LDS, int LOOP>
@@ -686,10 +756,43 @@ inline bool epi_loop_ab(const TileLaunch& L, const EpiParams& E, hipStream_t s, 
 // (fedavg_internal.h kAB): the burst form with 4 (two blocks per CU) or 9 (one block per CU) LDS-held tiles without a
 // chained sum, the pipelined per-tile form; A/B builds also the register-only burst form, the burst form over a
 // chained sum, the unpipelined per-tile form and the client-loop shapes.
+template <int OP, int FIN, int EPI, int REG>
+inline hipError_t launch_epi_few(const TileLaunch& L, const EpiParams& E, hipStream_t s, uint64_t* nl) {
+    f32x4* o = reinterpret_cast<f32x4*>(L.out);
+    return burst_launches(L.b4 / L.tile4, (L.e4 - 1) / L.tile4 + 1, L.grid, REG, nl, L.variant & kVariantAnyOrder,
+                          [&](int nb, int64_t t0, int64_t t_end, uint32_t flags) {
+                              hipExtLaunchKernelGGL((fedavg_tiles_epi_few_f32x4<OP, FIN, EPI, REG>), dim3(nb),
+                                                    dim3(kBlock), 0, s, nullptr, nullptr, flags, L.tab, L.k, L.tstride4,
+                                                    o, L.b4, L.e4, L.fin_val, E, t0, t_end);
+                          });
+}
+
+// the register-held few-client fused form (A/B builds with -DFEDAVG_AB_FEW, torch-mode FIN_DIV Adam with the AMD-host
+// sqrt, 2-3 client reads): launch variant bits 9-11 = 1-5 select 2, 3, 4, 5, 6 register-held tiles; measured at one
+// block per CU it ran 48-55 % of HBM peak against the per-tile form's 69 % (profiles/r05/s4/epifew_k*.jsonl): the
+// optimizer arithmetic is not overlapped with memory at one wave per SIMD.  fedavg_set_launch(2, 0) runs it at two.
+template <int OP, int FIN, int EPI>
+inline hipError_t launch_epi_few_any(const TileLaunch& L, const EpiParams& E, hipStream_t s, uint64_t* nl) {
+    if constexpr (kABFew && OP == FEDAVG_OP_TORCH && FIN == FEDAVG_FIN_DIV && EPI == (FEDAVG_EPI_ADAM | kEpiTorchSqrtAmd)) {
+        switch ((L.variant >> kVariantLoopShift) & 7) {
+            case 1: return launch_epi_few<OP, FIN, EPI, 2>(L, E, s, nl);
+            case 2: return launch_epi_few<OP, FIN, EPI, 3>(L, E, s, nl);
+            case 3: return launch_epi_few<OP, FIN, EPI, 4>(L, E, s, nl);
+            case 4: return launch_epi_few<OP, FIN, EPI, 5>(L, E, s, nl);
+            case 5: return launch_epi_few<OP, FIN, EPI, 6>(L, E, s, nl);
+            default: break;
+        }
+    }
+    return hipErrorInvalidValue;
+}
+
 template <int OP, int FIN, bool ACC_IN, int EPI>
 inline hipError_t launch_epi_k(const TileLaunch& L, const EpiParams& E, hipStream_t s, uint64_t* nl) {
     const f32x4* ai = reinterpret_cast<const f32x4*>(L.acc_in);
     f32x4* o = reinterpret_cast<f32x4*>(L.out);
+    if constexpr (kABFew && !ACC_IN) {
+        if (L.variant & kVariantEpiFew) return launch_epi_few_any<OP, FIN, EPI>(L, E, s, nl);
+    }
     if constexpr (kAB || !ACC_IN) {
         if (!(L.variant & (kVariantTileStores | kVariantEpiPrefetch))) {  // burst: one launch per grid x TPB tiles
             if constexpr (kAB) {

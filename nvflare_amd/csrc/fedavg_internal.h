@@ -56,6 +56,8 @@ constexpr int kVariantLoopShift = 9;       // bits 9-11: A/B shapes of the burst
                                            // (fedavg_epi.h launch_epi_loop_ab, fedavg_tiles.h launch_burst)
 constexpr int kVariantFew = 1 << 12;      // inside TileLaunch: the few-client burst kernel (fedavg_tiles.h
                                            // fedavg_tiles_few_f32x4), set by run_tiles for 1-2 reads, no chained sum
+constexpr int kVariantEpiFew = 1 << 13;   // inside TileLaunch, A/B builds (-DFEDAVG_AB_FEW): the register-held
+                                           // few-client fused form (fedavg_epi.h fedavg_tiles_epi_few_f32x4)
 // public variant bits a product build accepts (fedavg_set_variant): the fused per-tile pipelined form (2), burst
 // launches without the barrier bit (16), the 4-LDS-tile form on one-block-per-CU grids (64) -- each a routed form
 constexpr int kVariantProductMask = kVariantEpiPrefetch | kVariantAnyOrder | kVariantWideLds;

@@ -3,7 +3,9 @@
 #      (epilogue arithmetic kEmFast, operands loaded after the clients), tilee (kEmElem), pipe2 (the next tile's
 #      operands prefetched with its clients), pipe2e (both);
 #   2. config 5 (64 x 1e9, fused Adam) prod vs pf2 (the burst epilogue phase's operands two tiles ahead), 3 rounds;
-#   3. the every-kind 2-3-client fused tests on the product library.
+#   3. the every-kind 2-3-client fused tests on the product library;
+#   4. the register-held few-client fused form (A/B only, nvflare_amd/lib/ab/epifew.so) at TWO blocks per CU (2 / 3 / 4
+#      register-held tiles) against the per-tile form, interleaved in one process, outputs checked bit-equal.
 OUT=$GRAFT_REPO_ROOT/gpurun_out/r05_s5
 mkdir -p "$OUT"
 cd "$GRAFT_REPO_ROOT"
@@ -25,5 +27,8 @@ for R in 1 2 3; do
     timeout -k 10 300 python -u bench.py --config 5 --also none --no-cpu-baseline --sqrt torch_cpu_amd >> "$OUT/c5_$L.jsonl" 2>> "$OUT/err.log" || exit $?
   done
   echo "round $R done"
+done
+for K in 2 3; do
+  NVFLARE_AMD_FEDAVG_LIB=$GRAFT_REPO_ROOT/nvflare_amd/lib/ab/epifew.so timeout -k 10 300 python -u tools/ab_variants.py --clients $K --params 5e8 --variants 0:0:0,512:0:2,1024:0:2,1536:0:2,1024:0:1 --epilogues adam --sqrt torch_cpu_amd --rounds 3 --check > "$OUT/epifew_k$K.jsonl" 2>> "$OUT/err.log" || exit $?
 done
 echo done
