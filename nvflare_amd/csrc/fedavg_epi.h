@@ -371,11 +371,15 @@ __device__ __forceinline__ void fin_tile_em(f32x4 (&r)[CPL], const f32x4 (&a)[CP
     }
 }
 
-// the forms the kernels use (A/B builds: -DFEDAVG_EM_TILE=n / -DFEDAVG_EM_BURST=n)
+// the forms the kernels use (A/B builds: -DFEDAVG_EM_TILE=n / -DFEDAVG_EM_BURST=n), from interleaved A/Bs, fused Adam
+// with the AMD-host sqrt, % of 8 TB/s: the burst form kEmFast (64 clients x 2.5e8: 87.4 against 86.8 per element and
+// 86.8 with IEEE divisions, profiles/r05/s3/adam_k64_*); the per-tile form kEmElem (2 / 3 clients x 5e8: 69.4 / 68.9
+// against 68.5 / 68.7 with kEmFast, s5/adam_k*_tilee, _prod -- its epilogue is one tile at a time, and the fast
+// form's longer live ranges cost more there than its fewer branches save)
 #if defined(FEDAVG_EM_TILE)
 constexpr int kEmTile = FEDAVG_EM_TILE;
 #else
-constexpr int kEmTile = kEmFast;
+constexpr int kEmTile = kEmElem;
 #endif
 #if defined(FEDAVG_EM_BURST)
 constexpr int kEmBurst = FEDAVG_EM_BURST;
