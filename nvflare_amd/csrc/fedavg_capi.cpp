@@ -397,7 +397,10 @@ void run_tiles(fedavg_ctx* ctx, const void* const* bases, const double* weights,
         const int reads = kc + (cur_in ? 1 : 0);
         // 1-2 client reads without a chained sum: the few-client burst kernel (round 5) at the default geometry,
         // unless the public variant asks for the per-tile form (bit 3) or the general burst form (bit 8; A/B builds)
-        const bool few = reads < kBurstMinClients && !cur_in && kc >= 1 && L.tile4 == fedavg::kDefaultTile / 4 &&
+        // (A/B builds with -DFEDAVG_AB_FEW: 3-4 reads too when variant bits 9-11 are 1-6)
+        const int few_ab_ix = fedavg::kABFew ? (ctx->variant >> fedavg::kVariantLoopShift) & 7 : 0;
+        const bool few_reads = reads < kBurstMinClients || (kc <= 4 && few_ab_ix >= 1 && few_ab_ix <= 6);
+        const bool few = few_reads && !cur_in && kc >= 1 && L.tile4 == fedavg::kDefaultTile / 4 &&
                          L.unroll == fedavg::kDefaultUnroll &&
                          !(ctx->variant & (fedavg::kVariantTileStores | fedavg::kVariantTemporalLoads |
                                            fedavg::kVariantTemporalStores | kVariantFewBurst));

@@ -213,11 +213,16 @@ constexpr FewForm kFewDefault[3] = {{0, 0, 0, 0}, {2, 8, 4, 2}, {1, 4, 10, 1}};
 constexpr FewForm kFewAB[2][6] = {
     {{2, 8, 4, 2}, {1, 12, 10, 2}, {1, 8, 10, 1}, {2, 10, 4, 2}, {2, 8, 4, 4}, {1, 16, 10, 2}},
     {{1, 4, 10, 1}, {1, 6, 10, 1}, {1, 5, 10, 1}, {1, 4, 9, 1}, {1, 3, 10, 1}, {1, 4, 10, 2}}};
-// the few-client form of a launch with `reads` (1 or 2) client reads
+// A/B builds: the few-client kernel at 3-4 reads (variant bits 9-11 = 1-6; 0 keeps those reads on the burst form)
+constexpr FewForm kFewAB34[2][6] = {
+    {{1, 2, 10, 1}, {1, 3, 10, 1}, {1, 4, 10, 1}, {2, 2, 4, 1}, {1, 2, 8, 1}, {2, 3, 4, 1}},
+    {{1, 2, 10, 1}, {1, 3, 10, 1}, {1, 1, 10, 1}, {2, 2, 4, 1}, {1, 2, 8, 1}, {1, 2, 10, 2}}};
+
+// the few-client form of a launch with `reads` (1 or 2; A/B builds 3-4) client reads
 inline FewForm few_form(int reads, int variant) {
     if (kABFew) {
         const int ix = (variant >> kVariantLoopShift) & 7;
-        if (ix >= 1 && ix <= 6) return kFewAB[reads - 1][ix - 1];
+        if (ix >= 1 && ix <= 6) return reads <= 2 ? kFewAB[reads - 1][ix - 1] : kFewAB34[reads - 3][ix - 1];
     }
     return kFewDefault[reads];
 }

@@ -296,7 +296,7 @@ template <int OP, int FIN, int KC, int R, int L, int G>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, 2)))
 fedavg_tiles_few_f32x4(const RowTableF32 tab, const int64_t tstride4, f32x4* out, const int64_t b4, const int64_t e4,
                        const float fin_val, const int64_t t0, const int64_t t_end) {
-    static_assert(KC == 1 || KC == 2, "one or two row reads");
+    static_assert(KC >= 1 && KC <= 4, "one to four row reads (3-4: A/B builds only)");
     static_assert(L % G == 0 || L == 0, "whole LDS groups");
     constexpr int CPL = 4;
     constexpr int64_t T4 = (int64_t)CPL * kBlock;
@@ -311,7 +311,8 @@ fedavg_tiles_few_f32x4(const RowTableF32 tab, const int64_t tstride4, f32x4* out
 #pragma unroll
         for (int c = 0; c < CPL; ++c) {
             acc[c] = first4<OP>(v[0][c], tab.w[0]);
-            if constexpr (KC == 2) acc[c] = step4<OP>(acc[c], v[1][c], tab.w[1]);
+#pragma unroll
+            for (int j = 1; j < KC; ++j) acc[c] = step4<OP>(acc[c], v[j][c], tab.w[j]);
         }
     };
     // 1. the register-held tiles' loads
@@ -397,7 +398,7 @@ inline hipError_t launch_few(const TileLaunch& L, hipStream_t s, uint64_t* nl) {
             FEDAVG_FEW(8, 4, 4)
             FEDAVG_FEW(16, 10, 2)
         }
-    } else {
+    } else if constexpr (KC == 2) {
         FEDAVG_FEW(4, 10, 1)
         if constexpr (kABFew) {
             FEDAVG_FEW(6, 10, 1)
@@ -406,6 +407,20 @@ inline hipError_t launch_few(const TileLaunch& L, hipStream_t s, uint64_t* nl) {
             FEDAVG_FEW(3, 10, 1)
             FEDAVG_FEW(4, 10, 2)
         }
+    } else if constexpr (kABFew && KC == 3) {
+        FEDAVG_FEW(2, 10, 1)
+        FEDAVG_FEW(3, 10, 1)
+        FEDAVG_FEW(4, 10, 1)
+        FEDAVG_FEW(2, 4, 1)
+        FEDAVG_FEW(2, 8, 1)
+        FEDAVG_FEW(3, 4, 1)
+    } else if constexpr (kABFew && KC == 4) {
+        FEDAVG_FEW(2, 10, 1)
+        FEDAVG_FEW(3, 10, 1)
+        FEDAVG_FEW(1, 10, 1)
+        FEDAVG_FEW(2, 4, 1)
+        FEDAVG_FEW(2, 8, 1)
+        FEDAVG_FEW(2, 10, 2)
     }
 #undef FEDAVG_FEW
     return hipErrorInvalidValue;
@@ -457,6 +472,16 @@ inline hipError_t launch_burst(const TileLaunch& L, hipStream_t s, uint64_t* nl)
         if constexpr (kAB) {
             if (L.variant & kVariantRuntimeK) return launch_burst_kc<OP, FIN, ACC_IN, UNROLL, CPL, TPB, TPB_LDS, 0>(L, s, nl);
         }
+        if constexpr (kABFew) {  // A/B: bits 9-11 = 7 -- 3-6 clients on the remainder forms instead of a built-in count
+            if (((L.variant >> kVariantLoopShift) & 7) == 7) {
+                switch (L.k % 4) {
+                    case 1: return launch_burst_kc<OP, FIN, ACC_IN, UNROLL, CPL, TPB, TPB_LDS, -2>(L, s, nl);
+                    case 2: return launch_burst_kc<OP, FIN, ACC_IN, UNROLL, CPL, TPB, TPB_LDS, -3>(L, s, nl);
+                    case 3: return launch_burst_kc<OP, FIN, ACC_IN, UNROLL, CPL, TPB, TPB_LDS, -4>(L, s, nl);
+                    default: return launch_burst_kc<OP, FIN, ACC_IN, UNROLL, CPL, TPB, TPB_LDS, -1>(L, s, nl);
+                }
+            }
+        }
         if constexpr (kAB || (!ACC_IN && TPB_LDS != kBurstLdsTilesWide)) {
             switch (L.k) {
 #define FEDAVG_KC(N) \
@@ -501,10 +526,14 @@ template <int OP, int FIN, bool ACC_IN, int UNROLL, int CPL>
 inline hipError_t launch_tiles_v(const TileLaunch& L, hipStream_t s, uint64_t* nl) {
     const f32x4* ai = reinterpret_cast<const f32x4*>(L.acc_in);
     f32x4* o = reinterpret_cast<f32x4*>(L.out);
-    if (L.variant & kVariantFew) {  // 1-2 client reads, no chained sum (fedavg_capi.cpp run_tiles)
+    if (L.variant & kVariantFew) {  // 1-2 client reads, no chained sum (fedavg_capi.cpp run_tiles); A/B: 3-4 too
         if constexpr (!ACC_IN && CPL == 4 && UNROLL == 4) {
             if (L.k == 1) return launch_few<OP, FIN, 1>(L, s, nl);
             if (L.k == 2) return launch_few<OP, FIN, 2>(L, s, nl);
+            if constexpr (kABFew) {
+                if (L.k == 3) return launch_few<OP, FIN, 3>(L, s, nl);
+                if (L.k == 4) return launch_few<OP, FIN, 4>(L, s, nl);
+            }
         }
         return hipErrorInvalidValue;
     }
