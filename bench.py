@@ -527,8 +527,8 @@ def kernel_name(K, epilogue, variant):
     # per-tile-store kernels
     if epilogue != "none":
         return "fedavg_tiles_epi_burst_f32x4" if variant & 12 == 0 and K >= 4 else "fedavg_tiles_epi_f32x4"
-    if K < 3 and not variant & (11 | 256):
-        return ("fedavg_tiles_few_f32x4 (1-2 client reads: every register-held tile's loads issued before any "
+    if K <= 3 and not variant & (11 | 256):
+        return ("fedavg_tiles_few_f32x4 (1-3 client reads: every register-held tile's loads issued before any "
                 "arithmetic, results stored as chip-wide bursts)")
     if (variant & 11 or K < 3) and not (K < 3 and variant & 256 and not variant & 11):
         return "fedavg_tiles_f32x4"

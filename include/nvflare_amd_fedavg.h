@@ -336,12 +336,12 @@ int fedavg_set_launch(fedavg_ctx* ctx, int blocks_per_cu, int unroll);
  * tiles' results (the fused kernel: its differences) in registers and LDS and stores them (runs the epilogue) as
  * chip-wide bursts at the end of a short launch -- per launch 8 register-held tiles per block plus 4 LDS-held ones on
  * two-block-per-CU grids, or 10 (fused: 9) on the one-block-per-CU grids of the plain kernel at 32+ clients (fused:
- * 64+).  A plain launch with 1-2 client reads and no chained sum (most NVFlare jobs run 2 clients) runs the FEW-CLIENT
+ * 64+).  A plain launch with 1-3 client reads and no chained sum (most NVFlare jobs run 2 clients) runs the FEW-CLIENT
  * burst form (round 5): every register-held tile's loads go out before any arithmetic, the results are stored as a
  * burst; a chained sum with fewer than 3 reads runs the PER-TILE-STORE form, which stores each tile's results as it
  * finishes; the fused kernel under 4 reads its per-tile form pipelined across tiles.  Every load and store is
- * nontemporal.  The plain burst kernel has the launch's client count built in for 3-6 clients and the count's
- * remainder mod 4 from 7 on (no repeated loads); each full four-client group's loads go out as two pairs (plain burst
+ * nontemporal.  The plain burst kernel has the launch's client count built in for 5 clients and the count's
+ * remainder mod 4 otherwise (no repeated loads); each full four-client group's loads go out as two pairs (plain burst
  * kernel from 4 clients on, fused from 8).  Results are bit-identical in every variant.
  * The PRODUCT library (nvflare_amd/_build.py) carries only the routed kernel forms and accepts:
  * bit 2 = the fused per-tile form (pipelined across tiles: the next tile's first client loads overlap the epilogue) at
@@ -358,7 +358,9 @@ int fedavg_set_launch(fedavg_ctx* ctx, int blocks_per_cu, int unroll);
  * bit 8 = plain launches with fewer than 3 row reads on the general burst form;
  * bits 9-11 = the fused burst kernel's client loop in shape 1-6 (fedavg_epi.h launch_epi_loop_ab; built for torch-mode
  *         FIN_DIV Adam with the AMD-host sqrt and no chained partial sum), the plain burst kernel's (fedavg_tiles.h
- *         launch_burst), and for 1-2 reads the few-client form's geometry 1-6 (fedavg_internal.h kFewAB);
+ *         launch_burst; 6 / 7 = 3-6 clients on a built-in count / the remainder forms), the few-client form's
+ *         geometry at 1-2 reads (1-6) and 3-4 reads (1-5) (fedavg_internal.h kFewAB, kFewAB34), and the fused
+ *         register-held few-client form at 2-3 reads (fedavg_epi.h fedavg_tiles_epi_few_f32x4);
  * and unroll 8 (fedavg_set_launch) and tile widths 1024 / 2048 / 8192 (fedavg_set_tile, fedavg_accumulate_tiled).
  * A product library refuses those with an error ("... A/B form ..."), never running another form in their place. */
 int fedavg_set_variant(fedavg_ctx* ctx, int variant);

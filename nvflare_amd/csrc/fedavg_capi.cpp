@@ -397,9 +397,11 @@ void run_tiles(fedavg_ctx* ctx, const void* const* bases, const double* weights,
         const int reads = kc + (cur_in ? 1 : 0);
         // 1-2 client reads without a chained sum: the few-client burst kernel (round 5) at the default geometry,
         // unless the public variant asks for the per-tile form (bit 3) or the general burst form (bit 8; A/B builds)
-        // (A/B builds with -DFEDAVG_AB_FEW: 3-4 reads too when variant bits 9-11 are 1-6)
+        // 1-3 client reads (kFewMaxReads) without a chained sum; A/B builds with -DFEDAVG_AB_FEW: 4 reads with variant
+        // bits 9-11 = 1-5 too, and 3 reads with bits 9-11 = 6 or 7 on the burst form (its client-loop A/Bs)
         const int few_ab_ix = fedavg::kABFew ? (ctx->variant >> fedavg::kVariantLoopShift) & 7 : 0;
-        const bool few_reads = reads < kBurstMinClients || (kc <= 4 && few_ab_ix >= 1 && few_ab_ix <= 6);
+        const bool few_reads = (reads <= fedavg::kFewMaxReads && !(reads == 3 && few_ab_ix >= 6)) ||
+                               (kc == 4 && few_ab_ix >= 1 && few_ab_ix <= 5);
         const bool few = few_reads && !cur_in && kc >= 1 && L.tile4 == fedavg::kDefaultTile / 4 &&
                          L.unroll == fedavg::kDefaultUnroll &&
                          !(ctx->variant & (fedavg::kVariantTileStores | fedavg::kVariantTemporalLoads |

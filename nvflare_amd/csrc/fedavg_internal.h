@@ -208,21 +208,27 @@ struct FewForm {
 // 71.5 / 73.5 with 10 LDS tiles at one block per CU); 2 reads -- one block per CU, 4 register- + 10 LDS-held tiles, one
 // LDS tile's loads at a time (78.9, against 77.2 two at a time, 75.3 five, 77.5 with 6 register tiles, 74.1 / 73.8 at
 // two blocks per CU).  The same box's 1 : 1 and 2 : 1 burst patterns: 74.5 / 77.2 % (s3/mix_r*.jsonl).
-constexpr FewForm kFewDefault[3] = {{0, 0, 0, 0}, {2, 8, 4, 2}, {1, 4, 10, 1}};
+// 3 reads (round 5, session 6, profiles/r05/s6/few34_k3.jsonl): the same kernel at one block per CU, 4 + 10 tiles, 79.2
+// against 76.3 % for the burst form with the count built in (78.9 / 78.2 with 3 / 2 register-held tiles, 73.9 at two
+// blocks per CU); 4 reads stay on the burst form (the few-client kernel 71.6-74.8 against 76.2 %, s6/few34_k4.jsonl).
+constexpr int kFewMaxReads = 3;
+constexpr FewForm kFewDefault[kFewMaxReads + 1] = {{0, 0, 0, 0}, {2, 8, 4, 2}, {1, 4, 10, 1}, {1, 4, 10, 1}};
 // A/B builds: launch variant bits 9-11 pick one of these per read count (1-6; 0 = the default)
 constexpr FewForm kFewAB[2][6] = {
     {{2, 8, 4, 2}, {1, 12, 10, 2}, {1, 8, 10, 1}, {2, 10, 4, 2}, {2, 8, 4, 4}, {1, 16, 10, 2}},
     {{1, 4, 10, 1}, {1, 6, 10, 1}, {1, 5, 10, 1}, {1, 4, 9, 1}, {1, 3, 10, 1}, {1, 4, 10, 2}}};
-// A/B builds: the few-client kernel at 3-4 reads (variant bits 9-11 = 1-6; 0 keeps those reads on the burst form)
+// A/B builds: the few-client kernel at 3-4 reads in other forms (variant bits 9-11 = 1-5; 6 and 7 select the burst
+// form's client loop for 3-6 clients instead, fedavg_tiles.h launch_burst)
 constexpr FewForm kFewAB34[2][6] = {
     {{1, 2, 10, 1}, {1, 3, 10, 1}, {1, 4, 10, 1}, {2, 2, 4, 1}, {1, 2, 8, 1}, {2, 3, 4, 1}},
     {{1, 2, 10, 1}, {1, 3, 10, 1}, {1, 1, 10, 1}, {2, 2, 4, 1}, {1, 2, 8, 1}, {1, 2, 10, 2}}};
 
-// the few-client form of a launch with `reads` (1 or 2; A/B builds 3-4) client reads
+// the few-client form of a launch with `reads` (1-3; A/B builds 4) client reads
 inline FewForm few_form(int reads, int variant) {
     if (kABFew) {
         const int ix = (variant >> kVariantLoopShift) & 7;
-        if (ix >= 1 && ix <= 6) return reads <= 2 ? kFewAB[reads - 1][ix - 1] : kFewAB34[reads - 3][ix - 1];
+        if (reads <= 2 && ix >= 1 && ix <= 6) return kFewAB[reads - 1][ix - 1];
+        if (reads >= 3 && ix >= 1 && ix <= 5) return kFewAB34[reads - 3][ix - 1];
     }
     return kFewDefault[reads];
 }

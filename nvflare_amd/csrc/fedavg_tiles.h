@@ -407,13 +407,14 @@ inline hipError_t launch_few(const TileLaunch& L, hipStream_t s, uint64_t* nl) {
             FEDAVG_FEW(3, 10, 1)
             FEDAVG_FEW(4, 10, 2)
         }
-    } else if constexpr (kABFew && KC == 3) {
-        FEDAVG_FEW(2, 10, 1)
-        FEDAVG_FEW(3, 10, 1)
+    } else if constexpr (KC == 3) {
         FEDAVG_FEW(4, 10, 1)
-        FEDAVG_FEW(2, 4, 1)
-        FEDAVG_FEW(2, 8, 1)
-        FEDAVG_FEW(3, 4, 1)
+        if constexpr (kABFew) {
+            FEDAVG_FEW(2, 10, 1)
+            FEDAVG_FEW(3, 10, 1)
+            FEDAVG_FEW(2, 4, 1)
+            FEDAVG_FEW(2, 8, 1)
+        }
     } else if constexpr (kABFew && KC == 4) {
         FEDAVG_FEW(2, 10, 1)
         FEDAVG_FEW(3, 10, 1)
@@ -472,7 +473,16 @@ inline hipError_t launch_burst(const TileLaunch& L, hipStream_t s, uint64_t* nl)
         if constexpr (kAB) {
             if (L.variant & kVariantRuntimeK) return launch_burst_kc<OP, FIN, ACC_IN, UNROLL, CPL, TPB, TPB_LDS, 0>(L, s, nl);
         }
-        if constexpr (kABFew) {  // A/B: bits 9-11 = 7 -- 3-6 clients on the remainder forms instead of a built-in count
+        // A/B: bits 9-11 = 7 -- 3-6 clients on the remainder forms, 6 -- on a built-in count (1-2 with bit 8)
+        if constexpr (kABFew) {
+            if (((L.variant >> kVariantLoopShift) & 7) == 6 && L.k >= 3 && L.k <= 6) {
+                switch (L.k) {
+                    case 3: return launch_burst_kc<OP, FIN, ACC_IN, UNROLL, CPL, TPB, TPB_LDS, 3>(L, s, nl);
+                    case 4: return launch_burst_kc<OP, FIN, ACC_IN, UNROLL, CPL, TPB, TPB_LDS, 4>(L, s, nl);
+                    case 5: return launch_burst_kc<OP, FIN, ACC_IN, UNROLL, CPL, TPB, TPB_LDS, 5>(L, s, nl);
+                    default: return launch_burst_kc<OP, FIN, ACC_IN, UNROLL, CPL, TPB, TPB_LDS, 6>(L, s, nl);
+                }
+            }
             if (((L.variant >> kVariantLoopShift) & 7) == 7) {
                 switch (L.k % 4) {
                     case 1: return launch_burst_kc<OP, FIN, ACC_IN, UNROLL, CPL, TPB, TPB_LDS, -2>(L, s, nl);
@@ -482,15 +492,15 @@ inline hipError_t launch_burst(const TileLaunch& L, hipStream_t s, uint64_t* nl)
                 }
             }
         }
+        // the product's built-in count: 5 clients only (session 6, profiles/r05/s6/rem_k*.jsonl, 1e9, % of 8 TB/s: 5
+        // clients 79.8 built in against 76.6 on the remainder form; 6 clients 76.7 against 84.3, 4: 74.8 against 76.2
+        // -- those take the remainder forms; 3 clients take the few-client kernel, fedavg_capi.cpp run_tiles)
         if constexpr (kAB || (!ACC_IN && TPB_LDS != kBurstLdsTilesWide)) {
             switch (L.k) {
 #define FEDAVG_KC(N) \
     case N:          \
         return launch_burst_kc<OP, FIN, ACC_IN, UNROLL, CPL, TPB, TPB_LDS, N>(L, s, nl);
-                FEDAVG_KC(3)
-                FEDAVG_KC(4)
                 FEDAVG_KC(5)
-                FEDAVG_KC(6)
                 default:
                     break;
             }
@@ -530,8 +540,8 @@ inline hipError_t launch_tiles_v(const TileLaunch& L, hipStream_t s, uint64_t* n
         if constexpr (!ACC_IN && CPL == 4 && UNROLL == 4) {
             if (L.k == 1) return launch_few<OP, FIN, 1>(L, s, nl);
             if (L.k == 2) return launch_few<OP, FIN, 2>(L, s, nl);
+            if (L.k == 3) return launch_few<OP, FIN, 3>(L, s, nl);
             if constexpr (kABFew) {
-                if (L.k == 3) return launch_few<OP, FIN, 3>(L, s, nl);
                 if (L.k == 4) return launch_few<OP, FIN, 4>(L, s, nl);
             }
         }
