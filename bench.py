@@ -150,7 +150,8 @@ def launch_ranks(args, argv) -> int:
     (it has not imported torch): it only starts the ranks, so nothing re-executes a process that touched the GPU.
     The other ranks' stdout goes to stderr; every rank's stderr passes through (progress).  Returns the exit code: 0,
     the first failing rank's code (the others then get RANK_GRACE_S to end before they are killed), or 124 when the
-    ranks have not finished within --rank-timeout-s (all killed)."""
+    ranks have not finished within --rank-timeout-s (all killed).  The ranks never outlive this process: each is
+    started with PR_SET_PDEATHSIG = SIGKILL, and SIGTERM / SIGINT here kill them before this process exits."""
     import signal
     import subprocess
     import threading
@@ -173,13 +174,23 @@ def launch_ranks(args, argv) -> int:
             else:
                 sys.stderr.write(f"[rank {rank}] {line}")
 
+    def die_with_parent():  # Linux PR_SET_PDEATHSIG: a rank is killed when this process dies, however it dies
+        try:
+            import ctypes
+
+            ctypes.CDLL("libc.so.6", use_errno=True).prctl(1, signal.SIGKILL)
+        except OSError:
+            pass
+
+    # every rank first (no thread runs while preexec_fn does), then their output pumps
     for r in range(world):
         env = dict(base_env, RANK=str(r), LOCAL_RANK=str(r))
         p = subprocess.Popen([sys.executable, "-u", script, *argv], env=env, stdout=subprocess.PIPE,
-                             start_new_session=True)  # its own process group: killed as a whole on failure
-        t = threading.Thread(target=pump, args=(p, r), daemon=True)
+                             start_new_session=True,  # its own process group: killed as a whole on failure
+                             preexec_fn=die_with_parent)
+        procs.append((p, threading.Thread(target=pump, args=(p, r), daemon=True)))
+    for _, t in procs:
         t.start()
-        procs.append((p, t))
 
     def kill_all():
         for p, _ in procs:
@@ -188,6 +199,16 @@ def launch_ranks(args, argv) -> int:
                     os.killpg(p.pid, signal.SIGKILL)
                 except OSError:
                     pass
+
+    def on_signal(signum, frame):  # the driver's own time limit (SIGTERM) or ^C: the ranks go with this process
+        kill_all()
+        sys.stderr.write(f"bench: signal {signum}; the ranks were killed\n")
+        os._exit(128 + signum)
+
+    old_handlers = {}
+    if threading.current_thread() is threading.main_thread():
+        for sig in (signal.SIGTERM, signal.SIGINT):
+            old_handlers[sig] = signal.signal(sig, on_signal)
 
     deadline = time.monotonic() + args.rank_timeout_s
     code, failed_at = 0, None
@@ -214,6 +235,8 @@ def launch_ranks(args, argv) -> int:
         for p, t in procs:
             p.wait()
             t.join(timeout=5)
+        for sig, h in old_handlers.items():
+            signal.signal(sig, h)
     if code == 0 and len(lines) != 1:
         print("bench: rank 0 printed no result line", file=sys.stderr)
         code = 1

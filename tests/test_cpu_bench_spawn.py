@@ -76,3 +76,41 @@ def test_ranks_see_the_torchrun_environment(no_world, tmp_path, capfd):
     env = json.loads(lines[0])
     assert env["WORLD_SIZE"] == "3" and env["RANK"] == env["LOCAL_RANK"] == "0" and env["MASTER_ADDR"] == "127.0.0.1"
     assert "[rank 2] not on stdout" in cap.err and "'--steps', '4'" in cap.err
+
+
+@pytest.mark.timeout(120)
+def test_ranks_die_with_the_launcher(no_world, tmp_path):
+    """The driver's time limit kills the launcher (SIGTERM, or SIGKILL): no rank may keep running on a GPU after it."""
+    import signal
+    import subprocess
+    import time
+
+    pids = tmp_path / "pids"
+    pids.mkdir()
+    script = _script(tmp_path, f"open(os.path.join({str(pids)!r}, str(os.getpid())), 'w').close()\ntime.sleep(600)\n")
+    env = dict(os.environ, NVFLARE_AMD_BENCH_WORKER_SCRIPT=script)
+    for sig in (signal.SIGTERM, signal.SIGKILL):
+        for f in pids.iterdir():
+            f.unlink()
+        launcher = subprocess.Popen([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "3"], env=env,
+                                    stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+        deadline = time.time() + 60
+        while len(list(pids.iterdir())) < 3 and time.time() < deadline:
+            time.sleep(0.1)
+        ranks = [int(f.name) for f in pids.iterdir()]
+        assert len(ranks) == 3
+        launcher.send_signal(sig)
+        launcher.wait(timeout=30)
+        def running(pid):
+            try:
+                with open(f"/proc/{pid}/status") as f:
+                    return "zombie" not in f.read().lower()
+            except OSError:
+                return False
+
+        deadline = time.time() + 10
+        alive = ranks
+        while alive and time.time() < deadline:
+            alive = [p for p in ranks if running(p)]
+            time.sleep(0.1)
+        assert not alive, (sig, alive)
