@@ -536,10 +536,11 @@ def pmc_traffic(args, K, P, epilogue):
             rec = json.load(f)
     except (OSError, ValueError):
         return None, None
-    want = {"clients": K, "params": P, "tile": args.tile, "mode": args.mode, "epilogue": epilogue}
+    want = {"clients": K, "params": P, "tile": args.tile, "mode": args.mode, "epilogue": epilogue, "dtype": "fp32"}
     for r in rec.get("records", []):
         cfg = dict(r.get("config", {}))
         cfg.setdefault("epilogue", "none")
+        cfg.setdefault("dtype", "fp32")  # 16-bit records (tools/bench_narrow.py lines) never stand for a bench line
         if all(cfg.get(k) == v for k, v in want.items()):
             return float(r["bytes_per_launch"]), "profiles/pmc_traffic.json"
     return None, None

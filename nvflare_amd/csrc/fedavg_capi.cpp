@@ -372,7 +372,8 @@ double fin_scalar(int fin, double count) { return fin == FEDAVG_FIN_SCALE ? 1.0 
 // form wins by 1.5-14 points, profiles/r03/s25/, s26/).  The stand-alone server step (no clients, the aggregate as
 // acc_in: one read) takes the per-tile form.
 constexpr int kBurstMinClients = 3;
-constexpr int kVariantFewBurst = 256;  // public variant bit 8: launches under kBurstMinClients reads keep the burst form
+constexpr int kVariantFewBurst = 256;  // A/B variant bit 8 (A/B and -DFEDAVG_AB_FEW builds): launches under
+                                       // kBurstMinClients reads (16-bit: 1-3 reads) keep the burst form
 constexpr int kEpiBurstMinClients = 4;
 
 // Tile-kernel launches over [b, e) (elements, multiples of 4) for any number of clients: chunks of at
@@ -631,7 +632,12 @@ void run_tiles_narrow(fedavg_ctx* ctx, const void* const* bases, const double* w
     const void* cur_in = acc_in;
     do {
         const int kc = std::min(k_rows - k0, fedavg::kMaxRowsPerLaunch);
-        const int dflt = burst && op != FEDAVG_OP_NUMPY && kc >= fedavg::kNarrowOneBlockMinK ? 1 : 2;
+        // 1-3 client reads without a chained sum: the 16-bit few-client form (round 5); A/B builds with
+        // -DFEDAVG_AB_FEW pick its geometry with launch variant bits 9-11 = 1-4
+        const int few_ix = fedavg::kABFew ? (ctx->variant >> fedavg::kVariantLoopShift) & 7 : 0;
+        const bool few = burst && !cur_in && kc <= fedavg::kNarrowFewMaxReads && !(ctx->variant & kVariantFewBurst);
+        const int dflt = few ? fedavg::narrow_few_form(kc, few_ix).bpc
+                             : (burst && op != FEDAVG_OP_NUMPY && kc >= fedavg::kNarrowOneBlockMinK ? 1 : 2);
         const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)ctx->num_cus * ctx->bpc(dflt), n_tiles));
         fedavg::RowTableNarrow t;
         fill_narrow_table(t, bases, weights, k0, kc, fmt, op);
@@ -643,8 +649,9 @@ void run_tiles_narrow(fedavg_ctx* ctx, const void* const* bases, const double* w
         }
         HIP_CHECK(fedavg::launch_tiles_narrow(t, kc, tstride, cur_in, out, begin, end, fmt, narrow_kernel_op(op),
                                               last ? narrow_kernel_fin(fin) : FEDAVG_FIN_NONE, fv, grid,
-                                              burst ? ((ctx->variant & fedavg::kVariantRegisterTiles) ? 1 : 2) : 0, s,
-                                              &ctx->launches));
+                                              few ? 3 + (few_ix <= 4 ? few_ix : 0)
+                                                  : burst ? ((ctx->variant & fedavg::kVariantRegisterTiles) ? 1 : 2) : 0,
+                                              s, &ctx->launches));
         if (n_tails) {
             HIP_CHECK(fedavg::launch_scatter16(tails, tail_vals, n_tails, out, s));
             ++ctx->launches;
@@ -1462,7 +1469,7 @@ int fedavg_set_variant(fedavg_ctx* ctx, int variant) {
     return guarded([&] {
         if (!ctx) throw Error("ctx is NULL");
         if (variant < 0 || variant > 4095) throw Error("variant must be 0..4095");
-        const int accepted = fedavg::kVariantProductMask | (fedavg::kABFew ? 7 << fedavg::kVariantLoopShift : 0);
+        const int accepted = fedavg::kVariantProductMask | (fedavg::kABFew ? 7 << fedavg::kVariantLoopShift | kVariantFewBurst : 0);
         if (!fedavg::kAB && (variant & ~accepted))
             throw Error("variant bits " + std::to_string(variant & ~accepted) +
                         " are A/B forms this product library does not carry (it accepts bits 2, 4 and 6; "

@@ -232,6 +232,23 @@ inline FewForm few_form(int reads, int variant) {
     }
     return kFewDefault[reads];
 }
+// The 16-bit few-client form (fedavg_narrow.hip fedavg_tiles_narrow_few, 1-3 reads): {blocks/CU, register tiles, LDS
+// tiles, LDS tiles per load group} of 8 KiB tiles (at two blocks per CU at most 10 LDS tiles: 160 KiB per CU).
+// Defaults from the same-process sweeps of profiles/r05/s10/ and s11/ (bf16 x 1e9, packed arithmetic): 1 / 2 / 3
+// reads 67.5-68.0 / 71.8 / 73.8 % of 8 TB/s, against 38.0 / 55.9 / 66.0 % on the burst form (profiles/r05/s8/, s9/).
+constexpr int kNarrowFewMaxReads = 3;
+constexpr FewForm kNarrowFewDefault[kNarrowFewMaxReads + 1] = {{0, 0, 0, 0}, {2, 8, 8, 4}, {2, 8, 8, 4}, {1, 8, 20, 4}};
+// A/B builds (-DFEDAVG_AB_FEW): launch variant bits 9-11 = 1-4 pick one of these per read count
+constexpr FewForm kNarrowFewAB[3][4] = {
+    {{2, 16, 8, 4}, {2, 6, 8, 4}, {2, 8, 10, 2}, {2, 12, 8, 4}},
+    {{1, 8, 20, 2}, {1, 6, 20, 4}, {1, 8, 20, 4}, {1, 10, 20, 4}},
+    {{1, 6, 20, 2}, {1, 8, 20, 2}, {1, 4, 20, 2}, {2, 4, 8, 2}}};
+
+inline FewForm narrow_few_form(int reads, int form) {
+    if (kABFew && form >= 1 && form <= 4) return kNarrowFewAB[reads - 1][form - 1];
+    return kNarrowFewDefault[reads];
+}
+
 // whether launch_tiles_f32x4 takes the burst kernel for this geometry (it then wants one block per CU at
 // K >= kBurstOneBlockMinK clients, two below)
 bool tiles_use_burst(int64_t tile4, int unroll, int variant);

@@ -21,6 +21,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "fedavg_arith.h"  // FinConst / div_const_fast (the few-client form's FIN_DIV)
 #include "fedavg_internal.h"
 
 namespace fedavg {
@@ -124,6 +125,116 @@ __device__ __forceinline__ float elem16(const RowTableNarrow& tab, int K, const 
 
 __device__ __forceinline__ uint16_t half_of(const u32x4& v, int j) {
     return (uint16_t)((v[j >> 1] >> ((j & 1) * 16)) & 0xffffu);
+}
+
+// Packed forms of the steps above, two elements per 32-bit word (element 0 in the low half): the fp32 arithmetic on
+// f32x2 compiles to gfx950's packed v_pk_mul_f32 / v_pk_fma_f32 / v_pk_add_f32 (each lane computes both elements
+// with the per-element roundings of the scalar ops -- the same bits), and pack2 rounds both to the format in one
+// v_cvt_pk_{bf16,f16}_f32 (round to nearest even; bit-equal to bits16 per element for every fp32 input, NaN to a
+// NaN: tools/cvt_pk_probe.hip, exhaustive).  The opaque asm operands also keep fptrunc(fma) from folding into a
+// single-rounding mixed fma (see bits16).  Used by the few-client kernel below only: there it beat the per-element
+// form (bf16 1 client 68.0 against 62.6 % of 8 TB/s, profiles/r05/s9/, s10/), while in tile_sum16 (the burst and
+// per-tile forms) it lost badly (bf16 8 / 64 clients 71.7 / 64.5 % against 81.1 / 89.2 %, profiles/r05/s11/).
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef uint16_t u16x2 __attribute__((ext_vector_type(2)));
+
+template <int FMT>
+__device__ __forceinline__ f32x2 unpack2(const uint32_t d) {
+    if constexpr (FMT == FEDAVG_BF16) {
+        return f32x2{__uint_as_float(d << 16), __uint_as_float(d & 0xffff0000u)};
+    } else {
+        return f32x2{load16<FEDAVG_F16>((uint16_t)(d & 0xffffu)), load16<FEDAVG_F16>((uint16_t)(d >> 16))};
+    }
+}
+
+template <int FMT>
+__device__ __forceinline__ uint32_t pack2(const f32x2 x) {
+    uint32_t d;
+    if constexpr (FMT == FEDAVG_BF16) {
+        asm("v_cvt_pk_bf16_f32 %0, %1, %2" : "=v"(d) : "v"(x[0]), "v"(x[1]));
+    } else {
+        asm("v_cvt_pk_f16_f32 %0, %1, %2" : "=v"(d) : "v"(x[0]), "v"(x[1]));
+    }
+    return d;
+}
+
+// first16 / step16 on a word: returns the rounded running values' word; t their fp32 values
+template <int FMT, int OP>
+__device__ __forceinline__ uint32_t first2(const uint32_t d, const float w, f32x2& t) {
+    if constexpr (OP == FEDAVG_OP_UNWEIGHTED) {
+        t = unpack2<FMT>(d);
+        return d;
+    } else {
+        const uint32_t r = pack2<FMT>(unpack2<FMT>(d) * w);
+        t = unpack2<FMT>(r);
+        return r;
+    }
+}
+
+template <int FMT, int OP>
+__device__ __forceinline__ uint32_t step2(const uint32_t d, const float w, f32x2& t) {
+    const f32x2 v = unpack2<FMT>(d);
+    uint32_t r;
+    if constexpr (OP == FEDAVG_OP_TORCH) {
+        r = pack2<FMT>(__builtin_elementwise_fma(v, f32x2{w, w}, t));
+    } else if constexpr (OP == FEDAVG_OP_NUMPY) {
+        r = pack2<FMT>(t + unpack2<FMT>(pack2<FMT>(v * w)));
+    } else {
+        r = pack2<FMT>(t + v);
+    }
+    t = unpack2<FMT>(r);
+    return r;
+}
+
+// The finalisation on packed running values (CPL 8-element groups of a lane: words and their fp32 values), to the
+// output words.  FIN_DIV: rnd(T / float(count)), the exact fp32 quotient (div_const_fast's Markstein correction,
+// packed), then the rounding.  Its range condition on the dividends -- fp32 exponent 27..226, which a 16-bit T
+// meets unless it is zero, infinite or NaN, or a bfloat16 beyond 2^+-100 -- is checked on the words' magnitudes,
+// their packed 16-bit maximum and minimum over the tile (bit order = magnitude order); else the IEEE quotient.
+template <int FMT, int FIN, int CPL>
+__device__ __forceinline__ void fin_words(u32x4 (&res)[CPL], const uint32_t (&word)[CPL][4], const f32x2 (&t)[CPL][4],
+                                          const FinConst& fc, const float fv) {
+    if constexpr (FIN == FEDAVG_FIN_DIV) {
+        u16x2 mx = {0, 0}, mn = {0xffff, 0xffff};
+#pragma unroll
+        for (int c = 0; c < CPL; ++c)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const uint32_t a = word[c][e] & 0x7fff7fffu;
+                u16x2 h;
+                __builtin_memcpy(&h, &a, 4);
+                mx = __builtin_elementwise_max(mx, h);
+                mn = __builtin_elementwise_min(mn, h);
+            }
+        constexpr uint16_t lo = FMT == FEDAVG_BF16 ? 27u << 7 : 1u;          // bf16: exponent >= 27; f16: nonzero
+        constexpr uint16_t hi = FMT == FEDAVG_BF16 ? 227u << 7 : 0x7c00u;    // bf16: exponent <= 226; f16: finite
+        const bool slow = !fc.fast || mx[0] >= hi || mx[1] >= hi || mn[0] < lo || mn[1] < lo;
+        if (__builtin_expect(!slow, 1)) {
+#pragma unroll
+            for (int c = 0; c < CPL; ++c)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const f32x2 q = t[c][e] * fc.r;
+                    const f32x2 er = __builtin_elementwise_fma(-q, f32x2{fc.v, fc.v}, t[c][e]);
+                    res[c][e] = pack2<FMT>(__builtin_elementwise_fma(er, f32x2{fc.r, fc.r}, q));
+                }
+        } else {
+#pragma unroll
+            for (int c = 0; c < CPL; ++c)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) res[c][e] = pack2<FMT>(t[c][e] / fc.v);
+        }
+    } else if constexpr (FIN == FEDAVG_FIN_SCALE) {
+#pragma unroll
+        for (int c = 0; c < CPL; ++c)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) res[c][e] = pack2<FMT>(t[c][e] * fv);
+    } else {
+#pragma unroll
+        for (int c = 0; c < CPL; ++c)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) res[c][e] = word[c][e];
+    }
 }
 
 template <int FMT, int OP, int FIN, bool ACC_IN, bool VEC>
@@ -366,12 +477,148 @@ __attribute__((amdgpu_waves_per_eu(FEDAVG_NARROW_BURST_WAVES, FEDAVG_NARROW_BURS
     }
 }
 
+// FEW-CLIENT 16-bit burst form (round 5): 1-3 client reads, no chained sum -- the 16-bit twin of fedavg_tiles.h
+// fedavg_tiles_few_f32x4.  The burst form above loads its clients in groups of 4 or 6 from client 0 on, so at one or
+// two clients most of its loads re-read a row (bf16 x 1e9: 38 / 56 % of 8 TB/s at 1 / 2 clients, profiles/r05/s8/), and
+// its tile guard and per-element FIN_DIV keep one tile's loads in flight per wave.  Here every load is a real client's
+// and unconditional (a slot past the launch's last tile re-reads that tile; only real tiles are stored), the R
+// register-held tiles' loads go out first, the L LDS-held tiles stream through in groups of G, the arithmetic is the
+// packed form (pack2 / step2: two elements per instruction), and FIN_DIV is the exact fp32 quotient by Markstein's
+// correction with one rare-case branch per tile (fedavg_arith.h div_const_fast), rounded to the format as torch's
+// div_ rounds it.  Per-element sequence as tile_sum16's: the same bits.
+template <int FMT, int OP, int FIN, int KC, int R, int L, int G, int B>
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(B, 2)))  // B blocks per CU must co-reside
+fedavg_tiles_narrow_few(const RowTableNarrow tab, const int64_t tstride8, u32x4* out, const int64_t b8, const int64_t e8,
+                        const float fv, const int64_t t0, const int64_t t_end) {
+    static_assert(KC >= 1 && KC <= 3, "one to three row reads");
+    static_assert(L == 0 || L % G == 0, "whole LDS groups");
+    constexpr int CPL = kCpl16;
+    constexpr int64_t T8 = (int64_t)CPL * kBlock;
+    const FinConst fc = fin_const<FIN>(fv);
+    __shared__ u32x4 staged[L > 0 ? L * CPL * kBlock : 1];
+    const int64_t t_first = t0 + blockIdx.x;
+    auto tile_of = [&](const int m) __attribute__((always_inline)) {
+        const int64_t t = t_first + (int64_t)m * gridDim.x;
+        return t < t_end ? t : t_end - 1;
+    };
+    auto load_tile = [&](u32x4 (&v)[KC][CPL], const int m) __attribute__((always_inline)) {
+        const int64_t off = tile_of(m) * tstride8 + threadIdx.x;
+#pragma unroll
+        for (int j = 0; j < KC; ++j)
+#pragma unroll
+            for (int c = 0; c < CPL; ++c)
+                v[j][c] = __builtin_nontemporal_load(static_cast<const u32x4*>(tab.rows[j]) + off + c * kBlock);
+    };
+    auto finish = [&](u32x4 (&res)[CPL], const u32x4 (&v)[KC][CPL]) __attribute__((always_inline)) {
+        uint32_t word[CPL][4];  // the running values, rounded to the format, two per word
+        f32x2 t[CPL][4];        // and as fp32
+#pragma unroll
+        for (int c = 0; c < CPL; ++c)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                word[c][e] = first2<FMT, OP>(v[0][c][e], tab.w_first[0], t[c][e]);
+#pragma unroll
+                for (int j = 1; j < KC; ++j) word[c][e] = step2<FMT, OP>(v[j][c][e], tab.w_step[j], t[c][e]);
+            }
+        fin_words<FMT, FIN, CPL>(res, word, t, fc, fv);
+    };
+    // 1. the register-held tiles' loads (slots L .. L+R-1)
+    u32x4 vr[R][KC][CPL];
+#pragma unroll
+    for (int m = 0; m < R; ++m) load_tile(vr[m], L + m);
+    // 2. the LDS-held tiles (slots 0 .. L-1), G at a time
+#pragma unroll
+    for (int g = 0; g < L; g += G) {
+        u32x4 v[G][KC][CPL];
+#pragma unroll
+        for (int m = 0; m < G; ++m) load_tile(v[m], g + m);
+#pragma unroll
+        for (int m = 0; m < G; ++m) {
+            u32x4 r[CPL];
+            finish(r, v[m]);
+#pragma unroll
+            for (int c = 0; c < CPL; ++c) staged[((g + m) * CPL + c) * kBlock + threadIdx.x] = r[c];
+        }
+    }
+    // 3. the register-held tiles
+    u32x4 res[R][CPL];
+#pragma unroll
+    for (int m = 0; m < R; ++m) finish(res[m], vr[m]);
+    // 4. the write burst
+#pragma unroll
+    for (int m = 0; m < L + R; ++m) {
+        const int64_t t = t_first + (int64_t)m * gridDim.x;
+        if (t < t_end) {
+#pragma unroll
+            for (int c = 0; c < CPL; ++c) {
+                const int64_t i = t * T8 + threadIdx.x + c * kBlock;
+                const u32x4 r = m < L ? staged[(m * CPL + c) * kBlock + threadIdx.x] : res[m < L ? 0 : m - L][c];
+                if (i >= b8 && i < e8) __builtin_nontemporal_store(r, out + i);
+            }
+        }
+    }
+}
+
+template <int FMT, int OP, int FIN, int KC, int R, int L, int G, int B>
+static hipError_t launch_narrow_few_form(const RowTableNarrow& tab, int64_t tstride8, void* out, int64_t b8, int64_t e8,
+                                         float fv, int grid, hipStream_t s, uint64_t* nl) {
+    constexpr int64_t T8 = (int64_t)kCpl16 * kBlock;
+    u32x4* o = static_cast<u32x4*>(out);
+    return burst_launches(b8 / T8, (e8 - 1) / T8 + 1, grid, R + L, nl, false, [&](int nb, int64_t t0, int64_t t_end, uint32_t) {
+        hipLaunchKernelGGL((fedavg_tiles_narrow_few<FMT, OP, FIN, KC, R, L, G, B>), dim3(nb), dim3(kBlock), 0, s, tab, tstride8,
+                           o, b8, e8, fv, t0, t_end);
+    });
+}
+
+template <int FMT, int OP, int FIN, int KC>
+static hipError_t launch_narrow_few(const RowTableNarrow& tab, int64_t tstride8, void* out, int64_t b8, int64_t e8,
+                                    float fv, int grid, int form, hipStream_t s, uint64_t* nl) {
+    const FewForm f = narrow_few_form(KC, form);
+#define FEDAVG_NFEW(B, R, LL, G)                                      \
+    if (f.bpc == B && f.r == R && f.l == LL && f.g == G)              \
+        return launch_narrow_few_form<FMT, OP, FIN, KC, R, LL, G, B>(tab, tstride8, out, b8, e8, fv, grid, s, nl);
+    if constexpr (KC == 1) {
+        FEDAVG_NFEW(2, 8, 8, 4)
+        if constexpr (kABFew) {
+            FEDAVG_NFEW(2, 16, 8, 4)
+            FEDAVG_NFEW(2, 6, 8, 4)
+            FEDAVG_NFEW(2, 8, 10, 2)
+            FEDAVG_NFEW(2, 12, 8, 4)
+        }
+    } else if constexpr (KC == 2) {
+        FEDAVG_NFEW(2, 8, 8, 4)
+        if constexpr (kABFew) {
+            FEDAVG_NFEW(1, 8, 20, 2)
+            FEDAVG_NFEW(1, 6, 20, 4)
+            FEDAVG_NFEW(1, 8, 20, 4)
+            FEDAVG_NFEW(1, 10, 20, 4)
+        }
+    } else {
+        FEDAVG_NFEW(1, 8, 20, 4)
+        if constexpr (kABFew) {
+            FEDAVG_NFEW(1, 6, 20, 2)
+            FEDAVG_NFEW(1, 8, 20, 2)
+            FEDAVG_NFEW(1, 4, 20, 2)
+            FEDAVG_NFEW(2, 4, 8, 2)
+        }
+    }
+#undef FEDAVG_NFEW
+    return hipErrorInvalidValue;
+}
+
 template <int FMT, int OP, int FIN>
 static hipError_t launch_t16_a(const RowTableNarrow& tab, int K, int64_t tstride8, const void* acc_in, void* out,
                                int64_t b8, int64_t e8, float fv, int grid, int burst, hipStream_t s, uint64_t* nl) {
     const u32x4* ai = static_cast<const u32x4*>(acc_in);
     u32x4* o = static_cast<u32x4*>(out);
     constexpr int64_t T8 = (int64_t)kCpl16 * kBlock;
+    if (burst >= 3) {  // the few-client form (1-3 reads, no chained sum); burst - 3 = its A/B form index (0: default)
+        if (acc_in) return hipErrorInvalidValue;
+        if (K == 1) return launch_narrow_few<FMT, OP, FIN, 1>(tab, tstride8, out, b8, e8, fv, grid, burst - 3, s, nl);
+        if (K == 2) return launch_narrow_few<FMT, OP, FIN, 2>(tab, tstride8, out, b8, e8, fv, grid, burst - 3, s, nl);
+        if (K == 3) return launch_narrow_few<FMT, OP, FIN, 3>(tab, tstride8, out, b8, e8, fv, grid, burst - 3, s, nl);
+        return hipErrorInvalidValue;
+    }
     if (burst == 2 || !kAB) {  // default: kBurstTiles in registers + kBurstLdsTiles16 in LDS per block and launch
         // client groups of 4 under kNarrowUnroll4MaxK clients, of FEDAVG_NARROW_UNROLL (6) from there on
         const bool u4 = K < kNarrowUnroll4MaxK;

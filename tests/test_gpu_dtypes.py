@@ -394,3 +394,72 @@ def test_tiled64_vs_oracle(ctx, mode, K, slots, begin, end):
         assert same_bits(got[begin:end], exp)
     slab.close()
     out.close()
+
+
+@pytest.mark.parametrize("fmt,mode", [("bfloat16", "torch"), ("float16", "torch"), ("float16", "numpy"),
+                                      ("bfloat16", "unweighted")])
+@pytest.mark.parametrize("K", [1, 2, 3])
+@pytest.mark.parametrize("form", [0, 1, 2, 3, 4])
+def test_tiled16_few_client_forms(ctx, fmt, mode, K, form):
+    """The 16-bit few-client burst kernel (fedavg_narrow.hip fedavg_tiles_narrow_few; 1-3 client reads, no chained
+    sum): several launches and a short last one (13 001 tiles), unconditional loads (a launch's slots past its last
+    tile re-read that tile, nothing past it is stored), tiles of zeros, of huge and of tiny values (FIN_DIV's per-tile
+    rare-case branch), a sub-range starting and ending inside tiles with a sentinel around it; bit for bit.  Forms 1-4
+    (launch variant bits 9-11) are the A/B geometries (fedavg_internal.h kNarrowFewAB), in -DFEDAVG_AB_FEW builds."""
+    from nvflare_amd import _native as N
+    from nvflare_amd.device import TiledLayout
+
+    if form:
+        try:
+            ctx.set_variant(form << 9)
+        except N.FedAvgError:
+            pytest.skip("an A/B form: tools/build_rev_lib.py --product -D FEDAVG_AB_FEW builds the library carrying it")
+        ctx.set_variant(0)
+    n_tiles = 13_001
+    n = n_tiles * 4096
+    rng = np.random.default_rng(K * 10 + form)
+    rows = []
+    for _ in range(K):
+        x = (rng.standard_normal(n) * 4).astype(np.float32)
+        x[4096 * 5:4096 * 6] = 0.0  # a tile of zeros: the exact division's rare case
+        x[4096 * 9:4096 * 9 + 700] *= 1e30 if fmt == "bfloat16" else 1.0
+        x[4096 * 11:4096 * 11 + 300] *= 1e-30 if fmt == "bfloat16" else 1e-4
+        rows.append(_bits(x, fmt))
+    ws = [float(rng.random() * 20 + 1e-3) for _ in range(K)]
+    if mode in ("torch", "unweighted"):
+        op = N.FEDAVG_OP_TORCH if mode == "torch" else N.FEDAVG_OP_UNWEIGHTED
+        fin = N.FEDAVG_FIN_DIV
+    else:
+        op, fin = N.FEDAVG_OP_NUMPY, N.FEDAVG_FIN_SCALE
+
+    def expected(b, e):
+        if fin == N.FEDAVG_FIN_DIV:
+            return orc.torch16_vector_reference([_vals(r[b:e], fmt) for r in rows], ws, fmt, weighted=mode == "torch")
+        return orc.numpy_mode_reference([r[b:e].view(np.float16) for r in rows], ws).astype(np.float32)
+
+    code = N.FEDAVG_BF16 if fmt == "bfloat16" else N.FEDAVG_F16
+    lay = TiledLayout(4096, K)
+    slab = ctx.alloc(lay.slab_elems(n) * 2)
+    out = ctx.alloc(n * 2)
+    try:
+        bases = [slab.ptr + lay.slot_offset_elems(k) * 2 for k in range(K)]
+        for b, r in zip(bases, rows):
+            ctx.h2d_tiled(b, 4096 * 2, lay.tile_stride * 2, 0, r.ctypes.data, r.nbytes)
+        got = np.empty(n, np.uint16)
+        ctx.set_variant(form << 9)
+        n0 = ctx.launch_count()
+        ctx.accumulate_tiled16(code, bases, ws, 4096, lay.tile_stride, 0, n, out.ptr, op, fin, _count(ws))
+        assert ctx.launch_count() - n0 >= 2  # several launches, the last partial
+        ctx.d2h(got, out.ptr)
+        assert same_bits(_vals(got, fmt), expected(0, n)), (fmt, mode, K, form)
+        lo, hi = 4096 * 7 + 40, n - 4096 * 3 - 104
+        sentinel = np.full(n, 0x7E00, np.uint16)
+        ctx.h2d_ptr(out.ptr, sentinel.ctypes.data, sentinel.nbytes)
+        ctx.accumulate_tiled16(code, bases, ws, 4096, lay.tile_stride, lo, hi, out.ptr, op, fin, _count(ws))
+        ctx.d2h(got, out.ptr)
+        assert same_bits(_vals(got[lo:hi], fmt), expected(lo, hi))
+        assert np.all(got[:lo] == 0x7E00) and np.all(got[hi:] == 0x7E00)
+    finally:
+        ctx.set_variant(0)
+        slab.close()
+        out.close()

@@ -26,6 +26,7 @@ def main():
     ap.add_argument("--layout", choices=["rows", "tiled"], default="tiled",
                     help="rows: K separate client buffers (fedavg_accumulate); tiled: the engine's slab "
                          "(fedavg_accumulate_tiled16)")
+    ap.add_argument("--check", action="store_true", help="every configuration's output bit-equal to the first's")
     args = ap.parse_args()
     import torch
 
@@ -63,12 +64,20 @@ def main():
     alg = 2.0 * K * P + 2.0 * P
     cfgs = [(int(v), int(b)) for v in args.variants.split(",") for b in args.blocks_per_cu.split(",")]
     res = {c: [] for c in cfgs}
+    first = None
     for rep in range(3):
         for c in cfgs:
             ctx.set_variant(c[0])
             ctx.set_launch(c[1], 0)
+            if args.check and rep == 0:
+                out.fill_(float("nan"))
             launch()
             ctx.sync()
+            if args.check and rep == 0:
+                if first is None:
+                    first = out.clone()
+                elif not torch.equal(out.view(torch.int16), first.view(torch.int16)):
+                    raise SystemExit(f"variant {c[0]} blocks/CU {c[1]}: output differs from variant {cfgs[0][0]}'s")
             ctx.timing_begin()
             for _ in range(args.steps):
                 launch()

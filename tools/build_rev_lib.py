@@ -65,10 +65,14 @@ def main():
         only = [x for x in args.only.split(",") if x]
         if only and args.rev != "WORKTREE":
             raise SystemExit("--only needs --rev WORKTREE (the reused objects are the working tree's)")
-        reuse = B.OBJ_DIR if args.product else AB_OBJ  # --product: the in-tree product build's objects
+        # --only reuses: the last full WORKTREE A/B build's objects, or with --product the in-tree product build's,
+        # or with --product -D ... the last full WORKTREE build's with the same definitions (lib/obj_<defines>)
+        reuse = AB_OBJ if not args.product else (
+            os.path.join(B.PKG, "lib", "obj_" + "_".join(sorted(args.defines))) if args.defines else B.OBJ_DIR)
+        keep = args.rev == "WORKTREE" and not only and (args.product == bool(args.defines))
         if only and not os.path.isdir(reuse):
             raise SystemExit(f"--only reuses the objects of a full build ({reuse}): run one first")
-        if only and args.product and B.needs_build():
+        if only and args.product and not args.defines and B.needs_build():
             raise SystemExit("--only --product reuses the in-tree objects: build the in-tree library first")
 
         def compile_one(unit):
@@ -78,9 +82,9 @@ def main():
             obj = os.path.join(tmp, obj_name)
             defs = [f"-D{d}" for d in ([] if args.product else ["FEDAVG_AB"]) + args.defines]
             subprocess.run([B.HIPCC, *B.FLAGS, *extra, *defs, *inc, "-c", os.path.join(csrc, src), "-o", obj], check=True)
-            if args.rev == "WORKTREE" and not only and not args.defines and not args.product:  # for a later --only
-                os.makedirs(AB_OBJ, exist_ok=True)
-                shutil.copy(obj, os.path.join(AB_OBJ, obj_name))
+            if keep:  # for a later --only
+                os.makedirs(reuse, exist_ok=True)
+                shutil.copy(obj, os.path.join(reuse, obj_name))
             return obj
 
         with ThreadPoolExecutor(max_workers=min(8, len(units))) as pool:

@@ -18,7 +18,8 @@ TARGET = "hipv4-amdgcn-amd-amdhsa--gfx950"
 KEYS = ["global_load_dwordx4", "global_store_dwordx4", "global_load_dword", "ds_read_u16", "ds_read_b128",
         "ds_write_b128", "s_waitcnt", "s_cbranch_execz", "s_cbranch_execnz", "s_cbranch_scc0", "s_cbranch_scc1",
         "s_cbranch_vccnz", "s_cbranch_vccz", "s_branch", "v_div_scale_f32", "v_div_fixup_f32", "v_rcp_f32",
-        "v_sqrt_f32", "v_fma_f32", "v_cndmask_b32_e64", "v_cndmask_b32_e32", "s_and_saveexec_b64"]
+        "v_sqrt_f32", "v_fma_f32", "v_cndmask_b32_e64", "v_cndmask_b32_e32", "s_and_saveexec_b64",
+        "scratch_store_dword", "scratch_store_dwordx4", "scratch_load_dword", "scratch_load_dwordx4"]
 
 
 def disasm(obj: str, tmp: str) -> str:
@@ -53,6 +54,9 @@ def main():
             f.write(body)
     c = collections.Counter()
     n = 0
+    top = {"v": -1, "a": -1}  # the highest VGPR / AGPR index the kernel names (register pressure; spills show above)
+    for m in re.finditer(r"\b([va])(?:(\d+)\b|\[\d+:(\d+)\])", body):
+        top[m.group(1)] = max(top[m.group(1)], int(m.group(2) or m.group(3)))
     for line in body.splitlines():
         m = re.match(r"\s+(\w+)", line.split("//")[0])
         if m:
@@ -60,6 +64,7 @@ def main():
             n += 1
     print(name)
     print("instructions", n)
+    print("vgprs", top["v"] + 1, "agprs", top["a"] + 1)
     for k in KEYS:
         if c[k]:
             print(f"{k:24s} {c[k]}")
