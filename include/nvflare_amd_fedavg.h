@@ -340,8 +340,8 @@ int fedavg_set_launch(fedavg_ctx* ctx, int blocks_per_cu, int unroll);
  * burst form (round 5): every register-held tile's loads go out before any arithmetic, the results are stored as a
  * burst; a chained sum with fewer than 3 reads runs the PER-TILE-STORE form, which stores each tile's results as it
  * finishes; the fused kernel under 4 reads its per-tile form pipelined across tiles.  Every load and store is
- * nontemporal.  The 16-bit tile kernel (fedavg_accumulate_tiled16) likewise runs 1-3 client reads without a chained
- * sum on its few-client burst form, the rest on its burst form.  The plain burst kernel has the launch's client count
+ * nontemporal.  The 16-bit and fp64 tile kernels (fedavg_accumulate_tiled16 / _tiled64) likewise run 1-3 client
+ * reads without a chained sum on their few-client burst forms, the rest on their burst forms.  The plain burst kernel has the launch's client count
  * built in for 5 clients and the count's
  * remainder mod 4 otherwise (no repeated loads); each full four-client group's loads go out as two pairs (plain burst
  * kernel from 4 clients on, fused from 8).  Results are bit-identical in every variant.
@@ -357,13 +357,13 @@ int fedavg_set_launch(fedavg_ctx* ctx, int blocks_per_cu, int unroll);
  * bit 5 = the burst kernels without their LDS-held tiles (register-held tiles only: 8 per block per launch);
  * bit 7 = the plain burst kernel's round-3 runtime client loop (its last group of 4 re-loads the last client in the
  *         missing slots when the count is not a multiple of 4);
- * bit 8 = plain launches with fewer than 3 row reads (16-bit: 1-3) on the general burst form (also accepted by
+ * bit 8 = plain launches with fewer than 3 row reads (16-bit, fp64: 1-3) on the general burst form (also accepted by
  *         product-sized -DFEDAVG_AB_FEW builds);
  * bits 9-11 = the fused burst kernel's client loop in shape 1-6 (fedavg_epi.h launch_epi_loop_ab; built for torch-mode
  *         FIN_DIV Adam with the AMD-host sqrt and no chained partial sum), the plain burst kernel's (fedavg_tiles.h
  *         launch_burst; 6 / 7 = 3-6 clients on a built-in count / the remainder forms), the few-client form's
  *         geometry at 1-2 reads (1-6) and 3-4 reads (1-5) (fedavg_internal.h kFewAB, kFewAB34), the 16-bit
- *         few-client form's at 1-3 reads (1-4, kNarrowFewAB), and the fused
+ *         and fp64 few-client forms' at 1-3 reads (1-4, kNarrowFewAB, kF64FewAB), and the fused
  *         register-held few-client form at 2-3 reads (fedavg_epi.h fedavg_tiles_epi_few_f32x4);
  * and unroll 8 (fedavg_set_launch) and tile widths 1024 / 2048 / 8192 (fedavg_set_tile, fedavg_accumulate_tiled).
  * A product library refuses those with an error ("... A/B form ..."), never running another form in their place. */

@@ -1263,10 +1263,20 @@ int fedavg_accumulate_tiled64(fedavg_ctx* ctx, const void* const* bases, const d
                 t.w[j] = weights[k0 + j];
             }
             const bool last = k0 + kc >= k_rows;
+            // 1-3 client reads without a chained sum: the fp64 few-client form (round 5); A/B builds with
+            // -DFEDAVG_AB_FEW pick its geometry with launch variant bits 9-11 = 1-4
+            const int few_ix = fedavg::kABFew ? (ctx->variant >> fedavg::kVariantLoopShift) & 7 : 0;
+            const bool few = burst && !cur_in && kc <= fedavg::kF64FewMaxReads && !(ctx->variant & kVariantFewBurst);
+            const int fgrid = few ? (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)ctx->num_cus *
+                                                                                    ctx->bpc(fedavg::f64_few_form(kc, few_ix).bpc),
+                                                                                n_tiles))
+                                  : grid;
             HIP_CHECK(fedavg::launch_tiles_f64(t, kc, (int64_t)tile_stride, cur_in, out, (int64_t)begin, (int64_t)end,
-                                               op, last ? fin : FEDAVG_FIN_NONE, fv, grid,
-                                               burst ? ((ctx->variant & fedavg::kVariantRegisterTiles) ? 1 : 2) : 0, s,
-                                               &ctx->launches));
+                                               op, last ? fin : FEDAVG_FIN_NONE, fv, fgrid,
+                                               few    ? 3 + (few_ix <= 4 ? few_ix : 0)
+                                               : burst ? ((ctx->variant & fedavg::kVariantRegisterTiles) ? 1 : 2)
+                                                       : 0,
+                                               s, &ctx->launches));
             cur_in = out;
             k0 += kc;
         } while (k0 < k_rows);

@@ -249,6 +249,23 @@ inline FewForm narrow_few_form(int reads, int form) {
     return kNarrowFewDefault[reads];
 }
 
+// The fp64 few-client form (fedavg_kernels.hip fedavg_tiles_f64x2_few, 1-3 reads): the same geometry fields, 32 KiB
+// tiles (at two blocks per CU at most 2 LDS tiles per block, at one at most 5: 160 KiB per CU) -- the fp32 forms'
+// bytes in flight with half the tiles.  Defaults from the same-process sweep of profiles/r05/s14/ (5e8 params, numpy
+// mode): 1 / 2 / 3 reads 76.8 / 76.3 / 78.0 % of 8 TB/s against 74.0 / 73.7 / 75.0 % on the burst form.
+constexpr int kF64FewMaxReads = 3;
+constexpr FewForm kF64FewDefault[kF64FewMaxReads + 1] = {{0, 0, 0, 0}, {2, 4, 2, 2}, {1, 2, 5, 5}, {1, 3, 4, 1}};
+// A/B builds (-DFEDAVG_AB_FEW): launch variant bits 9-11 = 1-4 pick one of these per read count
+constexpr FewForm kF64FewAB[3][4] = {
+    {{2, 4, 2, 1}, {1, 4, 4, 2}, {2, 3, 2, 2}, {1, 6, 4, 2}},
+    {{1, 2, 5, 1}, {1, 3, 4, 1}, {1, 2, 4, 2}, {2, 2, 2, 1}},
+    {{1, 2, 5, 1}, {1, 2, 4, 2}, {2, 2, 2, 1}, {1, 2, 5, 5}}};
+
+inline FewForm f64_few_form(int reads, int form) {
+    if (kABFew && form >= 1 && form <= 4) return kF64FewAB[reads - 1][form - 1];
+    return kF64FewDefault[reads];
+}
+
 // whether launch_tiles_f32x4 takes the burst kernel for this geometry (it then wants one block per CU at
 // K >= kBurstOneBlockMinK clients, two below)
 bool tiles_use_burst(int64_t tile4, int unroll, int variant);

@@ -391,12 +391,128 @@ static hipError_t launch_rows_f64x2(const RowTableGeneric& tab, int K, const voi
     return launch_generic_t<double, double>(tail, K, tail_in, static_cast<double*>(out) + 2 * n2, 1, op, fin, fin_val, 1, s);
 }
 
+// FEW-CLIENT fp64 burst form (round 5): 1-3 client reads, no chained sum -- fedavg_tiles.h fedavg_tiles_few_f32x4's
+// shape with 32 KiB tiles: every load unconditional (a launch's slot past its last tile re-reads that tile; only real
+// tiles are stored), the R register-held tiles' loads first, the L LDS-held tiles in groups of G, every store at the
+// end.  The burst form's tile guard puts a basic-block boundary between its tiles' loads (fp64 x 1e9 at 1 / 2 clients:
+// 74.2 / 74.2 % of 8 TB/s, profiles/r05/s8/f64.jsonl).  Per-element sequence as tile_sum64's: the same bits.
+template <int OP, int FIN, int KC, int R, int L, int G, int B>
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(B, 2)))
+fedavg_tiles_f64x2_few(const RowTableGeneric tab, const int64_t tstride2, f64x2* out, const int64_t b2, const int64_t e2,
+                       const double fin_val, const int64_t t0, const int64_t t_end) {
+    static_assert(KC >= 1 && KC <= 3, "one to three row reads");
+    static_assert(L == 0 || L % G == 0, "whole LDS groups");
+    constexpr int CPL = kCpl64;
+    constexpr int64_t T2 = (int64_t)CPL * kBlock;
+    __shared__ f64x2 staged[L > 0 ? L * CPL * kBlock : 1];
+    const int64_t t_first = t0 + blockIdx.x;
+    auto load_tile = [&](f64x2 (&v)[KC][CPL], const int m) __attribute__((always_inline)) {
+        int64_t t = t_first + (int64_t)m * gridDim.x;
+        t = t < t_end ? t : t_end - 1;
+        const int64_t off = t * tstride2 + threadIdx.x;
+#pragma unroll
+        for (int j = 0; j < KC; ++j)
+#pragma unroll
+            for (int c = 0; c < CPL; ++c)
+                v[j][c] = __builtin_nontemporal_load(static_cast<const f64x2*>(tab.rows[j]) + off + c * kBlock);
+    };
+    auto finish = [&](f64x2 (&res)[CPL], const f64x2 (&v)[KC][CPL]) __attribute__((always_inline)) {
+#pragma unroll
+        for (int c = 0; c < CPL; ++c) {
+            f64x2 acc = f64x2{first_op<OP>(v[0][c][0], tab.w[0]), first_op<OP>(v[0][c][1], tab.w[0])};
+#pragma unroll
+            for (int j = 1; j < KC; ++j)
+                acc = f64x2{step_op<OP>(acc[0], v[j][c][0], tab.w[j]), step_op<OP>(acc[1], v[j][c][1], tab.w[j])};
+            res[c] = f64x2{fin_op<FIN>(acc[0], fin_val), fin_op<FIN>(acc[1], fin_val)};
+        }
+    };
+    f64x2 vr[R][KC][CPL];
+#pragma unroll
+    for (int m = 0; m < R; ++m) load_tile(vr[m], L + m);
+#pragma unroll
+    for (int g = 0; g < L; g += G) {
+        f64x2 v[G][KC][CPL];
+#pragma unroll
+        for (int m = 0; m < G; ++m) load_tile(v[m], g + m);
+#pragma unroll
+        for (int m = 0; m < G; ++m) {
+            f64x2 r[CPL];
+            finish(r, v[m]);
+#pragma unroll
+            for (int c = 0; c < CPL; ++c) staged[((g + m) * CPL + c) * kBlock + threadIdx.x] = r[c];
+        }
+    }
+    f64x2 res[R][CPL];
+#pragma unroll
+    for (int m = 0; m < R; ++m) finish(res[m], vr[m]);
+#pragma unroll
+    for (int m = 0; m < L + R; ++m) {
+        const int64_t t = t_first + (int64_t)m * gridDim.x;
+        if (t < t_end) {
+#pragma unroll
+            for (int c = 0; c < CPL; ++c) {
+                const int64_t i = t * T2 + threadIdx.x + c * kBlock;
+                const f64x2 r = m < L ? staged[(m * CPL + c) * kBlock + threadIdx.x] : res[m < L ? 0 : m - L][c];
+                if (i >= b2 && i < e2) __builtin_nontemporal_store(r, out + i);
+            }
+        }
+    }
+}
+
+template <int OP, int FIN, int KC>
+static hipError_t launch_f64_few(const RowTableGeneric& tab, int64_t ts2, f64x2* o, int64_t b2, int64_t e2,
+                                 double fin_val, int grid, int form, hipStream_t s, uint64_t* nl) {
+    constexpr int64_t T2 = (int64_t)kCpl64 * kBlock;
+    const FewForm f = f64_few_form(KC, form);
+#define FEDAVG_F64FEW(BB, RR, LL, GG)                                                                                    \
+    if (f.bpc == BB && f.r == RR && f.l == LL && f.g == GG)                                                             \
+        return burst_launches(b2 / T2, (e2 - 1) / T2 + 1, grid, RR + LL, nl, false,                                     \
+                              [&](int nb, int64_t t0, int64_t t_end, uint32_t) {                                         \
+                                  hipLaunchKernelGGL((fedavg_tiles_f64x2_few<OP, FIN, KC, RR, LL, GG, BB>), dim3(nb),   \
+                                                     dim3(kBlock), 0, s, tab, ts2, o, b2, e2, fin_val, t0, t_end);       \
+                              });
+    if constexpr (KC == 1) {
+        FEDAVG_F64FEW(2, 4, 2, 2)
+        if constexpr (kABFew) {
+            FEDAVG_F64FEW(2, 4, 2, 1)
+            FEDAVG_F64FEW(1, 4, 4, 2)
+            FEDAVG_F64FEW(2, 3, 2, 2)
+            FEDAVG_F64FEW(1, 6, 4, 2)
+        }
+    } else if constexpr (KC == 2) {
+        FEDAVG_F64FEW(1, 2, 5, 5)
+        if constexpr (kABFew) {
+            FEDAVG_F64FEW(1, 2, 5, 1)
+            FEDAVG_F64FEW(1, 3, 4, 1)
+            FEDAVG_F64FEW(1, 2, 4, 2)
+            FEDAVG_F64FEW(2, 2, 2, 1)
+        }
+    } else {
+        FEDAVG_F64FEW(1, 3, 4, 1)
+        if constexpr (kABFew) {
+            FEDAVG_F64FEW(1, 2, 5, 1)
+            FEDAVG_F64FEW(1, 2, 4, 2)
+            FEDAVG_F64FEW(2, 2, 2, 1)
+            FEDAVG_F64FEW(1, 2, 5, 5)
+        }
+    }
+#undef FEDAVG_F64FEW
+    return hipErrorInvalidValue;
+}
+
 template <int OP, int FIN>
 static hipError_t launch_t64_f(const RowTableGeneric& tab, int K, int64_t ts2, const void* acc_in, void* out, int64_t b2,
                                int64_t e2, double fin_val, int grid, int burst, hipStream_t s, uint64_t* nl) {
     const f64x2* ai = static_cast<const f64x2*>(acc_in);
     f64x2* o = static_cast<f64x2*>(out);
     constexpr int64_t T2 = (int64_t)kCpl64 * kBlock;
+    if (burst >= 3) {  // the few-client form (1-3 reads, no chained sum); burst - 3 = its A/B form index (0: default)
+        if (acc_in) return hipErrorInvalidValue;
+        if (K == 1) return launch_f64_few<OP, FIN, 1>(tab, ts2, o, b2, e2, fin_val, grid, burst - 3, s, nl);
+        if (K == 2) return launch_f64_few<OP, FIN, 2>(tab, ts2, o, b2, e2, fin_val, grid, burst - 3, s, nl);
+        if (K == 3) return launch_f64_few<OP, FIN, 3>(tab, ts2, o, b2, e2, fin_val, grid, burst - 3, s, nl);
+        return hipErrorInvalidValue;
+    }
     if (burst == 2 || !kAB) {  // default: kBurstTiles64 in registers + kBurstLdsTiles64 in LDS per block and launch
         return burst_launches(b2 / T2, (e2 - 1) / T2 + 1, grid, kBurstTiles64 + kBurstLdsTiles64, nl, false,
                               [&](int nb, int64_t t0, int64_t t_end, uint32_t) {

@@ -463,3 +463,68 @@ def test_tiled16_few_client_forms(ctx, fmt, mode, K, form):
         ctx.set_variant(0)
         slab.close()
         out.close()
+
+
+@pytest.mark.parametrize("mode", ["numpy", "torch", "unweighted"])
+@pytest.mark.parametrize("K", [1, 2, 3])
+@pytest.mark.parametrize("form", [0, 1, 2, 3, 4])
+def test_tiled64_few_client_forms(ctx, mode, K, form):
+    """The fp64 few-client burst kernel (fedavg_kernels.hip fedavg_tiles_f64x2_few; 1-3 client reads, no chained sum):
+    several launches and a short last one (4001 tiles), unconditional loads (a launch's slots past its last tile
+    re-read that tile, nothing past it is stored), zeros, huge, tiny and subnormal values, a sub-range starting and
+    ending inside tiles with a sentinel around it; bit for bit against the C oracle's fp64 restatement.  Forms 1-4
+    (launch variant bits 9-11) are the A/B geometries (fedavg_internal.h kF64FewAB), in -DFEDAVG_AB_FEW builds."""
+    from nvflare_amd import _native as N
+    from nvflare_amd.device import TiledLayout
+
+    if form:
+        try:
+            ctx.set_variant(form << 9)
+        except N.FedAvgError:
+            pytest.skip("an A/B form: tools/build_rev_lib.py --product -D FEDAVG_AB_FEW builds the library carrying it")
+        ctx.set_variant(0)
+    n = 4001 * 4096
+    rng = np.random.default_rng(K * 10 + form)
+    rows = []
+    for _ in range(K):
+        x = rng.standard_normal(n) * 4
+        x[4096 * 5:4096 * 6] = 0.0
+        x[4096 * 9:4096 * 9 + 700] *= 1e300
+        x[4096 * 11:4096 * 11 + 300] *= 1e-310
+        rows.append(x)
+    ws = [float(rng.random() * 20 + 1e-3) for _ in range(K)]
+    weighted = mode != "unweighted"
+    omode = orc.MODE_TORCH if mode == "torch" else orc.MODE_NUMPY
+    op = {"numpy": N.FEDAVG_OP_NUMPY, "torch": N.FEDAVG_OP_TORCH, "unweighted": N.FEDAVG_OP_UNWEIGHTED}[mode]
+    fin = N.FEDAVG_FIN_DIV if mode == "torch" else N.FEDAVG_FIN_SCALE
+    count = _count(ws) if weighted else float(K)
+
+    def expected(b, e):
+        return orc.fedavg_c([r[b:e].copy() for r in rows], ws, omode, weighted=weighted, fin=fin, count=count,
+                            nthreads=8)
+
+    lay = TiledLayout(4096, K)
+    slab = ctx.alloc(lay.slab_elems(n) * 8)
+    out = ctx.alloc(n * 8)
+    try:
+        bases = [slab.ptr + lay.slot_offset_elems(k) * 8 for k in range(K)]
+        for b, r in zip(bases, rows):
+            ctx.h2d_tiled(b, 4096 * 8, lay.tile_stride * 8, 0, r.ctypes.data, r.nbytes)
+        got = np.empty(n, np.float64)
+        ctx.set_variant(form << 9)
+        n0 = ctx.launch_count()
+        ctx.accumulate_tiled64(bases, ws, 4096, lay.tile_stride, 0, n, out.ptr, op, fin, count)
+        assert ctx.launch_count() - n0 >= 2  # several launches, the last partial
+        ctx.d2h(got, out.ptr)
+        assert same_bits(got, expected(0, n)), (mode, K, form)
+        lo, hi = 4096 * 7 + 42, n - 4096 * 3 - 106
+        sentinel = np.full(n, -7.0)
+        ctx.h2d_ptr(out.ptr, sentinel.ctypes.data, sentinel.nbytes)
+        ctx.accumulate_tiled64(bases, ws, 4096, lay.tile_stride, lo, hi, out.ptr, op, fin, count)
+        ctx.d2h(got, out.ptr)
+        assert same_bits(got[lo:hi], expected(lo, hi))
+        assert np.all(got[:lo] == -7.0) and np.all(got[hi:] == -7.0)
+    finally:
+        ctx.set_variant(0)
+        slab.close()
+        out.close()

@@ -23,6 +23,9 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--variants", default="0", help="comma list of fedavg_set_variant values, interleaved rounds")
     ap.add_argument("--blocks-per-cu", default="0", help="comma list, swept with every variant (0 = library default)")
+    ap.add_argument("--mode", choices=["numpy", "torch"], default="numpy",
+                    help="numpy: v*w then add, T * (1.0/count); torch: fma, T / count")
+    ap.add_argument("--check", action="store_true", help="every configuration's output bit-equal to the first's")
     ap.add_argument("--layout", choices=["rows", "tiled"], default="rows",
                     help="rows: K separate client buffers (fedavg_accumulate); tiled: the engine's fp64 slab "
                          "(fedavg_accumulate_tiled64, float64 only)")
@@ -39,6 +42,8 @@ def main():
     g = torch.Generator(device="cuda:0")
     g.manual_seed(0)
     ws = [float(1 + (37 * k) % 100) for k in range(K)]
+    op = N.FEDAVG_OP_TORCH if args.mode == "torch" else N.FEDAVG_OP_NUMPY
+    fin = N.FEDAVG_FIN_DIV if args.mode == "torch" else N.FEDAVG_FIN_SCALE
     if args.layout == "tiled":
         from nvflare_amd.device import TiledLayout
 
@@ -51,25 +56,33 @@ def main():
         out = torch.empty(end, dtype=tdt, device="cuda:0")
 
         def launch():
-            ctx.accumulate_tiled64(bases, ws, 4096, lay.tile_stride, 0, end, out.data_ptr(), N.FEDAVG_OP_NUMPY,
-                                   N.FEDAVG_FIN_SCALE, sum(ws))
+            ctx.accumulate_tiled64(bases, ws, 4096, lay.tile_stride, 0, end, out.data_ptr(), op, fin, sum(ws))
     else:
         rows = [torch.randn(P, dtype=tdt, device="cuda:0", generator=g) for _ in range(K)]
         out = torch.empty(P, dtype=tdt, device="cuda:0")
 
         def launch():
-            ctx.accumulate([r.data_ptr() for r in rows], ws, P, out.data_ptr(), code, code, N.FEDAVG_OP_NUMPY,
-                           N.FEDAVG_FIN_SCALE, sum(ws))
+            ctx.accumulate([r.data_ptr() for r in rows], ws, P, out.data_ptr(), code, code, op, fin, sum(ws))
     torch.cuda.synchronize()
 
     variants = [(int(v), int(b)) for v in args.variants.split(",") for b in args.blocks_per_cu.split(",")]
     res = {v: [] for v in variants}
+    first = None
     for rep in range(3):
         for v in variants:
             ctx.set_variant(v[0])
             ctx.set_launch(v[1], 0)
+            if args.check and rep == 0:
+                out.fill_(float("nan"))
+                torch.cuda.synchronize()  # torch's stream is not the library's: the fill must land before the launch
             launch()
             ctx.sync()
+            if args.check and rep == 0:
+                if first is None:
+                    first = out.clone()
+                elif not torch.equal(out.view(torch.int64 if out.element_size() == 8 else torch.int32),
+                                     first.view(torch.int64 if out.element_size() == 8 else torch.int32)):
+                    raise SystemExit(f"variant {v[0]} blocks/CU {v[1]}: output differs from variant {variants[0][0]}'s")
             ctx.timing_begin()
             for _ in range(args.steps):
                 launch()
@@ -79,7 +92,8 @@ def main():
     nbytes = (K + 1) * P * out.element_size()
     for v in variants:
         ms = sorted(res[v])[len(res[v]) // 2]
-        print(json.dumps({"tool": "bench_generic", "dtype": args.dtype, "layout": args.layout, "clients": K, "params": P,
+        print(json.dumps({"tool": "bench_generic", "dtype": args.dtype, "mode": args.mode, "layout": args.layout,
+                          "clients": K, "params": P,
                           "variant": v[0], "blocks_per_cu": v[1], "kernel_ms": round(ms, 3), "alg_GBs": round(nbytes / ms / 1e6, 1),
                           "frac_of_8TBs": round(nbytes / ms / 1e6 / 8000, 4)}), flush=True)
 

@@ -71,6 +71,7 @@ def main():
             ctx.set_launch(c[1], 0)
             if args.check and rep == 0:
                 out.fill_(float("nan"))
+                torch.cuda.synchronize()  # torch's stream is not the library's: the fill must land before the launch
             launch()
             ctx.sync()
             if args.check and rep == 0:
