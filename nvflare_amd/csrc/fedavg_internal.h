@@ -266,6 +266,30 @@ inline FewForm f64_few_form(int reads, int form) {
     return kF64FewDefault[reads];
 }
 
+// Every few-client geometry must fit the CU: its blocks' LDS-held tiles within gfx950's 160 KiB of LDS per CU, whole
+// load groups (a form that does not fit still runs, with fewer blocks resident than its grid assumes)
+constexpr int kLdsBytesPerCu = 160 * 1024;
+template <int N>
+constexpr bool few_forms_fit(const FewForm (&forms)[N], int tile_bytes) {
+    for (int i = 0; i < N; ++i) {
+        const FewForm& f = forms[i];
+        if (f.bpc == 0) continue;  // the unused read-count-0 slot
+        if (f.bpc < 1 || f.r < 1 || f.l < 0 || f.g < 1 || (f.l > 0 && f.l % f.g != 0)) return false;
+        if ((int64_t)f.bpc * f.l * tile_bytes > kLdsBytesPerCu) return false;
+    }
+    return true;
+}
+static_assert(few_forms_fit(kFewDefault, kDefaultTile * 4) && few_forms_fit(kFewAB[0], kDefaultTile * 4) &&
+                  few_forms_fit(kFewAB[1], kDefaultTile * 4) && few_forms_fit(kFewAB34[0], kDefaultTile * 4) &&
+                  few_forms_fit(kFewAB34[1], kDefaultTile * 4),
+              "fp32 few-client forms");
+static_assert(few_forms_fit(kNarrowFewDefault, 8192) && few_forms_fit(kNarrowFewAB[0], 8192) &&
+                  few_forms_fit(kNarrowFewAB[1], 8192) && few_forms_fit(kNarrowFewAB[2], 8192),
+              "16-bit few-client forms");
+static_assert(few_forms_fit(kF64FewDefault, 32768) && few_forms_fit(kF64FewAB[0], 32768) &&
+                  few_forms_fit(kF64FewAB[1], 32768) && few_forms_fit(kF64FewAB[2], 32768),
+              "fp64 few-client forms");
+
 // whether launch_tiles_f32x4 takes the burst kernel for this geometry (it then wants one block per CU at
 // K >= kBurstOneBlockMinK clients, two below)
 bool tiles_use_burst(int64_t tile4, int unroll, int variant);
