@@ -8,6 +8,7 @@ from __future__ import annotations
 import os
 import re
 import subprocess
+import time
 from concurrent.futures import ThreadPoolExecutor
 
 PKG = os.path.dirname(os.path.abspath(__file__))
@@ -27,6 +28,7 @@ EPI_UNITS_AB = [(f"{mode}_{fin}", op, fin_v) for mode, op in (("torch", 1), ("nu
                 for fin, fin_v in (("div", 2), ("scale", 1), ("none", 0))]
 EPI_UNITS = [u for u in EPI_UNITS_AB if u[0] in ("torch_div", "torch_scale", "numpy_scale", "unweighted_scale",
                                                   "unweighted_div")] + [("step", None, None)]
+NARROW_SOURCE = "fedavg_narrow.hip"
 SOURCES = [EPI_SOURCE, "fedavg_tiles_numpy.hip", "fedavg_tiles_torch.hip", "fedavg_tiles_unweighted.hip",
            "fedavg_kernels.hip", "fedavg_narrow.hip", "fedavg_dequant.hip", "fedavg_capi.cpp"]
 HEADERS = ["fedavg_internal.h", "fedavg_rsqrt14.h", "fedavg_arith.h", "fedavg_tiles.h",
@@ -60,7 +62,7 @@ def needs_build() -> bool:
 
 def compile_units(sources=SOURCES, ab=False):
     """(source, object name, extra flags) of every translation unit: the fused kernels' source once per EPI_UNITS
-    entry (EPI_UNITS_AB for an A/B build), the others once each."""
+    entry (EPI_UNITS_AB for an A/B build), the 16-bit source once per format, the others once each."""
     units = []
     for src in sources:
         if src == EPI_SOURCE:
@@ -68,6 +70,9 @@ def compile_units(sources=SOURCES, ab=False):
                        ["-DFEDAVG_EPI_STEP"] if op is None else
                        [f"-DFEDAVG_EPI_OP={op}", f"-DFEDAVG_EPI_FIN={fin}", f"-DFEDAVG_EPI_FN=launch_epi_{name}"])
                       for name, op, fin in (EPI_UNITS_AB if ab else EPI_UNITS)]
+        elif src == NARROW_SOURCE:  # once per 16-bit format (fedavg_narrow.hip FEDAVG_NARROW_PART)
+            units += [(src, "fedavg_narrow_bf16.hip.o", ["-DFEDAVG_NARROW_PART=1"]),
+                      (src, "fedavg_narrow_f16.hip.o", ["-DFEDAVG_NARROW_PART=2"])]
         else:
             units.append((src, src + ".o", []))
     return units
@@ -105,7 +110,9 @@ def build_library(force: bool = False, verbose: bool = False, jobs: int = 0) -> 
     os.makedirs(OBJ_DIR, exist_ok=True)
     inc = [f"-I{os.path.join(ROOT, 'include')}", f"-I{CSRC}"]
 
-    units = compile_units()
+    # the longest units first (the 16-bit and fused units take minutes each, the rest seconds to a minute), so the
+    # pool's critical path is one long unit, not a long unit started last
+    units = sorted(compile_units(), key=lambda u: 0 if u[0] in (NARROW_SOURCE, EPI_SOURCE) else 1)
 
     def compile_one(unit) -> str:
         src, obj_name, extra = unit
@@ -116,7 +123,10 @@ def build_library(force: bool = False, verbose: bool = False, jobs: int = 0) -> 
         cmd = [HIPCC, *FLAGS, *extra, *inc, "-c", os.path.join(CSRC, src), "-o", obj]
         if verbose:
             print(" ".join(cmd), flush=True)
+        t0 = time.time()
         subprocess.run(cmd, check=True)
+        if verbose:
+            print(f"{obj_name}: {time.time() - t0:.0f} s", flush=True)
         return obj
 
     jobs = jobs or min(len(units), max(1, min(16, os.cpu_count() or 1)))

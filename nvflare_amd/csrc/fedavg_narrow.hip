@@ -689,15 +689,20 @@ static hipError_t launch_t16_o(const RowTableNarrow& tab, int K, int64_t tstride
     }
 }
 
-hipError_t launch_tiles_narrow(const RowTableNarrow& tab, int K, int64_t tstride_elems, const void* acc_in, void* out,
-                               int64_t begin, int64_t end, int fmt, int op, int fin, float fin_val, int grid,
-                               int burst, hipStream_t s, uint64_t* nl) {
-    const int64_t ts8 = tstride_elems / 8, b8 = begin / 8, e8 = end / 8;
-    if (fmt == FEDAVG_BF16)
-        return launch_t16_o<FEDAVG_BF16>(tab, K, ts8, acc_in, out, b8, e8, op, fin, fin_val, grid, burst, s, nl);
-    if (fmt == FEDAVG_F16)
-        return launch_t16_o<FEDAVG_F16>(tab, K, ts8, acc_in, out, b8, e8, op, fin, fin_val, grid, burst, s, nl);
-    return hipErrorInvalidValue;
+// ---------------------------------------------------------------------------------------------
+// The build compiles this file twice (nvflare_amd/_build.py): FEDAVG_NARROW_PART=1 holds the bfloat16 kernels and the
+// dispatchers below, =2 the float16 kernels -- each format's entry points (tiles16_fmt, rows16_fmt, tails16_fmt) are
+// instantiated in its own unit, halving what was the build's longest translation unit.  Without the macro (a tool
+// compiling this file alone) one unit holds both.
+// ---------------------------------------------------------------------------------------------
+#if !defined(FEDAVG_NARROW_PART)
+#define FEDAVG_NARROW_PART 0
+#endif
+
+template <int FMT>
+hipError_t tiles16_fmt(const RowTableNarrow& tab, int K, int64_t ts8, const void* acc_in, void* out, int64_t b8,
+                       int64_t e8, int op, int fin, float fv, int grid, int burst, hipStream_t s, uint64_t* nl) {
+    return launch_t16_o<FMT>(tab, K, ts8, acc_in, out, b8, e8, op, fin, fv, grid, burst, s, nl);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -739,11 +744,6 @@ __global__ void __launch_bounds__(kBlock) fedavg_torch16_tails(const RowTableNar
     vals[j] = bits16<FMT>(fin16<FMT, FIN>(t, fv));
 }
 
-__global__ void __launch_bounds__(kBlock) fedavg_scatter16(const int64_t* idx, const uint16_t* vals, const int64_t m,
-                                                            uint16_t* out) {
-    const int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (j < m) out[idx[j]] = vals[j];
-}
 
 template <int FMT, int FIN, bool DEVICE>
 static hipError_t launch_tails_a(const RowTableNarrow& tab, int K, int64_t tile, int64_t tstride, const int64_t* idx,
@@ -772,28 +772,16 @@ static hipError_t launch_tails_f(const RowTableNarrow& tab, int K, int64_t tile,
     }
 }
 
-hipError_t launch_torch16_tails(const RowTableNarrow& tab, int K, int64_t tile, int64_t tstride, const int64_t* idx,
-                                int64_t m, const void* acc_in, void* vals, int fmt, int op, int fin, float fin_val,
-                                hipStream_t s) {
-    const int grid = (int)((m + kBlock - 1) / kBlock);
-    if (grid == 0) return hipSuccess;
-    if (op == FEDAVG_OP_TORCH_DEVICE) {  // float16 only: bfloat16 has no single-rounding path in torch-ROCm
-        if (fmt != FEDAVG_F16) return hipErrorInvalidValue;
-        return launch_tails_f<FEDAVG_F16, true>(tab, K, tile, tstride, idx, m, acc_in, vals, fin, fin_val, grid, s);
+template <int FMT>
+hipError_t tails16_fmt(const RowTableNarrow& tab, int K, int64_t tile, int64_t tstride, const int64_t* idx, int64_t m,
+                       const void* acc_in, void* vals, bool device, int fin, float fv, int grid, hipStream_t s) {
+    if (device) {  // float16 only: bfloat16 has no single-rounding path in torch-ROCm
+        if constexpr (FMT == FEDAVG_F16)
+            return launch_tails_f<FMT, true>(tab, K, tile, tstride, idx, m, acc_in, vals, fin, fv, grid, s);
+        else
+            return hipErrorInvalidValue;
     }
-    if (fmt == FEDAVG_BF16)
-        return launch_tails_f<FEDAVG_BF16, false>(tab, K, tile, tstride, idx, m, acc_in, vals, fin, fin_val, grid, s);
-    if (fmt == FEDAVG_F16)
-        return launch_tails_f<FEDAVG_F16, false>(tab, K, tile, tstride, idx, m, acc_in, vals, fin, fin_val, grid, s);
-    return hipErrorInvalidValue;
-}
-
-hipError_t launch_scatter16(const int64_t* idx, const void* vals, int64_t m, void* out, hipStream_t s) {
-    const int grid = (int)((m + kBlock - 1) / kBlock);
-    if (grid == 0) return hipSuccess;
-    hipLaunchKernelGGL(fedavg_scatter16, dim3(grid), dim3(kBlock), 0, s, idx, static_cast<const uint16_t*>(vals), m,
-                       static_cast<uint16_t*>(out));
-    return hipGetLastError();
+    return launch_tails_f<FMT, false>(tab, K, tile, tstride, idx, m, acc_in, vals, fin, fv, grid, s);
 }
 
 template <int FMT, int OP, int FIN, bool ACC_IN>
@@ -843,13 +831,73 @@ static hipError_t launch_n_o(const RowTableNarrow& tab, int K, const void* acc_i
     }
 }
 
+template <int FMT>
+hipError_t rows16_fmt(const RowTableNarrow& tab, int K, const void* acc_in, void* out, int64_t n, int op, int fin,
+                      float fv, int grid, bool vec, hipStream_t s) {
+    return launch_n_o<FMT>(tab, K, acc_in, out, n, op, fin, fv, grid, vec, s);
+}
+
+#define FEDAVG_NARROW_ENTRIES(PREFIX, FMT)                                                                             \
+    PREFIX hipError_t tiles16_fmt<FMT>(const RowTableNarrow&, int, int64_t, const void*, void*, int64_t, int64_t, int, \
+                                       int, float, int, int, hipStream_t, uint64_t*);                                 \
+    PREFIX hipError_t rows16_fmt<FMT>(const RowTableNarrow&, int, const void*, void*, int64_t, int, int, float, int,   \
+                                      bool, hipStream_t);                                                              \
+    PREFIX hipError_t tails16_fmt<FMT>(const RowTableNarrow&, int, int64_t, int64_t, const int64_t*, int64_t,          \
+                                       const void*, void*, bool, int, float, int, hipStream_t);
+#if FEDAVG_NARROW_PART == 1
+FEDAVG_NARROW_ENTRIES(extern template, FEDAVG_F16)  // in the float16 unit
+#elif FEDAVG_NARROW_PART == 2
+FEDAVG_NARROW_ENTRIES(template, FEDAVG_F16)
+#endif
+#undef FEDAVG_NARROW_ENTRIES
+
+#if FEDAVG_NARROW_PART != 2  // the dispatchers, and the format-free scatter
+hipError_t launch_tiles_narrow(const RowTableNarrow& tab, int K, int64_t tstride_elems, const void* acc_in, void* out,
+                               int64_t begin, int64_t end, int fmt, int op, int fin, float fin_val, int grid,
+                               int burst, hipStream_t s, uint64_t* nl) {
+    const int64_t ts8 = tstride_elems / 8, b8 = begin / 8, e8 = end / 8;
+    if (fmt == FEDAVG_BF16)
+        return tiles16_fmt<FEDAVG_BF16>(tab, K, ts8, acc_in, out, b8, e8, op, fin, fin_val, grid, burst, s, nl);
+    if (fmt == FEDAVG_F16)
+        return tiles16_fmt<FEDAVG_F16>(tab, K, ts8, acc_in, out, b8, e8, op, fin, fin_val, grid, burst, s, nl);
+    return hipErrorInvalidValue;
+}
+
 hipError_t launch_rows_narrow(const RowTableNarrow& tab, int K, const void* acc_in, void* out, int64_t n, int fmt,
                               int op, int fin, float fin_val, int grid, hipStream_t s) {
     bool vec = reinterpret_cast<uintptr_t>(out) % 16 == 0 && reinterpret_cast<uintptr_t>(acc_in) % 16 == 0;
     for (int k = 0; vec && k < K; ++k) vec = reinterpret_cast<uintptr_t>(tab.rows[k]) % 16 == 0;
-    if (fmt == FEDAVG_BF16) return launch_n_o<FEDAVG_BF16>(tab, K, acc_in, out, n, op, fin, fin_val, grid, vec, s);
-    if (fmt == FEDAVG_F16) return launch_n_o<FEDAVG_F16>(tab, K, acc_in, out, n, op, fin, fin_val, grid, vec, s);
+    if (fmt == FEDAVG_BF16) return rows16_fmt<FEDAVG_BF16>(tab, K, acc_in, out, n, op, fin, fin_val, grid, vec, s);
+    if (fmt == FEDAVG_F16) return rows16_fmt<FEDAVG_F16>(tab, K, acc_in, out, n, op, fin, fin_val, grid, vec, s);
     return hipErrorInvalidValue;
 }
+
+hipError_t launch_torch16_tails(const RowTableNarrow& tab, int K, int64_t tile, int64_t tstride, const int64_t* idx,
+                                int64_t m, const void* acc_in, void* vals, int fmt, int op, int fin, float fin_val,
+                                hipStream_t s) {
+    const int grid = (int)((m + kBlock - 1) / kBlock);
+    if (grid == 0) return hipSuccess;
+    const bool device = op == FEDAVG_OP_TORCH_DEVICE;
+    if (fmt == FEDAVG_BF16)
+        return tails16_fmt<FEDAVG_BF16>(tab, K, tile, tstride, idx, m, acc_in, vals, device, fin, fin_val, grid, s);
+    if (fmt == FEDAVG_F16)
+        return tails16_fmt<FEDAVG_F16>(tab, K, tile, tstride, idx, m, acc_in, vals, device, fin, fin_val, grid, s);
+    return hipErrorInvalidValue;
+}
+
+__global__ void __launch_bounds__(kBlock) fedavg_scatter16(const int64_t* idx, const uint16_t* vals, const int64_t m,
+                                                            uint16_t* out) {
+    const int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (j < m) out[idx[j]] = vals[j];
+}
+
+hipError_t launch_scatter16(const int64_t* idx, const void* vals, int64_t m, void* out, hipStream_t s) {
+    const int grid = (int)((m + kBlock - 1) / kBlock);
+    if (grid == 0) return hipSuccess;
+    hipLaunchKernelGGL(fedavg_scatter16, dim3(grid), dim3(kBlock), 0, s, idx, static_cast<const uint16_t*>(vals), m,
+                       static_cast<uint16_t*>(out));
+    return hipGetLastError();
+}
+#endif
 
 }  // namespace fedavg
