@@ -62,14 +62,19 @@ def needs_build() -> bool:
 
 def compile_units(sources=SOURCES, ab=False):
     """(source, object name, extra flags) of every translation unit: the fused kernels' source once per EPI_UNITS
-    entry (EPI_UNITS_AB for an A/B build), the 16-bit source once per format, the others once each."""
+    entry (EPI_UNITS_AB for an A/B build) in two halves by optimizer kind, the 16-bit source once per format, the others
+    once each."""
     units = []
     for src in sources:
-        if src == EPI_SOURCE:
-            units += [(src, f"fedavg_epi_{name}.hip.o",
-                       ["-DFEDAVG_EPI_STEP"] if op is None else
-                       [f"-DFEDAVG_EPI_OP={op}", f"-DFEDAVG_EPI_FIN={fin}", f"-DFEDAVG_EPI_FN=launch_epi_{name}"])
-                      for name, op, fin in (EPI_UNITS_AB if ab else EPI_UNITS)]
+        if src == EPI_SOURCE:  # each (mode, finalisation) pair in two halves (fedavg_epi_inst.hip FEDAVG_EPI_PART)
+            for name, op, fin in (EPI_UNITS_AB if ab else EPI_UNITS):
+                if op is None:
+                    units.append((src, f"fedavg_epi_{name}.hip.o", ["-DFEDAVG_EPI_STEP"]))
+                    continue
+                defs = [f"-DFEDAVG_EPI_OP={op}", f"-DFEDAVG_EPI_FIN={fin}", f"-DFEDAVG_EPI_FN=launch_epi_{name}",
+                        f"-DFEDAVG_EPI_FN2=launch_epi_{name}_part2"]
+                units += [(src, f"fedavg_epi_{name}.hip.o", defs + ["-DFEDAVG_EPI_PART=1"]),
+                          (src, f"fedavg_epi_{name}_part2.hip.o", defs + ["-DFEDAVG_EPI_PART=2"])]
         elif src == NARROW_SOURCE:  # once per 16-bit format (fedavg_narrow.hip FEDAVG_NARROW_PART)
             units += [(src, "fedavg_narrow_bf16.hip.o", ["-DFEDAVG_NARROW_PART=1"]),
                       (src, "fedavg_narrow_f16.hip.o", ["-DFEDAVG_NARROW_PART=2"])]
@@ -112,7 +117,8 @@ def build_library(force: bool = False, verbose: bool = False, jobs: int = 0) -> 
 
     # the longest units first (the 16-bit and fused units take minutes each, the rest seconds to a minute), so the
     # pool's critical path is one long unit, not a long unit started last
-    units = sorted(compile_units(), key=lambda u: 0 if u[0] in (NARROW_SOURCE, EPI_SOURCE) else 1)
+    units = sorted(compile_units(), key=lambda u: 0 if "_part2" in u[1] else 1 if u[0] == EPI_SOURCE else
+                   2 if u[0] == NARROW_SOURCE else 3)
 
     def compile_one(unit) -> str:
         src, obj_name, extra = unit

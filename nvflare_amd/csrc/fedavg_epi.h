@@ -858,40 +858,38 @@ inline hipError_t sqrt_mode(const TileLaunch& L, const EpiParams& E, hipStream_t
     return launch_epi_k<OP, FIN, ACC_IN, KIND>(L, E, s, nl);
 }
 
-template <int OP, int FIN, bool ACC_IN>
+// KINDS: the optimizer kinds this translation unit carries (bit k = kind k; the build splits each (mode,
+// finalisation) pair over two units, fedavg_epi_inst.hip); a kind outside it is refused, never run in another form
+template <int OP, int FIN, bool ACC_IN, unsigned KINDS = ~0u>
 inline hipError_t launch_epi_a(const TileLaunch& L, const EpiParams& E, hipStream_t s, uint64_t* nl) {
+#define FEDAVG_EPI_CASE(KIND, CALL)                                                                                    \
+    case KIND:                                                                                                       \
+        if constexpr ((KINDS >> KIND) & 1u) return CALL<OP, FIN, ACC_IN, KIND>(L, E, s, nl);                         \
+        else return hipErrorNotSupported;
     switch (E.kind) {
-        case FEDAVG_EPI_ADD_BASE:
-            return launch_epi_k<OP, FIN, ACC_IN, FEDAVG_EPI_ADD_BASE>(L, E, s, nl);
-        case FEDAVG_EPI_SGD:
-            return launch_epi_k<OP, FIN, ACC_IN, FEDAVG_EPI_SGD>(L, E, s, nl);
-        case FEDAVG_EPI_ADAM:
-            return sqrt_mode<OP, FIN, ACC_IN, FEDAVG_EPI_ADAM>(L, E, s, nl);
-        case FEDAVG_EPI_ADAGRAD:
-            return sqrt_mode<OP, FIN, ACC_IN, FEDAVG_EPI_ADAGRAD>(L, E, s, nl);
-        case FEDAVG_EPI_RMSPROP:
-            return sqrt_mode<OP, FIN, ACC_IN, FEDAVG_EPI_RMSPROP>(L, E, s, nl);
-        case FEDAVG_EPI_ADAMAX:
-            return launch_epi_k<OP, FIN, ACC_IN, FEDAVG_EPI_ADAMAX>(L, E, s, nl);
-        case FEDAVG_EPI_NADAM:
-            return sqrt_mode<OP, FIN, ACC_IN, FEDAVG_EPI_NADAM>(L, E, s, nl);
-        case FEDAVG_EPI_RADAM:
-            return sqrt_mode<OP, FIN, ACC_IN, FEDAVG_EPI_RADAM>(L, E, s, nl);
-        case FEDAVG_EPI_RPROP:
-            return launch_epi_k<OP, FIN, ACC_IN, FEDAVG_EPI_RPROP>(L, E, s, nl);
-        case FEDAVG_EPI_ASGD:
-            return launch_epi_k<OP, FIN, ACC_IN, FEDAVG_EPI_ASGD>(L, E, s, nl);
+        FEDAVG_EPI_CASE(FEDAVG_EPI_ADD_BASE, launch_epi_k)
+        FEDAVG_EPI_CASE(FEDAVG_EPI_SGD, launch_epi_k)
+        FEDAVG_EPI_CASE(FEDAVG_EPI_ADAM, sqrt_mode)
+        FEDAVG_EPI_CASE(FEDAVG_EPI_ADAGRAD, sqrt_mode)
+        FEDAVG_EPI_CASE(FEDAVG_EPI_RMSPROP, sqrt_mode)
+        FEDAVG_EPI_CASE(FEDAVG_EPI_ADAMAX, launch_epi_k)
+        FEDAVG_EPI_CASE(FEDAVG_EPI_NADAM, sqrt_mode)
+        FEDAVG_EPI_CASE(FEDAVG_EPI_RADAM, sqrt_mode)
+        FEDAVG_EPI_CASE(FEDAVG_EPI_RPROP, launch_epi_k)
+        FEDAVG_EPI_CASE(FEDAVG_EPI_ASGD, launch_epi_k)
         default:
             return hipErrorInvalidValue;
     }
+#undef FEDAVG_EPI_CASE
 }
 
 // one (mode, finalisation) pair's entry; product builds carry no chained-sum forms here (launch_epi_step has the
 // server step's, fedavg_internal.h epi_direct)
-template <int OP, int FIN>
+template <int OP, int FIN, unsigned KINDS = ~0u>
 inline hipError_t launch_epi_f(const TileLaunch& L, const EpiParams& E, hipStream_t s, uint64_t* nl) {
-    if constexpr (kAB) return L.acc_in ? launch_epi_a<OP, FIN, true>(L, E, s, nl) : launch_epi_a<OP, FIN, false>(L, E, s, nl);
-    return L.acc_in ? hipErrorNotSupported : launch_epi_a<OP, FIN, false>(L, E, s, nl);
+    if constexpr (kAB)
+        return L.acc_in ? launch_epi_a<OP, FIN, true, KINDS>(L, E, s, nl) : launch_epi_a<OP, FIN, false, KINDS>(L, E, s, nl);
+    return L.acc_in ? hipErrorNotSupported : launch_epi_a<OP, FIN, false, KINDS>(L, E, s, nl);
 }
 
 }  // namespace fedavg

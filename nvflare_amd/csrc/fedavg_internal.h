@@ -201,6 +201,7 @@ inline bool epi_direct(int op, int fin, int k, bool acc_in) {
 // the few-client forms' geometry: blocks per CU, register-held tiles R, LDS-held tiles L, LDS tiles per load group G
 struct FewForm {
     int bpc, r, l, g;
+    int p = 0;  // 16-bit form only: tiles per unit (0 / 1: one; 2: a pair of consecutive tiles, K x 16 KiB contiguous)
 };
 // the product's form per read count: the best of two sweeps (profiles/r05/s2/few_k*.jsonl, s3/few_k*.jsonl; 1e9
 // params, interleaved in one process, outputs bit-equal, % of 8 TB/s): 1 read -- two blocks per CU, 8 register- + 4
@@ -232,17 +233,21 @@ inline FewForm few_form(int reads, int variant) {
     }
     return kFewDefault[reads];
 }
-// The 16-bit few-client form (fedavg_narrow.hip fedavg_tiles_narrow_few, 1-3 reads): {blocks/CU, register tiles, LDS
-// tiles, LDS tiles per load group} of 8 KiB tiles (at two blocks per CU at most 10 LDS tiles: 160 KiB per CU).
-// Defaults from the same-process sweeps of profiles/r05/s10/ and s11/ (bf16 x 1e9, packed arithmetic): 1 / 2 / 3
-// reads 67.5-68.0 / 71.8 / 73.8 % of 8 TB/s, against 38.0 / 55.9 / 66.0 % on the burst form (profiles/r05/s8/, s9/).
+// The 16-bit few-client form (fedavg_narrow.hip fedavg_tiles_narrow_few, 1-3 reads): {blocks/CU, register units, LDS
+// units, LDS units per load group, tiles per unit} -- a unit one 8 KiB tile, or (p = 2) a pair of consecutive tiles,
+// K x 16 KiB of contiguous slab: the fp32 forms' geometry in bytes.  Session 17 found a 1-client COPY through single
+// tiles no faster than the arithmetic (64-66 % of 8 TB/s); on pairs it runs 76.6 % and the torch-mode line 74.5 %
+// (profiles/r05/s18/, same process, outputs bit-equal).  Defaults, bf16 x 1e9, % of 8 TB/s: 1 read -- pairs, G 4:
+// 74.5 against 66.0 single (38.0 on the burst form); 2 reads -- single tiles: 72.2 against 66.8-69.2 on pairs (the
+// 2-client arithmetic weighs on the longer units); 3 reads -- pairs, G 2: 75.0 against 73.9 single.
 constexpr int kNarrowFewMaxReads = 3;
-constexpr FewForm kNarrowFewDefault[kNarrowFewMaxReads + 1] = {{0, 0, 0, 0}, {2, 8, 8, 4}, {2, 8, 8, 4}, {1, 8, 20, 4}};
+constexpr FewForm kNarrowFewDefault[kNarrowFewMaxReads + 1] = {
+    {0, 0, 0, 0}, {2, 8, 4, 4, 2}, {2, 8, 8, 4}, {1, 4, 10, 2, 2}};
 // A/B builds (-DFEDAVG_AB_FEW): launch variant bits 9-11 = 1-4 pick one of these per read count
 constexpr FewForm kNarrowFewAB[3][4] = {
-    {{2, 16, 8, 4}, {2, 6, 8, 4}, {2, 8, 10, 2}, {2, 12, 8, 4}},
-    {{1, 8, 20, 2}, {1, 6, 20, 4}, {1, 8, 20, 4}, {1, 10, 20, 4}},
-    {{1, 6, 20, 2}, {1, 8, 20, 2}, {1, 4, 20, 2}, {2, 4, 8, 2}}};
+    {{2, 8, 8, 4}, {2, 8, 4, 2, 2}, {2, 6, 4, 4, 2}, {2, 16, 8, 4}},
+    {{1, 4, 10, 1, 2}, {1, 4, 10, 2, 2}, {1, 8, 20, 2}, {1, 6, 20, 4}},
+    {{1, 8, 20, 4}, {1, 4, 10, 1, 2}, {1, 8, 20, 2}, {1, 6, 20, 2}}};
 
 inline FewForm narrow_few_form(int reads, int form) {
     if (kABFew && form >= 1 && form <= 4) return kNarrowFewAB[reads - 1][form - 1];
@@ -275,7 +280,7 @@ constexpr bool few_forms_fit(const FewForm (&forms)[N], int tile_bytes) {
         const FewForm& f = forms[i];
         if (f.bpc == 0) continue;  // the unused read-count-0 slot
         if (f.bpc < 1 || f.r < 1 || f.l < 0 || f.g < 1 || (f.l > 0 && f.l % f.g != 0)) return false;
-        if ((int64_t)f.bpc * f.l * tile_bytes > kLdsBytesPerCu) return false;
+        if ((int64_t)f.bpc * f.l * tile_bytes * (f.p > 1 ? f.p : 1) > kLdsBytesPerCu) return false;
     }
     return true;
 }

@@ -486,14 +486,19 @@ __attribute__((amdgpu_waves_per_eu(FEDAVG_NARROW_BURST_WAVES, FEDAVG_NARROW_BURS
 // packed form (pack2 / step2: two elements per instruction), and FIN_DIV is the exact fp32 quotient by Markstein's
 // correction with one rare-case branch per tile (fedavg_arith.h div_const_fast), rounded to the format as torch's
 // div_ rounds it.  Per-element sequence as tile_sum16's: the same bits.
-template <int FMT, int OP, int FIN, int KC, int R, int L, int G, int B>
+// P = 2 (the 1- and 3-read defaults): a unit is a pair of consecutive tiles -- K x 16 KiB of contiguous slab per
+// unit, the fp32 forms' shape in bytes; the pair's second tile past the range's last tile re-reads that tile (never
+// stored).
+template <int FMT, int OP, int FIN, int KC, int R, int L, int G, int B, int P = 1>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(B, 2)))  // B blocks per CU must co-reside
 fedavg_tiles_narrow_few(const RowTableNarrow tab, const int64_t tstride8, u32x4* out, const int64_t b8, const int64_t e8,
                         const float fv, const int64_t t0, const int64_t t_end) {
     static_assert(KC >= 1 && KC <= 3, "one to three row reads");
     static_assert(L == 0 || L % G == 0, "whole LDS groups");
-    constexpr int CPL = kCpl16;
-    constexpr int64_t T8 = (int64_t)CPL * kBlock;
+    static_assert(P == 1 || P == 2, "single tiles or pairs");
+    constexpr int CPL = kCpl16 * P;                      // u32x4 per lane per unit
+    constexpr int64_t T8 = (int64_t)CPL * kBlock;        // u32x4 per unit
+    const int64_t last_tile = (e8 - 1) / ((int64_t)kCpl16 * kBlock);
     const FinConst fc = fin_const<FIN>(fv);
     __shared__ u32x4 staged[L > 0 ? L * CPL * kBlock : 1];
     const int64_t t_first = t0 + blockIdx.x;
@@ -502,12 +507,19 @@ fedavg_tiles_narrow_few(const RowTableNarrow tab, const int64_t tstride8, u32x4*
         return t < t_end ? t : t_end - 1;
     };
     auto load_tile = [&](u32x4 (&v)[KC][CPL], const int m) __attribute__((always_inline)) {
-        const int64_t off = tile_of(m) * tstride8 + threadIdx.x;
+        const int64_t u = tile_of(m);
 #pragma unroll
-        for (int j = 0; j < KC; ++j)
+        for (int h = 0; h < P; ++h) {
+            int64_t tile = u * P + h;
+            tile = tile <= last_tile ? tile : last_tile;
+            const int64_t off = tile * tstride8 + threadIdx.x;
 #pragma unroll
-            for (int c = 0; c < CPL; ++c)
-                v[j][c] = __builtin_nontemporal_load(static_cast<const u32x4*>(tab.rows[j]) + off + c * kBlock);
+            for (int j = 0; j < KC; ++j)
+#pragma unroll
+                for (int c = 0; c < kCpl16; ++c)
+                    v[j][h * kCpl16 + c] =
+                        __builtin_nontemporal_load(static_cast<const u32x4*>(tab.rows[j]) + off + c * kBlock);
+        }
     };
     auto finish = [&](u32x4 (&res)[CPL], const u32x4 (&v)[KC][CPL]) __attribute__((always_inline)) {
         uint32_t word[CPL][4];  // the running values, rounded to the format, two per word
@@ -559,14 +571,14 @@ fedavg_tiles_narrow_few(const RowTableNarrow tab, const int64_t tstride8, u32x4*
     }
 }
 
-template <int FMT, int OP, int FIN, int KC, int R, int L, int G, int B>
+template <int FMT, int OP, int FIN, int KC, int R, int L, int G, int B, int P = 1>
 static hipError_t launch_narrow_few_form(const RowTableNarrow& tab, int64_t tstride8, void* out, int64_t b8, int64_t e8,
                                          float fv, int grid, hipStream_t s, uint64_t* nl) {
-    constexpr int64_t T8 = (int64_t)kCpl16 * kBlock;
+    constexpr int64_t U8 = (int64_t)kCpl16 * kBlock * P;
     u32x4* o = static_cast<u32x4*>(out);
-    return burst_launches(b8 / T8, (e8 - 1) / T8 + 1, grid, R + L, nl, false, [&](int nb, int64_t t0, int64_t t_end, uint32_t) {
-        hipLaunchKernelGGL((fedavg_tiles_narrow_few<FMT, OP, FIN, KC, R, L, G, B>), dim3(nb), dim3(kBlock), 0, s, tab, tstride8,
-                           o, b8, e8, fv, t0, t_end);
+    return burst_launches(b8 / U8, (e8 - 1) / U8 + 1, grid, R + L, nl, false, [&](int nb, int64_t t0, int64_t t_end, uint32_t) {
+        hipLaunchKernelGGL((fedavg_tiles_narrow_few<FMT, OP, FIN, KC, R, L, G, B, P>), dim3(nb), dim3(kBlock), 0, s, tab,
+                           tstride8, o, b8, e8, fv, t0, t_end);
     });
 }
 
@@ -575,34 +587,38 @@ static hipError_t launch_narrow_few(const RowTableNarrow& tab, int64_t tstride8,
                                     float fv, int grid, int form, hipStream_t s, uint64_t* nl) {
     const FewForm f = narrow_few_form(KC, form);
 #define FEDAVG_NFEW(B, R, LL, G)                                      \
-    if (f.bpc == B && f.r == R && f.l == LL && f.g == G)              \
+    if (f.bpc == B && f.r == R && f.l == LL && f.g == G && f.p <= 1)  \
         return launch_narrow_few_form<FMT, OP, FIN, KC, R, LL, G, B>(tab, tstride8, out, b8, e8, fv, grid, s, nl);
+#define FEDAVG_NFEW2(B, R, LL, G)                                     \
+    if (f.bpc == B && f.r == R && f.l == LL && f.g == G && f.p == 2)  \
+        return launch_narrow_few_form<FMT, OP, FIN, KC, R, LL, G, B, 2>(tab, tstride8, out, b8, e8, fv, grid, s, nl);
     if constexpr (KC == 1) {
-        FEDAVG_NFEW(2, 8, 8, 4)
+        FEDAVG_NFEW2(2, 8, 4, 4)
         if constexpr (kABFew) {
+            FEDAVG_NFEW(2, 8, 8, 4)
+            FEDAVG_NFEW2(2, 8, 4, 2)
+            FEDAVG_NFEW2(2, 6, 4, 4)
             FEDAVG_NFEW(2, 16, 8, 4)
-            FEDAVG_NFEW(2, 6, 8, 4)
-            FEDAVG_NFEW(2, 8, 10, 2)
-            FEDAVG_NFEW(2, 12, 8, 4)
         }
     } else if constexpr (KC == 2) {
         FEDAVG_NFEW(2, 8, 8, 4)
         if constexpr (kABFew) {
+            FEDAVG_NFEW2(1, 4, 10, 1)
+            FEDAVG_NFEW2(1, 4, 10, 2)
             FEDAVG_NFEW(1, 8, 20, 2)
             FEDAVG_NFEW(1, 6, 20, 4)
-            FEDAVG_NFEW(1, 8, 20, 4)
-            FEDAVG_NFEW(1, 10, 20, 4)
         }
     } else {
-        FEDAVG_NFEW(1, 8, 20, 4)
+        FEDAVG_NFEW2(1, 4, 10, 2)
         if constexpr (kABFew) {
-            FEDAVG_NFEW(1, 6, 20, 2)
+            FEDAVG_NFEW(1, 8, 20, 4)
+            FEDAVG_NFEW2(1, 4, 10, 1)
             FEDAVG_NFEW(1, 8, 20, 2)
-            FEDAVG_NFEW(1, 4, 20, 2)
-            FEDAVG_NFEW(2, 4, 8, 2)
+            FEDAVG_NFEW(1, 6, 20, 2)
         }
     }
 #undef FEDAVG_NFEW
+#undef FEDAVG_NFEW2
     return hipErrorInvalidValue;
 }
 

@@ -19,7 +19,8 @@ def main():
     ap.add_argument("--params", type=float, default=1e9)
     ap.add_argument("--fmt", choices=["bfloat16", "float16"], default="bfloat16")
     ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--mode", choices=["torch", "numpy"], default="torch")
+    ap.add_argument("--mode", choices=["torch", "numpy", "copy"], default="torch",
+                    help="copy: unweighted, no finalisation -- the 1-client launch moves bytes only")
     ap.add_argument("--blocks-per-cu", default="0", help="comma list: interleaved same-process sweep (0 = default)")
     ap.add_argument("--variants", default="0", help="comma list of fedavg_set_variant values (0 = burst kernel, "
                                                       "8 = per-tile stores), swept with every blocks-per-cu value")
@@ -51,8 +52,8 @@ def main():
     out = torch.empty((P + 7) // 8 * 8, dtype=tdt, device="cuda:0")
     torch.cuda.synchronize()
     code = N.FEDAVG_BF16 if args.fmt == "bfloat16" else N.FEDAVG_F16
-    op = N.FEDAVG_OP_TORCH if args.mode == "torch" else N.FEDAVG_OP_NUMPY
-    fin = N.FEDAVG_FIN_DIV if args.mode == "torch" else N.FEDAVG_FIN_SCALE
+    op = {"torch": N.FEDAVG_OP_TORCH, "numpy": N.FEDAVG_OP_NUMPY, "copy": N.FEDAVG_OP_UNWEIGHTED}[args.mode]
+    fin = {"torch": N.FEDAVG_FIN_DIV, "numpy": N.FEDAVG_FIN_SCALE, "copy": N.FEDAVG_FIN_NONE}[args.mode]
     ws = [float(1 + (37 * k) % 100) for k in range(K)]
     end = (P + 7) // 8 * 8
 
