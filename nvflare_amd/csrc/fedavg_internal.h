@@ -215,13 +215,14 @@ struct FewForm {
 constexpr int kFewMaxReads = 3;
 constexpr FewForm kFewDefault[kFewMaxReads + 1] = {{0, 0, 0, 0}, {2, 8, 4, 2}, {1, 4, 10, 1}, {1, 4, 10, 1}};
 // A/B builds: launch variant bits 9-11 pick one of these per read count (1-6; 0 = the default)
+// (5-6: tile pairs, p = 2 -- 32 KiB per client per unit, session 18's 16-bit finding carried over)
 constexpr FewForm kFewAB[2][6] = {
-    {{2, 8, 4, 2}, {1, 12, 10, 2}, {1, 8, 10, 1}, {2, 10, 4, 2}, {2, 8, 4, 4}, {1, 16, 10, 2}},
-    {{1, 4, 10, 1}, {1, 6, 10, 1}, {1, 5, 10, 1}, {1, 4, 9, 1}, {1, 3, 10, 1}, {1, 4, 10, 2}}};
+    {{2, 8, 4, 2}, {1, 12, 10, 2}, {1, 8, 10, 1}, {2, 10, 4, 2}, {2, 4, 2, 1, 2}, {2, 4, 2, 2, 2}},
+    {{1, 4, 10, 1}, {1, 6, 10, 1}, {1, 5, 10, 1}, {1, 4, 9, 1}, {1, 2, 5, 1, 2}, {2, 2, 2, 1, 2}}};
 // A/B builds: the few-client kernel at 3-4 reads in other forms (variant bits 9-11 = 1-5; 6 and 7 select the burst
 // form's client loop for 3-6 clients instead, fedavg_tiles.h launch_burst)
 constexpr FewForm kFewAB34[2][6] = {
-    {{1, 2, 10, 1}, {1, 3, 10, 1}, {1, 4, 10, 1}, {2, 2, 4, 1}, {1, 2, 8, 1}, {2, 3, 4, 1}},
+    {{1, 2, 10, 1}, {1, 3, 10, 1}, {1, 4, 10, 1}, {1, 2, 5, 1, 2}, {1, 1, 5, 1, 2}, {2, 3, 4, 1}},
     {{1, 2, 10, 1}, {1, 3, 10, 1}, {1, 1, 10, 1}, {2, 2, 4, 1}, {1, 2, 8, 1}, {1, 2, 10, 2}}};
 
 // the few-client form of a launch with `reads` (1-3; A/B builds 4) client reads

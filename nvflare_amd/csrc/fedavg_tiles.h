@@ -292,14 +292,19 @@ fedavg_tiles_burst_f32x4(const RowTableF32 tab, const int K, const int64_t tstri
 //   4. every result stored: the LDS-held tiles', then the register-held tiles' -- the launch's write burst.
 // Per-element sequence as tile_sum_kc's (first4, then step4 for client 1), so the bits are the burst kernel's.
 // ---------------------------------------------------------------------------------------------
-template <int OP, int FIN, int KC, int R, int L, int G>
+// P = 2 (A/B forms): a unit is a pair of consecutive tiles, K x 32 KiB of contiguous slab; the pair's second tile past
+// the range's last tile re-reads that tile (never stored).
+template <int OP, int FIN, int KC, int R, int L, int G, int P = 1>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, 2)))
 fedavg_tiles_few_f32x4(const RowTableF32 tab, const int64_t tstride4, f32x4* out, const int64_t b4, const int64_t e4,
                        const float fin_val, const int64_t t0, const int64_t t_end) {
     static_assert(KC >= 1 && KC <= 4, "one to four row reads (3-4: A/B builds only)");
     static_assert(L % G == 0 || L == 0, "whole LDS groups");
-    constexpr int CPL = 4;
-    constexpr int64_t T4 = (int64_t)CPL * kBlock;
+    static_assert(P == 1 || P == 2, "single tiles or pairs");
+    constexpr int CPT = 4;  // float4 columns per lane per tile
+    constexpr int CPL = CPT * P;
+    constexpr int64_t T4 = (int64_t)CPL * kBlock;  // float4 per unit
+    const int64_t last_tile = (e4 - 1) / ((int64_t)CPT * kBlock);
     const FinConst fc = fin_const<FIN>(fin_val);
     __shared__ f32x4 staged[L > 0 ? L * CPL * kBlock : 1];
     const int64_t t_first = t0 + blockIdx.x;
@@ -315,28 +320,30 @@ fedavg_tiles_few_f32x4(const RowTableF32 tab, const int64_t tstride4, f32x4* out
             for (int j = 1; j < KC; ++j) acc[c] = step4<OP>(acc[c], v[j][c], tab.w[j]);
         }
     };
+    auto load_unit = [&](f32x4 (&v)[KC][CPL], const int m) __attribute__((always_inline)) {
+        const int64_t u = tile_of(m);
+#pragma unroll
+        for (int h = 0; h < P; ++h) {
+            int64_t tile = u * P + h;
+            tile = tile <= last_tile ? tile : last_tile;
+            const int64_t off = tile * tstride4 + threadIdx.x;
+#pragma unroll
+            for (int j = 0; j < KC; ++j)
+#pragma unroll
+                for (int c = 0; c < CPT; ++c)
+                    v[j][h * CPT + c] = __builtin_nontemporal_load(tab.rows[j] + off + c * kBlock);
+        }
+    };
     // 1. the register-held tiles' loads
     f32x4 vr[R][KC][CPL];
 #pragma unroll
-    for (int m = 0; m < R; ++m) {
-        const int64_t off = tile_of(L + m) * tstride4 + threadIdx.x;
-#pragma unroll
-        for (int j = 0; j < KC; ++j)
-#pragma unroll
-            for (int c = 0; c < CPL; ++c) vr[m][j][c] = __builtin_nontemporal_load(tab.rows[j] + off + c * kBlock);
-    }
+    for (int m = 0; m < R; ++m) load_unit(vr[m], L + m);
     // 2. the LDS-held tiles (slots 0 .. L-1), G at a time
 #pragma unroll
     for (int g = 0; g < L; g += G) {
         f32x4 v[G][KC][CPL];
 #pragma unroll
-        for (int m = 0; m < G; ++m) {
-            const int64_t off = tile_of(g + m) * tstride4 + threadIdx.x;
-#pragma unroll
-            for (int j = 0; j < KC; ++j)
-#pragma unroll
-                for (int c = 0; c < CPL; ++c) v[m][j][c] = __builtin_nontemporal_load(tab.rows[j] + off + c * kBlock);
-        }
+        for (int m = 0; m < G; ++m) load_unit(v[m], g + m);
 #pragma unroll
         for (int m = 0; m < G; ++m) {
             f32x4 acc[CPL], r[CPL];
@@ -372,14 +379,15 @@ fedavg_tiles_few_f32x4(const RowTableF32 tab, const int64_t tstride4, f32x4* out
 // ---------------------------------------------------------------------------------------------
 // launchers
 // ---------------------------------------------------------------------------------------------
-template <int OP, int FIN, int KC, int R, int L, int G>
+template <int OP, int FIN, int KC, int R, int L, int G, int P = 1>
 inline hipError_t launch_few_form(const TileLaunch& L_, hipStream_t s, uint64_t* nl) {
     f32x4* o = reinterpret_cast<f32x4*>(L_.out);
-    return burst_launches(L_.b4 / L_.tile4, (L_.e4 - 1) / L_.tile4 + 1, L_.grid, R + L, nl,
+    const int64_t u4 = L_.tile4 * P;
+    return burst_launches(L_.b4 / u4, (L_.e4 - 1) / u4 + 1, L_.grid, R + L, nl,
                           L_.variant & kVariantAnyOrder, [&](int nb, int64_t t0, int64_t t_end, uint32_t flags) {
-                              hipExtLaunchKernelGGL((fedavg_tiles_few_f32x4<OP, FIN, KC, R, L, G>), dim3(nb), dim3(kBlock),
-                                                    0, s, nullptr, nullptr, flags, L_.tab, L_.tstride4, o, L_.b4, L_.e4,
-                                                    L_.fin_val, t0, t_end);
+                              hipExtLaunchKernelGGL((fedavg_tiles_few_f32x4<OP, FIN, KC, R, L, G, P>), dim3(nb),
+                                                    dim3(kBlock), 0, s, nullptr, nullptr, flags, L_.tab, L_.tstride4, o,
+                                                    L_.b4, L_.e4, L_.fin_val, t0, t_end);
                           });
 }
 
@@ -388,15 +396,17 @@ template <int OP, int FIN, int KC>
 inline hipError_t launch_few(const TileLaunch& L, hipStream_t s, uint64_t* nl) {
     const FewForm f = few_form(KC, L.variant);
 #define FEDAVG_FEW(R, LL, G)                                                       \
-    if (f.r == R && f.l == LL && f.g == G) return launch_few_form<OP, FIN, KC, R, LL, G>(L, s, nl);
+    if (f.r == R && f.l == LL && f.g == G && f.p <= 1) return launch_few_form<OP, FIN, KC, R, LL, G>(L, s, nl);
+#define FEDAVG_FEW2(R, LL, G)                                                      \
+    if (f.r == R && f.l == LL && f.g == G && f.p == 2) return launch_few_form<OP, FIN, KC, R, LL, G, 2>(L, s, nl);
     if constexpr (KC == 1) {
         FEDAVG_FEW(8, 4, 2)
         if constexpr (kABFew) {
             FEDAVG_FEW(12, 10, 2)
             FEDAVG_FEW(8, 10, 1)
             FEDAVG_FEW(10, 4, 2)
-            FEDAVG_FEW(8, 4, 4)
-            FEDAVG_FEW(16, 10, 2)
+            FEDAVG_FEW2(4, 2, 1)
+            FEDAVG_FEW2(4, 2, 2)
         }
     } else if constexpr (KC == 2) {
         FEDAVG_FEW(4, 10, 1)
@@ -404,16 +414,16 @@ inline hipError_t launch_few(const TileLaunch& L, hipStream_t s, uint64_t* nl) {
             FEDAVG_FEW(6, 10, 1)
             FEDAVG_FEW(5, 10, 1)
             FEDAVG_FEW(4, 9, 1)
-            FEDAVG_FEW(3, 10, 1)
-            FEDAVG_FEW(4, 10, 2)
+            FEDAVG_FEW2(2, 5, 1)
+            FEDAVG_FEW2(2, 2, 1)
         }
     } else if constexpr (KC == 3) {
         FEDAVG_FEW(4, 10, 1)
         if constexpr (kABFew) {
             FEDAVG_FEW(2, 10, 1)
             FEDAVG_FEW(3, 10, 1)
-            FEDAVG_FEW(2, 4, 1)
-            FEDAVG_FEW(2, 8, 1)
+            FEDAVG_FEW2(2, 5, 1)
+            FEDAVG_FEW2(1, 5, 1)
         }
     } else if constexpr (kABFew && KC == 4) {
         FEDAVG_FEW(2, 10, 1)
@@ -424,6 +434,7 @@ inline hipError_t launch_few(const TileLaunch& L, hipStream_t s, uint64_t* nl) {
         FEDAVG_FEW(2, 10, 2)
     }
 #undef FEDAVG_FEW
+#undef FEDAVG_FEW2
     return hipErrorInvalidValue;
 }
 // one launch per grid x (TPB + TPB_LDS) tiles (fedavg_tiles_burst_f32x4)
