@@ -213,11 +213,14 @@ struct FewForm {
 // against 76.3 % for the burst form with the count built in (78.9 / 78.2 with 3 / 2 register-held tiles, 73.9 at two
 // blocks per CU); 4 reads stay on the burst form (the few-client kernel 71.6-74.8 against 76.2 %, s6/few34_k4.jsonl).
 constexpr int kFewMaxReads = 3;
-constexpr FewForm kFewDefault[kFewMaxReads + 1] = {{0, 0, 0, 0}, {2, 8, 4, 2}, {1, 4, 10, 1}, {1, 4, 10, 1}};
+// 1 read since session 20 (profiles/r05/s20/f32_k1.jsonl, 3 interleaved rounds, outputs bit-equal): tile PAIRS, two
+// blocks per CU, 4 register- + 2 LDS-held units of 2 x 16 KiB, LDS units two at a time -- 76.8 % against 74.5 % for
+// (2, 8, 4, 2) on single tiles; pairs lost at 2 and 3 reads (76.6-77.2 against 80.0 %, 78.4-79.7 against 80.2 %).
+constexpr FewForm kFewDefault[kFewMaxReads + 1] = {{0, 0, 0, 0}, {2, 4, 2, 2, 2}, {1, 4, 10, 1}, {1, 4, 10, 1}};
 // A/B builds: launch variant bits 9-11 pick one of these per read count (1-6; 0 = the default)
 // (5-6: tile pairs, p = 2 -- 32 KiB per client per unit, session 18's 16-bit finding carried over)
 constexpr FewForm kFewAB[2][6] = {
-    {{2, 8, 4, 2}, {1, 12, 10, 2}, {1, 8, 10, 1}, {2, 10, 4, 2}, {2, 4, 2, 1, 2}, {2, 4, 2, 2, 2}},
+    {{2, 8, 4, 2}, {1, 12, 10, 2}, {1, 8, 10, 1}, {2, 10, 4, 2}, {2, 4, 2, 1, 2}, {2, 3, 2, 2, 2}},
     {{1, 4, 10, 1}, {1, 6, 10, 1}, {1, 5, 10, 1}, {1, 4, 9, 1}, {1, 2, 5, 1, 2}, {2, 2, 2, 1, 2}}};
 // A/B builds: the few-client kernel at 3-4 reads in other forms (variant bits 9-11 = 1-5; 6 and 7 select the burst
 // form's client loop for 3-6 clients instead, fedavg_tiles.h launch_burst)

@@ -292,8 +292,8 @@ fedavg_tiles_burst_f32x4(const RowTableF32 tab, const int K, const int64_t tstri
 //   4. every result stored: the LDS-held tiles', then the register-held tiles' -- the launch's write burst.
 // Per-element sequence as tile_sum_kc's (first4, then step4 for client 1), so the bits are the burst kernel's.
 // ---------------------------------------------------------------------------------------------
-// P = 2 (A/B forms): a unit is a pair of consecutive tiles, K x 32 KiB of contiguous slab; the pair's second tile past
-// the range's last tile re-reads that tile (never stored).
+// P = 2 (the 1-read default since session 20): a unit is a pair of consecutive tiles, K x 32 KiB of contiguous slab;
+// the pair's second tile past the range's last tile re-reads that tile (never stored).
 template <int OP, int FIN, int KC, int R, int L, int G, int P = 1>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, 2)))
 fedavg_tiles_few_f32x4(const RowTableF32 tab, const int64_t tstride4, f32x4* out, const int64_t b4, const int64_t e4,
@@ -400,13 +400,14 @@ inline hipError_t launch_few(const TileLaunch& L, hipStream_t s, uint64_t* nl) {
 #define FEDAVG_FEW2(R, LL, G)                                                      \
     if (f.r == R && f.l == LL && f.g == G && f.p == 2) return launch_few_form<OP, FIN, KC, R, LL, G, 2>(L, s, nl);
     if constexpr (KC == 1) {
-        FEDAVG_FEW(8, 4, 2)
+        FEDAVG_FEW2(4, 2, 2)
         if constexpr (kABFew) {
+            FEDAVG_FEW(8, 4, 2)
             FEDAVG_FEW(12, 10, 2)
             FEDAVG_FEW(8, 10, 1)
             FEDAVG_FEW(10, 4, 2)
             FEDAVG_FEW2(4, 2, 1)
-            FEDAVG_FEW2(4, 2, 2)
+            FEDAVG_FEW2(3, 2, 2)
         }
     } else if constexpr (KC == 2) {
         FEDAVG_FEW(4, 10, 1)
