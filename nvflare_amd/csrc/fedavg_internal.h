@@ -249,7 +249,7 @@ constexpr FewForm kNarrowFewDefault[kNarrowFewMaxReads + 1] = {
     {0, 0, 0, 0}, {2, 8, 4, 4, 2}, {2, 8, 8, 4}, {1, 4, 10, 2, 2}};
 // A/B builds (-DFEDAVG_AB_FEW): launch variant bits 9-11 = 1-4 pick one of these per read count
 constexpr FewForm kNarrowFewAB[3][4] = {
-    {{2, 8, 8, 4}, {2, 8, 4, 2, 2}, {2, 6, 4, 4, 2}, {2, 16, 8, 4}},
+    {{2, 8, 8, 4}, {2, 8, 4, 2, 2}, {2, 4, 2, 2, 4}, {2, 4, 2, 1, 4}},
     {{1, 4, 10, 1, 2}, {1, 4, 10, 2, 2}, {1, 8, 20, 2}, {1, 6, 20, 4}},
     {{1, 8, 20, 4}, {1, 4, 10, 1, 2}, {1, 8, 20, 2}, {1, 6, 20, 2}}};
 

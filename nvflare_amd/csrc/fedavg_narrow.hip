@@ -495,7 +495,7 @@ fedavg_tiles_narrow_few(const RowTableNarrow tab, const int64_t tstride8, u32x4*
                         const float fv, const int64_t t0, const int64_t t_end) {
     static_assert(KC >= 1 && KC <= 3, "one to three row reads");
     static_assert(L == 0 || L % G == 0, "whole LDS groups");
-    static_assert(P == 1 || P == 2, "single tiles or pairs");
+    static_assert(P == 1 || P == 2 || P == 4, "single tiles, pairs or quads");
     constexpr int CPL = kCpl16 * P;                      // u32x4 per lane per unit
     constexpr int64_t T8 = (int64_t)CPL * kBlock;        // u32x4 per unit
     const int64_t last_tile = (e8 - 1) / ((int64_t)kCpl16 * kBlock);
@@ -592,13 +592,16 @@ static hipError_t launch_narrow_few(const RowTableNarrow& tab, int64_t tstride8,
 #define FEDAVG_NFEW2(B, R, LL, G)                                     \
     if (f.bpc == B && f.r == R && f.l == LL && f.g == G && f.p == 2)  \
         return launch_narrow_few_form<FMT, OP, FIN, KC, R, LL, G, B, 2>(tab, tstride8, out, b8, e8, fv, grid, s, nl);
+#define FEDAVG_NFEW4(B, R, LL, G)                                     \
+    if (f.bpc == B && f.r == R && f.l == LL && f.g == G && f.p == 4)  \
+        return launch_narrow_few_form<FMT, OP, FIN, KC, R, LL, G, B, 4>(tab, tstride8, out, b8, e8, fv, grid, s, nl);
     if constexpr (KC == 1) {
         FEDAVG_NFEW2(2, 8, 4, 4)
         if constexpr (kABFew) {
             FEDAVG_NFEW(2, 8, 8, 4)
             FEDAVG_NFEW2(2, 8, 4, 2)
-            FEDAVG_NFEW2(2, 6, 4, 4)
-            FEDAVG_NFEW(2, 16, 8, 4)
+            FEDAVG_NFEW4(2, 4, 2, 2)
+            FEDAVG_NFEW4(2, 4, 2, 1)
         }
     } else if constexpr (KC == 2) {
         FEDAVG_NFEW(2, 8, 8, 4)
@@ -619,6 +622,7 @@ static hipError_t launch_narrow_few(const RowTableNarrow& tab, int64_t tstride8,
     }
 #undef FEDAVG_NFEW
 #undef FEDAVG_NFEW2
+#undef FEDAVG_NFEW4
     return hipErrorInvalidValue;
 }
 
