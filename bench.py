@@ -60,6 +60,7 @@ PRESET_NAMES = {
     4: "BASELINE config 4: 256 clients x 350M fp32 params, param buckets sharded across the GPUs",
     5: "BASELINE config 5: FedOpt server optimizer (Adam on aggregated deltas), 64 clients x 1B params",
 }
+SHARE_GPUS = 8  # config 4 on fewer GPUs than it fits: one GPU's share of this many (BASELINE: "across 8 MI355X")
 CLIENT_SHARDED = 40  # --also token "4x": config 4 through the client-sharded exchange (run_client_sharded)
 HOST_RESIDENT = 20  # --also token "2h": config 2 with host-resident updates and result (run_host_resident)
 HOST_SHARDED = 21  # --also token "2s": the same round in ONE process over all N GPUs' buckets (run_host_resident)
@@ -85,7 +86,8 @@ def parse(argv=None):
                          "(comma list of 4 / 5 / 4x = config 4 through the client-sharded RCCL exchange / "
                          "2h = config 2 from host-resident updates to a host result, PCIe included, every rank / "
                          "2s = the same round in one process over all N GPUs' parameter buckets; "
-                         "'auto' = 5,4,2h,2s,4x for the default config 3 run; 'none')")
+                         "2 = config 2 device-resident (weak); "
+                         "'auto' = 2,5,4,2h,2s,4x for the default config 3 run; 'none')")
     ap.add_argument("--client-sharded-params", type=float, default=None,
                     help="model size of the 4x entry (default: config 4's 350M; smaller for one-GPU rehearsals)")
     ap.add_argument("--host-resident-params", type=float, default=None,
@@ -103,6 +105,7 @@ def parse(argv=None):
     ap.add_argument("--epilogue", choices=["none", "add_base", "sgd", "adam", "adamax", "nadam", "radam"], default=None,
                     help="fused server update (config 5 = adam: FedOpt Adam on the aggregated deltas)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-baseline-s", type=float, default=8.0, help="seconds of CPU work the baseline times")
     ap.add_argument("--cpu-sample-params", type=int, default=16 * 1024 * 1024)
     ap.add_argument("--spot-check", type=int, default=4096, help="sampled outputs checked against the oracle")
     ap.add_argument("--traffic-bytes", type=float, default=None,
@@ -125,7 +128,7 @@ def parse(argv=None):
                    for f in ("--clients", "--params", "--global-params", "--scaling", "--epilogue"))
     args.preset_exact = not explicit
     if args.also == "auto":
-        args.also = "5,4,2h,2s,4x" if (args.config == 3 and not explicit) else "none"
+        args.also = "2,5,4,2h,2s,4x" if (args.config == 3 and not explicit) else "none"
     tokens = {"4x": CLIENT_SHARDED, "2h": HOST_RESIDENT, "2s": HOST_SHARDED}
     args.also = [] if args.also in ("", "none") else [tokens.get(x.strip()) or int(x) for x in args.also.split(",")]
     return args
@@ -405,7 +408,7 @@ def cpu_baseline(args, K, P, op):
 
     torch.set_num_threads(threads)
     try:
-        reps, t_tot = timed(8.0)
+        reps, t_tot = timed(getattr(args, "cpu_baseline_s", 8.0))
     finally:
         torch.set_num_threads(prev_threads)
     gibs = 4.0 * K * Ps * reps / t_tot / 2**30
@@ -546,10 +549,88 @@ def pmc_traffic(args, K, P, epilogue):
     return None, None
 
 
+def gpu_monitor(local):
+    """tools/gpu_state.GpuMonitor for this rank's GPU, or None when switched off
+    (NVFLARE_AMD_BENCH_GPU_STATE=0) or unavailable; never fails the run."""
+    if os.environ.get("NVFLARE_AMD_BENCH_GPU_STATE", "1") == "0":
+        return None
+    try:
+        sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+        from tools.gpu_state import GpuMonitor
+
+        return GpuMonitor(local)
+    except Exception:  # noqa: BLE001 -- measurement context only
+        return None
+
+
+def gpu_sampler(args):
+    """A context manager sampling this rank's GPU state over a timed region (``None`` inside when off)."""
+    import contextlib
+
+    mon = getattr(args, "gpu_monitor", None)
+    return mon.sample() if mon is not None else contextlib.nullcontext(None)
+
+
+def gpu_snapshot(args):
+    mon = getattr(args, "gpu_monitor", None)
+    return mon.snapshot() if mon is not None else None
+
+
+def handout_pull(args, ctx, world, param_buf, P, reps=3):
+    """The FedOpt hand-out pull timed: after the server step the new weights leave for the clients
+    as an independent host copy -- ShardedServerOptimizer.to_host -> _pull (nvflare_amd/app_opt/pt/sharded_fedopt.py),
+    one fedavg_d2h_multi per GPU of its parameter bucket into one page-locked host array, every GPU over its own PCIe
+    link at once (here: every rank its bucket, in parallel); at N = 1 DeviceServerOptimizer's single-device pull.  The
+    host array is page-locked once before the timed pulls (the pool reuses it across rounds).  Returns the max over
+    ranks of the median pull time."""
+    from nvflare_amd.device import HostArenaPool
+
+    pool = HostArenaPool(depth=1)
+    host = pool.take(P, pin=ctx)
+    pieces = [(0, 0, 4 * P)]
+    ctx.d2h_multi(host, param_buf.ptr, pieces)  # first touch of the pages outside the timing
+    times = []
+    for _ in range(reps):
+        barrier_sync(world, ctx)
+        t0 = time.perf_counter()
+        ctx.d2h_multi(host, param_buf.ptr, pieces)
+        times.append(time.perf_counter() - t0)
+    dist_barrier(world)
+    t = max_over_ranks(world, sorted(times)[len(times) // 2])
+    del host
+    return {"ms": round(t * 1e3, 3), "bytes_per_gpu_rank0": 4 * P, "GBps_per_gpu_rank0": round(4 * P / t / 1e9, 2),
+            "reps": reps, "what": "new parameters D2H into one page-locked host array, every GPU its bucket at once "
+                                  "(ShardedServerOptimizer._pull / to_host; fedavg_d2h_multi); max over ranks of the "
+                                  "median of the reps"}
+
+
+def wait_for_rank0(world, rank, key, timeout_s=1800.0):
+    """Ranks != 0 block (sleeping on the rendezvous store's socket, not spinning on a GPU collective that would take
+    host cores from rank 0's CPU baseline) until rank 0 has set ``key``."""
+    if world == 1:
+        return
+    import datetime
+
+    import torch.distributed as dist
+
+    try:
+        store = dist.distributed_c10d._get_default_store()
+    except Exception:  # noqa: BLE001 -- no store API: a plain barrier
+        dist.barrier()
+        return
+    if rank == 0:
+        store.set(key, "1")
+    else:
+        store.wait([key], datetime.timedelta(seconds=timeout_s))
+
+
 def kernel_name(K, epilogue, variant):
     # fewer client reads per launch than fedavg_capi.cpp's kBurstMinClients / kEpiBurstMinClients take the
     # per-tile-store kernels
     if epilogue != "none":
+        if variant & 12 == 0 and K <= 3 and epilogue in ("adam", "sgd", "add_base"):
+            return ("fedavg_tiles_epi_dma_f32x4 (1-3 client reads: inputs HBM -> LDS by LDS-DMA, results held on chip "
+                    "and stored as chip-wide bursts)")
         return "fedavg_tiles_epi_burst_f32x4" if variant & 12 == 0 and K >= 4 else "fedavg_tiles_epi_f32x4"
     if K <= 3 and not variant & (11 | 256):
         return ("fedavg_tiles_few_f32x4 (1-3 client reads: every register-held tile's loads issued before any "
@@ -633,12 +714,13 @@ def run_workload(args, ctx, world, rank, K, P_spec, scaling, epilogue, baseline,
             step()
         barrier_sync(world, ctx)
         n_launch0 = ctx.launch_count()
-        ctx.timing_begin()
-        t0 = time.perf_counter()
-        for _ in range(args.steps):
-            step()
-        barrier_sync(world, ctx)
-        t1 = time.perf_counter()
+        with gpu_sampler(args) as sampler:  # this rank's GPU clocks, power, temperatures over the timed steps
+            ctx.timing_begin()
+            t0 = time.perf_counter()
+            for _ in range(args.steps):
+                step()
+            barrier_sync(world, ctx)
+            t1 = time.perf_counter()
         ev_ms = ctx.timing_end()
         launches_per_step = (ctx.launch_count() - n_launch0) / args.steps
         wall = max_over_ranks(world, t1 - t0)
@@ -650,7 +732,10 @@ def run_workload(args, ctx, world, rank, K, P_spec, scaling, epilogue, baseline,
             sc.update(sampled=sampled, mismatches=mism, ranks=world)
         res = {"K": K, "P": P, "P_total": P_spec * world if scaling == "weak" else P_spec, "col0": col0,
                "wall": wall, "kernel_ms": kernel_ms, "kernel_ms_max": kernel_ms_max,
-               "launches_per_step": launches_per_step, "spot_check": sc, "op": op}
+               "launches_per_step": launches_per_step, "spot_check": sc, "op": op,
+               "gpu_state": sampler.summary() if sampler is not None else None}
+        if epi is not None and epilogue != "add_base":
+            res["handout_pull"] = handout_pull(args, ctx, world, state[0], P)
     finally:
         slab.close()
         for b in state:
@@ -658,6 +743,20 @@ def run_workload(args, ctx, world, rank, K, P_spec, scaling, epilogue, baseline,
     if baseline:
         res["cpu_baseline"] = cpu_baseline(args, K, P, op)
     return res
+
+
+def fits_one_share(ctx, world, p):
+    """Whether preset p under strong scaling fits every rank's device at this world size (agreed over ranks)."""
+    from nvflare_amd.device import TiledLayout
+    from nvflare_amd.sharding import bucket_ranges
+
+    lay = TiledLayout(4096, p["clients"])
+    lo, hi = bucket_ranges(p["params"], world)[0]
+    need = lay.slab_elems(hi - lo) * 4 + (hi - lo + 3) // 4 * 16
+    free, _ = ctx.mem_info()
+    if os.environ.get("NVFLARE_AMD_BENCH_SHARED_DEVICE") == "1":
+        free //= world
+    return not sum_over_ranks(world, [0 if need + HEADROOM <= free else 1])[0]
 
 
 def run_client_sharded(args, world, rank, local, K, P, seed):
@@ -1032,12 +1131,14 @@ def main(argv=None):
     ctx = DeviceContext.get(local)
     ctx.set_launch(args.blocks_per_cu, args.unroll)
     ctx.set_variant(args.variant)
+    args.gpu_monitor = gpu_monitor(local)
+    state_before = gpu_snapshot(args) if rank == 0 else None
     K = args.clients
     label = (PRESET_NAMES[args.config] if args.preset_exact
              else f"custom (preset {args.config} overridden: {K} clients x {args.params} params, {args.epilogue})")
     t_main = time.perf_counter()
-    main_res = run_workload(args, ctx, world, rank, K, args.params, args.scaling, args.epilogue,
-                            baseline=(world == 1 and rank == 0 and not args.no_cpu_baseline), seed=args.seed)
+    main_res = run_workload(args, ctx, world, rank, K, args.params, args.scaling, args.epilogue, baseline=False,
+                            seed=args.seed)
     main_s = time.perf_counter() - t_main
     if "skipped" in main_res:
         raise SystemExit(f"rank {rank}: workload {main_res['skipped']}")
@@ -1047,17 +1148,32 @@ def main(argv=None):
         if cfg in (CLIENT_SHARDED, HOST_RESIDENT, HOST_SHARDED):
             continue  # last, each under a watchdog (below)
         p = PRESETS[cfg]
+        P_run, name, share = p["params"], PRESET_NAMES[cfg], None
+        if cfg == 4 and world < SHARE_GPUS and not fits_one_share(ctx, world, p):
+            # config 4 does not fit this many GPUs (one GPU: 359.8 GB of slab): run ONE GPU's share of the 8-GPU split
+            # instead -- the largest bucket of sharding.bucket_ranges(350M, 8), all 256 clients -- labelled as the share
+            from nvflare_amd.sharding import bucket_ranges
+
+            lo, hi = max(bucket_ranges(p["params"], SHARE_GPUS), key=lambda b: b[1] - b[0])  # the slowest GPU's
+            P_run, share = hi - lo, {"of_params_total": p["params"], "gpus": SHARE_GPUS, "bucket": [lo, hi]}
+            name = (f"{PRESET_NAMES[cfg]} -- ONE GPU's share of the {SHARE_GPUS}-GPU split (the largest bucket of "
+                    f"sharding.bucket_ranges({p['params']}, {SHARE_GPUS}): {p['clients']} clients x {P_run} params)")
         t_entry = time.perf_counter()
-        r = run_workload(args, ctx, world, rank, p["clients"], p["params"], p["scaling"], p["epilogue"],
+        r = run_workload(args, ctx, world, rank, p["clients"], P_run, "weak" if share else p["scaling"], p["epilogue"],
                          baseline=False, seed=args.seed)
         failed = failed or bool((r.get("spot_check") or {}).get("mismatches"))
         if rank == 0:
             if "skipped" in r:
-                also.append({"baseline_config": PRESET_NAMES[cfg], "n_gpus": world, "skipped": r["skipped"]})
+                also.append({"baseline_config": name, "n_gpus": world, "skipped": r["skipped"]})
             else:
-                entry = summarize(args, world, r, p["clients"], p["scaling"], p["epilogue"], PRESET_NAMES[cfg])
+                entry = summarize(args, world, r, p["clients"], "weak" if share else p["scaling"], p["epilogue"], name)
                 entry["n_gpus"] = world
                 entry["spot_check"] = r["spot_check"]
+                if share:
+                    entry["config"]["share"] = share
+                if r.get("handout_pull"):
+                    entry["handout_pull"] = r["handout_pull"]
+                entry["gpu_state"] = r.get("gpu_state")
                 entry["elapsed_s"] = round(time.perf_counter() - t_entry, 2)  # fill, warmup, steps, spot check
                 also.append(entry)
     line = None
@@ -1079,9 +1195,12 @@ def main(argv=None):
             "config": s["config"],
             "pct_hbm_peak": s["pct_hbm_peak"],
             "roofline": s["roofline"],
-            "cpu_baseline": main_res.get("cpu_baseline"),
-            "elapsed_s": round(main_s, 2),  # the main entry's wall time: fill, warmup, steps, spot check, CPU baseline
+            "cpu_baseline": None,  # rank 0, after every GPU entry (below)
+            "elapsed_s": round(main_s, 2),  # the main entry's wall time: fill, warmup, steps, spot check
+            "gpu_state": {"before": state_before, "main_timed": main_res.get("gpu_state")},
         }
+        if main_res.get("handout_pull"):
+            line["handout_pull"] = main_res["handout_pull"]
         if main_res.get("spot_check") is not None:
             line["spot_check"] = main_res["spot_check"]
     state, dog = {}, None
@@ -1091,7 +1210,22 @@ def main(argv=None):
                 dog.cancel()
             e_failed, dog = guarded_entry(args, world, rank, local, line, also, state, token)
             failed = e_failed or failed
+    if dog is not None:
+        dog.cancel()
+        dog = None
+    # the CPU baseline on rank 0 at EVERY N, after all GPU entries so it perturbs none of them;
+    # the other ranks sleep on the rendezvous store meanwhile (wait_for_rank0), not in a spinning collective
+    if rank == 0 and not args.no_cpu_baseline:
+        t_cpu = time.perf_counter()
+        try:
+            line["cpu_baseline"] = cpu_baseline(args, K, min(args.params, main_res["P"]), main_res["op"])
+            line["cpu_baseline"]["elapsed_s"] = round(time.perf_counter() - t_cpu, 2)
+            line["cpu_baseline"]["n_gpus_in_run"] = world
+        except Exception as e:  # noqa: BLE001 -- recorded; the GPU measurements stand
+            line["cpu_baseline"] = {"error": f"{type(e).__name__}: {e}"}
+    wait_for_rank0(world, rank, "nvflare_amd_bench_cpu_baseline_done")
     if rank == 0:
+        line["gpu_state"]["after"] = gpu_snapshot(args)
         if also:
             line["also"] = also
         state["printed"] = True
@@ -1099,8 +1233,14 @@ def main(argv=None):
         if failed:
             print("SPOT CHECK FAILED", file=sys.stderr)
     if world > 1:
+        import threading
+
         import torch.distributed as dist
 
+        # the teardown under a watchdog as well: the line is out; a stuck barrier must not hold the run
+        dog = threading.Timer(args.watchdog_s, lambda: (sys.stdout.flush(), sys.stderr.flush(), os._exit(3 if failed else 0)))
+        dog.daemon = True
+        dog.start()
         dist.barrier()
         dist.destroy_process_group()
     if dog is not None:

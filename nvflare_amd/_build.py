@@ -60,22 +60,39 @@ def needs_build() -> bool:
     return any(os.path.getmtime(f) > t for f in _inputs())
 
 
-def compile_units(sources=SOURCES, ab=False):
+def _mentions(csrc: str, src: str, macro: str) -> bool:
+    try:
+        with open(os.path.join(csrc, src)) as f:
+            return macro in f.read()
+    except OSError:
+        return False
+
+
+def compile_units(sources=SOURCES, ab=False, csrc=None):
     """(source, object name, extra flags) of every translation unit: the fused kernels' source once per EPI_UNITS
     entry (EPI_UNITS_AB for an A/B build) in two halves by optimizer kind, the 16-bit source once per format, the others
-    once each."""
+    once each.  ``csrc``: the directory of sources from another revision (tools/build_rev_lib.py): a source that does
+    not know a split macro (FEDAVG_EPI_PART, FEDAVG_NARROW_PART -- round 5) is compiled as one unit, and the stand-alone
+    server-step unit (FEDAVG_EPI_STEP) is left out where the sources lack it, so no symbol is defined twice."""
+    split_epi = csrc is None or _mentions(csrc, EPI_SOURCE, "FEDAVG_EPI_PART")
+    split_narrow = csrc is None or _mentions(csrc, NARROW_SOURCE, "FEDAVG_NARROW_PART")
+    has_step = csrc is None or _mentions(csrc, EPI_SOURCE, "FEDAVG_EPI_STEP")
     units = []
     for src in sources:
         if src == EPI_SOURCE:  # each (mode, finalisation) pair in two halves (fedavg_epi_inst.hip FEDAVG_EPI_PART)
             for name, op, fin in (EPI_UNITS_AB if ab else EPI_UNITS):
                 if op is None:
-                    units.append((src, f"fedavg_epi_{name}.hip.o", ["-DFEDAVG_EPI_STEP"]))
+                    if has_step:
+                        units.append((src, f"fedavg_epi_{name}.hip.o", ["-DFEDAVG_EPI_STEP"]))
                     continue
                 defs = [f"-DFEDAVG_EPI_OP={op}", f"-DFEDAVG_EPI_FIN={fin}", f"-DFEDAVG_EPI_FN=launch_epi_{name}",
                         f"-DFEDAVG_EPI_FN2=launch_epi_{name}_part2"]
+                if not split_epi:
+                    units.append((src, f"fedavg_epi_{name}.hip.o", defs))
+                    continue
                 units += [(src, f"fedavg_epi_{name}.hip.o", defs + ["-DFEDAVG_EPI_PART=1"]),
                           (src, f"fedavg_epi_{name}_part2.hip.o", defs + ["-DFEDAVG_EPI_PART=2"])]
-        elif src == NARROW_SOURCE:  # once per 16-bit format (fedavg_narrow.hip FEDAVG_NARROW_PART)
+        elif src == NARROW_SOURCE and split_narrow:  # once per 16-bit format (fedavg_narrow.hip FEDAVG_NARROW_PART)
             units += [(src, "fedavg_narrow_bf16.hip.o", ["-DFEDAVG_NARROW_PART=1"]),
                       (src, "fedavg_narrow_f16.hip.o", ["-DFEDAVG_NARROW_PART=2"])]
         else:

@@ -1392,17 +1392,22 @@ int fedavg_accumulate_tiled_epi(fedavg_ctx* ctx, const void* const* bases, const
         // (product builds: the pipelined per-tile form at every read count under kEpiBurstMinClients -- at one read it
         // carries client 0, or nothing for the server step -- and for a chained sum; the unpipelined one is A/B only)
         const int reads = L.k + (cur_in ? 1 : 0);
-        // A/B builds with -DFEDAVG_AB_FEW: 2-3 client reads with launch variant bits 9-11 set take the register-held
-        // few-client fused form (one block per CU unless fedavg_set_launch says otherwise)
-        const bool few_ab = fedavg::kABFew && !cur_in && reads >= 2 && reads <= 3 &&
-                            ((ctx->variant >> fedavg::kVariantLoopShift) & 7) != 0;
-        if (few_ab) L.variant |= fedavg::kVariantEpiFew;
-        if (!few_ab && (reads < kEpiBurstMinClients || (!fedavg::kAB && cur_in)))
+        // (round 5's register-held few-client fused form, A/B only, ran 53 % and was removed in round 6; the A/B builds'
+        // variant bits 9-11 now pick the LDS-DMA form's geometry, fedavg_epi.h launch_epi_dma_form)
+        const fedavg::EpiParams E = make_epi(ctx, *epi);
+        // 1-3 client reads without a chained sum or a separate aggregate output: the LDS-DMA few-client form (round 6;
+        // fedavg_epi.h fedavg_tiles_epi_dma_f32x4), one block per CU, unless the public variant asks for the per-tile
+        // form (bit 2, kVariantEpiPrefetch) or tile stores (bit 3)
+        const bool dma = !cur_in && L.k >= 1 && L.k <= 3 && fedavg::epi_dma_nin(E) > 0 &&
+                         (!out || epi->kind == FEDAVG_EPI_ADD_BASE) &&
+                         !(ctx->variant & (fedavg::kVariantEpiPrefetch | fedavg::kVariantTileStores));
+        if (dma) L.variant |= fedavg::kVariantEpiDma;
+        if (!dma && (reads < kEpiBurstMinClients || (!fedavg::kAB && cur_in)))
             L.variant |= (reads >= 2 || !fedavg::kAB) && !(ctx->variant & fedavg::kVariantTileStores)
                              ? fedavg::kVariantEpiPrefetch
                              : fedavg::kVariantTileStores;
-        const bool burst = !few_ab && !(L.variant & (fedavg::kVariantEpiPrefetch | fedavg::kVariantTileStores));
-        const int bpc = few_ab ? ctx->bpc(1) : burst ? ctx->bpc(L.k >= fedavg::kEpiOneBlockMinK ? 1 : 2) : ctx->bpc();
+        const bool burst = !dma && !(L.variant & (fedavg::kVariantEpiPrefetch | fedavg::kVariantTileStores));
+        const int bpc = dma ? 1 : burst ? ctx->bpc(L.k >= fedavg::kEpiOneBlockMinK ? 1 : 2) : ctx->bpc();
         // one block per CU: the LDS-held tiles fill the CU (9 instead of 4), unless the public variant has bit 6
         if (burst && bpc == 1 && !(ctx->variant & (fedavg::kVariantWideLds | fedavg::kVariantRegisterTiles)))
             L.variant |= fedavg::kVariantWideLds;
@@ -1410,7 +1415,7 @@ int fedavg_accumulate_tiled_epi(fedavg_ctx* ctx, const void* const* bases, const
         L.fin_val = (float)fin_scalar(fin, count);
         L.acc_in = cur_in;
         L.out = static_cast<float*>(out);
-        const hipError_t rc = fedavg::launch_tiles_epi_f32x4(L, make_epi(ctx, *epi), s, &ctx->launches);
+        const hipError_t rc = fedavg::launch_tiles_epi_f32x4(L, E, s, &ctx->launches);
         if (scratch) HIP_CHECK(hipFreeAsync(scratch, s));
         HIP_CHECK(rc);
         ts.done();

@@ -2,6 +2,8 @@
 // rows a9 / a10) and its launch templates; included by fedavg_epi_{numpy,torch,unweighted}.hip.
 #pragma once
 
+#include <type_traits>
+
 #include "fedavg_arith.h"
 
 namespace fedavg {
@@ -655,75 +657,265 @@ __global__ void __launch_bounds__(kBlock) fedavg_tiles_epi_f32x4(const RowTableF
     }
 }
 
-// A/B ONLY (-DFEDAVG_AB_FEW): a register-held FEW-CLIENT fused form (round 5), 2-3 client reads.  The per-tile form above stores
-// each tile's new parameters and states as it finishes -- small writes scattered through the read stream, the shape
-// the HBM handles worst (profiles/r04/s2/epi_r2.jsonl: the library's per-tile form 70.6 % of 8 TB/s at 2 clients) --
-// while the epilogue-shaped burst probe that holds REG tiles' results on chip and stores them at the end of a short
-// launch measured 76.3 % (e_burst_r4: one block per CU, 4 register-held tiles).  This is that shape with the real
-// arithmetic: per tile its operands (p, m, v ...) and client rows are loaded, d = fin(sum) and the optimizer step
-// computed, the new values held in registers; after the block's REG tiles every result is stored.  K (2 or 3 here,
-// any count is correct) is a launch argument: groups of up to four clients' loads, then their arrival-ordered steps.
-template <int OP, int FIN, int EPI, int REG>
-__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, 2)))
-fedavg_tiles_epi_few_f32x4(const RowTableF32 tab, const int K, const int64_t tstride4, f32x4* out, const int64_t b4,
-                           const int64_t e4, const float fin_val, const EpiParams E, const int64_t t0, const int64_t t_end) {
-    constexpr int CPL = kDefaultTile / (4 * kBlock);
-    constexpr int64_t T4 = (int64_t)CPL * kBlock;
-    const FinConst fc = fin_const<FIN>(fin_val);
-    const EpiConsts C = epi_consts<EPI>(E);
-    if constexpr ((EPI & kEpiTorchSqrt) != 0) rsqrt14_stage();
-    if constexpr ((EPI & kEpiTorchSqrtAmd) != 0) rsqrtps_stage(E.rsqrtps);
-    EpiIn res[REG][CPL];
-#pragma unroll
-    for (int m = 0; m < REG; ++m) {
-        const int64_t t = t0 + blockIdx.x + (int64_t)m * gridDim.x;
-        if (t < t_end) {
-            EpiIn in[CPL];
-#pragma unroll
-            for (int c = 0; c < CPL; ++c) {
-                int64_t i = t * T4 + threadIdx.x + c * kBlock;
-                i = i < b4 ? b4 : (i >= e4 ? e4 - 1 : i);  // a partial edge tile: in-range operands, not stored
-                in[c] = epi_load<EPI>(E, i);
-            }
-            f32x4 acc[CPL];
-            const int64_t off = t * tstride4 + threadIdx.x;
-            tile_sum_rrem<OP, false, CPL>(acc, tab, K, off, t * T4 + threadIdx.x, nullptr, b4, e4);
-            f32x4 dv[CPL];
-            fin_tile_em<FIN, kEmBurst, CPL>(dv, acc, fc);
-#pragma unroll
-            for (int c = 0; c < CPL; ++c) {
-                const int64_t i = t * T4 + threadIdx.x + c * kBlock;
-                if (out != nullptr && (EPI & 0xFF) != FEDAVG_EPI_ADD_BASE && i >= b4 && i < e4)
-                    store4<true>(out + i, dv[c]);  // the aggregate itself, when asked for (not held: rare)
-                uint32_t slow = 0;
-                if constexpr ((EPI & 0xFF) == FEDAVG_EPI_ADAM) slow = C.bc2s.fast ? 0u : 1u;
-                if constexpr ((EPI & 0xFF) == FEDAVG_EPI_NADAM) slow = C.bc2.fast ? 0u : 1u;
-                if constexpr ((EPI & 0xFF) == FEDAVG_EPI_RADAM) slow = C.bc1.fast ? 0u : 1u;
-                if constexpr (epi_has_rare<EPI>()) {
-                    res[m][c] = epi_compute<EPI, kEmFast>(E, C, dv[c], in[c], slow);
-                    if (__builtin_expect(slow != 0u, 0)) {
-                        uint32_t unused = 0;
-                        res[m][c] = epi_compute<EPI, kEmElem>(E, C, dv[c], in[c], unused);
-                    }
-                } else {
-                    res[m][c] = epi_compute<EPI, kEmElem>(E, C, dv[c], in[c], slow);
-                }
-            }
-        }
-    }
-#pragma unroll
-    for (int m = 0; m < REG; ++m) {
-        const int64_t t = t0 + blockIdx.x + (int64_t)m * gridDim.x;
-        if (t < t_end) {
-#pragma unroll
-            for (int c = 0; c < CPL; ++c) {
-                const int64_t i = t * T4 + threadIdx.x + c * kBlock;
-                if (i >= b4 && i < e4) epi_store<EPI>(E, i, res[m][c], out);
-            }
-        }
+// ---------------------------------------------------------------------------------------------
+// FEW-CLIENT fused form on LDS-DMA (round 6): 1-3 client reads, no chained sum.  The per-tile
+// form above (the route through round 5) stores each tile's new parameters and states as it finishes -- small writes
+// scattered through the read stream, a pattern that ran 67.9 % of 8 TB/s in the epilogue-shaped probe (e_tile2,
+// profiles/r04/s2/epi_r2.jsonl) against 76.3 % when a launch's results are held on chip and stored as one chip-wide
+// burst (e_burst_r4).  Holding the new p, m, v in registers with the loads in VGPRs ran 53 % (fedavg_tiles_epi_few_f32x4,
+// A/B only): at one wave per SIMD a tile's ~50 VALU per element of optimizer arithmetic ran with nothing in flight.
+// Here every input goes HBM -> LDS by LDS-DMA (global_load_lds_dwordx4: no VGPRs while in flight), so a wave keeps S
+// units' loads in flight while it computes:
+//   * a UNIT is one wave's 1 KiB piece of every input stream of a tile column (64 lanes x float4): the KC client segments
+//     and the NIN operand streams (p, exp_avg, exp_avg_sq ... by optimizer kind) -- G = KC + NIN DMAs, landing at
+//     ring[wave][slot][stream][lane], the lane's own element group, so a wave only ever reads what it loaded itself and
+//     its own counted `s_waitcnt vmcnt` orders the read (no barriers; MI355X_MICROARCH.md item 7);
+//   * a wave runs N units per launch (N / 4 tiles per block, the tiles dealt round-robin as in the burst kernels): units
+//     0 .. S-1 are issued at once; unit u is computed from its slot as soon as it lands (d = fin(sum) and the optimizer
+//     step, epi_compute), its results kept in VGPRs and the slot refilled with unit u + S; the last S units' results
+//     are written back into their slots;
+//   * then every result is stored -- the launch's write burst.
+// Only the LDS-DMA instructions touch global memory before the burst (the wait counts are exact: vmcnt counts them in
+// issue order, G per unit); inputs past the range are read at clamped in-range addresses and never stored.
+// Per-element sequence as the per-tile form's (first4 / step4, fin_tile, epi_compute): the bits are the same.
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t lds_byte_addr(const void* p) {
+    return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
+}
+
+// one LDS-DMA of 16 bytes per lane (the wave's 1 KiB lands at lds_dst + lane x 16); nontemporal like every client load.
+// M0 carries the LDS base and is written and restored inside the statement (cdna_hip_programming.md, inline asm).
+__device__ __forceinline__ void glds16(const void* gsrc, const uint32_t lds_dst) {
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(gsrc), "s"(lds_dst)
+                 : "memory");
+}
+
+// the wave's LDS reads done before an LDS-DMA into the same bytes is issued: hipcc issues a slot's ds_reads, then the
+// refill's DMAs, and waits for the reads only where it uses their values (the compute may be scheduled after the
+// DMAs); a DMA that hits in L2 -- a clamped tile re-read -- can then land before a queued read (round 6, session 2:
+// one wave-unit of 256 elements wrong in the last, partial launch)
+__device__ __forceinline__ void wait_lgkmcnt0() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+    static_assert(N >= 0 && N <= 63, "vmcnt is six bits on gfx950");
+    asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory");
+}
+
+template <int I, int END, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+    if constexpr (I < END) {
+        f(std::integral_constant<int, I>{});
+        static_for<I + 1, END>(f);
     }
 }
 
+// result streams an optimizer kind writes (the EpiIn fields .a .. .d it fills)
+template <int EPI>
+constexpr int epi_nout() {
+    constexpr int KIND = EPI & 0xFF;
+    if constexpr (KIND == FEDAVG_EPI_ADD_BASE) return 1;
+    if constexpr (KIND == FEDAVG_EPI_SGD || KIND == FEDAVG_EPI_ADAGRAD || KIND == FEDAVG_EPI_ASGD) return 2;
+    if constexpr (KIND == FEDAVG_EPI_RMSPROP) return 4;
+    return 3;  // ADAM (no amsgrad on this form), ADAMAX, NADAM, RADAM, RPROP
+}
+
+// LDS per block left for the ring beside the epilogue's sqrt table (16 KiB RSQRTPS table, or the AVX-512 path's 512 B)
+template <int EPI>
+constexpr int epi_dma_ring_bytes() {
+    return kLdsBytesPerCu - ((EPI & kEpiTorchSqrtAmd) ? 16 * 1024 : (EPI & kEpiTorchSqrt) ? 1024 : 0);
+}
+constexpr int kEpiDmaUnits = 16;  // units per wave per launch: 4 tiles per block (the probe's e_burst_r4 launch size)
+// ring slots per wave: as many as the LDS holds, with every in-flight DMA countable by vmcnt (<= 63), at most N
+template <int EPI, int G, int N = kEpiDmaUnits>
+constexpr int epi_dma_slots() {
+    const int by_lds = epi_dma_ring_bytes<EPI>() / (4 * G * 1024);
+    const int by_cnt = 63 / G + 1;
+    const int s = by_lds < by_cnt ? by_lds : by_cnt;
+    return s < N ? s : N;
+}
+
+// TDMA: the AMD hosts' 16 KiB RSQRTPS table staged by LDS-DMA too, each wave a quarter, issued before the units' DMAs
+// (so unit 0's wait covers it) and published by one barrier -- instead of rsqrtps_stage's loads, wait and barrier
+// ahead of every launch's first DMA.  EM: the epilogue arithmetic's form (kEmFast with one fallback per unit, or kEmElem)
+template <int OP, int FIN, int EPI, int KC, int NIN, int S, int N, bool TDMA = false, int EM = kEmFast>
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, 1)))
+fedavg_tiles_epi_dma_f32x4(const RowTableF32 tab, const int64_t tstride4, f32x4* out, const int64_t b4,
+                           const int64_t e4, const float fin_val, const EpiParams E_, const int64_t t0,
+                           const int64_t t_end) {
+    constexpr int G = KC + NIN;
+    constexpr int CPT = 4;  // float4 columns per lane per tile
+    constexpr int64_t T4 = (int64_t)CPT * kBlock;
+    constexpr int NOUT = epi_nout<EPI>();
+    static_assert(KC >= 1 && KC <= 3 && NIN >= 1 && NIN <= 3 && NOUT <= G, "few-client fused form");
+    static_assert(S >= 1 && S <= N && (S - 1) * G <= 63 && N % CPT == 0, "ring geometry");
+    static_assert((int64_t)4 * S * G * 1024 <= epi_dma_ring_bytes<EPI>(), "ring fits the CU's LDS");
+    __shared__ f32x4 ring[4][S][G][64];
+    EpiParams E = E_;
+    if constexpr ((EPI & 0xFF) == FEDAVG_EPI_ADAM) E.amsgrad = 0;  // amsgrad runs the per-tile form (4 operand streams)
+    const FinConst fc = fin_const<FIN>(fin_val);
+    const EpiConsts C = epi_consts<EPI>(E);
+    constexpr bool kTableDma = TDMA && (EPI & kEpiTorchSqrtAmd) != 0;
+    if constexpr ((EPI & kEpiTorchSqrt) != 0) rsqrt14_stage();
+    if constexpr ((EPI & kEpiTorchSqrtAmd) != 0 && !kTableDma) rsqrtps_stage(E.rsqrtps);
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if constexpr (kTableDma) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            glds16(reinterpret_cast<const uint4*>(E.rsqrtps) + (wave * 4 + j) * 64 + lane,
+                   lds_byte_addr(&g_rsqrtps_lds[(wave * 4 + j) * 256]));
+    }
+    // operand streams in EpiIn order (.a, .b, .c): the parameter (ADD_BASE: the base) and the optimizer states
+    const float* opnd[3] = {(EPI & 0xFF) == FEDAVG_EPI_ADD_BASE ? E.base : E.param, E.state1, E.state2};
+    const int64_t t_first = t0 + blockIdx.x;
+    auto tile_of = [&](const int u) __attribute__((always_inline)) {
+        const int64_t t = t_first + (int64_t)(u / CPT) * gridDim.x;
+        return t < t_end ? t : t_end - 1;
+    };
+    auto issue = [&](const int u, const int slot) __attribute__((always_inline)) {
+        const int64_t t = tile_of(u);
+        const int64_t col = (int64_t)(u % CPT) * kBlock + threadIdx.x;
+#pragma unroll
+        for (int k = 0; k < KC; ++k) glds16(tab.rows[k] + t * tstride4 + col, lds_byte_addr(&ring[wave][slot][k][0]));
+        int64_t i = t * T4 + col;
+        i = i < b4 ? b4 : (i >= e4 ? e4 - 1 : i);  // a partial edge tile: in-range operands, never stored
+#pragma unroll
+        for (int j = 0; j < NIN; ++j)
+            glds16(reinterpret_cast<const f32x4*>(opnd[j]) + i, lds_byte_addr(&ring[wave][slot][KC + j][0]));
+    };
+    static_for<0, S>([&](auto ic) {
+        constexpr int u = decltype(ic)::value;
+        issue(u, u);
+    });
+    EpiIn res[N > S ? N - S : 1];
+    static_for<0, N>([&](auto ic) {
+        constexpr int u = decltype(ic)::value;
+        constexpr int slot = u % S;
+        constexpr int issued = S + u < N ? S + u : N;  // units issued before unit u's wait
+        wait_vmcnt<(issued - u - 1) * G>();
+        if constexpr (kTableDma && u == 0) __builtin_amdgcn_s_barrier();  // every wave's quarter of the table landed
+        f32x4 acc = first4<OP>(ring[wave][slot][0][lane], tab.w[0]);
+#pragma unroll
+        for (int k = 1; k < KC; ++k) acc = step4<OP>(acc, ring[wave][slot][k][lane], tab.w[k]);
+        EpiIn in;
+        in.a = ring[wave][slot][KC][lane];
+        if constexpr (NIN > 1) in.b = ring[wave][slot][KC + 1][lane];
+        if constexpr (NIN > 2) in.c = ring[wave][slot][KC + 2][lane];
+        const f32x4 a1[1] = {acc};
+        f32x4 d1[1];
+        fin_tile<FIN, 1>(d1, a1, fc);
+        EpiIn o;
+        if constexpr (epi_has_rare<EPI>() && EM == kEmFast) {
+            uint32_t slow = 0;
+            if constexpr ((EPI & 0xFF) == FEDAVG_EPI_ADAM) slow = C.bc2s.fast ? 0u : 1u;
+            if constexpr ((EPI & 0xFF) == FEDAVG_EPI_NADAM) slow = C.bc2.fast ? 0u : 1u;
+            if constexpr ((EPI & 0xFF) == FEDAVG_EPI_RADAM) slow = C.bc1.fast ? 0u : 1u;
+            o = epi_compute<EPI, kEmFast>(E, C, d1[0], in, slow);
+            if (__builtin_expect(slow != 0u, 0)) {
+                uint32_t unused = 0;
+                o = epi_compute<EPI, kEmElem>(E, C, d1[0], in, unused);
+            }
+        } else {
+            uint32_t unused = 0;
+            o = epi_compute<EPI, EM == kEmFast ? kEmElem : EM>(E, C, d1[0], in, unused);
+        }
+        if constexpr (u < N - S) {
+            res[u] = o;
+            wait_lgkmcnt0();  // the slot's reads have landed in VGPRs before its refill is issued
+            issue(u + S, slot);
+        } else {  // held in its slot (its inputs are consumed): entries 0 .. NOUT-1 = .a .. .d
+            ring[wave][slot][0][lane] = o.a;
+            if constexpr (NOUT > 1) ring[wave][slot][1][lane] = o.b;
+            if constexpr (NOUT > 2) ring[wave][slot][2][lane] = o.c;
+            if constexpr (NOUT > 3) ring[wave][slot][3][lane] = o.d;
+        }
+    });
+    // the write burst
+    static_for<0, N>([&](auto ic) {
+        constexpr int u = decltype(ic)::value;
+        const int64_t t = t_first + (int64_t)(u / CPT) * gridDim.x;
+        const int64_t i = t * T4 + (int64_t)(u % CPT) * kBlock + threadIdx.x;
+        if (t < t_end && i >= b4 && i < e4) {
+            if constexpr (u < N - S) {
+                epi_store<EPI>(E, i, res[u], out);
+            } else {
+                constexpr int slot = u % S;
+                EpiIn o;
+                o.a = ring[wave][slot][0][lane];
+                if constexpr (NOUT > 1) o.b = ring[wave][slot][1][lane];
+                if constexpr (NOUT > 2) o.c = ring[wave][slot][2][lane];
+                if constexpr (NOUT > 3) o.d = ring[wave][slot][3][lane];
+                epi_store<EPI>(E, i, o, out);
+            }
+        }
+    });
+}
+
+// the LDS-DMA few-client form for this launch (1-3 client reads, no chained sum, no separate aggregate output):
+// NIN operand streams by optimizer kind and flags; false when the form does not carry this kind / flag set
+template <int OP, int FIN, int EPI, int KC, int NIN, int N = kEpiDmaUnits, bool TDMA = false, int EM = kEmFast>
+inline hipError_t launch_epi_dma_n(const TileLaunch& L, const EpiParams& E, hipStream_t s, uint64_t* nl) {
+    constexpr int S = epi_dma_slots<EPI, KC + NIN, N>();
+    f32x4* o = reinterpret_cast<f32x4*>(L.out);
+    return burst_launches(L.b4 / L.tile4, (L.e4 - 1) / L.tile4 + 1, L.grid, N / 4, nl, L.variant & kVariantAnyOrder,
+                          [&](int nb, int64_t t0, int64_t t_end, uint32_t flags) {
+                              hipExtLaunchKernelGGL((fedavg_tiles_epi_dma_f32x4<OP, FIN, EPI, KC, NIN, S, N, TDMA, EM>),
+                                                    dim3(nb), dim3(kBlock), 0, s, nullptr, nullptr, flags, L.tab,
+                                                    L.tstride4, o, L.b4, L.e4, L.fin_val, E, t0, t_end);
+                          });
+}
+
+// A/B builds with -DFEDAVG_AB_FEW (torch-mode FIN_DIV Adam with the AMD-host sqrt only): launch variant bits 9-11 = 1-7
+// pick units per wave per launch, the table's staging and the epilogue arithmetic's form
+template <int OP, int FIN, int EPI, int KC, int NIN>
+inline hipError_t launch_epi_dma_form(const TileLaunch& L, const EpiParams& E, hipStream_t s, uint64_t* nl) {
+    if constexpr (kABFew && OP == FEDAVG_OP_TORCH && FIN == FEDAVG_FIN_DIV && EPI == (FEDAVG_EPI_ADAM | kEpiTorchSqrtAmd)) {
+        switch ((L.variant >> kVariantLoopShift) & 7) {
+            case 1: return launch_epi_dma_n<OP, FIN, EPI, KC, NIN, 16, true>(L, E, s, nl);
+            case 2: return launch_epi_dma_n<OP, FIN, EPI, KC, NIN, 24, false>(L, E, s, nl);
+            case 3: return launch_epi_dma_n<OP, FIN, EPI, KC, NIN, 24, true>(L, E, s, nl);
+            case 4: return launch_epi_dma_n<OP, FIN, EPI, KC, NIN, 32, true>(L, E, s, nl);
+            case 5: return launch_epi_dma_n<OP, FIN, EPI, KC, NIN, 8, true>(L, E, s, nl);
+            case 6: return launch_epi_dma_n<OP, FIN, EPI, KC, NIN, 16, true, kEmElem>(L, E, s, nl);
+            case 7: return launch_epi_dma_n<OP, FIN, EPI, KC, NIN, 24, true, kEmElem>(L, E, s, nl);
+            default: break;
+        }
+    }
+    return launch_epi_dma_n<OP, FIN, EPI, KC, NIN>(L, E, s, nl);
+}
+
+template <int OP, int FIN, int EPI, int KC>
+inline hipError_t launch_epi_dma_k(const TileLaunch& L, const EpiParams& E, hipStream_t s, uint64_t* nl) {
+    constexpr int KIND = EPI & 0xFF;
+    const int nin = epi_dma_nin(E);
+    if constexpr (KIND == FEDAVG_EPI_ADD_BASE) {
+        if (nin == 1) return launch_epi_dma_form<OP, FIN, EPI, KC, 1>(L, E, s, nl);
+    } else if constexpr (KIND == FEDAVG_EPI_SGD) {
+        if (nin == 1) return launch_epi_dma_form<OP, FIN, EPI, KC, 1>(L, E, s, nl);
+        if (nin == 2) return launch_epi_dma_form<OP, FIN, EPI, KC, 2>(L, E, s, nl);
+    } else if constexpr (KIND == FEDAVG_EPI_ADAM) {
+        if (nin == 3) return launch_epi_dma_form<OP, FIN, EPI, KC, 3>(L, E, s, nl);
+    }
+    return hipErrorInvalidValue;
+}
+
+template <int OP, int FIN, int EPI>
+inline hipError_t launch_epi_dma(const TileLaunch& L, const EpiParams& E, hipStream_t s, uint64_t* nl) {
+    constexpr int KIND = EPI & 0xFF;
+    if constexpr (KIND == FEDAVG_EPI_ADD_BASE || KIND == FEDAVG_EPI_SGD || KIND == FEDAVG_EPI_ADAM) {
+        switch (L.k) {
+            case 1: return launch_epi_dma_k<OP, FIN, EPI, 1>(L, E, s, nl);
+            case 2: return launch_epi_dma_k<OP, FIN, EPI, 2>(L, E, s, nl);
+            case 3: return launch_epi_dma_k<OP, FIN, EPI, 3>(L, E, s, nl);
+            default: break;
+        }
+    }
+    return hipErrorInvalidValue;
+}
 
 // A/B of the burst kernel's client loop (launch variant bits 9-11 = LOOP 1-4), instantiated for one configuration only:
 // torch-mode FIN_DIV Adam with the AMD-host sqrt, no chained partial sum (bench.py --epilogue adam on the pool's boxes)
@@ -760,42 +952,12 @@ inline bool epi_loop_ab(const TileLaunch& L, const EpiParams& E, hipStream_t s, 
 // (fedavg_internal.h kAB): the burst form with 4 (two blocks per CU) or 9 (one block per CU) LDS-held tiles without a
 // chained sum, the pipelined per-tile form; A/B builds also the register-only burst form, the burst form over a
 // chained sum, the unpipelined per-tile form and the client-loop shapes.
-template <int OP, int FIN, int EPI, int REG>
-inline hipError_t launch_epi_few(const TileLaunch& L, const EpiParams& E, hipStream_t s, uint64_t* nl) {
-    f32x4* o = reinterpret_cast<f32x4*>(L.out);
-    return burst_launches(L.b4 / L.tile4, (L.e4 - 1) / L.tile4 + 1, L.grid, REG, nl, L.variant & kVariantAnyOrder,
-                          [&](int nb, int64_t t0, int64_t t_end, uint32_t flags) {
-                              hipExtLaunchKernelGGL((fedavg_tiles_epi_few_f32x4<OP, FIN, EPI, REG>), dim3(nb),
-                                                    dim3(kBlock), 0, s, nullptr, nullptr, flags, L.tab, L.k, L.tstride4,
-                                                    o, L.b4, L.e4, L.fin_val, E, t0, t_end);
-                          });
-}
-
-// the register-held few-client fused form (A/B builds with -DFEDAVG_AB_FEW, torch-mode FIN_DIV Adam with the AMD-host
-// sqrt, 2-3 client reads): launch variant bits 9-11 = 1-5 select 2, 3, 4, 5, 6 register-held tiles; measured at one
-// block per CU it ran 48-55 % of HBM peak against the per-tile form's 69 % (profiles/r05/s4/epifew_k*.jsonl): the
-// optimizer arithmetic is not overlapped with memory at one wave per SIMD.  fedavg_set_launch(2, 0) runs it at two.
-template <int OP, int FIN, int EPI>
-inline hipError_t launch_epi_few_any(const TileLaunch& L, const EpiParams& E, hipStream_t s, uint64_t* nl) {
-    if constexpr (kABFew && OP == FEDAVG_OP_TORCH && FIN == FEDAVG_FIN_DIV && EPI == (FEDAVG_EPI_ADAM | kEpiTorchSqrtAmd)) {
-        switch ((L.variant >> kVariantLoopShift) & 7) {
-            case 1: return launch_epi_few<OP, FIN, EPI, 2>(L, E, s, nl);
-            case 2: return launch_epi_few<OP, FIN, EPI, 3>(L, E, s, nl);
-            case 3: return launch_epi_few<OP, FIN, EPI, 4>(L, E, s, nl);
-            case 4: return launch_epi_few<OP, FIN, EPI, 5>(L, E, s, nl);
-            case 5: return launch_epi_few<OP, FIN, EPI, 6>(L, E, s, nl);
-            default: break;
-        }
-    }
-    return hipErrorInvalidValue;
-}
-
 template <int OP, int FIN, bool ACC_IN, int EPI>
 inline hipError_t launch_epi_k(const TileLaunch& L, const EpiParams& E, hipStream_t s, uint64_t* nl) {
     const f32x4* ai = reinterpret_cast<const f32x4*>(L.acc_in);
     f32x4* o = reinterpret_cast<f32x4*>(L.out);
-    if constexpr (kABFew && !ACC_IN) {
-        if (L.variant & kVariantEpiFew) return launch_epi_few_any<OP, FIN, EPI>(L, E, s, nl);
+    if constexpr (!ACC_IN) {
+        if (L.variant & kVariantEpiDma) return launch_epi_dma<OP, FIN, EPI>(L, E, s, nl);
     }
     if constexpr (kAB || !ACC_IN) {
         if (!(L.variant & (kVariantTileStores | kVariantEpiPrefetch))) {  // burst: one launch per grid x TPB tiles

@@ -56,8 +56,10 @@ constexpr int kVariantLoopShift = 9;       // bits 9-11: A/B shapes of the burst
                                            // (fedavg_epi.h launch_epi_loop_ab, fedavg_tiles.h launch_burst)
 constexpr int kVariantFew = 1 << 12;      // inside TileLaunch: the few-client burst kernel (fedavg_tiles.h
                                            // fedavg_tiles_few_f32x4), set by run_tiles for 1-2 reads, no chained sum
-constexpr int kVariantEpiFew = 1 << 13;   // inside TileLaunch, A/B builds (-DFEDAVG_AB_FEW): the register-held
-                                           // few-client fused form (fedavg_epi.h fedavg_tiles_epi_few_f32x4)
+constexpr int kVariantEpiDma = 1 << 14;   // inside TileLaunch: the LDS-DMA few-client fused form (fedavg_epi.h
+                                           // fedavg_tiles_epi_dma_f32x4), set by the C-ABI for 1-3 reads, no chained
+                                           // sum, kinds ADD_BASE / SGD / Adam without amsgrad; public bit 2 (the
+                                           // per-tile pipelined form) keeps the round-5 route for same-process A/Bs
 // public variant bits a product build accepts (fedavg_set_variant): the fused per-tile pipelined form (2), burst
 // launches without the barrier bit (16), the 4-LDS-tile form on one-block-per-CU grids (64) -- each a routed form
 constexpr int kVariantProductMask = kVariantEpiPrefetch | kVariantAnyOrder | kVariantWideLds;
@@ -130,6 +132,17 @@ struct EpiParams {
     int torch_sqrt;                               // FEDAVG_SQRT_*: torch CPU's sqrt (Intel / AMD host), or IEEE
     const uint32_t* rsqrtps;                      // FEDAVG_SQRT_TORCH_AMD: this host's RSQRTPS table (device, 16 KiB)
 };
+
+// operand streams the LDS-DMA few-client fused form (fedavg_epi.h fedavg_tiles_epi_dma_f32x4) reads for this kind and
+// step, or 0 when it does not take them (the C-ABI then routes the per-tile form)
+inline int epi_dma_nin(const EpiParams& E) {
+    switch (E.kind) {
+        case FEDAVG_EPI_ADD_BASE: return 1;
+        case FEDAVG_EPI_SGD: return (E.has_momentum && !E.first_step) ? 2 : 1;
+        case FEDAVG_EPI_ADAM: return E.amsgrad ? 0 : 3;
+        default: return 0;
+    }
+}
 
 struct DequantLaunch {
     int qtype;

@@ -20,7 +20,8 @@ from bench_fake_rank import small_presets  # noqa: E402
 
 WORLD = 8
 SMALL = small_presets(WORLD)
-ARGS = ["--gpus", str(WORLD), "--steps", "2", "--warmup", "1", "--host-resident-params", "10001", "--spot-check", "64"]
+ARGS = ["--gpus", str(WORLD), "--steps", "2", "--warmup", "1", "--host-resident-params", "10001", "--spot-check", "64",
+        "--cpu-baseline-s", "0.2", "--cpu-sample-params", "4096"]
 
 
 def _free_port():
@@ -60,8 +61,16 @@ def check_line(d, world=WORLD):
     def name(e):
         return e.get("baseline_config") or e["config"]["baseline_config"]
 
-    assert len(d["also"]) == 5, [name(e) for e in d["also"]]
+    assert len(d["also"]) == 6, [name(e) for e in d["also"]]
     assert not any("skipped" in e or "error" in e for e in d["also"]), d["also"]
+    # the CPU baseline on rank 0 at every N, after the GPU entries
+    cb = d["cpu_baseline"]
+    assert cb is not None and "error" not in cb, cb
+    assert cb["value"] > 0 and cb["cores"] >= 1 and cb["n_gpus_in_run"] == world and cb["kind"] == "port"
+    # config 2 device-resident (weak): every rank its own 8 x P bucket
+    c2 = next(e for e in d["also"] if e["config"].get("clients") == small[2]["clients"] and "roofline" in e)
+    assert c2["scaling"] == "weak" and c2["n_gpus"] == world and c2["config"]["params_total"] == small[2]["params"] * world
+    assert c2["spot_check"]["mismatches"] == 0 and c2["spot_check"]["ranks"] == world
     c5 = next(e for e in d["also"] if e["config"].get("epilogue") == "adam")
     c4 = next(e for e in d["also"] if e["config"].get("clients") == 256 and "client-sharded" not in name(e))
     for e, cfg in ((c5, small[5]), (c4, small[4])):  # strong: one model split into `world` buckets, counted once
@@ -70,6 +79,9 @@ def check_line(d, world=WORLD):
         assert e["spot_check"]["mismatches"] == 0 and e["spot_check"]["ranks"] == world
         assert e["value"] == pytest.approx(4.0 * cfg["clients"] * cfg["params"] / (e["ms_per_step"] / 1e3) / 2**30,
                                            rel=2e-3, abs=0.006)
+    # the FedOpt hand-out pull (ShardedServerOptimizer._pull's device work) timed in the config-5 entry
+    hp = c5["handout_pull"]
+    assert hp["ms"] > 0 and hp["bytes_per_gpu_rank0"] == 4 * c5["config"]["params_per_gpu"]
     h2 = [e for e in d["also"] if "host-resident updates" in name(e)]
     s2 = [e for e in d["also"] if "ONE server process" in name(e)]
     x4 = [e for e in d["also"] if "client-sharded" in name(e)]

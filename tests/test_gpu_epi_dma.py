@@ -1,0 +1,221 @@
+"""GPU parity of the LDS-DMA few-client fused form (round 6, fedavg_epi.h fedavg_tiles_epi_dma_f32x4): 1-3 client reads
+with a server-optimizer epilogue -- WEIGHT_DIFF apply (ADD_BASE), SGD (momentum buffer read or not) and Adam (every sqrt
+the epilogue knows) -- bit for bit against the oracle AND against the round-5 per-tile form (public variant bit 2, same
+process), over the shapes the kernel's indexing has to get right: less than one tile, a range that starts and ends
+inside a tile, operand buffers that exist only on [begin, end), more tiles than one launch, ragged last launches.
+Reference arithmetic: weighted_aggregation_helper.py:181-236 then app_opt/pt/fedopt.py:157-182 (torch's single-tensor
+SGD / Adam), restated by oracle/fedavg_oracle.c."""
+
+import numpy as np
+import pytest
+
+from golden_util import same_bits
+
+pytestmark = pytest.mark.gpu
+
+TILE = 4096
+ADAM = dict(lr=1e-3, beta1=0.9, beta2=0.999, eps=1e-8)
+ADAM_WD = dict(lr=1e-3, beta1=0.8, beta2=0.99, eps=1e-8, weight_decay=1e-2, decoupled_weight_decay=1)
+SGD = dict(lr=0.5, momentum=0.9, nesterov=1, weight_decay=1e-3, dampening=0.1)
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    from nvflare_amd.device import DeviceContext
+
+    c = DeviceContext.get(0)
+    c.set_variant(0)
+    return c
+
+
+def _sum(ws):
+    c = None
+    for w in ws:
+        c = w if c is None else c + w
+    return c
+
+
+def _epi(kind, **kw):
+    from nvflare_amd import _native as N
+
+    e = N.Epilogue()
+    e.kind = kind
+    for k, v in kw.items():
+        setattr(e, k, v)
+    return e
+
+
+class _Case:
+    """K client rows over global elements [begin, end) in a tiled slab; operand buffers allocated for exactly [begin, end)
+    (the C-ABI indexes them by global element, so the device pointer passed is the buffer minus begin)."""
+
+    def __init__(self, ctx, K, begin, end, seed):
+        from nvflare_amd.device import TiledLayout
+
+        self.ctx, self.K, self.begin, self.end = ctx, K, begin, end
+        self.n = end - begin
+        rng = np.random.default_rng(seed)
+        self.rng = rng
+        self.lay = TiledLayout(TILE, K)
+        self.slab = ctx.alloc(self.lay.slab_elems(end) * 4)
+        self.bases = [self.slab.ptr + self.lay.slot_offset_elems(k) * 4 for k in range(K)]
+        self.rows = [(rng.standard_normal(end) * 0.05).astype(np.float32) for _ in range(K)]
+        for b, r in zip(self.bases, self.rows):
+            ctx.h2d_tiled(b, TILE * 4, self.lay.tile_stride * 4, 0, r.ctypes.data, r.nbytes)
+        self.ws = [float(1 + (37 * k) % 100) for k in range(K)]
+        self.bufs = {}
+
+    def buf(self, name, host):
+        """A device buffer holding host (n elements) for [begin, end); returns the global-element-indexed pointer."""
+        b = self.bufs.get(name)
+        if b is None:
+            b = self.bufs[name] = self.ctx.alloc(self.n * 4)
+        self.ctx.h2d_ptr(b.ptr, host.ctypes.data, host.nbytes)
+        return b.ptr - 4 * self.begin
+
+    def get(self, name):
+        out = np.empty(self.n, np.float32)
+        self.ctx.d2h(out, self.bufs[name].ptr)
+        return out
+
+    def d(self, oracle, op):
+        rows = [r[self.begin:self.end] for r in self.rows]
+        mode = oracle.MODE_TORCH if op == 1 else oracle.MODE_NUMPY
+        return oracle.fedavg_c(rows, self.ws, mode, nthreads=8)
+
+    def close(self):
+        self.slab.close()
+        for b in self.bufs.values():
+            b.close()
+
+
+def _launches(ctx, begin, end):
+    t_first, t_stop = begin // TILE, (end - 1) // TILE + 1
+    per = min(ctx.num_cus, t_stop - t_first) * 4  # one block per CU, 4 tiles per block
+    return -(-(t_stop - t_first) // per)
+
+
+def _run(ctx, c, e, op, fin, out_ptr=None, variant=0):
+    ctx.set_variant(variant)
+    try:
+        n0 = ctx.launch_count()
+        ctx.accumulate_tiled_epi(c.bases, c.ws, TILE, c.lay.tile_stride, c.begin, c.end, out_ptr, op, fin,
+                                 _sum(c.ws), e)
+        ctx.sync()
+        return ctx.launch_count() - n0
+    finally:
+        ctx.set_variant(0)
+
+
+def _ranges(ctx):
+    big = ctx.num_cus * 4 * TILE  # one launch's tiles
+    return [
+        (0, 8),  # two float4 columns of one tile
+        (0, TILE),
+        (3 * TILE + 100, 3 * TILE + 100 + 2 * TILE + 36),  # starts and ends inside tiles
+        (TILE - 4, TILE + 4),  # straddles one tile boundary by a column each side
+        (0, 2 * big + 5 * TILE + 44),  # three launches, the last one ragged
+        (7 * TILE + 1024, 7 * TILE + 1024 + big + 12),
+    ]
+
+
+@pytest.mark.parametrize("K", [1, 2, 3])
+@pytest.mark.parametrize("rng_ix", range(6))
+@pytest.mark.parametrize("sqrt", ["ieee", "torch_cpu_amd", "torch_cpu"])
+def test_dma_adam_matches_oracle_and_per_tile(ctx, oracle, K, rng_ix, sqrt):
+    from nvflare_amd import _native as N
+
+    if sqrt != "torch_cpu_amd" and rng_ix not in (2, 4):
+        pytest.skip("the other sqrt paths on two of the ranges")
+    begin, end = _ranges(ctx)[rng_ix]
+    c = _Case(ctx, K, begin, end, seed=1000 + 10 * rng_ix + K)
+    try:
+        n = c.n
+        p = c.rng.standard_normal(n).astype(np.float32)
+        m = (c.rng.standard_normal(n) * 0.01).astype(np.float32)
+        v = (c.rng.random(n) * 1e-4 + 1e-6).astype(np.float32)
+        flag = {"ieee": N.FEDAVG_SQRT_IEEE, "torch_cpu": N.FEDAVG_SQRT_TORCH_AVX512,
+                "torch_cpu_amd": N.FEDAVG_SQRT_TORCH_AMD}[sqrt]
+        if sqrt == "torch_cpu_amd":
+            ctx.load_rsqrtps(oracle.rsqrtps_table())
+        got = {}
+        for variant in (0, 4):  # the LDS-DMA form, then the per-tile form on the same inputs
+            hp = ADAM if rng_ix % 2 == 0 else ADAM_WD
+            e = _epi(3, param=c.buf("p", p), state1=c.buf("m", m), state2=c.buf("v", v), step=3.0, torch_sqrt=flag, **hp)
+            nl = _run(ctx, c, e, N.FEDAVG_OP_TORCH, N.FEDAVG_FIN_DIV, variant=variant)
+            if variant == 0:
+                assert nl == _launches(ctx, begin, end)
+            got[variant] = [c.get(x) for x in ("p", "m", "v")]
+        pw, mw, vw = p.copy(), m.copy(), v.copy()
+        oracle.epilogue_apply(c.d(oracle, 1), oracle.EPI_ADAM, p=pw, m=mw, v=vw, step=3.0, torch_cpu_sqrt=sqrt,
+                              **(ADAM if rng_ix % 2 == 0 else ADAM_WD))
+        for a, b, w in zip(got[0], got[4], (pw, mw, vw)):
+            assert same_bits(a, w) and same_bits(b, w)
+    finally:
+        c.close()
+
+
+@pytest.mark.parametrize("K", [1, 2, 3])
+@pytest.mark.parametrize("rng_ix", [0, 2, 4, 5])
+@pytest.mark.parametrize("momentum", [0.0, 0.9])
+def test_dma_sgd_two_steps(ctx, oracle, K, rng_ix, momentum):
+    """SGD as the FedOpt generator's default (momentum 0.6-0.9): step 1 reads only p (the momentum buffer starts as g),
+    step 2 reads p and the buffer -- both operand counts of the form; without momentum only p."""
+    from nvflare_amd import _native as N
+
+    begin, end = _ranges(ctx)[rng_ix]
+    c = _Case(ctx, K, begin, end, seed=2000 + 10 * rng_ix + K)
+    hp = dict(SGD, momentum=momentum)
+    try:
+        p = c.rng.standard_normal(c.n).astype(np.float32)
+        buf = np.zeros(c.n, np.float32)
+        pp, pb = c.buf("p", p), c.buf("m", buf)
+        for step in (1, 2):
+            e = _epi(2, param=pp, state1=pb, first_step=int(step == 1), **hp)
+            nl = _run(ctx, c, e, N.FEDAVG_OP_TORCH, N.FEDAVG_FIN_DIV)
+            assert nl == _launches(ctx, begin, end)
+            oracle.epilogue_apply(c.d(oracle, 1), oracle.EPI_SGD, p=p, m=buf, first_step=int(step == 1), **hp)
+            assert same_bits(c.get("p"), p), step
+            if momentum:
+                assert same_bits(c.get("m"), buf), step
+    finally:
+        c.close()
+
+
+@pytest.mark.parametrize("K", [1, 2, 3])
+@pytest.mark.parametrize("rng_ix", [1, 2, 3, 4])
+@pytest.mark.parametrize("op,fin", [(1, 2), (0, 1)])
+def test_dma_add_base(ctx, oracle, K, rng_ix, op, fin):
+    """WEIGHT_DIFF apply (full_model_shareable_generator.py:58-67): w = base + d into out, numpy and torch modes."""
+    begin, end = _ranges(ctx)[rng_ix]
+    c = _Case(ctx, K, begin, end, seed=3000 + 10 * rng_ix + K)
+    try:
+        base = c.rng.standard_normal(c.n).astype(np.float32)
+        e = _epi(1, base=c.buf("base", base))
+        outp = c.buf("out", np.zeros(c.n, np.float32))
+        nl = _run(ctx, c, e, op, fin, out_ptr=outp)
+        assert nl == _launches(ctx, begin, end)
+        want = oracle.epilogue_apply(c.d(oracle, op), oracle.EPI_ADD_BASE, base=base)
+        assert same_bits(c.get("out"), want)
+        assert same_bits(c.get("base"), base)  # the base is an input only
+    finally:
+        c.close()
+
+
+def test_dma_route_leaves_others_on_the_per_tile_form(ctx, oracle):
+    """amsgrad (a fourth operand stream), a requested aggregate output and 4+ reads keep their round-5 routes: one
+    persistent per-tile launch, or the burst form."""
+    from nvflare_amd import _native as N
+
+    c = _Case(ctx, 2, 0, 3 * TILE + 8, seed=7)
+    try:
+        z = np.zeros(c.n, np.float32)
+        e = _epi(3, param=c.buf("p", z + 1), state1=c.buf("m", z), state2=c.buf("v", z), state3=c.buf("x", z),
+                 amsgrad=1, step=1.0, **ADAM)
+        assert _run(ctx, c, e, N.FEDAVG_OP_TORCH, N.FEDAVG_FIN_DIV) == 1
+        e = _epi(3, param=c.buf("p", z + 1), state1=c.buf("m", z), state2=c.buf("v", z), step=1.0, **ADAM)
+        assert _run(ctx, c, e, N.FEDAVG_OP_TORCH, N.FEDAVG_FIN_DIV, out_ptr=c.buf("d", z)) == 1
+        want = c.d(oracle, 1)
+        assert same_bits(c.get("d"), want)
+    finally:
+        c.close()

@@ -539,8 +539,8 @@ FEW_CASES = [  # (kind, hp, state names): every optimizer kind through the few-c
 @pytest.mark.parametrize("K", [2, 3])
 @pytest.mark.parametrize("case", range(len(FEW_CASES)))
 def test_few_client_fused_every_kind(ctx, oracle, K, case):
-    """2-3 client reads through the fused per-tile form (pipelined across tiles; the form most FedOpt jobs run) for
-    every optimizer kind and the Adam family's restated AMD-host sqrt: more tiles than blocks, a ragged end, states
+    """2-3 client reads through the fused few-client forms (the LDS-DMA form for ADD_BASE / SGD / Adam without amsgrad or
+    an aggregate output, the per-tile form pipelined across tiles for the rest) for every optimizer kind and the Adam family's restated AMD-host sqrt: more tiles than blocks, a ragged end, states
     from a non-zero start, two steps; every output and state bit for bit against the oracle.  ADD_BASE writes out;
     one Adam case also asks for d in out.  (Round 5 also ran these against a register-held burst form of the fused
     kernel, fedavg_tiles_epi_few_f32x4 -- bit-exact, but 53 % of HBM peak against the per-tile form's 69 %, so it
@@ -591,7 +591,11 @@ def test_few_client_fused_every_kind(ctx, oracle, K, case):
             ctx.accumulate_tiled_epi(dev.bases, ws, TILE, dev.lay.tile_stride, 0, dev.n4, out, N_.FEDAVG_OP_TORCH,
                                      N_.FEDAVG_FIN_DIV, _sum(ws), e)
             ctx.sync()
-            assert ctx.launch_count() - n_launch == 1  # the per-tile form: one persistent launch
+            # ADD_BASE and SGD take the LDS-DMA few-client form (round 6): one launch per num_cus x 4 tiles; the other
+            # kinds, amsgrad and a requested aggregate output the per-tile form: one persistent launch
+            tiles = (dev.n4 - 1) // TILE + 1
+            dma = kind in (1, 2)
+            assert ctx.launch_count() - n_launch == (-(-tiles // (min(ctx.num_cus, tiles) * 4)) if dma else 1)
             d = oracle.fedavg_c(rows, ws, oracle.MODE_TORCH, nthreads=8)
             if kind == 1:
                 assert same_bits(dev.get("out"), oracle.epilogue_apply(d, oracle.EPI_ADD_BASE, base=base)), step

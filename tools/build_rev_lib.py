@@ -61,7 +61,10 @@ def main():
         csrc = os.path.join(tmp, "nvflare_amd", "csrc")
         inc = [f"-I{os.path.join(tmp, 'include')}", f"-I{csrc}"]
         # an A/B library: every kernel form the sources know (-DFEDAVG_AB; ignored by revisions before round 5)
-        units = B.compile_units([s for s in B.SOURCES if os.path.exists(os.path.join(csrc, s))], ab=not args.product)
+        # the unit list the revision's sources support (round-4 sources define every fused / 16-bit entry
+        # once per source, so they must not be split into PART=1 / PART=2 objects)
+        units = B.compile_units([s for s in B.SOURCES if os.path.exists(os.path.join(csrc, s))], ab=not args.product,
+                                csrc=csrc)
         only = [x for x in args.only.split(",") if x]
         if only and args.rev != "WORKTREE":
             raise SystemExit("--only needs --rev WORKTREE (the reused objects are the working tree's)")
