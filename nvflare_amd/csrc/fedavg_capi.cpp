@@ -1348,8 +1348,17 @@ int fedavg_accumulate_tiled_epi(fedavg_ctx* ctx, const void* const* bases, const
             // more than 128 clients, a finalisation with no clients, numpy mode with FIN_DIV, FIN_NONE with clients):
             // the plain kernels finalise d = fin(acc) into a scratch, then the server step reads it as its chained sum
             // (no clients, FIN_NONE).  The per-element sequence is the fused one, so the bits are the same.
-            HIP_CHECK(hipMallocAsync(&scratch, (end - begin) * sizeof(float), s));
-            float* d = static_cast<float*>(scratch) - begin;  // indexed by global element, touched on [begin, end)
+            // the intermediate is `out` itself when it aliases no epilogue operand (the server step then reads d there and
+            // writes its result over it element by element, each thread reading before writing); else a scratch
+            // (no 4-byte-per-parameter scratch where the caller's output can hold d)
+            const void* operands[] = {epi->base, epi->param, epi->state1, epi->state2, epi->state3};
+            bool alias = !out;
+            for (const void* q : operands) alias = alias || (q && q == out);
+            float* d = static_cast<float*>(out);
+            if (alias) {
+                HIP_CHECK(hipMallocAsync(&scratch, (end - begin) * sizeof(float), s));
+                d = static_cast<float*>(scratch) - begin;  // indexed by global element, touched on [begin, end)
+            }
             run_tiles(ctx, bases, weights, k_rows, (int64_t)tile_elems, (int64_t)tile_stride, (int64_t)begin,
                       (int64_t)end, cur_in, d, op, fin, count, s);
             cur_in = d;

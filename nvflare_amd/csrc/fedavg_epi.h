@@ -730,9 +730,9 @@ constexpr int epi_dma_ring_bytes() {
 }
 constexpr int kEpiDmaUnits = 16;  // units per wave per launch: 4 tiles per block (the probe's e_burst_r4 launch size)
 // ring slots per wave: as many as the LDS holds, with every in-flight DMA countable by vmcnt (<= 63), at most N
-template <int EPI, int G, int N = kEpiDmaUnits>
+template <int EPI, int G, int N = kEpiDmaUnits, int W = 4>
 constexpr int epi_dma_slots() {
-    const int by_lds = epi_dma_ring_bytes<EPI>() / (4 * G * 1024);
+    const int by_lds = epi_dma_ring_bytes<EPI>() / (W * G * 1024);
     const int by_cnt = 63 / G + 1;
     const int s = by_lds < by_cnt ? by_lds : by_cnt;
     return s < N ? s : N;
@@ -741,19 +741,23 @@ constexpr int epi_dma_slots() {
 // TDMA: the AMD hosts' 16 KiB RSQRTPS table staged by LDS-DMA too, each wave a quarter, issued before the units' DMAs
 // (so unit 0's wait covers it) and published by one barrier -- instead of rsqrtps_stage's loads, wait and barrier
 // ahead of every launch's first DMA.  EM: the epilogue arithmetic's form (kEmFast with one fallback per unit, or kEmElem)
-template <int OP, int FIN, int EPI, int KC, int NIN, int S, int N, bool TDMA = false, int EM = kEmFast>
-__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, 1)))
+// W: waves per block (one block per CU): 4 -- one wave per SIMD, up to 512 registers each (arch + accumulation VGPRs
+// hold the results); 8 -- two waves per SIMD, 256 registers each, the SIMD's VALU issue shared by two instruction
+// streams (one wave alone issues a VALU op every 4 cycles, two every 2: MI355X_MICROARCH.md constants table)
+template <int OP, int FIN, int EPI, int KC, int NIN, int S, int N, bool TDMA = false, int EM = kEmFast, int W = 4>
+__global__ void __launch_bounds__(W * 64) __attribute__((amdgpu_waves_per_eu(W / 4, W / 4)))
 fedavg_tiles_epi_dma_f32x4(const RowTableF32 tab, const int64_t tstride4, f32x4* out, const int64_t b4,
                            const int64_t e4, const float fin_val, const EpiParams E_, const int64_t t0,
                            const int64_t t_end) {
     constexpr int G = KC + NIN;
-    constexpr int CPT = 4;  // float4 columns per lane per tile
-    constexpr int64_t T4 = (int64_t)CPT * kBlock;
+    static_assert(W == 4 || W == 8, "4 or 8 waves per block");
+    constexpr int CPT = 64 / (4 * W);       // float4 columns per lane per tile (4 at W = 4, 2 at W = 8)
+    constexpr int64_t T4 = kDefaultTile / 4;  // float4 per tile; a tile is 16 wave pieces of 64 float4
     constexpr int NOUT = epi_nout<EPI>();
     static_assert(KC >= 1 && KC <= 3 && NIN >= 1 && NIN <= 3 && NOUT <= G, "few-client fused form");
     static_assert(S >= 1 && S <= N && (S - 1) * G <= 63 && N % CPT == 0, "ring geometry");
-    static_assert((int64_t)4 * S * G * 1024 <= epi_dma_ring_bytes<EPI>(), "ring fits the CU's LDS");
-    __shared__ f32x4 ring[4][S][G][64];
+    static_assert((int64_t)W * S * G * 1024 <= epi_dma_ring_bytes<EPI>(), "ring fits the CU's LDS");
+    __shared__ f32x4 ring[W][S][G][64];
     EpiParams E = E_;
     if constexpr ((EPI & 0xFF) == FEDAVG_EPI_ADAM) E.amsgrad = 0;  // amsgrad runs the per-tile form (4 operand streams)
     const FinConst fc = fin_const<FIN>(fin_val);
@@ -765,9 +769,9 @@ fedavg_tiles_epi_dma_f32x4(const RowTableF32 tab, const int64_t tstride4, f32x4*
     const int lane = threadIdx.x & 63;
     if constexpr (kTableDma) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
-            glds16(reinterpret_cast<const uint4*>(E.rsqrtps) + (wave * 4 + j) * 64 + lane,
-                   lds_byte_addr(&g_rsqrtps_lds[(wave * 4 + j) * 256]));
+        for (int j = 0; j < 16 / W; ++j)  // 16 KiB: 16 / W pieces of 1 KiB per wave
+            glds16(reinterpret_cast<const uint4*>(E.rsqrtps) + (wave * (16 / W) + j) * 64 + lane,
+                   lds_byte_addr(&g_rsqrtps_lds[(wave * (16 / W) + j) * 256]));
     }
     // operand streams in EpiIn order (.a, .b, .c): the parameter (ADD_BASE: the base) and the optimizer states
     const float* opnd[3] = {(EPI & 0xFF) == FEDAVG_EPI_ADD_BASE ? E.base : E.param, E.state1, E.state2};
@@ -778,7 +782,7 @@ fedavg_tiles_epi_dma_f32x4(const RowTableF32 tab, const int64_t tstride4, f32x4*
     };
     auto issue = [&](const int u, const int slot) __attribute__((always_inline)) {
         const int64_t t = tile_of(u);
-        const int64_t col = (int64_t)(u % CPT) * kBlock + threadIdx.x;
+        const int64_t col = (int64_t)(u % CPT) * (W * 64) + threadIdx.x;
 #pragma unroll
         for (int k = 0; k < KC; ++k) glds16(tab.rows[k] + t * tstride4 + col, lds_byte_addr(&ring[wave][slot][k][0]));
         int64_t i = t * T4 + col;
@@ -838,7 +842,7 @@ fedavg_tiles_epi_dma_f32x4(const RowTableF32 tab, const int64_t tstride4, f32x4*
     static_for<0, N>([&](auto ic) {
         constexpr int u = decltype(ic)::value;
         const int64_t t = t_first + (int64_t)(u / CPT) * gridDim.x;
-        const int64_t i = t * T4 + (int64_t)(u % CPT) * kBlock + threadIdx.x;
+        const int64_t i = t * T4 + (int64_t)(u % CPT) * (W * 64) + threadIdx.x;
         if (t < t_end && i >= b4 && i < e4) {
             if constexpr (u < N - S) {
                 epi_store<EPI>(E, i, res[u], out);
@@ -857,35 +861,60 @@ fedavg_tiles_epi_dma_f32x4(const RowTableF32 tab, const int64_t tstride4, f32x4*
 
 // the LDS-DMA few-client form for this launch (1-3 client reads, no chained sum, no separate aggregate output):
 // NIN operand streams by optimizer kind and flags; false when the form does not carry this kind / flag set
-template <int OP, int FIN, int EPI, int KC, int NIN, int N = kEpiDmaUnits, bool TDMA = false, int EM = kEmFast>
+template <int OP, int FIN, int EPI, int KC, int NIN, int N = kEpiDmaUnits, bool TDMA = false, int EM = kEmFast,
+          int W = 4>
 inline hipError_t launch_epi_dma_n(const TileLaunch& L, const EpiParams& E, hipStream_t s, uint64_t* nl) {
-    constexpr int S = epi_dma_slots<EPI, KC + NIN, N>();
+    constexpr int S = epi_dma_slots<EPI, KC + NIN, N, W>();
+    constexpr int TPB = N * W / 16;  // tiles per block per launch
     f32x4* o = reinterpret_cast<f32x4*>(L.out);
-    return burst_launches(L.b4 / L.tile4, (L.e4 - 1) / L.tile4 + 1, L.grid, N / 4, nl, L.variant & kVariantAnyOrder,
+    return burst_launches(L.b4 / L.tile4, (L.e4 - 1) / L.tile4 + 1, L.grid, TPB, nl, L.variant & kVariantAnyOrder,
                           [&](int nb, int64_t t0, int64_t t_end, uint32_t flags) {
-                              hipExtLaunchKernelGGL((fedavg_tiles_epi_dma_f32x4<OP, FIN, EPI, KC, NIN, S, N, TDMA, EM>),
-                                                    dim3(nb), dim3(kBlock), 0, s, nullptr, nullptr, flags, L.tab,
+                              hipExtLaunchKernelGGL((fedavg_tiles_epi_dma_f32x4<OP, FIN, EPI, KC, NIN, S, N, TDMA, EM, W>),
+                                                    dim3(nb), dim3(W * 64), 0, s, nullptr, nullptr, flags, L.tab,
                                                     L.tstride4, o, L.b4, L.e4, L.fin_val, E, t0, t_end);
                           });
 }
 
-// A/B builds with -DFEDAVG_AB_FEW (torch-mode FIN_DIV Adam with the AMD-host sqrt only): launch variant bits 9-11 = 1-7
-// pick units per wave per launch, the table's staging and the epilogue arithmetic's form
+// The product geometry per optimizer kind and client reads: waves per block W, units per wave per launch N, the RSQRTPS
+// table by LDS-DMA.  Fused Adam with the AMD-host sqrt, 1e9 params, three interleaved rounds after a 3 s pre-warm, % of
+// 8 TB/s, outputs bit-equal (profiles/r06/s6/ab_k*.jsonl; the round-5 per-tile form on the same box 64.5 / 67.7 /
+// 67.4 at 1 / 2 / 3 clients):
+//   W = 4 (one wave per SIMD), N = 32:  65.6 / 73.1 / 79.2      N = 28: 65.1 / 73.0 / 78.2
+//   W = 8 (two per SIMD), N = 12 / 14 / 16 / 18:  74.1 / 74.1 / 73.3 / 73.4  |  73.6 / 74.0 / 74.3 / 74.0  |  74.2 / -- /
+//   74.8 / 74.0 (1 / 2 / 3 clients);  N = 16 with the table staged by loads: 72.2 / 74.8 / 78.2
+// One wave per SIMD issues a VALU op every 4 cycles; at 1-2 client reads Adam's ~400 instructions per wave-unit
+// (4 elements per lane) then take about as long as the unit's 5 KiB of HBM traffic, and two waves per SIMD (issue every
+// 2 cycles) win; at 3 reads the unit carries 6 KiB and one wave per SIMD with twice the ring slots (6 against 3) wins.
+// N: 16 against 24 / 32 at W = 4 (profiles/r06/s3/, s4/): 68.7 / 72.8 / 74.9 % at 2 clients -- a launch's fixed cost
+// (its start, its write burst's drain) over more units; at W = 8, 256 registers per wave hold 13 units' results.
+template <int EPI, int KC>
+struct EpiDmaGeom {
+    static constexpr bool kAdam = (EPI & 0xFF) == FEDAVG_EPI_ADAM;
+    static constexpr int W = kAdam && KC <= 2 ? 8 : 4;
+    static constexpr int N = !kAdam ? kEpiDmaUnits : KC == 1 ? 14 : KC == 2 ? 16 : 32;
+    static constexpr bool TDMA = kAdam && KC != 2;
+};
+
+// A/B builds with -DFEDAVG_AB_FEW (torch-mode FIN_DIV, ADD_BASE / SGD / Adam with the AMD-host sqrt): launch variant
+// bits 9-11 = 1-7 pick another geometry
 template <int OP, int FIN, int EPI, int KC, int NIN>
 inline hipError_t launch_epi_dma_form(const TileLaunch& L, const EpiParams& E, hipStream_t s, uint64_t* nl) {
-    if constexpr (kABFew && OP == FEDAVG_OP_TORCH && FIN == FEDAVG_FIN_DIV && EPI == (FEDAVG_EPI_ADAM | kEpiTorchSqrtAmd)) {
+    constexpr int KIND = EPI & 0xFF;
+    if constexpr (kABFew && OP == FEDAVG_OP_TORCH && FIN == FEDAVG_FIN_DIV &&
+                  (EPI == (FEDAVG_EPI_ADAM | kEpiTorchSqrtAmd) || KIND == FEDAVG_EPI_SGD || KIND == FEDAVG_EPI_ADD_BASE)) {
         switch ((L.variant >> kVariantLoopShift) & 7) {
-            case 1: return launch_epi_dma_n<OP, FIN, EPI, KC, NIN, 16, true>(L, E, s, nl);
-            case 2: return launch_epi_dma_n<OP, FIN, EPI, KC, NIN, 24, false>(L, E, s, nl);
-            case 3: return launch_epi_dma_n<OP, FIN, EPI, KC, NIN, 24, true>(L, E, s, nl);
-            case 4: return launch_epi_dma_n<OP, FIN, EPI, KC, NIN, 32, true>(L, E, s, nl);
-            case 5: return launch_epi_dma_n<OP, FIN, EPI, KC, NIN, 8, true>(L, E, s, nl);
-            case 6: return launch_epi_dma_n<OP, FIN, EPI, KC, NIN, 16, true, kEmElem>(L, E, s, nl);
-            case 7: return launch_epi_dma_n<OP, FIN, EPI, KC, NIN, 24, true, kEmElem>(L, E, s, nl);
+            case 1: return launch_epi_dma_n<OP, FIN, EPI, KC, NIN, 16, false>(L, E, s, nl);
+            case 2: return launch_epi_dma_n<OP, FIN, EPI, KC, NIN, 32, true>(L, E, s, nl);
+            case 3: return launch_epi_dma_n<OP, FIN, EPI, KC, NIN, 12, true, kEmFast, 8>(L, E, s, nl);
+            case 4: return launch_epi_dma_n<OP, FIN, EPI, KC, NIN, 16, true, kEmFast, 8>(L, E, s, nl);
+            case 5: return launch_epi_dma_n<OP, FIN, EPI, KC, NIN, 16, false, kEmFast, 8>(L, E, s, nl);
+            case 6: return launch_epi_dma_n<OP, FIN, EPI, KC, NIN, 24, true>(L, E, s, nl);
+            case 7: return launch_epi_dma_n<OP, FIN, EPI, KC, NIN, 40, true>(L, E, s, nl);
             default: break;
         }
     }
-    return launch_epi_dma_n<OP, FIN, EPI, KC, NIN>(L, E, s, nl);
+    using Geom = EpiDmaGeom<EPI, KC>;
+    return launch_epi_dma_n<OP, FIN, EPI, KC, NIN, Geom::N, Geom::TDMA, kEmFast, Geom::W>(L, E, s, nl);
 }
 
 template <int OP, int FIN, int EPI, int KC>

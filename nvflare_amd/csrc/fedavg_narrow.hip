@@ -499,6 +499,7 @@ fedavg_tiles_narrow_few(const RowTableNarrow tab, const int64_t tstride8, u32x4*
     constexpr int CPL = kCpl16 * P;                      // u32x4 per lane per unit
     constexpr int64_t T8 = (int64_t)CPL * kBlock;        // u32x4 per unit
     const int64_t last_tile = (e8 - 1) / ((int64_t)kCpl16 * kBlock);
+    const int64_t first_tile = b8 / ((int64_t)kCpl16 * kBlock);  // a unit's tiles before begin's are not read
     const FinConst fc = fin_const<FIN>(fv);
     __shared__ u32x4 staged[L > 0 ? L * CPL * kBlock : 1];
     const int64_t t_first = t0 + blockIdx.x;
@@ -512,6 +513,7 @@ fedavg_tiles_narrow_few(const RowTableNarrow tab, const int64_t tstride8, u32x4*
         for (int h = 0; h < P; ++h) {
             int64_t tile = u * P + h;
             tile = tile <= last_tile ? tile : last_tile;
+            tile = tile >= first_tile ? tile : first_tile;
             const int64_t off = tile * tstride8 + threadIdx.x;
 #pragma unroll
             for (int j = 0; j < KC; ++j)

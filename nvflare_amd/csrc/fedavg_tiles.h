@@ -305,6 +305,9 @@ fedavg_tiles_few_f32x4(const RowTableF32 tab, const int64_t tstride4, f32x4* out
     constexpr int CPL = CPT * P;
     constexpr int64_t T4 = (int64_t)CPL * kBlock;  // float4 per unit
     const int64_t last_tile = (e4 - 1) / ((int64_t)CPT * kBlock);
+    // a pair unit starting before begin's tile (begin's tile index odd) re-reads begin's tile instead of the one before
+    // it: the C-ABI only requires storage for the tiles [begin, end) touches
+    const int64_t first_tile = b4 / ((int64_t)CPT * kBlock);
     const FinConst fc = fin_const<FIN>(fin_val);
     __shared__ f32x4 staged[L > 0 ? L * CPL * kBlock : 1];
     const int64_t t_first = t0 + blockIdx.x;
@@ -326,6 +329,7 @@ fedavg_tiles_few_f32x4(const RowTableF32 tab, const int64_t tstride4, f32x4* out
         for (int h = 0; h < P; ++h) {
             int64_t tile = u * P + h;
             tile = tile <= last_tile ? tile : last_tile;
+            tile = tile >= first_tile ? tile : first_tile;
             const int64_t off = tile * tstride4 + threadIdx.x;
 #pragma unroll
             for (int j = 0; j < KC; ++j)

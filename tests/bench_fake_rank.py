@@ -52,6 +52,15 @@ def install(rank, world):
             sh = ShardedFedAvg(list(devices))
             for eng in sh.engines:
                 eng._ctx = FakeDeviceContext()
+            stall = os.environ.get("NVFLARE_AMD_FAKE_STALL_DEVICE")  # tests/test_cpu_host_sharded8.py: a device whose
+            if stall is not None:  # staging copies never return (the 2s entry must end through the watchdog)
+                import time
+
+                def stalled(*a, **k):
+                    time.sleep(3600)
+
+                ctx_ = sh.engines[int(stall)]._ctx
+                ctx_.h2d_tiled_multi = ctx_.h2d_ptr = ctx_.h2d = stalled
             h._engine = sh
             if hasattr(old, "release"):
                 old.release()

@@ -104,12 +104,14 @@ def test_strong_scaling_buckets_gloo(oracle, world):
 
 def test_bench_presets_follow_baseline():
     """bench.py --config N fills K, P, the epilogue and the scaling from BASELINE.json configs[1..4]; the default run
-    (config 3) also measures configs 5 and 4 under strong scaling and config 4 through the client-sharded exchange;
+    (config 3) also measures config 2 device-resident, configs 5 and 4 under strong scaling, config 2 host-resident and
+    config 4 through the client-sharded exchange;
     explicit overrides turn that off."""
     import bench
 
     a = bench.parse([])
-    assert (a.clients, a.params, a.epilogue, a.scaling, a.also) == (64, 10**9, "none", "weak", [5, 4, bench.HOST_RESIDENT, bench.HOST_SHARDED, bench.CLIENT_SHARDED])
+    assert (a.clients, a.params, a.epilogue, a.scaling, a.also) == \
+        (64, 10**9, "none", "weak", [2, 5, 4, bench.HOST_RESIDENT, bench.HOST_SHARDED, bench.CLIENT_SHARDED])
     assert bench.parse(["--also", "4x,5"]).also == [bench.CLIENT_SHARDED, 5]
     assert bench.parse(["--also", "2h"]).also == [bench.HOST_RESIDENT]
     assert bench.parse(["--also", "2s,2h"]).also == [bench.HOST_SHARDED, bench.HOST_RESIDENT]

@@ -89,9 +89,17 @@ class _Case:
             b.close()
 
 
-def _launches(ctx, begin, end):
+def _tiles_per_block(kind, K):
+    """Tiles per block per launch of the product geometry (fedavg_epi.h EpiDmaGeom: N units per wave x W waves / 16):
+    Adam 1 / 2 clients 8 waves x 14 / 16 units, 3 clients 4 waves x 32; ADD_BASE / SGD 4 waves x 16."""
+    if kind == 3:
+        return {1: 7, 2: 8, 3: 8}[K]
+    return 4
+
+
+def _launches(ctx, begin, end, kind=3, K=2):
     t_first, t_stop = begin // TILE, (end - 1) // TILE + 1
-    per = min(ctx.num_cus, t_stop - t_first) * 4  # one block per CU, 4 tiles per block
+    per = min(ctx.num_cus, t_stop - t_first) * _tiles_per_block(kind, K)  # one block per CU
     return -(-(t_stop - t_first) // per)
 
 
@@ -144,7 +152,7 @@ def test_dma_adam_matches_oracle_and_per_tile(ctx, oracle, K, rng_ix, sqrt):
             e = _epi(3, param=c.buf("p", p), state1=c.buf("m", m), state2=c.buf("v", v), step=3.0, torch_sqrt=flag, **hp)
             nl = _run(ctx, c, e, N.FEDAVG_OP_TORCH, N.FEDAVG_FIN_DIV, variant=variant)
             if variant == 0:
-                assert nl == _launches(ctx, begin, end)
+                assert nl == _launches(ctx, begin, end, 3, K)
             got[variant] = [c.get(x) for x in ("p", "m", "v")]
         pw, mw, vw = p.copy(), m.copy(), v.copy()
         oracle.epilogue_apply(c.d(oracle, 1), oracle.EPI_ADAM, p=pw, m=mw, v=vw, step=3.0, torch_cpu_sqrt=sqrt,
@@ -173,7 +181,7 @@ def test_dma_sgd_two_steps(ctx, oracle, K, rng_ix, momentum):
         for step in (1, 2):
             e = _epi(2, param=pp, state1=pb, first_step=int(step == 1), **hp)
             nl = _run(ctx, c, e, N.FEDAVG_OP_TORCH, N.FEDAVG_FIN_DIV)
-            assert nl == _launches(ctx, begin, end)
+            assert nl == _launches(ctx, begin, end, 2, K)
             oracle.epilogue_apply(c.d(oracle, 1), oracle.EPI_SGD, p=p, m=buf, first_step=int(step == 1), **hp)
             assert same_bits(c.get("p"), p), step
             if momentum:
@@ -194,7 +202,7 @@ def test_dma_add_base(ctx, oracle, K, rng_ix, op, fin):
         e = _epi(1, base=c.buf("base", base))
         outp = c.buf("out", np.zeros(c.n, np.float32))
         nl = _run(ctx, c, e, op, fin, out_ptr=outp)
-        assert nl == _launches(ctx, begin, end)
+        assert nl == _launches(ctx, begin, end, 1, K)
         want = oracle.epilogue_apply(c.d(oracle, op), oracle.EPI_ADD_BASE, base=base)
         assert same_bits(c.get("out"), want)
         assert same_bits(c.get("base"), base)  # the base is an input only
@@ -218,4 +226,25 @@ def test_dma_route_leaves_others_on_the_per_tile_form(ctx, oracle):
         want = c.d(oracle, 1)
         assert same_bits(c.get("d"), want)
     finally:
+        c.close()
+
+
+def test_ab_probe_keeps_the_variant(ctx):
+    """DeviceContext.ab_build() probes the library with variant bit 5 and restores the variant the context had (ADVICE
+    r05: it used to reset it to 0): with public bit 2 set, the 2-client fused Adam call still takes the per-tile form."""
+    from nvflare_amd import _native as N
+
+    c = _Case(ctx, 2, 0, 5 * ctx.num_cus * 4 * TILE, seed=9)
+    try:
+        z = np.zeros(c.n, np.float32)
+        e = _epi(3, param=c.buf("p", z + 1), state1=c.buf("m", z), state2=c.buf("v", z), step=1.0, **ADAM)
+        ctx.set_variant(4)
+        ctx.ab_build()
+        n0 = ctx.launch_count()
+        ctx.accumulate_tiled_epi(c.bases, c.ws, TILE, c.lay.tile_stride, c.begin, c.end, None, N.FEDAVG_OP_TORCH,
+                                 N.FEDAVG_FIN_DIV, _sum(c.ws), e)
+        ctx.sync()
+        assert ctx.launch_count() - n0 == 1  # the per-tile form, not the LDS-DMA form's 3 launches
+    finally:
+        ctx.set_variant(0)
         c.close()

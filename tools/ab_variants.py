@@ -33,6 +33,9 @@ def main():
     ap.add_argument("--check", action="store_true",
                     help="every config's output (the fused epilogues: p and the last state, from zeroed state) must "
                          "equal the first config's bit for bit")
+    ap.add_argument("--prewarm-s", type=float, default=0.0,
+                    help="seconds of the first config run back to back before the first round (the GPU's power state "
+                         "ramps over the first seconds of load: VERDICT r05 item 3)")
     ap.add_argument("--sqrt", choices=["ieee", "torch_cpu", "torch_cpu_amd"], default="ieee",
                     help="the fused epilogues' sqrt (EpiParams.torch_sqrt)")
     a = ap.parse_args()
@@ -40,6 +43,10 @@ def main():
     from nvflare_amd.device import DeviceContext, TiledLayout
 
     ctx = DeviceContext.get(0)
+    from tools.gpu_state import GpuMonitor
+
+    mon = GpuMonitor(0)  # clocks, power, temperatures per measurement
+    print(json.dumps({"gpu_state": mon.snapshot()}), flush=True)
     K, P = a.clients, int(a.params)
     lay = TiledLayout(4096, K)
     end = (P + 3) // 4 * 4
@@ -84,6 +91,21 @@ def main():
     epis = a.epilogues.split(",")
     res = {}
     ref_out = {}
+    if a.prewarm_s > 0:
+        import time
+
+        v = variants[0]
+        ctx.set_variant(v[0])
+        ctx.set_launch(v[2], v[1])
+        fn = launcher(epis[0], pads[0])
+        t_end = time.perf_counter() + a.prewarm_s
+        n = 0
+        while time.perf_counter() < t_end:
+            for _ in range(10):
+                fn()
+            ctx.sync()
+            n += 10
+        print(json.dumps({"prewarm_s": a.prewarm_s, "calls": n, "gpu_state": mon.snapshot()}), flush=True)
     for rnd in range(a.rounds):
         for epi, pad in [(e_, p_) for e_ in epis for p_ in pads]:
             fn = launcher(epi, pad)
@@ -110,15 +132,21 @@ def main():
                         if bad:
                             raise SystemExit(f"config {v}: {bad} outputs differ from config {variants[0]}")
                     ctx.memset(out.ptr, 0xFF, end * 4)
-                ctx.timing_begin()
-                for _ in range(a.reps):
-                    fn()
-                ms = ctx.timing_end() / a.reps
+                with mon.sample(0.02) as smp:
+                    ctx.timing_begin()
+                    for _ in range(a.reps):
+                        fn()
+                    ms = ctx.timing_end() / a.reps
+                st = smp.summary()
+                state = {k: (st[k]["median"] if isinstance(st.get(k), dict) else st.get(k))
+                         for k in ("current_gfxclk", "current_uclk", "current_socket_power", "temperature_hotspot",
+                                   "temperature_mem", "throttle_status", "samples") if k in st}
                 gbs = (4.0 * K * P + EXTRA[epi] * P) / ms / 1e6
                 res.setdefault((epi, pad, v), []).append(ms)
                 print(json.dumps({"round": rnd, "epilogue": epi, "pad": pad, "mode": a.mode,
                                   "variant": ":".join(map(str, v)), "clients": K, "params": P,
-                                  "ms": round(ms, 4), "GBps": round(gbs, 1), "frac_8TBps": round(gbs / 8000, 4)}),
+                                  "ms": round(ms, 4), "GBps": round(gbs, 1), "frac_8TBps": round(gbs / 8000, 4),
+                                  "gpu": state}),
                       flush=True)
     ctx.set_variant(0)
     ctx.set_launch(0, 0)
