@@ -728,7 +728,7 @@ template <int EPI>
 constexpr int epi_dma_ring_bytes() {
     return kLdsBytesPerCu - ((EPI & kEpiTorchSqrtAmd) ? 16 * 1024 : (EPI & kEpiTorchSqrt) ? 1024 : 0);
 }
-constexpr int kEpiDmaUnits = 16;  // units per wave per launch: 4 tiles per block (the probe's e_burst_r4 launch size)
+constexpr int kEpiDmaUnits = 16;  // units per wave per launch by default (A/B forms; EpiDmaGeom has the product's)
 // ring slots per wave: as many as the LDS holds, with every in-flight DMA countable by vmcnt (<= 63), at most N
 template <int EPI, int G, int N = kEpiDmaUnits, int W = 4>
 constexpr int epi_dma_slots() {
@@ -887,11 +887,15 @@ inline hipError_t launch_epi_dma_n(const TileLaunch& L, const EpiParams& E, hipS
 // 2 cycles) win; at 3 reads the unit carries 6 KiB and one wave per SIMD with twice the ring slots (6 against 3) wins.
 // N: 16 against 24 / 32 at W = 4 (profiles/r06/s3/, s4/): 68.7 / 72.8 / 74.9 % at 2 clients -- a launch's fixed cost
 // (its start, its write burst's drain) over more units; at W = 8, 256 registers per wave hold 13 units' results.
+// SGD (momentum) and ADD_BASE, the same sweep (profiles/r06/s8/ab_k*.jsonl, 1 / 2 / 3 clients): W = 4, N = 40: SGD 78.3 /
+// 78.9 / 77.1, ADD_BASE 75.4 / 75.3 / 77.3 (N = 32: 77.4 / 78.9 / 77.5, 72.8 / 75.2 / 76.3; N = 16: 69.1 / 75.0 / 75.7,
+// 67.3 / 71.3 / 72.3; W = 8, N = 16: 75.9 / 74.3 / 74.7, 72.9 / 75.0 / 74.3) -- lighter arithmetic, fewer result
+// registers per unit (8 and 4): one wave per SIMD keeps up, and 40 units fit its registers.
 template <int EPI, int KC>
 struct EpiDmaGeom {
     static constexpr bool kAdam = (EPI & 0xFF) == FEDAVG_EPI_ADAM;
     static constexpr int W = kAdam && KC <= 2 ? 8 : 4;
-    static constexpr int N = !kAdam ? kEpiDmaUnits : KC == 1 ? 14 : KC == 2 ? 16 : 32;
+    static constexpr int N = !kAdam ? 40 : KC == 1 ? 14 : KC == 2 ? 16 : 32;
     static constexpr bool TDMA = kAdam && KC != 2;
 };
 

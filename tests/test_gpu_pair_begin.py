@@ -73,8 +73,8 @@ def _run(ctx, elem, K, begin, end, from_tile, fmt=None):
 @pytest.mark.parametrize("begin_tile", [7, 13])
 @pytest.mark.parametrize("elem,K,fmt", [(4, 1, None), (2, 1, "bf16"), (2, 3, "bf16"), (2, 1, "f16"), (2, 3, "f16")])
 def test_pair_forms_read_nothing_before_begin(ctx, elem, K, fmt, begin_tile):
-    begin = begin_tile * TILE + 36
-    end = begin + 9 * TILE + 20  # several pair units, a ragged end
+    begin = begin_tile * TILE + 40  # multiples of 8 (the 16-bit entry's granule)
+    end = begin + 9 * TILE + 24  # several pair units, a ragged end
     full = _run(ctx, elem, K, begin, end, 0, fmt)
     own = _run(ctx, elem, K, begin, end, begin_tile, fmt)
     assert same_bits(own, full)

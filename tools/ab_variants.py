@@ -28,6 +28,9 @@ def main():
     ap.add_argument("--epilogues", default="none,adam")
     ap.add_argument("--pads", default="0", help="tile-stride pads in elements (multiples of 64): one slab each, "
                                                 "interleaved -- DRAM channel mapping of power-of-two strides")
+    ap.add_argument("--op-shifts", default="0",
+                    help="byte offsets (multiples of 256) of the fused epilogues' operand buffers (p, m, v / base): one "
+                         "set of configs each, interleaved -- where the write streams fall in HBM relative to the reads")
     ap.add_argument("--mode", choices=["torch", "numpy"], default="torch",
                     help="torch: fma steps, IEEE division at the end; numpy: mul + add, multiply by 1/count")
     ap.add_argument("--check", action="store_true",
@@ -64,14 +67,16 @@ def main():
     op, fin = (1, 2) if a.mode == "torch" else (0, 1)
     ws = [float(1 + (37 * k) % 100) for k in range(K)]
     cnt = sum(ws)
-    bufs = [ctx.alloc(end * 4) for _ in range(3)]
+    shifts = [int(x) for x in a.op_shifts.split(",")]
+    assert all(x % 256 == 0 and x >= 0 for x in shifts)
+    bufs = [ctx.alloc(end * 4 + max(shifts)) for _ in range(3)]
     for b in bufs:
-        ctx.memset(b.ptr, 0, end * 4)
+        ctx.memset(b.ptr, 0, end * 4 + max(shifts))
     out = ctx.alloc(end * 4)
     ctx.sync()
     kinds = {"add_base": N.FEDAVG_EPI_ADD_BASE, "sgd": N.FEDAVG_EPI_SGD, "adam": N.FEDAVG_EPI_ADAM}
 
-    def launcher(epi, pad):
+    def launcher(epi, pad, sh=0):
         _, bases, stride = slabs[pad]
         if epi == "none":
             return lambda: ctx.accumulate_tiled(bases, ws, lay.tile, stride, 0, end, out.ptr, op, fin, cnt)
@@ -81,9 +86,9 @@ def main():
         e.torch_sqrt = {"ieee": N.FEDAVG_SQRT_IEEE, "torch_cpu": N.FEDAVG_SQRT_TORCH_AVX512,
                         "torch_cpu_amd": N.FEDAVG_SQRT_TORCH_AMD}[a.sqrt]
         if epi == "add_base":
-            e.base, o = bufs[0].ptr, out.ptr
+            e.base, o = bufs[0].ptr + sh, out.ptr
         else:
-            e.param, e.state1, e.state2 = bufs[0].ptr, bufs[1].ptr, bufs[2].ptr
+            e.param, e.state1, e.state2 = bufs[0].ptr + sh, bufs[1].ptr + sh, bufs[2].ptr + sh
             o = None
         return lambda: ctx.accumulate_tiled_epi(bases, ws, lay.tile, stride, 0, end, o, op, fin, cnt, e)
 
@@ -107,22 +112,22 @@ def main():
             n += 10
         print(json.dumps({"prewarm_s": a.prewarm_s, "calls": n, "gpu_state": mon.snapshot()}), flush=True)
     for rnd in range(a.rounds):
-        for epi, pad in [(e_, p_) for e_ in epis for p_ in pads]:
-            fn = launcher(epi, pad)
+        for epi, pad, sh in [(e_, p_, s_) for e_ in epis for p_ in pads for s_ in shifts]:
+            fn = launcher(epi, pad, sh)
             for v in variants:
                 ctx.set_variant(v[0])
                 ctx.set_launch(v[2], v[1])
-                if a.check and epi != "none" and rnd == 0 and pad == pads[0]:
+                if a.check and epi != "none" and rnd == 0 and pad == pads[0] and sh == shifts[0]:
                     for b in bufs:  # the same state in for every config
                         ctx.memset(b.ptr, 0, end * 4)
                 fn()
-                if a.check and rnd == 0 and pad == pads[0]:
+                if a.check and rnd == 0 and pad == pads[0] and sh == shifts[0]:
                     host = np.empty(end, dtype=np.float32)
                     ctx.sync()
-                    ctx.d2h(host, out.ptr if epi in ("none", "add_base") else bufs[0].ptr)
+                    ctx.d2h(host, out.ptr if epi in ("none", "add_base") else bufs[0].ptr + shifts[0])
                     if epi not in ("none", "add_base"):
                         last = np.empty(end, dtype=np.float32)
-                        ctx.d2h(last, bufs[2 if epi == "adam" else 1].ptr)
+                        ctx.d2h(last, bufs[2 if epi == "adam" else 1].ptr + shifts[0])
                         host = np.concatenate([host, last])
                     if epi not in ref_out:
                         ref_out[epi] = host
@@ -142,18 +147,18 @@ def main():
                          for k in ("current_gfxclk", "current_uclk", "current_socket_power", "temperature_hotspot",
                                    "temperature_mem", "throttle_status", "samples") if k in st}
                 gbs = (4.0 * K * P + EXTRA[epi] * P) / ms / 1e6
-                res.setdefault((epi, pad, v), []).append(ms)
-                print(json.dumps({"round": rnd, "epilogue": epi, "pad": pad, "mode": a.mode,
+                res.setdefault((epi, pad, sh, v), []).append(ms)
+                print(json.dumps({"round": rnd, "epilogue": epi, "pad": pad, "op_shift": sh, "mode": a.mode,
                                   "variant": ":".join(map(str, v)), "clients": K, "params": P,
                                   "ms": round(ms, 4), "GBps": round(gbs, 1), "frac_8TBps": round(gbs / 8000, 4),
                                   "gpu": state}),
                       flush=True)
     ctx.set_variant(0)
     ctx.set_launch(0, 0)
-    for (epi, pad, v), xs in res.items():
+    for (epi, pad, sh, v), xs in res.items():
         ms = statistics.median(xs)
         gbs = (4.0 * K * P + EXTRA[epi] * P) / ms / 1e6
-        print(json.dumps({"summary": True, "epilogue": epi, "pad": pad, "mode": a.mode,
+        print(json.dumps({"summary": True, "epilogue": epi, "pad": pad, "op_shift": sh, "mode": a.mode,
                           "variant": ":".join(map(str, v)), "clients": K, "params": P,
                           "median_ms": round(ms, 4), "GBps": round(gbs, 1), "frac_8TBps": round(gbs / 8000, 4)}),
               flush=True)
