@@ -104,6 +104,11 @@ def parse(argv=None):
     ap.add_argument("--tile", type=int, default=4096, help="slab tile width (elements)")
     ap.add_argument("--epilogue", choices=["none", "add_base", "sgd", "adam", "adamax", "nadam", "radam"], default=None,
                     help="fused server update (config 5 = adam: FedOpt Adam on the aggregated deltas)")
+    ap.add_argument("--entry-warmup-s", type=float, default=0.5,
+                    help="the also entries' untimed warmup lasts at least this long (the main entry runs exactly "
+                         "--warmup steps): a short entry after an idle gap (a D2H, a fill) otherwise times the GPU "
+                         "while its clocks ramp back up (round 6: config 4's share at 1 666 MHz gfx, 85.7 %% against "
+                         "88.5 %% warm)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-baseline-s", type=float, default=8.0, help="seconds of CPU work the baseline times")
     ap.add_argument("--cpu-sample-params", type=int, default=16 * 1024 * 1024)
@@ -631,6 +636,9 @@ def kernel_name(K, epilogue, variant):
         if variant & 12 == 0 and K <= 3 and epilogue in ("adam", "sgd", "add_base"):
             return ("fedavg_tiles_epi_dma_f32x4 (1-3 client reads: inputs HBM -> LDS by LDS-DMA, results held on chip "
                     "and stored as chip-wide bursts)")
+        if variant & 12 == 0 and K >= 64 and epilogue == "adam" and not variant & ((1 << 15) | 64):
+            return ("fedavg_tiles_epi_split_f32x4 (the burst form's client phase on 4 waves, the epilogue on 8: "
+                    "4 register- + 9 LDS-held tiles per block per launch)")
         return "fedavg_tiles_epi_burst_f32x4" if variant & 12 == 0 and K >= 4 else "fedavg_tiles_epi_f32x4"
     if K <= 3 and not variant & (11 | 256):
         return ("fedavg_tiles_few_f32x4 (1-3 client reads: every register-held tile's loads issued before any "
@@ -643,7 +651,7 @@ def kernel_name(K, epilogue, variant):
                if K >= 32 and not variant & 64 else "8 register- + 4 LDS-held tiles per block per launch)"))
 
 
-def run_workload(args, ctx, world, rank, K, P_spec, scaling, epilogue, baseline, seed):
+def run_workload(args, ctx, world, rank, K, P_spec, scaling, epilogue, baseline, seed, min_warmup_s=0.0):
     """Stage one workload in HBM, time args.steps aggregations after args.warmup, spot-check, free it.
 
     Returns a dict (every rank) or, when the workload does not fit every rank's device, {"skipped": reason}."""
@@ -712,6 +720,15 @@ def run_workload(args, ctx, world, rank, K, P_spec, scaling, epilogue, baseline,
 
         for _ in range(args.warmup):
             step()
+        if min_warmup_s > 0:  # also entries: at least min_warmup_s of untimed steps (every rank decides the same)
+            t_w = time.perf_counter()
+            ctx.sync()
+            go = 1
+            while go:
+                for _ in range(4):
+                    step()
+                ctx.sync()
+                go = max_over_ranks(world, 1.0 if time.perf_counter() - t_w < min_warmup_s else 0.0) > 0
         barrier_sync(world, ctx)
         n_launch0 = ctx.launch_count()
         with gpu_sampler(args) as sampler:  # this rank's GPU clocks, power, temperatures over the timed steps
@@ -1160,7 +1177,7 @@ def main(argv=None):
                     f"sharding.bucket_ranges({p['params']}, {SHARE_GPUS}): {p['clients']} clients x {P_run} params)")
         t_entry = time.perf_counter()
         r = run_workload(args, ctx, world, rank, p["clients"], P_run, "weak" if share else p["scaling"], p["epilogue"],
-                         baseline=False, seed=args.seed)
+                         baseline=False, seed=args.seed, min_warmup_s=args.entry_warmup_s)
         failed = failed or bool((r.get("spot_check") or {}).get("mismatches"))
         if rank == 0:
             if "skipped" in r:

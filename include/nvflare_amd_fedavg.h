@@ -325,7 +325,8 @@ int fedavg_timing_end(fedavg_ctx* ctx, float* ms);
 /* Aggregation / epilogue / dequantization kernel launches issued on the context's compute stream so far.
  * One fedavg_accumulate* call may issue several (the fp32 burst kernels: one per grid x tiles-per-block tiles --
  * 18 tiles per block on the one-block-per-CU grids of the plain kernel at 32+ clients (17 for the fused kernel at
- * 64+), 12 on two-block grids); relates a profiler's per-launch durations to per-call times. */
+ * 64+), 12 on two-block grids; the fused LDS-DMA form at 1-3 reads 7-10 tiles per block, one block per CU); relates a
+ * profiler's per-launch durations to per-call times. */
 int fedavg_launch_count(fedavg_ctx* ctx, uint64_t* n);
 /* Launch tuning (0 = default): blocks per CU (default: each kernel's own -- 1 for the burst aggregation
  * kernel at >= 32 clients, the fused one at >= 64, the 16-bit one at >= 48 in torch mode, 2 otherwise),
@@ -339,7 +340,11 @@ int fedavg_set_launch(fedavg_ctx* ctx, int blocks_per_cu, int unroll);
  * 64+).  A plain launch with 1-3 client reads and no chained sum (most NVFlare jobs run 2 clients) runs the FEW-CLIENT
  * burst form (round 5): every register-held tile's loads go out before any arithmetic, the results are stored as a
  * burst; a chained sum with fewer than 3 reads runs the PER-TILE-STORE form, which stores each tile's results as it
- * finishes; the fused kernel under 4 reads its per-tile form pipelined across tiles.  Every load and store is
+ * finishes.  The fused kernel with 1-3 client reads, no chained sum and no separate aggregate output (out only for
+ * ADD_BASE) runs its LDS-DMA few-client form (round 6) for ADD_BASE, SGD and Adam without amsgrad: every input goes HBM
+ * -> LDS by LDS-DMA while the wave computes the units already landed, the results are held on chip and stored as a
+ * burst; other kinds, amsgrad and chained sums under 4 reads run its per-tile form pipelined across tiles.  Every load
+ * and store is
  * nontemporal.  The 16-bit and fp64 tile kernels (fedavg_accumulate_tiled16 / _tiled64) likewise run 1-3 client
  * reads without a chained sum on their few-client burst forms, the rest on their burst forms.  The plain burst kernel has the launch's client count
  * built in for 5 clients and the count's
@@ -347,7 +352,7 @@ int fedavg_set_launch(fedavg_ctx* ctx, int blocks_per_cu, int unroll);
  * kernel from 4 clients on, fused from 8).  Results are bit-identical in every variant.
  * The PRODUCT library (nvflare_amd/_build.py) carries only the routed kernel forms and accepts:
  * bit 2 = the fused per-tile form (pipelined across tiles: the next tile's first client loads overlap the epilogue) at
- *         every read count;
+ *         every read count (the round-5 route at 1-3 reads, instead of the LDS-DMA form);
  * bit 4 = burst launches after the first of a call go out without the AQL barrier bit (hipExtAnyOrderLaunch), so
  *         one launch's blocks start as the previous launch drains;
  * bit 6 = one-block-per-CU grids keep the 4-LDS-tile form (12 tiles per block per launch).
@@ -363,8 +368,9 @@ int fedavg_set_launch(fedavg_ctx* ctx, int blocks_per_cu, int unroll);
  *         FIN_DIV Adam with the AMD-host sqrt and no chained partial sum), the plain burst kernel's (fedavg_tiles.h
  *         launch_burst; 6 / 7 = 3-6 clients on a built-in count / the remainder forms), the few-client form's
  *         geometry at 1-2 reads (1-6) and 3-4 reads (1-5) (fedavg_internal.h kFewAB, kFewAB34), the 16-bit
- *         and fp64 few-client forms' at 1-3 reads (1-4, kNarrowFewAB, kF64FewAB), and the fused
- *         register-held few-client form at 2-3 reads (fedavg_epi.h fedavg_tiles_epi_few_f32x4);
+ *         and fp64 few-client forms' at 1-3 reads (1-4, kNarrowFewAB, kF64FewAB), and the fused LDS-DMA
+ *         form's geometry at 1-3 reads (1-7: waves per block, units per wave, the RSQRTPS table's staging; fedavg_epi.h
+ *         launch_epi_dma_form; torch-mode FIN_DIV ADD_BASE / SGD / Adam with the AMD-host sqrt, -DFEDAVG_AB_FEW builds);
  * and unroll 8 (fedavg_set_launch) and tile widths 1024 / 2048 / 8192 (fedavg_set_tile, fedavg_accumulate_tiled).
  * A product library refuses those with an error ("... A/B form ..."), never running another form in their place. */
 int fedavg_set_variant(fedavg_ctx* ctx, int variant);

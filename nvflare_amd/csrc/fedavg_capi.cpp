@@ -1389,7 +1389,8 @@ int fedavg_accumulate_tiled_epi(fedavg_ctx* ctx, const void* const* bases, const
         L.fin = fin;
         L.unroll = fedavg::kDefaultUnroll;
         L.variant = ctx->variant & (fedavg::kVariantEpiPrefetch | fedavg::kVariantTileStores | fedavg::kVariantAnyOrder |
-                                    fedavg::kVariantRegisterTiles | (7 << fedavg::kVariantLoopShift));
+                                    fedavg::kVariantRegisterTiles | fedavg::kVariantEpiNoSplit |
+                                    (7 << fedavg::kVariantLoopShift));
         L.tile4 = (int64_t)tile_elems / 4;
         L.tstride4 = (int64_t)tile_stride / 4;
         L.b4 = (int64_t)begin / 4;
@@ -1492,11 +1493,13 @@ int fedavg_set_launch(fedavg_ctx* ctx, int blocks_per_cu, int unroll) {
 int fedavg_set_variant(fedavg_ctx* ctx, int variant) {
     return guarded([&] {
         if (!ctx) throw Error("ctx is NULL");
-        if (variant < 0 || variant > 4095) throw Error("variant must be 0..4095");
+        // bits 0-11 and 15 are public; 12-14 are set inside the library by its routing (kVariantFew, kVariantEpiDma)
+        if (variant < 0 || (variant & ~(4095 | fedavg::kVariantEpiNoSplit)))
+            throw Error("variant must be 0..4095, optionally with bit 15 (32768)");
         const int accepted = fedavg::kVariantProductMask | (fedavg::kABFew ? 7 << fedavg::kVariantLoopShift | kVariantFewBurst : 0);
         if (!fedavg::kAB && (variant & ~accepted))
             throw Error("variant bits " + std::to_string(variant & ~accepted) +
-                        " are A/B forms this product library does not carry (it accepts bits 2, 4 and 6; "
+                        " are A/B forms this product library does not carry (it accepts bits 2, 4, 6 and 15; "
                         "tools/build_rev_lib.py builds A/B libraries)");
         ctx->variant = variant;
     });

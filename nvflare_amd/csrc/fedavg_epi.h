@@ -308,33 +308,43 @@ __device__ __forceinline__ EpiIn epi_compute(const EpiParams& E, const EpiConsts
     return o;
 }
 
+// the epilogue's stores are nontemporal; A/B builds with -DFEDAVG_EPI_TEMPORAL (tools/build_rev_lib.py -D) make them
+// temporal, for the device cache to absorb a launch's write burst and write it back on its own schedule: config 5 87.9
+// against 88.0 %, the 2-client LDS-DMA form 70.5 against 74.7 % (profiles/r06/s10/, processes alternating) -- not kept
+#if defined(FEDAVG_EPI_TEMPORAL)
+constexpr bool kEpiNtStores = false;
+#else
+constexpr bool kEpiNtStores = true;
+#endif
+
 template <int EPI>
 __device__ __forceinline__ void epi_store(const EpiParams& E, const int64_t i, const EpiIn& o, f32x4* out) {
     constexpr int KIND = EPI & 0xFF;
+    constexpr bool NT = kEpiNtStores;
     if constexpr (KIND == FEDAVG_EPI_ADD_BASE) {
-        store4<true>(out + i, o.a);
+        store4<NT>(out + i, o.a);
         return;
     }
-    store4<true>(reinterpret_cast<f32x4*>(E.param) + i, o.a);
+    store4<NT>(reinterpret_cast<f32x4*>(E.param) + i, o.a);
     f32x4* s1 = reinterpret_cast<f32x4*>(E.state1) + i;
     f32x4* s2 = reinterpret_cast<f32x4*>(E.state2) + i;
     f32x4* s3 = reinterpret_cast<f32x4*>(E.state3) + i;
     if constexpr (KIND == FEDAVG_EPI_SGD) {
-        if (E.has_momentum) store4<true>(s1, o.b);
+        if (E.has_momentum) store4<NT>(s1, o.b);
     } else if constexpr (KIND == FEDAVG_EPI_ADAGRAD || KIND == FEDAVG_EPI_ASGD) {
-        store4<true>(s1, o.b);
+        store4<NT>(s1, o.b);
     } else if constexpr (KIND == FEDAVG_EPI_RMSPROP) {
-        store4<true>(s1, o.b);
-        if (E.has_momentum) store4<true>(s2, o.c);
-        if (E.centered) store4<true>(s3, o.d);
+        store4<NT>(s1, o.b);
+        if (E.has_momentum) store4<NT>(s2, o.c);
+        if (E.centered) store4<NT>(s3, o.d);
     } else if constexpr (KIND == FEDAVG_EPI_ADAMAX || KIND == FEDAVG_EPI_RPROP || KIND == FEDAVG_EPI_NADAM ||
                          KIND == FEDAVG_EPI_RADAM) {
-        store4<true>(s1, o.b);
-        store4<true>(s2, o.c);
+        store4<NT>(s1, o.b);
+        store4<NT>(s2, o.c);
     } else {  // ADAM
-        store4<true>(s1, o.b);
-        store4<true>(s2, o.c);
-        if (E.amsgrad) store4<true>(s3, o.d);
+        store4<NT>(s1, o.b);
+        store4<NT>(s2, o.c);
+        if (E.amsgrad) store4<NT>(s3, o.d);
     }
 }
 
@@ -525,6 +535,117 @@ fedavg_tiles_epi_burst_f32x4(const RowTableF32 tab, const int K, const int64_t t
                       });
         if (PF == 1 && !PREFETCH && m + 1 < NT) operands(nxt, m + 1);
         rotate(m);
+    }
+}
+
+// SPLIT-EPILOGUE burst form (round 6; A/B only until measured): the burst form above with a second
+// group of four waves per block (512 threads, one block per CU, two waves per SIMD).  The client phase is the burst
+// form's, run by waves 0-3 alone (waves 4-7 wait at the block barrier holding no loads); in the epilogue phase both groups
+// work at once -- waves 0-3 the register-held tiles and the first XS LDS-held ones, waves 4-7 the other LDS-held tiles
+// (their d is in LDS, readable by any wave after the barrier) -- so the epilogue's optimizer arithmetic issues from two
+// waves per SIMD (a VALU op every 2 cycles instead of every 4) while the other group's operand loads and stores run.
+// Registers: 256 per wave at two waves per SIMD, so TPB register-held tiles are fewer than the burst form's 8.
+// (Waves 4-7 issuing their first tile's operand loads before the barrier keeps 48 more registers live through the
+// client phase: 100-190 bytes of scratch per lane at every geometry. Not done.)
+template <int OP, int FIN, int EPI, int TPB, int TPB_LDS, int XS>
+__global__ void __launch_bounds__(2 * kBlock) __attribute__((amdgpu_waves_per_eu(2, 2)))
+fedavg_tiles_epi_split_f32x4(const RowTableF32 tab, const int K, const int64_t tstride4, f32x4* out, const int64_t b4,
+                             const int64_t e4, const float fin_val, const EpiParams E, const int64_t t0,
+                             const int64_t t_end) {
+    constexpr int CPL = kDefaultTile / (4 * kBlock);
+    constexpr int64_t T4 = (int64_t)CPL * kBlock;
+    constexpr int NT = TPB + TPB_LDS;
+    static_assert(XS >= 0 && XS <= TPB_LDS, "split of the LDS-held tiles");
+    f32x4 dd[TPB][CPL];
+    __shared__ f32x4 staged[TPB_LDS > 0 ? TPB_LDS * CPL * kBlock : 1];
+    const FinConst fc = fin_const<FIN>(fin_val);
+    const EpiConsts C = epi_consts<EPI>(E);
+    if constexpr ((EPI & kEpiTorchSqrt) != 0) rsqrt14_stage();
+    if constexpr ((EPI & kEpiTorchSqrtAmd) != 0) rsqrtps_stage(E.rsqrtps);
+    const bool helper = __builtin_amdgcn_readfirstlane(threadIdx.x) >= kBlock;  // waves 4-7
+    const int tid = threadIdx.x & (kBlock - 1);
+    const int64_t t_base = t0 + blockIdx.x;
+    const int64_t t_cap = t_end - 1;
+    auto operands = [&](EpiIn (&in)[CPL], const int m) __attribute__((always_inline)) {
+        const int64_t t = t_base + (int64_t)m * gridDim.x;
+        const int64_t tc = t < t_cap ? t : t_cap;
+#pragma unroll
+        for (int c = 0; c < CPL; ++c) {
+            int64_t i = tc * T4 + tid + c * kBlock;
+            i = i < b4 ? b4 : (i >= e4 ? e4 - 1 : i);
+            in[c] = epi_load<EPI>(E, i);
+        }
+    };
+    EpiIn cur[CPL], nxt[CPL];
+    if (!helper) {  // the client phase: the burst form's, on waves 0-3
+        auto sum = [&](f32x4 (&acc)[CPL], const int64_t t) __attribute__((always_inline)) {
+            tile_sum_rrem<OP, false, CPL, -1>(acc, tab, K, t * tstride4 + tid, t * T4 + tid, nullptr, b4, e4);
+        };
+#pragma unroll
+        for (int m = 0; m < TPB; ++m) {
+            const int64_t t = t_base + (int64_t)m * gridDim.x;
+            if (t < t_end) {
+                f32x4 acc[CPL];
+                sum(acc, t);
+                fin_tile_em<FIN, kEmBurst, CPL>(dd[m], acc, fc);
+            }
+        }
+#pragma unroll 1
+        for (int m = TPB; m < NT; ++m) {
+            const int64_t t = t_base + (int64_t)m * gridDim.x;
+            if (t < t_end) {
+                f32x4 acc[CPL], r[CPL];
+                sum(acc, t);
+                fin_tile_em<FIN, kEmBurst, CPL>(r, acc, fc);
+#pragma unroll
+                for (int c = 0; c < CPL; ++c) staged[((m - TPB) * CPL + c) * kBlock + tid] = r[c];
+            }
+        }
+    }
+    __syncthreads();  // the LDS-held d visible to every wave
+    auto tile_epilogue = [&](const int64_t t, auto&& d_of) __attribute__((always_inline)) {
+        if (t < t_end) {
+#pragma unroll
+            for (int c = 0; c < CPL; ++c) {
+                const int64_t i = t * T4 + tid + c * kBlock;
+                if (i >= b4 && i < e4) {
+                    const f32x4 d = d_of(c);
+                    if (out != nullptr && (EPI & 0xFF) != FEDAVG_EPI_ADD_BASE) store4<true>(out + i, d);
+                    epilogue4<EPI, kEmBurst>(E, C, i, d, cur[c], out);
+                }
+            }
+        }
+    };
+    auto rotate = [&]() __attribute__((always_inline)) {
+#pragma unroll
+        for (int c = 0; c < CPL; ++c) cur[c] = nxt[c];
+    };
+    auto lds_d = [&](const int m) __attribute__((always_inline)) {
+        return [&, m](int c) __attribute__((always_inline)) { return staged[((m - TPB) * CPL + c) * kBlock + tid]; };
+    };
+    if (!helper) {  // the register-held tiles, then LDS-held tiles TPB .. TPB + XS - 1
+        constexpr int LAST = TPB + XS;
+        operands(cur, 0);
+#pragma unroll
+        for (int m = 0; m < TPB; ++m) {
+            if (m + 1 < LAST) operands(nxt, m + 1);
+            tile_epilogue(t_base + (int64_t)m * gridDim.x, [&](int c) __attribute__((always_inline)) { return dd[m][c]; });
+            rotate();
+        }
+#pragma unroll 1
+        for (int m = TPB; m < LAST; ++m) {
+            if (m + 1 < LAST) operands(nxt, m + 1);
+            tile_epilogue(t_base + (int64_t)m * gridDim.x, lds_d(m));
+            rotate();
+        }
+    } else {  // LDS-held tiles TPB + XS .. NT - 1
+        operands(cur, TPB + XS);
+#pragma unroll 1
+        for (int m = TPB + XS; m < NT; ++m) {
+            if (m + 1 < NT) operands(nxt, m + 1);
+            tile_epilogue(t_base + (int64_t)m * gridDim.x, lds_d(m));
+            rotate();
+        }
     }
 }
 
@@ -895,7 +1016,8 @@ template <int EPI, int KC>
 struct EpiDmaGeom {
     static constexpr bool kAdam = (EPI & 0xFF) == FEDAVG_EPI_ADAM;
     static constexpr int W = kAdam && KC <= 2 ? 8 : 4;
-    static constexpr int N = !kAdam ? 40 : KC == 1 ? 14 : KC == 2 ? 16 : 32;
+    // (SGD with its momentum buffer at 3 reads holds 40 units only with 600+ bytes of scratch per lane: 32 there)
+    static constexpr int N = !kAdam ? (KC == 3 ? 32 : 40) : KC == 1 ? 14 : KC == 2 ? 16 : 32;
     static constexpr bool TDMA = kAdam && KC != 2;
 };
 
@@ -985,12 +1107,52 @@ inline bool epi_loop_ab(const TileLaunch& L, const EpiParams& E, hipStream_t s, 
 // (fedavg_internal.h kAB): the burst form with 4 (two blocks per CU) or 9 (one block per CU) LDS-held tiles without a
 // chained sum, the pipelined per-tile form; A/B builds also the register-only burst form, the burst form over a
 // chained sum, the unpipelined per-tile form and the client-loop shapes.
+template <int OP, int FIN, int EPI, int TPB, int TPB_LDS, int XS>
+inline hipError_t launch_epi_split(const TileLaunch& L, const EpiParams& E, hipStream_t s, uint64_t* nl) {
+    f32x4* o = reinterpret_cast<f32x4*>(L.out);
+    return burst_launches(L.b4 / L.tile4, (L.e4 - 1) / L.tile4 + 1, L.grid, TPB + TPB_LDS, nl,
+                          L.variant & kVariantAnyOrder, [&](int nb, int64_t t0, int64_t t_end, uint32_t flags) {
+                              hipExtLaunchKernelGGL((fedavg_tiles_epi_split_f32x4<OP, FIN, EPI, TPB, TPB_LDS, XS>),
+                                                    dim3(nb), dim3(2 * kBlock), 0, s, nullptr, nullptr, flags, L.tab,
+                                                    L.k, L.tstride4, o, L.b4, L.e4, L.fin_val, E, t0, t_end);
+                          });
+}
+
+// A/B builds with -DFEDAVG_AB_FEW, torch-mode FIN_DIV Adam with the AMD-host sqrt, 4+ reads without a chained sum, one
+// block per CU: launch variant bits 9-11 = 1-5 run the split-epilogue form with (register-held, LDS-held, LDS-held
+// finished by waves 0-3) = (4, 9, 4), (4, 9, 5), (3, 9, 4), (4, 9, 3), (5, 9, 3)
+template <int OP, int FIN, int EPI>
+inline bool epi_split_ab(const TileLaunch& L, const EpiParams& E, hipStream_t s, uint64_t* nl, hipError_t* err) {
+    if constexpr (kABFew && OP == FEDAVG_OP_TORCH && FIN == FEDAVG_FIN_DIV && EPI == (FEDAVG_EPI_ADAM | kEpiTorchSqrtAmd)) {
+        switch ((L.variant >> kVariantLoopShift) & 7) {
+            case 1: *err = launch_epi_split<OP, FIN, EPI, 4, 9, 4>(L, E, s, nl); return true;
+            case 2: *err = launch_epi_split<OP, FIN, EPI, 4, 9, 5>(L, E, s, nl); return true;
+            case 3: *err = launch_epi_split<OP, FIN, EPI, 3, 9, 4>(L, E, s, nl); return true;
+            case 4: *err = launch_epi_split<OP, FIN, EPI, 4, 9, 3>(L, E, s, nl); return true;
+            case 5: *err = launch_epi_split<OP, FIN, EPI, 5, 9, 3>(L, E, s, nl); return true;
+            default: break;
+        }
+    }
+    return false;
+}
+
 template <int OP, int FIN, bool ACC_IN, int EPI>
 inline hipError_t launch_epi_k(const TileLaunch& L, const EpiParams& E, hipStream_t s, uint64_t* nl) {
     const f32x4* ai = reinterpret_cast<const f32x4*>(L.acc_in);
     f32x4* o = reinterpret_cast<f32x4*>(L.out);
     if constexpr (!ACC_IN) {
         if (L.variant & kVariantEpiDma) return launch_epi_dma<OP, FIN, EPI>(L, E, s, nl);
+        if (!(L.variant & (kVariantTileStores | kVariantEpiPrefetch)) && (L.variant & kVariantWideLds)) {
+            if constexpr (kABFew && !kAB) {
+                hipError_t ab_err = hipSuccess;
+                if (epi_split_ab<OP, FIN, EPI>(L, E, s, nl, &ab_err)) return ab_err;
+            }
+            // Adam at one block per CU (64+ clients: config 5): the split-epilogue form (round 6), unless the public
+            // variant asks for the round-5 burst form (kVariantEpiNoSplit)
+            if constexpr ((EPI & 0xFF) == FEDAVG_EPI_ADAM) {
+                if (!(L.variant & kVariantEpiNoSplit)) return launch_epi_split<OP, FIN, EPI, 4, 9, 4>(L, E, s, nl);
+            }
+        }
     }
     if constexpr (kAB || !ACC_IN) {
         if (!(L.variant & (kVariantTileStores | kVariantEpiPrefetch))) {  // burst: one launch per grid x TPB tiles

@@ -60,9 +60,13 @@ constexpr int kVariantEpiDma = 1 << 14;   // inside TileLaunch: the LDS-DMA few-
                                            // fedavg_tiles_epi_dma_f32x4), set by the C-ABI for 1-3 reads, no chained
                                            // sum, kinds ADD_BASE / SGD / Adam without amsgrad; public bit 2 (the
                                            // per-tile pipelined form) keeps the round-5 route for same-process A/Bs
+constexpr int kVariantEpiNoSplit = 1 << 15;  // fused Adam at one block per CU (64+ clients) on round 5's burst form
+                                              // instead of the split-epilogue form (fedavg_epi.h
+                                              // fedavg_tiles_epi_split_f32x4): a product-build A/B switch
 // public variant bits a product build accepts (fedavg_set_variant): the fused per-tile pipelined form (2), burst
-// launches without the barrier bit (16), the 4-LDS-tile form on one-block-per-CU grids (64) -- each a routed form
-constexpr int kVariantProductMask = kVariantEpiPrefetch | kVariantAnyOrder | kVariantWideLds;
+// launches without the barrier bit (16), the 4-LDS-tile form on one-block-per-CU grids (64), the fused burst form
+// without the split epilogue (1 << 15) -- each a routed form
+constexpr int kVariantProductMask = kVariantEpiPrefetch | kVariantAnyOrder | kVariantWideLds | kVariantEpiNoSplit;
 // epilogue template value: the optimizer kind | kEpiTorchSqrt when the step's sqrt is torch CPU's restated AVX-512
 // vsSqrt (EpiParams.torch_sqrt == FEDAVG_SQRT_TORCH_AVX512; fedavg_arith.h sqrt_torch_cpu) | kEpiTorchSqrtAmd for the
 // AMD hosts' path (FEDAVG_SQRT_TORCH_AMD; sqrt_mkl_rsqrtps) -- a compile-time choice, so the correctly rounded path

@@ -32,7 +32,18 @@ def test_no_kernel_uses_scratch(ks):
 
 def test_lds_and_registers_fit_a_cu(ks):
     assert all(k["lds"] <= 160 * 1024 for k in ks)
-    assert all(k["vgpr"] + k["agpr"] <= 512 for k in ks)
+    assert all(k["vgpr"] <= 512 for k in ks)  # .vgpr_count: arch and accumulation VGPRs together on gfx950
     names = [k["name"] for k in ks]
-    for needed in ("fedavg_tiles_burst_f32x4", "fedavg_tiles_epi_burst_f32x4", "fedavg_sqrt_f32"):
+    for needed in ("fedavg_tiles_burst_f32x4", "fedavg_tiles_epi_burst_f32x4", "fedavg_sqrt_f32",
+                   "fedavg_tiles_epi_dma_f32x4", "fedavg_tiles_epi_split_f32x4"):
         assert any(needed in n for n in names), needed
+
+
+def test_two_wave_per_simd_kernels_fit_256_registers(ks):
+    """The 512-thread kernels (two waves per SIMD, one block per CU: the split-epilogue form, the LDS-DMA form at W = 8)
+    get 256 registers per wave, arch and accumulation VGPRs together; more would not fit the block on a CU."""
+    wide = [k for k in ks if "fedavg_tiles_epi_split_f32x4" in k["name"] or
+            ("fedavg_tiles_epi_dma_f32x4" in k["name"] and "Li8EEEv" in k["name"])]  # mangled: W = 8 is the last arg
+    assert wide, "no 512-thread kernel found"
+    bad = [(k["name"], k["vgpr"], k["agpr"]) for k in wide if k["vgpr"] > 256]
+    assert not bad, bad[:5]

@@ -91,10 +91,10 @@ class _Case:
 
 def _tiles_per_block(kind, K):
     """Tiles per block per launch of the product geometry (fedavg_epi.h EpiDmaGeom: N units per wave x W waves / 16):
-    Adam 1 / 2 clients 8 waves x 14 / 16 units, 3 clients 4 waves x 32; ADD_BASE / SGD 4 waves x 40."""
+    Adam 1 / 2 clients 8 waves x 14 / 16 units, 3 clients 4 waves x 32; ADD_BASE / SGD 4 waves x 40 (x 32 at 3)."""
     if kind == 3:
         return {1: 7, 2: 8, 3: 8}[K]
-    return 10
+    return 8 if K == 3 else 10
 
 
 def _launches(ctx, begin, end, kind=3, K=2):

@@ -591,11 +591,12 @@ def test_few_client_fused_every_kind(ctx, oracle, K, case):
             ctx.accumulate_tiled_epi(dev.bases, ws, TILE, dev.lay.tile_stride, 0, dev.n4, out, N_.FEDAVG_OP_TORCH,
                                      N_.FEDAVG_FIN_DIV, _sum(ws), e)
             ctx.sync()
-            # ADD_BASE and SGD take the LDS-DMA few-client form (round 6): one launch per num_cus x 10 tiles; the other
+            # ADD_BASE and SGD take the LDS-DMA few-client form (round 6): one launch per num_cus x 10 (8) tiles; the other
             # kinds, amsgrad and a requested aggregate output the per-tile form: one persistent launch
             tiles = (dev.n4 - 1) // TILE + 1
             dma = kind in (1, 2)
-            assert ctx.launch_count() - n_launch == (-(-tiles // (min(ctx.num_cus, tiles) * 10)) if dma else 1)
+            tpb = 8 if K == 3 else 10  # fedavg_epi.h EpiDmaGeom: 4 waves x 40 units (x 32 at 3 reads)
+            assert ctx.launch_count() - n_launch == (-(-tiles // (min(ctx.num_cus, tiles) * tpb)) if dma else 1)
             d = oracle.fedavg_c(rows, ws, oracle.MODE_TORCH, nthreads=8)
             if kind == 1:
                 assert same_bits(dev.get("out"), oracle.epilogue_apply(d, oracle.EPI_ADD_BASE, base=base)), step

@@ -1,6 +1,8 @@
 """The fused burst kernel's launch forms at one block per CU (64+ clients), bit-exact against the oracle over
-more tiles than one launch holds (two launches, the second partial, ragged end): the default form (8 register-
-+ 9 LDS-held tiles per block, round 3), the 4-LDS-tile form (variant bit 6) and the register-only form (bit 5; A/B builds),
+more tiles than one launch holds (two launches, the second partial, ragged end): the default form for Adam (round 6:
+the split epilogue, fedavg_tiles_epi_split_f32x4 -- 4 register- + 9 LDS-held tiles per block, waves 4-7 joining the
+epilogue), round 5's burst form (variant bit 15; 8 register- + 9 LDS-held tiles, round 3), the 4-LDS-tile form (variant
+bit 6) and the register-only form (bit 5; A/B builds),
 with the correctly rounded and both restated torch-CPU sqrts (each stages its table in the same LDS: the Intel
 hosts' 512-byte segments, the AMD hosts' 16 KiB RSQRTPS table -- 160 KiB in all at one block per CU).  64 and 70 clients read 4 distinct uploaded rows cyclically (the kernel sees 64 / 70 row pointers; the
 oracle the same list), which keeps the host side small at 18 M elements per row."""
@@ -30,7 +32,7 @@ def rows():
 
 
 @pytest.mark.parametrize("torch_sqrt", [0, 1, 2])
-@pytest.mark.parametrize("variant", [0, 64, 32])
+@pytest.mark.parametrize("variant", [0, 1 << 15, 64, 32])
 @pytest.mark.parametrize("K", [64, 70])
 def test_fused_adam_launch_forms(ctx, oracle, rows, K, variant, torch_sqrt):
     from nvflare_amd import _native as N_
@@ -79,7 +81,9 @@ def test_fused_adam_launch_forms(ctx, oracle, rows, K, variant, torch_sqrt):
         for b in bufs:
             b.close()
     tiles = (N + TILE - 1) // TILE
-    per_launch = ctx.num_cus * (8 + {0: 9, 64: 4, 32: 0}[variant])
+    # variant 0: the split-epilogue form (round 6: 4 register- + 9 LDS-held tiles, 8 waves per block); 1 << 15: round 5's
+    # burst form (8 + 9); 64: the 4-LDS-tile form; 32: register-held tiles only (A/B builds)
+    per_launch = ctx.num_cus * {0: 4 + 9, 1 << 15: 8 + 9, 64: 8 + 4, 32: 8}[variant]
     assert launches == -(-tiles // per_launch)  # the form that ran is the one asked for
     d = oracle.fedavg_c([rows[k % len(rows)] for k in range(K)], ws, oracle.MODE_TORCH, nthreads=8)
     oracle.epilogue_apply(d, oracle.EPI_ADAM, p=p, m=m, v=v, step=2.0, lr=1e-3, beta1=0.9, beta2=0.999, eps=1e-8,
