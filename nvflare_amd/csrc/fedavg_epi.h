@@ -1012,12 +1012,20 @@ inline hipError_t launch_epi_dma_n(const TileLaunch& L, const EpiParams& E, hipS
 // 78.9 / 77.1, ADD_BASE 75.4 / 75.3 / 77.3 (N = 32: 77.4 / 78.9 / 77.5, 72.8 / 75.2 / 76.3; N = 16: 69.1 / 75.0 / 75.7,
 // 67.3 / 71.3 / 72.3; W = 8, N = 16: 75.9 / 74.3 / 74.7, 72.9 / 75.0 / 74.3) -- lighter arithmetic, fewer result
 // registers per unit (8 and 4): one wave per SIMD keeps up, and 40 units fit its registers.
+// The other kinds (round 6, later): the ones with a sqrt per element (NAdam, RAdam, Adagrad) take Adam's geometry, the
+// lighter ones (Adamax, Rprop, ASGD) SGD's.
 template <int EPI, int KC>
 struct EpiDmaGeom {
-    static constexpr bool kAdam = (EPI & 0xFF) == FEDAVG_EPI_ADAM;
+    static constexpr int KIND = EPI & 0xFF;
+    // the sqrt + division kinds: two waves per SIMD at 1-2 reads (Adagrad on SGD's 4 x 40 / 32 ran 48.6 / 57.2 / 63.6 %
+    // against 66.3 / 72.7 / 70.6 % here: profiles/r06/s16/, s15/)
+    static constexpr bool kAdam = KIND == FEDAVG_EPI_ADAM || KIND == FEDAVG_EPI_NADAM || KIND == FEDAVG_EPI_RADAM ||
+                                  KIND == FEDAVG_EPI_ADAGRAD;
+    static constexpr bool kThree = KIND == FEDAVG_EPI_ADAMAX || KIND == FEDAVG_EPI_RPROP;  // light, three streams
     static constexpr int W = kAdam && KC <= 2 ? 8 : 4;
-    // (SGD with its momentum buffer at 3 reads holds 40 units only with 600+ bytes of scratch per lane: 32 there)
-    static constexpr int N = !kAdam ? (KC == 3 ? 32 : 40) : KC == 1 ? 14 : KC == 2 ? 16 : 32;
+    // (SGD with its momentum buffer at 3 reads holds 40 units only with 600+ bytes of scratch per lane: 32 there; Adamax
+    // and Rprop hold three result streams per unit: 24)
+    static constexpr int N = kThree ? 24 : !kAdam ? (KC == 3 ? 32 : 40) : KC == 1 ? 14 : KC == 2 ? 16 : 32;
     static constexpr bool TDMA = kAdam && KC != 2;
 };
 
@@ -1052,8 +1060,11 @@ inline hipError_t launch_epi_dma_k(const TileLaunch& L, const EpiParams& E, hipS
     } else if constexpr (KIND == FEDAVG_EPI_SGD) {
         if (nin == 1) return launch_epi_dma_form<OP, FIN, EPI, KC, 1>(L, E, s, nl);
         if (nin == 2) return launch_epi_dma_form<OP, FIN, EPI, KC, 2>(L, E, s, nl);
-    } else if constexpr (KIND == FEDAVG_EPI_ADAM) {
+    } else if constexpr (KIND == FEDAVG_EPI_ADAM || KIND == FEDAVG_EPI_NADAM || KIND == FEDAVG_EPI_RADAM ||
+                         KIND == FEDAVG_EPI_ADAMAX || KIND == FEDAVG_EPI_RPROP) {
         if (nin == 3) return launch_epi_dma_form<OP, FIN, EPI, KC, 3>(L, E, s, nl);
+    } else if constexpr (KIND == FEDAVG_EPI_ADAGRAD || KIND == FEDAVG_EPI_ASGD) {
+        if (nin == 2) return launch_epi_dma_form<OP, FIN, EPI, KC, 2>(L, E, s, nl);
     }
     return hipErrorInvalidValue;
 }
@@ -1061,7 +1072,7 @@ inline hipError_t launch_epi_dma_k(const TileLaunch& L, const EpiParams& E, hipS
 template <int OP, int FIN, int EPI>
 inline hipError_t launch_epi_dma(const TileLaunch& L, const EpiParams& E, hipStream_t s, uint64_t* nl) {
     constexpr int KIND = EPI & 0xFF;
-    if constexpr (KIND == FEDAVG_EPI_ADD_BASE || KIND == FEDAVG_EPI_SGD || KIND == FEDAVG_EPI_ADAM) {
+    if constexpr (KIND != FEDAVG_EPI_RMSPROP) {
         switch (L.k) {
             case 1: return launch_epi_dma_k<OP, FIN, EPI, 1>(L, E, s, nl);
             case 2: return launch_epi_dma_k<OP, FIN, EPI, 2>(L, E, s, nl);

@@ -18,8 +18,28 @@ sys.path[:0] = [ROOT, os.path.join(ROOT, "tests")]
 from bench_fake_rank import install, small_presets  # noqa: E402
 
 
+@pytest.fixture
+def undo_install(monkeypatch):
+    """install() patches bench, torch.cuda and DeviceContext for the whole process: have monkeypatch put every one back
+    after the test (other tests in this process parse bench's real presets)."""
+    import torch
+
+    import bench
+    from nvflare_amd import device as device_mod
+
+    monkeypatch.setattr(bench, "PRESETS", dict(bench.PRESETS))
+    for name in ("dist_setup", "make_host_helper", "run_client_sharded"):
+        monkeypatch.setattr(bench, name, getattr(bench, name))
+    for name in ("synchronize", "empty_cache"):
+        monkeypatch.setattr(torch.cuda, name, getattr(torch.cuda, name))
+    monkeypatch.setattr(device_mod.DeviceContext, "get", device_mod.DeviceContext.__dict__["get"])
+    threads = torch.get_num_threads()  # install() runs torch on one thread
+    yield
+    torch.set_num_threads(threads)
+
+
 @pytest.mark.timeout(300)
-def test_default_run_at_one_gpu(monkeypatch):
+def test_default_run_at_one_gpu(monkeypatch, undo_install):
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
         monkeypatch.delenv(k, raising=False)
     bench = install(0, 1)

@@ -536,6 +536,17 @@ FEW_CASES = [  # (kind, hp, state names): every optimizer kind through the few-c
 ]
 
 
+def _dma_tiles_per_block(kind, K):
+    """Tiles per block per launch of the LDS-DMA form (fedavg_epi.h EpiDmaGeom, N units per wave x W waves / 16): the
+    Adam family and Adagrad 8 waves x 16 units at 2 reads, 4 x 32 at 3; Adamax / Rprop 4 x 24; the rest 4 x 40
+    (x 32 at 3 reads)."""
+    if kind in (3, 4, 7, 8):
+        return 8
+    if kind in (6, 9):
+        return 6
+    return 8 if K == 3 else 10
+
+
 @pytest.mark.parametrize("K", [2, 3])
 @pytest.mark.parametrize("case", range(len(FEW_CASES)))
 def test_few_client_fused_every_kind(ctx, oracle, K, case):
@@ -591,11 +602,11 @@ def test_few_client_fused_every_kind(ctx, oracle, K, case):
             ctx.accumulate_tiled_epi(dev.bases, ws, TILE, dev.lay.tile_stride, 0, dev.n4, out, N_.FEDAVG_OP_TORCH,
                                      N_.FEDAVG_FIN_DIV, _sum(ws), e)
             ctx.sync()
-            # ADD_BASE and SGD take the LDS-DMA few-client form (round 6): one launch per num_cus x 10 (8) tiles; the other
-            # kinds, amsgrad and a requested aggregate output the per-tile form: one persistent launch
+            # Every kind but RMSprop takes the LDS-DMA few-client form (round 6) unless it asks for amsgrad or an aggregate
+            # output: one launch per num_cus x tiles-per-block tiles; the rest the per-tile form: one persistent launch
             tiles = (dev.n4 - 1) // TILE + 1
-            dma = kind in (1, 2)
-            tpb = 8 if K == 3 else 10  # fedavg_epi.h EpiDmaGeom: 4 waves x 40 units (x 32 at 3 reads)
+            dma = kind != 5 and (out is None or kind == 1) and not hp.get("amsgrad")
+            tpb = _dma_tiles_per_block(kind, K)
             assert ctx.launch_count() - n_launch == (-(-tiles // (min(ctx.num_cus, tiles) * tpb)) if dma else 1)
             d = oracle.fedavg_c(rows, ws, oracle.MODE_TORCH, nthreads=8)
             if kind == 1:

@@ -15,7 +15,9 @@ import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
-EXTRA = {"none": 4.0, "add_base": 8.0, "sgd": 16.0, "adam": 24.0}  # algorithmic bytes per param beyond 4K
+EXTRA = {"none": 4.0, "add_base": 8.0, "sgd": 16.0, "adam": 24.0, "adagrad": 16.0, "adamax": 24.0, "nadam": 24.0,
+         "radam": 24.0, "rprop": 24.0, "asgd": 16.0}
+TWO_STATES = ("adam", "adamax", "nadam", "radam", "rprop")  # algorithmic bytes per param beyond 4K
 
 
 def main():
@@ -74,7 +76,9 @@ def main():
         ctx.memset(b.ptr, 0, end * 4 + max(shifts))
     out = ctx.alloc(end * 4)
     ctx.sync()
-    kinds = {"add_base": N.FEDAVG_EPI_ADD_BASE, "sgd": N.FEDAVG_EPI_SGD, "adam": N.FEDAVG_EPI_ADAM}
+    kinds = {"add_base": N.FEDAVG_EPI_ADD_BASE, "sgd": N.FEDAVG_EPI_SGD, "adam": N.FEDAVG_EPI_ADAM,
+             "adagrad": N.FEDAVG_EPI_ADAGRAD, "adamax": N.FEDAVG_EPI_ADAMAX, "nadam": N.FEDAVG_EPI_NADAM,
+             "radam": N.FEDAVG_EPI_RADAM, "rprop": N.FEDAVG_EPI_RPROP, "asgd": N.FEDAVG_EPI_ASGD}
 
     def launcher(epi, pad, sh=0):
         _, bases, stride = slabs[pad]
@@ -83,12 +87,16 @@ def main():
         e = N.Epilogue()
         e.kind = kinds[epi]
         e.lr, e.momentum, e.beta1, e.beta2, e.eps, e.step = 1e-3, 0.9, 0.9, 0.999, 1e-8, 1.0
+        e.etaminus, e.etaplus, e.step_size_min, e.step_size_max = 0.5, 1.2, 1e-6, 50.0
+        e.lambd, e.eta, e.mu = 1e-4, 1e-2, 0.5
         e.torch_sqrt = {"ieee": N.FEDAVG_SQRT_IEEE, "torch_cpu": N.FEDAVG_SQRT_TORCH_AVX512,
                         "torch_cpu_amd": N.FEDAVG_SQRT_TORCH_AMD}[a.sqrt]
         if epi == "add_base":
             e.base, o = bufs[0].ptr + sh, out.ptr
         else:
-            e.param, e.state1, e.state2 = bufs[0].ptr + sh, bufs[1].ptr + sh, bufs[2].ptr + sh
+            e.param, e.state1 = bufs[0].ptr + sh, bufs[1].ptr + sh
+            if epi in TWO_STATES or epi == "sgd":
+                e.state2 = bufs[2].ptr + sh
             o = None
         return lambda: ctx.accumulate_tiled_epi(bases, ws, lay.tile, stride, 0, end, o, op, fin, cnt, e)
 
@@ -127,7 +135,7 @@ def main():
                     ctx.d2h(host, out.ptr if epi in ("none", "add_base") else bufs[0].ptr + shifts[0])
                     if epi not in ("none", "add_base"):
                         last = np.empty(end, dtype=np.float32)
-                        ctx.d2h(last, bufs[2 if epi == "adam" else 1].ptr + shifts[0])
+                        ctx.d2h(last, bufs[2 if epi in TWO_STATES else 1].ptr + shifts[0])
                         host = np.concatenate([host, last])
                     if epi not in ref_out:
                         ref_out[epi] = host
