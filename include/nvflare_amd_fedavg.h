@@ -341,9 +341,10 @@ int fedavg_set_launch(fedavg_ctx* ctx, int blocks_per_cu, int unroll);
  * burst form (round 5): every register-held tile's loads go out before any arithmetic, the results are stored as a
  * burst; a chained sum with fewer than 3 reads runs the PER-TILE-STORE form, which stores each tile's results as it
  * finishes.  The fused kernel with 1-3 client reads, no chained sum and no separate aggregate output (out only for
- * ADD_BASE) runs its LDS-DMA few-client form (round 6) for every kind but RMSprop (Adam without amsgrad): every input
- * goes HBM -> LDS by LDS-DMA while the wave computes the units already landed, the results are held on chip and stored
- * as a burst; RMSprop, amsgrad and chained sums under 4 reads run its per-tile form pipelined across tiles.  Every load
+ * ADD_BASE) runs its LDS-DMA few-client form (round 6) for every kind (Adam without amsgrad, RMSprop not centered):
+ * every input goes HBM -> LDS by LDS-DMA while the wave computes the units already landed, the results are held on chip
+ * and stored as a burst; amsgrad, centered RMSprop and chained sums under 4 reads run its per-tile form pipelined across
+ * tiles.  Every load
  * and store is
  * nontemporal.  The 16-bit and fp64 tile kernels (fedavg_accumulate_tiled16 / _tiled64) likewise run 1-3 client
  * reads without a chained sum on their few-client burst forms, the rest on their burst forms.  The plain burst kernel has the launch's client count

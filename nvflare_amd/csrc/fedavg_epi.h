@@ -874,13 +874,20 @@ fedavg_tiles_epi_dma_f32x4(const RowTableF32 tab, const int64_t tstride4, f32x4*
     static_assert(W == 4 || W == 8, "4 or 8 waves per block");
     constexpr int CPT = 64 / (4 * W);       // float4 columns per lane per tile (4 at W = 4, 2 at W = 8)
     constexpr int64_t T4 = kDefaultTile / 4;  // float4 per tile; a tile is 16 wave pieces of 64 float4
-    constexpr int NOUT = epi_nout<EPI>();
+    constexpr int KIND = EPI & 0xFF;
+    // RMSprop on this form: not centered, its momentum buffer read iff NIN == 3 -- results p, square_avg (, buffer)
+    constexpr int NOUT = KIND == FEDAVG_EPI_RMSPROP ? NIN : epi_nout<EPI>();
     static_assert(KC >= 1 && KC <= 3 && NIN >= 1 && NIN <= 3 && NOUT <= G, "few-client fused form");
+    static_assert(KIND != FEDAVG_EPI_RMSPROP || NIN >= 2, "RMSprop reads p and square_avg");
     static_assert(S >= 1 && S <= N && (S - 1) * G <= 63 && N % CPT == 0, "ring geometry");
     static_assert((int64_t)W * S * G * 1024 <= epi_dma_ring_bytes<EPI>(), "ring fits the CU's LDS");
     __shared__ f32x4 ring[W][S][G][64];
     EpiParams E = E_;
-    if constexpr ((EPI & 0xFF) == FEDAVG_EPI_ADAM) E.amsgrad = 0;  // amsgrad runs the per-tile form (4 operand streams)
+    if constexpr (KIND == FEDAVG_EPI_ADAM) E.amsgrad = 0;  // amsgrad runs the per-tile form (4 operand streams)
+    if constexpr (KIND == FEDAVG_EPI_RMSPROP) {  // centered runs the per-tile form; NIN says whether momentum is on
+        E.centered = 0;
+        E.has_momentum = NIN == 3;
+    }
     const FinConst fc = fin_const<FIN>(fin_val);
     const EpiConsts C = epi_consts<EPI>(E);
     constexpr bool kTableDma = TDMA && (EPI & kEpiTorchSqrtAmd) != 0;
@@ -1012,20 +1019,26 @@ inline hipError_t launch_epi_dma_n(const TileLaunch& L, const EpiParams& E, hipS
 // 78.9 / 77.1, ADD_BASE 75.4 / 75.3 / 77.3 (N = 32: 77.4 / 78.9 / 77.5, 72.8 / 75.2 / 76.3; N = 16: 69.1 / 75.0 / 75.7,
 // 67.3 / 71.3 / 72.3; W = 8, N = 16: 75.9 / 74.3 / 74.7, 72.9 / 75.0 / 74.3) -- lighter arithmetic, fewer result
 // registers per unit (8 and 4): one wave per SIMD keeps up, and 40 units fit its registers.
-// The other kinds (round 6, later): the ones with a sqrt per element (NAdam, RAdam, Adagrad) take Adam's geometry, the
-// lighter ones (Adamax, Rprop, ASGD) SGD's.
-template <int EPI, int KC>
+// The other kinds (round 6, later): the ones with a sqrt and a division per element (NAdam, RAdam, Adagrad, RMSprop)
+// take Adam's geometry; Adamax and Rprop 4 waves x 24 units (three result streams per unit: 32 and 40 spill), ASGD SGD's.
+template <int EPI, int KC, int NIN>
 struct EpiDmaGeom {
     static constexpr int KIND = EPI & 0xFF;
     // the sqrt + division kinds: two waves per SIMD at 1-2 reads (Adagrad on SGD's 4 x 40 / 32 ran 48.6 / 57.2 / 63.6 %
     // against 66.3 / 72.7 / 70.6 % here: profiles/r06/s16/, s15/)
     static constexpr bool kAdam = KIND == FEDAVG_EPI_ADAM || KIND == FEDAVG_EPI_NADAM || KIND == FEDAVG_EPI_RADAM ||
-                                  KIND == FEDAVG_EPI_ADAGRAD;
+                                  KIND == FEDAVG_EPI_ADAGRAD || KIND == FEDAVG_EPI_RMSPROP;
     static constexpr bool kThree = KIND == FEDAVG_EPI_ADAMAX || KIND == FEDAVG_EPI_RPROP;  // light, three streams
     static constexpr int W = kAdam && KC <= 2 ? 8 : 4;
     // (SGD with its momentum buffer at 3 reads holds 40 units only with 600+ bytes of scratch per lane: 32 there; Adamax
     // and Rprop hold three result streams per unit: 24)
-    static constexpr int N = kThree ? 24 : !kAdam ? (KC == 3 ? 32 : 40) : KC == 1 ? 14 : KC == 2 ? 16 : 32;
+    // (RMSprop with its momentum buffer, IEEE sqrt: 14 / 24 units at 2 / 3 reads, 16 / 32 spill)
+    static constexpr bool kRmsMom = KIND == FEDAVG_EPI_RMSPROP && NIN == 3;
+    static constexpr int N = kThree ? 24
+                             : !kAdam ? (KC == 3 ? 32 : 40)
+                             : KC == 1 ? 14
+                             : KC == 2 ? (kRmsMom ? 14 : 16)
+                                       : (kRmsMom ? 24 : 32);
     static constexpr bool TDMA = kAdam && KC != 2;
 };
 
@@ -1047,7 +1060,7 @@ inline hipError_t launch_epi_dma_form(const TileLaunch& L, const EpiParams& E, h
             default: break;
         }
     }
-    using Geom = EpiDmaGeom<EPI, KC>;
+    using Geom = EpiDmaGeom<EPI, KC, NIN>;
     return launch_epi_dma_n<OP, FIN, EPI, KC, NIN, Geom::N, Geom::TDMA, kEmFast, Geom::W>(L, E, s, nl);
 }
 
@@ -1065,22 +1078,21 @@ inline hipError_t launch_epi_dma_k(const TileLaunch& L, const EpiParams& E, hipS
         if (nin == 3) return launch_epi_dma_form<OP, FIN, EPI, KC, 3>(L, E, s, nl);
     } else if constexpr (KIND == FEDAVG_EPI_ADAGRAD || KIND == FEDAVG_EPI_ASGD) {
         if (nin == 2) return launch_epi_dma_form<OP, FIN, EPI, KC, 2>(L, E, s, nl);
+    } else if constexpr (KIND == FEDAVG_EPI_RMSPROP) {
+        if (nin == 2) return launch_epi_dma_form<OP, FIN, EPI, KC, 2>(L, E, s, nl);
+        if (nin == 3) return launch_epi_dma_form<OP, FIN, EPI, KC, 3>(L, E, s, nl);
     }
     return hipErrorInvalidValue;
 }
 
 template <int OP, int FIN, int EPI>
 inline hipError_t launch_epi_dma(const TileLaunch& L, const EpiParams& E, hipStream_t s, uint64_t* nl) {
-    constexpr int KIND = EPI & 0xFF;
-    if constexpr (KIND != FEDAVG_EPI_RMSPROP) {
-        switch (L.k) {
-            case 1: return launch_epi_dma_k<OP, FIN, EPI, 1>(L, E, s, nl);
-            case 2: return launch_epi_dma_k<OP, FIN, EPI, 2>(L, E, s, nl);
-            case 3: return launch_epi_dma_k<OP, FIN, EPI, 3>(L, E, s, nl);
-            default: break;
-        }
+    switch (L.k) {
+        case 1: return launch_epi_dma_k<OP, FIN, EPI, 1>(L, E, s, nl);
+        case 2: return launch_epi_dma_k<OP, FIN, EPI, 2>(L, E, s, nl);
+        case 3: return launch_epi_dma_k<OP, FIN, EPI, 3>(L, E, s, nl);
+        default: return hipErrorInvalidValue;
     }
-    return hipErrorInvalidValue;
 }
 
 // A/B of the burst kernel's client loop (launch variant bits 9-11 = LOOP 1-4), instantiated for one configuration only:

@@ -58,7 +58,7 @@ constexpr int kVariantFew = 1 << 12;      // inside TileLaunch: the few-client b
                                            // fedavg_tiles_few_f32x4), set by run_tiles for 1-2 reads, no chained sum
 constexpr int kVariantEpiDma = 1 << 14;   // inside TileLaunch: the LDS-DMA few-client fused form (fedavg_epi.h
                                            // fedavg_tiles_epi_dma_f32x4), set by the C-ABI for 1-3 reads, no chained
-                                           // sum, every kind but RMSprop (Adam without amsgrad); public bit 2 (the
+                                           // sum, every kind (Adam without amsgrad, RMSprop not centered); public bit 2 (the
                                            // per-tile pipelined form) keeps the round-5 route for same-process A/Bs
 constexpr int kVariantEpiNoSplit = 1 << 15;  // fused Adam at one block per CU (64+ clients) on round 5's burst form
                                               // instead of the split-epilogue form (fedavg_epi.h
@@ -150,7 +150,8 @@ inline int epi_dma_nin(const EpiParams& E) {
         case FEDAVG_EPI_RPROP: return 3;  // p and two states
         case FEDAVG_EPI_ADAGRAD:
         case FEDAVG_EPI_ASGD: return 2;  // p and one state
-        default: return 0;  // RMSprop: its states depend on momentum / centered -- the per-tile form
+        case FEDAVG_EPI_RMSPROP: return E.centered ? 0 : E.has_momentum ? 3 : 2;  // centered: a 4th stream, per-tile
+        default: return 0;
     }
 }
 

@@ -1,6 +1,6 @@
 """GPU parity of the LDS-DMA few-client fused form (round 6, fedavg_epi.h fedavg_tiles_epi_dma_f32x4): 1-3 client reads
 with a server-optimizer epilogue -- WEIGHT_DIFF apply (ADD_BASE), SGD (momentum buffer read or not), Adam (every sqrt
-the epilogue knows) and the other kinds but RMSprop -- bit for bit against the oracle AND against the round-5 per-tile form (public variant bit 2, same
+the epilogue knows) and the other kinds (RMSprop not centered) -- bit for bit against the oracle AND against the round-5 per-tile form (public variant bit 2, same
 process), over the shapes the kernel's indexing has to get right: less than one tile, a range that starts and ends
 inside a tile, operand buffers that exist only on [begin, end), more tiles than one launch, ragged last launches.
 Reference arithmetic: weighted_aggregation_helper.py:181-236 then app_opt/pt/fedopt.py:157-182 (torch's single-tensor
@@ -89,20 +89,22 @@ class _Case:
             b.close()
 
 
-def _tiles_per_block(kind, K):
+def _tiles_per_block(kind, K, rms_momentum=False):
     """Tiles per block per launch of the product geometry (fedavg_epi.h EpiDmaGeom: N units per wave x W waves / 16):
-    Adam / NAdam / RAdam / Adagrad 1 / 2 clients 8 waves x 14 / 16 units, 3 clients 4 waves x 32; Adamax / Rprop 4
-    waves x 24; ADD_BASE / SGD / ASGD 4 waves x 40 (x 32 at 3)."""
-    if kind in (3, 4, 7, 8):
+    Adam / NAdam / RAdam / Adagrad / RMSprop 1 / 2 clients 8 waves x 14 / 16 units, 3 clients 4 waves x 32 (RMSprop
+    with momentum 14 / 14 / 24); Adamax / Rprop 4 waves x 24; ADD_BASE / SGD / ASGD 4 waves x 40 (x 32 at 3)."""
+    if kind == 5 and rms_momentum:
+        return {1: 7, 2: 7, 3: 6}[K]
+    if kind in (3, 4, 5, 7, 8):
         return {1: 7, 2: 8, 3: 8}[K]
     if kind in (6, 9):
         return 6
     return 8 if K == 3 else 10
 
 
-def _launches(ctx, begin, end, kind=3, K=2):
+def _launches(ctx, begin, end, kind=3, K=2, rms_momentum=False):
     t_first, t_stop = begin // TILE, (end - 1) // TILE + 1
-    per = min(ctx.num_cus, t_stop - t_first) * _tiles_per_block(kind, K)  # one block per CU
+    per = min(ctx.num_cus, t_stop - t_first) * _tiles_per_block(kind, K, rms_momentum)  # one block per CU
     return -(-(t_stop - t_first) // per)
 
 
@@ -213,28 +215,30 @@ def test_dma_add_base(ctx, oracle, K, rng_ix, op, fin):
         c.close()
 
 
-OTHER_KINDS = {  # kind: (hyper-parameters, state names, restated AMD-host sqrt)
-    4: (dict(lr=1e-2, weight_decay=1e-3, eps=1e-8, maximize=1), ("m",), True),  # Adagrad
-    6: (dict(lr=1e-2, beta1=0.8, beta2=0.95, eps=1e-6, weight_decay=1e-3), ("m", "v"), False),  # Adamax
-    7: (dict(lr=2e-3, beta1=0.9, beta2=0.999, eps=1e-8, momentum_decay=4e-3), ("m", "v"), True),  # NAdam
-    8: (dict(lr=1e-2, beta1=0.8, beta2=0.9, eps=1e-8, weight_decay=1e-3), ("m", "v"), True),  # RAdam
-    9: (dict(etaminus=0.5, etaplus=1.2, step_size_min=1e-6, step_size_max=50.0), ("m", "v"), False),  # Rprop
-    10: (dict(lambd=1e-4, eta=1e-2, mu=0.5, weight_decay=1e-3), ("m",), False),  # ASGD
-}
+OTHER_KINDS = [  # (kind, hyper-parameters, state names, restated AMD-host sqrt)
+    (4, dict(lr=1e-2, weight_decay=1e-3, eps=1e-8, maximize=1), ("m",), True),  # Adagrad
+    (5, dict(lr=1e-3, alpha=0.95, eps=1e-8, weight_decay=1e-3), ("m",), True),  # RMSprop: square_avg
+    (5, dict(lr=1e-3, alpha=0.9, eps=1e-6, momentum=0.5, maximize=1), ("m", "v"), False),  # + momentum buffer
+    (6, dict(lr=1e-2, beta1=0.8, beta2=0.95, eps=1e-6, weight_decay=1e-3), ("m", "v"), False),  # Adamax
+    (7, dict(lr=2e-3, beta1=0.9, beta2=0.999, eps=1e-8, momentum_decay=4e-3), ("m", "v"), True),  # NAdam
+    (8, dict(lr=1e-2, beta1=0.8, beta2=0.9, eps=1e-8, weight_decay=1e-3), ("m", "v"), True),  # RAdam
+    (9, dict(etaminus=0.5, etaplus=1.2, step_size_min=1e-6, step_size_max=50.0), ("m", "v"), False),  # Rprop
+    (10, dict(lambd=1e-4, eta=1e-2, mu=0.5, weight_decay=1e-3), ("m",), False),  # ASGD
+]
 
 
 @pytest.mark.parametrize("K", [1, 2, 3])
 @pytest.mark.parametrize("rng_ix", [2, 4])
-@pytest.mark.parametrize("kind", sorted(OTHER_KINDS))
-def test_dma_other_kinds(ctx, oracle, K, rng_ix, kind):
-    """The rest of the server optimizers on the LDS-DMA form (every kind but RMSprop, whose operand streams depend on
-    momentum / centered): two steps from non-zero states (RAdam's second on its rectified branch), every output and
-    state bit for bit against the oracle and against the per-tile form (public variant bit 2) on the same inputs."""
+@pytest.mark.parametrize("case", range(len(OTHER_KINDS)))
+def test_dma_other_kinds(ctx, oracle, K, rng_ix, case):
+    """The rest of the server optimizers on the LDS-DMA form (RMSprop not centered: with its momentum buffer or
+    without): two steps from non-zero states (RAdam's second on its rectified branch), every output and state bit for
+    bit against the oracle and against the per-tile form (public variant bit 2) on the same inputs."""
     from nvflare_amd import _native as N
 
-    hp, names, amd_sqrt = OTHER_KINDS[kind]
+    kind, hp, names, amd_sqrt = OTHER_KINDS[case]
     begin, end = _ranges(ctx)[rng_ix]
-    c = _Case(ctx, K, begin, end, seed=4000 + 100 * kind + 10 * rng_ix + K)
+    c = _Case(ctx, K, begin, end, seed=4000 + 100 * case + 10 * rng_ix + K)
     try:
         n = c.n
         p = c.rng.standard_normal(n).astype(np.float32)
@@ -242,6 +246,8 @@ def test_dma_other_kinds(ctx, oracle, K, rng_ix, kind):
               "v": (c.rng.random(n) * 1e-4 + 1e-6).astype(np.float32)}
         if kind == 4:  # Adagrad: a positive sum
             st["m"] = np.abs(st["m"]) + np.float32(0.1)
+        if kind == 5:  # RMSprop: square_avg, the momentum buffer
+            st["m"], st["v"] = (c.rng.random(n) * 1e-2 + 1e-3).astype(np.float32), st["m"]
         if kind == 9:  # Rprop: step sizes
             st["v"] = np.full(n, 0.01, np.float32)
         if kind == 10:  # ASGD: ax
@@ -257,7 +263,7 @@ def test_dma_other_kinds(ctx, oracle, K, rng_ix, kind):
                     kw[field] = c.buf(nm, st[nm])
                 nl = _run(ctx, c, _epi(kind, **kw), N.FEDAVG_OP_TORCH, N.FEDAVG_FIN_DIV, variant=variant)
                 if variant == 0:
-                    assert nl == _launches(ctx, begin, end, kind, K)
+                    assert nl == _launches(ctx, begin, end, kind, K, rms_momentum=len(names) == 2)
                 got[variant] = [c.get(x) for x in ("p",) + names]
             kw = {k: st[nm] for k, nm in zip(("m", "v"), names)}
             oracle.epilogue_apply(c.d(oracle, 1), kind, p=p, step=step,
@@ -269,7 +275,7 @@ def test_dma_other_kinds(ctx, oracle, K, rng_ix, kind):
 
 
 def test_dma_route_leaves_others_on_the_per_tile_form(ctx, oracle):
-    """amsgrad (a fourth operand stream), a requested aggregate output and 4+ reads keep their round-5 routes: one
+    """amsgrad and centered RMSprop (a fourth operand stream) and a requested aggregate output keep their round-5 routes: one
     persistent per-tile launch, or the burst form."""
     from nvflare_amd import _native as N
 
@@ -283,6 +289,9 @@ def test_dma_route_leaves_others_on_the_per_tile_form(ctx, oracle):
         assert _run(ctx, c, e, N.FEDAVG_OP_TORCH, N.FEDAVG_FIN_DIV, out_ptr=c.buf("d", z)) == 1
         want = c.d(oracle, 1)
         assert same_bits(c.get("d"), want)
+        e = _epi(5, param=c.buf("p", z + 1), state1=c.buf("m", z + 1e-3), state2=c.buf("v", z), state3=c.buf("x", z),
+                 lr=1e-3, alpha=0.9, eps=1e-8, momentum=0.5, centered=1)  # centered RMSprop: a fourth stream
+        assert _run(ctx, c, e, N.FEDAVG_OP_TORCH, N.FEDAVG_FIN_DIV) == 1
     finally:
         c.close()
 

@@ -602,10 +602,10 @@ def test_few_client_fused_every_kind(ctx, oracle, K, case):
             ctx.accumulate_tiled_epi(dev.bases, ws, TILE, dev.lay.tile_stride, 0, dev.n4, out, N_.FEDAVG_OP_TORCH,
                                      N_.FEDAVG_FIN_DIV, _sum(ws), e)
             ctx.sync()
-            # Every kind but RMSprop takes the LDS-DMA few-client form (round 6) unless it asks for amsgrad or an aggregate
+            # Every kind takes the LDS-DMA few-client form (round 6) unless it asks for centered RMSprop, amsgrad or an aggregate
             # output: one launch per num_cus x tiles-per-block tiles; the rest the per-tile form: one persistent launch
             tiles = (dev.n4 - 1) // TILE + 1
-            dma = kind != 5 and (out is None or kind == 1) and not hp.get("amsgrad")
+            dma = not hp.get("centered") and (out is None or kind == 1) and not hp.get("amsgrad")
             tpb = _dma_tiles_per_block(kind, K)
             assert ctx.launch_count() - n_launch == (-(-tiles // (min(ctx.num_cus, tiles) * tpb)) if dma else 1)
             d = oracle.fedavg_c(rows, ws, oracle.MODE_TORCH, nthreads=8)

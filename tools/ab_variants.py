@@ -16,8 +16,8 @@ import sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 EXTRA = {"none": 4.0, "add_base": 8.0, "sgd": 16.0, "adam": 24.0, "adagrad": 16.0, "adamax": 24.0, "nadam": 24.0,
-         "radam": 24.0, "rprop": 24.0, "asgd": 16.0}
-TWO_STATES = ("adam", "adamax", "nadam", "radam", "rprop")  # algorithmic bytes per param beyond 4K
+         "radam": 24.0, "rprop": 24.0, "asgd": 16.0, "rmsprop": 24.0}
+TWO_STATES = ("adam", "adamax", "nadam", "radam", "rprop", "rmsprop")  # rmsprop: square_avg, momentum buffer  # algorithmic bytes per param beyond 4K
 
 
 def main():
@@ -78,7 +78,8 @@ def main():
     ctx.sync()
     kinds = {"add_base": N.FEDAVG_EPI_ADD_BASE, "sgd": N.FEDAVG_EPI_SGD, "adam": N.FEDAVG_EPI_ADAM,
              "adagrad": N.FEDAVG_EPI_ADAGRAD, "adamax": N.FEDAVG_EPI_ADAMAX, "nadam": N.FEDAVG_EPI_NADAM,
-             "radam": N.FEDAVG_EPI_RADAM, "rprop": N.FEDAVG_EPI_RPROP, "asgd": N.FEDAVG_EPI_ASGD}
+             "radam": N.FEDAVG_EPI_RADAM, "rprop": N.FEDAVG_EPI_RPROP, "asgd": N.FEDAVG_EPI_ASGD,
+             "rmsprop": N.FEDAVG_EPI_RMSPROP}
 
     def launcher(epi, pad, sh=0):
         _, bases, stride = slabs[pad]
@@ -89,6 +90,7 @@ def main():
         e.lr, e.momentum, e.beta1, e.beta2, e.eps, e.step = 1e-3, 0.9, 0.9, 0.999, 1e-8, 1.0
         e.etaminus, e.etaplus, e.step_size_min, e.step_size_max = 0.5, 1.2, 1e-6, 50.0
         e.lambd, e.eta, e.mu = 1e-4, 1e-2, 0.5
+        e.alpha = 0.99  # RMSprop (with momentum 0.9: not centered, three operand streams)
         e.torch_sqrt = {"ieee": N.FEDAVG_SQRT_IEEE, "torch_cpu": N.FEDAVG_SQRT_TORCH_AVX512,
                         "torch_cpu_amd": N.FEDAVG_SQRT_TORCH_AMD}[a.sqrt]
         if epi == "add_base":
@@ -122,6 +124,8 @@ def main():
     for rnd in range(a.rounds):
         for epi, pad, sh in [(e_, p_, s_) for e_ in epis for p_ in pads for s_ in shifts]:
             fn = launcher(epi, pad, sh)
+            for b in bufs:  # every epilogue from zeroed states: not another kind's (an RMSprop square_avg holding Adam's
+                ctx.memset(b.ptr, 0, end * 4 + max(shifts))  # exp_avg goes negative and takes the sqrt's rare path)
             for v in variants:
                 ctx.set_variant(v[0])
                 ctx.set_launch(v[2], v[1])
