@@ -143,6 +143,31 @@ __device__ __forceinline__ float div_const_fast(const float a, const FinConst& f
     return __builtin_fmaf(e, f.r, q);
 }
 
+// div_const_fast with +0 on the fast form -- the epilogues' quotients (fedavg_epi.h div_x): q = +-0, e = +0 and the
+// result 0 with the divisor's sign, as a / v (-0 stays rare: the form returns +0 for -0 / v, v > 0).  A frozen
+// parameter (every client's update exactly 0) keeps Adam's exp_avg at 0, and its unit would otherwise recompute per
+// element on every step (round 6: the LDS-DMA form at 1 / 2 / 3 clients with half the parameters frozen 61.5 / 66.8 /
+// 55.9 % of HBM, live 75.3 / 73.9 / 78.7 %; profiles/r06/s20/).  The aggregation's own FIN_DIV (fin_tile) keeps the
+// one-compare form: a zero sum there costs only its group's IEEE divisions, and the plain few-client kernel lost 3
+// points to the extra compare (79.3 -> 76.2 % at 2 clients, s20).
+__device__ __forceinline__ float div_const_fast_z(const float a, const FinConst& f, uint32_t& slow) {
+#if defined(FEDAVG_AB_IEEE_DIV)
+    return a / f.v;
+#endif
+    const float q = a * f.r;
+    const float e = __builtin_fmaf(-q, f.v, a);
+    const uint32_t ab = __float_as_uint(a);
+    slow |= (uint32_t)(((ab >> 23) & 0xFFu) - 27u >= 200u && ab != 0u);
+    return __builtin_fmaf(e, f.r, q);
+}
+
+// A lane's rare-case flag made wave-uniform: the recompute then runs on every lane of the wave (each rare-case form is
+// bit-identical to its fast form) behind a scalar branch, with no exec mask to restore at the join.  With the branch
+// divergent, hipcc placed the register allocator's copy of a held result (a VGPR -> AGPR move) in the join block BEFORE
+// its exec restore, behind SGPR-spill writelanes: the lanes that had skipped the branch never got the value (round 6,
+// session 22: the LDS-DMA Adam form at 3 clients lost unit 14's parameter in every wave, tools/r06/diag_u14.py).
+__device__ __forceinline__ bool wave_any(const uint32_t slow) { return __builtin_amdgcn_ballot_w64(slow != 0u) != 0; }
+
 // fin4c over a lane's CPL columns of one tile, with one rare-case branch for all of them (div_const_fast)
 template <int FIN, int CPL>
 __device__ __forceinline__ void fin_tile(f32x4 (&r)[CPL], const f32x4 (&a)[CPL], const FinConst& f) {
@@ -152,7 +177,7 @@ __device__ __forceinline__ void fin_tile(f32x4 (&r)[CPL], const f32x4 (&a)[CPL],
         for (int c = 0; c < CPL; ++c)
 #pragma unroll
             for (int j = 0; j < 4; ++j) r[c][j] = div_const_fast(a[c][j], f, slow);
-        if (__builtin_expect(slow != 0u, 0)) {
+        if (__builtin_expect(wave_any(slow), 0)) {
 #pragma unroll
             for (int c = 0; c < CPL; ++c)
 #pragma unroll
@@ -400,7 +425,8 @@ __device__ __forceinline__ float sqrt_torch_cpu(const float x) {
 // sqrt_torch_cpu without its special-input branch: `slow` set where it would have taken the callout (the caller then
 // recomputes the group with sqrt_torch_cpu)
 __device__ __forceinline__ float sqrt_torch_cpu_fast(const float x, uint32_t& slow) {
-    slow |= (uint32_t)(!(x > 0.0f) || x == __builtin_inff());
+    // the callout for -0, negatives, inf and NaN; +0 runs the refinement (xs = 0, a finite estimate: s = r = res = +0)
+    slow |= (uint32_t)(__float_as_uint(x) >= 0x7F800000u);
     const bool tiny = x < 0x1p-96f;
     const float xs = tiny ? x * 0x1p64f : x;
     const uint32_t b = __float_as_uint(xs);
@@ -464,7 +490,11 @@ __device__ __forceinline__ float sqrt_mkl_rsqrtps(const float x) {
 // the group with sqrt_mkl_rsqrtps)
 __device__ __forceinline__ float sqrt_mkl_rsqrtps_fast(const float x, uint32_t& slow) {
     const uint32_t b = __float_as_uint(x);
-    slow |= (uint32_t)(b - 0x00800000u > 0x7F7FF000u - 0x00800000u);
+    // the callout for subnormals, the top finite values, inf, NaN, negatives and -0; +0 runs the refinement (a finite
+    // estimate for exponent -127: s = s1 = res = +0), so a frozen parameter's zero exp_avg_sq stays on the fast form
+    // (v_cmp_class for +subnormals (class bit 7), one unsigned compare for the top finite values, +inf, NaN and every
+    // negative -0 included: as many VALU compares as the range test that also sent +0 to the callout)
+    slow |= (uint32_t)(__builtin_amdgcn_class(x, 0x080) || b > 0x7F7FF000u);
     const int e = (int)((b >> 23) & 0xFFu) - 127;
     const int p = e & 1;
     const int k = (e - p) / 2;

@@ -111,7 +111,7 @@ __device__ __forceinline__ float sqrt_x(const EpiParams& E, const float x, uint3
 
 template <int EM>
 __device__ __forceinline__ float div_x(const float a, const FinConst& f, uint32_t& slow) {
-    if constexpr (EM == kEmFast) return div_const_fast(a, f, slow);
+    if constexpr (EM == kEmFast) return div_const_fast_z(a, f, slow);
     if constexpr (EM == kEmIeee) return a / f.v;
     return div_const(a, f);
 }
@@ -360,7 +360,7 @@ __device__ __forceinline__ void epilogue4(const EpiParams& E, const EpiConsts& C
         if constexpr ((EPI & 0xFF) == FEDAVG_EPI_NADAM) slow = C.bc2.fast ? 0u : 1u;
         if constexpr ((EPI & 0xFF) == FEDAVG_EPI_RADAM) slow = C.bc1.fast ? 0u : 1u;
         EpiIn o = epi_compute<EPI, kEmFast>(E, C, d, in, slow);
-        if (__builtin_expect(slow != 0u, 0)) {
+        if (__builtin_expect(wave_any(slow), 0)) {  // every lane: see wave_any
             uint32_t unused = 0;
             o = epi_compute<EPI, kEmElem>(E, C, d, in, unused);
         }
@@ -947,7 +947,7 @@ fedavg_tiles_epi_dma_f32x4(const RowTableF32 tab, const int64_t tstride4, f32x4*
             if constexpr ((EPI & 0xFF) == FEDAVG_EPI_NADAM) slow = C.bc2.fast ? 0u : 1u;
             if constexpr ((EPI & 0xFF) == FEDAVG_EPI_RADAM) slow = C.bc1.fast ? 0u : 1u;
             o = epi_compute<EPI, kEmFast>(E, C, d1[0], in, slow);
-            if (__builtin_expect(slow != 0u, 0)) {
+            if (__builtin_expect(wave_any(slow), 0)) {  // every lane: see wave_any
                 uint32_t unused = 0;
                 o = epi_compute<EPI, kEmElem>(E, C, d1[0], in, unused);
             }

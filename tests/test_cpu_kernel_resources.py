@@ -47,3 +47,19 @@ def test_two_wave_per_simd_kernels_fit_256_registers(ks):
     assert wide, "no 512-thread kernel found"
     bad = [(k["name"], k["vgpr"], k["agpr"]) for k in wide if k["vgpr"] > 256]
     assert not bad, bad[:5]
+
+
+@pytest.mark.timeout(600)
+def test_no_result_copy_before_a_join_blocks_exec_restore():
+    """No kernel of the product library holds the miscompile round 6 met in the LDS-DMA fused form (tools/
+    check_join_copies.py, fedavg_arith.h wave_any): a VALU write in a divergent branch's join block placed before the
+    block's exec restore, to a register written nowhere else -- the lanes that skipped the branch lose the value.  The
+    rare-case recomputes branch on a wave-uniform condition since; the library built before that had 18 such kernels."""
+    import check_join_copies as cj
+
+    lib = os.path.join(ROOT, "nvflare_amd", "lib", "libnvflare_amd_fedavg.so")
+    if not os.path.exists(lib) or not os.path.exists(os.path.join(cj.LLVM, "llvm-objdump")):
+        pytest.skip("the library or the ROCm LLVM tools are absent")
+    n, flagged = cj.scan_so(lib, jobs=min(8, os.cpu_count() or 1))
+    assert n > 1000
+    assert not flagged, [(k[:100], f[:2]) for k, f in flagged[:5]]

@@ -89,6 +89,12 @@ class _Case:
             b.close()
 
 
+def _diff(a, w):
+    """Mismatch count and the first few (index, got bits, want bits) for an assertion message."""
+    bad = np.flatnonzero((a.view(np.uint32) != w.view(np.uint32)) & ~(np.isnan(a) & np.isnan(w)))
+    return int(bad.size), [(int(i), hex(int(a.view(np.uint32)[i])), hex(int(w.view(np.uint32)[i]))) for i in bad[:4]]
+
+
 def _tiles_per_block(kind, K, rms_momentum=False):
     """Tiles per block per launch of the product geometry (fedavg_epi.h EpiDmaGeom: N units per wave x W waves / 16):
     Adam / NAdam / RAdam / Adagrad / RMSprop 1 / 2 clients 8 waves x 14 / 16 units, 3 clients 4 waves x 32 (RMSprop
@@ -162,8 +168,8 @@ def test_dma_adam_matches_oracle_and_per_tile(ctx, oracle, K, rng_ix, sqrt):
         pw, mw, vw = p.copy(), m.copy(), v.copy()
         oracle.epilogue_apply(c.d(oracle, 1), oracle.EPI_ADAM, p=pw, m=mw, v=vw, step=3.0, torch_cpu_sqrt=sqrt,
                               **(ADAM if rng_ix % 2 == 0 else ADAM_WD))
-        for a, b, w in zip(got[0], got[4], (pw, mw, vw)):
-            assert same_bits(a, w) and same_bits(b, w)
+        for a, b, w, nm in zip(got[0], got[4], (pw, mw, vw), "pmv"):
+            assert same_bits(a, w) and same_bits(b, w), (nm, _diff(a, w), _diff(b, w))
     finally:
         c.close()
 

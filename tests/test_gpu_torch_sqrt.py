@@ -225,3 +225,79 @@ def test_short_and_ragged_calls_match_the_hosts_torch(ctx, threads):
             assert _same(got, want) == 0, (n, threads, mode)
     finally:
         torch.set_num_threads(saved)
+
+
+FROZEN_KINDS = [
+    ("adam", dict(lr=1e-3, beta1=0.9, beta2=0.999, eps=1e-8)),  # (weight decay would make a frozen g non-zero)
+    ("adagrad", dict(lr=1e-2, lr_decay=0.05, eps=1e-10)),
+    ("rmsprop", dict(lr=1e-3, alpha=0.99, eps=1e-8, momentum=0.5)),
+    ("nadam", dict(lr=2e-3, beta1=0.9, beta2=0.999, eps=1e-8, momentum_decay=4e-3)),
+    ("radam", dict(lr=1e-3, beta1=0.9, beta2=0.999, eps=1e-8)),
+]
+
+
+@pytest.mark.parametrize("sqrt", ["ieee", "torch_cpu", "torch_cpu_amd"])
+@pytest.mark.parametrize("K", [2, 70])
+@pytest.mark.parametrize("name,hp", FROZEN_KINDS, ids=[k for k, _ in FROZEN_KINDS])
+def test_frozen_parameters_and_signed_zero_states(ctx, oracle, name, hp, K, sqrt):
+    """A frozen region (every client's update exactly 0: the states stay +0, the restated sqrt's and the quotients' +0
+    inputs run their fast forms since round 6) beside -0 and subnormal states (still the rare path), through the
+    LDS-DMA form (2 clients) and the burst form (70): p and every state bit for bit against the oracle, two steps."""
+    from nvflare_amd import _native as N
+
+    kind = {"adam": oracle.EPI_ADAM, "adagrad": oracle.EPI_ADAGRAD, "rmsprop": oracle.EPI_RMSPROP,
+            "nadam": oracle.EPI_NADAM, "radam": oracle.EPI_RADAM}[name]
+    rng = np.random.default_rng(77 + K)
+    n = 6 * 4096 + 36
+    frozen = 3 * 4096 + 1000  # tiles 0-2 whole and a piece of tile 3
+    p = rng.standard_normal(n).astype(np.float32)
+    m = (rng.standard_normal(n) * 1e-3).astype(np.float32)
+    v = (rng.random(n) * 1e-6).astype(np.float32)
+    m[:frozen] = 0.0
+    v[:frozen] = 0.0
+    sel = rng.choice(np.arange(frozen, n), 200, replace=False)
+    m[sel[:50]] = -0.0
+    v[sel[50:100]] = -0.0 if name != "adagrad" else 0.0  # Adagrad's sum: -0 + g*g
+    v[sel[100:150]] = np.float32(1e-40)  # subnormal
+    ws = [float(1 + (37 * k) % 100) for k in range(K)]
+    count = None
+    for w in ws:
+        count = w if count is None else count + w
+    flag = {"ieee": N.FEDAVG_SQRT_IEEE, "torch_cpu": N.FEDAVG_SQRT_TORCH_AVX512, "torch_cpu_amd": N.FEDAVG_SQRT_TORCH_AMD}
+    if sqrt == "torch_cpu_amd":
+        ctx.load_rsqrtps(oracle.rsqrtps_table())
+    for step in (1, 2):
+        rows = [(rng.standard_normal(n) * 0.01).astype(np.float32) for _ in range(K)]
+        for r in rows:
+            r[:frozen] = 0.0
+        d = oracle.fedavg_c(rows, ws, oracle.MODE_TORCH)
+        dev = _Dev(ctx, rows, n)
+        try:
+            e = N.Epilogue()
+            e.kind = kind
+            for k_, val in hp.items():
+                setattr(e, k_, val)
+            e.step, e.mu_product = float(step), 1.0
+            e.torch_sqrt = flag[sqrt]
+            e.param, e.state1 = dev.buf("p", p), dev.buf("m", m if name != "adagrad" and name != "rmsprop" else v)
+            if name == "rmsprop":
+                e.state2 = dev.buf("v", m)
+            elif name != "adagrad":
+                e.state2 = dev.buf("v", v)
+            ctx.accumulate_tiled_epi(dev.bases, ws, 4096, dev.lay.tile_stride, 0, dev.n4, None, N.FEDAVG_OP_TORCH,
+                                     N.FEDAVG_FIN_DIV, count, e)
+            got = {nm: dev.get(nm) for nm in dev.bufs}
+        finally:
+            dev.close()
+        if name == "adagrad":
+            oracle.epilogue_apply(d, kind, p=p, m=v, step=float(step), torch_cpu_sqrt=sqrt, **hp)
+            want = {"p": p, "m": v}
+        elif name == "rmsprop":  # square_avg in state1, the momentum buffer in state2
+            oracle.epilogue_apply(d, kind, p=p, m=v, v=m, step=float(step), torch_cpu_sqrt=sqrt, **hp)
+            want = {"p": p, "m": v, "v": m}
+        else:
+            oracle.epilogue_apply(d, kind, p=p, m=m, v=v, step=float(step), mu_product=1.0, torch_cpu_sqrt=sqrt, **hp)
+            want = {"p": p, "m": m, "v": v}
+        for nm, w in want.items():
+            assert same_bits(got[nm], w), (name, step, nm, int(np.count_nonzero(got[nm].view(np.uint32) !=
+                                                                                 w.view(np.uint32))))

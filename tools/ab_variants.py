@@ -38,6 +38,9 @@ def main():
     ap.add_argument("--check", action="store_true",
                     help="every config's output (the fused epilogues: p and the last state, from zeroed state) must "
                          "equal the first config's bit for bit")
+    ap.add_argument("--frozen-frac", type=float, default=0.0,
+                    help="this leading fraction of the parameters gets exactly-zero updates from every client (frozen "
+                         "layers): Adam's exp_avg_sq stays 0 there, the restated sqrt's and quotients' rare inputs")
     ap.add_argument("--prewarm-s", type=float, default=0.0,
                     help="seconds of the first config run back to back before the first round (the GPU's power state "
                          "ramps over the first seconds of load: VERDICT r05 item 3)")
@@ -65,6 +68,13 @@ def main():
         bases = [slab.ptr + k * lay.tile * 4 for k in range(K)]
         for k in range(K):
             ctx.fill_synthetic_f32(bases[k], P, 1234, k, 0, lay.tile, stride)
+        frozen = int(a.frozen_frac * P) // 4 * 4
+        if frozen:
+            zeros = np.zeros(min(frozen, 1 << 24), dtype=np.float32)
+            for k in range(K):
+                for off in range(0, frozen, zeros.size):
+                    n = min(zeros.size, frozen - off)
+                    ctx.h2d_tiled(bases[k], lay.tile * 4, stride * 4, off * 4, zeros.ctypes.data, n * 4)
         slabs[pad] = (slab, bases, stride)
     op, fin = (1, 2) if a.mode == "torch" else (0, 1)
     ws = [float(1 + (37 * k) % 100) for k in range(K)]
