@@ -1020,35 +1020,49 @@ inline hipError_t launch_epi_dma_n(const TileLaunch& L, const EpiParams& E, hipS
 // 67.3 / 71.3 / 72.3; W = 8, N = 16: 75.9 / 74.3 / 74.7, 72.9 / 75.0 / 74.3) -- lighter arithmetic, fewer result
 // registers per unit (8 and 4): one wave per SIMD keeps up, and 40 units fit its registers.
 // The other kinds (round 6, later): the ones with a sqrt and a division per element (NAdam, RAdam, Adagrad, RMSprop)
-// take Adam's geometry; Adamax and Rprop 4 waves x 24 units (three result streams per unit: 32 and 40 spill), ASGD SGD's.
+// start from Adam's geometry; Adamax and Rprop 4 waves x 24 units (three result streams per unit: 32 and 40 spill), ASGD
+// SGD's.  With the AMD-host sqrt (the pool's hosts, the one measured) a same-process sweep of every geometry per kind
+// (profiles/r06/s23/, A/B variant bits 9-11, 1 / 2 / 3 clients, % of 8 TB/s) moved:
+//   RAdam 1-2 reads to 4 waves x 40 units, table by DMA: 75.2 / 73.0 -> 76.5 / 78.5 (3 reads stay: 79.6)
+//   RMSprop (momentum) 1-2 reads, the same: 73.1 / 74.3 -> 75.2 / 78.3 (3 reads 78.5 against 79.4: kept)
+//   Adagrad 2 reads, the same: 72.5 -> 74.1
+//   NAdam to 8 waves x 16 units, table by DMA, at every read count: 73.6 / 74.0 / 73.5 -> 74.5 / 74.8 / 75.1
 template <int EPI, int KC, int NIN>
 struct EpiDmaGeom {
     static constexpr int KIND = EPI & 0xFF;
-    // the sqrt + division kinds: two waves per SIMD at 1-2 reads (Adagrad on SGD's 4 x 40 / 32 ran 48.6 / 57.2 / 63.6 %
-    // against 66.3 / 72.7 / 70.6 % here: profiles/r06/s16/, s15/)
     static constexpr bool kAdam = KIND == FEDAVG_EPI_ADAM || KIND == FEDAVG_EPI_NADAM || KIND == FEDAVG_EPI_RADAM ||
                                   KIND == FEDAVG_EPI_ADAGRAD || KIND == FEDAVG_EPI_RMSPROP;
     static constexpr bool kThree = KIND == FEDAVG_EPI_ADAMAX || KIND == FEDAVG_EPI_RPROP;  // light, three streams
-    static constexpr int W = kAdam && KC <= 2 ? 8 : 4;
+    static constexpr bool kAmd = (EPI & kEpiSqrtMask) == kEpiTorchSqrtAmd;
+    static constexpr bool kWide = kAmd && KC <= 2 &&
+                                  (KIND == FEDAVG_EPI_RADAM || KIND == FEDAVG_EPI_RMSPROP ||
+                                   (KIND == FEDAVG_EPI_ADAGRAD && KC == 2));
+    static constexpr bool kNadam = kAmd && KIND == FEDAVG_EPI_NADAM;
+    static constexpr int W = kWide ? 4 : kNadam ? 8 : kAdam && KC <= 2 ? 8 : 4;
     // (SGD with its momentum buffer at 3 reads holds 40 units only with 600+ bytes of scratch per lane: 32 there; Adamax
     // and Rprop hold three result streams per unit: 24)
     // (RMSprop with its momentum buffer, IEEE sqrt: 14 / 24 units at 2 / 3 reads, 16 / 32 spill)
     static constexpr bool kRmsMom = KIND == FEDAVG_EPI_RMSPROP && NIN == 3;
-    static constexpr int N = kThree ? 24
+    static constexpr int N = kWide ? 40
+                             : kNadam ? 16
+                             : kThree ? 24
                              : !kAdam ? (KC == 3 ? 32 : 40)
                              : KC == 1 ? 14
                              : KC == 2 ? (kRmsMom ? 14 : 16)
                                        : (kRmsMom ? 24 : 32);
-    static constexpr bool TDMA = kAdam && KC != 2;
+    static constexpr bool TDMA = kWide || kNadam || (kAdam && KC != 2);
 };
 
-// A/B builds with -DFEDAVG_AB_FEW (torch-mode FIN_DIV, ADD_BASE / SGD / Adam with the AMD-host sqrt): launch variant
-// bits 9-11 = 1-7 pick another geometry
+// A/B builds with -DFEDAVG_AB_FEW (torch-mode FIN_DIV, ADD_BASE / SGD, and Adam / NAdam / RAdam / Adagrad / RMSprop with
+// the AMD-host sqrt): launch variant bits 9-11 = 1-7 pick another geometry
 template <int OP, int FIN, int EPI, int KC, int NIN>
 inline hipError_t launch_epi_dma_form(const TileLaunch& L, const EpiParams& E, hipStream_t s, uint64_t* nl) {
     constexpr int KIND = EPI & 0xFF;
+    constexpr bool kSqrtKind = KIND == FEDAVG_EPI_ADAM || KIND == FEDAVG_EPI_NADAM || KIND == FEDAVG_EPI_RADAM ||
+                               KIND == FEDAVG_EPI_ADAGRAD || KIND == FEDAVG_EPI_RMSPROP;
     if constexpr (kABFew && OP == FEDAVG_OP_TORCH && FIN == FEDAVG_FIN_DIV &&
-                  (EPI == (FEDAVG_EPI_ADAM | kEpiTorchSqrtAmd) || KIND == FEDAVG_EPI_SGD || KIND == FEDAVG_EPI_ADD_BASE)) {
+                  ((kSqrtKind && (EPI & kEpiSqrtMask) == kEpiTorchSqrtAmd) || KIND == FEDAVG_EPI_SGD ||
+                   KIND == FEDAVG_EPI_ADD_BASE)) {
         switch ((L.variant >> kVariantLoopShift) & 7) {
             case 1: return launch_epi_dma_n<OP, FIN, EPI, KC, NIN, 16, false>(L, E, s, nl);
             case 2: return launch_epi_dma_n<OP, FIN, EPI, KC, NIN, 32, true>(L, E, s, nl);

@@ -95,10 +95,15 @@ def _diff(a, w):
     return int(bad.size), [(int(i), hex(int(a.view(np.uint32)[i])), hex(int(w.view(np.uint32)[i]))) for i in bad[:4]]
 
 
-def _tiles_per_block(kind, K, rms_momentum=False):
+def _tiles_per_block(kind, K, rms_momentum=False, amd=False):
     """Tiles per block per launch of the product geometry (fedavg_epi.h EpiDmaGeom: N units per wave x W waves / 16):
     Adam / NAdam / RAdam / Adagrad / RMSprop 1 / 2 clients 8 waves x 14 / 16 units, 3 clients 4 waves x 32 (RMSprop
-    with momentum 14 / 14 / 24); Adamax / Rprop 4 waves x 24; ADD_BASE / SGD / ASGD 4 waves x 40 (x 32 at 3)."""
+    with momentum 14 / 14 / 24); Adamax / Rprop 4 waves x 24; ADD_BASE / SGD / ASGD 4 waves x 40 (x 32 at 3).  With
+    the AMD-host sqrt: RAdam / RMSprop at 1-2 clients and Adagrad at 2 4 waves x 40, NAdam 8 x 16 at every count."""
+    if amd and K <= 2 and (kind in (5, 8) or (kind == 4 and K == 2)):
+        return 10
+    if amd and kind == 7:
+        return 8
     if kind == 5 and rms_momentum:
         return {1: 7, 2: 7, 3: 6}[K]
     if kind in (3, 4, 5, 7, 8):
@@ -108,9 +113,9 @@ def _tiles_per_block(kind, K, rms_momentum=False):
     return 8 if K == 3 else 10
 
 
-def _launches(ctx, begin, end, kind=3, K=2, rms_momentum=False):
+def _launches(ctx, begin, end, kind=3, K=2, rms_momentum=False, amd=False):
     t_first, t_stop = begin // TILE, (end - 1) // TILE + 1
-    per = min(ctx.num_cus, t_stop - t_first) * _tiles_per_block(kind, K, rms_momentum)  # one block per CU
+    per = min(ctx.num_cus, t_stop - t_first) * _tiles_per_block(kind, K, rms_momentum, amd)  # one block per CU
     return -(-(t_stop - t_first) // per)
 
 
@@ -269,7 +274,7 @@ def test_dma_other_kinds(ctx, oracle, K, rng_ix, case):
                     kw[field] = c.buf(nm, st[nm])
                 nl = _run(ctx, c, _epi(kind, **kw), N.FEDAVG_OP_TORCH, N.FEDAVG_FIN_DIV, variant=variant)
                 if variant == 0:
-                    assert nl == _launches(ctx, begin, end, kind, K, rms_momentum=len(names) == 2)
+                    assert nl == _launches(ctx, begin, end, kind, K, rms_momentum=len(names) == 2, amd=amd_sqrt)
                 got[variant] = [c.get(x) for x in ("p",) + names]
             kw = {k: st[nm] for k, nm in zip(("m", "v"), names)}
             oracle.epilogue_apply(c.d(oracle, 1), kind, p=p, step=step,
