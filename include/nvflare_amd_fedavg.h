@@ -325,7 +325,7 @@ int fedavg_timing_end(fedavg_ctx* ctx, float* ms);
 /* Aggregation / epilogue / dequantization kernel launches issued on the context's compute stream so far.
  * One fedavg_accumulate* call may issue several (the fp32 burst kernels: one per grid x tiles-per-block tiles --
  * 18 tiles per block on the one-block-per-CU grids of the plain kernel at 32+ clients (17 for the fused kernel at
- * 64+), 12 on two-block grids; the fused LDS-DMA form at 1-3 reads 6-10 tiles per block, one block per CU); relates a
+ * 64+), 12 on two-block grids; the fused LDS-DMA form at 1-3 reads 4-10 tiles per block, one block per CU); relates a
  * profiler's per-launch durations to per-call times. */
 int fedavg_launch_count(fedavg_ctx* ctx, uint64_t* n);
 /* Launch tuning (0 = default): blocks per CU (default: each kernel's own -- 1 for the burst aggregation
@@ -341,10 +341,10 @@ int fedavg_set_launch(fedavg_ctx* ctx, int blocks_per_cu, int unroll);
  * burst form (round 5): every register-held tile's loads go out before any arithmetic, the results are stored as a
  * burst; a chained sum with fewer than 3 reads runs the PER-TILE-STORE form, which stores each tile's results as it
  * finishes.  The fused kernel with 1-3 client reads, no chained sum and no separate aggregate output (out only for
- * ADD_BASE) runs its LDS-DMA few-client form (round 6) for every kind (Adam without amsgrad, RMSprop not centered):
- * every input goes HBM -> LDS by LDS-DMA while the wave computes the units already landed, the results are held on chip
- * and stored as a burst; amsgrad, centered RMSprop and chained sums under 4 reads run its per-tile form pipelined across
- * tiles.  Every load
+ * ADD_BASE) runs its LDS-DMA few-client form (round 6) for every kind (Adam with amsgrad at 3 reads only, RMSprop
+ * centered only with momentum): every input goes HBM -> LDS by LDS-DMA while the wave computes the units already
+ * landed, the results are held on chip and stored as a burst; the rest and chained sums under 4 reads run its per-tile
+ * form pipelined across tiles.  Every load
  * and store is
  * nontemporal.  The 16-bit and fp64 tile kernels (fedavg_accumulate_tiled16 / _tiled64) likewise run 1-3 client
  * reads without a chained sum on their few-client burst forms, the rest on their burst forms.  The plain burst kernel has the launch's client count

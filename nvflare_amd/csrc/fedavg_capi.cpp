@@ -1408,7 +1408,7 @@ int fedavg_accumulate_tiled_epi(fedavg_ctx* ctx, const void* const* bases, const
         // 1-3 client reads without a chained sum or a separate aggregate output: the LDS-DMA few-client form (round 6;
         // fedavg_epi.h fedavg_tiles_epi_dma_f32x4), one block per CU, unless the public variant asks for the per-tile
         // form (bit 2, kVariantEpiPrefetch) or tile stores (bit 3)
-        const bool dma = !cur_in && L.k >= 1 && L.k <= 3 && fedavg::epi_dma_nin(E) > 0 &&
+        const bool dma = !cur_in && L.k >= 1 && L.k <= 3 && fedavg::epi_dma_nin(E, L.k) > 0 &&
                          (!out || epi->kind == FEDAVG_EPI_ADD_BASE) &&
                          !(ctx->variant & (fedavg::kVariantEpiPrefetch | fedavg::kVariantTileStores));
         if (dma) L.variant |= fedavg::kVariantEpiDma;

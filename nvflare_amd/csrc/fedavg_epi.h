@@ -875,18 +875,20 @@ fedavg_tiles_epi_dma_f32x4(const RowTableF32 tab, const int64_t tstride4, f32x4*
     constexpr int CPT = 64 / (4 * W);       // float4 columns per lane per tile (4 at W = 4, 2 at W = 8)
     constexpr int64_t T4 = kDefaultTile / 4;  // float4 per tile; a tile is 16 wave pieces of 64 float4
     constexpr int KIND = EPI & 0xFF;
-    // RMSprop on this form: not centered, its momentum buffer read iff NIN == 3 -- results p, square_avg (, buffer)
-    constexpr int NOUT = KIND == FEDAVG_EPI_RMSPROP ? NIN : epi_nout<EPI>();
-    static_assert(KC >= 1 && KC <= 3 && NIN >= 1 && NIN <= 3 && NOUT <= G, "few-client fused form");
+    // RMSprop on this form: its momentum buffer read iff NIN >= 3, centered (grad_avg) iff NIN == 4 -- results p,
+    // square_avg (, buffer (, grad_avg)); Adam: amsgrad (max_exp_avg_sq) iff NIN == 4
+    constexpr int NOUT = KIND == FEDAVG_EPI_RMSPROP || (KIND == FEDAVG_EPI_ADAM && NIN == 4) ? NIN : epi_nout<EPI>();
+    static_assert(KC >= 1 && KC <= 3 && NIN >= 1 && NIN <= 4 && NOUT <= G, "few-client fused form");
     static_assert(KIND != FEDAVG_EPI_RMSPROP || NIN >= 2, "RMSprop reads p and square_avg");
+    static_assert(NIN < 4 || KIND == FEDAVG_EPI_ADAM || KIND == FEDAVG_EPI_RMSPROP, "four operand streams");
     static_assert(S >= 1 && S <= N && (S - 1) * G <= 63 && N % CPT == 0, "ring geometry");
     static_assert((int64_t)W * S * G * 1024 <= epi_dma_ring_bytes<EPI>(), "ring fits the CU's LDS");
     __shared__ f32x4 ring[W][S][G][64];
     EpiParams E = E_;
-    if constexpr (KIND == FEDAVG_EPI_ADAM) E.amsgrad = 0;  // amsgrad runs the per-tile form (4 operand streams)
-    if constexpr (KIND == FEDAVG_EPI_RMSPROP) {  // centered runs the per-tile form; NIN says whether momentum is on
-        E.centered = 0;
-        E.has_momentum = NIN == 3;
+    if constexpr (KIND == FEDAVG_EPI_ADAM) E.amsgrad = NIN == 4;  // the operand streams say which flags are on
+    if constexpr (KIND == FEDAVG_EPI_RMSPROP) {
+        E.centered = NIN == 4;
+        E.has_momentum = NIN >= 3;
     }
     const FinConst fc = fin_const<FIN>(fin_val);
     const EpiConsts C = epi_consts<EPI>(E);
@@ -901,8 +903,8 @@ fedavg_tiles_epi_dma_f32x4(const RowTableF32 tab, const int64_t tstride4, f32x4*
             glds16(reinterpret_cast<const uint4*>(E.rsqrtps) + (wave * (16 / W) + j) * 64 + lane,
                    lds_byte_addr(&g_rsqrtps_lds[(wave * (16 / W) + j) * 256]));
     }
-    // operand streams in EpiIn order (.a, .b, .c): the parameter (ADD_BASE: the base) and the optimizer states
-    const float* opnd[3] = {(EPI & 0xFF) == FEDAVG_EPI_ADD_BASE ? E.base : E.param, E.state1, E.state2};
+    // operand streams in EpiIn order (.a, .b, .c, .d): the parameter (ADD_BASE: the base) and the optimizer states
+    const float* opnd[4] = {(EPI & 0xFF) == FEDAVG_EPI_ADD_BASE ? E.base : E.param, E.state1, E.state2, E.state3};
     const int64_t t_first = t0 + blockIdx.x;
     auto tile_of = [&](const int u) __attribute__((always_inline)) {
         const int64_t t = t_first + (int64_t)(u / CPT) * gridDim.x;
@@ -937,6 +939,7 @@ fedavg_tiles_epi_dma_f32x4(const RowTableF32 tab, const int64_t tstride4, f32x4*
         in.a = ring[wave][slot][KC][lane];
         if constexpr (NIN > 1) in.b = ring[wave][slot][KC + 1][lane];
         if constexpr (NIN > 2) in.c = ring[wave][slot][KC + 2][lane];
+        if constexpr (NIN > 3) in.d = ring[wave][slot][KC + 3][lane];
         const f32x4 a1[1] = {acc};
         f32x4 d1[1];
         fin_tile<FIN, 1>(d1, a1, fc);
@@ -1038,19 +1041,23 @@ struct EpiDmaGeom {
                                   (KIND == FEDAVG_EPI_RADAM || KIND == FEDAVG_EPI_RMSPROP ||
                                    (KIND == FEDAVG_EPI_ADAGRAD && KC == 2));
     static constexpr bool kNadam = kAmd && KIND == FEDAVG_EPI_NADAM;
-    static constexpr int W = kWide ? 4 : kNadam ? 8 : kAdam && KC <= 2 ? 8 : 4;
+    // four operand streams (Adam amsgrad, RMSprop centered with momentum): one wave per SIMD, 16 result registers
+    // per unit -- 24 units (not swept; RMSprop at 3 reads 16: 24 spill with the IEEE sqrt)
+    static constexpr bool kQuad = NIN == 4;
+    static constexpr int W = kWide || kQuad ? 4 : kNadam ? 8 : kAdam && KC <= 2 ? 8 : 4;
     // (SGD with its momentum buffer at 3 reads holds 40 units only with 600+ bytes of scratch per lane: 32 there; Adamax
     // and Rprop hold three result streams per unit: 24)
     // (RMSprop with its momentum buffer, IEEE sqrt: 14 / 24 units at 2 / 3 reads, 16 / 32 spill)
     static constexpr bool kRmsMom = KIND == FEDAVG_EPI_RMSPROP && NIN == 3;
-    static constexpr int N = kWide ? 40
+    static constexpr int N = kQuad ? (KIND == FEDAVG_EPI_RMSPROP && KC == 3 ? 16 : 24)
+                             : kWide ? 40
                              : kNadam ? 16
                              : kThree ? 24
                              : !kAdam ? (KC == 3 ? 32 : 40)
                              : KC == 1 ? 14
                              : KC == 2 ? (kRmsMom ? 14 : 16)
                                        : (kRmsMom ? 24 : 32);
-    static constexpr bool TDMA = kWide || kNadam || (kAdam && KC != 2);
+    static constexpr bool TDMA = kWide || kNadam || kQuad || (kAdam && KC != 2);
 };
 
 // A/B builds with -DFEDAVG_AB_FEW (torch-mode FIN_DIV, ADD_BASE / SGD, and Adam / NAdam / RAdam / Adagrad / RMSprop with
@@ -1081,20 +1088,24 @@ inline hipError_t launch_epi_dma_form(const TileLaunch& L, const EpiParams& E, h
 template <int OP, int FIN, int EPI, int KC>
 inline hipError_t launch_epi_dma_k(const TileLaunch& L, const EpiParams& E, hipStream_t s, uint64_t* nl) {
     constexpr int KIND = EPI & 0xFF;
-    const int nin = epi_dma_nin(E);
+    const int nin = epi_dma_nin(E, KC);
     if constexpr (KIND == FEDAVG_EPI_ADD_BASE) {
         if (nin == 1) return launch_epi_dma_form<OP, FIN, EPI, KC, 1>(L, E, s, nl);
     } else if constexpr (KIND == FEDAVG_EPI_SGD) {
         if (nin == 1) return launch_epi_dma_form<OP, FIN, EPI, KC, 1>(L, E, s, nl);
         if (nin == 2) return launch_epi_dma_form<OP, FIN, EPI, KC, 2>(L, E, s, nl);
-    } else if constexpr (KIND == FEDAVG_EPI_ADAM || KIND == FEDAVG_EPI_NADAM || KIND == FEDAVG_EPI_RADAM ||
-                         KIND == FEDAVG_EPI_ADAMAX || KIND == FEDAVG_EPI_RPROP) {
+    } else if constexpr (KIND == FEDAVG_EPI_ADAM) {
+        if (nin == 3) return launch_epi_dma_form<OP, FIN, EPI, KC, 3>(L, E, s, nl);
+        if (nin == 4) return launch_epi_dma_form<OP, FIN, EPI, KC, 4>(L, E, s, nl);
+    } else if constexpr (KIND == FEDAVG_EPI_NADAM || KIND == FEDAVG_EPI_RADAM || KIND == FEDAVG_EPI_ADAMAX ||
+                         KIND == FEDAVG_EPI_RPROP) {
         if (nin == 3) return launch_epi_dma_form<OP, FIN, EPI, KC, 3>(L, E, s, nl);
     } else if constexpr (KIND == FEDAVG_EPI_ADAGRAD || KIND == FEDAVG_EPI_ASGD) {
         if (nin == 2) return launch_epi_dma_form<OP, FIN, EPI, KC, 2>(L, E, s, nl);
     } else if constexpr (KIND == FEDAVG_EPI_RMSPROP) {
         if (nin == 2) return launch_epi_dma_form<OP, FIN, EPI, KC, 2>(L, E, s, nl);
         if (nin == 3) return launch_epi_dma_form<OP, FIN, EPI, KC, 3>(L, E, s, nl);
+        if (nin == 4) return launch_epi_dma_form<OP, FIN, EPI, KC, 4>(L, E, s, nl);
     }
     return hipErrorInvalidValue;
 }

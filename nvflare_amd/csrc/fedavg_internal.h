@@ -58,7 +58,7 @@ constexpr int kVariantFew = 1 << 12;      // inside TileLaunch: the few-client b
                                            // fedavg_tiles_few_f32x4), set by run_tiles for 1-2 reads, no chained sum
 constexpr int kVariantEpiDma = 1 << 14;   // inside TileLaunch: the LDS-DMA few-client fused form (fedavg_epi.h
                                            // fedavg_tiles_epi_dma_f32x4), set by the C-ABI for 1-3 reads, no chained
-                                           // sum, every kind (Adam without amsgrad, RMSprop not centered); public bit 2 (the
+                                           // sum, every kind (RMSprop centered only with momentum); public bit 2 (the
                                            // per-tile pipelined form) keeps the round-5 route for same-process A/Bs
 constexpr int kVariantEpiNoSplit = 1 << 15;  // fused Adam at one block per CU (64+ clients) on round 5's burst form
                                               // instead of the split-epilogue form (fedavg_epi.h
@@ -139,18 +139,22 @@ struct EpiParams {
 
 // operand streams the LDS-DMA few-client fused form (fedavg_epi.h fedavg_tiles_epi_dma_f32x4) reads for this kind and
 // step, or 0 when it does not take them (the C-ABI then routes the per-tile form)
-inline int epi_dma_nin(const EpiParams& E) {
+// k: client reads.  Adam with amsgrad takes the form at 3 reads only: 65.7 / 72.2 / 76.2 % of HBM at 1 / 2 / 3 clients
+// against the per-tile form's 72.0 / 72.9 / 70.2 % (profiles/r06/s26/; 4 waves x 24 units, not swept)
+inline int epi_dma_nin(const EpiParams& E, const int k) {
     switch (E.kind) {
         case FEDAVG_EPI_ADD_BASE: return 1;
         case FEDAVG_EPI_SGD: return (E.has_momentum && !E.first_step) ? 2 : 1;
-        case FEDAVG_EPI_ADAM: return E.amsgrad ? 0 : 3;
+        case FEDAVG_EPI_ADAM: return E.amsgrad ? (k == 3 ? 4 : 0) : 3;  // p, exp_avg, exp_avg_sq (, max_exp_avg_sq)
         case FEDAVG_EPI_NADAM:
         case FEDAVG_EPI_RADAM:
         case FEDAVG_EPI_ADAMAX:
         case FEDAVG_EPI_RPROP: return 3;  // p and two states
         case FEDAVG_EPI_ADAGRAD:
         case FEDAVG_EPI_ASGD: return 2;  // p and one state
-        case FEDAVG_EPI_RMSPROP: return E.centered ? 0 : E.has_momentum ? 3 : 2;  // centered: a 4th stream, per-tile
+        // RMSprop: p, square_avg (, momentum buffer (, grad_avg)); centered without momentum would read state3 as the
+        // third stream: the per-tile form
+        case FEDAVG_EPI_RMSPROP: return E.centered ? (E.has_momentum ? 4 : 0) : E.has_momentum ? 3 : 2;
         default: return 0;
     }
 }

@@ -95,11 +95,14 @@ def _diff(a, w):
     return int(bad.size), [(int(i), hex(int(a.view(np.uint32)[i])), hex(int(w.view(np.uint32)[i]))) for i in bad[:4]]
 
 
-def _tiles_per_block(kind, K, rms_momentum=False, amd=False):
+def _tiles_per_block(kind, K, rms_momentum=False, amd=False, quad=False):
     """Tiles per block per launch of the product geometry (fedavg_epi.h EpiDmaGeom: N units per wave x W waves / 16):
     Adam / NAdam / RAdam / Adagrad / RMSprop 1 / 2 clients 8 waves x 14 / 16 units, 3 clients 4 waves x 32 (RMSprop
     with momentum 14 / 14 / 24); Adamax / Rprop 4 waves x 24; ADD_BASE / SGD / ASGD 4 waves x 40 (x 32 at 3).  With
-    the AMD-host sqrt: RAdam / RMSprop at 1-2 clients and Adagrad at 2 4 waves x 40, NAdam 8 x 16 at every count."""
+    the AMD-host sqrt: RAdam / RMSprop at 1-2 clients and Adagrad at 2 4 waves x 40, NAdam 8 x 16 at every count.
+    Four operand streams (amsgrad, centered RMSprop with momentum): 4 waves x 24 (RMSprop at 3 clients x 16)."""
+    if quad:
+        return 4 if kind == 5 and K == 3 else 6
     if amd and K <= 2 and (kind in (5, 8) or (kind == 4 and K == 2)):
         return 10
     if amd and kind == 7:
@@ -113,9 +116,9 @@ def _tiles_per_block(kind, K, rms_momentum=False, amd=False):
     return 8 if K == 3 else 10
 
 
-def _launches(ctx, begin, end, kind=3, K=2, rms_momentum=False, amd=False):
+def _launches(ctx, begin, end, kind=3, K=2, rms_momentum=False, amd=False, quad=False):
     t_first, t_stop = begin // TILE, (end - 1) // TILE + 1
-    per = min(ctx.num_cus, t_stop - t_first) * _tiles_per_block(kind, K, rms_momentum, amd)  # one block per CU
+    per = min(ctx.num_cus, t_stop - t_first) * _tiles_per_block(kind, K, rms_momentum, amd, quad)  # one block per CU
     return -(-(t_stop - t_first) // per)
 
 
@@ -230,6 +233,9 @@ OTHER_KINDS = [  # (kind, hyper-parameters, state names, restated AMD-host sqrt)
     (4, dict(lr=1e-2, weight_decay=1e-3, eps=1e-8, maximize=1), ("m",), True),  # Adagrad
     (5, dict(lr=1e-3, alpha=0.95, eps=1e-8, weight_decay=1e-3), ("m",), True),  # RMSprop: square_avg
     (5, dict(lr=1e-3, alpha=0.9, eps=1e-6, momentum=0.5, maximize=1), ("m", "v"), False),  # + momentum buffer
+    (5, dict(lr=1e-3, alpha=0.95, eps=1e-8, momentum=0.5, centered=1), ("m", "v", "x"), True),  # + grad_avg
+    (3, dict(lr=1e-3, beta1=0.5, beta2=0.9, eps=1e-8, amsgrad=1, weight_decay=1e-2, decoupled_weight_decay=1),
+     ("m", "v", "x"), True),  # AdamW with amsgrad: max_exp_avg_sq
     (6, dict(lr=1e-2, beta1=0.8, beta2=0.95, eps=1e-6, weight_decay=1e-3), ("m", "v"), False),  # Adamax
     (7, dict(lr=2e-3, beta1=0.9, beta2=0.999, eps=1e-8, momentum_decay=4e-3), ("m", "v"), True),  # NAdam
     (8, dict(lr=1e-2, beta1=0.8, beta2=0.9, eps=1e-8, weight_decay=1e-3), ("m", "v"), True),  # RAdam
@@ -257,8 +263,10 @@ def test_dma_other_kinds(ctx, oracle, K, rng_ix, case):
               "v": (c.rng.random(n) * 1e-4 + 1e-6).astype(np.float32)}
         if kind == 4:  # Adagrad: a positive sum
             st["m"] = np.abs(st["m"]) + np.float32(0.1)
-        if kind == 5:  # RMSprop: square_avg, the momentum buffer
+        st["x"] = (c.rng.random(n) * 1e-4 + 1e-6).astype(np.float32)  # Adam's max_exp_avg_sq
+        if kind == 5:  # RMSprop: square_avg, the momentum buffer, grad_avg (square_avg above grad_avg^2)
             st["m"], st["v"] = (c.rng.random(n) * 1e-2 + 1e-3).astype(np.float32), st["m"]
+            st["x"] = (c.rng.standard_normal(n) * 1e-3).astype(np.float32)
         if kind == 9:  # Rprop: step sizes
             st["v"] = np.full(n, 0.01, np.float32)
         if kind == 10:  # ASGD: ax
@@ -270,13 +278,16 @@ def test_dma_other_kinds(ctx, oracle, K, rng_ix, case):
             got = {}
             for variant in (0, 4):  # the LDS-DMA form, then the per-tile form from the same states
                 kw = dict(param=c.buf("p", p), step=step, **hp, **sq)
-                for nm, field in zip(names, ("state1", "state2")):
+                for nm, field in zip(names, ("state1", "state2", "state3")):
                     kw[field] = c.buf(nm, st[nm])
                 nl = _run(ctx, c, _epi(kind, **kw), N.FEDAVG_OP_TORCH, N.FEDAVG_FIN_DIV, variant=variant)
-                if variant == 0:
-                    assert nl == _launches(ctx, begin, end, kind, K, rms_momentum=len(names) == 2, amd=amd_sqrt)
+                if variant == 0 and kind == 3 and K < 3:  # amsgrad under 3 reads: the per-tile form (epi_dma_nin)
+                    assert nl == 1
+                elif variant == 0:
+                    assert nl == _launches(ctx, begin, end, kind, K, rms_momentum=len(names) == 2, amd=amd_sqrt,
+                                           quad=len(names) == 3)
                 got[variant] = [c.get(x) for x in ("p",) + names]
-            kw = {k: st[nm] for k, nm in zip(("m", "v"), names)}
+            kw = {k: st[nm] for k, nm in zip(("m", "v", "vmax"), names)}
             oracle.epilogue_apply(c.d(oracle, 1), kind, p=p, step=step,
                                   torch_cpu_sqrt="torch_cpu_amd" if amd_sqrt else False, **kw, **hp)
             for a, b, w, nm in zip(got[0], got[4], [p] + [st[x] for x in names], ("p",) + names):
@@ -286,23 +297,25 @@ def test_dma_other_kinds(ctx, oracle, K, rng_ix, case):
 
 
 def test_dma_route_leaves_others_on_the_per_tile_form(ctx, oracle):
-    """amsgrad and centered RMSprop (a fourth operand stream) and a requested aggregate output keep their round-5 routes: one
-    persistent per-tile launch, or the burst form."""
+    """A requested aggregate output, centered RMSprop without momentum (its grad_avg would be the third operand
+    stream, where the form reads state2) and amsgrad under 3 reads (the per-tile form measured faster, s26) keep their
+    round-5 route: one persistent per-tile launch.  (amsgrad at 3 reads and centered RMSprop with momentum -- four
+    operand streams -- run the LDS-DMA form since round 6: test_dma_other_kinds.)"""
     from nvflare_amd import _native as N
 
     c = _Case(ctx, 2, 0, 3 * TILE + 8, seed=7)
     try:
         z = np.zeros(c.n, np.float32)
-        e = _epi(3, param=c.buf("p", z + 1), state1=c.buf("m", z), state2=c.buf("v", z), state3=c.buf("x", z),
-                 amsgrad=1, step=1.0, **ADAM)
-        assert _run(ctx, c, e, N.FEDAVG_OP_TORCH, N.FEDAVG_FIN_DIV) == 1
         e = _epi(3, param=c.buf("p", z + 1), state1=c.buf("m", z), state2=c.buf("v", z), step=1.0, **ADAM)
         assert _run(ctx, c, e, N.FEDAVG_OP_TORCH, N.FEDAVG_FIN_DIV, out_ptr=c.buf("d", z)) == 1
         want = c.d(oracle, 1)
         assert same_bits(c.get("d"), want)
-        e = _epi(5, param=c.buf("p", z + 1), state1=c.buf("m", z + 1e-3), state2=c.buf("v", z), state3=c.buf("x", z),
-                 lr=1e-3, alpha=0.9, eps=1e-8, momentum=0.5, centered=1)  # centered RMSprop: a fourth stream
+        e = _epi(5, param=c.buf("p", z + 1), state1=c.buf("m", z + 1e-3), state3=c.buf("x", z),
+                 lr=1e-3, alpha=0.9, eps=1e-8, centered=1)
         assert _run(ctx, c, e, N.FEDAVG_OP_TORCH, N.FEDAVG_FIN_DIV) == 1
+        e = _epi(3, param=c.buf("p", z + 1), state1=c.buf("m", z), state2=c.buf("v", z), state3=c.buf("x", z),
+                 amsgrad=1, step=1.0, **ADAM)
+        assert _run(ctx, c, e, N.FEDAVG_OP_TORCH, N.FEDAVG_FIN_DIV) == 1  # amsgrad at 2 reads: the per-tile form
     finally:
         c.close()
 

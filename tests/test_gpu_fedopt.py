@@ -536,10 +536,12 @@ FEW_CASES = [  # (kind, hp, state names): every optimizer kind through the few-c
 ]
 
 
-def _dma_tiles_per_block(kind, K, amd=False):
+def _dma_tiles_per_block(kind, K, amd=False, quad=False):
     """Tiles per block per launch of the LDS-DMA form (fedavg_epi.h EpiDmaGeom, N units per wave x W waves / 16): the
     Adam family and Adagrad 8 waves x 16 units at 2 reads, 4 x 32 at 3; Adamax / Rprop 4 x 24; the rest 4 x 40
     (x 32 at 3 reads)."""
+    if quad:  # four operand streams (amsgrad, centered RMSprop with momentum): 4 waves x 24 (RMSprop at 3 x 16)
+        return 4 if kind == 5 and K == 3 else 6
     if amd and K <= 2 and (kind in (5, 8) or (kind == 4 and K == 2)):  # AMD-host sqrt: 4 waves x 40 at 1-2 reads
         return 10
     if kind in (3, 4, 7, 8):
@@ -604,11 +606,12 @@ def test_few_client_fused_every_kind(ctx, oracle, K, case):
             ctx.accumulate_tiled_epi(dev.bases, ws, TILE, dev.lay.tile_stride, 0, dev.n4, out, N_.FEDAVG_OP_TORCH,
                                      N_.FEDAVG_FIN_DIV, _sum(ws), e)
             ctx.sync()
-            # Every kind takes the LDS-DMA few-client form (round 6) unless it asks for centered RMSprop, amsgrad or an aggregate
+            # Every kind takes the LDS-DMA few-client form (round 6) unless it asks for centered RMSprop without momentum or an aggregate
             # output: one launch per num_cus x tiles-per-block tiles; the rest the per-tile form: one persistent launch
             tiles = (dev.n4 - 1) // TILE + 1
-            dma = not hp.get("centered") and (out is None or kind == 1) and not hp.get("amsgrad")
-            tpb = _dma_tiles_per_block(kind, K, amd=bool(sq))
+            dma = (not (hp.get("centered") and not hp.get("momentum")) and (out is None or kind == 1)
+                   and not (hp.get("amsgrad") and K < 3))
+            tpb = _dma_tiles_per_block(kind, K, amd=bool(sq), quad=len(names) == 3)
             assert ctx.launch_count() - n_launch == (-(-tiles // (min(ctx.num_cus, tiles) * tpb)) if dma else 1)
             d = oracle.fedavg_c(rows, ws, oracle.MODE_TORCH, nthreads=8)
             if kind == 1:

@@ -16,7 +16,8 @@ import sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 EXTRA = {"none": 4.0, "add_base": 8.0, "sgd": 16.0, "adam": 24.0, "adagrad": 16.0, "adamax": 24.0, "nadam": 24.0,
-         "radam": 24.0, "rprop": 24.0, "asgd": 16.0, "rmsprop": 24.0}
+         "radam": 24.0, "rprop": 24.0, "asgd": 16.0, "rmsprop": 24.0, "adam_ams": 32.0, "rmsprop_c": 32.0}
+FOUR = ("adam_ams", "rmsprop_c")  # amsgrad's max_exp_avg_sq / centered RMSprop's grad_avg in state3
 TWO_STATES = ("adam", "adamax", "nadam", "radam", "rprop", "rmsprop")  # rmsprop: square_avg, momentum buffer  # algorithmic bytes per param beyond 4K
 
 
@@ -81,7 +82,7 @@ def main():
     cnt = sum(ws)
     shifts = [int(x) for x in a.op_shifts.split(",")]
     assert all(x % 256 == 0 and x >= 0 for x in shifts)
-    bufs = [ctx.alloc(end * 4 + max(shifts)) for _ in range(3)]
+    bufs = [ctx.alloc(end * 4 + max(shifts)) for _ in range(4)]
     for b in bufs:
         ctx.memset(b.ptr, 0, end * 4 + max(shifts))
     out = ctx.alloc(end * 4)
@@ -89,7 +90,7 @@ def main():
     kinds = {"add_base": N.FEDAVG_EPI_ADD_BASE, "sgd": N.FEDAVG_EPI_SGD, "adam": N.FEDAVG_EPI_ADAM,
              "adagrad": N.FEDAVG_EPI_ADAGRAD, "adamax": N.FEDAVG_EPI_ADAMAX, "nadam": N.FEDAVG_EPI_NADAM,
              "radam": N.FEDAVG_EPI_RADAM, "rprop": N.FEDAVG_EPI_RPROP, "asgd": N.FEDAVG_EPI_ASGD,
-             "rmsprop": N.FEDAVG_EPI_RMSPROP}
+             "rmsprop": N.FEDAVG_EPI_RMSPROP, "adam_ams": N.FEDAVG_EPI_ADAM, "rmsprop_c": N.FEDAVG_EPI_RMSPROP}
 
     def launcher(epi, pad, sh=0):
         _, bases, stride = slabs[pad]
@@ -107,8 +108,11 @@ def main():
             e.base, o = bufs[0].ptr + sh, out.ptr
         else:
             e.param, e.state1 = bufs[0].ptr + sh, bufs[1].ptr + sh
-            if epi in TWO_STATES or epi == "sgd":
+            if epi in TWO_STATES or epi in FOUR or epi == "sgd":
                 e.state2 = bufs[2].ptr + sh
+            if epi in FOUR:
+                e.state3 = bufs[3].ptr + sh
+                e.amsgrad, e.centered = int(epi == "adam_ams"), int(epi == "rmsprop_c")
             o = None
         return lambda: ctx.accumulate_tiled_epi(bases, ws, lay.tile, stride, 0, end, o, op, fin, cnt, e)
 
@@ -149,7 +153,7 @@ def main():
                     ctx.d2h(host, out.ptr if epi in ("none", "add_base") else bufs[0].ptr + shifts[0])
                     if epi not in ("none", "add_base"):
                         last = np.empty(end, dtype=np.float32)
-                        ctx.d2h(last, bufs[2 if epi in TWO_STATES else 1].ptr + shifts[0])
+                        ctx.d2h(last, bufs[3 if epi in FOUR else 2 if epi in TWO_STATES else 1].ptr + shifts[0])
                         host = np.concatenate([host, last])
                     if epi not in ref_out:
                         ref_out[epi] = host
